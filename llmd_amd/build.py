@@ -1,0 +1,154 @@
+"""In-tree native build for llmd_amd (no JIT cache, no hipify).
+
+Two extension modules are produced next to this file:
+
+* ``_C``  - the HIP/CDNA4 op library: every ``csrc/ops/*.hip`` compiled by
+  ``hipcc --offload-arch=gfx950`` plus ``csrc/ops/bindings.cpp`` (torch
+  pybind11 bindings) compiled by g++, linked against torch's own HIP runtime.
+* ``_rt`` - the host C++ runtime (block manager / prefix cache, KV-event
+  index, GBDT latency predictor, offload/FS tier, ...): ``csrc/runtime/*.cpp``
+  with pybind11 only (no torch, no HIP), so CPU-only hosts can use it.
+
+Objects are cached by a content hash of (source, headers, flags), so a rebuild
+only recompiles what changed. ``python -m llmd_amd.build`` builds both.
+"""
+from __future__ import annotations
+
+import concurrent.futures as cf
+import hashlib
+import os
+import subprocess
+import sys
+import sysconfig
+from pathlib import Path
+
+PKG = Path(__file__).resolve().parent
+CSRC = PKG / "csrc"
+BUILD = PKG.parent / "build" / "llmd_native"
+ARCH = os.environ.get("LLMD_OFFLOAD_ARCH", "gfx950")
+ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
+EXT = sysconfig.get_config_var("EXT_SUFFIX") or ".so"
+
+
+def _torch_paths():
+    import torch.utils.cpp_extension as ce  # noqa: WPS433
+
+    inc = ce.include_paths()
+    lib = ce.library_paths()[0]
+    return inc, lib
+
+
+def _pybind_inc():
+    import pybind11
+
+    return pybind11.get_include()
+
+
+def _py_inc():
+    return sysconfig.get_paths()["include"]
+
+
+def _hash(paths, flags):
+    h = hashlib.sha256()
+    for p in paths:
+        h.update(Path(p).read_bytes())
+    h.update(" ".join(flags).encode())
+    return h.hexdigest()[:16]
+
+
+def _headers(d: Path):
+    return sorted(str(p) for p in d.rglob("*.h"))
+
+
+def _run(cmd):
+    r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"build failed: {' '.join(cmd)}\n{r.stdout}")
+    return r.stdout
+
+
+def _compile(src: Path, cmd_prefix, flags, deps, out_dir: Path):
+    key = _hash([src] + deps, cmd_prefix + flags)
+    obj = out_dir / f"{src.stem}.{key}.o"
+    if not obj.exists():
+        tmp = obj.with_suffix(".tmp.o")
+        _run(cmd_prefix + flags + ["-c", str(src), "-o", str(tmp)])
+        os.replace(tmp, obj)
+    return obj
+
+
+def _link(objs, out: Path, libs):
+    key = _hash(objs, libs)
+    stamp = out.with_name(out.name + ".stamp")
+    if out.exists() and stamp.exists() and stamp.read_text() == key:
+        return out
+    tmp = out.with_name(out.name + ".tmp")
+    _run(["g++", "-shared", "-o", str(tmp)] + [str(o) for o in objs] + libs)
+    os.replace(tmp, out)
+    stamp.write_text(key)
+    return out
+
+
+def build_ops(jobs: int = 8, verbose: bool = False) -> Path:
+    """Build the HIP op library ``llmd_amd/_C``."""
+    tinc, tlib = _torch_paths()
+    out_dir = BUILD / "ops"
+    out_dir.mkdir(parents=True, exist_ok=True)
+    inc = CSRC / "include"
+    deps = _headers(inc)
+    hip_srcs = sorted((CSRC / "ops").glob("*.hip"))
+    hip_flags = [
+        f"--offload-arch={ARCH}", "-O3", "-fPIC", "-std=c++17", f"-I{inc}",
+        "-ffp-contract=fast", "-munsafe-fp-atomics",
+    ]
+    cpp_flags = [
+        "-O2", "-fPIC", "-std=c++17", f"-I{inc}", f"-I{ROCM}/include", f"-I{_py_inc()}",
+        "-D__HIP_PLATFORM_AMD__=1", "-DUSE_ROCM=1", "-DTORCH_EXTENSION_NAME=_C",
+        "-DTORCH_API_INCLUDE_EXTENSION_H", "-D_GLIBCXX_USE_CXX11_ABI=1", "-w",
+    ] + [f"-I{p}" for p in tinc]
+    with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
+        futs = [ex.submit(_compile, s, [f"{ROCM}/bin/hipcc"], hip_flags, deps, out_dir) for s in hip_srcs]
+        futs.append(ex.submit(_compile, CSRC / "ops" / "bindings.cpp", ["g++"], cpp_flags, deps, out_dir))
+        objs = [f.result() for f in futs]
+    libs = [
+        f"-L{tlib}", "-lc10", "-lc10_hip", "-ltorch", "-ltorch_cpu", "-ltorch_hip",
+        "-ltorch_python", "-lamdhip64", f"-Wl,-rpath,{tlib}",
+    ]
+    out = _link(objs, PKG / f"_C{EXT}", libs)
+    if verbose:
+        print(f"[llmd build] {out}")
+    return out
+
+
+def build_runtime(jobs: int = 8, verbose: bool = False) -> Path:
+    """Build the host C++ runtime ``llmd_amd/_rt`` (pybind11, no torch/HIP)."""
+    out_dir = BUILD / "rt"
+    out_dir.mkdir(parents=True, exist_ok=True)
+    rdir = CSRC / "runtime"
+    deps = _headers(rdir) + _headers(CSRC / "include")
+    srcs = sorted(rdir.glob("*.cpp"))
+    flags = ["-O3", "-fPIC", "-std=c++17", f"-I{rdir}", f"-I{_pybind_inc()}", f"-I{_py_inc()}",
+             "-fvisibility=hidden", "-pthread"]
+    extra = os.environ.get("LLMD_RT_CFLAGS", "").split()
+    with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
+        objs = list(ex.map(lambda s: _compile(s, ["g++"], flags + extra, deps, out_dir), srcs))
+    return _link(objs, PKG / f"_rt{EXT}", ["-pthread"] + extra)
+
+
+def build_all(jobs: int | None = None, verbose: bool = True):
+    jobs = jobs or min(8, os.cpu_count() or 4)
+    rt = build_runtime(jobs, verbose)
+    ops = build_ops(jobs, verbose)
+    if verbose:
+        print(f"[llmd build] ok: {rt.name} {ops.name}")
+    return rt, ops
+
+
+if __name__ == "__main__":
+    what = sys.argv[1] if len(sys.argv) > 1 else "all"
+    if what == "ops":
+        build_ops(verbose=True)
+    elif what == "rt":
+        build_runtime(verbose=True)
+    else:
+        build_all()

@@ -1,0 +1,88 @@
+// Shared device helpers for the llmd_amd HIP op library (gfx950 / CDNA4 only).
+//
+// Conventions:
+//   * bf16 tensors are handled as raw 16-bit words (uint16_t) and widened to
+//     f32 with a shift; f32 -> bf16 uses the compiler's __bf16 conversion,
+//     which lowers to v_cvt_pk_bf16_f32 on gfx950 (RNE, NaN-preserving).
+//   * All memory-bound kernels move 16 B per lane (8 x bf16) per access.
+//   * Wave width is 64 everywhere (hard-coded, never warpSize).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define LLMD_WAVE 64
+
+typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4_t __attribute__((ext_vector_type(4)));
+typedef short s16x8_t __attribute__((ext_vector_type(8)));
+typedef short s16x4_t __attribute__((ext_vector_type(4)));
+typedef float f32x4_t __attribute__((ext_vector_type(4)));
+typedef float f32x16_t __attribute__((ext_vector_type(16)));
+typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x2_t __attribute__((ext_vector_type(2)));
+
+namespace llmd {
+
+__device__ __forceinline__ float bf2f(uint16_t x) {
+  return __uint_as_float(((uint32_t)x) << 16);
+}
+__device__ __forceinline__ uint16_t f2bf(float f) {
+  __bf16 h = (__bf16)f;
+  return __builtin_bit_cast(uint16_t, h);
+}
+// Unpack a 16-byte chunk of 8 bf16 into 8 floats.
+__device__ __forceinline__ void unpack8(const u32x4_t v, float* f) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    f[2 * i] = __uint_as_float(v[i] << 16);
+    f[2 * i + 1] = __uint_as_float(v[i] & 0xffff0000u);
+  }
+}
+__device__ __forceinline__ u32x4_t pack8(const float* f) {
+  u32x4_t v;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    v[i] = (uint32_t)f2bf(f[2 * i]) | ((uint32_t)f2bf(f[2 * i + 1]) << 16);
+  }
+  return v;
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// Block-wide sum for blockDim.x == NT (multiple of 64). `red` must hold NT/64 floats.
+template <int NT>
+__device__ __forceinline__ float block_sum(float v, float* red) {
+  v = wave_sum(v);
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  if (NT == 64) return v;
+  if (l == 0) red[w] = v;
+  __syncthreads();
+  float t = 0.f;
+#pragma unroll
+  for (int i = 0; i < NT / 64; ++i) t += red[i];
+  __syncthreads();
+  return t;
+}
+
+// XCD-aware bijective block remap (8 XCDs): consecutive logical tiles land on
+// the same XCD so neighbouring tiles share that XCD's L2.
+__device__ __forceinline__ int xcd_remap(int orig, int nwg) {
+  const int q = nwg / 8, r = nwg % 8;
+  const int xcd = orig % 8;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + orig / 8;
+}
+
+}  // namespace llmd
+
+#define LLMD_CHECK_LAUNCH() \
+  do {                      \
+  } while (0)

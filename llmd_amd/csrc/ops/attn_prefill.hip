@@ -1,0 +1,300 @@
+// Varlen causal prefill / chunked-prefill attention over the paged KV cache
+// (SURVEY K02/K04). New tokens' K/V must already be in the cache (rope_cache).
+//
+// Work decomposition: a host-built list of items (seq, first query token of a
+// 32*TPW-token block) x grid.y = (kv head, head group). A workgroup = 4 waves;
+// wave w owns 32 query tokens of one query head, and the HPW heads handled by
+// one workgroup all share the same KV head, so every K/V tile staged in LDS is
+// reused by all 4 waves (GQA reuse) and - for G >= 4 - all waves share the same
+// causal range (no imbalance).
+//
+// Per 64-key tile:
+//   S^T[key][q] = K[key] . Q[q]   (keys on the MFMA M axis -> P lands lane-local
+//                                  in the A-operand layout of the PV product)
+//     K image: padded rows (D*2+16 B) -> ds_read_b128 conflict-free
+//   O[q][dim] += P[q][key] . V[key][dim]
+//     V image: XOR-swizzled rows, ds_read_b64_tr_b16 transposed reads
+// K/V tiles are double-buffered; the next tile's global loads are issued before
+// the current tile's MFMAs and written to LDS after the barrier (T14 split).
+#include "llmd_common.h"
+
+using namespace llmd;
+
+namespace {
+
+constexpr int NT = 256;
+constexpr float NEG_INF = -__builtin_huge_valf();
+
+__device__ __forceinline__ int rowoff(int g) { return 4 * (g >> 1) + 8 * (g & 1); }
+
+template <int D>
+__device__ __forceinline__ int vimg_off(int row, int ch) {
+  if constexpr (D == 128) {
+    const int sw = ((row & 3) << 2) | ((row >> 2) & 3);
+    return row * 256 + 16 * (ch ^ sw);
+  } else {
+    const int sw = 2 * (((row >> 1) & 1) | (((row >> 3) & 1) << 1));
+    return row * 128 + 16 * (ch ^ sw);
+  }
+}
+template <int D>
+__device__ __forceinline__ int kimg_off(int row, int ch) {
+  return row * (D * 2 + 16) + 16 * ch;
+}
+
+template <int D>
+__global__ __launch_bounds__(NT, 2) void prefill_kernel(
+    const uint16_t* __restrict__ q, int64_t q_stride, const uint16_t* __restrict__ kc,
+    const uint16_t* __restrict__ vc, int64_t block_stride, int bs,
+    const int* __restrict__ block_tables, int bt_stride, const int* __restrict__ q_start,
+    const int* __restrict__ q_len, const int* __restrict__ ctx_len, const int* __restrict__ items,
+    int Hq, int Hkv, int G, int HPW, float scale_log2, int window,
+    const float* __restrict__ sinks, uint16_t* __restrict__ out, int64_t out_stride) {
+  constexpr int KS = D / 32, NB = D / 16, CPR = D / 8;
+  constexpr int KIMG = 64 * (D * 2 + 16);
+  constexpr int VIMG = 64 * D * 2;
+  constexpr int LPT = 64 * CPR / NT;  // chunks per thread per tile (K and V each)
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+
+  const int seq = items[2 * blockIdx.x], qb = items[2 * blockIdx.x + 1];
+  const int NHG = G / HPW;
+  const int kvh = blockIdx.y / NHG, hg = blockIdx.y % NHG;
+  const int TPW = 4 / HPW;  // token sub-blocks per workgroup
+  const int qs = q_start[seq], ql = q_len[seq], ctx = ctx_len[seq];
+  const int pbase = ctx - ql;  // position of query token 0
+  const int* bt = block_tables + (int64_t)seq * bt_stride;
+  const int64_t head_off = (int64_t)kvh * bs * D;
+
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, g = lane >> 4, c16 = lane & 15;
+  const int head = kvh * G + hg * HPW + (w % HPW);
+  const int tok0 = qb + (w / HPW) * 32;
+  const int ntok = max(0, min(32, ql - tok0));
+  const int p_lo = pbase + tok0, p_hi = pbase + tok0 + max(ntok, 1) - 1;
+
+  // workgroup key range
+  const int wg_tok_end = min(ql, qb + 32 * TPW);
+  const int wg_p_lo = pbase + qb, wg_p_hi = pbase + wg_tok_end - 1;
+  const int kmin = window > 0 ? max(0, wg_p_lo - window + 1) : 0;
+  const int t_first = kmin >> 6, t_last = wg_p_hi >> 6;
+
+  // Q fragments: B operand, [nb][s]
+  bf16x8_t qf[2][KS];
+#pragma unroll
+  for (int nb = 0; nb < 2; ++nb) {
+    const int tk = tok0 + 16 * nb + c16;
+    const uint16_t* qr = q + (int64_t)(qs + tk) * q_stride + (int64_t)head * D;
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      u32x4_t v = {0, 0, 0, 0};
+      if (tk < ql) v = *reinterpret_cast<const u32x4_t*>(qr + (4 * s + g) * 8);
+      qf[nb][s] = __builtin_bit_cast(bf16x8_t, v);
+    }
+  }
+
+  float m[2] = {NEG_INF, NEG_INF}, lsum[2] = {0.f, 0.f};
+  f32x4_t o[2][NB];
+#pragma unroll
+  for (int nb = 0; nb < 2; ++nb)
+#pragma unroll
+    for (int n = 0; n < NB; ++n) o[nb][n] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  // ---- tile loader (registers)
+  u32x4_t kr[LPT], vr[LPT];
+  auto load_tile = [&](int t) {
+    const int ts = t * 64;
+#pragma unroll
+    for (int i = 0; i < LPT; ++i) {
+      const int idx = threadIdx.x + NT * i;
+      const int row = idx / CPR, ch = idx % CPR;
+      int key = ts + row;
+      key = key < ctx ? key : ctx - 1;
+      const int phys = bt[key / bs];
+      const int64_t off = (int64_t)phys * block_stride + head_off + (int64_t)(key % bs) * D + ch * 8;
+      kr[i] = *reinterpret_cast<const u32x4_t*>(kc + off);
+      vr[i] = *reinterpret_cast<const u32x4_t*>(vc + off);
+    }
+  };
+  auto store_tile = [&](int buf) {
+    char* kimg = smem + buf * (KIMG + VIMG);
+    char* vimg = kimg + KIMG;
+#pragma unroll
+    for (int i = 0; i < LPT; ++i) {
+      const int idx = threadIdx.x + NT * i;
+      const int row = idx / CPR, ch = idx % CPR;
+      *reinterpret_cast<u32x4_t*>(kimg + kimg_off<D>(row, ch)) = kr[i];
+      *reinterpret_cast<u32x4_t*>(vimg + vimg_off<D>(row, ch)) = vr[i];
+    }
+  };
+
+  load_tile(t_first);
+  int buf = 0;
+  for (int t = t_first; t <= t_last; ++t) {
+    store_tile(buf);
+    __syncthreads();
+    if (t < t_last) load_tile(t + 1);
+    const int ts = t * 64;
+    const bool active = ntok > 0 && ts <= p_hi && (window <= 0 || ts + 63 > p_lo - window);
+    if (active) {
+      const char* kimg = smem + buf * (KIMG + VIMG);
+      const char* vimg = kimg + KIMG;
+      // ---- S^T
+      f32x4_t sc[4][2];
+#pragma unroll
+      for (int b4 = 0; b4 < 4; ++b4) {
+        const int row = 16 * b4 + rowoff(c16 >> 2) + (c16 & 3);
+        f32x4_t a0 = {0.f, 0.f, 0.f, 0.f}, a1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int s = 0; s < KS; ++s) {
+          const bf16x8_t ka = *reinterpret_cast<const bf16x8_t*>(kimg + kimg_off<D>(row, 4 * s + g));
+          a0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ka, qf[0][s], a0, 0, 0, 0);
+          a1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ka, qf[1][s], a1, 0, 0, 0);
+        }
+        sc[b4][0] = a0;
+        sc[b4][1] = a1;
+      }
+      // ---- mask + online softmax per q column
+      float alpha[2];
+#pragma unroll
+      for (int nb = 0; nb < 2; ++nb) {
+        const int qp = p_lo + 16 * nb + c16;
+        float mx = NEG_INF;
+#pragma unroll
+        for (int b4 = 0; b4 < 4; ++b4)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const int key = ts + 16 * b4 + rowoff(g) + i;
+            float v = sc[b4][nb][i] * scale_log2;
+            bool ok = key <= qp;
+            if (window > 0) ok = ok && key > qp - window;
+            v = ok ? v : NEG_INF;
+            sc[b4][nb][i] = v;
+            mx = fmaxf(mx, v);
+          }
+        mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+        mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+        const float mnew = fmaxf(m[nb], mx);
+        // rows fully masked so far keep m=-inf; guard the exp of (-inf) - (-inf)
+        const float msafe = mnew == NEG_INF ? 0.f : mnew;
+        alpha[nb] = exp2f(m[nb] - msafe);
+        float ps = 0.f;
+#pragma unroll
+        for (int b4 = 0; b4 < 4; ++b4)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const float p = exp2f(sc[b4][nb][i] - msafe);
+            sc[b4][nb][i] = p;
+            ps += p;
+          }
+        ps += __shfl_xor(ps, 16, 64);
+        ps += __shfl_xor(ps, 32, 64);
+        lsum[nb] = lsum[nb] * alpha[nb] + ps;
+        m[nb] = mnew;
+      }
+#pragma unroll
+      for (int nb = 0; nb < 2; ++nb)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const float a = __shfl(alpha[nb], 4 * g + i, 64);
+#pragma unroll
+          for (int n = 0; n < NB; ++n) o[nb][n][i] *= a;
+        }
+      // ---- O += P V
+      const int qq = c16 >> 2, pp = c16 & 3;
+#pragma unroll
+      for (int t2 = 0; t2 < 2; ++t2) {
+        bf16x8_t pa[2];
+#pragma unroll
+        for (int nb = 0; nb < 2; ++nb)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            pa[nb][j] = (__bf16)sc[2 * t2][nb][j];
+            pa[nb][4 + j] = (__bf16)sc[2 * t2 + 1][nb][j];
+          }
+#pragma unroll
+        for (int n = 0; n < NB; ++n) {
+          const int r0 = 32 * t2 + rowoff(g) + qq;
+          const int ch = 2 * n + (pp >> 1);
+          const int a0 = vimg_off<D>(r0, ch) + 8 * (pp & 1);
+          const int a1 = vimg_off<D>(r0 + 16, ch) + 8 * (pp & 1);
+          s16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+              (__attribute__((address_space(3))) s16x4_t*)(vimg + a0));
+          s16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+              (__attribute__((address_space(3))) s16x4_t*)(vimg + a1));
+          const bf16x8_t vb = __builtin_bit_cast(
+              bf16x8_t, s16x8_t{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]});
+          o[0][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pa[0], vb, o[0][n], 0, 0, 0);
+          o[1][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pa[1], vb, o[1][n], 0, 0, 0);
+        }
+      }
+    }
+    buf ^= 1;
+  }
+
+  // ---- epilogue: rows of O are q tokens 16*nb + 4g + i; their m/l live in lane 4g+i
+  if (ntok == 0) return;
+  const float sink = sinks ? sinks[head] * 1.4426950408889634f : NEG_INF;
+#pragma unroll
+  for (int nb = 0; nb < 2; ++nb) {
+    float den = lsum[nb];
+    if (sinks) den += exp2f(sink - (m[nb] == NEG_INF ? 0.f : m[nb]));
+    const float inv = den > 0.f ? 1.f / den : 0.f;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const float f = __shfl(inv, 4 * g + i, 64);
+      const int tk = tok0 + 16 * nb + 4 * g + i;
+      if (tk < ql) {
+        uint16_t* orow = out + (int64_t)(qs + tk) * out_stride + (int64_t)head * D;
+#pragma unroll
+        for (int n = 0; n < NB; ++n) orow[16 * n + c16] = f2bf(o[nb][n][i] * f);
+      }
+    }
+  }
+}
+
+}  // namespace
+
+extern "C" int llmd_paged_prefill(const void* q, int64_t q_stride, const void* kc, const void* vc,
+                                  int64_t block_stride, int bs, const int* block_tables,
+                                  int bt_stride, const int* q_start, const int* q_len,
+                                  const int* ctx_len, const int* items, int n_items, int Hq,
+                                  int Hkv, int D, float scale, int window, const float* sinks,
+                                  void* out, int64_t out_stride, hipStream_t st) {
+  if (n_items == 0) return 0;
+  const int G = Hq / Hkv;
+  const int HPW = (G % 4 == 0) ? 4 : ((G % 2 == 0) ? 2 : 1);  // 4 / HPW must be integral
+  const float scale_log2 = scale * 1.4426950408889634f;
+  dim3 grid(n_items, Hkv * (G / HPW)), blk(NT);
+  static bool attr_done = false;
+  if (!attr_done) {
+    hipFuncSetAttribute((const void*)prefill_kernel<128>,
+                        hipFuncAttributeMaxDynamicSharedMemorySize,
+                        2 * (64 * (128 * 2 + 16) + 64 * 128 * 2));
+    hipFuncSetAttribute((const void*)prefill_kernel<64>,
+                        hipFuncAttributeMaxDynamicSharedMemorySize,
+                        2 * (64 * (64 * 2 + 16) + 64 * 64 * 2));
+    attr_done = true;
+  }
+  if (D == 128) {
+    const size_t lds = 2 * (64 * (128 * 2 + 16) + 64 * 128 * 2);
+    hipLaunchKernelGGL(prefill_kernel<128>, grid, blk, lds, st, (const uint16_t*)q, q_stride,
+                       (const uint16_t*)kc, (const uint16_t*)vc, block_stride, bs, block_tables,
+                       bt_stride, q_start, q_len, ctx_len, items, Hq, Hkv, G, HPW, scale_log2,
+                       window, sinks, (uint16_t*)out, out_stride);
+  } else if (D == 64) {
+    const size_t lds = 2 * (64 * (64 * 2 + 16) + 64 * 64 * 2);
+    hipLaunchKernelGGL(prefill_kernel<64>, grid, blk, lds, st, (const uint16_t*)q, q_stride,
+                       (const uint16_t*)kc, (const uint16_t*)vc, block_stride, bs, block_tables,
+                       bt_stride, q_start, q_len, ctx_len, items, Hq, Hkv, G, HPW, scale_log2,
+                       window, sinks, (uint16_t*)out, out_stride);
+  } else {
+    return -1;
+  }
+  return 0;
+}
+
+// tokens per work item for a given GQA group size (host helper, mirrors the kernel)
+extern "C" int llmd_prefill_tokens_per_item(int Hq, int Hkv) {
+  const int G = Hq / Hkv;
+  const int HPW = (G % 4 == 0) ? 4 : ((G % 2 == 0) ? 2 : 1);
+  return 32 * (4 / HPW);
+}

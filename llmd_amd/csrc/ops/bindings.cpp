@@ -1,0 +1,219 @@
+// Python bindings for the llmd_amd HIP op library. Host C++ only (compiled by
+// g++ against the torch headers); the kernels live in the *.hip translation
+// units and are reached through their extern "C" launchers. Every binding
+// checks device, dtype, contiguity of the inner dimension and the shapes the
+// kernel's grid assumes, so a bad call raises instead of faulting the GPU.
+#include <torch/extension.h>
+#include <c10/hip/HIPStream.h>
+#include <hip/hip_runtime.h>
+
+extern "C" {
+void llmd_rms_norm(void*, int64_t, const void*, int64_t, const void*, int, int, float, hipStream_t);
+void llmd_fused_add_rms_norm(void*, int64_t, void*, int64_t, const void*, int, int, float,
+                             hipStream_t);
+void llmd_rope_cache(void*, int64_t, const int64_t*, const float*, int, int, int, int,
+                     const int64_t*, void*, void*, int64_t, int, int, int, hipStream_t);
+void llmd_gated_act(void*, int64_t, const void*, int64_t, int, int, int, float, float, hipStream_t);
+int llmd_paged_decode(const void*, int64_t, const void*, const void*, int64_t, int, const int*, int,
+                      const int*, int, int, int, int, float, int, const float*, int, int, void*,
+                      int64_t, float*, float*, hipStream_t);
+int llmd_paged_prefill(const void*, int64_t, const void*, const void*, int64_t, int, const int*, int,
+                       const int*, const int*, const int*, const int*, int, int, int, int, float,
+                       int, const float*, void*, int64_t, hipStream_t);
+int llmd_prefill_tokens_per_item(int, int);
+void llmd_sample(const void*, int64_t, int, int, int, const float*, const int64_t*, int64_t*, float*,
+                 hipStream_t);
+void llmd_topk_topp_mask(float*, int64_t, int, int, const int*, const float*, const float*,
+                         hipStream_t);
+}
+
+namespace {
+
+hipStream_t cur_stream() { return c10::hip::getCurrentHIPStream().stream(); }
+
+#define CHECK_CUDA(x) TORCH_CHECK((x).is_cuda(), #x " must be a GPU tensor")
+#define CHECK_BF16(x) TORCH_CHECK((x).scalar_type() == at::kBFloat16, #x " must be bf16")
+#define CHECK_INNER(x) TORCH_CHECK((x).stride(-1) == 1, #x " inner dim must be contiguous")
+#define CHECK_DT(x, t) TORCH_CHECK((x).scalar_type() == (t), #x " has wrong dtype")
+
+void rms_norm(torch::Tensor out, torch::Tensor x, torch::Tensor w, double eps) {
+  CHECK_CUDA(x); CHECK_BF16(x); CHECK_BF16(out); CHECK_BF16(w);
+  CHECK_INNER(x); CHECK_INNER(out);
+  TORCH_CHECK(x.dim() == 2 && out.dim() == 2 && w.is_contiguous(), "rms_norm: 2-D x/out");
+  const int d = x.size(1);
+  TORCH_CHECK(d % 8 == 0 && w.numel() == d && out.size(1) == d && out.size(0) == x.size(0),
+              "rms_norm shape");
+  TORCH_CHECK(x.stride(0) % 8 == 0 && out.stride(0) % 8 == 0, "rms_norm: 16-B aligned rows");
+  llmd_rms_norm(out.data_ptr(), out.stride(0), x.data_ptr(), x.stride(0), w.data_ptr(), x.size(0), d,
+                (float)eps, cur_stream());
+}
+
+void fused_add_rms_norm(torch::Tensor x, torch::Tensor residual, torch::Tensor w, double eps) {
+  CHECK_CUDA(x); CHECK_BF16(x); CHECK_BF16(residual); CHECK_BF16(w);
+  CHECK_INNER(x); CHECK_INNER(residual);
+  TORCH_CHECK(x.dim() == 2 && residual.sizes() == x.sizes(), "fused_add_rms_norm shape");
+  const int d = x.size(1);
+  TORCH_CHECK(d % 8 == 0 && w.numel() == d && w.is_contiguous(), "fused_add_rms_norm d");
+  TORCH_CHECK(x.stride(0) % 8 == 0 && residual.stride(0) % 8 == 0, "16-B aligned rows");
+  llmd_fused_add_rms_norm(x.data_ptr(), x.stride(0), residual.data_ptr(), residual.stride(0),
+                          w.data_ptr(), x.size(0), d, (float)eps, cur_stream());
+}
+
+// qkv [T, (Hq+2Hkv)*D]; k_cache/v_cache: per-layer strided views
+// [num_blocks, Hkv, bs, D] (block stride arbitrary, inner [Hkv,bs,D] contiguous)
+void rope_cache(torch::Tensor qkv, torch::Tensor positions, torch::Tensor cos_sin, int64_t Hq,
+                int64_t Hkv, int64_t D, torch::Tensor slots, torch::Tensor k_cache,
+                torch::Tensor v_cache, bool neox) {
+  CHECK_CUDA(qkv); CHECK_BF16(qkv); CHECK_INNER(qkv);
+  CHECK_DT(positions, at::kLong); CHECK_DT(slots, at::kLong); CHECK_DT(cos_sin, at::kFloat);
+  TORCH_CHECK(qkv.dim() == 2 && qkv.size(1) >= (Hq + 2 * Hkv) * D, "rope_cache: qkv width");
+  const int T = qkv.size(0);
+  TORCH_CHECK(positions.numel() == T && slots.numel() == T, "rope_cache: T mismatch");
+  TORCH_CHECK(cos_sin.dim() == 2 && cos_sin.is_contiguous(), "cos_sin 2-D contiguous");
+  const int rot = cos_sin.size(1);
+  TORCH_CHECK(rot % 16 == 0 && rot <= D && D % 8 == 0, "rope_cache: rotary dim");
+  TORCH_CHECK(qkv.stride(0) % 8 == 0, "rope_cache: 16-B aligned rows");
+  CHECK_BF16(k_cache); CHECK_BF16(v_cache);
+  TORCH_CHECK(k_cache.dim() == 4 && k_cache.size(1) == Hkv && k_cache.size(3) == D,
+              "k_cache [blocks, Hkv, bs, D]");
+  TORCH_CHECK(k_cache.stride(3) == 1 && k_cache.stride(2) == D && k_cache.stride(1) == k_cache.size(2) * D,
+              "k_cache inner layout");
+  TORCH_CHECK(v_cache.sizes() == k_cache.sizes() && v_cache.strides() == k_cache.strides(),
+              "v_cache layout");
+  llmd_rope_cache(qkv.data_ptr(), qkv.stride(0), positions.data_ptr<int64_t>(),
+                  cos_sin.data_ptr<float>(), rot, Hq, Hkv, D, slots.data_ptr<int64_t>(),
+                  k_cache.data_ptr(), v_cache.data_ptr(), k_cache.stride(0), k_cache.size(2), T,
+                  neox ? 1 : 0, cur_stream());
+}
+
+void gated_act(torch::Tensor out, torch::Tensor x, int64_t mode, double alpha, double limit) {
+  CHECK_CUDA(x); CHECK_BF16(x); CHECK_BF16(out); CHECK_INNER(x); CHECK_INNER(out);
+  TORCH_CHECK(x.dim() == 2 && out.dim() == 2 && x.size(0) == out.size(0), "gated_act shape");
+  const int F = out.size(1);
+  TORCH_CHECK(x.size(1) == 2 * F && F % 8 == 0, "gated_act: x must be [T, 2F], F % 8 == 0");
+  TORCH_CHECK(x.stride(0) % 8 == 0 && out.stride(0) % 8 == 0, "16-B aligned rows");
+  llmd_gated_act(out.data_ptr(), out.stride(0), x.data_ptr(), x.stride(0), x.size(0), F, (int)mode,
+                 (float)alpha, (float)limit, cur_stream());
+}
+
+void check_cache(const torch::Tensor& k, const torch::Tensor& v, int64_t Hkv, int64_t D) {
+  CHECK_BF16(k); CHECK_BF16(v);
+  TORCH_CHECK(k.dim() == 4 && k.size(1) == Hkv && k.size(3) == D, "cache [blocks, Hkv, bs, D]");
+  TORCH_CHECK(k.stride(3) == 1 && k.stride(2) == D && k.stride(1) == k.size(2) * D,
+              "cache inner layout");
+  TORCH_CHECK(v.sizes() == k.sizes() && v.strides() == k.strides(), "v_cache layout");
+}
+
+// q [B, >=Hq*D] (token stride), out [B, Hq*D]
+void paged_decode(torch::Tensor out, torch::Tensor q, torch::Tensor k_cache, torch::Tensor v_cache,
+                  torch::Tensor block_tables, torch::Tensor seq_lens, int64_t Hq, int64_t Hkv,
+                  int64_t D, double scale, int64_t window, c10::optional<torch::Tensor> sinks,
+                  int64_t split_size, int64_t nsplit, torch::Tensor part_o, torch::Tensor part_ml) {
+  CHECK_CUDA(q); CHECK_BF16(q); CHECK_BF16(out); CHECK_INNER(q); CHECK_INNER(out);
+  check_cache(k_cache, v_cache, Hkv, D);
+  CHECK_DT(block_tables, at::kInt); CHECK_DT(seq_lens, at::kInt);
+  TORCH_CHECK(block_tables.dim() == 2 && block_tables.stride(1) == 1, "block_tables 2-D");
+  const int B = q.size(0);
+  TORCH_CHECK(seq_lens.numel() == B && block_tables.size(0) >= B, "decode: batch mismatch");
+  TORCH_CHECK(Hq % Hkv == 0 && (D == 64 || D == 128), "decode: heads/D");
+  TORCH_CHECK(q.size(1) >= Hq * D && out.size(0) >= B && out.size(1) >= Hq * D, "decode: widths");
+  TORCH_CHECK(split_size % 64 == 0 && split_size > 0 && nsplit >= 1, "decode: split");
+  TORCH_CHECK(q.stride(0) % 8 == 0, "decode: 16-B aligned q rows");
+  const float* sk = nullptr;
+  if (sinks.has_value()) {
+    CHECK_DT(sinks.value(), at::kFloat);
+    TORCH_CHECK(sinks->numel() == Hq, "sinks [Hq]");
+    sk = sinks->data_ptr<float>();
+  }
+  if (nsplit > 1) {
+    CHECK_DT(part_o, at::kFloat); CHECK_DT(part_ml, at::kFloat);
+    TORCH_CHECK(part_o.numel() >= (int64_t)B * Hq * nsplit * D &&
+                    part_ml.numel() >= (int64_t)B * Hq * nsplit * 2, "decode workspace too small");
+  }
+  // the host must guarantee ctx <= nsplit*split_size (checked by the caller, no sync here)
+  int rc = llmd_paged_decode(q.data_ptr(), q.stride(0), k_cache.data_ptr(), v_cache.data_ptr(),
+                             k_cache.stride(0), k_cache.size(2), block_tables.data_ptr<int>(),
+                             block_tables.stride(0), seq_lens.data_ptr<int>(), B, Hq, Hkv, D,
+                             (float)scale, (int)window, sk, split_size, nsplit, out.data_ptr(),
+                             out.stride(0), nsplit > 1 ? part_o.data_ptr<float>() : nullptr,
+                             nsplit > 1 ? part_ml.data_ptr<float>() : nullptr, cur_stream());
+  TORCH_CHECK(rc == 0, "paged_decode: unsupported head dim");
+}
+
+void paged_prefill(torch::Tensor out, torch::Tensor q, torch::Tensor k_cache,
+                   torch::Tensor v_cache, torch::Tensor block_tables, torch::Tensor q_start,
+                   torch::Tensor q_len, torch::Tensor ctx_len, torch::Tensor items, int64_t Hq,
+                   int64_t Hkv, int64_t D, double scale, int64_t window,
+                   c10::optional<torch::Tensor> sinks) {
+  CHECK_CUDA(q); CHECK_BF16(q); CHECK_BF16(out); CHECK_INNER(q); CHECK_INNER(out);
+  check_cache(k_cache, v_cache, Hkv, D);
+  CHECK_DT(block_tables, at::kInt); CHECK_DT(q_start, at::kInt); CHECK_DT(q_len, at::kInt);
+  CHECK_DT(ctx_len, at::kInt); CHECK_DT(items, at::kInt);
+  TORCH_CHECK(block_tables.dim() == 2 && block_tables.stride(1) == 1, "block_tables 2-D");
+  TORCH_CHECK(items.dim() == 2 && items.size(1) == 2 && items.is_contiguous(), "items [n, 2]");
+  TORCH_CHECK(Hq % Hkv == 0 && (D == 64 || D == 128), "prefill: heads/D");
+  TORCH_CHECK(q.size(1) >= Hq * D && out.size(1) >= Hq * D && out.size(0) >= q.size(0), "widths");
+  TORCH_CHECK(q.stride(0) % 8 == 0, "prefill: 16-B aligned q rows");
+  const float* sk = nullptr;
+  if (sinks.has_value()) {
+    CHECK_DT(sinks.value(), at::kFloat);
+    TORCH_CHECK(sinks->numel() == Hq, "sinks [Hq]");
+    sk = sinks->data_ptr<float>();
+  }
+  int rc = llmd_paged_prefill(q.data_ptr(), q.stride(0), k_cache.data_ptr(), v_cache.data_ptr(),
+                              k_cache.stride(0), k_cache.size(2), block_tables.data_ptr<int>(),
+                              block_tables.stride(0), q_start.data_ptr<int>(),
+                              q_len.data_ptr<int>(), ctx_len.data_ptr<int>(),
+                              items.data_ptr<int>(), items.size(0), Hq, Hkv, D, (float)scale,
+                              (int)window, sk, out.data_ptr(), out.stride(0), cur_stream());
+  TORCH_CHECK(rc == 0, "paged_prefill: unsupported head dim");
+}
+
+void sample(torch::Tensor logits, c10::optional<torch::Tensor> temps,
+            c10::optional<torch::Tensor> seeds, torch::Tensor out_ids,
+            c10::optional<torch::Tensor> out_logprob) {
+  CHECK_CUDA(logits); CHECK_INNER(logits);
+  TORCH_CHECK(logits.dim() == 2, "logits 2-D");
+  const bool bf = logits.scalar_type() == at::kBFloat16;
+  TORCH_CHECK(bf || logits.scalar_type() == at::kFloat, "logits bf16/f32");
+  const int B = logits.size(0), V = logits.size(1);
+  TORCH_CHECK(logits.stride(0) % (bf ? 8 : 4) == 0, "16-B aligned logits rows");
+  CHECK_DT(out_ids, at::kLong);
+  TORCH_CHECK(out_ids.numel() >= B, "out_ids");
+  const float* t = nullptr;
+  const int64_t* s = nullptr;
+  float* lp = nullptr;
+  if (temps.has_value()) { CHECK_DT(temps.value(), at::kFloat); TORCH_CHECK(temps->numel() >= B); t = temps->data_ptr<float>(); }
+  if (seeds.has_value()) { CHECK_DT(seeds.value(), at::kLong); TORCH_CHECK(seeds->numel() >= B); s = seeds->data_ptr<int64_t>(); }
+  if (out_logprob.has_value()) { CHECK_DT(out_logprob.value(), at::kFloat); lp = out_logprob->data_ptr<float>(); }
+  llmd_sample(logits.data_ptr(), logits.stride(0), B, V, bf ? 1 : 0, t, s,
+              out_ids.data_ptr<int64_t>(), lp, cur_stream());
+}
+
+void topk_topp_mask(torch::Tensor logits, c10::optional<torch::Tensor> topk,
+                    c10::optional<torch::Tensor> topp, c10::optional<torch::Tensor> temps) {
+  CHECK_CUDA(logits); CHECK_DT(logits, at::kFloat); CHECK_INNER(logits);
+  const int B = logits.size(0), V = logits.size(1);
+  const int* k = nullptr;
+  const float* p = nullptr;
+  const float* t = nullptr;
+  if (topk.has_value()) { CHECK_DT(topk.value(), at::kInt); TORCH_CHECK(topk->numel() >= B); k = topk->data_ptr<int>(); }
+  if (topp.has_value()) { CHECK_DT(topp.value(), at::kFloat); TORCH_CHECK(topp->numel() >= B); p = topp->data_ptr<float>(); }
+  if (temps.has_value()) { CHECK_DT(temps.value(), at::kFloat); TORCH_CHECK(temps->numel() >= B); t = temps->data_ptr<float>(); }
+  llmd_topk_topp_mask(logits.data_ptr<float>(), logits.stride(0), B, V, k, p, t, cur_stream());
+}
+
+}  // namespace
+
+PYBIND11_MODULE(_C, m) {
+  m.doc() = "llmd_amd HIP/CDNA4 op library (gfx950)";
+  m.def("rms_norm", &rms_norm);
+  m.def("fused_add_rms_norm", &fused_add_rms_norm);
+  m.def("rope_cache", &rope_cache);
+  m.def("gated_act", &gated_act);
+  m.def("paged_decode", &paged_decode);
+  m.def("paged_prefill", &paged_prefill);
+  m.def("prefill_tokens_per_item", &llmd_prefill_tokens_per_item);
+  m.def("sample", &sample);
+  m.def("topk_topp_mask", &topk_topp_mask);
+}

@@ -1,0 +1,11 @@
+// pybind11 module for the llmd_amd host runtime (`llmd_amd._rt`).
+#include <pybind11/pybind11.h>
+
+namespace py = pybind11;
+
+void register_block_manager(py::module_& m);
+
+PYBIND11_MODULE(_rt, m) {
+  m.doc() = "llmd_amd native host runtime";
+  register_block_manager(m);
+}

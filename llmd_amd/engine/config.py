@@ -1,0 +1,299 @@
+"""Typed engine configuration with vLLM-compatible flag names.
+
+Model architectures are described by ``ModelConfig`` (HF ``config.json``
+field names). Presets cover the model families the reference's well-lit paths
+deploy (SURVEY §2.3 shapes): Llama-3 8B/70B, Qwen3-32B, gpt-oss-20b/120b,
+DeepSeek-V3/R1 (+ V2-Lite for scaled-down CI, reference
+``.github/scripts/e2e/wide-ep-transform.sh:15-138``), OPT-125m-sized tiny
+models for the CPU path, plus random tiny variants for tests.
+"""
+from __future__ import annotations
+
+import argparse
+import dataclasses
+import json
+import os
+from dataclasses import dataclass, field
+from typing import Any, Optional
+
+
+@dataclass
+class ModelConfig:
+    model_type: str = "llama"
+    hidden_size: int = 4096
+    intermediate_size: int = 14336
+    num_hidden_layers: int = 32
+    num_attention_heads: int = 32
+    num_key_value_heads: int = 8
+    head_dim: Optional[int] = None
+    vocab_size: int = 128256
+    max_position_embeddings: int = 131072
+    rope_theta: float = 500000.0
+    rope_scaling: Optional[dict] = None
+    rms_norm_eps: float = 1e-5
+    tie_word_embeddings: bool = False
+    hidden_act: str = "silu"
+    attention_bias: bool = False
+    bos_token_id: int = 128000
+    eos_token_id: Any = 128001
+    # sliding window / sinks (gpt-oss): layer_types[i] in {"full_attention","sliding_attention"}
+    sliding_window: int = 0
+    layer_types: Optional[list] = None
+    attention_sinks: bool = False
+    # MoE (gpt-oss / DeepSeek / Mixtral)
+    num_local_experts: int = 0
+    num_experts_per_tok: int = 0
+    moe_intermediate_size: int = 0
+    n_shared_experts: int = 0
+    first_k_dense_replace: int = 0
+    router_aux_bias: bool = False
+    swiglu_limit: float = 7.0
+    # MLA (DeepSeek)
+    q_lora_rank: Optional[int] = None
+    kv_lora_rank: int = 0
+    qk_nope_head_dim: int = 0
+    qk_rope_head_dim: int = 0
+    v_head_dim: int = 0
+    name: str = "custom"
+
+    def __post_init__(self):
+        if self.head_dim is None:
+            self.head_dim = self.hidden_size // self.num_attention_heads
+
+    @property
+    def is_moe(self) -> bool:
+        return self.num_local_experts > 0
+
+    @property
+    def eos_ids(self) -> list[int]:
+        e = self.eos_token_id
+        return list(e) if isinstance(e, (list, tuple)) else [int(e)]
+
+    def layer_window(self, i: int) -> int:
+        if self.layer_types and self.layer_types[i] == "sliding_attention":
+            return self.sliding_window
+        return 0
+
+    def num_params(self) -> int:
+        d, L = self.hidden_size, self.num_hidden_layers
+        hd = self.head_dim
+        attn = d * (self.num_attention_heads + 2 * self.num_key_value_heads) * hd + self.num_attention_heads * hd * d
+        if self.is_moe:
+            mlp = self.num_local_experts * 3 * d * self.moe_intermediate_size + d * self.num_local_experts
+        else:
+            mlp = 3 * d * self.intermediate_size
+        emb = self.vocab_size * d * (1 if self.tie_word_embeddings else 2)
+        return L * (attn + mlp + 2 * d) + emb + d
+
+    @classmethod
+    def from_hf(cls, path_or_dict) -> "ModelConfig":
+        if isinstance(path_or_dict, (str, os.PathLike)):
+            p = os.path.join(path_or_dict, "config.json") if os.path.isdir(path_or_dict) else path_or_dict
+            with open(p) as f:
+                d = json.load(f)
+        else:
+            d = dict(path_or_dict)
+        names = {f.name for f in dataclasses.fields(cls)}
+        kw = {k: v for k, v in d.items() if k in names}
+        if "num_experts" in d and "num_local_experts" not in d:
+            kw["num_local_experts"] = d["num_experts"]
+        if "n_routed_experts" in d:
+            kw["num_local_experts"] = d["n_routed_experts"]
+        if d.get("model_type") == "gpt_oss":
+            kw.setdefault("moe_intermediate_size", d.get("intermediate_size", 0))
+            kw["attention_sinks"] = True
+            kw["attention_bias"] = True
+        return cls(**kw)
+
+
+def _llama(name, d, ffn, L, hq, hkv, vocab=128256, **kw):
+    base = dict(model_type="llama", hidden_size=d, intermediate_size=ffn, num_hidden_layers=L,
+                num_attention_heads=hq, num_key_value_heads=hkv, vocab_size=vocab, name=name,
+                rope_theta=500000.0,
+                rope_scaling={"rope_type": "llama3", "factor": 8.0, "low_freq_factor": 1.0,
+                              "high_freq_factor": 4.0, "original_max_position_embeddings": 8192})
+    base.update(kw)
+    return ModelConfig(**base)
+
+
+PRESETS: dict[str, ModelConfig] = {}
+
+
+def _register(cfg: ModelConfig, *aliases):
+    PRESETS[cfg.name] = cfg
+    for a in aliases:
+        PRESETS[a] = cfg
+
+
+_register(_llama("llama-3-8b", 4096, 14336, 32, 32, 8), "meta-llama/Meta-Llama-3-8B",
+          "meta-llama/Llama-3.1-8B-Instruct", "Llama-3-8B")
+_register(_llama("llama-3-70b", 8192, 28672, 80, 64, 8), "meta-llama/Meta-Llama-3-70B",
+          "meta-llama/Llama-3.3-70B-Instruct", "Llama-3-70B", "amd/Llama-3.3-70B-Instruct-FP8-KV")
+_register(ModelConfig(model_type="qwen3", name="qwen3-32b", hidden_size=5120, intermediate_size=25600,
+                      num_hidden_layers=64, num_attention_heads=64, num_key_value_heads=8, head_dim=128,
+                      vocab_size=151936, rope_theta=1000000.0, rms_norm_eps=1e-6,
+                      bos_token_id=151643, eos_token_id=151645), "Qwen/Qwen3-32B")
+_register(ModelConfig(model_type="gpt_oss", name="gpt-oss-120b", hidden_size=2880, intermediate_size=2880,
+                      moe_intermediate_size=2880, num_hidden_layers=36, num_attention_heads=64,
+                      num_key_value_heads=8, head_dim=64, vocab_size=201088, rope_theta=150000.0,
+                      rope_scaling={"rope_type": "yarn", "factor": 32.0, "beta_fast": 32.0, "beta_slow": 1.0,
+                                    "original_max_position_embeddings": 4096},
+                      num_local_experts=128, num_experts_per_tok=4, sliding_window=128,
+                      layer_types=["sliding_attention", "full_attention"] * 18, attention_sinks=True,
+                      attention_bias=True, bos_token_id=199998, eos_token_id=[200002, 199999]),
+          "openai/gpt-oss-120b")
+_register(ModelConfig(model_type="gpt_oss", name="gpt-oss-20b", hidden_size=2880, intermediate_size=2880,
+                      moe_intermediate_size=2880, num_hidden_layers=24, num_attention_heads=64,
+                      num_key_value_heads=8, head_dim=64, vocab_size=201088, rope_theta=150000.0,
+                      rope_scaling={"rope_type": "yarn", "factor": 32.0, "beta_fast": 32.0, "beta_slow": 1.0,
+                                    "original_max_position_embeddings": 4096},
+                      num_local_experts=32, num_experts_per_tok=4, sliding_window=128,
+                      layer_types=["sliding_attention", "full_attention"] * 12, attention_sinks=True,
+                      attention_bias=True, bos_token_id=199998, eos_token_id=[200002, 199999]),
+          "openai/gpt-oss-20b")
+# tiny configs (CPU CI, smoke, GPU unit tests)
+_register(ModelConfig(model_type="llama", name="tiny-llama", hidden_size=256, intermediate_size=512,
+                      num_hidden_layers=2, num_attention_heads=4, num_key_value_heads=2, head_dim=64,
+                      vocab_size=512, max_position_embeddings=4096, rope_theta=10000.0,
+                      bos_token_id=1, eos_token_id=2))
+_register(ModelConfig(model_type="llama", name="small-llama", hidden_size=1024, intermediate_size=2816,
+                      num_hidden_layers=4, num_attention_heads=8, num_key_value_heads=2, head_dim=128,
+                      vocab_size=32000, max_position_embeddings=8192, rope_theta=10000.0,
+                      bos_token_id=1, eos_token_id=2), "opt-125m-sized")
+_register(ModelConfig(model_type="gpt_oss", name="tiny-gpt-oss", hidden_size=256, intermediate_size=256,
+                      moe_intermediate_size=256, num_hidden_layers=2, num_attention_heads=8,
+                      num_key_value_heads=2, head_dim=64, vocab_size=512, rope_theta=10000.0,
+                      num_local_experts=8, num_experts_per_tok=2, sliding_window=16,
+                      layer_types=["sliding_attention", "full_attention"], attention_sinks=True,
+                      attention_bias=True, bos_token_id=1, eos_token_id=2))
+
+
+def get_model_config(name_or_path: str) -> ModelConfig:
+    if name_or_path in PRESETS:
+        return dataclasses.replace(PRESETS[name_or_path])
+    if os.path.exists(name_or_path):
+        return ModelConfig.from_hf(name_or_path)
+    raise ValueError(f"unknown model {name_or_path!r}; presets: {sorted(set(c.name for c in PRESETS.values()))}")
+
+
+@dataclass
+class CacheConfig:
+    block_size: int = 64
+    gpu_memory_utilization: float = 0.92
+    kv_cache_memory_bytes: Optional[int] = None
+    num_gpu_blocks: Optional[int] = None
+    enable_prefix_caching: bool = True
+    kv_cache_dtype: str = "auto"
+
+
+@dataclass
+class SchedulerConfig:
+    max_num_seqs: int = 256
+    max_num_batched_tokens: int = 8192
+    max_model_len: int = 32768
+    enable_chunked_prefill: bool = True
+    policy: str = "fcfs"  # or "priority"
+    long_prefill_token_threshold: int = 0
+
+
+@dataclass
+class ParallelConfig:
+    tensor_parallel_size: int = 1
+    data_parallel_size: int = 1
+    data_parallel_rank: int = 0
+    enable_expert_parallel: bool = False
+    distributed_backend: str = "nccl"
+
+
+@dataclass
+class EngineConfig:
+    model: str = "tiny-llama"
+    model_config: ModelConfig = field(default_factory=ModelConfig)
+    cache: CacheConfig = field(default_factory=CacheConfig)
+    sched: SchedulerConfig = field(default_factory=SchedulerConfig)
+    parallel: ParallelConfig = field(default_factory=ParallelConfig)
+    device: str = "cuda"
+    dtype: str = "bfloat16"
+    seed: int = 0
+    load_format: str = "dummy"  # "dummy" (random init) | "safetensors"
+    weights_path: Optional[str] = None
+    tokenizer: Optional[str] = None
+    served_model_name: Optional[str] = None
+    enforce_eager: bool = False
+    cuda_graph_max_bs: int = 256
+    kv_transfer_config: Optional[dict] = None
+    kv_events_config: Optional[dict] = None
+    kv_offload_config: Optional[dict] = None
+    max_loras: int = 0
+    enable_lora: bool = False
+
+    @property
+    def served_name(self) -> str:
+        return self.served_model_name or self.model
+
+    @classmethod
+    def create(cls, model: str = "tiny-llama", **kw) -> "EngineConfig":
+        mc = kw.pop("model_config", None) or get_model_config(model)
+        sub = {"cache": CacheConfig, "sched": SchedulerConfig, "parallel": ParallelConfig}
+        parts = {k: c() for k, c in sub.items()}
+        top = {}
+        for k, v in kw.items():
+            placed = False
+            for name, c in sub.items():
+                if k in {f.name for f in dataclasses.fields(c)}:
+                    setattr(parts[name], k, v)
+                    placed = True
+            if not placed:
+                top[k] = v
+        cfg = cls(model=model, model_config=mc, **parts, **top)
+        cfg.sched.max_model_len = min(cfg.sched.max_model_len, mc.max_position_embeddings)
+        return cfg
+
+
+def _json_arg(s):
+    return json.loads(s) if s else None
+
+
+def add_engine_args(p: argparse.ArgumentParser) -> argparse.ArgumentParser:
+    """vLLM-compatible engine flags (subset with identical semantics)."""
+    p.add_argument("--model", default="tiny-llama")
+    p.add_argument("--served-model-name", default=None)
+    p.add_argument("--tokenizer", default=None)
+    p.add_argument("--load-format", default="dummy", choices=["dummy", "safetensors", "auto"])
+    p.add_argument("--weights-path", default=None)
+    p.add_argument("--dtype", default="bfloat16")
+    p.add_argument("--device", default="cuda")
+    p.add_argument("--seed", type=int, default=0)
+    p.add_argument("--block-size", type=int, default=64)
+    p.add_argument("--gpu-memory-utilization", type=float, default=0.92)
+    p.add_argument("--kv-cache-memory-bytes", type=int, default=None)
+    p.add_argument("--num-gpu-blocks-override", type=int, default=None)
+    p.add_argument("--no-enable-prefix-caching", action="store_true")
+    p.add_argument("--max-num-seqs", type=int, default=256)
+    p.add_argument("--max-num-batched-tokens", type=int, default=8192)
+    p.add_argument("--max-model-len", type=int, default=32768)
+    p.add_argument("--tensor-parallel-size", "-tp", type=int, default=1)
+    p.add_argument("--data-parallel-size", "-dp", type=int, default=1)
+    p.add_argument("--data-parallel-rank", type=int, default=0)
+    p.add_argument("--enable-expert-parallel", action="store_true")
+    p.add_argument("--enforce-eager", action="store_true")
+    p.add_argument("--kv-transfer-config", type=_json_arg, default=None)
+    p.add_argument("--kv-events-config", type=_json_arg, default=None)
+    p.add_argument("--kv-offload-config", type=_json_arg, default=None)
+    p.add_argument("--scheduling-policy", default="fcfs", choices=["fcfs", "priority"])
+    return p
+
+
+def engine_config_from_args(a) -> EngineConfig:
+    return EngineConfig.create(
+        a.model, served_model_name=a.served_model_name, tokenizer=a.tokenizer,
+        load_format=a.load_format, weights_path=a.weights_path, dtype=a.dtype, device=a.device,
+        seed=a.seed, block_size=a.block_size, gpu_memory_utilization=a.gpu_memory_utilization,
+        kv_cache_memory_bytes=a.kv_cache_memory_bytes, num_gpu_blocks=a.num_gpu_blocks_override,
+        enable_prefix_caching=not a.no_enable_prefix_caching, max_num_seqs=a.max_num_seqs,
+        max_num_batched_tokens=a.max_num_batched_tokens, max_model_len=a.max_model_len,
+        tensor_parallel_size=a.tensor_parallel_size, data_parallel_size=a.data_parallel_size,
+        data_parallel_rank=a.data_parallel_rank, enable_expert_parallel=a.enable_expert_parallel,
+        enforce_eager=a.enforce_eager, kv_transfer_config=a.kv_transfer_config,
+        kv_events_config=a.kv_events_config, kv_offload_config=a.kv_offload_config,
+        policy=a.scheduling_policy)

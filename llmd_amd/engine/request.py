@@ -1,0 +1,134 @@
+"""Request, sampling parameters and per-step outputs."""
+from __future__ import annotations
+
+import enum
+import itertools
+import time
+from dataclasses import dataclass, field
+from typing import Any, Optional
+
+
+@dataclass
+class SamplingParams:
+    max_tokens: int = 16
+    temperature: float = 1.0
+    top_p: float = 1.0
+    top_k: int = 0
+    min_tokens: int = 0
+    seed: Optional[int] = None
+    stop_token_ids: list[int] = field(default_factory=list)
+    stop: list[str] = field(default_factory=list)
+    ignore_eos: bool = False
+    logprobs: Optional[int] = None
+    n: int = 1
+
+    @property
+    def greedy(self) -> bool:
+        return self.temperature <= 0.0
+
+    @classmethod
+    def from_openai(cls, body: dict, default_max: int = 16) -> "SamplingParams":
+        stop = body.get("stop") or []
+        if isinstance(stop, str):
+            stop = [stop]
+        mt = body.get("max_completion_tokens", body.get("max_tokens"))
+        return cls(
+            max_tokens=int(mt) if mt is not None else default_max,
+            temperature=float(body.get("temperature", 1.0) if body.get("temperature") is not None else 1.0),
+            top_p=float(body.get("top_p", 1.0) or 1.0),
+            top_k=int(body.get("top_k", 0) or 0),
+            min_tokens=int(body.get("min_tokens", 0) or 0),
+            seed=body.get("seed"),
+            stop_token_ids=list(body.get("stop_token_ids") or []),
+            stop=stop,
+            ignore_eos=bool(body.get("ignore_eos", False)),
+            logprobs=body.get("logprobs") if isinstance(body.get("logprobs"), int) else (
+                1 if body.get("logprobs") is True else None),
+        )
+
+
+class Status(enum.Enum):
+    WAITING = 0
+    RUNNING = 1
+    PREEMPTED = 2
+    WAITING_FOR_REMOTE_KV = 3
+    FINISHED_STOPPED = 10
+    FINISHED_LENGTH = 11
+    FINISHED_ABORTED = 12
+    FINISHED_ERROR = 13
+
+    @property
+    def finished(self) -> bool:
+        return self.value >= 10
+
+
+FINISH_REASON = {
+    Status.FINISHED_STOPPED: "stop",
+    Status.FINISHED_LENGTH: "length",
+    Status.FINISHED_ABORTED: "abort",
+    Status.FINISHED_ERROR: "error",
+}
+
+_seq_counter = itertools.count(1)
+
+
+@dataclass
+class Request:
+    request_id: str
+    prompt_token_ids: list[int]
+    params: SamplingParams = field(default_factory=SamplingParams)
+    priority: int = 0
+    arrival_time: float = field(default_factory=time.monotonic)
+    lora_id: int = 0
+    # P/D disaggregation (vLLM NixlConnector-compatible kv_transfer_params)
+    kv_transfer_params: Optional[dict] = None
+    status: Status = Status.WAITING
+    output_token_ids: list[int] = field(default_factory=list)
+    output_logprobs: list[float] = field(default_factory=list)
+    num_computed_tokens: int = 0
+    num_cached_tokens: int = 0
+    num_preemptions: int = 0
+    seq_id: int = field(default_factory=lambda: next(_seq_counter))
+    # timing (monotonic seconds)
+    first_scheduled_time: Optional[float] = None
+    first_token_time: Optional[float] = None
+    last_token_time: Optional[float] = None
+    finished_time: Optional[float] = None
+    stop_reason: Any = None
+    extra: dict = field(default_factory=dict)
+
+    @property
+    def all_token_ids(self) -> list[int]:
+        return self.prompt_token_ids + self.output_token_ids
+
+    @property
+    def num_tokens(self) -> int:
+        return len(self.prompt_token_ids) + len(self.output_token_ids)
+
+    @property
+    def num_prompt_tokens(self) -> int:
+        return len(self.prompt_token_ids)
+
+    @property
+    def is_prefill(self) -> bool:
+        return self.num_computed_tokens < self.num_tokens - 1 or not self.output_token_ids and \
+            self.num_computed_tokens < self.num_prompt_tokens
+
+    @property
+    def finish_reason(self) -> Optional[str]:
+        return FINISH_REASON.get(self.status)
+
+
+@dataclass
+class RequestOutput:
+    request_id: str
+    new_token_ids: list[int]
+    new_logprobs: list[float]
+    finished: bool
+    finish_reason: Optional[str]
+    num_prompt_tokens: int
+    num_output_tokens: int
+    num_cached_tokens: int = 0
+    kv_transfer_params: Optional[dict] = None
+    ttft: Optional[float] = None
+    metrics: Optional[dict] = None

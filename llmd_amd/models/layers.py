@@ -1,0 +1,167 @@
+"""Model building blocks: TP-sharded linears, norms, embeddings, paged attention.
+
+Weights are plain bf16 tensors in [out, in] layout and GEMMs go to hipBLASLt
+through ``torch.nn.functional.linear`` ("hipBLASLt first").
+Fused elementwise work (norm + residual, rope + cache write, gated activation)
+runs in the hand-written HIP kernels of ``llmd_amd.ops``.
+"""
+from __future__ import annotations
+
+import math
+from typing import Optional
+
+import torch
+import torch.nn.functional as F
+
+from llmd_amd import ops
+from llmd_amd.engine.attn_meta import AttnMeta
+from llmd_amd.parallel.comm import tp_all_gather, tp_all_reduce
+from llmd_amd.parallel.state import get_state
+
+
+def _init_weight(t: torch.Tensor, std: float, gen: Optional[torch.Generator] = None):
+    with torch.no_grad():
+        if t.is_cuda:
+            t.normal_(0.0, std, generator=gen)
+        else:
+            t.copy_(torch.randn(t.shape, generator=gen) * std)
+    return t
+
+
+class ColumnLinear(torch.nn.Module):
+    """y = x W^T, W [out/tp, in]; output stays sharded."""
+
+    def __init__(self, in_f: int, out_f: int, bias=False, device=None, dtype=torch.bfloat16,
+                 shard=True, std=0.02):
+        super().__init__()
+        tp = get_state().tp_size if shard else 1
+        assert out_f % tp == 0, (out_f, tp)
+        self.in_f, self.out_f = in_f, out_f // tp
+        self.weight = torch.nn.Parameter(_init_weight(torch.empty(self.out_f, in_f, device=device, dtype=dtype), std),
+                                         requires_grad=False)
+        self.bias = torch.nn.Parameter(torch.zeros(self.out_f, device=device, dtype=dtype),
+                                       requires_grad=False) if bias else None
+
+    def forward(self, x):
+        return F.linear(x, self.weight, self.bias)
+
+
+class RowLinear(torch.nn.Module):
+    """y = all_reduce(x_shard W_shard^T), W [out, in/tp]."""
+
+    def __init__(self, in_f: int, out_f: int, bias=False, device=None, dtype=torch.bfloat16,
+                 reduce=True, std=0.02):
+        super().__init__()
+        tp = get_state().tp_size
+        assert in_f % tp == 0
+        self.in_f, self.out_f, self.reduce = in_f // tp, out_f, reduce
+        self.weight = torch.nn.Parameter(_init_weight(torch.empty(out_f, self.in_f, device=device, dtype=dtype), std),
+                                         requires_grad=False)
+        self.bias = torch.nn.Parameter(torch.zeros(out_f, device=device, dtype=dtype),
+                                       requires_grad=False) if bias else None
+
+    def forward(self, x):
+        y = F.linear(x, self.weight)
+        if self.reduce:
+            y = tp_all_reduce(y)
+        if self.bias is not None:
+            y = y + self.bias
+        return y
+
+
+class RMSNorm(torch.nn.Module):
+    def __init__(self, d: int, eps: float, device=None, dtype=torch.bfloat16):
+        super().__init__()
+        self.eps = eps
+        self.weight = torch.nn.Parameter(torch.ones(d, device=device, dtype=dtype), requires_grad=False)
+
+    def forward(self, x, residual: Optional[torch.Tensor] = None):
+        if residual is None:
+            return ops.rms_norm(x, self.weight, self.eps)
+        ops.fused_add_rms_norm(x, residual, self.weight, self.eps)
+        return x, residual
+
+
+class VocabEmbedding(torch.nn.Module):
+    """Vocab-parallel embedding: each TP rank holds a vocab slice."""
+
+    def __init__(self, vocab: int, d: int, device=None, dtype=torch.bfloat16):
+        super().__init__()
+        st = get_state()
+        self.tp, self.rank = st.tp_size, st.tp_rank
+        self.vocab = vocab
+        self.per = math.ceil(vocab / self.tp)
+        self.lo = self.rank * self.per
+        self.weight = torch.nn.Parameter(_init_weight(torch.empty(self.per, d, device=device, dtype=dtype), 0.02),
+                                         requires_grad=False)
+
+    def forward(self, ids):
+        if self.tp == 1:
+            return F.embedding(ids, self.weight)
+        local = ids - self.lo
+        mask = (local < 0) | (local >= self.per)
+        out = F.embedding(local.clamp(0, self.per - 1), self.weight)
+        out.masked_fill_(mask[:, None], 0)
+        return tp_all_reduce(out)
+
+
+class LMHead(torch.nn.Module):
+    def __init__(self, vocab: int, d: int, device=None, dtype=torch.bfloat16, tied: Optional[VocabEmbedding] = None):
+        super().__init__()
+        st = get_state()
+        self.tp = st.tp_size
+        self.vocab = vocab
+        self.per = math.ceil(vocab / self.tp)
+        if tied is not None:
+            self.weight = tied.weight
+        else:
+            self.weight = torch.nn.Parameter(_init_weight(torch.empty(self.per, d, device=device, dtype=dtype), 0.02),
+                                             requires_grad=False)
+
+    def forward(self, h):
+        logits = F.linear(h, self.weight)
+        if self.tp > 1:
+            logits = tp_all_gather(logits, -1)
+        return logits[:, : self.vocab]
+
+
+class PagedAttention(torch.nn.Module):
+    """QKV projection output -> rope + cache write -> decode/prefill attention."""
+
+    def __init__(self, layer_idx: int, num_heads: int, num_kv_heads: int, head_dim: int,
+                 rope_cos_sin: torch.Tensor, window: int = 0, sinks: bool = False, neox: bool = True,
+                 device=None):
+        super().__init__()
+        tp = get_state().tp_size
+        assert num_heads % tp == 0
+        self.layer_idx = layer_idx
+        self.Hq = num_heads // tp
+        self.Hkv = max(1, num_kv_heads // tp)
+        self.D = head_dim
+        self.scale = head_dim ** -0.5
+        self.window = window
+        self.neox = neox
+        self.cos_sin = rope_cos_sin
+        self.sinks = torch.nn.Parameter(torch.zeros(self.Hq, device=device, dtype=torch.float32),
+                                        requires_grad=False) if sinks else None
+        self.k_cache: Optional[torch.Tensor] = None
+        self.v_cache: Optional[torch.Tensor] = None
+
+    def forward(self, qkv: torch.Tensor, meta: AttnMeta) -> torch.Tensor:
+        T = qkv.shape[0]
+        Hq, Hkv, D = self.Hq, self.Hkv, self.D
+        ops.rope_cache(qkv, meta.positions, self.cos_sin, Hq, Hkv, D, meta.slot_mapping,
+                       self.k_cache, self.v_cache, self.neox)
+        out = torch.empty(T, Hq * D, dtype=qkv.dtype, device=qkv.device)
+        nd = meta.num_decode
+        if nd:
+            ops.paged_decode(qkv[:nd], self.k_cache, self.v_cache, meta.d_block_tables,
+                             meta.d_seq_lens, Hq, Hkv, D, self.scale, self.window, self.sinks,
+                             split=meta.d_split, out=out[:nd], workspace=meta.d_workspace,
+                             max_ctx=meta.d_max_ctx)
+        if meta.num_prefill_tokens:
+            items = meta.p_items
+            ops.paged_prefill(qkv[nd:], self.k_cache, self.v_cache, meta.p_block_tables,
+                              meta.p_q_start, meta.p_q_len, meta.p_ctx_len, Hq, Hkv, D, self.scale,
+                              self.window, self.sinks, items=items, out=out[nd:])
+        return out

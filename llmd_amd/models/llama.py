@@ -1,0 +1,109 @@
+"""Llama-family decoder (Llama-3 8B/70B, Qwen3 dense) on the paged-KV engine.
+
+Per layer (dense TP=k):
+  fused_add_rmsnorm -> QKV GEMM -> rope+cache write -> paged attention
+  -> O GEMM (+TP all-reduce) -> fused_add_rmsnorm -> gate_up GEMM
+  -> SiLU*mul -> down GEMM (+TP all-reduce)
+Residual stream is carried separately so every norm fuses the residual add.
+"""
+from __future__ import annotations
+
+import torch
+
+from llmd_amd import ops
+from llmd_amd.engine.attn_meta import AttnMeta
+from llmd_amd.engine.config import ModelConfig
+from llmd_amd.parallel.state import get_state
+
+from .layers import ColumnLinear, LMHead, PagedAttention, RMSNorm, RowLinear, VocabEmbedding
+
+
+class LlamaMLP(torch.nn.Module):
+    def __init__(self, cfg: ModelConfig, device):
+        super().__init__()
+        self.gate_up = ColumnLinear(cfg.hidden_size, 2 * cfg.intermediate_size, device=device)
+        self.down = RowLinear(cfg.intermediate_size, cfg.hidden_size, device=device)
+
+    def forward(self, x):
+        return self.down(ops.gated_act(self.gate_up(x), ops.ACT_SILU))
+
+
+class LlamaDecoderLayer(torch.nn.Module):
+    def __init__(self, cfg: ModelConfig, idx: int, cos_sin: torch.Tensor, device):
+        super().__init__()
+        d, D = cfg.hidden_size, cfg.head_dim
+        Hq, Hkv = cfg.num_attention_heads, cfg.num_key_value_heads
+        self.cfg = cfg
+        self.input_layernorm = RMSNorm(d, cfg.rms_norm_eps, device)
+        self.qkv = ColumnLinear(d, (Hq + 2 * Hkv) * D, bias=cfg.attention_bias, device=device)
+        self.attn = PagedAttention(idx, Hq, Hkv, D, cos_sin, window=cfg.layer_window(idx),
+                                   sinks=cfg.attention_sinks, device=device)
+        self.o_proj = RowLinear(Hq * D, d, device=device)
+        self.post_attention_layernorm = RMSNorm(d, cfg.rms_norm_eps, device)
+        self.mlp = self._make_mlp(cfg, idx, device)
+        # Qwen3: per-head RMSNorm on q and k before rope
+        self.qk_norm = cfg.model_type == "qwen3"
+        if self.qk_norm:
+            self.q_norm = RMSNorm(D, cfg.rms_norm_eps, device)
+            self.k_norm = RMSNorm(D, cfg.rms_norm_eps, device)
+
+    def _make_mlp(self, cfg, idx, device):
+        return LlamaMLP(cfg, device)
+
+    def _apply_qk_norm(self, qkv):
+        a = self.attn
+        T = qkv.shape[0]
+        q = qkv[:, : a.Hq * a.D].reshape(T * a.Hq, a.D)
+        k = qkv[:, a.Hq * a.D : (a.Hq + a.Hkv) * a.D].reshape(T * a.Hkv, a.D)
+        qkv[:, : a.Hq * a.D] = self.q_norm(q).view(T, -1)
+        qkv[:, a.Hq * a.D : (a.Hq + a.Hkv) * a.D] = self.k_norm(k).view(T, -1)
+
+    def forward(self, x, residual, meta: AttnMeta):
+        if residual is None:
+            residual = x.clone()
+            x = self.input_layernorm(x)
+        else:
+            x, residual = self.input_layernorm(x, residual)
+        qkv = self.qkv(x)
+        if self.qk_norm:
+            self._apply_qk_norm(qkv)
+        x = self.o_proj(self.attn(qkv, meta))
+        x, residual = self.post_attention_layernorm(x, residual)
+        return self.mlp(x), residual
+
+
+class LlamaForCausalLM(torch.nn.Module):
+    layer_cls = LlamaDecoderLayer
+
+    def __init__(self, cfg: ModelConfig, device="cuda", max_pos: int = 32768):
+        super().__init__()
+        self.cfg = cfg
+        rot = cfg.head_dim
+        self.register_buffer("cos_sin", ops.rope_cos_sin(rot, max_pos, cfg.rope_theta, cfg.rope_scaling,
+                                                         device=device), persistent=False)
+        self.embed = VocabEmbedding(cfg.vocab_size, cfg.hidden_size, device)
+        self.layers = torch.nn.ModuleList(
+            [self.layer_cls(cfg, i, self.cos_sin, device) for i in range(cfg.num_hidden_layers)])
+        self.norm = RMSNorm(cfg.hidden_size, cfg.rms_norm_eps, device)
+        self.lm_head = LMHead(cfg.vocab_size, cfg.hidden_size, device,
+                              tied=self.embed if cfg.tie_word_embeddings else None)
+
+    def attention_layers(self):
+        return [layer.attn for layer in self.layers]
+
+    @torch.no_grad()
+    def forward(self, input_ids: torch.Tensor, meta: AttnMeta) -> torch.Tensor:
+        x = self.embed(input_ids)
+        residual = None
+        for layer in self.layers:
+            x, residual = layer(x, residual, meta)
+        x, _ = self.norm(x, residual)
+        return x
+
+    @torch.no_grad()
+    def compute_logits(self, h: torch.Tensor) -> torch.Tensor:
+        return self.lm_head(h)
+
+
+def kv_head_count(cfg: ModelConfig) -> int:
+    return max(1, cfg.num_key_value_heads // get_state().tp_size)

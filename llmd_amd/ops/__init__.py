@@ -1,0 +1,202 @@
+"""Op layer: HIP/CDNA4 kernels for GPU tensors, fp32 torch references for CPU.
+
+GPU tensors ALWAYS go to the native ``llmd_amd._C`` library; if it is missing
+on a GPU host the call raises (no silent eager fallback). CPU tensors use
+``llmd_amd.ops.reference`` so the whole engine runs in CPU CI.
+"""
+from __future__ import annotations
+
+import math
+import os
+
+import torch
+
+from . import reference as ref
+
+_C = None
+_C_ERR: Exception | None = None
+
+
+def native():
+    """Return the loaded ``_C`` module, building/loading it on first use."""
+    global _C, _C_ERR
+    if _C is not None:
+        return _C
+    try:
+        from llmd_amd import _C as mod  # noqa: WPS433
+    except ImportError as e:  # pragma: no cover - exercised on GPU hosts only
+        _C_ERR = e
+        if os.environ.get("LLMD_AUTOBUILD", "1") == "1":
+            from llmd_amd.build import build_ops
+
+            build_ops()
+            from llmd_amd import _C as mod  # noqa: WPS433,F811
+        else:
+            raise RuntimeError(f"llmd_amd._C HIP extension not built: {e}") from e
+    _C = mod
+    return _C
+
+
+def _gpu(t: torch.Tensor) -> bool:
+    return t.is_cuda
+
+
+# ---------------------------------------------------------------- norms
+def rms_norm(x: torch.Tensor, w: torch.Tensor, eps: float, out: torch.Tensor | None = None):
+    if not _gpu(x):
+        r = ref.rms_norm(x, w, eps)
+        if out is not None:
+            out.copy_(r)
+            return out
+        return r
+    if out is None:
+        out = torch.empty_like(x)
+    native().rms_norm(out, x, w, eps)
+    return out
+
+
+def fused_add_rms_norm(x: torch.Tensor, residual: torch.Tensor, w: torch.Tensor, eps: float):
+    """residual += x; x = rmsnorm(residual) * w (both in place)."""
+    if not _gpu(x):
+        ref.fused_add_rms_norm(x, residual, w, eps)
+        return
+    native().fused_add_rms_norm(x, residual, w, eps)
+
+
+# ---------------------------------------------------------------- rope + cache
+def rope_cache(qkv, positions, cos_sin, Hq, Hkv, D, slots, k_cache, v_cache, neox=True):
+    if not _gpu(qkv):
+        ref.rope_cache(qkv, positions, cos_sin, Hq, Hkv, D, slots, k_cache, v_cache, neox)
+        return
+    native().rope_cache(qkv, positions, cos_sin, Hq, Hkv, D, slots, k_cache, v_cache, neox)
+
+
+# ---------------------------------------------------------------- activation
+ACT_SILU, ACT_GELU_TANH, ACT_SWIGLU_OAI = 0, 1, 2
+
+
+def gated_act(x: torch.Tensor, mode: int = ACT_SILU, alpha: float = 1.702, limit: float = 7.0,
+              out: torch.Tensor | None = None):
+    if not _gpu(x):
+        r = ref.gated_act(x, mode, alpha, limit)
+        if out is not None:
+            out.copy_(r)
+            return out
+        return r
+    F = x.shape[1] // 2
+    if out is None:
+        out = torch.empty(x.shape[0], F, dtype=x.dtype, device=x.device)
+    native().gated_act(out, x, mode, alpha, limit)
+    return out
+
+
+# ---------------------------------------------------------------- attention
+def prefill_tokens_per_item(Hq: int, Hkv: int) -> int:
+    G = Hq // Hkv
+    hpw = 4 if G % 4 == 0 else (2 if G % 2 == 0 else 1)
+    return 32 * (4 // hpw)
+
+
+def decode_split_plan(max_ctx: int, batch: int, Hkv: int, G: int, num_cus: int = 256,
+                      min_split: int = 256) -> tuple[int, int]:
+    """Pick (split_size, nsplit) for the decode kernel: enough workgroups to
+    fill 256 CUs at ~2 WGs/CU, splits a multiple of 64 keys."""
+    ng = (G + 15) // 16
+    base = max(1, batch * Hkv * ng)
+    target = 2 * num_cus
+    nsplit = max(1, min(math.ceil(max_ctx / min_split), math.ceil(target / base)))
+    split = math.ceil(max_ctx / nsplit / 64) * 64
+    split = max(split, 64)
+    nsplit = math.ceil(max_ctx / split)
+    return split, nsplit
+
+
+def paged_decode(q, k_cache, v_cache, block_tables, seq_lens, Hq, Hkv, D, scale, window=0,
+                 sinks=None, split=None, out=None, workspace=None, max_ctx=None):
+    """q: [B, >=Hq*D] -> out [B, Hq*D]."""
+    if not _gpu(q):
+        r = ref.paged_decode(q, k_cache, v_cache, block_tables, seq_lens, Hq, Hkv, D, scale,
+                             window, sinks)
+        if out is not None:
+            out.copy_(r)
+            return out
+        return r
+    B = q.shape[0]
+    if out is None:
+        out = torch.empty(B, Hq * D, dtype=q.dtype, device=q.device)
+    if split is None:
+        if max_ctx is None:
+            max_ctx = int(seq_lens.max().item()) if B else 1
+        if window and window > 0:
+            max_ctx = min(max_ctx, window)
+        split = decode_split_plan(max_ctx, B, Hkv, Hq // Hkv)
+    split_size, nsplit = split
+    if nsplit > 1:
+        if workspace is None:
+            part_o = torch.empty(B * Hq * nsplit * D, dtype=torch.float32, device=q.device)
+            part_ml = torch.empty(B * Hq * nsplit * 2, dtype=torch.float32, device=q.device)
+        else:
+            part_o, part_ml = workspace
+    else:
+        part_o = part_ml = out.new_empty(0, dtype=torch.float32)
+    native().paged_decode(out, q, k_cache, v_cache, block_tables, seq_lens, Hq, Hkv, D, scale,
+                          window, sinks, split_size, nsplit, part_o, part_ml)
+    return out
+
+
+def build_prefill_items(q_len: list[int], ctx_len: list[int], tpi: int) -> list[tuple[int, int]]:
+    """Work items (seq, first q token), heaviest (most keys) first."""
+    items = []
+    for s, (ql, cl) in enumerate(zip(q_len, ctx_len)):
+        for t0 in range(0, ql, tpi):
+            keys = cl - ql + min(ql, t0 + tpi)
+            items.append((keys, s, t0))
+    items.sort(key=lambda x: -x[0])
+    return [(s, t0) for _, s, t0 in items]
+
+
+def paged_prefill(q, k_cache, v_cache, block_tables, q_start, q_len, ctx_len, Hq, Hkv, D, scale,
+                  window=0, sinks=None, items=None, out=None):
+    if not _gpu(q):
+        r = ref.paged_prefill(q, k_cache, v_cache, block_tables, q_start, q_len, ctx_len, Hq, Hkv,
+                              D, scale, window, sinks)
+        if out is not None:
+            out.copy_(r)
+            return out
+        return r
+    if out is None:
+        out = torch.empty(q.shape[0], Hq * D, dtype=q.dtype, device=q.device)
+    if items is None:
+        tpi = prefill_tokens_per_item(Hq, Hkv)
+        it = build_prefill_items(q_len.tolist(), ctx_len.tolist(), tpi)
+        items = torch.tensor(it, dtype=torch.int32).view(-1, 2).to(q.device, non_blocking=True)
+    native().paged_prefill(out, q, k_cache, v_cache, block_tables, q_start, q_len, ctx_len, items,
+                           Hq, Hkv, D, scale, window, sinks)
+    return out
+
+
+# ---------------------------------------------------------------- sampling
+def sample(logits, temps=None, seeds=None, out_ids=None, want_logprob=False, generator=None):
+    if not _gpu(logits):
+        ids, lp = ref.sample(logits, temps, generator)
+        return ids, (lp if want_logprob else None)
+    B = logits.shape[0]
+    if out_ids is None:
+        out_ids = torch.empty(B, dtype=torch.int64, device=logits.device)
+    lp = torch.empty(B, dtype=torch.float32, device=logits.device) if want_logprob else None
+    native().sample(logits, temps, seeds, out_ids, lp)
+    return out_ids, lp
+
+
+def topk_topp_mask(logits, topk=None, topp=None, temps=None):
+    """In-place top-k then top-p filtering of f32 logits."""
+    if not _gpu(logits):
+        return ref.topk_topp_mask(logits, topk, topp, temps)
+    if topk is not None:
+        native().topk_topp_mask(logits, topk, None, temps)
+    if topp is not None:
+        native().topk_topp_mask(logits, None, topp, temps)
+    return logits
+
+
+rope_cos_sin = ref.rope_cos_sin

@@ -1,0 +1,68 @@
+"""Tensor/expert-parallel collectives.
+
+RCCL through torch.distributed for everything; a custom one-shot IPC
+all-reduce (``parallel.custom_ar``) takes over latency-bound decode-size
+messages when registered. All functions are no-ops at group size 1.
+"""
+from __future__ import annotations
+
+import torch
+import torch.distributed as dist
+
+from .state import get_state
+
+_custom_ar = None  # set by parallel.custom_ar.install()
+
+
+def set_custom_allreduce(impl):
+    global _custom_ar
+    _custom_ar = impl
+
+
+def tp_all_reduce(x: torch.Tensor) -> torch.Tensor:
+    st = get_state()
+    if st.tp_size == 1:
+        return x
+    if _custom_ar is not None and _custom_ar.should_use(x):
+        return _custom_ar.all_reduce(x)
+    dist.all_reduce(x, group=st.tp_group)
+    return x
+
+
+def tp_all_gather(x: torch.Tensor, dim: int = -1) -> torch.Tensor:
+    st = get_state()
+    if st.tp_size == 1:
+        return x
+    dim = dim % x.dim()
+    out = torch.empty((st.tp_size,) + tuple(x.shape), dtype=x.dtype, device=x.device)
+    dist.all_gather_into_tensor(out, x.contiguous(), group=st.tp_group)
+    return torch.cat(out.unbind(0), dim=dim)
+
+
+def ep_all_gather(x: torch.Tensor) -> torch.Tensor:
+    """[n, ...] per rank -> [world*n, ...] (all ranks must pass equal n)."""
+    st = get_state()
+    if st.ep_size == 1:
+        return x
+    out = torch.empty((st.ep_size * x.shape[0],) + tuple(x.shape[1:]), dtype=x.dtype, device=x.device)
+    dist.all_gather_into_tensor(out, x.contiguous(), group=st.ep_group)
+    return out
+
+
+def ep_reduce_scatter(x: torch.Tensor) -> torch.Tensor:
+    st = get_state()
+    if st.ep_size == 1:
+        return x
+    out = torch.empty((x.shape[0] // st.ep_size,) + tuple(x.shape[1:]), dtype=x.dtype, device=x.device)
+    dist.reduce_scatter_tensor(out, x.contiguous(), group=st.ep_group)
+    return out
+
+
+def dp_all_reduce_max_int(v: int) -> int:
+    """Tiny DP lock-step sync: max of an int across DP ranks."""
+    st = get_state()
+    if st.dp_size == 1:
+        return v
+    t = torch.tensor([v], dtype=torch.int64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX, group=st.cpu_group)
+    return int(t.item())
