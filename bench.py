@@ -1,0 +1,182 @@
+#!/usr/bin/env python3
+"""Serving benchmark: Llama-3-70B, ISL 5000 / OSL 250 (the reference's P/D
+benchmark shape, guides/pd-disaggregation/README.md:336-520), bf16, random-init
+weights, synthetic random-token prompts.
+
+A *step* is one engine iteration on every rank (continuous batching: decode
+tokens of all running requests + chunked-prefill tokens of new ones, within
+``--max-num-batched-tokens``). Each rank keeps ``--concurrency`` requests in
+flight (closed loop: a finished request is immediately replaced), W warmup
+steps bring the batch to steady state, then exactly K steps are timed between
+barrier+synchronize brackets; the slowest rank's time is used.
+
+Modes
+  agg  (default): every GPU is an independent aggregated replica (dp N) - the
+        optimized-baseline topology; per-GPU work fixed as N grows (weak scaling).
+  pd : ranks [0, P) prefill, [P, N) decode; KV moves over xGMI (kvx). N >= 2.
+
+Output: one JSON line on rank 0 (see README "bench.py contract").
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import statistics
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+METRIC = "output tok/s per decode GPU + p50 TTFT, Llama-3-70B P/D-disagg on 8×MI355X"
+REF_CONTEXT = ("reference publishes no Llama-3-70B number; its P/D headline is gpt-oss-120b on 16xH200 "
+               "(8 P TP1 + 2 D TP4): 12236.6 output tok/s total = 1529.6 per decode GPU, p50 TTFT 1.264 s "
+               "(guides/pd-disaggregation/README.md:336-460)")
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=40)
+    p.add_argument("--warmup", type=int, default=40)
+    p.add_argument("--model", default="llama-3-70b")
+    p.add_argument("--isl", type=int, default=5000)
+    p.add_argument("--osl", type=int, default=250)
+    p.add_argument("--concurrency", type=int, default=64, help="requests in flight per GPU")
+    p.add_argument("--max-num-batched-tokens", type=int, default=8192)
+    p.add_argument("--block-size", type=int, default=64)
+    p.add_argument("--mode", default="agg", choices=["agg", "pd"])
+    p.add_argument("--prefill-gpus", type=int, default=0, help="pd mode: number of prefill ranks")
+    p.add_argument("--enforce-eager", action="store_true")
+    p.add_argument("--seed", type=int, default=0)
+    p.add_argument("--json-out", default=None)
+    return p.parse_args()
+
+
+def log(rank, *a):
+    if rank == 0:
+        print("[bench]", *a, file=sys.stderr, flush=True)
+
+
+def main():
+    a = parse()
+    rank = int(os.environ.get("RANK", 0))
+    local_rank = int(os.environ.get("LOCAL_RANK", 0))
+    world = int(os.environ.get("WORLD_SIZE", 1))
+    if world != a.gpus and world > 1:
+        log(rank, f"warning: WORLD_SIZE={world} != --gpus {a.gpus}")
+    torch.cuda.set_device(local_rank)
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("nccl", rank=rank, world_size=world,
+                                device_id=torch.device("cuda", local_rank))
+
+    from llmd_amd.engine.config import EngineConfig
+    from llmd_amd.engine.engine import LLMEngine
+    from llmd_amd.engine.request import SamplingParams
+
+    max_len = a.isl + a.osl + 64
+    cfg = EngineConfig.create(
+        a.model, device="cuda", block_size=a.block_size, max_num_seqs=a.concurrency,
+        max_num_batched_tokens=a.max_num_batched_tokens, max_model_len=max_len,
+        enforce_eager=a.enforce_eager, seed=a.seed + rank, enable_prefix_caching=True,
+        cuda_graph_max_bs=a.concurrency)
+    t0 = time.time()
+    eng = LLMEngine(cfg)
+    torch.cuda.synchronize()
+    log(rank, f"engine up in {time.time() - t0:.1f}s: {cfg.model_config.name}, "
+              f"{eng.runner.num_blocks} KV blocks x {a.block_size}")
+    vocab = cfg.model_config.vocab_size
+    rng = np.random.default_rng(1234 + rank)
+    nreq = [0]
+
+    def new_request(max_tokens):
+        toks = rng.integers(100, vocab - 100, size=a.isl).tolist()
+        nreq[0] += 1
+        eng.add_request(f"r{rank}-{nreq[0]}", toks,
+                        SamplingParams(max_tokens=max_tokens, temperature=0.0, ignore_eos=True))
+
+    # staggered start: spread remaining output lengths so completions de-synchronise
+    for i in range(a.concurrency):
+        new_request(max(1, int(a.osl * (i + 1) / a.concurrency)))
+
+    def run_steps(n):
+        for _ in range(n):
+            for o in eng.step():
+                if o.finished:
+                    new_request(a.osl)
+
+    # warmup
+    tw = time.time()
+    run_steps(a.warmup)
+    torch.cuda.synchronize()
+    log(rank, f"warmup {a.warmup} steps in {time.time() - tw:.1f}s")
+    # timed
+    eng.metrics.ttfts.clear()
+    gen0 = eng.metrics.n_gen
+    prompt0 = eng.metrics.n_prompt
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    run_steps(a.steps)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t1
+    gen = eng.metrics.n_gen - gen0
+    ptoks = eng.metrics.n_prompt - prompt0
+    ttfts = list(eng.metrics.ttfts)
+    stats = torch.tensor([elapsed, gen, ptoks, len(ttfts)], dtype=torch.float64, device="cuda")
+    all_ttft = ttfts
+    if world > 1:
+        mx = stats.clone()
+        dist.all_reduce(mx, op=dist.ReduceOp.MAX)
+        sm = stats.clone()
+        dist.all_reduce(sm, op=dist.ReduceOp.SUM)
+        elapsed = float(mx[0])
+        gen, ptoks = float(sm[1]), float(sm[2])
+        gathered = [None] * world
+        dist.all_gather_object(gathered, ttfts)
+        all_ttft = [t for g in gathered for t in g]
+    value = gen / elapsed
+    p50 = statistics.median(all_ttft) if all_ttft else None
+    n_decode_gpus = world if a.mode == "agg" else world - a.prefill_gpus
+    result = {
+        "metric": METRIC,
+        "value": round(value, 2),
+        "unit": "output tok/s (whole job)",
+        "n_gpus": world,
+        "steps": a.steps,
+        "warmup": a.warmup,
+        "ms_per_step": round(1000 * elapsed / a.steps, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "bf16",
+        "data": "synthetic (random token prompts, random-init weights)",
+        "config": {"model": "Llama-3-70B" if a.model == "llama-3-70b" else a.model,
+                   "global_batch": a.concurrency * world, "seq_len": a.isl, "isl": a.isl, "osl": a.osl,
+                   "parallelism": f"dp{world}" if a.mode == "agg" else f"pd{a.prefill_gpus}p{world - a.prefill_gpus}d",
+                   "max_num_batched_tokens": a.max_num_batched_tokens, "block_size": a.block_size,
+                   "graphs": not a.enforce_eager},
+        "output_tok_s_per_decode_gpu": round(value / max(1, n_decode_gpus), 2),
+        "p50_ttft_s": round(p50, 4) if p50 is not None else None,
+        "prefill_tok_s": round(ptoks / elapsed, 1),
+        "reference_context": REF_CONTEXT,
+    }
+    if rank == 0:
+        line = json.dumps(result)
+        print(line, flush=True)
+        if a.json_out:
+            with open(a.json_out, "w") as f:
+                f.write(line + "\n")
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,126 @@
+"""LLMEngine: scheduler + native block manager + model runner + outputs.
+
+``step()`` = schedule -> execute (one forward over decodes + prefill chunks)
+-> sample -> update request state -> emit outputs, KV events and metrics.
+The HTTP layer (``llmd_amd.serving``) drives ``step()`` from a dedicated
+thread through ``AsyncEngine``.
+"""
+from __future__ import annotations
+
+import logging
+import time
+from typing import Iterable, Optional
+
+from llmd_amd import _rt_loader
+
+from .config import EngineConfig
+from .metrics import EngineMetrics
+from .model_runner import ModelRunner
+from .request import Request, RequestOutput, SamplingParams, Status
+from .scheduler import Scheduler, SchedulerOutput
+
+log = logging.getLogger("llmd.engine")
+
+
+class LLMEngine:
+    def __init__(self, cfg: EngineConfig, metrics: Optional[EngineMetrics] = None,
+                 runner: Optional[ModelRunner] = None, capture_graphs: bool = True):
+        self.cfg = cfg
+        self.runner = runner or ModelRunner(cfg)
+        nb = self.runner.profile_and_allocate() if self.runner.kv is None else self.runner.num_blocks
+        rt = _rt_loader.rt()
+        ev_on = bool(cfg.kv_events_config and cfg.kv_events_config.get("enable_kv_cache_events"))
+        self.bm = rt.BlockManager(nb, cfg.cache.block_size, cfg.cache.enable_prefix_caching,
+                                  ev_on or bool(cfg.kv_offload_config))
+        self.connector = None
+        if cfg.kv_transfer_config:
+            from llmd_amd.kvx.connector import make_connector
+
+            self.connector = make_connector(cfg, self)
+        self.sched = Scheduler(cfg, self.bm, self.connector)
+        self.metrics = metrics or EngineMetrics(cfg.served_name, cfg.cache.block_size, nb)
+        self.event_sink = None  # set by serving.kv_events.KVEventPublisher
+        self.offload = None
+        if cfg.kv_offload_config:
+            from llmd_amd.kvcache.offload import OffloadManager
+
+            self.offload = OffloadManager(cfg, self)
+        if capture_graphs:
+            self.runner.capture_graphs()
+        self.paused = False
+        self.step_count = 0
+
+    # ------------------------------------------------------------ API
+    def add_request(self, request_id: str, prompt_token_ids: list[int],
+                    params: Optional[SamplingParams] = None, priority: int = 0,
+                    kv_transfer_params: Optional[dict] = None, lora_id: int = 0,
+                    arrival_time: Optional[float] = None) -> Request:
+        r = Request(request_id, list(prompt_token_ids), params or SamplingParams(), priority=priority,
+                    kv_transfer_params=kv_transfer_params, lora_id=lora_id)
+        if arrival_time is not None:
+            r.arrival_time = arrival_time
+        self.sched.add_request(r)
+        self.metrics.on_arrival(r)
+        return r
+
+    def abort(self, request_id: str):
+        r = self.sched.abort(request_id)
+        if r is not None:
+            self.metrics.on_finish(r)
+
+    def has_unfinished(self) -> bool:
+        return self.sched.has_work()
+
+    def block_tables(self, so: SchedulerOutput) -> dict[int, list[int]]:
+        return {sr.req.seq_id: self.bm.block_table(sr.req.seq_id) for sr in so.all()}
+
+    def step(self) -> list[RequestOutput]:
+        if self.paused:
+            return []
+        if self.connector is not None:
+            self.connector.tick()
+        t0 = time.monotonic()
+        so = self.sched.schedule()
+        if so.empty:
+            self._flush_events()
+            return []
+        if self.offload is not None:
+            self.offload.before_step(so)
+        sampled = self.runner.execute(so, self.block_tables(so))
+        touched = self.sched.update(so, sampled)
+        dt = time.monotonic() - t0
+        self.step_count += 1
+        outs = []
+        for r in touched:
+            o = RequestOutput(r.request_id, [r.output_token_ids[-1]], [r.output_logprobs[-1]],
+                              r.status.finished, r.finish_reason, r.num_prompt_tokens,
+                              len(r.output_token_ids), r.num_cached_tokens)
+            if r.status.finished:
+                o.kv_transfer_params = r.extra.get("kv_transfer_params_out")
+                self.metrics.on_finish(r)
+            outs.append(o)
+        self.metrics.on_step(so, touched, dt, self.sched.num_running, self.sched.num_waiting,
+                             self.bm.usage(), self.bm.prefix_stats())
+        self._flush_events()
+        return outs
+
+    def _flush_events(self):
+        if self.offload is not None:
+            self.offload.after_step()
+        if self.event_sink is not None:
+            evs = self.bm.take_events()
+            if evs:
+                self.event_sink(evs)
+
+    # ------------------------------------------------------------ offline helpers
+    def generate(self, prompts: Iterable[list[int]], params: SamplingParams) -> list[Request]:
+        reqs = []
+        for i, p in enumerate(prompts):
+            reqs.append(self.add_request(f"gen-{self.step_count}-{i}-{time.monotonic_ns()}", p, params))
+        while self.has_unfinished():
+            self.step()
+        return reqs
+
+    def reset_prefix_cache(self):
+        self.bm.reset_prefix_cache()
+        self._flush_events()

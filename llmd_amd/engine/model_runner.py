@@ -1,0 +1,353 @@
+"""Model runner: owns the model, the paged KV cache and the per-step execution.
+
+KV cache: one tensor ``[num_blocks, L, 2, Hkv, block_size, D]`` bf16, i.e. a
+block of every layer is one contiguous slab. Per-layer views
+``kv[:, l, 0]`` / ``kv[:, l, 1]`` are what the kernels consume. Keeping a
+whole block contiguous across layers makes P/D transfer and host offload one
+large DMA per block (kvx).
+
+Decode-only steps replay a captured hipGraph per batch bucket:
+all inputs live in static device buffers, padded rows have ``slot = -1`` and
+``seq_len = 1`` so they neither write the cache nor read past it. Mixed
+steps (chunked prefill + decodes) run eagerly.
+"""
+from __future__ import annotations
+
+import logging
+import math
+import time
+from typing import Optional
+
+import numpy as np
+import torch
+
+from llmd_amd import ops
+from llmd_amd.models import build_model
+
+from .attn_meta import AttnMeta
+from .config import EngineConfig
+from .scheduler import ScheduledReq, SchedulerOutput
+
+log = logging.getLogger("llmd.runner")
+
+
+def _mix64(z: int) -> int:
+    z &= (1 << 64) - 1
+    z = ((z ^ (z >> 30)) * 0xBF58476D1CE4E5B9) & ((1 << 64) - 1)
+    z = ((z ^ (z >> 27)) * 0x94D049BB133111EB) & ((1 << 64) - 1)
+    return (z ^ (z >> 31)) & ((1 << 63) - 1)
+
+
+class ModelRunner:
+    def __init__(self, cfg: EngineConfig, device: Optional[str] = None):
+        self.cfg = cfg
+        self.mc = cfg.model_config
+        self.device = torch.device(device or cfg.device)
+        self.is_gpu = self.device.type == "cuda"
+        self.bs = cfg.cache.block_size
+        self.max_model_len = cfg.sched.max_model_len
+        self.width = math.ceil(self.max_model_len / self.bs) + 1
+        torch.manual_seed(cfg.seed)
+        t0 = time.time()
+        self.model = build_model(self.mc, device=self.device, max_pos=self.max_model_len + 1)
+        if cfg.load_format in ("safetensors", "auto") and cfg.weights_path:
+            from llmd_amd.models.loader import load_weights
+
+            load_weights(self.model, cfg.weights_path)
+        if self.is_gpu:
+            torch.cuda.synchronize()
+        log.info("model %s built in %.1fs", self.mc.name, time.time() - t0)
+        attn = self.model.attention_layers()
+        self.Hkv, self.D, self.L = attn[0].Hkv, attn[0].D, len(attn)
+        self.Hq = attn[0].Hq
+        self.kv = None
+        self.num_blocks = 0
+        self.graphs: dict[int, tuple] = {}
+        self._rng = np.random.default_rng(cfg.seed)
+        # graph-mode decode split plan: fixed for all buckets
+        split = max(512, math.ceil(self.max_model_len / 32 / 64) * 64)
+        self.graph_split = (split, math.ceil(self.max_model_len / split))
+
+    # ------------------------------------------------------------ KV cache
+    def block_bytes(self) -> int:
+        return self.L * 2 * self.Hkv * self.bs * self.D * 2
+
+    def _alloc_cache(self, num_blocks: int) -> torch.Tensor:
+        kv = torch.empty(num_blocks, self.L, 2, self.Hkv, self.bs, self.D, dtype=torch.bfloat16,
+                         device=self.device)
+        for i, a in enumerate(self.model.attention_layers()):
+            a.k_cache = kv[:, i, 0]
+            a.v_cache = kv[:, i, 1]
+        return kv
+
+    @torch.no_grad()
+    def profile_and_allocate(self) -> int:
+        cc = self.cfg.cache
+        if cc.num_gpu_blocks:
+            nb = cc.num_gpu_blocks
+        elif not self.is_gpu:
+            nb = max(64, (cc.kv_cache_memory_bytes or (256 << 20)) // self.block_bytes())
+        else:
+            # dummy max-size step on a scratch cache to measure activation peak
+            T = self.cfg.sched.max_num_batched_tokens
+            scratch_blocks = math.ceil(T / self.bs) + 2
+            self.kv = self._alloc_cache(scratch_blocks)
+            torch.cuda.synchronize()
+            torch.cuda.reset_peak_memory_stats()
+            base = torch.cuda.memory_allocated()
+            self._dummy_prefill(T, scratch_blocks)
+            torch.cuda.synchronize()
+            act_peak = torch.cuda.max_memory_allocated() - base
+            self.kv = None
+            for a in self.model.attention_layers():
+                a.k_cache = a.v_cache = None
+            torch.cuda.empty_cache()
+            free, total = torch.cuda.mem_get_info()
+            if cc.kv_cache_memory_bytes:
+                budget = cc.kv_cache_memory_bytes
+            else:
+                used = total - free
+                budget = int(total * cc.gpu_memory_utilization) - used - act_peak - (2 << 30)
+            nb = max(16, budget // self.block_bytes())
+            log.info("kv cache: %d blocks x %d tokens (%.1f GiB), activation peak %.2f GiB",
+                     nb, self.bs, nb * self.block_bytes() / 2**30, act_peak / 2**30)
+        self.num_blocks = int(nb)
+        self.kv = self._alloc_cache(self.num_blocks)
+        return self.num_blocks
+
+    def _dummy_prefill(self, T: int, nblocks: int):
+        nseq = max(1, math.ceil(T / self.bs))
+        ql = [min(self.bs, T - i * self.bs) for i in range(nseq)]
+        ql = [q for q in ql if q > 0]
+        bt = np.zeros((len(ql), self.width), dtype=np.int32)
+        for i in range(len(ql)):
+            bt[i, 0] = i % nblocks
+        ids = torch.zeros(sum(ql), dtype=torch.long, device=self.device)
+        pos = torch.cat([torch.arange(q) for q in ql]).to(self.device)
+        slots = torch.cat([torch.arange(q) + (i % nblocks) * self.bs for i, q in enumerate(ql)]).to(self.device)
+        qs = np.cumsum([0] + ql[:-1]).astype(np.int32)
+        meta = AttnMeta(num_tokens=sum(ql), positions=pos, slot_mapping=slots,
+                        num_prefill_tokens=sum(ql),
+                        p_block_tables=torch.from_numpy(bt).to(self.device),
+                        p_q_start=torch.from_numpy(qs).to(self.device),
+                        p_q_len=torch.tensor(ql, dtype=torch.int32, device=self.device),
+                        p_ctx_len=torch.tensor(ql, dtype=torch.int32, device=self.device))
+        meta.p_items = self._items(ql, ql)
+        h = self.model(ids, meta)
+        self.model.compute_logits(h[: min(len(ql), self.cfg.sched.max_num_seqs)])
+
+    def _items(self, q_len, ctx_len):
+        tpi = ops.prefill_tokens_per_item(self.Hq, self.Hkv)
+        it = ops.build_prefill_items(list(q_len), list(ctx_len), tpi)
+        return torch.tensor(it, dtype=torch.int32).view(-1, 2).to(self.device, non_blocking=True)
+
+    # ------------------------------------------------------------ inputs
+    def _prepare(self, so: SchedulerOutput, block_tables: dict[int, list[int]]):
+        dec, pre = so.decodes, so.prefills
+        nd = len(dec)
+        ids, pos, slots = [], [], []
+        bs = self.bs
+        d_bt = np.zeros((nd, self.width), dtype=np.int32)
+        d_len = np.zeros(nd, dtype=np.int32)
+        for i, sr in enumerate(dec):
+            r = sr.req
+            p = sr.start
+            tok = r.all_token_ids[p]
+            bt = block_tables[r.seq_id]
+            ids.append(tok)
+            pos.append(p)
+            slots.append(bt[p // bs] * bs + p % bs)
+            d_bt[i, : len(bt)] = bt
+            d_len[i] = p + 1
+        p_ql, p_ctx = [], []
+        p_bt = np.zeros((len(pre), self.width), dtype=np.int32)
+        for i, sr in enumerate(pre):
+            r = sr.req
+            bt = block_tables[r.seq_id]
+            toks = r.all_token_ids[sr.start : sr.start + sr.num_new_tokens]
+            ids.extend(toks)
+            ps = np.arange(sr.start, sr.start + sr.num_new_tokens)
+            pos.extend(ps.tolist())
+            bta = np.asarray(bt, dtype=np.int64)
+            slots.extend((bta[ps // bs] * bs + ps % bs).tolist())
+            p_bt[i, : len(bt)] = bt
+            p_ql.append(sr.num_new_tokens)
+            p_ctx.append(sr.start + sr.num_new_tokens)
+        return ids, pos, slots, d_bt, d_len, p_ql, p_ctx, p_bt
+
+    def _sample_rows(self, so: SchedulerOutput):
+        """Rows (token index) that produce a sampled token, and their requests."""
+        rows, reqs = [], []
+        for i, sr in enumerate(so.decodes):
+            if sr.samples:
+                rows.append(i)
+                reqs.append(sr.req)
+        off = len(so.decodes)
+        for sr in so.prefills:
+            off += sr.num_new_tokens
+            if sr.samples:
+                rows.append(off - 1)
+                reqs.append(sr.req)
+        return rows, reqs
+
+    def _sampling_tensors(self, reqs):
+        n = len(reqs)
+        temps = np.zeros(n, dtype=np.float32)
+        seeds = np.zeros(n, dtype=np.int64)
+        topk = np.zeros(n, dtype=np.int32)
+        topp = np.ones(n, dtype=np.float32)
+        any_rand = any_k = any_p = False
+        for i, r in enumerate(reqs):
+            sp = r.params
+            if sp.temperature > 0:
+                any_rand = True
+                temps[i] = sp.temperature
+                base = sp.seed if sp.seed is not None else r.extra.setdefault(
+                    "_seed", int(self._rng.integers(0, 2**62)))
+                seeds[i] = _mix64(base * 1000003 + len(r.output_token_ids))
+            if sp.top_k > 0:
+                topk[i] = sp.top_k
+                any_k = True
+            if sp.top_p < 1.0:
+                topp[i] = sp.top_p
+                any_p = True
+        return temps, seeds, topk, topp, any_rand, any_k, any_p
+
+    # ------------------------------------------------------------ execution
+    @torch.no_grad()
+    def execute(self, so: SchedulerOutput, block_tables: dict[int, list[int]]) -> dict[int, tuple[int, float]]:
+        if so.empty:
+            return {}
+        rows, reqs = self._sample_rows(so)
+        if not so.prefills and self._graph_ok(len(so.decodes)):
+            logits = self._run_decode_graph(so, block_tables, rows)
+        else:
+            h = self._run_eager(so, block_tables)
+            idx = torch.tensor(rows, dtype=torch.long).to(self.device, non_blocking=True)
+            logits = self.model.compute_logits(h.index_select(0, idx)) if rows else None
+        if not rows:
+            return {}
+        return self._sample(logits, reqs)
+
+    def _sample(self, logits, reqs):
+        temps, seeds, topk, topp, any_rand, any_k, any_p = self._sampling_tensors(reqs)
+        want_lp = any(r.params.logprobs for r in reqs)
+        dev = self.device
+        if any_k or any_p:
+            logits = logits.float()
+            ops.topk_topp_mask(logits, torch.from_numpy(topk).to(dev) if any_k else None,
+                               torch.from_numpy(topp).to(dev) if any_p else None,
+                               torch.from_numpy(temps).to(dev))
+        t = torch.from_numpy(temps).to(dev, non_blocking=True) if any_rand else None
+        s = torch.from_numpy(seeds).to(dev, non_blocking=True) if any_rand else None
+        gen = None
+        if not self.is_gpu and any_rand:
+            gen = torch.Generator().manual_seed(int(seeds[0]) & 0x7FFFFFFF)
+        ids, lp = ops.sample(logits, t, s, want_logprob=want_lp, generator=gen)
+        ids_h = ids.cpu().tolist()
+        lp_h = lp.cpu().tolist() if lp is not None else [0.0] * len(ids_h)
+        return {r.seq_id: (int(ids_h[i]), float(lp_h[i])) for i, r in enumerate(reqs)}
+
+    def _run_eager(self, so: SchedulerOutput, block_tables):
+        ids, pos, slots, d_bt, d_len, p_ql, p_ctx, p_bt = self._prepare(so, block_tables)
+        dev = self.device
+        nd = len(so.decodes)
+        T = len(ids)
+        host = torch.tensor([ids, pos, slots], dtype=torch.long)
+        if self.is_gpu:
+            host = host.pin_memory()
+        hd = host.to(dev, non_blocking=True)
+        meta = AttnMeta(num_tokens=T, positions=hd[1], slot_mapping=hd[2], num_decode=nd)
+        if nd:
+            meta.d_block_tables = torch.from_numpy(d_bt).to(dev, non_blocking=True)
+            meta.d_seq_lens = torch.from_numpy(d_len).to(dev, non_blocking=True)
+            meta.d_max_ctx = int(d_len.max())
+            w = [a.window for a in self.model.attention_layers()]
+            mctx = meta.d_max_ctx
+            meta.d_split = ops.decode_split_plan(mctx, nd, self.Hkv, self.Hq // self.Hkv)
+        if p_ql:
+            meta.num_prefill_tokens = sum(p_ql)
+            meta.p_block_tables = torch.from_numpy(p_bt).to(dev, non_blocking=True)
+            qs = np.cumsum([0] + p_ql[:-1]).astype(np.int32)
+            meta.p_q_start = torch.from_numpy(qs).to(dev, non_blocking=True)
+            meta.p_q_len = torch.tensor(p_ql, dtype=torch.int32).to(dev, non_blocking=True)
+            meta.p_ctx_len = torch.tensor(p_ctx, dtype=torch.int32).to(dev, non_blocking=True)
+            meta.p_items = self._items(p_ql, p_ctx)
+        return self.model(hd[0], meta)
+
+    # ------------------------------------------------------------ graphs
+    def _bucket(self, n: int) -> int:
+        b = 1
+        while b < n:
+            b *= 2
+        return b
+
+    def _graph_ok(self, n: int) -> bool:
+        return self.is_gpu and not self.cfg.enforce_eager and bool(self.graphs) and \
+            self._bucket(n) in self.graphs
+
+    @torch.no_grad()
+    def capture_graphs(self):
+        if not self.is_gpu or self.cfg.enforce_eager:
+            return
+        maxb = min(self.cfg.cuda_graph_max_bs, self.cfg.sched.max_num_seqs)
+        buckets = []
+        b = 1
+        while b <= maxb:
+            buckets.append(b)
+            b *= 2
+        if buckets[-1] < maxb:
+            buckets.append(self._bucket(maxb))
+        M = buckets[-1]
+        dev = self.device
+        split_size, nsplit = self.graph_split
+        self.g_ids = torch.zeros(M, dtype=torch.long, device=dev)
+        self.g_pos = torch.zeros(M, dtype=torch.long, device=dev)
+        self.g_slots = torch.full((M,), -1, dtype=torch.long, device=dev)
+        self.g_bt = torch.zeros(M, self.width, dtype=torch.int32, device=dev)
+        self.g_len = torch.ones(M, dtype=torch.int32, device=dev)
+        self.g_ws = (torch.empty(M * self.Hq * nsplit * self.D, dtype=torch.float32, device=dev),
+                     torch.empty(M * self.Hq * nsplit * 2, dtype=torch.float32, device=dev))
+        pool = torch.cuda.graph_pool_handle()
+        t0 = time.time()
+        for B in reversed(buckets):
+            meta = AttnMeta(num_tokens=B, positions=self.g_pos[:B], slot_mapping=self.g_slots[:B],
+                            num_decode=B, d_block_tables=self.g_bt[:B], d_seq_lens=self.g_len[:B],
+                            d_split=self.graph_split, d_workspace=self.g_ws, d_max_ctx=self.max_model_len)
+            s = torch.cuda.Stream()
+            s.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(s):
+                for _ in range(2):
+                    h = self.model(self.g_ids[:B], meta)
+                    lg = self.model.compute_logits(h)
+            torch.cuda.current_stream().wait_stream(s)
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, pool=pool):
+                h = self.model(self.g_ids[:B], meta)
+                lg = self.model.compute_logits(h)
+            self.graphs[B] = (g, lg)
+        torch.cuda.synchronize()
+        log.info("captured %d decode graphs in %.1fs", len(buckets), time.time() - t0)
+
+    def _run_decode_graph(self, so: SchedulerOutput, block_tables, rows):
+        n = len(so.decodes)
+        B = self._bucket(n)
+        g, lg = self.graphs[B]
+        ids, pos, slots, d_bt, d_len, *_ = self._prepare(so, block_tables)
+        if B > n:
+            pad = B - n
+            ids = ids + [0] * pad
+            pos = pos + [0] * pad
+            slots = slots + [-1] * pad
+            d_bt = np.concatenate([d_bt, np.zeros((pad, self.width), dtype=np.int32)])
+            d_len = np.concatenate([d_len, np.ones(pad, dtype=np.int32)])
+        host = torch.tensor([ids, pos, slots], dtype=torch.long).pin_memory()
+        self.g_ids[:B].copy_(host[0], non_blocking=True)
+        self.g_pos[:B].copy_(host[1], non_blocking=True)
+        self.g_slots[:B].copy_(host[2], non_blocking=True)
+        self.g_bt[:B].copy_(torch.from_numpy(d_bt).pin_memory(), non_blocking=True)
+        self.g_len[:B].copy_(torch.from_numpy(d_len).pin_memory(), non_blocking=True)
+        g.replay()
+        if len(rows) == B and rows == list(range(B)):
+            return lg
+        return lg[torch.tensor(rows, dtype=torch.long).to(self.device, non_blocking=True)]

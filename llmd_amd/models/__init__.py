@@ -1,0 +1,25 @@
+"""Model registry: HF ``model_type`` -> implementation."""
+from __future__ import annotations
+
+from llmd_amd.engine.config import ModelConfig
+
+
+def model_class(cfg: ModelConfig):
+    t = cfg.model_type
+    if t in ("llama", "qwen3", "qwen2", "mistral"):
+        from .llama import LlamaForCausalLM
+
+        return LlamaForCausalLM
+    if t == "gpt_oss":
+        from .gpt_oss import GptOssForCausalLM
+
+        return GptOssForCausalLM
+    if t in ("mixtral", "qwen3_moe"):
+        from .moe_llama import MoELlamaForCausalLM
+
+        return MoELlamaForCausalLM
+    raise ValueError(f"unsupported model_type {t!r}")
+
+
+def build_model(cfg: ModelConfig, device="cuda", max_pos: int = 32768):
+    return model_class(cfg)(cfg, device=device, max_pos=max_pos)

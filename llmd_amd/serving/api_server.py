@@ -1,0 +1,396 @@
+"""OpenAI-compatible HTTP server for the llmd_amd engine.
+
+Endpoints
+  GET  /health                     liveness (returns immediately)
+  GET  /v1/models                  readiness (model loaded) + LoRA adapters
+  GET  /metrics                    Prometheus, vLLM-compatible names
+  POST /v1/completions             (stream / non-stream, kv_transfer_params)
+  POST /v1/chat/completions
+  POST /v1/completions/render      exact token ids (router token-producer)
+  POST /v1/chat/completions/render
+  POST /tokenize, /detokenize
+  POST /pause, /resume, /reset_prefix_cache   (IRO-ready lifecycle hooks)
+  GET  /is_paused
+P/D: a body with ``kv_transfer_params.do_remote_decode`` makes this engine a
+prefill producer (the response carries the params the decoder needs);
+``do_remote_prefill`` makes it pull KV over kvx before decoding.
+"""
+from __future__ import annotations
+
+import argparse
+import asyncio
+import json
+import logging
+import os
+import time
+import uuid
+from typing import Optional
+
+from aiohttp import web
+
+from llmd_amd.engine.config import EngineConfig, add_engine_args, engine_config_from_args
+from llmd_amd.engine.request import SamplingParams
+
+from .async_engine import AsyncEngine, EngineDeadError
+from .tokenizer import load_tokenizer, render_chat
+
+log = logging.getLogger("llmd.api")
+
+
+def _err(status: int, msg: str, typ: str = "invalid_request_error"):
+    return web.json_response({"error": {"message": msg, "type": typ, "code": status}}, status=status)
+
+
+class OpenAIServer:
+    def __init__(self, aeng: AsyncEngine, cfg: EngineConfig, tokenizer=None, lora_manager=None):
+        self.aeng = aeng
+        self.cfg = cfg
+        self.name = cfg.served_name
+        mc = cfg.model_config
+        self.tok = tokenizer or load_tokenizer(cfg.tokenizer, mc.vocab_size, mc.bos_token_id, mc.eos_ids[0])
+        self.lora = lora_manager
+        self.chat_style = "llama3" if mc.model_type == "llama" else "chatml"
+        self.ready = True
+        self.extra_metrics = []  # callables returning bytes
+
+    # ------------------------------------------------------------ app
+    def app(self) -> web.Application:
+        app = web.Application(client_max_size=256 * 1024 * 1024)
+        r = app.router
+        r.add_get("/health", self.health)
+        r.add_get("/v1/models", self.models)
+        r.add_get("/metrics", self.metrics)
+        r.add_post("/v1/completions", self.completions)
+        r.add_post("/v1/chat/completions", self.chat)
+        r.add_post("/v1/completions/render", self.render_completion)
+        r.add_post("/v1/chat/completions/render", self.render_chat)
+        r.add_post("/tokenize", self.tokenize)
+        r.add_post("/detokenize", self.detokenize)
+        r.add_post("/pause", self.pause)
+        r.add_post("/resume", self.resume)
+        r.add_get("/is_paused", self.is_paused)
+        r.add_post("/reset_prefix_cache", self.reset_prefix_cache)
+        r.add_post("/v1/load_lora_adapter", self.load_lora)
+        r.add_post("/v1/unload_lora_adapter", self.unload_lora)
+        return app
+
+    async def health(self, req):
+        if self.aeng.dead is not None:
+            return web.Response(status=503, text="engine dead")
+        return web.Response(text="")
+
+    async def models(self, req):
+        data = [{"id": self.name, "object": "model", "created": int(time.time()), "owned_by": "llmd-amd",
+                 "root": self.cfg.model, "parent": None, "max_model_len": self.cfg.sched.max_model_len}]
+        if self.lora is not None:
+            for n in self.lora.names():
+                data.append({"id": n, "object": "model", "created": int(time.time()), "owned_by": "llmd-amd",
+                             "root": n, "parent": self.name})
+        return web.json_response({"object": "list", "data": data})
+
+    async def metrics(self, req):
+        body = self.aeng.engine.metrics.render()
+        for f in self.extra_metrics:
+            body += f()
+        return web.Response(body=body, content_type="text/plain", charset="utf-8")
+
+    # ------------------------------------------------------------ helpers
+    def _prompt_ids(self, body) -> list[list[int]]:
+        p = body.get("prompt")
+        if p is None:
+            raise ValueError("prompt is required")
+        if isinstance(p, str):
+            return [self.tok.encode(p)]
+        if isinstance(p, list) and p and isinstance(p[0], int):
+            return [list(p)]
+        if isinstance(p, list) and p and isinstance(p[0], str):
+            return [self.tok.encode(x) for x in p]
+        if isinstance(p, list) and p and isinstance(p[0], list):
+            return [list(x) for x in p]
+        raise ValueError("unsupported prompt format")
+
+    def _chat_ids(self, body) -> list[int]:
+        msgs = body.get("messages")
+        if not isinstance(msgs, list) or not msgs:
+            raise ValueError("messages is required")
+        return self.tok.encode(render_chat(msgs, body.get("add_generation_prompt", True), self.chat_style))
+
+    def _lora_id(self, body) -> int:
+        m = body.get("model")
+        if self.lora is not None and m and m != self.name:
+            return self.lora.id_of(m)
+        return 0
+
+    def _check_model(self, body):
+        m = body.get("model")
+        if m is None or m == self.name or m == self.cfg.model:
+            return None
+        if self.lora is not None and self.lora.has(m):
+            return None
+        return _err(404, f"The model `{m}` does not exist.", "NotFoundError")
+
+    @staticmethod
+    def _priority(req, body) -> int:
+        if "priority" in body:
+            return int(body["priority"])
+        return 0
+
+    # ------------------------------------------------------------ completions
+    async def completions(self, req: web.Request):
+        return await self._serve(req, chat=False)
+
+    async def chat(self, req: web.Request):
+        return await self._serve(req, chat=True)
+
+    async def _serve(self, req: web.Request, chat: bool):
+        try:
+            body = await req.json()
+        except Exception:  # noqa: BLE001
+            return _err(400, "invalid JSON body")
+        bad = self._check_model(body)
+        if bad is not None:
+            return bad
+        try:
+            prompts = [self._chat_ids(body)] if chat else self._prompt_ids(body)
+            params = SamplingParams.from_openai(body, default_max=16 if not chat else
+                                                max(1, self.cfg.sched.max_model_len - 1))
+        except (ValueError, TypeError) as e:
+            return _err(400, str(e))
+        for p in prompts:
+            if len(p) == 0:
+                return _err(400, "empty prompt")
+            if len(p) + 1 > self.cfg.sched.max_model_len:
+                return _err(400, f"This model's maximum context length is {self.cfg.sched.max_model_len} "
+                                 f"tokens. However, you requested {len(p)} tokens in the prompt.")
+            if chat:
+                params.max_tokens = min(params.max_tokens, self.cfg.sched.max_model_len - len(p))
+        ktp = body.get("kv_transfer_params")
+        prio = self._priority(req, body)
+        lora = self._lora_id(body)
+        rid_base = req.headers.get("x-request-id") or f"{'chatcmpl' if chat else 'cmpl'}-{uuid.uuid4().hex}"
+        stream = bool(body.get("stream", False))
+        include_usage = bool((body.get("stream_options") or {}).get("include_usage", False))
+        created = int(time.time())
+        model_name = body.get("model") or self.name
+        if stream:
+            return await self._stream(req, rid_base, prompts[0], params, prio, ktp, lora, chat, include_usage,
+                                      created, model_name)
+        # non-streaming: run all prompts concurrently
+        async def one(i, ids):
+            text_ids, lps, last = [], [], None
+            async for o in self.aeng.generate(f"{rid_base}-{i}" if len(prompts) > 1 else rid_base, ids, params,
+                                              prio, ktp, lora):
+                text_ids.extend(o.new_token_ids)
+                lps.extend(o.new_logprobs)
+                last = o
+                text = self.tok.decode(text_ids)
+                if params.stop and any(s in text for s in params.stop):
+                    self.aeng.abort(f"{rid_base}-{i}" if len(prompts) > 1 else rid_base)
+                    break
+            return ids, text_ids, lps, last
+        try:
+            results = await asyncio.gather(*[one(i, p) for i, p in enumerate(prompts)])
+        except EngineDeadError as e:
+            return _err(503, str(e), "ServiceUnavailable")
+        except Exception as e:  # noqa: BLE001
+            return _err(500, f"{type(e).__name__}: {e}", "InternalServerError")
+        choices, n_prompt, n_out = [], 0, 0
+        out_ktp = None
+        for i, (ids, toks, lps, last) in enumerate(results):
+            text = self.tok.decode(toks)
+            finish = last.finish_reason if last is not None else "abort"
+            if params.stop:
+                for s in params.stop:
+                    k = text.find(s)
+                    if k >= 0:
+                        text, finish = text[:k], "stop"
+            n_prompt += len(ids)
+            n_out += len(toks)
+            if last is not None and last.kv_transfer_params is not None:
+                out_ktp = last.kv_transfer_params
+            ch = {"index": i, "finish_reason": finish}
+            if chat:
+                ch["message"] = {"role": "assistant", "content": text}
+            else:
+                ch["text"] = text
+                if params.logprobs:
+                    ch["logprobs"] = {"token_logprobs": lps, "tokens": [self.tok.decode([t]) for t in toks]}
+            if body.get("return_token_ids"):
+                ch["token_ids"] = toks
+            choices.append(ch)
+        resp = {"id": rid_base, "object": "chat.completion" if chat else "text_completion", "created": created,
+                "model": model_name, "choices": choices,
+                "usage": {"prompt_tokens": n_prompt, "completion_tokens": n_out,
+                          "total_tokens": n_prompt + n_out}}
+        if out_ktp is not None or (ktp and ktp.get("do_remote_decode")):
+            resp["kv_transfer_params"] = out_ktp
+        return web.json_response(resp)
+
+    async def _stream(self, req, rid, ids, params, prio, ktp, lora, chat, include_usage, created, model_name):
+        resp = web.StreamResponse(headers={"Content-Type": "text/event-stream", "Cache-Control": "no-cache"})
+        await resp.prepare(req)
+        obj = "chat.completion.chunk" if chat else "text_completion"
+        toks: list[int] = []
+        sent = ""
+        n_out = 0
+
+        async def send(d):
+            await resp.write(b"data: " + json.dumps(d).encode() + b"\n\n")
+
+        if chat:
+            await send({"id": rid, "object": obj, "created": created, "model": model_name,
+                        "choices": [{"index": 0, "delta": {"role": "assistant", "content": ""},
+                                     "finish_reason": None}]})
+        finish = None
+        last = None
+        try:
+            async for o in self.aeng.generate(rid, ids, params, prio, ktp, lora):
+                last = o
+                toks.extend(o.new_token_ids)
+                n_out = len(toks)
+                text = self.tok.decode(toks)
+                stop_hit = False
+                if params.stop:
+                    for s in params.stop:
+                        k = text.find(s)
+                        if k >= 0:
+                            text, stop_hit = text[:k], True
+                delta = text[len(sent):] if text.startswith(sent) else text
+                sent = text
+                finish = "stop" if stop_hit else (o.finish_reason if o.finished else None)
+                ch = {"index": 0, "finish_reason": finish}
+                if chat:
+                    ch["delta"] = {"content": delta}
+                else:
+                    ch["text"] = delta
+                d = {"id": rid, "object": obj, "created": created, "model": model_name, "choices": [ch]}
+                if o.finished and o.kv_transfer_params is not None:
+                    d["kv_transfer_params"] = o.kv_transfer_params
+                await send(d)
+                if stop_hit:
+                    self.aeng.abort(rid)
+                    break
+        except (ConnectionResetError, asyncio.CancelledError):
+            self.aeng.abort(rid)
+            raise
+        except Exception as e:  # noqa: BLE001
+            await send({"error": {"message": str(e), "type": type(e).__name__}})
+        if include_usage:
+            await send({"id": rid, "object": obj, "created": created, "model": model_name, "choices": [],
+                        "usage": {"prompt_tokens": len(ids), "completion_tokens": n_out,
+                                  "total_tokens": len(ids) + n_out}})
+        await resp.write(b"data: [DONE]\n\n")
+        await resp.write_eof()
+        return resp
+
+    # ------------------------------------------------------------ render / tokenize
+    async def render_completion(self, req):
+        body = await req.json()
+        try:
+            ids = self._prompt_ids(body)
+        except ValueError as e:
+            return _err(400, str(e))
+        return web.json_response({"model": body.get("model") or self.name, "token_ids": ids[0],
+                                  "prompt_token_ids": ids[0], "count": len(ids[0]),
+                                  "max_model_len": self.cfg.sched.max_model_len})
+
+    async def render_chat(self, req):
+        body = await req.json()
+        try:
+            ids = self._chat_ids(body)
+        except ValueError as e:
+            return _err(400, str(e))
+        return web.json_response({"model": body.get("model") or self.name, "token_ids": ids,
+                                  "prompt_token_ids": ids, "count": len(ids),
+                                  "max_model_len": self.cfg.sched.max_model_len})
+
+    async def tokenize(self, req):
+        body = await req.json()
+        if "messages" in body:
+            ids = self._chat_ids(body)
+        else:
+            ids = self.tok.encode(body.get("prompt", ""))
+        return web.json_response({"tokens": ids, "count": len(ids), "max_model_len": self.cfg.sched.max_model_len})
+
+    async def detokenize(self, req):
+        body = await req.json()
+        return web.json_response({"prompt": self.tok.decode(body.get("tokens", []))})
+
+    # ------------------------------------------------------------ lifecycle
+    async def pause(self, req):
+        self.aeng.pause()
+        return web.json_response({"paused": True})
+
+    async def resume(self, req):
+        self.aeng.resume()
+        return web.json_response({"paused": False})
+
+    async def is_paused(self, req):
+        return web.json_response({"is_paused": self.aeng.engine.paused})
+
+    async def reset_prefix_cache(self, req):
+        await self.aeng.call(lambda e: e.reset_prefix_cache())
+        return web.json_response({"status": "ok"})
+
+    async def load_lora(self, req):
+        if self.lora is None:
+            return _err(400, "LoRA is not enabled (--enable-lora)")
+        body = await req.json()
+        try:
+            await self.aeng.call(lambda e: self.lora.load(body["lora_name"], body.get("lora_path")))
+        except Exception as e:  # noqa: BLE001
+            return _err(400, str(e))
+        return web.Response(text=f"Success: LoRA adapter '{body['lora_name']}' added successfully.")
+
+    async def unload_lora(self, req):
+        if self.lora is None:
+            return _err(400, "LoRA is not enabled (--enable-lora)")
+        body = await req.json()
+        await self.aeng.call(lambda e: self.lora.unload(body["lora_name"]))
+        return web.Response(text=f"Success: LoRA adapter '{body['lora_name']}' removed successfully.")
+
+
+def build_server(cfg: EngineConfig, engine=None):
+    from llmd_amd.engine.engine import LLMEngine
+
+    eng = engine or LLMEngine(cfg)
+    aeng = AsyncEngine(eng)
+    srv = OpenAIServer(aeng, cfg)
+    if cfg.kv_events_config and cfg.kv_events_config.get("enable_kv_cache_events"):
+        from .kv_events import KVEventPublisher
+
+        pub = KVEventPublisher.from_config(cfg.kv_events_config, cfg.served_name, cfg.cache.block_size)
+        eng.event_sink = pub.publish
+        srv.kv_event_publisher = pub
+    if eng.connector is not None:
+        srv.extra_metrics.append(eng.connector.render_metrics)
+    return srv
+
+
+def main(argv=None):
+    p = argparse.ArgumentParser("llmd-amd serve")
+    add_engine_args(p)
+    p.add_argument("--host", default="0.0.0.0")
+    p.add_argument("--port", type=int, default=8000)
+    p.add_argument("--shutdown-timeout", type=float, default=0.0)
+    p.add_argument("--log-level", default="info")
+    a = p.parse_args(argv)
+    logging.basicConfig(level=a.log_level.upper(), format="%(asctime)s %(levelname)s %(name)s: %(message)s")
+    cfg = engine_config_from_args(a)
+    srv = build_server(cfg)
+    app = srv.app()
+
+    async def on_shutdown(_app):
+        if a.shutdown_timeout > 0:
+            await srv.aeng.drain(a.shutdown_timeout)
+        srv.aeng.shutdown()
+
+    app.on_shutdown.append(on_shutdown)
+    # keep-alive must exceed the sidecar's 90 s idle timeout (VLLM_HTTP_TIMEOUT_KEEP_ALIVE=120)
+    keepalive = float(os.environ.get("VLLM_HTTP_TIMEOUT_KEEP_ALIVE", "120"))
+    web.run_app(app, host=a.host, port=a.port, keepalive_timeout=keepalive, access_log=None,
+                shutdown_timeout=max(a.shutdown_timeout, 1.0))
+
+
+if __name__ == "__main__":
+    main()

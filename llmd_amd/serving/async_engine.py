@@ -1,0 +1,167 @@
+"""AsyncEngine: drives ``LLMEngine.step()`` on a dedicated thread and fans
+outputs out to per-request asyncio queues.
+
+The GPU loop never runs on the event loop: HTTP handlers submit commands
+(add / abort / pause / resume / reset) through a thread-safe queue, the engine
+thread applies them between steps and pushes ``RequestOutput``s back with
+``loop.call_soon_threadsafe``. ``drain(timeout)`` implements graceful shutdown
+(``--shutdown-timeout`` semantics, SURVEY §5.3 "Graceful drain").
+"""
+from __future__ import annotations
+
+import asyncio
+import logging
+import queue
+import threading
+import time
+from typing import AsyncIterator, Optional
+
+from llmd_amd.engine.engine import LLMEngine
+from llmd_amd.engine.request import RequestOutput, SamplingParams
+
+log = logging.getLogger("llmd.async")
+
+
+class EngineDeadError(RuntimeError):
+    pass
+
+
+class AsyncEngine:
+    def __init__(self, engine: LLMEngine):
+        self.engine = engine
+        self.cmds: "queue.Queue[tuple]" = queue.Queue()
+        self.streams: dict[str, tuple[asyncio.AbstractEventLoop, asyncio.Queue]] = {}
+        self.wake = threading.Event()
+        self.stop_flag = False
+        self.dead: Optional[BaseException] = None
+        self.accepting = True
+        self.thread = threading.Thread(target=self._loop, name="llmd-engine", daemon=True)
+        self.thread.start()
+
+    # ------------------------------------------------------------ engine thread
+    def _loop(self):
+        eng = self.engine
+        try:
+            while not self.stop_flag:
+                self._apply_cmds()
+                if eng.has_unfinished() and not eng.paused:
+                    outs = eng.step()
+                    for o in outs:
+                        self._emit(o)
+                    if eng.connector is not None:
+                        for o in eng.connector.take_outputs():
+                            self._emit(o)
+                else:
+                    if eng.connector is not None:
+                        eng.connector.tick()
+                        for o in eng.connector.take_outputs():
+                            self._emit(o)
+                    self.wake.wait(0.005 if eng.has_unfinished() else 0.05)
+                    self.wake.clear()
+        except BaseException as e:  # pragma: no cover - surfaced to clients
+            log.exception("engine loop died")
+            self.dead = e
+            for rid, (loop, q) in list(self.streams.items()):
+                loop.call_soon_threadsafe(q.put_nowait, e)
+
+    def _apply_cmds(self):
+        while True:
+            try:
+                cmd = self.cmds.get_nowait()
+            except queue.Empty:
+                return
+            op = cmd[0]
+            try:
+                if op == "add":
+                    _, rid, toks, params, prio, ktp, lora, arrival = cmd
+                    self.engine.add_request(rid, toks, params, prio, ktp, lora, arrival)
+                elif op == "abort":
+                    self.engine.abort(cmd[1])
+                    self._close(cmd[1], None)
+                elif op == "call":
+                    fn, fut, loop = cmd[1], cmd[2], cmd[3]
+                    try:
+                        res = fn(self.engine)
+                        loop.call_soon_threadsafe(fut.set_result, res)
+                    except Exception as e:  # noqa: BLE001
+                        loop.call_soon_threadsafe(fut.set_exception, e)
+            except Exception as e:  # noqa: BLE001
+                if op == "add":
+                    self._close(cmd[1], e)
+
+    def _emit(self, o: RequestOutput):
+        ent = self.streams.get(o.request_id)
+        if ent is None:
+            return
+        loop, q = ent
+        loop.call_soon_threadsafe(q.put_nowait, o)
+        if o.finished:
+            self.streams.pop(o.request_id, None)
+
+    def _close(self, rid, err):
+        ent = self.streams.pop(rid, None)
+        if ent is not None:
+            loop, q = ent
+            loop.call_soon_threadsafe(q.put_nowait, err if err is not None else StopAsyncIteration())
+
+    # ------------------------------------------------------------ API (event loop)
+    async def generate(self, request_id: str, prompt_token_ids: list[int], params: SamplingParams,
+                       priority: int = 0, kv_transfer_params: Optional[dict] = None,
+                       lora_id: int = 0) -> AsyncIterator[RequestOutput]:
+        if self.dead is not None:
+            raise EngineDeadError(str(self.dead))
+        if not self.accepting:
+            raise EngineDeadError("server is shutting down")
+        loop = asyncio.get_running_loop()
+        q: asyncio.Queue = asyncio.Queue()
+        self.streams[request_id] = (loop, q)
+        self.cmds.put(("add", request_id, prompt_token_ids, params, priority, kv_transfer_params,
+                       lora_id, time.monotonic()))
+        self.wake.set()
+        try:
+            while True:
+                item = await q.get()
+                if isinstance(item, StopAsyncIteration):
+                    return
+                if isinstance(item, BaseException):
+                    raise item
+                yield item
+                if item.finished:
+                    return
+        finally:
+            if request_id in self.streams:
+                self.streams.pop(request_id, None)
+                self.cmds.put(("abort", request_id))
+                self.wake.set()
+
+    def abort(self, request_id: str):
+        self.cmds.put(("abort", request_id))
+        self.wake.set()
+
+    async def call(self, fn):
+        """Run fn(engine) on the engine thread between steps."""
+        loop = asyncio.get_running_loop()
+        fut = loop.create_future()
+        self.cmds.put(("call", fn, fut, loop))
+        self.wake.set()
+        return await fut
+
+    def pause(self):
+        self.engine.paused = True
+
+    def resume(self):
+        self.engine.paused = False
+        self.wake.set()
+
+    async def drain(self, timeout: float):
+        self.accepting = False
+        t0 = time.monotonic()
+        while self.streams and time.monotonic() - t0 < timeout:
+            await asyncio.sleep(0.05)
+        for rid in list(self.streams):
+            self.abort(rid)
+
+    def shutdown(self):
+        self.stop_flag = True
+        self.wake.set()
+        self.thread.join(timeout=5)
