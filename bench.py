@@ -40,7 +40,7 @@ def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=40)
-    p.add_argument("--warmup", type=int, default=40)
+    p.add_argument("--warmup", type=int, default=20)
     p.add_argument("--model", default="llama-3-70b")
     p.add_argument("--isl", type=int, default=5000)
     p.add_argument("--osl", type=int, default=250)
@@ -98,9 +98,23 @@ def main():
         eng.add_request(f"r{rank}-{nreq[0]}", toks,
                         SamplingParams(max_tokens=max_tokens, temperature=0.0, ignore_eos=True))
 
-    # staggered start: spread remaining output lengths so completions de-synchronise
+    # Setup (untimed, not part of warmup): admit C requests with staggered output
+    # lengths and run until every one of them is past its prefill, so warmup/timed
+    # steps see steady-state serving (decodes + chunked prefills of new arrivals)
+    # instead of the initial all-prefill ramp.
     for i in range(a.concurrency):
         new_request(max(1, int(a.osl * (i + 1) / a.concurrency)))
+    ts = time.time()
+    setup_steps = 0
+    while setup_steps < 100000:
+        eng.step()
+        setup_steps += 1
+        if eng.sched.num_waiting == 0 and all(r.output_token_ids for r in eng.sched.running):
+            break
+    while eng.sched.num_running + eng.sched.num_waiting < a.concurrency:
+        new_request(a.osl)
+    torch.cuda.synchronize()
+    log(rank, f"setup: {setup_steps} steps in {time.time() - ts:.1f}s (batch filled to {a.concurrency})")
 
     def run_steps(n):
         for _ in range(n):
