@@ -1,0 +1,79 @@
+"""Request parsers (docs/architecture/core/router/epp/request-handling.md:71-75,
+docs/api-reference/epp-http-apis.md)."""
+from __future__ import annotations
+
+import json
+
+from .. import headers as H
+from ..types import CIHeaders, InferenceRequest
+from .base import Parser, register
+
+OPENAI_PATHS = ("/v1/completions", "/v1/chat/completions", "/v1/embeddings", "/v1/responses",
+                "/v1/conversations", "/v1/messages", "/inference/v1/generate")
+
+
+def _flatten_prompt(body: dict) -> str:
+    if "messages" in body:
+        parts = []
+        for m in body.get("messages") or []:
+            c = m.get("content")
+            if isinstance(c, list):
+                c = "".join(p.get("text", "") for p in c if isinstance(p, dict))
+            parts.append(f"<{m.get('role', '')}>{c or ''}")
+        return "".join(parts)
+    if "input" in body:  # responses / embeddings
+        i = body["input"]
+        return i if isinstance(i, str) else json.dumps(i)
+    p = body.get("prompt", "")
+    if isinstance(p, list):
+        if p and isinstance(p[0], int):
+            return " ".join(map(str, p))
+        return "".join(x if isinstance(x, str) else " ".join(map(str, x)) for x in p)
+    return p or ""
+
+
+@register("openai-parser")
+class OpenAIParser(Parser):
+    def parse(self, path, body: bytes, headers) -> InferenceRequest:
+        try:
+            d = json.loads(body) if body else {}
+        except json.JSONDecodeError as e:
+            raise ValueError(f"invalid JSON body: {e}") from e
+        if not isinstance(d, dict):
+            raise ValueError("JSON object expected")
+        h = headers if isinstance(headers, CIHeaders) else CIHeaders(dict(headers))
+        req = InferenceRequest(path=path, body=d, headers=h, raw_size=len(body))
+        req.model = d.get("model", "") or ""
+        req.target_model = req.model
+        req.prompt = _flatten_prompt(d)
+        p = d.get("prompt")
+        if isinstance(p, list) and p and isinstance(p[0], int):
+            req.token_ids = list(p)
+        req.stream = bool(d.get("stream", False))
+        return req
+
+
+@register("passthrough-parser")
+class PassthroughParser(Parser):
+    def parse(self, path, body, headers):
+        h = headers if isinstance(headers, CIHeaders) else CIHeaders(dict(headers))
+        try:
+            d = json.loads(body) if body else {}
+        except json.JSONDecodeError:
+            d = {}
+        req = InferenceRequest(path=path, body=d if isinstance(d, dict) else {}, headers=h, raw_size=len(body))
+        req.model = req.body.get("model", "") if isinstance(req.body, dict) else ""
+        req.target_model = req.model
+        return req
+
+
+@register("vllmgrpc-parser")
+class VllmGrpcParser(OpenAIParser):
+    """vLLM gRPC Generate/Embed (token-in): the HTTP bridge forwards the
+    decoded message as JSON with `token_ids`."""
+
+    def parse(self, path, body, headers):
+        req = super().parse(path, body, headers)
+        if "token_ids" in req.body:
+            req.token_ids = list(req.body["token_ids"])
+        return req

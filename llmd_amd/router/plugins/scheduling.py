@@ -1,0 +1,463 @@
+"""Scheduling plugins: filters, scorers, pickers, profile handlers, deciders
+(docs/architecture/core/router/epp/scheduling.md:73-118,
+docs/architecture/advanced/disaggregation/README.md:50-102).
+
+Every scorer returns a score in [0, 1] per candidate; profiles multiply by the
+configured weight and sum.
+"""
+from __future__ import annotations
+
+import base64
+import math
+import random
+import time
+from typing import Optional
+
+from .. import headers as H
+from ..types import (ACTIVE_LORAS, KV_USAGE, MAX_LORA, RUNNING, WAITING, WAITING_LORAS, Endpoint,
+                     InferenceRequest, ProfileRunResult, SchedulingResult)
+from .base import Decider, Filter, Picker, PreRequest, ProfileHandler, ResponseProcessor, Scorer, register
+
+
+def _minmax_inverse(vals: dict[str, float]) -> dict[str, float]:
+    """Lower is better -> [0,1]; all-equal -> 1."""
+    if not vals:
+        return {}
+    lo, hi = min(vals.values()), max(vals.values())
+    if hi <= lo:
+        return {k: 1.0 for k in vals}
+    return {k: (hi - v) / (hi - lo) for k, v in vals.items()}
+
+
+# ======================================================================= filters
+@register("label-selector-filter", "by-label", "by-label-selector")
+class LabelSelectorFilter(Filter):
+    """Keeps endpoints matching `matchLabels` (all must match) or, in the
+    llm-d by-label form, whose `label` is in `validValues` (`allowsNoLabel`)."""
+
+    def filter(self, req, eps):
+        ml = self.p("matchLabels") or {}
+        label = self.p("label")
+        valid = set(self.p("validValues") or [])
+        allow_none = bool(self.p("allowsNoLabel", False))
+        out = []
+        for e in eps:
+            if any(e.labels.get(k) != v for k, v in ml.items()):
+                continue
+            if label is not None:
+                v = e.labels.get(label)
+                if v is None and not allow_none:
+                    continue
+                if v is not None and valid and v not in valid:
+                    continue
+            out.append(e)
+        return out
+
+
+@register("prefill-filter", "prefill-endpoints-filter")
+class PrefillFilter(Filter):
+    """llm-d.ai/role in {prefill, prefill-decode}."""
+
+    def filter(self, req, eps):
+        return [e for e in eps if e.labels.get("llm-d.ai/role", "prefill-decode") in ("prefill", "prefill-decode")]
+
+
+@register("decode-filter", "decode-endpoints-filter")
+class DecodeFilter(Filter):
+    """llm-d.ai/role in {decode, prefill-decode} (unlabelled pods count as both)."""
+
+    def filter(self, req, eps):
+        return [e for e in eps if e.labels.get("llm-d.ai/role", "prefill-decode") in ("decode", "prefill-decode")]
+
+
+@register("encode-filter")
+class EncodeFilter(Filter):
+    def filter(self, req, eps):
+        return [e for e in eps if e.labels.get("llm-d.ai/role") == "encode"]
+
+
+@register("prefix-cache-affinity-filter")
+class PrefixCacheAffinityFilter(Filter):
+    """Epsilon-greedy stickiness: keep endpoints whose prefix score >=
+    affinityThreshold (default 0.80) unless exploring (probability
+    explorationProbability) or the sticky set's estimated TTFT under load is
+    much worse than the best non-sticky one (TTFT load gate, using
+    peakPrefillThroughput tokens/s, default 15928)."""
+
+    def filter(self, req, eps):
+        thr = float(self.p("affinityThreshold", 0.80))
+        explore = float(self.p("explorationProbability", 0.0))
+        peak = float(self.p("peakPrefillThroughput", 15928))
+        gate = float(self.p("ttftLoadGateRatio", 2.0))
+        prod = self.p("prefixMatchInfoProducerName")
+        info = _prefix_info(req, prod)
+        sticky = [e for e in eps if info.get(e.key, 0.0) >= thr]
+        if not sticky or random.random() < explore:
+            return eps
+        others = [e for e in eps if e not in sticky]
+        if others:
+            n_tok = max(1, len(req.token_ids) if req.token_ids else len(req.prompt) // 4)
+
+            def est(e, hit):
+                queued = e.metric(WAITING, 0) + e.metric(RUNNING, 0) * 0.1
+                return (queued * n_tok + n_tok * (1 - hit)) / peak
+
+            best_sticky = min(est(e, info.get(e.key, 0.0)) for e in sticky)
+            best_other = min(est(e, info.get(e.key, 0.0)) for e in others)
+            if best_sticky > gate * best_other + 0.05:
+                return eps
+        return sticky
+
+
+@register("slo-headroom-tier-filter")
+class SloHeadroomTierFilter(Filter):
+    """Keep endpoints with non-negative predicted SLO headroom (positive tier);
+    if none, the negative tier; with explorationProbability keep all."""
+
+    def filter(self, req, eps):
+        pred = req.data.get("predicted_latency") or {}
+        if not pred:
+            return eps
+        if random.random() < float(self.p("explorationProbability", 0.0)):
+            return eps
+        pos = [e for e in eps if pred.get(e.key, {}).get("headroom", 0.0) >= 0]
+        return pos or eps
+
+
+# ======================================================================= scorers
+@register("queue-scorer", "queue-depth-scorer")
+class QueueScorer(Scorer):
+    def score(self, req, eps):
+        return _minmax_inverse({e.key: float(e.metric(WAITING, 0)) for e in eps})
+
+
+@register("kv-cache-utilization-scorer", "kv-cache-scorer")
+class KVCacheUtilizationScorer(Scorer):
+    def score(self, req, eps):
+        return {e.key: max(0.0, min(1.0, 1.0 - float(e.metric(KV_USAGE, 0.0)))) for e in eps}
+
+
+@register("running-requests-size-scorer")
+class RunningRequestsScorer(Scorer):
+    def score(self, req, eps):
+        return _minmax_inverse({e.key: float(e.metric(RUNNING, 0)) for e in eps})
+
+
+@register("active-request-scorer")
+class ActiveRequestScorer(Scorer, PreRequest, ResponseProcessor):
+    """Router-side in-flight request count (fewer is better); entries expire
+    after requestTimeout seconds (default 300) in case a response is lost."""
+
+    def __init__(self, *a, **k):
+        super().__init__(*a, **k)
+        self.active: dict[str, dict[str, float]] = {}
+
+    def _count(self, key):
+        tmo = float(self.p("requestTimeout", 300))
+        now = time.monotonic()
+        d = self.active.get(key, {})
+        for rid in [r for r, t in d.items() if now - t > tmo]:
+            d.pop(rid, None)
+        return len(d)
+
+    def score(self, req, eps):
+        counts = {e.key: self._count(e.key) for e in eps}
+        mx = max(counts.values()) if counts else 0
+        if mx == 0:
+            return {k: 1.0 for k in counts}
+        return {k: 1.0 - c / mx for k, c in counts.items()}
+
+    def pre_request(self, req, result):
+        for prof, r in result.profile_results.items():
+            for e in r.targets[:1]:
+                self.active.setdefault(e.key, {})[req.request_id + ":" + prof] = time.monotonic()
+
+    def on_response_complete(self, req, ep, info):
+        for d in self.active.values():
+            for k in [k for k in d if k.startswith(req.request_id + ":")]:
+                d.pop(k, None)
+
+
+@register("token-load-scorer")
+class TokenLoadScorer(Scorer):
+    """Scores by router-tracked in-flight token load (input + expected output)."""
+
+    def score(self, req, eps):
+        load = self.ctx.inflight_tokens if self.ctx is not None else {}
+        return _minmax_inverse({e.key: float(load.get(e.key, 0)) for e in eps})
+
+
+def _prefix_info(req: InferenceRequest, producer: Optional[str]) -> dict[str, float]:
+    """Per-endpoint prefix match fraction from a prefix producer."""
+    pm = req.data.get("prefix_match", {})
+    if producer and producer in pm:
+        return pm[producer]
+    if pm:
+        # prefer precise if present, else approximate
+        for k in ("precise-prefix-cache-producer", "approx-prefix-cache-producer"):
+            if k in pm:
+                return pm[k]
+        return next(iter(pm.values()))
+    return {}
+
+
+@register("prefix-cache-scorer", "prefix-scorer", "precise-prefix-cache-scorer")
+class PrefixCacheScorer(Scorer):
+    """Fraction of the request's prefix blocks cached on each endpoint, read
+    from a prefix producer (`prefixMatchInfoProducerName`)."""
+
+    def score(self, req, eps):
+        info = _prefix_info(req, self.p("prefixMatchInfoProducerName"))
+        return {e.key: float(info.get(e.key, 0.0)) for e in eps}
+
+
+@register("no-hit-lru-scorer")
+class NoHitLRUScorer(Scorer, PreRequest):
+    """Cold requests (no prefix hit anywhere) go to never-used endpoints
+    first, then least-recently-used; warm requests: all equal."""
+
+    def __init__(self, *a, **k):
+        super().__init__(*a, **k)
+        self.last_cold: dict[str, float] = {}
+
+    def _cold(self, req):
+        info = _prefix_info(req, self.p("prefixMatchInfoProducerName"))
+        return not any(v > 0 for v in info.values())
+
+    def score(self, req, eps):
+        if not self._cold(req):
+            return {e.key: 1.0 for e in eps}
+        never = [e for e in eps if e.key not in self.last_cold]
+        used = sorted([e for e in eps if e.key in self.last_cold], key=lambda e: self.last_cold[e.key])
+        out = {e.key: 1.0 for e in never}
+        n = len(used)
+        for i, e in enumerate(used):
+            out[e.key] = 0.5 * (1.0 - i / max(1, n)) if never else 1.0 - i / max(1, n)
+        return out
+
+    def pre_request(self, req, result):
+        if self._cold(req):
+            for r in result.profile_results.values():
+                for e in r.targets[:1]:
+                    self.last_cold[e.key] = time.monotonic()
+
+
+@register("lora-affinity-scorer")
+class LoraAffinityScorer(Scorer):
+    """1.0 adapter active, 0.8 loadable (slots free), 0.5 waiting there, 0 otherwise."""
+
+    def score(self, req, eps):
+        m = req.target_model or req.model
+        out = {}
+        for e in eps:
+            active = e.metric(ACTIVE_LORAS, set()) or set()
+            waiting = e.metric(WAITING_LORAS, set()) or set()
+            mx = int(e.metric(MAX_LORA, 0) or 0)
+            if m in active:
+                out[e.key] = 1.0
+            elif m in waiting:
+                out[e.key] = 0.5
+            elif mx and len(active) < mx:
+                out[e.key] = 0.8
+            else:
+                out[e.key] = 0.0 if mx else 1.0
+        return out
+
+
+SESSION_HEADER = "x-session-token"
+
+
+@register("session-affinity-scorer")
+class SessionAffinityScorer(Scorer, ResponseProcessor):
+    """Max score for the endpoint encoded in the request's session token; the
+    token is returned on responses (response header `x-session-token`)."""
+
+    def score(self, req, eps):
+        tok = req.headers.get(SESSION_HEADER)
+        target = None
+        if tok:
+            try:
+                target = base64.b64decode(tok).decode()
+            except Exception:  # noqa: BLE001
+                target = None
+        return {e.key: (1.0 if target == e.key else 0.0) for e in eps}
+
+    def on_response_headers(self, req, ep, status, headers):
+        headers[SESSION_HEADER] = base64.b64encode(ep.key.encode()).decode()
+
+
+@register("latency-scorer")
+class LatencyScorer(Scorer):
+    """Scores by predicted SLO headroom (predicted-latency-producer);
+    headroomSelectionStrategy least (pack: smallest non-negative headroom) or
+    most (spread). Falls back to a composite KV/queue/prefix score when no
+    predictions are available (predictor down)."""
+
+    def score(self, req, eps):
+        pred = req.data.get("predicted_latency") or {}
+        if not pred:
+            kv = KVCacheUtilizationScorer(self.name).score(req, eps)
+            q = QueueScorer(self.name).score(req, eps)
+            pre = PrefixCacheScorer(self.name).score(req, eps)
+            return {k: (kv[k] + q[k] + pre[k]) / 3 for k in kv}
+        strat = self.p("headroomSelectionStrategy", "least")
+        hr = {e.key: pred.get(e.key, {}).get("headroom", -1e9) for e in eps}
+        pos = {k: v for k, v in hr.items() if v >= 0}
+        out = {k: 0.0 for k in hr}
+        if pos:
+            lo, hi = min(pos.values()), max(pos.values())
+            for k, v in pos.items():
+                if hi <= lo:
+                    out[k] = 1.0
+                else:
+                    f = (v - lo) / (hi - lo)
+                    out[k] = 0.5 + 0.5 * (1 - f if strat == "least" else f)
+        else:
+            # nobody meets the SLO: prefer the least negative
+            lo, hi = min(hr.values()), max(hr.values())
+            for k, v in hr.items():
+                out[k] = 0.5 * ((v - lo) / (hi - lo) if hi > lo else 1.0)
+        return out
+
+
+# ======================================================================= pickers
+@register("max-score-picker")
+class MaxScorePicker(Picker):
+    def pick(self, req, scored):
+        n = int(self.p("maxNumOfEndpoints", 1))
+        if not scored:
+            return []
+        random.shuffle(scored)  # random tie-break
+        scored.sort(key=lambda x: -x[1])
+        return [e for e, _ in scored[:n]]
+
+
+@register("random-picker")
+class RandomPicker(Picker):
+    def pick(self, req, scored):
+        n = int(self.p("maxNumOfEndpoints", 1))
+        eps = [e for e, _ in scored]
+        random.shuffle(eps)
+        return eps[:n]
+
+
+@register("weighted-random-picker")
+class WeightedRandomPicker(Picker):
+    """Lottery scheduling: probability proportional to score."""
+
+    def pick(self, req, scored):
+        n = int(self.p("maxNumOfEndpoints", 1))
+        pool = [(e, max(s, 0.0)) for e, s in scored]
+        out = []
+        while pool and len(out) < n:
+            tot = sum(s for _, s in pool)
+            if tot <= 0:
+                i = random.randrange(len(pool))
+            else:
+                r = random.random() * tot
+                acc = 0.0
+                i = len(pool) - 1
+                for j, (_, s) in enumerate(pool):
+                    acc += s
+                    if r <= acc:
+                        i = j
+                        break
+            out.append(pool.pop(i)[0])
+        return out
+
+
+# ======================================================================= profile handlers
+@register("single-profile-handler", "data-parallel-profile-handler")
+class SingleProfileHandler(ProfileHandler):
+    def pick_profiles(self, req, profiles, results):
+        if results:
+            return []
+        name = self.p("profile") or next(iter(profiles))
+        return [name]
+
+    def process_results(self, req, results):
+        name = next(iter(results))
+        return SchedulingResult(name, results)
+
+
+@register("always-disagg-pd-decider")
+class AlwaysDisaggPD(Decider):
+    def should_disaggregate(self, req, decode_ep):
+        return True
+
+
+@register("prefix-based-pd-decider", "pd-threshold-decider")
+class ThresholdDecider(Decider):
+    """Disaggregate when the uncached suffix on the chosen decoder exceeds
+    `nonCachedTokens` (default 0 = always)."""
+
+    def should_disaggregate(self, req, decode_ep):
+        thr = int(self.p("nonCachedTokens", self.p("threshold", 0)))
+        n = len(req.token_ids) if req.token_ids else max(1, len(req.prompt) // 4)
+        hit = _prefix_info(req, None).get(decode_ep.key, 0.0) if decode_ep else 0.0
+        return n * (1.0 - hit) > thr
+
+
+@register("always-disagg-multimodal-decider")
+class AlwaysDisaggMM(Decider):
+    def should_disaggregate(self, req, decode_ep):
+        return bool(req.data.get("has_multimodal", False))
+
+
+@register("disagg-profile-handler", "pd-profile-handler")
+class DisaggProfileHandler(ProfileHandler):
+    """Runs the decode profile, asks the decider, then (maybe) the prefill and
+    encode profiles; D is the destination, P goes in `x-prefiller-host-port`
+    and E in `x-encoder-hosts-ports`."""
+
+    def _names(self, profiles):
+        dec = self.p("decodeProfile", "decode")
+        pre = self.p("prefillProfile", "prefill")
+        enc = self.p("encodeProfile", "encode")
+        return dec, pre, enc
+
+    def _decider(self, kind="prefill"):
+        ds = self.p("deciders") or {}
+        name = ds.get(kind) if isinstance(ds, dict) else None
+        if name is None and kind == "prefill":
+            name = self.p("deciderPluginName") or self.p("decider")
+        if name and self.ctx is not None:
+            return self.ctx.plugins.get(name)
+        return None
+
+    def pick_profiles(self, req, profiles, results):
+        dec, pre, enc = self._names(profiles)
+        if not results:
+            return [dec] if dec in profiles else [next(iter(profiles))]
+        if dec in results and pre not in results and "_disagg_decided" not in req.data:
+            req.data["_disagg_decided"] = True
+            d = results[dec].targets[0] if results[dec].targets else None
+            out = []
+            dz = self._decider("prefill")
+            if pre in profiles and d is not None and (dz is None or dz.should_disaggregate(req, d)):
+                out.append(pre)
+            ez = self._decider("encode")
+            if enc in profiles and ez is not None and ez.should_disaggregate(req, d):
+                out.append(enc)
+            return out
+        return []
+
+    def process_results(self, req, results):
+        dec, pre, enc = self._names(results)
+        hdrs = {}
+        if pre in results and results[pre].targets:
+            hdrs[H.PREFILLER] = ",".join(e.key for e in results[pre].targets)
+        if enc in results and results[enc].targets:
+            hdrs[H.ENCODER] = ",".join(e.key for e in results[enc].targets)
+        primary = dec if dec in results else next(iter(results))
+        req.data["pd_decision"] = "disagg" if H.PREFILLER in hdrs else "decode-only"
+        return SchedulingResult(primary, results, headers=hdrs)
+
+
+@register("disagg-headers-handler")
+class DisaggHeadersHandler(PreRequest):
+    """Pre-request hook that materialises the P/E headers set by the
+    disagg profile handler (kept as a separate plugin for config parity)."""
+
+    def pre_request(self, req, result):
+        req.data.setdefault("upstream_headers", {}).update(result.headers)

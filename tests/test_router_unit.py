@@ -1,0 +1,366 @@
+"""Router unit tests: config loader/validator, headers, rewrites, filters,
+scorers, pickers, profile handlers, flow control semantics, indexes, predictor."""
+import asyncio
+import time
+
+import numpy as np
+import pytest
+
+from llmd_amd.router import headers as H
+from llmd_amd.router.api import ControlPlane
+from llmd_amd.router.config import ConfigError, extract_config_text, load_config
+from llmd_amd.router.epp import EPP
+from llmd_amd.router.flow_control import (DISPATCHED, EVICTED_TTL, REJECTED_CAPACITY, FlowController,
+                                          parse_duration, parse_quantity)
+from llmd_amd.router.types import KV_USAGE, RUNNING, WAITING, CIHeaders, Endpoint, InferenceRequest
+
+OPT_BASELINE = """
+apiVersion: llm-d.ai/v1alpha1
+kind: EndpointPickerConfig
+plugins:
+- type: queue-scorer
+- type: kv-cache-utilization-scorer
+- type: prefix-cache-scorer
+- type: no-hit-lru-scorer
+schedulingProfiles:
+- name: default
+  plugins:
+  - pluginRef: queue-scorer
+    weight: 2
+  - pluginRef: kv-cache-utilization-scorer
+    weight: 2
+  - pluginRef: prefix-cache-scorer
+    weight: 3
+  - pluginRef: no-hit-lru-scorer
+    weight: 2
+"""
+
+PD_VALUES = """
+router:
+  epp:
+    pluginsConfigFile: "pd-config.yaml"
+    pluginsCustomConfig:
+      pd-config.yaml: |
+        apiVersion: llm-d.ai/v1alpha1
+        kind: EndpointPickerConfig
+        plugins:
+        - type: disagg-headers-handler
+        - type: always-disagg-pd-decider
+        - type: disagg-profile-handler
+          parameters:
+            deciderPluginName: always-disagg-pd-decider
+        - type: prefill-filter
+        - type: decode-filter
+        - type: prefix-cache-scorer
+        - type: queue-scorer
+        - type: kv-cache-utilization-scorer
+        - type: active-request-scorer
+        schedulingProfiles:
+        - name: prefill
+          plugins:
+          - pluginRef: prefill-filter
+          - pluginRef: prefix-cache-scorer
+            weight: 3
+          - pluginRef: queue-scorer
+            weight: 2
+        - name: decode
+          plugins:
+          - pluginRef: decode-filter
+          - pluginRef: active-request-scorer
+            weight: 2
+          - pluginRef: prefix-cache-scorer
+            weight: 3
+"""
+
+FLOW = """
+apiVersion: llm-d.ai/v1alpha1
+kind: EndpointPickerConfig
+featureGates: [flowControl]
+plugins:
+- type: round-robin-fairness-policy
+- type: fcfs-ordering-policy
+- type: concurrency-detector
+  parameters: {maxConcurrency: 1}
+- type: queue-scorer
+saturationDetector:
+  pluginRef: concurrency-detector
+flowControl:
+  maxRequests: "1k"
+  defaultRequestTTL: "60s"
+  priorityBands:
+  - priority: 100
+    fairnessPolicyRef: round-robin-fairness-policy
+  - priority: -10
+    maxRequests: 2
+"""
+
+
+def ep(i, role=None, **m):
+    labels = {"llm-d.ai/role": role} if role else {}
+    e = Endpoint(f"pod{i}", f"10.0.0.{i}", 8000, labels=labels)
+    e.attrs.update(m)
+    return e
+
+
+def req(prompt="hello", headers=None, **kw):
+    r = InferenceRequest("/v1/completions", {"prompt": prompt, "model": "m"}, CIHeaders(headers or {}))
+    r.prompt = prompt
+    r.model = r.target_model = "m"
+    for k, v in kw.items():
+        setattr(r, k, v)
+    return r
+
+
+# ------------------------------------------------------------------ config
+def test_load_reference_shaped_configs():
+    c = load_config(OPT_BASELINE)
+    assert list(c.profiles) == ["default"]
+    p = c.profiles["default"]
+    assert [w for _, w in p.scorers] == [2, 2, 3, 2]
+    assert p.picker.plugin_type == "max-score-picker"  # tier-3 injection
+    assert any(x.plugin_type == "approx-prefix-cache-producer" for x in c.producers)  # auto producer
+    assert any(s.plugin_type == "metrics-data-source" for s, _ in c.data_sources)  # injected default
+    c2 = load_config(extract_config_text(PD_VALUES))
+    assert c2.profile_handler.plugin_type == "disagg-profile-handler"
+    assert set(c2.profiles) == {"prefill", "decode"}
+    c3 = load_config(FLOW)
+    assert c3.flow_control_enabled and c3.saturation_detector.plugin_type == "concurrency-detector"
+
+
+def test_reference_guide_configs_parse():
+    import glob
+    import os
+
+    files = glob.glob("/root/reference/guides/*/router/*.values.yaml")
+    if not files:
+        pytest.skip("reference tree not mounted")
+    n = 0
+    for f in files:
+        text = open(f).read()
+        try:
+            extract_config_text(text)
+        except ConfigError:
+            continue  # values without a custom plugin config
+        load_config(text)
+        n += 1
+    assert n >= 5
+
+
+@pytest.mark.parametrize("bad,msg", [
+    ("plugins: [{type: queue-scorer}, {type: queue-scorer}]", "duplicate"),
+    ("plugins: [{type: queue-scorer}]\nschedulingProfiles: [{name: a, plugins: [{pluginRef: nope}]}]", "undefined"),
+    ("plugins: [{type: max-score-picker}, {type: random-picker}]", "more than one picker"),
+    ("plugins: [{type: queue-scorer}]\nschedulingProfiles: [{name: a}, {name: b}]", "profile handler"),
+    ("plugins: [{type: not-a-plugin}]", "unknown plugin"),
+    ("plugins: [{type: queue-scorer}]\nschedulingProfiles: [{name: a}, {name: a}]", "duplicate"),
+])
+def test_config_validation(bad, msg):
+    with pytest.raises(ConfigError, match=msg):
+        load_config("apiVersion: llm-d.ai/v1alpha1\nkind: EndpointPickerConfig\n" + bad)
+
+
+def test_quantities():
+    assert parse_quantity("1Gi") == 2**30 and parse_quantity("1k") == 1000 and parse_quantity(5) == 5
+    assert parse_duration("60s") == 60 and parse_duration("50ms") == 0.05 and parse_duration("1m30s") == 90
+
+
+# ------------------------------------------------------------------ headers / rewrites
+def test_header_alias_precedence():
+    h = CIHeaders({"X-Gateway-Inference-Fairness-Id": "old", "x-llm-d-inference-fairness-id": "new"})
+    assert H.lookup(h, H.FAIRNESS_ID) == "new"
+    h2 = CIHeaders({"X-SLO-TTFT-MS": "250"})
+    assert H.float_header(h2, H.SLO_TTFT) == 250.0
+
+
+def test_model_rewrite_precedence():
+    cp = ControlPlane()
+    cp.load_yaml("""
+kind: InferenceModelRewrite
+metadata: {name: generic}
+spec: {rules: [{targets: [{modelRewrite: g, weight: 1}]}]}
+---
+kind: InferenceModelRewrite
+metadata: {name: exact}
+spec: {rules: [{matches: [{model: {type: Exact, value: base}}], targets: [{modelRewrite: lora-a, weight: 100}, {modelRewrite: lora-b, weight: 0}]}]}
+---
+kind: InferenceObjective
+metadata: {name: premium}
+spec: {priority: 100}
+""")
+    assert cp.rewrite("base") == ("lora-a", "exact")
+    assert cp.rewrite("other") == ("g", "generic")
+    assert cp.priority_of("premium") == 100 and cp.priority_of("nope") == 0 and cp.priority_of(None) == 0
+
+
+# ------------------------------------------------------------------ scheduling plugins
+def test_scorers_and_picker():
+    c = load_config(OPT_BASELINE)
+    epp = EPP(c.raw)
+    eps = [ep(1, **{WAITING: 0, KV_USAGE: 0.9}), ep(2, **{WAITING: 10, KV_USAGE: 0.1}), ep(3, **{WAITING: 2, KV_USAGE: 0.2})]
+    r = req()
+    r.data["prefix_match"] = {"approx-prefix-cache-producer": {eps[0].key: 0.0, eps[1].key: 0.0, eps[2].key: 0.0}}
+    res = epp.run_profile(r, epp.cfg.profiles["default"], eps)
+    # ep3: queue 0.8*2 + kv 0.8*2 = 3.2 (+ lru) beats ep1 (2+0.2) and ep2 (0+1.8)
+    assert res.targets[0] is eps[2]
+
+
+def test_disagg_profile_handler_sets_prefiller_header():
+    epp = EPP(extract_config_text(PD_VALUES))
+    eps = [ep(1, "prefill"), ep(2, "decode"), ep(3, "decode"), ep(4, "prefill")]
+    res = epp.schedule(req(), eps)
+    assert res.target.role == "decode"
+    assert H.PREFILLER in res.headers
+    assert res.headers[H.PREFILLER] in (eps[0].key, eps[3].key)
+
+
+def test_filters():
+    from llmd_amd.router.plugins.scheduling import DecodeFilter, LabelSelectorFilter, PrefillFilter
+
+    eps = [ep(1, "prefill"), ep(2, "decode"), ep(3, "prefill-decode"), ep(4)]
+    assert [e.name for e in PrefillFilter("f").filter(req(), eps)] == ["pod1", "pod3", "pod4"]
+    assert [e.name for e in DecodeFilter("f").filter(req(), eps)] == ["pod2", "pod3", "pod4"]
+    f = LabelSelectorFilter("f", {"label": "llm-d.ai/role", "validValues": ["decode"]})
+    assert [e.name for e in f.filter(req(), eps)] == ["pod2"]
+
+
+def test_weighted_random_picker_distribution():
+    from llmd_amd.router.plugins.scheduling import WeightedRandomPicker
+
+    p = WeightedRandomPicker("p")
+    eps = [ep(1), ep(2)]
+    wins = sum(p.pick(req(), [(eps[0], 3.0), (eps[1], 1.0)])[0] is eps[0] for _ in range(4000))
+    assert 0.70 < wins / 4000 < 0.80
+
+
+def test_approx_prefix_affinity_learns():
+    epp = EPP(OPT_BASELINE)
+    eps = [ep(i, **{WAITING: 0, KV_USAGE: 0.0}) for i in range(1, 5)]
+
+    async def go():
+        epp.store.endpoints = {e.key: e for e in eps}
+        prompt = "x" * 3000
+        d1 = await epp.schedule_request(req(prompt), b"{}")
+        picks = set()
+        for _ in range(5):
+            d = await epp.schedule_request(req(prompt + "tail"), b"{}")
+            picks.add(d.endpoint.key)
+        return d1.endpoint.key, picks
+
+    first, picks = asyncio.run(go())
+    assert picks == {first}
+
+
+# ------------------------------------------------------------------ flow control
+def test_flow_control_priority_capacity_ttl():
+    c = load_config(FLOW)
+
+    class Det:
+        sat = 1.0
+
+        def saturation(self, eps):
+            return self.sat
+
+    det = Det()
+
+    async def go():
+        fc = FlowController({"priorityBands": [{"priority": -10, "maxRequests": 2}], "defaultRequestTTL": "0.3s"},
+                            c.plugins, det, lambda: [])
+        fc.start()
+        order = []
+
+        async def one(name, prio, fid="a"):
+            r = req(priority=prio, fairness_id=fid)
+            out = await fc.enqueue_and_wait(r)
+            order.append((name, out))
+
+        tasks = [asyncio.create_task(one("lo1", -10)), asyncio.create_task(one("lo2", -10))]
+        await asyncio.sleep(0.01)
+        rej = await fc.enqueue_and_wait(req(priority=-10))  # band full -> 429
+        tasks.append(asyncio.create_task(one("hi", 100)))
+        await asyncio.sleep(0.01)
+        det.sat = 0.0
+        fc.notify()
+        await asyncio.gather(*tasks)
+        # TTL: saturated forever -> evicted
+        det.sat = 1.0
+        ttl = await fc.enqueue_and_wait(req(priority=0))
+        await fc.stop()
+        return rej, order, ttl
+
+    rej, order, ttl = asyncio.run(go())
+    assert rej == REJECTED_CAPACITY
+    assert order[0] == ("hi", DISPATCHED)  # strict priority
+    assert {o for _, o in order} == {DISPATCHED}
+    assert ttl == EVICTED_TTL
+
+
+def test_round_robin_fairness():
+    from llmd_amd.router.flow_control import Band, Flow, QueueItem, RoundRobinFairness
+
+    rr = RoundRobinFairness("rr")
+    b = Band(0, 0, 0, None, rr)
+    for fid in ["a", "b", "c"]:
+        b.flows[fid] = Flow(fid, heap=[(0, 0, None)])
+    seq = [rr.pick_flow(b).fid for _ in range(6)]
+    assert seq == ["a", "b", "c", "a", "b", "c"]
+
+
+# ------------------------------------------------------------------ native indexes / predictor
+def test_precise_index_consecutive_prefix_and_tiers():
+    from llmd_amd import _rt_loader
+
+    R = _rt_loader.rt()
+    ix = R.KVBlockIndex(1000, 8)
+    ix.add("A", [1, 2, 3, 4], "gpu")
+    ix.add("B", [1, 2], "gpu")
+    ix.add("B", [4], "gpu")
+    ix.add("C", [3, 4], "gpu")
+    ix.add("D", [1, 2, 3], "cpu")
+    s = ix.score([1, 2, 3, 4, 5], ["A", "B", "C", "D"], [1.0, 0.8], 1.0)
+    assert s == {"A": 4.0, "B": 2.0, "C": 0.0, "D": pytest.approx(2.4)}
+    ix.remove("A", [2], "gpu")
+    assert ix.score([1, 2, 3], ["A"], [1.0, 0.8], 1.0)["A"] == 1.0
+    ix.add_speculative("E", [1, 2], 0.05)
+    assert ix.score([1, 2], ["E"], [1.0], 1.0)["E"] == 2.0
+    time.sleep(0.08)
+    assert ix.score([1, 2], ["E"], [1.0], 1.0)["E"] == 0.0
+    ix.clear_pod("B")
+    assert ix.score([1], ["B"], [1.0], 1.0)["B"] == 0.0
+
+
+def test_hash_chain_matches_engine_block_manager():
+    from llmd_amd import _rt_loader
+
+    R = _rt_loader.rt()
+    toks = np.arange(100, dtype=np.int32)
+    keys = R.hash_blocks(toks, 16, 0)
+    bm = R.BlockManager(32, 16, True, True)
+    bm.acquire(1, toks, 0)
+    bm.grow(1, 100)
+    bm.commit(1, toks, 100)
+    stored = [e[1] for e in bm.take_events() if e[0] == 0]
+    assert stored == keys[: len(stored)] and len(stored) == 6
+
+
+def test_gbdt_predictor_vs_numpy():
+    from llmd_amd.router.predictor import LatencyPredictor, mape
+
+    rng = np.random.default_rng(0)
+    lp = LatencyPredictor(min_samples=50, retrain_every=10**9)
+    X = []
+    for _ in range(3000):
+        f = {"kv_cache_percentage": rng.random(), "input_token_length": int(rng.integers(10, 8000)),
+             "num_request_waiting": int(rng.integers(0, 20)), "num_request_running": int(rng.integers(0, 64)),
+             "prefix_cache_score": rng.random(), "inflight_input_tokens": int(rng.integers(0, 50000)),
+             "num_tokens_generated": 0}
+        ttft = 20 + 0.05 * f["input_token_length"] * (1 - 0.8 * f["prefix_cache_score"]) + 30 * f["num_request_waiting"]
+        tpot = 8 + 0.1 * f["num_request_running"] + 10 * f["kv_cache_percentage"]
+        X.append((f, ttft, tpot))
+        lp.add_sample(f, ttft * (1 + 0.02 * rng.standard_normal()), tpot)
+    lp.train()
+    pred = lp.predict([f for f, _, _ in X[-500:]])
+    t = np.array([p["ttft_ms"] for p in pred])
+    y = np.array([x[1] for x in X[-500:]])
+    assert mape(t, y) < 0.10  # reference quotes ~5% MAPE on real traffic
+    tp = np.array([p["tpot_ms"] for p in pred])
+    assert mape(tp, np.array([x[2] for x in X[-500:]])) < 0.05
