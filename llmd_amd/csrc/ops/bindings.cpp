@@ -25,6 +25,13 @@ void llmd_sample(const void*, int64_t, int, int, int, const float*, const int64_
                  hipStream_t);
 void llmd_topk_topp_mask(float*, int64_t, int, int, const int*, const float*, const float*,
                          hipStream_t);
+int llmd_kvx_copy_blocks(void*, const void*, int64_t, int64_t, const int*, int, const int64_t*, int,
+                         int64_t, hipStream_t);
+int llmd_kvx_ipc_export(const void*, void*, int64_t*);
+int llmd_kvx_ipc_open(const void*, void**);
+int llmd_kvx_ipc_close(void*);
+int llmd_kvx_handle_size();
+int llmd_kvx_dma_blocks(void*, const void*, int64_t, int64_t, const int*, int, int64_t, hipStream_t);
 }
 
 namespace {
@@ -203,6 +210,50 @@ void topk_topp_mask(torch::Tensor logits, c10::optional<torch::Tensor> topk,
   llmd_topk_topp_mask(logits.data_ptr<float>(), logits.stride(0), B, V, k, p, t, cur_stream());
 }
 
+// ---------------------------------------------------------------- kvx
+// dst/src are base addresses of the two KV pools (src may be an IPC-mapped peer pointer)
+void kvx_copy_blocks(torch::Tensor dst, int64_t src_ptr, int64_t dst_stride, int64_t src_stride,
+                     torch::Tensor pairs, torch::Tensor segs, int64_t max_seg_bytes) {
+  CHECK_CUDA(dst); CHECK_CUDA(pairs); CHECK_CUDA(segs);
+  CHECK_DT(pairs, at::kInt); CHECK_DT(segs, at::kLong);
+  TORCH_CHECK(pairs.is_contiguous() && pairs.dim() == 2 && pairs.size(1) == 2, "pairs [n,2] int32");
+  TORCH_CHECK(segs.is_contiguous() && segs.dim() == 2 && segs.size(1) == 3, "segs [m,3] int64");
+  TORCH_CHECK(src_ptr != 0, "null source pool");
+  int rc = llmd_kvx_copy_blocks(dst.data_ptr(), (const void*)src_ptr, dst_stride, src_stride,
+                                pairs.data_ptr<int>(), pairs.size(0), segs.data_ptr<int64_t>(),
+                                segs.size(0), max_seg_bytes, cur_stream());
+  TORCH_CHECK(rc == 0, "kvx_copy_blocks failed: ", rc);
+}
+
+void kvx_dma_blocks(torch::Tensor dst, int64_t src_ptr, int64_t dst_stride, int64_t src_stride,
+                    torch::Tensor pairs_cpu, int64_t block_bytes) {
+  CHECK_CUDA(dst); CHECK_DT(pairs_cpu, at::kInt);
+  TORCH_CHECK(!pairs_cpu.is_cuda() && pairs_cpu.is_contiguous() && pairs_cpu.size(1) == 2, "pairs cpu [n,2]");
+  int rc = llmd_kvx_dma_blocks(dst.data_ptr(), (const void*)src_ptr, dst_stride, src_stride,
+                               pairs_cpu.data_ptr<int>(), pairs_cpu.size(0), block_bytes, cur_stream());
+  TORCH_CHECK(rc == 0, "kvx_dma_blocks failed: ", rc);
+}
+
+py::tuple kvx_ipc_export(torch::Tensor t) {
+  CHECK_CUDA(t);
+  std::string h(llmd_kvx_handle_size(), '\0');
+  int64_t off = 0;
+  int rc = llmd_kvx_ipc_export(t.data_ptr(), h.data(), &off);
+  TORCH_CHECK(rc == 0, "hipIpcGetMemHandle failed: ", rc);
+  return py::make_tuple(py::bytes(h), off);
+}
+
+int64_t kvx_ipc_open(py::bytes handle) {
+  std::string h = handle;
+  TORCH_CHECK((int)h.size() == llmd_kvx_handle_size(), "bad IPC handle size");
+  void* p = nullptr;
+  int rc = llmd_kvx_ipc_open(h.data(), &p);
+  TORCH_CHECK(rc == 0, "hipIpcOpenMemHandle failed: ", rc);
+  return (int64_t)p;
+}
+
+void kvx_ipc_close(int64_t p) { llmd_kvx_ipc_close((void*)p); }
+
 }  // namespace
 
 PYBIND11_MODULE(_C, m) {
@@ -216,4 +267,9 @@ PYBIND11_MODULE(_C, m) {
   m.def("prefill_tokens_per_item", &llmd_prefill_tokens_per_item);
   m.def("sample", &sample);
   m.def("topk_topp_mask", &topk_topp_mask);
+  m.def("kvx_copy_blocks", &kvx_copy_blocks);
+  m.def("kvx_dma_blocks", &kvx_dma_blocks);
+  m.def("kvx_ipc_export", &kvx_ipc_export);
+  m.def("kvx_ipc_open", &kvx_ipc_open);
+  m.def("kvx_ipc_close", &kvx_ipc_close);
 }

@@ -49,6 +49,7 @@ class LLMEngine:
             self.runner.capture_graphs()
         self.paused = False
         self.step_count = 0
+        self.last_step_empty = False
 
     # ------------------------------------------------------------ API
     def add_request(self, request_id: str, prompt_token_ids: list[int],
@@ -81,16 +82,18 @@ class LLMEngine:
             self.connector.tick()
         t0 = time.monotonic()
         so = self.sched.schedule()
+        err_outs = self._error_outputs()
+        self.last_step_empty = so.empty
         if so.empty:
             self._flush_events()
-            return []
+            return err_outs
         if self.offload is not None:
             self.offload.before_step(so)
         sampled = self.runner.execute(so, self.block_tables(so))
         touched = self.sched.update(so, sampled)
         dt = time.monotonic() - t0
         self.step_count += 1
-        outs = []
+        outs = err_outs
         for r in touched:
             o = RequestOutput(r.request_id, [r.output_token_ids[-1]], [r.output_logprobs[-1]],
                               r.status.finished, r.finish_reason, r.num_prompt_tokens,
@@ -102,6 +105,15 @@ class LLMEngine:
         self.metrics.on_step(so, touched, dt, self.sched.num_running, self.sched.num_waiting,
                              self.bm.usage(), self.bm.prefix_stats())
         self._flush_events()
+        return outs
+
+    def _error_outputs(self) -> list[RequestOutput]:
+        outs = []
+        for r in self.sched.errored:
+            outs.append(RequestOutput(r.request_id, [], [], True, r.finish_reason, r.num_prompt_tokens,
+                                      len(r.output_token_ids), r.num_cached_tokens))
+            self.metrics.on_finish(r)
+        self.sched.errored.clear()
         return outs
 
     def _flush_events(self):

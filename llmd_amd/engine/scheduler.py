@@ -129,6 +129,7 @@ class Scheduler:
         self.requests: dict[str, Request] = {}
         self.eos = set(cfg.model_config.eos_ids)
         self.num_preemptions_total = 0
+        self.errored: list[Request] = []  # finished by the scheduler itself (not via update)
         self._tok_arrays: dict[str, np.ndarray] = {}
 
     # ------------------------------------------------------------ admission
@@ -218,6 +219,7 @@ class Scheduler:
                     if policy == "fail":
                         self.bm.free(r.seq_id)
                         self._finish(r, Status.FINISHED_ERROR)
+                        self.errored.append(r)
                         continue
                     self.bm.free(r.seq_id)
                     r.num_computed_tokens = 0
@@ -285,6 +287,7 @@ class Scheduler:
                         self.waiting.pop()
                         self.bm.free(r.seq_id)
                         self._finish(r, Status.FINISHED_ERROR)
+                        self.errored.append(r)
                         continue
                 break
             self.waiting.pop()

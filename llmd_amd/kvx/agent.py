@@ -1,0 +1,367 @@
+"""kvx agent: P/D KV-cache transfer (the NIXL role in
+docs/architecture/advanced/disaggregation/README.md:133-178 and
+operations-vllm.md).
+
+Roles and protocol (vLLM NixlConnector-compatible ``kv_transfer_params``):
+* Prefill side (``do_remote_decode``): after the prefill the request's
+  blocks are *held*; the response carries
+  ``{do_remote_prefill, remote_engine_id, remote_host, remote_port,
+  remote_block_ids, remote_request_id, remote_tp_size, ...}``. Blocks are
+  released when the decoder sends ``free`` (after its READ) or after
+  ``abort_timeout`` (VLLM_NIXL_ABORT_REQUEST_TIMEOUT, default 480 s).
+* Decode side (``do_remote_prefill``): a transfer worker fetches the remote
+  agent's metadata once per peer over the TCP side channel (layout
+  compatibility check), then pulls the blocks one-sided:
+    - ``ipc``  (GPU, same node): the peer's whole KV pool is mapped once via
+      a HIP IPC handle and copied with the kvx HIP kernel (xGMI peer reads;
+      heterogeneous-TP head re-slicing via copy segments) or SDMA;
+    - ``tcp``  (CPU CI / fallback): block bytes streamed over the side channel.
+  Completion -> ``free`` notification to the prefiller.
+Side channel: length-prefixed msgpack request/response over TCP
+(VLLM_NIXL_SIDE_CHANNEL_HOST/PORT semantics; default port 5557).
+Fault injection: LLMD_KVX_FAULT=drop|delay:<s>|corrupt (probability
+LLMD_KVX_FAULT_P, default 1.0) for the failure-policy tests.
+"""
+from __future__ import annotations
+
+import logging
+import os
+import queue
+import random
+import socket
+import socketserver
+import struct
+import threading
+import time
+import uuid
+from dataclasses import dataclass, field
+from typing import Optional
+
+import msgpack
+import numpy as np
+import torch
+
+log = logging.getLogger("llmd.kvx")
+
+
+def _send(sock, obj):
+    b = msgpack.packb(obj, use_bin_type=True)
+    sock.sendall(struct.pack("<Q", len(b)) + b)
+
+
+def _recv(sock):
+    hdr = _recvn(sock, 8)
+    n = struct.unpack("<Q", hdr)[0]
+    return msgpack.unpackb(_recvn(sock, n), raw=False)
+
+
+def _recvn(sock, n):
+    buf = bytearray()
+    while len(buf) < n:
+        chunk = sock.recv(min(n - len(buf), 1 << 22))
+        if not chunk:
+            raise ConnectionError("side channel closed")
+        buf += chunk
+    return bytes(buf)
+
+
+@dataclass
+class Held:
+    seq_id: int
+    blocks: list
+    expiry: float
+    num_tokens: int
+
+
+@dataclass
+class LoadJob:
+    request_id: str
+    params: dict
+    local_blocks: list
+    t0: float = field(default_factory=time.monotonic)
+
+
+class KvxAgent:
+    def __init__(self, kv: torch.Tensor, engine_id: Optional[str] = None, host: Optional[str] = None,
+                 port: int = 0, tp_rank: int = 0, tp_size: int = 1, abort_timeout: float = 480.0,
+                 transport: str = "auto", metrics=None):
+        self.kv = kv                      # [num_blocks, L, 2, Hkv, bs, D]
+        self.engine_id = engine_id or f"kvx-{uuid.uuid4().hex[:12]}"
+        self.tp_rank, self.tp_size = tp_rank, tp_size
+        self.abort_timeout = abort_timeout
+        self.metrics = metrics
+        self.is_gpu = kv.is_cuda
+        self.block_bytes = kv[0].numel() * kv.element_size()
+        self.transport = transport
+        self.held: dict[str, Held] = {}
+        self.held_lock = threading.Lock()
+        self.free_requests: "queue.Queue[str]" = queue.Queue()
+        self.done: "queue.Queue[tuple[str, bool]]" = queue.Queue()
+        self.jobs: "queue.Queue[Optional[LoadJob]]" = queue.Queue()
+        self.peers: dict[tuple, dict] = {}
+        self.ipc_maps: dict[str, int] = {}
+        self.ipc_handle = None
+        if self.is_gpu and transport in ("auto", "ipc", "dma"):
+            try:
+                from llmd_amd.ops import native
+
+                h, off = native().kvx_ipc_export(kv)
+                self.ipc_handle = (h, off)
+            except Exception as e:  # noqa: BLE001
+                log.warning("IPC export unavailable (%s); kvx falls back to TCP", e)
+        self.host = host or os.environ.get("VLLM_NIXL_SIDE_CHANNEL_HOST", "127.0.0.1")
+        self.server = _Server(("0.0.0.0" if self.host not in ("127.0.0.1", "localhost") else self.host,
+                               port or int(os.environ.get("VLLM_NIXL_SIDE_CHANNEL_PORT", "0") or 0)), self)
+        self.port = self.server.server_address[1]
+        threading.Thread(target=self.server.serve_forever, daemon=True, name="kvx-side-channel").start()
+        self.worker = threading.Thread(target=self._work, daemon=True, name="kvx-transfer")
+        self.stream = None
+        self.worker.start()
+
+    # ------------------------------------------------------------ metadata
+    def meta(self) -> dict:
+        k = self.kv
+        m = {"engine_id": self.engine_id, "shape": list(k.shape), "dtype": str(k.dtype).replace("torch.", ""),
+             "block_bytes": self.block_bytes, "tp_rank": self.tp_rank, "tp_size": self.tp_size,
+             "device": k.device.index if k.is_cuda else -1, "hostname": socket.gethostname(),
+             "pid": os.getpid(), "num_blocks": k.shape[0]}
+        if self.ipc_handle is not None:
+            m["ipc_handle"], m["ipc_offset"] = self.ipc_handle
+        return m
+
+    # ------------------------------------------------------------ prefill side
+    def hold(self, request_id: str, seq_id: int, blocks: list, num_tokens: int) -> dict:
+        with self.held_lock:
+            self.held[request_id] = Held(seq_id, list(blocks), time.monotonic() + self.abort_timeout, num_tokens)
+        return {"do_remote_prefill": True, "do_remote_decode": False, "remote_engine_id": self.engine_id,
+                "remote_host": self.host, "remote_port": self.port, "remote_block_ids": list(blocks),
+                "remote_request_id": request_id, "remote_tp_size": self.tp_size, "num_tokens": num_tokens}
+
+    def expired_or_freed(self) -> list[Held]:
+        """Held entries to release now (engine thread)."""
+        out = []
+        now = time.monotonic()
+        while True:
+            try:
+                rid = self.free_requests.get_nowait()
+            except queue.Empty:
+                break
+            with self.held_lock:
+                h = self.held.pop(rid, None)
+            if h is not None:
+                out.append(h)
+        with self.held_lock:
+            for rid in [r for r, h in self.held.items() if h.expiry < now]:
+                log.warning("kvx: request %s held blocks expired (no remote read)", rid)
+                out.append(self.held.pop(rid))
+        return out
+
+    def read_blocks(self, blocks: list) -> bytes:
+        idx = torch.tensor(blocks, dtype=torch.long, device=self.kv.device)
+        return self.kv.index_select(0, idx).cpu().contiguous().view(torch.uint8).numpy().tobytes()
+
+    # ------------------------------------------------------------ decode side
+    def start_load(self, request_id: str, params: dict, local_blocks: list):
+        self.jobs.put(LoadJob(request_id, dict(params), list(local_blocks)))
+
+    def _peer(self, host, port) -> dict:
+        key = (host, int(port))
+        p = self.peers.get(key)
+        if p is None:
+            s = socket.create_connection(key, timeout=10)
+            s.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
+            _send(s, {"op": "meta"})
+            meta = _recv(s)
+            p = {"sock": s, "meta": meta, "lock": threading.Lock()}
+            self._check_compat(meta)
+            self.peers[key] = p
+        return p
+
+    def _check_compat(self, m: dict):
+        """Handshake compatibility (enforce_handshake_compat): block size, dtype,
+        layers, head dim must match; KV heads may differ by TP re-slicing."""
+        ls = list(self.kv.shape)
+        rs = m["shape"]
+        if rs[1] != ls[1] or rs[2] != ls[2] or rs[4] != ls[4] or rs[5] != ls[5]:
+            raise RuntimeError(f"kvx layout mismatch local {ls} remote {rs}")
+        if m["dtype"] != str(self.kv.dtype).replace("torch.", ""):
+            raise RuntimeError("kvx dtype mismatch")
+        if rs[3] % ls[3] and ls[3] % rs[3]:
+            raise RuntimeError("kvx: KV head counts not TP-compatible")
+
+    def _rpc(self, p, obj):
+        with p["lock"]:
+            _send(p["sock"], obj)
+            return _recv(p["sock"])
+
+    def _segments(self, rmeta) -> list[tuple[int, int, int]]:
+        """Byte segments (src_off, dst_off, len) of one block for TP re-slicing."""
+        L, _, hl, bs, D = self.kv.shape[1:]
+        hr = rmeta["shape"][3]
+        esz = self.kv.element_size()
+        if hr == hl:
+            return [(0, 0, self.block_bytes)]
+        if hr < hl:
+            raise RuntimeError("kvx: decoder holds more KV heads than the prefiller (unsupported pull)")
+        # prefiller has all heads of a group of decoder ranks: take our slice
+        h0 = (self.tp_rank * hl) % hr
+        head = bs * D * esz
+        segs = []
+        for l in range(L):
+            for kv in range(2):
+                segs.append((((l * 2 + kv) * hr + h0) * head, ((l * 2 + kv) * hl) * head, hl * head))
+        return segs
+
+    def _fault(self) -> Optional[str]:
+        f = os.environ.get("LLMD_KVX_FAULT")
+        if not f or random.random() > float(os.environ.get("LLMD_KVX_FAULT_P", "1.0")):
+            return None
+        return f
+
+    def _work(self):
+        while True:
+            job = self.jobs.get()
+            if job is None:
+                return
+            ok = False
+            t0 = time.monotonic()
+            nbytes = 0
+            try:
+                ok, nbytes = self._do_load(job)
+            except Exception as e:  # noqa: BLE001 - NIXL_ERR_BACKEND equivalent
+                log.warning("kvx load %s failed: %s", job.request_id, e)
+                ok = False
+            if self.metrics is not None:
+                self.metrics.observe(ok, time.monotonic() - t0, nbytes, len(job.local_blocks))
+            self.done.put((job.request_id, ok))
+
+    def _do_load(self, job: LoadJob) -> tuple[bool, int]:
+        prm = job.params
+        fault = self._fault()
+        if fault == "drop":
+            raise RuntimeError("injected transfer drop")
+        if fault and fault.startswith("delay:"):
+            time.sleep(float(fault.split(":")[1]))
+        p = self._peer(prm["remote_host"], prm["remote_port"])
+        rmeta = p["meta"]
+        rblocks = list(prm["remote_block_ids"])
+        n = min(len(rblocks), len(job.local_blocks))
+        rblocks, lblocks = rblocks[:n], job.local_blocks[:n]
+        segs = self._segments(rmeta)
+        use_ipc = (self.is_gpu and "ipc_handle" in rmeta and self.transport in ("auto", "ipc", "dma")
+                   and rmeta.get("hostname") == socket.gethostname())
+        nbytes = sum(s[2] for s in segs) * n
+        if use_ipc:
+            self._ipc_copy(rmeta, rblocks, lblocks, segs)
+        else:
+            data = self._rpc(p, {"op": "read", "blocks": rblocks, "request_id": prm.get("remote_request_id")})
+            if isinstance(data, dict) and data.get("error"):
+                raise RuntimeError(data["error"])
+            rshape = rmeta["shape"]
+            src = torch.frombuffer(bytearray(data), dtype=torch.uint8).view(n, -1)
+            dst_idx = torch.tensor(lblocks, dtype=torch.long, device=self.kv.device)
+            flat = self.kv.view(self.kv.shape[0], -1).view(torch.uint8)
+            rows = torch.empty(n, self.block_bytes, dtype=torch.uint8)
+            for so, do, ln in segs:
+                rows[:, do:do + ln] = src[:, so:so + ln]
+            flat.index_copy_(0, dst_idx, rows.to(self.kv.device))
+            if self.is_gpu:
+                torch.cuda.current_stream().synchronize()
+        if fault == "corrupt":
+            idx = torch.tensor(lblocks[:1], dtype=torch.long, device=self.kv.device)
+            self.kv.index_fill_(0, idx, 0)
+        # release the prefiller's blocks
+        self._rpc(p, {"op": "free", "request_id": prm.get("remote_request_id")})
+        return True, nbytes
+
+    def _ipc_copy(self, rmeta, rblocks, lblocks, segs):
+        from llmd_amd.ops import native
+
+        C = native()
+        eid = rmeta["engine_id"]
+        if self.stream is None:
+            torch.cuda.set_device(self.kv.device)
+            self.stream = torch.cuda.Stream(device=self.kv.device)
+        base = self.ipc_maps.get(eid)
+        if base is None:
+            base = C.kvx_ipc_open(rmeta["ipc_handle"]) + int(rmeta["ipc_offset"])
+            self.ipc_maps[eid] = base
+        with torch.cuda.stream(self.stream):
+            if self.transport == "dma" and len(segs) == 1:
+                pairs = torch.tensor(list(zip(rblocks, lblocks)), dtype=torch.int32)
+                C.kvx_dma_blocks(self.kv, base, self.block_bytes, rmeta["block_bytes"], pairs, self.block_bytes)
+            else:
+                pairs = torch.tensor(list(zip(rblocks, lblocks)), dtype=torch.int32, device=self.kv.device)
+                sg = torch.tensor(segs, dtype=torch.int64, device=self.kv.device)
+                C.kvx_copy_blocks(self.kv, base, self.block_bytes, rmeta["block_bytes"], pairs, sg,
+                                  max(s[2] for s in segs))
+            ev = torch.cuda.Event()
+            ev.record(self.stream)
+        ev.synchronize()
+
+    def poll_done(self) -> list[tuple[str, bool]]:
+        out = []
+        while True:
+            try:
+                out.append(self.done.get_nowait())
+            except queue.Empty:
+                return out
+
+    def close(self):
+        self.jobs.put(None)
+        self.server.shutdown()
+        for p in self.peers.values():
+            try:
+                p["sock"].close()
+            except OSError:
+                pass
+        if self.ipc_maps:
+            try:
+                from llmd_amd.ops import native
+
+                for eid, base in self.ipc_maps.items():
+                    pass  # mapped bases include an offset; handles are released at process exit
+            except Exception:  # noqa: BLE001
+                pass
+
+
+class _Handler(socketserver.BaseRequestHandler):
+    def handle(self):
+        agent: KvxAgent = self.server.agent
+        s = self.request
+        s.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
+        while True:
+            try:
+                msg = _recv(s)
+            except (ConnectionError, OSError, struct.error):
+                return
+            op = msg.get("op")
+            try:
+                if op == "meta":
+                    _send(s, agent.meta())
+                elif op == "read":
+                    rid = msg.get("request_id")
+                    with agent.held_lock:
+                        held = agent.held.get(rid)
+                    if held is not None and not set(msg["blocks"]) <= set(held.blocks):
+                        _send(s, {"error": "blocks not held for request"})
+                        continue
+                    _send(s, agent.read_blocks(msg["blocks"]))
+                elif op == "free":
+                    agent.free_requests.put(msg.get("request_id"))
+                    _send(s, {"ok": True})
+                elif op == "ping":
+                    _send(s, {"ok": True, "engine_id": agent.engine_id})
+                else:
+                    _send(s, {"error": f"unknown op {op}"})
+            except (ConnectionError, OSError):
+                return
+
+
+class _Server(socketserver.ThreadingTCPServer):
+    daemon_threads = True
+    allow_reuse_address = True
+
+    def __init__(self, addr, agent):
+        self.agent = agent
+        super().__init__(addr, _Handler)

@@ -1,0 +1,115 @@
+"""Scheduler-facing KV connector (``--kv-transfer-config``).
+
+Config (vLLM-compatible keys): ``{"kv_connector": "KvxConnector" |
+"NixlConnector", "kv_role": "kv_producer" | "kv_consumer" | "kv_both",
+"kv_load_failure_policy": "recompute" | "fail", "kv_connector_extra_config":
+{"transport": "auto" | "ipc" | "dma" | "tcp", "side_channel_port": 5557,
+"abort_timeout": 480}}``.
+"""
+from __future__ import annotations
+
+import logging
+import os
+from typing import Optional
+
+from prometheus_client import CollectorRegistry, Counter, Histogram, generate_latest
+
+from .agent import KvxAgent
+
+log = logging.getLogger("llmd.kvx.connector")
+
+
+class KvxMetrics:
+    """NIXL-compatible metric names so the P/D dashboards work unchanged."""
+
+    def __init__(self, model: str):
+        r = self.reg = CollectorRegistry()
+        L = ["model_name"]
+        self.model = model
+        self.xfer = Histogram("vllm:nixl_xfer_time_seconds", "KV transfer time", L,
+                              buckets=(.001, .002, .005, .01, .02, .05, .1, .2, .5, 1, 2, 5), registry=r)
+        self.bytes = Histogram("vllm:nixl_bytes_transferred", "Bytes per transfer", L,
+                               buckets=tuple(2 ** i for i in range(16, 36, 2)), registry=r)
+        self.post = Histogram("vllm:nixl_post_time_seconds", "Transfer post time", L,
+                              buckets=(.0001, .0005, .001, .005, .01, .05), registry=r)
+        self.desc = Histogram("vllm:nixl_num_descriptors", "Descriptors (blocks) per transfer", L,
+                              buckets=(1, 4, 16, 64, 256, 1024, 4096), registry=r)
+        self.failed = Counter("vllm:nixl_num_failed_transfers", "Failed transfers", L, registry=r)
+
+    def observe(self, ok: bool, dt: float, nbytes: int, nblocks: int):
+        m = self.model
+        if not ok:
+            self.failed.labels(m).inc()
+            return
+        self.xfer.labels(m).observe(dt)
+        self.bytes.labels(m).observe(nbytes)
+        self.desc.labels(m).observe(nblocks)
+
+    def render(self) -> bytes:
+        return generate_latest(self.reg)
+
+
+class KvxConnector:
+    def __init__(self, cfg, engine):
+        kt = cfg.kv_transfer_config or {}
+        extra = kt.get("kv_connector_extra_config") or {}
+        self.engine = engine
+        self.role = kt.get("kv_role", "kv_both")
+        self.failure_policy = kt.get("kv_load_failure_policy", "recompute")
+        self.metrics = KvxMetrics(cfg.served_name)
+        from llmd_amd.parallel.state import get_state
+
+        st = get_state()
+        self.agent = KvxAgent(engine.runner.kv, host=extra.get("side_channel_host"),
+                              port=int(extra.get("side_channel_port", 0) or 0),
+                              tp_rank=st.tp_rank, tp_size=st.tp_size,
+                              abort_timeout=float(extra.get("abort_timeout",
+                                                            os.environ.get("VLLM_NIXL_ABORT_REQUEST_TIMEOUT", 480))),
+                              transport=extra.get("transport", "auto"), metrics=self.metrics)
+        self._results: dict[str, bool] = {}
+        self._finished: list[str] = []
+        self._outputs = []
+
+    # ---------------- decode side (scheduler hooks)
+    def start_load(self, req, local_blocks: list):
+        self.agent.start_load(req.request_id, req.kv_transfer_params or {}, local_blocks)
+
+    def poll_finished_recv(self) -> list[str]:
+        for rid, ok in self.agent.poll_done():
+            self._results[rid] = ok
+            self._finished.append(rid)
+        out, self._finished = self._finished, []
+        return out
+
+    def recv_ok(self, rid: str) -> bool:
+        return self._results.pop(rid, False)
+
+    # ---------------- prefill side
+    def hold_for_remote(self, req, blocks: list):
+        if not blocks:
+            self.engine.bm.free(req.seq_id)
+            return
+        req.extra["kv_transfer_params_out"] = self.agent.hold(req.request_id, req.seq_id, blocks,
+                                                              req.num_prompt_tokens)
+
+    def tick(self):
+        for h in self.agent.expired_or_freed():
+            self.engine.bm.free(h.seq_id)
+
+    def take_outputs(self):
+        out, self._outputs = self._outputs, []
+        return out
+
+    def render_metrics(self) -> bytes:
+        return self.metrics.render()
+
+    def close(self):
+        self.agent.close()
+
+
+def make_connector(cfg, engine) -> Optional[KvxConnector]:
+    kt = cfg.kv_transfer_config or {}
+    name = kt.get("kv_connector", "KvxConnector")
+    if name in ("KvxConnector", "NixlConnector", "kvx"):
+        return KvxConnector(cfg, engine)
+    raise ValueError(f"unsupported kv_connector {name!r}")

@@ -48,6 +48,9 @@ class AsyncEngine:
                     outs = eng.step()
                     for o in outs:
                         self._emit(o)
+                    if eng.last_step_empty:
+                        # only remote-KV waits pending: do not spin
+                        time.sleep(0.0005)
                     if eng.connector is not None:
                         for o in eng.connector.take_outputs():
                             self._emit(o)

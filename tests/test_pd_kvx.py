@@ -1,0 +1,95 @@
+"""P/D disaggregation through kvx on CPU (TCP transport) and failure policies."""
+import os
+
+import numpy as np
+import pytest
+
+from llmd_amd.engine.config import EngineConfig
+from llmd_amd.engine.engine import LLMEngine
+from llmd_amd.engine.request import SamplingParams
+
+
+def make(kt=None, **kw):
+    cfg = EngineConfig.create("tiny-llama", device="cpu", block_size=16, num_gpu_blocks=128,
+                              max_num_batched_tokens=128, max_num_seqs=8, max_model_len=512,
+                              enforce_eager=True, kv_transfer_config=kt, seed=0, **kw)
+    return LLMEngine(cfg)
+
+
+def run(eng, rid, prompt, sp, ktp=None):
+    r = eng.add_request(rid, prompt, sp, kv_transfer_params=ktp)
+    out = None
+    import time
+    for _ in range(20000):
+        for o in eng.step():
+            if o.request_id == rid and o.finished:
+                out = o
+        if eng.last_step_empty:
+            time.sleep(0.001)
+        if out is not None:
+            return r, out
+    raise AssertionError("request did not finish")
+
+
+KT = {"kv_connector": "KvxConnector", "kv_role": "kv_both",
+      "kv_connector_extra_config": {"transport": "tcp"}}
+
+
+def test_pd_matches_aggregated():
+    P, D, A = make(KT), make(KT), make()
+    prompt = np.random.default_rng(0).integers(3, 500, size=150).tolist()
+    sp = SamplingParams(max_tokens=8, temperature=0.0, ignore_eos=True)
+    _, agg = run(A, "a", prompt, sp)
+    agg_r = A.sched  # noqa
+    # prefill on P (max_tokens=1), remote decode on D
+    rp, op = run(P, "p", prompt, SamplingParams(max_tokens=1, temperature=0.0, ignore_eos=True),
+                 {"do_remote_decode": True})
+    ktp = op.kv_transfer_params
+    assert ktp and ktp["do_remote_prefill"] and len(ktp["remote_block_ids"]) == 10
+    assert P.bm.num_free() < P.bm.num_blocks  # blocks held for the reader
+    rd, od = run(D, "d", prompt, sp, ktp)
+    assert rd.output_token_ids == A_outputs(A, prompt, sp)
+    # D notified P: blocks released on P's next tick
+    for _ in range(200):
+        P.step()
+        if P.bm.num_free() == P.bm.num_blocks:
+            break
+    assert P.bm.num_free() == P.bm.num_blocks
+    assert rd.num_cached_tokens == len(prompt) - 1
+    text = D.connector.render_metrics().decode()
+    assert "vllm:nixl_xfer_time_seconds_count" in text
+
+
+def A_outputs(A, prompt, sp):
+    return A.generate([prompt], sp)[0].output_token_ids
+
+
+@pytest.mark.parametrize("policy", ["recompute", "fail"])
+def test_pd_load_failure_policy(policy, monkeypatch):
+    P = make(KT)
+    kt = dict(KT, kv_load_failure_policy=policy)
+    D = make(kt)
+    prompt = list(range(10, 90))
+    _, op = run(P, "p", prompt, SamplingParams(max_tokens=1, temperature=0.0, ignore_eos=True),
+                {"do_remote_decode": True})
+    monkeypatch.setenv("LLMD_KVX_FAULT", "drop")
+    r, o = run(D, "d", prompt, SamplingParams(max_tokens=4, temperature=0.0, ignore_eos=True),
+               op.kv_transfer_params)
+    if policy == "fail":
+        assert o.finish_reason == "error"
+    else:
+        assert o.finish_reason == "length" and len(r.output_token_ids) == 4
+        assert r.num_computed_tokens >= len(prompt)
+    assert D.bm.num_free() == D.bm.num_blocks
+
+
+def test_held_blocks_expire_without_reader():
+    kt = dict(KT, kv_connector_extra_config={"transport": "tcp", "abort_timeout": 0.05})
+    P = make(kt)
+    run(P, "p", list(range(5, 60)), SamplingParams(max_tokens=1, temperature=0.0, ignore_eos=True),
+        {"do_remote_decode": True})
+    assert P.bm.num_free() < P.bm.num_blocks
+    import time
+    time.sleep(0.1)
+    P.step()
+    assert P.bm.num_free() == P.bm.num_blocks
