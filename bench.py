@@ -51,6 +51,8 @@ def parse():
     p.add_argument("--prefill-gpus", type=int, default=0, help="pd mode: number of prefill ranks")
     p.add_argument("--enforce-eager", action="store_true")
     p.add_argument("--seed", type=int, default=0)
+    p.add_argument("--gpu-memory-utilization", type=float, default=0.92)
+    p.add_argument("--kv-cache-gb", type=float, default=None)
     p.add_argument("--json-out", default=None)
     return p.parse_args()
 
@@ -67,11 +69,48 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", 1))
     if world != a.gpus and world > 1:
         log(rank, f"warning: WORLD_SIZE={world} != --gpus {a.gpus}")
-    torch.cuda.set_device(local_rank)
+    # LLMD_BENCH_DEVICE pins every rank to one GPU (multi-process rehearsal on a
+    # 1-GPU box); RCCL refuses duplicate GPUs, so that mode uses gloo for control.
+    forced = os.environ.get("LLMD_BENCH_DEVICE")
+    dev = int(forced) if forced is not None else local_rank
+    torch.cuda.set_device(dev)
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", rank=rank, world_size=world,
-                                device_id=torch.device("cuda", local_rank))
+        if forced is None:
+            dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", dev))
+        else:
+            dist.init_process_group("gloo", rank=rank, world_size=world)
+
+    if a.mode == "pd":
+        from llmd_amd.bench_pd import run_pd
+
+        res = run_pd(a, rank, world, local_rank, log)
+        if rank == 0:
+            value = res["gen"] / res["elapsed"]
+            out = {
+                "metric": METRIC, "value": round(value, 2), "unit": "output tok/s (whole job)",
+                "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
+                "ms_per_step": round(1000 * res["elapsed"] / a.steps, 3), "higher_is_better": True,
+                "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
+                "data": "synthetic (random token prompts, random-init weights)",
+                "config": {"model": "Llama-3-70B" if a.model == "llama-3-70b" else a.model,
+                           "global_batch": a.concurrency * res["decode_ranks"], "seq_len": a.isl,
+                           "isl": a.isl, "osl": a.osl,
+                           "parallelism": f"pd{res['prefill_ranks']}p{res['decode_ranks']}d",
+                           "max_num_batched_tokens": a.max_num_batched_tokens, "block_size": a.block_size,
+                           "kv_transfer": "kvx ipc over xGMI"},
+                "output_tok_s_per_decode_gpu": round(value / res["decode_ranks"], 2),
+                "p50_ttft_s": round(res["p50_ttft"], 4) if res["p50_ttft"] is not None else None,
+                "reference_context": REF_CONTEXT,
+            }
+            line = json.dumps(out)
+            print(line, flush=True)
+            if a.json_out:
+                with open(a.json_out, "w") as f:
+                    f.write(line + "\n")
+        dist.barrier()
+        dist.destroy_process_group()
+        return
 
     from llmd_amd.engine.config import EngineConfig
     from llmd_amd.engine.engine import LLMEngine
@@ -82,7 +121,8 @@ def main():
         a.model, device="cuda", block_size=a.block_size, max_num_seqs=a.concurrency,
         max_num_batched_tokens=a.max_num_batched_tokens, max_model_len=max_len,
         enforce_eager=a.enforce_eager, seed=a.seed + rank, enable_prefix_caching=True,
-        cuda_graph_max_bs=a.concurrency)
+        cuda_graph_max_bs=a.concurrency, gpu_memory_utilization=a.gpu_memory_utilization,
+        kv_cache_memory_bytes=int(a.kv_cache_gb * 2**30) if a.kv_cache_gb else None)
     t0 = time.time()
     eng = LLMEngine(cfg)
     torch.cuda.synchronize()
@@ -143,7 +183,8 @@ def main():
     gen = eng.metrics.n_gen - gen0
     ptoks = eng.metrics.n_prompt - prompt0
     ttfts = list(eng.metrics.ttfts)
-    stats = torch.tensor([elapsed, gen, ptoks, len(ttfts)], dtype=torch.float64, device="cuda")
+    stats = torch.tensor([elapsed, gen, ptoks, len(ttfts)], dtype=torch.float64,
+                         device="cuda" if forced is None else "cpu")
     all_ttft = ttfts
     if world > 1:
         mx = stats.clone()

@@ -1,0 +1,256 @@
+"""P/D-disaggregated serving benchmark driver (used by bench.py --mode pd).
+
+Topology inside one torchrun job (one process per GPU):
+  ranks [0, P)   prefill engines, each serving the real OpenAI endpoint on
+                 127.0.0.1:<base+rank> (AsyncEngine + aiohttp) with a
+                 ``kv_transfer_config`` (kvx producer);
+  ranks [P, N)   decode engines (kvx consumer, IPC pull over xGMI) driven by
+                 an in-process routing-sidecar loop: every new request is sent
+                 to a prefill rank (least outstanding) with
+                 ``kv_transfer_params{do_remote_decode}`` / ``max_tokens=1``,
+                 the returned params are handed to the local decoder which
+                 pulls the KV and decodes (the reference's nixlv2 protocol,
+                 docs/architecture/advanced/disaggregation/README.md:119-131).
+Timing: K decode steps on every decode rank between gloo barriers (+ device
+sync); prefill ranks serve continuously. Reported value = total output
+tokens / max elapsed; TTFT measured at the decode side from the moment the
+prefill request is issued (the "true TTFT" a client would see).
+"""
+from __future__ import annotations
+
+import asyncio
+import json
+import os
+import queue
+import statistics
+import threading
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+
+def run_pd(a, rank: int, world: int, local_rank: int, log) -> dict | None:
+    from llmd_amd.engine.config import EngineConfig
+    from llmd_amd.engine.engine import LLMEngine
+    from llmd_amd.engine.request import SamplingParams
+
+    P = a.prefill_gpus or max(1, (3 * world) // 4)
+    if not 0 < P < world:
+        raise SystemExit(f"pd mode needs 0 < prefill ranks ({P}) < world ({world})")
+    is_prefill = rank < P
+    ctl = dist.new_group(backend="gloo")
+    base_port = int(os.environ.get("LLMD_PD_BASE_PORT", "18200"))
+    max_len = a.isl + a.osl + 64
+    kt = {"kv_connector": "KvxConnector", "kv_role": "kv_producer" if is_prefill else "kv_consumer",
+          "kv_load_failure_policy": "recompute",
+          "kv_connector_extra_config": {"transport": os.environ.get("LLMD_KVX_TRANSPORT", "auto")}}
+    n_decode = world - P
+    conc = a.concurrency
+    cfg = EngineConfig.create(
+        a.model, device="cuda", block_size=a.block_size,
+        max_num_seqs=max(conc, 8) if not is_prefill else 64,
+        max_num_batched_tokens=a.max_num_batched_tokens, max_model_len=max_len,
+        enforce_eager=a.enforce_eager or is_prefill, seed=a.seed, enable_prefix_caching=True,
+        cuda_graph_max_bs=conc, kv_transfer_config=kt, gpu_memory_utilization=a.gpu_memory_utilization,
+        kv_cache_memory_bytes=int(a.kv_cache_gb * 2**30) if a.kv_cache_gb else None)
+    t0 = time.time()
+    eng = LLMEngine(cfg, capture_graphs=not is_prefill)
+    torch.cuda.synchronize()
+    log(rank, f"{'prefill' if is_prefill else 'decode'} engine up in {time.time() - t0:.1f}s "
+              f"({eng.runner.num_blocks} KV blocks)")
+    if is_prefill:
+        srv_thread = _start_server(cfg, eng, base_port + rank)
+        dist.barrier(group=ctl)              # servers up
+        dist.barrier(group=ctl)              # decoders finished setup+warmup
+        torch.cuda.synchronize()
+        dist.barrier(group=ctl)              # timed region start
+        dist.barrier(group=ctl)              # timed region end
+        torch.cuda.synchronize()
+        stats = [0.0, 0.0, 0.0]
+        gathered = [None] * world
+        dist.all_gather_object(gathered, {"elapsed": 0.0, "gen": 0, "ttft": [], "prefill": True,
+                                          "prompt_tok": eng.metrics.n_prompt}, group=ctl)
+        dist.barrier(group=ctl)
+        srv_thread.stop()
+        return _summarize(gathered, P, world)
+    # ------------------------------------------------------------------ decode rank
+    dist.barrier(group=ctl)  # prefill servers up
+    prefill_urls = [f"http://127.0.0.1:{base_port + r}/v1/completions" for r in range(P)]
+    sc = _SidecarThread(prefill_urls, a.model)
+    vocab = cfg.model_config.vocab_size
+    rng = np.random.default_rng(1234 + rank)
+    issued = {}
+    nreq = [0]
+
+    def new_request(max_tokens):
+        toks = rng.integers(100, vocab - 100, size=a.isl).tolist()
+        nreq[0] += 1
+        rid = f"d{rank}-{nreq[0]}"
+        issued[rid] = (toks, max_tokens, time.monotonic())
+        sc.submit(rid, toks)
+
+    def drain_arrivals():
+        n = 0
+        while True:
+            try:
+                rid, ktp, ok = sc.results.get_nowait()
+            except queue.Empty:
+                return n
+            toks, mt, t_issue = issued.pop(rid)
+            eng.add_request(rid, toks, SamplingParams(max_tokens=mt, temperature=0.0, ignore_eos=True),
+                            kv_transfer_params=ktp if ok else None, arrival_time=t_issue)
+            n += 1
+
+    in_flight = lambda: eng.sched.num_running + eng.sched.num_waiting + len(issued)  # noqa: E731
+
+    def run_steps(n, until_full=False):
+        k = 0
+        while k < n:
+            drain_arrivals()
+            outs = eng.step()
+            for o in outs:
+                if o.finished:
+                    new_request(a.osl)
+            if eng.last_step_empty:
+                time.sleep(0.0005)
+                if not until_full:
+                    continue  # an empty step is not a decode step
+            k += 1
+
+    for i in range(conc):
+        new_request(max(1, int(a.osl * (i + 1) / conc)))
+    ts = time.time()
+    # setup: wait until the batch is filled and decoding
+    while True:
+        drain_arrivals()
+        eng.step()
+        if eng.last_step_empty:
+            time.sleep(0.001)
+        if not issued and eng.sched.num_waiting == 0 and all(r.output_token_ids for r in eng.sched.running):
+            break
+        if time.time() - ts > 1800:
+            break
+    while in_flight() < conc:
+        new_request(a.osl)
+    log(rank, f"pd setup done in {time.time() - ts:.1f}s")
+    run_steps(a.warmup)
+    dist.barrier(group=ctl)
+    eng.metrics.ttfts.clear()
+    gen0 = eng.metrics.n_gen
+    torch.cuda.synchronize()
+    dist.barrier(group=ctl)
+    t1 = time.perf_counter()
+    run_steps(a.steps)
+    torch.cuda.synchronize()
+    dist.barrier(group=ctl)
+    elapsed = time.perf_counter() - t1
+    gen = eng.metrics.n_gen - gen0
+    gathered = [None] * world
+    dist.all_gather_object(gathered, {"elapsed": elapsed, "gen": gen, "ttft": list(eng.metrics.ttfts),
+                                      "prefill": False}, group=ctl)
+    dist.barrier(group=ctl)
+    sc.stop()
+    return _summarize(gathered, P, world)
+
+
+def _summarize(gathered, P, world):
+    dec = [g for g in gathered if not g["prefill"]]
+    el = max(g["elapsed"] for g in dec)
+    tot = sum(g["gen"] for g in dec)
+    tt = [t for g in dec for t in g["ttft"]]
+    return {"elapsed": el, "gen": tot, "p50_ttft": statistics.median(tt) if tt else None,
+            "prefill_ranks": P, "decode_ranks": world - P, "n_ttft": len(tt)}
+
+
+class _SidecarThread:
+    """Async HTTP client loop (routing-sidecar logic) on a private thread."""
+
+    def __init__(self, urls, model):
+        self.urls = urls
+        self.model = model
+        self.outstanding = [0] * len(urls)
+        self.results: "queue.Queue[tuple]" = queue.Queue()
+        self.loop = asyncio.new_event_loop()
+        self.thread = threading.Thread(target=self.loop.run_forever, daemon=True)
+        self.thread.start()
+        self.session = None
+
+    def submit(self, rid, toks):
+        asyncio.run_coroutine_threadsafe(self._one(rid, toks), self.loop)
+
+    async def _one(self, rid, toks):
+        import aiohttp
+
+        if self.session is None:
+            self.session = aiohttp.ClientSession(timeout=aiohttp.ClientTimeout(total=3600))
+        i = min(range(len(self.urls)), key=lambda k: self.outstanding[k])
+        self.outstanding[i] += 1
+        body = {"model": self.model, "prompt": toks, "max_tokens": 1, "temperature": 0.0, "stream": False,
+                "kv_transfer_params": {"do_remote_decode": True, "do_remote_prefill": False}}
+        try:
+            async with self.session.post(self.urls[i], json=body, headers={"x-request-id": rid}) as r:
+                d = await r.json()
+                ktp = d.get("kv_transfer_params")
+                self.results.put((rid, ktp, r.status == 200 and bool(ktp)))
+        except Exception:  # noqa: BLE001 - prefill failure: decode-only fallback
+            self.results.put((rid, None, False))
+        finally:
+            self.outstanding[i] -= 1
+
+    def stop(self):
+        async def close():
+            if self.session:
+                await self.session.close()
+        asyncio.run_coroutine_threadsafe(close(), self.loop).result(timeout=10)
+        self.loop.call_soon_threadsafe(self.loop.stop)
+
+
+class _ServerThread(threading.Thread):
+    def __init__(self, app, port):
+        super().__init__(daemon=True)
+        self.app, self.port = app, port
+        self.loop = asyncio.new_event_loop()
+        self.ready = threading.Event()
+        self.runner = None
+
+    def run(self):
+        from aiohttp import web
+
+        asyncio.set_event_loop(self.loop)
+
+        async def start():
+            self.runner = web.AppRunner(self.app, access_log=None)
+            await self.runner.setup()
+            await web.TCPSite(self.runner, "127.0.0.1", self.port).start()
+            self.ready.set()
+
+        self.loop.run_until_complete(start())
+        self.loop.run_forever()
+
+    def stop(self):
+        async def cleanup():
+            await self.runner.cleanup()
+        try:
+            asyncio.run_coroutine_threadsafe(cleanup(), self.loop).result(timeout=10)
+        except Exception:  # noqa: BLE001
+            pass
+        self.loop.call_soon_threadsafe(self.loop.stop)
+
+
+def _start_server(cfg, eng, port):
+    from llmd_amd.serving.api_server import build_server
+
+    srv = build_server(cfg, eng)
+    t = _ServerThread(srv.app(), port)
+    t.srv = srv
+    t.start()
+    t.ready.wait(60)
+    orig_stop = t.stop
+
+    def stop():
+        orig_stop()
+        srv.aeng.shutdown()
+    t.stop = stop
+    return t

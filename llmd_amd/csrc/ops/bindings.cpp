@@ -32,6 +32,14 @@ int llmd_kvx_ipc_open(const void*, void**);
 int llmd_kvx_ipc_close(void*);
 int llmd_kvx_handle_size();
 int llmd_kvx_dma_blocks(void*, const void*, int64_t, int64_t, const int*, int, int64_t, hipStream_t);
+void llmd_moe_topk(const float*, int, int, int, int, const float*, int, int, int, float, int*, float*,
+                   hipStream_t);
+void llmd_moe_align(const int*, int, int, int, int*, int*, int*, int, int*, int*, hipStream_t);
+int llmd_moe_gemm_tile_m();
+void llmd_moe_gemm(const void*, int64_t, int, const int*, const int*, int, const void*, int64_t, int, int,
+                   void*, int64_t, int, int, float, float, int, const void*, hipStream_t);
+void llmd_moe_combine(const void*, int64_t, const int*, const float*, int, int, int, void*, int64_t,
+                      hipStream_t);
 }
 
 namespace {
@@ -254,6 +262,70 @@ int64_t kvx_ipc_open(py::bytes handle) {
 
 void kvx_ipc_close(int64_t p) { llmd_kvx_ipc_close((void*)p); }
 
+// ---------------------------------------------------------------- MoE
+void moe_topk(torch::Tensor logits, int64_t k, int64_t scoring, c10::optional<torch::Tensor> bias,
+              int64_t n_group, int64_t topk_group, bool renorm, double routed_scale, torch::Tensor ids,
+              torch::Tensor wts) {
+  CHECK_CUDA(logits); CHECK_DT(logits, at::kFloat);
+  TORCH_CHECK(logits.is_contiguous() && logits.dim() == 2, "logits [T, E] contiguous f32");
+  const int T = logits.size(0), E = logits.size(1);
+  TORCH_CHECK(E <= 512 && k >= 1 && k <= 16 && k <= E, "moe_topk: E <= 512, 1 <= k <= 16");
+  TORCH_CHECK(n_group <= 64 && (n_group <= 1 || E % n_group == 0), "moe_topk groups");
+  CHECK_DT(ids, at::kInt); CHECK_DT(wts, at::kFloat);
+  TORCH_CHECK(ids.numel() >= (int64_t)T * k && wts.numel() >= (int64_t)T * k, "moe_topk outputs");
+  const float* b = nullptr;
+  if (bias.has_value()) { CHECK_DT(bias.value(), at::kFloat); TORCH_CHECK(bias->numel() == E); b = bias->data_ptr<float>(); }
+  llmd_moe_topk(logits.data_ptr<float>(), T, E, k, scoring, b, n_group, topk_group, renorm ? 1 : 0,
+                (float)routed_scale, ids.data_ptr<int>(), wts.data_ptr<float>(), cur_stream());
+}
+
+void moe_align(torch::Tensor ids, int64_t E, torch::Tensor sorted_ids, torch::Tensor tile_expert,
+               torch::Tensor expert_offsets, torch::Tensor total_p, torch::Tensor inv) {
+  CHECK_CUDA(ids); CHECK_DT(ids, at::kInt); CHECK_DT(sorted_ids, at::kInt); CHECK_DT(tile_expert, at::kInt);
+  const int n = ids.numel();
+  const int bm = llmd_moe_gemm_tile_m();
+  const int max_p = sorted_ids.numel();
+  TORCH_CHECK(max_p % bm == 0 && max_p >= n + E * (bm - 1), "sorted_ids too small");
+  TORCH_CHECK(tile_expert.numel() >= max_p / bm && expert_offsets.numel() >= E + 1 && inv.numel() >= n,
+              "moe_align buffers");
+  TORCH_CHECK(E <= 4096, "too many experts");
+  llmd_moe_align(ids.data_ptr<int>(), n, E, bm, sorted_ids.data_ptr<int>(), tile_expert.data_ptr<int>(),
+                 expert_offsets.data_ptr<int>(), max_p, total_p.data_ptr<int>(), inv.data_ptr<int>(),
+                 cur_stream());
+}
+
+void moe_gemm(torch::Tensor X, int64_t topk, torch::Tensor sorted_ids, torch::Tensor tile_expert,
+              torch::Tensor W, torch::Tensor Y, int64_t mode, int64_t act, double alpha, double limit,
+              bool a_rows_are_slots, c10::optional<torch::Tensor> bias) {
+  CHECK_CUDA(X); CHECK_BF16(X); CHECK_BF16(W); CHECK_BF16(Y); CHECK_INNER(X); CHECK_INNER(Y);
+  TORCH_CHECK(W.dim() == 3 && W.is_contiguous(), "W [E, N, K] contiguous");
+  const int N = W.size(1), K = W.size(2);
+  TORCH_CHECK(X.size(1) == K && K % 8 == 0, "moe_gemm: K");
+  const int bm = llmd_moe_gemm_tile_m();
+  const int P = sorted_ids.numel();
+  TORCH_CHECK(P % bm == 0 && tile_expert.numel() >= P / bm && Y.size(0) >= P, "moe_gemm: rows");
+  TORCH_CHECK(Y.size(1) >= (mode == 1 ? N / 2 : N) && N % 2 == 0, "moe_gemm: Y width");
+  TORCH_CHECK(X.stride(0) % 8 == 0, "16-B aligned rows");
+  const void* bp = nullptr;
+  if (bias.has_value()) {
+    CHECK_BF16(bias.value());
+    TORCH_CHECK(bias->is_contiguous() && bias->numel() == (int64_t)W.size(0) * N, "bias [E, N]");
+    bp = bias->data_ptr();
+  }
+  llmd_moe_gemm(X.data_ptr(), X.stride(0), topk, sorted_ids.data_ptr<int>(), tile_expert.data_ptr<int>(), P / bm,
+                W.data_ptr(), W.stride(0), N, K, Y.data_ptr(), Y.stride(0), mode, act, (float)alpha, (float)limit,
+                a_rows_are_slots ? 1 : 0, bp, cur_stream());
+}
+
+void moe_combine(torch::Tensor Y, torch::Tensor inv, torch::Tensor w, int64_t topk, torch::Tensor out) {
+  CHECK_CUDA(Y); CHECK_BF16(Y); CHECK_BF16(out); CHECK_DT(inv, at::kInt); CHECK_DT(w, at::kFloat);
+  const int T = out.size(0), d = out.size(1);
+  TORCH_CHECK(d % 8 == 0 && Y.size(1) >= d && inv.numel() >= (int64_t)T * topk && w.numel() >= (int64_t)T * topk,
+              "moe_combine shapes");
+  llmd_moe_combine(Y.data_ptr(), Y.stride(0), inv.data_ptr<int>(), w.data_ptr<float>(), T, topk, d,
+                   out.data_ptr(), out.stride(0), cur_stream());
+}
+
 }  // namespace
 
 PYBIND11_MODULE(_C, m) {
@@ -272,4 +344,9 @@ PYBIND11_MODULE(_C, m) {
   m.def("kvx_ipc_export", &kvx_ipc_export);
   m.def("kvx_ipc_open", &kvx_ipc_open);
   m.def("kvx_ipc_close", &kvx_ipc_close);
+  m.def("moe_topk", &moe_topk);
+  m.def("moe_align", &moe_align);
+  m.def("moe_gemm", &moe_gemm);
+  m.def("moe_combine", &moe_combine);
+  m.def("moe_tile_m", &llmd_moe_gemm_tile_m);
 }

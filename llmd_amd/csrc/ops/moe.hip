@@ -1,0 +1,400 @@
+// Mixture-of-Experts kernels: gating top-k, expert
+// alignment/permutation, MFMA grouped GEMM with fused epilogues, combine.
+//
+//   moe_topk      one wave per token: softmax / sigmoid scoring, optional
+//                 per-expert bias (DeepSeek correction bias), grouped top-k
+//                 (n_group / topk_group), renormalisation, routed scaling.
+//   moe_align     per-expert counts -> offsets padded to the GEMM M-tile ->
+//                 sorted_ids[P] (token*topk + slot, -1 for padding) and the
+//                 expert id of every M-tile; single workgroup (T*k <= 64k).
+//   moe_gemm      grouped GEMM  Y[p, :] = X[tok(p), :] . W[e(tile)]^T
+//                 MFMA 16x16x32 bf16, 64x128 output tile per 256-thread
+//                 workgroup (2x2 waves of 32x64), K-step 64 double-buffered
+//                 in LDS with register staging (next tile's loads in flight
+//                 during the current tile's MFMAs). A rows are gathered by
+//                 sorted_ids; W is [E, N, K] row-major so both operands are
+//                 K-contiguous rows (16-B loads, ds_read_b128 fragments).
+//                 Epilogue modes: 0 = store bf16, 1 = gated act on an
+//                 interleaved [g0,u0,g1,u1..] N axis (SiLU or gpt-oss clamped
+//                 SwiGLU) storing N/2 columns.
+//   moe_combine   out[t] = sum_j w[t,j] * Y[inv(t,j)]  (deterministic, no atomics)
+// Weights of every expert are read exactly once per M-tile, which at decode
+// sizes (a few tokens per expert) is the HBM-bound optimum.
+#include "llmd_common.h"
+
+using namespace llmd;
+
+namespace {
+
+constexpr float NEG_INF = -__builtin_huge_valf();
+
+// ---------------------------------------------------------------- gating
+// scoring: 0 softmax over all experts, 1 sigmoid, 2 softmax over the selected top-k (gpt-oss)
+__global__ __launch_bounds__(256) void moe_topk_kernel(const float* __restrict__ logits, int T, int E, int K,
+                                                       int scoring, const float* __restrict__ bias,
+                                                       int n_group, int topk_group, int renorm,
+                                                       float routed_scale, int* __restrict__ ids,
+                                                       float* __restrict__ wts) {
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int t = blockIdx.x * 4 + wave;
+  if (t >= T) return;
+  const float* l = logits + (int64_t)t * E;
+  constexpr int MAXV = 8;  // up to 512 experts
+  float sc[MAXV], sel[MAXV];
+  const int nv = (E + 63) / 64;
+  float mx = NEG_INF;
+#pragma unroll
+  for (int i = 0; i < MAXV; ++i) {
+    const int e = lane + 64 * i;
+    float v = (i < nv && e < E) ? l[e] : NEG_INF;
+    sc[i] = v;
+    mx = fmaxf(mx, v);
+  }
+  if (scoring == 0) {
+    mx = wave_max(mx);
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < MAXV; ++i) {
+      sc[i] = (sc[i] == NEG_INF) ? 0.f : __expf(sc[i] - mx);
+      s += sc[i];
+    }
+    s = wave_sum(s);
+#pragma unroll
+    for (int i = 0; i < MAXV; ++i) sc[i] /= s;
+  } else if (scoring == 1) {
+#pragma unroll
+    for (int i = 0; i < MAXV; ++i) sc[i] = (sc[i] == NEG_INF) ? 0.f : 1.f / (1.f + __expf(-sc[i]));
+  }
+  // selection scores (+ bias); invalid experts -inf
+#pragma unroll
+  for (int i = 0; i < MAXV; ++i) {
+    const int e = lane + 64 * i;
+    sel[i] = (i < nv && e < E) ? sc[i] + (bias ? bias[e] : 0.f) : NEG_INF;
+  }
+  // group-limited routing: keep topk_group groups by the sum of their top-2 selection scores
+  if (n_group > 1) {
+    const int gsz = E / n_group;
+    __shared__ float gscore[4][64];
+    __shared__ int gkeep[4][64];
+    if (lane < n_group) {
+      float a = NEG_INF, b = NEG_INF;
+      for (int j = 0; j < gsz; ++j) {
+        const int e = lane * gsz + j;
+        float v = l[e];
+        if (scoring == 1) v = 1.f / (1.f + __expf(-v));
+        else if (scoring == 0) v = __expf(v - mx);
+        v += bias ? bias[e] : 0.f;
+        if (v > a) { b = a; a = v; } else if (v > b) b = v;
+      }
+      gscore[wave][lane] = a + (gsz > 1 ? b : 0.f);
+    }
+    __builtin_amdgcn_wave_barrier();
+    if (lane == 0) {
+      for (int g = 0; g < n_group; ++g) gkeep[wave][g] = 0;
+      for (int r = 0; r < topk_group; ++r) {
+        int best = -1;
+        float bv = NEG_INF;
+        for (int g = 0; g < n_group; ++g)
+          if (!gkeep[wave][g] && gscore[wave][g] > bv) { bv = gscore[wave][g]; best = g; }
+        if (best >= 0) gkeep[wave][best] = 1;
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int i = 0; i < MAXV; ++i) {
+      const int e = lane + 64 * i;
+      if (e < E && !gkeep[wave][e / gsz]) sel[i] = NEG_INF;
+    }
+  }
+  // iterative top-k by wave argmax
+  float wsum = 0.f, myw = 0.f;
+  int myid = 0;
+  float topv[16];
+  for (int k = 0; k < K; ++k) {
+    float bv = NEG_INF;
+    int bi = 0x7fffffff;
+#pragma unroll
+    for (int i = 0; i < MAXV; ++i) {
+      const int e = lane + 64 * i;
+      if (sel[i] > bv || (sel[i] == bv && e < bi)) { bv = sel[i]; bi = e; }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const float ov = __shfl_xor(bv, o, 64);
+      const int oi = __shfl_xor(bi, o, 64);
+      if (ov > bv || (ov == bv && oi < bi)) { bv = ov; bi = oi; }
+    }
+    // gate weight: the unbiased score of the chosen expert
+    float w = 0.f;
+#pragma unroll
+    for (int i = 0; i < MAXV; ++i) {
+      const int e = lane + 64 * i;
+      if (e == bi) {
+        w = (scoring == 2) ? l[e] : sc[i];
+        sel[i] = NEG_INF;
+      }
+    }
+    w = wave_sum(w);  // exactly one lane contributed
+    if (k < 16) topv[k] = w;
+    if (lane == k) { myid = bi; myw = w; }
+  }
+  if (scoring == 2) {  // softmax over the selected logits
+    float m2 = NEG_INF;
+    for (int k = 0; k < K && k < 16; ++k) m2 = fmaxf(m2, topv[k]);
+    float s = 0.f;
+    for (int k = 0; k < K && k < 16; ++k) s += __expf(topv[k] - m2);
+    myw = __expf(myw - m2) / s;
+  } else if (renorm) {
+    for (int k = 0; k < K && k < 16; ++k) wsum += topv[k];
+    myw = myw / (wsum > 0.f ? wsum : 1.f);
+  }
+  if (lane < K) {
+    ids[(int64_t)t * K + lane] = myid;
+    wts[(int64_t)t * K + lane] = myw * routed_scale;
+  }
+}
+
+// ---------------------------------------------------------------- align
+__global__ __launch_bounds__(1024) void moe_align_kernel(const int* __restrict__ ids, int n, int E, int BM,
+                                                         int* __restrict__ sorted_ids, int* __restrict__ tile_expert,
+                                                         int* __restrict__ expert_offsets, int max_p,
+                                                         int* __restrict__ total_p) {
+  extern __shared__ int sm[];  // counts[E], offs[E+1], cursor[E]
+  int* cnt = sm;
+  int* off = sm + E;
+  int* cur = sm + 2 * E + 1;
+  for (int e = threadIdx.x; e < E; e += blockDim.x) cnt[e] = 0;
+  __syncthreads();
+  for (int i = threadIdx.x; i < n; i += blockDim.x) {
+    const int e = ids[i];
+    if (e >= 0 && e < E) atomicAdd(&cnt[e], 1);
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int acc = 0;
+    for (int e = 0; e < E; ++e) {
+      off[e] = acc;
+      acc += ((cnt[e] + BM - 1) / BM) * BM;
+    }
+    off[E] = acc;
+    *total_p = acc;
+  }
+  __syncthreads();
+  const int P = off[E];
+  for (int p = threadIdx.x; p < max_p; p += blockDim.x) sorted_ids[p] = -1;
+  for (int e = threadIdx.x; e < E; e += blockDim.x) {
+    cur[e] = off[e];
+    expert_offsets[e] = off[e];
+    for (int tt = off[e] / BM; tt < off[e + 1] / BM; ++tt) tile_expert[tt] = e;
+  }
+  if (threadIdx.x == 0) expert_offsets[E] = P;
+  for (int tt = P / BM + threadIdx.x; tt < max_p / BM; tt += blockDim.x) tile_expert[tt] = -1;
+  __syncthreads();
+  // stable scatter: one pass per thread-chunk keeps order deterministic per expert
+  if (threadIdx.x == 0) {
+    for (int i = 0; i < n; ++i) {
+      const int e = ids[i];
+      if (e >= 0 && e < E) sorted_ids[cur[e]++] = i;
+    }
+  }
+}
+
+// ---------------------------------------------------------------- grouped GEMM
+constexpr int BM = 64, BN = 128, BK = 64, NT = 256;
+constexpr int LDA = BK + 8;  // padded LDS row (elements): 144 B rows -> conflict-light b128 reads
+
+template <int MODE>
+__global__ __launch_bounds__(NT, 2) void moe_gemm_kernel(
+    const uint16_t* __restrict__ X, int64_t x_stride, int topk, const int* __restrict__ sorted_ids,
+    const int* __restrict__ tile_expert, const uint16_t* __restrict__ W, int64_t w_expert_stride, int N, int K,
+    uint16_t* __restrict__ Y, int64_t y_stride, int act, float alpha, float limit, int a_rows_are_slots,
+    const uint16_t* __restrict__ bias) {
+  __shared__ __attribute__((aligned(16))) uint16_t As[2][BM][LDA];
+  __shared__ __attribute__((aligned(16))) uint16_t Bs[2][BN][LDA];
+  const int mt = blockIdx.y, nt = blockIdx.x;
+  const int e = tile_expert[mt];
+  if (e < 0) return;
+  const int m0 = mt * BM, n0 = nt * BN;
+  const uint16_t* We = W + (int64_t)e * w_expert_stride;
+  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+  const int wm = w >> 1, wn = w & 1;  // wave tile 32 x 64
+  // staging: A tile 64 rows x 64 k = 512 chunks (2 per thread); B 128 x 64 = 1024 (4 per thread)
+  int arow[2], achk[2];
+  const uint16_t* aptr[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int c = tid + NT * i;
+    arow[i] = c >> 3;
+    achk[i] = c & 7;
+    const int sid = sorted_ids[m0 + arow[i]];
+    const int tok = sid < 0 ? -1 : (a_rows_are_slots ? sid : sid / topk);
+    aptr[i] = tok < 0 ? nullptr : X + (int64_t)tok * x_stride;
+  }
+  u32x4_t ra[2], rb[4];
+  auto load = [&](int k0) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      u32x4_t v = {0, 0, 0, 0};
+      if (aptr[i] && k0 + achk[i] * 8 < K) v = *reinterpret_cast<const u32x4_t*>(aptr[i] + k0 + achk[i] * 8);
+      ra[i] = v;
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int c = tid + NT * i;
+      const int r = c >> 3, ch = c & 7;
+      u32x4_t v = {0, 0, 0, 0};
+      if (n0 + r < N && k0 + ch * 8 < K)
+        v = *reinterpret_cast<const u32x4_t*>(We + (int64_t)(n0 + r) * K + k0 + ch * 8);
+      rb[i] = v;
+    }
+  };
+  auto store = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) *reinterpret_cast<u32x4_t*>(&As[buf][arow[i]][achk[i] * 8]) = ra[i];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int c = tid + NT * i;
+      *reinterpret_cast<u32x4_t*>(&Bs[buf][c >> 3][(c & 7) * 8]) = rb[i];
+    }
+  };
+  f32x4_t acc[2][4];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  const int nk = (K + BK - 1) / BK;
+  load(0);
+  store(0);
+  __syncthreads();
+  const int r16 = lane & 15, kq = lane >> 4;
+  for (int kt = 0; kt < nk; ++kt) {
+    const int buf = kt & 1;
+    if (kt + 1 < nk) load((kt + 1) * BK);
+#pragma unroll
+    for (int ks = 0; ks < BK / 32; ++ks) {
+      bf16x8_t af[2], bfr[4];
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+        af[i] = *reinterpret_cast<const bf16x8_t*>(&As[buf][wm * 32 + i * 16 + r16][ks * 32 + kq * 8]);
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        bfr[j] = *reinterpret_cast<const bf16x8_t*>(&Bs[buf][wn * 64 + j * 16 + r16][ks * 32 + kq * 8]);
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+    if (kt + 1 < nk) {
+      __syncthreads();
+      store(buf ^ 1);
+      __syncthreads();
+    }
+  }
+  // epilogue: C[row = 4*kq + r][col = r16] within each 16x16 fragment
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int row = m0 + wm * 32 + i * 16 + kq * 4 + r;
+      if (sorted_ids[row] < 0) continue;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int col = n0 + wn * 64 + j * 16 + r16;
+        float v = acc[i][j][r];
+        if (bias && col < N) v += bf2f(bias[(int64_t)e * N + col]);
+        if (MODE == 0) {
+          if (col < N) Y[(int64_t)row * y_stride + col] = f2bf(v);
+        } else {
+          // interleaved gate/up: even col = gate, odd col = up (partner lane r16^1)
+          const float other = __shfl_xor(v, 1, 64);
+          if ((r16 & 1) == 0) {
+            float g = v, u = other, o;
+            if (act == 2) {
+              g = fminf(g, limit);
+              u = fminf(fmaxf(u, -limit), limit);
+              o = (u + 1.f) * g / (1.f + __expf(-alpha * g));
+            } else {
+              o = g / (1.f + __expf(-g)) * u;
+            }
+            if (col < N) Y[(int64_t)row * y_stride + col / 2] = f2bf(o);
+          }
+        }
+      }
+    }
+  }
+}
+
+// out[t, :] = sum_j w[t, j] * Y[pos(t, j), :]  with pos from the inverse permutation
+__global__ __launch_bounds__(256) void moe_combine_kernel(const uint16_t* __restrict__ Y, int64_t y_stride,
+                                                          const int* __restrict__ inv, const float* __restrict__ w,
+                                                          int topk, int d, uint16_t* __restrict__ out,
+                                                          int64_t out_stride) {
+  const int t = blockIdx.x;
+  for (int c = threadIdx.x; c < d / 8; c += 256) {
+    float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    for (int j = 0; j < topk; ++j) {
+      const int p = inv[(int64_t)t * topk + j];
+      if (p < 0) continue;
+      const float ww = w[(int64_t)t * topk + j];
+      float f[8];
+      unpack8(*reinterpret_cast<const u32x4_t*>(Y + (int64_t)p * y_stride + c * 8), f);
+#pragma unroll
+      for (int q = 0; q < 8; ++q) acc[q] += ww * f[q];
+    }
+    *reinterpret_cast<u32x4_t*>(out + (int64_t)t * out_stride + c * 8) = pack8(acc);
+  }
+}
+
+__global__ void moe_invert_kernel(const int* __restrict__ sorted_ids, int P, int* __restrict__ inv) {
+  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p < P) {
+    const int s = sorted_ids[p];
+    if (s >= 0) inv[s] = p;
+  }
+}
+
+}  // namespace
+
+extern "C" {
+
+void llmd_moe_topk(const float* logits, int T, int E, int K, int scoring, const float* bias, int n_group,
+                   int topk_group, int renorm, float routed_scale, int* ids, float* wts, hipStream_t st) {
+  if (T == 0) return;
+  hipLaunchKernelGGL(moe_topk_kernel, dim3((T + 3) / 4), dim3(256), 0, st, logits, T, E, K, scoring, bias,
+                     n_group, topk_group, renorm, routed_scale, ids, wts);
+}
+
+// max_p = n + E*(BM-1) rounded to BM
+void llmd_moe_align(const int* ids, int n, int E, int bm, int* sorted_ids, int* tile_expert,
+                    int* expert_offsets, int max_p, int* total_p, int* inv, hipStream_t st) {
+  const size_t lds = (size_t)(3 * E + 1) * sizeof(int);
+  hipLaunchKernelGGL(moe_align_kernel, dim3(1), dim3(1024), lds, st, ids, n, E, bm, sorted_ids, tile_expert,
+                     expert_offsets, max_p, total_p);
+  hipLaunchKernelGGL(moe_invert_kernel, dim3((max_p + 255) / 256), dim3(256), 0, st, sorted_ids, max_p, inv);
+}
+
+int llmd_moe_gemm_tile_m() { return BM; }
+
+void llmd_moe_gemm(const void* X, int64_t x_stride, int topk, const int* sorted_ids, const int* tile_expert,
+                   int num_tiles, const void* W, int64_t w_expert_stride, int N, int K, void* Y, int64_t y_stride,
+                   int mode, int act, float alpha, float limit, int a_rows_are_slots, const void* bias,
+                   hipStream_t st) {
+  if (num_tiles == 0) return;
+  dim3 grid((N + BN - 1) / BN, num_tiles);
+  if (mode == 0)
+    hipLaunchKernelGGL(moe_gemm_kernel<0>, grid, dim3(NT), 0, st, (const uint16_t*)X, x_stride, topk, sorted_ids,
+                       tile_expert, (const uint16_t*)W, w_expert_stride, N, K, (uint16_t*)Y, y_stride, act, alpha,
+                       limit, a_rows_are_slots, (const uint16_t*)bias);
+  else
+    hipLaunchKernelGGL(moe_gemm_kernel<1>, grid, dim3(NT), 0, st, (const uint16_t*)X, x_stride, topk, sorted_ids,
+                       tile_expert, (const uint16_t*)W, w_expert_stride, N, K, (uint16_t*)Y, y_stride, act, alpha,
+                       limit, a_rows_are_slots, (const uint16_t*)bias);
+}
+
+void llmd_moe_combine(const void* Y, int64_t y_stride, const int* inv, const float* w, int T, int topk, int d,
+                      void* out, int64_t out_stride, hipStream_t st) {
+  if (T == 0) return;
+  hipLaunchKernelGGL(moe_combine_kernel, dim3(T), dim3(256), 0, st, (const uint16_t*)Y, y_stride, inv, w, topk,
+                     d, (uint16_t*)out, out_stride);
+}
+}

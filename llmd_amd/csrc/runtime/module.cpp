@@ -6,10 +6,12 @@ namespace py = pybind11;
 void register_block_manager(py::module_& m);
 void register_kv_index(py::module_& m);
 void register_gbdt(py::module_& m);
+void register_fs_store(py::module_& m);
 
 PYBIND11_MODULE(_rt, m) {
   m.doc() = "llmd_amd native host runtime";
   register_block_manager(m);
   register_kv_index(m);
   register_gbdt(m);
+  register_fs_store(m);
 }

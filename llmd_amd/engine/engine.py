@@ -45,6 +45,7 @@ class LLMEngine:
             from llmd_amd.kvcache.offload import OffloadManager
 
             self.offload = OffloadManager(cfg, self)
+            self.sched.offload = self.offload
         if capture_graphs:
             self.runner.capture_graphs()
         self.paused = False
@@ -117,12 +118,13 @@ class LLMEngine:
         return outs
 
     def _flush_events(self):
+        evs = self.bm.take_events() if (self.offload is not None or self.event_sink is not None) else []
         if self.offload is not None:
+            self.offload.on_block_events(evs)
             self.offload.after_step()
-        if self.event_sink is not None:
-            evs = self.bm.take_events()
-            if evs:
-                self.event_sink(evs)
+            evs = list(evs) + self.offload.take_events()
+        if self.event_sink is not None and evs:
+            self.event_sink(evs)
 
     # ------------------------------------------------------------ offline helpers
     def generate(self, prompts: Iterable[list[int]], params: SamplingParams) -> list[Request]:

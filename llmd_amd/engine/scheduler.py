@@ -123,6 +123,7 @@ class Scheduler:
         self.bm = block_manager
         self.bs = block_manager.block_size
         self.connector = connector
+        self.offload = None  # set by the engine when a KV offload tier is configured
         self.waiting = _WaitQueue(self.sc.policy)
         self.running: list[Request] = []
         self.remote_wait: dict[str, Request] = {}
@@ -270,7 +271,10 @@ class Scheduler:
                 self.connector.start_load(r, blocks)
                 continue
             if not self.bm.has_seq(r.seq_id):
-                cached = self.bm.acquire(r.seq_id, self._tokens(r), r.lora_id)
+                toks = self._tokens(r)
+                cached = self.bm.acquire(r.seq_id, toks, r.lora_id)
+                if self.offload is not None and self.cfg.cache.enable_prefix_caching:
+                    cached += self.offload.load_prefix(r, toks, cached, self.bm)
                 r.num_computed_tokens = cached
                 if r.num_preemptions == 0:
                     r.num_cached_tokens = cached

@@ -1,0 +1,172 @@
+"""Tiered KV offload: GPU -> pinned host DRAM -> filesystem (SURVEY N14-N16,
+C-M15; docs/architecture/advanced/kv-management/kv-offloader.md).
+
+Policy: *write-through*. A block is immutable once full, so as soon as the
+engine commits a full block (BlockStored) it is copied D2H on a dedicated
+low-priority HIP stream (ordered after the compute stream that produced it)
+into a pinned host pool; no copy is ever on the eviction critical path.
+The host tier is an LRU over block keys (``cpu_bytes_to_use``); with an FS
+tier configured, host-resident blocks are also persisted as one file per block
+(``<root>/<key[:2]>/<key>.kv``) by the native C++ thread pool, so KV survives
+engine restarts (the llm-d FS connector behaviour).
+
+On admission the scheduler asks ``load_prefix``: blocks continuing the
+request's GPU-cached prefix are looked up host-then-disk, copied H2D on the
+compute stream (ordered before the forward) into freshly allocated blocks and
+committed, so those tokens are skipped by prefill.
+Tier changes are published as KV events with ``medium`` cpu / disk so the
+router's precise index scores them with tier weights.
+
+Whole-block contiguity of the KV layout ([num_blocks, L, 2, Hkv, bs, D]) makes
+every transfer a single contiguous DMA of ``block_bytes``.
+"""
+from __future__ import annotations
+
+import collections
+import logging
+import os
+import threading
+from typing import Optional
+
+import numpy as np
+import torch
+
+from llmd_amd import _rt_loader
+
+log = logging.getLogger("llmd.offload")
+
+
+class OffloadManager:
+    def __init__(self, cfg, engine):
+        oc = dict(cfg.kv_offload_config or {})
+        extra = oc.get("kv_connector_extra_config", oc)
+        self.engine = engine
+        self.kv = engine.runner.kv
+        self.block_bytes = self.kv[0].numel() * self.kv.element_size()
+        cpu_bytes = int(extra.get("cpu_bytes_to_use", extra.get("cpu_bytes", 1 << 30)))
+        self.n_slots = max(1, cpu_bytes // self.block_bytes)
+        pin = self.kv.is_cuda
+        self.host = torch.empty(self.n_slots, self.block_bytes, dtype=torch.uint8, pin_memory=pin)
+        self.slot_of: "collections.OrderedDict[int, int]" = collections.OrderedDict()  # key -> slot (LRU)
+        self.free_slots = list(range(self.n_slots - 1, -1, -1))
+        self.pending: list = []  # (event, [(key, slot)])
+        self.fs = None
+        fs = extra.get("fs_root") or next((t.get("root_dir") for t in extra.get("secondary_tiers", [])
+                                           if t.get("type") == "fs"), None)
+        if fs:
+            rt = _rt_loader.rt()
+            threads = int(extra.get("n_write_threads", 8))
+            self.fs = rt.FsStore(fs, threads)
+        self.stream = torch.cuda.Stream(priority=0) if self.kv.is_cuda else None
+        self.events_out: list = []
+        self.stats = {"offloaded": 0, "loaded_cpu": 0, "loaded_fs": 0, "evicted_cpu": 0}
+        self.lock = threading.Lock()
+
+    # ------------------------------------------------------------ write-through
+    def on_block_events(self, events: list):
+        """Engine BlockManager events of the step just executed."""
+        todo = [(int(h), int(b)) for kind, h, parent, b, toks in events if kind == 0]
+        if not todo:
+            return
+        todo = [(h, b) for h, b in todo if h not in self.slot_of]
+        if not todo:
+            return
+        assign = []
+        for h, b in todo:
+            slot = self._alloc_slot()
+            if slot is None:
+                break
+            assign.append((h, b, slot))
+        if not assign:
+            return
+        if self.stream is not None:
+            self.stream.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(self.stream):
+                for h, b, slot in assign:
+                    self.host[slot].copy_(self.kv[b].view(-1).view(torch.uint8), non_blocking=True)
+                ev = torch.cuda.Event()
+                ev.record(self.stream)
+            self.pending.append((ev, [(h, s) for h, _, s in assign]))
+        else:
+            for h, b, slot in assign:
+                self.host[slot].copy_(self.kv[b].reshape(-1).view(torch.uint8))
+            self._commit_host([(h, s) for h, _, s in assign])
+
+    def _alloc_slot(self) -> Optional[int]:
+        if self.free_slots:
+            return self.free_slots.pop()
+        if not self.slot_of:
+            return None
+        key, slot = self.slot_of.popitem(last=False)  # LRU victim
+        self.stats["evicted_cpu"] += 1
+        self.events_out.append((1, key, 0, -1, [], "cpu"))
+        return slot
+
+    def _commit_host(self, pairs):
+        for h, s in pairs:
+            self.slot_of[h] = s
+            self.stats["offloaded"] += 1
+            self.events_out.append((0, h, 0, -1, [], "cpu"))
+            if self.fs is not None:
+                self.fs.write(f"{h:016x}", self.host[s].numpy())
+
+    def poll(self):
+        keep = []
+        for ev, pairs in self.pending:
+            if ev.query():
+                self._commit_host(pairs)
+            else:
+                keep.append((ev, pairs))
+        self.pending = keep
+
+    # ------------------------------------------------------------ engine hooks
+    def before_step(self, so):
+        self.poll()
+
+    def after_step(self):
+        self.poll()
+
+    def take_events(self) -> list:
+        out, self.events_out = self.events_out, []
+        return out
+
+    # ------------------------------------------------------------ reload
+    def load_prefix(self, req, tokens: np.ndarray, cached: int, bm) -> int:
+        """Extend the request's cached prefix from host/disk. Returns the number
+        of additional tokens now resident (multiple of block size)."""
+        bs = bm.block_size
+        rt = _rt_loader.rt()
+        keys = rt.hash_blocks(tokens[: max(0, len(tokens) - 1)], bs, req.lora_id)
+        first = cached // bs
+        found = []
+        for i in range(first, len(keys)):
+            k = int(keys[i])
+            s = self.slot_of.get(k)
+            if s is not None:
+                found.append(("cpu", k, s))
+                continue
+            if self.fs is not None and self.fs.exists(f"{k:016x}"):
+                found.append(("fs", k, None))
+                continue
+            break
+        if not found:
+            return 0
+        n = len(found)
+        if not bm.grow(req.seq_id, (first + n) * bs):
+            return 0
+        table = bm.block_table(req.seq_id)
+        for j, (tier, k, s) in enumerate(found):
+            dst = self.kv[table[first + j]].view(-1).view(torch.uint8)
+            if tier == "cpu":
+                self.slot_of.move_to_end(k)
+                dst.copy_(self.host[s], non_blocking=True)
+                self.stats["loaded_cpu"] += 1
+            else:
+                buf = torch.empty(self.block_bytes, dtype=torch.uint8, pin_memory=self.kv.is_cuda)
+                ok = self.fs.read(f"{k:016x}", buf.numpy())
+                if not ok:
+                    n = j
+                    break
+                dst.copy_(buf, non_blocking=True)
+                self.stats["loaded_fs"] += 1
+        return n * bs

@@ -38,7 +38,7 @@ class LlamaDecoderLayer(torch.nn.Module):
         self.qkv = ColumnLinear(d, (Hq + 2 * Hkv) * D, bias=cfg.attention_bias, device=device)
         self.attn = PagedAttention(idx, Hq, Hkv, D, cos_sin, window=cfg.layer_window(idx),
                                    sinks=cfg.attention_sinks, device=device)
-        self.o_proj = RowLinear(Hq * D, d, device=device)
+        self.o_proj = RowLinear(Hq * D, d, bias=cfg.attention_bias and cfg.model_type == "gpt_oss", device=device)
         self.post_attention_layernorm = RMSNorm(d, cfg.rms_norm_eps, device)
         self.mlp = self._make_mlp(cfg, idx, device)
         # Qwen3: per-head RMSNorm on q and k before rope

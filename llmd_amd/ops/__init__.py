@@ -200,3 +200,57 @@ def topk_topp_mask(logits, topk=None, topp=None, temps=None):
 
 
 rope_cos_sin = ref.rope_cos_sin
+
+
+# ---------------------------------------------------------------- MoE
+def moe_tile_m() -> int:
+    return 64
+
+
+def moe_topk(logits, k, scoring=0, bias=None, n_group=1, topk_group=1, renorm=False, routed_scale=1.0):
+    if not _gpu(logits):
+        return ref.moe_topk(logits, k, scoring, bias, n_group, topk_group, renorm, routed_scale)
+    T = logits.shape[0]
+    ids = torch.empty(T, k, dtype=torch.int32, device=logits.device)
+    w = torch.empty(T, k, dtype=torch.float32, device=logits.device)
+    native().moe_topk(logits.float().contiguous(), k, scoring, bias, n_group, topk_group, renorm,
+                      routed_scale, ids, w)
+    return ids, w
+
+
+def moe_experts(x, ids, wts, w1, w2, act=0, alpha=1.702, limit=7.0, out=None, b1=None, b2=None):
+    """Fused routed-expert FFN: align -> grouped GEMM (gate_up + gated act) ->
+    grouped GEMM (down) -> weighted combine. w1 [E, 2F, d] (interleaved
+    gate/up rows), w2 [E, d, F]."""
+    if not _gpu(x):
+        r = ref.moe_forward(x, ids, wts, w1, w2, act, alpha, limit, b1, b2)
+        if out is not None:
+            out.copy_(r)
+            return out
+        return r
+    C = native()
+    T, d = x.shape
+    k = ids.shape[1]
+    E, N1, _ = w1.shape
+    F = N1 // 2
+    bm = C.moe_tile_m()
+    n = T * k
+    max_p = ((n + E * (bm - 1)) + bm - 1) // bm * bm
+    dev = x.device
+    sorted_ids = torch.empty(max_p, dtype=torch.int32, device=dev)
+    tile_e = torch.empty(max_p // bm, dtype=torch.int32, device=dev)
+    offs = torch.empty(E + 1, dtype=torch.int32, device=dev)
+    total = torch.empty(1, dtype=torch.int32, device=dev)
+    inv = torch.full((n,), -1, dtype=torch.int32, device=dev)
+    C.moe_align(ids.contiguous().view(-1), E, sorted_ids, tile_e, offs, total, inv)
+    h = torch.empty(max_p, F, dtype=x.dtype, device=dev)
+    C.moe_gemm(x, k, sorted_ids, tile_e, w1, h, 1, act, alpha, limit, False, b1)
+    y = torch.empty(max_p, d, dtype=x.dtype, device=dev)
+    # second GEMM: A rows are the sorted slots themselves (row p of h)
+    ident = torch.arange(max_p, dtype=torch.int32, device=dev)
+    ident = torch.where(sorted_ids >= 0, ident, torch.full_like(ident, -1))
+    C.moe_gemm(h, 1, ident, tile_e, w2, y, 0, 0, 0.0, 0.0, True, b2)
+    if out is None:
+        out = torch.empty(T, d, dtype=x.dtype, device=dev)
+    C.moe_combine(y, inv, wts.contiguous().view(-1), k, out)
+    return out

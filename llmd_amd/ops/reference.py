@@ -227,3 +227,61 @@ def yarn_inv_freq(rot_dim, base, sc):
     if mscale is not None and not sc.get("mscale_all_dim"):
         m = 0.1 * mscale * math.log(factor) + 1.0 if factor > 1 else 1.0
     return inv, m
+
+
+# ---------------------------------------------------------------- MoE references
+def moe_topk(logits, k, scoring=0, bias=None, n_group=1, topk_group=1, renorm=False, routed_scale=1.0):
+    """scoring: 0 softmax, 1 sigmoid, 2 softmax over the selected top-k logits (gpt-oss)."""
+    lf = logits.float()
+    if scoring == 0:
+        sc = torch.softmax(lf, -1)
+    elif scoring == 1:
+        sc = torch.sigmoid(lf)
+    else:
+        sc = lf
+    sel = sc + (bias.float() if bias is not None else 0.0)
+    if scoring == 2:
+        sel = lf + (bias.float() if bias is not None else 0.0)
+    T, E = lf.shape
+    if n_group > 1:
+        g = sel.view(T, n_group, E // n_group)
+        gs = g.topk(min(2, E // n_group), -1).values.sum(-1)
+        keep = torch.zeros(T, n_group, dtype=torch.bool, device=lf.device)
+        keep.scatter_(1, gs.topk(topk_group, -1).indices, True)
+        sel = sel.masked_fill(~keep.repeat_interleave(E // n_group, 1), float("-inf"))
+    ids = sel.topk(k, -1).indices
+    w = sc.gather(-1, ids)
+    if scoring == 2:
+        w = torch.softmax(lf.gather(-1, ids), -1)
+    elif renorm:
+        w = w / w.sum(-1, keepdim=True)
+    return ids.int(), (w * routed_scale).float()
+
+
+def moe_forward(x, ids, wts, w1, w2, act=0, alpha=1.702, limit=7.0, b1=None, b2=None):
+    """Dense reference: w1 [E, 2F, d] with interleaved gate/up rows, w2 [E, d, F]."""
+    T, d = x.shape
+    out = torch.zeros(T, d, dtype=torch.float32, device=x.device)
+    xf = x.float()
+    for t in range(T):
+        for j in range(ids.shape[1]):
+            e = int(ids[t, j])
+            if e < 0:
+                continue
+            h = w1[e].float() @ xf[t]
+            if b1 is not None:
+                h = h + b1[e].float()
+            g, u = h[0::2], h[1::2]
+            if act == 2:
+                g = g.clamp(max=limit)
+                u = u.clamp(-limit, limit)
+                a = (u + 1) * g * torch.sigmoid(alpha * g)
+            else:
+                a = torch.nn.functional.silu(g) * u
+            a = a.to(x.dtype).float()
+            y = w2[e].float() @ a
+            if b2 is not None:
+                y = y + b2[e].float()
+            y = y.to(x.dtype).float()
+            out[t] += float(wts[t, j]) * y
+    return out.to(x.dtype)

@@ -31,10 +31,12 @@ log = logging.getLogger("llmd.kvevents")
 HWM = 10000
 
 
-def encode_batch(events: list, block_size: int, medium: str = "GPU") -> dict:
+def encode_batch(events: list, block_size: int, medium0: str = "GPU") -> dict:
     """Engine BlockManager events -> wire dicts."""
     out = []
-    for kind, h, parent, block, tokens in events:
+    for ev in events:
+        kind, h, parent, block, tokens = ev[:5]
+        medium = ev[5].upper() if len(ev) > 5 else medium0
         if kind == 0:
             out.append({"type": "BlockStored", "block_hashes": [int(h)], "parent_block_hash": int(parent),
                         "token_ids": list(tokens), "block_size": block_size, "lora_id": None, "medium": medium})

@@ -41,7 +41,7 @@ def plain_forward(model, ids: list[int]) -> torch.Tensor:
         q = qkv[:, : Hq * D].view(T, Hq, D)
         o = ref.attention_ref(q, k, v, pos, a.scale, a.window,
                               a.sinks if a.sinks is not None else None).to(x.dtype).reshape(T, Hq * D)
-        x = torch.nn.functional.linear(o, layer.o_proj.weight)
+        x = torch.nn.functional.linear(o, layer.o_proj.weight, layer.o_proj.bias)
         ref.fused_add_rms_norm(x, residual, layer.post_attention_layernorm.weight, cfg.rms_norm_eps)
         x = layer.mlp(x)
     ref.fused_add_rms_norm(x, residual, model.norm.weight, cfg.rms_norm_eps)
@@ -123,6 +123,15 @@ def test_stop_conditions_and_sampling_seed():
     assert a.output_token_ids == b.output_token_ids
 
 
+def test_gpt_oss_moe_engine_matches_plain_forward():
+    eng = make_engine(model="tiny-gpt-oss")
+    prompts = _prompts(6, [7, 50, 33])
+    sp = SamplingParams(max_tokens=4, temperature=0.0, ignore_eos=True)
+    reqs = eng.generate(prompts, sp)
+    for p, r in zip(prompts, reqs):
+        assert r.output_token_ids == greedy_reference(eng.runner.model, p, 4)
+
+
 def test_metrics_exposed():
     eng = make_engine()
     eng.generate(_prompts(4, [20, 30]), SamplingParams(max_tokens=3, temperature=0.0, ignore_eos=True))
@@ -151,3 +160,15 @@ def test_engine_gpu_matches_plain_forward():
         agree += sum(int(a == b) for a, b in zip(r.output_token_ids, refo))
         total += len(refo)
     assert agree / total > 0.8
+
+
+@pytest.mark.gpu
+def test_gpt_oss_engine_gpu_runs():
+    eng = make_engine(device="cuda", num_gpu_blocks=128, max_num_batched_tokens=256,
+                      model="tiny-gpt-oss", max_num_seqs=8)
+    prompts = _prompts(7, [5, 100, 40])
+    sp = SamplingParams(max_tokens=6, temperature=0.0, ignore_eos=True)
+    reqs = eng.generate(prompts, sp)
+    model = eng.runner.model
+    for p, r in zip(prompts, reqs):
+        assert r.output_token_ids[0] == greedy_reference(model, p, 1)[0]

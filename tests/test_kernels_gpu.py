@@ -181,3 +181,70 @@ def test_topk_topp_mask():
     a = ops.topk_topp_mask(x.clone(), None, topp, temps)
     b = ref.topk_topp_mask(x.clone(), None, topp, temps)
     assert torch.equal(torch.isinf(a), torch.isinf(b))
+
+
+def test_kvx_copy_blocks_and_reslice():
+    C = ops.native()
+    L, H, bs, D = 3, 8, 16, 128
+    src = torch.randn(10, L, 2, H, bs, D, device=DEV).to(torch.bfloat16)
+    dst = torch.zeros(12, L, 2, H, bs, D, device=DEV, dtype=torch.bfloat16)
+    bb = src[0].numel() * 2
+    pairs = torch.tensor([[1, 5], [7, 0], [3, 11]], dtype=torch.int32, device=DEV)
+    segs = torch.tensor([[0, 0, bb]], dtype=torch.int64, device=DEV)
+    C.kvx_copy_blocks(dst, src.data_ptr(), bb, bb, pairs, segs, bb)
+    torch.cuda.synchronize()
+    for s_, d_ in [(1, 5), (7, 0), (3, 11)]:
+        assert torch.equal(dst[d_], src[s_])
+    # TP re-slice: decoder rank 1 of 4 takes heads [2, 4)
+    hl = 2
+    dst2 = torch.zeros(4, L, 2, hl, bs, D, device=DEV, dtype=torch.bfloat16)
+    head = bs * D * 2
+    sg = [(((l * 2 + kv) * H + 2) * head, ((l * 2 + kv) * hl) * head, hl * head) for l in range(L) for kv in range(2)]
+    C.kvx_copy_blocks(dst2, src.data_ptr(), dst2[0].numel() * 2, bb,
+                      torch.tensor([[4, 2]], dtype=torch.int32, device=DEV),
+                      torch.tensor(sg, dtype=torch.int64, device=DEV), hl * head)
+    torch.cuda.synchronize()
+    assert torch.equal(dst2[2], src[4][:, :, 2:4])
+    # SDMA path
+    dst3 = torch.zeros_like(dst)
+    C.kvx_dma_blocks(dst3, src.data_ptr(), bb, bb, torch.tensor([[2, 3], [3, 4], [9, 1]], dtype=torch.int32), bb)
+    torch.cuda.synchronize()
+    assert torch.equal(dst3[3], src[2]) and torch.equal(dst3[4], src[3]) and torch.equal(dst3[1], src[9])
+
+
+@pytest.mark.parametrize("E,k,scoring,ng,tg,renorm", [(128, 4, 2, 1, 1, False), (32, 4, 2, 1, 1, False),
+                                                       (256, 8, 1, 8, 4, True), (64, 6, 0, 1, 1, False)])
+def test_moe_topk(E, k, scoring, ng, tg, renorm):
+    torch.manual_seed(9)
+    T = 37
+    logits = torch.randn(T, E, device=DEV)
+    bias = torch.randn(E, device=DEV) * 0.1 if scoring == 1 else None
+    ids, w = ops.moe_topk(logits, k, scoring, bias, ng, tg, renorm, 2.5 if scoring == 1 else 1.0)
+    rid, rw = ref.moe_topk(logits, k, scoring, bias, ng, tg, renorm, 2.5 if scoring == 1 else 1.0)
+    # same expert sets (order may differ only on exact ties)
+    assert torch.equal(torch.sort(ids.long(), -1).values, torch.sort(rid.long(), -1).values)
+    po = torch.sort(ids.long(), -1).indices
+    pr = torch.sort(rid.long(), -1).indices
+    _close(w.gather(-1, po), rw.gather(-1, pr), atol=1e-5, rtol=1e-5)
+
+
+@pytest.mark.parametrize("T,E,k,d,F,act", [(1, 8, 2, 256, 128, 2), (37, 32, 4, 2880, 2880, 2),
+                                            (19, 128, 4, 512, 256, 2), (64, 16, 2, 1024, 512, 0)])
+def test_moe_experts(T, E, k, d, F, act):
+    torch.manual_seed(10)
+    x = torch.randn(T, d, device=DEV, dtype=torch.bfloat16)
+    w1 = (torch.randn(E, 2 * F, d, device=DEV) * d ** -0.5).to(torch.bfloat16)
+    w2 = (torch.randn(E, d, F, device=DEV) * F ** -0.5).to(torch.bfloat16)
+    b1 = (torch.randn(E, 2 * F, device=DEV) * 0.1).to(torch.bfloat16)
+    b2 = (torch.randn(E, d, device=DEV) * 0.1).to(torch.bfloat16)
+    logits = torch.randn(T, E, device=DEV)
+    ids, w = ops.moe_topk(logits, k, 2)
+    o = ops.moe_experts(x, ids, w, w1, w2, act, b1=b1, b2=b2)
+    r = ref.moe_forward(x, ids, w, w1, w2, act, b1=b1, b2=b2)
+    _close(o, r, atol=3e-2, rtol=3e-2)
+    # EP-style masking: experts outside the local range are ignored
+    ids2 = ids.clone()
+    ids2[ids2 >= E // 2] = -1
+    o2 = ops.moe_experts(x, ids2, w, w1, w2, act, b1=b1, b2=b2)
+    r2 = ref.moe_forward(x, ids2, w, w1, w2, act, b1=b1, b2=b2)
+    _close(o2, r2, atol=3e-2, rtol=3e-2)
