@@ -57,6 +57,11 @@ def parse():
     return p.parse_args()
 
 
+def _sync(a):
+    if a.device == "cuda":
+        torch.cuda.synchronize()
+
+
 def log(rank, *a):
     if rank == 0:
         print("[bench]", *a, file=sys.stderr, flush=True)
@@ -64,6 +69,10 @@ def log(rank, *a):
 
 def main():
     a = parse()
+    if os.environ.get("LLMD_BENCH_STACKS"):
+        import faulthandler
+
+        faulthandler.dump_traceback_later(float(os.environ["LLMD_BENCH_STACKS"]), repeat=True)
     rank = int(os.environ.get("RANK", 0))
     local_rank = int(os.environ.get("LOCAL_RANK", 0))
     world = int(os.environ.get("WORLD_SIZE", 1))
@@ -72,8 +81,10 @@ def main():
     # LLMD_BENCH_DEVICE pins every rank to one GPU (multi-process rehearsal on a
     # 1-GPU box); RCCL refuses duplicate GPUs, so that mode uses gloo for control.
     forced = os.environ.get("LLMD_BENCH_DEVICE")
-    dev = int(forced) if forced is not None else local_rank
-    torch.cuda.set_device(dev)
+    a.device = "cpu" if forced == "cpu" else "cuda"  # cpu: logic rehearsal with tiny models
+    dev = local_rank if forced in (None, "cpu") else int(forced)
+    if a.device == "cuda":
+        torch.cuda.set_device(dev)
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         if forced is None:
@@ -118,14 +129,14 @@ def main():
 
     max_len = a.isl + a.osl + 64
     cfg = EngineConfig.create(
-        a.model, device="cuda", block_size=a.block_size, max_num_seqs=a.concurrency,
+        a.model, device=a.device, block_size=a.block_size, max_num_seqs=a.concurrency,
         max_num_batched_tokens=a.max_num_batched_tokens, max_model_len=max_len,
         enforce_eager=a.enforce_eager, seed=a.seed + rank, enable_prefix_caching=True,
         cuda_graph_max_bs=a.concurrency, gpu_memory_utilization=a.gpu_memory_utilization,
         kv_cache_memory_bytes=int(a.kv_cache_gb * 2**30) if a.kv_cache_gb else None)
     t0 = time.time()
     eng = LLMEngine(cfg)
-    torch.cuda.synchronize()
+    _sync(a)
     log(rank, f"engine up in {time.time() - t0:.1f}s: {cfg.model_config.name}, "
               f"{eng.runner.num_blocks} KV blocks x {a.block_size}")
     vocab = cfg.model_config.vocab_size
@@ -153,7 +164,7 @@ def main():
             break
     while eng.sched.num_running + eng.sched.num_waiting < a.concurrency:
         new_request(a.osl)
-    torch.cuda.synchronize()
+    _sync(a)
     log(rank, f"setup: {setup_steps} steps in {time.time() - ts:.1f}s (batch filled to {a.concurrency})")
 
     def run_steps(n):
@@ -165,7 +176,7 @@ def main():
     # warmup
     tw = time.time()
     run_steps(a.warmup)
-    torch.cuda.synchronize()
+    _sync(a)
     log(rank, f"warmup {a.warmup} steps in {time.time() - tw:.1f}s")
     # timed
     eng.metrics.ttfts.clear()
@@ -173,10 +184,10 @@ def main():
     prompt0 = eng.metrics.n_prompt
     if world > 1:
         dist.barrier()
-    torch.cuda.synchronize()
+    _sync(a)
     t1 = time.perf_counter()
     run_steps(a.steps)
-    torch.cuda.synchronize()
+    _sync(a)
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t1

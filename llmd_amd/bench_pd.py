@@ -23,6 +23,7 @@ import json
 import os
 import queue
 import statistics
+import sys
 import threading
 import time
 
@@ -31,10 +32,18 @@ import torch
 import torch.distributed as dist
 
 
+def _sync(a):
+    if a.device == "cuda":
+        torch.cuda.synchronize()
+
+
 def run_pd(a, rank: int, world: int, local_rank: int, log) -> dict | None:
     from llmd_amd.engine.config import EngineConfig
     from llmd_amd.engine.engine import LLMEngine
     from llmd_amd.engine.request import SamplingParams
+
+    def log(_rank, *m):  # every rank reports (hang diagnosis on multi-GPU runs)
+        print(f"[bench-pd rank {rank}]", *m, file=sys.stderr, flush=True)
 
     P = a.prefill_gpus or max(1, (3 * world) // 4)
     if not 0 < P < world:
@@ -49,7 +58,7 @@ def run_pd(a, rank: int, world: int, local_rank: int, log) -> dict | None:
     n_decode = world - P
     conc = a.concurrency
     cfg = EngineConfig.create(
-        a.model, device="cuda", block_size=a.block_size,
+        a.model, device=a.device, block_size=a.block_size,
         max_num_seqs=max(conc, 8) if not is_prefill else 64,
         max_num_batched_tokens=a.max_num_batched_tokens, max_model_len=max_len,
         enforce_eager=a.enforce_eager or is_prefill, seed=a.seed, enable_prefix_caching=True,
@@ -57,17 +66,17 @@ def run_pd(a, rank: int, world: int, local_rank: int, log) -> dict | None:
         kv_cache_memory_bytes=int(a.kv_cache_gb * 2**30) if a.kv_cache_gb else None)
     t0 = time.time()
     eng = LLMEngine(cfg, capture_graphs=not is_prefill)
-    torch.cuda.synchronize()
+    _sync(a)
     log(rank, f"{'prefill' if is_prefill else 'decode'} engine up in {time.time() - t0:.1f}s "
               f"({eng.runner.num_blocks} KV blocks)")
     if is_prefill:
         srv_thread = _start_server(cfg, eng, base_port + rank)
         dist.barrier(group=ctl)              # servers up
         dist.barrier(group=ctl)              # decoders finished setup+warmup
-        torch.cuda.synchronize()
+        _sync(a)
         dist.barrier(group=ctl)              # timed region start
         dist.barrier(group=ctl)              # timed region end
-        torch.cuda.synchronize()
+        _sync(a)
         stats = [0.0, 0.0, 0.0]
         gathered = [None] * world
         dist.all_gather_object(gathered, {"elapsed": 0.0, "gen": 0, "ttft": [], "prefill": True,
@@ -121,7 +130,7 @@ def run_pd(a, rank: int, world: int, local_rank: int, log) -> dict | None:
 
     for i in range(conc):
         new_request(max(1, int(a.osl * (i + 1) / conc)))
-    ts = time.time()
+    ts = t_log = time.time()
     # setup: wait until the batch is filled and decoding
     while True:
         drain_arrivals()
@@ -132,6 +141,11 @@ def run_pd(a, rank: int, world: int, local_rank: int, log) -> dict | None:
             break
         if time.time() - ts > 1800:
             break
+        if time.time() - t_log > 15:
+            t_log = time.time()
+            print(f"[bench-pd rank {rank}] setup {t_log - ts:.0f}s: issued={len(issued)} "
+                  f"waiting={eng.sched.num_waiting} running={eng.sched.num_running} "
+                  f"remote_wait={len(eng.sched.remote_wait)} gen={eng.metrics.n_gen}", flush=True)
     while in_flight() < conc:
         new_request(a.osl)
     log(rank, f"pd setup done in {time.time() - ts:.1f}s")
@@ -139,11 +153,11 @@ def run_pd(a, rank: int, world: int, local_rank: int, log) -> dict | None:
     dist.barrier(group=ctl)
     eng.metrics.ttfts.clear()
     gen0 = eng.metrics.n_gen
-    torch.cuda.synchronize()
+    _sync(a)
     dist.barrier(group=ctl)
     t1 = time.perf_counter()
     run_steps(a.steps)
-    torch.cuda.synchronize()
+    _sync(a)
     dist.barrier(group=ctl)
     elapsed = time.perf_counter() - t1
     gen = eng.metrics.n_gen - gen0

@@ -4,6 +4,7 @@
 // checks device, dtype, contiguity of the inner dimension and the shapes the
 // kernel's grid assumes, so a bad call raises instead of faulting the GPU.
 #include <torch/extension.h>
+#include <c10/hip/HIPGuard.h>
 #include <c10/hip/HIPStream.h>
 #include <hip/hip_runtime.h>
 
@@ -44,6 +45,13 @@ void llmd_moe_combine(const void*, int64_t, const int*, const float*, int, int, 
 
 namespace {
 
+// Kernels launch on the tensor's device even from threads whose current device
+// differs (engine / kvx threads); CPU tensors fall through to the CHECKs.
+std::optional<c10::DeviceIndex> dev_of(const torch::Tensor& t) {
+  if (t.is_cuda()) return t.get_device();
+  return std::nullopt;
+}
+
 hipStream_t cur_stream() { return c10::hip::getCurrentHIPStream().stream(); }
 
 #define CHECK_CUDA(x) TORCH_CHECK((x).is_cuda(), #x " must be a GPU tensor")
@@ -52,6 +60,7 @@ hipStream_t cur_stream() { return c10::hip::getCurrentHIPStream().stream(); }
 #define CHECK_DT(x, t) TORCH_CHECK((x).scalar_type() == (t), #x " has wrong dtype")
 
 void rms_norm(torch::Tensor out, torch::Tensor x, torch::Tensor w, double eps) {
+  const c10::hip::OptionalHIPGuard device_guard(dev_of(out));
   CHECK_CUDA(x); CHECK_BF16(x); CHECK_BF16(out); CHECK_BF16(w);
   CHECK_INNER(x); CHECK_INNER(out);
   TORCH_CHECK(x.dim() == 2 && out.dim() == 2 && w.is_contiguous(), "rms_norm: 2-D x/out");
@@ -64,6 +73,7 @@ void rms_norm(torch::Tensor out, torch::Tensor x, torch::Tensor w, double eps) {
 }
 
 void fused_add_rms_norm(torch::Tensor x, torch::Tensor residual, torch::Tensor w, double eps) {
+  const c10::hip::OptionalHIPGuard device_guard(dev_of(x));
   CHECK_CUDA(x); CHECK_BF16(x); CHECK_BF16(residual); CHECK_BF16(w);
   CHECK_INNER(x); CHECK_INNER(residual);
   TORCH_CHECK(x.dim() == 2 && residual.sizes() == x.sizes(), "fused_add_rms_norm shape");
@@ -79,6 +89,7 @@ void fused_add_rms_norm(torch::Tensor x, torch::Tensor residual, torch::Tensor w
 void rope_cache(torch::Tensor qkv, torch::Tensor positions, torch::Tensor cos_sin, int64_t Hq,
                 int64_t Hkv, int64_t D, torch::Tensor slots, torch::Tensor k_cache,
                 torch::Tensor v_cache, bool neox) {
+  const c10::hip::OptionalHIPGuard device_guard(dev_of(qkv));
   CHECK_CUDA(qkv); CHECK_BF16(qkv); CHECK_INNER(qkv);
   CHECK_DT(positions, at::kLong); CHECK_DT(slots, at::kLong); CHECK_DT(cos_sin, at::kFloat);
   TORCH_CHECK(qkv.dim() == 2 && qkv.size(1) >= (Hq + 2 * Hkv) * D, "rope_cache: qkv width");
@@ -102,6 +113,7 @@ void rope_cache(torch::Tensor qkv, torch::Tensor positions, torch::Tensor cos_si
 }
 
 void gated_act(torch::Tensor out, torch::Tensor x, int64_t mode, double alpha, double limit) {
+  const c10::hip::OptionalHIPGuard device_guard(dev_of(out));
   CHECK_CUDA(x); CHECK_BF16(x); CHECK_BF16(out); CHECK_INNER(x); CHECK_INNER(out);
   TORCH_CHECK(x.dim() == 2 && out.dim() == 2 && x.size(0) == out.size(0), "gated_act shape");
   const int F = out.size(1);
@@ -124,6 +136,7 @@ void paged_decode(torch::Tensor out, torch::Tensor q, torch::Tensor k_cache, tor
                   torch::Tensor block_tables, torch::Tensor seq_lens, int64_t Hq, int64_t Hkv,
                   int64_t D, double scale, int64_t window, c10::optional<torch::Tensor> sinks,
                   int64_t split_size, int64_t nsplit, torch::Tensor part_o, torch::Tensor part_ml) {
+  const c10::hip::OptionalHIPGuard device_guard(dev_of(out));
   CHECK_CUDA(q); CHECK_BF16(q); CHECK_BF16(out); CHECK_INNER(q); CHECK_INNER(out);
   check_cache(k_cache, v_cache, Hkv, D);
   CHECK_DT(block_tables, at::kInt); CHECK_DT(seq_lens, at::kInt);
@@ -160,6 +173,7 @@ void paged_prefill(torch::Tensor out, torch::Tensor q, torch::Tensor k_cache,
                    torch::Tensor q_len, torch::Tensor ctx_len, torch::Tensor items, int64_t Hq,
                    int64_t Hkv, int64_t D, double scale, int64_t window,
                    c10::optional<torch::Tensor> sinks) {
+  const c10::hip::OptionalHIPGuard device_guard(dev_of(out));
   CHECK_CUDA(q); CHECK_BF16(q); CHECK_BF16(out); CHECK_INNER(q); CHECK_INNER(out);
   check_cache(k_cache, v_cache, Hkv, D);
   CHECK_DT(block_tables, at::kInt); CHECK_DT(q_start, at::kInt); CHECK_DT(q_len, at::kInt);
@@ -187,6 +201,7 @@ void paged_prefill(torch::Tensor out, torch::Tensor q, torch::Tensor k_cache,
 void sample(torch::Tensor logits, c10::optional<torch::Tensor> temps,
             c10::optional<torch::Tensor> seeds, torch::Tensor out_ids,
             c10::optional<torch::Tensor> out_logprob) {
+  const c10::hip::OptionalHIPGuard device_guard(dev_of(logits));
   CHECK_CUDA(logits); CHECK_INNER(logits);
   TORCH_CHECK(logits.dim() == 2, "logits 2-D");
   const bool bf = logits.scalar_type() == at::kBFloat16;
@@ -207,6 +222,7 @@ void sample(torch::Tensor logits, c10::optional<torch::Tensor> temps,
 
 void topk_topp_mask(torch::Tensor logits, c10::optional<torch::Tensor> topk,
                     c10::optional<torch::Tensor> topp, c10::optional<torch::Tensor> temps) {
+  const c10::hip::OptionalHIPGuard device_guard(dev_of(logits));
   CHECK_CUDA(logits); CHECK_DT(logits, at::kFloat); CHECK_INNER(logits);
   const int B = logits.size(0), V = logits.size(1);
   const int* k = nullptr;
@@ -222,6 +238,7 @@ void topk_topp_mask(torch::Tensor logits, c10::optional<torch::Tensor> topk,
 // dst/src are base addresses of the two KV pools (src may be an IPC-mapped peer pointer)
 void kvx_copy_blocks(torch::Tensor dst, int64_t src_ptr, int64_t dst_stride, int64_t src_stride,
                      torch::Tensor pairs, torch::Tensor segs, int64_t max_seg_bytes) {
+  const c10::hip::OptionalHIPGuard device_guard(dev_of(dst));
   CHECK_CUDA(dst); CHECK_CUDA(pairs); CHECK_CUDA(segs);
   CHECK_DT(pairs, at::kInt); CHECK_DT(segs, at::kLong);
   TORCH_CHECK(pairs.is_contiguous() && pairs.dim() == 2 && pairs.size(1) == 2, "pairs [n,2] int32");
@@ -235,6 +252,7 @@ void kvx_copy_blocks(torch::Tensor dst, int64_t src_ptr, int64_t dst_stride, int
 
 void kvx_dma_blocks(torch::Tensor dst, int64_t src_ptr, int64_t dst_stride, int64_t src_stride,
                     torch::Tensor pairs_cpu, int64_t block_bytes) {
+  const c10::hip::OptionalHIPGuard device_guard(dev_of(dst));
   CHECK_CUDA(dst); CHECK_DT(pairs_cpu, at::kInt);
   TORCH_CHECK(!pairs_cpu.is_cuda() && pairs_cpu.is_contiguous() && pairs_cpu.size(1) == 2, "pairs cpu [n,2]");
   int rc = llmd_kvx_dma_blocks(dst.data_ptr(), (const void*)src_ptr, dst_stride, src_stride,
@@ -243,6 +261,7 @@ void kvx_dma_blocks(torch::Tensor dst, int64_t src_ptr, int64_t dst_stride, int6
 }
 
 py::tuple kvx_ipc_export(torch::Tensor t) {
+  const c10::hip::OptionalHIPGuard device_guard(dev_of(t));
   CHECK_CUDA(t);
   std::string h(llmd_kvx_handle_size(), '\0');
   int64_t off = 0;
@@ -266,6 +285,7 @@ void kvx_ipc_close(int64_t p) { llmd_kvx_ipc_close((void*)p); }
 void moe_topk(torch::Tensor logits, int64_t k, int64_t scoring, c10::optional<torch::Tensor> bias,
               int64_t n_group, int64_t topk_group, bool renorm, double routed_scale, torch::Tensor ids,
               torch::Tensor wts) {
+  const c10::hip::OptionalHIPGuard device_guard(dev_of(logits));
   CHECK_CUDA(logits); CHECK_DT(logits, at::kFloat);
   TORCH_CHECK(logits.is_contiguous() && logits.dim() == 2, "logits [T, E] contiguous f32");
   const int T = logits.size(0), E = logits.size(1);
@@ -281,6 +301,7 @@ void moe_topk(torch::Tensor logits, int64_t k, int64_t scoring, c10::optional<to
 
 void moe_align(torch::Tensor ids, int64_t E, torch::Tensor sorted_ids, torch::Tensor tile_expert,
                torch::Tensor expert_offsets, torch::Tensor total_p, torch::Tensor inv) {
+  const c10::hip::OptionalHIPGuard device_guard(dev_of(ids));
   CHECK_CUDA(ids); CHECK_DT(ids, at::kInt); CHECK_DT(sorted_ids, at::kInt); CHECK_DT(tile_expert, at::kInt);
   const int n = ids.numel();
   const int bm = llmd_moe_gemm_tile_m();
@@ -297,6 +318,7 @@ void moe_align(torch::Tensor ids, int64_t E, torch::Tensor sorted_ids, torch::Te
 void moe_gemm(torch::Tensor X, int64_t topk, torch::Tensor sorted_ids, torch::Tensor tile_expert,
               torch::Tensor W, torch::Tensor Y, int64_t mode, int64_t act, double alpha, double limit,
               bool a_rows_are_slots, c10::optional<torch::Tensor> bias) {
+  const c10::hip::OptionalHIPGuard device_guard(dev_of(X));
   CHECK_CUDA(X); CHECK_BF16(X); CHECK_BF16(W); CHECK_BF16(Y); CHECK_INNER(X); CHECK_INNER(Y);
   TORCH_CHECK(W.dim() == 3 && W.is_contiguous(), "W [E, N, K] contiguous");
   const int N = W.size(1), K = W.size(2);
@@ -318,6 +340,7 @@ void moe_gemm(torch::Tensor X, int64_t topk, torch::Tensor sorted_ids, torch::Te
 }
 
 void moe_combine(torch::Tensor Y, torch::Tensor inv, torch::Tensor w, int64_t topk, torch::Tensor out) {
+  const c10::hip::OptionalHIPGuard device_guard(dev_of(Y));
   CHECK_CUDA(Y); CHECK_BF16(Y); CHECK_BF16(out); CHECK_DT(inv, at::kInt); CHECK_DT(w, at::kFloat);
   const int T = out.size(0), d = out.size(1);
   TORCH_CHECK(d % 8 == 0 && Y.size(1) >= d && inv.numel() >= (int64_t)T * topk && w.numel() >= (int64_t)T * topk,

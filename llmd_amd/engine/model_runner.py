@@ -43,6 +43,9 @@ class ModelRunner:
         self.cfg = cfg
         self.mc = cfg.model_config
         self.device = torch.device(device or cfg.device)
+        if self.device.type == "cuda" and self.device.index is None:
+            # pin the index: engine threads (AsyncEngine, kvx) start on device 0
+            self.device = torch.device("cuda", torch.cuda.current_device())
         self.is_gpu = self.device.type == "cuda"
         self.bs = cfg.cache.block_size
         self.max_model_len = cfg.sched.max_model_len

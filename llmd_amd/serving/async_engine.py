@@ -16,6 +16,8 @@ import threading
 import time
 from typing import AsyncIterator, Optional
 
+import torch
+
 from llmd_amd.engine.engine import LLMEngine
 from llmd_amd.engine.request import RequestOutput, SamplingParams
 
@@ -41,6 +43,9 @@ class AsyncEngine:
     # ------------------------------------------------------------ engine thread
     def _loop(self):
         eng = self.engine
+        dev = getattr(eng.runner, "device", None)
+        if dev is not None and torch.device(dev).type == "cuda":
+            torch.cuda.set_device(dev)  # the current HIP device is per thread
         try:
             while not self.stop_flag:
                 self._apply_cmds()
