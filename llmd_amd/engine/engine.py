@@ -135,6 +135,18 @@ class LLMEngine:
             self.step()
         return reqs
 
+    def shutdown(self):
+        """Release TP followers (their loop exits) and the KV transfer agent."""
+        if getattr(self, "_shut", False):
+            return
+        self._shut = True
+        if self.runner.tp_size > 1:
+            from .tp_worker import stop_followers
+
+            stop_followers()
+        if self.connector is not None and hasattr(self.connector, "close"):
+            self.connector.close()
+
     def reset_prefix_cache(self):
         self.bm.reset_prefix_cache()
         self._flush_events()

@@ -23,6 +23,8 @@ import torch
 
 from llmd_amd import ops
 from llmd_amd.models import build_model
+from llmd_amd.parallel.comm import tp_broadcast_plan, tp_min_int
+from llmd_amd.parallel.state import get_state
 
 from .attn_meta import AttnMeta
 from .config import EngineConfig
@@ -47,6 +49,7 @@ class ModelRunner:
             # pin the index: engine threads (AsyncEngine, kvx) start on device 0
             self.device = torch.device("cuda", torch.cuda.current_device())
         self.is_gpu = self.device.type == "cuda"
+        self.tp_size = get_state().tp_size
         self.bs = cfg.cache.block_size
         self.max_model_len = cfg.sched.max_model_len
         self.width = math.ceil(self.max_model_len / self.bs) + 1
@@ -114,6 +117,8 @@ class ModelRunner:
             nb = max(16, budget // self.block_bytes())
             log.info("kv cache: %d blocks x %d tokens (%.1f GiB), activation peak %.2f GiB",
                      nb, self.bs, nb * self.block_bytes() / 2**30, act_peak / 2**30)
+        if self.tp_size > 1:
+            nb = tp_min_int(int(nb))  # every TP rank must hold the same block pool
         self.num_blocks = int(nb)
         self.kv = self._alloc_cache(self.num_blocks)
         return self.num_blocks
@@ -221,16 +226,33 @@ class ModelRunner:
     def execute(self, so: SchedulerOutput, block_tables: dict[int, list[int]]) -> dict[int, tuple[int, float]]:
         if so.empty:
             return {}
-        rows, reqs = self._sample_rows(so)
-        if not so.prefills and self._graph_ok(len(so.decodes)):
-            logits = self._run_decode_graph(so, block_tables, rows)
-        else:
-            h = self._run_eager(so, block_tables)
-            idx = torch.tensor(rows, dtype=torch.long).to(self.device, non_blocking=True)
-            logits = self.model.compute_logits(h.index_select(0, idx)) if rows else None
-        if not rows:
+        pl, reqs = self.plan(so, block_tables)
+        if self.tp_size > 1:
+            tp_broadcast_plan(pl)  # TP followers run the same plan (engine/tp_worker.py)
+        logits = self.run_plan(pl)
+        if not reqs:
             return {}
         return self._sample(logits, reqs)
+
+    def plan(self, so: SchedulerOutput, block_tables: dict[int, list[int]]) -> tuple[dict, list]:
+        """Host-side step description: everything a (TP) rank needs to run the
+        forward, independent of the scheduler's request objects."""
+        rows, reqs = self._sample_rows(so)
+        ids, pos, slots, d_bt, d_len, p_ql, p_ctx, p_bt = self._prepare(so, block_tables)
+        graph = not so.prefills and self._graph_ok(len(so.decodes))
+        return {"graph": graph, "nd": len(so.decodes), "ids": ids, "pos": pos, "slots": slots, "d_bt": d_bt,
+                "d_len": d_len, "p_ql": p_ql, "p_ctx": p_ctx, "p_bt": p_bt, "rows": rows}, reqs
+
+    @torch.no_grad()
+    def run_plan(self, pl: dict):
+        rows = pl["rows"]
+        if pl["graph"]:
+            return self._run_decode_graph(pl)
+        h = self._run_eager(pl)
+        if not rows:
+            return None
+        idx = torch.tensor(rows, dtype=torch.long).to(self.device, non_blocking=True)
+        return self.model.compute_logits(h.index_select(0, idx))
 
     def _sample(self, logits, reqs):
         temps, seeds, topk, topp, any_rand, any_k, any_p = self._sampling_tensors(reqs)
@@ -251,10 +273,11 @@ class ModelRunner:
         lp_h = lp.cpu().tolist() if lp is not None else [0.0] * len(ids_h)
         return {r.seq_id: (int(ids_h[i]), float(lp_h[i])) for i, r in enumerate(reqs)}
 
-    def _run_eager(self, so: SchedulerOutput, block_tables):
-        ids, pos, slots, d_bt, d_len, p_ql, p_ctx, p_bt = self._prepare(so, block_tables)
+    def _run_eager(self, pl: dict):
+        ids, pos, slots, d_bt, d_len = pl["ids"], pl["pos"], pl["slots"], pl["d_bt"], pl["d_len"]
+        p_ql, p_ctx, p_bt = pl["p_ql"], pl["p_ctx"], pl["p_bt"]
         dev = self.device
-        nd = len(so.decodes)
+        nd = pl["nd"]
         T = len(ids)
         host = torch.tensor([ids, pos, slots], dtype=torch.long)
         if self.is_gpu:
@@ -332,11 +355,11 @@ class ModelRunner:
         torch.cuda.synchronize()
         log.info("captured %d decode graphs in %.1fs", len(buckets), time.time() - t0)
 
-    def _run_decode_graph(self, so: SchedulerOutput, block_tables, rows):
-        n = len(so.decodes)
+    def _run_decode_graph(self, pl: dict):
+        n, rows = pl["nd"], pl["rows"]
         B = self._bucket(n)
         g, lg = self.graphs[B]
-        ids, pos, slots, d_bt, d_len, *_ = self._prepare(so, block_tables)
+        ids, pos, slots, d_bt, d_len = pl["ids"], pl["pos"], pl["slots"], pl["d_bt"], pl["d_len"]
         if B > n:
             pad = B - n
             ids = ids + [0] * pad

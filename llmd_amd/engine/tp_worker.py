@@ -1,0 +1,51 @@
+"""Tensor-parallel follower ranks (SURVEY §2.5 TP, M01/M02).
+
+One process per GPU. TP rank 0 of a replica runs the full engine (scheduler,
+block manager, API); every other TP rank runs only a ModelRunner holding its
+weight and KV-head shard. Each step the driver broadcasts the step plan
+(token ids, positions, slots, block tables, sequence lengths, sample rows;
+``ModelRunner.plan``) over the replica's gloo group and all ranks execute the
+same forward - RCCL all-reduces inside the layers keep them in lock-step, and
+decode buckets replay the same hipGraphs on every rank. Logits are
+all-gathered by the LM head; only the driver samples.
+
+Start-up mirrors the driver exactly (profile -> agree on the block count with
+a MIN all-reduce -> allocate -> capture graphs), so collectives line up.
+"""
+from __future__ import annotations
+
+import logging
+
+import torch
+
+from llmd_amd.parallel.comm import tp_broadcast_plan, tp_recv_plan
+
+from .config import EngineConfig
+from .model_runner import ModelRunner
+
+log = logging.getLogger("llmd.tp")
+
+STOP = {"stop": True}
+
+
+def run_follower(cfg: EngineConfig, capture_graphs: bool = True) -> int:
+    """Blocking loop for TP ranks != 0. Returns the number of steps executed."""
+    runner = ModelRunner(cfg)
+    runner.profile_and_allocate()
+    if capture_graphs:
+        runner.capture_graphs()
+    n = 0
+    with torch.no_grad():
+        while True:
+            pl = tp_recv_plan()
+            if pl is None or pl.get("stop"):
+                break
+            runner.run_plan(pl)
+            n += 1
+    log.info("tp follower exiting after %d steps", n)
+    return n
+
+
+def stop_followers():
+    """Driver side: release the followers' loops."""
+    tp_broadcast_plan(STOP)

@@ -91,6 +91,43 @@ class LlamaForCausalLM(torch.nn.Module):
     def attention_layers(self):
         return [layer.attn for layer in self.layers]
 
+    def weight_specs(self) -> list:
+        """HF checkpoint names -> this rank's parameters (models/loader.py)."""
+        cfg = self.cfg
+        D, Hq, Hkv = cfg.head_dim, cfg.num_attention_heads, cfg.num_key_value_heads
+        specs = [("model.embed_tokens.weight", self.embed.weight, "vocab", None),
+                 ("model.norm.weight", self.norm.weight, "replicate", None)]
+        if not cfg.tie_word_embeddings:
+            specs.append(("lm_head.weight", self.lm_head.weight, "vocab", None))
+        for i, layer in enumerate(self.layers):
+            pre = f"model.layers.{i}."
+            a = layer.attn
+            q_rows, kv_rows = a.Hq * D, a.Hkv * D
+            specs += [(pre + "input_layernorm.weight", layer.input_layernorm.weight, "replicate", None),
+                      (pre + "post_attention_layernorm.weight", layer.post_attention_layernorm.weight,
+                       "replicate", None),
+                      (pre + "self_attn.o_proj.weight", layer.o_proj.weight, "row", None)]
+            for nm, off, nh in (("q_proj", 0, Hq), ("k_proj", q_rows, Hkv), ("v_proj", q_rows + kv_rows, Hkv)):
+                specs.append((pre + f"self_attn.{nm}.weight", layer.qkv.weight, "fused", (off, nh, D)))
+                if layer.qkv.bias is not None:
+                    specs.append((pre + f"self_attn.{nm}.bias", layer.qkv.bias, "fused", (off, nh, D)))
+            if layer.o_proj.bias is not None:
+                specs.append((pre + "self_attn.o_proj.bias", layer.o_proj.bias, "replicate", None))
+            if layer.qk_norm:
+                specs += [(pre + "self_attn.q_norm.weight", layer.q_norm.weight, "replicate", None),
+                          (pre + "self_attn.k_norm.weight", layer.k_norm.weight, "replicate", None)]
+            if a.sinks is not None:
+                specs.append((pre + "self_attn.sinks", a.sinks, "col", None))
+            specs += self._mlp_specs(pre, layer.mlp)
+        return specs
+
+    def _mlp_specs(self, pre: str, mlp) -> list:
+        F_total = self.cfg.intermediate_size
+        F_local = mlp.gate_up.weight.shape[0] // 2
+        return [(pre + "mlp.gate_proj.weight", mlp.gate_up.weight, "fused", (0, F_total, 1)),
+                (pre + "mlp.up_proj.weight", mlp.gate_up.weight, "fused", (F_local, F_total, 1)),
+                (pre + "mlp.down_proj.weight", mlp.down.weight, "row", None)]
+
     @torch.no_grad()
     def forward(self, input_ids: torch.Tensor, meta: AttnMeta) -> torch.Tensor:
         x = self.embed(input_ids)

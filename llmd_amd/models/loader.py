@@ -1,0 +1,110 @@
+"""Checkpoint loading: HuggingFace safetensors -> TP-sharded
+modules, and the inverse export (TP=1) used by tests and tools.
+
+Each model class describes its parameters with ``weight_specs()``: a list of
+``(hf_name, param, kind, extra)`` entries where ``kind`` says how a full
+checkpoint tensor maps onto this rank's shard:
+
+  replicate            copy as is (norms, q/k norms, router)
+  col                  split dim 0 into tp chunks (column-parallel weight/bias)
+  row                  split dim 1 into tp chunks (row-parallel weight)
+  vocab                rows [rank*per, rank*per+per) of a vocab-parallel table
+                       (zero-padded past the vocabulary)
+  fused                a slice [off, off+len) of a fused column-parallel param
+                       (q|k|v or gate|up); ``extra = (off, n_heads_total,
+                       head_rows)`` - heads are split across ranks, KV heads
+                       replicated when there are fewer KV heads than ranks.
+
+Only safetensors are read (``safe_open``: no pickle, nothing executed).
+"""
+from __future__ import annotations
+
+import glob
+import os
+
+import torch
+
+from llmd_amd.parallel.state import get_state
+
+
+def _files(path: str) -> list[str]:
+    if os.path.isdir(path):
+        fs = sorted(glob.glob(os.path.join(path, "*.safetensors")))
+        if not fs:
+            raise FileNotFoundError(f"no *.safetensors under {path}")
+        return fs
+    return [path]
+
+
+def _shard_heads(t: torch.Tensor, n_heads: int, head_rows: int, tp: int, rank: int) -> torch.Tensor:
+    """Rows of this rank's heads from a [n_heads*head_rows, ...] tensor."""
+    if n_heads >= tp:
+        per = n_heads // tp
+        return t[rank * per * head_rows:(rank + 1) * per * head_rows]
+    h = rank // (tp // n_heads)  # fewer heads than ranks: replicate
+    return t[h * head_rows:(h + 1) * head_rows]
+
+
+def place(param: torch.Tensor, full: torch.Tensor, kind: str, extra=None):
+    st = get_state()
+    tp, rank = st.tp_size, st.tp_rank
+    full = full.to(param.dtype)
+    with torch.no_grad():
+        if kind == "replicate":
+            param.copy_(full.view_as(param))
+        elif kind == "col":
+            param.copy_(full.chunk(tp, 0)[rank])
+        elif kind == "row":
+            param.copy_(full.chunk(tp, 1)[rank])
+        elif kind == "vocab":
+            per = param.shape[0]
+            part = full[rank * per:(rank + 1) * per]
+            param.zero_()
+            param[: part.shape[0]].copy_(part)
+        elif kind == "fused":
+            off, n_heads, head_rows = extra
+            part = _shard_heads(full, n_heads, head_rows, tp, rank)
+            param[off:off + part.shape[0]].copy_(part)
+        else:
+            raise ValueError(kind)
+
+
+def load_weights(model: torch.nn.Module, path: str, strict: bool = True) -> int:
+    from safetensors import safe_open
+
+    specs = {name: (p, kind, extra) for name, p, kind, extra in model.weight_specs()}
+    seen = set()
+    for f in _files(path):
+        with safe_open(f, framework="pt", device="cpu") as fh:
+            for name in fh.keys():
+                if name not in specs:
+                    continue
+                p, kind, extra = specs[name]
+                place(p, fh.get_tensor(name).to(p.device), kind, extra)
+                seen.add(name)
+    missing = set(specs) - seen
+    if missing and strict:
+        raise KeyError(f"checkpoint is missing {len(missing)} tensors, e.g. {sorted(missing)[:4]}")
+    return len(seen)
+
+
+def export_hf(model: torch.nn.Module) -> dict[str, torch.Tensor]:
+    """Full HF-named state dict of a TP=1 model (inverse of load_weights)."""
+    if get_state().tp_size != 1:
+        raise RuntimeError("export_hf needs tp_size == 1")
+    out: dict[str, torch.Tensor] = {}
+    for name, p, kind, extra in model.weight_specs():
+        if kind == "fused":
+            off, n_heads, head_rows = extra
+            out[name] = p[off:off + n_heads * head_rows].detach().cpu().clone()
+        elif kind == "vocab":
+            out[name] = p[: model.cfg.vocab_size].detach().cpu().clone()
+        else:
+            out[name] = p.detach().cpu().clone()
+    return out
+
+
+def save_safetensors(tensors: dict[str, torch.Tensor], path: str):
+    from safetensors.torch import save_file
+
+    save_file({k: v.contiguous() for k, v in tensors.items()}, path)

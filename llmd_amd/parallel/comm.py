@@ -34,8 +34,11 @@ def tp_all_gather(x: torch.Tensor, dim: int = -1) -> torch.Tensor:
     if st.tp_size == 1:
         return x
     dim = dim % x.dim()
-    out = torch.empty((st.tp_size,) + tuple(x.shape), dtype=x.dtype, device=x.device)
+    out = torch.empty((st.tp_size * x.shape[0],) + tuple(x.shape[1:]), dtype=x.dtype, device=x.device)
     dist.all_gather_into_tensor(out, x.contiguous(), group=st.tp_group)
+    out = out.view((st.tp_size,) + tuple(x.shape))
+    if dim == 0:
+        return out.reshape((-1,) + tuple(x.shape[1:]))
     return torch.cat(out.unbind(0), dim=dim)
 
 
@@ -65,4 +68,31 @@ def dp_all_reduce_max_int(v: int) -> int:
         return v
     t = torch.tensor([v], dtype=torch.int64)
     dist.all_reduce(t, op=dist.ReduceOp.MAX, group=st.cpu_group)
+    return int(t.item())
+
+
+def tp_src_rank() -> int:
+    st = get_state()
+    return st.dp_rank * st.tp_size  # TP rank 0 of this replica drives the step
+
+
+def tp_broadcast_plan(plan) -> None:
+    """Driver side: send one step plan (small dict of host arrays) to TP followers."""
+    st = get_state()
+    dist.broadcast_object_list([plan], src=tp_src_rank(), group=st.tp_cpu_group)
+
+
+def tp_recv_plan():
+    st = get_state()
+    box = [None]
+    dist.broadcast_object_list(box, src=tp_src_rank(), group=st.tp_cpu_group)
+    return box[0]
+
+
+def tp_min_int(v: int) -> int:
+    st = get_state()
+    if st.tp_size == 1:
+        return v
+    t = torch.tensor([v], dtype=torch.int64)
+    dist.all_reduce(t, op=dist.ReduceOp.MIN, group=st.tp_cpu_group)
     return int(t.item())

@@ -7,6 +7,8 @@ Groups:
   * dp       - data-parallel replicas (same TP rank across replicas)
   * ep       - expert parallel = tp x dp flattened (wide-EP)
   * cpu      - gloo group mirroring world, for host-side control messages
+  * tp_cpu   - gloo group of one TP replica: the driver rank broadcasts each
+               step's plan to its TP followers (engine/tp_worker.py)
 Backend "nccl" is RCCL on ROCm. On CPU-only hosts the backend is gloo.
 """
 from __future__ import annotations
@@ -33,6 +35,7 @@ class ParallelState:
     dp_group: Optional[object] = None
     ep_group: Optional[object] = None
     cpu_group: Optional[object] = None
+    tp_cpu_group: Optional[object] = None  # gloo: TP step-plan broadcast
     backend: str = "none"
 
     @property
@@ -82,8 +85,10 @@ def init_distributed(tp_size: int = 1, backend: Optional[str] = None,
         for d in range(st.dp_size):
             ranks = list(range(d * tp_size, (d + 1) * tp_size))
             g = dist.new_group(ranks) if tp_size > 1 else None
+            gc = (dist.new_group(ranks, backend="gloo") if backend != "gloo" else g) if tp_size > 1 else None
             if rank in ranks:
                 st.tp_group = g
+                st.tp_cpu_group = gc
         for t in range(tp_size):
             ranks = list(range(t, world, tp_size))
             g = dist.new_group(ranks) if st.dp_size > 1 else None

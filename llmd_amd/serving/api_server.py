@@ -377,6 +377,17 @@ def main(argv=None):
     a = p.parse_args(argv)
     logging.basicConfig(level=a.log_level.upper(), format="%(asctime)s %(levelname)s %(name)s: %(message)s")
     cfg = engine_config_from_args(a)
+    if cfg.parallel.tensor_parallel_size > 1:
+        # one process per GPU under torchrun; TP rank 0 serves, the others follow
+        from llmd_amd.parallel.state import init_distributed
+
+        st = init_distributed(tp_size=cfg.parallel.tensor_parallel_size,
+                              backend=None if cfg.device == "cuda" else "gloo")
+        if st.tp_rank != 0:
+            from llmd_amd.engine.tp_worker import run_follower
+
+            run_follower(cfg, capture_graphs=not cfg.enforce_eager)
+            return
     srv = build_server(cfg)
     app = srv.app()
 

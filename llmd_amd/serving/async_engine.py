@@ -173,3 +173,5 @@ class AsyncEngine:
         self.stop_flag = True
         self.wake.set()
         self.thread.join(timeout=5)
+        if hasattr(self.engine, "shutdown"):
+            self.engine.shutdown()
