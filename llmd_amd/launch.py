@@ -1,0 +1,209 @@
+"""Single-node launcher: the pod-group role of LeaderWorkerSet / Helm on one
+8xMI355X host (reference guides/wide-ep-lws/modelserver/gpu/
+vllm/base/decode.yaml:1-21,85,104-108 for the LWS env contract).
+
+A topology YAML names the model, the router and the engine roles::
+
+  model: llama-3-70b
+  gpus: 8                      # GPUs on the host (default: all visible)
+  router: {port: 8000, config: <EndpointPickerConfig path or inline YAML>}
+  roles:
+    - name: prefill            # llm-d.ai/role label: prefill | decode | prefill-decode
+      replicas: 6
+      tp: 1                    # GPUs per replica (torchrun ranks for tp > 1)
+      port: 8200               # engine port of replica 0 (+1 per replica)
+      args: ["--max-num-batched-tokens", "8192"]
+      kv_transfer: true        # kvx producer/consumer by role
+    - name: decode
+      replicas: 2
+      tp: 1
+      port: 8300
+      sidecar_port: 8400       # routing sidecar in front of each decode engine
+
+Every replica gets a disjoint GPU set (``HIP_VISIBLE_DEVICES``; TP replicas
+are packed onto neighbouring GPUs so TP traffic stays on direct xGMI links),
+LWS-compatible env (``LWS_GROUP_SIZE`` = tp, ``LWS_LEADER_ADDRESS``,
+``LWS_WORKER_INDEX``), ``POD_IP``/``POD_PORT`` (KV-event topic), and the
+router gets an ``endpoints.yaml`` for file discovery with role labels.
+``plan()`` is pure (testable); ``Launcher.start()/stop()`` run processes in
+their own sessions and stop them by process group.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import signal
+import subprocess
+import sys
+import tempfile
+import time
+from dataclasses import dataclass, field
+from typing import Optional
+
+import yaml
+
+PY = sys.executable
+
+
+@dataclass
+class ProcSpec:
+    name: str
+    cmd: list[str]
+    env: dict[str, str] = field(default_factory=dict)
+    gpus: list[int] = field(default_factory=list)
+    port: Optional[int] = None
+    role: str = ""
+
+
+def _kv_transfer(role: str) -> str:
+    r = {"prefill": "kv_producer", "decode": "kv_consumer"}.get(role, "kv_both")
+    return json.dumps({"kv_connector": "KvxConnector", "kv_role": r})
+
+
+def plan(topo: dict, workdir: str) -> tuple[list[ProcSpec], dict]:
+    """Returns (process specs, router endpoints doc)."""
+    n_gpus = int(topo.get("gpus", 8))
+    model = topo["model"]
+    free = list(range(n_gpus))
+    procs: list[ProcSpec] = []
+    endpoints = []
+    master_port = int(topo.get("master_port_base", 29600))
+    for role in topo.get("roles", []):
+        name, tp = role["name"], int(role.get("tp", 1))
+        for i in range(int(role.get("replicas", 1))):
+            if len(free) < tp:
+                raise ValueError(f"not enough GPUs for {name} replica {i} (tp={tp}, free={free})")
+            gpus, free = free[:tp], free[tp:]
+            port = int(role.get("port", 8200)) + i
+            args = ["--model", model, "--port", str(port), "--tensor-parallel-size", str(tp)] + \
+                [str(x) for x in role.get("args", [])]
+            if role.get("kv_transfer", name in ("prefill", "decode")):
+                args += ["--kv-transfer-config", _kv_transfer(name)]
+            if role.get("kv_events", False):
+                args += ["--kv-events-config", json.dumps(
+                    {"enable_kv_cache_events": True, "publisher": "zmq",
+                     "endpoint": f"tcp://*:{int(role.get('kv_events_port', 5556)) + len(procs)}"})]
+            server = ["-m", "llmd_amd.serving.api_server"] + args
+            if tp > 1:
+                cmd = [PY, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={tp}",
+                       "--master-addr=127.0.0.1", f"--master-port={master_port}"] + server
+                master_port += 1
+            else:
+                cmd = [PY] + server
+            env = {"HIP_VISIBLE_DEVICES": ",".join(map(str, gpus)), "LWS_GROUP_SIZE": str(tp),
+                   "LWS_LEADER_ADDRESS": "127.0.0.1", "LWS_WORKER_INDEX": "0", "POD_IP": "127.0.0.1",
+                   "POD_PORT": str(port), "HSA_ENABLE_IPC_MODE_LEGACY": "0"}
+            rid = f"{name}-{i}"
+            procs.append(ProcSpec(rid, cmd, env, gpus, port, name))
+            front = port
+            if name == "decode" and role.get("sidecar_port"):
+                front = int(role["sidecar_port"]) + i
+                procs.append(ProcSpec(rid + "-sidecar",
+                                      [PY, "-m", "llmd_amd.sidecar.routing_sidecar", "--port", str(front),
+                                       "--vllm-port", str(port), "--connector", role.get("connector", "nixlv2")],
+                                      {}, [], front, "sidecar"))
+            labels = {"llm-d.ai/role": name if name in ("prefill", "decode", "encode") else "prefill-decode",
+                      "llm-d.ai/model": model}
+            if role.get("kv_events", False):
+                labels["llm-d.ai/kv-events-port"] = str(int(role.get("kv_events_port", 5556)) + len(procs) - 1)
+            endpoints.append({"name": rid, "address": "127.0.0.1", "port": front, "labels": labels,
+                              "metricsPort": port})
+    doc = {"endpoints": endpoints}
+    r = topo.get("router")
+    if r:
+        ep_file = os.path.join(workdir, "endpoints.yaml")
+        cmd = [PY, "-m", "llmd_amd.router.proxy", "--port", str(r.get("port", 8000)), "--endpoints-file", ep_file]
+        conf = r.get("config")
+        if conf:
+            if os.path.exists(str(conf)):
+                cmd += ["--config-file", str(conf)]
+            else:
+                cmd += ["--config-text", conf if isinstance(conf, str) else yaml.safe_dump(conf)]
+        procs.append(ProcSpec("router", cmd, {}, [], int(r.get("port", 8000)), "router"))
+    return procs, doc
+
+
+class Launcher:
+    def __init__(self, topo: dict, workdir: Optional[str] = None, log_dir: Optional[str] = None):
+        self.topo = topo
+        self.workdir = workdir or tempfile.mkdtemp(prefix="llmd-launch-")
+        self.log_dir = log_dir or self.workdir
+        self.specs, self.endpoints = plan(topo, self.workdir)
+        self.procs: list[tuple[ProcSpec, subprocess.Popen]] = []
+
+    def start(self):
+        with open(os.path.join(self.workdir, "endpoints.yaml"), "w") as f:
+            yaml.safe_dump(self.endpoints, f)
+        for s in self.specs:
+            env = dict(os.environ, **s.env)
+            log = open(os.path.join(self.log_dir, f"{s.name}.log"), "w")
+            p = subprocess.Popen(s.cmd, env=env, stdout=log, stderr=subprocess.STDOUT, start_new_session=True)
+            self.procs.append((s, p))
+        return self
+
+    def wait_ready(self, timeout: float = 1800.0) -> bool:
+        import urllib.request
+
+        t0 = time.time()
+        pending = [s for s, _ in self.procs if s.port and s.role != "router"]
+        while pending and time.time() - t0 < timeout:
+            for s in list(pending):
+                try:
+                    with urllib.request.urlopen(f"http://127.0.0.1:{s.port}/health", timeout=2) as r:
+                        if r.status == 200:
+                            pending.remove(s)
+                except OSError:
+                    pass
+            if any(p.poll() is not None for _, p in self.procs):
+                return False
+            time.sleep(1.0)
+        return not pending
+
+    def stop(self, grace: float = 30.0):
+        for s, p in reversed(self.procs):
+            if p.poll() is None:
+                try:
+                    os.killpg(p.pid, signal.SIGTERM)
+                except ProcessLookupError:
+                    pass
+        t0 = time.time()
+        for s, p in self.procs:
+            while p.poll() is None and time.time() - t0 < grace:
+                time.sleep(0.1)
+            if p.poll() is None:
+                os.killpg(p.pid, signal.SIGKILL)
+                p.wait()
+        self.procs.clear()
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser("llmd-launch")
+    ap.add_argument("topology", help="topology YAML")
+    ap.add_argument("--dry-run", action="store_true", help="print the process plan and exit")
+    ap.add_argument("--log-dir", default=None)
+    a = ap.parse_args(argv)
+    with open(a.topology) as f:
+        topo = yaml.safe_load(f)
+    if a.dry_run:
+        specs, doc = plan(topo, "<workdir>")
+        for s in specs:
+            print(f"{s.name:18} gpus={s.gpus} port={s.port} env={s.env.get('HIP_VISIBLE_DEVICES', '')}\n"
+                  f"    {' '.join(s.cmd)}")
+        print(yaml.safe_dump(doc))
+        return
+    la = Launcher(topo, log_dir=a.log_dir).start()
+    try:
+        ok = la.wait_ready()
+        print("all engines ready" if ok else "an engine exited during start-up; see logs in " + la.log_dir,
+              flush=True)
+        while ok and all(p.poll() is None for _, p in la.procs):
+            time.sleep(1.0)
+    except KeyboardInterrupt:
+        pass
+    finally:
+        la.stop()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,66 @@
+"""Single-node launcher plan (C40/C41): GPU assignment, TP packing, LWS env,
+P/D roles with sidecars, router endpoints file."""
+import os
+
+import yaml
+
+from llmd_amd.launch import plan
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_pd_topology_plan():
+    with open(os.path.join(ROOT, "deploy/single-node/pd-70b-6p2d.yaml")) as f:
+        topo = yaml.safe_load(f)
+    specs, doc = plan(topo, "/tmp/w")
+    eng = [s for s in specs if s.role in ("prefill", "decode")]
+    assert [s.gpus for s in eng] == [[i] for i in range(8)]
+    assert sum(s.role == "sidecar" for s in specs) == 2 and specs[-1].name == "router"
+    pre = [s for s in eng if s.role == "prefill"]
+    assert all("kv_producer" in " ".join(s.cmd) for s in pre)
+    roles = [e["labels"]["llm-d.ai/role"] for e in doc["endpoints"]]
+    assert roles == ["prefill"] * 6 + ["decode"] * 2
+    assert [e["port"] for e in doc["endpoints"]][-2:] == [8400, 8401]  # decode via sidecar
+
+
+def test_tp_packing_and_overflow():
+    topo = {"model": "llama-3-70b", "gpus": 8,
+            "roles": [{"name": "decode", "replicas": 2, "tp": 4, "port": 9000}]}
+    specs, _ = plan(topo, "/tmp/w")
+    assert [s.gpus for s in specs] == [[0, 1, 2, 3], [4, 5, 6, 7]]
+    assert specs[0].env["LWS_GROUP_SIZE"] == "4" and "torch.distributed.run" in specs[0].cmd
+    topo["roles"][0]["replicas"] = 3
+    try:
+        plan(topo, "/tmp/w")
+        raise AssertionError("expected overflow")
+    except ValueError:
+        pass
+
+
+def test_baseline_kv_events_labels():
+    with open(os.path.join(ROOT, "deploy/single-node/optimized-baseline-8b.yaml")) as f:
+        topo = yaml.safe_load(f)
+    specs, doc = plan(topo, "/tmp/w")
+    ports = [e["labels"]["llm-d.ai/kv-events-port"] for e in doc["endpoints"]]
+    assert len(set(ports)) == 8
+    assert all("--kv-events-config" in s.cmd for s in specs if s.role == "prefill-decode")
+
+
+def test_deploy_values_and_router_configs_valid():
+    import glob
+
+    from llmd_amd.router.config import load_config
+
+    files = glob.glob(os.path.join(ROOT, "deploy/**/*.yaml"), recursive=True)
+    files = [f for f in files if "/templates/" not in f]
+    assert len(files) >= 10
+    n_cfg = 0
+    for f in files:
+        with open(f) as fh:
+            doc = yaml.safe_load(fh)
+        conf = ((doc or {}).get("router") or {})
+        text = conf.get("pluginsConfig") or conf.get("config")
+        if isinstance(text, str):
+            load_config(text)
+            n_cfg += 1
+    assert n_cfg >= 4
