@@ -10,10 +10,12 @@ flight (closed loop: a finished request is immediately replaced), W warmup
 steps bring the batch to steady state, then exactly K steps are timed between
 barrier+synchronize brackets; the slowest rank's time is used.
 
-Modes
-  agg  (default): every GPU is an independent aggregated replica (dp N) - the
+Modes (default ``auto``: agg for N = 1, pd for N >= 2)
+  agg : every GPU is an independent aggregated replica (dp N) - the
         optimized-baseline topology; per-GPU work fixed as N grows (weak scaling).
-  pd : ranks [0, P) prefill, [P, N) decode; KV moves over xGMI (kvx). N >= 2.
+  pd  : ranks [0, P) prefill, [P, N) decode (P = 3N/4 unless --prefill-gpus;
+        ISL 5000 / OSL 250 is prefill-heavy, so 6P2D is the throughput-optimal
+        split on 8 GPUs); KV moves over xGMI (kvx VMM-chunked IPC pool).
 
 Output: one JSON line on rank 0 (see README "bench.py contract").
 """
@@ -47,7 +49,8 @@ def parse():
     p.add_argument("--concurrency", type=int, default=64, help="requests in flight per GPU")
     p.add_argument("--max-num-batched-tokens", type=int, default=8192)
     p.add_argument("--block-size", type=int, default=64)
-    p.add_argument("--mode", default="agg", choices=["agg", "pd"])
+    p.add_argument("--mode", default="auto", choices=["auto", "agg", "pd"],
+                   help="auto: agg on 1 GPU, P/D disaggregation (3/4 prefill ranks) on N >= 2")
     p.add_argument("--prefill-gpus", type=int, default=0, help="pd mode: number of prefill ranks")
     p.add_argument("--enforce-eager", action="store_true")
     p.add_argument("--seed", type=int, default=0)
@@ -92,6 +95,8 @@ def main():
         else:
             dist.init_process_group("gloo", rank=rank, world_size=world)
 
+    if a.mode == "auto":
+        a.mode = "pd" if world > 1 else "agg"
     if a.mode == "pd":
         from llmd_amd.bench_pd import run_pd
 

@@ -7,6 +7,11 @@
 #include <c10/hip/HIPGuard.h>
 #include <c10/hip/HIPStream.h>
 #include <hip/hip_runtime.h>
+#include <pybind11/stl.h>
+
+#include <map>
+#include <memory>
+#include <vector>
 
 extern "C" {
 void llmd_rms_norm(void*, int64_t, const void*, int64_t, const void*, int, int, float, hipStream_t);
@@ -31,6 +36,11 @@ int llmd_kvx_copy_blocks(void*, const void*, int64_t, int64_t, const int*, int, 
 int llmd_kvx_ipc_export(const void*, void*, int64_t*);
 int llmd_kvx_ipc_open(const void*, void**);
 int llmd_kvx_ipc_close(void*);
+int llmd_vmm_granularity(int, size_t*);
+int llmd_vmm_alloc(int, size_t, int, void**, uint64_t*);
+int llmd_vmm_export_fd(uint64_t, int*);
+int llmd_vmm_import(const int*, int, size_t, int, void**, uint64_t*);
+int llmd_vmm_free(void*, size_t, int, const uint64_t*);
 int llmd_kvx_handle_size();
 int llmd_kvx_dma_blocks(void*, const void*, int64_t, int64_t, const int*, int, int64_t, hipStream_t);
 void llmd_moe_topk(const float*, int, int, int, int, const float*, int, int, int, float, int*, float*,
@@ -281,6 +291,58 @@ int64_t kvx_ipc_open(py::bytes handle) {
 
 void kvx_ipc_close(int64_t p) { llmd_kvx_ipc_close((void*)p); }
 
+int64_t vmm_granularity(int64_t device) {
+  size_t g = 0;
+  int rc = llmd_vmm_granularity((int)device, &g);
+  TORCH_CHECK(rc == 0, "hipMemGetAllocationGranularity failed: ", rc);
+  return (int64_t)g;
+}
+
+// Chunked VMM pool as one uint8 tensor + one exported dmabuf fd per chunk.
+py::tuple vmm_pool(int64_t device, int64_t chunk_bytes, int64_t n_chunks) {
+  TORCH_CHECK(chunk_bytes > 0 && n_chunks > 0, "vmm_pool: bad size");
+  const c10::hip::HIPGuard guard((c10::DeviceIndex)device);
+  auto handles = std::make_shared<std::vector<uint64_t>>(n_chunks);
+  void* base = nullptr;
+  int rc = llmd_vmm_alloc((int)device, (size_t)chunk_bytes, (int)n_chunks, &base, handles->data());
+  TORCH_CHECK(rc == 0, "vmm alloc failed: ", rc);
+  std::vector<int> fds(n_chunks, -1);
+  for (int64_t i = 0; i < n_chunks; ++i) {
+    rc = llmd_vmm_export_fd((*handles)[i], &fds[i]);
+    TORCH_CHECK(rc == 0, "hipMemExportToShareableHandle failed: ", rc);
+  }
+  const size_t cb = (size_t)chunk_bytes;
+  const int nc = (int)n_chunks;
+  auto t = torch::from_blob(
+      base, {chunk_bytes * n_chunks},
+      [handles, cb, nc](void* p) { llmd_vmm_free(p, cb, nc, handles->data()); },
+      torch::TensorOptions().dtype(torch::kUInt8).device(torch::kCUDA, (c10::DeviceIndex)device));
+  py::list pyfds;
+  for (int fd : fds) pyfds.append(fd);
+  return py::make_tuple(t, pyfds);
+}
+
+struct Imported { size_t chunk; std::vector<uint64_t> handles; };
+std::map<int64_t, Imported>& imported() { static std::map<int64_t, Imported> m; return m; }
+
+int64_t vmm_import(std::vector<int64_t> fds, int64_t chunk_bytes, int64_t device) {
+  const c10::hip::HIPGuard guard((c10::DeviceIndex)device);
+  std::vector<int> f(fds.begin(), fds.end());
+  Imported im{(size_t)chunk_bytes, std::vector<uint64_t>(f.size())};
+  void* base = nullptr;
+  int rc = llmd_vmm_import(f.data(), (int)f.size(), (size_t)chunk_bytes, (int)device, &base, im.handles.data());
+  TORCH_CHECK(rc == 0, "vmm import failed: ", rc);
+  imported()[(int64_t)base] = std::move(im);
+  return (int64_t)base;
+}
+
+void vmm_release(int64_t base) {
+  auto it = imported().find(base);
+  TORCH_CHECK(it != imported().end(), "vmm_release: unknown base");
+  llmd_vmm_free((void*)base, it->second.chunk, (int)it->second.handles.size(), it->second.handles.data());
+  imported().erase(it);
+}
+
 // ---------------------------------------------------------------- MoE
 void moe_topk(torch::Tensor logits, int64_t k, int64_t scoring, c10::optional<torch::Tensor> bias,
               int64_t n_group, int64_t topk_group, bool renorm, double routed_scale, torch::Tensor ids,
@@ -367,6 +429,10 @@ PYBIND11_MODULE(_C, m) {
   m.def("kvx_ipc_export", &kvx_ipc_export);
   m.def("kvx_ipc_open", &kvx_ipc_open);
   m.def("kvx_ipc_close", &kvx_ipc_close);
+  m.def("vmm_granularity", &vmm_granularity);
+  m.def("vmm_pool", &vmm_pool);
+  m.def("vmm_import", &vmm_import);
+  m.def("vmm_release", &vmm_release);
   m.def("moe_topk", &moe_topk);
   m.def("moe_align", &moe_align);
   m.def("moe_gemm", &moe_gemm);

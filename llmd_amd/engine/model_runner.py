@@ -15,6 +15,7 @@ from __future__ import annotations
 
 import logging
 import math
+import os
 import time
 from typing import Optional
 
@@ -38,6 +39,9 @@ def _mix64(z: int) -> int:
     z = ((z ^ (z >> 30)) * 0xBF58476D1CE4E5B9) & ((1 << 64) - 1)
     z = ((z ^ (z >> 27)) * 0x94D049BB133111EB) & ((1 << 64) - 1)
     return (z ^ (z >> 31)) & ((1 << 63) - 1)
+
+
+VMM_CHUNK = 2 << 30  # bytes per exportable KV-pool chunk
 
 
 class ModelRunner:
@@ -78,9 +82,29 @@ class ModelRunner:
     def block_bytes(self) -> int:
         return self.L * 2 * self.Hkv * self.bs * self.D * 2
 
-    def _alloc_cache(self, num_blocks: int) -> torch.Tensor:
-        kv = torch.empty(num_blocks, self.L, 2, self.Hkv, self.bs, self.D, dtype=torch.bfloat16,
-                         device=self.device)
+    def _wants_vmm(self) -> bool:
+        """KV producers export their pool to other processes (kvx); a single
+        >4 GiB allocation cannot be imported through hipIpc on this stack, so
+        the pool is built from exportable 2 GiB VMM chunks (kvx_vmm.hip)."""
+        kt = self.cfg.kv_transfer_config or {}
+        return (self.is_gpu and kt.get("kv_role") in ("kv_producer", "kv_both")
+                and os.environ.get("LLMD_KV_VMM", "1") != "0")
+
+    def _alloc_cache(self, num_blocks: int, scratch: bool = False) -> torch.Tensor:
+        shape = (num_blocks, self.L, 2, self.Hkv, self.bs, self.D)
+        self.vmm = None
+        if not scratch and self._wants_vmm():
+            C = ops.native()
+            chunk = VMM_CHUNK
+            gran = C.vmm_granularity(self.device.index)
+            chunk = (chunk + gran - 1) // gran * gran
+            need = num_blocks * self.block_bytes()
+            n = (need + chunk - 1) // chunk
+            pool, fds = C.vmm_pool(self.device.index, chunk, n)
+            kv = pool[:need].view(torch.bfloat16).view(shape)
+            self.vmm = {"fds": list(fds), "chunk": chunk, "n": n, "pool": pool}
+        else:
+            kv = torch.empty(shape, dtype=torch.bfloat16, device=self.device)
         for i, a in enumerate(self.model.attention_layers()):
             a.k_cache = kv[:, i, 0]
             a.v_cache = kv[:, i, 1]
@@ -97,7 +121,7 @@ class ModelRunner:
             # dummy max-size step on a scratch cache to measure activation peak
             T = self.cfg.sched.max_num_batched_tokens
             scratch_blocks = math.ceil(T / self.bs) + 2
-            self.kv = self._alloc_cache(scratch_blocks)
+            self.kv = self._alloc_cache(scratch_blocks, scratch=True)
             torch.cuda.synchronize()
             torch.cuda.reset_peak_memory_stats()
             base = torch.cuda.memory_allocated()

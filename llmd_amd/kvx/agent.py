@@ -81,11 +81,15 @@ class LoadJob:
     t0: float = field(default_factory=time.monotonic)
 
 
+LEGACY_IPC_MAX = 4 << 30  # hipIpcOpenMemHandle hangs importing larger allocations
+
+
 class KvxAgent:
     def __init__(self, kv: torch.Tensor, engine_id: Optional[str] = None, host: Optional[str] = None,
                  port: int = 0, tp_rank: int = 0, tp_size: int = 1, abort_timeout: float = 480.0,
-                 transport: str = "auto", metrics=None):
+                 transport: str = "auto", metrics=None, vmm: Optional[dict] = None):
         self.kv = kv                      # [num_blocks, L, 2, Hkv, bs, D]
+        self.vmm = vmm                    # chunked exportable pool (model_runner._alloc_cache)
         self.engine_id = engine_id or f"kvx-{uuid.uuid4().hex[:12]}"
         self.tp_rank, self.tp_size = tp_rank, tp_size
         self.abort_timeout = abort_timeout
@@ -101,14 +105,26 @@ class KvxAgent:
         self.peers: dict[tuple, dict] = {}
         self.ipc_maps: dict[str, int] = {}
         self.ipc_handle = None
+        self.uds_name = None
         if self.is_gpu and transport in ("auto", "ipc", "dma"):
-            try:
-                from llmd_amd.ops import native
+            if vmm is not None:
+                # hand the chunk fds to same-host peers over an abstract Unix socket
+                self.uds_name = f"\0llmd-kvx-{self.engine_id}"
+                self.uds = socket.socket(socket.AF_UNIX, socket.SOCK_STREAM)
+                self.uds.bind(self.uds_name)
+                self.uds.listen(16)
+                threading.Thread(target=self._serve_fds, daemon=True, name="kvx-fds").start()
+            elif kv.numel() * kv.element_size() <= LEGACY_IPC_MAX:
+                try:
+                    from llmd_amd.ops import native
 
-                h, off = native().kvx_ipc_export(kv)
-                self.ipc_handle = (h, off)
-            except Exception as e:  # noqa: BLE001
-                log.warning("IPC export unavailable (%s); kvx falls back to TCP", e)
+                    h, off = native().kvx_ipc_export(kv)
+                    self.ipc_handle = (h, off)
+                except Exception as e:  # noqa: BLE001
+                    log.warning("IPC export unavailable (%s); kvx falls back to TCP", e)
+            else:
+                log.warning("KV pool of %.1f GiB is not VMM-chunked; hipIpc cannot import >4 GiB, "
+                            "kvx falls back to TCP", kv.numel() * kv.element_size() / 2**30)
         self.host = host or os.environ.get("VLLM_NIXL_SIDE_CHANNEL_HOST", "127.0.0.1")
         self.server = _Server(("0.0.0.0" if self.host not in ("127.0.0.1", "localhost") else self.host,
                                port or int(os.environ.get("VLLM_NIXL_SIDE_CHANNEL_PORT", "0") or 0)), self)
@@ -117,6 +133,20 @@ class KvxAgent:
         self.worker = threading.Thread(target=self._work, daemon=True, name="kvx-transfer")
         self.stream = None
         self.worker.start()
+
+    def _serve_fds(self):
+        fds = self.vmm["fds"]
+        while True:
+            try:
+                c, _ = self.uds.accept()
+            except OSError:
+                return
+            try:
+                socket.send_fds(c, [struct.pack("<I", len(fds))], fds)
+            except OSError:
+                pass
+            finally:
+                c.close()
 
     # ------------------------------------------------------------ metadata
     def meta(self) -> dict:
@@ -127,6 +157,9 @@ class KvxAgent:
              "pid": os.getpid(), "num_blocks": k.shape[0]}
         if self.ipc_handle is not None:
             m["ipc_handle"], m["ipc_offset"] = self.ipc_handle
+        if self.uds_name is not None:
+            off = self.kv.data_ptr() - self.vmm["pool"].data_ptr()
+            m["vmm"] = {"uds": self.uds_name, "chunk": self.vmm["chunk"], "n": self.vmm["n"], "offset": off}
         return m
 
     # ------------------------------------------------------------ prefill side
@@ -248,12 +281,18 @@ class KvxAgent:
         n = min(len(rblocks), len(job.local_blocks))
         rblocks, lblocks = rblocks[:n], job.local_blocks[:n]
         segs = self._segments(rmeta)
-        use_ipc = (self.is_gpu and "ipc_handle" in rmeta and self.transport in ("auto", "ipc", "dma")
+        use_ipc = (self.is_gpu and ("ipc_handle" in rmeta or "vmm" in rmeta)
+                   and self.transport in ("auto", "ipc", "dma") and not p.get("no_ipc")
                    and rmeta.get("hostname") == socket.gethostname())
         nbytes = sum(s[2] for s in segs) * n
         if use_ipc:
-            self._ipc_copy(rmeta, rblocks, lblocks, segs)
-        else:
+            try:
+                self._ipc_copy(rmeta, rblocks, lblocks, segs)
+            except Exception as e:  # noqa: BLE001 - mapping failed: degrade this peer to TCP
+                log.warning("kvx IPC path to %s failed (%s); using TCP for this peer", rmeta.get("engine_id"), e)
+                p["no_ipc"] = True
+                use_ipc = False
+        if not use_ipc:
             data = self._rpc(p, {"op": "read", "blocks": rblocks, "request_id": prm.get("remote_request_id")})
             if isinstance(data, dict) and data.get("error"):
                 raise RuntimeError(data["error"])
@@ -284,7 +323,20 @@ class KvxAgent:
             self.stream = torch.cuda.Stream(device=self.kv.device)
         base = self.ipc_maps.get(eid)
         if base is None:
-            base = C.kvx_ipc_open(rmeta["ipc_handle"]) + int(rmeta["ipc_offset"])
+            if "vmm" in rmeta:
+                vm = rmeta["vmm"]
+                c = socket.socket(socket.AF_UNIX, socket.SOCK_STREAM)
+                c.settimeout(30)
+                c.connect(vm["uds"])
+                _, fds, _, _ = socket.recv_fds(c, 16, int(vm["n"]))
+                c.close()
+                try:
+                    base = C.vmm_import(list(fds), int(vm["chunk"]), self.kv.device.index) + int(vm["offset"])
+                finally:
+                    for fd in fds:
+                        os.close(fd)
+            else:
+                base = C.kvx_ipc_open(rmeta["ipc_handle"]) + int(rmeta["ipc_offset"])
             self.ipc_maps[eid] = base
         with torch.cuda.stream(self.stream):
             if self.transport == "dma" and len(segs) == 1:

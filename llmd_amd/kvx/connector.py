@@ -60,7 +60,8 @@ class KvxConnector:
         from llmd_amd.parallel.state import get_state
 
         st = get_state()
-        self.agent = KvxAgent(engine.runner.kv, host=extra.get("side_channel_host"),
+        self.agent = KvxAgent(engine.runner.kv, vmm=getattr(engine.runner, "vmm", None),
+                              host=extra.get("side_channel_host"),
                               port=int(extra.get("side_channel_port", 0) or 0),
                               tp_rank=st.tp_rank, tp_size=st.tp_size,
                               abort_timeout=float(extra.get("abort_timeout",
