@@ -152,52 +152,76 @@ __global__ __launch_bounds__(NT, 2) void prefill_kernel(
         sc[b4][0] = a0;
         sc[b4][1] = a1;
       }
-      // ---- mask + online softmax per q column
-      float alpha[2];
+      // ---- mask (only tiles that touch the diagonal / window edge) + online softmax.
+      // Scores stay raw; the row max m is kept in scaled log2 units and
+      // p = exp2(s*scale_log2 - m) is one FMA + v_exp. Lazy rescaling: m only
+      // moves when some row's max grows by more than 8 (p <= 2^8 stays exact
+      // enough in bf16/fp32), so O/l rescales are rare after the first tiles.
+      const bool need_mask = (ts + 63 > p_lo) || (window > 0 && ts <= p_hi - window);
+      if (need_mask) {
+#pragma unroll
+        for (int nb = 0; nb < 2; ++nb) {
+          const int qp = p_lo + 16 * nb + c16;
+#pragma unroll
+          for (int b4 = 0; b4 < 4; ++b4)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+              const int key = ts + 16 * b4 + rowoff(g) + i;
+              bool ok = key <= qp;
+              if (window > 0) ok = ok && key > qp - window;
+              sc[b4][nb][i] = ok ? sc[b4][nb][i] : NEG_INF;
+            }
+        }
+      }
+      float mt[2];
+      bool grow = false;
 #pragma unroll
       for (int nb = 0; nb < 2; ++nb) {
-        const int qp = p_lo + 16 * nb + c16;
         float mx = NEG_INF;
 #pragma unroll
         for (int b4 = 0; b4 < 4; ++b4)
 #pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            const int key = ts + 16 * b4 + rowoff(g) + i;
-            float v = sc[b4][nb][i] * scale_log2;
-            bool ok = key <= qp;
-            if (window > 0) ok = ok && key > qp - window;
-            v = ok ? v : NEG_INF;
-            sc[b4][nb][i] = v;
-            mx = fmaxf(mx, v);
-          }
+          for (int i = 0; i < 4; ++i) mx = fmaxf(mx, sc[b4][nb][i]);
         mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
         mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-        const float mnew = fmaxf(m[nb], mx);
-        // rows fully masked so far keep m=-inf; guard the exp of (-inf) - (-inf)
-        const float msafe = mnew == NEG_INF ? 0.f : mnew;
-        alpha[nb] = exp2f(m[nb] - msafe);
+        mt[nb] = mx * scale_log2;
+        grow = grow || (mt[nb] > m[nb] + 8.f);
+      }
+      if (__ballot(grow) != 0) {  // wave-uniform
+        float alpha[2];
+#pragma unroll
+        for (int nb = 0; nb < 2; ++nb) {
+          const float mnew = fmaxf(m[nb], mt[nb]);
+          alpha[nb] = (mnew == NEG_INF) ? 1.f : __builtin_amdgcn_exp2f(m[nb] - mnew);
+          lsum[nb] *= alpha[nb];
+          m[nb] = mnew;
+        }
+#pragma unroll
+        for (int nb = 0; nb < 2; ++nb)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const float a = __shfl(alpha[nb], 4 * g + i, 64);
+#pragma unroll
+            for (int n = 0; n < NB; ++n) o[nb][n][i] *= a;
+          }
+      }
+#pragma unroll
+      for (int nb = 0; nb < 2; ++nb) {
+        // fully masked rows so far keep m = -inf: their p must be 0, not exp2(nan)
+        const float msub = (m[nb] == NEG_INF) ? 0.f : m[nb];
         float ps = 0.f;
 #pragma unroll
         for (int b4 = 0; b4 < 4; ++b4)
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
-            const float p = exp2f(sc[b4][nb][i] - msafe);
+            const float p = __builtin_amdgcn_exp2f(fmaf(sc[b4][nb][i], scale_log2, -msub));
             sc[b4][nb][i] = p;
             ps += p;
           }
         ps += __shfl_xor(ps, 16, 64);
         ps += __shfl_xor(ps, 32, 64);
-        lsum[nb] = lsum[nb] * alpha[nb] + ps;
-        m[nb] = mnew;
+        lsum[nb] += ps;
       }
-#pragma unroll
-      for (int nb = 0; nb < 2; ++nb)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const float a = __shfl(alpha[nb], 4 * g + i, 64);
-#pragma unroll
-          for (int n = 0; n < NB; ++n) o[nb][n][i] *= a;
-        }
       // ---- O += P V
       const int qq = c16 >> 2, pp = c16 & 3;
 #pragma unroll

@@ -1,0 +1,116 @@
+"""Microbenchmark of the paged attention kernels (prefill + decode) at the
+serving shapes: Llama-3-70B TP1 heads (64 q / 8 kv, D=128), block 64.
+
+  python scripts/bench_attn.py [--ctx 5000] [--chunk 8192] [--check]
+
+Prefill: one sequence of `ctx` tokens prefilled in one call (causal), FLOPs =
+4*Hq*D*sum_q(keys visible). Decode: batch B at context `ctx`. Prints TF/s and
+GB/s; --check compares against the fp32 reference on a smaller shape first.
+"""
+import argparse
+import math
+import os
+import sys
+import time
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+if "--so" in sys.argv:  # benchmark another build of the extension (A/B)
+    import importlib.machinery
+    import importlib.util
+
+    so = sys.argv[sys.argv.index("--so") + 1]
+    loader = importlib.machinery.ExtensionFileLoader("llmd_amd._C", so)
+    spec = importlib.util.spec_from_file_location("llmd_amd._C", so, loader=loader)
+    mod = importlib.util.module_from_spec(spec)
+    loader.exec_module(mod)
+    sys.modules["llmd_amd._C"] = mod
+
+from llmd_amd import ops  # noqa: E402
+from llmd_amd.ops import reference as ref  # noqa: E402
+
+
+def make_cache(nctx, Hkv, D, bs, dev, seqs=1):
+    nb = seqs * math.ceil(nctx / bs) + 1
+    kc = torch.randn(nb, Hkv, bs, D, device=dev, dtype=torch.bfloat16)
+    vc = torch.randn(nb, Hkv, bs, D, device=dev, dtype=torch.bfloat16)
+    per = math.ceil(nctx / bs)
+    bt = torch.stack([torch.randperm(nb - 1, device=dev)[:per] for _ in range(seqs)]).int()
+    return kc, vc, bt
+
+
+def time_it(fn, iters=20):
+    for _ in range(3):
+        fn()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(iters):
+        fn()
+    torch.cuda.synchronize()
+    return (time.perf_counter() - t0) / iters
+
+
+def prefill(ctx, q_len, Hq, Hkv, D, bs, check=False):
+    dev = "cuda"
+    kc, vc, bt = make_cache(ctx, Hkv, D, bs, dev)
+    q = torch.randn(q_len, Hq * D, device=dev, dtype=torch.bfloat16)
+    q_start = torch.tensor([0], dtype=torch.int32, device=dev)
+    ql = torch.tensor([q_len], dtype=torch.int32, device=dev)
+    cl = torch.tensor([ctx], dtype=torch.int32, device=dev)
+    tpi = ops.prefill_tokens_per_item(Hq, Hkv)
+    items = torch.tensor(ops.build_prefill_items([q_len], [ctx], tpi), dtype=torch.int32, device=dev).view(-1, 2)
+    scale = D ** -0.5
+    out = torch.empty(q_len, Hq * D, device=dev, dtype=torch.bfloat16)
+    fn = lambda: ops.paged_prefill(q, kc, vc, bt, q_start, ql, cl, Hq, Hkv, D, scale, 0, None,  # noqa: E731
+                                   items=items, out=out)
+    if check:
+        fn()
+        r = ref.paged_prefill(q, kc, vc, bt, q_start, ql, cl, Hq, Hkv, D, scale, 0, None)
+        err = (out.float() - r.float()).abs().max().item()
+        print(f"  prefill check ctx={ctx} q={q_len}: max abs err {err:.4f}")
+        assert err < 0.05
+    t = time_it(fn)
+    p0 = ctx - q_len
+    vis = sum(p0 + i + 1 for i in range(q_len))
+    fl = 4 * Hq * D * vis
+    print(f"prefill ctx={ctx} q={q_len} Hq={Hq} Hkv={Hkv} D={D}: {t * 1e3:.3f} ms  {fl / t / 1e12:.1f} TF/s")
+    return t
+
+
+def decode(ctx, B, Hq, Hkv, D, bs):
+    dev = "cuda"
+    kc, vc, bt = make_cache(ctx, Hkv, D, bs, dev, seqs=B)
+    q = torch.randn(B, Hq * D, device=dev, dtype=torch.bfloat16)
+    sl = torch.full((B,), ctx, dtype=torch.int32, device=dev)
+    out = torch.empty(B, Hq * D, device=dev, dtype=torch.bfloat16)
+    split = ops.decode_split_plan(ctx, B, Hkv, Hq // Hkv)
+    fn = lambda: ops.paged_decode(q, kc, vc, bt, sl, Hq, Hkv, D, D ** -0.5, 0, None, split=split,  # noqa: E731
+                                  out=out, max_ctx=ctx)
+    t = time_it(fn)
+    by = B * ctx * Hkv * D * 2 * 2
+    print(f"decode B={B} ctx={ctx}: {t * 1e6:.1f} us  {by / t / 1e9:.0f} GB/s (KV read)")
+    return t
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--ctx", type=int, default=5000)
+    ap.add_argument("--check", action="store_true")
+    ap.add_argument("--D", type=int, default=128)
+    ap.add_argument("--so", default=None)
+    a = ap.parse_args()
+    if a.check:
+        prefill(700, 300, 16, 2, a.D, 64, check=True)
+        prefill(600, 600, 64, 8, a.D, 64, check=True)
+    prefill(a.ctx, a.ctx, 64, 8, a.D, 64)
+    prefill(a.ctx, 512, 64, 8, a.D, 64)
+    prefill(8192, 8192, 64, 8, a.D, 64)
+    decode(a.ctx, 64, 64, 8, a.D, 64)
+    decode(a.ctx, 8, 64, 8, a.D, 64)
+
+
+if __name__ == "__main__":
+    main()
