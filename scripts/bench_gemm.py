@@ -1,0 +1,48 @@
+"""Dense GEMM throughput at the Llama-3-70B TP1 prefill shapes (M tokens x
+[QKV, O, gate_up, down]) through F.linear (hipBLASLt), optionally with
+PyTorch TunableOp selecting among hipBLASLt/rocBLAS solutions.
+  python scripts/bench_gemm.py [--tunable] [--m 8192]"""
+import argparse
+import os
+import time
+
+import torch
+import torch.nn.functional as F
+
+
+def bench(M, N, K, iters=20):
+    x = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
+    w = torch.randn(N, K, device="cuda", dtype=torch.bfloat16)
+    for _ in range(3):
+        F.linear(x, w)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(iters):
+        F.linear(x, w)
+    torch.cuda.synchronize()
+    t = (time.perf_counter() - t0) / iters
+    return t, 2 * M * N * K / t / 1e12
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--tunable", action="store_true")
+    ap.add_argument("--m", type=int, nargs="*", default=[8192, 4096, 64])
+    a = ap.parse_args()
+    if a.tunable:
+        torch.cuda.tunable.enable(True)
+        torch.cuda.tunable.tuning_enable(True)
+        torch.cuda.tunable.set_filename(os.path.join("gpurun_out", "tunableop_results.csv"))
+    shapes = {"qkv": (10240, 8192), "o": (8192, 8192), "gate_up": (57344, 8192), "down": (8192, 28672),
+              "lm_head": (128256, 8192)}
+    tot_t = 0.0
+    for M in a.m:
+        for name, (N, K) in shapes.items():
+            t, tf = bench(M, N, K)
+            print(f"M={M:5d} {name:8s} N={N:6d} K={K:6d}: {t * 1e3:8.3f} ms {tf:7.1f} TF/s", flush=True)
+    if a.tunable:
+        torch.cuda.tunable.write_file()
+
+
+if __name__ == "__main__":
+    main()
