@@ -1,0 +1,300 @@
+// Multi-head latent attention (DeepSeek-V2/V3 MLA) over a paged
+// latent cache, in the weight-absorbed form: every query row carries per-head
+// 576-d queries [W_UK-absorbed q_nope (512) | roped q_pe (64)] against ONE
+// shared 576-d key per token [c_kv (512) | k_pe (64)]; the value is c_kv.
+// The same kernel serves decode (one row per sequence) and prefill (one row
+// per query token, row_len = position + 1) - MQA with a 128-head group.
+//
+// Grid (split, head group of 16, row); 256 threads = 4 waves cooperating on a
+// 64-key tile staged once in LDS (576 bf16 per key, rows padded to 1168 B so
+// 16-row ds_read_b128 are conflict-free):
+//   S^T[key][head] : wave w takes keys 16w..16w+15, 18 x mfma_16x16x32_bf16
+//                    (A = K rows from LDS, B = Q fragments in registers)
+//   softmax        : per-head max / sum exchanged through LDS (4 floats x 16
+//                    heads per wave), lazy O rescale (threshold 2^8)
+//   O[head][dim]   : wave w owns dims 128w..128w+127, 16 MFMAs per tile
+//                    (A = P[head][key] from LDS, B = c_kv^T via ds_read_b64_tr_b16)
+// The next tile is prefetched into registers while the current one computes.
+// nsplit > 1 writes unnormalised partials (O, max, sum in log2 units) merged
+// by mla_reduce_kernel.
+#include "llmd_common.h"
+
+using namespace llmd;
+
+namespace {
+
+constexpr int NT = 256;
+constexpr int DQK = 576, DV = 512;
+constexpr int ROWB = DQK * 2 + 16;       // padded LDS row bytes
+constexpr int KTILE = 64 * ROWB;         // 74,752 B
+constexpr int PIMG = 16 * 64 * 2;        // P[head][key] bf16
+constexpr int CPR = DQK / 8;             // 72 16-B chunks per key
+constexpr int LPT = 64 * CPR / NT;       // 18 chunks per thread per tile
+constexpr float NEG_INF = -__builtin_huge_valf();
+
+__device__ __forceinline__ int rowoff(int g) { return 4 * (g >> 1) + 8 * (g & 1); }
+
+__global__ __launch_bounds__(NT, 1) void mla_kernel(
+    const uint16_t* __restrict__ q, int64_t q_row_stride, const uint16_t* __restrict__ kc,
+    int64_t block_stride, int bs, const int* __restrict__ block_tables, int bt_stride,
+    const int* __restrict__ row_seq, const int* __restrict__ row_len, int H, float scale_log2,
+    int split_size, int nsplit, uint16_t* __restrict__ out, int64_t out_row_stride,
+    float* __restrict__ part_o, float* __restrict__ part_ml) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  char* ktile = smem;
+  char* pimg = smem + KTILE;
+  float* red = reinterpret_cast<float*>(pimg + PIMG);  // [2][4 waves][16 heads]
+
+  const int sp = blockIdx.x, hg = blockIdx.y, r = blockIdx.z;
+  const int len = row_len[r];
+  const int k0 = sp * split_size, k1 = min(len, k0 + split_size);
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, g = lane >> 4, c16 = lane & 15;
+  const int head = hg * 16 + c16;
+  const int* bt = block_tables + (int64_t)row_seq[r] * bt_stride;
+
+  float m = NEG_INF, l = 0.f;  // per head c16 (identical in every wave)
+  f32x4_t o[8];
+#pragma unroll
+  for (int n = 0; n < 8; ++n) o[n] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  if (k0 < k1) {
+    // Q fragments (B operand): lane = head c16, dims 32s + 8g .. +7
+    bf16x8_t qf[18];
+    const uint16_t* qr = q + (int64_t)r * q_row_stride + (int64_t)head * DQK;
+#pragma unroll
+    for (int s = 0; s < 18; ++s) {
+      u32x4_t v = {0, 0, 0, 0};
+      if (head < H) v = *reinterpret_cast<const u32x4_t*>(qr + 32 * s + 8 * g);
+      qf[s] = __builtin_bit_cast(bf16x8_t, v);
+    }
+    u32x4_t kr[LPT];
+    auto load_tile = [&](int ts) {
+#pragma unroll
+      for (int i = 0; i < LPT; ++i) {
+        const int idx = threadIdx.x + NT * i;
+        const int row = idx / CPR, ch = idx % CPR;
+        int key = ts + row;
+        key = key < k1 ? key : k1 - 1;
+        const int64_t off = (int64_t)bt[key / bs] * block_stride + (int64_t)(key % bs) * DQK + ch * 8;
+        kr[i] = *reinterpret_cast<const u32x4_t*>(kc + off);
+      }
+    };
+    load_tile(k0);
+    for (int ts = k0; ts < k1; ts += 64) {
+      __syncthreads();  // previous tile fully consumed
+#pragma unroll
+      for (int i = 0; i < LPT; ++i) {
+        const int idx = threadIdx.x + NT * i;
+        const int row = idx / CPR, ch = idx % CPR;
+        *reinterpret_cast<u32x4_t*>(ktile + row * ROWB + ch * 16) = kr[i];
+      }
+      __syncthreads();
+      if (ts + 64 < k1) load_tile(ts + 64);
+      // ---- S^T for keys 16w .. 16w+15
+      f32x4_t sc = {0.f, 0.f, 0.f, 0.f};
+      const char* krow = ktile + (16 * w + c16) * ROWB;
+#pragma unroll
+      for (int s = 0; s < 18; ++s) {
+        const bf16x8_t ka = *reinterpret_cast<const bf16x8_t*>(krow + 64 * s + 16 * g);
+        sc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ka, qf[s], sc, 0, 0, 0);
+      }
+      // rows of sc: keys 16w + 4g + i, column: head c16
+      float mx = NEG_INF;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int key = ts + 16 * w + 4 * g + i;
+        sc[i] = key < k1 ? sc[i] : NEG_INF;
+        mx = fmaxf(mx, sc[i]);
+      }
+      mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      if (g == 0) red[w * 16 + c16] = mx;
+      __syncthreads();
+      float tm = fmaxf(fmaxf(red[c16], red[16 + c16]), fmaxf(red[32 + c16], red[48 + c16]));
+      tm *= scale_log2;
+      const bool grow = tm > m + 8.f;
+      if (__ballot(grow) != 0) {  // wave-uniform; identical decision in all waves
+        const float mnew = fmaxf(m, tm);
+        const float alpha = (mnew == NEG_INF) ? 1.f : __builtin_amdgcn_exp2f(m - mnew);
+        l *= alpha;
+        m = mnew;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const float a = __shfl(alpha, 4 * g + i, 64);
+#pragma unroll
+          for (int n = 0; n < 8; ++n) o[n][i] *= a;
+        }
+      }
+      const float msub = (m == NEG_INF) ? 0.f : m;
+      float ps = 0.f;
+      uint16_t pb[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float p = __builtin_amdgcn_exp2f(fmaf(sc[i], scale_log2, -msub));
+        ps += p;
+        pb[i] = f2bf(p);
+      }
+      *reinterpret_cast<uint2*>(pimg + c16 * 128 + (16 * w + 4 * g) * 2) =
+          make_uint2((uint32_t)pb[0] | ((uint32_t)pb[1] << 16), (uint32_t)pb[2] | ((uint32_t)pb[3] << 16));
+      ps += __shfl_xor(ps, 16, 64);
+      ps += __shfl_xor(ps, 32, 64);
+      if (g == 0) red[64 + w * 16 + c16] = ps;
+      __syncthreads();
+      l += red[64 + c16] + red[80 + c16] + red[96 + c16] + red[112 + c16];
+      // ---- O[head][dim] += P[head][key] . V[key][dim], dims 128w ..
+      const int qq = c16 >> 2, pp = c16 & 3;
+#pragma unroll
+      for (int t2 = 0; t2 < 2; ++t2) {
+        const char* prow = pimg + c16 * 128 + (32 * t2 + rowoff(g)) * 2;
+        const uint2 plo = *reinterpret_cast<const uint2*>(prow);
+        const uint2 phi = *reinterpret_cast<const uint2*>(prow + 32);
+        const bf16x8_t pa = __builtin_bit_cast(bf16x8_t, u32x4_t{plo.x, plo.y, phi.x, phi.y});
+        const int r0 = 32 * t2 + rowoff(g) + qq;
+#pragma unroll
+        for (int n = 0; n < 8; ++n) {
+          const int colb = (128 * w + 16 * n + 4 * pp) * 2;
+          s16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+              (__attribute__((address_space(3))) s16x4_t*)(ktile + r0 * ROWB + colb));
+          s16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+              (__attribute__((address_space(3))) s16x4_t*)(ktile + (r0 + 16) * ROWB + colb));
+          const bf16x8_t vb = __builtin_bit_cast(
+              bf16x8_t, s16x8_t{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]});
+          o[n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pa, vb, o[n], 0, 0, 0);
+        }
+      }
+    }
+  }
+  // ---- epilogue: O rows are heads 4g + i (stats in lane 4g + i), columns dims
+  if (nsplit == 1) {
+    const float inv = l > 0.f ? 1.f / l : 0.f;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const float f = __shfl(inv, 4 * g + i, 64);
+      const int hh = hg * 16 + 4 * g + i;
+      if (hh < H) {
+        uint16_t* orow = out + (int64_t)r * out_row_stride + (int64_t)hh * DV + 128 * w;
+#pragma unroll
+        for (int n = 0; n < 8; ++n) orow[16 * n + c16] = f2bf(o[n][i] * f);
+      }
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int hh = hg * 16 + 4 * g + i;
+      if (hh < H) {
+        float* po = part_o + (((int64_t)r * H + hh) * nsplit + sp) * DV + 128 * w;
+#pragma unroll
+        for (int n = 0; n < 8; ++n) po[16 * n + c16] = o[n][i];
+      }
+    }
+    if (w == 0 && g == 0 && head < H) {
+      float* pm = part_ml + (((int64_t)r * H + head) * nsplit + sp) * 2;
+      pm[0] = m;
+      pm[1] = l;
+    }
+  }
+}
+
+__global__ __launch_bounds__(128) void mla_reduce_kernel(const float* __restrict__ part_o,
+                                                         const float* __restrict__ part_ml,
+                                                         const int* __restrict__ row_len, int H, int nsplit,
+                                                         int split_size, uint16_t* __restrict__ out,
+                                                         int64_t out_row_stride) {
+  const int hh = blockIdx.x, r = blockIdx.y;
+  const int len = row_len[r];
+  const int nact = min(nsplit, (len + split_size - 1) / split_size);
+  const int64_t base = ((int64_t)r * H + hh) * nsplit;
+  float M = NEG_INF;
+  for (int s = 0; s < nact; ++s) M = fmaxf(M, part_ml[(base + s) * 2]);
+  float den = 0.f;
+  for (int s = 0; s < nact; ++s) {
+    const float ms = part_ml[(base + s) * 2];
+    if (ms != NEG_INF) den += exp2f(ms - M) * part_ml[(base + s) * 2 + 1];
+  }
+  const float inv = den > 0.f ? 1.f / den : 0.f;
+  uint16_t* orow = out + (int64_t)r * out_row_stride + (int64_t)hh * DV;
+  for (int d = threadIdx.x; d < DV; d += 128) {
+    float acc = 0.f;
+    for (int s = 0; s < nact; ++s) {
+      const float ms = part_ml[(base + s) * 2];
+      if (ms != NEG_INF) acc += exp2f(ms - M) * part_o[(base + s) * DV + d];
+    }
+    orow[d] = f2bf(acc * inv);
+  }
+}
+
+}  // namespace
+
+extern "C" int llmd_mla_attention(const void* q, int64_t q_row_stride, const void* kc, int64_t block_stride,
+                                  int bs, const int* block_tables, int bt_stride, const int* row_seq,
+                                  const int* row_len, int R, int H, float scale, int split_size, int nsplit,
+                                  void* out, int64_t out_row_stride, float* part_o, float* part_ml,
+                                  hipStream_t st) {
+  if (R == 0) return 0;
+  if (split_size % 64 != 0 || nsplit < 1) return -1;
+  const size_t lds = KTILE + PIMG + 128 * sizeof(float);
+  static bool attr_done = false;
+  if (!attr_done) {
+    hipFuncSetAttribute((const void*)mla_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    attr_done = true;
+  }
+  const float scale_log2 = scale * 1.4426950408889634f;
+  dim3 grid(nsplit, (H + 15) / 16, R);
+  hipLaunchKernelGGL(mla_kernel, grid, dim3(NT), lds, st, (const uint16_t*)q, q_row_stride,
+                     (const uint16_t*)kc, block_stride, bs, block_tables, bt_stride, row_seq, row_len, H,
+                     scale_log2, split_size, nsplit, (uint16_t*)out, out_row_stride, part_o, part_ml);
+  if (nsplit > 1) {
+    hipLaunchKernelGGL(mla_reduce_kernel, dim3(H, R), dim3(128), 0, st, part_o, part_ml, row_len, H, nsplit,
+                       split_size, (uint16_t*)out, out_row_stride);
+  }
+  return (int)hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// MLA rope + latent-cache write. One workgroup per token:
+//   q_lat[t, h, 512:576] = rope(q[t, h, 128:192])   (GPT-J interleaved pairs)
+//   cache[slot] = [kv_c[t] (512) | rope(k_pe[t]) (64)]
+namespace {
+__global__ __launch_bounds__(256) void mla_rope_cache_kernel(
+    const uint16_t* __restrict__ q, int64_t q_stride, uint16_t* __restrict__ q_lat, int64_t ql_stride,
+    const uint16_t* __restrict__ kv_c, int64_t kvc_stride, const uint16_t* __restrict__ k_pe,
+    int64_t kpe_stride, const int64_t* __restrict__ positions, const float* __restrict__ cos_sin, int H,
+    const int64_t* __restrict__ slots, uint16_t* __restrict__ cache, int64_t block_stride, int bs) {
+  const int t = blockIdx.x;
+  const float* cs = cos_sin + positions[t] * 64;
+  // q_pe: H heads x 32 pairs
+  for (int i = threadIdx.x; i < H * 32; i += 256) {
+    const int h = i >> 5, p = i & 31;
+    const uint16_t* src = q + (int64_t)t * q_stride + h * 192 + 128 + 2 * p;
+    const float x0 = bf2f(src[0]), x1 = bf2f(src[1]);
+    const float c = cs[p], s = cs[32 + p];
+    uint16_t* dst = q_lat + (int64_t)t * ql_stride + h * 576 + 512 + 2 * p;
+    dst[0] = f2bf(x0 * c - x1 * s);
+    dst[1] = f2bf(x0 * s + x1 * c);
+  }
+  const int64_t slot = slots[t];
+  if (slot < 0) return;
+  uint16_t* row = cache + (slot / bs) * block_stride + (slot % bs) * 576;
+  for (int i = threadIdx.x; i < 512 / 8; i += 256)
+    reinterpret_cast<u32x4_t*>(row)[i] = reinterpret_cast<const u32x4_t*>(kv_c + (int64_t)t * kvc_stride)[i];
+  if (threadIdx.x < 32) {
+    const int p = threadIdx.x;
+    const uint16_t* src = k_pe + (int64_t)t * kpe_stride + 2 * p;
+    const float x0 = bf2f(src[0]), x1 = bf2f(src[1]);
+    const float c = cs[p], s = cs[32 + p];
+    row[512 + 2 * p] = f2bf(x0 * c - x1 * s);
+    row[512 + 2 * p + 1] = f2bf(x0 * s + x1 * c);
+  }
+}
+}  // namespace
+
+extern "C" int llmd_mla_rope_cache(const void* q, int64_t q_stride, void* q_lat, int64_t ql_stride, const void* kv_c,
+                                   int64_t kvc_stride, const void* k_pe, int64_t kpe_stride, const int64_t* positions,
+                                   const float* cos_sin, int T, int H, const int64_t* slots, void* cache,
+                                   int64_t block_stride, int bs, hipStream_t st) {
+  if (T == 0) return 0;
+  hipLaunchKernelGGL(mla_rope_cache_kernel, dim3(T), dim3(256), 0, st, (const uint16_t*)q, q_stride,
+                     (uint16_t*)q_lat, ql_stride, (const uint16_t*)kv_c, kvc_stride, (const uint16_t*)k_pe,
+                     kpe_stride, positions, cos_sin, H, slots, (uint16_t*)cache, block_stride, bs);
+  return (int)hipGetLastError();
+}

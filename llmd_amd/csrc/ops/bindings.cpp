@@ -36,6 +36,10 @@ int llmd_kvx_copy_blocks(void*, const void*, int64_t, int64_t, const int*, int, 
 int llmd_kvx_ipc_export(const void*, void*, int64_t*);
 int llmd_kvx_ipc_open(const void*, void**);
 int llmd_kvx_ipc_close(void*);
+int llmd_mla_attention(const void*, int64_t, const void*, int64_t, int, const int*, int, const int*,
+                       const int*, int, int, float, int, int, void*, int64_t, float*, float*, hipStream_t);
+int llmd_mla_rope_cache(const void*, int64_t, void*, int64_t, const void*, int64_t, const void*, int64_t,
+                        const int64_t*, const float*, int, int, const int64_t*, void*, int64_t, int, hipStream_t);
 int llmd_vmm_granularity(int, size_t*);
 int llmd_vmm_alloc(int, size_t, int, void**, uint64_t*);
 int llmd_vmm_export_fd(uint64_t, int*);
@@ -176,6 +180,57 @@ void paged_decode(torch::Tensor out, torch::Tensor q, torch::Tensor k_cache, tor
                              out.stride(0), nsplit > 1 ? part_o.data_ptr<float>() : nullptr,
                              nsplit > 1 ? part_ml.data_ptr<float>() : nullptr, cur_stream());
   TORCH_CHECK(rc == 0, "paged_decode: unsupported head dim");
+}
+
+// MLA (absorbed form): q [R, H*576], cache [blocks, bs, 576] (block stride free),
+// out [R, H*512]; row r attends to keys [0, row_len[r]) of sequence row_seq[r].
+void mla_attention(torch::Tensor out, torch::Tensor q, torch::Tensor cache, torch::Tensor block_tables,
+                   torch::Tensor row_seq, torch::Tensor row_len, int64_t H, double scale, int64_t split_size,
+                   int64_t nsplit, torch::Tensor part_o, torch::Tensor part_ml) {
+  const c10::hip::OptionalHIPGuard device_guard(dev_of(out));
+  CHECK_CUDA(q); CHECK_BF16(q); CHECK_BF16(out); CHECK_BF16(cache); CHECK_INNER(q); CHECK_INNER(out);
+  CHECK_DT(block_tables, at::kInt); CHECK_DT(row_seq, at::kInt); CHECK_DT(row_len, at::kInt);
+  TORCH_CHECK(cache.dim() == 3 && cache.size(2) == 576 && cache.stride(2) == 1 && cache.stride(1) == 576,
+              "mla cache [blocks, bs, 576] with contiguous rows");
+  TORCH_CHECK(block_tables.dim() == 2 && block_tables.stride(1) == 1, "block_tables 2-D");
+  const int R = q.size(0);
+  TORCH_CHECK(row_seq.numel() == R && row_len.numel() == R, "mla: rows mismatch");
+  TORCH_CHECK(q.size(1) >= H * 576 && out.size(0) >= R && out.size(1) >= H * 512, "mla: widths");
+  TORCH_CHECK(q.stride(0) % 8 == 0 && out.stride(0) % 8 == 0, "mla: 16-B aligned rows");
+  TORCH_CHECK(split_size % 64 == 0 && split_size > 0 && nsplit >= 1, "mla: split");
+  if (nsplit > 1) {
+    CHECK_DT(part_o, at::kFloat); CHECK_DT(part_ml, at::kFloat);
+    TORCH_CHECK(part_o.numel() >= (int64_t)R * H * nsplit * 512 && part_ml.numel() >= (int64_t)R * H * nsplit * 2,
+                "mla workspace too small");
+  }
+  int rc = llmd_mla_attention(q.data_ptr(), q.stride(0), cache.data_ptr(), cache.stride(0), cache.size(1),
+                              block_tables.data_ptr<int>(), block_tables.stride(0), row_seq.data_ptr<int>(),
+                              row_len.data_ptr<int>(), R, H, (float)scale, split_size, nsplit, out.data_ptr(),
+                              out.stride(0), nsplit > 1 ? part_o.data_ptr<float>() : nullptr,
+                              nsplit > 1 ? part_ml.data_ptr<float>() : nullptr, cur_stream());
+  TORCH_CHECK(rc == 0, "mla_attention failed: ", rc);
+}
+
+void mla_rope_cache(torch::Tensor q, torch::Tensor q_lat, torch::Tensor kv_c, torch::Tensor k_pe,
+                    torch::Tensor positions, torch::Tensor cos_sin, int64_t H, torch::Tensor slots,
+                    torch::Tensor cache) {
+  const c10::hip::OptionalHIPGuard device_guard(dev_of(q));
+  CHECK_CUDA(q); CHECK_BF16(q); CHECK_BF16(q_lat); CHECK_BF16(kv_c); CHECK_BF16(k_pe); CHECK_BF16(cache);
+  CHECK_INNER(q); CHECK_INNER(q_lat); CHECK_INNER(kv_c); CHECK_INNER(k_pe);
+  CHECK_DT(positions, at::kLong); CHECK_DT(slots, at::kLong); CHECK_DT(cos_sin, at::kFloat);
+  const int T = q.size(0);
+  TORCH_CHECK(q.size(1) >= H * 192 && q_lat.size(0) >= T && q_lat.size(1) >= H * 576, "mla_rope: q widths");
+  TORCH_CHECK(kv_c.size(0) >= T && kv_c.size(1) == 512 && k_pe.size(0) >= T && k_pe.size(1) == 64,
+              "mla_rope: kv_c [T,512], k_pe [T,64]");
+  TORCH_CHECK(kv_c.stride(0) % 8 == 0, "mla_rope: 16-B aligned kv_c rows");
+  TORCH_CHECK(positions.numel() >= T && slots.numel() >= T, "mla_rope: positions/slots");
+  TORCH_CHECK(cos_sin.dim() == 2 && cos_sin.size(1) == 64 && cos_sin.is_contiguous(), "mla_rope: cos_sin [P,64]");
+  TORCH_CHECK(cache.dim() == 3 && cache.size(2) == 576 && cache.stride(1) == 576, "mla_rope: cache [blocks,bs,576]");
+  int rc = llmd_mla_rope_cache(q.data_ptr(), q.stride(0), q_lat.data_ptr(), q_lat.stride(0), kv_c.data_ptr(),
+                               kv_c.stride(0), k_pe.data_ptr(), k_pe.stride(0), positions.data_ptr<int64_t>(),
+                               cos_sin.data_ptr<float>(), T, H, slots.data_ptr<int64_t>(), cache.data_ptr(),
+                               cache.stride(0), cache.size(1), cur_stream());
+  TORCH_CHECK(rc == 0, "mla_rope_cache failed: ", rc);
 }
 
 void paged_prefill(torch::Tensor out, torch::Tensor q, torch::Tensor k_cache,
@@ -429,6 +484,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("kvx_ipc_export", &kvx_ipc_export);
   m.def("kvx_ipc_open", &kvx_ipc_open);
   m.def("kvx_ipc_close", &kvx_ipc_close);
+  m.def("mla_attention", &mla_attention);
+  m.def("mla_rope_cache", &mla_rope_cache);
   m.def("vmm_granularity", &vmm_granularity);
   m.def("vmm_pool", &vmm_pool);
   m.def("vmm_import", &vmm_import);

@@ -33,6 +33,13 @@ class AttnMeta:
     p_ctx_len: Optional[torch.Tensor] = None
     p_items: Optional[torch.Tensor] = None         # [n, 2] int32
     p_items_per_window: Optional[dict] = None
+    # MLA (one attention row per decode sequence / prefill token)
+    mla_d_rows: Optional[torch.Tensor] = None      # [Bd] int32 = arange (row -> d_block_tables row)
+    mla_split: Optional[tuple] = None              # fixed (split_size, nsplit) under graph capture
+    mla_workspace: Optional[tuple] = None
+    p_row_seq: Optional[torch.Tensor] = None       # [Tp] int32 prefill token -> p_block_tables row
+    p_row_len: Optional[torch.Tensor] = None       # [Tp] int32 keys visible (= position + 1)
+    p_max_ctx: int = 0
 
     @property
     def has_prefill(self) -> bool:

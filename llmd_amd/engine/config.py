@@ -48,6 +48,12 @@ class ModelConfig:
     first_k_dense_replace: int = 0
     router_aux_bias: bool = False
     swiglu_limit: float = 7.0
+    # DeepSeek routing
+    n_group: int = 1
+    topk_group: int = 1
+    routed_scaling_factor: float = 1.0
+    norm_topk_prob: bool = False
+    scoring_func: str = "softmax"
     # MLA (DeepSeek)
     q_lora_rank: Optional[int] = None
     kv_lora_rank: int = 0
@@ -99,6 +105,8 @@ class ModelConfig:
             kw["num_local_experts"] = d["num_experts"]
         if "n_routed_experts" in d:
             kw["num_local_experts"] = d["n_routed_experts"]
+        if d.get("model_type") in ("deepseek_v3", "deepseek_v2"):
+            kw["model_type"] = "deepseek"
         if d.get("model_type") == "gpt_oss":
             kw.setdefault("moe_intermediate_size", d.get("intermediate_size", 0))
             kw["attention_sinks"] = True
@@ -151,6 +159,25 @@ _register(ModelConfig(model_type="gpt_oss", name="gpt-oss-20b", hidden_size=2880
                       layer_types=["sliding_attention", "full_attention"] * 12, attention_sinks=True,
                       attention_bias=True, bos_token_id=199998, eos_token_id=[200002, 199999]),
           "openai/gpt-oss-20b")
+_DSV3_ROPE = {"rope_type": "yarn", "factor": 40.0, "beta_fast": 32.0, "beta_slow": 1.0, "mscale": 1.0,
+              "mscale_all_dim": 1.0, "original_max_position_embeddings": 4096}
+_register(ModelConfig(model_type="deepseek", name="deepseek-v3", hidden_size=7168, intermediate_size=18432,
+                      moe_intermediate_size=2048, num_hidden_layers=61, num_attention_heads=128,
+                      num_key_value_heads=128, vocab_size=129280, max_position_embeddings=163840,
+                      rope_theta=10000.0, rope_scaling=_DSV3_ROPE, rms_norm_eps=1e-6, num_local_experts=256,
+                      num_experts_per_tok=8, n_shared_experts=1, first_k_dense_replace=3, n_group=8, topk_group=4,
+                      routed_scaling_factor=2.5, norm_topk_prob=True, scoring_func="sigmoid", router_aux_bias=True,
+                      q_lora_rank=1536, kv_lora_rank=512, qk_nope_head_dim=128, qk_rope_head_dim=64,
+                      v_head_dim=128, head_dim=192, bos_token_id=0, eos_token_id=1),
+          "deepseek-ai/DeepSeek-V3", "deepseek-ai/DeepSeek-R1", "deepseek-ai/DeepSeek-R1-0528", "deepseek-r1")
+_register(ModelConfig(model_type="deepseek", name="deepseek-v2-lite", hidden_size=2048, intermediate_size=10944,
+                      moe_intermediate_size=1408, num_hidden_layers=27, num_attention_heads=16,
+                      num_key_value_heads=16, vocab_size=102400, max_position_embeddings=163840,
+                      rope_theta=10000.0, rope_scaling=dict(_DSV3_ROPE, mscale=0.707, mscale_all_dim=0.707),
+                      rms_norm_eps=1e-6, num_local_experts=64, num_experts_per_tok=6, n_shared_experts=2,
+                      first_k_dense_replace=1, q_lora_rank=None, kv_lora_rank=512, qk_nope_head_dim=128,
+                      qk_rope_head_dim=64, v_head_dim=128, head_dim=192, bos_token_id=100000,
+                      eos_token_id=100001), "deepseek-ai/DeepSeek-V2-Lite", "deepseek-ai/DeepSeek-V2-Lite-Chat")
 # tiny configs (CPU CI, smoke, GPU unit tests)
 _register(ModelConfig(model_type="llama", name="tiny-llama", hidden_size=256, intermediate_size=512,
                       num_hidden_layers=2, num_attention_heads=4, num_key_value_heads=2, head_dim=64,
@@ -166,6 +193,16 @@ _register(ModelConfig(model_type="gpt_oss", name="tiny-gpt-oss", hidden_size=256
                       num_local_experts=8, num_experts_per_tok=2, sliding_window=16,
                       layer_types=["sliding_attention", "full_attention"], attention_sinks=True,
                       attention_bias=True, bos_token_id=1, eos_token_id=2))
+
+
+_register(ModelConfig(model_type="deepseek", name="tiny-deepseek", hidden_size=256, intermediate_size=512,
+                      moe_intermediate_size=128, num_hidden_layers=3, num_attention_heads=20,
+                      num_key_value_heads=20, vocab_size=512, max_position_embeddings=4096, rope_theta=10000.0,
+                      rope_scaling=dict(_DSV3_ROPE, factor=4.0), rms_norm_eps=1e-6, num_local_experts=16,
+                      num_experts_per_tok=4, n_shared_experts=1, first_k_dense_replace=1, n_group=4,
+                      topk_group=2, routed_scaling_factor=2.5, norm_topk_prob=True, scoring_func="sigmoid",
+                      router_aux_bias=True, q_lora_rank=96, kv_lora_rank=512, qk_nope_head_dim=128,
+                      qk_rope_head_dim=64, v_head_dim=128, head_dim=192, bos_token_id=1, eos_token_id=2))
 
 
 def get_model_config(name_or_path: str) -> ModelConfig:

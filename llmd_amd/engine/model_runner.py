@@ -70,6 +70,10 @@ class ModelRunner:
         attn = self.model.attention_layers()
         self.Hkv, self.D, self.L = attn[0].Hkv, attn[0].D, len(attn)
         self.Hq = attn[0].Hq
+        # cache geometry per layer: (planes, heads, dim) - K/V planes of GQA heads,
+        # or one latent row per token for MLA
+        self.kv_spec = self.model.kv_spec() if hasattr(self.model, "kv_spec") else (2, self.Hkv, self.D)
+        self.is_mla = bool(getattr(self.model, "needs_mla_rows", False))
         self.kv = None
         self.num_blocks = 0
         self.graphs: dict[int, tuple] = {}
@@ -80,7 +84,8 @@ class ModelRunner:
 
     # ------------------------------------------------------------ KV cache
     def block_bytes(self) -> int:
-        return self.L * 2 * self.Hkv * self.bs * self.D * 2
+        planes, heads, dim = self.kv_spec
+        return self.L * planes * heads * self.bs * dim * 2
 
     def _wants_vmm(self) -> bool:
         """KV producers export their pool to other processes (kvx); a single
@@ -91,7 +96,8 @@ class ModelRunner:
                 and os.environ.get("LLMD_KV_VMM", "1") != "0")
 
     def _alloc_cache(self, num_blocks: int, scratch: bool = False) -> torch.Tensor:
-        shape = (num_blocks, self.L, 2, self.Hkv, self.bs, self.D)
+        planes, heads, dim = self.kv_spec
+        shape = (num_blocks, self.L, planes, heads, self.bs, dim)
         self.vmm = None
         if not scratch and self._wants_vmm():
             C = ops.native()
@@ -105,10 +111,32 @@ class ModelRunner:
             self.vmm = {"fds": list(fds), "chunk": chunk, "n": n, "pool": pool}
         else:
             kv = torch.empty(shape, dtype=torch.bfloat16, device=self.device)
-        for i, a in enumerate(self.model.attention_layers()):
-            a.k_cache = kv[:, i, 0]
-            a.v_cache = kv[:, i, 1]
+        self._bind(kv)
         return kv
+
+    def _bind(self, kv: Optional[torch.Tensor]):
+        for i, a in enumerate(self.model.attention_layers()):
+            if hasattr(a, "bind_cache"):
+                a.bind_cache(kv[:, i]) if kv is not None else setattr(a, "cache", None)
+            else:
+                a.k_cache = kv[:, i, 0] if kv is not None else None
+                a.v_cache = kv[:, i, 1] if kv is not None else None
+
+    def _mla_rows(self, meta: AttnMeta, nd: int, p_ql, p_ctx):
+        """Row metadata of the latent-attention kernel (decode rows + one row per
+        prefill token with its causal key count)."""
+        dev = self.device
+        if nd:
+            meta.mla_d_rows = torch.arange(nd, dtype=torch.int32).to(dev, non_blocking=True)
+        if p_ql:
+            ql = np.asarray(p_ql, dtype=np.int64)
+            ctx = np.asarray(p_ctx, dtype=np.int64)
+            seq = np.repeat(np.arange(len(ql), dtype=np.int32), ql)
+            first = np.repeat(ctx - ql, ql)
+            within = np.arange(int(ql.sum()), dtype=np.int64) - np.repeat(np.cumsum(ql) - ql, ql)
+            meta.p_row_seq = torch.from_numpy(seq).to(dev, non_blocking=True)
+            meta.p_row_len = torch.from_numpy((first + within + 1).astype(np.int32)).to(dev, non_blocking=True)
+            meta.p_max_ctx = int(ctx.max())
 
     @torch.no_grad()
     def profile_and_allocate(self) -> int:
@@ -129,8 +157,7 @@ class ModelRunner:
             torch.cuda.synchronize()
             act_peak = torch.cuda.max_memory_allocated() - base
             self.kv = None
-            for a in self.model.attention_layers():
-                a.k_cache = a.v_cache = None
+            self._bind(None)
             torch.cuda.empty_cache()
             free, total = torch.cuda.mem_get_info()
             if cc.kv_cache_memory_bytes:
@@ -165,6 +192,8 @@ class ModelRunner:
                         p_q_len=torch.tensor(ql, dtype=torch.int32, device=self.device),
                         p_ctx_len=torch.tensor(ql, dtype=torch.int32, device=self.device))
         meta.p_items = self._items(ql, ql)
+        if self.is_mla:
+            self._mla_rows(meta, 0, ql, ql)
         h = self.model(ids, meta)
         self.model.compute_logits(h[: min(len(ql), self.cfg.sched.max_num_seqs)])
 
@@ -323,6 +352,8 @@ class ModelRunner:
             meta.p_q_len = torch.tensor(p_ql, dtype=torch.int32).to(dev, non_blocking=True)
             meta.p_ctx_len = torch.tensor(p_ctx, dtype=torch.int32).to(dev, non_blocking=True)
             meta.p_items = self._items(p_ql, p_ctx)
+        if self.is_mla:
+            self._mla_rows(meta, nd, p_ql, p_ctx)
         return self.model(hd[0], meta)
 
     # ------------------------------------------------------------ graphs
@@ -358,12 +389,20 @@ class ModelRunner:
         self.g_len = torch.ones(M, dtype=torch.int32, device=dev)
         self.g_ws = (torch.empty(M * self.Hq * nsplit * self.D, dtype=torch.float32, device=dev),
                      torch.empty(M * self.Hq * nsplit * 2, dtype=torch.float32, device=dev))
+        if self.is_mla:  # fixed per-bucket latent-attention split plans + one shared workspace
+            self.g_rows = torch.arange(M, dtype=torch.int32, device=dev)
+            self.mla_plans = {B: ops.mla_split_plan(self.max_model_len, B, self.Hq) for B in buckets}
+            need = max(B * p[1] for B, p in self.mla_plans.items())
+            self.g_mla_ws = (torch.empty(need * self.Hq * 512, dtype=torch.float32, device=dev),
+                             torch.empty(need * self.Hq * 2, dtype=torch.float32, device=dev))
         pool = torch.cuda.graph_pool_handle()
         t0 = time.time()
         for B in reversed(buckets):
             meta = AttnMeta(num_tokens=B, positions=self.g_pos[:B], slot_mapping=self.g_slots[:B],
                             num_decode=B, d_block_tables=self.g_bt[:B], d_seq_lens=self.g_len[:B],
                             d_split=self.graph_split, d_workspace=self.g_ws, d_max_ctx=self.max_model_len)
+            if self.is_mla:
+                meta.mla_d_rows, meta.mla_split, meta.mla_workspace = self.g_rows[:B], self.mla_plans[B], self.g_mla_ws
             s = torch.cuda.Stream()
             s.wait_stream(torch.cuda.current_stream())
             with torch.cuda.stream(s):

@@ -14,6 +14,10 @@ def model_class(cfg: ModelConfig):
         from .gpt_oss import GptOssForCausalLM
 
         return GptOssForCausalLM
+    if t in ("deepseek", "deepseek_v3", "deepseek_v2"):
+        from .deepseek import DeepseekForCausalLM
+
+        return DeepseekForCausalLM
     if t in ("mixtral", "qwen3_moe"):
         from .moe_llama import MoELlamaForCausalLM
 

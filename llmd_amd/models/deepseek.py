@@ -1,0 +1,256 @@
+"""DeepSeek-V3 / R1 / V2-Lite: multi-head latent attention + fine-grained MoE
+with shared experts (the reference's wide-EP model, guides/wide-ep-lws).
+
+Attention (MLA, weight-absorbed):
+  q = q_b(norm(q_a(x))) [T, H, 128 nope | 64 rope]        (q_proj when q_lora_rank is None)
+  [c_kv | k_pe] = kv_a(x);  c_kv = norm(c_kv)              512 + 64, one "head"
+  cache[slot] = [c_kv | rope(k_pe)]                         576 bf16 per token per layer
+  q_lat = [q_nope @ W_UK | rope(q_pe)]  [T, H, 576]         (W_UK from kv_b_proj)
+  o_lat = softmax(q_lat . cache^T * scale) . c_kv           csrc/ops/attn_mla.hip
+  out = o_proj(o_lat @ W_UV^T)
+The latent cache is 1152 B/token/layer (vs 32 KiB for the un-absorbed K/V of
+128 heads), which is what makes 128-head decode bandwidth-feasible.
+
+MoE: sigmoid (V3) or softmax (V2) router with grouped top-k and score
+correction bias (selection only), renormalised top-k weights x
+routed_scaling_factor; routed experts on the grouped MFMA GEMM, shared
+experts as a dense MLP. Under TP the experts are sharded expert-parallel over
+the TP group (tokens are replicated), the shared expert is TP-sharded, and
+ONE all-reduce per layer sums both.
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn.functional as F
+
+from llmd_amd import ops
+from llmd_amd.engine.attn_meta import AttnMeta
+from llmd_amd.engine.config import ModelConfig
+from llmd_amd.ops.reference import yarn_softmax_mscale
+from llmd_amd.parallel.comm import tp_all_reduce
+from llmd_amd.parallel.state import get_state
+
+from .layers import ColumnLinear, LMHead, RMSNorm, RowLinear, VocabEmbedding, _init_weight
+from .llama import LlamaMLP
+
+KV_LORA, NOPE, ROPE, VDIM = 512, 128, 64, 128
+
+
+class MLAAttention(torch.nn.Module):
+    is_mla = True
+
+    def __init__(self, cfg: ModelConfig, idx: int, cos_sin: torch.Tensor, device):
+        super().__init__()
+        if (cfg.kv_lora_rank, cfg.qk_nope_head_dim, cfg.qk_rope_head_dim, cfg.v_head_dim) != (KV_LORA, NOPE, ROPE,
+                                                                                              VDIM):
+            raise ValueError("MLA kernels are built for kv_lora 512 / nope 128 / rope 64 / v 128")
+        st = get_state()
+        tp = st.tp_size
+        Ht = cfg.num_attention_heads
+        assert Ht % tp == 0
+        self.H_total, self.H = Ht, Ht // tp
+        d = cfg.hidden_size
+        self.layer_idx = idx
+        self.q_lora = cfg.q_lora_rank
+        if self.q_lora:
+            self.q_a = ColumnLinear(d, self.q_lora, shard=False, device=device)
+            self.q_a_norm = RMSNorm(self.q_lora, cfg.rms_norm_eps, device)
+            self.q_b = ColumnLinear(self.q_lora, Ht * (NOPE + ROPE), device=device)
+        else:
+            self.q_proj = ColumnLinear(d, Ht * (NOPE + ROPE), device=device)
+        self.kv_a = ColumnLinear(d, KV_LORA + ROPE, shard=False, device=device)
+        self.kv_a_norm = RMSNorm(KV_LORA, cfg.rms_norm_eps, device)
+        # kv_b_proj rows of this rank's heads: per head [128 k_nope rows | 128 v rows] x 512
+        self.kv_b = torch.nn.Parameter(_init_weight(torch.empty(self.H * (NOPE + VDIM), KV_LORA, device=device,
+                                                                dtype=torch.bfloat16), 0.02), requires_grad=False)
+        self.o_proj = RowLinear(Ht * VDIM, d, device=device)
+        self.scale = (NOPE + ROPE) ** -0.5 * yarn_softmax_mscale(cfg.rope_scaling)
+        self.cos_sin = cos_sin
+        self.cache = None
+        # attributes the runner reads for generic bookkeeping
+        self.Hq, self.Hkv, self.D, self.window, self.sinks = self.H, 1, KV_LORA + ROPE, 0, None
+
+    def bind_cache(self, kv_layer: torch.Tensor):
+        """kv_layer [blocks, 1, 1, bs, 576] -> [blocks, bs, 576] view."""
+        self.cache = kv_layer[:, 0, 0]
+
+    def w_uk(self):
+        return self.kv_b.view(self.H, NOPE + VDIM, KV_LORA)[:, :NOPE]            # [H, 128, 512]
+
+    def w_uv_t(self):
+        return self.kv_b.view(self.H, NOPE + VDIM, KV_LORA)[:, NOPE:].transpose(1, 2)  # [H, 512, 128]
+
+    def forward(self, x: torch.Tensor, meta: AttnMeta) -> torch.Tensor:
+        T, H = x.shape[0], self.H
+        q = self.q_b(self.q_a_norm(self.q_a(x))) if self.q_lora else self.q_proj(x)   # [T, H*192]
+        kv = self.kv_a(x)                                                              # [T, 576]
+        kv_c = self.kv_a_norm(kv[:, :KV_LORA])
+        q_lat = torch.empty(T, H * (KV_LORA + ROPE), dtype=x.dtype, device=x.device)
+        ops.mla_rope_cache(q, q_lat, kv_c, kv[:, KV_LORA:], meta.positions, self.cos_sin, H,
+                           meta.slot_mapping, self.cache)
+        qn = q.view(T, H, NOPE + ROPE)[:, :, :NOPE].transpose(0, 1)                    # [H, T, 128]
+        q_lat.view(T, H, KV_LORA + ROPE)[:, :, :KV_LORA].copy_(torch.bmm(qn, self.w_uk()).transpose(0, 1))
+        o_lat = torch.empty(T, H * KV_LORA, dtype=x.dtype, device=x.device)
+        nd = meta.num_decode
+        if nd:
+            ops.mla_attention(q_lat[:nd], self.cache, meta.d_block_tables, meta.mla_d_rows, meta.d_seq_lens, H,
+                              self.scale, max_len=meta.d_max_ctx, split=meta.mla_split, out=o_lat[:nd],
+                              workspace=meta.mla_workspace)
+        if meta.num_prefill_tokens:
+            ops.mla_attention(q_lat[nd:], self.cache, meta.p_block_tables, meta.p_row_seq, meta.p_row_len, H,
+                              self.scale, max_len=meta.p_max_ctx, out=o_lat[nd:])
+        o = torch.bmm(o_lat.view(T, H, KV_LORA).transpose(0, 1), self.w_uv_t())          # [H, T, 128]
+        return self.o_proj(o.transpose(0, 1).reshape(T, H * VDIM))
+
+
+class DeepseekMoE(torch.nn.Module):
+    def __init__(self, cfg: ModelConfig, device):
+        super().__init__()
+        st = get_state()
+        self.tp, self.rank = st.tp_size, st.tp_rank
+        E, d, Fh = cfg.num_local_experts, cfg.hidden_size, cfg.moe_intermediate_size
+        if E % self.tp:
+            raise ValueError(f"{E} experts do not split over TP={self.tp}")
+        self.E, self.E_local, self.k = E, E // self.tp, cfg.num_experts_per_tok
+        self.lo = self.rank * self.E_local
+        self.cfg = cfg
+        dt = torch.bfloat16
+        self.gate = torch.nn.Parameter(_init_weight(torch.empty(E, d, device=device, dtype=dt), 0.02),
+                                       requires_grad=False)
+        self.bias = torch.nn.Parameter(torch.zeros(E, device=device, dtype=torch.float32),
+                                       requires_grad=False) if cfg.router_aux_bias else None
+        self.w1 = torch.nn.Parameter(_init_weight(torch.empty(self.E_local, 2 * Fh, d, device=device, dtype=dt),
+                                                  0.02), requires_grad=False)
+        self.w2 = torch.nn.Parameter(_init_weight(torch.empty(self.E_local, d, Fh, device=device, dtype=dt),
+                                                  0.02), requires_grad=False)
+        self.shared = None
+        if cfg.n_shared_experts:
+            self.shared = LlamaMLP(_shared_cfg(cfg), device)
+            self.shared.down.reduce = False  # summed with the routed output in one all-reduce
+
+    def forward(self, x):
+        cfg = self.cfg
+        logits = F.linear(x, self.gate).float()
+        ids, w = ops.moe_topk(logits, self.k, scoring=1 if cfg.scoring_func == "sigmoid" else 0, bias=self.bias,
+                              n_group=cfg.n_group, topk_group=cfg.topk_group, renorm=cfg.norm_topk_prob,
+                              routed_scale=cfg.routed_scaling_factor)
+        if self.tp > 1:
+            local = (ids >= self.lo) & (ids < self.lo + self.E_local)
+            ids = torch.where(local, ids - self.lo, torch.full_like(ids, -1))
+            w = torch.where(local, w, torch.zeros_like(w))
+        y = ops.moe_experts(x, ids, w, self.w1, self.w2, ops.ACT_SILU)
+        if self.shared is not None:
+            y = y + self.shared(x)
+        return tp_all_reduce(y) if self.tp > 1 else y
+
+
+def _shared_cfg(cfg: ModelConfig) -> ModelConfig:
+    import dataclasses
+
+    return dataclasses.replace(cfg, intermediate_size=cfg.moe_intermediate_size * cfg.n_shared_experts)
+
+
+class DeepseekDecoderLayer(torch.nn.Module):
+    def __init__(self, cfg: ModelConfig, idx: int, cos_sin, device):
+        super().__init__()
+        d = cfg.hidden_size
+        self.input_layernorm = RMSNorm(d, cfg.rms_norm_eps, device)
+        self.attn = MLAAttention(cfg, idx, cos_sin, device)
+        self.post_attention_layernorm = RMSNorm(d, cfg.rms_norm_eps, device)
+        self.is_moe = cfg.is_moe and idx >= cfg.first_k_dense_replace
+        self.mlp = DeepseekMoE(cfg, device) if self.is_moe else LlamaMLP(cfg, device)
+
+    def forward(self, x, residual, meta: AttnMeta):
+        if residual is None:
+            residual = x.clone()
+            x = self.input_layernorm(x)
+        else:
+            x, residual = self.input_layernorm(x, residual)
+        x = self.attn(x, meta)
+        x, residual = self.post_attention_layernorm(x, residual)
+        return self.mlp(x), residual
+
+
+class DeepseekForCausalLM(torch.nn.Module):
+    needs_mla_rows = True
+
+    def __init__(self, cfg: ModelConfig, device="cuda", max_pos: int = 32768):
+        super().__init__()
+        self.cfg = cfg
+        self.register_buffer("cos_sin", ops.rope_cos_sin(ROPE, max_pos, cfg.rope_theta, cfg.rope_scaling,
+                                                         device=device), persistent=False)
+        self.embed = VocabEmbedding(cfg.vocab_size, cfg.hidden_size, device)
+        self.layers = torch.nn.ModuleList(
+            [DeepseekDecoderLayer(cfg, i, self.cos_sin, device) for i in range(cfg.num_hidden_layers)])
+        self.norm = RMSNorm(cfg.hidden_size, cfg.rms_norm_eps, device)
+        self.lm_head = LMHead(cfg.vocab_size, cfg.hidden_size, device,
+                              tied=self.embed if cfg.tie_word_embeddings else None)
+
+    def attention_layers(self):
+        return [layer.attn for layer in self.layers]
+
+    def kv_spec(self) -> tuple[int, int, int]:
+        return 1, 1, KV_LORA + ROPE  # (planes, heads, dim): one latent row per token
+
+    @torch.no_grad()
+    def forward(self, input_ids, meta: AttnMeta):
+        x = self.embed(input_ids)
+        residual = None
+        for layer in self.layers:
+            x, residual = layer(x, residual, meta)
+        x, _ = self.norm(x, residual)
+        return x
+
+    @torch.no_grad()
+    def compute_logits(self, h):
+        return self.lm_head(h)
+
+    def weight_specs(self) -> list:
+        cfg = self.cfg
+        Ht = cfg.num_attention_heads
+        specs = [("model.embed_tokens.weight", self.embed.weight, "vocab", None),
+                 ("model.norm.weight", self.norm.weight, "replicate", None)]
+        if not cfg.tie_word_embeddings:
+            specs.append(("lm_head.weight", self.lm_head.weight, "vocab", None))
+        for i, layer in enumerate(self.layers):
+            pre = f"model.layers.{i}."
+            a = layer.attn
+            specs += [(pre + "input_layernorm.weight", layer.input_layernorm.weight, "replicate", None),
+                      (pre + "post_attention_layernorm.weight", layer.post_attention_layernorm.weight,
+                       "replicate", None),
+                      (pre + "self_attn.kv_a_proj_with_mqa.weight", a.kv_a.weight, "replicate", None),
+                      (pre + "self_attn.kv_a_layernorm.weight", a.kv_a_norm.weight, "replicate", None),
+                      (pre + "self_attn.kv_b_proj.weight", a.kv_b, "fused", (0, Ht, NOPE + VDIM)),
+                      (pre + "self_attn.o_proj.weight", a.o_proj.weight, "row", None)]
+            if a.q_lora:
+                specs += [(pre + "self_attn.q_a_proj.weight", a.q_a.weight, "replicate", None),
+                          (pre + "self_attn.q_a_layernorm.weight", a.q_a_norm.weight, "replicate", None),
+                          (pre + "self_attn.q_b_proj.weight", a.q_b.weight, "fused", (0, Ht, NOPE + ROPE))]
+            else:
+                specs.append((pre + "self_attn.q_proj.weight", a.q_proj.weight, "fused", (0, Ht, NOPE + ROPE)))
+            m = layer.mlp
+            if not layer.is_moe:
+                F_total, F_local = cfg.intermediate_size, m.gate_up.weight.shape[0] // 2
+                specs += _mlp_specs(pre + "mlp.", m, F_total, F_local)
+                continue
+            specs.append((pre + "mlp.gate.weight", m.gate, "replicate", None))
+            if m.bias is not None:
+                specs.append((pre + "mlp.gate.e_score_correction_bias", m.bias, "replicate", None))
+            for el in range(m.E_local):
+                e = m.lo + el
+                ep = f"{pre}mlp.experts.{e}."
+                specs += [(ep + "gate_proj.weight", m.w1[el], "rows", (0, 2)),
+                          (ep + "up_proj.weight", m.w1[el], "rows", (1, 2)),
+                          (ep + "down_proj.weight", m.w2[el], "replicate", None)]
+            if m.shared is not None:
+                F_total = cfg.moe_intermediate_size * cfg.n_shared_experts
+                specs += _mlp_specs(pre + "mlp.shared_experts.", m.shared, F_total,
+                                    m.shared.gate_up.weight.shape[0] // 2)
+        return specs
+
+
+def _mlp_specs(pre, mlp, F_total, F_local):
+    return [(pre + "gate_proj.weight", mlp.gate_up.weight, "fused", (0, F_total, 1)),
+            (pre + "up_proj.weight", mlp.gate_up.weight, "fused", (F_local, F_total, 1)),
+            (pre + "down_proj.weight", mlp.down.weight, "row", None)]
+

@@ -10,6 +10,7 @@ checkpoint tensor maps onto this rank's shard:
   row                  split dim 1 into tp chunks (row-parallel weight)
   vocab                rows [rank*per, rank*per+per) of a vocab-parallel table
                        (zero-padded past the vocabulary)
+  rows                 rows start::step of the param (gate/up interleaving of MoE w1)
   fused                a slice [off, off+len) of a fused column-parallel param
                        (q|k|v or gate|up); ``extra = (off, n_heads_total,
                        head_rows)`` - heads are split across ranks, KV heads
@@ -65,6 +66,9 @@ def place(param: torch.Tensor, full: torch.Tensor, kind: str, extra=None):
             off, n_heads, head_rows = extra
             part = _shard_heads(full, n_heads, head_rows, tp, rank)
             param[off:off + part.shape[0]].copy_(part)
+        elif kind == "rows":  # interleaved rows (gate/up pairs of a fused expert weight)
+            start, step = extra
+            param[start::step].copy_(full)
         else:
             raise ValueError(kind)
 
@@ -99,6 +103,9 @@ def export_hf(model: torch.nn.Module) -> dict[str, torch.Tensor]:
             out[name] = p[off:off + n_heads * head_rows].detach().cpu().clone()
         elif kind == "vocab":
             out[name] = p[: model.cfg.vocab_size].detach().cpu().clone()
+        elif kind == "rows":
+            start, step = extra
+            out[name] = p[start::step].detach().cpu().clone()
         else:
             out[name] = p.detach().cpu().clone()
     return out

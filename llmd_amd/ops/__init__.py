@@ -254,3 +254,50 @@ def moe_experts(x, ids, wts, w1, w2, act=0, alpha=1.702, limit=7.0, out=None, b1
         out = torch.empty(T, d, dtype=x.dtype, device=dev)
     C.moe_combine(y, inv, wts.contiguous().view(-1), k, out)
     return out
+
+
+def mla_split_plan(max_len: int, rows: int, H: int, num_cus: int = 256) -> tuple[int, int]:
+    """(split_size, nsplit) so rows x head-groups x splits fills ~2 WGs per CU."""
+    base = max(1, rows * ((H + 15) // 16))
+    target = 2 * num_cus
+    want = max(1, min(math.ceil(max_len / 64), math.ceil(target / base)))
+    split = max(64, math.ceil(math.ceil(max_len / want) / 64) * 64)
+    return split, math.ceil(max(1, max_len) / split)
+
+
+def mla_attention(q, cache, block_tables, row_seq, row_len, H, scale, max_len=None, split=None, out=None,
+                  workspace=None):
+    """Absorbed-MLA attention over the paged latent cache (csrc/ops/attn_mla.hip).
+    q [R, H*576] bf16, cache [blocks, bs, 576] -> out [R, H*512]."""
+    if not _gpu(q):
+        r = ref.mla_attention(q, cache, block_tables, row_seq, row_len, H, scale)
+        if out is not None:
+            out.copy_(r)
+            return out
+        return r
+    R = q.shape[0]
+    if out is None:
+        out = torch.empty(R, H * 512, dtype=q.dtype, device=q.device)
+    if split is None:
+        if max_len is None:
+            max_len = int(row_len.max().item()) if R else 1
+        split = mla_split_plan(max_len, R, H)
+    split_size, nsplit = split
+    if nsplit > 1:
+        if workspace is None:
+            part_o = torch.empty(R * H * nsplit * 512, dtype=torch.float32, device=q.device)
+            part_ml = torch.empty(R * H * nsplit * 2, dtype=torch.float32, device=q.device)
+        else:
+            part_o, part_ml = workspace
+    else:
+        part_o = part_ml = out.new_empty(0, dtype=torch.float32)
+    native().mla_attention(out, q, cache, block_tables, row_seq, row_len, H, scale, split_size, nsplit,
+                           part_o, part_ml)
+    return out
+
+
+def mla_rope_cache(q, q_lat, kv_c, k_pe, positions, cos_sin, H, slots, cache):
+    """RoPE q_pe into q_lat[..., 512:] and write [kv_c | rope(k_pe)] to the latent cache."""
+    if not _gpu(q):
+        return ref.mla_rope_cache(q, q_lat, kv_c, k_pe, positions, cos_sin, H, slots, cache)
+    native().mla_rope_cache(q, q_lat, kv_c, k_pe, positions, cos_sin, H, slots, cache)

@@ -220,13 +220,45 @@ def yarn_inv_freq(rot_dim, base, sc):
     ramp = torch.clamp((torch.arange(rot_dim // 2, dtype=torch.float64) - low) / max(high - low, 1e-3), 0, 1)
     mask = 1 - ramp
     inv = inter * (1 - mask) + extra * mask
-    mscale = sc.get("mscale", None)
-    m = 0.1 * math.log(factor) + 1.0 if factor > 1 else 1.0
-    if sc.get("mscale_all_dim"):
-        m = m / (0.1 * sc["mscale_all_dim"] * math.log(factor) + 1.0)
-    if mscale is not None and not sc.get("mscale_all_dim"):
-        m = 0.1 * mscale * math.log(factor) + 1.0 if factor > 1 else 1.0
+    def get_mscale(ms):
+        return 0.1 * ms * math.log(factor) + 1.0 if factor > 1 else 1.0
+
+    if sc.get("mscale_all_dim"):  # DeepSeek: cos/sin scaled by mscale/mscale_all_dim
+        m = get_mscale(sc.get("mscale", 1.0)) / get_mscale(sc["mscale_all_dim"])
+    else:
+        m = get_mscale(sc.get("mscale", 1.0))
     return inv, m
+
+
+def yarn_softmax_mscale(sc: dict | None) -> float:
+    """DeepSeek YaRN: the softmax scale is multiplied by mscale_all_dim-mscale squared."""
+    if not sc or sc.get("rope_type", sc.get("type")) != "yarn" or not sc.get("mscale_all_dim"):
+        return 1.0
+    f = sc["factor"]
+    m = 0.1 * sc["mscale_all_dim"] * math.log(f) + 1.0 if f > 1 else 1.0
+    return m * m
+
+
+def mla_rope_cache(q, q_lat, kv_c, k_pe, positions, cos_sin, H, slots, cache):
+    """q [T, H*192] (nope 128 | pe 64) -> q_lat[:, h*576+512:+64] = rope(q_pe);
+    cache.view(-1, 576)[slot] = [kv_c | rope(k_pe)] (GPT-J interleaved pairs)."""
+    T = q.shape[0]
+    cs = cos_sin[positions.long()].float()
+    cos, sin = cs[:, :32], cs[:, 32:]
+
+    def rot(x):  # x [..., 64] pairs (2i, 2i+1)
+        x0, x1 = x[..., 0::2].float(), x[..., 1::2].float()
+        c, s_ = cos.view(T, *([1] * (x.dim() - 2)), 32), sin.view(T, *([1] * (x.dim() - 2)), 32)
+        y = torch.stack([x0 * c - x1 * s_, x0 * s_ + x1 * c], -1)
+        return y.flatten(-2)
+
+    qp = q[:, : H * 192].view(T, H, 192)[:, :, 128:]
+    q_lat.view(T, H, 576)[:, :, 512:] = rot(qp).to(q_lat.dtype)
+    bs = cache.shape[1]
+    ok = slots >= 0
+    row = torch.cat([kv_c.float(), rot(k_pe)], -1).to(cache.dtype)
+    sl = slots[ok].long()
+    cache[sl // bs, sl % bs] = row[ok]
 
 
 # ---------------------------------------------------------------- MoE references
@@ -285,3 +317,21 @@ def moe_forward(x, ids, wts, w1, w2, act=0, alpha=1.702, limit=7.0, b1=None, b2=
             y = y.to(x.dtype).float()
             out[t] += float(wts[t, j]) * y
     return out.to(x.dtype)
+
+
+def mla_attention(q, cache, block_tables, row_seq, row_len, H, scale):
+    """Absorbed MLA: q [R, H*576], cache [blocks, bs, 576] -> out [R, H*512]
+    (value = first 512 dims of the cached latent)."""
+    R = q.shape[0]
+    bs = cache.shape[1]
+    out = torch.zeros(R, H, 512, dtype=torch.float32, device=q.device)
+    qf = q[:, : H * 576].float().view(R, H, 576)
+    for r in range(R):
+        L = int(row_len[r])
+        bt = block_tables[int(row_seq[r])]
+        idx = torch.arange(L, device=q.device)
+        kv = cache[bt[idx // bs].long(), idx % bs].float()  # [L, 576]
+        s = (qf[r] @ kv.T) * scale                           # [H, L]
+        p = torch.softmax(s, -1)
+        out[r] = p @ kv[:, :512]
+    return out.view(R, H * 512).to(q.dtype)
