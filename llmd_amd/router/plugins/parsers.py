@@ -6,20 +6,37 @@ import json
 
 from .. import headers as H
 from ..types import CIHeaders, InferenceRequest
+from ..multimodal import TokenEstimator, asset_hash, image_url_of, virtual_segment
 from .base import Parser, register
+
+_DEFAULT_EST = TokenEstimator()
 
 OPENAI_PATHS = ("/v1/completions", "/v1/chat/completions", "/v1/embeddings", "/v1/responses",
                 "/v1/conversations", "/v1/messages", "/inference/v1/generate")
 
 
-def _flatten_prompt(body: dict) -> str:
+def _content_text(c, est: TokenEstimator, assets: list) -> str:
+    if not isinstance(c, list):
+        return c or ""
+    out = []
+    for p in c:
+        if not isinstance(p, dict):
+            continue
+        url = image_url_of(p)
+        if url:  # multimodal asset -> virtual segment of its estimated token footprint
+            assets.append((asset_hash(url), est.tokens(url)))
+            out.append(virtual_segment(url, est))
+        else:
+            out.append(p.get("text", ""))
+    return "".join(out)
+
+
+def _flatten_prompt(body: dict, est: TokenEstimator = _DEFAULT_EST, assets: list | None = None) -> str:
+    assets = [] if assets is None else assets
     if "messages" in body:
         parts = []
         for m in body.get("messages") or []:
-            c = m.get("content")
-            if isinstance(c, list):
-                c = "".join(p.get("text", "") for p in c if isinstance(p, dict))
-            parts.append(f"<{m.get('role', '')}>{c or ''}")
+            parts.append(f"<{m.get('role', '')}>{_content_text(m.get('content'), est, assets)}")
         return "".join(parts)
     if "input" in body:  # responses / embeddings
         i = body["input"]
@@ -45,7 +62,12 @@ class OpenAIParser(Parser):
         req = InferenceRequest(path=path, body=d, headers=h, raw_size=len(body))
         req.model = d.get("model", "") or ""
         req.target_model = req.model
-        req.prompt = _flatten_prompt(d)
+        est = getattr(self, "_est", None)
+        if est is None:
+            est = self._est = TokenEstimator.from_params((getattr(self, "params", None) or {}).get("multimodal"))
+        assets: list = []
+        req.prompt = _flatten_prompt(d, est, assets)
+        req.mm_assets = assets
         p = d.get("prompt")
         if isinstance(p, list) and p and isinstance(p[0], int):
             req.token_ids = list(p)

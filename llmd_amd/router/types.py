@@ -121,6 +121,7 @@ class InferenceRequest:
     slo_tpot_ms: Optional[float] = None
     prompt: str = ""                      # flattened text used for approximate hashing
     token_ids: Optional[list[int]] = None  # exact tokens (token-producer)
+    mm_assets: list = field(default_factory=list)  # (asset hash, estimated tokens) per image
     stream: bool = False
     data: dict = field(default_factory=dict)  # producer outputs
     arrival: float = field(default_factory=time.monotonic)

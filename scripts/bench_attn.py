@@ -95,12 +95,38 @@ def decode(ctx, B, Hq, Hkv, D, bs):
     return t
 
 
+def mla(ctx, R, H, prefill=False, bs=64):
+    dev = "cuda"
+    nseq = 1 if prefill else R
+    per = math.ceil(ctx / bs)
+    nb = nseq * per + 1
+    cache = torch.randn(nb, bs, 576, device=dev, dtype=torch.bfloat16)
+    bt = torch.stack([torch.randperm(nb - 1, device=dev)[:per] for _ in range(nseq)]).int()
+    q = torch.randn(R, H * 576, device=dev, dtype=torch.bfloat16)
+    if prefill:
+        rows = torch.zeros(R, dtype=torch.int32, device=dev)
+        ln = torch.arange(ctx - R + 1, ctx + 1, dtype=torch.int32, device=dev)
+    else:
+        rows = torch.arange(R, dtype=torch.int32, device=dev)
+        ln = torch.full((R,), ctx, dtype=torch.int32, device=dev)
+    out = torch.empty(R, H * 512, device=dev, dtype=torch.bfloat16)
+    fn = lambda: ops.mla_attention(q, cache, bt, rows, ln, H, 0.07, max_len=ctx, out=out)  # noqa: E731
+    t = time_it(fn)
+    keys = float(ln.sum().item())
+    fl = 2 * H * keys * (576 + 512)
+    by = (nseq * ctx) * 576 * 2
+    kind = "prefill" if prefill else "decode"
+    print(f"mla {kind} rows={R} ctx={ctx} H={H}: {t * 1e3:.3f} ms  {fl / t / 1e12:.1f} TF/s  "
+          f"{by / t / 1e9:.0f} GB/s latent read")
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--ctx", type=int, default=5000)
     ap.add_argument("--check", action="store_true")
     ap.add_argument("--D", type=int, default=128)
     ap.add_argument("--so", default=None)
+    ap.add_argument("--mla", action="store_true")
     a = ap.parse_args()
     if a.check:
         prefill(700, 300, 16, 2, a.D, 64, check=True)
@@ -110,6 +136,10 @@ def main():
     prefill(8192, 8192, 64, 8, a.D, 64)
     decode(a.ctx, 64, 64, 8, a.D, 64)
     decode(a.ctx, 8, 64, 8, a.D, 64)
+    if a.mla:
+        mla(4096, 64, 128)
+        mla(4096, 8, 128)
+        mla(4096, 2048, 128, prefill=True)
 
 
 if __name__ == "__main__":
