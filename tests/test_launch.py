@@ -64,3 +64,24 @@ def test_deploy_values_and_router_configs_valid():
             load_config(text)
             n_cfg += 1
     assert n_cfg >= 4
+
+
+def test_dashboards_reference_exported_metrics():
+    import glob
+    import json
+    import re
+
+    from llmd_amd.engine.metrics import EngineMetrics
+    from llmd_amd.router.metrics import EPPMetrics
+
+    names = set(re.findall(r"^# TYPE (\S+)", EngineMetrics("m", 16, 100).render().decode(), re.M))
+    names |= set(re.findall(r"^# TYPE (\S+)", EPPMetrics().render().decode(), re.M))
+    names |= {"vllm:nixl_xfer_time_seconds", "vllm:nixl_bytes_transferred", "vllm:nixl_num_failed_transfers"}
+    files = glob.glob(os.path.join(ROOT, "deploy/observability/grafana/dashboards/*.json"))
+    assert len(files) == 4
+    for f in files:
+        for p in json.load(open(f))["panels"]:
+            for t in p["targets"]:
+                for m in re.findall(r"(vllm:[a-z_]+|inference_[a-z_]+|llm_d_[a-z_]+)", t["expr"]):
+                    base = re.sub(r"_(bucket|sum|count|total)$", "", m)
+                    assert base in names or m in names, (f, m)
