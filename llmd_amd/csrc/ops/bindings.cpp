@@ -40,6 +40,8 @@ int llmd_mla_attention(const void*, int64_t, const void*, int64_t, int, const in
                        const int*, int, int, float, int, int, void*, int64_t, float*, float*, hipStream_t);
 int llmd_mla_rope_cache(const void*, int64_t, void*, int64_t, const void*, int64_t, const void*, int64_t,
                         const int64_t*, const float*, int, int, const int64_t*, void*, int64_t, int, hipStream_t);
+int llmd_lora_bgmv(const void*, int64_t, const void*, const void*, int, int, int, int, const int*, float*, void*,
+                   int64_t, hipStream_t);
 int llmd_vmm_granularity(int, size_t*);
 int llmd_vmm_alloc(int, size_t, int, void**, uint64_t*);
 int llmd_vmm_export_fd(uint64_t, int*);
@@ -231,6 +233,23 @@ void mla_rope_cache(torch::Tensor q, torch::Tensor q_lat, torch::Tensor kv_c, to
                                cos_sin.data_ptr<float>(), T, H, slots.data_ptr<int64_t>(), cache.data_ptr(),
                                cache.stride(0), cache.size(1), cur_stream());
   TORCH_CHECK(rc == 0, "mla_rope_cache failed: ", rc);
+}
+
+// y[t] += B[slot[t]] @ (A[slot[t]] @ x[t]); A [S, R, in], B [S, out, R] bf16, slot [T] int32
+void lora_bgmv(torch::Tensor y, torch::Tensor x, torch::Tensor A, torch::Tensor B, torch::Tensor slot,
+               torch::Tensor h) {
+  const c10::hip::OptionalHIPGuard device_guard(dev_of(y));
+  CHECK_CUDA(x); CHECK_BF16(x); CHECK_BF16(y); CHECK_BF16(A); CHECK_BF16(B); CHECK_INNER(x); CHECK_INNER(y);
+  CHECK_DT(slot, at::kInt); CHECK_DT(h, at::kFloat);
+  TORCH_CHECK(A.dim() == 3 && B.dim() == 3 && A.is_contiguous() && B.is_contiguous(), "lora: A [S,R,in], B [S,out,R]");
+  const int T = x.size(0), R = A.size(1), in = A.size(2), out = B.size(1);
+  TORCH_CHECK(B.size(0) == A.size(0) && B.size(2) == R && R <= 128, "lora: slot/rank mismatch");
+  TORCH_CHECK(x.size(1) == in && y.size(0) == T && y.size(1) == out && slot.numel() >= T, "lora: shapes");
+  TORCH_CHECK(in % 8 == 0 && in <= 32768 && x.stride(0) % 8 == 0, "lora: in dim");
+  TORCH_CHECK(h.numel() >= (int64_t)T * R, "lora: workspace");
+  int rc = llmd_lora_bgmv(x.data_ptr(), x.stride(0), A.data_ptr(), B.data_ptr(), T, R, in, out, slot.data_ptr<int>(),
+                          h.data_ptr<float>(), y.data_ptr(), y.stride(0), cur_stream());
+  TORCH_CHECK(rc == 0, "lora_bgmv failed: ", rc);
 }
 
 void paged_prefill(torch::Tensor out, torch::Tensor q, torch::Tensor k_cache,
@@ -485,6 +504,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("kvx_ipc_open", &kvx_ipc_open);
   m.def("kvx_ipc_close", &kvx_ipc_close);
   m.def("mla_attention", &mla_attention);
+  m.def("lora_bgmv", &lora_bgmv);
   m.def("mla_rope_cache", &mla_rope_cache);
   m.def("vmm_granularity", &vmm_granularity);
   m.def("vmm_pool", &vmm_pool);

@@ -263,6 +263,8 @@ class EngineConfig:
     kv_offload_config: Optional[dict] = None
     max_loras: int = 0
     enable_lora: bool = False
+    max_lora_rank: int = 16
+    lora_modules: Optional[dict] = None  # name -> adapter dir, loaded at start-up
 
     @property
     def served_name(self) -> str:
@@ -318,6 +320,10 @@ def add_engine_args(p: argparse.ArgumentParser) -> argparse.ArgumentParser:
     p.add_argument("--kv-events-config", type=_json_arg, default=None)
     p.add_argument("--kv-offload-config", type=_json_arg, default=None)
     p.add_argument("--scheduling-policy", default="fcfs", choices=["fcfs", "priority"])
+    p.add_argument("--enable-lora", action="store_true")
+    p.add_argument("--max-loras", type=int, default=4)
+    p.add_argument("--max-lora-rank", type=int, default=16)
+    p.add_argument("--lora-modules", nargs="*", default=None, help="name=path adapters loaded at start-up")
     return p
 
 
@@ -333,4 +339,6 @@ def engine_config_from_args(a) -> EngineConfig:
         data_parallel_rank=a.data_parallel_rank, enable_expert_parallel=a.enable_expert_parallel,
         enforce_eager=a.enforce_eager, kv_transfer_config=a.kv_transfer_config,
         kv_events_config=a.kv_events_config, kv_offload_config=a.kv_offload_config,
-        policy=a.scheduling_policy)
+        policy=a.scheduling_policy, enable_lora=getattr(a, "enable_lora", False),
+        max_loras=getattr(a, "max_loras", 4), max_lora_rank=getattr(a, "max_lora_rank", 16),
+        lora_modules=dict(m.split("=", 1) for m in (getattr(a, "lora_modules", None) or [])) or None)

@@ -22,6 +22,18 @@ from .scheduler import Scheduler, SchedulerOutput
 log = logging.getLogger("llmd.engine")
 
 
+def make_lora_manager(cfg: EngineConfig, runner: ModelRunner, driver: bool):
+    from llmd_amd.parallel.comm import tp_broadcast_plan
+
+    from .lora import LoRAManager
+
+    n = max(cfg.sched.max_num_batched_tokens, cfg.cuda_graph_max_bs) + 64
+    bc = tp_broadcast_plan if (driver and runner.tp_size > 1) else None
+    mgr = LoRAManager(runner.model, max(1, cfg.max_loras), cfg.max_lora_rank, n, runner.device, broadcast=bc)
+    runner.lora = mgr
+    return mgr
+
+
 class LLMEngine:
     def __init__(self, cfg: EngineConfig, metrics: Optional[EngineMetrics] = None,
                  runner: Optional[ModelRunner] = None, capture_graphs: bool = True):
@@ -38,7 +50,8 @@ class LLMEngine:
 
             self.connector = make_connector(cfg, self)
         self.sched = Scheduler(cfg, self.bm, self.connector)
-        self.metrics = metrics or EngineMetrics(cfg.served_name, cfg.cache.block_size, nb)
+        self.metrics = metrics or EngineMetrics(cfg.served_name, cfg.cache.block_size, nb,
+                                                max_lora=cfg.max_loras if cfg.enable_lora else 0)
         self.event_sink = None  # set by serving.kv_events.KVEventPublisher
         self.offload = None
         if cfg.kv_offload_config:
@@ -46,6 +59,11 @@ class LLMEngine:
 
             self.offload = OffloadManager(cfg, self)
             self.sched.offload = self.offload
+        self.lora = None
+        if cfg.enable_lora:
+            self.lora = make_lora_manager(cfg, self.runner, driver=True)
+            for name, path in (cfg.lora_modules or {}).items():
+                self.lora.load(name, path)
         if capture_graphs:
             self.runner.capture_graphs()
         self.paused = False
@@ -83,6 +101,10 @@ class LLMEngine:
             self.connector.tick()
         t0 = time.monotonic()
         so = self.sched.schedule()
+        if self.lora is not None:
+            nm = self.lora.name_of
+            self.metrics.set_lora(sorted({nm(r.lora_id) for r in self.sched.running if r.lora_id} - {None}),
+                                  sorted({nm(r.lora_id) for r in self.sched.waiting if r.lora_id} - {None}))
         err_outs = self._error_outputs()
         self.last_step_empty = so.empty
         if so.empty:
@@ -127,10 +149,12 @@ class LLMEngine:
             self.event_sink(evs)
 
     # ------------------------------------------------------------ offline helpers
-    def generate(self, prompts: Iterable[list[int]], params: SamplingParams) -> list[Request]:
+    def generate(self, prompts: Iterable[list[int]], params: SamplingParams,
+                 lora_ids: Optional[list[int]] = None) -> list[Request]:
         reqs = []
         for i, p in enumerate(prompts):
-            reqs.append(self.add_request(f"gen-{self.step_count}-{i}-{time.monotonic_ns()}", p, params))
+            reqs.append(self.add_request(f"gen-{self.step_count}-{i}-{time.monotonic_ns()}", p, params,
+                                         lora_id=lora_ids[i] if lora_ids else 0))
         while self.has_unfinished():
             self.step()
         return reqs

@@ -74,6 +74,7 @@ class ModelRunner:
         # or one latent row per token for MLA
         self.kv_spec = self.model.kv_spec() if hasattr(self.model, "kv_spec") else (2, self.Hkv, self.D)
         self.is_mla = bool(getattr(self.model, "needs_mla_rows", False))
+        self.lora = None  # engine/lora.py LoRAManager (set by the engine / TP follower)
         self.kv = None
         self.num_blocks = 0
         self.graphs: dict[int, tuple] = {}
@@ -293,12 +294,23 @@ class ModelRunner:
         rows, reqs = self._sample_rows(so)
         ids, pos, slots, d_bt, d_len, p_ql, p_ctx, p_bt = self._prepare(so, block_tables)
         graph = not so.prefills and self._graph_ok(len(so.decodes))
-        return {"graph": graph, "nd": len(so.decodes), "ids": ids, "pos": pos, "slots": slots, "d_bt": d_bt,
-                "d_len": d_len, "p_ql": p_ql, "p_ctx": p_ctx, "p_bt": p_bt, "rows": rows}, reqs
+        pl = {"graph": graph, "nd": len(so.decodes), "ids": ids, "pos": pos, "slots": slots, "d_bt": d_bt,
+              "d_len": d_len, "p_ql": p_ql, "p_ctx": p_ctx, "p_bt": p_bt, "rows": rows}
+        if self.lora is not None:
+            lo = [sr.req.lora_id for sr in so.decodes]
+            for sr in so.prefills:
+                lo.extend([sr.req.lora_id] * sr.num_new_tokens)
+            pl["lora"] = lo
+        return pl, reqs
 
     @torch.no_grad()
     def run_plan(self, pl: dict):
         rows = pl["rows"]
+        if self.lora is not None:
+            lo = pl.get("lora") or [0] * len(pl["ids"])
+            if pl["graph"]:  # padded rows of the bucket must not pick up stale adapter slots
+                lo = list(lo) + [0] * (self._bucket(pl["nd"]) - len(lo))
+            self.lora.set_tokens(lo)
         if pl["graph"]:
             return self._run_decode_graph(pl)
         h = self._run_eager(pl)

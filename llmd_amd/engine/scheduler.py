@@ -93,6 +93,9 @@ class _WaitQueue:
             return heapq.heappop(self.heap)[3]
         return self.dq.popleft()
 
+    def __iter__(self):
+        return iter([e[3] for e in self.heap] if self.policy == "priority" else list(self.dq))
+
     def remove(self, r: Request) -> bool:
         if self.policy == "priority":
             for i, e in enumerate(self.heap):

@@ -32,6 +32,10 @@ def run_follower(cfg: EngineConfig, capture_graphs: bool = True) -> int:
     """Blocking loop for TP ranks != 0. Returns the number of steps executed."""
     runner = ModelRunner(cfg)
     runner.profile_and_allocate()
+    if cfg.enable_lora:
+        from .engine import make_lora_manager
+
+        make_lora_manager(cfg, runner, driver=False)
     if capture_graphs:
         runner.capture_graphs()
     n = 0
@@ -40,6 +44,9 @@ def run_follower(cfg: EngineConfig, capture_graphs: bool = True) -> int:
             pl = tp_recv_plan()
             if pl is None or pl.get("stop"):
                 break
+            if "lora_cmd" in pl:  # adapter load/unload issued on the driver
+                runner.lora.apply_cmd(pl["lora_cmd"])
+                continue
             runner.run_plan(pl)
             n += 1
     log.info("tp follower exiting after %d steps", n)

@@ -42,8 +42,13 @@ class ColumnLinear(torch.nn.Module):
         self.bias = torch.nn.Parameter(torch.zeros(self.out_f, device=device, dtype=dtype),
                                        requires_grad=False) if bias else None
 
+    lora = None  # engine/lora.py LoRATarget when multi-LoRA is enabled
+
     def forward(self, x):
-        return F.linear(x, self.weight, self.bias)
+        y = F.linear(x, self.weight, self.bias)
+        if self.lora is not None:
+            self.lora.apply(y, x)
+        return y
 
 
 class RowLinear(torch.nn.Module):
@@ -60,8 +65,12 @@ class RowLinear(torch.nn.Module):
         self.bias = torch.nn.Parameter(torch.zeros(out_f, device=device, dtype=dtype),
                                        requires_grad=False) if bias else None
 
+    lora = None
+
     def forward(self, x):
         y = F.linear(x, self.weight)
+        if self.lora is not None:  # partial sums join the layer's all-reduce
+            self.lora.apply(y, x)
         if self.reduce:
             y = tp_all_reduce(y)
         if self.bias is not None:

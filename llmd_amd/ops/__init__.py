@@ -301,3 +301,13 @@ def mla_rope_cache(q, q_lat, kv_c, k_pe, positions, cos_sin, H, slots, cache):
     if not _gpu(q):
         return ref.mla_rope_cache(q, q_lat, kv_c, k_pe, positions, cos_sin, H, slots, cache)
     native().mla_rope_cache(q, q_lat, kv_c, k_pe, positions, cos_sin, H, slots, cache)
+
+
+def lora_bgmv(y, x, A, B, slot, h=None):
+    """Multi-LoRA batched GEMV, in place on y (csrc/ops/lora.hip)."""
+    if not _gpu(x):
+        return ref.lora_bgmv(y, x, A, B, slot)
+    if h is None:
+        h = torch.empty(x.shape[0] * A.shape[1], dtype=torch.float32, device=x.device)
+    native().lora_bgmv(y, x, A, B, slot, h)
+    return y

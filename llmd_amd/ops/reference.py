@@ -335,3 +335,14 @@ def mla_attention(q, cache, block_tables, row_seq, row_len, H, scale):
         p = torch.softmax(s, -1)
         out[r] = p @ kv[:, :512]
     return out.view(R, H * 512).to(q.dtype)
+
+
+def lora_bgmv(y, x, A, B, slot):
+    """y[t] += B[slot[t]] @ (A[slot[t]] @ x[t]) (slot 0 = no adapter); in place."""
+    s = slot[: x.shape[0]].long()
+    on = s > 0
+    if bool(on.any()):
+        xa = torch.einsum("ti,tri->tr", x[on].float(), A[s[on]].float())
+        d = torch.einsum("tr,tor->to", xa, B[s[on]].float())
+        y[on] = (y[on].float() + d).to(y.dtype)
+    return y

@@ -355,7 +355,7 @@ def build_server(cfg: EngineConfig, engine=None):
 
     eng = engine or LLMEngine(cfg)
     aeng = AsyncEngine(eng)
-    srv = OpenAIServer(aeng, cfg)
+    srv = OpenAIServer(aeng, cfg, lora_manager=eng.lora)
     if cfg.kv_events_config and cfg.kv_events_config.get("enable_kv_cache_events"):
         from .kv_events import KVEventPublisher
 
