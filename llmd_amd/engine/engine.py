@@ -11,6 +11,8 @@ import logging
 import time
 from typing import Iterable, Optional
 
+import torch
+
 from llmd_amd import _rt_loader
 
 from .config import EngineConfig
@@ -59,6 +61,11 @@ class LLMEngine:
 
             self.offload = OffloadManager(cfg, self)
             self.sched.offload = self.offload
+        from llmd_amd.parallel import ep
+
+        ep.set_backend(cfg.parallel.all2all_backend)
+        self.dp_lockstep = ep.ep_active() and self.runner.mc.is_moe
+        self.last_global_idle = False
         self.lora = None
         if cfg.enable_lora:
             self.lora = make_lora_manager(cfg, self.runner, driver=True)
@@ -107,12 +114,61 @@ class LLMEngine:
                                   sorted({nm(r.lora_id) for r in self.sched.waiting if r.lora_id} - {None}))
         err_outs = self._error_outputs()
         self.last_step_empty = so.empty
+        if self.dp_lockstep:
+            return self._lockstep_step(so, err_outs, t0)
         if so.empty:
             self._flush_events()
             return err_outs
         if self.offload is not None:
             self.offload.before_step(so)
         sampled = self.runner.execute(so, self.block_tables(so))
+        return self._finish_step(so, sampled, err_outs, t0)
+
+    # ------------------------------------------------------------ DP lockstep
+    def _lockstep_step(self, so, err_outs, t0) -> list[RequestOutput]:
+        """Wide-EP (DP attention + EP MoE): every rank runs a forward
+        whenever ANY rank has work - idle ranks a dummy one - with agreed shapes:
+        all-decode steps replay the bucket of the largest decode batch, steps with
+        a prefill anywhere run eager with MoE rows padded to the largest step."""
+        import torch.distributed as dist
+
+        from llmd_amd.parallel import ep
+        from llmd_amd.parallel.state import get_state
+
+        v = torch.tensor([so.num_tokens, int(bool(so.prefills)), len(so.decodes)], dtype=torch.int64)
+        dist.all_reduce(v, op=dist.ReduceOp.MAX, group=get_state().cpu_group)
+        t_max, any_prefill, nd_max = v.tolist()
+        self.last_global_idle = t_max == 0
+        if t_max == 0:
+            self._flush_events()
+            return err_outs
+        bucket = None
+        if not any_prefill and self.runner.graphs:
+            b = self.runner._bucket(max(nd_max, 1))
+            bucket = b if b in self.runner.graphs else None
+        ep.set_step_rows(0 if bucket is not None else t_max)
+        if so.empty:
+            self.runner.execute_dummy(bucket)
+            self._flush_events()
+            return err_outs
+        if self.offload is not None:
+            self.offload.before_step(so)
+        sampled = self.runner.execute(so, self.block_tables(so), force_eager=bucket is None, bucket=bucket)
+        return self._finish_step(so, sampled, err_outs, t0)
+
+    def dp_has_unfinished(self) -> bool:
+        """True while any DP rank of the EP group still has requests."""
+        if not self.dp_lockstep:
+            return self.has_unfinished()
+        import torch.distributed as dist
+
+        from llmd_amd.parallel.state import get_state
+
+        v = torch.tensor([int(self.has_unfinished())], dtype=torch.int64)
+        dist.all_reduce(v, op=dist.ReduceOp.MAX, group=get_state().cpu_group)
+        return bool(v.item())
+
+    def _finish_step(self, so, sampled, err_outs, t0) -> list[RequestOutput]:
         touched = self.sched.update(so, sampled)
         dt = time.monotonic() - t0
         self.step_count += 1

@@ -277,10 +277,17 @@ class ModelRunner:
 
     # ------------------------------------------------------------ execution
     @torch.no_grad()
-    def execute(self, so: SchedulerOutput, block_tables: dict[int, list[int]]) -> dict[int, tuple[int, float]]:
+    def execute(self, so: SchedulerOutput, block_tables: dict[int, list[int]], force_eager: bool = False,
+                bucket: Optional[int] = None) -> dict[int, tuple[int, float]]:
+        """force_eager / bucket: DP-lockstep overrides (every EP rank must run the
+        same kind of step with the same collective shapes)."""
         if so.empty:
             return {}
         pl, reqs = self.plan(so, block_tables)
+        if force_eager:
+            pl["graph"] = False
+        elif bucket is not None and pl["graph"]:
+            pl["bucket"] = bucket
         if self.tp_size > 1:
             tp_broadcast_plan(pl)  # TP followers run the same plan (engine/tp_worker.py)
         logits = self.run_plan(pl)
@@ -309,7 +316,7 @@ class ModelRunner:
         if self.lora is not None:
             lo = pl.get("lora") or [0] * len(pl["ids"])
             if pl["graph"]:  # padded rows of the bucket must not pick up stale adapter slots
-                lo = list(lo) + [0] * (self._bucket(pl["nd"]) - len(lo))
+                lo = list(lo) + [0] * ((pl.get("bucket") or self._bucket(pl["nd"])) - len(lo))
             self.lora.set_tokens(lo)
         if pl["graph"]:
             return self._run_decode_graph(pl)
@@ -430,9 +437,25 @@ class ModelRunner:
         torch.cuda.synchronize()
         log.info("captured %d decode graphs in %.1fs", len(buckets), time.time() - t0)
 
+    @torch.no_grad()
+    def execute_dummy(self, graph_bucket: Optional[int] = None):
+        """Idle DP rank in a lockstep step: run a forward with no real tokens so
+        the MoE collectives of the busy ranks complete."""
+        w = self.width
+        empty = np.zeros((0, w), dtype=np.int32)
+        if graph_bucket is not None and graph_bucket in self.graphs:
+            pl = {"graph": True, "nd": 0, "bucket": graph_bucket, "ids": [], "pos": [], "slots": [], "d_bt": empty,
+                  "d_len": np.zeros(0, dtype=np.int32), "p_ql": [], "p_ctx": [], "p_bt": empty, "rows": []}
+        else:  # one padding decode token: no cache write (slot -1), one visible key
+            pl = {"graph": False, "nd": 1, "ids": [0], "pos": [0], "slots": [-1], "d_bt": np.zeros((1, w), np.int32),
+                  "d_len": np.ones(1, dtype=np.int32), "p_ql": [], "p_ctx": [], "p_bt": empty, "rows": []}
+        if self.lora is not None:
+            pl["lora"] = []
+        self.run_plan(pl)
+
     def _run_decode_graph(self, pl: dict):
         n, rows = pl["nd"], pl["rows"]
-        B = self._bucket(n)
+        B = pl.get("bucket") or self._bucket(n)
         g, lg = self.graphs[B]
         ids, pos, slots, d_bt, d_len = pl["ids"], pl["pos"], pl["slots"], pl["d_bt"], pl["d_len"]
         if B > n:

@@ -28,6 +28,7 @@ from llmd_amd.engine.attn_meta import AttnMeta
 from llmd_amd.engine.config import ModelConfig
 from llmd_amd.ops.reference import yarn_softmax_mscale
 from llmd_amd.parallel.comm import tp_all_reduce
+from llmd_amd.parallel.ep import ep_active, moe_ep
 from llmd_amd.parallel.state import get_state
 
 from .layers import ColumnLinear, LMHead, RMSNorm, RowLinear, VocabEmbedding, _init_weight
@@ -108,11 +109,13 @@ class DeepseekMoE(torch.nn.Module):
         super().__init__()
         st = get_state()
         self.tp, self.rank = st.tp_size, st.tp_rank
+        self.dp_ep = ep_active()  # DP attention + EP MoE: experts over the whole EP group
+        n_ep, r_ep = (st.ep_size, st.ep_rank) if self.dp_ep else (self.tp, self.rank)
         E, d, Fh = cfg.num_local_experts, cfg.hidden_size, cfg.moe_intermediate_size
-        if E % self.tp:
-            raise ValueError(f"{E} experts do not split over TP={self.tp}")
-        self.E, self.E_local, self.k = E, E // self.tp, cfg.num_experts_per_tok
-        self.lo = self.rank * self.E_local
+        if E % n_ep:
+            raise ValueError(f"{E} experts do not split over EP={n_ep}")
+        self.E, self.E_local, self.k = E, E // n_ep, cfg.num_experts_per_tok
+        self.lo = r_ep * self.E_local
         self.cfg = cfg
         dt = torch.bfloat16
         self.gate = torch.nn.Parameter(_init_weight(torch.empty(E, d, device=device, dtype=dt), 0.02),
@@ -134,7 +137,11 @@ class DeepseekMoE(torch.nn.Module):
         ids, w = ops.moe_topk(logits, self.k, scoring=1 if cfg.scoring_func == "sigmoid" else 0, bias=self.bias,
                               n_group=cfg.n_group, topk_group=cfg.topk_group, renorm=cfg.norm_topk_prob,
                               routed_scale=cfg.routed_scaling_factor)
-        if self.tp > 1:
+        if self.dp_ep:  # tokens differ per rank: exchange them with the expert owners
+            y = moe_ep(x, ids, w, self.E_local,
+                       lambda xx, ii, ww: ops.moe_experts(xx, ii, ww, self.w1, self.w2, ops.ACT_SILU))
+            return y + self.shared(x) if self.shared is not None else y
+        if self.tp > 1:  # tokens replicated over TP: mask to the local experts, one all-reduce
             local = (ids >= self.lo) & (ids < self.lo + self.E_local)
             ids = torch.where(local, ids - self.lo, torch.full_like(ids, -1))
             w = torch.where(local, w, torch.zeros_like(w))

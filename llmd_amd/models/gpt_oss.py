@@ -12,10 +12,10 @@ MoE execution: native gating (``moe_topk``), expert alignment and two MFMA
 grouped GEMMs with fused activation / bias, deterministic weighted combine
 (``llmd_amd/csrc/ops/moe.hip``). Expert weights use the interleaved
 gate/up row layout ([E, 2F, d]) so the activation fuses into GEMM-1.
-With expert parallelism (EP = world) every rank owns E/EP experts; tokens
-are all-gathered, each rank computes its experts' contributions, and a
-reduce-scatter returns the token rows (the reference's
-``allgather_reducescatter`` all2all backend).
+With expert parallelism every rank owns E/EP experts: under TP the tokens are
+replicated and one all-reduce sums the expert owners' contributions; under
+DP attention (wide-EP) tokens are exchanged with ``parallel/ep.py``
+(all-gather/reduce-scatter or all-to-all dispatch/combine).
 """
 from __future__ import annotations
 
@@ -24,7 +24,8 @@ import torch.nn.functional as F
 
 from llmd_amd import ops
 from llmd_amd.engine.config import ModelConfig
-from llmd_amd.parallel.comm import ep_all_gather, ep_reduce_scatter
+from llmd_amd.parallel.comm import tp_all_reduce
+from llmd_amd.parallel.ep import ep_active, moe_ep
 from llmd_amd.parallel.state import get_state
 
 from .layers import _init_weight
@@ -36,6 +37,8 @@ class GptOssMoE(torch.nn.Module):
         super().__init__()
         st = get_state()
         self.ep = ep and st.ep_size > 1
+        self.dp_ep = self.ep and ep_active()   # DP attention: exchange tokens with expert owners
+        self.tp = st.tp_size
         self.ep_size = st.ep_size if self.ep else 1
         self.ep_rank = st.ep_rank if self.ep else 0
         E = cfg.num_local_experts
@@ -62,17 +65,16 @@ class GptOssMoE(torch.nn.Module):
         if not self.ep:
             return ops.moe_experts(x, ids, w, self.w1, self.w2, ops.ACT_SWIGLU_OAI, self.alpha, self.limit,
                                    b1=self.b1, b2=self.b2)
-        # EP: all-gather tokens + routing, compute local experts, reduce-scatter
-        xs = ep_all_gather(x)
-        ids_all = ep_all_gather(ids)
-        w_all = ep_all_gather(w)
+        fn = lambda xx, ii, ww: ops.moe_experts(xx, ii, ww, self.w1, self.w2, ops.ACT_SWIGLU_OAI,  # noqa: E731
+                                                self.alpha, self.limit, b1=self.b1, b2=self.b2)
+        if self.dp_ep:  # DP+EP: all-gather/reduce-scatter or all-to-all dispatch/combine
+            return moe_ep(x, ids, w, self.E_local, fn)
+        # EP over TP ranks (tokens replicated): local experts only, then one all-reduce.
+        # b2 is added once per (token, expert) by the owner rank, so the sum stays exact.
         lo = self.ep_rank * self.E_local
-        local = (ids_all >= lo) & (ids_all < lo + self.E_local)
-        lids = torch.where(local, ids_all - lo, torch.full_like(ids_all, -1))
-        lw = torch.where(local, w_all, torch.zeros_like(w_all))
-        y = ops.moe_experts(xs, lids, lw, self.w1, self.w2, ops.ACT_SWIGLU_OAI, self.alpha, self.limit,
-                            b1=self.b1, b2=self.b2)
-        return ep_reduce_scatter(y)
+        local = (ids >= lo) & (ids < lo + self.E_local)
+        y = fn(x, torch.where(local, ids - lo, torch.full_like(ids, -1)), torch.where(local, w, torch.zeros_like(w)))
+        return tp_all_reduce(y)
 
 
 class GptOssDecoderLayer(LlamaDecoderLayer):
@@ -82,3 +84,14 @@ class GptOssDecoderLayer(LlamaDecoderLayer):
 
 class GptOssForCausalLM(LlamaForCausalLM):
     layer_cls = GptOssDecoderLayer
+
+    def _mlp_specs(self, pre: str, mlp) -> list:
+        """HF gpt-oss MoE tensors: router.{weight,bias}, experts.gate_up_proj [E, d, 2F]
+        (gate/up interleaved columns), experts.down_proj [E, F, d] (+ biases)."""
+        lo, n = mlp.ep_rank * mlp.E_local, mlp.E_local
+        return [(pre + "mlp.router.weight", mlp.router_w, "replicate", None),
+                (pre + "mlp.router.bias", mlp.router_b, "replicate", None),
+                (pre + "mlp.experts.gate_up_proj", mlp.w1, "experts_t", (lo, n)),
+                (pre + "mlp.experts.gate_up_proj_bias", mlp.b1, "experts", (lo, n)),
+                (pre + "mlp.experts.down_proj", mlp.w2, "experts_t", (lo, n)),
+                (pre + "mlp.experts.down_proj_bias", mlp.b2, "experts", (lo, n))]

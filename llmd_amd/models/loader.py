@@ -11,6 +11,8 @@ checkpoint tensor maps onto this rank's shard:
   vocab                rows [rank*per, rank*per+per) of a vocab-parallel table
                        (zero-padded past the vocabulary)
   rows                 rows start::step of the param (gate/up interleaving of MoE w1)
+  experts(_t)          rows [lo, lo+n) of a stacked [E, ...] expert tensor (optionally
+                       transposed per expert: HF gpt-oss stores [E, in, out])
   fused                a slice [off, off+len) of a fused column-parallel param
                        (q|k|v or gate|up); ``extra = (off, n_heads_total,
                        head_rows)`` - heads are split across ranks, KV heads
@@ -66,6 +68,10 @@ def place(param: torch.Tensor, full: torch.Tensor, kind: str, extra=None):
             off, n_heads, head_rows = extra
             part = _shard_heads(full, n_heads, head_rows, tp, rank)
             param[off:off + part.shape[0]].copy_(part)
+        elif kind in ("experts", "experts_t"):  # [E, ...] stacked experts -> this rank's slice
+            lo, n = extra
+            part = full[lo:lo + n]
+            param.copy_(part.transpose(1, 2) if kind == "experts_t" else part)
         elif kind == "rows":  # interleaved rows (gate/up pairs of a fused expert weight)
             start, step = extra
             param[start::step].copy_(full)
@@ -106,6 +112,8 @@ def export_hf(model: torch.nn.Module) -> dict[str, torch.Tensor]:
         elif kind == "rows":
             start, step = extra
             out[name] = p[start::step].detach().cpu().clone()
+        elif kind == "experts_t":
+            out[name] = p.transpose(1, 2).detach().cpu().contiguous()
         else:
             out[name] = p.detach().cpu().clone()
     return out

@@ -49,11 +49,15 @@ class AsyncEngine:
         try:
             while not self.stop_flag:
                 self._apply_cmds()
-                if eng.has_unfinished() and not eng.paused:
+                # DP-lockstep (wide-EP) ranks step even when idle: busy peers need
+                # this rank in every MoE collective
+                if (eng.has_unfinished() or getattr(eng, "dp_lockstep", False)) and not eng.paused:
                     outs = eng.step()
                     for o in outs:
                         self._emit(o)
-                    if eng.last_step_empty:
+                    if getattr(eng, "dp_lockstep", False) and eng.last_global_idle:
+                        time.sleep(0.001)
+                    elif eng.last_step_empty:
                         # only remote-KV waits pending: do not spin
                         time.sleep(0.0005)
                     if eng.connector is not None:
