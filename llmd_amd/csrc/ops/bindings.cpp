@@ -42,6 +42,8 @@ int llmd_mla_rope_cache(const void*, int64_t, void*, int64_t, const void*, int64
                         const int64_t*, const float*, int, int, const int64_t*, void*, int64_t, int, hipStream_t);
 int llmd_lora_bgmv(const void*, int64_t, const void*, const void*, int, int, int, int, const int*, float*, void*,
                    int64_t, hipStream_t);
+int llmd_skinny_gemm(const void*, int64_t, const void*, int64_t, int, int, int, int, void*, int64_t, float*,
+                     hipStream_t);
 int llmd_vmm_granularity(int, size_t*);
 int llmd_vmm_alloc(int, size_t, int, void**, uint64_t*);
 int llmd_vmm_export_fd(uint64_t, int*);
@@ -250,6 +252,24 @@ void lora_bgmv(torch::Tensor y, torch::Tensor x, torch::Tensor A, torch::Tensor 
   int rc = llmd_lora_bgmv(x.data_ptr(), x.stride(0), A.data_ptr(), B.data_ptr(), T, R, in, out, slot.data_ptr<int>(),
                           h.data_ptr<float>(), y.data_ptr(), y.stride(0), cur_stream());
   TORCH_CHECK(rc == 0, "lora_bgmv failed: ", rc);
+}
+
+// y [M, N] = x [M, K] . w [N, K]^T for M <= 64 (decode GEMMs), nsplit-way split-K
+void skinny_gemm(torch::Tensor y, torch::Tensor x, torch::Tensor w, int64_t nsplit, torch::Tensor part) {
+  const c10::hip::OptionalHIPGuard device_guard(dev_of(y));
+  CHECK_CUDA(x); CHECK_BF16(x); CHECK_BF16(w); CHECK_BF16(y); CHECK_INNER(x); CHECK_INNER(w); CHECK_INNER(y);
+  TORCH_CHECK(x.dim() == 2 && w.dim() == 2 && y.dim() == 2, "skinny_gemm: 2-D operands");
+  const int M = x.size(0), K = x.size(1), N = w.size(0);
+  TORCH_CHECK(M >= 1 && M <= 64 && w.size(1) == K && K % 128 == 0, "skinny_gemm: M <= 64, K % 128 == 0");
+  TORCH_CHECK(y.size(0) == M && y.size(1) == N, "skinny_gemm: output shape");
+  TORCH_CHECK(x.stride(0) % 8 == 0 && w.stride(0) % 8 == 0 && y.stride(0) % 4 == 0, "skinny_gemm: row alignment");
+  if (nsplit > 1) {
+    CHECK_DT(part, at::kFloat);
+    TORCH_CHECK(part.numel() >= nsplit * (int64_t)M * N, "skinny_gemm: workspace");
+  }
+  int rc = llmd_skinny_gemm(x.data_ptr(), x.stride(0), w.data_ptr(), w.stride(0), M, N, K, (int)nsplit, y.data_ptr(),
+                            y.stride(0), nsplit > 1 ? part.data_ptr<float>() : nullptr, cur_stream());
+  TORCH_CHECK(rc == 0, "skinny_gemm failed: ", rc);
 }
 
 void paged_prefill(torch::Tensor out, torch::Tensor q, torch::Tensor k_cache,
@@ -504,6 +524,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("kvx_ipc_open", &kvx_ipc_open);
   m.def("kvx_ipc_close", &kvx_ipc_close);
   m.def("mla_attention", &mla_attention);
+  m.def("skinny_gemm", &skinny_gemm);
   m.def("lora_bgmv", &lora_bgmv);
   m.def("mla_rope_cache", &mla_rope_cache);
   m.def("vmm_granularity", &vmm_granularity);

@@ -79,9 +79,7 @@ class ModelRunner:
         self.num_blocks = 0
         self.graphs: dict[int, tuple] = {}
         self._rng = np.random.default_rng(cfg.seed)
-        # graph-mode decode split plan: fixed for all buckets
-        split = max(512, math.ceil(self.max_model_len / 32 / 64) * 64)
-        self.graph_split = (split, math.ceil(self.max_model_len / split))
+        self.graph_plans: dict[int, tuple] = {}
 
     # ------------------------------------------------------------ KV cache
     def block_bytes(self) -> int:
@@ -400,14 +398,19 @@ class ModelRunner:
             buckets.append(self._bucket(maxb))
         M = buckets[-1]
         dev = self.device
-        split_size, nsplit = self.graph_split
+        # per-bucket split plans (valid up to max_model_len): large buckets get few
+        # long splits, small ones many - one fixed plan for all buckets starved the
+        # big batches (2.6 TB/s KV read at batch 64 vs 4.7 with a sized plan)
+        self.graph_plans = {B: ops.decode_split_plan(self.max_model_len, B, self.Hkv, self.Hq // self.Hkv)
+                            for B in buckets}
+        ws_rows = max(B * p[1] for B, p in self.graph_plans.items())
         self.g_ids = torch.zeros(M, dtype=torch.long, device=dev)
         self.g_pos = torch.zeros(M, dtype=torch.long, device=dev)
         self.g_slots = torch.full((M,), -1, dtype=torch.long, device=dev)
         self.g_bt = torch.zeros(M, self.width, dtype=torch.int32, device=dev)
         self.g_len = torch.ones(M, dtype=torch.int32, device=dev)
-        self.g_ws = (torch.empty(M * self.Hq * nsplit * self.D, dtype=torch.float32, device=dev),
-                     torch.empty(M * self.Hq * nsplit * 2, dtype=torch.float32, device=dev))
+        self.g_ws = (torch.empty(ws_rows * self.Hq * self.D, dtype=torch.float32, device=dev),
+                     torch.empty(ws_rows * self.Hq * 2, dtype=torch.float32, device=dev))
         if self.is_mla:  # fixed per-bucket latent-attention split plans + one shared workspace
             self.g_rows = torch.arange(M, dtype=torch.int32, device=dev)
             self.mla_plans = {B: ops.mla_split_plan(self.max_model_len, B, self.Hq) for B in buckets}
@@ -419,7 +422,7 @@ class ModelRunner:
         for B in reversed(buckets):
             meta = AttnMeta(num_tokens=B, positions=self.g_pos[:B], slot_mapping=self.g_slots[:B],
                             num_decode=B, d_block_tables=self.g_bt[:B], d_seq_lens=self.g_len[:B],
-                            d_split=self.graph_split, d_workspace=self.g_ws, d_max_ctx=self.max_model_len)
+                            d_split=self.graph_plans[B], d_workspace=self.g_ws, d_max_ctx=self.max_model_len)
             if self.is_mla:
                 meta.mla_d_rows, meta.mla_split, meta.mla_workspace = self.g_rows[:B], self.mla_plans[B], self.g_mla_ws
             s = torch.cuda.Stream()

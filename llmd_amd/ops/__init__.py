@@ -8,6 +8,7 @@ from __future__ import annotations
 
 import math
 import os
+from typing import Optional
 
 import torch
 
@@ -311,3 +312,32 @@ def lora_bgmv(y, x, A, B, slot, h=None):
         h = torch.empty(x.shape[0] * A.shape[1], dtype=torch.float32, device=x.device)
     native().lora_bgmv(y, x, A, B, slot, h)
     return y
+
+
+SKINNY_MAX_M = 64
+
+
+def skinny_splits(M: int, N: int, K: int, target_wgs: int = 512) -> int:
+    tiles = (N + 255) // 256
+    return max(1, min(K // 128, math.ceil(target_wgs / tiles)))
+
+
+def linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Dense projection: decode-sized M (<= 64) on the skinny MFMA stream kernel
+    (csrc/ops/skinny_gemm.hip), everything else on hipBLASLt."""
+    M = x.shape[0] if x.dim() == 2 else -1
+    if (_gpu(x) and _SKINNY and 1 <= M <= SKINNY_MAX_M and x.shape[1] % 128 == 0 and x.dtype == torch.bfloat16
+            and x.stride(-1) == 1 and x.stride(0) % 8 == 0 and w.is_contiguous()):
+        N, K = w.shape
+        y = torch.empty(M, N, dtype=x.dtype, device=x.device)
+        ns = skinny_splits(M, N, K)
+        part = torch.empty(ns * M * N if ns > 1 else 0, dtype=torch.float32, device=x.device)
+        native().skinny_gemm(y, x, w, ns, part)
+        return y if bias is None else y.add_(bias)
+    return torch.nn.functional.linear(x, w, bias)
+
+
+# off by default: hipBLASLt streams W at 5.3-6.1 TB/s for most decode shapes
+# (profiles/skinny_gemm_vs_hipblaslt.txt); the skinny kernel only wins on
+# the K=28672 down projection at M=64
+_SKINNY = os.environ.get("LLMD_SKINNY_GEMM", "0") == "1"

@@ -1,0 +1,48 @@
+"""Decode-only step time of one engine (the P/D decode rank's job): B
+sequences at context ~ISL decode with hipGraphs; prints ms/step and tok/s.
+  python scripts/bench_decode.py [--model llama-3-70b] [--batch 64] [--isl 5000] [--steps 50]"""
+import argparse
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+from llmd_amd.engine.config import EngineConfig  # noqa: E402
+from llmd_amd.engine.engine import LLMEngine  # noqa: E402
+from llmd_amd.engine.request import SamplingParams  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--model", default="llama-3-70b")
+    ap.add_argument("--batch", type=int, default=64)
+    ap.add_argument("--isl", type=int, default=5000)
+    ap.add_argument("--steps", type=int, default=50)
+    a = ap.parse_args()
+    cfg = EngineConfig.create(a.model, device="cuda", block_size=64, max_num_seqs=a.batch,
+                              max_num_batched_tokens=8192, max_model_len=a.isl + a.steps + 200,
+                              cuda_graph_max_bs=a.batch)
+    eng = LLMEngine(cfg)
+    rng = np.random.default_rng(0)
+    sp = SamplingParams(max_tokens=a.steps + 20, temperature=0.0, ignore_eos=True)
+    for i in range(a.batch):
+        eng.add_request(f"r{i}", rng.integers(100, 30000, size=a.isl).tolist(), sp)
+    while eng.sched.num_waiting or any(not r.output_token_ids for r in eng.sched.running):
+        eng.step()
+    for _ in range(5):
+        eng.step()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        eng.step()
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / a.steps
+    print(f"{a.model} decode batch={a.batch} ctx~{a.isl}: {dt * 1e3:.2f} ms/step  {a.batch / dt:.0f} tok/s", flush=True)
+
+
+if __name__ == "__main__":
+    main()
