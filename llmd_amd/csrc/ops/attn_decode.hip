@@ -97,19 +97,27 @@ __global__ __launch_bounds__(NT, 2) void paged_decode_kernel(
   char* vimg = smem + w * (64 * D * 2);
   const int ntile = (s1 - s0 + 63) >> 6;
 
-  for (int t = w; t < ntile; t += 4) {
-    const int ts = s0 + 64 * t;
-    // ---- issue K loads (A operand rows, permuted by rowoff) and V loads
-    u32x4_t kf[4][KS];
+  // K of tile t is loaded one iteration ahead (issued right after the
+  // previous tile's S product retires its registers), V of tile t is issued
+  // at the top of the iteration: its latency hides behind S + softmax, K's
+  // behind the whole previous PV. Register footprint stays one K + one V set.
+  u32x4_t kf[4][KS];
+  auto load_k = [&](int tt) {
+    const int tts = s0 + 64 * tt;
 #pragma unroll
     for (int b4 = 0; b4 < 4; ++b4) {
-      int key = ts + 16 * b4 + rowoff(c16 >> 2) + (c16 & 3);
+      int key = tts + 16 * b4 + rowoff(c16 >> 2) + (c16 & 3);
       key = key < s1 ? key : s0;
       const int phys = bt[key / bs];
       const uint16_t* kr = kc + (int64_t)phys * block_stride + head_off + (int64_t)(key % bs) * D;
 #pragma unroll
       for (int s = 0; s < KS; ++s) kf[b4][s] = *reinterpret_cast<const u32x4_t*>(kr + (4 * s + g) * 8);
     }
+  };
+  if (w < ntile) load_k(w);
+
+  for (int t = w; t < ntile; t += 4) {
+    const int ts = s0 + 64 * t;
     u32x4_t vr[VLD];
 #pragma unroll
     for (int i = 0; i < VLD; ++i) {
@@ -131,6 +139,7 @@ __global__ __launch_bounds__(NT, 2) void paged_decode_kernel(
                                                       qf[s], acc, 0, 0, 0);
       sc[b4] = acc;
     }
+    if (t + 4 < ntile) load_k(t + 4);
     // ---- online softmax (log2 domain); element i of group g is key ts+16*b4+rowoff(g)+i
     float mx = NEG_INF;
 #pragma unroll
