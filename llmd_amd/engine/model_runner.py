@@ -54,6 +54,12 @@ class ModelRunner:
             self.device = torch.device("cuda", torch.cuda.current_device())
         self.is_gpu = self.device.type == "cuda"
         self.tp_size = get_state().tp_size
+        if self.is_gpu:
+            from llmd_amd.ops.gemm_tuning import enable_lookup
+
+            tuned = enable_lookup()
+            if tuned:
+                log.info("GEMM selection from %s", tuned)
         self.bs = cfg.cache.block_size
         self.max_model_len = cfg.sched.max_model_len
         self.width = math.ceil(self.max_model_len / self.bs) + 1
