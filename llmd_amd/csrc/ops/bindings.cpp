@@ -59,6 +59,20 @@ void llmd_moe_gemm(const void*, int64_t, int, const int*, const int*, int, const
                    void*, int64_t, int, int, float, float, int, const void*, hipStream_t);
 void llmd_moe_combine(const void*, int64_t, const int*, const float*, int, int, int, void*, int64_t,
                       hipStream_t);
+int llmd_symm_alloc(size_t, void**);
+int llmd_symm_free(void*);
+int64_t llmd_symm_sig_bytes();
+int llmd_symm_grid();
+int llmd_symm_max_ranks();
+int llmd_symm_channels();
+int llmd_symm_error(const void*, uint32_t*);
+int llmd_symm_clear_error(void*);
+int llmd_symm_all_reduce(const int64_t*, int, int, int, int, int64_t, int64_t, const void*, void*, int64_t,
+                         hipStream_t);
+int llmd_symm_ep_dispatch(const int64_t*, int, int, int, const int64_t*, const void*, int64_t, const int*,
+                          const float*, int, int, int, int, int, hipStream_t);
+int llmd_symm_ep_combine(const int64_t*, int, int, int, const int64_t*, const void*, int64_t, const int*, int, int,
+                         int, int, int, void*, int64_t, hipStream_t);
 }
 
 namespace {
@@ -505,6 +519,77 @@ void moe_combine(torch::Tensor Y, torch::Tensor inv, torch::Tensor w, int64_t to
                    out.data_ptr(), out.stride(0), cur_stream());
 }
 
+// ---------------------------------------------------------------- symm heap
+torch::Tensor symm_alloc(int64_t bytes, int64_t device) {
+  const c10::hip::HIPGuard guard((c10::DeviceIndex)device);
+  TORCH_CHECK(bytes > llmd_symm_sig_bytes() && bytes % 4096 == 0, "symm_alloc: size");
+  void* p = nullptr;
+  int rc = llmd_symm_alloc((size_t)bytes, &p);
+  TORCH_CHECK(rc == 0, "symm_alloc (hipExtMallocWithFlags uncached) failed: ", rc);
+  return torch::from_blob(p, {bytes}, [](void* q) { llmd_symm_free(q); },
+                          torch::TensorOptions().dtype(torch::kUInt8).device(torch::kCUDA, (c10::DeviceIndex)device));
+}
+
+int64_t symm_error(torch::Tensor heap, bool clear) {
+  const c10::hip::OptionalHIPGuard device_guard(dev_of(heap));
+  uint32_t e = 0;
+  TORCH_CHECK(llmd_symm_error(heap.data_ptr(), &e) == 0, "symm_error: copy failed");
+  if (clear) llmd_symm_clear_error(heap.data_ptr());
+  return (int64_t)e;
+}
+
+void check_bases(const std::vector<int64_t>& bases, int64_t rank) {
+  TORCH_CHECK((int)bases.size() >= 1 && (int)bases.size() <= llmd_symm_max_ranks(), "symm: 1..8 ranks");
+  TORCH_CHECK(rank >= 0 && rank < (int64_t)bases.size(), "symm: rank");
+  for (auto b : bases) TORCH_CHECK(b != 0 && b % 256 == 0, "symm: bad peer base");
+}
+
+void symm_all_reduce(std::vector<int64_t> bases, int64_t rank, int64_t ch, int64_t mode, int64_t data_off,
+                     int64_t slot_bytes, torch::Tensor inp, torch::Tensor out) {
+  const c10::hip::OptionalHIPGuard device_guard(dev_of(inp));
+  check_bases(bases, rank);
+  CHECK_CUDA(inp); CHECK_BF16(inp); CHECK_BF16(out);
+  TORCH_CHECK(inp.is_contiguous() && out.is_contiguous() && inp.numel() == out.numel(), "all_reduce: contiguous");
+  TORCH_CHECK(inp.numel() % 8 == 0, "all_reduce: numel % 8");
+  TORCH_CHECK(data_off >= llmd_symm_sig_bytes() && (mode == 1 || mode == 2), "all_reduce: layout/mode");
+  int rc = llmd_symm_all_reduce(bases.data(), (int)bases.size(), (int)rank, (int)ch, (int)mode, data_off, slot_bytes,
+                                inp.data_ptr(), out.data_ptr(), inp.numel() / 8, cur_stream());
+  TORCH_CHECK(rc == 0, "symm_all_reduce failed: ", rc);
+}
+
+void symm_ep_dispatch(std::vector<int64_t> bases, int64_t rank, int64_t ch, std::vector<int64_t> layout,
+                      torch::Tensor x, torch::Tensor ids, torch::Tensor w, int64_t R, int64_t E_local) {
+  const c10::hip::OptionalHIPGuard device_guard(dev_of(x));
+  check_bases(bases, rank);
+  CHECK_CUDA(x); CHECK_BF16(x); CHECK_INNER(x); CHECK_DT(ids, at::kInt); CHECK_DT(w, at::kFloat);
+  TORCH_CHECK(layout.size() == 5, "ep layout");
+  const int T = x.size(0), d = x.size(1);
+  TORCH_CHECK(ids.dim() == 2 && ids.is_contiguous() && w.sizes() == ids.sizes() && w.is_contiguous() &&
+                  ids.size(0) == T, "ep_dispatch: ids/w [T, k]");
+  const int k = ids.size(1);
+  TORCH_CHECK(T <= R && d % 8 == 0 && k <= 64 && x.stride(0) % 8 == 0, "ep_dispatch shape");
+  int rc = llmd_symm_ep_dispatch(bases.data(), (int)bases.size(), (int)rank, (int)ch, layout.data(), x.data_ptr(),
+                                 x.stride(0), ids.data_ptr<int>(), w.data_ptr<float>(), T, (int)R, d, k, (int)E_local,
+                                 cur_stream());
+  TORCH_CHECK(rc == 0, "symm_ep_dispatch failed: ", rc);
+}
+
+void symm_ep_combine(std::vector<int64_t> bases, int64_t rank, int64_t ch, std::vector<int64_t> layout,
+                     torch::Tensor y, torch::Tensor ids, int64_t R, int64_t E_local, torch::Tensor out) {
+  const c10::hip::OptionalHIPGuard device_guard(dev_of(y));
+  check_bases(bases, rank);
+  CHECK_CUDA(y); CHECK_BF16(y); CHECK_BF16(out); CHECK_INNER(y); CHECK_INNER(out); CHECK_DT(ids, at::kInt);
+  TORCH_CHECK(layout.size() == 5, "ep layout");
+  const int T = out.size(0), d = out.size(1);
+  TORCH_CHECK(ids.dim() == 2 && ids.is_contiguous() && ids.size(0) == T, "ep_combine: ids [T, k]");
+  TORCH_CHECK(y.size(0) == (int64_t)bases.size() * R && y.size(1) >= d && d % 8 == 0 && T <= R, "ep_combine shape");
+  TORCH_CHECK(y.stride(0) % 8 == 0 && out.stride(0) % 8 == 0, "16-B aligned rows");
+  int rc = llmd_symm_ep_combine(bases.data(), (int)bases.size(), (int)rank, (int)ch, layout.data(), y.data_ptr(),
+                                y.stride(0), ids.data_ptr<int>(), T, (int)R, d, (int)ids.size(1), (int)E_local,
+                                out.data_ptr(), out.stride(0), cur_stream());
+  TORCH_CHECK(rc == 0, "symm_ep_combine failed: ", rc);
+}
+
 }  // namespace
 
 PYBIND11_MODULE(_C, m) {
@@ -536,4 +621,12 @@ PYBIND11_MODULE(_C, m) {
   m.def("moe_gemm", &moe_gemm);
   m.def("moe_combine", &moe_combine);
   m.def("moe_tile_m", &llmd_moe_gemm_tile_m);
+  m.def("symm_alloc", &symm_alloc);
+  m.def("symm_error", &symm_error);
+  m.def("symm_sig_bytes", &llmd_symm_sig_bytes);
+  m.def("symm_grid", &llmd_symm_grid);
+  m.def("symm_channels", &llmd_symm_channels);
+  m.def("symm_all_reduce", &symm_all_reduce);
+  m.def("symm_ep_dispatch", &symm_ep_dispatch);
+  m.def("symm_ep_combine", &symm_ep_combine);
 }

@@ -241,6 +241,7 @@ class ParallelConfig:
     enable_expert_parallel: bool = False
     distributed_backend: str = "nccl"
     all2all_backend: str = "allgather_reducescatter"  # wide-EP token exchange (parallel/ep.py)
+    disable_custom_all_reduce: bool = False  # TP all-reduce over the symm IPC heap (parallel/symm.py)
 
 
 @dataclass
@@ -317,7 +318,9 @@ def add_engine_args(p: argparse.ArgumentParser) -> argparse.ArgumentParser:
     p.add_argument("--data-parallel-rank", type=int, default=0)
     p.add_argument("--enable-expert-parallel", action="store_true")
     p.add_argument("--all2all-backend", default="allgather_reducescatter",
-                   choices=["allgather_reducescatter", "alltoall"])
+                   choices=["allgather_reducescatter", "alltoall", "symm_ll", "deepep_low_latency",
+                            "deepep_high_throughput"])
+    p.add_argument("--disable-custom-all-reduce", action="store_true")
     p.add_argument("--enforce-eager", action="store_true")
     p.add_argument("--kv-transfer-config", type=_json_arg, default=None)
     p.add_argument("--kv-events-config", type=_json_arg, default=None)
@@ -341,6 +344,7 @@ def engine_config_from_args(a) -> EngineConfig:
         tensor_parallel_size=a.tensor_parallel_size, data_parallel_size=a.data_parallel_size,
         data_parallel_rank=a.data_parallel_rank, enable_expert_parallel=a.enable_expert_parallel,
         all2all_backend=getattr(a, "all2all_backend", "allgather_reducescatter"),
+        disable_custom_all_reduce=getattr(a, "disable_custom_all_reduce", False),
         enforce_eager=a.enforce_eager, kv_transfer_config=a.kv_transfer_config,
         kv_events_config=a.kv_events_config, kv_offload_config=a.kv_offload_config,
         policy=a.scheduling_policy, enable_lora=getattr(a, "enable_lora", False),

@@ -86,6 +86,26 @@ class ModelRunner:
         self.graphs: dict[int, tuple] = {}
         self._rng = np.random.default_rng(cfg.seed)
         self.graph_plans: dict[int, tuple] = {}
+        self._init_symm()
+
+    def _init_symm(self):
+        """Symmetric IPC heap users (parallel/symm.py): the TP custom all-reduce
+        and the wide-EP low-latency dispatch/combine. Collective: every rank of
+        the group constructs its runner, so the handle exchange lines up."""
+        if not self.is_gpu:
+            return
+        from llmd_amd.parallel import ep as ep_mod
+        from llmd_amd.parallel import symm
+
+        st = get_state()
+        pc = self.cfg.parallel
+        if self.tp_size > 1 and not pc.disable_custom_all_reduce and symm.enabled_by_env():
+            symm.init(st.tp_rank, st.tp_size, group=st.tp_cpu_group, tp_allreduce=True)
+        elif (ep_mod.canonical(pc.all2all_backend) == "symm_ll" and st.dp_size > 1 and st.tp_size == 1
+              and self.mc.is_moe):
+            rows = max(self.cfg.cuda_graph_max_bs, 256)
+            symm.init(st.ep_rank, st.ep_size, group=st.cpu_group, ep_rows=rows, hidden=self.mc.hidden_size,
+                      topk=self.mc.num_experts_per_tok)
 
     # ------------------------------------------------------------ KV cache
     def block_bytes(self) -> int:

@@ -16,6 +16,13 @@ Each rank owns E / EP experts and its own tokens. Two exchange backends:
   Moves ~(distinct ranks per token)/EP of the all-gather volume; needs the
   split sizes on the host (one small count exchange per layer), so eager only.
 
+* ``symm_ll`` (alias ``deepep_low_latency``): the HIP dispatch/combine
+  kernels over the symmetric IPC heap (parallel/symm.py) for steps of at most
+  the heap's row capacity: each token row is pushed straight into the
+  owning ranks' receive buffers over xGMI (7 links at once), fixed shapes, so
+  decode graphs capture it. Larger (prefill) steps fall back to ``alltoall``
+  eagerly - the reference's LL-for-decode / HT-for-prefill split.
+
 ``expert_fn(x, local_ids, weights) -> y`` computes the weighted sum over the
 given local experts (-1 ids are skipped).
 """
@@ -26,13 +33,19 @@ import torch.distributed as dist
 
 from .state import get_state
 
-BACKENDS = ("allgather_reducescatter", "alltoall")
+BACKENDS = ("allgather_reducescatter", "alltoall", "symm_ll")
+ALIASES = {"deepep_low_latency": "symm_ll", "deepep_high_throughput": "alltoall"}
 _backend = "allgather_reducescatter"
 _step_rows = 0  # max token rows of this step over the EP group (DP coordinator)
 
 
+def canonical(name: str) -> str:
+    return ALIASES.get(name, name)
+
+
 def set_backend(name: str):
     global _backend
+    name = canonical(name)
     if name not in BACKENDS:
         raise ValueError(f"all2all backend must be one of {BACKENDS}")
     _backend = name
@@ -54,7 +67,14 @@ def ep_active() -> bool:
 
 def moe_ep(x: torch.Tensor, ids: torch.Tensor, w: torch.Tensor, E_local: int, expert_fn) -> torch.Tensor:
     capturing = x.is_cuda and torch.cuda.is_current_stream_capturing()
-    if _backend == "alltoall" and not capturing:
+    if _backend == "symm_ll" and x.is_cuda:
+        from . import symm
+
+        sep = symm.ep()
+        R = max(x.shape[0], _step_rows)
+        if sep is not None and R <= sep.R_max:
+            return sep.moe(x, ids, w, E_local, R, expert_fn)
+    if _backend in ("alltoall", "symm_ll") and not capturing:
         return _alltoall(x, ids, w, E_local, expert_fn)
     return _allgather(x, ids, w, E_local, expert_fn)
 
