@@ -47,6 +47,62 @@ __device__ __forceinline__ u32x4_t pack8(const float* f) {
   return v;
 }
 
+// ---- FP8 (OCP e4m3fn on gfx950). KV-cache / activation storage
+// format; math stays bf16/f32. Scales are applied outside (folded into the
+// softmax scale / output), so conversions here are unscaled.
+constexpr float FP8_MAX = 448.f;
+
+// 8 floats -> 8 e4m3fn bytes (saturating: v_cvt_pk_fp8_f32 alone would map
+// |x| > 448 to NaN).
+__device__ __forceinline__ u32x2_t f32x8_to_fp8(const float* f) {
+  float c[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) c[i] = fminf(fmaxf(f[i], -FP8_MAX), FP8_MAX);
+  u32x2_t r;
+  int lo = __builtin_amdgcn_cvt_pk_fp8_f32(c[0], c[1], 0, false);
+  r[0] = (uint32_t)__builtin_amdgcn_cvt_pk_fp8_f32(c[2], c[3], lo, true);
+  int hi = __builtin_amdgcn_cvt_pk_fp8_f32(c[4], c[5], 0, false);
+  r[1] = (uint32_t)__builtin_amdgcn_cvt_pk_fp8_f32(c[6], c[7], hi, true);
+  return r;
+}
+
+typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+
+// 8 e4m3fn bytes -> 8 bf16 (exact: every e4m3 value is representable in bf16)
+__device__ __forceinline__ u32x4_t fp8x8_to_bf16x8(const u32x2_t v) {
+  u32x4_t r;
+  r[0] = __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(v[0], 1.f, false));
+  r[1] = __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(v[0], 1.f, true));
+  r[2] = __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(v[1], 1.f, false));
+  r[3] = __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(v[1], 1.f, true));
+  return r;
+}
+
+// Load 8 consecutive cache elements as 8 bf16 (16 B), from a bf16 or fp8 cache.
+template <bool F8>
+__device__ __forceinline__ u32x4_t load8_as_bf16(const void* base, int64_t elem_off) {
+  if constexpr (F8) {
+    return fp8x8_to_bf16x8(*reinterpret_cast<const u32x2_t*>(reinterpret_cast<const uint8_t*>(base) + elem_off));
+  } else {
+    return *reinterpret_cast<const u32x4_t*>(reinterpret_cast<const uint16_t*>(base) + elem_off);
+  }
+}
+
+// Store 8 bf16 (packed in 16 B) to a bf16 or fp8 cache at element offset;
+// fp8 stores multiply by inv_scale first.
+template <bool F8>
+__device__ __forceinline__ void store8_from_bf16(void* base, int64_t elem_off, const u32x4_t v, float inv_scale) {
+  if constexpr (F8) {
+    float f[8];
+    unpack8(v, f);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) f[i] *= inv_scale;
+    *reinterpret_cast<u32x2_t*>(reinterpret_cast<uint8_t*>(base) + elem_off) = f32x8_to_fp8(f);
+  } else {
+    *reinterpret_cast<u32x4_t*>(reinterpret_cast<uint16_t*>(base) + elem_off) = v;
+  }
+}
+
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);

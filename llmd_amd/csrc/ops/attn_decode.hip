@@ -46,14 +46,43 @@ __device__ __forceinline__ int vimg_off(int row, int ch) {
   }
 }
 
-template <int D>
+// Raw cache registers: bf16 keeps 16 B per 8 elements, fp8 (e4m3fn) 8 B. fp8
+// values stay packed while their loads are in flight and are widened to bf16
+// (exact) right before the MFMA / LDS staging, so the prefetch distance is
+// unchanged and the K/V bytes read from HBM halve. k_scale is folded into the
+// softmax scale on the host, v_scale into the output (`vscale`).
+template <bool F8>
+struct CacheReg {
+  using T = u32x4_t;
+};
+template <>
+struct CacheReg<true> {
+  using T = u32x2_t;
+};
+template <bool F8>
+__device__ __forceinline__ typename CacheReg<F8>::T ld_cache(const void* base, int64_t off) {
+  if constexpr (F8)
+    return *reinterpret_cast<const u32x2_t*>(reinterpret_cast<const uint8_t*>(base) + off);
+  else
+    return *reinterpret_cast<const u32x4_t*>(reinterpret_cast<const uint16_t*>(base) + off);
+}
+template <bool F8>
+__device__ __forceinline__ u32x4_t widen(const typename CacheReg<F8>::T v) {
+  if constexpr (F8)
+    return fp8x8_to_bf16x8(v);
+  else
+    return v;
+}
+
+template <int D, bool F8>
 __global__ __launch_bounds__(NT, 2) void paged_decode_kernel(
-    const uint16_t* __restrict__ q, int64_t q_stride, const uint16_t* __restrict__ kc,
-    const uint16_t* __restrict__ vc, int64_t block_stride, int bs,
+    const uint16_t* __restrict__ q, int64_t q_stride, const void* __restrict__ kc,
+    const void* __restrict__ vc, int64_t block_stride, int bs,
     const int* __restrict__ block_tables, int bt_stride, const int* __restrict__ seq_lens,
     int Hq, int Hkv, int G, int NG, float scale_log2, int window,
     const float* __restrict__ sinks, int split_size, int nsplit, uint16_t* __restrict__ out,
-    int64_t out_stride, float* __restrict__ part_o, float* __restrict__ part_ml) {
+    int64_t out_stride, float* __restrict__ part_o, float* __restrict__ part_ml, float vscale) {
+  using CR = typename CacheReg<F8>::T;
   constexpr int KS = D / 32;   // k-steps of the QK^T product
   constexpr int NB = D / 16;   // 16-wide dim blocks of the PV product
   constexpr int CPR = D / 8;   // 16-B chunks per row
@@ -101,7 +130,7 @@ __global__ __launch_bounds__(NT, 2) void paged_decode_kernel(
   // previous tile's S product retires its registers), V of tile t is issued
   // at the top of the iteration: its latency hides behind S + softmax, K's
   // behind the whole previous PV. Register footprint stays one K + one V set.
-  u32x4_t kf[4][KS];
+  CR kf[4][KS];
   auto load_k = [&](int tt) {
     const int tts = s0 + 64 * tt;
 #pragma unroll
@@ -109,24 +138,24 @@ __global__ __launch_bounds__(NT, 2) void paged_decode_kernel(
       int key = tts + 16 * b4 + rowoff(c16 >> 2) + (c16 & 3);
       key = key < s1 ? key : s0;
       const int phys = bt[key / bs];
-      const uint16_t* kr = kc + (int64_t)phys * block_stride + head_off + (int64_t)(key % bs) * D;
+      const int64_t kr = (int64_t)phys * block_stride + head_off + (int64_t)(key % bs) * D;
 #pragma unroll
-      for (int s = 0; s < KS; ++s) kf[b4][s] = *reinterpret_cast<const u32x4_t*>(kr + (4 * s + g) * 8);
+      for (int s = 0; s < KS; ++s) kf[b4][s] = ld_cache<F8>(kc, kr + (4 * s + g) * 8);
     }
   };
   if (w < ntile) load_k(w);
 
   for (int t = w; t < ntile; t += 4) {
     const int ts = s0 + 64 * t;
-    u32x4_t vr[VLD];
+    CR vr[VLD];
 #pragma unroll
     for (int i = 0; i < VLD; ++i) {
       const int row = i * RPI + lane / CPR;
       int key = ts + row;
       key = key < s1 ? key : s0;
       const int phys = bt[key / bs];
-      const uint16_t* vp = vc + (int64_t)phys * block_stride + head_off + (int64_t)(key % bs) * D;
-      vr[i] = *reinterpret_cast<const u32x4_t*>(vp + (lane % CPR) * 8);
+      const int64_t vp = (int64_t)phys * block_stride + head_off + (int64_t)(key % bs) * D;
+      vr[i] = ld_cache<F8>(vc, vp + (lane % CPR) * 8);
     }
     // ---- S^T = K Q^T
     f32x4_t sc[4];
@@ -135,7 +164,7 @@ __global__ __launch_bounds__(NT, 2) void paged_decode_kernel(
       f32x4_t acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int s = 0; s < KS; ++s)
-        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, kf[b4][s]),
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, widen<F8>(kf[b4][s])),
                                                       qf[s], acc, 0, 0, 0);
       sc[b4] = acc;
     }
@@ -180,7 +209,7 @@ __global__ __launch_bounds__(NT, 2) void paged_decode_kernel(
 #pragma unroll
     for (int i = 0; i < VLD; ++i) {
       const int row = i * RPI + lane / CPR;
-      *reinterpret_cast<u32x4_t*>(vimg + vimg_off<D>(row, lane % CPR)) = vr[i];
+      *reinterpret_cast<u32x4_t*>(vimg + vimg_off<D>(row, lane % CPR)) = widen<F8>(vr[i]);
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     // ---- O += P V
@@ -247,6 +276,7 @@ __global__ __launch_bounds__(NT, 2) void paged_decode_kernel(
       Ls += f * ml[(ww * 16 + h) * 2 + 1];
       acc += ob[(ww * 16 + h) * D + d];
     }
+    acc *= vscale;
     const int hq = h0 + h;
     if (nsplit == 1) {
       float den = Ls;
@@ -293,33 +323,30 @@ extern "C" int llmd_paged_decode(const void* q, int64_t q_stride, const void* kc
                                  int bt_stride, const int* seq_lens, int B, int Hq, int Hkv, int D,
                                  float scale, int window, const float* sinks, int split_size,
                                  int nsplit, void* out, int64_t out_stride, float* part_o,
-                                 float* part_ml, hipStream_t st) {
+                                 float* part_ml, int fp8, float k_scale, float v_scale, hipStream_t st) {
   if (B == 0) return 0;
   const int G = Hq / Hkv;
   const int NG = (G + 15) / 16;
-  const float scale_log2 = scale * 1.4426950408889634f;
+  const float scale_log2 = scale * k_scale * 1.4426950408889634f;
   dim3 grid(nsplit, Hkv * NG, B), blk(NT);
   const size_t lds = (size_t)4 * 64 * D * 2;
+#define LAUNCH(DD, F8)                                                                                    \
+  do {                                                                                                    \
+    hipLaunchKernelGGL((paged_decode_kernel<DD, F8>), grid, blk, lds, st, (const uint16_t*)q, q_stride, kc, \
+                       vc, block_stride, bs, block_tables, bt_stride, seq_lens, Hq, Hkv, G, NG, scale_log2, \
+                       window, sinks, split_size, nsplit, (uint16_t*)out, out_stride, part_o, part_ml,     \
+                       v_scale);                                                                          \
+    if (nsplit > 1)                                                                                       \
+      hipLaunchKernelGGL(decode_reduce_kernel<DD>, dim3(Hq, B), dim3(64), 0, st, part_o, part_ml, seq_lens, \
+                         Hq, nsplit, split_size, window, sinks, (uint16_t*)out, out_stride);                \
+  } while (0)
   if (D == 128) {
-    hipLaunchKernelGGL(paged_decode_kernel<128>, grid, blk, lds, st, (const uint16_t*)q, q_stride,
-                       (const uint16_t*)kc, (const uint16_t*)vc, block_stride, bs, block_tables,
-                       bt_stride, seq_lens, Hq, Hkv, G, NG, scale_log2, window, sinks, split_size,
-                       nsplit, (uint16_t*)out, out_stride, part_o, part_ml);
-    if (nsplit > 1)
-      hipLaunchKernelGGL(decode_reduce_kernel<128>, dim3(Hq, B), dim3(64), 0, st, part_o, part_ml,
-                         seq_lens, Hq, nsplit, split_size, window, sinks, (uint16_t*)out,
-                         out_stride);
+    if (fp8) LAUNCH(128, true); else LAUNCH(128, false);
   } else if (D == 64) {
-    hipLaunchKernelGGL(paged_decode_kernel<64>, grid, blk, lds, st, (const uint16_t*)q, q_stride,
-                       (const uint16_t*)kc, (const uint16_t*)vc, block_stride, bs, block_tables,
-                       bt_stride, seq_lens, Hq, Hkv, G, NG, scale_log2, window, sinks, split_size,
-                       nsplit, (uint16_t*)out, out_stride, part_o, part_ml);
-    if (nsplit > 1)
-      hipLaunchKernelGGL(decode_reduce_kernel<64>, dim3(Hq, B), dim3(64), 0, st, part_o, part_ml,
-                         seq_lens, Hq, nsplit, split_size, window, sinks, (uint16_t*)out,
-                         out_stride);
+    if (fp8) LAUNCH(64, true); else LAUNCH(64, false);
   } else {
     return -1;
   }
+#undef LAUNCH
   return 0;
 }

@@ -42,14 +42,26 @@ __device__ __forceinline__ int kimg_off(int row, int ch) {
   return row * (D * 2 + 16) + 16 * ch;
 }
 
-template <int D>
+// fp8 (e4m3fn) caches: tiles are loaded packed (8 B per 8 elements) and widened
+// to bf16 when written to LDS, so the LDS images and MFMAs are unchanged.
+template <bool F8>
+struct CacheReg {
+  using T = u32x4_t;
+};
+template <>
+struct CacheReg<true> {
+  using T = u32x2_t;
+};
+
+template <int D, bool F8>
 __global__ __launch_bounds__(NT, 2) void prefill_kernel(
-    const uint16_t* __restrict__ q, int64_t q_stride, const uint16_t* __restrict__ kc,
-    const uint16_t* __restrict__ vc, int64_t block_stride, int bs,
+    const uint16_t* __restrict__ q, int64_t q_stride, const void* __restrict__ kc,
+    const void* __restrict__ vc, int64_t block_stride, int bs,
     const int* __restrict__ block_tables, int bt_stride, const int* __restrict__ q_start,
     const int* __restrict__ q_len, const int* __restrict__ ctx_len, const int* __restrict__ items,
     int Hq, int Hkv, int G, int HPW, float scale_log2, int window,
-    const float* __restrict__ sinks, uint16_t* __restrict__ out, int64_t out_stride) {
+    const float* __restrict__ sinks, uint16_t* __restrict__ out, int64_t out_stride, float vscale) {
+  using CR = typename CacheReg<F8>::T;
   constexpr int KS = D / 32, NB = D / 16, CPR = D / 8;
   constexpr int KIMG = 64 * (D * 2 + 16);
   constexpr int VIMG = 64 * D * 2;
@@ -99,7 +111,7 @@ __global__ __launch_bounds__(NT, 2) void prefill_kernel(
     for (int n = 0; n < NB; ++n) o[nb][n] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 
   // ---- tile loader (registers)
-  u32x4_t kr[LPT], vr[LPT];
+  CR kr[LPT], vr[LPT];
   auto load_tile = [&](int t) {
     const int ts = t * 64;
 #pragma unroll
@@ -110,8 +122,13 @@ __global__ __launch_bounds__(NT, 2) void prefill_kernel(
       key = key < ctx ? key : ctx - 1;
       const int phys = bt[key / bs];
       const int64_t off = (int64_t)phys * block_stride + head_off + (int64_t)(key % bs) * D + ch * 8;
-      kr[i] = *reinterpret_cast<const u32x4_t*>(kc + off);
-      vr[i] = *reinterpret_cast<const u32x4_t*>(vc + off);
+      if constexpr (F8) {
+        kr[i] = *reinterpret_cast<const u32x2_t*>(reinterpret_cast<const uint8_t*>(kc) + off);
+        vr[i] = *reinterpret_cast<const u32x2_t*>(reinterpret_cast<const uint8_t*>(vc) + off);
+      } else {
+        kr[i] = *reinterpret_cast<const u32x4_t*>(reinterpret_cast<const uint16_t*>(kc) + off);
+        vr[i] = *reinterpret_cast<const u32x4_t*>(reinterpret_cast<const uint16_t*>(vc) + off);
+      }
     }
   };
   auto store_tile = [&](int buf) {
@@ -121,8 +138,13 @@ __global__ __launch_bounds__(NT, 2) void prefill_kernel(
     for (int i = 0; i < LPT; ++i) {
       const int idx = threadIdx.x + NT * i;
       const int row = idx / CPR, ch = idx % CPR;
-      *reinterpret_cast<u32x4_t*>(kimg + kimg_off<D>(row, ch)) = kr[i];
-      *reinterpret_cast<u32x4_t*>(vimg + vimg_off<D>(row, ch)) = vr[i];
+      if constexpr (F8) {
+        *reinterpret_cast<u32x4_t*>(kimg + kimg_off<D>(row, ch)) = fp8x8_to_bf16x8(kr[i]);
+        *reinterpret_cast<u32x4_t*>(vimg + vimg_off<D>(row, ch)) = fp8x8_to_bf16x8(vr[i]);
+      } else {
+        *reinterpret_cast<u32x4_t*>(kimg + kimg_off<D>(row, ch)) = kr[i];
+        *reinterpret_cast<u32x4_t*>(vimg + vimg_off<D>(row, ch)) = vr[i];
+      }
     }
   };
 
@@ -261,7 +283,7 @@ __global__ __launch_bounds__(NT, 2) void prefill_kernel(
   for (int nb = 0; nb < 2; ++nb) {
     float den = lsum[nb];
     if (sinks) den += exp2f(sink - (m[nb] == NEG_INF ? 0.f : m[nb]));
-    const float inv = den > 0.f ? 1.f / den : 0.f;
+    const float inv = den > 0.f ? vscale / den : 0.f;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const float f = __shfl(inv, 4 * g + i, 64);
@@ -282,37 +304,35 @@ extern "C" int llmd_paged_prefill(const void* q, int64_t q_stride, const void* k
                                   int bt_stride, const int* q_start, const int* q_len,
                                   const int* ctx_len, const int* items, int n_items, int Hq,
                                   int Hkv, int D, float scale, int window, const float* sinks,
-                                  void* out, int64_t out_stride, hipStream_t st) {
+                                  void* out, int64_t out_stride, int fp8, float k_scale, float v_scale,
+                                  hipStream_t st) {
   if (n_items == 0) return 0;
   const int G = Hq / Hkv;
   const int HPW = (G % 4 == 0) ? 4 : ((G % 2 == 0) ? 2 : 1);  // 4 / HPW must be integral
-  const float scale_log2 = scale * 1.4426950408889634f;
+  const float scale_log2 = scale * k_scale * 1.4426950408889634f;
   dim3 grid(n_items, Hkv * (G / HPW)), blk(NT);
   static bool attr_done = false;
   if (!attr_done) {
-    hipFuncSetAttribute((const void*)prefill_kernel<128>,
-                        hipFuncAttributeMaxDynamicSharedMemorySize,
-                        2 * (64 * (128 * 2 + 16) + 64 * 128 * 2));
-    hipFuncSetAttribute((const void*)prefill_kernel<64>,
-                        hipFuncAttributeMaxDynamicSharedMemorySize,
-                        2 * (64 * (64 * 2 + 16) + 64 * 64 * 2));
+    const int l128 = 2 * (64 * (128 * 2 + 16) + 64 * 128 * 2), l64 = 2 * (64 * (64 * 2 + 16) + 64 * 64 * 2);
+    (void)hipFuncSetAttribute((const void*)prefill_kernel<128, false>, hipFuncAttributeMaxDynamicSharedMemorySize, l128);
+    (void)hipFuncSetAttribute((const void*)prefill_kernel<128, true>, hipFuncAttributeMaxDynamicSharedMemorySize, l128);
+    (void)hipFuncSetAttribute((const void*)prefill_kernel<64, false>, hipFuncAttributeMaxDynamicSharedMemorySize, l64);
+    (void)hipFuncSetAttribute((const void*)prefill_kernel<64, true>, hipFuncAttributeMaxDynamicSharedMemorySize, l64);
     attr_done = true;
   }
+#define LAUNCH(DD, F8)                                                                                        \
+  hipLaunchKernelGGL((prefill_kernel<DD, F8>), grid, blk, (size_t)(2 * (64 * (DD * 2 + 16) + 64 * DD * 2)), st, \
+                     (const uint16_t*)q, q_stride, kc, vc, block_stride, bs, block_tables, bt_stride, q_start,   \
+                     q_len, ctx_len, items, Hq, Hkv, G, HPW, scale_log2, window, sinks, (uint16_t*)out,        \
+                     out_stride, v_scale)
   if (D == 128) {
-    const size_t lds = 2 * (64 * (128 * 2 + 16) + 64 * 128 * 2);
-    hipLaunchKernelGGL(prefill_kernel<128>, grid, blk, lds, st, (const uint16_t*)q, q_stride,
-                       (const uint16_t*)kc, (const uint16_t*)vc, block_stride, bs, block_tables,
-                       bt_stride, q_start, q_len, ctx_len, items, Hq, Hkv, G, HPW, scale_log2,
-                       window, sinks, (uint16_t*)out, out_stride);
+    if (fp8) LAUNCH(128, true); else LAUNCH(128, false);
   } else if (D == 64) {
-    const size_t lds = 2 * (64 * (64 * 2 + 16) + 64 * 64 * 2);
-    hipLaunchKernelGGL(prefill_kernel<64>, grid, blk, lds, st, (const uint16_t*)q, q_stride,
-                       (const uint16_t*)kc, (const uint16_t*)vc, block_stride, bs, block_tables,
-                       bt_stride, q_start, q_len, ctx_len, items, Hq, Hkv, G, HPW, scale_log2,
-                       window, sinks, (uint16_t*)out, out_stride);
+    if (fp8) LAUNCH(64, true); else LAUNCH(64, false);
   } else {
     return -1;
   }
+#undef LAUNCH
   return 0;
 }
 

@@ -18,14 +18,14 @@ void llmd_rms_norm(void*, int64_t, const void*, int64_t, const void*, int, int, 
 void llmd_fused_add_rms_norm(void*, int64_t, void*, int64_t, const void*, int, int, float,
                              hipStream_t);
 void llmd_rope_cache(void*, int64_t, const int64_t*, const float*, int, int, int, int,
-                     const int64_t*, void*, void*, int64_t, int, int, int, hipStream_t);
+                     const int64_t*, void*, void*, int64_t, int, int, int, int, float, float, hipStream_t);
 void llmd_gated_act(void*, int64_t, const void*, int64_t, int, int, int, float, float, hipStream_t);
 int llmd_paged_decode(const void*, int64_t, const void*, const void*, int64_t, int, const int*, int,
                       const int*, int, int, int, int, float, int, const float*, int, int, void*,
-                      int64_t, float*, float*, hipStream_t);
+                      int64_t, float*, float*, int, float, float, hipStream_t);
 int llmd_paged_prefill(const void*, int64_t, const void*, const void*, int64_t, int, const int*, int,
                        const int*, const int*, const int*, const int*, int, int, int, int, float,
-                       int, const float*, void*, int64_t, hipStream_t);
+                       int, const float*, void*, int64_t, int, float, float, hipStream_t);
 int llmd_prefill_tokens_per_item(int, int);
 void llmd_sample(const void*, int64_t, int, int, int, const float*, const int64_t*, int64_t*, float*,
                  hipStream_t);
@@ -116,11 +116,19 @@ void fused_add_rms_norm(torch::Tensor x, torch::Tensor residual, torch::Tensor w
                           w.data_ptr(), x.size(0), d, (float)eps, cur_stream());
 }
 
+// KV caches are bf16 or fp8 e4m3fn (OCP, gfx950's native fp8)
+bool is_fp8_cache(const torch::Tensor& c) {
+  TORCH_CHECK(c.is_cuda(), "cache must be a GPU tensor");
+  const auto t = c.scalar_type();
+  TORCH_CHECK(t == at::kBFloat16 || t == at::kFloat8_e4m3fn, "KV cache must be bf16 or float8_e4m3fn");
+  return t == at::kFloat8_e4m3fn;
+}
+
 // qkv [T, (Hq+2Hkv)*D]; k_cache/v_cache: per-layer strided views
 // [num_blocks, Hkv, bs, D] (block stride arbitrary, inner [Hkv,bs,D] contiguous)
 void rope_cache(torch::Tensor qkv, torch::Tensor positions, torch::Tensor cos_sin, int64_t Hq,
                 int64_t Hkv, int64_t D, torch::Tensor slots, torch::Tensor k_cache,
-                torch::Tensor v_cache, bool neox) {
+                torch::Tensor v_cache, bool neox, double k_scale, double v_scale) {
   const c10::hip::OptionalHIPGuard device_guard(dev_of(qkv));
   CHECK_CUDA(qkv); CHECK_BF16(qkv); CHECK_INNER(qkv);
   CHECK_DT(positions, at::kLong); CHECK_DT(slots, at::kLong); CHECK_DT(cos_sin, at::kFloat);
@@ -131,7 +139,8 @@ void rope_cache(torch::Tensor qkv, torch::Tensor positions, torch::Tensor cos_si
   const int rot = cos_sin.size(1);
   TORCH_CHECK(rot % 16 == 0 && rot <= D && D % 8 == 0, "rope_cache: rotary dim");
   TORCH_CHECK(qkv.stride(0) % 8 == 0, "rope_cache: 16-B aligned rows");
-  CHECK_BF16(k_cache); CHECK_BF16(v_cache);
+  const bool f8 = is_fp8_cache(k_cache);
+  TORCH_CHECK(v_cache.scalar_type() == k_cache.scalar_type(), "k/v cache dtype");
   TORCH_CHECK(k_cache.dim() == 4 && k_cache.size(1) == Hkv && k_cache.size(3) == D,
               "k_cache [blocks, Hkv, bs, D]");
   TORCH_CHECK(k_cache.stride(3) == 1 && k_cache.stride(2) == D && k_cache.stride(1) == k_cache.size(2) * D,
@@ -141,7 +150,7 @@ void rope_cache(torch::Tensor qkv, torch::Tensor positions, torch::Tensor cos_si
   llmd_rope_cache(qkv.data_ptr(), qkv.stride(0), positions.data_ptr<int64_t>(),
                   cos_sin.data_ptr<float>(), rot, Hq, Hkv, D, slots.data_ptr<int64_t>(),
                   k_cache.data_ptr(), v_cache.data_ptr(), k_cache.stride(0), k_cache.size(2), T,
-                  neox ? 1 : 0, cur_stream());
+                  neox ? 1 : 0, f8 ? 1 : 0, (float)(1.0 / k_scale), (float)(1.0 / v_scale), cur_stream());
 }
 
 void gated_act(torch::Tensor out, torch::Tensor x, int64_t mode, double alpha, double limit) {
@@ -156,7 +165,8 @@ void gated_act(torch::Tensor out, torch::Tensor x, int64_t mode, double alpha, d
 }
 
 void check_cache(const torch::Tensor& k, const torch::Tensor& v, int64_t Hkv, int64_t D) {
-  CHECK_BF16(k); CHECK_BF16(v);
+  is_fp8_cache(k);
+  TORCH_CHECK(v.scalar_type() == k.scalar_type(), "k/v cache dtype");
   TORCH_CHECK(k.dim() == 4 && k.size(1) == Hkv && k.size(3) == D, "cache [blocks, Hkv, bs, D]");
   TORCH_CHECK(k.stride(3) == 1 && k.stride(2) == D && k.stride(1) == k.size(2) * D,
               "cache inner layout");
@@ -167,7 +177,8 @@ void check_cache(const torch::Tensor& k, const torch::Tensor& v, int64_t Hkv, in
 void paged_decode(torch::Tensor out, torch::Tensor q, torch::Tensor k_cache, torch::Tensor v_cache,
                   torch::Tensor block_tables, torch::Tensor seq_lens, int64_t Hq, int64_t Hkv,
                   int64_t D, double scale, int64_t window, c10::optional<torch::Tensor> sinks,
-                  int64_t split_size, int64_t nsplit, torch::Tensor part_o, torch::Tensor part_ml) {
+                  int64_t split_size, int64_t nsplit, torch::Tensor part_o, torch::Tensor part_ml,
+                  double k_scale, double v_scale) {
   const c10::hip::OptionalHIPGuard device_guard(dev_of(out));
   CHECK_CUDA(q); CHECK_BF16(q); CHECK_BF16(out); CHECK_INNER(q); CHECK_INNER(out);
   check_cache(k_cache, v_cache, Hkv, D);
@@ -196,7 +207,8 @@ void paged_decode(torch::Tensor out, torch::Tensor q, torch::Tensor k_cache, tor
                              block_tables.stride(0), seq_lens.data_ptr<int>(), B, Hq, Hkv, D,
                              (float)scale, (int)window, sk, split_size, nsplit, out.data_ptr(),
                              out.stride(0), nsplit > 1 ? part_o.data_ptr<float>() : nullptr,
-                             nsplit > 1 ? part_ml.data_ptr<float>() : nullptr, cur_stream());
+                             nsplit > 1 ? part_ml.data_ptr<float>() : nullptr, is_fp8_cache(k_cache) ? 1 : 0,
+                             (float)k_scale, (float)v_scale, cur_stream());
   TORCH_CHECK(rc == 0, "paged_decode: unsupported head dim");
 }
 
@@ -290,7 +302,7 @@ void paged_prefill(torch::Tensor out, torch::Tensor q, torch::Tensor k_cache,
                    torch::Tensor v_cache, torch::Tensor block_tables, torch::Tensor q_start,
                    torch::Tensor q_len, torch::Tensor ctx_len, torch::Tensor items, int64_t Hq,
                    int64_t Hkv, int64_t D, double scale, int64_t window,
-                   c10::optional<torch::Tensor> sinks) {
+                   c10::optional<torch::Tensor> sinks, double k_scale, double v_scale) {
   const c10::hip::OptionalHIPGuard device_guard(dev_of(out));
   CHECK_CUDA(q); CHECK_BF16(q); CHECK_BF16(out); CHECK_INNER(q); CHECK_INNER(out);
   check_cache(k_cache, v_cache, Hkv, D);
@@ -312,7 +324,8 @@ void paged_prefill(torch::Tensor out, torch::Tensor q, torch::Tensor k_cache,
                               block_tables.stride(0), q_start.data_ptr<int>(),
                               q_len.data_ptr<int>(), ctx_len.data_ptr<int>(),
                               items.data_ptr<int>(), items.size(0), Hq, Hkv, D, (float)scale,
-                              (int)window, sk, out.data_ptr(), out.stride(0), cur_stream());
+                              (int)window, sk, out.data_ptr(), out.stride(0), is_fp8_cache(k_cache) ? 1 : 0,
+                              (float)k_scale, (float)v_scale, cur_stream());
   TORCH_CHECK(rc == 0, "paged_prefill: unsupported head dim");
 }
 

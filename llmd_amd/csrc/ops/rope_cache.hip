@@ -20,12 +20,14 @@ namespace {
 constexpr int NT = 256;
 
 // NEOX = rotate_half pairing (d, d + R/2); otherwise GPT-J interleaved pairs (2i, 2i+1).
-template <bool NEOX>
+// F8: the cache is e4m3fn; K/V are multiplied by kinv/vinv (1/k_scale, 1/v_scale)
+// and saturated on the way in (SURVEY K06 "quantize K/V", K16).
+template <bool NEOX, bool F8>
 __global__ __launch_bounds__(NT) void rope_cache_kernel(
     uint16_t* __restrict__ qkv, int64_t qkv_stride, const int64_t* __restrict__ positions,
     const float* __restrict__ cos_sin, int rot, int Hq, int Hkv, int D,
-    const int64_t* __restrict__ slots, uint16_t* __restrict__ kc, uint16_t* __restrict__ vc,
-    int64_t block_stride, int bs) {
+    const int64_t* __restrict__ slots, void* __restrict__ kc, void* __restrict__ vc,
+    int64_t block_stride, int bs, float kinv, float vinv) {
   const int t = blockIdx.x;
   const int64_t pos = positions[t];
   const float* cs = cos_sin + pos * rot;
@@ -98,9 +100,9 @@ __global__ __launch_bounds__(NT) void rope_cache_kernel(
       *reinterpret_cast<u32x4_t*>(hp + ia) = pa;
       *reinterpret_cast<u32x4_t*>(hp + ib) = pb;
     } else if (cache_off >= 0) {
-      uint16_t* dst = kc + cache_off + (int64_t)(h - Hq) * bs * D;
-      *reinterpret_cast<u32x4_t*>(dst + ia) = pa;
-      *reinterpret_cast<u32x4_t*>(dst + ib) = pb;
+      const int64_t dst = cache_off + (int64_t)(h - Hq) * bs * D;
+      store8_from_bf16<F8>(kc, dst + ia, pa, kinv);
+      store8_from_bf16<F8>(kc, dst + ib, pb, kinv);
     }
   }
   if (cache_off < 0) return;
@@ -114,11 +116,11 @@ __global__ __launch_bounds__(NT) void rope_cache_kernel(
     if (c < kpass) {
       const int e = rot + c * 8;
       u32x4_t v = *reinterpret_cast<const u32x4_t*>(row + (Hq + h) * D + e);
-      *reinterpret_cast<u32x4_t*>(kc + cache_off + (int64_t)h * bs * D + e) = v;
+      store8_from_bf16<F8>(kc, cache_off + (int64_t)h * bs * D + e, v, kinv);
     } else {
       const int e = (c - kpass) * 8;
       u32x4_t v = *reinterpret_cast<const u32x4_t*>(row + (Hq + Hkv + h) * D + e);
-      *reinterpret_cast<u32x4_t*>(vc + cache_off + (int64_t)h * bs * D + e) = v;
+      store8_from_bf16<F8>(vc, cache_off + (int64_t)h * bs * D + e, v, vinv);
     }
   }
 }
@@ -128,15 +130,16 @@ __global__ __launch_bounds__(NT) void rope_cache_kernel(
 extern "C" void llmd_rope_cache(void* qkv, int64_t qkv_stride, const int64_t* positions,
                                 const float* cos_sin, int rot, int Hq, int Hkv, int D,
                                 const int64_t* slots, void* kc, void* vc, int64_t block_stride,
-                                int bs, int T, int neox, hipStream_t st) {
+                                int bs, int T, int neox, int fp8, float kinv, float vinv, hipStream_t st) {
   if (T == 0) return;
   dim3 g(T), b(NT);
-  if (neox)
-    hipLaunchKernelGGL(rope_cache_kernel<true>, g, b, 0, st, (uint16_t*)qkv, qkv_stride,
-                       positions, cos_sin, rot, Hq, Hkv, D, slots, (uint16_t*)kc, (uint16_t*)vc,
-                       block_stride, bs);
-  else
-    hipLaunchKernelGGL(rope_cache_kernel<false>, g, b, 0, st, (uint16_t*)qkv, qkv_stride,
-                       positions, cos_sin, rot, Hq, Hkv, D, slots, (uint16_t*)kc, (uint16_t*)vc,
-                       block_stride, bs);
+#define LAUNCH(NX, F8)                                                                                \
+  hipLaunchKernelGGL((rope_cache_kernel<NX, F8>), g, b, 0, st, (uint16_t*)qkv, qkv_stride, positions, \
+                     cos_sin, rot, Hq, Hkv, D, slots, kc, vc, block_stride, bs, kinv, vinv)
+  if (neox) {
+    if (fp8) LAUNCH(true, true); else LAUNCH(true, false);
+  } else {
+    if (fp8) LAUNCH(false, true); else LAUNCH(false, false);
+  }
+#undef LAUNCH
 }

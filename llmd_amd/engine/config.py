@@ -306,6 +306,8 @@ def add_engine_args(p: argparse.ArgumentParser) -> argparse.ArgumentParser:
     p.add_argument("--device", default="cuda")
     p.add_argument("--seed", type=int, default=0)
     p.add_argument("--block-size", type=int, default=64)
+    p.add_argument("--kv-cache-dtype", default="auto", choices=["auto", "bfloat16", "fp8", "fp8_e4m3"],
+                   help="KV cache storage: bf16 (auto) or OCP fp8 e4m3fn")
     p.add_argument("--gpu-memory-utilization", type=float, default=0.92)
     p.add_argument("--kv-cache-memory-bytes", type=int, default=None)
     p.add_argument("--num-gpu-blocks-override", type=int, default=None)
@@ -337,7 +339,7 @@ def engine_config_from_args(a) -> EngineConfig:
     return EngineConfig.create(
         a.model, served_model_name=a.served_model_name, tokenizer=a.tokenizer,
         load_format=a.load_format, weights_path=a.weights_path, dtype=a.dtype, device=a.device,
-        seed=a.seed, block_size=a.block_size, gpu_memory_utilization=a.gpu_memory_utilization,
+        seed=a.seed, block_size=a.block_size, kv_cache_dtype=getattr(a, "kv_cache_dtype", "auto"), gpu_memory_utilization=a.gpu_memory_utilization,
         kv_cache_memory_bytes=a.kv_cache_memory_bytes, num_gpu_blocks=a.num_gpu_blocks_override,
         enable_prefix_caching=not a.no_enable_prefix_caching, max_num_seqs=a.max_num_seqs,
         max_num_batched_tokens=a.max_num_batched_tokens, max_model_len=a.max_model_len,

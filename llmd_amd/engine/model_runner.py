@@ -80,6 +80,18 @@ class ModelRunner:
         # or one latent row per token for MLA
         self.kv_spec = self.model.kv_spec() if hasattr(self.model, "kv_spec") else (2, self.Hkv, self.D)
         self.is_mla = bool(getattr(self.model, "needs_mla_rows", False))
+        # KV storage dtype (vLLM --kv-cache-dtype): bf16 or OCP fp8
+        # e4m3fn (gfx950 native) with per-layer dequant scales (k_scale/v_scale,
+        # 1.0 unless the checkpoint carries calibrated ones).
+        kvd = (cfg.cache.kv_cache_dtype or "auto").lower()
+        if kvd in ("auto", "bf16", "bfloat16"):
+            self.kv_dtype = torch.bfloat16
+        elif kvd in ("fp8", "fp8_e4m3", "fp8_e4m3fn"):
+            if self.is_mla:
+                raise NotImplementedError("fp8 KV cache is not supported for MLA (latent) caches yet")
+            self.kv_dtype = torch.float8_e4m3fn
+        else:
+            raise ValueError(f"unsupported --kv-cache-dtype {cfg.cache.kv_cache_dtype}")
         self.lora = None  # engine/lora.py LoRAManager (set by the engine / TP follower)
         self.kv = None
         self.num_blocks = 0
@@ -110,7 +122,7 @@ class ModelRunner:
     # ------------------------------------------------------------ KV cache
     def block_bytes(self) -> int:
         planes, heads, dim = self.kv_spec
-        return self.L * planes * heads * self.bs * dim * 2
+        return self.L * planes * heads * self.bs * dim * torch.empty(0, dtype=self.kv_dtype).element_size()
 
     def _wants_vmm(self) -> bool:
         """KV producers export their pool to other processes (kvx); a single
@@ -132,10 +144,10 @@ class ModelRunner:
             need = num_blocks * self.block_bytes()
             n = (need + chunk - 1) // chunk
             pool, fds = C.vmm_pool(self.device.index, chunk, n)
-            kv = pool[:need].view(torch.bfloat16).view(shape)
+            kv = pool[:need].view(self.kv_dtype).view(shape)
             self.vmm = {"fds": list(fds), "chunk": chunk, "n": n, "pool": pool}
         else:
-            kv = torch.empty(shape, dtype=torch.bfloat16, device=self.device)
+            kv = torch.empty(shape, dtype=self.kv_dtype, device=self.device)
         self._bind(kv)
         return kv
 

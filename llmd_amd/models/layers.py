@@ -155,22 +155,26 @@ class PagedAttention(torch.nn.Module):
                                         requires_grad=False) if sinks else None
         self.k_cache: Optional[torch.Tensor] = None
         self.v_cache: Optional[torch.Tensor] = None
+        # fp8 KV dequant scales (checkpoint `self_attn.{k,v}_scale`; 1.0 otherwise)
+        self.k_scale = 1.0
+        self.v_scale = 1.0
 
     def forward(self, qkv: torch.Tensor, meta: AttnMeta) -> torch.Tensor:
         T = qkv.shape[0]
         Hq, Hkv, D = self.Hq, self.Hkv, self.D
         ops.rope_cache(qkv, meta.positions, self.cos_sin, Hq, Hkv, D, meta.slot_mapping,
-                       self.k_cache, self.v_cache, self.neox)
+                       self.k_cache, self.v_cache, self.neox, self.k_scale, self.v_scale)
         out = torch.empty(T, Hq * D, dtype=qkv.dtype, device=qkv.device)
         nd = meta.num_decode
         if nd:
             ops.paged_decode(qkv[:nd], self.k_cache, self.v_cache, meta.d_block_tables,
                              meta.d_seq_lens, Hq, Hkv, D, self.scale, self.window, self.sinks,
                              split=meta.d_split, out=out[:nd], workspace=meta.d_workspace,
-                             max_ctx=meta.d_max_ctx)
+                             max_ctx=meta.d_max_ctx, k_scale=self.k_scale, v_scale=self.v_scale)
         if meta.num_prefill_tokens:
             items = meta.p_items
             ops.paged_prefill(qkv[nd:], self.k_cache, self.v_cache, meta.p_block_tables,
                               meta.p_q_start, meta.p_q_len, meta.p_ctx_len, Hq, Hkv, D, self.scale,
-                              self.window, self.sinks, items=items, out=out[nd:])
+                              self.window, self.sinks, items=items, out=out[nd:], k_scale=self.k_scale,
+                              v_scale=self.v_scale)
         return out

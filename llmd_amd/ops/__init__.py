@@ -65,11 +65,13 @@ def fused_add_rms_norm(x: torch.Tensor, residual: torch.Tensor, w: torch.Tensor,
 
 
 # ---------------------------------------------------------------- rope + cache
-def rope_cache(qkv, positions, cos_sin, Hq, Hkv, D, slots, k_cache, v_cache, neox=True):
+def rope_cache(qkv, positions, cos_sin, Hq, Hkv, D, slots, k_cache, v_cache, neox=True, k_scale=1.0,
+               v_scale=1.0):
+    """RoPE + paged KV write; bf16 or fp8 e4m3fn caches (fp8 stores x / scale)."""
     if not _gpu(qkv):
-        ref.rope_cache(qkv, positions, cos_sin, Hq, Hkv, D, slots, k_cache, v_cache, neox)
+        ref.rope_cache(qkv, positions, cos_sin, Hq, Hkv, D, slots, k_cache, v_cache, neox, k_scale, v_scale)
         return
-    native().rope_cache(qkv, positions, cos_sin, Hq, Hkv, D, slots, k_cache, v_cache, neox)
+    native().rope_cache(qkv, positions, cos_sin, Hq, Hkv, D, slots, k_cache, v_cache, neox, k_scale, v_scale)
 
 
 # ---------------------------------------------------------------- activation
@@ -113,11 +115,11 @@ def decode_split_plan(max_ctx: int, batch: int, Hkv: int, G: int, num_cus: int =
 
 
 def paged_decode(q, k_cache, v_cache, block_tables, seq_lens, Hq, Hkv, D, scale, window=0,
-                 sinks=None, split=None, out=None, workspace=None, max_ctx=None):
-    """q: [B, >=Hq*D] -> out [B, Hq*D]."""
+                 sinks=None, split=None, out=None, workspace=None, max_ctx=None, k_scale=1.0, v_scale=1.0):
+    """q: [B, >=Hq*D] -> out [B, Hq*D]. k/v caches bf16 or fp8 e4m3fn (dequant scales)."""
     if not _gpu(q):
         r = ref.paged_decode(q, k_cache, v_cache, block_tables, seq_lens, Hq, Hkv, D, scale,
-                             window, sinks)
+                             window, sinks, k_scale, v_scale)
         if out is not None:
             out.copy_(r)
             return out
@@ -141,7 +143,7 @@ def paged_decode(q, k_cache, v_cache, block_tables, seq_lens, Hq, Hkv, D, scale,
     else:
         part_o = part_ml = out.new_empty(0, dtype=torch.float32)
     native().paged_decode(out, q, k_cache, v_cache, block_tables, seq_lens, Hq, Hkv, D, scale,
-                          window, sinks, split_size, nsplit, part_o, part_ml)
+                          window, sinks, split_size, nsplit, part_o, part_ml, k_scale, v_scale)
     return out
 
 
@@ -157,10 +159,10 @@ def build_prefill_items(q_len: list[int], ctx_len: list[int], tpi: int) -> list[
 
 
 def paged_prefill(q, k_cache, v_cache, block_tables, q_start, q_len, ctx_len, Hq, Hkv, D, scale,
-                  window=0, sinks=None, items=None, out=None):
+                  window=0, sinks=None, items=None, out=None, k_scale=1.0, v_scale=1.0):
     if not _gpu(q):
         r = ref.paged_prefill(q, k_cache, v_cache, block_tables, q_start, q_len, ctx_len, Hq, Hkv,
-                              D, scale, window, sinks)
+                              D, scale, window, sinks, k_scale, v_scale)
         if out is not None:
             out.copy_(r)
             return out
@@ -172,7 +174,7 @@ def paged_prefill(q, k_cache, v_cache, block_tables, q_start, q_len, ctx_len, Hq
         it = build_prefill_items(q_len.tolist(), ctx_len.tolist(), tpi)
         items = torch.tensor(it, dtype=torch.int32).view(-1, 2).to(q.device, non_blocking=True)
     native().paged_prefill(out, q, k_cache, v_cache, block_tables, q_start, q_len, ctx_len, items,
-                           Hq, Hkv, D, scale, window, sinks)
+                           Hq, Hkv, D, scale, window, sinks, k_scale, v_scale)
     return out
 
 

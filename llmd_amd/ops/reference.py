@@ -25,7 +25,18 @@ def fused_add_rms_norm(x: torch.Tensor, residual: torch.Tensor, w: torch.Tensor,
     x.copy_(rms_norm(r, w, eps))
 
 
-def rope_cache(qkv, positions, cos_sin, Hq, Hkv, D, slots, k_cache, v_cache, neox=True):
+FP8_MAX = 448.0
+
+
+def to_cache(x: torch.Tensor, cache_dtype, scale: float = 1.0) -> torch.Tensor:
+    """Cache storage conversion: bf16 as is; fp8 e4m3fn = saturate(x / scale)."""
+    if cache_dtype == torch.float8_e4m3fn:
+        return (x.float() / scale).clamp(-FP8_MAX, FP8_MAX).to(cache_dtype)
+    return x.to(cache_dtype)
+
+
+def rope_cache(qkv, positions, cos_sin, Hq, Hkv, D, slots, k_cache, v_cache, neox=True, k_scale=1.0,
+               v_scale=1.0):
     """Rotate Q (in place in qkv) and K, write K/V into the paged cache at slots."""
     T = qkv.shape[0]
     if T == 0:
@@ -56,8 +67,8 @@ def rope_cache(qkv, positions, cos_sin, Hq, Hkv, D, slots, k_cache, v_cache, neo
     if valid.any():
         sl = slots[valid]
         blk, off = sl // bs, sl % bs
-        k_cache[blk, :, off, :] = k_full[valid]
-        v_cache[blk, :, off, :] = v_full[valid]
+        k_cache[blk, :, off, :] = to_cache(k_full[valid], k_cache.dtype, k_scale)
+        v_cache[blk, :, off, :] = to_cache(v_full[valid], v_cache.dtype, v_scale)
 
 
 def gated_act(x: torch.Tensor, mode: int = 0, alpha: float = 1.702, limit: float = 7.0):
@@ -76,13 +87,13 @@ def gated_act(x: torch.Tensor, mode: int = 0, alpha: float = 1.702, limit: float
     return (a * u).to(x.dtype)
 
 
-def _gather_kv(k_cache, v_cache, block_table, L):
+def _gather_kv(k_cache, v_cache, block_table, L, k_scale=1.0, v_scale=1.0):
     bs = k_cache.shape[2]
     nb = (L + bs - 1) // bs
     blocks = block_table[:nb].long()
     k = k_cache[blocks].permute(1, 0, 2, 3).reshape(k_cache.shape[1], nb * bs, -1)[:, :L]
     v = v_cache[blocks].permute(1, 0, 2, 3).reshape(v_cache.shape[1], nb * bs, -1)[:, :L]
-    return k.float(), v.float()  # [Hkv, L, D]
+    return k.float() * k_scale, v.float() * v_scale  # [Hkv, L, D]
 
 
 def attention_ref(q, k, v, q_pos, scale, window=0, sinks=None):
@@ -108,12 +119,12 @@ def attention_ref(q, k, v, q_pos, scale, window=0, sinks=None):
 
 
 def paged_decode(q, k_cache, v_cache, block_tables, seq_lens, Hq, Hkv, D, scale, window=0,
-                 sinks=None):
+                 sinks=None, k_scale=1.0, v_scale=1.0):
     B = q.shape[0]
     out = torch.empty(B, Hq, D, dtype=q.dtype, device=q.device)
     for b in range(B):
         L = int(seq_lens[b])
-        k, v = _gather_kv(k_cache, v_cache, block_tables[b], L)
+        k, v = _gather_kv(k_cache, v_cache, block_tables[b], L, k_scale, v_scale)
         qb = q[b, : Hq * D].view(1, Hq, D)
         o = attention_ref(qb, k, v, torch.tensor([L - 1], device=q.device), scale, window, sinks)
         out[b] = o[0].to(q.dtype)
@@ -121,14 +132,14 @@ def paged_decode(q, k_cache, v_cache, block_tables, seq_lens, Hq, Hkv, D, scale,
 
 
 def paged_prefill(q, k_cache, v_cache, block_tables, q_start, q_len, ctx_len, Hq, Hkv, D, scale,
-                  window=0, sinks=None):
+                  window=0, sinks=None, k_scale=1.0, v_scale=1.0):
     T = q.shape[0]
     out = torch.zeros(T, Hq * D, dtype=q.dtype, device=q.device)
     for i in range(len(q_len)):
         qs, ql, ctx = int(q_start[i]), int(q_len[i]), int(ctx_len[i])
         if ql == 0:
             continue
-        k, v = _gather_kv(k_cache, v_cache, block_tables[i], ctx)
+        k, v = _gather_kv(k_cache, v_cache, block_tables[i], ctx, k_scale, v_scale)
         qi = q[qs : qs + ql, : Hq * D].view(ql, Hq, D)
         qpos = torch.arange(ctx - ql, ctx, device=q.device)
         o = attention_ref(qi, k, v, qpos, scale, window, sinks)

@@ -33,10 +33,13 @@ from llmd_amd import ops  # noqa: E402
 from llmd_amd.ops import reference as ref  # noqa: E402
 
 
+KV_DTYPE = torch.bfloat16
+
+
 def make_cache(nctx, Hkv, D, bs, dev, seqs=1):
     nb = seqs * math.ceil(nctx / bs) + 1
-    kc = torch.randn(nb, Hkv, bs, D, device=dev, dtype=torch.bfloat16)
-    vc = torch.randn(nb, Hkv, bs, D, device=dev, dtype=torch.bfloat16)
+    kc = torch.randn(nb, Hkv, bs, D, device=dev, dtype=torch.bfloat16).to(KV_DTYPE)
+    vc = torch.randn(nb, Hkv, bs, D, device=dev, dtype=torch.bfloat16).to(KV_DTYPE)
     per = math.ceil(nctx / bs)
     bt = torch.stack([torch.randperm(nb - 1, device=dev)[:per] for _ in range(seqs)]).int()
     return kc, vc, bt
@@ -76,7 +79,8 @@ def prefill(ctx, q_len, Hq, Hkv, D, bs, check=False):
     p0 = ctx - q_len
     vis = sum(p0 + i + 1 for i in range(q_len))
     fl = 4 * Hq * D * vis
-    print(f"prefill ctx={ctx} q={q_len} Hq={Hq} Hkv={Hkv} D={D}: {t * 1e3:.3f} ms  {fl / t / 1e12:.1f} TF/s")
+    print(f"prefill ctx={ctx} q={q_len} Hq={Hq} Hkv={Hkv} D={D} kv={str(KV_DTYPE)[6:]}: {t * 1e3:.3f} ms  "
+          f"{fl / t / 1e12:.1f} TF/s")
     return t
 
 
@@ -90,8 +94,8 @@ def decode(ctx, B, Hq, Hkv, D, bs):
     fn = lambda: ops.paged_decode(q, kc, vc, bt, sl, Hq, Hkv, D, D ** -0.5, 0, None, split=split,  # noqa: E731
                                   out=out, max_ctx=ctx)
     t = time_it(fn)
-    by = B * ctx * Hkv * D * 2 * 2
-    print(f"decode B={B} ctx={ctx}: {t * 1e6:.1f} us  {by / t / 1e9:.0f} GB/s (KV read)")
+    by = B * ctx * Hkv * D * 2 * kc.element_size()
+    print(f"decode B={B} ctx={ctx} kv={str(KV_DTYPE)[6:]}: {t * 1e6:.1f} us  {by / t / 1e9:.0f} GB/s (KV read)")
     return t
 
 
@@ -127,7 +131,10 @@ def main():
     ap.add_argument("--D", type=int, default=128)
     ap.add_argument("--so", default=None)
     ap.add_argument("--mla", action="store_true")
+    ap.add_argument("--kv-dtype", default="bf16", choices=["bf16", "fp8"])
     a = ap.parse_args()
+    global KV_DTYPE
+    KV_DTYPE = torch.float8_e4m3fn if a.kv_dtype == "fp8" else torch.bfloat16
     if a.check:
         prefill(700, 300, 16, 2, a.D, 64, check=True)
         prefill(600, 600, 64, 8, a.D, 64, check=True)
