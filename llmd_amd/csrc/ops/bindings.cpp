@@ -59,6 +59,7 @@ void llmd_moe_gemm(const void*, int64_t, int, const int*, const int*, int, const
                    void*, int64_t, int, int, float, float, int, const void*, hipStream_t);
 void llmd_moe_combine(const void*, int64_t, const int*, const float*, int, int, int, void*, int64_t,
                       hipStream_t);
+int llmd_quant_fp8_rows(const void*, int64_t, void*, int64_t, float*, int, int, hipStream_t);
 int llmd_symm_alloc(size_t, void**);
 int llmd_symm_free(void*);
 int64_t llmd_symm_sig_bytes();
@@ -532,6 +533,18 @@ void moe_combine(torch::Tensor Y, torch::Tensor inv, torch::Tensor w, int64_t to
                    out.data_ptr(), out.stride(0), cur_stream());
 }
 
+// ---------------------------------------------------------------- fp8 quant
+void quant_fp8_rows(torch::Tensor x, torch::Tensor q, torch::Tensor scale) {
+  const c10::hip::OptionalHIPGuard device_guard(dev_of(x));
+  CHECK_CUDA(x); CHECK_BF16(x); CHECK_INNER(x); CHECK_INNER(q); CHECK_DT(q, at::kFloat8_e4m3fn);
+  CHECK_DT(scale, at::kFloat);
+  TORCH_CHECK(x.dim() == 2 && q.sizes() == x.sizes() && scale.numel() >= x.size(0), "quant_fp8_rows shapes");
+  TORCH_CHECK(x.size(1) % 8 == 0 && x.stride(0) % 8 == 0 && q.stride(0) % 8 == 0, "quant_fp8_rows: 16-B rows");
+  int rc = llmd_quant_fp8_rows(x.data_ptr(), x.stride(0), q.data_ptr(), q.stride(0), scale.data_ptr<float>(),
+                               x.size(0), x.size(1), cur_stream());
+  TORCH_CHECK(rc == 0, "quant_fp8_rows failed: ", rc);
+}
+
 // ---------------------------------------------------------------- symm heap
 torch::Tensor symm_alloc(int64_t bytes, int64_t device) {
   const c10::hip::HIPGuard guard((c10::DeviceIndex)device);
@@ -634,6 +647,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("moe_gemm", &moe_gemm);
   m.def("moe_combine", &moe_combine);
   m.def("moe_tile_m", &llmd_moe_gemm_tile_m);
+  m.def("quant_fp8_rows", &quant_fp8_rows);
   m.def("symm_alloc", &symm_alloc);
   m.def("symm_error", &symm_error);
   m.def("symm_sig_bytes", &llmd_symm_sig_bytes);

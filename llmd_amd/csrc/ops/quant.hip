@@ -1,0 +1,60 @@
+// Dynamic per-token FP8 quantisation (vLLM `dynamic_per_token_scaled_fp8_quant`).
+//
+// x [T, d] bf16 -> q [T, d] e4m3fn (OCP, gfx950) and scale [T] f32 with
+// q = sat(x / scale), scale = max(|x_t|) / 448. One workgroup per row: pass 1
+// reduces the row's amax (16-B loads, wave64 DPP reduction), pass 2 re-reads
+// the row (L2/L1-resident after pass 1) and writes 8-B fp8 packets. This is the
+// activation side of the FP8 linear (W8A8, per-channel weight scales), whose
+// GEMM runs in hipBLASLt via torch._scaled_mm.
+#include "llmd_common.h"
+
+using namespace llmd;
+
+namespace {
+
+constexpr int NT = 256;
+
+__global__ __launch_bounds__(NT) void quant_fp8_rows_kernel(const uint16_t* __restrict__ x, int64_t xs,
+                                                            uint8_t* __restrict__ q, int64_t qs,
+                                                            float* __restrict__ scale, int d, float floor_) {
+  __shared__ float red[NT / 64];
+  const int64_t t = blockIdx.x;
+  const u32x4_t* xr = reinterpret_cast<const u32x4_t*>(x + t * xs);
+  const int nc = d / 8;
+  float amax = 0.f;
+  for (int c = threadIdx.x; c < nc; c += NT) {
+    float f[8];
+    unpack8(xr[c], f);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) amax = fmaxf(amax, fabsf(f[i]));
+  }
+  amax = wave_max(amax);
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  if (l == 0) red[w] = amax;
+  __syncthreads();
+  float m = red[0];
+#pragma unroll
+  for (int i = 1; i < NT / 64; ++i) m = fmaxf(m, red[i]);
+  const float s = fmaxf(m / FP8_MAX, floor_);
+  const float inv = 1.f / s;
+  if (threadIdx.x == 0) scale[t] = s;
+  u32x2_t* qr = reinterpret_cast<u32x2_t*>(q + t * qs);
+  for (int c = threadIdx.x; c < nc; c += NT) {
+    float f[8];
+    unpack8(xr[c], f);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) f[i] *= inv;
+    qr[c] = f32x8_to_fp8(f);
+  }
+}
+
+}  // namespace
+
+extern "C" int llmd_quant_fp8_rows(const void* x, int64_t xs, void* q, int64_t qs, float* scale, int T, int d,
+                                   hipStream_t st) {
+  if (T == 0) return 0;
+  if (d % 8) return -1;
+  hipLaunchKernelGGL(quant_fp8_rows_kernel, dim3(T), dim3(NT), 0, st, (const uint16_t*)x, xs, (uint8_t*)q, qs,
+                     scale, d, 1e-12f);
+  return (int)hipGetLastError();
+}

@@ -256,6 +256,7 @@ class EngineConfig:
     seed: int = 0
     load_format: str = "dummy"  # "dummy" (random init) | "safetensors"
     weights_path: Optional[str] = None
+    quantization: Optional[str] = None  # None | "fp8" (W8A8: per-channel fp8 weights, per-token activations)
     tokenizer: Optional[str] = None
     served_model_name: Optional[str] = None
     enforce_eager: bool = False
@@ -306,6 +307,8 @@ def add_engine_args(p: argparse.ArgumentParser) -> argparse.ArgumentParser:
     p.add_argument("--device", default="cuda")
     p.add_argument("--seed", type=int, default=0)
     p.add_argument("--block-size", type=int, default=64)
+    p.add_argument("--quantization", "-q", default=None, choices=[None, "fp8"],
+                   help="fp8: online W8A8 quantisation of the dense linears (hipBLASLt fp8 GEMM)")
     p.add_argument("--kv-cache-dtype", default="auto", choices=["auto", "bfloat16", "fp8", "fp8_e4m3"],
                    help="KV cache storage: bf16 (auto) or OCP fp8 e4m3fn")
     p.add_argument("--gpu-memory-utilization", type=float, default=0.92)
@@ -339,7 +342,8 @@ def engine_config_from_args(a) -> EngineConfig:
     return EngineConfig.create(
         a.model, served_model_name=a.served_model_name, tokenizer=a.tokenizer,
         load_format=a.load_format, weights_path=a.weights_path, dtype=a.dtype, device=a.device,
-        seed=a.seed, block_size=a.block_size, kv_cache_dtype=getattr(a, "kv_cache_dtype", "auto"), gpu_memory_utilization=a.gpu_memory_utilization,
+        seed=a.seed, block_size=a.block_size, kv_cache_dtype=getattr(a, "kv_cache_dtype", "auto"),
+        quantization=getattr(a, "quantization", None), gpu_memory_utilization=a.gpu_memory_utilization,
         kv_cache_memory_bytes=a.kv_cache_memory_bytes, num_gpu_blocks=a.num_gpu_blocks_override,
         enable_prefix_caching=not a.no_enable_prefix_caching, max_num_seqs=a.max_num_seqs,
         max_num_batched_tokens=a.max_num_batched_tokens, max_model_len=a.max_model_len,

@@ -70,6 +70,13 @@ class ModelRunner:
             from llmd_amd.models.loader import load_weights
 
             load_weights(self.model, cfg.weights_path)
+        if cfg.quantization == "fp8":
+            from llmd_amd.models.layers import quantize_fp8
+
+            n = quantize_fp8(self.model)
+            log.info("fp8 W8A8: quantised %d linears", n)
+        elif cfg.quantization:
+            raise ValueError(f"unsupported quantization {cfg.quantization}")
         if self.is_gpu:
             torch.cuda.synchronize()
         log.info("model %s built in %.1fs", self.mc.name, time.time() - t0)

@@ -28,6 +28,30 @@ def _init_weight(t: torch.Tensor, std: float, gen: Optional[torch.Generator] = N
     return t
 
 
+def _linear(mod, x, bias):
+    """bf16 weights -> hipBLASLt GEMM; fp8 weights (quantize_fp8) -> W8A8 GEMM
+    with dynamic per-token activation scales."""
+    w = mod.weight
+    if w.dtype == torch.float8_e4m3fn:
+        return ops.fp8_linear(x, w, mod.weight_scale, bias)
+    return F.linear(x, w, bias)
+
+
+def quantize_fp8(model: torch.nn.Module) -> int:
+    """Online FP8 weight quantisation (vLLM ``--quantization fp8``): every
+    Column/Row linear gets e4m3fn weights with per-output-channel scales;
+    embeddings, LM head, norms, routers and expert weights stay bf16.
+    Returns the number of quantised linears."""
+    n = 0
+    for m in model.modules():
+        if isinstance(m, (ColumnLinear, RowLinear)) and m.weight.dtype == torch.bfloat16:
+            wq, s = ops.quant_fp8_weight(m.weight.data)
+            m.weight = torch.nn.Parameter(wq, requires_grad=False)
+            m.weight_scale = torch.nn.Parameter(s, requires_grad=False)
+            n += 1
+    return n
+
+
 class ColumnLinear(torch.nn.Module):
     """y = x W^T, W [out/tp, in]; output stays sharded."""
 
@@ -45,7 +69,7 @@ class ColumnLinear(torch.nn.Module):
     lora = None  # engine/lora.py LoRATarget when multi-LoRA is enabled
 
     def forward(self, x):
-        y = F.linear(x, self.weight, self.bias)
+        y = _linear(self, x, self.bias)
         if self.lora is not None:
             self.lora.apply(y, x)
         return y
@@ -68,7 +92,7 @@ class RowLinear(torch.nn.Module):
     lora = None
 
     def forward(self, x):
-        y = F.linear(x, self.weight)
+        y = _linear(self, x, None)
         if self.lora is not None:  # partial sums join the layer's all-reduce
             self.lora.apply(y, x)
         if self.reduce:

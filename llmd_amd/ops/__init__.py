@@ -178,6 +178,49 @@ def paged_prefill(q, k_cache, v_cache, block_tables, q_start, q_len, ctx_len, Hq
     return out
 
 
+# ---------------------------------------------------------------- fp8 linear (W8A8)
+FP8 = torch.float8_e4m3fn
+FP8_MAX = 448.0
+
+
+def quant_fp8_rows(x: torch.Tensor):
+    """Dynamic per-token fp8: x [T, d] bf16 -> (q [T, d] e4m3fn, scale [T, 1] f32)."""
+    if not _gpu(x):
+        s = (x.float().abs().amax(1, keepdim=True) / FP8_MAX).clamp(min=1e-12)
+        return (x.float() / s).clamp(-FP8_MAX, FP8_MAX).to(FP8), s
+    x = x if x.stride(-1) == 1 and x.stride(0) % 8 == 0 else x.contiguous()
+    q = torch.empty(x.shape, dtype=FP8, device=x.device)
+    s = torch.empty(x.shape[0], 1, dtype=torch.float32, device=x.device)
+    native().quant_fp8_rows(x, q, s)
+    return q, s
+
+
+def quant_fp8_weight(w: torch.Tensor):
+    """Per-output-channel weight quantisation: w [N, K] -> (wq [N, K] e4m3fn, scale [1, N] f32)."""
+    s = (w.float().abs().amax(1) / FP8_MAX).clamp(min=1e-12)
+    wq = (w.float() / s[:, None]).clamp(-FP8_MAX, FP8_MAX).to(FP8)
+    return wq, s.view(1, -1).contiguous()
+
+
+def fp8_linear(x: torch.Tensor, wq: torch.Tensor, w_scale: torch.Tensor, bias=None) -> torch.Tensor:
+    """y = (q_x s_x) (q_w s_w)^T (+ bias), bf16 out. Activations are quantised
+    per token on the fly (HIP kernel); the GEMM is hipBLASLt's fp8 GEMM with
+    row-wise scales through torch._scaled_mm (a plain library GEMM)."""
+    lead = x.shape[:-1]
+    x2 = x.reshape(-1, x.shape[-1])
+    if not _gpu(x2):
+        xq, xs = quant_fp8_rows(x2)
+        y = (xq.float() * xs) @ (wq.float() * w_scale.view(-1, 1)).t()
+        if bias is not None:
+            y = y + bias.float()
+        return y.to(torch.bfloat16).reshape(*lead, -1)
+    if x2.shape[0] == 0:
+        return x2.new_empty(0, wq.shape[0]).reshape(*lead, -1)
+    xq, xs = quant_fp8_rows(x2)
+    y = torch._scaled_mm(xq, wq.t(), scale_a=xs, scale_b=w_scale, bias=bias, out_dtype=torch.bfloat16)
+    return y.reshape(*lead, -1)
+
+
 # ---------------------------------------------------------------- sampling
 def sample(logits, temps=None, seeds=None, out_ids=None, want_logprob=False, generator=None):
     if not _gpu(logits):

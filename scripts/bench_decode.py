@@ -22,11 +22,15 @@ def main():
     ap.add_argument("--batch", type=int, default=64)
     ap.add_argument("--isl", type=int, default=5000)
     ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--quantization", default=None)
+    ap.add_argument("--kv-cache-dtype", default="auto")
     a = ap.parse_args()
     cfg = EngineConfig.create(a.model, device="cuda", block_size=64, max_num_seqs=a.batch,
                               max_num_batched_tokens=8192, max_model_len=a.isl + a.steps + 200,
-                              cuda_graph_max_bs=a.batch)
+                              cuda_graph_max_bs=a.batch, quantization=a.quantization,
+                              kv_cache_dtype=a.kv_cache_dtype)
     eng = LLMEngine(cfg)
+    tstart = time.perf_counter()
     rng = np.random.default_rng(0)
     sp = SamplingParams(max_tokens=a.steps + 20, temperature=0.0, ignore_eos=True)
     for i in range(a.batch):
@@ -41,7 +45,9 @@ def main():
         eng.step()
     torch.cuda.synchronize()
     dt = (time.perf_counter() - t0) / a.steps
-    print(f"{a.model} decode batch={a.batch} ctx~{a.isl}: {dt * 1e3:.2f} ms/step  {a.batch / dt:.0f} tok/s", flush=True)
+    tp = time.perf_counter()
+    print(f"{a.model} q={a.quantization} kv={a.kv_cache_dtype} decode batch={a.batch} ctx~{a.isl}: "
+          f"{dt * 1e3:.2f} ms/step  {a.batch / dt:.0f} tok/s (prefill phase {t0 - tstart:.1f}s)", flush=True)
 
 
 if __name__ == "__main__":

@@ -135,3 +135,47 @@ def test_paged_prefill_fp8(Hq, Hkv, D):
     r = ref.paged_prefill(q, kc, vc, bt, *args, Hq, Hkv, D, 1 / math.sqrt(D), k_scale=ks, v_scale=vs)
     o = ops.paged_prefill(q, kc, vc, bt, *args, Hq, Hkv, D, 1 / math.sqrt(D), k_scale=ks, v_scale=vs)
     _close(o, r)
+
+
+def test_fp8_linear_cpu_matches_fp32():
+    torch.manual_seed(0)
+    x = torch.randn(5, 64, dtype=torch.bfloat16)
+    w = torch.randn(48, 64, dtype=torch.bfloat16) * 0.05
+    wq, ws = ops.quant_fp8_weight(w)
+    y = ops.fp8_linear(x, wq, ws)
+    r = x.float() @ w.float().t()
+    assert y.shape == (5, 48)
+    # W8A8 e4m3: ~2 x 2^-4 relative error per product, averaged over K
+    assert (y.float() - r).abs().max() < 0.08 * r.abs().max()
+
+
+def test_engine_fp8_w8a8_cpu():
+    from llmd_amd.engine.config import EngineConfig
+    from llmd_amd.engine.engine import LLMEngine
+    from llmd_amd.engine.request import SamplingParams
+
+    cfg = EngineConfig.create("tiny-llama", device="cpu", block_size=16, num_gpu_blocks=64,
+                              max_num_batched_tokens=256, max_num_seqs=4, max_model_len=512,
+                              quantization="fp8", kv_cache_dtype="fp8")
+    eng = LLMEngine(cfg, capture_graphs=False)
+    qkv = eng.runner.model.layers[0].qkv
+    if qkv is not None:
+        assert qkv.weight.dtype == F8 and qkv.weight_scale.shape == (1, qkv.weight.shape[0])
+    reqs = eng.generate([list(range(3, 30))], SamplingParams(max_tokens=4, temperature=0.0, ignore_eos=True))
+    assert len(reqs[0].output_token_ids) == 4
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("T,K,N", [(1, 8192, 10240), (64, 8192, 8192), (300, 4096, 28672), (2048, 7168, 4096)])
+def test_fp8_linear_gpu(T, K, N):
+    torch.manual_seed(0)
+    x = torch.randn(T, K, device="cuda", dtype=torch.bfloat16)
+    w = torch.randn(N, K, device="cuda", dtype=torch.bfloat16) * 0.02
+    wq, ws = ops.quant_fp8_weight(w)
+    xq, xs = ops.quant_fp8_rows(x)
+    rq, rs = ops.quant_fp8_rows(x.cpu())
+    torch.testing.assert_close(xs.cpu(), rs, rtol=1e-6, atol=0)
+    assert (xq.cpu().float() - rq.float()).abs().max() <= 32  # at most 1 ulp at the top of the range
+    y = ops.fp8_linear(x, wq, ws)
+    r = (xq.float() * xs) @ (wq.float() * ws.view(-1, 1)).t()
+    torch.testing.assert_close(y.float(), r, atol=2e-2 * r.abs().max().item(), rtol=2e-2)
