@@ -57,6 +57,9 @@ def parse():
     p.add_argument("--gpu-memory-utilization", type=float, default=0.92)
     p.add_argument("--kv-cache-gb", type=float, default=None)
     p.add_argument("--json-out", default=None)
+    p.add_argument("--quantization", default=None, choices=[None, "fp8"],
+                   help="fp8 = W8A8 linears (the reference AMD recipe serves Llama-3.3-70B-FP8); default bf16")
+    p.add_argument("--kv-cache-dtype", default="auto", choices=["auto", "fp8"])
     return p.parse_args()
 
 
@@ -107,7 +110,7 @@ def main():
                 "metric": METRIC, "value": round(value, 2), "unit": "output tok/s (whole job)",
                 "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
                 "ms_per_step": round(1000 * res["elapsed"] / a.steps, 3), "higher_is_better": True,
-                "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
+                "scaling": "weak", "vs_baseline": None, "dtype": "fp8" if a.quantization == "fp8" else "bf16",
                 "data": "synthetic (random token prompts, random-init weights)",
                 "config": {"model": "Llama-3-70B" if a.model == "llama-3-70b" else a.model,
                            "global_batch": a.concurrency * res["decode_ranks"], "seq_len": a.isl,
@@ -138,7 +141,8 @@ def main():
         max_num_batched_tokens=a.max_num_batched_tokens, max_model_len=max_len,
         enforce_eager=a.enforce_eager, seed=a.seed + rank, enable_prefix_caching=True,
         cuda_graph_max_bs=a.concurrency, gpu_memory_utilization=a.gpu_memory_utilization,
-        kv_cache_memory_bytes=int(a.kv_cache_gb * 2**30) if a.kv_cache_gb else None)
+        kv_cache_memory_bytes=int(a.kv_cache_gb * 2**30) if a.kv_cache_gb else None,
+        quantization=a.quantization, kv_cache_dtype=a.kv_cache_dtype)
     t0 = time.time()
     eng = LLMEngine(cfg)
     _sync(a)
@@ -226,13 +230,13 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "bf16",
+        "dtype": "fp8" if a.quantization == "fp8" else "bf16",
         "data": "synthetic (random token prompts, random-init weights)",
         "config": {"model": "Llama-3-70B" if a.model == "llama-3-70b" else a.model,
                    "global_batch": a.concurrency * world, "seq_len": a.isl, "isl": a.isl, "osl": a.osl,
                    "parallelism": f"dp{world}" if a.mode == "agg" else f"pd{a.prefill_gpus}p{world - a.prefill_gpus}d",
                    "max_num_batched_tokens": a.max_num_batched_tokens, "block_size": a.block_size,
-                   "graphs": not a.enforce_eager},
+                   "graphs": not a.enforce_eager, "kv_cache_dtype": a.kv_cache_dtype},
         "output_tok_s_per_decode_gpu": round(value / max(1, n_decode_gpus), 2),
         "p50_ttft_s": round(p50, 4) if p50 is not None else None,
         "prefill_tok_s": round(ptoks / elapsed, 1),

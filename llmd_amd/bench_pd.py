@@ -63,7 +63,8 @@ def run_pd(a, rank: int, world: int, local_rank: int, log) -> dict | None:
         max_num_batched_tokens=a.max_num_batched_tokens, max_model_len=max_len,
         enforce_eager=a.enforce_eager or is_prefill, seed=a.seed, enable_prefix_caching=True,
         cuda_graph_max_bs=conc, kv_transfer_config=kt, gpu_memory_utilization=a.gpu_memory_utilization,
-        kv_cache_memory_bytes=int(a.kv_cache_gb * 2**30) if a.kv_cache_gb else None)
+        kv_cache_memory_bytes=int(a.kv_cache_gb * 2**30) if a.kv_cache_gb else None,
+        quantization=a.quantization, kv_cache_dtype=a.kv_cache_dtype)
     t0 = time.time()
     eng = LLMEngine(cfg, capture_graphs=not is_prefill)
     _sync(a)
