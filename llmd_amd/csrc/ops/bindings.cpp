@@ -60,6 +60,10 @@ void llmd_moe_gemm(const void*, int64_t, int, const int*, const int*, int, const
 void llmd_moe_combine(const void*, int64_t, const int*, const float*, int, int, int, void*, int64_t,
                       hipStream_t);
 int llmd_quant_fp8_rows(const void*, int64_t, void*, int64_t, float*, int, int, hipStream_t);
+int llmd_quant_fp8_groups(const void*, int64_t, void*, int64_t, float*, int64_t, int, int, hipStream_t);
+void llmd_moe_gemm_fp8(const void*, int64_t, const float*, int64_t, int, const int*, const int*, int, const void*,
+                       int64_t, const float*, int, int, void*, int64_t, int, int, float, float, int, const void*,
+                       hipStream_t);
 int llmd_symm_alloc(size_t, void**);
 int llmd_symm_free(void*);
 int64_t llmd_symm_sig_bytes();
@@ -545,6 +549,49 @@ void quant_fp8_rows(torch::Tensor x, torch::Tensor q, torch::Tensor scale) {
   TORCH_CHECK(rc == 0, "quant_fp8_rows failed: ", rc);
 }
 
+void quant_fp8_groups(torch::Tensor x, torch::Tensor q, torch::Tensor scale) {
+  const c10::hip::OptionalHIPGuard device_guard(dev_of(x));
+  CHECK_CUDA(x); CHECK_BF16(x); CHECK_INNER(x); CHECK_INNER(q); CHECK_DT(q, at::kFloat8_e4m3fn);
+  CHECK_DT(scale, at::kFloat);
+  const int d = x.size(1);
+  TORCH_CHECK(x.dim() == 2 && q.sizes() == x.sizes() && d % 8 == 0, "quant_fp8_groups shapes");
+  TORCH_CHECK(scale.dim() == 2 && scale.size(0) >= x.size(0) && scale.size(1) >= (d + 127) / 128 &&
+                  scale.stride(1) == 1, "quant_fp8_groups: scale [T, ceil(d/128)]");
+  TORCH_CHECK(x.stride(0) % 8 == 0 && q.stride(0) % 8 == 0, "16-B rows");
+  int rc = llmd_quant_fp8_groups(x.data_ptr(), x.stride(0), q.data_ptr(), q.stride(0), scale.data_ptr<float>(),
+                                 scale.stride(0), x.size(0), d, cur_stream());
+  TORCH_CHECK(rc == 0, "quant_fp8_groups failed: ", rc);
+}
+
+void moe_gemm_fp8(torch::Tensor X, torch::Tensor xs, int64_t topk, torch::Tensor sorted_ids, torch::Tensor tile_expert,
+                  torch::Tensor W, torch::Tensor ws, torch::Tensor Y, int64_t mode, int64_t act, double alpha,
+                  double limit, bool a_rows_are_slots, c10::optional<torch::Tensor> bias) {
+  const c10::hip::OptionalHIPGuard device_guard(dev_of(X));
+  CHECK_CUDA(X); CHECK_DT(X, at::kFloat8_e4m3fn); CHECK_DT(W, at::kFloat8_e4m3fn); CHECK_BF16(Y);
+  CHECK_INNER(X); CHECK_INNER(Y); CHECK_DT(xs, at::kFloat); CHECK_DT(ws, at::kFloat);
+  TORCH_CHECK(W.dim() == 3 && W.is_contiguous() && ws.is_contiguous(), "W [E, N, K] / ws contiguous");
+  const int E = W.size(0), N = W.size(1), K = W.size(2);
+  TORCH_CHECK(X.size(1) == K && K % 16 == 0 && X.stride(0) % 16 == 0, "moe_gemm_fp8: K");
+  TORCH_CHECK(ws.dim() == 3 && ws.size(0) == E && ws.size(1) == (N + 127) / 128 && ws.size(2) == (K + 127) / 128,
+              "ws [E, ceil(N/128), ceil(K/128)]");
+  TORCH_CHECK(xs.dim() == 2 && xs.size(0) >= X.size(0) && xs.size(1) >= (K + 127) / 128 && xs.stride(1) == 1,
+              "xs [rows, ceil(K/128)]");
+  const int bm = llmd_moe_gemm_tile_m();
+  const int P = sorted_ids.numel();
+  TORCH_CHECK(P % bm == 0 && tile_expert.numel() >= P / bm && Y.size(0) >= P, "moe_gemm_fp8: rows");
+  TORCH_CHECK(Y.size(1) >= (mode == 1 ? N / 2 : N) && N % 2 == 0, "moe_gemm_fp8: Y width");
+  const void* bp = nullptr;
+  if (bias.has_value()) {
+    CHECK_BF16(bias.value());
+    TORCH_CHECK(bias->is_contiguous() && bias->numel() == (int64_t)E * N, "bias [E, N]");
+    bp = bias->data_ptr();
+  }
+  llmd_moe_gemm_fp8(X.data_ptr(), X.stride(0), xs.data_ptr<float>(), xs.stride(0), topk, sorted_ids.data_ptr<int>(),
+                    tile_expert.data_ptr<int>(), P / bm, W.data_ptr(), W.stride(0), ws.data_ptr<float>(), N, K,
+                    Y.data_ptr(), Y.stride(0), mode, act, (float)alpha, (float)limit, a_rows_are_slots ? 1 : 0, bp,
+                    cur_stream());
+}
+
 // ---------------------------------------------------------------- symm heap
 torch::Tensor symm_alloc(int64_t bytes, int64_t device) {
   const c10::hip::HIPGuard guard((c10::DeviceIndex)device);
@@ -648,6 +695,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("moe_combine", &moe_combine);
   m.def("moe_tile_m", &llmd_moe_gemm_tile_m);
   m.def("quant_fp8_rows", &quant_fp8_rows);
+  m.def("quant_fp8_groups", &quant_fp8_groups);
+  m.def("moe_gemm_fp8", &moe_gemm_fp8);
   m.def("symm_alloc", &symm_alloc);
   m.def("symm_error", &symm_error);
   m.def("symm_sig_bytes", &llmd_symm_sig_bytes);

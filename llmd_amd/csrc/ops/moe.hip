@@ -324,6 +324,164 @@ __global__ __launch_bounds__(NT, 2) void moe_gemm_kernel(
   }
 }
 
+// ---------------------------------------------------------------- FP8 grouped GEMM
+// DeepGEMM role: e4m3fn operands with DeepSeek-style block
+// scales - activations per (row, 128-K group) xs[row][kb], weights per
+// (128-N x 128-K block) ws[e][nb][kb]. Same 64x128 tile and 4-wave layout as
+// the bf16 kernel; a K-step is 128 fp8 = one scale block = the same 128-byte
+// LDS row, so staging is byte-identical. Each K-step accumulates 4
+// mfma_f32_16x16x32_fp8_fp8 into a block accumulator that is folded into the
+// output accumulator with (xs[row][kb] * ws[e][nb][kb]) - exact block scaling,
+// f32 accumulation. BN = 128 = the weight block height, so one weight scale per
+// workgroup per K-step.
+constexpr int BK8 = 128;
+constexpr int LDA8 = BK8 + 16;  // bytes
+
+template <int MODE>
+__global__ __launch_bounds__(NT, 2) void moe_gemm_fp8_kernel(
+    const uint8_t* __restrict__ X, int64_t x_stride, const float* __restrict__ xs, int64_t xs_stride, int topk,
+    const int* __restrict__ sorted_ids, const int* __restrict__ tile_expert, const uint8_t* __restrict__ W,
+    int64_t w_expert_stride, const float* __restrict__ ws, int N, int K, uint16_t* __restrict__ Y,
+    int64_t y_stride, int act, float alpha, float limit, int a_rows_are_slots, const uint16_t* __restrict__ bias) {
+  __shared__ __attribute__((aligned(16))) uint8_t As[2][BM][LDA8];
+  __shared__ __attribute__((aligned(16))) uint8_t Bs[2][BN][LDA8];
+  const int mt = blockIdx.y, nt = blockIdx.x;
+  const int e = tile_expert[mt];
+  if (e < 0) return;
+  const int m0 = mt * BM, n0 = nt * BN;
+  const int nkb = (K + BK8 - 1) / BK8, nnb = (N + BN - 1) / BN;
+  const uint8_t* We = W + (int64_t)e * w_expert_stride;
+  const float* wse = ws + ((int64_t)e * nnb + nt) * nkb;
+  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+  const int wm = w >> 1, wn = w & 1;
+  const int r16 = lane & 15, kq = lane >> 4;
+  auto tok_of = [&](int row) {
+    const int sid = sorted_ids[row];
+    return sid < 0 ? -1 : (a_rows_are_slots ? sid : sid / topk);
+  };
+  int arow[2], achk[2];
+  const uint8_t* aptr[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int c = tid + NT * i;
+    arow[i] = c >> 3;
+    achk[i] = c & 7;
+    const int tok = tok_of(m0 + arow[i]);
+    aptr[i] = tok < 0 ? nullptr : X + (int64_t)tok * x_stride;
+  }
+  // activation-scale rows of this lane's output rows (i, r)
+  const float* xsr[2][4];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int tok = tok_of(m0 + wm * 32 + i * 16 + kq * 4 + r);
+      xsr[i][r] = tok < 0 ? nullptr : xs + (int64_t)tok * xs_stride;
+    }
+  u32x4_t ra[2], rb[4];
+  auto load = [&](int k0) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      u32x4_t v = {0, 0, 0, 0};
+      if (aptr[i] && k0 + achk[i] * 16 < K) v = *reinterpret_cast<const u32x4_t*>(aptr[i] + k0 + achk[i] * 16);
+      ra[i] = v;
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int c = tid + NT * i;
+      const int r = c >> 3, ch = c & 7;
+      u32x4_t v = {0, 0, 0, 0};
+      if (n0 + r < N && k0 + ch * 16 < K)
+        v = *reinterpret_cast<const u32x4_t*>(We + (int64_t)(n0 + r) * K + k0 + ch * 16);
+      rb[i] = v;
+    }
+  };
+  auto store = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) *reinterpret_cast<u32x4_t*>(&As[buf][arow[i]][achk[i] * 16]) = ra[i];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int c = tid + NT * i;
+      *reinterpret_cast<u32x4_t*>(&Bs[buf][c >> 3][(c & 7) * 16]) = rb[i];
+    }
+  };
+  f32x4_t acc[2][4];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  load(0);
+  store(0);
+  __syncthreads();
+  for (int kt = 0; kt < nkb; ++kt) {
+    const int buf = kt & 1;
+    if (kt + 1 < nkb) load((kt + 1) * BK8);
+    f32x4_t blk[2][4];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) blk[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ks = 0; ks < BK8 / 32; ++ks) {
+      long af[2], bfr[4];
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+        af[i] = *reinterpret_cast<const long*>(&As[buf][wm * 32 + i * 16 + r16][ks * 32 + kq * 8]);
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        bfr[j] = *reinterpret_cast<const long*>(&Bs[buf][wn * 64 + j * 16 + r16][ks * 32 + kq * 8]);
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) blk[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_fp8_fp8(af[i], bfr[j], blk[i][j], 0, 0, 0);
+    }
+    const float wsv = wse[kt];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float sc = xsr[i][r] ? xsr[i][r][kt] * wsv : 0.f;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j][r] += blk[i][j][r] * sc;
+      }
+    if (kt + 1 < nkb) {
+      __syncthreads();
+      store(buf ^ 1);
+      __syncthreads();
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int row = m0 + wm * 32 + i * 16 + kq * 4 + r;
+      if (sorted_ids[row] < 0) continue;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int col = n0 + wn * 64 + j * 16 + r16;
+        float v = acc[i][j][r];
+        if (bias && col < N) v += bf2f(bias[(int64_t)e * N + col]);
+        if (MODE == 0) {
+          if (col < N) Y[(int64_t)row * y_stride + col] = f2bf(v);
+        } else {
+          const float other = __shfl_xor(v, 1, 64);
+          if ((r16 & 1) == 0) {
+            float g = v, u = other, o;
+            if (act == 2) {
+              g = fminf(g, limit);
+              u = fminf(fmaxf(u, -limit), limit);
+              o = (u + 1.f) * g / (1.f + __expf(-alpha * g));
+            } else {
+              o = g / (1.f + __expf(-g)) * u;
+            }
+            if (col < N) Y[(int64_t)row * y_stride + col / 2] = f2bf(o);
+          }
+        }
+      }
+    }
+  }
+}
+
 // out[t, :] = sum_j w[t, j] * Y[pos(t, j), :]  with pos from the inverse permutation
 __global__ __launch_bounds__(256) void moe_combine_kernel(const uint16_t* __restrict__ Y, int64_t y_stride,
                                                           const int* __restrict__ inv, const float* __restrict__ w,
@@ -389,6 +547,22 @@ void llmd_moe_gemm(const void* X, int64_t x_stride, int topk, const int* sorted_
     hipLaunchKernelGGL(moe_gemm_kernel<1>, grid, dim3(NT), 0, st, (const uint16_t*)X, x_stride, topk, sorted_ids,
                        tile_expert, (const uint16_t*)W, w_expert_stride, N, K, (uint16_t*)Y, y_stride, act, alpha,
                        limit, a_rows_are_slots, (const uint16_t*)bias);
+}
+
+void llmd_moe_gemm_fp8(const void* X, int64_t x_stride, const float* xs, int64_t xs_stride, int topk,
+                       const int* sorted_ids, const int* tile_expert, int num_tiles, const void* W,
+                       int64_t w_expert_stride, const float* ws, int N, int K, void* Y, int64_t y_stride, int mode,
+                       int act, float alpha, float limit, int a_rows_are_slots, const void* bias, hipStream_t st) {
+  if (num_tiles == 0) return;
+  dim3 grid((N + BN - 1) / BN, num_tiles);
+  if (mode == 0)
+    hipLaunchKernelGGL(moe_gemm_fp8_kernel<0>, grid, dim3(NT), 0, st, (const uint8_t*)X, x_stride, xs, xs_stride,
+                       topk, sorted_ids, tile_expert, (const uint8_t*)W, w_expert_stride, ws, N, K, (uint16_t*)Y,
+                       y_stride, act, alpha, limit, a_rows_are_slots, (const uint16_t*)bias);
+  else
+    hipLaunchKernelGGL(moe_gemm_fp8_kernel<1>, grid, dim3(NT), 0, st, (const uint8_t*)X, x_stride, xs, xs_stride,
+                       topk, sorted_ids, tile_expert, (const uint8_t*)W, w_expert_stride, ws, N, K, (uint16_t*)Y,
+                       y_stride, act, alpha, limit, a_rows_are_slots, (const uint16_t*)bias);
 }
 
 void llmd_moe_combine(const void* Y, int64_t y_stride, const int* inv, const float* w, int T, int topk, int d,

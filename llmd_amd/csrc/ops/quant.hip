@@ -48,7 +48,47 @@ __global__ __launch_bounds__(NT) void quant_fp8_rows_kernel(const uint16_t* __re
   }
 }
 
+// Per (row, 128-element group) scales (DeepSeek / DeepGEMM activation format):
+// 16 consecutive lanes own one group's 16 packets; the group amax is a 16-lane
+// xor-shuffle reduction. s[t][g] = amax / 448.
+__global__ __launch_bounds__(NT) void quant_fp8_groups_kernel(const uint16_t* __restrict__ x, int64_t xs,
+                                                              uint8_t* __restrict__ q, int64_t qs,
+                                                              float* __restrict__ scale, int64_t ss, int d,
+                                                              float floor_) {
+  const int64_t t = blockIdx.x;
+  const u32x4_t* xr = reinterpret_cast<const u32x4_t*>(x + t * xs);
+  u32x2_t* qr = reinterpret_cast<u32x2_t*>(q + t * qs);
+  const int nc = d / 8;
+  const int span = (nc + 15) / 16 * 16;
+  for (int c0 = 0; c0 < span; c0 += NT) {
+    const int c = c0 + threadIdx.x;
+    const bool ok = c < nc;
+    float f[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (ok) unpack8(xr[c], f);
+    float a = 0.f;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) a = fmaxf(a, fabsf(f[i]));
+#pragma unroll
+    for (int o = 8; o > 0; o >>= 1) a = fmaxf(a, __shfl_xor(a, o, 64));
+    const float s = fmaxf(a / FP8_MAX, floor_);
+    if (ok && (c & 15) == 0) scale[t * ss + c / 16] = s;
+    const float inv = 1.f / s;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) f[i] *= inv;
+    if (ok) qr[c] = f32x8_to_fp8(f);
+  }
+}
+
 }  // namespace
+
+extern "C" int llmd_quant_fp8_groups(const void* x, int64_t xs, void* q, int64_t qs, float* scale, int64_t ss,
+                                     int T, int d, hipStream_t st) {
+  if (T == 0) return 0;
+  if (d % 8) return -1;
+  hipLaunchKernelGGL(quant_fp8_groups_kernel, dim3(T), dim3(NT), 0, st, (const uint16_t*)x, xs, (uint8_t*)q, qs,
+                     scale, ss, d, 1e-12f);
+  return (int)hipGetLastError();
+}
 
 extern "C" int llmd_quant_fp8_rows(const void* x, int64_t xs, void* q, int64_t qs, float* scale, int T, int d,
                                    hipStream_t st) {

@@ -31,7 +31,7 @@ from llmd_amd.parallel.comm import tp_all_reduce
 from llmd_amd.parallel.ep import ep_active, moe_ep
 from llmd_amd.parallel.state import get_state
 
-from .layers import ColumnLinear, LMHead, RMSNorm, RowLinear, VocabEmbedding, _init_weight
+from .layers import ColumnLinear, LMHead, RMSNorm, RowLinear, VocabEmbedding, _init_weight, run_experts
 from .llama import LlamaMLP
 
 KV_LORA, NOPE, ROPE, VDIM = 512, 128, 64, 128
@@ -139,13 +139,13 @@ class DeepseekMoE(torch.nn.Module):
                               routed_scale=cfg.routed_scaling_factor)
         if self.dp_ep:  # tokens differ per rank: exchange them with the expert owners
             y = moe_ep(x, ids, w, self.E_local,
-                       lambda xx, ii, ww: ops.moe_experts(xx, ii, ww, self.w1, self.w2, ops.ACT_SILU))
+                       lambda xx, ii, ww: run_experts(self, xx, ii, ww, ops.ACT_SILU))
             return y + self.shared(x) if self.shared is not None else y
         if self.tp > 1:  # tokens replicated over TP: mask to the local experts, one all-reduce
             local = (ids >= self.lo) & (ids < self.lo + self.E_local)
             ids = torch.where(local, ids - self.lo, torch.full_like(ids, -1))
             w = torch.where(local, w, torch.zeros_like(w))
-        y = ops.moe_experts(x, ids, w, self.w1, self.w2, ops.ACT_SILU)
+        y = run_experts(self, x, ids, w, ops.ACT_SILU)
         if self.shared is not None:
             y = y + self.shared(x)
         return tp_all_reduce(y) if self.tp > 1 else y

@@ -28,7 +28,7 @@ from llmd_amd.parallel.comm import tp_all_reduce
 from llmd_amd.parallel.ep import ep_active, moe_ep
 from llmd_amd.parallel.state import get_state
 
-from .layers import _init_weight
+from .layers import _init_weight, run_experts
 from .llama import LlamaDecoderLayer, LlamaForCausalLM
 
 
@@ -63,10 +63,9 @@ class GptOssMoE(torch.nn.Module):
         logits = F.linear(x, self.router_w, self.router_b).float()
         ids, w = ops.moe_topk(logits, self.k, scoring=2)
         if not self.ep:
-            return ops.moe_experts(x, ids, w, self.w1, self.w2, ops.ACT_SWIGLU_OAI, self.alpha, self.limit,
-                                   b1=self.b1, b2=self.b2)
-        fn = lambda xx, ii, ww: ops.moe_experts(xx, ii, ww, self.w1, self.w2, ops.ACT_SWIGLU_OAI,  # noqa: E731
-                                                self.alpha, self.limit, b1=self.b1, b2=self.b2)
+            return run_experts(self, x, ids, w, ops.ACT_SWIGLU_OAI, self.alpha, self.limit, b1=self.b1, b2=self.b2)
+        fn = lambda xx, ii, ww: run_experts(self, xx, ii, ww, ops.ACT_SWIGLU_OAI,  # noqa: E731
+                                            self.alpha, self.limit, b1=self.b1, b2=self.b2)
         if self.dp_ep:  # DP+EP: all-gather/reduce-scatter or all-to-all dispatch/combine
             return moe_ep(x, ids, w, self.E_local, fn)
         # EP over TP ranks (tokens replicated): local experts only, then one all-reduce.

@@ -39,9 +39,10 @@ def _linear(mod, x, bias):
 
 def quantize_fp8(model: torch.nn.Module) -> int:
     """Online FP8 weight quantisation (vLLM ``--quantization fp8``): every
-    Column/Row linear gets e4m3fn weights with per-output-channel scales;
-    embeddings, LM head, norms, routers and expert weights stay bf16.
-    Returns the number of quantised linears."""
+    Column/Row linear gets e4m3fn weights with per-output-channel scales, and
+    routed-expert weights (modules with 3-D ``w1``/``w2``) get DeepSeek-style
+    128x128 block scales for the fp8 grouped GEMM. Embeddings, LM head, norms
+    and routers stay bf16. Returns the number of quantised tensors."""
     n = 0
     for m in model.modules():
         if isinstance(m, (ColumnLinear, RowLinear)) and m.weight.dtype == torch.bfloat16:
@@ -49,7 +50,22 @@ def quantize_fp8(model: torch.nn.Module) -> int:
             m.weight = torch.nn.Parameter(wq, requires_grad=False)
             m.weight_scale = torch.nn.Parameter(s, requires_grad=False)
             n += 1
+        for name in ("w1", "w2"):
+            w = getattr(m, name, None)
+            if isinstance(w, torch.Tensor) and w.dim() == 3 and w.dtype == torch.bfloat16:
+                wq, s = ops.quant_fp8_block_weight(w.data)
+                setattr(m, name, torch.nn.Parameter(wq, requires_grad=False))
+                setattr(m, name + "_scale", torch.nn.Parameter(s, requires_grad=False))
+                n += 1
     return n
+
+
+def run_experts(mod, x, ids, w, act, alpha=1.702, limit=7.0, b1=None, b2=None):
+    """Routed-expert FFN of an MoE module: bf16 or block-fp8 grouped GEMMs."""
+    if mod.w1.dtype == torch.float8_e4m3fn:
+        return ops.moe_experts_fp8(x, ids, w, mod.w1, mod.w1_scale, mod.w2, mod.w2_scale, act, alpha, limit,
+                                   b1=b1, b2=b2)
+    return ops.moe_experts(x, ids, w, mod.w1, mod.w2, act, alpha, limit, b1=b1, b2=b2)
 
 
 class ColumnLinear(torch.nn.Module):

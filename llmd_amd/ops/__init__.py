@@ -221,6 +221,84 @@ def fp8_linear(x: torch.Tensor, wq: torch.Tensor, w_scale: torch.Tensor, bias=No
     return y.reshape(*lead, -1)
 
 
+def quant_fp8_groups(x: torch.Tensor, group: int = 128):
+    """Per (token, 128-group) fp8: x [T, d] -> (q [T, d] e4m3fn, scale [T, ceil(d/128)] f32)."""
+    T, d = x.shape
+    ng = (d + group - 1) // group
+    if not _gpu(x):
+        pad = ng * group - d
+        xf = torch.nn.functional.pad(x.float(), (0, pad)).view(T, ng, group)
+        s = (xf.abs().amax(2) / FP8_MAX).clamp(min=1e-12)
+        q = (xf / s[:, :, None]).clamp(-FP8_MAX, FP8_MAX).view(T, ng * group)[:, :d].to(FP8)
+        return q, s
+    assert group == 128
+    x = x if x.stride(-1) == 1 and x.stride(0) % 8 == 0 else x.contiguous()
+    q = torch.empty(x.shape, dtype=FP8, device=x.device)
+    s = torch.empty(T, ng, dtype=torch.float32, device=x.device)
+    native().quant_fp8_groups(x, q, s)
+    return q, s
+
+
+def quant_fp8_block_weight(w: torch.Tensor, block: int = 128):
+    """Expert weights [E, N, K] -> (e4m3fn, scales [E, ceil(N/128), ceil(K/128)]) per 128x128 block."""
+    E, N, K = w.shape
+    nb, kb = (N + block - 1) // block, (K + block - 1) // block
+    wf = torch.nn.functional.pad(w.float(), (0, kb * block - K, 0, nb * block - N))
+    wf = wf.view(E, nb, block, kb, block)
+    s = (wf.abs().amax(dim=(2, 4)) / FP8_MAX).clamp(min=1e-12)
+    q = (wf / s[:, :, None, :, None]).clamp(-FP8_MAX, FP8_MAX)
+    q = q.view(E, nb * block, kb * block)[:, :N, :K].contiguous().to(FP8)
+    return q, s.contiguous()
+
+
+def dequant_fp8_block_weight(q: torch.Tensor, s: torch.Tensor, block: int = 128) -> torch.Tensor:
+    E, N, K = q.shape
+    full = s.repeat_interleave(block, 1).repeat_interleave(block, 2)[:, :N, :K]
+    return q.float() * full
+
+
+def moe_experts_fp8(x, ids, wts, w1q, w1s, w2q, w2s, act=0, alpha=1.702, limit=7.0, out=None, b1=None, b2=None):
+    """Block-scaled FP8 routed experts (DeepGEMM role): activations quantised per
+    (token, 128) group, grouped fp8 MFMA GEMMs with 128x128 weight-block scales,
+    the gated activation fused into GEMM 1, bf16 weighted combine."""
+    if not _gpu(x):
+        xq, xs = quant_fp8_groups(x)
+        xd = (xq.float().view(x.shape[0], -1) * xs.repeat_interleave(128, 1)[:, :x.shape[1]]).to(torch.bfloat16)
+        r = ref.moe_forward(xd, ids, wts, dequant_fp8_block_weight(w1q, w1s).to(torch.bfloat16),
+                            dequant_fp8_block_weight(w2q, w2s).to(torch.bfloat16), act, alpha, limit, b1, b2)
+        if out is not None:
+            out.copy_(r)
+            return out
+        return r
+    C = native()
+    T, d = x.shape
+    k = ids.shape[1]
+    E, N1, _ = w1q.shape
+    F = N1 // 2
+    bm = C.moe_tile_m()
+    n = T * k
+    max_p = ((n + E * (bm - 1)) + bm - 1) // bm * bm
+    dev = x.device
+    sorted_ids = torch.empty(max_p, dtype=torch.int32, device=dev)
+    tile_e = torch.empty(max_p // bm, dtype=torch.int32, device=dev)
+    offs = torch.empty(E + 1, dtype=torch.int32, device=dev)
+    total = torch.empty(1, dtype=torch.int32, device=dev)
+    inv = torch.full((n,), -1, dtype=torch.int32, device=dev)
+    C.moe_align(ids.contiguous().view(-1).to(torch.int32), E, sorted_ids, tile_e, offs, total, inv)
+    xq, xs = quant_fp8_groups(x)
+    h = torch.empty(max_p, F, dtype=torch.bfloat16, device=dev)
+    C.moe_gemm_fp8(xq, xs, k, sorted_ids, tile_e, w1q, w1s, h, 1, act, alpha, limit, False, b1)
+    hq, hs = quant_fp8_groups(h)
+    y = torch.empty(max_p, d, dtype=torch.bfloat16, device=dev)
+    ident = torch.arange(max_p, dtype=torch.int32, device=dev)
+    ident = torch.where(sorted_ids >= 0, ident, torch.full_like(ident, -1))
+    C.moe_gemm_fp8(hq, hs, 1, ident, tile_e, w2q, w2s, y, 0, 0, 0.0, 0.0, True, b2)
+    if out is None:
+        out = torch.empty(T, d, dtype=torch.bfloat16, device=dev)
+    C.moe_combine(y, inv, wts.contiguous().view(-1).float(), k, out)
+    return out
+
+
 # ---------------------------------------------------------------- sampling
 def sample(logits, temps=None, seeds=None, out_ids=None, want_logprob=False, generator=None):
     if not _gpu(logits):

@@ -1,0 +1,48 @@
+"""Grouped expert GEMM microbenchmark: bf16 vs block-fp8 (moe_experts /
+moe_experts_fp8) at DeepSeek-V3 EP8 shapes (32 local experts, d=7168,
+F=2048, top-8) and gpt-oss-120b (128 experts, d=F=2880, top-4).
+  python scripts/bench_moe.py"""
+import os
+import sys
+import time
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from llmd_amd import ops  # noqa: E402
+
+
+def t_it(fn, it=20):
+    for _ in range(3):
+        fn()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(it):
+        fn()
+    torch.cuda.synchronize()
+    return (time.perf_counter() - t0) / it
+
+
+def run(name, T, E, k, d, F, act):
+    dev = "cuda"
+    x = torch.randn(T, d, device=dev, dtype=torch.bfloat16)
+    w1 = torch.randn(E, 2 * F, d, device=dev, dtype=torch.bfloat16) * 0.02
+    w2 = torch.randn(E, d, F, device=dev, dtype=torch.bfloat16) * 0.02
+    w1q, w1s = ops.quant_fp8_block_weight(w1)
+    w2q, w2s = ops.quant_fp8_block_weight(w2)
+    ids, wts = ops.moe_topk(torch.randn(T, E, device=dev), k, scoring=0)
+    tb = t_it(lambda: ops.moe_experts(x, ids, wts, w1, w2, act))
+    tf = t_it(lambda: ops.moe_experts_fp8(x, ids, wts, w1q, w1s, w2q, w2s, act))
+    active = min(E, T * k)
+    flops = 2 * T * k * (2 * F * d + d * F)
+    wbytes_bf = active * 3 * F * d * 2
+    print(f"{name} T={T}: bf16 {tb * 1e3:.3f} ms ({flops / tb / 1e12:.0f} TF/s, {wbytes_bf / tb / 1e9:.0f} GB/s w) | "
+          f"fp8 {tf * 1e3:.3f} ms ({flops / tf / 1e12:.0f} TF/s, {wbytes_bf / 2 / tf / 1e9:.0f} GB/s w) "
+          f"speedup {tb / tf:.2f}x", flush=True)
+
+
+if __name__ == "__main__":
+    for T in (64, 256, 4096):
+        run("deepseek-ep8", T, 32, 8, 7168, 2048, 0)
+    for T in (64, 1024):
+        run("gpt-oss-120b", T, 128, 4, 2880, 2880, 2)

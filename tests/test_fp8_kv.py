@@ -179,3 +179,55 @@ def test_fp8_linear_gpu(T, K, N):
     y = ops.fp8_linear(x, wq, ws)
     r = (xq.float() * xs) @ (wq.float() * ws.view(-1, 1)).t()
     torch.testing.assert_close(y.float(), r, atol=2e-2 * r.abs().max().item(), rtol=2e-2)
+
+
+def test_moe_fp8_block_quant_cpu():
+    torch.manual_seed(0)
+    E, N, K = 3, 200, 272
+    w = torch.randn(E, N, K) * 0.05
+    q, s = ops.quant_fp8_block_weight(w)
+    assert q.shape == (E, N, K) and s.shape == (E, 2, 3)
+    back = ops.dequant_fp8_block_weight(q, s)
+    assert (back - w).abs().max() < 0.07 * w.abs().max()
+    x = torch.randn(5, 300).to(torch.bfloat16)
+    xq, xs = ops.quant_fp8_groups(x)
+    assert xs.shape == (5, 3)
+    xd = xq.float() * xs.repeat_interleave(128, 1)[:, :300]
+    assert (xd - x.float()).abs().max() < 0.07 * x.float().abs().max()
+
+
+def test_engine_fp8_moe_cpu():
+    from llmd_amd.engine.config import EngineConfig
+    from llmd_amd.engine.engine import LLMEngine
+    from llmd_amd.engine.request import SamplingParams
+
+    cfg = EngineConfig.create("tiny-gpt-oss", device="cpu", block_size=16, num_gpu_blocks=64,
+                              max_num_batched_tokens=256, max_num_seqs=4, max_model_len=512, quantization="fp8")
+    eng = LLMEngine(cfg, capture_graphs=False)
+    mlp = eng.runner.model.layers[0].mlp
+    assert mlp.w1.dtype == F8 and mlp.w1_scale.dim() == 3
+    reqs = eng.generate([list(range(3, 30))], SamplingParams(max_tokens=3, temperature=0.0, ignore_eos=True))
+    assert len(reqs[0].output_token_ids) == 3
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("T,E,k,d,F,act", [(1, 8, 2, 256, 128, 0), (37, 32, 4, 2880, 2880, 2),
+                                           (100, 16, 8, 7168, 2048, 0), (64, 128, 4, 2880, 2880, 2)])
+def test_moe_experts_fp8_gpu(T, E, k, d, F, act):
+    torch.manual_seed(0)
+    dev = "cuda"
+    x = torch.randn(T, d, device=dev, dtype=torch.bfloat16)
+    w1 = torch.randn(E, 2 * F, d, device=dev, dtype=torch.bfloat16) * 0.03
+    w2 = torch.randn(E, d, F, device=dev, dtype=torch.bfloat16) * 0.03
+    w1q, w1s = ops.quant_fp8_block_weight(w1)
+    w2q, w2s = ops.quant_fp8_block_weight(w2)
+    logits = torch.randn(T, E, device=dev)
+    ids, wts = ops.moe_topk(logits, k, scoring=0)
+    # group quant matches the CPU reference
+    xq, xs = ops.quant_fp8_groups(x)
+    rq, rs = ops.quant_fp8_groups(x.cpu())
+    torch.testing.assert_close(xs.cpu(), rs, rtol=1e-6, atol=0)
+    y = ops.moe_experts_fp8(x, ids, wts, w1q, w1s, w2q, w2s, act)
+    r = ops.moe_experts_fp8(x.cpu(), ids.cpu(), wts.cpu(), w1q.cpu(), w1s.cpu(), w2q.cpu(), w2s.cpu(), act)
+    err = (y.float().cpu() - r.float()).abs().max().item()
+    assert err < 0.06 * r.float().abs().max().item() + 1e-3, err
