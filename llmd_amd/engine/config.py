@@ -242,6 +242,8 @@ class ParallelConfig:
     distributed_backend: str = "nccl"
     all2all_backend: str = "allgather_reducescatter"  # wide-EP token exchange (parallel/ep.py)
     disable_custom_all_reduce: bool = False  # TP all-reduce over the symm IPC heap (parallel/symm.py)
+    enable_eplb: bool = False  # expert load balancing with redundant experts (parallel/eplb.py)
+    eplb_config: Optional[dict] = None  # {"window_size", "step_interval", "num_redundant_experts"}
 
 
 @dataclass
@@ -326,6 +328,8 @@ def add_engine_args(p: argparse.ArgumentParser) -> argparse.ArgumentParser:
                    choices=["allgather_reducescatter", "alltoall", "symm_ll", "deepep_low_latency",
                             "deepep_high_throughput"])
     p.add_argument("--disable-custom-all-reduce", action="store_true")
+    p.add_argument("--enable-eplb", action="store_true")
+    p.add_argument("--eplb-config", type=_json_arg, default=None)
     p.add_argument("--enforce-eager", action="store_true")
     p.add_argument("--kv-transfer-config", type=_json_arg, default=None)
     p.add_argument("--kv-events-config", type=_json_arg, default=None)
@@ -351,6 +355,7 @@ def engine_config_from_args(a) -> EngineConfig:
         data_parallel_rank=a.data_parallel_rank, enable_expert_parallel=a.enable_expert_parallel,
         all2all_backend=getattr(a, "all2all_backend", "allgather_reducescatter"),
         disable_custom_all_reduce=getattr(a, "disable_custom_all_reduce", False),
+        enable_eplb=getattr(a, "enable_eplb", False), eplb_config=getattr(a, "eplb_config", None),
         enforce_eager=a.enforce_eager, kv_transfer_config=a.kv_transfer_config,
         kv_events_config=a.kv_events_config, kv_offload_config=a.kv_offload_config,
         policy=a.scheduling_policy, enable_lora=getattr(a, "enable_lora", False),

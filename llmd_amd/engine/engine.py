@@ -149,11 +149,13 @@ class LLMEngine:
         ep.set_step_rows(0 if bucket is not None else t_max)
         if so.empty:
             self.runner.execute_dummy(bucket)
+            self.runner.eplb_tick()
             self._flush_events()
             return err_outs
         if self.offload is not None:
             self.offload.before_step(so)
         sampled = self.runner.execute(so, self.block_tables(so), force_eager=bucket is None, bucket=bucket)
+        self.runner.eplb_tick()
         return self._finish_step(so, sampled, err_outs, t0)
 
     def dp_has_unfinished(self) -> bool:

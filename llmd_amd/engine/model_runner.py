@@ -65,6 +65,9 @@ class ModelRunner:
         self.width = math.ceil(self.max_model_len / self.bs) + 1
         torch.manual_seed(cfg.seed)
         t0 = time.time()
+        from llmd_amd.parallel import eplb
+
+        eplb.configure(cfg.parallel.enable_eplb, cfg.parallel.eplb_config)
         self.model = build_model(self.mc, device=self.device, max_pos=self.max_model_len + 1)
         if cfg.load_format in ("safetensors", "auto") and cfg.weights_path:
             from llmd_amd.models.loader import load_weights
@@ -106,6 +109,16 @@ class ModelRunner:
         self._rng = np.random.default_rng(cfg.seed)
         self.graph_plans: dict[int, tuple] = {}
         self._init_symm()
+
+    def eplb_tick(self):
+        """Count one executed forward for EPLB; rebalances every step_interval."""
+        from llmd_amd.parallel import eplb
+
+        if not eplb.config().enabled:
+            return False
+        mods = [m for m in self.model.modules() if getattr(m, "eplb", None) is not None]
+        return eplb.on_forward(group=get_state().ep_group,
+                               params_of=lambda: [(m.eplb, m.expert_params()) for m in mods])
 
     def _init_symm(self):
         """Symmetric IPC heap users (parallel/symm.py): the TP custom all-reduce

@@ -28,6 +28,7 @@ from llmd_amd.engine.attn_meta import AttnMeta
 from llmd_amd.engine.config import ModelConfig
 from llmd_amd.ops.reference import yarn_softmax_mscale
 from llmd_amd.parallel.comm import tp_all_reduce
+from llmd_amd.parallel import eplb
 from llmd_amd.parallel.ep import ep_active, moe_ep
 from llmd_amd.parallel.state import get_state
 
@@ -116,6 +117,10 @@ class DeepseekMoE(torch.nn.Module):
             raise ValueError(f"{E} experts do not split over EP={n_ep}")
         self.E, self.E_local, self.k = E, E // n_ep, cfg.num_experts_per_tok
         self.lo = r_ep * self.E_local
+        self.eplb = None
+        if self.dp_ep and eplb.config().enabled:  # physical slots incl. redundant replicas
+            self.eplb = eplb.EplbLayer(E, n_ep, r_ep, device, eplb.config().num_redundant_experts)
+            self.E_local = self.eplb.P_local
         self.cfg = cfg
         dt = torch.bfloat16
         self.gate = torch.nn.Parameter(_init_weight(torch.empty(E, d, device=device, dtype=dt), 0.02),
@@ -138,6 +143,8 @@ class DeepseekMoE(torch.nn.Module):
                               n_group=cfg.n_group, topk_group=cfg.topk_group, renorm=cfg.norm_topk_prob,
                               routed_scale=cfg.routed_scaling_factor)
         if self.dp_ep:  # tokens differ per rank: exchange them with the expert owners
+            if self.eplb is not None:
+                ids = self.eplb.route(ids)
             y = moe_ep(x, ids, w, self.E_local,
                        lambda xx, ii, ww: run_experts(self, xx, ii, ww, ops.ACT_SILU))
             return y + self.shared(x) if self.shared is not None else y
@@ -149,6 +156,15 @@ class DeepseekMoE(torch.nn.Module):
         if self.shared is not None:
             y = y + self.shared(x)
         return tp_all_reduce(y) if self.tp > 1 else y
+
+
+    def expert_params(self) -> list:
+        """Per-physical-slot tensors moved by EPLB rebalancing."""
+        ps = [self.w1.data, self.w2.data]
+        for nm in ("w1_scale", "w2_scale"):
+            if hasattr(self, nm):
+                ps.append(getattr(self, nm).data)
+        return ps
 
 
 def _shared_cfg(cfg: ModelConfig) -> ModelConfig:
@@ -243,8 +259,9 @@ class DeepseekForCausalLM(torch.nn.Module):
             specs.append((pre + "mlp.gate.weight", m.gate, "replicate", None))
             if m.bias is not None:
                 specs.append((pre + "mlp.gate.e_score_correction_bias", m.bias, "replicate", None))
+            logical = m.eplb.local_logical() if m.eplb is not None else [m.lo + i for i in range(m.E_local)]
             for el in range(m.E_local):
-                e = m.lo + el
+                e = logical[el]
                 ep = f"{pre}mlp.experts.{e}."
                 specs += [(ep + "gate_proj.weight", m.w1[el], "rows", (0, 2)),
                           (ep + "up_proj.weight", m.w1[el], "rows", (1, 2)),

@@ -25,6 +25,7 @@ import torch.nn.functional as F
 from llmd_amd import ops
 from llmd_amd.engine.config import ModelConfig
 from llmd_amd.parallel.comm import tp_all_reduce
+from llmd_amd.parallel import eplb
 from llmd_amd.parallel.ep import ep_active, moe_ep
 from llmd_amd.parallel.state import get_state
 
@@ -45,6 +46,10 @@ class GptOssMoE(torch.nn.Module):
         assert E % self.ep_size == 0
         self.E, self.E_local = E, E // self.ep_size
         self.k = cfg.num_experts_per_tok
+        self.eplb = None
+        if self.dp_ep and eplb.config().enabled:  # physical slots incl. redundant replicas
+            self.eplb = eplb.EplbLayer(E, self.ep_size, self.ep_rank, device, eplb.config().num_redundant_experts)
+            self.E_local = self.eplb.P_local
         d, Fh = cfg.hidden_size, cfg.moe_intermediate_size
         dt = torch.bfloat16
         self.router_w = torch.nn.Parameter(_init_weight(torch.empty(E, d, device=device, dtype=dt), 0.02),
@@ -67,6 +72,8 @@ class GptOssMoE(torch.nn.Module):
         fn = lambda xx, ii, ww: run_experts(self, xx, ii, ww, ops.ACT_SWIGLU_OAI,  # noqa: E731
                                             self.alpha, self.limit, b1=self.b1, b2=self.b2)
         if self.dp_ep:  # DP+EP: all-gather/reduce-scatter or all-to-all dispatch/combine
+            if self.eplb is not None:
+                ids = self.eplb.route(ids)
             return moe_ep(x, ids, w, self.E_local, fn)
         # EP over TP ranks (tokens replicated): local experts only, then one all-reduce.
         # b2 is added once per (token, expert) by the owner rank, so the sum stays exact.
@@ -74,6 +81,14 @@ class GptOssMoE(torch.nn.Module):
         local = (ids >= lo) & (ids < lo + self.E_local)
         y = fn(x, torch.where(local, ids - lo, torch.full_like(ids, -1)), torch.where(local, w, torch.zeros_like(w)))
         return tp_all_reduce(y)
+
+
+    def expert_params(self) -> list:
+        ps = [self.w1.data, self.b1.data, self.w2.data, self.b2.data]
+        for nm in ("w1_scale", "w2_scale"):
+            if hasattr(self, nm):
+                ps.append(getattr(self, nm).data)
+        return ps
 
 
 class GptOssDecoderLayer(LlamaDecoderLayer):
@@ -87,6 +102,8 @@ class GptOssForCausalLM(LlamaForCausalLM):
     def _mlp_specs(self, pre: str, mlp) -> list:
         """HF gpt-oss MoE tensors: router.{weight,bias}, experts.gate_up_proj [E, d, 2F]
         (gate/up interleaved columns), experts.down_proj [E, F, d] (+ biases)."""
+        if mlp.eplb is not None:
+            raise NotImplementedError("gpt-oss checkpoint loading with EPLB redundant experts")
         lo, n = mlp.ep_rank * mlp.E_local, mlp.E_local
         return [(pre + "mlp.router.weight", mlp.router_w, "replicate", None),
                 (pre + "mlp.router.bias", mlp.router_b, "replicate", None),
