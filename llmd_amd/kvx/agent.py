@@ -21,6 +21,13 @@ Side channel: length-prefixed msgpack request/response over TCP
 (VLLM_NIXL_SIDE_CHANNEL_HOST/PORT semantics; default port 5557).
 Fault injection: LLMD_KVX_FAULT=drop|delay:<s>|corrupt (probability
 LLMD_KVX_FAULT_P, default 1.0) for the failure-policy tests.
+Prefiller liveness (SGLang-style heartbeat, SURVEY M13,
+operations-sglang.md:93-98): the decode side pings every known prefiller
+every ``LLMD_KVX_HEARTBEAT_S`` (5 s) on a fresh connection; after
+``LLMD_KVX_HEARTBEAT_FAILS`` (2) consecutive misses the peer is marked dead,
+its cached connection and mapping are dropped, and pulls from it fail at once
+(-> kv_load_failure_policy) instead of hanging on a dead socket. A later
+successful ping revives it.
 """
 from __future__ import annotations
 
@@ -133,6 +140,51 @@ class KvxAgent:
         self.worker = threading.Thread(target=self._work, daemon=True, name="kvx-transfer")
         self.stream = None
         self.worker.start()
+        self.hb_interval = float(os.environ.get("LLMD_KVX_HEARTBEAT_S", "5"))
+        self.hb_max_fails = int(os.environ.get("LLMD_KVX_HEARTBEAT_FAILS", "2"))
+        self.hb_fails: dict[tuple, int] = {}
+        self.known_peers: set[tuple] = set()
+        self.dead_peers: set[tuple] = set()
+        self._stop = threading.Event()
+        if self.hb_interval > 0:
+            threading.Thread(target=self._heartbeat, daemon=True, name="kvx-heartbeat").start()
+
+    # ------------------------------------------------------------ liveness
+    def ping(self, key: tuple, timeout: float = 2.0) -> bool:
+        try:
+            with socket.create_connection(key, timeout=timeout) as s:
+                s.settimeout(timeout)
+                _send(s, {"op": "ping"})
+                return bool(_recv(s).get("ok"))
+        except (OSError, ConnectionError, struct.error, ValueError):
+            return False
+
+    def heartbeat_once(self):
+        for key in list(self.known_peers):
+            if self.ping(key):
+                self.hb_fails[key] = 0
+                if key in self.dead_peers:
+                    log.info("kvx peer %s:%d is back", *key)
+                    self.dead_peers.discard(key)
+                continue
+            n = self.hb_fails.get(key, 0) + 1
+            self.hb_fails[key] = n
+            if n >= self.hb_max_fails and key not in self.dead_peers:
+                log.warning("kvx peer %s:%d missed %d heartbeats: marking dead", key[0], key[1], n)
+                self.dead_peers.add(key)
+                p = self.peers.pop(key, None)
+                if p is not None:
+                    try:
+                        p["sock"].close()
+                    except OSError:
+                        pass
+
+    def _heartbeat(self):
+        while not self._stop.wait(self.hb_interval):
+            self.heartbeat_once()
+
+    def peer_status(self) -> dict:
+        return {f"{h}:{p}": ("dead" if (h, p) in self.dead_peers else "alive") for h, p in self.known_peers}
 
     def _serve_fds(self):
         fds = self.vmm["fds"]
@@ -199,6 +251,9 @@ class KvxAgent:
 
     def _peer(self, host, port) -> dict:
         key = (host, int(port))
+        self.known_peers.add(key)
+        if key in self.dead_peers:
+            raise RuntimeError(f"prefiller {host}:{port} failed its heartbeat")
         p = self.peers.get(key)
         if p is None:
             s = socket.create_connection(key, timeout=10)
@@ -360,6 +415,7 @@ class KvxAgent:
                 return out
 
     def close(self):
+        self._stop.set()
         self.jobs.put(None)
         self.server.shutdown()
         for p in self.peers.values():

@@ -93,3 +93,28 @@ def test_held_blocks_expire_without_reader():
     time.sleep(0.1)
     P.step()
     assert P.bm.num_free() == P.bm.num_blocks
+
+
+def test_prefiller_heartbeat_marks_dead_and_fails_fast(monkeypatch):
+    """M13: D pings known prefillers; after 2 misses pulls from that P fail at
+    once (recompute policy -> the request still completes locally)."""
+    monkeypatch.setenv("LLMD_KVX_HEARTBEAT_S", "0")  # drive heartbeats by hand
+    P = make(KT)
+    D = make(dict(KT, kv_load_failure_policy="recompute"))
+    prompt = list(range(20, 100))
+    sp1 = SamplingParams(max_tokens=1, temperature=0.0, ignore_eos=True)
+    _, op = run(P, "p1", prompt, sp1, {"do_remote_decode": True})
+    run(D, "d1", prompt, SamplingParams(max_tokens=2, temperature=0.0, ignore_eos=True), op.kv_transfer_params)
+    ag = D.connector.agent
+    key = (op.kv_transfer_params["remote_host"], int(op.kv_transfer_params["remote_port"]))
+    assert ag.peer_status()[f"{key[0]}:{key[1]}"] == "alive"
+    _, op2 = run(P, "p2", prompt[::-1], sp1, {"do_remote_decode": True})
+    P.connector.agent.server.shutdown()          # the prefiller's side channel goes away
+    P.connector.agent.server.server_close()
+    ag.heartbeat_once()
+    assert key not in ag.dead_peers               # one miss is tolerated
+    ag.heartbeat_once()
+    assert key in ag.dead_peers
+    r, o = run(D, "d2", prompt[::-1], SamplingParams(max_tokens=3, temperature=0.0, ignore_eos=True),
+               op2.kv_transfer_params)
+    assert o.finish_reason == "length" and len(r.output_token_ids) == 3   # recomputed locally
