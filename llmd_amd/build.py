@@ -135,6 +135,36 @@ def build_runtime(jobs: int = 8, verbose: bool = False) -> Path:
     return _link(objs, PKG / f"_rt{EXT}", ["-pthread"] + extra)
 
 
+def build_sanitized_runtime(verbose: bool = False) -> Path:
+    """ASan+UBSan executable embedding CPython with the runtime compiled in
+    (tests/native/rt_sanitize_main.cpp). Host code only - GPU
+    sanitizers are not used."""
+    rdir = CSRC / "runtime"
+    srcs = [s for s in sorted(rdir.glob("*.cpp")) if s.name != "module.cpp"]
+    main = PKG.parent / "tests" / "native" / "rt_sanitize_main.cpp"
+    out = BUILD / "rt_sanitize"
+    BUILD.mkdir(parents=True, exist_ok=True)
+    libdir = sysconfig.get_config_var("LIBDIR")
+    ver = sysconfig.get_config_var("LDVERSION")
+    flags = ["-O1", "-g", "-std=c++17", "-fsanitize=address,undefined", "-fno-omit-frame-pointer",
+             "-fno-sanitize-recover=undefined", f"-I{rdir}", f"-I{_pybind_inc()}", f"-I{_py_inc()}", "-pthread"]
+    odir = BUILD / "rt_san"
+    odir.mkdir(parents=True, exist_ok=True)
+    deps = _headers(rdir)
+    with cf.ThreadPoolExecutor(max_workers=min(8, os.cpu_count() or 4)) as ex:
+        objs = list(ex.map(lambda src: _compile(src, ["g++"], flags, deps, odir), srcs + [main]))
+    key = _hash(objs, flags)
+    stamp = out.with_name(out.name + ".stamp")
+    if out.exists() and stamp.exists() and stamp.read_text() == key:
+        return out
+    _run(["g++", "-fsanitize=address,undefined", "-pthread"] + [str(o) for o in objs] +
+         ["-o", str(out), f"-L{libdir}", f"-lpython{ver}", f"-Wl,-rpath,{libdir}"])
+    stamp.write_text(key)
+    if verbose:
+        print(f"[llmd build] {out}")
+    return out
+
+
 def build_all(jobs: int | None = None, verbose: bool = True):
     jobs = jobs or min(8, os.cpu_count() or 4)
     rt = build_runtime(jobs, verbose)
@@ -150,5 +180,7 @@ if __name__ == "__main__":
         build_ops(verbose=True)
     elif what == "rt":
         build_runtime(verbose=True)
+    elif what == "sanitize":
+        build_sanitized_runtime(verbose=True)
     else:
         build_all()
