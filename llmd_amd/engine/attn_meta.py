@@ -40,6 +40,9 @@ class AttnMeta:
     p_row_seq: Optional[torch.Tensor] = None       # [Tp] int32 prefill token -> p_block_tables row
     p_row_len: Optional[torch.Tensor] = None       # [Tp] int32 keys visible (= position + 1)
     p_max_ctx: int = 0
+    # multimodal: step rows that are image placeholders and their embeddings
+    mm_rows: Optional[torch.Tensor] = None         # [n] int64
+    mm_embeds: Optional[torch.Tensor] = None       # [n, d_model]
 
     @property
     def has_prefill(self) -> bool:

@@ -60,6 +60,9 @@ class ModelConfig:
     qk_nope_head_dim: int = 0
     qk_rope_head_dim: int = 0
     v_head_dim: int = 0
+    # multimodal (llava-style: vision tower + LM; models/vision.py)
+    vision_config: Optional[dict] = None
+    image_token_id: int = 0
     name: str = "custom"
 
     def __post_init__(self):
@@ -178,6 +181,20 @@ _register(ModelConfig(model_type="deepseek", name="deepseek-v2-lite", hidden_siz
                       first_k_dense_replace=1, q_lora_rank=None, kv_lora_rank=512, qk_nope_head_dim=128,
                       qk_rope_head_dim=64, v_head_dim=128, head_dim=192, bos_token_id=100000,
                       eos_token_id=100001), "deepseek-ai/DeepSeek-V2-Lite", "deepseek-ai/DeepSeek-V2-Lite-Chat")
+_register(ModelConfig(model_type="mixtral", name="mixtral-8x7b", hidden_size=4096, intermediate_size=14336,
+                      moe_intermediate_size=14336, num_hidden_layers=32, num_attention_heads=32,
+                      num_key_value_heads=8, head_dim=128, vocab_size=32000, rope_theta=1000000.0,
+                      num_local_experts=8, num_experts_per_tok=2, norm_topk_prob=True, bos_token_id=1,
+                      eos_token_id=2), "mistralai/Mixtral-8x7B-Instruct-v0.1")
+_register(ModelConfig(model_type="qwen3_moe", name="qwen3-30b-a3b", hidden_size=2048, intermediate_size=6144,
+                      moe_intermediate_size=768, num_hidden_layers=48, num_attention_heads=32,
+                      num_key_value_heads=4, head_dim=128, vocab_size=151936, rope_theta=1000000.0,
+                      rms_norm_eps=1e-6, num_local_experts=128, num_experts_per_tok=8, norm_topk_prob=True,
+                      bos_token_id=151643, eos_token_id=151645), "Qwen/Qwen3-30B-A3B")
+# multimodal (E/PD guide shape: Qwen2.5-VL-7B-class LM + ViT; image tokens = W*H/784)
+_register(_llama("llama-3-8b-vl", 4096, 14336, 32, 32, 8, model_type="llava", image_token_id=128256,
+                 vocab_size=128257, vision_config={"hidden_size": 1280, "num_layers": 32, "num_heads": 16}),
+          "llava-llama-3-8b")
 # tiny configs (CPU CI, smoke, GPU unit tests)
 _register(ModelConfig(model_type="llama", name="tiny-llama", hidden_size=256, intermediate_size=512,
                       num_hidden_layers=2, num_attention_heads=4, num_key_value_heads=2, head_dim=64,
@@ -187,6 +204,17 @@ _register(ModelConfig(model_type="llama", name="small-llama", hidden_size=1024, 
                       num_hidden_layers=4, num_attention_heads=8, num_key_value_heads=2, head_dim=128,
                       vocab_size=32000, max_position_embeddings=8192, rope_theta=10000.0,
                       bos_token_id=1, eos_token_id=2), "opt-125m-sized")
+_register(ModelConfig(model_type="llava", name="tiny-vl", hidden_size=256, intermediate_size=512,
+                      num_hidden_layers=2, num_attention_heads=4, num_key_value_heads=2, head_dim=64,
+                      vocab_size=513, max_position_embeddings=4096, rope_theta=10000.0, bos_token_id=1,
+                      eos_token_id=2, image_token_id=512,
+                      vision_config={"hidden_size": 64, "num_layers": 2, "num_heads": 4,
+                                     "max_pixels": 16 * 28 * 28, "min_pixels": 4 * 28 * 28}))
+_register(ModelConfig(model_type="qwen3_moe", name="tiny-moe", hidden_size=256, intermediate_size=512,
+                      moe_intermediate_size=128, num_hidden_layers=2, num_attention_heads=4,
+                      num_key_value_heads=2, head_dim=64, vocab_size=512, max_position_embeddings=4096,
+                      rope_theta=10000.0, num_local_experts=8, num_experts_per_tok=2, norm_topk_prob=True,
+                      bos_token_id=1, eos_token_id=2))
 _register(ModelConfig(model_type="gpt_oss", name="tiny-gpt-oss", hidden_size=256, intermediate_size=256,
                       moe_intermediate_size=256, num_hidden_layers=2, num_attention_heads=8,
                       num_key_value_heads=2, head_dim=64, vocab_size=512, rope_theta=10000.0,

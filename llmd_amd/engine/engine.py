@@ -81,9 +81,9 @@ class LLMEngine:
     def add_request(self, request_id: str, prompt_token_ids: list[int],
                     params: Optional[SamplingParams] = None, priority: int = 0,
                     kv_transfer_params: Optional[dict] = None, lora_id: int = 0,
-                    arrival_time: Optional[float] = None) -> Request:
+                    arrival_time: Optional[float] = None, mm_inputs: Optional[list] = None) -> Request:
         r = Request(request_id, list(prompt_token_ids), params or SamplingParams(), priority=priority,
-                    kv_transfer_params=kv_transfer_params, lora_id=lora_id)
+                    kv_transfer_params=kv_transfer_params, lora_id=lora_id, mm_inputs=mm_inputs or None)
         if arrival_time is not None:
             r.arrival_time = arrival_time
         self.sched.add_request(r)

@@ -364,7 +364,28 @@ class ModelRunner:
             for sr in so.prefills:
                 lo.extend([sr.req.lora_id] * sr.num_new_tokens)
             pl["lora"] = lo
+        mm = self._mm_rows(so)
+        if mm is not None:
+            pl["mm"] = mm
         return pl, reqs
+
+    def _mm_rows(self, so: SchedulerOutput):
+        """Image-placeholder rows of this step's prefill chunks + their embeddings."""
+        if not any(sr.req.mm_inputs for sr in so.prefills):
+            return None
+        from llmd_amd.models.vision import chunk_mm_rows
+
+        rows, embs = [], []
+        row0 = len(so.decodes)
+        for sr in so.prefills:
+            if sr.req.mm_inputs:
+                r, e = chunk_mm_rows(sr.req.mm_inputs, sr.start, sr.num_new_tokens, row0)
+                rows += r
+                embs += e
+            row0 += sr.num_new_tokens
+        if not rows:
+            return None
+        return rows, torch.cat([e.to(self.device) for e in embs])
 
     @torch.no_grad()
     def run_plan(self, pl: dict):
@@ -429,6 +450,10 @@ class ModelRunner:
             meta.p_items = self._items(p_ql, p_ctx)
         if self.is_mla:
             self._mla_rows(meta, nd, p_ql, p_ctx)
+        if pl.get("mm") is not None:
+            rows, embs = pl["mm"]
+            meta.mm_rows = torch.tensor(rows, dtype=torch.long).to(dev, non_blocking=True)
+            meta.mm_embeds = embs.to(dev)
         return self.model(hd[0], meta)
 
     # ------------------------------------------------------------ graphs

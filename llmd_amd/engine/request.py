@@ -96,6 +96,17 @@ class Request:
     finished_time: Optional[float] = None
     stop_reason: Any = None
     extra: dict = field(default_factory=dict)
+    # multimodal inputs (models/vision.py MMInput): image placeholder runs + embeddings
+    mm_inputs: Optional[list] = None
+
+    @property
+    def cache_extra(self) -> int:
+        """Block-key namespace: LoRA adapter and, for multimodal prompts, the images."""
+        if not self.mm_inputs:
+            return self.lora_id
+        from llmd_amd.models.vision import mm_cache_key
+
+        return (mm_cache_key(self.mm_inputs) ^ (self.lora_id * 0x9E3779B97F4A7C15)) & ((1 << 63) - 1)
 
     @property
     def all_token_ids(self) -> list[int]:

@@ -264,7 +264,7 @@ class Scheduler:
             r = self.waiting.peek()
             if r.status == Status.WAITING_FOR_REMOTE_KV:
                 # allocate destination blocks and start the pull
-                blocks = self.bm.allocate_remote(r.seq_id, r.num_prompt_tokens, r.lora_id)
+                blocks = self.bm.allocate_remote(r.seq_id, r.num_prompt_tokens, r.cache_extra)
                 if not blocks:
                     break
                 self.waiting.pop()
@@ -275,7 +275,7 @@ class Scheduler:
                 continue
             if not self.bm.has_seq(r.seq_id):
                 toks = self._tokens(r)
-                cached = self.bm.acquire(r.seq_id, toks, r.lora_id)
+                cached = self.bm.acquire(r.seq_id, toks, r.cache_extra)
                 if self.offload is not None and self.cfg.cache.enable_prefix_caching:
                     cached += self.offload.load_prefix(r, toks, cached, self.bm)
                 r.num_computed_tokens = cached

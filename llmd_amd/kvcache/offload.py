@@ -136,7 +136,7 @@ class OffloadManager:
         of additional tokens now resident (multiple of block size)."""
         bs = bm.block_size
         rt = _rt_loader.rt()
-        keys = rt.hash_blocks(tokens[: max(0, len(tokens) - 1)], bs, req.lora_id)
+        keys = rt.hash_blocks(tokens[: max(0, len(tokens) - 1)], bs, req.cache_extra)
         first = cached // bs
         found = []
         for i in range(first, len(keys)):

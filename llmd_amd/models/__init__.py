@@ -10,6 +10,10 @@ def model_class(cfg: ModelConfig):
         from .llama import LlamaForCausalLM
 
         return LlamaForCausalLM
+    if t == "llava":
+        from .vision import LlavaForCausalLM
+
+        return LlavaForCausalLM
     if t == "gpt_oss":
         from .gpt_oss import GptOssForCausalLM
 

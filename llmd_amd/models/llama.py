@@ -42,7 +42,7 @@ class LlamaDecoderLayer(torch.nn.Module):
         self.post_attention_layernorm = RMSNorm(d, cfg.rms_norm_eps, device)
         self.mlp = self._make_mlp(cfg, idx, device)
         # Qwen3: per-head RMSNorm on q and k before rope
-        self.qk_norm = cfg.model_type == "qwen3"
+        self.qk_norm = cfg.model_type in ("qwen3", "qwen3_moe")
         if self.qk_norm:
             self.q_norm = RMSNorm(D, cfg.rms_norm_eps, device)
             self.k_norm = RMSNorm(D, cfg.rms_norm_eps, device)

@@ -52,6 +52,12 @@ class OpenAIServer:
         self.chat_style = "llama3" if mc.model_type == "llama" else "chatml"
         self.ready = True
         self.extra_metrics = []  # callables returning bytes
+        self.mm = None
+        if mc.vision_config is not None:  # multimodal model: image parts, EC connector, encode role
+            from .multimodal import MultimodalFrontend
+
+            self.mm = MultimodalFrontend(aeng, cfg, self.tok)
+            self.extra_metrics.append(lambda: self.mm.metrics_text().encode())
 
     # ------------------------------------------------------------ app
     def app(self) -> web.Application:
@@ -72,6 +78,9 @@ class OpenAIServer:
         r.add_post("/reset_prefix_cache", self.reset_prefix_cache)
         r.add_post("/v1/load_lora_adapter", self.load_lora)
         r.add_post("/v1/unload_lora_adapter", self.unload_lora)
+        if self.mm is not None:
+            r.add_post("/v1/encode", self.mm.http_encode)
+            r.add_get("/v1/ec/{mm_hash}", self.mm.http_ec)
         return app
 
     async def health(self, req):
@@ -113,7 +122,25 @@ class OpenAIServer:
         msgs = body.get("messages")
         if not isinstance(msgs, list) or not msgs:
             raise ValueError("messages is required")
+        if self.mm is not None and self._has_images(body):
+            raise ValueError("image inputs need the async multimodal path")
         return self.tok.encode(render_chat(msgs, body.get("add_generation_prompt", True), self.chat_style))
+
+    @staticmethod
+    def _has_images(body) -> bool:
+        from .multimodal import image_parts
+
+        return bool(image_parts(body.get("messages") or []))
+
+    async def _chat_mm(self, body, headers):
+        """Chat prompt with image parts -> (token ids with placeholders, MMInputs with embeddings)."""
+        from .multimodal import mark_images
+
+        msgs = body.get("messages")
+        if not isinstance(msgs, list) or not msgs:
+            raise ValueError("messages is required")
+        text = render_chat(mark_images(msgs), body.get("add_generation_prompt", True), self.chat_style)
+        return await self.mm.prepare(body, text, headers)
 
     def _lora_id(self, body) -> int:
         m = body.get("model")
@@ -150,12 +177,19 @@ class OpenAIServer:
         bad = self._check_model(body)
         if bad is not None:
             return bad
+        mm = None
         try:
-            prompts = [self._chat_ids(body)] if chat else self._prompt_ids(body)
+            if chat and self.mm is not None and self._has_images(body):
+                ids0, mm = await self._chat_mm(body, req.headers)
+                prompts = [ids0]
+            else:
+                prompts = [self._chat_ids(body)] if chat else self._prompt_ids(body)
             params = SamplingParams.from_openai(body, default_max=16 if not chat else
                                                 max(1, self.cfg.sched.max_model_len - 1))
         except (ValueError, TypeError) as e:
             return _err(400, str(e))
+        except RuntimeError as e:  # encoder (EC connector) failure
+            return _err(502, str(e), "BadGateway")
         for p in prompts:
             if len(p) == 0:
                 return _err(400, "empty prompt")
@@ -174,12 +208,12 @@ class OpenAIServer:
         model_name = body.get("model") or self.name
         if stream:
             return await self._stream(req, rid_base, prompts[0], params, prio, ktp, lora, chat, include_usage,
-                                      created, model_name)
+                                      created, model_name, mm)
         # non-streaming: run all prompts concurrently
         async def one(i, ids):
             text_ids, lps, last = [], [], None
             async for o in self.aeng.generate(f"{rid_base}-{i}" if len(prompts) > 1 else rid_base, ids, params,
-                                              prio, ktp, lora):
+                                              prio, ktp, lora, mm):
                 text_ids.extend(o.new_token_ids)
                 lps.extend(o.new_logprobs)
                 last = o
@@ -226,7 +260,8 @@ class OpenAIServer:
             resp["kv_transfer_params"] = out_ktp
         return web.json_response(resp)
 
-    async def _stream(self, req, rid, ids, params, prio, ktp, lora, chat, include_usage, created, model_name):
+    async def _stream(self, req, rid, ids, params, prio, ktp, lora, chat, include_usage, created, model_name,
+                      mm=None):
         resp = web.StreamResponse(headers={"Content-Type": "text/event-stream", "Cache-Control": "no-cache"})
         await resp.prepare(req)
         obj = "chat.completion.chunk" if chat else "text_completion"
@@ -244,7 +279,7 @@ class OpenAIServer:
         finish = None
         last = None
         try:
-            async for o in self.aeng.generate(rid, ids, params, prio, ktp, lora):
+            async for o in self.aeng.generate(rid, ids, params, prio, ktp, lora, mm):
                 last = o
                 toks.extend(o.new_token_ids)
                 n_out = len(toks)
@@ -392,6 +427,8 @@ def main(argv=None):
     app = srv.app()
 
     async def on_shutdown(_app):
+        if srv.mm is not None:
+            await srv.mm.close()
         if a.shutdown_timeout > 0:
             await srv.aeng.drain(a.shutdown_timeout)
         srv.aeng.shutdown()

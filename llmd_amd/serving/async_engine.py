@@ -85,8 +85,8 @@ class AsyncEngine:
             op = cmd[0]
             try:
                 if op == "add":
-                    _, rid, toks, params, prio, ktp, lora, arrival = cmd
-                    self.engine.add_request(rid, toks, params, prio, ktp, lora, arrival)
+                    _, rid, toks, params, prio, ktp, lora, arrival, mm = cmd
+                    self.engine.add_request(rid, toks, params, prio, ktp, lora, arrival, mm_inputs=mm)
                 elif op == "abort":
                     self.engine.abort(cmd[1])
                     self._close(cmd[1], None)
@@ -119,7 +119,7 @@ class AsyncEngine:
     # ------------------------------------------------------------ API (event loop)
     async def generate(self, request_id: str, prompt_token_ids: list[int], params: SamplingParams,
                        priority: int = 0, kv_transfer_params: Optional[dict] = None,
-                       lora_id: int = 0) -> AsyncIterator[RequestOutput]:
+                       lora_id: int = 0, mm_inputs: Optional[list] = None) -> AsyncIterator[RequestOutput]:
         if self.dead is not None:
             raise EngineDeadError(str(self.dead))
         if not self.accepting:
@@ -128,7 +128,7 @@ class AsyncEngine:
         q: asyncio.Queue = asyncio.Queue()
         self.streams[request_id] = (loop, q)
         self.cmds.put(("add", request_id, prompt_token_ids, params, priority, kv_transfer_params,
-                       lora_id, time.monotonic()))
+                       lora_id, time.monotonic(), mm_inputs))
         self.wake.set()
         try:
             while True:
