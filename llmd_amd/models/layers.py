@@ -139,7 +139,8 @@ class VocabEmbedding(torch.nn.Module):
         st = get_state()
         self.tp, self.rank = st.tp_size, st.tp_rank
         self.vocab = vocab
-        self.per = math.ceil(vocab / self.tp)
+        # padded to 64 rows: logits rows stay 16-B aligned for the sampling kernel (odd vocabs, e.g. +1 image token)
+        self.per = math.ceil(math.ceil(vocab / self.tp) / 64) * 64
         self.lo = self.rank * self.per
         self.weight = torch.nn.Parameter(_init_weight(torch.empty(self.per, d, device=device, dtype=dtype), 0.02),
                                          requires_grad=False)
@@ -160,7 +161,8 @@ class LMHead(torch.nn.Module):
         st = get_state()
         self.tp = st.tp_size
         self.vocab = vocab
-        self.per = math.ceil(vocab / self.tp)
+        # padded to 64 rows: logits rows stay 16-B aligned for the sampling kernel (odd vocabs, e.g. +1 image token)
+        self.per = math.ceil(math.ceil(vocab / self.tp) / 64) * 64
         if tied is not None:
             self.weight = tied.weight
         else:
