@@ -11,6 +11,10 @@ Endpoints
   POST /tokenize, /detokenize
   POST /pause, /resume, /reset_prefix_cache   (IRO-ready lifecycle hooks)
   GET  /is_paused
+  GET  /fault_tolerance/status, POST /fault_tolerance/apply   (Inference
+       Resilience Operator EngineAdapter contract, proposals/
+       inference-resilience-operator.md:66-256; faults are also published as
+       ``vllm_fault`` events on the KV-event channel when it is enabled)
 P/D: a body with ``kv_transfer_params.do_remote_decode`` makes this engine a
 prefill producer (the response carries the params the decoder needs);
 ``do_remote_prefill`` makes it pull KV over kvx before decoding.
@@ -76,6 +80,8 @@ class OpenAIServer:
         r.add_post("/resume", self.resume)
         r.add_get("/is_paused", self.is_paused)
         r.add_post("/reset_prefix_cache", self.reset_prefix_cache)
+        r.add_get("/fault_tolerance/status", self.ft_status)
+        r.add_post("/fault_tolerance/apply", self.ft_apply)
         r.add_post("/v1/load_lora_adapter", self.load_lora)
         r.add_post("/v1/unload_lora_adapter", self.unload_lora)
         if self.mm is not None:
@@ -359,6 +365,52 @@ class OpenAIServer:
     async def resume(self, req):
         self.aeng.resume()
         return web.json_response({"paused": False})
+
+    # ------------------------------------------------------------ resilience (IRO)
+    def faults(self) -> list[dict]:
+        out = []
+        if self.aeng.dead is not None:
+            out.append({"kind": "engine_dead", "detail": repr(self.aeng.dead)})
+        conn = self.aeng.engine.connector
+        ag = getattr(conn, "agent", None)
+        if ag is not None:
+            for peer, st in ag.peer_status().items():
+                if st == "dead":
+                    out.append({"kind": "kv_peer_unreachable", "detail": peer})
+        return out
+
+    async def ft_status(self, req):
+        faults = self.faults()
+        eng = self.aeng.engine
+        state = "faulted" if faults else ("paused" if eng.paused else "healthy")
+        return web.json_response({"status": state, "faults": faults, "paused": eng.paused,
+                                  "accepting": self.aeng.accepting, "num_running": eng.sched.num_running,
+                                  "num_waiting": eng.sched.num_waiting})
+
+    async def ft_apply(self, req):
+        """Recovery actions: pause | resume | drain {timeout} | abort_all | reset_prefix_cache."""
+        body = await req.json()
+        act = body.get("action")
+        if act == "pause":
+            self.aeng.pause()
+        elif act == "resume":
+            self.aeng.accepting = True
+            self.aeng.resume()
+        elif act == "drain":
+            await self.aeng.drain(float(body.get("timeout", 30)))
+        elif act == "abort_all":
+            for rid in list(self.aeng.streams):
+                self.aeng.abort(rid)
+        elif act == "reset_prefix_cache":
+            await self.aeng.call(lambda e: e.reset_prefix_cache())
+        else:
+            return _err(400, f"unknown action {act!r}")
+        pub = getattr(self, "kv_event_publisher", None)
+        if pub is not None:
+            pub.publish_batch({"ts": time.time(), "events": [{"type": "vllm_fault", "action": act,
+                                                              "faults": self.faults()}]},
+                              topic=f"fault@{self.name}")
+        return web.json_response({"applied": act})
 
     async def is_paused(self, req):
         return web.json_response({"is_paused": self.aeng.engine.paused})
