@@ -142,6 +142,18 @@ class LLMEngine:
         if t_max == 0:
             self._flush_events()
             return err_outs
+        pc = self.cfg.parallel
+        if pc.enable_dbo and not any_prefill and t_max >= pc.dbo_decode_token_threshold:
+            # dual-batch overlap: two micro-batches of ceil(t_max/2) MoE rows on every rank
+            ep.set_step_rows((t_max + 1) // 2)
+            if so.empty:
+                self.runner.execute_dbo(None, {})
+                self.runner.eplb_tick()
+                self._flush_events()
+                return err_outs
+            sampled = self.runner.execute_dbo(so, self.block_tables(so))
+            self.runner.eplb_tick()
+            return self._finish_step(so, sampled, err_outs, t0)
         bucket = None
         if not any_prefill and self.runner.graphs:
             b = self.runner._bucket(max(nd_max, 1))

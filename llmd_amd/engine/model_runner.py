@@ -137,7 +137,7 @@ class ModelRunner:
               and self.mc.is_moe):
             rows = max(self.cfg.cuda_graph_max_bs, 256)
             symm.init(st.ep_rank, st.ep_size, group=st.cpu_group, ep_rows=rows, hidden=self.mc.hidden_size,
-                      topk=self.mc.num_experts_per_tok)
+                      topk=self.mc.num_experts_per_tok, micro_batches=2 if pc.enable_dbo else 1)
 
     # ------------------------------------------------------------ KV cache
     def block_bytes(self) -> int:
@@ -423,6 +423,10 @@ class ModelRunner:
         return {r.seq_id: (int(ids_h[i]), float(lp_h[i])) for i, r in enumerate(reqs)}
 
     def _run_eager(self, pl: dict):
+        ids, meta = self._eager_meta(pl)
+        return self.model(ids, meta)
+
+    def _eager_meta(self, pl: dict):
         ids, pos, slots, d_bt, d_len = pl["ids"], pl["pos"], pl["slots"], pl["d_bt"], pl["d_len"]
         p_ql, p_ctx, p_bt = pl["p_ql"], pl["p_ctx"], pl["p_bt"]
         dev = self.device
@@ -454,7 +458,94 @@ class ModelRunner:
             rows, embs = pl["mm"]
             meta.mm_rows = torch.tensor(rows, dtype=torch.long).to(dev, non_blocking=True)
             meta.mm_embeds = embs.to(dev)
-        return self.model(hd[0], meta)
+        return hd[0], meta
+
+    # ------------------------------------------------------------ dual-batch overlap
+    def _forward_steps(self, ids, meta):
+        """model.forward as a generator yielding after every decoder layer
+        (embed -> layers -> norm is the structure of every model here)."""
+        m = self.model
+        x = m.embed(ids)
+        residual = None
+        for layer in m.layers:
+            x, residual = layer(x, residual, meta)
+            yield None
+        x, _ = m.norm(x, residual)
+        yield x
+
+    @torch.no_grad()
+    def execute_dbo(self, so: Optional[SchedulerOutput], block_tables: dict) -> dict:
+        """Dual-batch overlap (reference --enable-dbo,
+        guides/wide-ep-lws/modelserver/gpu/vllm/base/decode.yaml:112-113) for a
+        decode-only wide-EP step: the decodes split into two micro-batches,
+        each with its own attention metadata and its own symm EP channel /
+        receive buffers; their layers are issued alternately on two HIP
+        streams so one micro-batch's dispatch/combine kernels (bounded to 64
+        workgroups) run while the other's attention/expert GEMMs occupy the
+        remaining CUs. ``so=None``: idle DP rank, two one-token dummy halves."""
+        from llmd_amd.parallel import symm
+
+        plans, reqs = [], []
+        if so is None or so.empty:
+            for _ in range(2):
+                w = self.width
+                plans.append({"graph": False, "nd": 1, "ids": [0], "pos": [0], "slots": [-1],
+                              "d_bt": np.zeros((1, w), np.int32), "d_len": np.ones(1, dtype=np.int32),
+                              "p_ql": [], "p_ctx": [], "p_bt": np.zeros((0, w), np.int32), "rows": []})
+        else:
+            h = (len(so.decodes) + 1) // 2
+            for part in (so.decodes[:h], so.decodes[h:]):
+                sub = SchedulerOutput(decodes=list(part))
+                if part:
+                    pl, rq = self.plan(sub, block_tables)
+                else:  # odd split of a 1-token step: a dummy half keeps the collectives paired
+                    w = self.width
+                    pl, rq = ({"graph": False, "nd": 1, "ids": [0], "pos": [0], "slots": [-1],
+                               "d_bt": np.zeros((1, w), np.int32), "d_len": np.ones(1, dtype=np.int32),
+                               "p_ql": [], "p_ctx": [], "p_bt": np.zeros((0, w), np.int32), "rows": []}, [])
+                plans.append(pl)
+                reqs.append(rq)
+        metas = [self._eager_meta(pl) for pl in plans]
+        if self.is_gpu:
+            main = torch.cuda.current_stream()
+            if not hasattr(self, "_dbo_streams"):
+                self._dbo_streams = (torch.cuda.Stream(device=self.device), torch.cuda.Stream(device=self.device))
+            streams = self._dbo_streams
+            for s in streams:
+                s.wait_stream(main)
+        gens = [self._forward_steps(ids, meta) for ids, meta in metas]
+        outs = [None, None]
+        done = [False, False]
+        while not all(done):
+            for m in (0, 1):
+                if done[m]:
+                    continue
+                symm.set_active_mb(m)
+                if self.is_gpu:
+                    with torch.cuda.stream(streams[m]):
+                        y = next(gens[m])
+                else:
+                    y = next(gens[m])
+                if y is not None:
+                    outs[m] = y
+                    done[m] = True
+        symm.set_active_mb(0)
+        if self.is_gpu:
+            for s in streams:
+                main.wait_stream(s)
+            for o in outs:
+                o.record_stream(main)
+        if so is None or so.empty:
+            return {}
+        logits, all_reqs = [], []
+        for pl, rq, h in zip(plans, reqs, outs):
+            if pl["rows"]:
+                idx = torch.tensor(pl["rows"], dtype=torch.long).to(self.device, non_blocking=True)
+                logits.append(self.model.compute_logits(h.index_select(0, idx)))
+                all_reqs.extend(rq)
+        if not all_reqs:
+            return {}
+        return self._sample(torch.cat(logits), all_reqs)
 
     # ------------------------------------------------------------ graphs
     def _bucket(self, n: int) -> int:

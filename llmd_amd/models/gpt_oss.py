@@ -102,12 +102,14 @@ class GptOssForCausalLM(LlamaForCausalLM):
     def _mlp_specs(self, pre: str, mlp) -> list:
         """HF gpt-oss MoE tensors: router.{weight,bias}, experts.gate_up_proj [E, d, 2F]
         (gate/up interleaved columns), experts.down_proj [E, F, d] (+ biases)."""
-        if mlp.eplb is not None:
-            raise NotImplementedError("gpt-oss checkpoint loading with EPLB redundant experts")
-        lo, n = mlp.ep_rank * mlp.E_local, mlp.E_local
+        if mlp.eplb is not None:  # physical slots -> logical experts (replicas load their expert)
+            sel = list(mlp.eplb.local_logical())
+        else:
+            lo, n = mlp.ep_rank * mlp.E_local, mlp.E_local
+            sel = (lo, n)
         return [(pre + "mlp.router.weight", mlp.router_w, "replicate", None),
                 (pre + "mlp.router.bias", mlp.router_b, "replicate", None),
-                (pre + "mlp.experts.gate_up_proj", mlp.w1, "experts_t", (lo, n)),
-                (pre + "mlp.experts.gate_up_proj_bias", mlp.b1, "experts", (lo, n)),
-                (pre + "mlp.experts.down_proj", mlp.w2, "experts_t", (lo, n)),
-                (pre + "mlp.experts.down_proj_bias", mlp.b2, "experts", (lo, n))]
+                (pre + "mlp.experts.gate_up_proj", mlp.w1, "experts_t", sel),
+                (pre + "mlp.experts.gate_up_proj_bias", mlp.b1, "experts", sel),
+                (pre + "mlp.experts.down_proj", mlp.w2, "experts_t", sel),
+                (pre + "mlp.experts.down_proj_bias", mlp.b2, "experts", sel)]

@@ -69,8 +69,11 @@ def place(param: torch.Tensor, full: torch.Tensor, kind: str, extra=None):
             part = _shard_heads(full, n_heads, head_rows, tp, rank)
             param[off:off + part.shape[0]].copy_(part)
         elif kind in ("experts", "experts_t"):  # [E, ...] stacked experts -> this rank's slice
-            lo, n = extra
-            part = full[lo:lo + n]
+            if isinstance(extra, list):  # explicit logical experts per physical slot (EPLB replicas)
+                part = full[extra]
+            else:
+                lo, n = extra
+                part = full[lo:lo + n]
             param.copy_(part.transpose(1, 2) if kind == "experts_t" else part)
         elif kind == "rows":  # interleaved rows (gate/up pairs of a fused expert weight)
             start, step = extra

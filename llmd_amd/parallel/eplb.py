@@ -163,6 +163,8 @@ def _move_experts(old: list[int], new: list[int], rank: int, n: int, P_local: in
         holders.setdefault(e, []).append(p)
     lo = rank * P_local
     snap = [t.detach().clone() for t in params]  # old local contents
+    # gloo moves host tensors only: stage device weights through CPU (RCCL peer copies otherwise)
+    host = dist.is_initialized() and dist.get_backend(group) == "gloo" and params and params[0].is_cuda
     ops = []
     recv_into = []
     # receives / local copies for our new slots
@@ -177,7 +179,7 @@ def _move_experts(old: list[int], new: list[int], rank: int, n: int, P_local: in
             continue
         src_slot = holders[e][0]
         for t in params:
-            buf = torch.empty_like(t[i])
+            buf = torch.empty_like(t[i], device="cpu" if host else t.device)
             ops.append(dist.P2POp(dist.irecv, buf, _global(src_slot // P_local, group), group))
             recv_into.append((t, i, buf))
     # sends: for every slot on another rank that needs an expert whose first holder is here
@@ -191,7 +193,8 @@ def _move_experts(old: list[int], new: list[int], rank: int, n: int, P_local: in
         if src_slot // P_local != rank:
             continue
         for s in snap:
-            ops.append(dist.P2POp(dist.isend, s[src_slot - lo].contiguous(), _global(r_dst, group), group))
+            src = s[src_slot - lo].contiguous()
+            ops.append(dist.P2POp(dist.isend, src.cpu() if host else src, _global(r_dst, group), group))
     if ops:
         for req in dist.batch_isend_irecv(ops):
             req.wait()

@@ -193,33 +193,42 @@ class SymmEP:
 
 
 _heap: Optional[SymmHeap] = None
-_ep: Optional[SymmEP] = None
+_eps: list[SymmEP] = []
+_active_mb = 0  # dual-batch overlap: micro-batch m uses EP channel CH_EP + m and its own buffers
 
 
 def init(rank: int, world: int, group=None, tp_allreduce: bool = False, ep_rows: int = 0, hidden: int = 0,
-         topk: int = 0, ar_max_bytes: int = 16 << 20) -> SymmHeap:
-    """Create the process-wide heap and install the users that were asked for."""
-    global _heap, _ep
+         topk: int = 0, ar_max_bytes: int = 16 << 20, micro_batches: int = 1) -> SymmHeap:
+    """Create the process-wide heap and install the users that were asked for.
+    ``micro_batches=2`` (DBO) gives each micro-batch its own EP channel/buffers."""
+    global _heap, _eps
     n = 1 << 20
     if tp_allreduce:
         slot = _align(max(512 << 10, ar_max_bytes // max(world, 1) + 16), 256)
         n += 4 * world * slot + 4096
     if ep_rows:
-        n += SymmEP.heap_bytes(world, ep_rows, hidden, topk)
+        n += micro_batches * SymmEP.heap_bytes(world, ep_rows, hidden, topk)
     _heap = SymmHeap(n + (1 << 20), rank, world, group)
     if tp_allreduce:
         from .comm import set_custom_allreduce
 
         set_custom_allreduce(CustomAllReduce(_heap, max_bytes=ar_max_bytes))
     if ep_rows:
-        _ep = SymmEP(_heap, ep_rows, hidden, topk)
+        _eps = [SymmEP(_heap, ep_rows, hidden, topk, channel=CH_EP + m) for m in range(micro_batches)]
     log.info("symm heap %.1f MiB on rank %d/%d (allreduce=%s, ep_rows=%d)", _heap.nbytes / 2**20, rank, world,
              tp_allreduce, ep_rows)
     return _heap
 
 
 def ep() -> Optional[SymmEP]:
-    return _ep
+    if not _eps:
+        return None
+    return _eps[min(_active_mb, len(_eps) - 1)]
+
+
+def set_active_mb(m: int):
+    global _active_mb
+    _active_mb = m
 
 
 def heap() -> Optional[SymmHeap]:
@@ -227,13 +236,13 @@ def heap() -> Optional[SymmHeap]:
 
 
 def shutdown():
-    global _heap, _ep
+    global _heap, _eps
     from .comm import set_custom_allreduce
 
     set_custom_allreduce(None)
     if _heap is not None:
         _heap.close()
-    _heap, _ep = None, None
+    _heap, _eps = None, []
 
 
 def enabled_by_env() -> bool:

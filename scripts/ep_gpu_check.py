@@ -1,0 +1,96 @@
+"""Wide-EP on the GPU with the symm (DeepEP-LL role) backend, hipGraph decode
+buckets, EPLB and dual-batch overlap - N processes sharing one GPU (the 1-GPU
+rig: expert exchange through hipIpc-mapped peer memory and per-workgroup
+epoch barriers; control over gloo).
+
+  torchrun --nproc-per-node 2 scripts/ep_gpu_check.py [--dbo] [--eplb] [--model tiny-gpt-oss]
+
+Every rank serves its own prompts; greedy outputs are compared with a plain
+single-process engine on the same safetensors weights. Prints one JSON line.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--model", default="tiny-gpt-oss")
+    ap.add_argument("--dbo", action="store_true")
+    ap.add_argument("--eplb", action="store_true")
+    ap.add_argument("--weights", default=None)
+    a = ap.parse_args()
+    a.weights = a.weights or f"/tmp/llmd_ep_gpu_check_{a.model}.safetensors"
+    rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
+    torch.cuda.set_device(0)
+    from llmd_amd.engine.config import EngineConfig
+    from llmd_amd.engine.engine import LLMEngine
+    from llmd_amd.engine.request import SamplingParams
+    from llmd_amd.parallel import symm
+    from llmd_amd.parallel.state import ParallelState, get_state, init_distributed, set_state
+
+    st = init_distributed(tp_size=1, backend="gloo")
+
+    def cfg(**kw):
+        return EngineConfig.create(a.model, device="cuda", block_size=64, num_gpu_blocks=96,
+                                   max_num_batched_tokens=256, max_num_seqs=8, max_model_len=1024,
+                                   cuda_graph_max_bs=8, load_format="safetensors", weights_path=a.weights, **kw)
+
+    if rank == 0 and not os.path.exists(a.weights):
+        from llmd_amd.models import build_model
+        from llmd_amd.models.loader import export_hf, save_safetensors
+
+        set_state(ParallelState())
+        save_safetensors(export_hf(build_model(cfg().model_config, device="cpu", max_pos=1100)), a.weights)
+        set_state(st)
+    dist.barrier()
+    rng = np.random.default_rng(100 + rank)
+    prompts = [rng.integers(3, 400, size=n).tolist() for n in ((40, 90, 17) if rank == 0 else (60, 33))]
+    ntok = 12 if rank == 0 else 6
+    sp = SamplingParams(max_tokens=ntok, temperature=0.0, ignore_eos=True)
+    extra = {}
+    if a.dbo:
+        extra.update(enable_dbo=True, dbo_decode_token_threshold=2)
+    if a.eplb:
+        extra.update(enable_eplb=True, eplb_config={"num_redundant_experts": 2 * world, "step_interval": 3})
+    eng = LLMEngine(cfg(data_parallel_size=world, enable_expert_parallel=True, all2all_backend="symm_ll", **extra))
+    assert eng.dp_lockstep and symm.ep() is not None
+    reqs = [eng.add_request(f"r{rank}-{i}", p, sp) for i, p in enumerate(prompts)]
+    steps = 0
+    while eng.dp_has_unfinished():
+        eng.step()
+        steps += 1
+    torch.cuda.synchronize()
+    got = [r.output_token_ids for r in reqs]
+    err = symm.heap().error()
+    # reference: single-process engine (no EP) on the same weights
+    set_state(ParallelState())
+    ref = LLMEngine(cfg(enforce_eager=True))
+    want = [r.output_token_ids for r in ref.generate(prompts, sp)]
+    set_state(st)
+    agree = sum(int(x == y) for g, w in zip(got, want) for x, y in zip(g, w))
+    total = sum(len(w) for w in want)
+    ok = err == 0 and all(g[:3] == w[:3] for g, w in zip(got, want)) and agree >= 0.8 * total
+    flags = [None] * world
+    dist.all_gather_object(flags, {"rank": rank, "ok": ok, "agree": agree, "total": total, "steps": steps,
+                                   "timeout_flag": err})
+    if rank == 0:
+        print(json.dumps({"model": a.model, "dbo": a.dbo, "eplb": a.eplb, "world": world,
+                          "ok": all(f["ok"] for f in flags), "ranks": flags}), flush=True)
+    dist.barrier()
+    symm.shutdown()
+    dist.destroy_process_group()
+    sys.exit(0 if all(f["ok"] for f in flags) else 1)
+
+
+if __name__ == "__main__":
+    main()

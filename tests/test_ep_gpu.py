@@ -1,0 +1,25 @@
+"""Wide-EP on the GPU through the symm heap (DeepEP-LL role) with hipGraph
+decode, dual-batch overlap and EPLB: scripts/ep_gpu_check.py with 2 processes
+sharing cuda:0, outputs compared with a single-process engine (GPU only)."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.mark.parametrize("model,flags,port", [("tiny-gpt-oss", [], 29751),
+                                               ("tiny-deepseek", ["--dbo", "--eplb"], 29752)])
+def test_wide_ep_symm_gpu(model, flags, port, tmp_path):
+    env = dict(os.environ, LLMD_SYMM_DEVICE="0", HSA_ENABLE_IPC_MODE_LEGACY="0")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.join(ROOT, "scripts", "ep_gpu_check.py"),
+           "--model", model, "--weights", str(tmp_path / "w.safetensors")] + flags
+    r = subprocess.run(cmd, env=env, cwd=ROOT, capture_output=True, text=True, timeout=220)
+    assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-4000:])
+    d = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+    assert d["ok"] and all(x["timeout_flag"] == 0 for x in d["ranks"])
