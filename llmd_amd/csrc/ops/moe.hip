@@ -20,6 +20,8 @@
 //   moe_combine   out[t] = sum_j w[t,j] * Y[inv(t,j)]  (deterministic, no atomics)
 // Weights of every expert are read exactly once per M-tile, which at decode
 // sizes (a few tokens per expert) is the HBM-bound optimum.
+#include <cstdlib>
+
 #include "llmd_common.h"
 
 using namespace llmd;
@@ -190,12 +192,13 @@ __global__ __launch_bounds__(1024) void moe_align_kernel(const int* __restrict__
   if (threadIdx.x == 0) expert_offsets[E] = P;
   for (int tt = P / BM + threadIdx.x; tt < max_p / BM; tt += blockDim.x) tile_expert[tt] = -1;
   __syncthreads();
-  // stable scatter: one pass per thread-chunk keeps order deterministic per expert
-  if (threadIdx.x == 0) {
-    for (int i = 0; i < n; ++i) {
-      const int e = ids[i];
-      if (e >= 0 && e < E) sorted_ids[cur[e]++] = i;
-    }
+  // parallel scatter through LDS cursors. The order of rows inside an expert
+  // segment is not fixed, but every row's GEMM result is independent of its
+  // neighbours and moe_combine reads rows through `inv`, so outputs are
+  // bitwise identical run to run.
+  for (int i = threadIdx.x; i < n; i += blockDim.x) {
+    const int e = ids[i];
+    if (e >= 0 && e < E) sorted_ids[atomicAdd(&cur[e], 1)] = i;
   }
 }
 
@@ -306,6 +309,140 @@ __global__ __launch_bounds__(NT, 2) void moe_gemm_kernel(
           if (col < N) Y[(int64_t)row * y_stride + col] = f2bf(v);
         } else {
           // interleaved gate/up: even col = gate, odd col = up (partner lane r16^1)
+          const float other = __shfl_xor(v, 1, 64);
+          if ((r16 & 1) == 0) {
+            float g = v, u = other, o;
+            if (act == 2) {
+              g = fminf(g, limit);
+              u = fminf(fmaxf(u, -limit), limit);
+              o = (u + 1.f) * g / (1.f + __expf(-alpha * g));
+            } else {
+              o = g / (1.f + __expf(-g)) * u;
+            }
+            if (col < N) Y[(int64_t)row * y_stride + col / 2] = f2bf(o);
+          }
+        }
+      }
+    }
+  }
+}
+
+
+// ---------------------------------------------------------------- grouped GEMM v2 (LDS-DMA)
+// Same contract as moe_gemm_kernel (64-row expert tiles from moe_align), for
+// K % 64 == 0. 64 x 256 output tile per 256-thread workgroup, each wave 64 x 64
+// (4 x 4 mfma_f32_16x16x32_bf16 tiles, 64 accumulator VGPRs). Operands go
+// global -> LDS with global_load_lds_dwordx4 (no VGPR staging, per-lane source
+// addresses do the sorted-row gather), two LDS buffers in separate
+// allocations so the compiler can see the next tile's DMA does not alias the
+// tile being read, one vmcnt(0) + barrier per K-step. LDS rows are 128 B
+// (64 bf16) with the 16-B chunk XOR-swizzled by (row >> 1) & 7 on the SOURCE
+// side (DMA images are lane-linear): every ds_read_b128 lane group of a
+// fragment read then covers 16 distinct slots of a 256-B bank row.
+constexpr int G2_BM = 64, G2_BN = 256, G2_NT = 256;
+constexpr int G2_AB = G2_BM * 128, G2_BB = G2_BN * 128, G2_BUF = G2_AB + G2_BB;
+
+__device__ __forceinline__ int g2_swz(int row, int c) { return c ^ ((row >> 1) & 7); }
+
+__device__ __forceinline__ void g2_dma(const void* src, char* lds_base) {
+  __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)src,
+                                   (void __attribute__((address_space(3)))*)lds_base, 16, 0, 0);
+}
+
+template <int MODE>
+__global__ __launch_bounds__(G2_NT, 2) void moe_gemm2_kernel(
+    const uint16_t* __restrict__ X, int64_t x_stride, int topk, const int* __restrict__ sorted_ids,
+    const int* __restrict__ tile_expert, const uint16_t* __restrict__ W, int64_t w_expert_stride, int N, int K,
+    uint16_t* __restrict__ Y, int64_t y_stride, int act, float alpha, float limit, int a_rows_are_slots,
+    const uint16_t* __restrict__ bias) {
+  __shared__ __attribute__((aligned(1024))) char buf0[G2_BUF];
+  __shared__ __attribute__((aligned(1024))) char buf1[G2_BUF];
+  const int mt = blockIdx.y, nt = blockIdx.x;
+  const int e = tile_expert[mt];
+  if (e < 0) return;
+  const int m0 = mt * G2_BM, n0 = nt * G2_BN;
+  const uint16_t* We = W + (int64_t)e * w_expert_stride;
+  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+  const int lr = lane >> 3, lp = lane & 7;
+  // DMA sources: A row groups {2w, 2w+1} (8 rows each), B row groups {8w .. 8w+7}
+  const uint16_t* asrc[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int row = 8 * (2 * w + i) + lr;
+    const int sid = sorted_ids[m0 + row];
+    const int tok = sid < 0 ? 0 : (a_rows_are_slots ? sid : sid / topk);  // padding rows read row 0 (discarded)
+    asrc[i] = X + (int64_t)tok * x_stride + g2_swz(row, lp) * 8;
+  }
+  const uint16_t* bsrc[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int row = 8 * (8 * w + i) + lr;
+    const int n = min(n0 + row, N - 1);  // tail columns read a valid row (discarded)
+    bsrc[i] = We + (int64_t)n * K + g2_swz(row, lp) * 8;
+  }
+  auto issue = [&](char* base, int k0) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) g2_dma(asrc[i] + k0, base + (2 * w + i) * 1024);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) g2_dma(bsrc[i] + k0, base + G2_AB + (8 * w + i) * 1024);
+  };
+  f32x4_t acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  const int r16 = lane & 15, kq = lane >> 4;
+  auto compute = [&](const char* base) {
+    const char* A = base;
+    const char* B = base + G2_AB;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      bf16x8_t af[4], bfr[4];
+      const int c = 4 * s + kq;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int row = 16 * i + r16;
+        af[i] = *reinterpret_cast<const bf16x8_t*>(A + row * 128 + g2_swz(row, c) * 16);
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int row = 64 * w + 16 * j + r16;
+        bfr[j] = *reinterpret_cast<const bf16x8_t*>(B + row * 128 + g2_swz(row, c) * 16);
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+  };
+  const int nk = K / 64;
+  issue(buf0, 0);
+  for (int kt = 0; kt < nk; kt += 2) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (kt + 1 < nk) issue(buf1, (kt + 1) * 64);
+    compute(buf0);
+    if (kt + 1 >= nk) break;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (kt + 2 < nk) issue(buf0, (kt + 2) * 64);
+    compute(buf1);
+  }
+  // epilogue: C[row = 16i + 4kq + r][col = 64w + 16j + r16]
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int row = m0 + 16 * i + kq * 4 + r;
+      if (sorted_ids[row] < 0) continue;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int col = n0 + 64 * w + 16 * j + r16;
+        float v = acc[i][j][r];
+        if (bias && col < N) v += bf2f(bias[(int64_t)e * N + col]);
+        if (MODE == 0) {
+          if (col < N) Y[(int64_t)row * y_stride + col] = f2bf(v);
+        } else {
           const float other = __shfl_xor(v, 1, 64);
           if ((r16 & 1) == 0) {
             float g = v, u = other, o;
@@ -482,6 +619,149 @@ __global__ __launch_bounds__(NT, 2) void moe_gemm_fp8_kernel(
   }
 }
 
+
+// FP8 variant of the v2 grouped GEMM: a K-step is 128 e4m3 = the same 128-B LDS
+// row, so staging is byte-identical to the bf16 kernel. Fragments are 8 B
+// (ds_read_b64: row*128 + swz(row, 2s + kq/2)*16 + 8*(kq&1), conflict-free for
+// the two 32-lane halves), 4 mfma_f32_16x16x32_fp8_fp8 per K-step into a block
+// accumulator folded with xs[row][kb] * ws[e][nb][kb] (each wave's 64 columns
+// sit in one 128-column weight-scale block).
+template <int MODE>
+__global__ __launch_bounds__(G2_NT, 2) void moe_gemm2_fp8_kernel(
+    const uint8_t* __restrict__ X, int64_t x_stride, const float* __restrict__ xs, int64_t xs_stride, int topk,
+    const int* __restrict__ sorted_ids, const int* __restrict__ tile_expert, const uint8_t* __restrict__ W,
+    int64_t w_expert_stride, const float* __restrict__ ws, int N, int K, uint16_t* __restrict__ Y, int64_t y_stride,
+    int act, float alpha, float limit, int a_rows_are_slots, const uint16_t* __restrict__ bias) {
+  __shared__ __attribute__((aligned(1024))) char buf0[G2_BUF];
+  __shared__ __attribute__((aligned(1024))) char buf1[G2_BUF];
+  const int mt = blockIdx.y, nt = blockIdx.x;
+  const int e = tile_expert[mt];
+  if (e < 0) return;
+  const int m0 = mt * G2_BM, n0 = nt * G2_BN;
+  const int nkb = K / 128, nnb = (N + 127) / 128;
+  const uint8_t* We = W + (int64_t)e * w_expert_stride;
+  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+  const int lr = lane >> 3, lp = lane & 7;
+  auto tok_of = [&](int row) {
+    const int sid = sorted_ids[row];
+    return sid < 0 ? -1 : (a_rows_are_slots ? sid : sid / topk);
+  };
+  const uint8_t* asrc[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int row = 8 * (2 * w + i) + lr;
+    const int tok = tok_of(m0 + row);
+    asrc[i] = X + (int64_t)(tok < 0 ? 0 : tok) * x_stride + g2_swz(row, lp) * 16;
+  }
+  const uint8_t* bsrc[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int row = 8 * (8 * w + i) + lr;
+    const int n = min(n0 + row, N - 1);
+    bsrc[i] = We + (int64_t)n * K + g2_swz(row, lp) * 16;
+  }
+  auto issue = [&](char* base, int k0) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) g2_dma(asrc[i] + k0, base + (2 * w + i) * 1024);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) g2_dma(bsrc[i] + k0, base + G2_AB + (8 * w + i) * 1024);
+  };
+  const int r16 = lane & 15, kq = lane >> 4;
+  const float* xsr[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int tok = tok_of(m0 + 16 * i + 4 * kq + r);
+      xsr[i][r] = tok < 0 ? nullptr : xs + (int64_t)tok * xs_stride;
+    }
+  const float* wsr = ws + ((int64_t)e * nnb + (n0 + 64 * w) / 128) * nkb;
+  f32x4_t acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  auto compute = [&](const char* base, int kb) {
+    const char* A = base;
+    const char* B = base + G2_AB;
+    f32x4_t blk[4][4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) blk[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      long af[4], bfr[4];
+      const int c = 2 * s + (kq >> 1), h = 8 * (kq & 1);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int row = 16 * i + r16;
+        af[i] = *reinterpret_cast<const long*>(A + row * 128 + g2_swz(row, c) * 16 + h);
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int row = 64 * w + 16 * j + r16;
+        bfr[j] = *reinterpret_cast<const long*>(B + row * 128 + g2_swz(row, c) * 16 + h);
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) blk[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_fp8_fp8(af[i], bfr[j], blk[i][j], 0, 0, 0);
+    }
+    const float wsv = wsr[kb];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float sc = xsr[i][r] ? xsr[i][r][kb] * wsv : 0.f;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j][r] += blk[i][j][r] * sc;
+      }
+  };
+  issue(buf0, 0);
+  for (int kt = 0; kt < nkb; kt += 2) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (kt + 1 < nkb) issue(buf1, (kt + 1) * 128);
+    compute(buf0, kt);
+    if (kt + 1 >= nkb) break;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (kt + 2 < nkb) issue(buf0, (kt + 2) * 128);
+    compute(buf1, kt + 1);
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int row = m0 + 16 * i + kq * 4 + r;
+      if (sorted_ids[row] < 0) continue;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int col = n0 + 64 * w + 16 * j + r16;
+        float v = acc[i][j][r];
+        if (bias && col < N) v += bf2f(bias[(int64_t)e * N + col]);
+        if (MODE == 0) {
+          if (col < N) Y[(int64_t)row * y_stride + col] = f2bf(v);
+        } else {
+          const float other = __shfl_xor(v, 1, 64);
+          if ((r16 & 1) == 0) {
+            float g = v, u = other, o;
+            if (act == 2) {
+              g = fminf(g, limit);
+              u = fminf(fmaxf(u, -limit), limit);
+              o = (u + 1.f) * g / (1.f + __expf(-alpha * g));
+            } else {
+              o = g / (1.f + __expf(-g)) * u;
+            }
+            if (col < N) Y[(int64_t)row * y_stride + col / 2] = f2bf(o);
+          }
+        }
+      }
+    }
+  }
+}
+
 // out[t, :] = sum_j w[t, j] * Y[pos(t, j), :]  with pos from the inverse permutation
 __global__ __launch_bounds__(256) void moe_combine_kernel(const uint16_t* __restrict__ Y, int64_t y_stride,
                                                           const int* __restrict__ inv, const float* __restrict__ w,
@@ -538,6 +818,22 @@ void llmd_moe_gemm(const void* X, int64_t x_stride, int topk, const int* sorted_
                    int mode, int act, float alpha, float limit, int a_rows_are_slots, const void* bias,
                    hipStream_t st) {
   if (num_tiles == 0) return;
+  static const bool v2 = [] {
+    const char* e = getenv("LLMD_MOE_GEMM_V1");
+    return !(e && e[0] == '1');
+  }();
+  if (v2 && K % 64 == 0 && (x_stride % 8) == 0 && (w_expert_stride % 8) == 0) {
+    dim3 grid2((N + G2_BN - 1) / G2_BN, num_tiles);
+    if (mode == 0)
+      hipLaunchKernelGGL(moe_gemm2_kernel<0>, grid2, dim3(G2_NT), 0, st, (const uint16_t*)X, x_stride, topk,
+                         sorted_ids, tile_expert, (const uint16_t*)W, w_expert_stride, N, K, (uint16_t*)Y, y_stride,
+                         act, alpha, limit, a_rows_are_slots, (const uint16_t*)bias);
+    else
+      hipLaunchKernelGGL(moe_gemm2_kernel<1>, grid2, dim3(G2_NT), 0, st, (const uint16_t*)X, x_stride, topk,
+                         sorted_ids, tile_expert, (const uint16_t*)W, w_expert_stride, N, K, (uint16_t*)Y, y_stride,
+                         act, alpha, limit, a_rows_are_slots, (const uint16_t*)bias);
+    return;
+  }
   dim3 grid((N + BN - 1) / BN, num_tiles);
   if (mode == 0)
     hipLaunchKernelGGL(moe_gemm_kernel<0>, grid, dim3(NT), 0, st, (const uint16_t*)X, x_stride, topk, sorted_ids,
@@ -554,6 +850,22 @@ void llmd_moe_gemm_fp8(const void* X, int64_t x_stride, const float* xs, int64_t
                        int64_t w_expert_stride, const float* ws, int N, int K, void* Y, int64_t y_stride, int mode,
                        int act, float alpha, float limit, int a_rows_are_slots, const void* bias, hipStream_t st) {
   if (num_tiles == 0) return;
+  static const bool v2 = [] {
+    const char* e = getenv("LLMD_MOE_GEMM_V1");
+    return !(e && e[0] == '1');
+  }();
+  if (v2 && K % 128 == 0 && x_stride % 16 == 0 && w_expert_stride % 16 == 0) {
+    dim3 grid2((N + G2_BN - 1) / G2_BN, num_tiles);
+    if (mode == 0)
+      hipLaunchKernelGGL(moe_gemm2_fp8_kernel<0>, grid2, dim3(G2_NT), 0, st, (const uint8_t*)X, x_stride, xs,
+                         xs_stride, topk, sorted_ids, tile_expert, (const uint8_t*)W, w_expert_stride, ws, N, K,
+                         (uint16_t*)Y, y_stride, act, alpha, limit, a_rows_are_slots, (const uint16_t*)bias);
+    else
+      hipLaunchKernelGGL(moe_gemm2_fp8_kernel<1>, grid2, dim3(G2_NT), 0, st, (const uint8_t*)X, x_stride, xs,
+                         xs_stride, topk, sorted_ids, tile_expert, (const uint8_t*)W, w_expert_stride, ws, N, K,
+                         (uint16_t*)Y, y_stride, act, alpha, limit, a_rows_are_slots, (const uint16_t*)bias);
+    return;
+  }
   dim3 grid((N + BN - 1) / BN, num_tiles);
   if (mode == 0)
     hipLaunchKernelGGL(moe_gemm_fp8_kernel<0>, grid, dim3(NT), 0, st, (const uint8_t*)X, x_stride, xs, xs_stride,
