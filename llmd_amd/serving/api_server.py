@@ -176,6 +176,15 @@ class OpenAIServer:
         return await self._serve(req, chat=True)
 
     async def _serve(self, req: web.Request, chat: bool):
+        """Engine request span ``llm_request`` (vLLM's name), child of
+        the incoming W3C ``traceparent`` (router / sidecar)."""
+        from llmd_amd.utils.tracing import span
+
+        with span("llm_request", {"path": req.path, "model": self.name},
+                  traceparent=req.headers.get("traceparent")):
+            return await self._serve_inner(req, chat)
+
+    async def _serve_inner(self, req: web.Request, chat: bool):
         try:
             body = await req.json()
         except Exception:  # noqa: BLE001

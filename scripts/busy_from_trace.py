@@ -37,5 +37,26 @@ def main():
           f"largest {max(gaps) if gaps else 0:.1f} ms")
 
 
+def breakdown(path, window):
+    rows = []
+    with open(path) as f:
+        for row in csv.DictReader(f):
+            rows.append((int(row["Start_Timestamp"]), int(row["End_Timestamp"]), row.get("Kernel_Name", "")))
+    end = max(e for _, e, _ in rows)
+    lo = end - int(window * 1e9)
+    agg = {}
+    for s, e, n in rows:
+        if e > lo:
+            k = n.split("(")[0][:90]
+            t, c = agg.get(k, (0, 0))
+            agg[k] = (t + e - max(s, lo), c + 1)
+    tot = sum(t for t, _ in agg.values())
+    print(f"per-kernel time in the last {window:.1f}s (total kernel {tot / 1e6:.1f} ms):")
+    for k, (t, c) in sorted(agg.items(), key=lambda kv: -kv[1][0])[:16]:
+        print(f"  {t / 1e6:9.1f} ms {100 * t / tot:5.1f}% {c:6d}  {k}")
+
+
 if __name__ == "__main__":
+    if len(sys.argv) > 3 and sys.argv[3] == "--breakdown":
+        breakdown(sys.argv[1], float(sys.argv[2]))
     main()

@@ -364,3 +364,18 @@ def test_gbdt_predictor_vs_numpy():
     assert mape(t, y) < 0.10  # reference quotes ~5% MAPE on real traffic
     tp = np.array([p["tpot_ms"] for p in pred])
     assert mape(tp, np.array([x[2] for x in X[-500:]])) < 0.05
+
+
+def test_adapter_rollout_manifest_weighted_split():
+    """deploy/gateway/rollouts/adapter-rollout-rewrite.yaml: 80/20 split (C42)."""
+    import collections
+    import os
+
+    cp = ControlPlane()
+    path = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                        "deploy", "gateway", "rollouts", "adapter-rollout-rewrite.yaml")
+    cp.load_yaml(open(path).read())
+    c = collections.Counter(cp.rewrite("food-review")[0] for _ in range(4000))
+    assert set(c) == {"food-review-v1", "food-review-v2"}
+    assert 0.74 < c["food-review-v1"] / 4000 < 0.86
+    assert cp.rewrite("other-model")[0] == "other-model"
