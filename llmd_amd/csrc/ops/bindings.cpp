@@ -60,6 +60,9 @@ void llmd_moe_gemm(const void*, int64_t, int, const int*, const int*, int, const
 void llmd_moe_combine(const void*, int64_t, const int*, const float*, int, int, int, void*, int64_t,
                       hipStream_t);
 int llmd_quant_fp8_rows(const void*, int64_t, void*, int64_t, float*, int, int, hipStream_t);
+void llmd_rms_norm_quant(void*, int64_t, float*, const void*, int64_t, void*, int64_t, const void*, int, int, float,
+                         hipStream_t);
+void llmd_gated_act_quant(void*, int64_t, float*, const void*, int64_t, int, int, int, float, float, hipStream_t);
 int llmd_quant_fp8_groups(const void*, int64_t, void*, int64_t, float*, int64_t, int, int, hipStream_t);
 void llmd_moe_gemm_fp8(const void*, int64_t, const float*, int64_t, int, const int*, const int*, int, const void*,
                        int64_t, const float*, int, int, void*, int64_t, int, int, float, float, int, const void*,
@@ -549,6 +552,41 @@ void quant_fp8_rows(torch::Tensor x, torch::Tensor q, torch::Tensor scale) {
   TORCH_CHECK(rc == 0, "quant_fp8_rows failed: ", rc);
 }
 
+// q, scale <- fp8(rmsnorm(x [+= residual]) * w)
+void rms_norm_quant(torch::Tensor q, torch::Tensor scale, torch::Tensor x, c10::optional<torch::Tensor> residual,
+                    torch::Tensor w, double eps) {
+  const c10::hip::OptionalHIPGuard device_guard(dev_of(x));
+  CHECK_CUDA(x); CHECK_BF16(x); CHECK_BF16(w); CHECK_INNER(x); CHECK_INNER(q);
+  CHECK_DT(q, at::kFloat8_e4m3fn); CHECK_DT(scale, at::kFloat);
+  TORCH_CHECK(x.dim() == 2 && q.sizes() == x.sizes() && scale.numel() >= x.size(0), "rms_norm_quant shapes");
+  const int d = x.size(1);
+  TORCH_CHECK(d % 8 == 0 && w.numel() == d && w.is_contiguous(), "rms_norm_quant d");
+  TORCH_CHECK(x.stride(0) % 8 == 0 && q.stride(0) % 8 == 0, "16-B aligned rows");
+  void* rp = nullptr;
+  int64_t rs = 0;
+  if (residual.has_value()) {
+    CHECK_BF16(residual.value()); CHECK_INNER(residual.value());
+    TORCH_CHECK(residual->sizes() == x.sizes() && residual->stride(0) % 8 == 0, "residual shape");
+    rp = residual->data_ptr();
+    rs = residual->stride(0);
+  }
+  llmd_rms_norm_quant(q.data_ptr(), q.stride(0), scale.data_ptr<float>(), x.data_ptr(), x.stride(0), rp, rs,
+                      w.data_ptr(), x.size(0), d, (float)eps, cur_stream());
+}
+
+void gated_act_quant(torch::Tensor q, torch::Tensor scale, torch::Tensor x, int64_t mode, double alpha,
+                     double limit) {
+  const c10::hip::OptionalHIPGuard device_guard(dev_of(x));
+  CHECK_CUDA(x); CHECK_BF16(x); CHECK_INNER(x); CHECK_INNER(q);
+  CHECK_DT(q, at::kFloat8_e4m3fn); CHECK_DT(scale, at::kFloat);
+  TORCH_CHECK(x.dim() == 2 && q.dim() == 2 && q.size(0) == x.size(0), "gated_act_quant shape");
+  const int F = q.size(1);
+  TORCH_CHECK(x.size(1) == 2 * F && F % 8 == 0 && scale.numel() >= x.size(0), "gated_act_quant widths");
+  TORCH_CHECK(x.stride(0) % 8 == 0 && q.stride(0) % 8 == 0, "16-B aligned rows");
+  llmd_gated_act_quant(q.data_ptr(), q.stride(0), scale.data_ptr<float>(), x.data_ptr(), x.stride(0), x.size(0), F,
+                       (int)mode, (float)alpha, (float)limit, cur_stream());
+}
+
 void quant_fp8_groups(torch::Tensor x, torch::Tensor q, torch::Tensor scale) {
   const c10::hip::OptionalHIPGuard device_guard(dev_of(x));
   CHECK_CUDA(x); CHECK_BF16(x); CHECK_INNER(x); CHECK_INNER(q); CHECK_DT(q, at::kFloat8_e4m3fn);
@@ -696,6 +734,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("moe_tile_m", &llmd_moe_gemm_tile_m);
   m.def("quant_fp8_rows", &quant_fp8_rows);
   m.def("quant_fp8_groups", &quant_fp8_groups);
+  m.def("rms_norm_quant", &rms_norm_quant);
+  m.def("gated_act_quant", &gated_act_quant);
   m.def("moe_gemm_fp8", &moe_gemm_fp8);
   m.def("symm_alloc", &symm_alloc);
   m.def("symm_error", &symm_error);

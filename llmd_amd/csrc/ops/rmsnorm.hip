@@ -83,9 +83,113 @@ void launch(uint16_t* out, int64_t os, uint16_t* x, int64_t xs, uint16_t* res, i
 #undef L
 }
 
+// RMSNorm (optionally fused with the residual add) emitting fp8 e4m3fn with a
+// per-row dynamic scale for the next W8A8 GEMM (SURVEY K05 "+ optional FP8
+// quant"): the normalised row (rounded to bf16, as the unfused path would
+// store it) stays in registers, a second block reduction takes its amax, and
+// 8-B fp8 packets are written - no bf16 activation round trip through HBM.
+template <int VPT, bool FUSED_ADD>
+__global__ __launch_bounds__(NT) void rmsnorm_quant_kernel(
+    uint8_t* __restrict__ q, int64_t q_stride, float* __restrict__ scale,
+    const uint16_t* __restrict__ x, int64_t x_stride,
+    uint16_t* __restrict__ residual, int64_t res_stride,
+    const uint16_t* __restrict__ w, int d, float eps) {
+  __shared__ float red[NT / 64];
+  const int row = blockIdx.x;
+  const int nchunk = d >> 3;
+  const uint16_t* xr = x + (int64_t)row * x_stride;
+  float v[VPT][8];
+  float ss = 0.f;
+#pragma unroll
+  for (int c = 0; c < VPT; ++c) {
+    const int ci = threadIdx.x + c * NT;
+    if (ci < nchunk) {
+      u32x4_t a = *reinterpret_cast<const u32x4_t*>(xr + ci * 8);
+      unpack8(a, v[c]);
+      if constexpr (FUSED_ADD) {
+        uint16_t* rr = residual + (int64_t)row * res_stride;
+        u32x4_t r = *reinterpret_cast<const u32x4_t*>(rr + ci * 8);
+        float rf[8];
+        unpack8(r, rf);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[c][j] += rf[j];
+        u32x4_t p = pack8(v[c]);
+        *reinterpret_cast<u32x4_t*>(rr + ci * 8) = p;
+        unpack8(p, v[c]);
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) ss += v[c][j] * v[c][j];
+    }
+  }
+  ss = block_sum<NT>(ss, red);
+  const float inv = rsqrtf(ss / (float)d + eps);
+  float amax = 0.f;
+#pragma unroll
+  for (int c = 0; c < VPT; ++c) {
+    const int ci = threadIdx.x + c * NT;
+    if (ci < nchunk) {
+      u32x4_t wa = *reinterpret_cast<const u32x4_t*>(w + ci * 8);
+      float wf[8];
+      unpack8(wa, wf);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[c][j] = v[c][j] * inv * wf[j];
+      unpack8(pack8(v[c]), v[c]);  // bf16 rounding of the normalised value
+#pragma unroll
+      for (int j = 0; j < 8; ++j) amax = fmaxf(amax, fabsf(v[c][j]));
+    }
+  }
+  amax = wave_max(amax);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = amax;
+  __syncthreads();
+  float m = red[0];
+#pragma unroll
+  for (int i = 1; i < NT / 64; ++i) m = fmaxf(m, red[i]);
+  const float s = fmaxf(m / FP8_MAX, 1e-12f);
+  const float is = 1.f / s;
+  if (threadIdx.x == 0) scale[row] = s;
+  u32x2_t* qr = reinterpret_cast<u32x2_t*>(q + (int64_t)row * q_stride);
+#pragma unroll
+  for (int c = 0; c < VPT; ++c) {
+    const int ci = threadIdx.x + c * NT;
+    if (ci < nchunk) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[c][j] *= is;
+      qr[ci] = f32x8_to_fp8(v[c]);
+    }
+  }
+}
+
+template <bool FUSED>
+void launch_q(uint8_t* q, int64_t qs, float* scale, const uint16_t* x, int64_t xs, uint16_t* res, int64_t rs,
+              const uint16_t* w, int rows, int d, float eps, hipStream_t st) {
+  const int nchunk = d / 8;
+  const int vpt = (nchunk + NT - 1) / NT;
+  dim3 g(rows), b(NT);
+#define L(V) \
+  hipLaunchKernelGGL((rmsnorm_quant_kernel<V, FUSED>), g, b, 0, st, q, qs, scale, x, xs, res, rs, w, d, eps)
+  if (vpt <= 1) L(1);
+  else if (vpt <= 2) L(2);
+  else if (vpt <= 4) L(4);
+  else if (vpt <= 8) L(8);
+  else L(16);
+#undef L
+}
+
 }  // namespace
 
 extern "C" {
+// q, scale = fp8_per_row(rmsnorm(x [+ residual]) * w); residual updated in place when given
+void llmd_rms_norm_quant(void* q, int64_t q_stride, float* scale, const void* x, int64_t x_stride, void* residual,
+                         int64_t res_stride, const void* w, int rows, int d, float eps, hipStream_t st) {
+  if (rows == 0) return;
+  if (residual)
+    launch_q<true>((uint8_t*)q, q_stride, scale, (const uint16_t*)x, x_stride, (uint16_t*)residual, res_stride,
+                   (const uint16_t*)w, rows, d, eps, st);
+  else
+    launch_q<false>((uint8_t*)q, q_stride, scale, (const uint16_t*)x, x_stride, nullptr, 0, (const uint16_t*)w,
+                    rows, d, eps, st);
+}
+
 // out[rows, d] = x * rsqrt(mean(x^2) + eps) * w
 void llmd_rms_norm(void* out, int64_t out_stride, const void* x, int64_t x_stride,
                    const void* w, int rows, int d, float eps, hipStream_t st) {

@@ -37,6 +37,11 @@ def _linear(mod, x, bias):
     return F.linear(x, w, bias)
 
 
+def wants_fp8_input(lin) -> bool:
+    """A linear that can consume a pre-quantised (q, scale) activation."""
+    return lin.weight.dtype == torch.float8_e4m3fn and lin.lora is None
+
+
 def quantize_fp8(model: torch.nn.Module) -> int:
     """Online FP8 weight quantisation (vLLM ``--quantization fp8``): every
     Column/Row linear gets e4m3fn weights with per-output-channel scales, and
@@ -124,7 +129,11 @@ class RMSNorm(torch.nn.Module):
         self.eps = eps
         self.weight = torch.nn.Parameter(torch.ones(d, device=device, dtype=dtype), requires_grad=False)
 
-    def forward(self, x, residual: Optional[torch.Tensor] = None):
+    def forward(self, x, residual: Optional[torch.Tensor] = None, quant: bool = False):
+        """quant=True: emit (fp8 q, per-row scale) for a W8A8 consumer (fused K05 + K16)."""
+        if quant:
+            q = ops.rms_norm_quant(x, self.weight, self.eps, residual)
+            return q if residual is None else (q, residual)
         if residual is None:
             return ops.rms_norm(x, self.weight, self.eps)
         ops.fused_add_rms_norm(x, residual, self.weight, self.eps)

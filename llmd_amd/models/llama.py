@@ -15,7 +15,7 @@ from llmd_amd.engine.attn_meta import AttnMeta
 from llmd_amd.engine.config import ModelConfig
 from llmd_amd.parallel.state import get_state
 
-from .layers import ColumnLinear, LMHead, PagedAttention, RMSNorm, RowLinear, VocabEmbedding
+from .layers import ColumnLinear, LMHead, PagedAttention, RMSNorm, RowLinear, VocabEmbedding, wants_fp8_input
 
 
 class LlamaMLP(torch.nn.Module):
@@ -25,7 +25,10 @@ class LlamaMLP(torch.nn.Module):
         self.down = RowLinear(cfg.intermediate_size, cfg.hidden_size, device=device)
 
     def forward(self, x):
-        return self.down(ops.gated_act(self.gate_up(x), ops.ACT_SILU))
+        h = self.gate_up(x)
+        if wants_fp8_input(self.down):  # SiLU*up fused with the down proj's fp8 activation quant
+            return self.down(ops.gated_act_quant(h, ops.ACT_SILU))
+        return self.down(ops.gated_act(h, ops.ACT_SILU))
 
 
 class LlamaDecoderLayer(torch.nn.Module):
@@ -59,16 +62,19 @@ class LlamaDecoderLayer(torch.nn.Module):
         qkv[:, a.Hq * a.D : (a.Hq + a.Hkv) * a.D] = self.k_norm(k).view(T, -1)
 
     def forward(self, x, residual, meta: AttnMeta):
+        # W8A8: the norms emit fp8 + per-row scales straight into the fp8 GEMMs
+        q_in = wants_fp8_input(self.qkv)
         if residual is None:
             residual = x.clone()
-            x = self.input_layernorm(x)
+            x = self.input_layernorm(x, quant=q_in)
         else:
-            x, residual = self.input_layernorm(x, residual)
+            x, residual = self.input_layernorm(x, residual, quant=q_in)
         qkv = self.qkv(x)
         if self.qk_norm:
             self._apply_qk_norm(qkv)
         x = self.o_proj(self.attn(qkv, meta))
-        x, residual = self.post_attention_layernorm(x, residual)
+        q_mlp = isinstance(self.mlp, LlamaMLP) and wants_fp8_input(self.mlp.gate_up)
+        x, residual = self.post_attention_layernorm(x, residual, quant=q_mlp)
         return self.mlp(x), residual
 
 

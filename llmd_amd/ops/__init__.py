@@ -202,10 +202,49 @@ def quant_fp8_weight(w: torch.Tensor):
     return wq, s.view(1, -1).contiguous()
 
 
-def fp8_linear(x: torch.Tensor, wq: torch.Tensor, w_scale: torch.Tensor, bias=None) -> torch.Tensor:
+def rms_norm_quant(x: torch.Tensor, w: torch.Tensor, eps: float, residual: Optional[torch.Tensor] = None):
+    """(q fp8 [T, d], scale [T, 1]) of rmsnorm(x [+ residual]) * w; with ``residual``
+    it is updated in place (residual += x) like fused_add_rms_norm."""
+    if not _gpu(x):
+        if residual is not None:
+            residual.copy_((residual.float() + x.float()).to(residual.dtype))
+            y = ref.rms_norm(residual, w, eps)
+        else:
+            y = ref.rms_norm(x, w, eps)
+        return quant_fp8_rows(y)
+    q = torch.empty(x.shape, dtype=FP8, device=x.device)
+    s = torch.empty(x.shape[0], 1, dtype=torch.float32, device=x.device)
+    native().rms_norm_quant(q, s, x, residual, w, eps)
+    return q, s
+
+
+def gated_act_quant(x: torch.Tensor, mode: int = 0, alpha: float = 1.702, limit: float = 7.0):
+    """(q fp8 [T, F], scale [T, 1]) of the gated activation (SURVEY K07 + K16)."""
+    if not _gpu(x):
+        return quant_fp8_rows(ref.gated_act(x, mode, alpha, limit))
+    F = x.shape[1] // 2
+    q = torch.empty(x.shape[0], F, dtype=FP8, device=x.device)
+    s = torch.empty(x.shape[0], 1, dtype=torch.float32, device=x.device)
+    native().gated_act_quant(q, s, x, mode, alpha, limit)
+    return q, s
+
+
+def fp8_linear(x, wq: torch.Tensor, w_scale: torch.Tensor, bias=None) -> torch.Tensor:
     """y = (q_x s_x) (q_w s_w)^T (+ bias), bf16 out. Activations are quantised
     per token on the fly (HIP kernel); the GEMM is hipBLASLt's fp8 GEMM with
-    row-wise scales through torch._scaled_mm (a plain library GEMM)."""
+    row-wise scales through torch._scaled_mm (a plain library GEMM).
+    ``x`` may already be quantised: a (q, scale) pair from rms_norm_quant /
+    gated_act_quant."""
+    if isinstance(x, tuple):
+        xq, xs = x
+        if not _gpu(xq):
+            y = (xq.float() * xs) @ (wq.float() * w_scale.view(-1, 1)).t()
+            if bias is not None:
+                y = y + bias.float()
+            return y.to(torch.bfloat16)
+        if xq.shape[0] == 0:
+            return torch.empty(0, wq.shape[0], dtype=torch.bfloat16, device=xq.device)
+        return torch._scaled_mm(xq, wq.t(), scale_a=xs, scale_b=w_scale, bias=bias, out_dtype=torch.bfloat16)
     lead = x.shape[:-1]
     x2 = x.reshape(-1, x.shape[-1])
     if not _gpu(x2):

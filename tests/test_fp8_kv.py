@@ -231,3 +231,46 @@ def test_moe_experts_fp8_gpu(T, E, k, d, F, act):
     r = ops.moe_experts_fp8(x.cpu(), ids.cpu(), wts.cpu(), w1q.cpu(), w1s.cpu(), w2q.cpu(), w2s.cpu(), act)
     err = (y.float().cpu() - r.float()).abs().max().item()
     assert err < 0.06 * r.float().abs().max().item() + 1e-3, err
+
+
+def test_fused_norm_act_quant_cpu_matches_unfused():
+    torch.manual_seed(0)
+    x = torch.randn(6, 256).to(torch.bfloat16)
+    res = torch.randn(6, 256).to(torch.bfloat16)
+    w = (torch.rand(256) + 0.5).to(torch.bfloat16)
+    r2 = res.clone()
+    q, s = ops.rms_norm_quant(x, w, 1e-5, r2)
+    xx, rr = x.clone(), res.clone()
+    ops.fused_add_rms_norm(xx, rr, w, 1e-5)
+    q2, s2 = ops.quant_fp8_rows(xx)
+    assert torch.equal(r2, rr) and torch.allclose(s, s2) and torch.equal(q.float(), q2.float())
+    h = torch.randn(6, 2 * 128).to(torch.bfloat16)
+    qa, sa = ops.gated_act_quant(h, ops.ACT_SILU)
+    qb, sb = ops.quant_fp8_rows(ops.gated_act(h, ops.ACT_SILU))
+    assert torch.allclose(sa, sb) and torch.equal(qa.float(), qb.float())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("d", [256, 4096, 8192])
+def test_fused_norm_act_quant_gpu(d):
+    torch.manual_seed(1)
+    x = torch.randn(37, d, device="cuda").to(torch.bfloat16)
+    res = torch.randn(37, d, device="cuda").to(torch.bfloat16)
+    w = (torch.rand(d, device="cuda") + 0.5).to(torch.bfloat16)
+    for with_res in (False, True):
+        r_gpu = res.clone() if with_res else None
+        q, s = ops.rms_norm_quant(x, w, 1e-5, r_gpu)
+        r_cpu = res.cpu().clone() if with_res else None
+        qr, sr = ops.rms_norm_quant(x.cpu(), w.cpu(), 1e-5, r_cpu)
+        if with_res:
+            torch.testing.assert_close(r_gpu.cpu().float(), r_cpu.float(), atol=0, rtol=0)
+        torch.testing.assert_close(s.cpu(), sr, rtol=2e-2, atol=1e-6)
+        deq, deq_r = q.float().cpu() * s.cpu(), qr.float() * sr
+        assert (deq - deq_r).abs().max() <= 0.07 * deq_r.abs().max()
+    h = torch.randn(37, 2 * d, device="cuda").to(torch.bfloat16)
+    for mode in (0, 2):
+        qa, sa = ops.gated_act_quant(h, mode)
+        qb, sb = ops.gated_act_quant(h.cpu(), mode)
+        torch.testing.assert_close(sa.cpu(), sb, rtol=2e-2, atol=1e-6)
+        deq, deq_r = qa.float().cpu() * sa.cpu(), qb.float() * sb
+        assert (deq - deq_r).abs().max() <= 0.07 * deq_r.abs().max()
