@@ -620,12 +620,23 @@ __global__ __launch_bounds__(NT, 2) void moe_gemm_fp8_kernel(
 }
 
 
-// FP8 variant of the v2 grouped GEMM: a K-step is 128 e4m3 = the same 128-B LDS
-// row, so staging is byte-identical to the bf16 kernel. Fragments are 8 B
-// (ds_read_b64: row*128 + swz(row, 2s + kq/2)*16 + 8*(kq&1), conflict-free for
-// the two 32-lane halves), 4 mfma_f32_16x16x32_fp8_fp8 per K-step into a block
-// accumulator folded with xs[row][kb] * ws[e][nb][kb] (each wave's 64 columns
-// sit in one 128-column weight-scale block).
+// FP8 variant of the v2 grouped GEMM on the block-scaled MFMA
+// v_mfma_scale_f32_16x16x128_f8f6f4 (e4m3 x e4m3, unit E8M0 scales): one
+// instruction per 16x16 tile per 128-K step at 2x the bf16 rate
+// (MI355X_MICROARCH.md "FP8"). A K-step is 128 e4m3 = the same 128-B LDS row
+// as the bf16 kernel, so the DMA staging is unchanged; lane l takes the 32
+// bytes [32*(l>>4), +32) of its row (operand layout probed by
+// scripts/probes/mfma_scale_layout.hip) with two ds_read_b128. The 16-B chunk
+// swizzle is g3(row) = tab[(row>>1)&7], tab = {0,1,4,5,6,7,2,3}, which keeps
+// both halves of those 32-B reads (and 16-B bf16-style reads) free of bank
+// conflicts for all four ds_read_b128 lane groups. Each step's product is
+// folded into the accumulator with xs[row][kb] * ws[e][nb][kb] (DeepSeek
+// 1x128 activation / 128x128 weight block scales; each wave's 64 columns sit
+// in one weight-scale block).
+__device__ __forceinline__ int g3_swz(int row, int c) { return c ^ ((0x32765410 >> (4 * ((row >> 1) & 7))) & 7); }
+
+typedef int i32x8_t __attribute__((ext_vector_type(8)));
+
 template <int MODE>
 __global__ __launch_bounds__(G2_NT, 2) void moe_gemm2_fp8_kernel(
     const uint8_t* __restrict__ X, int64_t x_stride, const float* __restrict__ xs, int64_t xs_stride, int topk,
@@ -651,30 +662,32 @@ __global__ __launch_bounds__(G2_NT, 2) void moe_gemm2_fp8_kernel(
   for (int i = 0; i < 2; ++i) {
     const int row = 8 * (2 * w + i) + lr;
     const int tok = tok_of(m0 + row);
-    asrc[i] = X + (int64_t)(tok < 0 ? 0 : tok) * x_stride + g2_swz(row, lp) * 16;
+    asrc[i] = X + (int64_t)(tok < 0 ? 0 : tok) * x_stride + g3_swz(row, lp) * 16;
   }
-  const uint8_t* bsrc[8];
+  int boff[8];  // 32-bit offsets into this expert's weights (fewer live VGPRs than 8 pointers)
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
     const int row = 8 * (8 * w + i) + lr;
     const int n = min(n0 + row, N - 1);
-    bsrc[i] = We + (int64_t)n * K + g2_swz(row, lp) * 16;
+    boff[i] = n * K + g3_swz(row, lp) * 16;
   }
   auto issue = [&](char* base, int k0) {
 #pragma unroll
     for (int i = 0; i < 2; ++i) g2_dma(asrc[i] + k0, base + (2 * w + i) * 1024);
 #pragma unroll
-    for (int i = 0; i < 8; ++i) g2_dma(bsrc[i] + k0, base + G2_AB + (8 * w + i) * 1024);
+    for (int i = 0; i < 8; ++i) g2_dma(We + boff[i] + k0, base + G2_AB + (8 * w + i) * 1024);
   };
   const int r16 = lane & 15, kq = lane >> 4;
-  const float* xsr[4][4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int tok = tok_of(m0 + 16 * i + 4 * kq + r);
-      xsr[i][r] = tok < 0 ? nullptr : xs + (int64_t)tok * xs_stride;
-    }
+  // activation scales of the tile's 64 rows: wave 0 lane r loads xs[row r][kb+1]
+  // together with the next tile's DMA and publishes it to xs_sm before the next
+  // barrier, so the fold reads 4 contiguous floats per 16-row block from LDS.
+  // Padding rows read row 0 (their outputs are never stored).
+  __shared__ float xs_sm[2][G2_BM];
+  const float* xs_row = nullptr;
+  if (w == 0) {
+    const int tok = tok_of(m0 + lane);
+    xs_row = xs + (int64_t)(tok < 0 ? 0 : tok) * xs_stride;
+  }
   const float* wsr = ws + ((int64_t)e * nnb + (n0 + 64 * w) / 128) * nkb;
   f32x4_t acc[4][4];
 #pragma unroll
@@ -684,50 +697,57 @@ __global__ __launch_bounds__(G2_NT, 2) void moe_gemm2_fp8_kernel(
   auto compute = [&](const char* base, int kb) {
     const char* A = base;
     const char* B = base + G2_AB;
-    f32x4_t blk[4][4];
+    i32x8_t bfr[4];
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) blk[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      long af[4], bfr[4];
-      const int c = 2 * s + (kq >> 1), h = 8 * (kq & 1);
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int row = 16 * i + r16;
-        af[i] = *reinterpret_cast<const long*>(A + row * 128 + g2_swz(row, c) * 16 + h);
-      }
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int row = 64 * w + 16 * j + r16;
-        bfr[j] = *reinterpret_cast<const long*>(B + row * 128 + g2_swz(row, c) * 16 + h);
-      }
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) blk[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_fp8_fp8(af[i], bfr[j], blk[i][j], 0, 0, 0);
+    for (int j = 0; j < 4; ++j) {
+      const int row = 64 * w + 16 * j + r16;
+      const u32x4_t lo = *reinterpret_cast<const u32x4_t*>(B + row * 128 + g3_swz(row, 2 * kq) * 16);
+      const u32x4_t hi = *reinterpret_cast<const u32x4_t*>(B + row * 128 + g3_swz(row, 2 * kq + 1) * 16);
+      bfr[j] = i32x8_t{(int)lo[0], (int)lo[1], (int)lo[2], (int)lo[3], (int)hi[0], (int)hi[1], (int)hi[2], (int)hi[3]};
     }
     const float wsv = wsr[kb];
+    const float* xsb = xs_sm[kb & 1];
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < 4; ++i) {  // one 16-row block at a time keeps the block accumulators at 16 VGPRs
+      const int row = 16 * i + r16;
+      const u32x4_t lo = *reinterpret_cast<const u32x4_t*>(A + row * 128 + g3_swz(row, 2 * kq) * 16);
+      const u32x4_t hi = *reinterpret_cast<const u32x4_t*>(A + row * 128 + g3_swz(row, 2 * kq + 1) * 16);
+      const i32x8_t af =
+          i32x8_t{(int)lo[0], (int)lo[1], (int)lo[2], (int)lo[3], (int)hi[0], (int)hi[1], (int)hi[2], (int)hi[3]};
+      f32x4_t blk[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        blk[j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(af, bfr[j], f32x4_t{0.f, 0.f, 0.f, 0.f}, 0, 0, 0,
+                                                                  127, 0, 127);
+      const f32x4_t sx = *reinterpret_cast<const f32x4_t*>(xsb + 16 * i + 4 * kq);
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const float sc = xsr[i][r] ? xsr[i][r][kb] * wsv : 0.f;
+        const float sc = sx[r] * wsv;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j][r] += blk[i][j][r] * sc;
+        for (int j = 0; j < 4; ++j) acc[i][j][r] += blk[j][r] * sc;
       }
+    }
   };
+  float xs_next = 0.f;
   issue(buf0, 0);
+  if (w == 0) xs_next = xs_row[0];
   for (int kt = 0; kt < nkb; kt += 2) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (w == 0) xs_sm[0][lane] = xs_next;
     __syncthreads();
-    if (kt + 1 < nkb) issue(buf1, (kt + 1) * 128);
+    if (kt + 1 < nkb) {
+      issue(buf1, (kt + 1) * 128);
+      if (w == 0) xs_next = xs_row[kt + 1];
+    }
     compute(buf0, kt);
     if (kt + 1 >= nkb) break;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (w == 0) xs_sm[1][lane] = xs_next;
     __syncthreads();
-    if (kt + 2 < nkb) issue(buf0, (kt + 2) * 128);
+    if (kt + 2 < nkb) {
+      issue(buf0, (kt + 2) * 128);
+      if (w == 0) xs_next = xs_row[kt + 2];
+    }
     compute(buf1, kt + 1);
   }
 #pragma unroll
