@@ -193,6 +193,7 @@ class LLMEngine:
                               len(r.output_token_ids), r.num_cached_tokens)
             if r.status.finished:
                 o.kv_transfer_params = r.extra.get("kv_transfer_params_out")
+                o.embedding = r.extra.get("embedding")
                 self.metrics.on_finish(r)
             outs.append(o)
         self.metrics.on_step(so, touched, dt, self.sched.num_running, self.sched.num_waiting,

@@ -349,6 +349,12 @@ class ModelRunner:
         logits = self.run_plan(pl)
         if not reqs:
             return {}
+        if pl.get("embed") and getattr(self, "_last_hidden", None) is not None:
+            # pooling for /v1/embeddings: last-token final hidden state, L2-normalised
+            e = torch.nn.functional.normalize(self._last_hidden.float(), dim=-1).cpu()
+            for i, r in enumerate(reqs):
+                if r.params.embed:
+                    r.extra["embedding"] = e[i].tolist()
         return self._sample(logits, reqs)
 
     def plan(self, so: SchedulerOutput, block_tables: dict[int, list[int]]) -> tuple[dict, list]:
@@ -367,6 +373,9 @@ class ModelRunner:
         mm = self._mm_rows(so)
         if mm is not None:
             pl["mm"] = mm
+        if any(r.params.embed for r in reqs):
+            pl["embed"] = True
+            pl["graph"] = False
         return pl, reqs
 
     def _mm_rows(self, so: SchedulerOutput):
@@ -401,7 +410,9 @@ class ModelRunner:
         if not rows:
             return None
         idx = torch.tensor(rows, dtype=torch.long).to(self.device, non_blocking=True)
-        return self.model.compute_logits(h.index_select(0, idx))
+        hs = h.index_select(0, idx)
+        self._last_hidden = hs if pl.get("embed") else None
+        return self.model.compute_logits(hs)
 
     def _sample(self, logits, reqs):
         temps, seeds, topk, topp, any_rand, any_k, any_p = self._sampling_tensors(reqs)

@@ -21,6 +21,7 @@ class SamplingParams:
     ignore_eos: bool = False
     logprobs: Optional[int] = None
     n: int = 1
+    embed: bool = False  # /v1/embeddings: keep the final hidden state of the last prompt token
 
     @property
     def greedy(self) -> bool:
@@ -141,5 +142,6 @@ class RequestOutput:
     num_output_tokens: int
     num_cached_tokens: int = 0
     kv_transfer_params: Optional[dict] = None
+    embedding: Optional[list] = None
     ttft: Optional[float] = None
     metrics: Optional[dict] = None

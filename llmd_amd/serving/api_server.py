@@ -5,7 +5,10 @@ Endpoints
   GET  /v1/models                  readiness (model loaded) + LoRA adapters
   GET  /metrics                    Prometheus, vLLM-compatible names
   POST /v1/completions             (stream / non-stream, kv_transfer_params)
-  POST /v1/chat/completions
+  POST /v1/chat/completions        (text + image parts)
+  POST /v1/embeddings, /v1/responses, /v1/messages (Anthropic),
+       /inference/v1/generate (token in / token out) - the request surfaces
+       the router's openai-parser knows (docs/api-reference/epp-http-apis.md)
   POST /v1/completions/render      exact token ids (router token-producer)
   POST /v1/chat/completions/render
   POST /tokenize, /detokenize
@@ -82,6 +85,10 @@ class OpenAIServer:
         r.add_post("/reset_prefix_cache", self.reset_prefix_cache)
         r.add_get("/fault_tolerance/status", self.ft_status)
         r.add_post("/fault_tolerance/apply", self.ft_apply)
+        r.add_post("/v1/embeddings", self.embeddings)
+        r.add_post("/v1/responses", self.responses)
+        r.add_post("/v1/messages", self.messages)
+        r.add_post("/inference/v1/generate", self.generate_tokens)
         r.add_post("/v1/load_lora_adapter", self.load_lora)
         r.add_post("/v1/unload_lora_adapter", self.unload_lora)
         if self.mm is not None:
@@ -374,6 +381,142 @@ class OpenAIServer:
     async def resume(self, req):
         self.aeng.resume()
         return web.json_response({"paused": False})
+
+    # ------------------------------------------------------------ other OpenAI / vLLM / Anthropic surfaces
+    async def _run_one(self, req, ids, params, prio=0, lora=0, mm=None):
+        rid = req.headers.get("x-request-id") or f"req-{uuid.uuid4().hex}"
+        toks, last = [], None
+        async for o in self.aeng.generate(rid, ids, params, prio, None, lora, mm):
+            toks.extend(o.new_token_ids)
+            last = o
+        return toks, last
+
+    async def embeddings(self, req: web.Request):
+        """OpenAI /v1/embeddings: last-token final hidden state, L2-normalised
+        (the pooling of decoder-only embedding models)."""
+        body = await req.json()
+        inp = body.get("input")
+        if inp is None:
+            return _err(400, "input is required")
+        try:
+            if isinstance(inp, str) or (isinstance(inp, list) and inp and isinstance(inp[0], int)):
+                inputs = [inp]
+            else:
+                inputs = list(inp)
+            id_lists = [self.tok.encode(x) if isinstance(x, str) else list(x) for x in inputs]
+        except (TypeError, ValueError) as e:
+            return _err(400, str(e))
+        params = SamplingParams(max_tokens=1, temperature=0.0, ignore_eos=True, embed=True)
+        res = await asyncio.gather(*[self._run_one(req, ids, params, lora=self._lora_id(body)) for ids in id_lists])
+        data = [{"object": "embedding", "index": i, "embedding": (last.embedding if last else None) or []}
+                for i, (_, last) in enumerate(res)]
+        n = sum(len(x) for x in id_lists)
+        return web.json_response({"object": "list", "data": data, "model": body.get("model") or self.name,
+                                  "usage": {"prompt_tokens": n, "total_tokens": n}})
+
+    async def responses(self, req: web.Request):
+        """OpenAI Responses API (non-streaming): `input` (text or messages) +
+        `instructions` -> one assistant message output item."""
+        body = await req.json()
+        inp = body.get("input")
+        msgs = []
+        if body.get("instructions"):
+            msgs.append({"role": "system", "content": body["instructions"]})
+        if isinstance(inp, str):
+            msgs.append({"role": "user", "content": inp})
+        elif isinstance(inp, list):
+            for m in inp:
+                c = m.get("content")
+                if isinstance(c, list):
+                    c = "".join(p.get("text", "") for p in c if isinstance(p, dict))
+                msgs.append({"role": m.get("role", "user"), "content": c or ""})
+        else:
+            return _err(400, "input is required")
+        ids = self.tok.encode(render_chat(msgs, True, self.chat_style))
+        params = SamplingParams.from_openai(dict(body, max_tokens=body.get("max_output_tokens")),
+                                            default_max=max(1, self.cfg.sched.max_model_len - len(ids) - 1))
+        toks, last = await self._run_one(req, ids, params, lora=self._lora_id(body))
+        text = self.tok.decode(toks)
+        rid = f"resp_{uuid.uuid4().hex}"
+        return web.json_response({
+            "id": rid, "object": "response", "created_at": int(time.time()),
+            "status": "completed" if last and last.finish_reason != "error" else "failed",
+            "model": body.get("model") or self.name,
+            "output": [{"type": "message", "id": f"msg_{uuid.uuid4().hex}", "status": "completed",
+                        "role": "assistant", "content": [{"type": "output_text", "text": text, "annotations": []}]}],
+            "usage": {"input_tokens": len(ids), "output_tokens": len(toks), "total_tokens": len(ids) + len(toks)}})
+
+    async def messages(self, req: web.Request):
+        """Anthropic Messages API (non-streaming): system + messages with text
+        (and base64 image) blocks -> one assistant text block."""
+        body = await req.json()
+        if body.get("stream"):
+            return _err(400, "streaming is not supported on /v1/messages; use /v1/chat/completions")
+        msgs = []
+        sysm = body.get("system")
+        if isinstance(sysm, list):
+            sysm = "".join(b.get("text", "") for b in sysm if isinstance(b, dict))
+        if sysm:
+            msgs.append({"role": "system", "content": sysm})
+        for m in body.get("messages") or []:
+            c = m.get("content")
+            if isinstance(c, list):
+                parts = []
+                for b in c:
+                    if b.get("type") == "text":
+                        parts.append({"type": "text", "text": b.get("text", "")})
+                    elif b.get("type") == "image" and (b.get("source") or {}).get("type") == "base64":
+                        src = b["source"]
+                        parts.append({"type": "image_url", "image_url": {
+                            "url": f"data:{src.get('media_type', 'image/png')};base64,{src.get('data', '')}"}})
+                c = parts
+            msgs.append({"role": m.get("role", "user"), "content": c})
+        if not msgs:
+            return _err(400, "messages is required")
+        chat_body = {"messages": msgs, "max_tokens": body.get("max_tokens", 16),
+                     "temperature": body.get("temperature", 1.0), "top_p": body.get("top_p", 1.0),
+                     "top_k": body.get("top_k", 0), "stop": body.get("stop_sequences") or []}
+        try:
+            mm = None
+            if self.mm is not None and self._has_images(chat_body):
+                ids, mm = await self._chat_mm(chat_body, req.headers)
+            else:
+                ids = self._chat_ids(chat_body)
+            params = SamplingParams.from_openai(chat_body)
+        except (ValueError, TypeError) as e:
+            return _err(400, str(e))
+        toks, last = await self._run_one(req, ids, params, lora=self._lora_id(body), mm=mm)
+        text = self.tok.decode(toks)
+        stop_seq = None
+        for s in params.stop:
+            k = text.find(s)
+            if k >= 0:
+                text, stop_seq = text[:k], s
+        reason = "stop_sequence" if stop_seq else ("max_tokens" if last and last.finish_reason == "length"
+                                                   else "end_turn")
+        return web.json_response({"id": f"msg_{uuid.uuid4().hex}", "type": "message", "role": "assistant",
+                                  "model": body.get("model") or self.name,
+                                  "content": [{"type": "text", "text": text}], "stop_reason": reason,
+                                  "stop_sequence": stop_seq,
+                                  "usage": {"input_tokens": len(ids), "output_tokens": len(toks)}})
+
+    async def generate_tokens(self, req: web.Request):
+        """vLLM token-in / token-out generate API (`/inference/v1/generate`, the
+        router's vllmgrpc-style path): {"token_ids"|"prompt", "sampling_params"}."""
+        body = await req.json()
+        if "token_ids" in body:
+            ids = list(body["token_ids"])
+        elif isinstance(body.get("prompt"), str):
+            ids = self.tok.encode(body["prompt"])
+        else:
+            return _err(400, "token_ids or prompt is required")
+        sp = dict(body.get("sampling_params") or {})
+        params = SamplingParams.from_openai(sp, default_max=16)
+        toks, last = await self._run_one(req, ids, params, lora=self._lora_id(body))
+        return web.json_response({"request_id": req.headers.get("x-request-id"), "prompt_token_ids": ids,
+                                  "choices": [{"index": 0, "token_ids": toks,
+                                               "finish_reason": last.finish_reason if last else "abort"}],
+                                  "usage": {"prompt_tokens": len(ids), "completion_tokens": len(toks)}})
 
     # ------------------------------------------------------------ resilience (IRO)
     def faults(self) -> list[dict]:

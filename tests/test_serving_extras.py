@@ -64,3 +64,53 @@ def test_render_server_matches_engine_and_ft_endpoints():
     assert res["eng_chat"] == res["render_chat"] and res["eng_comp"] == res["render_comp"]
     assert res["st0"]["status"] == "healthy" and res["st1"]["status"] == "paused"
     assert res["bad"] == 400 and res["after"] == 200
+
+
+def test_embeddings_responses_messages_generate_endpoints():
+    async def main():
+        eng = build_server(_cfg())
+        r1, p1 = await _serve(eng.app())
+        base = f"http://127.0.0.1:{p1}"
+        out = {}
+        try:
+            async with aiohttp.ClientSession() as s:
+                async with s.post(base + "/v1/embeddings", json={"model": "tiny-llama",
+                                                                 "input": ["hello world", "goodbye"]}) as r:
+                    out["emb"] = (r.status, await r.json())
+                async with s.post(base + "/v1/responses", json={"model": "tiny-llama", "input": "hi",
+                                                                "instructions": "be brief", "max_output_tokens": 4,
+                                                                "temperature": 0}) as r:
+                    out["resp"] = (r.status, await r.json())
+                async with s.post(base + "/v1/messages", json={
+                        "model": "tiny-llama", "max_tokens": 3, "system": "sys", "temperature": 0,
+                        "messages": [{"role": "user", "content": [{"type": "text", "text": "hello"}]}]}) as r:
+                    out["msg"] = (r.status, await r.json())
+                async with s.post(base + "/inference/v1/generate", json={
+                        "token_ids": [5, 6, 7, 8], "sampling_params": {"max_tokens": 5, "temperature": 0,
+                                                                        "ignore_eos": True}}) as r:
+                    out["gen"] = (r.status, await r.json())
+                async with s.post(base + "/v1/completions", json={"model": "tiny-llama", "prompt": [5, 6, 7, 8],
+                                                                  "max_tokens": 5, "temperature": 0,
+                                                                  "ignore_eos": True,
+                                                                  "return_token_ids": True}) as r:
+                    out["cmp"] = (r.status, await r.json())
+        finally:
+            await r1.cleanup()
+            eng.aeng.shutdown()
+        return out
+
+    out = asyncio.run(main())
+    st, emb = out["emb"]
+    assert st == 200 and len(emb["data"]) == 2
+    v = emb["data"][0]["embedding"]
+    assert len(v) == 256 and abs(sum(x * x for x in v) - 1.0) < 1e-3
+    assert emb["data"][0]["embedding"] != emb["data"][1]["embedding"]
+    st, resp = out["resp"]
+    assert st == 200 and resp["object"] == "response" and resp["usage"]["output_tokens"] == 4
+    assert resp["output"][0]["content"][0]["type"] == "output_text"
+    st, msg = out["msg"]
+    assert st == 200 and msg["type"] == "message" and msg["stop_reason"] == "max_tokens"
+    assert msg["usage"]["output_tokens"] == 3
+    st, gen = out["gen"]
+    assert st == 200 and len(gen["choices"][0]["token_ids"]) == 5
+    assert gen["choices"][0]["token_ids"] == out["cmp"][1]["choices"][0]["token_ids"]
