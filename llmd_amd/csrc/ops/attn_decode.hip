@@ -105,6 +105,7 @@ __global__ __launch_bounds__(NT, 2) void paged_decode_kernel(
   const int g = lane >> 4, c16 = lane & 15;
   const int* bt = block_tables + (int64_t)b * bt_stride;
   const int64_t head_off = (int64_t)kvh * bs * D;
+  const int lbs = __builtin_ctz(bs);  // block size is a power of two (checked on the host)
 
   // ---- Q fragments (B operand of S^T = K Q^T)
   bf16x8_t qf[KS];
@@ -137,8 +138,8 @@ __global__ __launch_bounds__(NT, 2) void paged_decode_kernel(
     for (int b4 = 0; b4 < 4; ++b4) {
       int key = tts + 16 * b4 + rowoff(c16 >> 2) + (c16 & 3);
       key = key < s1 ? key : s0;
-      const int phys = bt[key / bs];
-      const int64_t kr = (int64_t)phys * block_stride + head_off + (int64_t)(key % bs) * D;
+      const int phys = bt[key >> lbs];
+      const int64_t kr = (int64_t)phys * block_stride + head_off + (int64_t)(key & (bs - 1)) * D;
 #pragma unroll
       for (int s = 0; s < KS; ++s) kf[b4][s] = ld_cache<F8>(kc, kr + (4 * s + g) * 8);
     }
@@ -153,8 +154,8 @@ __global__ __launch_bounds__(NT, 2) void paged_decode_kernel(
       const int row = i * RPI + lane / CPR;
       int key = ts + row;
       key = key < s1 ? key : s0;
-      const int phys = bt[key / bs];
-      const int64_t vp = (int64_t)phys * block_stride + head_off + (int64_t)(key % bs) * D;
+      const int phys = bt[key >> lbs];
+      const int64_t vp = (int64_t)phys * block_stride + head_off + (int64_t)(key & (bs - 1)) * D;
       vr[i] = ld_cache<F8>(vc, vp + (lane % CPR) * 8);
     }
     // ---- S^T = K Q^T

@@ -68,6 +68,7 @@ __global__ __launch_bounds__(NT, 1) void mla_kernel(
       qf[s] = __builtin_bit_cast(bf16x8_t, v);
     }
     u32x4_t kr[LPT];
+    const int lbs = __builtin_ctz(bs);  // power-of-two block size (checked on the host)
     auto load_tile = [&](int ts) {
 #pragma unroll
       for (int i = 0; i < LPT; ++i) {
@@ -75,7 +76,7 @@ __global__ __launch_bounds__(NT, 1) void mla_kernel(
         const int row = idx / CPR, ch = idx % CPR;
         int key = ts + row;
         key = key < k1 ? key : k1 - 1;
-        const int64_t off = (int64_t)bt[key / bs] * block_stride + (int64_t)(key % bs) * DQK + ch * 8;
+        const int64_t off = (int64_t)bt[key >> lbs] * block_stride + (int64_t)(key & (bs - 1)) * DQK + ch * 8;
         kr[i] = *reinterpret_cast<const u32x4_t*>(kc + off);
       }
     };

@@ -76,6 +76,7 @@ __global__ __launch_bounds__(NT, 2) void prefill_kernel(
   const int pbase = ctx - ql;  // position of query token 0
   const int* bt = block_tables + (int64_t)seq * bt_stride;
   const int64_t head_off = (int64_t)kvh * bs * D;
+  const int lbs = __builtin_ctz(bs);  // block size is a power of two (checked on the host)
 
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, g = lane >> 4, c16 = lane & 15;
   const int head = kvh * G + hg * HPW + (w % HPW);
@@ -120,8 +121,8 @@ __global__ __launch_bounds__(NT, 2) void prefill_kernel(
       const int row = idx / CPR, ch = idx % CPR;
       int key = ts + row;
       key = key < ctx ? key : ctx - 1;
-      const int phys = bt[key / bs];
-      const int64_t off = (int64_t)phys * block_stride + head_off + (int64_t)(key % bs) * D + ch * 8;
+      const int phys = bt[key >> lbs];
+      const int64_t off = (int64_t)phys * block_stride + head_off + (int64_t)(key & (bs - 1)) * D + ch * 8;
       if constexpr (F8) {
         kr[i] = *reinterpret_cast<const u32x2_t*>(reinterpret_cast<const uint8_t*>(kc) + off);
         vr[i] = *reinterpret_cast<const u32x2_t*>(reinterpret_cast<const uint8_t*>(vc) + off);

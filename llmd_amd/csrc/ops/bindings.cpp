@@ -179,6 +179,7 @@ void check_cache(const torch::Tensor& k, const torch::Tensor& v, int64_t Hkv, in
   TORCH_CHECK(k.stride(3) == 1 && k.stride(2) == D && k.stride(1) == k.size(2) * D,
               "cache inner layout");
   TORCH_CHECK(v.sizes() == k.sizes() && v.strides() == k.strides(), "v_cache layout");
+  TORCH_CHECK(k.size(2) > 0 && (k.size(2) & (k.size(2) - 1)) == 0, "KV block size must be a power of two");
 }
 
 // q [B, >=Hq*D] (token stride), out [B, Hq*D]
@@ -230,6 +231,7 @@ void mla_attention(torch::Tensor out, torch::Tensor q, torch::Tensor cache, torc
   CHECK_DT(block_tables, at::kInt); CHECK_DT(row_seq, at::kInt); CHECK_DT(row_len, at::kInt);
   TORCH_CHECK(cache.dim() == 3 && cache.size(2) == 576 && cache.stride(2) == 1 && cache.stride(1) == 576,
               "mla cache [blocks, bs, 576] with contiguous rows");
+  TORCH_CHECK(cache.size(1) > 0 && (cache.size(1) & (cache.size(1) - 1)) == 0, "MLA block size must be a power of two");
   TORCH_CHECK(block_tables.dim() == 2 && block_tables.stride(1) == 1, "block_tables 2-D");
   const int R = q.size(0);
   TORCH_CHECK(row_seq.numel() == R && row_len.numel() == R, "mla: rows mismatch");

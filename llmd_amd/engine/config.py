@@ -250,6 +250,11 @@ class CacheConfig:
     enable_prefix_caching: bool = True
     kv_cache_dtype: str = "auto"
 
+    def __post_init__(self):
+        # the attention kernels index blocks with shifts/masks
+        if self.block_size <= 0 or self.block_size & (self.block_size - 1):
+            raise ValueError(f"block_size must be a power of two, got {self.block_size}")
+
 
 @dataclass
 class SchedulerConfig:
