@@ -144,14 +144,16 @@ class LLMEngine:
             return err_outs
         pc = self.cfg.parallel
         if pc.enable_dbo and not any_prefill and t_max >= pc.dbo_decode_token_threshold:
-            # dual-batch overlap: two micro-batches of ceil(t_max/2) MoE rows on every rank
-            ep.set_step_rows((t_max + 1) // 2)
+            # dual-batch overlap: two micro-batches of ceil(t_max/2) MoE rows on every rank,
+            # or bucket/2 rows when the step replays a captured dual-batch graph
+            dbo_b = self.runner.dbo_bucket(t_max)
+            ep.set_step_rows(dbo_b // 2 if dbo_b else (t_max + 1) // 2)
             if so.empty:
-                self.runner.execute_dbo(None, {})
+                self.runner.execute_dbo(None, {}, bucket=dbo_b)
                 self.runner.eplb_tick()
                 self._flush_events()
                 return err_outs
-            sampled = self.runner.execute_dbo(so, self.block_tables(so))
+            sampled = self.runner.execute_dbo(so, self.block_tables(so), bucket=dbo_b)
             self.runner.eplb_tick()
             return self._finish_step(so, sampled, err_outs, t0)
         bucket = None

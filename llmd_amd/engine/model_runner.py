@@ -106,6 +106,7 @@ class ModelRunner:
         self.kv = None
         self.num_blocks = 0
         self.graphs: dict[int, tuple] = {}
+        self.dbo_graphs: dict[int, tuple] = {}  # bucket -> (graph, logits) of two B/2 micro-batches
         self._rng = np.random.default_rng(cfg.seed)
         self.graph_plans: dict[int, tuple] = {}
         self._init_symm()
@@ -485,7 +486,7 @@ class ModelRunner:
         yield x
 
     @torch.no_grad()
-    def execute_dbo(self, so: Optional[SchedulerOutput], block_tables: dict) -> dict:
+    def execute_dbo(self, so: Optional[SchedulerOutput], block_tables: dict, bucket: Optional[int] = None) -> dict:
         """Dual-batch overlap (reference --enable-dbo,
         guides/wide-ep-lws/modelserver/gpu/vllm/base/decode.yaml:112-113) for a
         decode-only wide-EP step: the decodes split into two micro-batches,
@@ -493,9 +494,13 @@ class ModelRunner:
         receive buffers; their layers are issued alternately on two HIP
         streams so one micro-batch's dispatch/combine kernels (bounded to 64
         workgroups) run while the other's attention/expert GEMMs occupy the
-        remaining CUs. ``so=None``: idle DP rank, two one-token dummy halves."""
+        remaining CUs. ``so=None``: idle DP rank, two one-token dummy halves.
+        ``bucket``: replay the captured dual-batch graph of that size instead
+        (the caller sets the EP step rows to bucket/2 on every rank)."""
         from llmd_amd.parallel import symm
 
+        if bucket is not None and (so is None or not any(sr.req.params.embed for sr in so.decodes)):
+            return self._replay_dbo(so, block_tables, bucket)
         plans, reqs = [], []
         if so is None or so.empty:
             for _ in range(2):
@@ -622,8 +627,115 @@ class ModelRunner:
                 h = self.model(self.g_ids[:B], meta)
                 lg = self.model.compute_logits(h)
             self.graphs[B] = (g, lg)
+        if self._dbo_graphable():
+            self._capture_dbo_graphs(buckets, pool)
         torch.cuda.synchronize()
-        log.info("captured %d decode graphs in %.1fs", len(buckets), time.time() - t0)
+        log.info("captured %d decode graphs (+%d dual-batch) in %.1fs", len(buckets), len(self.dbo_graphs),
+                 time.time() - t0)
+
+    # ------------------------------------------------------------ dual-batch overlap under hipGraphs
+    def _dbo_graphable(self) -> bool:
+        from llmd_amd.parallel import symm
+
+        return bool(self.cfg.parallel.enable_dbo) and self.lora is None and symm.micro_batches() >= 2
+
+    def _dbo_meta(self, m: int, h: int, ws) -> AttnMeta:
+        """Attention metadata of micro-batch m: rows [m*h, (m+1)*h) of the static
+        buffers, its own split-KV workspace (the halves run concurrently)."""
+        lo, hi = m * h, (m + 1) * h
+        meta = AttnMeta(num_tokens=h, positions=self.g_pos[lo:hi], slot_mapping=self.g_slots[lo:hi], num_decode=h,
+                        d_block_tables=self.g_bt[lo:hi], d_seq_lens=self.g_len[lo:hi], d_split=self.graph_plans[h],
+                        d_workspace=ws[0], d_max_ctx=self.max_model_len)
+        if self.is_mla:
+            meta.mla_d_rows, meta.mla_split, meta.mla_workspace = self.g_rows[:h], self.mla_plans[h], ws[1]
+        return meta
+
+    def _dbo_forward(self, B: int, metas, streams):
+        """Layers of the two micro-batches issued alternately on their own
+        streams, forked from and joined back into the current stream (which is
+        the capture stream under torch.cuda.graph, so both branches are
+        recorded as parallel graph nodes)."""
+        from llmd_amd.parallel import symm
+
+        h = B // 2
+        cur = torch.cuda.current_stream()
+        for s in streams:
+            s.wait_stream(cur)
+        gens = [self._forward_steps(self.g_ids[m * h:(m + 1) * h], metas[m]) for m in (0, 1)]
+        outs = [None, None]
+        while outs[0] is None or outs[1] is None:
+            for m in (0, 1):
+                if outs[m] is None:
+                    symm.set_active_mb(m)
+                    with torch.cuda.stream(streams[m]):
+                        outs[m] = next(gens[m])
+        symm.set_active_mb(0)
+        for s in streams:
+            cur.wait_stream(s)
+        return self.model.compute_logits(torch.cat(outs))
+
+    def _capture_dbo_graphs(self, buckets, pool):
+        """One graph per bucket B >= 2 holding both micro-batches of B/2 rows
+        (symm EP channel / receive buffers per micro-batch, R = B/2 rows per
+        rank). Every EP rank captures the same buckets in the same order."""
+        dev = self.device
+        ws0 = (self.g_ws, getattr(self, "g_mla_ws", None))
+        ws1 = (tuple(torch.empty_like(t) for t in self.g_ws),
+               tuple(torch.empty_like(t) for t in self.g_mla_ws) if self.is_mla else None)
+        if not hasattr(self, "_dbo_streams"):
+            self._dbo_streams = (torch.cuda.Stream(device=dev), torch.cuda.Stream(device=dev))
+        streams = self._dbo_streams
+        for B in reversed([b for b in buckets if b >= 2]):
+            h = B // 2
+            metas = [self._dbo_meta(0, h, ws0), self._dbo_meta(1, h, ws1)]
+            s = torch.cuda.Stream()
+            s.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(s):
+                for _ in range(2):
+                    self._dbo_forward(B, metas, streams)
+            torch.cuda.current_stream().wait_stream(s)
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, pool=pool):
+                lg = self._dbo_forward(B, metas, streams)
+            self.dbo_graphs[B] = (g, lg)
+
+    def dbo_bucket(self, t_max: int) -> Optional[int]:
+        """Captured dual-batch bucket for a lockstep step of at most t_max decode rows per rank."""
+        b = self._bucket(max(t_max, 2))
+        return b if b in self.dbo_graphs else None
+
+    def _replay_dbo(self, so: Optional[SchedulerOutput], block_tables: dict, B: int) -> dict:
+        """The first ceil(nd/2) decodes fill micro-batch 0 from row 0, the rest
+        micro-batch 1 from row B/2; other rows are padding (slot -1, len 1).
+        ``so=None``: idle DP rank, all padding."""
+        g, lg = self.dbo_graphs[B]
+        h = B // 2
+        ids = np.zeros(B, np.int64)
+        pos = np.zeros(B, np.int64)
+        slots = np.full(B, -1, np.int64)
+        bt = np.zeros((B, self.width), np.int32)
+        ln = np.ones(B, np.int32)
+        reqs, grow = [], []
+        if so is not None and not so.empty:
+            pl, reqs = self.plan(so, block_tables)
+            nd = pl["nd"]
+            h0 = (nd + 1) // 2
+            if h0 > h or nd - h0 > h:
+                raise ValueError(f"dual-batch bucket {B} too small for {nd} decodes")
+            perm = np.concatenate([np.arange(h0), h + np.arange(nd - h0)]).astype(np.int64)
+            ids[perm], pos[perm], slots[perm] = pl["ids"], pl["pos"], pl["slots"]
+            bt[perm], ln[perm] = pl["d_bt"], pl["d_len"]
+            grow = perm[pl["rows"]].tolist()
+        host = torch.from_numpy(np.stack([ids, pos, slots])).pin_memory()
+        self.g_ids[:B].copy_(host[0], non_blocking=True)
+        self.g_pos[:B].copy_(host[1], non_blocking=True)
+        self.g_slots[:B].copy_(host[2], non_blocking=True)
+        self.g_bt[:B].copy_(torch.from_numpy(bt).pin_memory(), non_blocking=True)
+        self.g_len[:B].copy_(torch.from_numpy(ln).pin_memory(), non_blocking=True)
+        g.replay()
+        if not reqs:
+            return {}
+        return self._sample(lg[torch.tensor(grow, dtype=torch.long).to(self.device, non_blocking=True)], reqs)
 
     @torch.no_grad()
     def execute_dummy(self, graph_bucket: Optional[int] = None):

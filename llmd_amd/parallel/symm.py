@@ -226,6 +226,11 @@ def ep() -> Optional[SymmEP]:
     return _eps[min(_active_mb, len(_eps) - 1)]
 
 
+def micro_batches() -> int:
+    """Number of EP micro-batch channels installed (2 with dual-batch overlap)."""
+    return len(_eps)
+
+
 def set_active_mb(m: int):
     global _active_mb
     _active_mb = m

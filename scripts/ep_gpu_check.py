@@ -28,6 +28,7 @@ def main():
     ap.add_argument("--dbo", action="store_true")
     ap.add_argument("--eplb", action="store_true")
     ap.add_argument("--weights", default=None)
+    ap.add_argument("--dbo-eager", action="store_true", help="drop the captured dual-batch graphs")
     a = ap.parse_args()
     a.weights = a.weights or f"/tmp/llmd_ep_gpu_check_{a.model}.safetensors"
     rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
@@ -64,6 +65,9 @@ def main():
         extra.update(enable_eplb=True, eplb_config={"num_redundant_experts": 2 * world, "step_interval": 3})
     eng = LLMEngine(cfg(data_parallel_size=world, enable_expert_parallel=True, all2all_backend="symm_ll", **extra))
     assert eng.dp_lockstep and symm.ep() is not None
+    if a.dbo_eager:
+        eng.runner.dbo_graphs.clear()
+    dbo_graphs = sorted(eng.runner.dbo_graphs)
     reqs = [eng.add_request(f"r{rank}-{i}", p, sp) for i, p in enumerate(prompts)]
     steps = 0
     while eng.dp_has_unfinished():
@@ -84,7 +88,7 @@ def main():
     dist.all_gather_object(flags, {"rank": rank, "ok": ok, "agree": agree, "total": total, "steps": steps,
                                    "timeout_flag": err})
     if rank == 0:
-        print(json.dumps({"model": a.model, "dbo": a.dbo, "eplb": a.eplb, "world": world,
+        print(json.dumps({"model": a.model, "dbo": a.dbo, "dbo_graphs": dbo_graphs, "eplb": a.eplb, "world": world,
                           "ok": all(f["ok"] for f in flags), "ranks": flags}), flush=True)
     dist.barrier()
     symm.shutdown()

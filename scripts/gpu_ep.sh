@@ -8,4 +8,4 @@ run() {  # name, args...
     || { echo "ep check $name failed"; tail -40 gpurun_out/ep_$name.log; return 1; }
   grep '^{' gpurun_out/ep_$name.log
 }
-run base && run dbo --dbo && run eplb --eplb && run deepseek_dbo --model tiny-deepseek --dbo && run deepseek_eplb_dbo --model tiny-deepseek --dbo --eplb
+run base && run dbo --dbo && run dbo_eager --dbo --dbo-eager && run eplb --eplb && run deepseek_dbo --model tiny-deepseek --dbo && run deepseek_eplb_dbo --model tiny-deepseek --dbo --eplb
