@@ -279,6 +279,7 @@ class ParallelConfig:
     eplb_config: Optional[dict] = None  # {"window_size", "step_interval", "num_redundant_experts"}
     enable_dbo: bool = False  # dual-batch overlap of EP exchange with compute (decode steps)
     dbo_decode_token_threshold: int = 32
+    dbo_prefill_token_threshold: int = 32  # steps with prefills (reference prefill.yaml:83-84)
 
 
 @dataclass
@@ -367,6 +368,7 @@ def add_engine_args(p: argparse.ArgumentParser) -> argparse.ArgumentParser:
     p.add_argument("--eplb-config", type=_json_arg, default=None)
     p.add_argument("--enable-dbo", action="store_true")
     p.add_argument("--dbo-decode-token-threshold", type=int, default=32)
+    p.add_argument("--dbo-prefill-token-threshold", type=int, default=32)
     p.add_argument("--enforce-eager", action="store_true")
     p.add_argument("--kv-transfer-config", type=_json_arg, default=None)
     p.add_argument("--kv-events-config", type=_json_arg, default=None)
@@ -395,6 +397,7 @@ def engine_config_from_args(a) -> EngineConfig:
         enable_eplb=getattr(a, "enable_eplb", False), eplb_config=getattr(a, "eplb_config", None),
         enable_dbo=getattr(a, "enable_dbo", False),
         dbo_decode_token_threshold=getattr(a, "dbo_decode_token_threshold", 32),
+        dbo_prefill_token_threshold=getattr(a, "dbo_prefill_token_threshold", 32),
         enforce_eager=a.enforce_eager, kv_transfer_config=a.kv_transfer_config,
         kv_events_config=a.kv_events_config, kv_offload_config=a.kv_offload_config,
         policy=a.scheduling_policy, enable_lora=getattr(a, "enable_lora", False),

@@ -143,16 +143,20 @@ class LLMEngine:
             self._flush_events()
             return err_outs
         pc = self.cfg.parallel
-        if pc.enable_dbo and not any_prefill and t_max >= pc.dbo_decode_token_threshold:
-            # dual-batch overlap: two micro-batches of ceil(t_max/2) MoE rows on every rank,
-            # or bucket/2 rows when the step replays a captured dual-batch graph
-            dbo_b = self.runner.dbo_bucket(t_max)
-            ep.set_step_rows(dbo_b // 2 if dbo_b else (t_max + 1) // 2)
+        if self._use_dbo(t_max, bool(any_prefill)):
+            # dual-batch overlap. Decode-only: two micro-batches of ceil(t_max/2) MoE
+            # rows on every rank, or bucket/2 rows when the step replays a captured
+            # dual-batch graph. With prefills the chunks are not split, so a half
+            # may hold up to t_max rows.
+            dbo_b = None if any_prefill else self.runner.dbo_bucket(t_max)
+            ep.set_step_rows(dbo_b // 2 if dbo_b else (t_max if any_prefill else (t_max + 1) // 2))
             if so.empty:
                 self.runner.execute_dbo(None, {}, bucket=dbo_b)
                 self.runner.eplb_tick()
                 self._flush_events()
                 return err_outs
+            if self.offload is not None:
+                self.offload.before_step(so)
             sampled = self.runner.execute_dbo(so, self.block_tables(so), bucket=dbo_b)
             self.runner.eplb_tick()
             return self._finish_step(so, sampled, err_outs, t0)
@@ -171,6 +175,24 @@ class LLMEngine:
         sampled = self.runner.execute(so, self.block_tables(so), force_eager=bucket is None, bucket=bucket)
         self.runner.eplb_tick()
         return self._finish_step(so, sampled, err_outs, t0)
+
+    def _use_dbo(self, t_max: int, any_prefill: bool) -> bool:
+        """Same decision on every EP rank (inputs are group-wide maxima). On the
+        GPU the micro-batches run on two streams, which needs the per-micro-batch
+        symm EP channels (RCCL calls of one communicator are not interleaved
+        across streams) and rows within the symm receive buffers."""
+        pc = self.cfg.parallel
+        if not pc.enable_dbo:
+            return False
+        thr = pc.dbo_prefill_token_threshold if any_prefill else pc.dbo_decode_token_threshold
+        if t_max < thr:
+            return False
+        if not self.runner.is_gpu:
+            return True
+        from llmd_amd.parallel import symm
+
+        sep = symm.ep()
+        return symm.micro_batches() >= 2 and sep is not None and t_max <= sep.R_max
 
     def dp_has_unfinished(self) -> bool:
         """True while any DP rank of the EP group still has requests."""

@@ -488,8 +488,8 @@ class ModelRunner:
     @torch.no_grad()
     def execute_dbo(self, so: Optional[SchedulerOutput], block_tables: dict, bucket: Optional[int] = None) -> dict:
         """Dual-batch overlap (reference --enable-dbo,
-        guides/wide-ep-lws/modelserver/gpu/vllm/base/decode.yaml:112-113) for a
-        decode-only wide-EP step: the decodes split into two micro-batches,
+        guides/wide-ep-lws/modelserver/gpu/vllm/base/decode.yaml:112-113,
+        prefill.yaml:83-84) for a wide-EP step: the step splits into two micro-batches,
         each with its own attention metadata and its own symm EP channel /
         receive buffers; their layers are issued alternately on two HIP
         streams so one micro-batch's dispatch/combine kernels (bounded to 64
@@ -509,10 +509,8 @@ class ModelRunner:
                               "d_bt": np.zeros((1, w), np.int32), "d_len": np.ones(1, dtype=np.int32),
                               "p_ql": [], "p_ctx": [], "p_bt": np.zeros((0, w), np.int32), "rows": []})
         else:
-            h = (len(so.decodes) + 1) // 2
-            for part in (so.decodes[:h], so.decodes[h:]):
-                sub = SchedulerOutput(decodes=list(part))
-                if part:
+            for sub in self._dbo_split(so):
+                if not sub.empty:
                     pl, rq = self.plan(sub, block_tables)
                 else:  # odd split of a 1-token step: a dummy half keeps the collectives paired
                     w = self.width
@@ -562,6 +560,16 @@ class ModelRunner:
         if not all_reqs:
             return {}
         return self._sample(torch.cat(logits), all_reqs)
+
+    @staticmethod
+    def _dbo_split(so: SchedulerOutput) -> tuple[SchedulerOutput, SchedulerOutput]:
+        """Two micro-batches of a step: decodes halved, then each prefill chunk
+        to the half with fewer tokens so far (chunks are not split)."""
+        h = (len(so.decodes) + 1) // 2
+        halves = (SchedulerOutput(decodes=list(so.decodes[:h])), SchedulerOutput(decodes=list(so.decodes[h:])))
+        for sr in sorted(so.prefills, key=lambda s: -s.num_new_tokens):
+            min(halves, key=lambda x: x.num_tokens).prefills.append(sr)
+        return halves
 
     # ------------------------------------------------------------ graphs
     def _bucket(self, n: int) -> int:

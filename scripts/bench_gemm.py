@@ -50,7 +50,13 @@ def main():
     ap.add_argument("--tunable", action="store_true")
     ap.add_argument("--m", type=int, nargs="*", default=[8192, 4096, 64])
     ap.add_argument("--skinny", action="store_true")
+    ap.add_argument("--lookup", action="store_true", help="use the repo's tuned GEMM table (what the engine runs)")
     a = ap.parse_args()
+    if a.lookup:
+        import sys
+        sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+        from llmd_amd.ops.gemm_tuning import enable_lookup
+        print("lookup:", enable_lookup())
     if a.skinny:
         shapes = {"qkv": (10240, 8192), "o": (8192, 8192), "gate_up": (57344, 8192), "down": (8192, 28672),
                   "lm_head": (128256, 8192)}

@@ -60,7 +60,7 @@ def main():
     sp = SamplingParams(max_tokens=ntok, temperature=0.0, ignore_eos=True)
     extra = {}
     if a.dbo:
-        extra.update(enable_dbo=True, dbo_decode_token_threshold=2)
+        extra.update(enable_dbo=True, dbo_decode_token_threshold=2, dbo_prefill_token_threshold=2)
     if a.eplb:
         extra.update(enable_eplb=True, eplb_config={"num_redundant_experts": 2 * world, "step_interval": 3})
     eng = LLMEngine(cfg(data_parallel_size=world, enable_expert_parallel=True, all2all_backend="symm_ll", **extra))
@@ -84,9 +84,13 @@ def main():
     agree = sum(int(x == y) for g, w in zip(got, want) for x, y in zip(g, w))
     total = sum(len(w) for w in want)
     ok = err == 0 and all(g[:3] == w[:3] for g, w in zip(got, want)) and agree >= 0.8 * total
+    # first divergence per request: (request, token index, got, want)
+    div = [(i, next((j for j, (x, y) in enumerate(zip(g, w)) if x != y), None)) for i, (g, w) in
+           enumerate(zip(got, want))]
+    div = [(i, j, got[i][j], want[i][j]) for i, j in div if j is not None]
     flags = [None] * world
     dist.all_gather_object(flags, {"rank": rank, "ok": ok, "agree": agree, "total": total, "steps": steps,
-                                   "timeout_flag": err})
+                                   "timeout_flag": err, "diverge": div})
     if rank == 0:
         print(json.dumps({"model": a.model, "dbo": a.dbo, "dbo_graphs": dbo_graphs, "eplb": a.eplb, "world": world,
                           "ok": all(f["ok"] for f in flags), "ranks": flags}), flush=True)

@@ -1,5 +1,6 @@
-"""Dual-batch overlap on CPU, world 2 (gloo): decode steps split
-into two micro-batches whose layers alternate (two HIP streams on GPU, each
+"""Dual-batch overlap on CPU, world 2 (gloo): decode steps (and
+steps with prefill chunks above --dbo-prefill-token-threshold) split into two
+micro-batches whose layers alternate (two HIP streams on GPU, each
 with its own EP channel); greedy outputs still match a single-process engine,
 including the early-finishing rank that keeps stepping with dummy halves."""
 import os
@@ -23,19 +24,21 @@ def _worker(rank, world, port, model, path, backend, out):
     init_distributed(tp_size=1, backend="gloo")
     eng = LLMEngine(_cfg(model, path, data_parallel_size=world, enable_expert_parallel=True,
                          all2all_backend=backend, enable_dbo=True, dbo_decode_token_threshold=1))
-    calls = {"n": 0}
+    calls = {"n": 0, "p": 0}
     orig = eng.runner.execute_dbo
 
-    def counted(*a, **k):
+    def counted(so, *a, **k):
         calls["n"] += 1
-        return orig(*a, **k)
+        calls["p"] += int(so is not None and bool(so.prefills))
+        return orig(so, *a, **k)
 
     eng.runner.execute_dbo = counted
     sp = SamplingParams(max_tokens=NTOK[rank], temperature=0.0, ignore_eos=True)
     reqs = [eng.add_request(f"r{rank}-{i}", p, sp) for i, p in enumerate(_prompts(rank))]
     while eng.dp_has_unfinished():
         eng.step()
-    torch.save({"tokens": [r.output_token_ids for r in reqs], "dbo_steps": calls["n"]}, f"{out}.{rank}")
+    torch.save({"tokens": [r.output_token_ids for r in reqs], "dbo_steps": calls["n"],
+                "dbo_prefill_steps": calls["p"]}, f"{out}.{rank}")
     destroy()
 
 
@@ -56,7 +59,7 @@ def test_dbo_world2_matches_single_process(tmp_path, backend):
     mp.spawn(_worker, args=(2, _free_port(), model, path, backend, out), nprocs=2, join=True)
     for rank in (0, 1):
         d = torch.load(f"{out}.{rank}", weights_only=True)
-        assert d["dbo_steps"] >= 3
+        assert d["dbo_steps"] >= 3 and d["dbo_prefill_steps"] >= 1
         got = d["tokens"]
         agree = sum(int(a == b) for g, w in zip(got, want[rank]) for a, b in zip(g, w))
         total = sum(len(w) for w in want[rank])
