@@ -5,7 +5,7 @@
 // The same kernel serves decode (one row per sequence) and prefill (one row
 // per query token, row_len = position + 1) - MQA with a 128-head group.
 //
-// Grid (split, head group of 16, row); 256 threads = 4 waves cooperating on a
+// v1 (H not 64/128, or LLMD_MLA_V1=1). Grid (split, head group of 16, row); 256 threads = 4 waves cooperating on a
 // 64-key tile staged once in LDS (576 bf16 per key, rows padded to 1168 B so
 // 16-row ds_read_b128 are conflict-free):
 //   S^T[key][head] : wave w takes keys 16w..16w+15, 18 x mfma_16x16x32_bf16
@@ -17,6 +17,8 @@
 // The next tile is prefetched into registers while the current one computes.
 // nsplit > 1 writes unnormalised partials (O, max, sum in log2 units) merged
 // by mla_reduce_kernel.
+#include <cstdlib>
+
 #include "llmd_common.h"
 
 using namespace llmd;
@@ -196,6 +198,211 @@ __global__ __launch_bounds__(NT, 1) void mla_kernel(
   }
 }
 
+// ---------------------------------------------------------------- v2: all heads per workgroup
+// Grid (split, H / (16 NW), row); NW waves, wave w of head group y owns heads
+// 16 (NW y + w) .. +15
+// over the whole 64-key tile, so every K/V tile is fetched from HBM/L2 once per
+// row (v1 re-fetched it per 16-head group), the softmax stays inside the wave
+// (P lane-local in the PV A-operand layout, no LDS round trip or cross-wave
+// reduction) and there is one barrier per tile.
+//   tile: 64 keys x 1152 B, no padding; 16-B chunk c of row r stored at slot
+//         c ^ mla_swz(r). global_load_lds_dwordx4 (LDS-DMA) fills it
+//         lane-linearly (the swizzle is applied on the SOURCE side), double
+//         buffered: 2 x 73,728 B.
+//   mla_swz(r) = (r & 2) | ((r >> 1) & 4) makes both the S^T A-operand reads
+//   (ds_read_b128, lane groups {0-3,12-15,20-27}, {4-11,16-19,28-31}, ...)
+//   and the transposed V reads (ds_read_b64_tr_b16, 32-lane groups) cover
+//   every bank exactly once (searched exhaustively over 16-row patterns).
+//   per wave per tile: 72 MFMAs for S^T (4 key blocks x 18 k-steps), 64 for
+//   O += P V (2 key halves x 32 dim blocks); O = 128 accumulator registers.
+constexpr int V2_ROWB = DQK * 2;          // 1152 B
+constexpr int V2_TILE = 64 * V2_ROWB;     // 73,728 B
+constexpr int V2_UNITS = 64 * CPR;        // 4608 16-B slots = 72 DMA wave-instructions
+
+__device__ __forceinline__ int mla_swz(int r) { return (r & 2) | ((r >> 1) & 4); }
+
+template <int NW, bool BIG>
+__global__ __launch_bounds__(64 * NW, 1) void mla_v2_kernel(
+    const uint16_t* __restrict__ q, int64_t q_row_stride, const uint16_t* __restrict__ kc,
+    int64_t block_stride, int bs, const int* __restrict__ block_tables, int bt_stride,
+    const int* __restrict__ row_seq, const int* __restrict__ row_len, int H, float scale_log2,
+    int split_size, int nsplit, uint16_t* __restrict__ out, int64_t out_row_stride,
+    float* __restrict__ part_o, float* __restrict__ part_ml) {
+  __shared__ __attribute__((aligned(1024))) char buf0[V2_TILE];
+  __shared__ __attribute__((aligned(1024))) char buf1[V2_TILE];
+  const int sp = blockIdx.x, r = blockIdx.z;
+  const int len = row_len[r];
+  const int k0 = sp * split_size, k1 = min(len, k0 + split_size);
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, g = lane >> 4, c16 = lane & 15;
+  const int h0 = 16 * (NW * blockIdx.y + w);  // this wave's first head
+  const int head = h0 + c16;
+  const int* bt = block_tables + (int64_t)row_seq[r] * bt_stride;
+  const int lbs = __builtin_ctz(bs);
+
+  float m = NEG_INF, l = 0.f;  // stats of head c16 of this wave
+  f32x4_t o[32];
+#pragma unroll
+  for (int n = 0; n < 32; ++n) o[n] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  if (k0 < k1) {
+    bf16x8_t qf[18];
+    {
+      const uint16_t* qr = q + (int64_t)r * q_row_stride + (int64_t)head * DQK;
+#pragma unroll
+      for (int s = 0; s < 18; ++s) qf[s] = *reinterpret_cast<const bf16x8_t*>(qr + 32 * s + 8 * g);
+    }
+    // DMA: slot u = 64 * (w + NW * k) + lane of the tile image
+    auto issue = [&](char* base, int ts) {
+      int64_t tile_off = 0;
+      if constexpr (BIG) tile_off = (int64_t)bt[ts >> lbs] * block_stride + (int64_t)(ts & (bs - 1)) * DQK;
+#pragma unroll
+      for (int k = 0; k < 72 / NW; ++k) {
+        const int u = 64 * (w + NW * k) + lane;
+        const int row = u / CPR, ch = (u - row * CPR) ^ mla_swz(row);
+        const int key = min(ts + row, k1 - 1);
+        int64_t off;
+        if constexpr (BIG) {
+          off = tile_off + (int64_t)(key - ts) * DQK;
+        } else {
+          off = (int64_t)bt[key >> lbs] * block_stride + (int64_t)(key & (bs - 1)) * DQK;
+        }
+        __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)(kc + off + ch * 8),
+                                         (void __attribute__((address_space(3)))*)(base + 1024 * (w + NW * k)),
+                                         16, 0, 0);
+      }
+    };
+    // Per-lane LDS offsets. The swizzle depends on row & 15 only, so every read
+    // below is one of 6 lane registers + a compile-time immediate (buffer,
+    // key block, k-step, dim block), which keeps the address registers out of
+    // the way of the 128 accumulators and 72 Q registers.
+    //   S^T A operand: row srow (+16 b4), chunk (4s + g) ^ ssw
+    //     = 4s + (g ^ (ssw & 2)) +/- (ssw & 4)   (+ for even s, - for odd s)
+    //   V^T B operand: row vrow (+32 t2, +16), chunk (2n + (pp >> 1)) ^ vsw
+    //     = 2 ((n & ~3) + ((n & 3) ^ (vsw >> 1))) + (pp >> 1)
+    const int qq = c16 >> 2, pp = c16 & 3;
+    const int srow = rowoff(c16 >> 2) + (c16 & 3), ssw = mla_swz(srow);
+    const int gx = g ^ (ssw & 2);
+    const int offE = srow * V2_ROWB + 16 * (gx + (ssw & 4));
+    const int offO = srow * V2_ROWB + 16 * (gx - (ssw & 4));
+    const int vrow = rowoff(g) + qq, vk = mla_swz(vrow) >> 1;
+    int voff[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) voff[j] = vrow * V2_ROWB + 8 * (pp & 1) + 16 * (pp >> 1) + 32 * (j ^ vk);
+    auto compute = [&](const char* kt, int ts) {
+      // ---- S^T[key][head] = K . Q^T over 576 dims
+      f32x4_t sc[4];
+#pragma unroll
+      for (int b4 = 0; b4 < 4; ++b4) {
+        f32x4_t a = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int s = 0; s < 18; ++s) {
+          const char* p = kt + ((s & 1) ? offO : offE) + b4 * 16 * V2_ROWB + 64 * s;
+          const bf16x8_t ka = *reinterpret_cast<const bf16x8_t*>(p);
+          a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ka, qf[s], a, 0, 0, 0);
+        }
+        sc[b4] = a;
+      }
+      // rows of sc[b4]: keys ts + 16 b4 + rowoff(g) + i, column: head c16
+      if (ts + 64 > k1) {
+#pragma unroll
+        for (int b4 = 0; b4 < 4; ++b4)
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+            if (ts + 16 * b4 + rowoff(g) + i >= k1) sc[b4][i] = NEG_INF;
+      }
+      float mx = NEG_INF;
+#pragma unroll
+      for (int b4 = 0; b4 < 4; ++b4)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) mx = fmaxf(mx, sc[b4][i]);
+      mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      const float tm = mx * scale_log2;
+      if (__ballot(tm > m + 8.f) != 0) {  // lazy rescale (threshold 2^8), wave-uniform
+        const float mnew = fmaxf(m, tm);
+        const float alpha = (mnew == NEG_INF) ? 1.f : __builtin_amdgcn_exp2f(m - mnew);
+        l *= alpha;
+        m = mnew;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const float a = __shfl(alpha, 4 * g + i, 64);
+#pragma unroll
+          for (int n = 0; n < 32; ++n) o[n][i] *= a;
+        }
+      }
+      const float msub = (m == NEG_INF) ? 0.f : m;
+      float ps = 0.f;
+#pragma unroll
+      for (int b4 = 0; b4 < 4; ++b4)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const float p = __builtin_amdgcn_exp2f(fmaf(sc[b4][i], scale_log2, -msub));
+          sc[b4][i] = p;
+          ps += p;
+        }
+      ps += __shfl_xor(ps, 16, 64);
+      ps += __shfl_xor(ps, 32, 64);
+      l += ps;
+      // ---- O[head][dim] += P[head][key] . V[key][dim]   (V = first 512 dims of the key row)
+#pragma unroll
+      for (int t2 = 0; t2 < 2; ++t2) {
+        bf16x8_t pa;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          pa[j] = (__bf16)sc[2 * t2][j];
+          pa[4 + j] = (__bf16)sc[2 * t2 + 1][j];
+        }
+#pragma unroll
+        for (int n = 0; n < 32; ++n) {
+          const char* p0 = kt + voff[n & 3] + 32 * t2 * V2_ROWB + 32 * (n & ~3);
+          s16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4_t*)p0);
+          s16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+              (__attribute__((address_space(3))) s16x4_t*)(p0 + 16 * V2_ROWB));
+          const bf16x8_t vb = __builtin_bit_cast(
+              bf16x8_t, s16x8_t{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]});
+          o[n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pa, vb, o[n], 0, 0, 0);
+        }
+      }
+    };
+    const int nt = (k1 - k0 + 63) >> 6;
+    issue(buf0, k0);
+    for (int t = 0; t < nt; t += 2) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (t + 1 < nt) issue(buf1, k0 + 64 * (t + 1));
+      compute(buf0, k0 + 64 * t);
+      if (t + 1 >= nt) break;
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (t + 2 < nt) issue(buf0, k0 + 64 * (t + 2));
+      compute(buf1, k0 + 64 * (t + 1));
+    }
+  }
+  // ---- epilogue: O rows are heads 16w + 4g + i (stats in lane 4g + i), columns dims 16n + c16
+  if (nsplit == 1) {
+    const float inv = l > 0.f ? 1.f / l : 0.f;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const float f = __shfl(inv, 4 * g + i, 64);
+      uint16_t* orow = out + (int64_t)r * out_row_stride + (int64_t)(h0 + 4 * g + i) * DV;
+#pragma unroll
+      for (int n = 0; n < 32; ++n) orow[16 * n + c16] = f2bf(o[n][i] * f);
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      float* po = part_o + (((int64_t)r * H + h0 + 4 * g + i) * nsplit + sp) * DV;
+#pragma unroll
+      for (int n = 0; n < 32; ++n) po[16 * n + c16] = o[n][i];
+    }
+    if (g == 0) {
+      float* pm = part_ml + (((int64_t)r * H + head) * nsplit + sp) * 2;
+      pm[0] = m;
+      pm[1] = l;
+    }
+  }
+}
+
 __global__ __launch_bounds__(128) void mla_reduce_kernel(const float* __restrict__ part_o,
                                                          const float* __restrict__ part_ml,
                                                          const int* __restrict__ row_len, int H, int nsplit,
@@ -226,6 +433,26 @@ __global__ __launch_bounds__(128) void mla_reduce_kernel(const float* __restrict
 
 }  // namespace
 
+// v2 waves per workgroup for H = 128: 8 (all heads, 2 waves/SIMD, register
+// budget 256) or 4 (two 64-head workgroups, 1 wave/SIMD, 512 registers);
+// LLMD_MLA_NW overrides.
+extern "C" int llmd_mla_v2_waves() {
+  static const int nw = [] {
+    const char* e = getenv("LLMD_MLA_NW");
+    return (e && e[0] == '4') ? 4 : 8;
+  }();
+  return nw;
+}
+
+// v2 (64-head groups per workgroup) for 64 or 128 heads; LLMD_MLA_V1=1 forces v1
+extern "C" int llmd_mla_uses_v2(int H) {
+  static const int force_v1 = [] {
+    const char* e = getenv("LLMD_MLA_V1");
+    return e && e[0] == '1';
+  }();
+  return !force_v1 && (H == 64 || H == 128);
+}
+
 extern "C" int llmd_mla_attention(const void* q, int64_t q_row_stride, const void* kc, int64_t block_stride,
                                   int bs, const int* block_tables, int bt_stride, const int* row_seq,
                                   const int* row_len, int R, int H, float scale, int split_size, int nsplit,
@@ -240,10 +467,25 @@ extern "C" int llmd_mla_attention(const void* q, int64_t q_row_stride, const voi
     attr_done = true;
   }
   const float scale_log2 = scale * 1.4426950408889634f;
-  dim3 grid(nsplit, (H + 15) / 16, R);
-  hipLaunchKernelGGL(mla_kernel, grid, dim3(NT), lds, st, (const uint16_t*)q, q_row_stride,
-                     (const uint16_t*)kc, block_stride, bs, block_tables, bt_stride, row_seq, row_len, H,
-                     scale_log2, split_size, nsplit, (uint16_t*)out, out_row_stride, part_o, part_ml);
+  if (llmd_mla_uses_v2(H)) {
+#define V2(NW, BIG)                                                                                            \
+  hipLaunchKernelGGL((mla_v2_kernel<NW, BIG>), dim3(nsplit, H / (16 * NW), R), dim3(64 * NW), 0, st,          \
+                     (const uint16_t*)q,                                                                        \
+                     q_row_stride, (const uint16_t*)kc, block_stride, bs, block_tables, bt_stride, row_seq,   \
+                     row_len, H, scale_log2, split_size, nsplit, (uint16_t*)out, out_row_stride, part_o, part_ml)
+    const bool big = bs >= 64;
+    if (H == 128 && llmd_mla_v2_waves() == 8) {
+      if (big) V2(8, true); else V2(8, false);
+    } else {
+      if (big) V2(4, true); else V2(4, false);
+    }
+#undef V2
+  } else {
+    dim3 grid(nsplit, (H + 15) / 16, R);
+    hipLaunchKernelGGL(mla_kernel, grid, dim3(NT), lds, st, (const uint16_t*)q, q_row_stride,
+                       (const uint16_t*)kc, block_stride, bs, block_tables, bt_stride, row_seq, row_len, H,
+                       scale_log2, split_size, nsplit, (uint16_t*)out, out_row_stride, part_o, part_ml);
+  }
   if (nsplit > 1) {
     hipLaunchKernelGGL(mla_reduce_kernel, dim3(H, R), dim3(128), 0, st, part_o, part_ml, row_len, H, nsplit,
                        split_size, (uint16_t*)out, out_row_stride);

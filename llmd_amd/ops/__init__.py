@@ -420,7 +420,17 @@ def moe_experts(x, ids, wts, w1, w2, act=0, alpha=1.702, limit=7.0, out=None, b1
 
 
 def mla_split_plan(max_len: int, rows: int, H: int, num_cus: int = 256) -> tuple[int, int]:
-    """(split_size, nsplit) so rows x head-groups x splits fills ~2 WGs per CU."""
+    """(split_size, nsplit) so rows x head-groups x splits fills ~2 WGs per CU
+    (the v2 kernel runs all 64/128 heads of a row in one workgroup)."""
+    v2 = H in (64, 128) and os.environ.get("LLMD_MLA_V1", "0") != "1"
+    if v2:
+        # one 147 KB-LDS workgroup per CU; a split re-loads the row's 128-head Q
+        # (147 KB), so keep >= 4 tiles per split (scripts/bench_mla_split.py sweep:
+        # rows 1/8/32/64/128 at ctx 4096 best at 256/256/512/1024/2048 keys)
+        groups = 1 if (H == 64 or os.environ.get("LLMD_MLA_NW", "8") != "4") else 2
+        want = max(1, min(math.ceil(max_len / 256), math.ceil(num_cus / max(1, rows * groups))))
+        split = max(64, math.ceil(math.ceil(max_len / want) / 64) * 64)
+        return split, math.ceil(max(1, max_len) / split)
     base = max(1, rows * ((H + 15) // 16))
     target = 2 * num_cus
     want = max(1, min(math.ceil(max_len / 64), math.ceil(target / base)))

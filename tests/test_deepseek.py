@@ -121,7 +121,8 @@ def test_deepseek_hf_roundtrip_and_tp_ep_specs(tmp_path):
 def test_mla_kernel_matches_reference():
     torch.manual_seed(0)
     dev = "cuda"
-    for H, lens, bs in ((20, [1, 63, 64, 65, 300], 16), (128, [1000, 4096, 7], 64), (16, [2500], 64)):
+    for H, lens, bs in ((20, [1, 63, 64, 65, 300], 16), (128, [1000, 4096, 7], 64), (16, [2500], 64),
+                      (128, [1, 65, 300], 16), (64, [777, 64, 129], 64)):
         nb_per = max(math.ceil(L / bs) for L in lens)
         nseq = len(lens)
         nb = nseq * nb_per + 3
