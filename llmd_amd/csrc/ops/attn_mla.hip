@@ -18,6 +18,7 @@
 // nsplit > 1 writes unnormalised partials (O, max, sum in log2 units) merged
 // by mla_reduce_kernel.
 #include <cstdlib>
+#include <type_traits>
 
 #include "llmd_common.h"
 
@@ -36,12 +37,15 @@ constexpr float NEG_INF = -__builtin_huge_valf();
 
 __device__ __forceinline__ int rowoff(int g) { return 4 * (g >> 1) + 8 * (g & 1); }
 
+template <bool F8>
 __global__ __launch_bounds__(NT, 1) void mla_kernel(
-    const uint16_t* __restrict__ q, int64_t q_row_stride, const uint16_t* __restrict__ kc,
+    const uint16_t* __restrict__ q, int64_t q_row_stride, const void* __restrict__ kcv,
     int64_t block_stride, int bs, const int* __restrict__ block_tables, int bt_stride,
     const int* __restrict__ row_seq, const int* __restrict__ row_len, int H, float scale_log2,
     int split_size, int nsplit, uint16_t* __restrict__ out, int64_t out_row_stride,
-    float* __restrict__ part_o, float* __restrict__ part_ml) {
+    float* __restrict__ part_o, float* __restrict__ part_ml, float kv_scale) {
+  // fp8 (e4m3fn) latent caches: 8-B loads widened to bf16 when written to LDS
+  using CR = typename std::conditional<F8, u32x2_t, u32x4_t>::type;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   char* ktile = smem;
   char* pimg = smem + KTILE;
@@ -69,7 +73,7 @@ __global__ __launch_bounds__(NT, 1) void mla_kernel(
       if (head < H) v = *reinterpret_cast<const u32x4_t*>(qr + 32 * s + 8 * g);
       qf[s] = __builtin_bit_cast(bf16x8_t, v);
     }
-    u32x4_t kr[LPT];
+    CR kr[LPT];
     const int lbs = __builtin_ctz(bs);  // power-of-two block size (checked on the host)
     auto load_tile = [&](int ts) {
 #pragma unroll
@@ -79,7 +83,11 @@ __global__ __launch_bounds__(NT, 1) void mla_kernel(
         int key = ts + row;
         key = key < k1 ? key : k1 - 1;
         const int64_t off = (int64_t)bt[key >> lbs] * block_stride + (int64_t)(key & (bs - 1)) * DQK + ch * 8;
-        kr[i] = *reinterpret_cast<const u32x4_t*>(kc + off);
+        if constexpr (F8) {
+          kr[i] = *reinterpret_cast<const u32x2_t*>(reinterpret_cast<const uint8_t*>(kcv) + off);
+        } else {
+          kr[i] = *reinterpret_cast<const u32x4_t*>(reinterpret_cast<const uint16_t*>(kcv) + off);
+        }
       }
     };
     load_tile(k0);
@@ -89,7 +97,11 @@ __global__ __launch_bounds__(NT, 1) void mla_kernel(
       for (int i = 0; i < LPT; ++i) {
         const int idx = threadIdx.x + NT * i;
         const int row = idx / CPR, ch = idx % CPR;
-        *reinterpret_cast<u32x4_t*>(ktile + row * ROWB + ch * 16) = kr[i];
+        if constexpr (F8) {
+          *reinterpret_cast<u32x4_t*>(ktile + row * ROWB + ch * 16) = fp8x8_to_bf16x8(kr[i]);
+        } else {
+          *reinterpret_cast<u32x4_t*>(ktile + row * ROWB + ch * 16) = kr[i];
+        }
       }
       __syncthreads();
       if (ts + 64 < k1) load_tile(ts + 64);
@@ -169,7 +181,7 @@ __global__ __launch_bounds__(NT, 1) void mla_kernel(
   }
   // ---- epilogue: O rows are heads 4g + i (stats in lane 4g + i), columns dims
   if (nsplit == 1) {
-    const float inv = l > 0.f ? 1.f / l : 0.f;
+    const float inv = l > 0.f ? kv_scale / l : 0.f;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const float f = __shfl(inv, 4 * g + i, 64);
@@ -187,7 +199,7 @@ __global__ __launch_bounds__(NT, 1) void mla_kernel(
       if (hh < H) {
         float* po = part_o + (((int64_t)r * H + hh) * nsplit + sp) * DV + 128 * w;
 #pragma unroll
-        for (int n = 0; n < 8; ++n) po[16 * n + c16] = o[n][i];
+        for (int n = 0; n < 8; ++n) po[16 * n + c16] = o[n][i] * kv_scale;
       }
     }
     if (w == 0 && g == 0 && head < H) {
@@ -221,15 +233,23 @@ constexpr int V2_UNITS = 64 * CPR;        // 4608 16-B slots = 72 DMA wave-instr
 
 __device__ __forceinline__ int mla_swz(int r) { return (r & 2) | ((r >> 1) & 4); }
 
-template <int NW, bool BIG>
+// fp8 (e4m3fn) latent caches (F8): one bf16 tile + two 36,864-B fp8 staging
+// buffers (same 147,456 B of LDS). The DMA fills the next staging buffer
+// lane-linearly (unswizzled) while all threads widen the current one into the
+// swizzled bf16 tile; K/V dequant (x kv_scale) is folded into the softmax
+// scale and the output normalisation.
+constexpr int V2_STAGE = 64 * DQK;        // fp8 tile bytes
+
+template <int NW, bool BIG, bool F8>
 __global__ __launch_bounds__(64 * NW, 1) void mla_v2_kernel(
-    const uint16_t* __restrict__ q, int64_t q_row_stride, const uint16_t* __restrict__ kc,
+    const uint16_t* __restrict__ q, int64_t q_row_stride, const void* __restrict__ kcv,
     int64_t block_stride, int bs, const int* __restrict__ block_tables, int bt_stride,
     const int* __restrict__ row_seq, const int* __restrict__ row_len, int H, float scale_log2,
     int split_size, int nsplit, uint16_t* __restrict__ out, int64_t out_row_stride,
-    float* __restrict__ part_o, float* __restrict__ part_ml) {
+    float* __restrict__ part_o, float* __restrict__ part_ml, float kv_scale) {
   __shared__ __attribute__((aligned(1024))) char buf0[V2_TILE];
   __shared__ __attribute__((aligned(1024))) char buf1[V2_TILE];
+  const uint16_t* kc = reinterpret_cast<const uint16_t*>(kcv);
   const int sp = blockIdx.x, r = blockIdx.z;
   const int len = row_len[r];
   const int k0 = sp * split_size, k1 = min(len, k0 + split_size);
@@ -365,6 +385,47 @@ __global__ __launch_bounds__(64 * NW, 1) void mla_v2_kernel(
       }
     };
     const int nt = (k1 - k0 + 63) >> 6;
+    if constexpr (F8) {
+      const uint8_t* k8 = reinterpret_cast<const uint8_t*>(kcv);
+      // 64 rows x 36 16-B units = 36 wave-instructions, unswizzled rows of 576 B
+      auto issue8 = [&](char* base, int ts) {
+        int64_t tile_off = 0;
+        if constexpr (BIG) tile_off = (int64_t)bt[ts >> lbs] * block_stride + (int64_t)(ts & (bs - 1)) * DQK;
+#pragma unroll
+        for (int k = 0; k < (36 + NW - 1) / NW; ++k) {
+          const int j = w + NW * k;
+          if (j < 36) {
+            const int u = 64 * j + lane;
+            const int row = u / 36, c = u - row * 36;
+            const int key = min(ts + row, k1 - 1);
+            int64_t off;
+            if constexpr (BIG) {
+              off = tile_off + (int64_t)(key - ts) * DQK;
+            } else {
+              off = (int64_t)bt[key >> lbs] * block_stride + (int64_t)(key & (bs - 1)) * DQK;
+            }
+            __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)(k8 + off + c * 16),
+                                             (void __attribute__((address_space(3)))*)(base + 1024 * j), 16, 0, 0);
+          }
+        }
+      };
+      issue8(buf1, k0);
+      for (int t = 0; t < nt; ++t) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();  // stage t landed; tile of t-1 fully consumed
+        if (t + 1 < nt) issue8(buf1 + ((t + 1) & 1) * V2_STAGE, k0 + 64 * (t + 1));
+        const char* st8 = buf1 + (t & 1) * V2_STAGE;
+#pragma unroll
+        for (int i = 0; i < 72 / NW; ++i) {
+          const int v = threadIdx.x + 64 * NW * i;
+          const int row = v / CPR, ch = v - row * CPR;
+          const u32x2_t f = *reinterpret_cast<const u32x2_t*>(st8 + row * DQK + ch * 8);
+          *reinterpret_cast<u32x4_t*>(buf0 + row * V2_ROWB + 16 * (ch ^ mla_swz(row))) = fp8x8_to_bf16x8(f);
+        }
+        __syncthreads();
+        compute(buf0, k0 + 64 * t);
+      }
+    } else {
     issue(buf0, k0);
     for (int t = 0; t < nt; t += 2) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -377,10 +438,11 @@ __global__ __launch_bounds__(64 * NW, 1) void mla_v2_kernel(
       if (t + 2 < nt) issue(buf0, k0 + 64 * (t + 2));
       compute(buf1, k0 + 64 * (t + 1));
     }
+    }
   }
   // ---- epilogue: O rows are heads 16w + 4g + i (stats in lane 4g + i), columns dims 16n + c16
   if (nsplit == 1) {
-    const float inv = l > 0.f ? 1.f / l : 0.f;
+    const float inv = l > 0.f ? kv_scale / l : 0.f;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const float f = __shfl(inv, 4 * g + i, 64);
@@ -393,7 +455,7 @@ __global__ __launch_bounds__(64 * NW, 1) void mla_v2_kernel(
     for (int i = 0; i < 4; ++i) {
       float* po = part_o + (((int64_t)r * H + h0 + 4 * g + i) * nsplit + sp) * DV;
 #pragma unroll
-      for (int n = 0; n < 32; ++n) po[16 * n + c16] = o[n][i];
+      for (int n = 0; n < 32; ++n) po[16 * n + c16] = o[n][i] * kv_scale;
     }
     if (g == 0) {
       float* pm = part_ml + (((int64_t)r * H + head) * nsplit + sp) * 2;
@@ -456,35 +518,49 @@ extern "C" int llmd_mla_uses_v2(int H) {
 extern "C" int llmd_mla_attention(const void* q, int64_t q_row_stride, const void* kc, int64_t block_stride,
                                   int bs, const int* block_tables, int bt_stride, const int* row_seq,
                                   const int* row_len, int R, int H, float scale, int split_size, int nsplit,
-                                  void* out, int64_t out_row_stride, float* part_o, float* part_ml,
-                                  hipStream_t st) {
+                                  void* out, int64_t out_row_stride, float* part_o, float* part_ml, int fp8,
+                                  float kv_scale, hipStream_t st) {
   if (R == 0) return 0;
   if (split_size % 64 != 0 || nsplit < 1) return -1;
   const size_t lds = KTILE + PIMG + 128 * sizeof(float);
   static bool attr_done = false;
   if (!attr_done) {
-    hipFuncSetAttribute((const void*)mla_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    (void)hipFuncSetAttribute((const void*)mla_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    (void)hipFuncSetAttribute((const void*)mla_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     attr_done = true;
   }
-  const float scale_log2 = scale * 1.4426950408889634f;
+  const float scale_log2 = scale * kv_scale * 1.4426950408889634f;
   if (llmd_mla_uses_v2(H)) {
-#define V2(NW, BIG)                                                                                            \
-  hipLaunchKernelGGL((mla_v2_kernel<NW, BIG>), dim3(nsplit, H / (16 * NW), R), dim3(64 * NW), 0, st,          \
-                     (const uint16_t*)q,                                                                        \
-                     q_row_stride, (const uint16_t*)kc, block_stride, bs, block_tables, bt_stride, row_seq,   \
-                     row_len, H, scale_log2, split_size, nsplit, (uint16_t*)out, out_row_stride, part_o, part_ml)
+#define V2(NW, BIG, F8)                                                                                        \
+  hipLaunchKernelGGL((mla_v2_kernel<NW, BIG, F8>), dim3(nsplit, H / (16 * NW), R), dim3(64 * NW), 0, st,      \
+                     (const uint16_t*)q, q_row_stride, kc, block_stride, bs, block_tables, bt_stride, row_seq, \
+                     row_len, H, scale_log2, split_size, nsplit, (uint16_t*)out, out_row_stride, part_o, part_ml, \
+                     kv_scale)
+#define V2NW(NW)                                   \
+  if (fp8) {                                       \
+    if (big) V2(NW, true, true); else V2(NW, false, true);   \
+  } else {                                         \
+    if (big) V2(NW, true, false); else V2(NW, false, false); \
+  }
     const bool big = bs >= 64;
     if (H == 128 && llmd_mla_v2_waves() == 8) {
-      if (big) V2(8, true); else V2(8, false);
+      V2NW(8)
     } else {
-      if (big) V2(4, true); else V2(4, false);
+      V2NW(4)
     }
+#undef V2NW
 #undef V2
   } else {
     dim3 grid(nsplit, (H + 15) / 16, R);
-    hipLaunchKernelGGL(mla_kernel, grid, dim3(NT), lds, st, (const uint16_t*)q, q_row_stride,
-                       (const uint16_t*)kc, block_stride, bs, block_tables, bt_stride, row_seq, row_len, H,
-                       scale_log2, split_size, nsplit, (uint16_t*)out, out_row_stride, part_o, part_ml);
+    if (fp8) {
+      hipLaunchKernelGGL(mla_kernel<true>, grid, dim3(NT), lds, st, (const uint16_t*)q, q_row_stride, kc,
+                         block_stride, bs, block_tables, bt_stride, row_seq, row_len, H, scale_log2, split_size,
+                         nsplit, (uint16_t*)out, out_row_stride, part_o, part_ml, kv_scale);
+    } else {
+      hipLaunchKernelGGL(mla_kernel<false>, grid, dim3(NT), lds, st, (const uint16_t*)q, q_row_stride, kc,
+                         block_stride, bs, block_tables, bt_stride, row_seq, row_len, H, scale_log2, split_size,
+                         nsplit, (uint16_t*)out, out_row_stride, part_o, part_ml, kv_scale);
+    }
   }
   if (nsplit > 1) {
     hipLaunchKernelGGL(mla_reduce_kernel, dim3(H, R), dim3(128), 0, st, part_o, part_ml, row_len, H, nsplit,
@@ -498,11 +574,12 @@ extern "C" int llmd_mla_attention(const void* q, int64_t q_row_stride, const voi
 //   q_lat[t, h, 512:576] = rope(q[t, h, 128:192])   (GPT-J interleaved pairs)
 //   cache[slot] = [kv_c[t] (512) | rope(k_pe[t]) (64)]
 namespace {
+template <bool F8>
 __global__ __launch_bounds__(256) void mla_rope_cache_kernel(
     const uint16_t* __restrict__ q, int64_t q_stride, uint16_t* __restrict__ q_lat, int64_t ql_stride,
     const uint16_t* __restrict__ kv_c, int64_t kvc_stride, const uint16_t* __restrict__ k_pe,
     int64_t kpe_stride, const int64_t* __restrict__ positions, const float* __restrict__ cos_sin, int H,
-    const int64_t* __restrict__ slots, uint16_t* __restrict__ cache, int64_t block_stride, int bs) {
+    const int64_t* __restrict__ slots, void* __restrict__ cache, int64_t block_stride, int bs, float kv_inv) {
   const int t = blockIdx.x;
   const float* cs = cos_sin + positions[t] * 64;
   // q_pe: H heads x 32 pairs
@@ -517,7 +594,35 @@ __global__ __launch_bounds__(256) void mla_rope_cache_kernel(
   }
   const int64_t slot = slots[t];
   if (slot < 0) return;
-  uint16_t* row = cache + (slot / bs) * block_stride + (slot % bs) * 576;
+  const int64_t roff = (slot / bs) * block_stride + (slot % bs) * 576;  // elements
+  if constexpr (F8) {  // stored as saturate(x / kv_scale), 8 elements per thread
+    uint8_t* row8 = reinterpret_cast<uint8_t*>(cache) + roff;
+    const int i = threadIdx.x;
+    float f[8];
+    if (i < 64) {
+      const u32x4_t v = reinterpret_cast<const u32x4_t*>(kv_c + (int64_t)t * kvc_stride)[i];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        f[2 * j] = __uint_as_float(v[j] << 16) * kv_inv;
+        f[2 * j + 1] = __uint_as_float(v[j] & 0xffff0000u) * kv_inv;
+      }
+      *reinterpret_cast<u32x2_t*>(row8 + 8 * i) = f32x8_to_fp8(f);
+    } else if (i < 72) {
+      const int p0 = 4 * (i - 64);  // pairs p0 .. p0+3
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int p = p0 + j;
+        const uint16_t* src = k_pe + (int64_t)t * kpe_stride + 2 * p;
+        const float x0 = bf2f(src[0]), x1 = bf2f(src[1]);
+        const float c = cs[p], s = cs[32 + p];
+        f[2 * j] = (x0 * c - x1 * s) * kv_inv;
+        f[2 * j + 1] = (x0 * s + x1 * c) * kv_inv;
+      }
+      *reinterpret_cast<u32x2_t*>(row8 + 512 + 2 * p0) = f32x8_to_fp8(f);
+    }
+    return;
+  }
+  uint16_t* row = reinterpret_cast<uint16_t*>(cache) + roff;
   for (int i = threadIdx.x; i < 512 / 8; i += 256)
     reinterpret_cast<u32x4_t*>(row)[i] = reinterpret_cast<const u32x4_t*>(kv_c + (int64_t)t * kvc_stride)[i];
   if (threadIdx.x < 32) {
@@ -534,10 +639,13 @@ __global__ __launch_bounds__(256) void mla_rope_cache_kernel(
 extern "C" int llmd_mla_rope_cache(const void* q, int64_t q_stride, void* q_lat, int64_t ql_stride, const void* kv_c,
                                    int64_t kvc_stride, const void* k_pe, int64_t kpe_stride, const int64_t* positions,
                                    const float* cos_sin, int T, int H, const int64_t* slots, void* cache,
-                                   int64_t block_stride, int bs, hipStream_t st) {
+                                   int64_t block_stride, int bs, int fp8, float kv_inv, hipStream_t st) {
   if (T == 0) return 0;
-  hipLaunchKernelGGL(mla_rope_cache_kernel, dim3(T), dim3(256), 0, st, (const uint16_t*)q, q_stride,
-                     (uint16_t*)q_lat, ql_stride, (const uint16_t*)kv_c, kvc_stride, (const uint16_t*)k_pe,
-                     kpe_stride, positions, cos_sin, H, slots, (uint16_t*)cache, block_stride, bs);
+#define RC(F8)                                                                                                 \
+  hipLaunchKernelGGL(mla_rope_cache_kernel<F8>, dim3(T), dim3(256), 0, st, (const uint16_t*)q, q_stride,      \
+                     (uint16_t*)q_lat, ql_stride, (const uint16_t*)kv_c, kvc_stride, (const uint16_t*)k_pe,   \
+                     kpe_stride, positions, cos_sin, H, slots, cache, block_stride, bs, kv_inv)
+  if (fp8) RC(true); else RC(false);
+#undef RC
   return (int)hipGetLastError();
 }

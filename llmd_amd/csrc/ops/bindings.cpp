@@ -37,9 +37,11 @@ int llmd_kvx_ipc_export(const void*, void*, int64_t*);
 int llmd_kvx_ipc_open(const void*, void**);
 int llmd_kvx_ipc_close(void*);
 int llmd_mla_attention(const void*, int64_t, const void*, int64_t, int, const int*, int, const int*,
-                       const int*, int, int, float, int, int, void*, int64_t, float*, float*, hipStream_t);
+                       const int*, int, int, float, int, int, void*, int64_t, float*, float*, int, float,
+                       hipStream_t);
 int llmd_mla_rope_cache(const void*, int64_t, void*, int64_t, const void*, int64_t, const void*, int64_t,
-                        const int64_t*, const float*, int, int, const int64_t*, void*, int64_t, int, hipStream_t);
+                        const int64_t*, const float*, int, int, const int64_t*, void*, int64_t, int, int, float,
+                        hipStream_t);
 int llmd_lora_bgmv(const void*, int64_t, const void*, const void*, int, int, int, int, const int*, float*, void*,
                    int64_t, hipStream_t);
 int llmd_skinny_gemm(const void*, int64_t, const void*, int64_t, int, int, int, int, void*, int64_t, float*,
@@ -225,9 +227,10 @@ void paged_decode(torch::Tensor out, torch::Tensor q, torch::Tensor k_cache, tor
 // out [R, H*512]; row r attends to keys [0, row_len[r]) of sequence row_seq[r].
 void mla_attention(torch::Tensor out, torch::Tensor q, torch::Tensor cache, torch::Tensor block_tables,
                    torch::Tensor row_seq, torch::Tensor row_len, int64_t H, double scale, int64_t split_size,
-                   int64_t nsplit, torch::Tensor part_o, torch::Tensor part_ml) {
+                   int64_t nsplit, torch::Tensor part_o, torch::Tensor part_ml, double kv_scale) {
   const c10::hip::OptionalHIPGuard device_guard(dev_of(out));
-  CHECK_CUDA(q); CHECK_BF16(q); CHECK_BF16(out); CHECK_BF16(cache); CHECK_INNER(q); CHECK_INNER(out);
+  CHECK_CUDA(q); CHECK_BF16(q); CHECK_BF16(out); CHECK_INNER(q); CHECK_INNER(out);
+  const bool f8 = is_fp8_cache(cache);
   CHECK_DT(block_tables, at::kInt); CHECK_DT(row_seq, at::kInt); CHECK_DT(row_len, at::kInt);
   TORCH_CHECK(cache.dim() == 3 && cache.size(2) == 576 && cache.stride(2) == 1 && cache.stride(1) == 576,
               "mla cache [blocks, bs, 576] with contiguous rows");
@@ -247,15 +250,18 @@ void mla_attention(torch::Tensor out, torch::Tensor q, torch::Tensor cache, torc
                               block_tables.data_ptr<int>(), block_tables.stride(0), row_seq.data_ptr<int>(),
                               row_len.data_ptr<int>(), R, H, (float)scale, split_size, nsplit, out.data_ptr(),
                               out.stride(0), nsplit > 1 ? part_o.data_ptr<float>() : nullptr,
-                              nsplit > 1 ? part_ml.data_ptr<float>() : nullptr, cur_stream());
+                              nsplit > 1 ? part_ml.data_ptr<float>() : nullptr, f8 ? 1 : 0, (float)kv_scale,
+                              cur_stream());
   TORCH_CHECK(rc == 0, "mla_attention failed: ", rc);
 }
 
 void mla_rope_cache(torch::Tensor q, torch::Tensor q_lat, torch::Tensor kv_c, torch::Tensor k_pe,
                     torch::Tensor positions, torch::Tensor cos_sin, int64_t H, torch::Tensor slots,
-                    torch::Tensor cache) {
+                    torch::Tensor cache, double kv_scale) {
   const c10::hip::OptionalHIPGuard device_guard(dev_of(q));
-  CHECK_CUDA(q); CHECK_BF16(q); CHECK_BF16(q_lat); CHECK_BF16(kv_c); CHECK_BF16(k_pe); CHECK_BF16(cache);
+  CHECK_CUDA(q); CHECK_BF16(q); CHECK_BF16(q_lat); CHECK_BF16(kv_c); CHECK_BF16(k_pe);
+  const bool f8 = is_fp8_cache(cache);
+  TORCH_CHECK(kv_scale > 0, "mla_rope: kv_scale must be positive");
   CHECK_INNER(q); CHECK_INNER(q_lat); CHECK_INNER(kv_c); CHECK_INNER(k_pe);
   CHECK_DT(positions, at::kLong); CHECK_DT(slots, at::kLong); CHECK_DT(cos_sin, at::kFloat);
   const int T = q.size(0);
@@ -269,7 +275,7 @@ void mla_rope_cache(torch::Tensor q, torch::Tensor q_lat, torch::Tensor kv_c, to
   int rc = llmd_mla_rope_cache(q.data_ptr(), q.stride(0), q_lat.data_ptr(), q_lat.stride(0), kv_c.data_ptr(),
                                kv_c.stride(0), k_pe.data_ptr(), k_pe.stride(0), positions.data_ptr<int64_t>(),
                                cos_sin.data_ptr<float>(), T, H, slots.data_ptr<int64_t>(), cache.data_ptr(),
-                               cache.stride(0), cache.size(1), cur_stream());
+                               cache.stride(0), cache.size(1), f8 ? 1 : 0, (float)(1.0 / kv_scale), cur_stream());
   TORCH_CHECK(rc == 0, "mla_rope_cache failed: ", rc);
 }
 

@@ -97,8 +97,6 @@ class ModelRunner:
         if kvd in ("auto", "bf16", "bfloat16"):
             self.kv_dtype = torch.bfloat16
         elif kvd in ("fp8", "fp8_e4m3", "fp8_e4m3fn"):
-            if self.is_mla:
-                raise NotImplementedError("fp8 KV cache is not supported for MLA (latent) caches yet")
             self.kv_dtype = torch.float8_e4m3fn
         else:
             raise ValueError(f"unsupported --kv-cache-dtype {cfg.cache.kv_cache_dtype}")

@@ -69,6 +69,7 @@ class MLAAttention(torch.nn.Module):
         self.scale = (NOPE + ROPE) ** -0.5 * yarn_softmax_mscale(cfg.rope_scaling)
         self.cos_sin = cos_sin
         self.cache = None
+        self.kv_scale = 1.0  # latent-cache dequant scale (fp8 e4m3fn caches; 1.0 unless calibrated)
         # attributes the runner reads for generic bookkeeping
         self.Hq, self.Hkv, self.D, self.window, self.sinks = self.H, 1, KV_LORA + ROPE, 0, None
 
@@ -89,7 +90,7 @@ class MLAAttention(torch.nn.Module):
         kv_c = self.kv_a_norm(kv[:, :KV_LORA])
         q_lat = torch.empty(T, H * (KV_LORA + ROPE), dtype=x.dtype, device=x.device)
         ops.mla_rope_cache(q, q_lat, kv_c, kv[:, KV_LORA:], meta.positions, self.cos_sin, H,
-                           meta.slot_mapping, self.cache)
+                           meta.slot_mapping, self.cache, kv_scale=self.kv_scale)
         qn = q.view(T, H, NOPE + ROPE)[:, :, :NOPE].transpose(0, 1)                    # [H, T, 128]
         q_lat.view(T, H, KV_LORA + ROPE)[:, :, :KV_LORA].copy_(torch.bmm(qn, self.w_uk()).transpose(0, 1))
         o_lat = torch.empty(T, H * KV_LORA, dtype=x.dtype, device=x.device)
@@ -97,10 +98,10 @@ class MLAAttention(torch.nn.Module):
         if nd:
             ops.mla_attention(q_lat[:nd], self.cache, meta.d_block_tables, meta.mla_d_rows, meta.d_seq_lens, H,
                               self.scale, max_len=meta.d_max_ctx, split=meta.mla_split, out=o_lat[:nd],
-                              workspace=meta.mla_workspace)
+                              workspace=meta.mla_workspace, kv_scale=self.kv_scale)
         if meta.num_prefill_tokens:
             ops.mla_attention(q_lat[nd:], self.cache, meta.p_block_tables, meta.p_row_seq, meta.p_row_len, H,
-                              self.scale, max_len=meta.p_max_ctx, out=o_lat[nd:])
+                              self.scale, max_len=meta.p_max_ctx, out=o_lat[nd:], kv_scale=self.kv_scale)
         o = torch.bmm(o_lat.view(T, H, KV_LORA).transpose(0, 1), self.w_uv_t())          # [H, T, 128]
         return self.o_proj(o.transpose(0, 1).reshape(T, H * VDIM))
 

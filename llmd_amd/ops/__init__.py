@@ -439,11 +439,12 @@ def mla_split_plan(max_len: int, rows: int, H: int, num_cus: int = 256) -> tuple
 
 
 def mla_attention(q, cache, block_tables, row_seq, row_len, H, scale, max_len=None, split=None, out=None,
-                  workspace=None):
+                  workspace=None, kv_scale=1.0):
     """Absorbed-MLA attention over the paged latent cache (csrc/ops/attn_mla.hip).
-    q [R, H*576] bf16, cache [blocks, bs, 576] -> out [R, H*512]."""
+    q [R, H*576] bf16, cache [blocks, bs, 576] bf16 or fp8 e4m3fn (dequant
+    x kv_scale) -> out [R, H*512]."""
     if not _gpu(q):
-        r = ref.mla_attention(q, cache, block_tables, row_seq, row_len, H, scale)
+        r = ref.mla_attention(q, cache, block_tables, row_seq, row_len, H, scale, kv_scale)
         if out is not None:
             out.copy_(r)
             return out
@@ -465,15 +466,16 @@ def mla_attention(q, cache, block_tables, row_seq, row_len, H, scale, max_len=No
     else:
         part_o = part_ml = out.new_empty(0, dtype=torch.float32)
     native().mla_attention(out, q, cache, block_tables, row_seq, row_len, H, scale, split_size, nsplit,
-                           part_o, part_ml)
+                           part_o, part_ml, kv_scale)
     return out
 
 
-def mla_rope_cache(q, q_lat, kv_c, k_pe, positions, cos_sin, H, slots, cache):
-    """RoPE q_pe into q_lat[..., 512:] and write [kv_c | rope(k_pe)] to the latent cache."""
+def mla_rope_cache(q, q_lat, kv_c, k_pe, positions, cos_sin, H, slots, cache, kv_scale=1.0):
+    """RoPE q_pe into q_lat[..., 512:] and write [kv_c | rope(k_pe)] to the latent
+    cache (fp8 e4m3fn caches store saturate(x / kv_scale))."""
     if not _gpu(q):
-        return ref.mla_rope_cache(q, q_lat, kv_c, k_pe, positions, cos_sin, H, slots, cache)
-    native().mla_rope_cache(q, q_lat, kv_c, k_pe, positions, cos_sin, H, slots, cache)
+        return ref.mla_rope_cache(q, q_lat, kv_c, k_pe, positions, cos_sin, H, slots, cache, kv_scale)
+    native().mla_rope_cache(q, q_lat, kv_c, k_pe, positions, cos_sin, H, slots, cache, kv_scale)
 
 
 def lora_bgmv(y, x, A, B, slot, h=None):

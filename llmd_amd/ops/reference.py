@@ -250,7 +250,7 @@ def yarn_softmax_mscale(sc: dict | None) -> float:
     return m * m
 
 
-def mla_rope_cache(q, q_lat, kv_c, k_pe, positions, cos_sin, H, slots, cache):
+def mla_rope_cache(q, q_lat, kv_c, k_pe, positions, cos_sin, H, slots, cache, kv_scale=1.0):
     """q [T, H*192] (nope 128 | pe 64) -> q_lat[:, h*576+512:+64] = rope(q_pe);
     cache.view(-1, 576)[slot] = [kv_c | rope(k_pe)] (GPT-J interleaved pairs)."""
     T = q.shape[0]
@@ -267,7 +267,7 @@ def mla_rope_cache(q, q_lat, kv_c, k_pe, positions, cos_sin, H, slots, cache):
     q_lat.view(T, H, 576)[:, :, 512:] = rot(qp).to(q_lat.dtype)
     bs = cache.shape[1]
     ok = slots >= 0
-    row = torch.cat([kv_c.float(), rot(k_pe)], -1).to(cache.dtype)
+    row = to_cache(torch.cat([kv_c.float(), rot(k_pe)], -1), cache.dtype, kv_scale)
     sl = slots[ok].long()
     cache[sl // bs, sl % bs] = row[ok]
 
@@ -330,7 +330,7 @@ def moe_forward(x, ids, wts, w1, w2, act=0, alpha=1.702, limit=7.0, b1=None, b2=
     return out.to(x.dtype)
 
 
-def mla_attention(q, cache, block_tables, row_seq, row_len, H, scale):
+def mla_attention(q, cache, block_tables, row_seq, row_len, H, scale, kv_scale=1.0):
     """Absorbed MLA: q [R, H*576], cache [blocks, bs, 576] -> out [R, H*512]
     (value = first 512 dims of the cached latent)."""
     R = q.shape[0]
@@ -341,7 +341,7 @@ def mla_attention(q, cache, block_tables, row_seq, row_len, H, scale):
         L = int(row_len[r])
         bt = block_tables[int(row_seq[r])]
         idx = torch.arange(L, device=q.device)
-        kv = cache[bt[idx // bs].long(), idx % bs].float()  # [L, 576]
+        kv = cache[bt[idx // bs].long(), idx % bs].float() * kv_scale  # [L, 576]
         s = (qf[r] @ kv.T) * scale                           # [H, L]
         p = torch.softmax(s, -1)
         out[r] = p @ kv[:, :512]

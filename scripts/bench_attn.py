@@ -104,7 +104,7 @@ def mla(ctx, R, H, prefill=False, bs=64):
     nseq = 1 if prefill else R
     per = math.ceil(ctx / bs)
     nb = nseq * per + 1
-    cache = torch.randn(nb, bs, 576, device=dev, dtype=torch.bfloat16)
+    cache = torch.randn(nb, bs, 576, device=dev, dtype=torch.bfloat16).to(KV_DTYPE)
     bt = torch.stack([torch.randperm(nb - 1, device=dev)[:per] for _ in range(nseq)]).int()
     q = torch.randn(R, H * 576, device=dev, dtype=torch.bfloat16)
     if prefill:
@@ -118,9 +118,9 @@ def mla(ctx, R, H, prefill=False, bs=64):
     t = time_it(fn)
     keys = float(ln.sum().item())
     fl = 2 * H * keys * (576 + 512)
-    by = (nseq * ctx) * 576 * 2
+    by = (nseq * ctx) * 576 * cache.element_size()
     kind = "prefill" if prefill else "decode"
-    print(f"mla {kind} rows={R} ctx={ctx} H={H}: {t * 1e3:.3f} ms  {fl / t / 1e12:.1f} TF/s  "
+    print(f"mla {kind} rows={R} ctx={ctx} H={H} kv={cache.dtype}: {t * 1e3:.3f} ms  {fl / t / 1e12:.1f} TF/s  "
           f"{by / t / 1e9:.0f} GB/s latent read")
 
 

@@ -274,3 +274,66 @@ def test_fused_norm_act_quant_gpu(d):
         torch.testing.assert_close(sa.cpu(), sb, rtol=2e-2, atol=1e-6)
         deq, deq_r = qa.float().cpu() * sa.cpu(), qb.float() * sb
         assert (deq - deq_r).abs().max() <= 0.07 * deq_r.abs().max()
+
+
+# ---------------------------------------------------------------- fp8 latent (MLA) cache
+def test_engine_fp8_mla_kv_cpu():
+    """DeepSeek (MLA) with an fp8 latent cache runs end to end (CPU reference ops)."""
+    from llmd_amd.engine.config import EngineConfig
+    from llmd_amd.engine.engine import LLMEngine
+    from llmd_amd.engine.request import SamplingParams
+
+    outs = {}
+    for kvd in ("auto", "fp8"):
+        cfg = EngineConfig.create("tiny-deepseek", device="cpu", block_size=16, num_gpu_blocks=64,
+                                  max_num_batched_tokens=256, max_num_seqs=4, max_model_len=512,
+                                  kv_cache_dtype=kvd)
+        eng = LLMEngine(cfg, capture_graphs=False)
+        assert eng.runner.kv.dtype == (F8 if kvd == "fp8" else torch.bfloat16)
+        reqs = eng.generate([list(range(3, 40)), [7] * 20], SamplingParams(max_tokens=6, temperature=0.0,
+                                                                           ignore_eos=True))
+        outs[kvd] = [r.output_token_ids for r in reqs]
+    assert all(len(o) == 6 for o in outs["fp8"])
+    assert [o[0] for o in outs["fp8"]] == [o[0] for o in outs["auto"]]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("H,bs,lens", [(128, 64, [1000, 4096, 7]), (128, 16, [1, 65, 300]),
+                                       (64, 64, [777, 129]), (20, 16, [1, 63, 300])])
+def test_mla_fp8_cache_kernels(H, bs, lens):
+    """HIP rope+latent-cache write (fp8) and MLA attention (v2 for 64/128 heads,
+    v1 otherwise) vs the fp32 reference over the same fp8 cache."""
+    dev = "cuda"
+    torch.manual_seed(3)
+    ks = 0.5
+    nb_per = max(math.ceil(L / bs) for L in lens)
+    nb = len(lens) * nb_per + 3
+    pool = torch.zeros(nb, 2, bs, 576, dtype=F8, device=dev)  # non-contiguous layer view
+    cache = pool[:, 1]
+    cache.copy_(ref.to_cache(torch.randn(nb, bs, 576, device=dev) * 2, F8, ks))
+    bt = torch.stack([torch.randperm(nb, device=dev)[:nb_per] for _ in lens]).int()
+    R = len(lens)
+    q = torch.randn(R, H * 576, dtype=torch.bfloat16, device=dev)
+    rows = torch.arange(R, dtype=torch.int32, device=dev)
+    ln = torch.tensor(lens, dtype=torch.int32, device=dev)
+    want = ref.mla_attention(q, cache, bt, rows, ln, H, 576 ** -0.5, ks)
+    for split in (None, (64, math.ceil(max(lens) / 64))):
+        got = ops.mla_attention(q, cache, bt, rows, ln, H, 576 ** -0.5, split=split, kv_scale=ks)
+        _close(got, want)
+    # rope + fp8 latent write: HIP vs reference on the same inputs
+    T = 29
+    qf = torch.randn(T, H * 192, dtype=torch.bfloat16, device=dev)
+    kv = torch.randn(T, 576, dtype=torch.bfloat16, device=dev) * 3
+    pos = torch.randint(0, 4000, (T,), device=dev)
+    cs = ref.rope_cos_sin(64, 4096, 10000.0, device=dev)
+    slots = torch.randperm(8 * bs, device=dev)[:T]
+    slots[2] = -1
+    ca = torch.zeros(8, bs, 576, dtype=F8, device=dev)
+    cb = torch.zeros_like(ca)
+    qa = torch.zeros(T, H * 576, dtype=torch.bfloat16, device=dev)
+    qb = torch.zeros_like(qa)
+    ops.mla_rope_cache(qf, qa, kv[:, :512], kv[:, 512:], pos, cs, H, slots, ca, kv_scale=ks)
+    ref.mla_rope_cache(qf, qb, kv[:, :512], kv[:, 512:], pos, cs, H, slots, cb, ks)
+    _close(qa, qb, atol=2e-2, rtol=2e-2)
+    # fp8 codes may differ by one ulp where the bf16 -> fp32 rounding paths differ
+    _close(ca.float() * ks, cb.float() * ks, atol=0.07 * ks, rtol=0.07)
