@@ -16,6 +16,8 @@
 //     V image: XOR-swizzled rows, ds_read_b64_tr_b16 transposed reads
 // K/V tiles are double-buffered; the next tile's global loads are issued before
 // the current tile's MFMAs and written to LDS after the barrier (T14 split).
+#include <cstdlib>
+
 #include "llmd_common.h"
 
 using namespace llmd;
@@ -298,6 +300,241 @@ __global__ __launch_bounds__(NT, 2) void prefill_kernel(
   }
 }
 
+// ---------------------------------------------------------------- v2 (bf16 cache, D = 128, block >= 64)
+// Same work decomposition and math as prefill_kernel; the tiles move
+// global -> LDS with global_load_lds_dwordx4 (no VGPR staging, no ds_write),
+// one vmcnt + barrier per tile, double-buffered. Images are unpadded 256-B rows
+// with per-row XOR swizzles of the 16-B chunk, applied on the DMA source side:
+//   K: slot = c ^ pk(r), pk(r) = ((r >> 1) & 7) | ((r & 1) << 3): every
+//      ds_read_b128 lane group of the S^T A-operand reads covers 16 distinct
+//      16-B bank slots (rows {0-3,12-15} vs {4-11} at chunks 4s+g / 4s+g^1).
+//   V: slot = c ^ pv(r), pv(r) = 2 ((r & 3) | (((r >> 3) & 1) << 2)): the 32-lane
+//      ds_read_b64_tr_b16 groups (rows {0-3,8-11} / {4-7,12-15}, chunk pairs
+//      2n, 2n+1) hit 32 distinct 8-B slots.
+// All LDS reads are a per-lane register + an immediate (buffer, key block, dim block).
+constexpr int P2_IMG = 64 * 256;  // one 64-key x 128-dim bf16 image
+
+__device__ __forceinline__ int p2_pk(int r) { return ((r >> 1) & 7) | ((r & 1) << 3); }
+__device__ __forceinline__ int p2_pv(int r) { return 2 * ((r & 3) | (((r >> 3) & 1) << 2)); }
+
+__global__ __launch_bounds__(NT, 2) void prefill_v2_kernel(
+    const uint16_t* __restrict__ q, int64_t q_stride, const uint16_t* __restrict__ kc,
+    const uint16_t* __restrict__ vc, int64_t block_stride, int bs,
+    const int* __restrict__ block_tables, int bt_stride, const int* __restrict__ q_start,
+    const int* __restrict__ q_len, const int* __restrict__ ctx_len, const int* __restrict__ items,
+    int Hq, int Hkv, int G, int HPW, float scale_log2, int window,
+    const float* __restrict__ sinks, uint16_t* __restrict__ out, int64_t out_stride, float vscale) {
+  constexpr int D = 128, KS = 4, NB = 8;
+  __shared__ __attribute__((aligned(1024))) char buf0[2 * P2_IMG];  // K | V of even tiles
+  __shared__ __attribute__((aligned(1024))) char buf1[2 * P2_IMG];  // K | V of odd tiles
+
+  const int seq = items[2 * blockIdx.x], qb = items[2 * blockIdx.x + 1];
+  const int NHG = G / HPW;
+  const int kvh = blockIdx.y / NHG, hg = blockIdx.y % NHG;
+  const int TPW = 4 / HPW;
+  const int qs = q_start[seq], ql = q_len[seq], ctx = ctx_len[seq];
+  const int pbase = ctx - ql;
+  const int* bt = block_tables + (int64_t)seq * bt_stride;
+  const int64_t head_off = (int64_t)kvh * bs * D;
+  const int lbs = __builtin_ctz(bs);
+
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, g = lane >> 4, c16 = lane & 15;
+  const int head = kvh * G + hg * HPW + (w % HPW);
+  const int tok0 = qb + (w / HPW) * 32;
+  const int ntok = max(0, min(32, ql - tok0));
+  const int p_lo = pbase + tok0, p_hi = pbase + tok0 + max(ntok, 1) - 1;
+  const int wg_tok_end = min(ql, qb + 32 * TPW);
+  const int wg_p_lo = pbase + qb, wg_p_hi = pbase + wg_tok_end - 1;
+  const int kmin = window > 0 ? max(0, wg_p_lo - window + 1) : 0;
+  const int t_first = kmin >> 6, t_last = wg_p_hi >> 6;
+
+  bf16x8_t qf[2][KS];
+#pragma unroll
+  for (int nb = 0; nb < 2; ++nb) {
+    const int tk = tok0 + 16 * nb + c16;
+    const uint16_t* qr = q + (int64_t)(qs + tk) * q_stride + (int64_t)head * D;
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      u32x4_t v = {0, 0, 0, 0};
+      if (tk < ql) v = *reinterpret_cast<const u32x4_t*>(qr + (4 * s + g) * 8);
+      qf[nb][s] = __builtin_bit_cast(bf16x8_t, v);
+    }
+  }
+  float m[2] = {NEG_INF, NEG_INF}, lsum[2] = {0.f, 0.f};
+  f32x4_t o[2][NB];
+#pragma unroll
+  for (int nb = 0; nb < 2; ++nb)
+#pragma unroll
+    for (int n = 0; n < NB; ++n) o[nb][n] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  // DMA: 16 K + 16 V wave-instructions of 4 rows x 256 B; wave w issues j = w + 4i
+  auto issue = [&](char* base, int t) {
+    const int ts = t * 64;
+    const int64_t toff = (int64_t)bt[ts >> lbs] * block_stride + head_off + (int64_t)(ts & (bs - 1)) * D;
+    const int rlim = ctx - 1 - ts;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int j = w + 4 * i;
+      const int u = 64 * j + lane;
+      const int row = u >> 4, sl = u & 15;
+      const int64_t ro = toff + (int64_t)min(row, rlim) * D;
+      __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)(kc + ro + 8 * (sl ^ p2_pk(row))),
+                                       (void __attribute__((address_space(3)))*)(base + 1024 * j), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)(vc + ro + 8 * (sl ^ p2_pv(row))),
+                                       (void __attribute__((address_space(3)))*)(base + P2_IMG + 1024 * j), 16, 0,
+                                       0);
+    }
+  };
+  // per-lane LDS offsets (see the header): K rows 16 b4 + srow, chunk 4s + g;
+  // V rows 32 t2 + vrow (+16), chunk 2n + (pp >> 1), half pp & 1
+  const int qq = c16 >> 2, pp = c16 & 3;
+  const int srow = rowoff(c16 >> 2) + (c16 & 3), kp = p2_pk(srow);
+  int kofs[KS];
+#pragma unroll
+  for (int s = 0; s < KS; ++s) kofs[s] = srow * 256 + 16 * ((4 * s + g) ^ kp);
+  const int vrow = rowoff(g) + qq, vp = p2_pv(vrow);
+  int vofs[NB];
+#pragma unroll
+  for (int n = 0; n < NB; ++n) vofs[n] = P2_IMG + vrow * 256 + 16 * ((2 * n + (pp >> 1)) ^ vp) + 8 * (pp & 1);
+
+  auto compute = [&](const char* img, int t) {
+    const int ts = t * 64;
+    const bool active = ntok > 0 && ts <= p_hi && (window <= 0 || ts + 63 > p_lo - window);
+    if (!active) return;
+    f32x4_t sc[4][2];
+#pragma unroll
+    for (int b4 = 0; b4 < 4; ++b4) {
+      f32x4_t a0 = {0.f, 0.f, 0.f, 0.f}, a1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s = 0; s < KS; ++s) {
+        const bf16x8_t ka = *reinterpret_cast<const bf16x8_t*>(img + kofs[s] + b4 * 16 * 256);
+        a0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ka, qf[0][s], a0, 0, 0, 0);
+        a1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ka, qf[1][s], a1, 0, 0, 0);
+      }
+      sc[b4][0] = a0;
+      sc[b4][1] = a1;
+    }
+    const bool need_mask = (ts + 63 > p_lo) || (window > 0 && ts <= p_hi - window);
+    if (need_mask) {
+#pragma unroll
+      for (int nb = 0; nb < 2; ++nb) {
+        const int qp = p_lo + 16 * nb + c16;
+#pragma unroll
+        for (int b4 = 0; b4 < 4; ++b4)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const int key = ts + 16 * b4 + rowoff(g) + i;
+            bool ok = key <= qp;
+            if (window > 0) ok = ok && key > qp - window;
+            sc[b4][nb][i] = ok ? sc[b4][nb][i] : NEG_INF;
+          }
+      }
+    }
+    float mt[2];
+    bool grow = false;
+#pragma unroll
+    for (int nb = 0; nb < 2; ++nb) {
+      float mx = NEG_INF;
+#pragma unroll
+      for (int b4 = 0; b4 < 4; ++b4)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) mx = fmaxf(mx, sc[b4][nb][i]);
+      mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      mt[nb] = mx * scale_log2;
+      grow = grow || (mt[nb] > m[nb] + 8.f);
+    }
+    if (__ballot(grow) != 0) {
+      float alpha[2];
+#pragma unroll
+      for (int nb = 0; nb < 2; ++nb) {
+        const float mnew = fmaxf(m[nb], mt[nb]);
+        alpha[nb] = (mnew == NEG_INF) ? 1.f : __builtin_amdgcn_exp2f(m[nb] - mnew);
+        lsum[nb] *= alpha[nb];
+        m[nb] = mnew;
+      }
+#pragma unroll
+      for (int nb = 0; nb < 2; ++nb)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const float a = __shfl(alpha[nb], 4 * g + i, 64);
+#pragma unroll
+          for (int n = 0; n < NB; ++n) o[nb][n][i] *= a;
+        }
+    }
+#pragma unroll
+    for (int nb = 0; nb < 2; ++nb) {
+      const float msub = (m[nb] == NEG_INF) ? 0.f : m[nb];
+      float ps = 0.f;
+#pragma unroll
+      for (int b4 = 0; b4 < 4; ++b4)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const float p = __builtin_amdgcn_exp2f(fmaf(sc[b4][nb][i], scale_log2, -msub));
+          sc[b4][nb][i] = p;
+          ps += p;
+        }
+      ps += __shfl_xor(ps, 16, 64);
+      ps += __shfl_xor(ps, 32, 64);
+      lsum[nb] += ps;
+    }
+#pragma unroll
+    for (int t2 = 0; t2 < 2; ++t2) {
+      bf16x8_t pa[2];
+#pragma unroll
+      for (int nb = 0; nb < 2; ++nb)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          pa[nb][j] = (__bf16)sc[2 * t2][nb][j];
+          pa[nb][4 + j] = (__bf16)sc[2 * t2 + 1][nb][j];
+        }
+#pragma unroll
+      for (int n = 0; n < NB; ++n) {
+        const char* p0 = img + vofs[n] + 32 * t2 * 256;
+        s16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4_t*)p0);
+        s16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            (__attribute__((address_space(3))) s16x4_t*)(p0 + 16 * 256));
+        const bf16x8_t vb = __builtin_bit_cast(
+            bf16x8_t, s16x8_t{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]});
+        o[0][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pa[0], vb, o[0][n], 0, 0, 0);
+        o[1][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pa[1], vb, o[1][n], 0, 0, 0);
+      }
+    }
+  };
+
+  issue(buf0, t_first);
+  for (int t = t_first; t <= t_last; t += 2) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (t + 1 <= t_last) issue(buf1, t + 1);
+    compute(buf0, t);
+    if (t + 1 > t_last) break;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (t + 2 <= t_last) issue(buf0, t + 2);
+    compute(buf1, t + 1);
+  }
+
+  if (ntok == 0) return;
+  const float sink = sinks ? sinks[head] * 1.4426950408889634f : NEG_INF;
+#pragma unroll
+  for (int nb = 0; nb < 2; ++nb) {
+    float den = lsum[nb];
+    if (sinks) den += exp2f(sink - (m[nb] == NEG_INF ? 0.f : m[nb]));
+    const float inv = den > 0.f ? vscale / den : 0.f;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const float f = __shfl(inv, 4 * g + i, 64);
+      const int tk = tok0 + 16 * nb + 4 * g + i;
+      if (tk < ql) {
+        uint16_t* orow = out + (int64_t)(qs + tk) * out_stride + (int64_t)head * D;
+#pragma unroll
+        for (int n = 0; n < NB; ++n) orow[16 * n + c16] = f2bf(o[nb][n][i] * f);
+      }
+    }
+  }
+}
+
 }  // namespace
 
 extern "C" int llmd_paged_prefill(const void* q, int64_t q_stride, const void* kc, const void* vc,
@@ -326,7 +563,15 @@ extern "C" int llmd_paged_prefill(const void* q, int64_t q_stride, const void* k
                      (const uint16_t*)q, q_stride, kc, vc, block_stride, bs, block_tables, bt_stride, q_start,   \
                      q_len, ctx_len, items, Hq, Hkv, G, HPW, scale_log2, window, sinks, (uint16_t*)out,        \
                      out_stride, v_scale)
-  if (D == 128) {
+  static const bool v1_only = [] {
+    const char* e = getenv("LLMD_PREFILL_V1");
+    return e && e[0] == '1';
+  }();
+  if (D == 128 && !fp8 && bs >= 64 && !v1_only) {
+    hipLaunchKernelGGL(prefill_v2_kernel, grid, blk, 0, st, (const uint16_t*)q, q_stride, (const uint16_t*)kc,
+                       (const uint16_t*)vc, block_stride, bs, block_tables, bt_stride, q_start, q_len, ctx_len,
+                       items, Hq, Hkv, G, HPW, scale_log2, window, sinks, (uint16_t*)out, out_stride, v_scale);
+  } else if (D == 128) {
     if (fp8) LAUNCH(128, true); else LAUNCH(128, false);
   } else if (D == 64) {
     if (fp8) LAUNCH(64, true); else LAUNCH(64, false);
