@@ -300,7 +300,7 @@ __global__ __launch_bounds__(NT, 2) void prefill_kernel(
   }
 }
 
-// ---------------------------------------------------------------- v2 (bf16 cache, D = 128, block >= 64)
+// ---------------------------------------------------------------- v2 (bf16 cache, D = 64/128, block >= 64)
 // Same work decomposition and math as prefill_kernel; the tiles move
 // global -> LDS with global_load_lds_dwordx4 (no VGPR staging, no ds_write),
 // one vmcnt + barrier per tile, double-buffered. Images are unpadded 256-B rows
@@ -311,12 +311,22 @@ __global__ __launch_bounds__(NT, 2) void prefill_kernel(
 //   V: slot = c ^ pv(r), pv(r) = 2 ((r & 3) | (((r >> 3) & 1) << 2)): the 32-lane
 //      ds_read_b64_tr_b16 groups (rows {0-3,8-11} / {4-7,12-15}, chunk pairs
 //      2n, 2n+1) hit 32 distinct 8-B slots.
+//   D = 64 (128-B rows, 8 chunks; odd rows shift banks by half a bank row):
+//      K and V both use (r & 2) | ((r >> 1) & 4), found by the same exhaustive
+//      search as the MLA latent tile, which has the same bank geometry.
 // All LDS reads are a per-lane register + an immediate (buffer, key block, dim block).
-constexpr int P2_IMG = 64 * 256;  // one 64-key x 128-dim bf16 image
+template <int D>
+__device__ __forceinline__ int p2_pk(int r) {
+  if constexpr (D == 128) return ((r >> 1) & 7) | ((r & 1) << 3);
+  else return (r & 2) | ((r >> 1) & 4);
+}
+template <int D>
+__device__ __forceinline__ int p2_pv(int r) {
+  if constexpr (D == 128) return 2 * ((r & 3) | (((r >> 3) & 1) << 2));
+  else return (r & 2) | ((r >> 1) & 4);
+}
 
-__device__ __forceinline__ int p2_pk(int r) { return ((r >> 1) & 7) | ((r & 1) << 3); }
-__device__ __forceinline__ int p2_pv(int r) { return 2 * ((r & 3) | (((r >> 3) & 1) << 2)); }
-
+template <int D>
 __global__ __launch_bounds__(NT, 2) void prefill_v2_kernel(
     const uint16_t* __restrict__ q, int64_t q_stride, const uint16_t* __restrict__ kc,
     const uint16_t* __restrict__ vc, int64_t block_stride, int bs,
@@ -324,7 +334,9 @@ __global__ __launch_bounds__(NT, 2) void prefill_v2_kernel(
     const int* __restrict__ q_len, const int* __restrict__ ctx_len, const int* __restrict__ items,
     int Hq, int Hkv, int G, int HPW, float scale_log2, int window,
     const float* __restrict__ sinks, uint16_t* __restrict__ out, int64_t out_stride, float vscale) {
-  constexpr int D = 128, KS = 4, NB = 8;
+  constexpr int KS = D / 32, NB = D / 16, RB = 2 * D;  // row bytes
+  constexpr int P2_IMG = 64 * RB;                       // one 64-key bf16 image
+  constexpr int NI = 64 * (D / 8) / 64;                 // DMA wave-instructions per image (16 / 8)
   __shared__ __attribute__((aligned(1024))) char buf0[2 * P2_IMG];  // K | V of even tiles
   __shared__ __attribute__((aligned(1024))) char buf1[2 * P2_IMG];  // K | V of odd tiles
 
@@ -367,20 +379,20 @@ __global__ __launch_bounds__(NT, 2) void prefill_v2_kernel(
 #pragma unroll
     for (int n = 0; n < NB; ++n) o[nb][n] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 
-  // DMA: 16 K + 16 V wave-instructions of 4 rows x 256 B; wave w issues j = w + 4i
+  // DMA: NI K + NI V wave-instructions of 1 KB (1024 / RB rows); wave w issues j = w + 4i
   auto issue = [&](char* base, int t) {
     const int ts = t * 64;
     const int64_t toff = (int64_t)bt[ts >> lbs] * block_stride + head_off + (int64_t)(ts & (bs - 1)) * D;
     const int rlim = ctx - 1 - ts;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
+    for (int i = 0; i < NI / 4; ++i) {
       const int j = w + 4 * i;
       const int u = 64 * j + lane;
-      const int row = u >> 4, sl = u & 15;
+      const int row = u / (D / 8), sl = u % (D / 8);
       const int64_t ro = toff + (int64_t)min(row, rlim) * D;
-      __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)(kc + ro + 8 * (sl ^ p2_pk(row))),
+      __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)(kc + ro + 8 * (sl ^ p2_pk<D>(row))),
                                        (void __attribute__((address_space(3)))*)(base + 1024 * j), 16, 0, 0);
-      __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)(vc + ro + 8 * (sl ^ p2_pv(row))),
+      __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)(vc + ro + 8 * (sl ^ p2_pv<D>(row))),
                                        (void __attribute__((address_space(3)))*)(base + P2_IMG + 1024 * j), 16, 0,
                                        0);
     }
@@ -388,14 +400,14 @@ __global__ __launch_bounds__(NT, 2) void prefill_v2_kernel(
   // per-lane LDS offsets (see the header): K rows 16 b4 + srow, chunk 4s + g;
   // V rows 32 t2 + vrow (+16), chunk 2n + (pp >> 1), half pp & 1
   const int qq = c16 >> 2, pp = c16 & 3;
-  const int srow = rowoff(c16 >> 2) + (c16 & 3), kp = p2_pk(srow);
+  const int srow = rowoff(c16 >> 2) + (c16 & 3), kp = p2_pk<D>(srow);
   int kofs[KS];
 #pragma unroll
-  for (int s = 0; s < KS; ++s) kofs[s] = srow * 256 + 16 * ((4 * s + g) ^ kp);
-  const int vrow = rowoff(g) + qq, vp = p2_pv(vrow);
+  for (int s = 0; s < KS; ++s) kofs[s] = srow * RB + 16 * ((4 * s + g) ^ kp);
+  const int vrow = rowoff(g) + qq, vp = p2_pv<D>(vrow);
   int vofs[NB];
 #pragma unroll
-  for (int n = 0; n < NB; ++n) vofs[n] = P2_IMG + vrow * 256 + 16 * ((2 * n + (pp >> 1)) ^ vp) + 8 * (pp & 1);
+  for (int n = 0; n < NB; ++n) vofs[n] = P2_IMG + vrow * RB + 16 * ((2 * n + (pp >> 1)) ^ vp) + 8 * (pp & 1);
 
   auto compute = [&](const char* img, int t) {
     const int ts = t * 64;
@@ -407,7 +419,7 @@ __global__ __launch_bounds__(NT, 2) void prefill_v2_kernel(
       f32x4_t a0 = {0.f, 0.f, 0.f, 0.f}, a1 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int s = 0; s < KS; ++s) {
-        const bf16x8_t ka = *reinterpret_cast<const bf16x8_t*>(img + kofs[s] + b4 * 16 * 256);
+        const bf16x8_t ka = *reinterpret_cast<const bf16x8_t*>(img + kofs[s] + b4 * 16 * RB);
         a0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ka, qf[0][s], a0, 0, 0, 0);
         a1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ka, qf[1][s], a1, 0, 0, 0);
       }
@@ -490,10 +502,10 @@ __global__ __launch_bounds__(NT, 2) void prefill_v2_kernel(
         }
 #pragma unroll
       for (int n = 0; n < NB; ++n) {
-        const char* p0 = img + vofs[n] + 32 * t2 * 256;
+        const char* p0 = img + vofs[n] + 32 * t2 * RB;
         s16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4_t*)p0);
         s16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-            (__attribute__((address_space(3))) s16x4_t*)(p0 + 16 * 256));
+            (__attribute__((address_space(3))) s16x4_t*)(p0 + 16 * RB));
         const bf16x8_t vb = __builtin_bit_cast(
             bf16x8_t, s16x8_t{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]});
         o[0][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pa[0], vb, o[0][n], 0, 0, 0);
@@ -567,8 +579,9 @@ extern "C" int llmd_paged_prefill(const void* q, int64_t q_stride, const void* k
     const char* e = getenv("LLMD_PREFILL_V1");
     return e && e[0] == '1';
   }();
-  if (D == 128 && !fp8 && bs >= 64 && !v1_only) {
-    hipLaunchKernelGGL(prefill_v2_kernel, grid, blk, 0, st, (const uint16_t*)q, q_stride, (const uint16_t*)kc,
+  if ((D == 128 || D == 64) && !fp8 && bs >= 64 && !v1_only) {
+    auto kern = D == 128 ? prefill_v2_kernel<128> : prefill_v2_kernel<64>;
+    hipLaunchKernelGGL(kern, grid, blk, 0, st, (const uint16_t*)q, q_stride, (const uint16_t*)kc,
                        (const uint16_t*)vc, block_stride, bs, block_tables, bt_stride, q_start, q_len, ctx_len,
                        items, Hq, Hkv, G, HPW, scale_log2, window, sinks, (uint16_t*)out, out_stride, v_scale);
   } else if (D == 128) {

@@ -133,8 +133,9 @@ def test_paged_prefill(Hq, Hkv, D, bs):
     _close(o, r)
 
 
-def test_paged_prefill_window_sinks():
-    Hq, Hkv, D, bs = 64, 8, 64, 16
+@pytest.mark.parametrize("D,bs", [(64, 16), (64, 64), (128, 64)])
+def test_paged_prefill_window_sinks(D, bs):
+    Hq, Hkv = 64, 8
     shapes = [(300, 300), (77, 500)]
     ctx = [c for _, c in shapes]
     kc, vc, bt = _paged_setup(ctx, Hkv, D, bs, seed=6)
@@ -143,8 +144,8 @@ def test_paged_prefill_window_sinks():
     q = torch.randn(sum(ql), Hq * D, device=DEV, dtype=torch.bfloat16)
     sinks = torch.randn(Hq, device=DEV)
     args = [torch.tensor(x, dtype=torch.int32, device=DEV) for x in (qs, ql, ctx)]
-    r = ref.paged_prefill(q, kc, vc, bt, *args, Hq, Hkv, D, 0.125, 128, sinks)
-    o = ops.paged_prefill(q, kc, vc, bt, *args, Hq, Hkv, D, 0.125, 128, sinks)
+    r = ref.paged_prefill(q, kc, vc, bt, *args, Hq, Hkv, D, D ** -0.5, 128, sinks)
+    o = ops.paged_prefill(q, kc, vc, bt, *args, Hq, Hkv, D, D ** -0.5, 128, sinks)
     _close(o, r)
 
 
