@@ -94,7 +94,7 @@ LEGACY_IPC_MAX = 4 << 30  # hipIpcOpenMemHandle hangs importing larger allocatio
 class KvxAgent:
     def __init__(self, kv: torch.Tensor, engine_id: Optional[str] = None, host: Optional[str] = None,
                  port: int = 0, tp_rank: int = 0, tp_size: int = 1, abort_timeout: float = 480.0,
-                 transport: str = "auto", metrics=None, vmm: Optional[dict] = None):
+                 transport: str = "auto", metrics=None, vmm: Optional[dict] = None, exports: bool = True):
         self.kv = kv                      # [num_blocks, L, 2, Hkv, bs, D]
         self.vmm = vmm                    # chunked exportable pool (model_runner._alloc_cache)
         self.engine_id = engine_id or f"kvx-{uuid.uuid4().hex[:12]}"
@@ -129,7 +129,7 @@ class KvxAgent:
                     self.ipc_handle = (h, off)
                 except Exception as e:  # noqa: BLE001
                     log.warning("IPC export unavailable (%s); kvx falls back to TCP", e)
-            else:
+            elif exports:  # a pure consumer only pulls, nobody maps its pool
                 log.warning("KV pool of %.1f GiB is not VMM-chunked; hipIpc cannot import >4 GiB, "
                             "kvx falls back to TCP", kv.numel() * kv.element_size() / 2**30)
         self.host = host or os.environ.get("VLLM_NIXL_SIDE_CHANNEL_HOST", "127.0.0.1")

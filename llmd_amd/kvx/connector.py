@@ -66,7 +66,8 @@ class KvxConnector:
                               tp_rank=st.tp_rank, tp_size=st.tp_size,
                               abort_timeout=float(extra.get("abort_timeout",
                                                             os.environ.get("VLLM_NIXL_ABORT_REQUEST_TIMEOUT", 480))),
-                              transport=extra.get("transport", "auto"), metrics=self.metrics)
+                              transport=extra.get("transport", "auto"), metrics=self.metrics,
+                              exports=self.role != "kv_consumer")
         self._results: dict[str, bool] = {}
         self._finished: list[str] = []
         self._outputs = []
