@@ -269,7 +269,7 @@ class ModelRunner:
         for i, sr in enumerate(dec):
             r = sr.req
             p = sr.start
-            tok = r.all_token_ids[p]
+            tok = r.token_at(p)
             bt = block_tables[r.seq_id]
             ids.append(tok)
             pos.append(p)
@@ -281,7 +281,7 @@ class ModelRunner:
         for i, sr in enumerate(pre):
             r = sr.req
             bt = block_tables[r.seq_id]
-            toks = r.all_token_ids[sr.start : sr.start + sr.num_new_tokens]
+            toks = r.token_range(sr.start, sr.start + sr.num_new_tokens)
             ids.extend(toks)
             ps = np.arange(sr.start, sr.start + sr.num_new_tokens)
             pos.extend(ps.tolist())

@@ -113,6 +113,20 @@ class Request:
     def all_token_ids(self) -> list[int]:
         return self.prompt_token_ids + self.output_token_ids
 
+    def token_at(self, i: int) -> int:
+        """Token i of prompt+output without materialising the concatenation
+        (the per-step decode path must stay O(1) in the context length)."""
+        n = len(self.prompt_token_ids)
+        return self.prompt_token_ids[i] if i < n else self.output_token_ids[i - n]
+
+    def token_range(self, a: int, b: int) -> list[int]:
+        n = len(self.prompt_token_ids)
+        if b <= n:
+            return self.prompt_token_ids[a:b]
+        if a >= n:
+            return self.output_token_ids[a - n:b - n]
+        return self.prompt_token_ids[a:] + self.output_token_ids[:b - n]
+
     @property
     def num_tokens(self) -> int:
         return len(self.prompt_token_ids) + len(self.output_token_ids)

@@ -313,12 +313,17 @@ class Scheduler:
         Returns requests that produced new tokens or finished this step."""
         touched = []
         now = time.monotonic()
+        bs = self.cfg.cache.block_size
         for sr in out.all():
             r = sr.req
             if r.status.finished:
                 continue
             r.num_computed_tokens = sr.start + sr.num_new_tokens
-            if self.bm.has_seq(r.seq_id) and self.cfg.cache.enable_prefix_caching:
+            # hash/register newly completed blocks only (a decode completes one
+            # every block_size steps; converting the whole context each step cost
+            # O(ctx) host time per request)
+            if (self.cfg.cache.enable_prefix_caching and r.num_computed_tokens // bs > sr.start // bs
+                    and self.bm.has_seq(r.seq_id)):
                 self.bm.commit(r.seq_id, self._tokens(r), r.num_computed_tokens)
             if r.seq_id in sampled:
                 tok, lp = sampled[r.seq_id]

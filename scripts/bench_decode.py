@@ -24,6 +24,7 @@ def main():
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--quantization", default=None)
     ap.add_argument("--kv-cache-dtype", default="auto")
+    ap.add_argument("--host-profile", action="store_true", help="cProfile 20 steps (host-side cost ranking)")
     a = ap.parse_args()
     cfg = EngineConfig.create(a.model, device="cuda", block_size=64, max_num_seqs=a.batch,
                               max_num_batched_tokens=8192, max_model_len=a.isl + a.steps + 200,
@@ -45,7 +46,17 @@ def main():
         eng.step()
     torch.cuda.synchronize()
     dt = (time.perf_counter() - t0) / a.steps
-    tp = time.perf_counter()
+    if a.host_profile:
+        import cProfile
+        import pstats
+
+        pr = cProfile.Profile()
+        pr.enable()
+        for _ in range(20):
+            eng.step()
+        torch.cuda.synchronize()
+        pr.disable()
+        pstats.Stats(pr).sort_stats("tottime").print_stats(25)
     print(f"{a.model} q={a.quantization} kv={a.kv_cache_dtype} decode batch={a.batch} ctx~{a.isl}: "
           f"{dt * 1e3:.2f} ms/step  {a.batch / dt:.0f} tok/s (prefill phase {t0 - tstart:.1f}s)", flush=True)
 

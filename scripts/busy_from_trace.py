@@ -47,12 +47,12 @@ def breakdown(path, window):
     agg = {}
     for s, e, n in rows:
         if e > lo:
-            k = n.split("(")[0][:90]
+            k = n.replace("void ", "", 1).replace("(anonymous namespace)::", "").split("(")[0][:90] or "<unnamed>"
             t, c = agg.get(k, (0, 0))
             agg[k] = (t + e - max(s, lo), c + 1)
     tot = sum(t for t, _ in agg.values())
     print(f"per-kernel time in the last {window:.1f}s (total kernel {tot / 1e6:.1f} ms):")
-    for k, (t, c) in sorted(agg.items(), key=lambda kv: -kv[1][0])[:16]:
+    for k, (t, c) in sorted(agg.items(), key=lambda kv: -kv[1][0])[:24]:
         print(f"  {t / 1e6:9.1f} ms {100 * t / tot:5.1f}% {c:6d}  {k}")
 
 
