@@ -264,6 +264,12 @@ class SchedulerConfig:
     enable_chunked_prefill: bool = True
     policy: str = "fcfs"  # or "priority"
     long_prefill_token_threshold: int = 0
+    # Steps carrying a prefill chunk are trimmed so their token count (the M of
+    # every dense GEMM) is a multiple of this: hipBLASLt's tile/stream-K choice
+    # is erratic at arbitrary M (Llama-3-70B layer at M=5064 costs more than at
+    # M=6000, profiles/gemm_prefill_odd_m.txt) and the committed TunableOp table
+    # covers the aligned sizes. -1 = auto (512 on GPU, off on CPU), 0 = off.
+    prefill_token_align: int = -1
 
 
 @dataclass
@@ -327,6 +333,8 @@ class EngineConfig:
                 top[k] = v
         cfg = cls(model=model, model_config=mc, **parts, **top)
         cfg.sched.max_model_len = min(cfg.sched.max_model_len, mc.max_position_embeddings)
+        if cfg.sched.prefill_token_align < 0:
+            cfg.sched.prefill_token_align = 512 if str(cfg.device).startswith("cuda") else 0
         return cfg
 
 
@@ -374,6 +382,9 @@ def add_engine_args(p: argparse.ArgumentParser) -> argparse.ArgumentParser:
     p.add_argument("--kv-events-config", type=_json_arg, default=None)
     p.add_argument("--kv-offload-config", type=_json_arg, default=None)
     p.add_argument("--scheduling-policy", default="fcfs", choices=["fcfs", "priority"])
+    p.add_argument("--prefill-token-align", type=int, default=-1,
+                   help="trim prefill-carrying steps to a multiple of this many tokens (GEMM M); "
+                        "-1 auto (512 on GPU), 0 off")
     p.add_argument("--enable-lora", action="store_true")
     p.add_argument("--max-loras", type=int, default=4)
     p.add_argument("--max-lora-rank", type=int, default=16)
@@ -400,6 +411,7 @@ def engine_config_from_args(a) -> EngineConfig:
         dbo_prefill_token_threshold=getattr(a, "dbo_prefill_token_threshold", 32),
         enforce_eager=a.enforce_eager, kv_transfer_config=a.kv_transfer_config,
         kv_events_config=a.kv_events_config, kv_offload_config=a.kv_offload_config,
-        policy=a.scheduling_policy, enable_lora=getattr(a, "enable_lora", False),
+        policy=a.scheduling_policy, prefill_token_align=getattr(a, "prefill_token_align", -1),
+        enable_lora=getattr(a, "enable_lora", False),
         max_loras=getattr(a, "max_loras", 4), max_lora_rank=getattr(a, "max_lora_rank", 16),
         lora_modules=dict(m.split("=", 1) for m in (getattr(a, "lora_modules", None) or [])) or None)

@@ -305,9 +305,25 @@ class Scheduler:
             sr = ScheduledReq(r, n, r.num_computed_tokens)
             (out.decodes if sr.is_decode else out.prefills).append(sr)
             budget -= n
+        self._align_tokens(out)
         return out
 
-    # ------------------------------------------------------------ update
+    def _align_tokens(self, out: SchedulerOutput) -> None:
+        """Trim the newest prefill chunk so the step's token count is a multiple
+        of ``prefill_token_align`` (GEMM-friendly M). Steps below two alignment
+        units, or whose last chunk is too short to give up the remainder and
+        keep a full unit, run as scheduled; trimmed tokens go in the next step
+        (their blocks stay allocated, so the next ``grow`` is a no-op)."""
+        a = self.sc.prefill_token_align
+        if a <= 0 or not out.prefills:
+            return
+        total = out.num_tokens
+        rem = total % a
+        if total < 2 * a or rem == 0:
+            return
+        sr = out.prefills[-1]
+        if sr.num_new_tokens - rem >= a:
+            sr.num_new_tokens -= rem
     def update(self, out: SchedulerOutput, sampled: dict[int, tuple[int, float]]) -> list[Request]:
         """Apply a step's results. `sampled`: seq_id -> (token, logprob).
         Returns requests that produced new tokens or finished this step."""

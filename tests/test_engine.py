@@ -84,6 +84,33 @@ def test_engine_greedy_matches_plain_forward():
     assert eng.bm.num_free() == eng.bm.num_blocks
 
 
+def test_prefill_token_align_trims_steps_and_keeps_outputs():
+    # align 16 with a 64-token budget: prefill-carrying steps of >= 32 tokens
+    # are cut to a multiple of 16 (GEMM-friendly M), outputs unchanged
+    eng = make_engine(prefill_token_align=16)
+    assert eng.cfg.sched.prefill_token_align == 16
+    assert make_engine().cfg.sched.prefill_token_align == 0  # auto: off on CPU
+    seen = []
+    orig = eng.sched.schedule
+
+    def spy():
+        so = orig()
+        if so.prefills:
+            seen.append(so.num_tokens)
+        return so
+
+    eng.sched.schedule = spy
+    prompts = _prompts(5, [37, 90, 23, 61])
+    sp = SamplingParams(max_tokens=5, temperature=0.0, ignore_eos=True)
+    reqs = eng.generate(prompts, sp)
+    for p, r in zip(prompts, reqs):
+        assert r.output_token_ids == greedy_reference(eng.runner.model, p, 5)
+    assert seen and all(n < 32 or n % 16 == 0 for n in seen), seen
+    assert any(n % 16 == 0 and n >= 32 for n in seen)
+    eng.bm.check_invariants()
+    assert eng.bm.num_free() == eng.bm.num_blocks
+
+
 def test_prefix_cache_hit_and_same_output():
     eng = make_engine()
     base = _prompts(1, [80])[0]
