@@ -20,6 +20,13 @@ def test_wide_ep_symm_gpu(model, flags, port, tmp_path):
            "--master-addr=127.0.0.1", f"--master-port={port}", os.path.join(ROOT, "scripts", "ep_gpu_check.py"),
            "--model", model, "--weights", str(tmp_path / "w.safetensors")] + flags
     r = subprocess.run(cmd, env=env, cwd=ROOT, capture_output=True, text=True, timeout=220)
-    assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-4000:])
+    err = []
+    if r.returncode != 0:
+        # torchrun's trailer hides the failing rank's traceback: keep the whole log.
+        os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
+        with open(os.path.join(ROOT, "gpurun_out", f"ep_gpu_{model}.log"), "w") as f:
+            f.write(r.stdout + "\n---- stderr ----\n" + r.stderr)
+        err = [l for l in r.stderr.splitlines() if "rror" in l or "Traceback" in l]
+    assert r.returncode == 0, (r.stdout[-2000:], err[-20:], r.stderr[-4000:])
     d = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
     assert d["ok"] and all(x["timeout_flag"] == 0 for x in d["ranks"])
