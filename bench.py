@@ -159,20 +159,22 @@ def main():
                         SamplingParams(max_tokens=max_tokens, temperature=0.0, ignore_eos=True))
 
     # Setup (untimed, not part of warmup): admit C requests with staggered output
-    # lengths and run until every one of them is past its prefill, so warmup/timed
-    # steps see steady-state serving (decodes + chunked prefills of new arrivals)
-    # instead of the initial all-prefill ramp.
+    # lengths, replacing each finished one at once (closed loop, as in the timed
+    # region), and run until nothing waits and every running request is past its
+    # prefill. Completions are then spread evenly over the next OSL steps, so
+    # warmup/timed steps see steady-state serving (decodes + one new prefill per
+    # OSL/C steps) instead of the initial all-prefill ramp or a refill burst.
     for i in range(a.concurrency):
         new_request(max(1, int(a.osl * (i + 1) / a.concurrency)))
     ts = time.time()
     setup_steps = 0
     while setup_steps < 100000:
-        eng.step()
+        for o in eng.step():
+            if o.finished:
+                new_request(a.osl)
         setup_steps += 1
         if eng.sched.num_waiting == 0 and all(r.output_token_ids for r in eng.sched.running):
             break
-    while eng.sched.num_running + eng.sched.num_waiting < a.concurrency:
-        new_request(a.osl)
     _sync(a)
     log(rank, f"setup: {setup_steps} steps in {time.time() - ts:.1f}s (batch filled to {a.concurrency})")
 

@@ -159,7 +159,6 @@ class BlockManager {
     seqs_.erase(it);
   }
 
-  // Drop the last `n` blocks' worth of capacity (used by preemption-by-recompute).
   bool has_seq(int64_t seq_id) const { return seqs_.count(seq_id) > 0; }
 
   std::vector<int32_t> block_table(int64_t seq_id) const {
@@ -237,8 +236,8 @@ class BlockManager {
     return it == cache_.end() ? -1 : it->second;
   }
 
-  // Register an already-filled block (e.g. loaded back from an offload tier)
-  // under a hash; takes a reference for `seq_id`.
+  // Blocks reloaded from an offload tier are hashed by the request's next
+  // `commit` (its committed index still points before them).
   void check_invariants() const {
     int refd = 0;
     for (size_t i = 0; i < blocks_.size(); ++i)

@@ -93,9 +93,6 @@ class _WaitQueue:
             return heapq.heappop(self.heap)[3]
         return self.dq.popleft()
 
-    def __iter__(self):
-        return iter([e[3] for e in self.heap] if self.policy == "priority" else list(self.dq))
-
     def remove(self, r: Request) -> bool:
         if self.policy == "priority":
             for i, e in enumerate(self.heap):
@@ -114,9 +111,10 @@ class _WaitQueue:
         return len(self.heap) if self.policy == "priority" else len(self.dq)
 
     def __iter__(self):
+        # iterate over a snapshot: callers may remove entries while iterating
         if self.policy == "priority":
             return iter([e[3] for e in sorted(self.heap)])
-        return iter(self.dq)
+        return iter(list(self.dq))
 
 
 class Scheduler:
@@ -130,6 +128,9 @@ class Scheduler:
         self.waiting = _WaitQueue(self.sc.policy)
         self.running: list[Request] = []
         self.remote_wait: dict[str, Request] = {}
+        # aborted while their KV pull was in flight: request id -> seq id whose
+        # blocks stay allocated until the connector reports the pull finished
+        self.aborted_remote: dict[str, int] = {}
         self.requests: dict[str, Request] = {}
         self.eos = set(cfg.model_config.eos_ids)
         self.num_preemptions_total = 0
@@ -156,9 +157,15 @@ class Scheduler:
             return None
         if r in self.running:
             self.running.remove(r)
+        elif self.remote_wait.pop(request_id, None) is not None:
+            # the transfer worker may still be writing into this request's local
+            # blocks: keep them allocated until the pull reports done
+            self.connector.cancel_load(request_id)
+            self.aborted_remote[request_id] = r.seq_id
+            self._finish(r, Status.FINISHED_ABORTED, free_blocks=False)
+            return r
         else:
             self.waiting.remove(r)
-            self.remote_wait.pop(request_id, None)
         self._finish(r, Status.FINISHED_ABORTED)
         return r
 
@@ -171,7 +178,8 @@ class Scheduler:
         return len(self.running)
 
     def has_work(self) -> bool:
-        return bool(self.running) or len(self.waiting) > 0 or bool(self.remote_wait)
+        return (bool(self.running) or len(self.waiting) > 0 or bool(self.remote_wait)
+                or bool(self.aborted_remote))
 
     # ------------------------------------------------------------ helpers
     def _tokens(self, r: Request) -> np.ndarray:
@@ -207,6 +215,11 @@ class Scheduler:
         # 0. remote-KV arrivals (P/D decode side)
         if self.connector is not None:
             for rid in self.connector.poll_finished_recv():
+                seq = self.aborted_remote.pop(rid, None)
+                if seq is not None:
+                    self.connector.recv_ok(rid)  # drop the result
+                    self.bm.free(seq)
+                    continue
                 r = self.remote_wait.pop(rid, None)
                 if r is None:
                     continue
@@ -309,10 +322,11 @@ class Scheduler:
         return out
 
     def _align_tokens(self, out: SchedulerOutput) -> None:
-        """Trim the newest prefill chunk so the step's token count is a multiple
-        of ``prefill_token_align`` (GEMM-friendly M). Steps below two alignment
-        units, or whose last chunk is too short to give up the remainder and
-        keep a full unit, run as scheduled; trimmed tokens go in the next step
+        """Trim prefill chunks, newest first, so the step's token count is a
+        multiple of ``prefill_token_align`` (GEMM-friendly M). Each trimmed chunk
+        keeps at least two tokens (a one-token chunk would read as a decode);
+        steps below two alignment units, or whose chunks cannot give up the
+        whole remainder, run as scheduled. Trimmed tokens go in the next step
         (their blocks stay allocated, so the next ``grow`` is a no-op)."""
         a = self.sc.prefill_token_align
         if a <= 0 or not out.prefills:
@@ -321,9 +335,15 @@ class Scheduler:
         rem = total % a
         if total < 2 * a or rem == 0:
             return
-        sr = out.prefills[-1]
-        if sr.num_new_tokens - rem >= a:
-            sr.num_new_tokens -= rem
+        if sum(max(sr.num_new_tokens - 2, 0) for sr in out.prefills) < rem:
+            return
+        for sr in reversed(out.prefills):
+            take = min(rem, max(sr.num_new_tokens - 2, 0))
+            sr.num_new_tokens -= take
+            rem -= take
+            if rem == 0:
+                break
+
     def update(self, out: SchedulerOutput, sampled: dict[int, tuple[int, float]]) -> list[Request]:
         """Apply a step's results. `sampled`: seq_id -> (token, logprob).
         Returns requests that produced new tokens or finished this step."""
@@ -372,14 +392,14 @@ class Scheduler:
             self.running.remove(r)
         self._finish(r, status)
 
-    def _finish(self, r: Request, status: Status):
+    def _finish(self, r: Request, status: Status, free_blocks: bool = True):
         r.status = status
         r.finished_time = time.monotonic()
         ktp = r.kv_transfer_params or {}
         if ktp.get("do_remote_decode") and self.connector is not None and status != Status.FINISHED_ABORTED:
             # P side: keep blocks for the remote reader; the connector frees them
             self.connector.hold_for_remote(r, self.bm.block_table(r.seq_id) if self.bm.has_seq(r.seq_id) else [])
-        else:
+        elif free_blocks:
             self.bm.free(r.seq_id)
         self.requests.pop(r.request_id, None)
 

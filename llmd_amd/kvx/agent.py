@@ -109,6 +109,8 @@ class KvxAgent:
         self.free_requests: "queue.Queue[str]" = queue.Queue()
         self.done: "queue.Queue[tuple[str, bool]]" = queue.Queue()
         self.jobs: "queue.Queue[Optional[LoadJob]]" = queue.Queue()
+        self.cancelled: set[str] = set()
+        self.cancel_lock = threading.Lock()
         self.peers: dict[tuple, dict] = {}
         self.ipc_maps: dict[str, int] = {}
         self.ipc_handle = None
@@ -249,6 +251,25 @@ class KvxAgent:
     def start_load(self, request_id: str, params: dict, local_blocks: list):
         self.jobs.put(LoadJob(request_id, dict(params), list(local_blocks)))
 
+    def cancel(self, request_id: str):
+        with self.cancel_lock:
+            self.cancelled.add(request_id)
+
+    def _take_cancel(self, request_id: str) -> bool:
+        with self.cancel_lock:
+            if request_id in self.cancelled:
+                self.cancelled.discard(request_id)
+                return True
+            return False
+
+    def _notify_free(self, prm: dict):
+        """Abort notif: tell the prefiller it can release the held blocks."""
+        try:
+            p = self._peer(prm["remote_host"], prm["remote_port"])
+            self._rpc(p, {"op": "free", "request_id": prm.get("remote_request_id")})
+        except Exception as e:  # noqa: BLE001 - the prefiller's abort timeout reclaims them
+            log.warning("kvx abort notif for %s failed: %s", prm.get("remote_request_id"), e)
+
     def _peer(self, host, port) -> dict:
         key = (host, int(port))
         self.known_peers.add(key)
@@ -314,6 +335,11 @@ class KvxAgent:
             ok = False
             t0 = time.monotonic()
             nbytes = 0
+            if self._take_cancel(job.request_id):
+                # aborted before the pull started: nothing was written locally
+                self._notify_free(job.params)
+                self.done.put((job.request_id, False))
+                continue
             try:
                 ok, nbytes = self._do_load(job)
             except Exception as e:  # noqa: BLE001 - NIXL_ERR_BACKEND equivalent
@@ -321,6 +347,7 @@ class KvxAgent:
                 ok = False
             if self.metrics is not None:
                 self.metrics.observe(ok, time.monotonic() - t0, nbytes, len(job.local_blocks))
+            self._take_cancel(job.request_id)  # a cancel that raced the running pull
             self.done.put((job.request_id, ok))
 
     def _do_load(self, job: LoadJob) -> tuple[bool, int]:

@@ -76,6 +76,14 @@ class KvxConnector:
     def start_load(self, req, local_blocks: list):
         self.agent.start_load(req.request_id, req.kv_transfer_params or {}, local_blocks)
 
+    def cancel_load(self, request_id: str):
+        """The request was aborted while its pull is queued or running. A queued
+        pull is skipped (the prefiller is still told to free its blocks); a
+        running one completes. Either way the id is reported through
+        ``poll_finished_recv`` so the scheduler can release the local blocks
+        only once nothing writes into them any more."""
+        self.agent.cancel(request_id)
+
     def poll_finished_recv(self) -> list[str]:
         for rid, ok in self.agent.poll_done():
             self._results[rid] = ok

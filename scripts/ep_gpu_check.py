@@ -80,14 +80,31 @@ def main():
     set_state(ParallelState())
     ref = LLMEngine(cfg(enforce_eager=True))
     want = [r.output_token_ids for r in ref.generate(prompts, sp)]
-    set_state(st)
     agree = sum(int(x == y) for g, w in zip(got, want) for x, y in zip(g, w))
     total = sum(len(w) for w in want)
-    ok = err == 0 and all(g[:3] == w[:3] for g, w in zip(got, want)) and agree >= 0.8 * total
-    # first divergence per request: (request, token index, got, want)
-    div = [(i, next((j for j, (x, y) in enumerate(zip(g, w)) if x != y), None)) for i, (g, w) in
-           enumerate(zip(got, want))]
-    div = [(i, j, got[i][j], want[i][j]) for i, j in div if j is not None]
+    # first divergence per request: (request, token index, got, want, margin).
+    # Tiny random-init models have near-flat logits, and the EP path sums expert
+    # outputs in another order than the single-process engine, so a greedy
+    # argmax may flip between two almost-equal logits. A divergence is accepted
+    # only if the reference's logit margin of its token over ours at that
+    # position is within bf16 rounding; later tokens are not compared since
+    # the contexts differ from there on.
+    div = []
+    for i, (g, w) in enumerate(zip(got, want)):
+        j = next((j for j, (x, y) in enumerate(zip(g, w)) if x != y), None)
+        if j is None:
+            continue
+        probe = ref.generate([prompts[i] + w[:j]], SamplingParams(max_tokens=1, temperature=0.0,
+                                                                 ignore_eos=True, embed=True))
+        logits = ref.runner.model.compute_logits(ref.runner._last_hidden)[0].float()
+        logits = logits[: ref.cfg.model_config.vocab_size]
+        margin = float(logits[w[j]] - logits[g[j]])
+        tol = max(0.05, 0.01 * float(logits.abs().max()))
+        assert probe[0].output_token_ids[0] == w[j]
+        div.append({"req": i, "pos": j, "got": g[j], "want": w[j], "margin": round(margin, 4),
+                    "tol": round(tol, 4), "near_tie": margin <= tol})
+    set_state(st)
+    ok = err == 0 and all(d["near_tie"] for d in div)
     flags = [None] * world
     dist.all_gather_object(flags, {"rank": rank, "ok": ok, "agree": agree, "total": total, "steps": steps,
                                    "timeout_flag": err, "diverge": div})

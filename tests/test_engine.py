@@ -96,7 +96,10 @@ def test_prefill_token_align_trims_steps_and_keeps_outputs():
     def spy():
         so = orig()
         if so.prefills:
-            seen.append(so.num_tokens)
+            # the trim keeps >= 2 tokens per chunk: a step is left unaligned
+            # only when its chunks could not give up the remainder
+            slack = sum(sr.num_new_tokens - 2 for sr in so.prefills)
+            seen.append((so.num_tokens, slack))
         return so
 
     eng.sched.schedule = spy
@@ -105,8 +108,8 @@ def test_prefill_token_align_trims_steps_and_keeps_outputs():
     reqs = eng.generate(prompts, sp)
     for p, r in zip(prompts, reqs):
         assert r.output_token_ids == greedy_reference(eng.runner.model, p, 5)
-    assert seen and all(n < 32 or n % 16 == 0 for n in seen), seen
-    assert any(n % 16 == 0 and n >= 32 for n in seen)
+    assert seen and all(n < 32 or n % 16 == 0 or slack < n % 16 for n, slack in seen), seen
+    assert any(n % 16 == 0 and n >= 32 for n, _ in seen)
     eng.bm.check_invariants()
     assert eng.bm.num_free() == eng.bm.num_blocks
 

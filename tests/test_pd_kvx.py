@@ -118,3 +118,70 @@ def test_prefiller_heartbeat_marks_dead_and_fails_fast(monkeypatch):
     r, o = run(D, "d2", prompt[::-1], SamplingParams(max_tokens=3, temperature=0.0, ignore_eos=True),
                op2.kv_transfer_params)
     assert o.finish_reason == "length" and len(r.output_token_ids) == 3   # recomputed locally
+
+
+def test_abort_during_remote_pull_keeps_blocks_until_done(monkeypatch):
+    """aborting a request whose KV pull is in flight must not
+    free its destination blocks while the transfer worker can still write them.
+    The blocks are released only once the pull reports done, the prefiller is
+    told to free its held blocks, and a request admitted meanwhile decodes the
+    same tokens as on an aggregated engine."""
+    import time
+
+    P = make(KT)
+    D = make(KT)
+    A = make()
+    sp1 = SamplingParams(max_tokens=1, temperature=0.0, ignore_eos=True)
+    sp = SamplingParams(max_tokens=6, temperature=0.0, ignore_eos=True)
+    prompt = list(range(30, 130))
+    other = np.random.default_rng(1).integers(3, 500, size=90).tolist()
+    want = A_outputs(A, other, sp)
+    _, op = run(P, "p", prompt, sp1, {"do_remote_decode": True})
+    assert P.bm.num_free() < P.bm.num_blocks
+    monkeypatch.setenv("LLMD_KVX_FAULT", "delay:0.3")
+    D.add_request("d", prompt, sp, kv_transfer_params=op.kv_transfer_params)
+    D.step()                                    # allocates blocks, starts the (delayed) pull
+    assert "d" in D.sched.remote_wait
+    held = D.bm.num_blocks - D.bm.num_free()
+    assert held > 0
+    D.abort("d")
+    assert D.bm.num_blocks - D.bm.num_free() == held   # still owned by the in-flight pull
+    monkeypatch.delenv("LLMD_KVX_FAULT")
+    r2, o2 = run(D, "d2", other, sp)             # admitted while the pull is running
+    assert r2.output_token_ids == want
+    deadline = time.monotonic() + 10
+    while (D.sched.aborted_remote or P.bm.num_free() != P.bm.num_blocks) and time.monotonic() < deadline:
+        D.step()
+        P.step()
+        time.sleep(0.01)
+    assert not D.sched.aborted_remote
+    assert D.bm.num_free() == D.bm.num_blocks
+    assert P.bm.num_free() == P.bm.num_blocks    # abort notif / post-read free reached P
+    assert "d" not in D.connector._results
+
+
+def test_abort_before_pull_starts_notifies_prefiller(monkeypatch):
+    """A pull aborted while still queued behind another one is skipped: nothing
+    is written locally, P is told to free its held blocks, and D releases the
+    destination blocks once the worker reports the skipped job."""
+    import time
+
+    P = make(KT)
+    D = make(KT)
+    sp1 = SamplingParams(max_tokens=1, temperature=0.0, ignore_eos=True)
+    _, op1 = run(P, "p1", list(range(40, 120)), sp1, {"do_remote_decode": True})
+    _, op2 = run(P, "p2", list(range(140, 220)), sp1, {"do_remote_decode": True})
+    monkeypatch.setenv("LLMD_KVX_FAULT", "delay:0.3")
+    D.add_request("d1", list(range(40, 120)), SamplingParams(max_tokens=2), kv_transfer_params=op1.kv_transfer_params)
+    D.add_request("d2", list(range(140, 220)), SamplingParams(max_tokens=2), kv_transfer_params=op2.kv_transfer_params)
+    D.step()                                    # both pulls queued; the worker sleeps in d1's
+    assert {"d1", "d2"} <= set(D.sched.remote_wait)
+    D.abort("d2")
+    monkeypatch.delenv("LLMD_KVX_FAULT")
+    deadline = time.monotonic() + 10
+    while (D.has_unfinished() or P.bm.num_free() != P.bm.num_blocks) and time.monotonic() < deadline:
+        D.step()
+        P.step()
+        time.sleep(0.01)
+    assert P.bm.num_free() == P.bm.num_blocks
+    assert D.bm.num_free() == D.bm.num_blocks
