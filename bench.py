@@ -10,12 +10,18 @@ flight (closed loop: a finished request is immediately replaced), W warmup
 steps bring the batch to steady state, then exactly K steps are timed between
 barrier+synchronize brackets; the slowest rank's time is used.
 
-Modes (default ``auto``: agg for N = 1, pd for N >= 2)
+Modes (default ``auto``: agg for N < 4, pd for N >= 4)
   agg : every GPU is an independent aggregated replica (dp N) - the
         optimized-baseline topology; per-GPU work fixed as N grows (weak scaling).
   pd  : ranks [0, P) prefill, [P, N) decode (P = 3N/4 unless --prefill-gpus;
         ISL 5000 / OSL 250 is prefill-heavy, so 6P2D is the throughput-optimal
         split on 8 GPUs); KV moves over xGMI (kvx VMM-chunked IPC pool).
+        One 70B bf16 prefill GPU feeds ~10k prompt tok/s = ~500 output tok/s
+        of decode, a quarter of what one decode GPU sustains at batch 64, so a
+        P:D split needs >= 4 GPUs to be balanced (the reference tunes the ratio
+        per workload, guides/pd-disaggregation/README.md:15-33); on 2 GPUs a
+        1P1D split would idle the decoder and auto runs two aggregated
+        replicas instead.
 
 Output: one JSON line on rank 0 (see README "bench.py contract").
 """
@@ -50,7 +56,7 @@ def parse():
     p.add_argument("--max-num-batched-tokens", type=int, default=8192)
     p.add_argument("--block-size", type=int, default=64)
     p.add_argument("--mode", default="auto", choices=["auto", "agg", "pd"],
-                   help="auto: agg on 1 GPU, P/D disaggregation (3/4 prefill ranks) on N >= 2")
+                   help="auto: aggregated replicas on N < 4, P/D disaggregation (3/4 prefill ranks) on N >= 4")
     p.add_argument("--prefill-gpus", type=int, default=0, help="pd mode: number of prefill ranks")
     p.add_argument("--enforce-eager", action="store_true")
     p.add_argument("--seed", type=int, default=0)
@@ -99,7 +105,7 @@ def main():
             dist.init_process_group("gloo", rank=rank, world_size=world)
 
     if a.mode == "auto":
-        a.mode = "pd" if world > 1 else "agg"
+        a.mode = "pd" if world >= 4 else "agg"
     if a.mode == "pd":
         from llmd_amd.bench_pd import run_pd
 

@@ -44,8 +44,9 @@ int llmd_mla_rope_cache(const void*, int64_t, void*, int64_t, const void*, int64
                         hipStream_t);
 int llmd_lora_bgmv(const void*, int64_t, const void*, const void*, int, int, int, int, const int*, float*, void*,
                    int64_t, hipStream_t);
-int llmd_skinny_gemm(const void*, int64_t, const void*, int64_t, int, int, int, int, void*, int64_t, float*,
-                     hipStream_t);
+int llmd_skinny_gemm(const void*, int64_t, const void*, int64_t, int, int, int, int, int, int, void*, int64_t,
+                     float*, hipStream_t);
+int llmd_dgemm_supported(int, int, int);
 int llmd_vmm_granularity(int, size_t*);
 int llmd_vmm_alloc(int, size_t, int, void**, uint64_t*);
 int llmd_vmm_export_fd(uint64_t, int*);
@@ -296,23 +297,30 @@ void lora_bgmv(torch::Tensor y, torch::Tensor x, torch::Tensor A, torch::Tensor 
   TORCH_CHECK(rc == 0, "lora_bgmv failed: ", rc);
 }
 
-// y [M, N] = x [M, K] . w [N, K]^T for M <= 64 (decode GEMMs), nsplit-way split-K
-void skinny_gemm(torch::Tensor y, torch::Tensor x, torch::Tensor w, int64_t nsplit, torch::Tensor part) {
+// y [M, N] = x [M, K] . w [N, K]^T for M <= 64 (decode GEMMs): rb row blocks of
+// 16 per workgroup, nsplit-way split-K, occ workgroups per CU (ops.skinny_plan)
+void skinny_gemm(torch::Tensor y, torch::Tensor x, torch::Tensor w, int64_t rb, int64_t nsplit, int64_t occ,
+                 torch::Tensor part) {
   const c10::hip::OptionalHIPGuard device_guard(dev_of(y));
   CHECK_CUDA(x); CHECK_BF16(x); CHECK_BF16(w); CHECK_BF16(y); CHECK_INNER(x); CHECK_INNER(w); CHECK_INNER(y);
   TORCH_CHECK(x.dim() == 2 && w.dim() == 2 && y.dim() == 2, "skinny_gemm: 2-D operands");
   const int M = x.size(0), K = x.size(1), N = w.size(0);
-  TORCH_CHECK(M >= 1 && M <= 64 && w.size(1) == K && K % 128 == 0, "skinny_gemm: M <= 64, K % 128 == 0");
+  TORCH_CHECK(M >= 1 && M <= 64 && w.size(1) == K && K % 256 == 0, "skinny_gemm: M <= 64, K % 256 == 0");
+  TORCH_CHECK(N % 4 == 0, "skinny_gemm: N % 4 == 0");
   TORCH_CHECK(y.size(0) == M && y.size(1) == N, "skinny_gemm: output shape");
   TORCH_CHECK(x.stride(0) % 8 == 0 && w.stride(0) % 8 == 0 && y.stride(0) % 4 == 0, "skinny_gemm: row alignment");
+  TORCH_CHECK(llmd_dgemm_supported(M, (int)rb, (int)occ), "skinny_gemm: no kernel for rb=", rb, " occ=", occ);
   if (nsplit > 1) {
     CHECK_DT(part, at::kFloat);
     TORCH_CHECK(part.numel() >= nsplit * (int64_t)M * N, "skinny_gemm: workspace");
   }
-  int rc = llmd_skinny_gemm(x.data_ptr(), x.stride(0), w.data_ptr(), w.stride(0), M, N, K, (int)nsplit, y.data_ptr(),
-                            y.stride(0), nsplit > 1 ? part.data_ptr<float>() : nullptr, cur_stream());
+  int rc = llmd_skinny_gemm(x.data_ptr(), x.stride(0), w.data_ptr(), w.stride(0), M, N, K, (int)rb, (int)nsplit,
+                            (int)occ, y.data_ptr(), y.stride(0), nsplit > 1 ? part.data_ptr<float>() : nullptr,
+                            cur_stream());
   TORCH_CHECK(rc == 0, "skinny_gemm failed: ", rc);
 }
+
+bool skinny_supported(int64_t M, int64_t rb, int64_t occ) { return llmd_dgemm_supported((int)M, (int)rb, (int)occ); }
 
 void paged_prefill(torch::Tensor out, torch::Tensor q, torch::Tensor k_cache,
                    torch::Tensor v_cache, torch::Tensor block_tables, torch::Tensor q_start,
@@ -729,6 +737,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("kvx_ipc_close", &kvx_ipc_close);
   m.def("mla_attention", &mla_attention);
   m.def("skinny_gemm", &skinny_gemm);
+  m.def("skinny_supported", &skinny_supported);
   m.def("lora_bgmv", &lora_bgmv);
   m.def("mla_rope_cache", &mla_rope_cache);
   m.def("vmm_granularity", &vmm_granularity);

@@ -1,17 +1,22 @@
-// Skinny (decode) GEMM: Y[M, N] = X[M, K] . W[N, K]^T for M <= 64, bf16 in,
-// fp32 accumulate, bf16 out (SURVEY K08 decode shapes: M = decode batch,
-// N/K = 8k..57k). At these M the op is a stream over W; hipBLASLt reaches
-// ~4.5 TB/s here (profiles/r1_llama70b_decode_kernel_stats.txt), this kernel
-// is built to keep more bytes in flight.
+// Decode GEMM: Y[M, N] = X[M, K] . W[N, K]^T for decode-sized M (1..64), bf16 in,
+// fp32 accumulate, bf16 out (SURVEY K08 decode shapes: M = decode batch, N/K of
+// the dense projections). At these M the op is a stream over W, so the kernel is
+// built around keeping W bytes in flight with NO barrier in the main loop (a
+// __syncthreads() fence waits vmcnt(0) and drains the prefetch - the reason the
+// round-1 LDS-staged version streamed at 2.4-4 TB/s).
 //
-// Orientation Y^T = W . X^T: W rows on the MFMA M axis (A operand straight
-// from HBM, 16 B per lane), the decode rows on the N axis (B operand from a
-// padded LDS image of X shared by the workgroup's 4 waves).
-// Workgroup = 256 W rows (wave w: rows 64w..64w+63 = 4 MFMA row blocks) x one
-// K split; K advances in 128-wide stages; the next stage's W (64 VGPRs) and X
-// are loaded while the current one feeds 4 x 4 x MB mfma_16x16x32_bf16.
-// Epilogue: accumulators -> LDS transpose -> coalesced [M][N] rows, bf16 when
-// the K range is whole, else fp32 partials reduced by skinny_reduce_kernel.
+// Orientation Y^T = W . X^T on mfma_f32_16x16x32_bf16:
+//   A = W rows, 16 B per lane straight from HBM (row r = 16 rb + lane % 16,
+//       k = 8 (lane / 16) .. +7 of the current 32-wide k-step);
+//   B = X rows, same 16-B fragment shape, straight from L2 (X is re-read by the
+//       N / R workgroups of a K range; X/W traffic = M / R).
+// Decomposition (host planner `plan`): a workgroup owns R = 16 RB output
+// columns (W rows) and one K range of a split-K; its 4 waves split that range
+// again in 4 and are summed through LDS at the end (a 2-level tree), so every
+// wave streams whole 32-k steps of all RB row blocks. Loads run one chunk of U
+// k-steps ahead in two statically indexed register sets.
+// Epilogue: bf16 rows when the K range is whole (gridDim.y == 1), else fp32
+// partials [split][M][N] summed and rounded by dgemm_reduce_kernel.
 #include "llmd_common.h"
 
 using namespace llmd;
@@ -19,211 +24,241 @@ using namespace llmd;
 namespace {
 
 constexpr int NT = 256;
-constexpr int ROWS = 256;          // W rows per workgroup
-constexpr int KST = 128;           // K per stage
-constexpr int XROW = KST * 2 + 16; // padded LDS bytes per X row (conflict-free b128 reads)
 
-template <int MB>
-__global__ __launch_bounds__(NT, (MB >= 4 ? 1 : 2)) void skinny_gemm_kernel(const uint16_t* __restrict__ x, int64_t x_stride,
-                                                            const uint16_t* __restrict__ wt, int64_t w_stride,
-                                                            int M, int N, int K, int stages_per_split,
-                                                            uint16_t* __restrict__ y, int64_t y_stride,
-                                                            float* __restrict__ part) {
-  constexpr int MP = 16 * MB;  // padded M
-  extern __shared__ __attribute__((aligned(16))) char smem[];
+template <int RB, int MB, int U, int OCC>
+__global__ __launch_bounds__(NT, OCC) void dgemm_kernel(const uint16_t* __restrict__ x, int64_t x_stride,
+                                                        const uint16_t* __restrict__ wt, int64_t w_stride,
+                                                        int M, int N, int K, int nquad_split,
+                                                        uint16_t* __restrict__ y, int64_t y_stride,
+                                                        float* __restrict__ part) {
+  __shared__ __attribute__((aligned(16))) f32x4_t red[2][RB][MB][64];
   const int tile = blockIdx.x, sp = blockIdx.y, nsplit = gridDim.y;
-  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, g = lane >> 4, c16 = lane & 15;
-  const int nst = K / KST;
-  const int st0 = sp * stages_per_split, st1 = min(nst, st0 + stages_per_split);
-  const int row_base = tile * ROWS + 64 * w;
+  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63, g = lane >> 4, c16 = lane & 15;
+  const int row0 = tile * (16 * RB);
+  // k range: split sp owns 256-wide blocks [q0, q1); wave wv streams its own
+  // contiguous quarter of them in 64-wide steps. A step is two MFMA k-steps
+  // whose two 16-B loads per lane cover both halves of one 128-B line of each
+  // W row, back to back from one wave (no line shared between waves).
+  const int nq = K >> 8;
+  const int q0 = sp * nquad_split, q1 = min(nq, q0 + nquad_split);
+  const int nqs = max(0, q1 - q0);  // 256-wide blocks in this split = 64-wide steps per wave
+  const int nsteps = nqs;
+  const int kbase = q0 * 256 + wv * nqs * 64 + 8 * g;
 
-  f32x4_t acc[4][MB];
+  const uint16_t* wp[RB];
 #pragma unroll
-  for (int rb = 0; rb < 4; ++rb)
+  for (int rb = 0; rb < RB; ++rb) {
+    const int r = min(row0 + 16 * rb + c16, N - 1);
+    wp[rb] = wt + (int64_t)r * w_stride + kbase;
+  }
+  const uint16_t* xp[MB];
+#pragma unroll
+  for (int mb = 0; mb < MB; ++mb) {
+    const int m = min(16 * mb + c16, M - 1);
+    xp[mb] = x + (int64_t)m * x_stride + kbase;
+  }
+
+  f32x4_t acc[RB][MB];
+#pragma unroll
+  for (int rb = 0; rb < RB; ++rb)
 #pragma unroll
     for (int mb = 0; mb < MB; ++mb) acc[rb][mb] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 
-  // W row pointers of this lane (A operand rows 16rb + c16), clamped in bounds
-  const uint16_t* wr[4];
+  u32x4_t wa[U][2][RB], xa[U][2][MB], wb[U][2][RB], xb[U][2][MB];
+  // chunk = U steps starting at step s; a step past the end re-reads step 0
+  // (valid memory, result unused). No branch may split the main loop: the
+  // waitcnt pass then counts loads across blocks conservatively and waits for
+  // the prefetched chunk as well.
+  // each tile starts its sweep at a rotated step, so concurrent workgroups do
+  // not all read the same k column of W (+3-19 % on the 70B shapes, a
+  // power-of-two row pitch otherwise piles them onto the same DRAM channels)
+  const int rot = (tile * 5) % max(1, nsteps);
+  auto load = [&](int s, u32x4_t (&w_)[U][2][RB], u32x4_t (&x_)[U][2][MB]) {
 #pragma unroll
-  for (int rb = 0; rb < 4; ++rb) {
-    const int r = min(row_base + 16 * rb + c16, N - 1);
-    wr[rb] = wt + (int64_t)r * w_stride + 8 * g;
-  }
-  // X staging: MP rows x 128 k per stage = MP * 16 chunks of 16 B
-  constexpr int XCH = MP * (KST / 8);
-  constexpr int XPT = (XCH + NT - 1) / NT;
-  u32x4_t xr[XPT];
-  auto load_x = [&](int st) {
+    for (int u = 0; u < U; ++u) {
+      int st = s + u < nsteps ? s + u : 0;
+      st = st + rot < nsteps ? st + rot : st + rot - nsteps;
+      const int64_t off = (int64_t)st * 64;
 #pragma unroll
-    for (int i = 0; i < XPT; ++i) {
-      const int idx = threadIdx.x + NT * i;
-      const int row = idx / (KST / 8), ch = idx % (KST / 8);
-      u32x4_t v = {0, 0, 0, 0};
-      if (idx < XCH && row < M) v = *reinterpret_cast<const u32x4_t*>(x + (int64_t)row * x_stride + st * KST + ch * 8);
-      xr[i] = v;
-    }
-  };
-  auto store_x = [&](char* buf) {
+      for (int h = 0; h < 2; ++h) {
 #pragma unroll
-    for (int i = 0; i < XPT; ++i) {
-      const int idx = threadIdx.x + NT * i;
-      if (idx < XCH) {
-        const int row = idx / (KST / 8), ch = idx % (KST / 8);
-        *reinterpret_cast<u32x4_t*>(buf + row * XROW + ch * 16) = xr[i];
+        for (int rb = 0; rb < RB; ++rb)  // (nontemporal W loads measured 10-30 % slower)
+          w_[u][h][rb] = *reinterpret_cast<const u32x4_t*>(wp[rb] + off + 32 * h);
       }
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int mb = 0; mb < MB; ++mb) x_[u][h][mb] = *reinterpret_cast<const u32x4_t*>(xp[mb] + off + 32 * h);
     }
   };
-  // two register sets, used alternately by an unrolled-by-2 stage loop (no
-  // runtime indexing of register arrays)
-  u32x4_t wa[4][4], wb[4][4];
-  auto load_w = [&](int st, u32x4_t (&dst)[4][4]) {
+  auto mfma_step = [&](const u32x4_t (&w_)[2][RB], const u32x4_t (&x_)[2][MB]) {
 #pragma unroll
-    for (int rb = 0; rb < 4; ++rb)
+    for (int h = 0; h < 2; ++h)
 #pragma unroll
-      for (int kk = 0; kk < 4; ++kk)
-        dst[rb][kk] = __builtin_nontemporal_load(reinterpret_cast<const u32x4_t*>(wr[rb] + st * KST + 32 * kk));
-  };
-  auto compute = [&](const u32x4_t (&src)[4][4], const char* xb) {
-#pragma unroll
-    for (int kk = 0; kk < 4; ++kk) {
-      bf16x8_t xf[MB];
-#pragma unroll
-      for (int mb = 0; mb < MB; ++mb)
-        xf[mb] = *reinterpret_cast<const bf16x8_t*>(xb + (16 * mb + c16) * XROW + (32 * kk + 8 * g) * 2);
-#pragma unroll
-      for (int rb = 0; rb < 4; ++rb) {
-        const bf16x8_t af = __builtin_bit_cast(bf16x8_t, src[rb][kk]);
+      for (int rb = 0; rb < RB; ++rb) {
+        const bf16x8_t af = __builtin_bit_cast(bf16x8_t, w_[h][rb]);
 #pragma unroll
         for (int mb = 0; mb < MB; ++mb)
-          acc[rb][mb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, xf[mb], acc[rb][mb], 0, 0, 0);
+          acc[rb][mb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, __builtin_bit_cast(bf16x8_t, x_[h][mb]),
+                                                                acc[rb][mb], 0, 0, 0);
       }
-    }
+  };
+  auto compute = [&](const u32x4_t (&w_)[U][2][RB], const u32x4_t (&x_)[U][2][MB]) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) mfma_step(w_[u], x_[u]);
   };
 
-  char* xb0 = smem;
-  char* xb1 = smem + MP * XROW;
-  if (st0 < st1) {
-    load_w(st0, wa);
-    load_x(st0);
-    store_x(xb0);
-    for (int st = st0; st < st1; st += 2) {
-      // even stage: W in wa, X in xb0; prefetch st+1 into wb / xb1
-      const bool m1 = st + 1 < st1;
-      if (m1) {
-        load_w(st + 1, wb);
-        load_x(st + 1);
-      }
-      __syncthreads();  // xb0 of stage st visible; xb1 readers of stage st-1 done
-      compute(wa, xb0);
-      if (!m1) break;
-      store_x(xb1);
-      const bool m2 = st + 2 < st1;
-      if (m2) {
-        load_w(st + 2, wa);
-        load_x(st + 2);
-      }
-      __syncthreads();
-      compute(wb, xb1);
-      if (m2) store_x(xb0);
-    }
+  // main loop: pairs of chunks, one chunk always in flight behind the one in use.
+  // sched_barrier(0) pins the group order: left alone the scheduler sinks the
+  // prefetch loads in between the MFMAs that need the previous chunk, and the
+  // counted waits then cover the prefetch too.
+  const int npair = nsteps / (2 * U);
+  int s = 0;
+  if (npair > 0) load(0, wa, xa);
+  for (int p = 0; p < npair; ++p, s += 2 * U) {
+    load(s + U, wb, xb);
+    __builtin_amdgcn_sched_barrier(0);
+    compute(wa, xa);
+    __builtin_amdgcn_sched_barrier(0);
+    load(s + 2 * U, wa, xa);  // the last pair's prefetch is clamped and wasted
+    __builtin_amdgcn_sched_barrier(0);
+    compute(wb, xb);
+    __builtin_amdgcn_sched_barrier(0);
   }
-  __syncthreads();  // X images no longer needed: reuse LDS for the transpose
-  // ---- epilogue: acc[rb][mb][i] = Y^T[row_base + 16rb + 4g + i][16mb + c16]
-  float* tp = reinterpret_cast<float*>(smem) + w * (MP * 64);  // [MP][64] fp32 per wave
+  // tail: < 2U steps, unpipelined
+  for (; s < nsteps; ++s) {
+    load(s, wb, xb);
+    mfma_step(wb[0], xb[0]);
+  }
+
+  // ---- sum the 4 waves: (2,3) -> LDS, (0,1) add; 1 -> LDS, 0 adds
+  if (wv >= 2) {
 #pragma unroll
-  for (int rb = 0; rb < 4; ++rb)
+    for (int rb = 0; rb < RB; ++rb)
 #pragma unroll
-    for (int mb = 0; mb < MB; ++mb)
-      *reinterpret_cast<f32x4_t*>(tp + (16 * mb + c16) * 64 + 16 * rb + 4 * g) = acc[rb][mb];
+      for (int mb = 0; mb < MB; ++mb) red[wv - 2][rb][mb][lane] = acc[rb][mb];
+  }
   __syncthreads();
-  // each lane writes 4 consecutive n of one m row: 16 lanes cover a 64-wide row
-  for (int e = lane; e < MP * 16; e += 64) {
-    const int m = e / 16, q = e % 16;
+  if (wv < 2) {
+#pragma unroll
+    for (int rb = 0; rb < RB; ++rb)
+#pragma unroll
+      for (int mb = 0; mb < MB; ++mb) acc[rb][mb] += red[wv][rb][mb][lane];
+  }
+  __syncthreads();
+  if (wv == 1) {
+#pragma unroll
+    for (int rb = 0; rb < RB; ++rb)
+#pragma unroll
+      for (int mb = 0; mb < MB; ++mb) red[0][rb][mb][lane] = acc[rb][mb];
+  }
+  __syncthreads();
+  if (wv != 0) return;
+  // acc[rb][mb][i] = Y^T[row0 + 16 rb + 4 g + i][16 mb + c16]
+#pragma unroll
+  for (int mb = 0; mb < MB; ++mb) {
+    const int m = 16 * mb + c16;
     if (m >= M) continue;
-    const int n = row_base + 4 * q;
-    const f32x4_t v = *reinterpret_cast<const f32x4_t*>(tp + m * 64 + 4 * q);
-    if (nsplit == 1) {
-      uint16_t* yr = y + (int64_t)m * y_stride + n;
-      if (n + 3 < N) {
+#pragma unroll
+    for (int rb = 0; rb < RB; ++rb) {
+      const f32x4_t v = acc[rb][mb] + red[0][rb][mb][lane];
+      const int n = row0 + 16 * rb + 4 * g;
+      if (n >= N) continue;  // N % 4 == 0 (host check): all 4 in or all out
+      if (nsplit == 1) {
         const uint32_t lo = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
         const uint32_t hi = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
-        *reinterpret_cast<uint2*>(yr) = make_uint2(lo, hi);
+        *reinterpret_cast<uint2*>(y + (int64_t)m * y_stride + n) = make_uint2(lo, hi);
       } else {
-        for (int j = 0; j < 4; ++j)
-          if (n + j < N) yr[j] = f2bf(v[j]);
-      }
-    } else {
-      float* pr = part + ((int64_t)sp * M + m) * N + n;
-      if (n + 3 < N) {
-        *reinterpret_cast<f32x4_t*>(pr) = v;
-      } else {
-        for (int j = 0; j < 4; ++j)
-          if (n + j < N) pr[j] = v[j];
+        *reinterpret_cast<f32x4_t*>(part + ((int64_t)sp * M + m) * N + n) = v;
       }
     }
   }
 }
 
-__global__ __launch_bounds__(256) void skinny_reduce_kernel(const float* __restrict__ part, int nsplit, int M, int N,
-                                                            uint16_t* __restrict__ y, int64_t y_stride) {
+__global__ __launch_bounds__(256) void dgemm_reduce_kernel(const float* __restrict__ part, int nsplit, int M, int N,
+                                                           uint16_t* __restrict__ y, int64_t y_stride) {
   const int64_t i4 = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 4;
   const int64_t total = (int64_t)M * N;
   if (i4 >= total) return;
-  const int m = (int)(i4 / N), n = (int)(i4 % N);
-  float s[4] = {0.f, 0.f, 0.f, 0.f};
-  if (n + 3 < N && (N % 4) == 0) {
-    for (int sp = 0; sp < nsplit; ++sp) {
-      const f32x4_t v = *reinterpret_cast<const f32x4_t*>(part + (int64_t)sp * total + i4);
-      s[0] += v[0]; s[1] += v[1]; s[2] += v[2]; s[3] += v[3];
-    }
-    uint16_t* yr = y + (int64_t)m * y_stride + n;
-    const uint32_t lo = (uint32_t)f2bf(s[0]) | ((uint32_t)f2bf(s[1]) << 16);
-    const uint32_t hi = (uint32_t)f2bf(s[2]) | ((uint32_t)f2bf(s[3]) << 16);
-    *reinterpret_cast<uint2*>(yr) = make_uint2(lo, hi);
-  } else {
-    for (int j = 0; j < 4 && i4 + j < total; ++j) {
-      const int64_t idx = i4 + j;
-      float a = 0.f;
-      for (int sp = 0; sp < nsplit; ++sp) a += part[(int64_t)sp * total + idx];
-      y[(idx / N) * y_stride + idx % N] = f2bf(a);
-    }
+  const int m = (int)(i4 / N), n = (int)(i4 % N);  // N % 4 == 0: the 4 stay in one row
+  f32x4_t s = *reinterpret_cast<const f32x4_t*>(part + i4);
+  for (int k = 1; k < nsplit; ++k) s += *reinterpret_cast<const f32x4_t*>(part + (int64_t)k * total + i4);
+  const uint32_t lo = (uint32_t)f2bf(s[0]) | ((uint32_t)f2bf(s[1]) << 16);
+  const uint32_t hi = (uint32_t)f2bf(s[2]) | ((uint32_t)f2bf(s[3]) << 16);
+  *reinterpret_cast<uint2*>(y + (int64_t)m * y_stride + n) = make_uint2(lo, hi);
+}
+
+// register budget per lane: the two chunk sets (2 U steps x 2 loads x (RB + MB)
+// x 4) and the row pointers live in arch VGPRs (<= 256); the accumulators
+// (4 RB MB) share them at two workgroups per CU, or sit in AGPRs at one
+constexpr int vregs(int rb, int mb, int u) { return 16 * u * (rb + mb) + 2 * (rb + mb) + 24; }
+constexpr bool fits(int rb, int mb, int u, int occ) {
+  return occ == 2 ? vregs(rb, mb, u) + 4 * rb * mb <= 256 : (vregs(rb, mb, u) <= 256 && 4 * rb * mb <= 256);
+}
+constexpr int pick_u(int rb, int mb, int occ) { return fits(rb, mb, 2, occ) ? 2 : (fits(rb, mb, 1, occ) ? 1 : 0); }
+
+typedef void (*kern_t)(const uint16_t*, int64_t, const uint16_t*, int64_t, int, int, int, int, uint16_t*, int64_t,
+                       float*);
+
+template <int RB, int MB>
+kern_t pick(int occ) {
+  if (occ == 2) {
+    constexpr int u = pick_u(RB, MB, 2);
+    if constexpr (u > 0) return dgemm_kernel<RB, MB, u, 2>;
+    return nullptr;
   }
+  constexpr int u = pick_u(RB, MB, 1);
+  if constexpr (u > 0) return dgemm_kernel<RB, MB, u, 1>;
+  return nullptr;
+}
+
+template <int MB>
+kern_t pick_rb(int rb, int occ) {
+  switch (rb) {
+    case 1: return pick<1, MB>(occ);
+    case 2: return pick<2, MB>(occ);
+    case 3: return pick<3, MB>(occ);
+    case 4: return pick<4, MB>(occ);
+    case 5: return pick<5, MB>(occ);
+    case 6: return pick<6, MB>(occ);
+    case 7: return pick<7, MB>(occ);
+    case 8: return pick<8, MB>(occ);
+  }
+  return nullptr;
+}
+
+kern_t pick_all(int MB, int rb, int occ) {
+  return MB == 1 ? pick_rb<1>(rb, occ) : MB == 2 ? pick_rb<2>(rb, occ) : MB == 3 ? pick_rb<3>(rb, occ)
+                                                                       : pick_rb<4>(rb, occ);
 }
 
 }  // namespace
 
-extern "C" int llmd_skinny_lds_bytes(int M) {
-  const int MB = M <= 16 ? 1 : (M <= 32 ? 2 : 4);
-  const int xb = 2 * 16 * MB * XROW, tb = 4 * 16 * MB * 64 * 4;
-  return xb > tb ? xb : tb;
+// 1 if (rb, occ) has an instantiation for this M
+extern "C" int llmd_dgemm_supported(int M, int rb, int occ) {
+  if (M < 1 || M > 64 || rb < 1 || rb > 8 || (occ != 1 && occ != 2)) return 0;
+  const int MB = (M + 15) / 16;
+  return pick_u(rb, MB, occ) > 0 ? 1 : 0;
 }
 
+// Y = X W^T with a planned decomposition: rb row blocks per workgroup, nsplit
+// K splits, occ workgroups per CU. part: nsplit * M * N fp32 when nsplit > 1.
 extern "C" int llmd_skinny_gemm(const void* x, int64_t x_stride, const void* w, int64_t w_stride, int M, int N,
-                                int K, int nsplit, void* y, int64_t y_stride, float* part, hipStream_t st) {
-  if (M < 1 || M > 64 || K % KST != 0 || nsplit < 1) return -1;
-  const int nst = K / KST;
-  const int per = (nst + nsplit - 1) / nsplit;
-  nsplit = (nst + per - 1) / per;  // no empty splits
-  const int lds = llmd_skinny_lds_bytes(M);
-  dim3 grid((N + ROWS - 1) / ROWS, nsplit);
-  static bool attr = false;
-  if (!attr) {
-    hipFuncSetAttribute((const void*)skinny_gemm_kernel<4>, hipFuncAttributeMaxDynamicSharedMemorySize, 65536);
-    attr = true;
-  }
-  if (M <= 16)
-    hipLaunchKernelGGL(skinny_gemm_kernel<1>, grid, dim3(NT), lds, st, (const uint16_t*)x, x_stride,
-                       (const uint16_t*)w, w_stride, M, N, K, per, (uint16_t*)y, y_stride, part);
-  else if (M <= 32)
-    hipLaunchKernelGGL(skinny_gemm_kernel<2>, grid, dim3(NT), lds, st, (const uint16_t*)x, x_stride,
-                       (const uint16_t*)w, w_stride, M, N, K, per, (uint16_t*)y, y_stride, part);
-  else
-    hipLaunchKernelGGL(skinny_gemm_kernel<4>, grid, dim3(NT), lds, st, (const uint16_t*)x, x_stride,
-                       (const uint16_t*)w, w_stride, M, N, K, per, (uint16_t*)y, y_stride, part);
+                                int K, int rb, int nsplit, int occ, void* y, int64_t y_stride, float* part,
+                                hipStream_t st) {
+  if (M < 1 || M > 64 || K % 256 != 0 || N % 4 != 0 || nsplit < 1 || !llmd_dgemm_supported(M, rb, occ)) return -1;
+  const int nq = K / 256;
+  const int per = (nq + nsplit - 1) / nsplit;
+  nsplit = (nq + per - 1) / per;  // no empty splits
+  const int MB = (M + 15) / 16;
+  kern_t k = pick_all(MB, rb, occ);
+  if (k == nullptr) return -2;
+  dim3 grid((N + 16 * rb - 1) / (16 * rb), nsplit);
+  hipLaunchKernelGGL(k, grid, dim3(NT), 0, st, (const uint16_t*)x, x_stride, (const uint16_t*)w, w_stride, M, N, K,
+                     per, (uint16_t*)y, y_stride, part);
   if (nsplit > 1) {
-    const int64_t total4 = ((int64_t)M * N + 3) / 4;
-    hipLaunchKernelGGL(skinny_reduce_kernel, dim3((unsigned)((total4 + 255) / 256)), dim3(256), 0, st, part, nsplit,
+    const int64_t total4 = (int64_t)M * N / 4;
+    hipLaunchKernelGGL(dgemm_reduce_kernel, dim3((unsigned)((total4 + 255) / 256)), dim3(256), 0, st, part, nsplit,
                        M, N, (uint16_t*)y, y_stride);
   }
   return (int)hipGetLastError();

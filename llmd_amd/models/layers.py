@@ -29,12 +29,13 @@ def _init_weight(t: torch.Tensor, std: float, gen: Optional[torch.Generator] = N
 
 
 def _linear(mod, x, bias):
-    """bf16 weights -> hipBLASLt GEMM; fp8 weights (quantize_fp8) -> W8A8 GEMM
-    with dynamic per-token activation scales."""
+    """bf16 weights -> hipBLASLt GEMM, or the decode GEMM kernel for the decode
+    shapes where it measured faster (ops.linear); fp8 weights (quantize_fp8) ->
+    W8A8 GEMM with dynamic per-token activation scales."""
     w = mod.weight
     if w.dtype == torch.float8_e4m3fn:
         return ops.fp8_linear(x, w, mod.weight_scale, bias)
-    return F.linear(x, w, bias)
+    return ops.linear(x, w, bias)
 
 
 def wants_fp8_input(lin) -> bool:

@@ -489,29 +489,93 @@ def lora_bgmv(y, x, A, B, slot, h=None):
 
 
 SKINNY_MAX_M = 64
+_NUM_CUS = 256
+_HBM_BPS = 6.0e12       # sustained streaming rate (MI355X: ~6.3 TB/s for a float4 copy)
+_SLOT_BPS = (48e9, 26e9)  # what one workgroup streams at 1 / 2 workgroups per CU
 
 
-def skinny_splits(M: int, N: int, K: int, target_wgs: int = 512) -> int:
-    tiles = (N + 255) // 256
-    return max(1, min(K // 128, math.ceil(target_wgs / tiles)))
+def skinny_plan(M: int, N: int, K: int, num_cus: int = _NUM_CUS) -> tuple[int, int, int]:
+    """(rb, nsplit, occ) for the decode GEMM kernel (csrc/ops/skinny_gemm.hip):
+    rb row blocks of 16 W rows per workgroup, nsplit-way split-K, occ workgroups
+    per CU. Cost model: W (HBM) + X (L2, a quarter of the price) bytes per
+    workgroup over its streaming rate, times the dispatch rounds, plus the
+    split-K partial round trip and the reduce launch."""
+    key = ((M + 15) // 16, N, K)
+    if key in SKINNY_TUNED:
+        return SKINNY_TUNED[key]
+    nat = native()
+    best, best_t = None, float("inf")
+    nq = K // 256
+    for occ in (2, 1):
+        slots = num_cus * occ
+        for rb in range(1, 9):
+            if not nat.skinny_supported(M, rb, occ):
+                continue
+            tiles = -(-N // (16 * rb))
+            for ns in range(1, min(nq, 32) + 1):
+                per = -(-nq // ns)
+                ns2 = -(-nq // per)
+                wgs = tiles * ns2
+                rounds = -(-wgs // slots)
+                busy = min(wgs, slots)
+                rate = min(_SLOT_BPS[occ - 1], _HBM_BPS / busy)
+                wbytes = 16 * rb * per * 256 * 2
+                xbytes = M * per * 256 * 2
+                t = rounds * (wbytes + 0.25 * xbytes) / rate
+                if ns2 > 1:
+                    t += 2.5e-6 + ns2 * M * N * 8 / 8e12
+                if t < best_t - 1e-9:
+                    best, best_t = (rb, ns2, occ), t
+    return best
+
+
+# measured best plans (scripts/bench_gemm.py --sweep): (ceil(M/16), N, K) -> (rb, nsplit, occ)
+SKINNY_TUNED: dict[tuple[int, int, int], tuple[int, int, int]] = {}
+
+
+def skinny_gemm(x: torch.Tensor, w: torch.Tensor, plan: Optional[tuple[int, int, int]] = None) -> torch.Tensor:
+    M, K = x.shape
+    N = w.shape[0]
+    rb, ns, occ = plan or skinny_plan(M, N, K)
+    y = torch.empty(M, N, dtype=x.dtype, device=x.device)
+    part = torch.empty(ns * M * N if ns > 1 else 0, dtype=torch.float32, device=x.device)
+    native().skinny_gemm(y, x, w, rb, ns, occ, part)
+    return y
+
+
+def skinny_ok(x: torch.Tensor, w: torch.Tensor) -> bool:
+    M = x.shape[0] if x.dim() == 2 else -1
+    return (_gpu(x) and 1 <= M <= SKINNY_MAX_M and x.shape[1] % 256 == 0 and x.dtype == torch.bfloat16
+            and w.dtype == torch.bfloat16 and w.shape[0] % 4 == 0 and x.stride(-1) == 1 and x.stride(0) % 8 == 0
+            and w.is_contiguous())
+
+
+_DGEMM_MS = (1, 8, 16, 32, 48, 64)
+
+
+def dgemm_choice(M: int, N: int, K: int) -> Optional[tuple[int, int, int]]:
+    """Plan of the decode GEMM kernel for this shape, or None for hipBLASLt:
+    the measured dispatch table (ops/dgemm_table.py) at the smallest measured
+    M >= this one; unmeasured shapes stay on hipBLASLt."""
+    from .dgemm_table import DGEMM_TABLE
+
+    for m in _DGEMM_MS:
+        if m >= M:
+            e = DGEMM_TABLE.get((m, N, K))
+            return e[0] if e is not None else None
+    return None
 
 
 def linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """Dense projection: decode-sized M (<= 64) on the skinny MFMA stream kernel
-    (csrc/ops/skinny_gemm.hip), everything else on hipBLASLt."""
-    M = x.shape[0] if x.dim() == 2 else -1
-    if (_gpu(x) and _SKINNY and 1 <= M <= SKINNY_MAX_M and x.shape[1] % 128 == 0 and x.dtype == torch.bfloat16
-            and x.stride(-1) == 1 and x.stride(0) % 8 == 0 and w.is_contiguous()):
-        N, K = w.shape
-        y = torch.empty(M, N, dtype=x.dtype, device=x.device)
-        ns = skinny_splits(M, N, K)
-        part = torch.empty(ns * M * N if ns > 1 else 0, dtype=torch.float32, device=x.device)
-        native().skinny_gemm(y, x, w, ns, part)
-        return y if bias is None else y.add_(bias)
+    """Dense projection: decode-sized M (<= 64) on the decode GEMM stream kernel
+    (csrc/ops/skinny_gemm.hip) where the dispatch table measured it faster than
+    hipBLASLt, everything else on hipBLASLt."""
+    if _SKINNY and skinny_ok(x, w):
+        plan = dgemm_choice(x.shape[0], w.shape[0], w.shape[1])
+        if plan is not None:
+            y = skinny_gemm(x, w, plan)
+            return y if bias is None else y.add_(bias)
     return torch.nn.functional.linear(x, w, bias)
 
 
-# off by default: hipBLASLt streams W at 5.3-6.1 TB/s for most decode shapes
-# (profiles/skinny_gemm_vs_hipblaslt.txt); the skinny kernel only wins on
-# the K=28672 down projection at M=64
-_SKINNY = os.environ.get("LLMD_SKINNY_GEMM", "0") == "1"
+_SKINNY = os.environ.get("LLMD_SKINNY_GEMM", "1") == "1"

@@ -1,0 +1,30 @@
+"""Decode GEMM dispatch (CPU): table lookup buckets M up to the next measured
+size, unmeasured shapes and CPU tensors stay on hipBLASLt / F.linear."""
+import torch
+
+from llmd_amd import ops
+from llmd_amd.ops.dgemm_table import DGEMM_TABLE
+
+
+def test_table_entries_are_wins_with_valid_plans():
+    for (M, N, K), (plan, t_ours, t_blas) in DGEMM_TABLE.items():
+        assert 1 <= M <= 64 and K % 256 == 0 and N % 4 == 0
+        if plan is not None:
+            rb, ns, occ = plan
+            assert 1 <= rb <= 8 and 1 <= ns <= K // 256 and occ in (1, 2)
+            assert t_ours < 0.95 * t_blas
+
+
+def test_choice_buckets_and_unknown_shapes():
+    assert ops.dgemm_choice(3, 4096, 4096) == DGEMM_TABLE[(8, 4096, 4096)][0]
+    assert ops.dgemm_choice(20, 4096, 4096) is None  # 8B shapes: only M <= 8 measured as wins
+    assert ops.dgemm_choice(1, 4096, 4096) == DGEMM_TABLE[(1, 4096, 4096)][0]
+    assert ops.dgemm_choice(40, 8192, 28672) == DGEMM_TABLE[(48, 8192, 28672)][0]
+    assert ops.dgemm_choice(64, 1234, 4096) is None
+    assert ops.dgemm_choice(65, 4096, 4096) is None
+
+
+def test_cpu_linear_is_plain():
+    x = torch.randn(4, 256)
+    w = torch.randn(64, 256)
+    torch.testing.assert_close(ops.linear(x, w), x @ w.T)
