@@ -400,9 +400,13 @@ class ScaleFromZero:
 class WVAEngine:
     """Runs the pipeline over all pools once per interval (default 30 s)."""
 
-    def __init__(self, config: Optional[dict] = None, actuator=None, gpu_budget: Optional[int] = None):
+    def __init__(self, config: Optional[dict] = None, actuator=None, gpu_budget: Optional[int] = None,
+                 elector=None):
         cfg = dict(config or {})
         self.cfg = cfg
+        # HA (--leader-elect, wva.md:397-400): only the lease holder analyses and
+        # actuates; standbys keep nothing that a takeover would need
+        self.elector = elector
         name = cfg.get("analyzerName", "")
         if cfg.get("sloMultiplier") is not None or cfg.get("targetTTFT") is not None:
             self.analyzer = SLOAnalyzer(**cfg)
@@ -420,6 +424,8 @@ class WVAEngine:
 
     def step(self, pools: dict[str, list[Variant]], epp_queue: Optional[dict[str, float]] = None,
              requests_in_retention: Optional[dict[str, float]] = None) -> dict[str, dict[str, int]]:
+        if self.elector is not None and not self.elector.is_leader:
+            return {}
         epp_queue = epp_queue or {}
         reqs = {}
         for m, vs in pools.items():
@@ -442,6 +448,8 @@ class WVAEngine:
         return decisions
 
     def fast_step(self, pools: dict[str, list[Variant]], epp_queue: dict[str, float]):
+        if self.elector is not None and not self.elector.is_leader:
+            return
         for m, vs in pools.items():
             d = self.sfz.check(vs, epp_queue.get(m, 0.0))
             if d is not None:

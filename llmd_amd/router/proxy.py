@@ -8,6 +8,11 @@ Failure semantics: InferencePool ``failureMode`` FailOpen (route to a random
 healthy endpoint if the EPP itself errors) or FailClose (503);
 EPP-generated rejections carry ``x-llm-d-request-dropped-reason``.
 
+High availability (configuration.md:455-459, active-passive): with
+``--ha-enable-leader-election`` every replica campaigns for a lease
+(llmd_amd.utils.leader); only the leader reports ready on /health and serves
+inference, standbys answer 503 until they take over.
+
 CLI (mirrors the EPP flags, guides/no-kubernetes-deployment/README.md:153-190):
   python -m llmd_amd.router.proxy --config-file epp.yaml --endpoints-file endpoints.yaml \
       --port 8081 --metrics-port 9090 --pool-name pool
@@ -40,11 +45,16 @@ HOP = {"host", "content-length", "transfer-encoding", "connection", "keep-alive"
 
 
 class RouterProxy:
-    def __init__(self, epp: EPP, failure_mode: str = "FailClose", timeout: float = 1000.0):
+    def __init__(self, epp: EPP, failure_mode: str = "FailClose", timeout: float = 1000.0, elector=None):
         self.epp = epp
         self.failure_mode = failure_mode
         self.timeout = timeout
         self.session: Optional[aiohttp.ClientSession] = None
+        self.elector = elector  # utils.leader.LeaseElector when HA is on
+
+    @property
+    def active(self) -> bool:
+        return self.elector is None or self.elector.is_leader
 
     async def _session(self):
         if self.session is None:
@@ -64,8 +74,12 @@ class RouterProxy:
 
     async def _on_start(self, app):
         await self.epp.start()
+        if self.elector is not None:
+            self.elector.start()
 
     async def _on_stop(self, app):
+        if self.elector is not None:
+            self.elector.stop()
         await self.epp.stop()
         if self.session:
             await self.session.close()
@@ -74,11 +88,16 @@ class RouterProxy:
         return web.Response(body=self.epp.render_metrics(), content_type="text/plain")
 
     async def health(self, req):
+        if not self.active:
+            return web.Response(text="standby", status=503)
         return web.Response(text="ok" if self.epp.store.all() else "no endpoints",
                             status=200 if self.epp.store.all() else 503)
 
     async def handle(self, req: web.Request):
         path = "/" + req.match_info["tail"]
+        if not self.active:
+            return web.json_response({"error": {"message": "endpoint picker standby (not the HA leader)"}},
+                                     status=503, headers={"x-llm-d-epp-role": "standby"})
         body = await req.read()
         if req.method != "POST" or path not in INFERENCE_PATHS:
             return await self._passthrough(req, path, body)
@@ -193,6 +212,12 @@ def main(argv=None):
     p.add_argument("--port", type=int, default=8081)
     p.add_argument("--metrics-port", type=int, default=9090)
     p.add_argument("--failure-mode", default="FailOpen", choices=["FailOpen", "FailClose"])
+    p.add_argument("--ha-enable-leader-election", action="store_true",
+                   help="active-passive HA: only the lease holder serves")
+    p.add_argument("--ha-lease-file", default=None, help="lease record shared by the replicas")
+    p.add_argument("--ha-lease-duration", type=float, default=15.0)
+    p.add_argument("--ha-renew-deadline", type=float, default=10.0)
+    p.add_argument("--ha-retry-period", type=float, default=2.0)
     p.add_argument("--v", type=int, default=1)
     a = p.parse_args(argv)
     logging.basicConfig(level=logging.DEBUG if a.v >= 3 else logging.INFO)
@@ -202,7 +227,14 @@ def main(argv=None):
         cp.load_yaml(open(a.control_plane).read())
     store = EndpointStore()
     epp = EPP(text, store, cp, a.pool_name)
-    prox = RouterProxy(epp, a.failure_mode)
+    elector = None
+    if a.ha_enable_leader_election:
+        from llmd_amd.utils.leader import LeaseElector
+
+        elector = LeaseElector(a.ha_lease_file or f"/tmp/llmd-epp-{a.pool_namespace}-{a.pool_name}.lease",
+                               lease_duration=a.ha_lease_duration, renew_deadline=a.ha_renew_deadline,
+                               retry_period=a.ha_retry_period)
+    prox = RouterProxy(epp, a.failure_mode, elector=elector)
     app = prox.app()
 
     async def seed(app):
