@@ -379,22 +379,51 @@ __global__ __launch_bounds__(NT, 2) void prefill_v2_kernel(
 #pragma unroll
     for (int n = 0; n < NB; ++n) o[nb][n] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 
-  // DMA: NI K + NI V wave-instructions of 1 KB (1024 / RB rows); wave w issues j = w + 4i
+  // DMA: NI K + NI V wave-instructions of 1 KB (1024 / RB rows); wave w issues
+  // j = w + 4i. The per-lane source offsets inside a 64-row tile are constant
+  // (row * RB + swizzled 16-B slot), so a tile costs one scalar base (block
+  // table lookup) plus a VGPR offset per load (global_load_lds saddr+voffset,
+  // -12 % VALU instructions); only a sequence's last, partial tile clamps rows
+  // (its V rows past the end must stay finite: P = 0 there, but 0 * NaN would
+  // poison O).
+  const int ws = __builtin_amdgcn_readfirstlane(w);
+  uint32_t koff[NI / 4], voff[NI / 4];
+#pragma unroll
+  for (int i = 0; i < NI / 4; ++i) {
+    const int u = 64 * (w + 4 * i) + lane;
+    const int row = u / (D / 8), sl = u % (D / 8);
+    koff[i] = (uint32_t)(row * RB + 16 * (sl ^ p2_pk<D>(row)));
+    voff[i] = (uint32_t)(row * RB + 16 * (sl ^ p2_pv<D>(row)));
+  }
   auto issue = [&](char* base, int t) {
     const int ts = t * 64;
-    const int64_t toff = (int64_t)bt[ts >> lbs] * block_stride + head_off + (int64_t)(ts & (bs - 1)) * D;
+    const int64_t tb = 2 * ((int64_t)bt[ts >> lbs] * block_stride + head_off + (int64_t)(ts & (bs - 1)) * D);
+    const char* kb = reinterpret_cast<const char*>(kc) + tb;
+    const char* vb = reinterpret_cast<const char*>(vc) + tb;
     const int rlim = ctx - 1 - ts;
+    if (rlim >= 63) {
 #pragma unroll
-    for (int i = 0; i < NI / 4; ++i) {
-      const int j = w + 4 * i;
-      const int u = 64 * j + lane;
-      const int row = u / (D / 8), sl = u % (D / 8);
-      const int64_t ro = toff + (int64_t)min(row, rlim) * D;
-      __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)(kc + ro + 8 * (sl ^ p2_pk<D>(row))),
-                                       (void __attribute__((address_space(3)))*)(base + 1024 * j), 16, 0, 0);
-      __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)(vc + ro + 8 * (sl ^ p2_pv<D>(row))),
-                                       (void __attribute__((address_space(3)))*)(base + P2_IMG + 1024 * j), 16, 0,
-                                       0);
+      for (int i = 0; i < NI / 4; ++i) {
+        char* dst = base + 1024 * (ws + 4 * i);
+        __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)(kb + koff[i]),
+                                         (void __attribute__((address_space(3)))*)dst, 16, 0, 0);
+        __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)(vb + voff[i]),
+                                         (void __attribute__((address_space(3)))*)(dst + P2_IMG), 16, 0, 0);
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < NI / 4; ++i) {
+        const int u = 64 * (w + 4 * i) + lane;
+        const int row = u / (D / 8), sl = u % (D / 8);
+        const int64_t ro = (int64_t)min(row, rlim) * RB;
+        char* dst = base + 1024 * (ws + 4 * i);
+        __builtin_amdgcn_global_load_lds(
+            (const void __attribute__((address_space(1)))*)(kb + ro + 16 * (sl ^ p2_pk<D>(row))),
+            (void __attribute__((address_space(3)))*)dst, 16, 0, 0);
+        __builtin_amdgcn_global_load_lds(
+            (const void __attribute__((address_space(1)))*)(vb + ro + 16 * (sl ^ p2_pv<D>(row))),
+            (void __attribute__((address_space(3)))*)(dst + P2_IMG), 16, 0, 0);
+      }
     }
   };
   // per-lane LDS offsets (see the header): K rows 16 b4 + srow, chunk 4s + g;
@@ -595,8 +624,11 @@ extern "C" int llmd_paged_prefill(const void* q, int64_t q_stride, const void* k
   return 0;
 }
 
-// tokens per work item for a given GQA group size (host helper, mirrors the kernel)
-extern "C" int llmd_prefill_tokens_per_item(int Hq, int Hkv) {
+// tokens per work item (host helper, mirrors the kernel llmd_paged_prefill
+// dispatches: 32 query tokens per wave, 4 / HPW waves stacked along the
+// tokens for every variant; D, block size and fp8 select among v1 / v2 but
+// not the item shape)
+extern "C" int llmd_prefill_tokens_per_item(int Hq, int Hkv, int /*D*/, int /*bs*/, int /*fp8*/) {
   const int G = Hq / Hkv;
   const int HPW = (G % 4 == 0) ? 4 : ((G % 2 == 0) ? 2 : 1);
   return 32 * (4 / HPW);

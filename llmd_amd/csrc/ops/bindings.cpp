@@ -26,7 +26,7 @@ int llmd_paged_decode(const void*, int64_t, const void*, const void*, int64_t, i
 int llmd_paged_prefill(const void*, int64_t, const void*, const void*, int64_t, int, const int*, int,
                        const int*, const int*, const int*, const int*, int, int, int, int, float,
                        int, const float*, void*, int64_t, int, float, float, hipStream_t);
-int llmd_prefill_tokens_per_item(int, int);
+int llmd_prefill_tokens_per_item(int, int, int, int, int);
 void llmd_sample(const void*, int64_t, int, int, int, const float*, const int64_t*, int64_t*, float*,
                  hipStream_t);
 void llmd_topk_topp_mask(float*, int64_t, int, int, const int*, const float*, const float*,
@@ -727,7 +727,9 @@ PYBIND11_MODULE(_C, m) {
   m.def("gated_act", &gated_act);
   m.def("paged_decode", &paged_decode);
   m.def("paged_prefill", &paged_prefill);
-  m.def("prefill_tokens_per_item", &llmd_prefill_tokens_per_item);
+  m.def("prefill_tokens_per_item", [](int64_t Hq, int64_t Hkv, int64_t D, int64_t bs, bool fp8) {
+    return llmd_prefill_tokens_per_item((int)Hq, (int)Hkv, (int)D, (int)bs, fp8 ? 1 : 0);
+  });
   m.def("sample", &sample);
   m.def("topk_topp_mask", &topk_topp_mask);
   m.def("kvx_copy_blocks", &kvx_copy_blocks);

@@ -254,7 +254,8 @@ class ModelRunner:
         self.model.compute_logits(h[: min(len(ql), self.cfg.sched.max_num_seqs)])
 
     def _items(self, q_len, ctx_len):
-        tpi = ops.prefill_tokens_per_item(self.Hq, self.Hkv)
+        tpi = ops.prefill_tokens_per_item(self.Hq, self.Hkv, self.D, self.cfg.cache.block_size,
+                                          self.kv_dtype == torch.float8_e4m3fn)
         it = ops.build_prefill_items(list(q_len), list(ctx_len), tpi)
         return torch.tensor(it, dtype=torch.int32).view(-1, 2).to(self.device, non_blocking=True)
 

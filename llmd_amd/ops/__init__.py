@@ -94,10 +94,15 @@ def gated_act(x: torch.Tensor, mode: int = ACT_SILU, alpha: float = 1.702, limit
 
 
 # ---------------------------------------------------------------- attention
-def prefill_tokens_per_item(Hq: int, Hkv: int) -> int:
-    G = Hq // Hkv
-    hpw = 4 if G % 4 == 0 else (2 if G % 2 == 0 else 1)
-    return 32 * (4 // hpw)
+def prefill_tokens_per_item(Hq: int, Hkv: int, D: int = 128, block_size: int = 64, fp8: bool = False) -> int:
+    """Query tokens per prefill work item of the kernel the native dispatcher
+    picks for these arguments (the native helper is the single source)."""
+    try:
+        return int(native().prefill_tokens_per_item(Hq, Hkv, D, block_size, fp8))
+    except (ImportError, OSError):  # CPU-only environment: the reference path ignores items
+        G = Hq // Hkv
+        hpw = 4 if G % 4 == 0 else (2 if G % 2 == 0 else 1)
+        return 32 * (4 // hpw)
 
 
 def decode_split_plan(max_ctx: int, batch: int, Hkv: int, G: int, num_cus: int = 256,
@@ -170,7 +175,7 @@ def paged_prefill(q, k_cache, v_cache, block_tables, q_start, q_len, ctx_len, Hq
     if out is None:
         out = torch.empty(q.shape[0], Hq * D, dtype=q.dtype, device=q.device)
     if items is None:
-        tpi = prefill_tokens_per_item(Hq, Hkv)
+        tpi = prefill_tokens_per_item(Hq, Hkv, D, k_cache.shape[-2], k_cache.dtype == torch.float8_e4m3fn)
         it = build_prefill_items(q_len.tolist(), ctx_len.tolist(), tpi)
         items = torch.tensor(it, dtype=torch.int32).view(-1, 2).to(q.device, non_blocking=True)
     native().paged_prefill(out, q, k_cache, v_cache, block_tables, q_start, q_len, ctx_len, items,

@@ -63,7 +63,7 @@ def prefill(ctx, q_len, Hq, Hkv, D, bs, check=False):
     q_start = torch.tensor([0], dtype=torch.int32, device=dev)
     ql = torch.tensor([q_len], dtype=torch.int32, device=dev)
     cl = torch.tensor([ctx], dtype=torch.int32, device=dev)
-    tpi = ops.prefill_tokens_per_item(Hq, Hkv)
+    tpi = ops.prefill_tokens_per_item(Hq, Hkv, D, bs, KV_DTYPE == torch.float8_e4m3fn)
     items = torch.tensor(ops.build_prefill_items([q_len], [ctx], tpi), dtype=torch.int32, device=dev).view(-1, 2)
     scale = D ** -0.5
     out = torch.empty(q_len, Hq * D, device=dev, dtype=torch.bfloat16)

@@ -1,0 +1,7 @@
+# Prefill/decode attention: numerics tests, then the kernel microbenchmarks.
+set -o pipefail
+mkdir -p gpurun_out
+timeout -k 10 400 python -u -m pytest tests/test_kernels_gpu.py tests/test_fp8_kv.py -x -q --timeout 120 --timeout-method thread -k "prefill or attention or window" > gpurun_out/attn_tests.log 2>&1 || { echo "attn tests failed"; tail -40 gpurun_out/attn_tests.log; exit 1; }
+tail -1 gpurun_out/attn_tests.log
+timeout -k 10 300 python -u scripts/bench_attn.py --check > gpurun_out/attn_bench.log 2>&1 || { echo "bench failed"; tail -20 gpurun_out/attn_bench.log; exit 1; }
+grep -v amdgpu.ids gpurun_out/attn_bench.log
