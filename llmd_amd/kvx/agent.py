@@ -21,6 +21,11 @@ Side channel: length-prefixed msgpack request/response over TCP
 (VLLM_NIXL_SIDE_CHANNEL_HOST/PORT semantics; default port 5557).
 Fault injection: LLMD_KVX_FAULT=drop|delay:<s>|corrupt (probability
 LLMD_KVX_FAULT_P, default 1.0) for the failure-policy tests.
+Concurrency (the UCCL multi-path role, SURVEY N04, on one node): pulls run on
+``LLMD_KVX_WORKERS`` (default 4) transfer threads, each with its own HIP
+stream, so KV from different prefillers - different xGMI links - lands in
+parallel instead of queueing behind one copy; a peer's connection, metadata
+and pool mapping are set up once under a lock and shared by the workers.
 Prefiller liveness (SGLang-style heartbeat, SURVEY M13,
 operations-sglang.md:93-98): the decode side pings every known prefiller
 every ``LLMD_KVX_HEARTBEAT_S`` (5 s) on a fresh connection; after
@@ -94,7 +99,8 @@ LEGACY_IPC_MAX = 4 << 30  # hipIpcOpenMemHandle hangs importing larger allocatio
 class KvxAgent:
     def __init__(self, kv: torch.Tensor, engine_id: Optional[str] = None, host: Optional[str] = None,
                  port: int = 0, tp_rank: int = 0, tp_size: int = 1, abort_timeout: float = 480.0,
-                 transport: str = "auto", metrics=None, vmm: Optional[dict] = None, exports: bool = True):
+                 transport: str = "auto", metrics=None, vmm: Optional[dict] = None, exports: bool = True,
+                 workers: Optional[int] = None):
         self.kv = kv                      # [num_blocks, L, 2, Hkv, bs, D]
         self.vmm = vmm                    # chunked exportable pool (model_runner._alloc_cache)
         self.engine_id = engine_id or f"kvx-{uuid.uuid4().hex[:12]}"
@@ -139,9 +145,13 @@ class KvxAgent:
                                port or int(os.environ.get("VLLM_NIXL_SIDE_CHANNEL_PORT", "0") or 0)), self)
         self.port = self.server.server_address[1]
         threading.Thread(target=self.server.serve_forever, daemon=True, name="kvx-side-channel").start()
-        self.worker = threading.Thread(target=self._work, daemon=True, name="kvx-transfer")
-        self.stream = None
-        self.worker.start()
+        self.peer_lock = threading.Lock()   # peers / ipc_maps setup, shared by the workers
+        self._tls = threading.local()       # per-worker HIP stream
+        self.n_workers = max(1, int(workers or os.environ.get("LLMD_KVX_WORKERS", "4")))
+        self.workers = [threading.Thread(target=self._work, daemon=True, name=f"kvx-transfer-{i}")
+                        for i in range(self.n_workers)]
+        for t in self.workers:
+            t.start()
         self.hb_interval = float(os.environ.get("LLMD_KVX_HEARTBEAT_S", "5"))
         self.hb_max_fails = int(os.environ.get("LLMD_KVX_HEARTBEAT_FAILS", "2"))
         self.hb_fails: dict[tuple, int] = {}
@@ -275,15 +285,16 @@ class KvxAgent:
         self.known_peers.add(key)
         if key in self.dead_peers:
             raise RuntimeError(f"prefiller {host}:{port} failed its heartbeat")
-        p = self.peers.get(key)
-        if p is None:
-            s = socket.create_connection(key, timeout=10)
-            s.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
-            _send(s, {"op": "meta"})
-            meta = _recv(s)
-            p = {"sock": s, "meta": meta, "lock": threading.Lock()}
-            self._check_compat(meta)
-            self.peers[key] = p
+        with self.peer_lock:
+            p = self.peers.get(key)
+            if p is None:
+                s = socket.create_connection(key, timeout=10)
+                s.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
+                _send(s, {"op": "meta"})
+                meta = _recv(s)
+                p = {"sock": s, "meta": meta, "lock": threading.Lock()}
+                self._check_compat(meta)
+                self.peers[key] = p
         return p
 
     def _check_compat(self, m: dict):
@@ -400,9 +411,27 @@ class KvxAgent:
 
         C = native()
         eid = rmeta["engine_id"]
-        if self.stream is None:
+        stream = getattr(self._tls, "stream", None)
+        if stream is None:
             torch.cuda.set_device(self.kv.device)
-            self.stream = torch.cuda.Stream(device=self.kv.device)
+            stream = self._tls.stream = torch.cuda.Stream(device=self.kv.device)
+        with self.peer_lock:
+            base = self._map_peer(C, eid, rmeta)
+        with torch.cuda.stream(stream):
+            if self.transport == "dma" and len(segs) == 1:
+                pairs = torch.tensor(list(zip(rblocks, lblocks)), dtype=torch.int32)
+                C.kvx_dma_blocks(self.kv, base, self.block_bytes, rmeta["block_bytes"], pairs, self.block_bytes)
+            else:
+                pairs = torch.tensor(list(zip(rblocks, lblocks)), dtype=torch.int32, device=self.kv.device)
+                sg = torch.tensor(segs, dtype=torch.int64, device=self.kv.device)
+                C.kvx_copy_blocks(self.kv, base, self.block_bytes, rmeta["block_bytes"], pairs, sg,
+                                  max(s[2] for s in segs))
+            ev = torch.cuda.Event()
+            ev.record(stream)
+        ev.synchronize()
+
+    def _map_peer(self, C, eid, rmeta) -> int:
+        """Base pointer of a peer's KV pool in this process (mapped once)."""
         base = self.ipc_maps.get(eid)
         if base is None:
             if "vmm" in rmeta:
@@ -420,18 +449,7 @@ class KvxAgent:
             else:
                 base = C.kvx_ipc_open(rmeta["ipc_handle"]) + int(rmeta["ipc_offset"])
             self.ipc_maps[eid] = base
-        with torch.cuda.stream(self.stream):
-            if self.transport == "dma" and len(segs) == 1:
-                pairs = torch.tensor(list(zip(rblocks, lblocks)), dtype=torch.int32)
-                C.kvx_dma_blocks(self.kv, base, self.block_bytes, rmeta["block_bytes"], pairs, self.block_bytes)
-            else:
-                pairs = torch.tensor(list(zip(rblocks, lblocks)), dtype=torch.int32, device=self.kv.device)
-                sg = torch.tensor(segs, dtype=torch.int64, device=self.kv.device)
-                C.kvx_copy_blocks(self.kv, base, self.block_bytes, rmeta["block_bytes"], pairs, sg,
-                                  max(s[2] for s in segs))
-            ev = torch.cuda.Event()
-            ev.record(self.stream)
-        ev.synchronize()
+        return base
 
     def poll_done(self) -> list[tuple[str, bool]]:
         out = []
@@ -443,7 +461,8 @@ class KvxAgent:
 
     def close(self):
         self._stop.set()
-        self.jobs.put(None)
+        for _ in self.workers:
+            self.jobs.put(None)
         self.server.shutdown()
         for p in self.peers.values():
             try:

@@ -166,6 +166,7 @@ def test_abort_before_pull_starts_notifies_prefiller(monkeypatch):
     destination blocks once the worker reports the skipped job."""
     import time
 
+    monkeypatch.setenv("LLMD_KVX_WORKERS", "1")  # one transfer thread: d2 really waits in the queue
     P = make(KT)
     D = make(KT)
     sp1 = SamplingParams(max_tokens=1, temperature=0.0, ignore_eos=True)
@@ -185,3 +186,33 @@ def test_abort_before_pull_starts_notifies_prefiller(monkeypatch):
         time.sleep(0.01)
     assert P.bm.num_free() == P.bm.num_blocks
     assert D.bm.num_free() == D.bm.num_blocks
+
+
+def test_pulls_from_different_prefillers_run_concurrently(monkeypatch):
+    """N04 (multi-path role): pulls from two prefillers overlap on separate
+    transfer workers instead of queueing behind one copy."""
+    import time
+
+    P1, P2 = make(KT), make(KT)
+    D = make(KT)
+    assert D.connector.agent.n_workers >= 2
+    sp1 = SamplingParams(max_tokens=1, temperature=0.0, ignore_eos=True)
+    a, b = list(range(10, 90)), list(range(100, 180))
+    _, o1 = run(P1, "p1", a, sp1, {"do_remote_decode": True})
+    _, o2 = run(P2, "p2", b, sp1, {"do_remote_decode": True})
+    monkeypatch.setenv("LLMD_KVX_FAULT", "delay:0.4")
+    sp = SamplingParams(max_tokens=2, temperature=0.0, ignore_eos=True)
+    t0 = time.monotonic()
+    D.add_request("d1", a, sp, kv_transfer_params=o1.kv_transfer_params)
+    D.add_request("d2", b, sp, kv_transfer_params=o2.kv_transfer_params)
+    done = set()
+    while len(done) < 2 and time.monotonic() - t0 < 10:
+        for o in D.step():
+            if o.finished:
+                done.add(o.request_id)
+        time.sleep(0.002)
+    elapsed = time.monotonic() - t0
+    assert done == {"d1", "d2"}
+    assert elapsed < 0.75, elapsed   # two 0.4 s pulls overlapped (serial would be >= 0.8 s)
+    for r in ("d1", "d2"):
+        assert D.connector._results.get(r) is None
