@@ -339,7 +339,7 @@ __global__ __launch_bounds__(NT, 2) void moe_gemm_kernel(
 // (64 bf16) with the 16-B chunk XOR-swizzled by (row >> 1) & 7 on the SOURCE
 // side (DMA images are lane-linear): every ds_read_b128 lane group of a
 // fragment read then covers 16 distinct slots of a 256-B bank row.
-constexpr int G2_BM = 64, G2_BN = 256, G2_NT = 256;
+constexpr int G2_BM = 64, G2_BN = 256, G2_NT = 256, G2_MAX_KB = 64;
 constexpr int G2_AB = G2_BM * 128, G2_BB = G2_BN * 128, G2_BUF = G2_AB + G2_BB;
 
 __device__ __forceinline__ int g2_swz(int row, int c) { return c ^ ((row >> 1) & 7); }
@@ -632,7 +632,12 @@ __global__ __launch_bounds__(NT, 2) void moe_gemm_fp8_kernel(
 // conflicts for all four ds_read_b128 lane groups. Each step's product is
 // folded into the accumulator with xs[row][kb] * ws[e][nb][kb] (DeepSeek
 // 1x128 activation / 128x128 weight block scales; each wave's 64 columns sit
-// in one weight-scale block).
+// in one weight-scale block). The K loop issues no VGPR-destination load: the
+// weight scale is a scalar load and the 64 activation scales of the next step
+// ride the tile's LDS-DMA (a 4-byte global_load_lds per row) into their own
+// per-buffer LDS array - an ordinary vector load there made hipcc wait
+// vmcnt(0) inside every step, i.e. for the next tile's DMA too, serialising
+// DMA and MFMAs (613 TF/s at T=4096, below the bf16 kernel).
 __device__ __forceinline__ int g3_swz(int row, int c) { return c ^ ((0x32765410 >> (4 * ((row >> 1) & 7))) & 7); }
 
 typedef int i32x8_t __attribute__((ext_vector_type(8)));
@@ -671,30 +676,37 @@ __global__ __launch_bounds__(G2_NT, 2) void moe_gemm2_fp8_kernel(
     const int n = min(n0 + row, N - 1);
     boff[i] = n * K + g3_swz(row, lp) * 16;
   }
-  auto issue = [&](char* base, int k0) {
+  // activation scales of the tile's 64 rows: wave 0 lane r DMAs xs[row r][kb]
+  // next to the tile of step kb into xs_sm<buf>, so the fold reads 4
+  // contiguous floats per 16-row block from LDS. Padding rows read row 0
+  // (their outputs are never stored).
+  __shared__ __attribute__((aligned(256))) float xs_sm0[G2_BM];
+  __shared__ __attribute__((aligned(256))) float xs_sm1[G2_BM];
+  const int wu = __builtin_amdgcn_readfirstlane(w);
+  const float* xs_row = xs + (int64_t)max(0, tok_of(m0 + lane)) * xs_stride;
+  auto issue = [&](char* base, float* xsb, int k0) {
 #pragma unroll
     for (int i = 0; i < 2; ++i) g2_dma(asrc[i] + k0, base + (2 * w + i) * 1024);
 #pragma unroll
     for (int i = 0; i < 8; ++i) g2_dma(We + boff[i] + k0, base + G2_AB + (8 * w + i) * 1024);
+    if (wu == 0)
+      __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)(xs_row + k0 / 128),
+                                       (void __attribute__((address_space(3)))*)xsb, 4, 0, 0);
   };
   const int r16 = lane & 15, kq = lane >> 4;
-  // activation scales of the tile's 64 rows: wave 0 lane r loads xs[row r][kb+1]
-  // together with the next tile's DMA and publishes it to xs_sm before the next
-  // barrier, so the fold reads 4 contiguous floats per 16-row block from LDS.
-  // Padding rows read row 0 (their outputs are never stored).
-  __shared__ float xs_sm[2][G2_BM];
-  const float* xs_row = nullptr;
-  if (w == 0) {
-    const int tok = tok_of(m0 + lane);
-    xs_row = xs + (int64_t)(tok < 0 ? 0 : tok) * xs_stride;
+  // weight scales of the wave's 128-column block for every K step, staged in
+  // LDS before the loop (host: nkb <= G2_MAX_KB)
+  __shared__ float ws_sm[4][G2_MAX_KB];
+  {
+    const float* wsr = ws + ((int64_t)e * nnb + (n0 + 64 * w) / 128) * nkb;
+    for (int kb = lane; kb < nkb; kb += 64) ws_sm[w][kb] = wsr[kb];
   }
-  const float* wsr = ws + ((int64_t)e * nnb + (n0 + 64 * w) / 128) * nkb;
   f32x4_t acc[4][4];
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-  auto compute = [&](const char* base, int kb) {
+  auto compute = [&](const char* base, const float* xsb, int kb) {
     const char* A = base;
     const char* B = base + G2_AB;
     i32x8_t bfr[4];
@@ -705,8 +717,7 @@ __global__ __launch_bounds__(G2_NT, 2) void moe_gemm2_fp8_kernel(
       const u32x4_t hi = *reinterpret_cast<const u32x4_t*>(B + row * 128 + g3_swz(row, 2 * kq + 1) * 16);
       bfr[j] = i32x8_t{(int)lo[0], (int)lo[1], (int)lo[2], (int)lo[3], (int)hi[0], (int)hi[1], (int)hi[2], (int)hi[3]};
     }
-    const float wsv = wsr[kb];
-    const float* xsb = xs_sm[kb & 1];
+    const float wsv = ws_sm[wu][kb];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {  // one 16-row block at a time keeps the block accumulators at 16 VGPRs
       const int row = 16 * i + r16;
@@ -728,27 +739,17 @@ __global__ __launch_bounds__(G2_NT, 2) void moe_gemm2_fp8_kernel(
       }
     }
   };
-  float xs_next = 0.f;
-  issue(buf0, 0);
-  if (w == 0) xs_next = xs_row[0];
+  issue(buf0, xs_sm0, 0);  // the first barrier below also publishes ws_sm
   for (int kt = 0; kt < nkb; kt += 2) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    if (w == 0) xs_sm[0][lane] = xs_next;
     __syncthreads();
-    if (kt + 1 < nkb) {
-      issue(buf1, (kt + 1) * 128);
-      if (w == 0) xs_next = xs_row[kt + 1];
-    }
-    compute(buf0, kt);
+    if (kt + 1 < nkb) issue(buf1, xs_sm1, (kt + 1) * 128);
+    compute(buf0, xs_sm0, kt);
     if (kt + 1 >= nkb) break;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    if (w == 0) xs_sm[1][lane] = xs_next;
     __syncthreads();
-    if (kt + 2 < nkb) {
-      issue(buf0, (kt + 2) * 128);
-      if (w == 0) xs_next = xs_row[kt + 2];
-    }
-    compute(buf1, kt + 1);
+    if (kt + 2 < nkb) issue(buf0, xs_sm0, (kt + 2) * 128);
+    compute(buf1, xs_sm1, kt + 1);
   }
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
@@ -874,7 +875,7 @@ void llmd_moe_gemm_fp8(const void* X, int64_t x_stride, const float* xs, int64_t
     const char* e = getenv("LLMD_MOE_GEMM_V1");
     return !(e && e[0] == '1');
   }();
-  if (v2 && K % 128 == 0 && x_stride % 16 == 0 && w_expert_stride % 16 == 0) {
+  if (v2 && K % 128 == 0 && K / 128 <= G2_MAX_KB && x_stride % 16 == 0 && w_expert_stride % 16 == 0) {
     dim3 grid2((N + G2_BN - 1) / G2_BN, num_tiles);
     if (mode == 0)
       hipLaunchKernelGGL(moe_gemm2_fp8_kernel<0>, grid2, dim3(G2_NT), 0, st, (const uint8_t*)X, x_stride, xs,
