@@ -496,14 +496,19 @@ __global__ __launch_bounds__(128) void mla_reduce_kernel(const float* __restrict
 }  // namespace
 
 // v2 waves per workgroup for H = 128: 8 (all heads, 2 waves/SIMD, register
-// budget 256) or 4 (two 64-head workgroups, 1 wave/SIMD, 512 registers);
-// LLMD_MLA_NW overrides.
-extern "C" int llmd_mla_v2_waves() {
-  static const int nw = [] {
+// budget 256: the 128 accumulators + 72 Q registers spill a few dozen values)
+// or 4 (two 64-head workgroups, 1 wave/SIMD, 512 registers, no spills, each
+// K/V tile fetched twice). Measured (profiles/mla_v2.txt, round 2): 4 wins
+// bf16 decode (rows 64: 0.18 vs 0.21 ms, rows 8: 0.058 vs 0.073) and tiny fp8
+// batches, 8 wins prefill (596 vs 508 TF/s) and fp8 decode at 64 rows.
+// LLMD_MLA_NW=4|8 forces one.
+extern "C" int llmd_mla_v2_waves(int R, int fp8) {
+  static const int forced = [] {
     const char* e = getenv("LLMD_MLA_NW");
-    return (e && e[0] == '4') ? 4 : 8;
+    return e ? atoi(e) : 0;
   }();
-  return nw;
+  if (forced == 4 || forced == 8) return forced;
+  return R <= (fp8 ? 16 : 256) ? 4 : 8;
 }
 
 // v2 (64-head groups per workgroup) for 64 or 128 heads; LLMD_MLA_V1=1 forces v1
@@ -543,7 +548,7 @@ extern "C" int llmd_mla_attention(const void* q, int64_t q_row_stride, const voi
     if (big) V2(NW, true, false); else V2(NW, false, false); \
   }
     const bool big = bs >= 64;
-    if (H == 128 && llmd_mla_v2_waves() == 8) {
+    if (H == 128 && llmd_mla_v2_waves(R, fp8) == 8) {
       V2NW(8)
     } else {
       V2NW(4)
