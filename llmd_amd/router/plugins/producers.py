@@ -8,6 +8,7 @@ from __future__ import annotations
 import asyncio
 import json
 import logging
+import os
 import time
 from typing import Optional
 
@@ -249,19 +250,30 @@ class InflightLoadProducer(DataProducer, PreRequest, ResponseProcessor):
 @register("predicted-latency-producer")
 class PredictedLatencyProducer(DataProducer, PreRequest, ResponseProcessor):
     """Per-endpoint TTFT/TPOT predictions + SLO headroom; streams training
-    samples to the latency predictor (C20). Params: predictionServerURL
-    (http, optional: in-process predictor if absent), streamingMode."""
+    samples to the latency predictor (C20, latency-predictor.md:18-52).
+    Params: predictionServerURL / trainingServerURL (http; env
+    PREDICTION_SERVER_URL / TRAINING_SERVER_URL; with neither the predictor
+    runs in-process), streamingMode. Training samples (features of the chosen
+    endpoint + the observed TTFT/TPOT) are batched and POSTed to the training
+    server's /add_training_data_bulk in the background."""
 
     def __init__(self, *a, **k):
         super().__init__(*a, **k)
         from llmd_amd.router.predictor import LatencyPredictor
 
-        self.url = self.p("predictionServerURL") or self.p("predictionServerUrl")
+        self.url = (self.p("predictionServerURL") or self.p("predictionServerUrl")
+                    or os.environ.get("PREDICTION_SERVER_URL"))
+        self.train_url = (self.p("trainingServerURL") or self.p("trainingServerUrl")
+                          or os.environ.get("TRAINING_SERVER_URL"))
         self.local = None if self.url else LatencyPredictor(min_samples=int(self.p("minSamples", 50)))
         self.session = None
         self.ctx_reqs: dict[str, dict] = {}
         self.ttft_pred_count = 0
         self.available = True
+        self.pending: list[dict] = []     # samples waiting for the training server
+        self.flush_every = int(self.p("trainingBatchSize", 8))
+        self._flushing = False
+        self.samples_sent = 0
 
     def features(self, req, ep: Endpoint, prefix_hit: float, inflight_tokens: int):
         n_in = len(req.token_ids) if req.token_ids else max(1, len(req.prompt) // CHARS_PER_TOKEN)
@@ -271,16 +283,51 @@ class PredictedLatencyProducer(DataProducer, PreRequest, ResponseProcessor):
                 "prefix_cache_score": prefix_hit, "num_tokens_generated": 0,
                 "inflight_input_tokens": inflight_tokens}
 
-    async def _predict(self, feats: list[dict]):
-        if self.local is not None:
-            return self.local.predict(feats)
+    def _sess(self):
         import aiohttp
 
         if self.session is None:
             self.session = aiohttp.ClientSession(timeout=aiohttp.ClientTimeout(total=1))
-        async with self.session.post(self.url.rstrip("/") + "/predict/bulk", json={"requests": feats}) as r:
+        return self.session
+
+    async def _predict(self, feats: list[dict]):
+        if self.local is not None:
+            return self.local.predict(feats)
+        async with self._sess().post(self.url.rstrip("/") + "/predict/bulk", json={"requests": feats}) as r:
             r.raise_for_status()
             return (await r.json())["predictions"]
+
+    async def _flush(self):
+        if self._flushing or not self.pending or not self.train_url:
+            return
+        self._flushing = True
+        batch, self.pending = self.pending, []
+        try:
+            async with self._sess().post(self.train_url.rstrip("/") + "/add_training_data_bulk",
+                                         json={"entries": batch}) as r:
+                r.raise_for_status()
+                self.samples_sent += len(batch)
+        except Exception as e:  # noqa: BLE001 - training server outage: drop, keep routing
+            log.debug("training server unavailable: %s", e)
+        finally:
+            self._flushing = False
+
+    async def _flush_loop(self):
+        while True:
+            await asyncio.sleep(float(self.p("trainingFlushIntervalS", 0.5)))
+            await self._flush()
+
+    async def start(self):
+        if self.train_url:
+            self._flush_task = asyncio.get_running_loop().create_task(self._flush_loop())
+
+    async def stop(self):
+        t = getattr(self, "_flush_task", None)
+        if t is not None:
+            t.cancel()
+        await self._flush()
+        if self.session is not None:
+            await self.session.close()
 
     async def produce(self, req, eps):
         from .scheduling import _prefix_info
@@ -288,6 +335,9 @@ class PredictedLatencyProducer(DataProducer, PreRequest, ResponseProcessor):
         hits = _prefix_info(req, None)
         infl = req.data.get("inflight", {})
         feats = [self.features(req, e, hits.get(e.key, 0.0), infl.get(e.key, (0, 0))[1]) for e in eps]
+        # features are kept even without a model: the chosen endpoint's become
+        # the training sample that bootstraps the first model
+        req.data["latency_features"] = {e.key: f for e, f in zip(eps, feats)}
         try:
             preds = await self._predict(feats)
             self.available = True
@@ -308,19 +358,32 @@ class PredictedLatencyProducer(DataProducer, PreRequest, ResponseProcessor):
 
     def pre_request(self, req, result):
         pred = req.data.get("predicted_latency") or {}
+        feats = req.data.get("latency_features") or {}
         t = result.target
-        if t is not None and t.key in pred:
+        if t is None:
+            return
+        if t.key in pred:
             self.ctx_reqs[req.request_id] = {"features": pred[t.key]["features"], "pred": pred[t.key]}
             if self.ctx is not None and getattr(self.ctx, "metrics", None) is not None:
                 self.ctx.metrics.observe_prediction(req, pred[t.key])
+        elif t.key in feats:
+            self.ctx_reqs[req.request_id] = {"features": feats[t.key], "pred": None}
 
     def on_response_complete(self, req, ep, info):
         st = self.ctx_reqs.pop(req.request_id, None)
-        if st is None or self.local is None:
+        if st is None or info.get("ttft") is None:
             return
-        if info.get("ttft") is not None:
-            self.local.add_sample(st["features"], ttft_ms=1000 * info["ttft"],
-                                  tpot_ms=1000 * info["tpot"] if info.get("tpot") else None)
+        ttft_ms = 1000 * info["ttft"]
+        tpot_ms = 1000 * info["tpot"] if info.get("tpot") else None
+        if self.local is not None:
+            self.local.add_sample(st["features"], ttft_ms=ttft_ms, tpot_ms=tpot_ms)
+        elif self.train_url:
+            self.pending.append(dict(st["features"], actual_ttft_ms=ttft_ms, actual_tpot_ms=tpot_ms))
+            if len(self.pending) >= self.flush_every:
+                try:
+                    asyncio.get_running_loop().create_task(self._flush())
+                except RuntimeError:  # no loop (sync caller): the periodic flush sends it
+                    pass
 
 
 @register("latency-slo-admitter")

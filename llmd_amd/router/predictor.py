@@ -233,8 +233,11 @@ def main(argv=None):
     p.add_argument("--role", choices=["training", "prediction", "combined"], default="combined")
     p.add_argument("--port", type=int, default=8000)
     p.add_argument("--model-path", default=os.environ.get("LATENCY_MODEL_PATH"))
+    p.add_argument("--min-samples", type=int, default=int(os.environ.get("LATENCY_MIN_SAMPLES", "50")))
+    p.add_argument("--retrain-every", type=int, default=int(os.environ.get("LATENCY_RETRAIN_EVERY", "100")),
+                   help="samples between retrains (training role)")
     a = p.parse_args(argv)
-    pred = LatencyPredictor(background=True)
+    pred = LatencyPredictor(background=True, min_samples=a.min_samples, retrain_every=a.retrain_every)
     if a.role == "prediction" and a.model_path:
         pred.load(a.model_path)
     web.run_app(make_app(pred, a.role, a.model_path), port=a.port, access_log=None)

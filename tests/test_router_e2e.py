@@ -332,3 +332,121 @@ def test_precise_prefix_routing_with_kv_events():
                 eng.pub.close()
             await r.cleanup()
     asyncio.run(main())
+
+
+PREDICTED = """
+apiVersion: llm-d.ai/v1alpha1
+kind: EndpointPickerConfig
+plugins:
+- type: approx-prefix-cache-producer
+- type: predicted-latency-producer
+  parameters: {streamingMode: true, predictionServerURL: "PRED", trainingServerURL: "TRAIN",
+               trainingBatchSize: 4, trainingFlushIntervalS: 0.1}
+- type: latency-scorer
+- type: weighted-random-picker
+- type: metrics-data-source
+  parameters: {interval: 20ms}
+- type: core-metrics-extractor
+dataLayer:
+  sources:
+  - pluginRef: metrics-data-source
+    extractors: [{pluginRef: core-metrics-extractor}]
+schedulingProfiles:
+- name: default
+  plugins:
+  - pluginRef: predicted-latency-producer
+  - pluginRef: latency-scorer
+  - pluginRef: weighted-random-picker
+"""
+
+
+def test_predicted_latency_served_e2e(tmp_path):
+    """Mirror of e2e-validate-predicted-latency.sh with the deployed shape of
+    the predictor (latency-predictor.md:18-52): a training server and a
+    prediction server sharing a model file; the router streams training
+    samples to the first and asks the second. After 100 requests at
+    concurrency 8 the predicted-TTFT histogram must have samples next to the
+    actual-TTFT one - predictions were served, not silently skipped."""
+    import os
+    import socket
+    import subprocess
+    import sys
+    import time
+
+    def free_port():
+        s = socket.socket()
+        s.bind(("127.0.0.1", 0))
+        p = s.getsockname()[1]
+        s.close()
+        return p
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    model = tmp_path / "latency_model.bin"
+    tp, pp = free_port(), free_port()
+    env = dict(os.environ, MODEL_SYNC_INTERVAL_SEC="0.2")
+    common = [sys.executable, "-m", "llmd_amd.router.predictor", "--model-path", str(model),
+              "--min-samples", "20", "--retrain-every", "20"]
+    procs = [subprocess.Popen(common + ["--role", "training", "--port", str(tp)], cwd=root, env=env,
+                              stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL, start_new_session=True),
+             subprocess.Popen(common + ["--role", "prediction", "--port", str(pp)], cwd=root, env=env,
+                              stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL, start_new_session=True)]
+
+    async def main():
+        sims = [await start_sim(model="m", prefill_tps=2e5, decode_step_s=0.002) for _ in range(2)]
+        eps = [{"name": f"s{i}", "address": "127.0.0.1", "port": s[2]} for i, s in enumerate(sims)]
+        cfg = PREDICTED.replace("PRED", f"http://127.0.0.1:{pp}").replace("TRAIN", f"http://127.0.0.1:{tp}")
+        async with aiohttp.ClientSession() as s:
+            deadline = time.time() + 60
+            while time.time() < deadline:      # both predictor servers up
+                try:
+                    ok = 0
+                    for port in (tp, pp):
+                        async with s.get(f"http://127.0.0.1:{port}/healthz") as r:
+                            ok += r.status == 200
+                    if ok == 2:
+                        break
+                except aiohttp.ClientError:
+                    pass
+                await asyncio.sleep(0.2)
+            rr, epp, port = await _router(cfg, eps)
+            url = f"http://127.0.0.1:{port}/v1/completions"
+            sem = asyncio.Semaphore(8)
+
+            async def one(i):
+                async with sem:
+                    body = {"model": "m", "prompt": f"request {i} " + "x " * (20 + 7 * (i % 13)), "max_tokens": 4,
+                            "stream": True, "stream_options": {"include_usage": True}}
+                    async with s.post(url, json=body) as r:
+                        await r.read()
+                        return r.status
+
+            assert all(st == 200 for st in await asyncio.gather(*[one(i) for i in range(100)]))
+            # the prediction server picks up the model the training server wrote
+            deadline = time.time() + 30
+            while time.time() < deadline:
+                async with s.get(f"http://127.0.0.1:{pp}/healthz") as r:
+                    if (await r.json()).get("ready"):
+                        break
+                await asyncio.sleep(0.2)
+            assert all(st == 200 for st in await asyncio.gather(*[one(100 + i) for i in range(40)]))
+            from prometheus_client.parser import text_string_to_metric_families
+
+            counts = {}
+            for fam in text_string_to_metric_families(epp.render_metrics().decode()):
+                for smp in fam.samples:
+                    if smp.name.endswith("_count"):
+                        counts[smp.name] = counts.get(smp.name, 0) + smp.value
+            await rr.cleanup()
+        for sm in sims:
+            await sm[0].cleanup()
+        return counts
+
+    try:
+        counts = asyncio.run(main())
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                os.killpg(p.pid, 9)
+                p.wait()
+    assert counts.get("inference_objective_request_ttft_seconds_count", 0) > 0
+    assert counts.get("inference_objective_request_predicted_ttft_seconds_count", 0) > 0, counts
