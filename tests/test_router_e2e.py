@@ -450,3 +450,47 @@ def test_predicted_latency_served_e2e(tmp_path):
                 p.wait()
     assert counts.get("inference_objective_request_ttft_seconds_count", 0) > 0
     assert counts.get("inference_objective_request_predicted_ttft_seconds_count", 0) > 0, counts
+
+
+import glob as _glob
+
+_GUIDES = sorted(_glob.glob("/root/reference/guides/*/router/*.values.yaml"))
+
+
+@pytest.mark.parametrize("values", _GUIDES or ["<reference tree not mounted>"],
+                         ids=[p.split("guides/")[1] for p in _GUIDES] or ["none"])
+def test_reference_guide_configs_route(values):
+    """Every EndpointPickerConfig the reference's guides ship (plugin graphs
+    verbatim from guides/*/router/*.values.yaml) loads and routes plain and
+    streamed completions over HTTP to role-labelled simulators."""
+    from llmd_amd.router.config import ConfigError, extract_config_text
+
+    if not _GUIDES:
+        pytest.skip("reference tree not mounted")
+    try:
+        cfg = extract_config_text(open(values).read())
+    except ConfigError:
+        pytest.skip("values file without a custom plugin config")
+
+    async def main():
+        roles = ("prefill", "prefill", "decode", "decode")
+        sims = [await start_sim(model="m", prefill_tps=1e6, decode_step_s=0.001, role=r) for r in roles]
+        eps = [{"name": f"s{i}", "address": "127.0.0.1", "port": s[2], "labels": {"llm-d.ai/role": r}}
+               for i, (s, r) in enumerate(zip(sims, roles))]
+        rr, epp, port = await _router(cfg, eps)
+        out = []
+        async with aiohttp.ClientSession() as s:
+            for i in range(6):
+                body = {"model": "m", "prompt": "hello world " * (i + 1), "max_tokens": 3, "stream": i % 2 == 1,
+                        "stream_options": {"include_usage": True}}
+                async with s.post(f"http://127.0.0.1:{port}/v1/completions", json=body) as r:
+                    data = await r.read()
+                    out.append((r.status, data))
+        await rr.cleanup()
+        for sm in sims:
+            await sm[0].cleanup()
+        return out
+
+    res = asyncio.run(main())
+    assert all(st == 200 for st, _ in res), [(st, d[:200]) for st, d in res]
+    assert all(b"choices" in d or b"data:" in d for _, d in res)
