@@ -58,6 +58,8 @@ def parse():
     p.add_argument("--mode", default="auto", choices=["auto", "agg", "pd"],
                    help="auto: aggregated replicas on N < 4, P/D disaggregation (3/4 prefill ranks) on N >= 4")
     p.add_argument("--prefill-gpus", type=int, default=0, help="pd mode: number of prefill ranks")
+    p.add_argument("--decode-tp", type=int, default=0,
+                   help="pd mode: TP degree of each decode replica (0 = 2 when the decode ranks pair up, else 1)")
     p.add_argument("--enforce-eager", action="store_true")
     p.add_argument("--seed", type=int, default=0)
     p.add_argument("--gpu-memory-utilization", type=float, default=0.92)
@@ -110,7 +112,7 @@ def main():
         from llmd_amd.bench_pd import run_pd
 
         res = run_pd(a, rank, world, local_rank, log)
-        if rank == 0:
+        if rank == 0 and res is not None:
             value = res["gen"] / res["elapsed"]
             out = {
                 "metric": METRIC, "value": round(value, 2), "unit": "output tok/s (whole job)",
@@ -121,7 +123,8 @@ def main():
                 "config": {"model": "Llama-3-70B" if a.model == "llama-3-70b" else a.model,
                            "global_batch": a.concurrency * res["decode_ranks"], "seq_len": a.isl,
                            "isl": a.isl, "osl": a.osl,
-                           "parallelism": f"pd{res['prefill_ranks']}p{res['decode_ranks']}d",
+                           "parallelism": f"pd{res['prefill_ranks']}p{res['decode_ranks']}d"
+                                          + (f"-dtp{res['decode_tp']}" if res.get("decode_tp", 1) > 1 else ""),
                            "max_num_batched_tokens": a.max_num_batched_tokens, "block_size": a.block_size,
                            "kv_transfer": "kvx ipc over xGMI"},
                 "output_tok_s_per_decode_gpu": round(value / res["decode_ranks"], 2),

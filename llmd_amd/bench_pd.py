@@ -4,14 +4,25 @@ Topology inside one torchrun job (one process per GPU):
   ranks [0, P)   prefill engines, each serving the real OpenAI endpoint on
                  127.0.0.1:<base+rank> (AsyncEngine + aiohttp) with a
                  ``kv_transfer_config`` (kvx producer);
-  ranks [P, N)   decode engines (kvx consumer, IPC pull over xGMI) driven by
+  ranks [P, N)   decode engines (kvx consumer, IPC pull over xGMI), in
+                 groups of ``--decode-tp`` consecutive ranks (one TP replica
+                 each: the reference's P/D headline runs its decoders TP4,
+                 guides/pd-disaggregation/README.md:336-460). The group's
+                 first rank is the TP driver (scheduler + sidecar), the
+                 others TP followers (engine/tp_worker.py) that pull their
+                 own KV-head slice. The driver is driven by
                  an in-process routing-sidecar loop: every new request is sent
                  to a prefill rank (least outstanding) with
                  ``kv_transfer_params{do_remote_decode}`` / ``max_tokens=1``,
                  the returned params are handed to the local decoder which
                  pulls the KV and decodes (the reference's nixlv2 protocol,
                  docs/architecture/advanced/disaggregation/README.md:119-131).
-Timing: K decode steps on every decode rank between gloo barriers (+ device
+Why TP on the decode side: a decode GPU is KV-capacity bound. A TP1 70B
+replica spends 141 GB of HBM on weights and fits ~64 ISL-5000 sequences
+(50.9 ms/step -> ~1260 tok/s per GPU); a TP2 replica holds half the weights
+per GPU, so the same two GPUs fit ~3x the sequences and read each weight byte
+once per step for twice the rows.
+Timing: K decode steps on every decode driver between gloo barriers (+ device
 sync); prefill ranks serve continuously. Reported value = total output
 tokens / max elapsed; TTFT measured at the decode side from the moment the
 prefill request is issued (the "true TTFT" a client would see).
@@ -48,45 +59,72 @@ def run_pd(a, rank: int, world: int, local_rank: int, log) -> dict | None:
     P = a.prefill_gpus or max(1, (3 * world) // 4)
     if not 0 < P < world:
         raise SystemExit(f"pd mode needs 0 < prefill ranks ({P}) < world ({world})")
+    n_dec = world - P
+    dtp = a.decode_tp or (2 if n_dec % 2 == 0 else 1)
+    if n_dec % dtp:
+        raise SystemExit(f"pd mode: {n_dec} decode ranks not divisible by --decode-tp {dtp}")
     is_prefill = rank < P
-    ctl = dist.new_group(backend="gloo")
+    world_ctl = dist.new_group(backend="gloo")
+    drivers = list(range(P, world, dtp))
+    # timing / result group: prefill ranks + decode drivers (followers sit in
+    # their step-plan loop and are released by the driver's shutdown)
+    ctl = dist.new_group(list(range(P)) + drivers, backend="gloo") if dtp > 1 else world_ctl
+    is_follower = False
+    if dtp > 1:
+        from llmd_amd.parallel.state import ParallelState, set_state
+
+        for d in drivers:  # collective: every rank creates every group
+            ranks = list(range(d, d + dtp))
+            tg = dist.new_group(ranks)
+            tgc = dist.new_group(ranks, backend="gloo")
+            if rank in ranks:
+                set_state(ParallelState(world_size=world, rank=rank, local_rank=local_rank, tp_size=dtp,
+                                        tp_rank=rank - d, tp_group=tg, tp_cpu_group=tgc, cpu_group=tgc,
+                                        backend=dist.get_backend(), tp_src=d))
+                is_follower = rank != d
     base_port = int(os.environ.get("LLMD_PD_BASE_PORT", "18200"))
     max_len = a.isl + a.osl + 64
     kt = {"kv_connector": "KvxConnector", "kv_role": "kv_producer" if is_prefill else "kv_consumer",
           "kv_load_failure_policy": "recompute",
           "kv_connector_extra_config": {"transport": os.environ.get("LLMD_KVX_TRANSPORT", "auto")}}
-    n_decode = world - P
-    conc = a.concurrency
+    conc = a.concurrency * (1 if is_prefill else dtp)  # --concurrency is per GPU
     cfg = EngineConfig.create(
         a.model, device=a.device, block_size=a.block_size,
         max_num_seqs=max(conc, 8) if not is_prefill else 64,
         max_num_batched_tokens=a.max_num_batched_tokens, max_model_len=max_len,
-        enforce_eager=a.enforce_eager or is_prefill, seed=a.seed, enable_prefix_caching=True,
+        enforce_eager=a.enforce_eager or is_prefill or (dtp > 1 and os.environ.get("LLMD_BENCH_DEVICE") is not None),
+        seed=a.seed, enable_prefix_caching=True,
         cuda_graph_max_bs=conc, kv_transfer_config=kt, gpu_memory_utilization=a.gpu_memory_utilization,
         kv_cache_memory_bytes=int(a.kv_cache_gb * 2**30) if a.kv_cache_gb else None,
         quantization=a.quantization, kv_cache_dtype=a.kv_cache_dtype)
     t0 = time.time()
+    if is_follower:
+        from llmd_amd.engine.tp_worker import run_follower
+
+        n = run_follower(cfg, on_ready=lambda: dist.barrier(group=world_ctl))  # barrier: servers up
+        log(rank, f"decode TP follower done after {n} steps")
+        return None
     eng = LLMEngine(cfg, capture_graphs=not is_prefill)
     _sync(a)
     log(rank, f"{'prefill' if is_prefill else 'decode'} engine up in {time.time() - t0:.1f}s "
               f"({eng.runner.num_blocks} KV blocks)")
     if is_prefill:
         srv_thread = _start_server(cfg, eng, base_port + rank)
-        dist.barrier(group=ctl)              # servers up
+        dist.barrier(group=world_ctl)        # servers up
         dist.barrier(group=ctl)              # decoders finished setup+warmup
         _sync(a)
         dist.barrier(group=ctl)              # timed region start
         dist.barrier(group=ctl)              # timed region end
         _sync(a)
         stats = [0.0, 0.0, 0.0]
-        gathered = [None] * world
+        gathered = [None] * dist.get_world_size(ctl)
         dist.all_gather_object(gathered, {"elapsed": 0.0, "gen": 0, "ttft": [], "prefill": True,
                                           "prompt_tok": eng.metrics.n_prompt}, group=ctl)
         dist.barrier(group=ctl)
         srv_thread.stop()
-        return _summarize(gathered, P, world)
+        return _summarize(gathered, P, world, dtp)
     # ------------------------------------------------------------------ decode rank
-    dist.barrier(group=ctl)  # prefill servers up
+    dist.barrier(group=world_ctl)  # prefill servers up
     prefill_urls = [f"http://127.0.0.1:{base_port + r}/v1/completions" for r in range(P)]
     sc = _SidecarThread(prefill_urls, a.model)
     vocab = cfg.model_config.vocab_size
@@ -162,21 +200,22 @@ def run_pd(a, rank: int, world: int, local_rank: int, log) -> dict | None:
     dist.barrier(group=ctl)
     elapsed = time.perf_counter() - t1
     gen = eng.metrics.n_gen - gen0
-    gathered = [None] * world
+    gathered = [None] * dist.get_world_size(ctl)
     dist.all_gather_object(gathered, {"elapsed": elapsed, "gen": gen, "ttft": list(eng.metrics.ttfts),
                                       "prefill": False}, group=ctl)
     dist.barrier(group=ctl)
     sc.stop()
-    return _summarize(gathered, P, world)
+    eng.shutdown()  # releases the TP followers and the kvx agent
+    return _summarize(gathered, P, world, dtp)
 
 
-def _summarize(gathered, P, world):
+def _summarize(gathered, P, world, dtp=1):
     dec = [g for g in gathered if not g["prefill"]]
     el = max(g["elapsed"] for g in dec)
     tot = sum(g["gen"] for g in dec)
     tt = [t for g in dec for t in g["ttft"]]
     return {"elapsed": el, "gen": tot, "p50_ttft": statistics.median(tt) if tt else None,
-            "prefill_ranks": P, "decode_ranks": world - P, "n_ttft": len(tt)}
+            "prefill_ranks": P, "decode_ranks": world - P, "decode_tp": dtp, "n_ttft": len(tt)}
 
 
 class _SidecarThread:

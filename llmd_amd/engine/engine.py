@@ -108,6 +108,8 @@ class LLMEngine:
             self.connector.tick()
         t0 = time.monotonic()
         so = self.sched.schedule()
+        if self.connector is not None and self.runner.tp_size > 1:
+            self.connector.flush_tp()
         if self.lora is not None:
             nm = self.lora.name_of
             self.metrics.set_lora(sorted({nm(r.lora_id) for r in self.sched.running if r.lora_id} - {None}),

@@ -130,6 +130,10 @@ class ModelRunner:
 
         st = get_state()
         pc = self.cfg.parallel
+        if self.tp_size > 1:
+            from llmd_amd.parallel.comm import warm_tp_group
+
+            warm_tp_group(self.device)
         if self.tp_size > 1 and not pc.disable_custom_all_reduce and symm.enabled_by_env():
             symm.init(st.tp_rank, st.tp_size, group=st.tp_cpu_group, tp_allreduce=True)
         elif (ep_mod.canonical(pc.all2all_backend) == "symm_ll" and st.dp_size > 1 and st.tp_size == 1

@@ -28,16 +28,25 @@ log = logging.getLogger("llmd.tp")
 STOP = {"stop": True}
 
 
-def run_follower(cfg: EngineConfig, capture_graphs: bool = True) -> int:
-    """Blocking loop for TP ranks != 0. Returns the number of steps executed."""
+def run_follower(cfg: EngineConfig, capture_graphs: bool = True, on_ready=None) -> int:
+    """Blocking loop for TP ranks != 0. Returns the number of steps executed.
+    ``on_ready`` runs once the runner is built (the driver's engine is up at
+    the same point), before the first plan is received."""
     runner = ModelRunner(cfg)
     runner.profile_and_allocate()
     if cfg.enable_lora:
         from .engine import make_lora_manager
 
         make_lora_manager(cfg, runner, driver=False)
+    kvx = None
+    if cfg.kv_transfer_config:
+        from llmd_amd.kvx.connector import KvxFollower
+
+        kvx = KvxFollower(cfg, runner)
     if capture_graphs:
         runner.capture_graphs()
+    if on_ready is not None:
+        on_ready()
     n = 0
     with torch.no_grad():
         while True:
@@ -47,8 +56,13 @@ def run_follower(cfg: EngineConfig, capture_graphs: bool = True) -> int:
             if "lora_cmd" in pl:  # adapter load/unload issued on the driver
                 runner.lora.apply_cmd(pl["lora_cmd"])
                 continue
+            if "kvx_cmd" in pl:  # P/D: KV pulls / cancels scheduled on the driver
+                kvx.apply(pl)
+                continue
             runner.run_plan(pl)
             n += 1
+    if kvx is not None:
+        kvx.close()
     log.info("tp follower exiting after %d steps", n)
     return n
 

@@ -33,6 +33,17 @@ every ``LLMD_KVX_HEARTBEAT_S`` (5 s) on a fresh connection; after
 its cached connection and mapping are dropped, and pulls from it fail at once
 (-> kv_load_failure_policy) instead of hanging on a dead socket. A later
 successful ping revives it.
+Tensor-parallel decoders (the reference's ``D TP4`` P/D deployments,
+guides/pd-disaggregation/README.md:336-460): every TP rank of a decode
+replica owns a slice of the KV heads and pulls that slice itself, straight
+from the prefiller's pool into its own (head re-slicing by copy segments; no
+GPU writes into another GPU's memory, so no stale-L2 hazard). The driver rank
+(TP rank 0, which runs the scheduler) forwards each load / cancel to its
+followers through the step-plan channel (``KvxConnector.flush_tp``);
+followers report completion to the driver's side channel (``tp_done``), and
+the driver reports a request as loaded only once every rank has. Each rank
+sends its own ``free`` with ``{rank, of}`` and the prefiller releases the
+blocks after ``of`` distinct ranks have (no rank can read freed blocks).
 """
 from __future__ import annotations
 
@@ -83,6 +94,7 @@ class Held:
     blocks: list
     expiry: float
     num_tokens: int
+    frees: set = field(default_factory=set)  # consumer TP ranks done reading
 
 
 @dataclass
@@ -91,6 +103,7 @@ class LoadJob:
     params: dict
     local_blocks: list
     t0: float = field(default_factory=time.monotonic)
+    report: Optional[tuple] = None  # TP follower: the driver's side channel
 
 
 LEGACY_IPC_MAX = 4 << 30  # hipIpcOpenMemHandle hangs importing larger allocations
@@ -112,11 +125,14 @@ class KvxAgent:
         self.transport = transport
         self.held: dict[str, Held] = {}
         self.held_lock = threading.Lock()
-        self.free_requests: "queue.Queue[str]" = queue.Queue()
+        self.free_requests: "queue.Queue[tuple]" = queue.Queue()
         self.done: "queue.Queue[tuple[str, bool]]" = queue.Queue()
         self.jobs: "queue.Queue[Optional[LoadJob]]" = queue.Queue()
         self.cancelled: set[str] = set()
         self.cancel_lock = threading.Lock()
+        # TP driver: per request, [ranks reported, all ok] until every rank has
+        self.tp_wait: dict[str, list] = {}
+        self.tp_lock = threading.Lock()
         self.peers: dict[tuple, dict] = {}
         self.ipc_maps: dict[str, int] = {}
         self.ipc_handle = None
@@ -240,13 +256,18 @@ class KvxAgent:
         now = time.monotonic()
         while True:
             try:
-                rid = self.free_requests.get_nowait()
+                rid, rank, of = self.free_requests.get_nowait()
             except queue.Empty:
                 break
             with self.held_lock:
-                h = self.held.pop(rid, None)
-            if h is not None:
-                out.append(h)
+                h = self.held.get(rid)
+                if h is None:
+                    continue
+                h.frees.add(rank)
+                if len(h.frees) < of:
+                    continue  # other decoder TP ranks still read these blocks
+                del self.held[rid]
+            out.append(h)
         with self.held_lock:
             for rid in [r for r, h in self.held.items() if h.expiry < now]:
                 log.warning("kvx: request %s held blocks expired (no remote read)", rid)
@@ -258,8 +279,38 @@ class KvxAgent:
         return self.kv.index_select(0, idx).cpu().contiguous().view(torch.uint8).numpy().tobytes()
 
     # ------------------------------------------------------------ decode side
-    def start_load(self, request_id: str, params: dict, local_blocks: list):
-        self.jobs.put(LoadJob(request_id, dict(params), list(local_blocks)))
+    def start_load(self, request_id: str, params: dict, local_blocks: list, report: Optional[tuple] = None):
+        """Queue a pull. ``report`` (TP followers) is the driver's side-channel
+        address: completion goes there instead of this agent's ``done``."""
+        if self.tp_size > 1 and report is None:
+            with self.tp_lock:
+                self.tp_wait[request_id] = [0, True]
+        self.jobs.put(LoadJob(request_id, dict(params), list(local_blocks), report=report))
+
+    def _complete(self, job: LoadJob, ok: bool):
+        if job.report is not None:
+            try:
+                with socket.create_connection(tuple(job.report), timeout=10) as s:
+                    _send(s, {"op": "tp_done", "request_id": job.request_id, "ok": bool(ok)})
+                    _recv(s)
+            except (OSError, ConnectionError, struct.error) as e:
+                log.warning("kvx: cannot report %s to the TP driver: %s", job.request_id, e)
+            return
+        self.tp_report(job.request_id, ok)
+
+    def tp_report(self, request_id: str, ok: bool):
+        """One TP rank (this one, or a follower over ``tp_done``) finished."""
+        if self.tp_size == 1:
+            self.done.put((request_id, ok))
+            return
+        with self.tp_lock:
+            w = self.tp_wait.setdefault(request_id, [0, True])
+            w[0] += 1
+            w[1] = w[1] and ok
+            if w[0] < self.tp_size:
+                return
+            del self.tp_wait[request_id]
+        self.done.put((request_id, w[1]))
 
     def cancel(self, request_id: str):
         with self.cancel_lock:
@@ -276,9 +327,13 @@ class KvxAgent:
         """Abort notif: tell the prefiller it can release the held blocks."""
         try:
             p = self._peer(prm["remote_host"], prm["remote_port"])
-            self._rpc(p, {"op": "free", "request_id": prm.get("remote_request_id")})
+            self._rpc(p, self._free_msg(prm))
         except Exception as e:  # noqa: BLE001 - the prefiller's abort timeout reclaims them
             log.warning("kvx abort notif for %s failed: %s", prm.get("remote_request_id"), e)
+
+    def _free_msg(self, prm: dict) -> dict:
+        return {"op": "free", "request_id": prm.get("remote_request_id"), "rank": self.tp_rank,
+                "of": self.tp_size}
 
     def _peer(self, host, port) -> dict:
         key = (host, int(port))
@@ -349,7 +404,7 @@ class KvxAgent:
             if self._take_cancel(job.request_id):
                 # aborted before the pull started: nothing was written locally
                 self._notify_free(job.params)
-                self.done.put((job.request_id, False))
+                self._complete(job, False)
                 continue
             try:
                 ok, nbytes = self._do_load(job)
@@ -359,7 +414,7 @@ class KvxAgent:
             if self.metrics is not None:
                 self.metrics.observe(ok, time.monotonic() - t0, nbytes, len(job.local_blocks))
             self._take_cancel(job.request_id)  # a cancel that raced the running pull
-            self.done.put((job.request_id, ok))
+            self._complete(job, ok)
 
     def _do_load(self, job: LoadJob) -> tuple[bool, int]:
         prm = job.params
@@ -402,8 +457,8 @@ class KvxAgent:
         if fault == "corrupt":
             idx = torch.tensor(lblocks[:1], dtype=torch.long, device=self.kv.device)
             self.kv.index_fill_(0, idx, 0)
-        # release the prefiller's blocks
-        self._rpc(p, {"op": "free", "request_id": prm.get("remote_request_id")})
+        # release the prefiller's blocks (this rank's share)
+        self._rpc(p, self._free_msg(prm))
         return True, nbytes
 
     def _ipc_copy(self, rmeta, rblocks, lblocks, segs):
@@ -502,7 +557,11 @@ class _Handler(socketserver.BaseRequestHandler):
                         continue
                     _send(s, agent.read_blocks(msg["blocks"]))
                 elif op == "free":
-                    agent.free_requests.put(msg.get("request_id"))
+                    agent.free_requests.put((msg.get("request_id"), int(msg.get("rank", 0)),
+                                             int(msg.get("of", 1))))
+                    _send(s, {"ok": True})
+                elif op == "tp_done":
+                    agent.tp_report(msg["request_id"], bool(msg.get("ok")))
                     _send(s, {"ok": True})
                 elif op == "ping":
                     _send(s, {"ok": True, "engine_id": agent.engine_id})

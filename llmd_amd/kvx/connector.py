@@ -71,10 +71,15 @@ class KvxConnector:
         self._results: dict[str, bool] = {}
         self._finished: list[str] = []
         self._outputs = []
+        self.tp_size = st.tp_size
+        self._tp_cmds: list = []  # loads / cancels for the TP followers (flush_tp)
 
     # ---------------- decode side (scheduler hooks)
     def start_load(self, req, local_blocks: list):
-        self.agent.start_load(req.request_id, req.kv_transfer_params or {}, local_blocks)
+        prm = req.kv_transfer_params or {}
+        self.agent.start_load(req.request_id, prm, local_blocks)
+        if self.tp_size > 1:
+            self._tp_cmds.append(("load", req.request_id, dict(prm), list(local_blocks)))
 
     def cancel_load(self, request_id: str):
         """The request was aborted while its pull is queued or running. A queued
@@ -83,6 +88,19 @@ class KvxConnector:
         ``poll_finished_recv`` so the scheduler can release the local blocks
         only once nothing writes into them any more."""
         self.agent.cancel(request_id)
+        if self.tp_size > 1:
+            self._tp_cmds.append(("cancel", request_id))
+
+    def flush_tp(self):
+        """TP driver, once per engine step after scheduling: forward this step's
+        loads and cancels to the followers over the step-plan channel (every
+        TP rank pulls its own KV-head slice; see kvx/agent.py)."""
+        if not self._tp_cmds:
+            return
+        from llmd_amd.parallel.comm import tp_broadcast_plan
+
+        cmds, self._tp_cmds = self._tp_cmds, []
+        tp_broadcast_plan({"kvx_cmd": cmds, "driver": (self.agent.host, self.agent.port)})
 
     def poll_finished_recv(self) -> list[str]:
         for rid, ok in self.agent.poll_done():
@@ -112,6 +130,35 @@ class KvxConnector:
 
     def render_metrics(self) -> bytes:
         return self.metrics.render()
+
+    def close(self):
+        self.agent.close()
+
+
+class KvxFollower:
+    """A decode TP follower's half of the connector: pulls its KV-head slice
+    for the loads its driver forwards and reports back (engine/tp_worker.py)."""
+
+    def __init__(self, cfg, runner):
+        kt = cfg.kv_transfer_config or {}
+        extra = kt.get("kv_connector_extra_config") or {}
+        from llmd_amd.parallel.state import get_state
+
+        st = get_state()
+        if kt.get("kv_role", "kv_both") != "kv_consumer":
+            raise NotImplementedError("kvx with TP > 1 is supported on the decode (kv_consumer) side")
+        self.agent = KvxAgent(runner.kv, vmm=getattr(runner, "vmm", None), host=extra.get("side_channel_host"),
+                              tp_rank=st.tp_rank, tp_size=st.tp_size,
+                              abort_timeout=float(extra.get("abort_timeout", 480)),
+                              transport=extra.get("transport", "auto"), exports=False)
+
+    def apply(self, pl: dict):
+        drv = tuple(pl["driver"])
+        for c in pl["kvx_cmd"]:
+            if c[0] == "load":
+                self.agent.start_load(c[1], c[2], c[3], report=drv)
+            elif c[0] == "cancel":
+                self.agent.cancel(c[1])
 
     def close(self):
         self.agent.close()

@@ -25,6 +25,11 @@ def tp_all_reduce(x: torch.Tensor) -> torch.Tensor:
         return x
     if _custom_ar is not None and _custom_ar.should_use(x):
         return _custom_ar.all_reduce(x)
+    if x.is_cuda and st.backend == "gloo":  # 1-GPU multi-process rehearsal: stage on the host
+        h = x.cpu()
+        dist.all_reduce(h, group=st.tp_group)
+        x.copy_(h)
+        return x
     dist.all_reduce(x, group=st.tp_group)
     return x
 
@@ -35,7 +40,12 @@ def tp_all_gather(x: torch.Tensor, dim: int = -1) -> torch.Tensor:
         return x
     dim = dim % x.dim()
     out = torch.empty((st.tp_size * x.shape[0],) + tuple(x.shape[1:]), dtype=x.dtype, device=x.device)
-    dist.all_gather_into_tensor(out, x.contiguous(), group=st.tp_group)
+    if x.is_cuda and st.backend == "gloo":  # 1-GPU multi-process rehearsal: stage on the host
+        parts = [torch.empty(x.shape, dtype=x.dtype) for _ in range(st.tp_size)]
+        dist.all_gather(parts, x.cpu(), group=st.tp_group)
+        out.copy_(torch.cat(parts, 0))
+    else:
+        dist.all_gather_into_tensor(out, x.contiguous(), group=st.tp_group)
     out = out.view((st.tp_size,) + tuple(x.shape))
     if dim == 0:
         return out.reshape((-1,) + tuple(x.shape[1:]))
@@ -71,8 +81,23 @@ def dp_all_reduce_max_int(v: int) -> int:
     return int(t.item())
 
 
+def warm_tp_group(device: torch.device):
+    """Create the TP communicator with a first collective outside any hipGraph
+    capture (RCCL must not initialise inside a capture)."""
+    st = get_state()
+    if st.tp_size == 1 or st.backend != "nccl":
+        return
+    t = torch.zeros(64, device=device)
+    dist.all_reduce(t, group=st.tp_group)
+    out = torch.empty(64 * st.tp_size, device=device)
+    dist.all_gather_into_tensor(out, t, group=st.tp_group)
+    torch.cuda.synchronize(device)
+
+
 def tp_src_rank() -> int:
     st = get_state()
+    if st.tp_src is not None:  # replica groups not laid out from rank 0 (bench_pd decode groups)
+        return st.tp_src
     return st.dp_rank * st.tp_size  # TP rank 0 of this replica drives the step
 
 

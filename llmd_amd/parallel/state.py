@@ -37,6 +37,7 @@ class ParallelState:
     cpu_group: Optional[object] = None
     tp_cpu_group: Optional[object] = None  # gloo: TP step-plan broadcast
     backend: str = "none"
+    tp_src: Optional[int] = None  # global rank of this replica's TP driver (default dp_rank * tp_size)
 
     @property
     def ep_size(self) -> int:

@@ -25,11 +25,28 @@ def main():
     ap.add_argument("--quantization", default=None)
     ap.add_argument("--kv-cache-dtype", default="auto")
     ap.add_argument("--host-profile", action="store_true", help="cProfile 20 steps (host-side cost ranking)")
+    ap.add_argument("--tp-shard", type=int, default=1,
+                    help="emulate one rank of a TP-N replica on one GPU: heads, FFN and vocab divided by N "
+                         "(the rank's GEMM/attention/KV work; the TP all-reduces are not included)")
+    ap.add_argument("--kv-cache-gb", type=float, default=None)
     a = ap.parse_args()
+    if a.tp_shard > 1:
+        import dataclasses
+
+        from llmd_amd.engine import config as C
+
+        mc = C.get_model_config(a.model)
+        n = a.tp_shard
+        C._register(dataclasses.replace(
+            mc, name=f"{a.model}-tp{n}-shard", head_dim=mc.head_dim, num_attention_heads=mc.num_attention_heads // n,
+            num_key_value_heads=mc.num_key_value_heads // n, intermediate_size=mc.intermediate_size // n,
+            vocab_size=mc.vocab_size // n))
+        a.model = f"{a.model}-tp{n}-shard"
     cfg = EngineConfig.create(a.model, device="cuda", block_size=64, max_num_seqs=a.batch,
                               max_num_batched_tokens=8192, max_model_len=a.isl + a.steps + 200,
                               cuda_graph_max_bs=a.batch, quantization=a.quantization,
-                              kv_cache_dtype=a.kv_cache_dtype)
+                              kv_cache_dtype=a.kv_cache_dtype,
+                              kv_cache_memory_bytes=int(a.kv_cache_gb * 2**30) if a.kv_cache_gb else None)
     eng = LLMEngine(cfg)
     tstart = time.perf_counter()
     rng = np.random.default_rng(0)
