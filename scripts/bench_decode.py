@@ -42,15 +42,19 @@ def main():
             num_key_value_heads=mc.num_key_value_heads // n, intermediate_size=mc.intermediate_size // n,
             vocab_size=mc.vocab_size // n))
         a.model = f"{a.model}-tp{n}-shard"
+    # requests admitted early decode during the whole chunked-prefill phase
+    # (~batch*isl/8192 steps): size max_tokens so none finishes before the end
+    # of the timed window (the batch must stay full while it is timed)
+    mt = a.steps + 40 + (a.batch * a.isl) // 8192
     cfg = EngineConfig.create(a.model, device="cuda", block_size=64, max_num_seqs=a.batch,
-                              max_num_batched_tokens=8192, max_model_len=a.isl + a.steps + 200,
+                              max_num_batched_tokens=8192, max_model_len=a.isl + mt + 64,
                               cuda_graph_max_bs=a.batch, quantization=a.quantization,
                               kv_cache_dtype=a.kv_cache_dtype,
                               kv_cache_memory_bytes=int(a.kv_cache_gb * 2**30) if a.kv_cache_gb else None)
     eng = LLMEngine(cfg)
     tstart = time.perf_counter()
     rng = np.random.default_rng(0)
-    sp = SamplingParams(max_tokens=a.steps + 20, temperature=0.0, ignore_eos=True)
+    sp = SamplingParams(max_tokens=mt, temperature=0.0, ignore_eos=True)
     for i in range(a.batch):
         eng.add_request(f"r{i}", rng.integers(100, 30000, size=a.isl).tolist(), sp)
     while eng.sched.num_waiting or any(not r.output_token_ids for r in eng.sched.running):
@@ -59,10 +63,14 @@ def main():
         eng.step()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
+    g0 = eng.metrics.n_gen
     for _ in range(a.steps):
         eng.step()
     torch.cuda.synchronize()
     dt = (time.perf_counter() - t0) / a.steps
+    ran = (eng.metrics.n_gen - g0) / a.steps
+    if ran < a.batch:
+        print(f"WARNING: only {ran:.1f} of {a.batch} sequences decoded per timed step", flush=True)
     if a.host_profile:
         import cProfile
         import pstats
@@ -75,7 +83,7 @@ def main():
         pr.disable()
         pstats.Stats(pr).sort_stats("tottime").print_stats(25)
     print(f"{a.model} q={a.quantization} kv={a.kv_cache_dtype} decode batch={a.batch} ctx~{a.isl}: "
-          f"{dt * 1e3:.2f} ms/step  {a.batch / dt:.0f} tok/s (prefill phase {t0 - tstart:.1f}s)", flush=True)
+          f"{dt * 1e3:.2f} ms/step  {ran / dt:.0f} tok/s (running {ran:.0f}) (prefill phase {t0 - tstart:.1f}s)", flush=True)
 
 
 if __name__ == "__main__":

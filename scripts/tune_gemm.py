@@ -41,13 +41,14 @@ def main():
     ap.add_argument("--models", nargs="*", default=["llama-3-70b"])
     ap.add_argument("--ms", type=int, nargs="*", default=[1, 2, 4, 8, 16, 32, 64, 128])
     ap.add_argument("--duration-ms", type=int, default=10)
+    ap.add_argument("--tp", type=int, default=1, help="shapes of one rank of a TP-N replica")
     ap.add_argument("--out", default="gpurun_out/tunableop_gfx950.csv")
     ap.add_argument("--names", nargs="*", default=None,
                     help="subset of qkv/o/gate_up/down/lm_head (prefill M: lm_head only sees sampled rows)")
     a = ap.parse_args()
     shapes = []
     for m in a.models:
-        for name, (N, K) in model_gemm_shapes(m).items():
+        for name, (N, K) in model_gemm_shapes(m, tp=a.tp).items():
             if a.names and name not in a.names:
                 continue
             for M in a.ms:
