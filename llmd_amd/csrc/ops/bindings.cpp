@@ -47,6 +47,9 @@ int llmd_lora_bgmv(const void*, int64_t, const void*, const void*, int, int, int
 int llmd_skinny_gemm(const void*, int64_t, const void*, int64_t, int, int, int, int, int, int, void*, int64_t,
                      float*, hipStream_t);
 int llmd_dgemm_supported(int, int, int);
+int llmd_mgemm(const void*, int64_t, const void*, int64_t, int, int, int, int, int, int, void*, int64_t, float*,
+               hipStream_t);
+int llmd_mgemm_lds(int, int, int);
 int llmd_vmm_granularity(int, size_t*);
 int llmd_vmm_alloc(int, size_t, int, void**, uint64_t*);
 int llmd_vmm_export_fd(uint64_t, int*);
@@ -321,6 +324,29 @@ void skinny_gemm(torch::Tensor y, torch::Tensor x, torch::Tensor w, int64_t rb, 
 }
 
 bool skinny_supported(int64_t M, int64_t rb, int64_t occ) { return llmd_dgemm_supported((int)M, (int)rb, (int)occ); }
+
+// y [M, N] = x [M, K] . w [N, K]^T for 33 <= M <= 128 (decode batches of a P/D
+// decode replica): LDS-DMA staged tiles of 64 wrb W rows x all M, nsplit-way
+// split-K, 3- or 4-stage ring (csrc/ops/mgemm.hip)
+void mgemm(torch::Tensor y, torch::Tensor x, torch::Tensor w, int64_t wrb, int64_t nsplit, int64_t stages,
+           torch::Tensor part) {
+  const c10::hip::OptionalHIPGuard device_guard(dev_of(y));
+  CHECK_CUDA(x); CHECK_BF16(x); CHECK_BF16(w); CHECK_BF16(y); CHECK_INNER(x); CHECK_INNER(w); CHECK_INNER(y);
+  TORCH_CHECK(x.dim() == 2 && w.dim() == 2 && y.dim() == 2, "mgemm: 2-D operands");
+  const int M = x.size(0), K = x.size(1), N = w.size(0);
+  TORCH_CHECK(M >= 1 && M <= 128 && w.size(1) == K && K % 64 == 0, "mgemm: M <= 128, K % 64 == 0");
+  TORCH_CHECK(N % 4 == 0 && y.size(0) == M && y.size(1) == N, "mgemm: output shape / N % 4");
+  TORCH_CHECK(x.stride(0) % 8 == 0 && w.stride(0) % 8 == 0 && y.stride(0) % 4 == 0, "mgemm: row alignment");
+  TORCH_CHECK(llmd_mgemm_lds(M, (int)wrb, (int)stages) > 0, "mgemm: no kernel for wrb=", wrb, " stages=", stages);
+  if (nsplit > 1) {
+    CHECK_DT(part, at::kFloat);
+    TORCH_CHECK(part.numel() >= nsplit * (int64_t)M * N, "mgemm: workspace");
+  }
+  int rc = llmd_mgemm(x.data_ptr(), x.stride(0), w.data_ptr(), w.stride(0), M, N, K, (int)wrb, (int)nsplit,
+                      (int)stages, y.data_ptr(), y.stride(0), nsplit > 1 ? part.data_ptr<float>() : nullptr,
+                      cur_stream());
+  TORCH_CHECK(rc == 0, "mgemm failed: ", rc);
+}
 
 void paged_prefill(torch::Tensor out, torch::Tensor q, torch::Tensor k_cache,
                    torch::Tensor v_cache, torch::Tensor block_tables, torch::Tensor q_start,
@@ -740,6 +766,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("mla_attention", &mla_attention);
   m.def("skinny_gemm", &skinny_gemm);
   m.def("skinny_supported", &skinny_supported);
+  m.def("mgemm", &mgemm);
+  m.def("mgemm_lds", [](int64_t M, int64_t wrb, int64_t stages) { return llmd_mgemm_lds((int)M, (int)wrb, (int)stages); });
   m.def("lora_bgmv", &lora_bgmv);
   m.def("mla_rope_cache", &mla_rope_cache);
   m.def("vmm_granularity", &vmm_granularity);

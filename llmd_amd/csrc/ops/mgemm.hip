@@ -1,0 +1,299 @@
+// Medium-M decode GEMM: Y[M, N] = X[M, K] . W[N, K]^T for M = 33..128 (a decode
+// batch on a P/D decode replica: 64-128 rows per step), bf16 in,
+// fp32 accumulate, bf16 out.
+//
+// Why not skinny_gemm.hip's structure: there every wave streams its own K range
+// of W straight to VGPRs and loads X fragments itself, so X traffic is M / R of
+// the W bytes per workgroup - fine for M <= 16, but at M = 128 the four waves of
+// a 64-row tile pull 8x the W bytes of X through the CU's load path. hipBLASLt's
+// decode picks (MT32x128 tiles, no K split) have the same problem at 2-3.5 TB/s
+// on these shapes (profiles/decode_tp2_shard_70b.log).
+//
+// Here one workgroup owns BN = 64 WRB rows of W (16 WRB per wave, the waves
+// split N) and all M rows of X for one K range of a split-K; per 64-deep k-step
+// the W tile (BN x 128 B) and the X tile (16 MB x 128 B) are copied global -> LDS
+// by LDS-DMA (global_load_lds_dwordx4: no VGPR staging, every byte of W read once
+// from HBM, X read once per workgroup from L2 in whole 128-B lines) into an
+// S-stage ring of separate __shared__ arrays (the waitcnt pass then tells the
+// stages apart and the counted vmcnt keeps S-1 stages in flight across the
+// barrier); each wave reads its A fragments (W) and every B fragment (X) with
+// ds_read_b128 and runs 2 WRB MB mfma_f32_16x16x32_bf16 per k-step.
+// LDS images: 128-B rows, 16-B slot c of row r stored at c ^ ((r >> 1) & 7)
+// (swizzle applied on the DMA source address; destination stays lane-linear):
+// the 16 lanes of a ds_read_b128 pass (16 rows, one k chunk) hit 16 distinct
+// slots of the 256-B bank row.
+// Split-K partials: fp32 [split][M][N], summed and rounded by mgemm_reduce_kernel.
+#include "llmd_common.h"
+
+using namespace llmd;
+
+namespace {
+
+constexpr int NT = 256;  // 4 waves
+
+__device__ __forceinline__ int msw(int r) { return (r >> 1) & 7; }
+
+template <int MB, int WRB, int S>
+struct Geo {
+  static constexpr int BN = 64 * WRB;        // W rows per workgroup
+  static constexpr int BM = 16 * MB;         // X rows (tokens) per workgroup
+  static constexpr int WIMG = BN * 128;      // W image bytes per stage
+  static constexpr int XIMG = BM * 128;      // X image bytes per stage
+  static constexpr int STAGE = WIMG + XIMG;
+  static constexpr int NW = BN / 32;         // W DMA instructions per wave per stage (1 KB = 8 rows each)
+  static constexpr int NX = BM / 32;         // X DMA instructions per wave per stage
+  static constexpr int P = NW + NX;          // DMA instructions per wave per stage
+  static_assert(BM % 32 == 0, "MB must be even");
+};
+
+template <int MB, int WRB, int S>
+__global__ __launch_bounds__(NT, 1) void mgemm_kernel(const uint16_t* __restrict__ x, int64_t x_stride,
+                                                      const uint16_t* __restrict__ wt, int64_t w_stride, int M,
+                                                      int N, int K, int steps_per_split, uint16_t* __restrict__ y,
+                                                      int64_t y_stride, float* __restrict__ part) {
+  using G = Geo<MB, WRB, S>;
+  __shared__ __attribute__((aligned(1024))) char st0[G::STAGE];
+  __shared__ __attribute__((aligned(1024))) char st1[G::STAGE];
+  __shared__ __attribute__((aligned(1024))) char st2[G::STAGE];
+  __shared__ __attribute__((aligned(1024))) char st3[S > 3 ? G::STAGE : 16];
+  const int tile = blockIdx.x, sp = blockIdx.y;
+  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63, g = lane >> 4, c16 = lane & 15;
+  const int ws = __builtin_amdgcn_readfirstlane(wv);
+  const int row0 = tile * G::BN;
+  const int nk = K >> 6;
+  const int s0 = sp * steps_per_split;
+  const int nsteps = min(nk, s0 + steps_per_split) - s0;  // >= 1: the host plans no empty split
+
+  // per-lane DMA source offsets (elements) inside a k-step: instruction j of the
+  // stage fills image rows 8 j .. 8 j + 7; lane L -> row 8 j + L / 8, slot L % 8,
+  // reading global chunk slot ^ msw(row). Wave ws issues j = ws + 4 i.
+  uint32_t woff[G::NW], xoff[G::NX];
+#pragma unroll
+  for (int i = 0; i < G::NW; ++i) {
+    const int r = 8 * (ws + 4 * i) + (lane >> 3);
+    const int gr = min(row0 + r, N - 1);  // rows past N re-read the last row (result dropped)
+    woff[i] = (uint32_t)((int64_t)(gr - row0) * w_stride + 8 * ((lane & 7) ^ msw(r)));
+  }
+#pragma unroll
+  for (int i = 0; i < G::NX; ++i) {
+    const int r = 8 * (ws + 4 * i) + (lane >> 3);
+    xoff[i] = (uint32_t)((int64_t)min(r, M - 1) * x_stride + 8 * ((lane & 7) ^ msw(r)));
+  }
+  const uint16_t* wbase = wt + (int64_t)row0 * w_stride;
+  // each tile starts its K sweep at a rotated step so concurrent workgroups do
+  // not stream the same k columns of W at once (DRAM channel spread)
+  const int rot = nsteps > 0 ? (tile * 5) % nsteps : 0;
+
+  auto issue = [&](char* stg, int t) {
+    const int k0 = (s0 + (t + rot) % nsteps) * 64;
+#pragma unroll
+    for (int i = 0; i < G::NW; ++i)
+      __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)(wbase + k0 + woff[i]),
+                                       (void __attribute__((address_space(3)))*)(stg + 1024 * (ws + 4 * i)), 16, 0,
+                                       0);
+#pragma unroll
+    for (int i = 0; i < G::NX; ++i)
+      __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)(x + k0 + xoff[i]),
+                                       (void __attribute__((address_space(3)))*)(stg + G::WIMG + 1024 * (ws + 4 * i)),
+                                       16, 0, 0);
+  };
+
+  // per-lane LDS read offsets: A (W) rows 16 (WRB wv + rb) + c16, B (X) rows
+  // 16 mb + c16; k chunk 4 h + g for mfma h of the step
+  int aofs[WRB][2], bofs[MB][2];
+#pragma unroll
+  for (int rb = 0; rb < WRB; ++rb) {
+    const int r = 16 * (WRB * wv + rb) + c16;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) aofs[rb][h] = r * 128 + 16 * ((4 * h + g) ^ msw(r));
+  }
+#pragma unroll
+  for (int mb = 0; mb < MB; ++mb) {
+    const int r = 16 * mb + c16;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) bofs[mb][h] = G::WIMG + r * 128 + 16 * ((4 * h + g) ^ msw(r));
+  }
+
+  f32x4_t acc[WRB][MB];
+#pragma unroll
+  for (int rb = 0; rb < WRB; ++rb)
+#pragma unroll
+    for (int mb = 0; mb < MB; ++mb) acc[rb][mb] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  auto compute = [&](const char* stg) {
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      bf16x8_t a[WRB], b[MB];
+#pragma unroll
+      for (int rb = 0; rb < WRB; ++rb) a[rb] = *reinterpret_cast<const bf16x8_t*>(stg + aofs[rb][h]);
+#pragma unroll
+      for (int mb = 0; mb < MB; ++mb) b[mb] = *reinterpret_cast<const bf16x8_t*>(stg + bofs[mb][h]);
+#pragma unroll
+      for (int rb = 0; rb < WRB; ++rb)
+#pragma unroll
+        for (int mb = 0; mb < MB; ++mb)
+          acc[rb][mb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[rb], b[mb], acc[rb][mb], 0, 0, 0);
+    }
+  };
+
+  // ring: stage t lives in st[t % S]; before computing t every wave waits for
+  // its own DMAs of t (leaving the later stages in flight), the barrier makes
+  // all waves' DMAs of t visible, then stage t + S - 1 is issued into the slot
+  // computed at t - 1 (every wave is past that compute: the barrier; its
+  // ds_reads are retired by the lgkmcnt(0) in front of it).
+  // The steady-state loop runs only whole rounds in which every step keeps
+  // S - 2 stages in flight and issues one: no branch inside it, so the waitcnt
+  // pass keeps the per-slot (per-array) DMA bookkeeping instead of falling
+  // back to vmcnt(0) before the LDS reads. vmcnt(n): gfx9 encoding (bits [3:0]
+  // and [15:14]); lgkm/exp fields left open.
+#define MG_WAIT(n) __builtin_amdgcn_s_waitcnt(((n) & 15) | (((n) >> 4) << 14) | (0x7 << 4) | (0xF << 8))
+#define MG_LGKM0() __builtin_amdgcn_s_waitcnt(0xC07F)
+  auto full = [&](char* cur, char* nxt, int t) {
+    MG_WAIT((S - 2) * G::P);
+    MG_LGKM0();
+    __builtin_amdgcn_s_barrier();
+    issue(nxt, t + S - 1);
+    __builtin_amdgcn_sched_barrier(0);
+    compute(cur);
+  };
+  auto tail = [&](char* cur, char* nxt, int t) {
+    if (t >= nsteps) return;
+    const int ahead = min(S - 2, nsteps - 1 - t);
+    if (ahead >= 2) MG_WAIT(2 * G::P);
+    else if (ahead == 1) MG_WAIT(G::P);
+    else MG_WAIT(0);
+    MG_LGKM0();
+    __builtin_amdgcn_s_barrier();
+    if (t + S - 1 < nsteps) issue(nxt, t + S - 1);
+    compute(cur);
+  };
+  // prologue with the arrays named statically (a pointer select would hide the
+  // DMA targets from the waitcnt pass and cost a vmcnt(0) at the loop head)
+  // (unconditional: a stage index past nsteps wraps to a valid k-step and is
+  // never computed; the last step's vmcnt(0) drains it before the exit)
+  issue(st0, 0);
+  issue(st1, 1);
+  if constexpr (S == 4) issue(st2, 2);
+  int t = 0;
+  if constexpr (S == 3) {
+    for (; t + 3 + 2 <= nsteps; t += 3) {
+      full(st0, st2, t);
+      full(st1, st0, t + 1);
+      full(st2, st1, t + 2);
+    }
+    // < 5 steps left
+    tail(st0, st2, t);
+    tail(st1, st0, t + 1);
+    tail(st2, st1, t + 2);
+    tail(st0, st2, t + 3);
+    tail(st1, st0, t + 4);
+  } else {
+    for (; t + 4 + 3 <= nsteps; t += 4) {
+      full(st0, st3, t);
+      full(st1, st0, t + 1);
+      full(st2, st1, t + 2);
+      full(st3, st2, t + 3);
+    }
+    // < 7 steps left
+    tail(st0, st3, t);
+    tail(st1, st0, t + 1);
+    tail(st2, st1, t + 2);
+    tail(st3, st2, t + 3);
+    tail(st0, st3, t + 4);
+    tail(st1, st0, t + 5);
+    tail(st2, st1, t + 6);
+  }
+#undef MG_WAIT
+#undef MG_LGKM0
+
+  // acc[rb][mb][i] = Y^T[row0 + 16 (WRB wv + rb) + 4 g + i][16 mb + c16]
+  const bool whole = gridDim.y == 1;
+#pragma unroll
+  for (int mb = 0; mb < MB; ++mb) {
+    const int m = 16 * mb + c16;
+    if (m >= M) continue;
+#pragma unroll
+    for (int rb = 0; rb < WRB; ++rb) {
+      const int n = row0 + 16 * (WRB * wv + rb) + 4 * g;
+      if (n >= N) continue;  // N % 4 == 0 (host check)
+      const f32x4_t v = acc[rb][mb];
+      if (whole) {
+        const uint32_t lo = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
+        const uint32_t hi = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
+        *reinterpret_cast<uint2*>(y + (int64_t)m * y_stride + n) = make_uint2(lo, hi);
+      } else {
+        *reinterpret_cast<f32x4_t*>(part + ((int64_t)sp * M + m) * N + n) = v;
+      }
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void mgemm_reduce_kernel(const float* __restrict__ part, int nsplit, int M, int N,
+                                                           uint16_t* __restrict__ y, int64_t y_stride) {
+  const int64_t i4 = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 4;
+  const int64_t total = (int64_t)M * N;
+  if (i4 >= total) return;
+  const int m = (int)(i4 / N), n = (int)(i4 % N);
+  f32x4_t s = *reinterpret_cast<const f32x4_t*>(part + i4);
+  for (int k = 1; k < nsplit; ++k) s += *reinterpret_cast<const f32x4_t*>(part + (int64_t)k * total + i4);
+  const uint32_t lo = (uint32_t)f2bf(s[0]) | ((uint32_t)f2bf(s[1]) << 16);
+  const uint32_t hi = (uint32_t)f2bf(s[2]) | ((uint32_t)f2bf(s[3]) << 16);
+  *reinterpret_cast<uint2*>(y + (int64_t)m * y_stride + n) = make_uint2(lo, hi);
+}
+
+typedef void (*mkern_t)(const uint16_t*, int64_t, const uint16_t*, int64_t, int, int, int, int, uint16_t*, int64_t,
+                        float*);
+
+template <int MB>
+mkern_t pick_w(int wrb, int stages) {
+  if (wrb == 1) return stages == 3 ? mgemm_kernel<MB, 1, 3> : mgemm_kernel<MB, 1, 4>;
+  if (wrb == 2) return stages == 3 ? mgemm_kernel<MB, 2, 3> : mgemm_kernel<MB, 2, 4>;
+  if (wrb == 4) {
+    if (stages == 3) return mgemm_kernel<MB, 4, 3>;
+    if constexpr (MB == 4) return mgemm_kernel<MB, 4, 4>;  // 160 KB: the only 4-stage ring of 256-row tiles that fits
+  }
+  return nullptr;
+}
+
+mkern_t pick_m(int mb, int wrb, int stages) {
+  switch (mb) {
+    case 4: return pick_w<4>(wrb, stages);
+    case 6: return pick_w<6>(wrb, stages);
+    case 8: return pick_w<8>(wrb, stages);
+  }
+  return nullptr;
+}
+
+}  // namespace
+
+// LDS bytes of one (M, wrb, stages) configuration; 0 if not instantiated
+extern "C" int llmd_mgemm_lds(int M, int wrb, int stages) {
+  if (M < 1 || M > 128 || (wrb != 1 && wrb != 2 && wrb != 4) || (stages != 3 && stages != 4)) return 0;
+  const int mb = M <= 64 ? 4 : M <= 96 ? 6 : 8;
+  const int lds = stages * (64 * wrb * 128 + 16 * mb * 128);
+  return lds <= 160 * 1024 ? lds : 0;
+}
+
+// Y = X W^T, M <= 128, K % 64 == 0, N % 4 == 0; wrb: 64-row W tiles per workgroup
+// (1, 2 or 4), nsplit K splits (part: nsplit * M * N fp32 when > 1), stages 3 or 4.
+extern "C" int llmd_mgemm(const void* x, int64_t x_stride, const void* w, int64_t w_stride, int M, int N, int K,
+                          int wrb, int nsplit, int stages, void* y, int64_t y_stride, float* part, hipStream_t st) {
+  if (M < 1 || M > 128 || K % 64 != 0 || N % 4 != 0 || nsplit < 1 || x_stride % 8 || w_stride % 8) return -1;
+  if (llmd_mgemm_lds(M, wrb, stages) == 0) return -1;
+  const int mb = M <= 64 ? 4 : M <= 96 ? 6 : 8;
+  mkern_t k = pick_m(mb, wrb, stages);
+  if (k == nullptr) return -2;
+  const int nk = K / 64;
+  const int per = (nk + nsplit - 1) / nsplit;
+  nsplit = (nk + per - 1) / per;  // no empty splits
+  const int bn = 64 * wrb;
+  dim3 grid((N + bn - 1) / bn, nsplit);
+  hipLaunchKernelGGL(k, grid, dim3(NT), 0, st, (const uint16_t*)x, x_stride, (const uint16_t*)w, w_stride, M, N, K,
+                     per, (uint16_t*)y, y_stride, part);
+  if (nsplit > 1) {
+    const int64_t total4 = (int64_t)M * N / 4;
+    hipLaunchKernelGGL(mgemm_reduce_kernel, dim3((unsigned)((total4 + 255) / 256)), dim3(256), 0, st, part, nsplit,
+                       M, N, (uint16_t*)y, y_stride);
+  }
+  return (int)hipGetLastError();
+}

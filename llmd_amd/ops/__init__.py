@@ -571,15 +571,60 @@ def dgemm_choice(M: int, N: int, K: int) -> Optional[tuple[int, int, int]]:
     return None
 
 
+def mgemm(x: torch.Tensor, w: torch.Tensor, plan: tuple[int, int, int]) -> torch.Tensor:
+    """Y = X W^T for 33 <= M <= 128 on the LDS-DMA medium-M decode GEMM
+    (csrc/ops/mgemm.hip); plan = (wrb: 64-row W tiles per workgroup, nsplit,
+    stages)."""
+    M, K = x.shape
+    N = w.shape[0]
+    wrb, ns, stages = plan
+    y = torch.empty(M, N, dtype=x.dtype, device=x.device)
+    part = torch.empty(ns * M * N if ns > 1 else 0, dtype=torch.float32, device=x.device)
+    native().mgemm(y, x, w, wrb, ns, stages, part)
+    return y
+
+
+def mgemm_ok(x: torch.Tensor, w: torch.Tensor) -> bool:
+    M = x.shape[0] if x.dim() == 2 else -1
+    return (_gpu(x) and 1 <= M <= 128 and x.shape[1] % 64 == 0 and x.dtype == torch.bfloat16
+            and w.dtype == torch.bfloat16 and w.shape[0] % 4 == 0 and x.stride(-1) == 1 and x.stride(0) % 8 == 0
+            and w.is_contiguous())
+
+
+_MGEMM_MS = (64, 96, 128)
+
+
+def mgemm_choice(M: int, N: int, K: int) -> Optional[tuple[int, int, int]]:
+    """Plan of the medium-M decode GEMM for this shape, or None: the measured
+    table (ops/mgemm_table.py, winners over hipBLASLt and the small-M kernel)
+    at the smallest measured M >= this one."""
+    from .mgemm_table import MGEMM_TABLE
+
+    for m in _MGEMM_MS:
+        if m >= M:
+            e = MGEMM_TABLE.get((m, N, K))
+            return e[0] if e is not None else None
+    return None
+
+
 def linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """Dense projection: decode-sized M (<= 64) on the decode GEMM stream kernel
-    (csrc/ops/skinny_gemm.hip) where the dispatch table measured it faster than
-    hipBLASLt, everything else on hipBLASLt."""
-    if _SKINNY and skinny_ok(x, w):
-        plan = dgemm_choice(x.shape[0], w.shape[0], w.shape[1])
-        if plan is not None:
-            y = skinny_gemm(x, w, plan)
-            return y if bias is None else y.add_(bias)
+    """Dense projection: decode-sized M on our decode GEMM kernels where their
+    measured dispatch tables have them ahead of hipBLASLt - the medium-M LDS-DMA
+    kernel (csrc/ops/mgemm.hip, M 33..128, ops/mgemm_table.py) first, then the
+    stream kernel (csrc/ops/skinny_gemm.hip, M <= 64, ops/dgemm_table.py) -
+    everything else on hipBLASLt."""
+    if _SKINNY:
+        M = x.shape[0] if x.dim() == 2 else 0
+        if 33 <= M <= 128 and mgemm_ok(x, w):
+            plan = mgemm_choice(M, w.shape[0], w.shape[1])
+            if plan is not None:
+                y = mgemm(x, w, plan)
+                return y if bias is None else y.add_(bias)
+        if skinny_ok(x, w):
+            plan = dgemm_choice(M, w.shape[0], w.shape[1])
+            if plan is not None:
+                y = skinny_gemm(x, w, plan)
+                return y if bias is None else y.add_(bias)
     return torch.nn.functional.linear(x, w, bias)
 
 
