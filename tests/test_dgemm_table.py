@@ -28,3 +28,21 @@ def test_cpu_linear_is_plain():
     x = torch.randn(4, 256)
     w = torch.randn(64, 256)
     torch.testing.assert_close(ops.linear(x, w), x @ w.T)
+
+
+def test_mgemm_table_entries_and_buckets():
+    from llmd_amd.ops.mgemm_table import MGEMM_TABLE
+
+    for (M, N, K), (plan, t_ours, t_other) in MGEMM_TABLE.items():
+        assert M in (64, 96, 128) and K % 64 == 0 and N % 4 == 0
+        if plan is not None:
+            wrb, ns, stages = plan
+            assert wrb in (1, 2, 4) and 1 <= ns <= K // 64 and stages in (3, 4)
+            mb = 4 if M <= 64 else 6 if M <= 96 else 8
+            assert stages * (64 * wrb * 128 + 16 * mb * 128) <= 160 * 1024  # LDS of the instantiation
+            assert t_ours < 0.95 * t_other
+    # M 65..96 use the 96 row, 97..128 the 128 row; unmeasured M/shape -> None
+    assert ops.mgemm_choice(80, 5120, 8192) == MGEMM_TABLE[(96, 5120, 8192)][0]
+    assert ops.mgemm_choice(100, 5120, 8192) == MGEMM_TABLE[(128, 5120, 8192)][0]
+    assert ops.mgemm_choice(129, 5120, 8192) is None
+    assert ops.mgemm_choice(64, 1234, 4096) is None
