@@ -89,7 +89,7 @@ def warm_tp_group(device: torch.device):
         return
     t = torch.zeros(64, device=device)
     dist.all_reduce(t, group=st.tp_group)
-    out = torch.empty(64 * st.tp_size, device=device)
+    out = torch.empty(64 * dist.get_world_size(st.tp_group), device=device)
     dist.all_gather_into_tensor(out, t, group=st.tp_group)
     torch.cuda.synchronize(device)
 
