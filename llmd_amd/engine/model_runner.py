@@ -135,7 +135,18 @@ class ModelRunner:
 
             warm_tp_group(self.device)
         if self.tp_size > 1 and not pc.disable_custom_all_reduce and symm.enabled_by_env():
-            symm.init(st.tp_rank, st.tp_size, group=st.tp_cpu_group, tp_allreduce=True)
+            # every TP rank must agree: a rank that could not map a peer's heap
+            # would otherwise wait on epochs its peers never write
+            ok = 1
+            try:
+                symm.init(st.tp_rank, st.tp_size, group=st.tp_cpu_group, tp_allreduce=True)
+            except Exception as e:  # noqa: BLE001 - fall back to RCCL all-reduce
+                log.warning("custom all-reduce unavailable (%s); using RCCL", e)
+                ok = 0
+            from llmd_amd.parallel.comm import tp_min_int
+
+            if tp_min_int(ok) == 0:
+                symm.shutdown()
         elif (ep_mod.canonical(pc.all2all_backend) == "symm_ll" and st.dp_size > 1 and st.tp_size == 1
               and self.mc.is_moe):
             rows = max(self.cfg.cuda_graph_max_bs, 256)

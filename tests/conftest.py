@@ -26,3 +26,15 @@ def pytest_collection_modifyitems(config, items):
     for it in items:
         if "gpu" in it.keywords:
             it.add_marker(skip)
+
+
+@pytest.fixture(autouse=True)
+def _seed_torch():
+    """This PyTorch build seeds its default generator randomly per process, and
+    many tests build random-init tiny models whose greedy outputs are compared
+    across parallel layouts (TP / EP / DBO sum in other orders): a fixed seed
+    keeps those models - and any near-ties in their logits - the same every run."""
+    import torch
+
+    torch.manual_seed(int(os.environ.get("LLMD_TEST_SEED", "0")))
+    yield

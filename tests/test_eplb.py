@@ -15,6 +15,7 @@ from llmd_amd.engine.request import SamplingParams
 from llmd_amd.parallel import eplb
 
 from test_wide_ep import NTOK, _cfg, _free_port, _prompts
+from greedy_check import assert_greedy_match
 
 
 def test_plan_placement_invariants():
@@ -92,6 +93,5 @@ def test_eplb_world2_matches_single_process(tmp_path):
         assert d["P_local"] == 9  # (16 experts + 2 redundant) / 2 ranks
         assert d["moved"]         # at least one rebalance changed the placement
         got = d["tokens"]
-        agree = sum(int(a == b) for g, w in zip(got, want[rank]) for a, b in zip(g, w))
-        total = sum(len(w) for w in want[rank])
-        assert all(g[:3] == w[:3] for g, w in zip(got, want[rank])) and agree >= 0.8 * total, (rank, got, want)
+        # EP combines expert partial sums in another order (bf16): greedy_check
+        assert_greedy_match(ref, _prompts(rank), got, want[rank])

@@ -11,6 +11,7 @@ import torch.multiprocessing as mp
 from llmd_amd.engine.config import EngineConfig
 from llmd_amd.engine.engine import LLMEngine
 from llmd_amd.engine.request import SamplingParams
+from greedy_check import assert_greedy_match
 
 MODEL = "tiny-llama"
 
@@ -59,15 +60,19 @@ def test_tp2_matches_tp1(tmp_path):
 
     path = str(tmp_path / "model.safetensors")
     cfg1 = _cfg(None)
+    torch.manual_seed(0)  # fixed weights: TP sums in another order, so a random model can hold near-ties
     save_safetensors(export_hf(build_model(cfg1.model_config, device="cpu", max_pos=600)), path)
     eng = LLMEngine(_cfg(path))
     ref = eng.generate(_prompts(), SamplingParams(max_tokens=6, temperature=0.0, ignore_eos=True, logprobs=1))
     out = str(tmp_path / "tp2.pt")
     mp.spawn(_worker, args=(2, _free_port(), path, out), nprocs=2, join=True)
     got = torch.load(out, weights_only=True)
+    # TP all-reduces sum the row-parallel shards in another order (bf16): a
+    # first divergence must be a near-tie of the TP1 engine (greedy_check)
+    assert_greedy_match(eng, _prompts(), got["tokens"], [r.output_token_ids for r in ref])
     for r, toks, lps in zip(ref, got["tokens"], got["lp"]):
-        assert toks == r.output_token_ids
-        assert np.allclose(lps, r.output_logprobs, atol=0.05)
+        if toks == r.output_token_ids:
+            assert np.allclose(lps, r.output_logprobs, atol=0.05)
 
 
 def _pd_worker(rank, world, port, path, out):
@@ -142,14 +147,15 @@ def test_pd_tp1_prefill_to_tp2_decode(tmp_path):
     from llmd_amd.models.loader import export_hf, save_safetensors
 
     path = str(tmp_path / "model.safetensors")
+    torch.manual_seed(0)
     save_safetensors(export_hf(build_model(_cfg(None).model_config, device="cpu", max_pos=600)), path)
-    ref = LLMEngine(_cfg(path)).generate(_prompts(), SamplingParams(max_tokens=6, temperature=0.0,
-                                                                     ignore_eos=True))
+    ref_eng = LLMEngine(_cfg(path))
+    ref = ref_eng.generate(_prompts(), SamplingParams(max_tokens=6, temperature=0.0, ignore_eos=True))
     out = str(tmp_path / "pd.pt")
     mp.spawn(_pd_worker, args=(3, _free_port(), path, out), nprocs=3, join=True)
     got = torch.load(out, weights_only=True)
-    for r, toks, cached, p in zip(ref, got["tokens"], got["cached"], _prompts()):
-        assert toks == r.output_token_ids
+    assert_greedy_match(ref_eng, _prompts(), got["tokens"], [r.output_token_ids for r in ref])
+    for cached, p in zip(got["cached"], _prompts()):
         assert cached == len(p) - 1  # prompt KV came over kvx, not recomputed
     pg = torch.load(out + ".p", weights_only=True)
     assert pg["held_before"] == 3 and pg["held_after"] == 0 and pg["free"] == pg["total"]
