@@ -14,6 +14,7 @@ from typing import Iterable, Optional
 import torch
 
 from llmd_amd import _rt_loader
+from llmd_amd.utils import markers
 
 from .config import EngineConfig
 from .metrics import EngineMetrics
@@ -107,7 +108,8 @@ class LLMEngine:
         if self.connector is not None:
             self.connector.tick()
         t0 = time.monotonic()
-        so = self.sched.schedule()
+        with markers.range("llmd.schedule"):
+            so = self.sched.schedule()
         if self.connector is not None and self.runner.tp_size > 1:
             self.connector.flush_tp()
         if self.lora is not None:
@@ -124,7 +126,8 @@ class LLMEngine:
         if self.offload is not None:
             self.offload.before_step(so)
         sampled = self.runner.execute(so, self.block_tables(so))
-        return self._finish_step(so, sampled, err_outs, t0)
+        with markers.range("llmd.update"):
+            return self._finish_step(so, sampled, err_outs, t0)
 
     # ------------------------------------------------------------ DP lockstep
     def _lockstep_step(self, so, err_outs, t0) -> list[RequestOutput]:

@@ -26,6 +26,7 @@ from llmd_amd import ops
 from llmd_amd.models import build_model
 from llmd_amd.parallel.comm import tp_broadcast_plan, tp_min_int
 from llmd_amd.parallel.state import get_state
+from llmd_amd.utils import markers
 
 from .attn_meta import AttnMeta
 from .config import EngineConfig
@@ -354,14 +355,16 @@ class ModelRunner:
         same kind of step with the same collective shapes)."""
         if so.empty:
             return {}
-        pl, reqs = self.plan(so, block_tables)
-        if force_eager:
-            pl["graph"] = False
-        elif bucket is not None and pl["graph"]:
-            pl["bucket"] = bucket
-        if self.tp_size > 1:
-            tp_broadcast_plan(pl)  # TP followers run the same plan (engine/tp_worker.py)
-        logits = self.run_plan(pl)
+        with markers.range("llmd.plan"):
+            pl, reqs = self.plan(so, block_tables)
+            if force_eager:
+                pl["graph"] = False
+            elif bucket is not None and pl["graph"]:
+                pl["bucket"] = bucket
+            if self.tp_size > 1:
+                tp_broadcast_plan(pl)  # TP followers run the same plan (engine/tp_worker.py)
+        with markers.range("llmd.forward"):
+            logits = self.run_plan(pl)
         if not reqs:
             return {}
         if pl.get("embed") and getattr(self, "_last_hidden", None) is not None:
@@ -370,7 +373,8 @@ class ModelRunner:
             for i, r in enumerate(reqs):
                 if r.params.embed:
                     r.extra["embedding"] = e[i].tolist()
-        return self._sample(logits, reqs)
+        with markers.range("llmd.sample"):
+            return self._sample(logits, reqs)
 
     def plan(self, so: SchedulerOutput, block_tables: dict[int, list[int]]) -> tuple[dict, list]:
         """Host-side step description: everything a (TP) rank needs to run the

@@ -64,6 +64,8 @@ import msgpack
 import numpy as np
 import torch
 
+from llmd_amd.utils import markers
+
 log = logging.getLogger("llmd.kvx")
 
 
@@ -406,11 +408,13 @@ class KvxAgent:
                 self._notify_free(job.params)
                 self._complete(job, False)
                 continue
+            mk = markers.start(f"llmd.kvx.pull {job.request_id}")
             try:
                 ok, nbytes = self._do_load(job)
             except Exception as e:  # noqa: BLE001 - NIXL_ERR_BACKEND equivalent
                 log.warning("kvx load %s failed: %s", job.request_id, e)
                 ok = False
+            markers.stop(mk)
             if self.metrics is not None:
                 self.metrics.observe(ok, time.monotonic() - t0, nbytes, len(job.local_blocks))
             self._take_cancel(job.request_id)  # a cancel that raced the running pull
