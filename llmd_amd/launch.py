@@ -7,6 +7,9 @@ A topology YAML names the model, the router and the engine roles::
   model: llama-3-70b
   gpus: 8                      # GPUs on the host (default: all visible)
   router: {port: 8000, config: <EndpointPickerConfig path or inline YAML>}
+                               # mode: extproc -> the EPP as an Envoy ext_proc
+                               # gRPC server on grpc_port (9002) for an external
+                               # Envoy / Gateway instead of the built-in proxy
   roles:
     - name: prefill            # llm-d.ai/role label: prefill | decode | prefill-decode
       replicas: 6
@@ -113,14 +116,21 @@ def plan(topo: dict, workdir: str) -> tuple[list[ProcSpec], dict]:
     r = topo.get("router")
     if r:
         ep_file = os.path.join(workdir, "endpoints.yaml")
-        cmd = [PY, "-m", "llmd_amd.router.proxy", "--port", str(r.get("port", 8000)), "--endpoints-file", ep_file]
+        if r.get("mode", "proxy") == "extproc":
+            cmd = [PY, "-m", "llmd_amd.router.extproc", "--grpc-port", str(r.get("grpc_port", 9002)),
+                   "--grpc-health-port", str(r.get("grpc_health_port", 9003)),
+                   "--metrics-port", str(r.get("metrics_port", 9090)), "--endpoints-file", ep_file]
+        else:
+            cmd = [PY, "-m", "llmd_amd.router.proxy", "--port", str(r.get("port", 8000)),
+                   "--endpoints-file", ep_file]
         conf = r.get("config")
         if conf:
             if os.path.exists(str(conf)):
                 cmd += ["--config-file", str(conf)]
             else:
                 cmd += ["--config-text", conf if isinstance(conf, str) else yaml.safe_dump(conf)]
-        procs.append(ProcSpec("router", cmd, {}, [], int(r.get("port", 8000)), "router"))
+        rport = int(r.get("grpc_port", 9002)) if r.get("mode") == "extproc" else int(r.get("port", 8000))
+        procs.append(ProcSpec("router", cmd, {}, [], rport, "router"))
     return procs, doc
 
 

@@ -85,3 +85,20 @@ def test_dashboards_reference_exported_metrics():
                 for m in re.findall(r"(vllm:[a-z_]+|inference_[a-z_]+|llm_d_[a-z_]+)", t["expr"]):
                     base = re.sub(r"_(bucket|sum|count|total)$", "", m)
                     assert base in names or m in names, (f, m)
+
+
+def test_router_extproc_mode_and_envoy_config():
+    topo = {"model": "llama-3-8b", "gpus": 2, "roles": [{"name": "both", "replicas": 2}],
+            "router": {"mode": "extproc", "grpc_port": 9102}}
+    specs, _ = plan(topo, "/tmp/w")
+    r = specs[-1]
+    assert r.name == "router" and r.port == 9102 and "llmd_amd.router.extproc" in r.cmd
+    with open(os.path.join(ROOT, "deploy/standalone/envoy-extproc.yaml")) as f:
+        env = yaml.safe_load(f)
+    hcm = env["static_resources"]["listeners"][0]["filter_chains"][0]["filters"][0]["typed_config"]
+    ext = hcm["http_filters"][0]["typed_config"]
+    assert ext["processing_mode"]["request_body_mode"] == "FULL_DUPLEX_STREAMED"
+    cl = {c["name"]: c for c in env["static_resources"]["clusters"]}
+    assert cl["picked_endpoint"]["original_dst_lb_config"]["http_header_name"] == "x-gateway-destination-endpoint"
+    ep = cl["llmd_epp"]["load_assignment"]["endpoints"][0]["lb_endpoints"][0]["endpoint"]["address"]
+    assert ep["socket_address"]["port_value"] == 9002
