@@ -335,10 +335,12 @@ __global__ __launch_bounds__(64 * NW, 1) void mla_v2_kernel(
       for (int b4 = 0; b4 < 4; ++b4)
 #pragma unroll
         for (int i = 0; i < 4; ++i) mx = fmaxf(mx, sc[b4][i]);
-      mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
-      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-      const float tm = mx * scale_log2;
-      if (__ballot(tm > m + 8.f) != 0) {  // lazy rescale (threshold 2^8), wave-uniform
+      // lane-local max decides; the cross-lane max only when a head's row grows
+      // (attn_prefill.hip prefill_v2_kernel); l is a per-lane partial until the epilogue
+      const float tl = mx * scale_log2;
+      if (__ballot(tl > m + 8.f) != 0) {  // lazy rescale (threshold 2^8), wave-uniform
+        float tm = fmaxf(tl, __shfl_xor(tl, 16, 64));
+        tm = fmaxf(tm, __shfl_xor(tm, 32, 64));
         const float mnew = fmaxf(m, tm);
         const float alpha = (mnew == NEG_INF) ? 1.f : __builtin_amdgcn_exp2f(m - mnew);
         l *= alpha;
@@ -360,8 +362,6 @@ __global__ __launch_bounds__(64 * NW, 1) void mla_v2_kernel(
           sc[b4][i] = p;
           ps += p;
         }
-      ps += __shfl_xor(ps, 16, 64);
-      ps += __shfl_xor(ps, 32, 64);
       l += ps;
       // ---- O[head][dim] += P[head][key] . V[key][dim]   (V = first 512 dims of the key row)
 #pragma unroll
@@ -441,6 +441,8 @@ __global__ __launch_bounds__(64 * NW, 1) void mla_v2_kernel(
     }
   }
   // ---- epilogue: O rows are heads 16w + 4g + i (stats in lane 4g + i), columns dims 16n + c16
+  l += __shfl_xor(l, 16, 64);  // the head's 4 lane partials
+  l += __shfl_xor(l, 32, 64);
   if (nsplit == 1) {
     const float inv = l > 0.f ? kv_scale / l : 0.f;
 #pragma unroll

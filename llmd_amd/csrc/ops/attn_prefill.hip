@@ -207,16 +207,16 @@ __global__ __launch_bounds__(NT, 2) void prefill_kernel(
         for (int b4 = 0; b4 < 4; ++b4)
 #pragma unroll
           for (int i = 0; i < 4; ++i) mx = fmaxf(mx, sc[b4][nb][i]);
-        mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
-        mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-        mt[nb] = mx * scale_log2;
+        mt[nb] = mx * scale_log2;  // lane-local (see prefill_v2_kernel)
         grow = grow || (mt[nb] > m[nb] + 8.f);
       }
       if (__ballot(grow) != 0) {  // wave-uniform
         float alpha[2];
 #pragma unroll
         for (int nb = 0; nb < 2; ++nb) {
-          const float mnew = fmaxf(m[nb], mt[nb]);
+          float mx = fmaxf(mt[nb], __shfl_xor(mt[nb], 16, 64));
+          mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+          const float mnew = fmaxf(m[nb], mx);
           alpha[nb] = (mnew == NEG_INF) ? 1.f : __builtin_amdgcn_exp2f(m[nb] - mnew);
           lsum[nb] *= alpha[nb];
           m[nb] = mnew;
@@ -243,9 +243,7 @@ __global__ __launch_bounds__(NT, 2) void prefill_kernel(
             sc[b4][nb][i] = p;
             ps += p;
           }
-        ps += __shfl_xor(ps, 16, 64);
-        ps += __shfl_xor(ps, 32, 64);
-        lsum[nb] += ps;
+        lsum[nb] += ps;  // lane-partial, reduced in the epilogue
       }
       // ---- O += P V
       const int qq = c16 >> 2, pp = c16 & 3;
@@ -284,7 +282,8 @@ __global__ __launch_bounds__(NT, 2) void prefill_kernel(
   const float sink = sinks ? sinks[head] * 1.4426950408889634f : NEG_INF;
 #pragma unroll
   for (int nb = 0; nb < 2; ++nb) {
-    float den = lsum[nb];
+    float den = lsum[nb] + __shfl_xor(lsum[nb], 16, 64);
+    den += __shfl_xor(den, 32, 64);
     if (sinks) den += exp2f(sink - (m[nb] == NEG_INF ? 0.f : m[nb]));
     const float inv = den > 0.f ? vscale / den : 0.f;
 #pragma unroll
