@@ -10,18 +10,22 @@ flight (closed loop: a finished request is immediately replaced), W warmup
 steps bring the batch to steady state, then exactly K steps are timed between
 barrier+synchronize brackets; the slowest rank's time is used.
 
-Modes (default ``auto``: agg for N < 4, pd for N >= 4)
+Modes (default ``auto``: agg for N < 8, pd for N >= 8)
   agg : every GPU is an independent aggregated replica (dp N) - the
         optimized-baseline topology; per-GPU work fixed as N grows (weak scaling).
-  pd  : ranks [0, P) prefill, [P, N) decode (P = 3N/4 unless --prefill-gpus;
-        ISL 5000 / OSL 250 is prefill-heavy, so 6P2D is the throughput-optimal
-        split on 8 GPUs); KV moves over xGMI (kvx VMM-chunked IPC pool).
-        One 70B bf16 prefill GPU feeds ~10k prompt tok/s = ~500 output tok/s
-        of decode, a quarter of what one decode GPU sustains at batch 64, so a
-        P:D split needs >= 4 GPUs to be balanced (the reference tunes the ratio
-        per workload, guides/pd-disaggregation/README.md:15-33); on 2 GPUs a
-        1P1D split would idle the decoder and auto runs two aggregated
-        replicas instead.
+  pd  : ranks [0, P) prefill, [P, N) decode (P = 3N/4 unless --prefill-gpus),
+        decode ranks paired into TP2 replicas when they can (--decode-tp);
+        KV moves over xGMI (kvx VMM-chunked IPC pool). Measured on one
+        MI355X: a 70B bf16 prefill rank feeds 481-497 output tok/s
+        (scripts/bench_prefill_rate.py), a TP1 decode replica at batch 64
+        sustains 1349 tok/s (47.5 ms/step) and one aggregated GPU 358 tok/s.
+        So 1P1D (N=2) idles the decoder and 3P1D (N=4) is decode-bound at
+        ~1350 < 4 x 358: both run aggregated. From N=8, 6P + one TP2 decode
+        replica (two GPUs, batch 128 in ~40 ms + the TP all-reduces) balances
+        the six prefill GPUs at ~2900-3000 tok/s, above 8 aggregated GPUs
+        (~2860), with the prefill of every request on a dedicated GPU. The
+        reference tunes the P:D ratio per workload the same way
+        (guides/pd-disaggregation/README.md:15-33).
 
 Output: one JSON line on rank 0 (see README "bench.py contract").
 """
@@ -56,7 +60,7 @@ def parse():
     p.add_argument("--max-num-batched-tokens", type=int, default=8192)
     p.add_argument("--block-size", type=int, default=64)
     p.add_argument("--mode", default="auto", choices=["auto", "agg", "pd"],
-                   help="auto: aggregated replicas on N < 4, P/D disaggregation (3/4 prefill ranks) on N >= 4")
+                   help="auto: aggregated replicas on N < 8, P/D disaggregation (3/4 prefill ranks) on N >= 8")
     p.add_argument("--prefill-gpus", type=int, default=0, help="pd mode: number of prefill ranks")
     p.add_argument("--decode-tp", type=int, default=0,
                    help="pd mode: TP degree of each decode replica (0 = 2 when the decode ranks pair up, else 1)")
@@ -107,7 +111,7 @@ def main():
             dist.init_process_group("gloo", rank=rank, world_size=world)
 
     if a.mode == "auto":
-        a.mode = "pd" if world >= 4 else "agg"
+        a.mode = "pd" if world >= 8 else "agg"
     if a.mode == "pd":
         from llmd_amd.bench_pd import run_pd
 

@@ -2,7 +2,7 @@
 set -o pipefail
 mkdir -p gpurun_out
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
-timeout -k 10 600 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/prof_d70 -o run -- python3 scripts/bench_decode.py --model llama-3-70b --batch 64 --isl 5000 --steps 30 > gpurun_out/d70_bench.log 2>&1 || { echo "prof failed"; tail -20 gpurun_out/d70_bench.log; exit 1; }
+timeout -k 10 600 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/prof_d70 -o run -- python3 scripts/bench_decode.py --model llama-3-70b --batch 64 --isl 5000 --steps 40 > gpurun_out/d70_bench.log 2>&1 || { echo "prof failed"; tail -20 gpurun_out/d70_bench.log; exit 1; }
 f=$(find gpurun_out/prof_d70 -name '*kernel_trace.csv' | head -1)
 { grep "decode batch" gpurun_out/d70_bench.log; python scripts/busy_from_trace.py "$f" 1.0 --breakdown; } | tee gpurun_out/d70_summary.txt
 rm -f "$f"
