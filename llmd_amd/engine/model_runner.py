@@ -1,10 +1,13 @@
 """Model runner: owns the model, the paged KV cache and the per-step execution.
 
-KV cache: one tensor ``[num_blocks, L, 2, Hkv, block_size, D]`` bf16, i.e. a
-block of every layer is one contiguous slab. Per-layer views
-``kv[:, l, 0]`` / ``kv[:, l, 1]`` are what the kernels consume. Keeping a
-whole block contiguous across layers makes P/D transfer and host offload one
-large DMA per block (kvx).
+KV cache: one tensor ``[L, num_blocks, 2, Hkv, block_size, D]`` (layer-major):
+per-layer views ``kv[l, :, 0]`` / ``kv[l, :, 1]`` are contiguous pools, which
+is what the attention kernels stream. A block-major layout (one block of
+every layer contiguous, a single DMA per block for P/D and offload) cost the
+decode kernel 5-11 % (203-208 vs 219-227 us per 70B layer at batch 64 ctx
+5000, profiles/attn_decode_layout.txt): a sequence's blocks of one layer then
+sit 20 MB apart across a 100+ GB range. Transfers instead move a block as 2 L
+per-layer segments (kvx copy kernel segment lists, offload gathers).
 
 Decode-only steps replay a captured hipGraph per batch bucket:
 all inputs live in static device buffers, padded rows have ``slot = -1`` and
@@ -169,7 +172,7 @@ class ModelRunner:
 
     def _alloc_cache(self, num_blocks: int, scratch: bool = False) -> torch.Tensor:
         planes, heads, dim = self.kv_spec
-        shape = (num_blocks, self.L, planes, heads, self.bs, dim)
+        shape = (self.L, num_blocks, planes, heads, self.bs, dim)
         self.vmm = None
         if not scratch and self._wants_vmm():
             C = ops.native()
@@ -189,10 +192,10 @@ class ModelRunner:
     def _bind(self, kv: Optional[torch.Tensor]):
         for i, a in enumerate(self.model.attention_layers()):
             if hasattr(a, "bind_cache"):
-                a.bind_cache(kv[:, i]) if kv is not None else setattr(a, "cache", None)
+                a.bind_cache(kv[i]) if kv is not None else setattr(a, "cache", None)
             else:
-                a.k_cache = kv[:, i, 0] if kv is not None else None
-                a.v_cache = kv[:, i, 1] if kv is not None else None
+                a.k_cache = kv[i, :, 0] if kv is not None else None
+                a.v_cache = kv[i, :, 1] if kv is not None else None
 
     def _mla_rows(self, meta: AttnMeta, nd: int, p_ql, p_ctx):
         """Row metadata of the latent-attention kernel (decode rows + one row per

@@ -17,8 +17,11 @@ committed, so those tokens are skipped by prefill.
 Tier changes are published as KV events with ``medium`` cpu / disk so the
 router's precise index scores them with tier weights.
 
-Whole-block contiguity of the KV layout ([num_blocks, L, 2, Hkv, bs, D]) makes
-every transfer a single contiguous DMA of ``block_bytes``.
+The device pool is layer-major ([L, num_blocks, 2, Hkv, bs, D], see
+engine/model_runner.py); a host slot holds one block block-major
+([L, 2, Hkv, bs, D], ``block_bytes``), so the side stream gathers the step's
+blocks into one contiguous staging tensor (one kernel) and DMAs each row to
+its slot; reloads DMA a slot into a staging row and scatter it back.
 """
 from __future__ import annotations
 
@@ -42,7 +45,8 @@ class OffloadManager:
         extra = oc.get("kv_connector_extra_config", oc)
         self.engine = engine
         self.kv = engine.runner.kv
-        self.block_bytes = self.kv[0].numel() * self.kv.element_size()
+        self.block_bytes = self.kv[:, 0].numel() * self.kv.element_size()
+        self.blk_shape = (self.kv.shape[0],) + tuple(self.kv.shape[2:])  # one block, block-major
         cpu_bytes = int(extra.get("cpu_bytes_to_use", extra.get("cpu_bytes", 1 << 30)))
         self.n_slots = max(1, cpu_bytes // self.block_bytes)
         pin = self.kv.is_cuda
@@ -79,17 +83,21 @@ class OffloadManager:
             assign.append((h, b, slot))
         if not assign:
             return
+        idx = torch.tensor([b for _, b, _ in assign], dtype=torch.long, device=self.kv.device)
         if self.stream is not None:
             self.stream.wait_stream(torch.cuda.current_stream())
             with torch.cuda.stream(self.stream):
-                for h, b, slot in assign:
-                    self.host[slot].copy_(self.kv[b].view(-1).view(torch.uint8), non_blocking=True)
+                g = self.kv.index_select(1, idx).transpose(0, 1).contiguous()  # [n, L, ...] staging
+                rows = g.view(len(assign), -1).view(torch.uint8)
+                for i, (h, b, slot) in enumerate(assign):
+                    self.host[slot].copy_(rows[i], non_blocking=True)
                 ev = torch.cuda.Event()
                 ev.record(self.stream)
-            self.pending.append((ev, [(h, s) for h, _, s in assign]))
+            self.pending.append((ev, [(h, s) for h, _, s in assign], g))  # g lives until the DMAs land
         else:
-            for h, b, slot in assign:
-                self.host[slot].copy_(self.kv[b].reshape(-1).view(torch.uint8))
+            rows = self.kv.index_select(1, idx).transpose(0, 1).contiguous().view(len(assign), -1)
+            for i, (h, b, slot) in enumerate(assign):
+                self.host[slot].copy_(rows[i].view(torch.uint8))
             self._commit_host([(h, s) for h, _, s in assign])
 
     def _alloc_slot(self) -> Optional[int]:
@@ -112,11 +120,11 @@ class OffloadManager:
 
     def poll(self):
         keep = []
-        for ev, pairs in self.pending:
-            if ev.query():
-                self._commit_host(pairs)
+        for item in self.pending:
+            if item[0].query():
+                self._commit_host(item[1])
             else:
-                keep.append((ev, pairs))
+                keep.append(item)
         self.pending = keep
 
     # ------------------------------------------------------------ engine hooks
@@ -155,11 +163,11 @@ class OffloadManager:
         if not bm.grow(req.seq_id, (first + n) * bs):
             return 0
         table = bm.block_table(req.seq_id)
+        stage = torch.empty(n, self.block_bytes, dtype=torch.uint8, device=self.kv.device)
         for j, (tier, k, s) in enumerate(found):
-            dst = self.kv[table[first + j]].view(-1).view(torch.uint8)
             if tier == "cpu":
                 self.slot_of.move_to_end(k)
-                dst.copy_(self.host[s], non_blocking=True)
+                stage[j].copy_(self.host[s], non_blocking=True)
                 self.stats["loaded_cpu"] += 1
             else:
                 buf = torch.empty(self.block_bytes, dtype=torch.uint8, pin_memory=self.kv.is_cuda)
@@ -167,6 +175,11 @@ class OffloadManager:
                 if not ok:
                     n = j
                     break
-                dst.copy_(buf, non_blocking=True)
+                stage[j].copy_(buf, non_blocking=True)
                 self.stats["loaded_fs"] += 1
+        if n:
+            # scatter the staged block-major rows into the layer-major pool (compute stream, before the forward)
+            idx = torch.tensor(table[first:first + n], dtype=torch.long, device=self.kv.device)
+            blk = stage[:n].view(self.kv.dtype).view((n,) + self.blk_shape)
+            self.kv.index_copy_(1, idx, blk.transpose(0, 1))
         return n * bs

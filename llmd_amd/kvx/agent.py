@@ -14,7 +14,9 @@ Roles and protocol (vLLM NixlConnector-compatible ``kv_transfer_params``):
   compatibility check), then pulls the blocks one-sided:
     - ``ipc``  (GPU, same node): the peer's whole KV pool is mapped once via
       a HIP IPC handle and copied with the kvx HIP kernel (xGMI peer reads;
-      heterogeneous-TP head re-slicing via copy segments) or SDMA;
+      heterogeneous-TP head re-slicing via copy segments; the layer-major pools
+      make a block 2 L pieces, so the transfer is always the copy kernel and
+      "dma" is kept only as an alias of "ipc");
     - ``tcp``  (CPU CI / fallback): block bytes streamed over the side channel.
   Completion -> ``free`` notification to the prefiller.
 Side channel: length-prefixed msgpack request/response over TCP
@@ -116,14 +118,17 @@ class KvxAgent:
                  port: int = 0, tp_rank: int = 0, tp_size: int = 1, abort_timeout: float = 480.0,
                  transport: str = "auto", metrics=None, vmm: Optional[dict] = None, exports: bool = True,
                  workers: Optional[int] = None):
-        self.kv = kv                      # [num_blocks, L, 2, Hkv, bs, D]
+        self.kv = kv                      # [L, num_blocks, planes, Hkv, bs, D] (layer-major)
         self.vmm = vmm                    # chunked exportable pool (model_runner._alloc_cache)
         self.engine_id = engine_id or f"kvx-{uuid.uuid4().hex[:12]}"
         self.tp_rank, self.tp_size = tp_rank, tp_size
         self.abort_timeout = abort_timeout
         self.metrics = metrics
         self.is_gpu = kv.is_cuda
-        self.block_bytes = kv[0].numel() * kv.element_size()
+        esz = kv.element_size()
+        self.block_bytes = kv[:, 0].numel() * esz        # one block, every layer
+        self.layer_block_bytes = kv[0, 0].numel() * esz  # one block of one layer (pair stride)
+        self.layer_stride = kv.stride(0) * esz           # one layer's pool
         self.transport = transport
         self.held: dict[str, Held] = {}
         self.held_lock = threading.Lock()
@@ -234,9 +239,10 @@ class KvxAgent:
     def meta(self) -> dict:
         k = self.kv
         m = {"engine_id": self.engine_id, "shape": list(k.shape), "dtype": str(k.dtype).replace("torch.", ""),
-             "block_bytes": self.block_bytes, "tp_rank": self.tp_rank, "tp_size": self.tp_size,
+             "block_bytes": self.block_bytes, "layout": "layer_major", "layer_block_bytes": self.layer_block_bytes,
+             "layer_stride": self.layer_stride, "tp_rank": self.tp_rank, "tp_size": self.tp_size,
              "device": k.device.index if k.is_cuda else -1, "hostname": socket.gethostname(),
-             "pid": os.getpid(), "num_blocks": k.shape[0]}
+             "pid": os.getpid(), "num_blocks": k.shape[1]}
         if self.ipc_handle is not None:
             m["ipc_handle"], m["ipc_offset"] = self.ipc_handle
         if self.uds_name is not None:
@@ -277,8 +283,10 @@ class KvxAgent:
         return out
 
     def read_blocks(self, blocks: list) -> bytes:
+        """Wire format (TCP path): each block's bytes block-major [L, planes, H, bs, D]."""
         idx = torch.tensor(blocks, dtype=torch.long, device=self.kv.device)
-        return self.kv.index_select(0, idx).cpu().contiguous().view(torch.uint8).numpy().tobytes()
+        g = self.kv.index_select(1, idx).transpose(0, 1).contiguous()
+        return g.cpu().view(torch.uint8).numpy().tobytes()
 
     # ------------------------------------------------------------ decode side
     def start_load(self, request_id: str, params: dict, local_blocks: list, report: Optional[tuple] = None):
@@ -355,11 +363,13 @@ class KvxAgent:
         return p
 
     def _check_compat(self, m: dict):
-        """Handshake compatibility (enforce_handshake_compat): block size, dtype,
-        layers, head dim must match; KV heads may differ by TP re-slicing."""
+        """Handshake compatibility (enforce_handshake_compat): layout, block size,
+        dtype, layers, head dim must match; KV heads may differ by TP re-slicing."""
         ls = list(self.kv.shape)
         rs = m["shape"]
-        if rs[1] != ls[1] or rs[2] != ls[2] or rs[4] != ls[4] or rs[5] != ls[5]:
+        if m.get("layout") != "layer_major":
+            raise RuntimeError("kvx: peer KV pool is not layer-major (incompatible version)")
+        if rs[0] != ls[0] or rs[2] != ls[2] or rs[4] != ls[4] or rs[5] != ls[5]:
             raise RuntimeError(f"kvx layout mismatch local {ls} remote {rs}")
         if m["dtype"] != str(self.kv.dtype).replace("torch.", ""):
             raise RuntimeError("kvx dtype mismatch")
@@ -371,23 +381,36 @@ class KvxAgent:
             _send(p["sock"], obj)
             return _recv(p["sock"])
 
-    def _segments(self, rmeta) -> list[tuple[int, int, int]]:
-        """Byte segments (src_off, dst_off, len) of one block for TP re-slicing."""
-        L, _, hl, bs, D = self.kv.shape[1:]
-        hr = rmeta["shape"][3]
-        esz = self.kv.element_size()
-        if hr == hl:
-            return [(0, 0, self.block_bytes)]
+    def _head_slice(self, rmeta) -> tuple[int, int, int]:
+        """(remote heads, local heads, first remote head of this rank's slice)."""
+        hl, hr = self.kv.shape[3], rmeta["shape"][3]
         if hr < hl:
             raise RuntimeError("kvx: decoder holds more KV heads than the prefiller (unsupported pull)")
-        # prefiller has all heads of a group of decoder ranks: take our slice
-        h0 = (self.tp_rank * hl) % hr
-        head = bs * D * esz
-        segs = []
-        for l in range(L):
-            for kv in range(2):
-                segs.append((((l * 2 + kv) * hr + h0) * head, ((l * 2 + kv) * hl) * head, hl * head))
-        return segs
+        return hr, hl, (self.tp_rank * hl) % hr  # prefiller has all heads of a group of decoder ranks
+
+    def _segments(self, rmeta) -> list[tuple[int, int, int]]:
+        """IPC copy segments (src_off, dst_off, len) of one block, relative to
+        block * layer_block_bytes in each pool: one per layer (per layer and
+        plane when TP re-slices heads) - a block is 2 L pieces of the
+        layer-major pools."""
+        L, _, planes, _, bs, D = self.kv.shape
+        hr, hl, h0 = self._head_slice(rmeta)
+        lsr, lsl = int(rmeta["layer_stride"]), self.layer_stride
+        if hr == hl:
+            return [(l * lsr, l * lsl, self.layer_block_bytes) for l in range(L)]
+        head = bs * D * self.kv.element_size()
+        return [(l * lsr + (p * hr + h0) * head, l * lsl + p * hl * head, hl * head)
+                for l in range(L) for p in range(planes)]
+
+    def _wire_segments(self, rmeta) -> list[tuple[int, int, int]]:
+        """TCP path: segments inside one block-major wire block (read_blocks)."""
+        L, _, planes, _, bs, D = self.kv.shape
+        hr, hl, h0 = self._head_slice(rmeta)
+        if hr == hl:
+            return [(0, 0, self.block_bytes)]
+        head = bs * D * self.kv.element_size()
+        return [(((l * planes + p) * hr + h0) * head, ((l * planes + p) * hl) * head, hl * head)
+                for l in range(L) for p in range(planes)]
 
     def _fault(self) -> Optional[str]:
         f = os.environ.get("LLMD_KVX_FAULT")
@@ -448,19 +471,18 @@ class KvxAgent:
             data = self._rpc(p, {"op": "read", "blocks": rblocks, "request_id": prm.get("remote_request_id")})
             if isinstance(data, dict) and data.get("error"):
                 raise RuntimeError(data["error"])
-            rshape = rmeta["shape"]
             src = torch.frombuffer(bytearray(data), dtype=torch.uint8).view(n, -1)
             dst_idx = torch.tensor(lblocks, dtype=torch.long, device=self.kv.device)
-            flat = self.kv.view(self.kv.shape[0], -1).view(torch.uint8)
             rows = torch.empty(n, self.block_bytes, dtype=torch.uint8)
-            for so, do, ln in segs:
+            for so, do, ln in self._wire_segments(rmeta):
                 rows[:, do:do + ln] = src[:, so:so + ln]
-            flat.index_copy_(0, dst_idx, rows.to(self.kv.device))
+            blk = rows.view(self.kv.dtype).view((n,) + tuple(self.kv.shape[:1]) + tuple(self.kv.shape[2:]))
+            self.kv.index_copy_(1, dst_idx, blk.transpose(0, 1).to(self.kv.device))
             if self.is_gpu:
                 torch.cuda.current_stream().synchronize()
         if fault == "corrupt":
             idx = torch.tensor(lblocks[:1], dtype=torch.long, device=self.kv.device)
-            self.kv.index_fill_(0, idx, 0)
+            self.kv.index_fill_(1, idx, 0)
         # release the prefiller's blocks (this rank's share)
         self._rpc(p, self._free_msg(prm))
         return True, nbytes
@@ -477,14 +499,11 @@ class KvxAgent:
         with self.peer_lock:
             base = self._map_peer(C, eid, rmeta)
         with torch.cuda.stream(stream):
-            if self.transport == "dma" and len(segs) == 1:
-                pairs = torch.tensor(list(zip(rblocks, lblocks)), dtype=torch.int32)
-                C.kvx_dma_blocks(self.kv, base, self.block_bytes, rmeta["block_bytes"], pairs, self.block_bytes)
-            else:
-                pairs = torch.tensor(list(zip(rblocks, lblocks)), dtype=torch.int32, device=self.kv.device)
-                sg = torch.tensor(segs, dtype=torch.int64, device=self.kv.device)
-                C.kvx_copy_blocks(self.kv, base, self.block_bytes, rmeta["block_bytes"], pairs, sg,
-                                  max(s[2] for s in segs))
+            # block b of layer l sits at pool + l * layer_stride + b * layer_block_bytes
+            pairs = torch.tensor(list(zip(rblocks, lblocks)), dtype=torch.int32, device=self.kv.device)
+            sg = torch.tensor(segs, dtype=torch.int64, device=self.kv.device)
+            C.kvx_copy_blocks(self.kv, base, self.layer_block_bytes, int(rmeta["layer_block_bytes"]), pairs, sg,
+                              max(s[2] for s in segs))
             ev = torch.cuda.Event()
             ev.record(stream)
         ev.synchronize()

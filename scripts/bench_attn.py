@@ -84,9 +84,19 @@ def prefill(ctx, q_len, Hq, Hkv, D, bs, check=False):
     return t
 
 
-def decode(ctx, B, Hq, Hkv, D, bs):
+def decode(ctx, B, Hq, Hkv, D, bs, layers=0):
+    """layers > 0: the engine's cache layout [blocks, layers, 2, Hkv, bs, D]
+    (one block of every layer contiguous, for whole-block transfers) viewed at
+    one layer, instead of a per-layer [blocks, Hkv, bs, D] pool."""
     dev = "cuda"
-    kc, vc, bt = make_cache(ctx, Hkv, D, bs, dev, seqs=B)
+    if layers:
+        per = math.ceil(ctx / bs)
+        nb = B * per + 1
+        big = torch.randn(nb, layers, 2, Hkv, bs, D, device=dev, dtype=torch.bfloat16).to(KV_DTYPE)
+        kc, vc = big[:, layers // 2, 0], big[:, layers // 2, 1]
+        bt = torch.randperm(nb - 1, device=dev)[:B * per].view(B, per).int()
+    else:
+        kc, vc, bt = make_cache(ctx, Hkv, D, bs, dev, seqs=B)
     q = torch.randn(B, Hq * D, device=dev, dtype=torch.bfloat16)
     sl = torch.full((B,), ctx, dtype=torch.int32, device=dev)
     out = torch.empty(B, Hq * D, device=dev, dtype=torch.bfloat16)
@@ -95,7 +105,8 @@ def decode(ctx, B, Hq, Hkv, D, bs):
                                   out=out, max_ctx=ctx)
     t = time_it(fn)
     by = B * ctx * Hkv * D * 2 * kc.element_size()
-    print(f"decode B={B} ctx={ctx} kv={str(KV_DTYPE)[6:]}: {t * 1e6:.1f} us  {by / t / 1e9:.0f} GB/s (KV read)")
+    lay = f" engine layout L={layers}" if layers else ""
+    print(f"decode B={B} ctx={ctx} kv={str(KV_DTYPE)[6:]}{lay}: {t * 1e6:.1f} us  {by / t / 1e9:.0f} GB/s (KV read)")
     return t
 
 
@@ -132,9 +143,17 @@ def main():
     ap.add_argument("--so", default=None)
     ap.add_argument("--mla", action="store_true")
     ap.add_argument("--kv-dtype", default="bf16", choices=["bf16", "fp8"])
+    ap.add_argument("--decode-layout", action="store_true",
+                    help="decode only: per-layer pool vs the engine's [blocks, layers, 2, ...] layout")
     a = ap.parse_args()
     global KV_DTYPE
     KV_DTYPE = torch.float8_e4m3fn if a.kv_dtype == "fp8" else torch.bfloat16
+    if a.decode_layout:
+        for _ in range(2):
+            decode(a.ctx, 64, 64, 8, a.D, 64)
+            decode(a.ctx, 64, 64, 8, a.D, 64, layers=80)
+            torch.cuda.empty_cache()
+        return
     if a.check:
         prefill(700, 300, 16, 2, a.D, 64, check=True)
         prefill(600, 600, 64, 8, a.D, 64, check=True)
