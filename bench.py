@@ -32,6 +32,7 @@ Output: one JSON line on rank 0 (see README "bench.py contract").
 from __future__ import annotations
 
 import argparse
+import collections
 import json
 import os
 import statistics
@@ -191,11 +192,14 @@ def main():
     _sync(a)
     log(rank, f"setup: {setup_steps} steps in {time.time() - ts:.1f}s (batch filled to {a.concurrency})")
 
+    step_tokens = []
+
     def run_steps(n):
         for _ in range(n):
             for o in eng.step():
                 if o.finished:
                     new_request(a.osl)
+            step_tokens.append(eng.last_num_tokens)
 
     # warmup
     tw = time.time()
@@ -210,11 +214,14 @@ def main():
         dist.barrier()
     _sync(a)
     t1 = time.perf_counter()
+    step_tokens.clear()
     run_steps(a.steps)
     _sync(a)
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t1
+    hist = collections.Counter(step_tokens)
+    log(rank, "timed step sizes (tokens: steps): " + ", ".join(f"{k}: {v}" for k, v in sorted(hist.items())))
     gen = eng.metrics.n_gen - gen0
     ptoks = eng.metrics.n_prompt - prompt0
     ttfts = list(eng.metrics.ttfts)

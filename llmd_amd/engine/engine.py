@@ -77,6 +77,7 @@ class LLMEngine:
         self.paused = False
         self.step_count = 0
         self.last_step_empty = False
+        self.last_num_tokens = 0
 
     # ------------------------------------------------------------ API
     def add_request(self, request_id: str, prompt_token_ids: list[int],
@@ -118,6 +119,7 @@ class LLMEngine:
                                   sorted({nm(r.lora_id) for r in self.sched.waiting if r.lora_id} - {None}))
         err_outs = self._error_outputs()
         self.last_step_empty = so.empty
+        self.last_num_tokens = so.num_tokens
         if self.dp_lockstep:
             return self._lockstep_step(so, err_outs, t0)
         if so.empty:
