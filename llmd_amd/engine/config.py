@@ -191,6 +191,29 @@ _register(ModelConfig(model_type="qwen3_moe", name="qwen3-30b-a3b", hidden_size=
                       num_key_value_heads=4, head_dim=128, vocab_size=151936, rope_theta=1000000.0,
                       rms_norm_eps=1e-6, num_local_experts=128, num_experts_per_tok=8, norm_topk_prob=True,
                       bos_token_id=151643, eos_token_id=151645), "Qwen/Qwen3-30B-A3B")
+# further models the reference guides deploy (public HF configs)
+_QW = dict(vocab_size=151936, rope_theta=1000000.0, rms_norm_eps=1e-6, bos_token_id=151643, eos_token_id=151645)
+_register(ModelConfig(model_type="qwen3", name="qwen3-8b", hidden_size=4096, intermediate_size=12288,
+                      num_hidden_layers=36, num_attention_heads=32, num_key_value_heads=8, head_dim=128, **_QW),
+          "Qwen/Qwen3-8B")
+_register(ModelConfig(model_type="qwen3", name="qwen3-0.6b", hidden_size=1024, intermediate_size=3072,
+                      num_hidden_layers=28, num_attention_heads=16, num_key_value_heads=8, head_dim=128,
+                      tie_word_embeddings=True, **_QW),
+          "Qwen/Qwen3-0.6B", "Qwen/Qwen3-Embedding-0.6B")
+_register(ModelConfig(model_type="qwen2", name="qwen2.5-3b", hidden_size=2048, intermediate_size=11008,
+                      num_hidden_layers=36, num_attention_heads=16, num_key_value_heads=2, head_dim=128,
+                      tie_word_embeddings=True, attention_bias=True, **dict(_QW, eos_token_id=151645)),
+          "Qwen/Qwen2.5-3B-Instruct")
+_register(_llama("llama-3.2-3b", 3072, 8192, 28, 24, 8, tie_word_embeddings=True,
+                 rope_scaling={"rope_type": "llama3", "factor": 32.0, "low_freq_factor": 1.0,
+                               "high_freq_factor": 4.0, "original_max_position_embeddings": 8192}),
+          "meta-llama/Llama-3.2-3B-Instruct")
+_register(ModelConfig(model_type="qwen3_moe", name="qwen3-coder-480b-a35b", hidden_size=6144, intermediate_size=8192,
+                      moe_intermediate_size=2560, num_hidden_layers=62, num_attention_heads=96,
+                      num_key_value_heads=8, head_dim=128, max_position_embeddings=262144,
+                      num_local_experts=160, num_experts_per_tok=8, norm_topk_prob=True,
+                      **dict(_QW, rope_theta=10000000.0)),
+          "Qwen/Qwen3-Coder-480B-A35B-Instruct", "Qwen/Qwen3-Coder-480B-A35B-Instruct-FP8")
 # multimodal (E/PD guide shape: Qwen2.5-VL-7B-class LM + ViT; image tokens = W*H/784)
 _register(_llama("llama-3-8b-vl", 4096, 14336, 32, 32, 8, model_type="llava", image_token_id=128256,
                  vocab_size=128257, vision_config={"hidden_size": 1280, "num_layers": 32, "num_heads": 16}),
