@@ -89,21 +89,25 @@ def _link(objs, out: Path, libs):
     return out
 
 
-def build_ops(jobs: int = 8, verbose: bool = False) -> Path:
-    """Build the HIP op library ``llmd_amd/_C``."""
+def build_ops(jobs: int = 8, verbose: bool = False, debug: bool = False) -> Path:
+    """Build the HIP op library ``llmd_amd/_C`` - or, with ``debug``,
+    ``llmd_amd/_C_debug``: -O1 -g kernels with the LLMD_DCHECK device
+    assertions compiled in (SURVEY §5.2 debug kernel build; select it at run
+    time with LLMD_KERNEL_DEBUG=1, best together with AMD_SERIALIZE_KERNEL=3)."""
     tinc, tlib = _torch_paths()
-    out_dir = BUILD / "ops"
+    name = "_C_debug" if debug else "_C"
+    out_dir = BUILD / ("ops_debug" if debug else "ops")
     out_dir.mkdir(parents=True, exist_ok=True)
     inc = CSRC / "include"
     deps = _headers(inc)
     hip_srcs = sorted((CSRC / "ops").glob("*.hip"))
     hip_flags = [
-        f"--offload-arch={ARCH}", "-O3", "-fPIC", "-std=c++17", f"-I{inc}",
+        f"--offload-arch={ARCH}", "-O1" if debug else "-O3", "-fPIC", "-std=c++17", f"-I{inc}",
         "-ffp-contract=fast", "-munsafe-fp-atomics",
-    ]
+    ] + (["-g", "-DLLMD_KERNEL_DEBUG=1"] if debug else [])
     cpp_flags = [
         "-O2", "-fPIC", "-std=c++17", f"-I{inc}", f"-I{ROCM}/include", f"-I{_py_inc()}",
-        "-D__HIP_PLATFORM_AMD__=1", "-DUSE_ROCM=1", "-DTORCH_EXTENSION_NAME=_C",
+        "-D__HIP_PLATFORM_AMD__=1", "-DUSE_ROCM=1", f"-DTORCH_EXTENSION_NAME={name}",
         "-DTORCH_API_INCLUDE_EXTENSION_H", "-D_GLIBCXX_USE_CXX11_ABI=1", "-w",
     ] + [f"-I{p}" for p in tinc]
     with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
@@ -114,7 +118,7 @@ def build_ops(jobs: int = 8, verbose: bool = False) -> Path:
         f"-L{tlib}", "-lc10", "-lc10_hip", "-ltorch", "-ltorch_cpu", "-ltorch_hip",
         "-ltorch_python", "-lamdhip64", f"-Wl,-rpath,{tlib}",
     ]
-    out = _link(objs, PKG / f"_C{EXT}", libs)
+    out = _link(objs, PKG / f"{name}{EXT}", libs)
     if verbose:
         print(f"[llmd build] {out}")
     return out
@@ -182,5 +186,7 @@ if __name__ == "__main__":
         build_runtime(verbose=True)
     elif what == "sanitize":
         build_sanitized_runtime(verbose=True)
+    elif what == "debug":
+        build_ops(verbose=True, debug=True)
     else:
         build_all()

@@ -12,6 +12,17 @@
 
 #define LLMD_WAVE 64
 
+// Device-side invariant checks, compiled in only for the debug op library
+// (python -m llmd_amd.build debug -> llmd_amd/_C_debug, loaded when
+// LLMD_KERNEL_DEBUG=1): a violated check aborts the kernel with
+// file:line instead of faulting on a wild address.
+#ifdef LLMD_KERNEL_DEBUG
+#include <cassert>
+#define LLMD_DCHECK(cond) assert(cond)
+#else
+#define LLMD_DCHECK(cond) ((void)0)
+#endif
+
 typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x4_t __attribute__((ext_vector_type(4)));
 typedef short s16x8_t __attribute__((ext_vector_type(8)));

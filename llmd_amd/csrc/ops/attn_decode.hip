@@ -94,6 +94,7 @@ __global__ __launch_bounds__(NT, 2) void paged_decode_kernel(
   const int kvh = blockIdx.y / NG, gi = blockIdx.y % NG;
   const int b = blockIdx.z;
   const int L = seq_lens[b];
+  LLMD_DCHECK(L >= 0 && L <= bt_stride * bs);  // the block table covers the sequence
   const int start = window > 0 ? max(0, L - window) : 0;
   const int s0 = start + sp * split_size;
   if (s0 >= L) return;
@@ -139,6 +140,7 @@ __global__ __launch_bounds__(NT, 2) void paged_decode_kernel(
       int key = tts + 16 * b4 + rowoff(c16 >> 2) + (c16 & 3);
       key = key < s1 ? key : s0;
       const int phys = bt[key >> lbs];
+      LLMD_DCHECK(phys >= 0);
       const int64_t kr = (int64_t)phys * block_stride + head_off + (int64_t)(key & (bs - 1)) * D;
 #pragma unroll
       for (int s = 0; s < KS; ++s) kf[b4][s] = ld_cache<F8>(kc, kr + (4 * s + g) * 8);

@@ -396,6 +396,7 @@ __global__ __launch_bounds__(NT, 2) void prefill_v2_kernel(
   }
   auto issue = [&](char* base, int t) {
     const int ts = t * 64;
+    LLMD_DCHECK(ts < ctx && bt[ts >> lbs] >= 0 && ctx <= bt_stride * bs);
     const int64_t tb = 2 * ((int64_t)bt[ts >> lbs] * block_stride + head_off + (int64_t)(ts & (bs - 1)) * D);
     const char* kb = reinterpret_cast<const char*>(kc) + tb;
     const char* vb = reinterpret_cast<const char*>(vc) + tb;

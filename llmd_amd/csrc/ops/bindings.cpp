@@ -745,7 +745,7 @@ void symm_ep_combine(std::vector<int64_t> bases, int64_t rank, int64_t ch, std::
 
 }  // namespace
 
-PYBIND11_MODULE(_C, m) {
+PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {  // _C, or _C_debug (llmd_amd/build.py)
   m.doc() = "llmd_amd HIP/CDNA4 op library (gfx950)";
   m.def("rms_norm", &rms_norm);
   m.def("fused_add_rms_norm", &fused_add_rms_norm);

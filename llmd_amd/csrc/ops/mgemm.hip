@@ -63,6 +63,7 @@ __global__ __launch_bounds__(NT, 1) void mgemm_kernel(const uint16_t* __restrict
   const int nk = K >> 6;
   const int s0 = sp * steps_per_split;
   const int nsteps = min(nk, s0 + steps_per_split) - s0;  // >= 1: the host plans no empty split
+  LLMD_DCHECK(nsteps >= 1 && M >= 1 && M <= 16 * MB);
 
   // per-lane DMA source offsets (elements) inside a k-step: instruction j of the
   // stage fills image rows 8 j .. 8 j + 7; lane L -> row 8 j + L / 8, slot L % 8,

@@ -33,6 +33,7 @@ __global__ __launch_bounds__(NT) void rope_cache_kernel(
   const float* cs = cos_sin + pos * rot;
   uint16_t* row = qkv + (int64_t)t * qkv_stride;
   const int64_t slot = slots ? slots[t] : -1;
+  LLMD_DCHECK(slot >= -1);  // -1 = padded row (graph buckets), else a cache slot
   int64_t cache_off = -1;
   if (slot >= 0) {
     const int64_t blk = slot / bs, r = slot % bs;

@@ -23,17 +23,21 @@ def native():
     global _C, _C_ERR
     if _C is not None:
         return _C
+    import importlib
+
+    debug = os.environ.get("LLMD_KERNEL_DEBUG", "0") == "1"  # kernels with LLMD_DCHECK assertions
+    name = "llmd_amd._C_debug" if debug else "llmd_amd._C"
     try:
-        from llmd_amd import _C as mod  # noqa: WPS433
+        mod = importlib.import_module(name)
     except ImportError as e:  # pragma: no cover - exercised on GPU hosts only
         _C_ERR = e
         if os.environ.get("LLMD_AUTOBUILD", "1") == "1":
             from llmd_amd.build import build_ops
 
-            build_ops()
-            from llmd_amd import _C as mod  # noqa: WPS433,F811
+            build_ops(debug=debug)
+            mod = importlib.import_module(name)
         else:
-            raise RuntimeError(f"llmd_amd._C HIP extension not built: {e}") from e
+            raise RuntimeError(f"{name} HIP extension not built: {e}") from e
     _C = mod
     return _C
 
