@@ -15,6 +15,8 @@
 
 extern "C" {
 void llmd_rms_norm(void*, int64_t, const void*, int64_t, const void*, int, int, float, hipStream_t);
+void llmd_layer_norm(void*, int64_t, void*, int64_t, void*, int64_t, const void*, const void*, int, int, float,
+                     hipStream_t);
 void llmd_fused_add_rms_norm(void*, int64_t, void*, int64_t, const void*, int, int, float,
                              hipStream_t);
 void llmd_rope_cache(void*, int64_t, const int64_t*, const float*, int, int, int, int,
@@ -128,6 +130,29 @@ void fused_add_rms_norm(torch::Tensor x, torch::Tensor residual, torch::Tensor w
   TORCH_CHECK(x.stride(0) % 8 == 0 && residual.stride(0) % 8 == 0, "16-B aligned rows");
   llmd_fused_add_rms_norm(x.data_ptr(), x.stride(0), residual.data_ptr(), residual.stride(0),
                           w.data_ptr(), x.size(0), d, (float)eps, cur_stream());
+}
+
+// out = layernorm(x) w + b, or (residual given) residual += x; x = layernorm(residual) w + b in place
+void layer_norm(torch::Tensor out, torch::Tensor x, c10::optional<torch::Tensor> residual, torch::Tensor w,
+                torch::Tensor b, double eps) {
+  const c10::hip::OptionalHIPGuard device_guard(dev_of(x));
+  CHECK_CUDA(x); CHECK_BF16(x); CHECK_BF16(out); CHECK_BF16(w); CHECK_BF16(b);
+  CHECK_INNER(x); CHECK_INNER(out);
+  TORCH_CHECK(x.dim() == 2 && out.sizes() == x.sizes(), "layer_norm: 2-D x/out of one shape");
+  const int d = x.size(1);
+  TORCH_CHECK(d % 8 == 0 && w.numel() == d && b.numel() == d && w.is_contiguous() && b.is_contiguous(),
+              "layer_norm: d % 8 == 0, contiguous w/b of d elements");
+  TORCH_CHECK(x.stride(0) % 8 == 0 && out.stride(0) % 8 == 0, "layer_norm: 16-B aligned rows");
+  void* rp = nullptr;
+  int64_t rs = 0;
+  if (residual.has_value()) {
+    CHECK_BF16(*residual); CHECK_INNER(*residual);
+    TORCH_CHECK(residual->sizes() == x.sizes() && residual->stride(0) % 8 == 0, "layer_norm residual shape");
+    rp = residual->data_ptr();
+    rs = residual->stride(0);
+  }
+  llmd_layer_norm(out.data_ptr(), out.stride(0), x.data_ptr(), x.stride(0), rp, rs, w.data_ptr(), b.data_ptr(),
+                  x.size(0), d, (float)eps, cur_stream());
 }
 
 // KV caches are bf16 or fp8 e4m3fn (OCP, gfx950's native fp8)
@@ -749,6 +774,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {  // _C, or _C_debug (llmd_amd/build.p
   m.doc() = "llmd_amd HIP/CDNA4 op library (gfx950)";
   m.def("rms_norm", &rms_norm);
   m.def("fused_add_rms_norm", &fused_add_rms_norm);
+  m.def("layer_norm", &layer_norm);
   m.def("rope_cache", &rope_cache);
   m.def("gated_act", &gated_act);
   m.def("paged_decode", &paged_decode);

@@ -60,6 +60,10 @@ class ModelConfig:
     qk_nope_head_dim: int = 0
     qk_rope_head_dim: int = 0
     v_head_dim: int = 0
+    # OPT (models/opt.py): token-embedding width when it differs from hidden_size
+    # (project_in/out), pre- vs post-LayerNorm; attention_bias doubles as enable_bias
+    word_embed_proj_dim: int = 0
+    do_layer_norm_before: bool = True
     # multimodal (llava-style: vision tower + LM; models/vision.py)
     vision_config: Optional[dict] = None
     image_token_id: int = 0
@@ -110,6 +114,13 @@ class ModelConfig:
             kw["num_local_experts"] = d["n_routed_experts"]
         if d.get("model_type") in ("deepseek_v3", "deepseek_v2"):
             kw["model_type"] = "deepseek"
+        if d.get("model_type") == "opt":
+            kw["intermediate_size"] = d.get("ffn_dim", 4 * d["hidden_size"])
+            kw["num_key_value_heads"] = d["num_attention_heads"]
+            kw["attention_bias"] = d.get("enable_bias", True)
+            kw["hidden_act"] = d.get("activation_function", "relu")
+            kw["tie_word_embeddings"] = d.get("tie_word_embeddings", True)
+            kw.setdefault("rms_norm_eps", 1e-5)
         if d.get("model_type") == "gpt_oss":
             kw.setdefault("moe_intermediate_size", d.get("intermediate_size", 0))
             kw["attention_sinks"] = True
@@ -218,6 +229,11 @@ _register(ModelConfig(model_type="qwen3_moe", name="qwen3-coder-480b-a35b", hidd
 _register(_llama("llama-3-8b-vl", 4096, 14336, 32, 32, 8, model_type="llava", image_token_id=128256,
                  vocab_size=128257, vision_config={"hidden_size": 1280, "num_layers": 32, "num_heads": 16}),
           "llava-llama-3-8b")
+# OPT (the reference's CPU optimized-baseline model)
+_register(ModelConfig(model_type="opt", name="opt-125m", hidden_size=768, intermediate_size=3072,
+                      num_hidden_layers=12, num_attention_heads=12, num_key_value_heads=12, vocab_size=50272,
+                      max_position_embeddings=2048, hidden_act="relu", attention_bias=True,
+                      tie_word_embeddings=True, bos_token_id=2, eos_token_id=2), "facebook/opt-125m")
 # tiny configs (CPU CI, smoke, GPU unit tests)
 _register(ModelConfig(model_type="llama", name="tiny-llama", hidden_size=256, intermediate_size=512,
                       num_hidden_layers=2, num_attention_heads=4, num_key_value_heads=2, head_dim=64,
@@ -227,6 +243,10 @@ _register(ModelConfig(model_type="llama", name="small-llama", hidden_size=1024, 
                       num_hidden_layers=4, num_attention_heads=8, num_key_value_heads=2, head_dim=128,
                       vocab_size=32000, max_position_embeddings=8192, rope_theta=10000.0,
                       bos_token_id=1, eos_token_id=2), "opt-125m-sized")
+_register(ModelConfig(model_type="opt", name="tiny-opt", hidden_size=256, intermediate_size=512,
+                      num_hidden_layers=2, num_attention_heads=4, num_key_value_heads=4, vocab_size=512,
+                      max_position_embeddings=4096, hidden_act="relu", attention_bias=True,
+                      tie_word_embeddings=True, bos_token_id=2, eos_token_id=2))
 _register(ModelConfig(model_type="llava", name="tiny-vl", hidden_size=256, intermediate_size=512,
                       num_hidden_layers=2, num_attention_heads=4, num_key_value_heads=2, head_dim=64,
                       vocab_size=513, max_position_embeddings=4096, rope_theta=10000.0, bos_token_id=1,

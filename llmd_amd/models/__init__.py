@@ -10,6 +10,10 @@ def model_class(cfg: ModelConfig):
         from .llama import LlamaForCausalLM
 
         return LlamaForCausalLM
+    if t == "opt":
+        from .opt import OPTForCausalLM
+
+        return OPTForCausalLM
     if t == "llava":
         from .vision import LlavaForCausalLM
 

@@ -90,11 +90,12 @@ def load_weights(model: torch.nn.Module, path: str, strict: bool = True) -> int:
     for f in _files(path):
         with safe_open(f, framework="pt", device="cpu") as fh:
             for name in fh.keys():
-                if name not in specs:
+                key = name if name in specs else "model." + name  # base-model checkpoints (e.g. facebook/opt-*)
+                if key not in specs:
                     continue
-                p, kind, extra = specs[name]
+                p, kind, extra = specs[key]
                 place(p, fh.get_tensor(name).to(p.device), kind, extra)
-                seen.add(name)
+                seen.add(key)
     missing = set(specs) - seen
     if missing and strict:
         raise KeyError(f"checkpoint is missing {len(missing)} tensors, e.g. {sorted(missing)[:4]}")

@@ -68,6 +68,22 @@ def fused_add_rms_norm(x: torch.Tensor, residual: torch.Tensor, w: torch.Tensor,
     native().fused_add_rms_norm(x, residual, w, eps)
 
 
+def layer_norm(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, eps: float):
+    if not _gpu(x):
+        return ref.layer_norm(x, w, b, eps)
+    out = torch.empty_like(x)
+    native().layer_norm(out, x, None, w, b, eps)
+    return out
+
+
+def fused_add_layer_norm(x: torch.Tensor, residual: torch.Tensor, w: torch.Tensor, b: torch.Tensor, eps: float):
+    """residual += x; x = layernorm(residual) * w + b (both in place)."""
+    if not _gpu(x):
+        ref.fused_add_layer_norm(x, residual, w, b, eps)
+        return
+    native().layer_norm(x, x, residual, w, b, eps)
+
+
 # ---------------------------------------------------------------- rope + cache
 def rope_cache(qkv, positions, cos_sin, Hq, Hkv, D, slots, k_cache, v_cache, neox=True, k_scale=1.0,
                v_scale=1.0):

@@ -25,6 +25,17 @@ def fused_add_rms_norm(x: torch.Tensor, residual: torch.Tensor, w: torch.Tensor,
     x.copy_(rms_norm(r, w, eps))
 
 
+def layer_norm(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, eps: float) -> torch.Tensor:
+    return torch.nn.functional.layer_norm(x.float(), (x.shape[-1],), w.float(), b.float(), eps).to(x.dtype)
+
+
+def fused_add_layer_norm(x: torch.Tensor, residual: torch.Tensor, w: torch.Tensor, b: torch.Tensor, eps: float):
+    """In place: residual += x (rounded to x.dtype); x = layernorm(residual) * w + b."""
+    r = (x.float() + residual.float()).to(residual.dtype)
+    residual.copy_(r)
+    x.copy_(layer_norm(r, w, b, eps))
+
+
 FP8_MAX = 448.0
 
 
