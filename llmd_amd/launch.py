@@ -6,6 +6,8 @@ A topology YAML names the model, the router and the engine roles::
 
   model: llama-3-70b
   gpus: 8                      # GPUs on the host (default: all visible)
+  device: cuda                 # cpu: CPU engines, no GPU assignment (the
+                               # reference's docker/Dockerfile.cpu path)
   router: {port: 8000, config: <EndpointPickerConfig path or inline YAML>}
                                # mode: extproc -> the EPP as an Envoy ext_proc
                                # gRPC server on grpc_port (9002) for an external
@@ -66,7 +68,8 @@ def _kv_transfer(role: str) -> str:
 
 def plan(topo: dict, workdir: str) -> tuple[list[ProcSpec], dict]:
     """Returns (process specs, router endpoints doc)."""
-    n_gpus = int(topo.get("gpus", 8))
+    cpu = topo.get("device", "cuda") == "cpu"
+    n_gpus = 0 if cpu else int(topo.get("gpus", 8))
     model = topo["model"]
     free = list(range(n_gpus))
     procs: list[ProcSpec] = []
@@ -75,12 +78,15 @@ def plan(topo: dict, workdir: str) -> tuple[list[ProcSpec], dict]:
     for role in topo.get("roles", []):
         name, tp = role["name"], int(role.get("tp", 1))
         for i in range(int(role.get("replicas", 1))):
-            if len(free) < tp:
+            if cpu:
+                gpus = []
+            elif len(free) < tp:
                 raise ValueError(f"not enough GPUs for {name} replica {i} (tp={tp}, free={free})")
-            gpus, free = free[:tp], free[tp:]
+            else:
+                gpus, free = free[:tp], free[tp:]
             port = int(role.get("port", 8200)) + i
             args = ["--model", model, "--port", str(port), "--tensor-parallel-size", str(tp)] + \
-                [str(x) for x in role.get("args", [])]
+                (["--device", "cpu"] if cpu else []) + [str(x) for x in role.get("args", [])]
             if role.get("kv_transfer", name in ("prefill", "decode")):
                 args += ["--kv-transfer-config", _kv_transfer(name)]
             if role.get("kv_events", False):
@@ -94,7 +100,7 @@ def plan(topo: dict, workdir: str) -> tuple[list[ProcSpec], dict]:
                 master_port += 1
             else:
                 cmd = [PY] + server
-            env = {"HIP_VISIBLE_DEVICES": ",".join(map(str, gpus)), "LWS_GROUP_SIZE": str(tp),
+            env = {"HIP_VISIBLE_DEVICES": ",".join(map(str, gpus)) if not cpu else "", "LWS_GROUP_SIZE": str(tp),
                    "LWS_LEADER_ADDRESS": "127.0.0.1", "LWS_WORKER_INDEX": "0", "POD_IP": "127.0.0.1",
                    "POD_PORT": str(port), "HSA_ENABLE_IPC_MODE_LEGACY": "0"}
             rid = f"{name}-{i}"

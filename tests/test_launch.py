@@ -1,6 +1,7 @@
 """Single-node launcher plan (C40/C41): GPU assignment, TP packing, LWS env,
 P/D roles with sidecars, router endpoints file."""
 import os
+import time
 
 import yaml
 
@@ -102,3 +103,40 @@ def test_router_extproc_mode_and_envoy_config():
     assert cl["picked_endpoint"]["original_dst_lb_config"]["http_header_name"] == "x-gateway-destination-endpoint"
     ep = cl["llmd_epp"]["load_assignment"]["endpoints"][0]["lb_endpoints"][0]["endpoint"]["address"]
     assert ep["socket_address"]["port_value"] == 9002
+
+
+def test_cpu_opt125m_baseline_end_to_end(tmp_path):
+    """The reference's CPU optimized-baseline config (OPT-125m on CPU engines,
+    docker/Dockerfile.cpu): launcher -> 2 CPU engines + router -> completions
+    served through the router."""
+    import json
+    import urllib.request
+
+    from llmd_amd.launch import Launcher
+
+    with open(os.path.join(ROOT, "deploy/single-node/optimized-baseline-opt125m-cpu.yaml")) as f:
+        topo = yaml.safe_load(f)
+    topo["router"]["port"] = 18310
+    topo["roles"][0]["port"] = 18320
+    specs, _ = plan(topo, str(tmp_path))
+    eng = [s for s in specs if s.role == "prefill-decode"]
+    assert len(eng) == 2 and all(s.gpus == [] and "--device" in s.cmd for s in eng)
+    la = Launcher(topo, workdir=str(tmp_path)).start()
+    try:
+        assert la.wait_ready(timeout=300), open(tmp_path / "prefill-decode-0.log").read()[-3000:]
+        body = json.dumps({"model": "facebook/opt-125m", "prompt": "the quick brown fox " * 20,
+                           "max_tokens": 4}).encode()
+        outs = []
+        for _ in range(30):  # the router may need a scrape before it serves
+            try:
+                req = urllib.request.Request("http://127.0.0.1:18310/v1/completions", data=body,
+                                             headers={"content-type": "application/json"})
+                with urllib.request.urlopen(req, timeout=60) as r:
+                    outs.append((json.loads(r.read()), r.status))
+                if len(outs) == 2:
+                    break
+            except OSError:
+                time.sleep(1.0)
+        assert len(outs) == 2 and all(o["usage"]["completion_tokens"] == 4 for o, _ in outs)
+    finally:
+        la.stop()
