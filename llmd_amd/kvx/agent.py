@@ -547,14 +547,8 @@ class KvxAgent:
                 p["sock"].close()
             except OSError:
                 pass
-        if self.ipc_maps:
-            try:
-                from llmd_amd.ops import native
-
-                for eid, base in self.ipc_maps.items():
-                    pass  # mapped bases include an offset; handles are released at process exit
-            except Exception:  # noqa: BLE001
-                pass
+        # peer pools mapped into this process (self.ipc_maps) stay mapped until
+        # process exit: a pull kernel may still reference them on another stream
 
 
 class _Handler(socketserver.BaseRequestHandler):
