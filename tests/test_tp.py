@@ -5,6 +5,7 @@ import os
 import socket
 
 import numpy as np
+import pytest
 import torch
 import torch.multiprocessing as mp
 
@@ -16,8 +17,8 @@ from greedy_check import assert_greedy_match
 MODEL = "tiny-llama"
 
 
-def _cfg(path, **kw):
-    return EngineConfig.create(MODEL, device="cpu", block_size=16, num_gpu_blocks=64, max_num_batched_tokens=64,
+def _cfg(path, model=MODEL, **kw):
+    return EngineConfig.create(model, device="cpu", block_size=16, num_gpu_blocks=64, max_num_batched_tokens=64,
                                max_num_seqs=8, max_model_len=512, enforce_eager=True, load_format="safetensors",
                                weights_path=path, **kw)
 
@@ -27,13 +28,13 @@ def _prompts():
     return [rng.integers(3, 500, size=n).tolist() for n in (37, 90, 5)]
 
 
-def _worker(rank, world, port, path, out):
+def _worker(rank, world, port, path, out, model=MODEL):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
                       LOCAL_RANK=str(rank))
     from llmd_amd.parallel.state import destroy, init_distributed
 
     init_distributed(tp_size=world, backend="gloo")
-    cfg = _cfg(path, tensor_parallel_size=world)
+    cfg = _cfg(path, model, tensor_parallel_size=world)
     if rank == 0:
         eng = LLMEngine(cfg)
         reqs = eng.generate(_prompts(), SamplingParams(max_tokens=6, temperature=0.0, ignore_eos=True,
@@ -54,18 +55,23 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def test_tp2_matches_tp1(tmp_path):
+@pytest.mark.parametrize("model", [MODEL, "tiny-opt"])
+def test_tp2_matches_tp1(tmp_path, model):
     from llmd_amd.models import build_model
     from llmd_amd.models.loader import export_hf, save_safetensors
 
     path = str(tmp_path / "model.safetensors")
-    cfg1 = _cfg(None)
+    cfg1 = _cfg(None, model)
     torch.manual_seed(0)  # fixed weights: TP sums in another order, so a random model can hold near-ties
-    save_safetensors(export_hf(build_model(cfg1.model_config, device="cpu", max_pos=600)), path)
-    eng = LLMEngine(_cfg(path))
+    m = build_model(cfg1.model_config, device="cpu", max_pos=600)
+    for n, prm in m.named_parameters():  # non-zero biases (OPT): sharded / replicated biases must be placed right
+        if n.endswith("bias"):
+            torch.nn.init.normal_(prm, std=0.05)
+    save_safetensors(export_hf(m), path)
+    eng = LLMEngine(_cfg(path, model))
     ref = eng.generate(_prompts(), SamplingParams(max_tokens=6, temperature=0.0, ignore_eos=True, logprobs=1))
     out = str(tmp_path / "tp2.pt")
-    mp.spawn(_worker, args=(2, _free_port(), path, out), nprocs=2, join=True)
+    mp.spawn(_worker, args=(2, _free_port(), path, out, model), nprocs=2, join=True)
     got = torch.load(out, weights_only=True)
     # TP all-reduces sum the row-parallel shards in another order (bf16): a
     # first divergence must be a near-tie of the TP1 engine (greedy_check)
