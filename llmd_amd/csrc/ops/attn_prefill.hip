@@ -332,16 +332,28 @@ __global__ __launch_bounds__(NT, 2) void prefill_v2_kernel(
     const int* __restrict__ block_tables, int bt_stride, const int* __restrict__ q_start,
     const int* __restrict__ q_len, const int* __restrict__ ctx_len, const int* __restrict__ items,
     int Hq, int Hkv, int G, int HPW, float scale_log2, int window,
-    const float* __restrict__ sinks, uint16_t* __restrict__ out, int64_t out_stride, float vscale) {
+    const float* __restrict__ sinks, uint16_t* __restrict__ out, int64_t out_stride, float vscale, int xcd) {
   constexpr int KS = D / 32, NB = D / 16, RB = 2 * D;  // row bytes
   constexpr int P2_IMG = 64 * RB;                       // one 64-key bf16 image
   constexpr int NI = 64 * (D / 8) / 64;                 // DMA wave-instructions per image (16 / 8)
   __shared__ __attribute__((aligned(1024))) char buf0[2 * P2_IMG];  // K | V of even tiles
   __shared__ __attribute__((aligned(1024))) char buf1[2 * P2_IMG];  // K | V of odd tiles
 
-  const int seq = items[2 * blockIdx.x], qb = items[2 * blockIdx.x + 1];
+  // xcd: the dispatcher deals workgroups round-robin over the 8 XCDs; remap so
+  // each XCD runs a contiguous (head group, item) range - one KV head's K/V
+  // (5000 tokens: 2.5 MB) stays in that XCD's 4 MB L2 instead of every XCD
+  // streaming all heads' tiles. Measured (profiles/attn_prefill_r2_lanelocal.txt):
+  // ISL 5000 776 -> 833 TF/s, 8k 932 -> 1016; a one-wave grid (5000 x 512
+  // chunk, 256 workgroups) loses 2 %, so the host enables it from 1024 workgroups
+  int bx = blockIdx.x, by = blockIdx.y;
+  if (xcd) {
+    const int l = xcd_remap(by * gridDim.x + bx, gridDim.x * gridDim.y);
+    bx = l % gridDim.x;
+    by = l / gridDim.x;
+  }
+  const int seq = items[2 * bx], qb = items[2 * bx + 1];
   const int NHG = G / HPW;
-  const int kvh = blockIdx.y / NHG, hg = blockIdx.y % NHG;
+  const int kvh = by / NHG, hg = by % NHG;
   const int TPW = 4 / HPW;
   const int qs = q_start[seq], ql = q_len[seq], ctx = ctx_len[seq];
   const int pbase = ctx - ql;
@@ -610,11 +622,16 @@ extern "C" int llmd_paged_prefill(const void* q, int64_t q_stride, const void* k
     const char* e = getenv("LLMD_PREFILL_V1");
     return e && e[0] == '1';
   }();
+  static const bool xcd_map = [] {  // LLMD_PREFILL_XCD=0: plain round-robin dispatch (A/B)
+    const char* e = getenv("LLMD_PREFILL_XCD");
+    return !(e && e[0] == '0');
+  }();
   if ((D == 128 || D == 64) && !fp8 && bs >= 64 && !v1_only) {
     auto kern = D == 128 ? prefill_v2_kernel<128> : prefill_v2_kernel<64>;
     hipLaunchKernelGGL(kern, grid, blk, 0, st, (const uint16_t*)q, q_stride, (const uint16_t*)kc,
                        (const uint16_t*)vc, block_stride, bs, block_tables, bt_stride, q_start, q_len, ctx_len,
-                       items, Hq, Hkv, G, HPW, scale_log2, window, sinks, (uint16_t*)out, out_stride, v_scale);
+                       items, Hq, Hkv, G, HPW, scale_log2, window, sinks, (uint16_t*)out, out_stride, v_scale,
+                       xcd_map && (int64_t)n_items * grid.y >= 1024 ? 1 : 0);
   } else if (D == 128) {
     if (fp8) LAUNCH(128, true); else LAUNCH(128, false);
   } else if (D == 64) {
