@@ -104,7 +104,7 @@ class LLMEngine:
         return {sr.req.seq_id: self.bm.block_table(sr.req.seq_id) for sr in so.all()}
 
     def step(self) -> list[RequestOutput]:
-        if self.paused:
+        if self.paused or self.sleeping:  # asleep: new requests queue until wake_up
             return []
         if self.connector is not None:
             self.connector.tick()
@@ -276,3 +276,37 @@ class LLMEngine:
     def reset_prefix_cache(self):
         self.bm.reset_prefix_cache()
         self._flush_events()
+
+    # ------------------------------------------------------------ RL weight sync / sleep (M17)
+    @property
+    def weight_sync(self):
+        ws = getattr(self.runner, "weight_sync", None)
+        if ws is None:
+            from llmd_amd.parallel.comm import tp_broadcast_plan
+
+            from .weight_sync import WeightSync
+
+            ws = WeightSync(self.runner, tp_broadcast_plan if self.runner.tp_size > 1 else None)
+            self.runner.weight_sync = ws
+        return ws
+
+    def weight_sync_cmd(self, cmd: dict) -> dict:
+        """init_group / update_from_group / update_from_disk / destroy_group /
+        sleep / wake_up on every TP rank of this replica (engine/weight_sync.py).
+        Cached prefixes were computed with the old weights (or lost in sleep):
+        the prefix cache is reset after every weight change."""
+        op = cmd["op"]
+        if op == "sleep" and self.has_unfinished():
+            raise RuntimeError("cannot sleep with requests in flight (pause and drain first)")
+        if self.weight_sync.sleeping and op not in ("wake_up", "sleep", "init_group", "destroy_group"):
+            # level 2 woke up with uninitialised weights: the trainer sends them after wake_up
+            raise RuntimeError("engine is asleep: wake_up first")
+        res = self.weight_sync.apply(cmd)
+        if op in ("update_from_group", "update_from_disk", "sleep", "wake_up"):
+            self.reset_prefix_cache()
+        return res
+
+    @property
+    def sleeping(self) -> int:
+        ws = getattr(self.runner, "weight_sync", None)
+        return ws.sleeping if ws is not None else 0

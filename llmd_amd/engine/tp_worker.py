@@ -56,6 +56,13 @@ def run_follower(cfg: EngineConfig, capture_graphs: bool = True, on_ready=None) 
             if "lora_cmd" in pl:  # adapter load/unload issued on the driver
                 runner.lora.apply_cmd(pl["lora_cmd"])
                 continue
+            if "ws_cmd" in pl:  # RL weight sync / sleep / wake issued on the driver
+                if getattr(runner, "weight_sync", None) is None:
+                    from .weight_sync import WeightSync
+
+                    runner.weight_sync = WeightSync(runner)
+                runner.weight_sync.apply(pl["ws_cmd"])
+                continue
             if "kvx_cmd" in pl:  # P/D: KV pulls / cancels scheduled on the driver
                 kvx.apply(pl)
                 continue

@@ -14,6 +14,9 @@ Endpoints
   POST /tokenize, /detokenize
   POST /pause, /resume, /reset_prefix_cache   (IRO-ready lifecycle hooks)
   GET  /is_paused
+  POST /init_weight_update_group, /update_weights, /update_weights_from_disk,
+       /destroy_weight_update_group, /sleep, /wake_up; GET /is_sleeping
+       (RL rollout weight sync + engine sleep, SURVEY M17, engine/weight_sync.py)
   GET  /fault_tolerance/status, POST /fault_tolerance/apply   (Inference
        Resilience Operator EngineAdapter contract, proposals/
        inference-resilience-operator.md:66-256; faults are also published as
@@ -83,6 +86,13 @@ class OpenAIServer:
         r.add_post("/resume", self.resume)
         r.add_get("/is_paused", self.is_paused)
         r.add_post("/reset_prefix_cache", self.reset_prefix_cache)
+        r.add_post("/init_weight_update_group", self.init_weight_update_group)
+        r.add_post("/update_weights", self.update_weights)
+        r.add_post("/update_weights_from_disk", self.update_weights_from_disk)
+        r.add_post("/destroy_weight_update_group", self.destroy_weight_update_group)
+        r.add_post("/sleep", self.sleep)
+        r.add_post("/wake_up", self.wake_up)
+        r.add_get("/is_sleeping", self.is_sleeping)
         r.add_get("/fault_tolerance/status", self.ft_status)
         r.add_post("/fault_tolerance/apply", self.ft_apply)
         r.add_post("/v1/embeddings", self.embeddings)
@@ -381,6 +391,51 @@ class OpenAIServer:
     async def resume(self, req):
         self.aeng.resume()
         return web.json_response({"paused": False})
+
+    # ------------------------------------------------------------ RL weight sync + sleep (M17)
+    async def _ws(self, cmd: dict):
+        try:
+            res = await self.aeng.call(lambda e: e.weight_sync_cmd(cmd))
+        except (RuntimeError, ValueError, KeyError, FileNotFoundError) as e:
+            return _err(409 if isinstance(e, RuntimeError) else 400, str(e))
+        return web.json_response(res)
+
+    async def init_weight_update_group(self, req):
+        b = await req.json()
+        return await self._ws({"op": "init_group", "addr": b.get("master_address", "127.0.0.1"),
+                               "port": int(b["master_port"]), "rank_offset": int(b.get("rank_offset", 1)),
+                               "world_size": int(b["world_size"]), "backend": b.get("backend"),
+                               "timeout_s": float(b.get("timeout_s", 300.0))})
+
+    async def update_weights(self, req):
+        b = await req.json()
+        if "metas" in b:
+            metas = [tuple(m) for m in b["metas"]]
+        else:
+            metas = list(zip(b["names"], b["dtypes"], b["shapes"]))
+        return await self._ws({"op": "update_from_group", "metas": metas})
+
+    async def update_weights_from_disk(self, req):
+        b = await req.json()
+        return await self._ws({"op": "update_from_disk", "path": b["path"]})
+
+    async def destroy_weight_update_group(self, req):
+        return await self._ws({"op": "destroy_group"})
+
+    async def sleep(self, req):
+        level = int(req.query.get("level", 1))
+        if req.can_read_body:
+            level = int((await req.json()).get("level", level))
+        return await self._ws({"op": "sleep", "level": level})
+
+    async def wake_up(self, req):
+        r = await self._ws({"op": "wake_up"})
+        self.aeng.wake.set()
+        return r
+
+    async def is_sleeping(self, req):
+        return web.json_response({"is_sleeping": bool(self.aeng.engine.sleeping),
+                                  "level": self.aeng.engine.sleeping})
 
     # ------------------------------------------------------------ other OpenAI / vLLM / Anthropic surfaces
     async def _run_one(self, req, ids, params, prio=0, lora=0, mm=None):

@@ -51,7 +51,8 @@ class AsyncEngine:
                 self._apply_cmds()
                 # DP-lockstep (wide-EP) ranks step even when idle: busy peers need
                 # this rank in every MoE collective
-                if (eng.has_unfinished() or getattr(eng, "dp_lockstep", False)) and not eng.paused:
+                if (eng.has_unfinished() or getattr(eng, "dp_lockstep", False)) and not eng.paused \
+                        and not getattr(eng, "sleeping", 0):
                     outs = eng.step()
                     for o in outs:
                         self._emit(o)
