@@ -193,13 +193,16 @@ def main():
     log(rank, f"setup: {setup_steps} steps in {time.time() - ts:.1f}s (batch filled to {a.concurrency})")
 
     step_tokens = []
+    step_ms = collections.defaultdict(list)  # step size -> wall ms (a step ends in a host sync on sampling)
 
     def run_steps(n):
         for _ in range(n):
+            ts0 = time.perf_counter()
             for o in eng.step():
                 if o.finished:
                     new_request(a.osl)
             step_tokens.append(eng.last_num_tokens)
+            step_ms[eng.last_num_tokens].append(1000 * (time.perf_counter() - ts0))
 
     # warmup
     tw = time.time()
@@ -215,13 +218,15 @@ def main():
     _sync(a)
     t1 = time.perf_counter()
     step_tokens.clear()
+    step_ms.clear()
     run_steps(a.steps)
     _sync(a)
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t1
     hist = collections.Counter(step_tokens)
-    log(rank, "timed step sizes (tokens: steps): " + ", ".join(f"{k}: {v}" for k, v in sorted(hist.items())))
+    log(rank, "timed step sizes (tokens: steps, mean ms): " + ", ".join(
+        f"{k}: {v} x {statistics.mean(step_ms[k]):.1f}" for k, v in sorted(hist.items())))
     gen = eng.metrics.n_gen - gen0
     ptoks = eng.metrics.n_prompt - prompt0
     ttfts = list(eng.metrics.ttfts)
