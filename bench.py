@@ -49,6 +49,27 @@ REF_CONTEXT = ("reference publishes no Llama-3-70B number; its P/D headline is g
                "(guides/pd-disaggregation/README.md:336-460)")
 
 
+# The reference's published P/D run (guides/pd-disaggregation/README.md:336-460):
+# gpt-oss-120b, ISL ~5150 / OSL ~250, 16 H200 = 8 prefill TP1 + 2 decode TP4.
+REF_GPTOSS_TOK_S, REF_GPTOSS_GPUS = 12236.6, 16
+
+
+def _metric(model: str) -> str:
+    if model == "llama-3-70b":
+        return METRIC
+    return f"output tok/s per decode GPU + p50 TTFT, {model}"
+
+
+def _reference(model: str, value: float, n_gpus: int) -> dict:
+    if model != "gpt-oss-120b":
+        return {"reference_context": REF_CONTEXT}
+    per_gpu = REF_GPTOSS_TOK_S / REF_GPTOSS_GPUS
+    return {"reference_context": "reference gpt-oss-120b P/D on 16xH200 (mxfp4 weights): 12236.6 output tok/s "
+                                 "= 764.8 per GPU (guides/pd-disaggregation/README.md:336-460)",
+            "reference_output_tok_s_per_gpu": round(per_gpu, 1),
+            "output_tok_s_per_gpu_vs_reference": round(value / n_gpus / per_gpu, 3)}
+
+
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
@@ -120,7 +141,7 @@ def main():
         if rank == 0 and res is not None:
             value = res["gen"] / res["elapsed"]
             out = {
-                "metric": METRIC, "value": round(value, 2), "unit": "output tok/s (whole job)",
+                "metric": _metric(a.model), "value": round(value, 2), "unit": "output tok/s (whole job)",
                 "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
                 "ms_per_step": round(1000 * res["elapsed"] / a.steps, 3), "higher_is_better": True,
                 "scaling": "weak", "vs_baseline": None, "dtype": "fp8" if a.quantization == "fp8" else "bf16",
@@ -134,7 +155,7 @@ def main():
                            "kv_transfer": "kvx ipc over xGMI"},
                 "output_tok_s_per_decode_gpu": round(value / res["decode_ranks"], 2),
                 "p50_ttft_s": round(res["p50_ttft"], 4) if res["p50_ttft"] is not None else None,
-                "reference_context": REF_CONTEXT,
+                **_reference(a.model, value, world),
             }
             line = json.dumps(out)
             print(line, flush=True)
@@ -247,7 +268,7 @@ def main():
     p50 = statistics.median(all_ttft) if all_ttft else None
     n_decode_gpus = world if a.mode == "agg" else world - a.prefill_gpus
     result = {
-        "metric": METRIC,
+        "metric": _metric(a.model),
         "value": round(value, 2),
         "unit": "output tok/s (whole job)",
         "n_gpus": world,
@@ -267,7 +288,7 @@ def main():
         "output_tok_s_per_decode_gpu": round(value / max(1, n_decode_gpus), 2),
         "p50_ttft_s": round(p50, 4) if p50 is not None else None,
         "prefill_tok_s": round(ptoks / elapsed, 1),
-        "reference_context": REF_CONTEXT,
+        **_reference(a.model, value, world),
     }
     if rank == 0:
         line = json.dumps(result)
