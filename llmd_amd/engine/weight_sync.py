@@ -113,10 +113,12 @@ class WeightSync:
         m, attr = own
         s = getattr(m, attr + "_scale" if attr in ("w1", "w2") else "weight_scale")
         with torch.no_grad():
-            if p.dim() == 3:  # block-fp8 experts [E, N, K], scales [E, N/128, K/128]
-                stage = ops.dequant_fp8_block_weight(p, s).to(torch.bfloat16)
+            if p.dim() == 3:  # block-fp8 experts [E, N, K(padded to 128 on GPU)], scales [E, N/128, K/128]
+                k = full.shape[1] if kind == "experts_t" else full.shape[-1]
+                stage = ops.dequant_fp8_block_weight(p, s)[..., :k].to(torch.bfloat16).contiguous()
                 place(stage, full, kind, extra)
                 q, ns = ops.quant_fp8_block_weight(stage)
+                q = ops.pad_fp8_k(q, p.shape[-1])
             else:  # per-output-channel [N, K], scale [1, N]
                 stage = (p.float() * s.view(-1, 1)).to(torch.bfloat16)
                 place(stage, full, kind, extra)

@@ -60,6 +60,8 @@ def quantize_fp8(model: torch.nn.Module) -> int:
             w = getattr(m, name, None)
             if isinstance(w, torch.Tensor) and w.dim() == 3 and w.dtype == torch.bfloat16:
                 wq, s = ops.quant_fp8_block_weight(w.data)
+                if w.is_cuda and w.shape[2] % 128:  # whole 128-wide K-steps for the v2 grouped GEMM
+                    wq = ops.pad_fp8_k(wq, (w.shape[2] + 127) // 128 * 128)
                 setattr(m, name, torch.nn.Parameter(wq, requires_grad=False))
                 setattr(m, name + "_scale", torch.nn.Parameter(s, requires_grad=False))
                 n += 1

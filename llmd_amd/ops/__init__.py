@@ -315,6 +315,30 @@ def quant_fp8_block_weight(w: torch.Tensor, block: int = 128):
     return q, s.contiguous()
 
 
+def _quant_groups_padded(x: torch.Tensor, kp: int):
+    """quant_fp8_groups into rows of ``kp`` >= d columns, zeros past d (GPU)."""
+    T, d = x.shape
+    if kp == d:
+        return quant_fp8_groups(x)
+    x = x if x.stride(-1) == 1 and x.stride(0) % 8 == 0 else x.contiguous()
+    q = torch.empty(T, kp, dtype=FP8, device=x.device)
+    q.view(torch.uint8)[:, d:].zero_()
+    s = torch.empty(T, (kp + 127) // 128, dtype=torch.float32, device=x.device)
+    native().quant_fp8_groups(x, q[:, :d], s)
+    return q, s
+
+
+def pad_fp8_k(q: torch.Tensor, kp: int) -> torch.Tensor:
+    """Zero-pad the K (last) dim of fp8 [..., K] to ``kp`` columns (e4m3 0x00 = +0).
+    The v2 grouped GEMM streams whole 128-byte K-steps (one scale block), so
+    expert weights whose K is not a multiple of 128 (gpt-oss: 2880) are stored
+    padded on the GPU and activations are quantised into padded rows."""
+    k = q.shape[-1]
+    if kp == k:
+        return q
+    return torch.nn.functional.pad(q.view(torch.uint8), (0, kp - k)).view(FP8)
+
+
 def dequant_fp8_block_weight(q: torch.Tensor, s: torch.Tensor, block: int = 128) -> torch.Tensor:
     E, N, K = q.shape
     full = s.repeat_interleave(block, 1).repeat_interleave(block, 2)[:, :N, :K]
@@ -337,8 +361,9 @@ def moe_experts_fp8(x, ids, wts, w1q, w1s, w2q, w2s, act=0, alpha=1.702, limit=7
     C = native()
     T, d = x.shape
     k = ids.shape[1]
-    E, N1, _ = w1q.shape
+    E, N1, Kp1 = w1q.shape
     F = N1 // 2
+    Kp2 = w2q.shape[2]
     bm = C.moe_tile_m()
     n = T * k
     max_p = ((n + E * (bm - 1)) + bm - 1) // bm * bm
@@ -349,10 +374,10 @@ def moe_experts_fp8(x, ids, wts, w1q, w1s, w2q, w2s, act=0, alpha=1.702, limit=7
     total = torch.empty(1, dtype=torch.int32, device=dev)
     inv = torch.full((n,), -1, dtype=torch.int32, device=dev)
     C.moe_align(ids.contiguous().view(-1).to(torch.int32), E, sorted_ids, tile_e, offs, total, inv)
-    xq, xs = quant_fp8_groups(x)
+    xq, xs = _quant_groups_padded(x, Kp1)
     h = torch.empty(max_p, F, dtype=torch.bfloat16, device=dev)
     C.moe_gemm_fp8(xq, xs, k, sorted_ids, tile_e, w1q, w1s, h, 1, act, alpha, limit, False, b1)
-    hq, hs = quant_fp8_groups(h)
+    hq, hs = _quant_groups_padded(h, Kp2)
     y = torch.empty(max_p, d, dtype=torch.bfloat16, device=dev)
     ident = torch.arange(max_p, dtype=torch.int32, device=dev)
     ident = torch.where(sorted_ids >= 0, ident, torch.full_like(ident, -1))

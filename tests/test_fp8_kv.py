@@ -231,6 +231,12 @@ def test_moe_experts_fp8_gpu(T, E, k, d, F, act):
     r = ops.moe_experts_fp8(x.cpu(), ids.cpu(), wts.cpu(), w1q.cpu(), w1s.cpu(), w2q.cpu(), w2s.cpu(), act)
     err = (y.float().cpu() - r.float()).abs().max().item()
     assert err < 0.06 * r.float().abs().max().item() + 1e-3, err
+    if d % 128 or F % 128:  # K padded to whole 128-wide steps (quantize_fp8 on GPU): the v2 kernel path
+        c128 = lambda n: (n + 127) // 128 * 128  # noqa: E731
+        yp = ops.moe_experts_fp8(x, ids, wts, ops.pad_fp8_k(w1q, c128(d)), w1s, ops.pad_fp8_k(w2q, c128(F)), w2s,
+                                 act)
+        errp = (yp.float().cpu() - r.float()).abs().max().item()
+        assert errp < 0.06 * r.float().abs().max().item() + 1e-3, errp
 
 
 def test_fused_norm_act_quant_cpu_matches_unfused():
