@@ -676,37 +676,30 @@ __global__ __launch_bounds__(G2_NT, 2) void moe_gemm2_fp8_kernel(
     const int n = min(n0 + row, N - 1);
     boff[i] = n * K + g3_swz(row, lp) * 16;
   }
-  // activation scales of the tile's 64 rows: wave 0 lane r DMAs xs[row r][kb]
-  // next to the tile of step kb into xs_sm<buf>, so the fold reads 4
-  // contiguous floats per 16-row block from LDS. Padding rows read row 0
+  // Scales stay out of LDS so the kernel holds exactly two 40 KB tile buffers
+  // (80 KB): two workgroups per CU. (Staging them in LDS - 1.5 KB more - left
+  // one workgroup per CU and half the bytes in flight.) Lane r keeps the
+  // activation scale xs[row r][kb] in a VGPR, loaded one K-step ahead right
+  // after that step's DMA, so the loop-top vmcnt(0) covers it; rows are
+  // fetched across lanes with ds_bpermute. The wave's weight-block scale is a
+  // uniform (scalar) load, also one step ahead. Padding rows read row 0
   // (their outputs are never stored).
-  __shared__ __attribute__((aligned(256))) float xs_sm0[G2_BM];
-  __shared__ __attribute__((aligned(256))) float xs_sm1[G2_BM];
   const int wu = __builtin_amdgcn_readfirstlane(w);
   const float* xs_row = xs + (int64_t)max(0, tok_of(m0 + lane)) * xs_stride;
-  auto issue = [&](char* base, float* xsb, int k0) {
+  const float* wsr = ws + ((int64_t)e * nnb + (n0 + 64 * wu) / 128) * nkb;
+  auto issue = [&](char* base, int k0) {
 #pragma unroll
     for (int i = 0; i < 2; ++i) g2_dma(asrc[i] + k0, base + (2 * w + i) * 1024);
 #pragma unroll
     for (int i = 0; i < 8; ++i) g2_dma(We + boff[i] + k0, base + G2_AB + (8 * w + i) * 1024);
-    if (wu == 0)
-      __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)(xs_row + k0 / 128),
-                                       (void __attribute__((address_space(3)))*)xsb, 4, 0, 0);
   };
   const int r16 = lane & 15, kq = lane >> 4;
-  // weight scales of the wave's 128-column block for every K step, staged in
-  // LDS before the loop (host: nkb <= G2_MAX_KB)
-  __shared__ float ws_sm[4][G2_MAX_KB];
-  {
-    const float* wsr = ws + ((int64_t)e * nnb + (n0 + 64 * w) / 128) * nkb;
-    for (int kb = lane; kb < nkb; kb += 64) ws_sm[w][kb] = wsr[kb];
-  }
   f32x4_t acc[4][4];
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-  auto compute = [&](const char* base, const float* xsb, int kb) {
+  auto compute = [&](const char* base, float xv, float wsv) {
     const char* A = base;
     const char* B = base + G2_AB;
     i32x8_t bfr[4];
@@ -717,7 +710,6 @@ __global__ __launch_bounds__(G2_NT, 2) void moe_gemm2_fp8_kernel(
       const u32x4_t hi = *reinterpret_cast<const u32x4_t*>(B + row * 128 + g3_swz(row, 2 * kq + 1) * 16);
       bfr[j] = i32x8_t{(int)lo[0], (int)lo[1], (int)lo[2], (int)lo[3], (int)hi[0], (int)hi[1], (int)hi[2], (int)hi[3]};
     }
-    const float wsv = ws_sm[wu][kb];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {  // one 16-row block at a time keeps the block accumulators at 16 VGPRs
       const int row = 16 * i + r16;
@@ -730,26 +722,35 @@ __global__ __launch_bounds__(G2_NT, 2) void moe_gemm2_fp8_kernel(
       for (int j = 0; j < 4; ++j)
         blk[j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(af, bfr[j], f32x4_t{0.f, 0.f, 0.f, 0.f}, 0, 0, 0,
                                                                   127, 0, 127);
-      const f32x4_t sx = *reinterpret_cast<const f32x4_t*>(xsb + 16 * i + 4 * kq);
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const float sc = sx[r] * wsv;
+        const float sc = __shfl(xv, 16 * i + 4 * kq + r, 64) * wsv;
 #pragma unroll
         for (int j = 0; j < 4; ++j) acc[i][j][r] += blk[j][r] * sc;
       }
     }
   };
-  issue(buf0, xs_sm0, 0);  // the first barrier below also publishes ws_sm
+  float xv0 = xs_row[0], wv0 = wsr[0];
+  issue(buf0, 0);
   for (int kt = 0; kt < nkb; kt += 2) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    if (kt + 1 < nkb) issue(buf1, xs_sm1, (kt + 1) * 128);
-    compute(buf0, xs_sm0, kt);
+    float xv1 = 0.f, wv1 = 0.f;
+    if (kt + 1 < nkb) {
+      issue(buf1, (kt + 1) * 128);
+      xv1 = xs_row[kt + 1];
+      wv1 = wsr[kt + 1];
+    }
+    compute(buf0, xv0, wv0);
     if (kt + 1 >= nkb) break;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    if (kt + 2 < nkb) issue(buf0, xs_sm0, (kt + 2) * 128);
-    compute(buf1, xs_sm1, kt + 1);
+    if (kt + 2 < nkb) {
+      issue(buf0, (kt + 2) * 128);
+      xv0 = xs_row[kt + 2];
+      wv0 = wsr[kt + 2];
+    }
+    compute(buf1, xv1, wv1);
   }
 #pragma unroll
   for (int i = 0; i < 4; ++i) {

@@ -30,6 +30,8 @@ def run(name, T, E, k, d, F, act):
     w2 = torch.randn(E, d, F, device=dev, dtype=torch.bfloat16) * 0.02
     w1q, w1s = ops.quant_fp8_block_weight(w1)
     w2q, w2s = ops.quant_fp8_block_weight(w2)
+    c128 = lambda n: (n + 127) // 128 * 128  # noqa: E731 - K padded as quantize_fp8 stores it on the GPU
+    w1q, w2q = ops.pad_fp8_k(w1q, c128(d)), ops.pad_fp8_k(w2q, c128(F))
     ids, wts = ops.moe_topk(torch.randn(T, E, device=dev), k, scoring=0)
     tb = t_it(lambda: ops.moe_experts(x, ids, wts, w1, w2, act))
     tf = t_it(lambda: ops.moe_experts_fp8(x, ids, wts, w1q, w1s, w2q, w2s, act))
@@ -44,5 +46,5 @@ def run(name, T, E, k, d, F, act):
 if __name__ == "__main__":
     for T in (64, 256, 4096):
         run("deepseek-ep8", T, 32, 8, 7168, 2048, 0)
-    for T in (64, 1024):
+    for T in (64, 128, 1024, 5120):
         run("gpt-oss-120b", T, 128, 4, 2880, 2880, 2)
