@@ -160,7 +160,7 @@ __global__ __launch_bounds__(256) void moe_topk_kernel(const float* __restrict__
 __global__ __launch_bounds__(1024) void moe_align_kernel(const int* __restrict__ ids, int n, int E, int BM,
                                                          int* __restrict__ sorted_ids, int* __restrict__ tile_expert,
                                                          int* __restrict__ expert_offsets, int max_p,
-                                                         int* __restrict__ total_p) {
+                                                         int* __restrict__ total_p, int* __restrict__ inv) {
   extern __shared__ int sm[];  // counts[E], offs[E+1], cursor[E]
   int* cnt = sm;
   int* off = sm + E;
@@ -184,6 +184,7 @@ __global__ __launch_bounds__(1024) void moe_align_kernel(const int* __restrict__
   __syncthreads();
   const int P = off[E];
   for (int p = threadIdx.x; p < max_p; p += blockDim.x) sorted_ids[p] = -1;
+  for (int i = threadIdx.x; i < n; i += blockDim.x) inv[i] = -1;  // pairs routed off this rank stay -1
   for (int e = threadIdx.x; e < E; e += blockDim.x) {
     cur[e] = off[e];
     expert_offsets[e] = off[e];
@@ -230,7 +231,7 @@ __global__ __launch_bounds__(NT, 2) void moe_gemm_kernel(
     arow[i] = c >> 3;
     achk[i] = c & 7;
     const int sid = sorted_ids[m0 + arow[i]];
-    const int tok = sid < 0 ? -1 : (a_rows_are_slots ? sid : sid / topk);
+    const int tok = sid < 0 ? -1 : (a_rows_are_slots ? m0 + arow[i] : sid / topk);
     aptr[i] = tok < 0 ? nullptr : X + (int64_t)tok * x_stride;
   }
   u32x4_t ra[2], rb[4];
@@ -370,7 +371,7 @@ __global__ __launch_bounds__(G2_NT, 2) void moe_gemm2_kernel(
   for (int i = 0; i < 2; ++i) {
     const int row = 8 * (2 * w + i) + lr;
     const int sid = sorted_ids[m0 + row];
-    const int tok = sid < 0 ? 0 : (a_rows_are_slots ? sid : sid / topk);  // padding rows read row 0 (discarded)
+    const int tok = sid < 0 ? 0 : (a_rows_are_slots ? m0 + row : sid / topk);  // padding rows read row 0 (discarded)
     asrc[i] = X + (int64_t)tok * x_stride + g2_swz(row, lp) * 8;
   }
   const uint16_t* bsrc[8];
@@ -494,7 +495,7 @@ __global__ __launch_bounds__(NT, 2) void moe_gemm_fp8_kernel(
   const int r16 = lane & 15, kq = lane >> 4;
   auto tok_of = [&](int row) {
     const int sid = sorted_ids[row];
-    return sid < 0 ? -1 : (a_rows_are_slots ? sid : sid / topk);
+    return sid < 0 ? -1 : (a_rows_are_slots ? row : sid / topk);
   };
   int arow[2], achk[2];
   const uint8_t* aptr[2];
@@ -660,7 +661,7 @@ __global__ __launch_bounds__(G2_NT, 2) void moe_gemm2_fp8_kernel(
   const int lr = lane >> 3, lp = lane & 7;
   auto tok_of = [&](int row) {
     const int sid = sorted_ids[row];
-    return sid < 0 ? -1 : (a_rows_are_slots ? sid : sid / topk);
+    return sid < 0 ? -1 : (a_rows_are_slots ? row : sid / topk);
   };
   const uint8_t* asrc[2];
 #pragma unroll
@@ -829,7 +830,7 @@ void llmd_moe_align(const int* ids, int n, int E, int bm, int* sorted_ids, int* 
                     int* expert_offsets, int max_p, int* total_p, int* inv, hipStream_t st) {
   const size_t lds = (size_t)(3 * E + 1) * sizeof(int);
   hipLaunchKernelGGL(moe_align_kernel, dim3(1), dim3(1024), lds, st, ids, n, E, bm, sorted_ids, tile_expert,
-                     expert_offsets, max_p, total_p);
+                     expert_offsets, max_p, total_p, inv);
   hipLaunchKernelGGL(moe_invert_kernel, dim3((max_p + 255) / 256), dim3(256), 0, st, sorted_ids, max_p, inv);
 }
 

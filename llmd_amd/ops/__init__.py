@@ -372,16 +372,15 @@ def moe_experts_fp8(x, ids, wts, w1q, w1s, w2q, w2s, act=0, alpha=1.702, limit=7
     tile_e = torch.empty(max_p // bm, dtype=torch.int32, device=dev)
     offs = torch.empty(E + 1, dtype=torch.int32, device=dev)
     total = torch.empty(1, dtype=torch.int32, device=dev)
-    inv = torch.full((n,), -1, dtype=torch.int32, device=dev)
+    inv = torch.empty(n, dtype=torch.int32, device=dev)  # moe_align fills it (-1 = not on this rank)
     C.moe_align(ids.contiguous().view(-1).to(torch.int32), E, sorted_ids, tile_e, offs, total, inv)
     xq, xs = _quant_groups_padded(x, Kp1)
     h = torch.empty(max_p, F, dtype=torch.bfloat16, device=dev)
     C.moe_gemm_fp8(xq, xs, k, sorted_ids, tile_e, w1q, w1s, h, 1, act, alpha, limit, False, b1)
     hq, hs = _quant_groups_padded(h, Kp2)
     y = torch.empty(max_p, d, dtype=torch.bfloat16, device=dev)
-    ident = torch.arange(max_p, dtype=torch.int32, device=dev)
-    ident = torch.where(sorted_ids >= 0, ident, torch.full_like(ident, -1))
-    C.moe_gemm_fp8(hq, hs, 1, ident, tile_e, w2q, w2s, y, 0, 0, 0.0, 0.0, True, b2)
+    # second GEMM: A rows are the sorted slots themselves (row p of hq; a_rows_are_slots)
+    C.moe_gemm_fp8(hq, hs, 1, sorted_ids, tile_e, w2q, w2s, y, 0, 0, 0.0, 0.0, True, b2)
     if out is None:
         out = torch.empty(T, d, dtype=torch.bfloat16, device=dev)
     C.moe_combine(y, inv, wts.contiguous().view(-1).float(), k, out)
@@ -454,15 +453,13 @@ def moe_experts(x, ids, wts, w1, w2, act=0, alpha=1.702, limit=7.0, out=None, b1
     tile_e = torch.empty(max_p // bm, dtype=torch.int32, device=dev)
     offs = torch.empty(E + 1, dtype=torch.int32, device=dev)
     total = torch.empty(1, dtype=torch.int32, device=dev)
-    inv = torch.full((n,), -1, dtype=torch.int32, device=dev)
+    inv = torch.empty(n, dtype=torch.int32, device=dev)  # moe_align fills it (-1 = not on this rank)
     C.moe_align(ids.contiguous().view(-1), E, sorted_ids, tile_e, offs, total, inv)
     h = torch.empty(max_p, F, dtype=x.dtype, device=dev)
     C.moe_gemm(x, k, sorted_ids, tile_e, w1, h, 1, act, alpha, limit, False, b1)
     y = torch.empty(max_p, d, dtype=x.dtype, device=dev)
-    # second GEMM: A rows are the sorted slots themselves (row p of h)
-    ident = torch.arange(max_p, dtype=torch.int32, device=dev)
-    ident = torch.where(sorted_ids >= 0, ident, torch.full_like(ident, -1))
-    C.moe_gemm(h, 1, ident, tile_e, w2, y, 0, 0, 0.0, 0.0, True, b2)
+    # second GEMM: A rows are the sorted slots themselves (row p of h; a_rows_are_slots)
+    C.moe_gemm(h, 1, sorted_ids, tile_e, w2, y, 0, 0, 0.0, 0.0, True, b2)
     if out is None:
         out = torch.empty(T, d, dtype=x.dtype, device=dev)
     C.moe_combine(y, inv, wts.contiguous().view(-1), k, out)
