@@ -203,11 +203,16 @@ def main():
         new_request(max(1, int(a.osl * (i + 1) / a.concurrency)))
     ts = time.time()
     setup_steps = 0
+    t_note = ts
     while setup_steps < 100000:
         for o in eng.step():
             if o.finished:
                 new_request(a.osl)
         setup_steps += 1
+        if time.time() - t_note > 30:  # progress for long setups (silent runs read as hung)
+            t_note = time.time()
+            log(rank, f"setup: {setup_steps} steps, {len(eng.sched.running)} running, "
+                      f"{eng.sched.num_waiting} waiting")
         if eng.sched.num_waiting == 0 and all(r.output_token_ids for r in eng.sched.running):
             break
     _sync(a)
