@@ -204,16 +204,22 @@ def main():
     ts = time.time()
     setup_steps = 0
     t_note = ts
+    # With C > OSL about one request completes per step, so a replacement always
+    # waits at the check: then only this step's replacements may still wait.
+    may_wait = a.concurrency > a.osl
     while setup_steps < 100000:
+        added = 0
         for o in eng.step():
             if o.finished:
                 new_request(a.osl)
+                added += 1
         setup_steps += 1
         if time.time() - t_note > 30:  # progress for long setups (silent runs read as hung)
             t_note = time.time()
             log(rank, f"setup: {setup_steps} steps, {len(eng.sched.running)} running, "
                       f"{eng.sched.num_waiting} waiting")
-        if eng.sched.num_waiting == 0 and all(r.output_token_ids for r in eng.sched.running):
+        if eng.sched.num_waiting <= (added if may_wait else 0) and \
+                all(r.output_token_ids for r in eng.sched.running):
             break
     _sync(a)
     log(rank, f"setup: {setup_steps} steps in {time.time() - ts:.1f}s (batch filled to {a.concurrency})")
