@@ -298,12 +298,19 @@ class LLMEngine:
         op = cmd["op"]
         if op == "sleep" and self.has_unfinished():
             raise RuntimeError("cannot sleep with requests in flight (pause and drain first)")
+        if op == "sleep" and self.connector is not None:
+            raise RuntimeError("P/D engines cannot sleep: peers hold mappings of the KV pool")
         if self.weight_sync.sleeping and op not in ("wake_up", "sleep", "init_group", "destroy_group"):
             # level 2 woke up with uninitialised weights: the trainer sends them after wake_up
             raise RuntimeError("engine is asleep: wake_up first")
         res = self.weight_sync.apply(cmd)
         if op in ("update_from_group", "update_from_disk", "sleep", "wake_up"):
             self.reset_prefix_cache()
+        if self.offload is not None:
+            if op in ("update_from_group", "update_from_disk"):
+                self.offload.invalidate(self.weight_sync.version)  # offloaded KV is of the old weights
+            elif op == "wake_up":
+                self.offload.rebind(self.runner.kv)
         return res
 
     @property

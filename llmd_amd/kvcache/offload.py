@@ -65,6 +65,31 @@ class OffloadManager:
         self.events_out: list = []
         self.stats = {"offloaded": 0, "loaded_cpu": 0, "loaded_fs": 0, "evicted_cpu": 0}
         self.lock = threading.Lock()
+        self.weights_version = 0  # FS keys of KV computed by updated weights carry it (weight sync)
+
+    def _fs_key(self, h: int) -> str:
+        return f"{h:016x}" if self.weights_version == 0 else f"{h:016x}-w{self.weights_version}"
+
+    # ------------------------------------------------------------ weight sync / sleep (engine/weight_sync.py)
+    def invalidate(self, weights_version: int):
+        """New weights: every cached block holds KV of the old ones. Drop the host
+        tier (removal events for the router's index) and move FS keys to a new
+        namespace, so files of the old weights are never read again."""
+        if self.stream is not None:
+            self.stream.synchronize()
+        self.pending = []
+        for key in list(self.slot_of):
+            self.events_out.append((1, key, 0, -1, [], "cpu"))
+        self.slot_of.clear()
+        self.free_slots = list(range(self.n_slots - 1, -1, -1))
+        self.weights_version = weights_version
+
+    def rebind(self, kv):
+        """The device pool was re-allocated (wake-up after sleep)."""
+        if self.stream is not None:
+            self.stream.synchronize()
+        self.pending = []
+        self.kv = kv
 
     # ------------------------------------------------------------ write-through
     def on_block_events(self, events: list):
@@ -116,7 +141,7 @@ class OffloadManager:
             self.stats["offloaded"] += 1
             self.events_out.append((0, h, 0, -1, [], "cpu"))
             if self.fs is not None:
-                self.fs.write(f"{h:016x}", self.host[s].numpy())
+                self.fs.write(self._fs_key(h), self.host[s].numpy())
 
     def poll(self):
         keep = []
@@ -153,7 +178,7 @@ class OffloadManager:
             if s is not None:
                 found.append(("cpu", k, s))
                 continue
-            if self.fs is not None and self.fs.exists(f"{k:016x}"):
+            if self.fs is not None and self.fs.exists(self._fs_key(k)):
                 found.append(("fs", k, None))
                 continue
             break
@@ -171,7 +196,7 @@ class OffloadManager:
                 self.stats["loaded_cpu"] += 1
             else:
                 buf = torch.empty(self.block_bytes, dtype=torch.uint8, pin_memory=self.kv.is_cuda)
-                ok = self.fs.read(f"{k:016x}", buf.numpy())
+                ok = self.fs.read(self._fs_key(k), buf.numpy())
                 if not ok:
                     n = j
                     break

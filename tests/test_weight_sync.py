@@ -207,3 +207,21 @@ def test_update_from_disk_fp8_gpu(tmp_path):
     eng = LLMEngine(_cfg(b, device="cuda", quantization="fp8"))
     eng.weight_sync_cmd({"op": "update_from_disk", "path": a})
     assert [t for t, _ in _run(eng)] == [t for t, _ in ref]
+
+
+def test_update_invalidates_offloaded_kv(tmp_path):
+    """Host / FS KV tiers hold KV of the old weights: after an update a request
+    with the same prefix must recompute it, not reload it."""
+    a, b = _ckpts(tmp_path)
+    ref = _run(LLMEngine(_cfg(a)))
+    eng = LLMEngine(_cfg(b, kv_offload_config={"cpu_bytes_to_use": 64 << 20, "fs_root": str(tmp_path / "kv")}))
+    _run(eng)
+    off = eng.offload
+    off.poll()
+    assert off.stats["offloaded"] > 0 and off.slot_of
+    eng.weight_sync_cmd({"op": "update_from_disk", "path": a})
+    assert not off.slot_of and off.weights_version == 1
+    assert [e[0] for e in off.take_events()].count(1) > 0  # host-tier removals reach the router's index
+    loaded = (off.stats["loaded_cpu"], off.stats["loaded_fs"])
+    assert _run(eng) == ref
+    assert (off.stats["loaded_cpu"], off.stats["loaded_fs"]) == loaded
