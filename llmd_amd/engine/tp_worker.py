@@ -61,7 +61,10 @@ def run_follower(cfg: EngineConfig, capture_graphs: bool = True, on_ready=None) 
                     from .weight_sync import WeightSync
 
                     runner.weight_sync = WeightSync(runner)
-                runner.weight_sync.apply(pl["ws_cmd"])
+                try:  # a failed update (bad path, ...) fails on the driver too: stay in the loop
+                    runner.weight_sync.apply(pl["ws_cmd"])
+                except Exception:  # noqa: BLE001
+                    log.exception("weight-sync command %s failed", pl["ws_cmd"].get("op"))
                 continue
             if "kvx_cmd" in pl:  # P/D: KV pulls / cancels scheduled on the driver
                 kvx.apply(pl)

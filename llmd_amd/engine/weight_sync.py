@@ -138,6 +138,8 @@ class WeightSync:
     # ------------------------------------------------------------ commands
     def apply(self, cmd: dict):
         """Entry point on every rank (the driver forwards to TP followers first)."""
+        if cmd["op"] == "update_from_group" and self.pg is None:  # refuse before followers block in it
+            raise RuntimeError("no weight-sync group: call init_group first")
         if self.broadcast_cmd is not None:
             self.broadcast_cmd({"ws_cmd": cmd})
         op = cmd["op"]
