@@ -104,7 +104,9 @@ class LLMEngine:
         return {sr.req.seq_id: self.bm.block_table(sr.req.seq_id) for sr in so.all()}
 
     def step(self) -> list[RequestOutput]:
-        if self.paused or self.sleeping:  # asleep: new requests queue until wake_up
+        # asleep, or woken from level 2 with the trainer's weights not yet sent:
+        # new requests queue until the weights are real again
+        if self.paused or self.sleeping or self.weights_pending:
             return []
         if self.connector is not None:
             self.connector.tick()
@@ -303,12 +305,21 @@ class LLMEngine:
         if self.weight_sync.sleeping and op not in ("wake_up", "sleep", "init_group", "destroy_group"):
             # level 2 woke up with uninitialised weights: the trainer sends them after wake_up
             raise RuntimeError("engine is asleep: wake_up first")
-        res = self.weight_sync.apply(cmd)
+        if op == "sleep" and self.offload is not None and not self.weight_sync.sleeping:
+            # the offloader holds the pool (and staging copies of it): let go first,
+            # or the pool stays allocated while sleep reports it freed
+            self.offload.rebind(None)
+        try:
+            res = self.weight_sync.apply(cmd)
+        except BaseException:
+            if op == "sleep" and self.offload is not None and not self.weight_sync.sleeping:
+                self.offload.rebind(self.runner.kv)
+            raise
         if op in ("update_from_group", "update_from_disk", "sleep", "wake_up"):
             self.reset_prefix_cache()
         if self.offload is not None:
             if op in ("update_from_group", "update_from_disk"):
-                self.offload.invalidate(self.weight_sync.version)  # offloaded KV is of the old weights
+                self.offload.invalidate(self.weight_sync.weights_id)  # offloaded KV is of the old weights
             elif op == "wake_up":
                 self.offload.rebind(self.runner.kv)
         return res
@@ -317,3 +328,8 @@ class LLMEngine:
     def sleeping(self) -> int:
         ws = getattr(self.runner, "weight_sync", None)
         return ws.sleeping if ws is not None else 0
+
+    @property
+    def weights_pending(self) -> bool:
+        ws = getattr(self.runner, "weight_sync", None)
+        return ws.weights_pending if ws is not None else False

@@ -33,8 +33,11 @@ idle engine; KV producers (their pool is exported to decoders) cannot sleep.
 from __future__ import annotations
 
 import datetime
+import hashlib
 import logging
+import os
 import time
+import uuid
 from typing import Optional
 
 import torch
@@ -68,6 +71,30 @@ def new_group(addr: str, port: int, rank: int, world_size: int, backend: str, de
     return pg, store
 
 
+def checkpoint_identity(path: str) -> str:
+    """A stable name for the weights in a safetensors checkpoint: file names,
+    sizes, mtimes and each file's header (tensor names, dtypes, offsets). Two
+    replicas loading the same files agree on it; a re-written checkpoint gets a
+    new one. Hashing the payload itself (140 GB for a 70B model) would cost
+    more than the load."""
+    h = hashlib.sha256()
+    for f in _files(path):
+        st = os.stat(f)
+        h.update(f"{os.path.basename(f)}:{st.st_size}:{st.st_mtime_ns}".encode())
+        with open(f, "rb") as fh:
+            n = int.from_bytes(fh.read(8), "little")
+            h.update(fh.read(min(n, 1 << 24)))
+    return "ckpt:" + h.hexdigest()[:20]
+
+
+def initial_identity(cfg) -> str:
+    """Identity of the weights an engine starts with (before any update)."""
+    q = cfg.quantization or "none"
+    if cfg.load_format == "safetensors" and cfg.weights_path:
+        return f"{checkpoint_identity(cfg.weights_path)}:{q}"
+    return f"dummy:{cfg.model_config.name}:{cfg.seed}:{cfg.dtype}:{q}"
+
+
 def broadcast(pg, t: torch.Tensor, root: int = 0):
     o = dist.BroadcastOptions()
     o.rootRank = root
@@ -84,8 +111,16 @@ class WeightSync:
         self._store = None
         self.group_rank = -1
         self.sleeping = 0
+        # after a level-2 wake-up the weights are uninitialised storage until an
+        # update lands: the engine must not step (engine.step checks this)
+        self.weights_pending = False
         self._host: dict[str, torch.Tensor] = {}
-        self.version = 0
+        self.version = 0  # per-process update counter (metrics / logs only)
+        cfg = getattr(runner, "cfg", None)
+        # stable identity of the current weights: the FS KV tier namespaces its
+        # keys by it, so KV computed by other weights - in this process, an earlier
+        # one, or another replica sharing the directory - is never reloaded
+        self.weights_id = initial_identity(cfg) if cfg is not None else "unknown"
 
     # ------------------------------------------------------------ placement
     def _specs(self) -> dict:
@@ -127,13 +162,16 @@ class WeightSync:
             s.copy_(ns.view_as(s))
         return True
 
-    def _finish(self, n: int, t0: float, src: str) -> dict:
+    def _finish(self, n: int, t0: float, src: str, weights_id: str) -> dict:
         if self.runner.is_gpu:
             torch.cuda.synchronize(self.runner.device)
         self.version += 1
-        log.info("weights updated from %s: %d tensors in %.2fs (version %d)", src, n, time.time() - t0,
-                 self.version)
-        return {"updated": n, "version": self.version, "seconds": round(time.time() - t0, 3)}
+        self.weights_id = weights_id
+        self.weights_pending = False
+        log.info("weights updated from %s: %d tensors in %.2fs (version %d, id %s)", src, n, time.time() - t0,
+                 self.version, weights_id)
+        return {"updated": n, "version": self.version, "weights_id": weights_id,
+                "seconds": round(time.time() - t0, 3)}
 
     # ------------------------------------------------------------ commands
     def apply(self, cmd: dict):
@@ -147,9 +185,9 @@ class WeightSync:
             return self.init_group(cmd["addr"], cmd["port"], cmd["rank_offset"], cmd["world_size"],
                                    cmd.get("backend"), cmd.get("timeout_s", 300.0))
         if op == "update_from_group":
-            return self.update_from_group(cmd["metas"])
+            return self.update_from_group(cmd["metas"], cmd.get("weights_version"))
         if op == "update_from_disk":
-            return self.update_from_disk(cmd["path"])
+            return self.update_from_disk(cmd["path"], cmd.get("weights_version"))
         if op == "destroy_group":
             return self.destroy_group()
         if op == "sleep":
@@ -177,8 +215,10 @@ class WeightSync:
         return {"destroyed": True}
 
     @torch.no_grad()
-    def update_from_group(self, metas: list) -> dict:
-        """metas: [(hf_name, dtype name, shape)], broadcast by group rank 0 in order."""
+    def update_from_group(self, metas: list, weights_version: Optional[str] = None) -> dict:
+        """metas: [(hf_name, dtype name, shape)], broadcast by group rank 0 in order.
+        ``weights_version``: the trainer's name for these weights (e.g. its step);
+        without one the update gets a unique id, so its KV is never shared."""
         if self.pg is None:
             raise RuntimeError("no weight-sync group: call init_group first")
         if self.sleeping == 2:
@@ -191,20 +231,26 @@ class WeightSync:
             buf = torch.empty(tuple(shape), dtype=dtype_of(dt), device=dev)
             broadcast(self.pg, buf, 0)
             n += self._load_one(specs, name, buf)
-        return self._finish(n, t0, "group")
+        wid = f"trainer:{weights_version}" if weights_version is not None else f"group:{uuid.uuid4().hex}"
+        return self._finish(n, t0, "group", self._with_quant(wid))
 
     @torch.no_grad()
-    def update_from_disk(self, path: str) -> dict:
+    def update_from_disk(self, path: str, weights_version: Optional[str] = None) -> dict:
         from safetensors import safe_open
 
         t0 = time.time()
+        wid = f"trainer:{weights_version}" if weights_version is not None else checkpoint_identity(path)
         specs = self._specs()
         n = 0
         for f in _files(path):
             with safe_open(f, framework="pt", device="cpu") as fh:
                 for name in fh.keys():
                     n += self._load_one(specs, name, fh.get_tensor(name))
-        return self._finish(n, t0, path)
+        return self._finish(n, t0, path, self._with_quant(wid))
+
+    def _with_quant(self, wid: str) -> str:
+        cfg = getattr(self.runner, "cfg", None)
+        return f"{wid}:{(cfg.quantization if cfg is not None else None) or 'none'}"
 
     # ------------------------------------------------------------ sleep / wake
     def _tensors(self):
@@ -278,8 +324,11 @@ class WeightSync:
             r.kv = r._alloc_cache(r.num_blocks)
             r.capture_graphs()
         level, self.sleeping = self.sleeping, 0
+        if level == 2:  # storage is back but holds garbage until the trainer's update
+            self.weights_pending = True
         log.info("woke from level %d in %.2fs", level, time.time() - t0)
-        return {"sleeping": 0, "woke_from": level, "seconds": round(time.time() - t0, 3)}
+        return {"sleeping": 0, "woke_from": level, "weights_pending": self.weights_pending,
+                "seconds": round(time.time() - t0, 3)}
 
 
 # ---------------------------------------------------------------- trainer side

@@ -26,6 +26,7 @@ its slot; reloads DMA a slot into a staging row and scatter it back.
 from __future__ import annotations
 
 import collections
+import hashlib
 import logging
 import os
 import threading
@@ -65,16 +66,25 @@ class OffloadManager:
         self.events_out: list = []
         self.stats = {"offloaded": 0, "loaded_cpu": 0, "loaded_fs": 0, "evicted_cpu": 0}
         self.lock = threading.Lock()
-        self.weights_version = 0  # FS keys of KV computed by updated weights carry it (weight sync)
+        # FS keys carry a namespace derived from the weights' stable identity
+        # (engine/weight_sync.py: checkpoint identity, trainer version or a unique
+        # id per update), not a per-process counter: a restarted engine, or another
+        # replica sharing fs_root, only ever reads KV computed by the same weights
+        self.weights_id = engine.weight_sync.weights_id
+        self.ns = self._namespace(self.weights_id)
+
+    @staticmethod
+    def _namespace(weights_id: str) -> str:
+        return hashlib.sha256(weights_id.encode()).hexdigest()[:12]
 
     def _fs_key(self, h: int) -> str:
-        return f"{h:016x}" if self.weights_version == 0 else f"{h:016x}-w{self.weights_version}"
+        return f"{h:016x}-{self.ns}"
 
     # ------------------------------------------------------------ weight sync / sleep (engine/weight_sync.py)
-    def invalidate(self, weights_version: int):
+    def invalidate(self, weights_id: str):
         """New weights: every cached block holds KV of the old ones. Drop the host
-        tier (removal events for the router's index) and move FS keys to a new
-        namespace, so files of the old weights are never read again."""
+        tier (removal events for the router's index) and move FS keys to the new
+        weights' namespace, so files of the old weights are never read again."""
         if self.stream is not None:
             self.stream.synchronize()
         self.pending = []
@@ -82,10 +92,15 @@ class OffloadManager:
             self.events_out.append((1, key, 0, -1, [], "cpu"))
         self.slot_of.clear()
         self.free_slots = list(range(self.n_slots - 1, -1, -1))
-        self.weights_version = weights_version
+        self.weights_id = weights_id
+        self.ns = self._namespace(weights_id)
 
     def rebind(self, kv):
-        """The device pool was re-allocated (wake-up after sleep)."""
+        """The device pool is released (``kv=None``, sleep) or was re-allocated
+        (wake-up). In-flight D2H copies read the old pool: wait for them, and
+        drop their staging tensors, before the pool can be freed. Blocks whose
+        copy had not been committed are not published (their KV events were
+        never sent)."""
         if self.stream is not None:
             self.stream.synchronize()
         self.pending = []
@@ -95,7 +110,7 @@ class OffloadManager:
     def on_block_events(self, events: list):
         """Engine BlockManager events of the step just executed."""
         todo = [(int(h), int(b)) for kind, h, parent, b, toks in events if kind == 0]
-        if not todo:
+        if not todo or self.kv is None:
             return
         todo = [(h, b) for h, b in todo if h not in self.slot_of]
         if not todo:
@@ -118,7 +133,10 @@ class OffloadManager:
                     self.host[slot].copy_(rows[i], non_blocking=True)
                 ev = torch.cuda.Event()
                 ev.record(self.stream)
-            self.pending.append((ev, [(h, s) for h, _, s in assign], g))  # g lives until the DMAs land
+            # idx (made on the compute stream, read by the side stream's gather) and
+            # the staging tensor g stay referenced until the copies land, so the
+            # caching allocator cannot hand their memory to the compute stream early
+            self.pending.append((ev, [(h, s) for h, _, s in assign], g, idx))
         else:
             rows = self.kv.index_select(1, idx).transpose(0, 1).contiguous().view(len(assign), -1)
             for i, (h, b, slot) in enumerate(assign):

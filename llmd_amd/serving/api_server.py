@@ -413,11 +413,21 @@ class OpenAIServer:
             metas = [tuple(m) for m in b["metas"]]
         else:
             metas = list(zip(b["names"], b["dtypes"], b["shapes"]))
-        return await self._ws({"op": "update_from_group", "metas": metas})
+        cmd = {"op": "update_from_group", "metas": metas}
+        if b.get("weights_version") is not None:  # the trainer's name for these weights (FS KV namespace)
+            cmd["weights_version"] = str(b["weights_version"])
+        r = await self._ws(cmd)
+        self.aeng.wake.set()  # requests held after a level-2 wake-up can run now
+        return r
 
     async def update_weights_from_disk(self, req):
         b = await req.json()
-        return await self._ws({"op": "update_from_disk", "path": b["path"]})
+        cmd = {"op": "update_from_disk", "path": b["path"]}
+        if b.get("weights_version") is not None:
+            cmd["weights_version"] = str(b["weights_version"])
+        r = await self._ws(cmd)
+        self.aeng.wake.set()
+        return r
 
     async def destroy_weight_update_group(self, req):
         return await self._ws({"op": "destroy_group"})
@@ -435,7 +445,8 @@ class OpenAIServer:
 
     async def is_sleeping(self, req):
         return web.json_response({"is_sleeping": bool(self.aeng.engine.sleeping),
-                                  "level": self.aeng.engine.sleeping})
+                                  "level": self.aeng.engine.sleeping,
+                                  "weights_pending": bool(self.aeng.engine.weights_pending)})
 
     # ------------------------------------------------------------ other OpenAI / vLLM / Anthropic surfaces
     async def _run_one(self, req, ids, params, prio=0, lora=0, mm=None):

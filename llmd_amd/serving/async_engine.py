@@ -52,7 +52,7 @@ class AsyncEngine:
                 # DP-lockstep (wide-EP) ranks step even when idle: busy peers need
                 # this rank in every MoE collective
                 if (eng.has_unfinished() or getattr(eng, "dp_lockstep", False)) and not eng.paused \
-                        and not getattr(eng, "sleeping", 0):
+                        and not getattr(eng, "sleeping", 0) and not getattr(eng, "weights_pending", False):
                     outs = eng.step()
                     for o in outs:
                         self._emit(o)
