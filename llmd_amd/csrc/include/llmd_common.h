@@ -63,6 +63,20 @@ __device__ __forceinline__ u32x4_t pack8(const float* f) {
 // softmax scale / output), so conversions here are unscaled.
 constexpr float FP8_MAX = 448.f;
 
+// Smallest power of two >= r (r > 0, normal): block scales of the fp8 MoE path
+// are powers of two so the grouped GEMM can hand them to the MFMA as E8M0
+// exponents (v_mfma_scale_*: scale = 2^(e - 127)) instead of re-scaling block
+// partial sums on the VALU. e4m3's relative precision does not depend on the
+// binade, so a power-of-two scale only gives up the unused top of [amax, 448].
+__device__ __forceinline__ float pow2_ceil(float r) {
+  unsigned u = __float_as_uint(r);
+  unsigned e = u >> 23;
+  if (u & 0x7fffffu) ++e;
+  return __uint_as_float(e << 23);
+}
+// E8M0 exponent byte of a power-of-two float scale.
+__device__ __forceinline__ int e8m0_of(float pow2) { return (int)((__float_as_uint(pow2) >> 23) & 0xffu); }
+
 // 8 floats -> 8 e4m3fn bytes (saturating: v_cvt_pk_fp8_f32 alone would map
 // |x| > 448 to NaN).
 __device__ __forceinline__ u32x2_t f32x8_to_fp8(const float* f) {

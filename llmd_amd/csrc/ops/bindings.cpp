@@ -75,6 +75,10 @@ int llmd_quant_fp8_groups(const void*, int64_t, void*, int64_t, float*, int64_t,
 void llmd_moe_gemm_fp8(const void*, int64_t, const float*, int64_t, int, const int*, const int*, int, const void*,
                        int64_t, const float*, int, int, void*, int64_t, int, int, float, float, int, const void*,
                        hipStream_t);
+int llmd_moe_gemm3_fp8(const void*, int64_t, const float*, int64_t, int, const int*, const int*, int, const void*,
+                       int64_t, const float*, int, int, void*, int64_t, int, int, float, float, int, const void*,
+                       hipStream_t);
+int llmd_moe_gemm3_tile_m();
 int llmd_symm_alloc(size_t, void**);
 int llmd_symm_free(void*);
 int64_t llmd_symm_sig_bytes();
@@ -558,11 +562,12 @@ void moe_topk(torch::Tensor logits, int64_t k, int64_t scoring, c10::optional<to
 }
 
 void moe_align(torch::Tensor ids, int64_t E, torch::Tensor sorted_ids, torch::Tensor tile_expert,
-               torch::Tensor expert_offsets, torch::Tensor total_p, torch::Tensor inv) {
+               torch::Tensor expert_offsets, torch::Tensor total_p, torch::Tensor inv, int64_t tile_m) {
   const c10::hip::OptionalHIPGuard device_guard(dev_of(ids));
   CHECK_CUDA(ids); CHECK_DT(ids, at::kInt); CHECK_DT(sorted_ids, at::kInt); CHECK_DT(tile_expert, at::kInt);
   const int n = ids.numel();
-  const int bm = llmd_moe_gemm_tile_m();
+  const int bm = tile_m > 0 ? (int)tile_m : llmd_moe_gemm_tile_m();
+  TORCH_CHECK(bm == llmd_moe_gemm_tile_m() || bm == llmd_moe_gemm3_tile_m(), "moe_align: tile_m");
   const int max_p = sorted_ids.numel();
   TORCH_CHECK(max_p % bm == 0 && max_p >= n + E * (bm - 1), "sorted_ids too small");
   TORCH_CHECK(tile_expert.numel() >= max_p / bm && expert_offsets.numel() >= E + 1 && inv.numel() >= n,
@@ -670,7 +675,7 @@ void quant_fp8_groups(torch::Tensor x, torch::Tensor q, torch::Tensor scale) {
 
 void moe_gemm_fp8(torch::Tensor X, torch::Tensor xs, int64_t topk, torch::Tensor sorted_ids, torch::Tensor tile_expert,
                   torch::Tensor W, torch::Tensor ws, torch::Tensor Y, int64_t mode, int64_t act, double alpha,
-                  double limit, bool a_rows_are_slots, c10::optional<torch::Tensor> bias) {
+                  double limit, bool a_rows_are_slots, c10::optional<torch::Tensor> bias, int64_t tile_m) {
   const c10::hip::OptionalHIPGuard device_guard(dev_of(X));
   CHECK_CUDA(X); CHECK_DT(X, at::kFloat8_e4m3fn); CHECK_DT(W, at::kFloat8_e4m3fn); CHECK_BF16(Y);
   CHECK_INNER(X); CHECK_INNER(Y); CHECK_DT(xs, at::kFloat); CHECK_DT(ws, at::kFloat);
@@ -681,7 +686,9 @@ void moe_gemm_fp8(torch::Tensor X, torch::Tensor xs, int64_t topk, torch::Tensor
               "ws [E, ceil(N/128), ceil(K/128)]");
   TORCH_CHECK(xs.dim() == 2 && xs.size(0) >= X.size(0) && xs.size(1) >= (K + 127) / 128 && xs.stride(1) == 1,
               "xs [rows, ceil(K/128)]");
-  const int bm = llmd_moe_gemm_tile_m();
+  const bool v3 = tile_m == llmd_moe_gemm3_tile_m();
+  TORCH_CHECK(tile_m <= 0 || tile_m == llmd_moe_gemm_tile_m() || v3, "moe_gemm_fp8: tile_m");
+  const int bm = v3 ? (int)tile_m : llmd_moe_gemm_tile_m();
   const int P = sorted_ids.numel();
   TORCH_CHECK(P % bm == 0 && tile_expert.numel() >= P / bm && Y.size(0) >= P, "moe_gemm_fp8: rows");
   TORCH_CHECK(Y.size(1) >= (mode == 1 ? N / 2 : N) && N % 2 == 0, "moe_gemm_fp8: Y width");
@@ -690,6 +697,15 @@ void moe_gemm_fp8(torch::Tensor X, torch::Tensor xs, int64_t topk, torch::Tensor
     CHECK_BF16(bias.value());
     TORCH_CHECK(bias->is_contiguous() && bias->numel() == (int64_t)E * N, "bias [E, N]");
     bp = bias->data_ptr();
+  }
+  if (v3) {  // 256-row expert tiles: power-of-two scales, K % 128 == 0, 16-B rows
+    TORCH_CHECK(K % 128 == 0 && X.stride(0) % 16 == 0 && W.stride(0) % 16 == 0, "moe_gemm_fp8 (256-row tiles): K");
+    const int rc = llmd_moe_gemm3_fp8(X.data_ptr(), X.stride(0), xs.data_ptr<float>(), xs.stride(0), topk,
+                                      sorted_ids.data_ptr<int>(), tile_expert.data_ptr<int>(), P / bm, W.data_ptr(),
+                                      W.stride(0), ws.data_ptr<float>(), N, K, Y.data_ptr(), Y.stride(0), mode, act,
+                                      (float)alpha, (float)limit, a_rows_are_slots ? 1 : 0, bp, cur_stream());
+    TORCH_CHECK(rc == 0, "moe_gemm3_fp8 failed: ", rc);
+    return;
   }
   llmd_moe_gemm_fp8(X.data_ptr(), X.stride(0), xs.data_ptr<float>(), xs.stride(0), topk, sorted_ids.data_ptr<int>(),
                     tile_expert.data_ptr<int>(), P / bm, W.data_ptr(), W.stride(0), ws.data_ptr<float>(), N, K,
@@ -801,7 +817,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {  // _C, or _C_debug (llmd_amd/build.p
   m.def("vmm_import", &vmm_import);
   m.def("vmm_release", &vmm_release);
   m.def("moe_topk", &moe_topk);
-  m.def("moe_align", &moe_align);
+  m.def("moe_align", &moe_align, py::arg("ids"), py::arg("E"), py::arg("sorted_ids"), py::arg("tile_expert"),
+        py::arg("expert_offsets"), py::arg("total_p"), py::arg("inv"), py::arg("tile_m") = 0);
   m.def("moe_gemm", &moe_gemm);
   m.def("moe_combine", &moe_combine);
   m.def("moe_tile_m", &llmd_moe_gemm_tile_m);
@@ -809,7 +826,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {  // _C, or _C_debug (llmd_amd/build.p
   m.def("quant_fp8_groups", &quant_fp8_groups);
   m.def("rms_norm_quant", &rms_norm_quant);
   m.def("gated_act_quant", &gated_act_quant);
-  m.def("moe_gemm_fp8", &moe_gemm_fp8);
+  m.def("moe_gemm_fp8", &moe_gemm_fp8, py::arg("X"), py::arg("xs"), py::arg("topk"), py::arg("sorted_ids"),
+        py::arg("tile_expert"), py::arg("W"), py::arg("ws"), py::arg("Y"), py::arg("mode"), py::arg("act"),
+        py::arg("alpha"), py::arg("limit"), py::arg("a_rows_are_slots"), py::arg("bias"), py::arg("tile_m") = 0);
+  m.def("moe_tile_m_prefill", &llmd_moe_gemm3_tile_m);
   m.def("symm_alloc", &symm_alloc);
   m.def("symm_error", &symm_error);
   m.def("symm_sig_bytes", &llmd_symm_sig_bytes);

@@ -643,7 +643,14 @@ __device__ __forceinline__ int g3_swz(int row, int c) { return c ^ ((0x32765410 
 
 typedef int i32x8_t __attribute__((ext_vector_type(8)));
 
-template <int MODE>
+// HWS (hardware scales): the block scales are powers of two (quant_fp8_groups /
+// quant_fp8_block_weight make them so), handed to the MFMA as E8M0 exponents -
+// lane l's scale_a applies to A row l&15, scale_b to B column l&15, over the
+// instruction's whole 128-deep K step when all four lane groups carry the same
+// value (probed: scripts/probes/mfma_scale_map2.hip) - and the product is
+// accumulated in place: no per-step block accumulator, no VALU re-scaling
+// (~10 VALU per MFMA before), MFMAs back to back.
+template <int MODE, bool HWS>
 __global__ __launch_bounds__(G2_NT, 2) void moe_gemm2_fp8_kernel(
     const uint8_t* __restrict__ X, int64_t x_stride, const float* __restrict__ xs, int64_t xs_stride, int topk,
     const int* __restrict__ sorted_ids, const int* __restrict__ tile_expert, const uint8_t* __restrict__ W,
@@ -711,6 +718,22 @@ __global__ __launch_bounds__(G2_NT, 2) void moe_gemm2_fp8_kernel(
       const u32x4_t hi = *reinterpret_cast<const u32x4_t*>(B + row * 128 + g3_swz(row, 2 * kq + 1) * 16);
       bfr[j] = i32x8_t{(int)lo[0], (int)lo[1], (int)lo[2], (int)lo[3], (int)hi[0], (int)hi[1], (int)hi[2], (int)hi[3]};
     }
+    if constexpr (HWS) {
+      const int xe = e8m0_of(xv), we = e8m0_of(wsv);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int row = 16 * i + r16;
+        const u32x4_t lo = *reinterpret_cast<const u32x4_t*>(A + row * 128 + g3_swz(row, 2 * kq) * 16);
+        const u32x4_t hi = *reinterpret_cast<const u32x4_t*>(A + row * 128 + g3_swz(row, 2 * kq + 1) * 16);
+        const i32x8_t af =
+            i32x8_t{(int)lo[0], (int)lo[1], (int)lo[2], (int)lo[3], (int)hi[0], (int)hi[1], (int)hi[2], (int)hi[3]};
+        const int sa = __shfl(xe, row, 64);  // lane `row` holds the scale of tile row `row`
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(af, bfr[j], acc[i][j], 0, 0, 0, sa, 0, we);
+      }
+      return;
+    }
 #pragma unroll
     for (int i = 0; i < 4; ++i) {  // one 16-row block at a time keeps the block accumulators at 16 VGPRs
       const int row = 16 * i + r16;
@@ -769,6 +792,177 @@ __global__ __launch_bounds__(G2_NT, 2) void moe_gemm2_fp8_kernel(
         } else {
           const float other = __shfl_xor(v, 1, 64);
           if ((r16 & 1) == 0) {
+            float g = v, u = other, o;
+            if (act == 2) {
+              g = fminf(g, limit);
+              u = fminf(fmaxf(u, -limit), limit);
+              o = (u + 1.f) * g / (1.f + __expf(-alpha * g));
+            } else {
+              o = g / (1.f + __expf(-g)) * u;
+            }
+            if (col < N) Y[(int64_t)row * y_stride + col / 2] = f2bf(o);
+          }
+        }
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------- FP8 grouped GEMM v3 (prefill shapes)
+// For steps where experts receive many rows (prefill: gpt-oss ~160 rows per
+// expert at 5k tokens, DeepSeek EP8 ~1k). v2's 64-row tiles re-read an
+// expert's whole weight panel once per 64 rows - at gpt-oss shapes three
+// passes over 3.2 GB of weights per layer - and 64x256 tiles carry only 105
+// FLOP per staged byte. v3 takes 256-row expert tiles (moe_align with
+// bm = 256: one tile holds every row of a gpt-oss expert) x 256 columns on
+// ONE 512-thread workgroup per CU:
+//   * 8 waves as 2 (M) x 4 (N), each 128 x 64 = 4 x 2 tiles of
+//     v_mfma_scale_f32_32x32x64_f8f6f4 (128 accumulator VGPRs; layout probed by
+//     scripts/probes/mfma32_scale_layout.hip); E8M0 hardware block scales
+//     (power-of-two scales, see HWS above): the K loop is MFMAs, fragment
+//     reads and DMA issue only;
+//   * K-steps of 64 fp8 through a 4-deep LDS ring (34 KB per stage: A 256 x
+//     64 B gathered through sorted_ids by the DMA's per-lane source address,
+//     B 256 x 64 B, and the step's activation scales, which ride the DMA too:
+//     an ordinary vector load in the loop would make hipcc drain vmcnt(0)),
+//     three stages in flight across raw s_barriers with COUNTED vmcnt waits;
+//     64-B rows, 16-B chunks XOR-swizzled by (row >> 2) & 3 on the DMA source
+//     so every ds_read_b128 lane group covers 16 distinct bank slots;
+//   * rows past the expert's last row (moe_align pads experts to 256) are
+//     loaded (from token 0, L2 hits: the DMA count per stage stays fixed for
+//     the counted waits) but not multiplied or stored: the valid rows are a
+//     prefix, each wave skips its 32-row blocks past it (wave-uniform).
+constexpr int G3_BM = 256, G3_BN = 256, G3_NT = 512, G3_NS = 4;
+constexpr int G3_A = G3_BM * 64, G3_B = G3_BN * 64, G3_SC = 8 * 256;
+constexpr int G3_STAGE = G3_A + G3_B + G3_SC;  // 34 KB
+constexpr int G3_OPS = 5;                       // VMEM ops per wave per stage: 2 A + 2 B + 1 scale
+
+typedef float f32x16v_t __attribute__((ext_vector_type(16)));
+
+__device__ __forceinline__ int g3r_swz(int row, int c) { return c ^ ((row >> 2) & 3); }
+
+__device__ __forceinline__ void g3_dma4(const void* src, char* lds_base) {
+  __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)src,
+                                   (void __attribute__((address_space(3)))*)lds_base, 4, 0, 0);
+}
+
+template <int MODE>
+__global__ __launch_bounds__(G3_NT, 1) void moe_gemm3_fp8_kernel(
+    const uint8_t* __restrict__ X, int64_t x_stride, const float* __restrict__ xs, int64_t xs_stride, int topk,
+    const int* __restrict__ sorted_ids, const int* __restrict__ tile_expert, const uint8_t* __restrict__ W,
+    int64_t w_expert_stride, const float* __restrict__ ws, int N, int K, uint16_t* __restrict__ Y, int64_t y_stride,
+    int act, float alpha, float limit, int a_rows_are_slots, const uint16_t* __restrict__ bias) {
+  // ONE __shared__ array (a second LDS object can make hipcc drain vmcnt before every ds_read)
+  __shared__ __attribute__((aligned(1024))) char lds[G3_NS * G3_STAGE];
+  const int mt = blockIdx.y, nt = blockIdx.x;
+  const int e = tile_expert[mt];
+  if (e < 0) return;
+  const int m0 = mt * G3_BM, n0 = nt * G3_BN;
+  const int nk = K / 64, nkb = K / 128, nnb = (N + 127) / 128;
+  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+  const int wm = w >> 2, wn = w & 3;
+  const int l32 = lane & 31, h = lane >> 5;
+  // valid rows of this tile (a prefix: moe_align pads each expert at its end), counted per wave
+  // with ballots: no LDS object besides the staging ring (a second one, like __syncthreads_count's,
+  // makes hipcc wait vmcnt(0) for the in-flight DMAs before every ds_read)
+  int nvalid = 0;
+#pragma unroll
+  for (int q = 0; q < G3_BM / 64; ++q) nvalid += __popcll(__ballot(sorted_ids[m0 + 64 * q + lane] >= 0));
+  auto tok_of = [&](int row) {
+    const int sid = sorted_ids[row];
+    return sid < 0 ? -1 : (a_rows_are_slots ? row : sid / topk);
+  };
+  // DMA sources: a 1 KB piece = 16 rows x 64 B; wave w moves A pieces {2w, 2w+1}, B pieces {2w, 2w+1}
+  // and the activation scales of rows 32w + (lane & 31)
+  const int lr = lane >> 2, lp = lane & 3;
+  int aoff[2], boff[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int row = 16 * (2 * w + i) + lr;
+    const int tok = tok_of(m0 + row);
+    aoff[i] = (tok < 0 ? 0 : tok) * (int)x_stride + g3r_swz(row, lp) * 16;
+    boff[i] = min(n0 + row, N - 1) * K + g3r_swz(row, lp) * 16;  // tail columns: a valid row, never stored
+  }
+  const int stok = tok_of(m0 + 32 * w + l32);
+  const float* xsr = xs + (int64_t)(stok < 0 ? 0 : stok) * xs_stride;
+  const uint8_t* We = W + (int64_t)e * w_expert_stride;
+  auto issue = [&](int kt) {
+    char* st = lds + (kt & (G3_NS - 1)) * G3_STAGE;
+    const int k0 = kt * 64;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) g2_dma(X + aoff[i] + k0, st + (2 * w + i) * 1024);
+#pragma unroll
+    for (int i = 0; i < 2; ++i) g2_dma(We + boff[i] + k0, st + G3_A + (2 * w + i) * 1024);
+    g3_dma4(xsr + (kt >> 1), st + G3_A + G3_B + w * 256);
+  };
+  const float* wsr = ws + ((int64_t)e * nnb + (n0 + 64 * __builtin_amdgcn_readfirstlane(wn)) / 128) * nkb;
+  const int rb_live = min(4, max(0, (nvalid - 128 * wm + 31) / 32));  // live 32-row blocks of this wave
+  // fragment reads: lane (l32, h) takes row l32 of a 32-row block, bytes [32h, 32h+32) = chunks 2h, 2h+1;
+  // the swizzle key (row >> 2) & 3 is the same for every 32-row block
+  const int sw_lo = g3r_swz(l32, 2 * h) * 16, sw_hi = g3r_swz(l32, 2 * h + 1) * 16;
+  const int a_off = (128 * wm + l32) * 64, b_off = G3_A + (64 * wn + l32) * 64;
+  const int s_off = G3_A + G3_B + (128 * wm / 32) * 256 + l32 * 4;  // scale of row 128*wm + 32i + l32: + i*256
+  f32x16v_t acc[4][2];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = f32x16v_t{};
+  auto compute = [&](int kt) {
+    const char* st = lds + (kt & (G3_NS - 1)) * G3_STAGE;
+    const int we = e8m0_of(wsr[kt >> 1]);
+    i32x8_t bfr[2];
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const u32x4_t lo = *reinterpret_cast<const u32x4_t*>(st + b_off + j * 2048 + sw_lo);
+      const u32x4_t hi = *reinterpret_cast<const u32x4_t*>(st + b_off + j * 2048 + sw_hi);
+      bfr[j] = i32x8_t{(int)lo[0], (int)lo[1], (int)lo[2], (int)lo[3], (int)hi[0], (int)hi[1], (int)hi[2], (int)hi[3]};
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      if (i >= rb_live) break;  // wave-uniform: 32-row blocks past the expert's rows
+      const u32x4_t lo = *reinterpret_cast<const u32x4_t*>(st + a_off + i * 2048 + sw_lo);
+      const u32x4_t hi = *reinterpret_cast<const u32x4_t*>(st + a_off + i * 2048 + sw_hi);
+      const i32x8_t af =
+          i32x8_t{(int)lo[0], (int)lo[1], (int)lo[2], (int)lo[3], (int)hi[0], (int)hi[1], (int)hi[2], (int)hi[3]};
+      const int sa = e8m0_of(*reinterpret_cast<const float*>(st + s_off + i * 256));
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(af, bfr[j], acc[i][j], 0, 0, 0, sa, 0, we);
+      __builtin_amdgcn_sched_barrier(0);  // keep each block's fragment reads next to its MFMAs
+    }
+  };
+#pragma unroll
+  for (int s = 0; s < G3_NS - 1; ++s)
+    if (s < nk) issue(s);
+  for (int kt = 0; kt < nk; ++kt) {
+    // stage kt landed (this wave's DMAs; the barrier extends it to every wave's), and every
+    // wave is done reading the stage that issue(kt + 3) overwrites (it was read in step kt - 1)
+    if (kt + 2 < nk) asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
+    else if (kt + 1 < nk) asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (kt + G3_NS - 1 < nk) issue(kt + G3_NS - 1);
+    compute(kt);
+  }
+  // epilogue: acc[i][j][r] = C[row 128*wm + 32i + (r&3) + 8(r>>2) + 4h][col 64*wn + 32j + l32]
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    if (i >= rb_live) break;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int row = m0 + 128 * wm + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * h;
+      const bool live = sorted_ids[row] >= 0;
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int col = n0 + 64 * wn + 32 * j + l32;
+        float v = acc[i][j][r];
+        if (bias && col < N) v += bf2f(bias[(int64_t)e * N + col]);
+        if (MODE == 0) {
+          if (live && col < N) Y[(int64_t)row * y_stride + col] = f2bf(v);
+        } else {
+          const float other = __shfl_xor(v, 1, 64);
+          if (live && (l32 & 1) == 0) {
             float g = v, u = other, o;
             if (act == 2) {
               g = fminf(g, limit);
@@ -868,6 +1062,28 @@ void llmd_moe_gemm(const void* X, int64_t x_stride, int topk, const int* sorted_
                        limit, a_rows_are_slots, (const uint16_t*)bias);
 }
 
+int llmd_moe_gemm3_tile_m() { return G3_BM; }
+
+// 256-row expert tiles (sorted by moe_align with bm = 256): the v3 kernel.
+// Needs power-of-two scales, K % 128 == 0 and 16-B aligned rows.
+int llmd_moe_gemm3_fp8(const void* X, int64_t x_stride, const float* xs, int64_t xs_stride, int topk,
+                       const int* sorted_ids, const int* tile_expert, int num_tiles, const void* W,
+                       int64_t w_expert_stride, const float* ws, int N, int K, void* Y, int64_t y_stride, int mode,
+                       int act, float alpha, float limit, int a_rows_are_slots, const void* bias, hipStream_t st) {
+  if (K % 128 || x_stride % 16 || w_expert_stride % 16) return -1;
+  if (num_tiles == 0) return 0;
+  dim3 grid((N + G3_BN - 1) / G3_BN, num_tiles);
+  if (mode == 0)
+    hipLaunchKernelGGL(moe_gemm3_fp8_kernel<0>, grid, dim3(G3_NT), 0, st, (const uint8_t*)X, x_stride, xs, xs_stride,
+                       topk, sorted_ids, tile_expert, (const uint8_t*)W, w_expert_stride, ws, N, K, (uint16_t*)Y,
+                       y_stride, act, alpha, limit, a_rows_are_slots, (const uint16_t*)bias);
+  else
+    hipLaunchKernelGGL(moe_gemm3_fp8_kernel<1>, grid, dim3(G3_NT), 0, st, (const uint8_t*)X, x_stride, xs, xs_stride,
+                       topk, sorted_ids, tile_expert, (const uint8_t*)W, w_expert_stride, ws, N, K, (uint16_t*)Y,
+                       y_stride, act, alpha, limit, a_rows_are_slots, (const uint16_t*)bias);
+  return (int)hipGetLastError();
+}
+
 void llmd_moe_gemm_fp8(const void* X, int64_t x_stride, const float* xs, int64_t xs_stride, int topk,
                        const int* sorted_ids, const int* tile_expert, int num_tiles, const void* W,
                        int64_t w_expert_stride, const float* ws, int N, int K, void* Y, int64_t y_stride, int mode,
@@ -877,16 +1093,26 @@ void llmd_moe_gemm_fp8(const void* X, int64_t x_stride, const float* xs, int64_t
     const char* e = getenv("LLMD_MOE_GEMM_V1");
     return !(e && e[0] == '1');
   }();
+  // power-of-two scales (every quantiser of this code base) run on the MFMA's
+  // own E8M0 scales; LLMD_MOE_FP8_SOFT_SCALE=1 keeps the VALU block re-scaling
+  static const bool hws = [] {
+    const char* e = getenv("LLMD_MOE_FP8_SOFT_SCALE");
+    return !(e && e[0] == '1');
+  }();
   if (v2 && K % 128 == 0 && K / 128 <= G2_MAX_KB && x_stride % 16 == 0 && w_expert_stride % 16 == 0) {
     dim3 grid2((N + G2_BN - 1) / G2_BN, num_tiles);
-    if (mode == 0)
-      hipLaunchKernelGGL(moe_gemm2_fp8_kernel<0>, grid2, dim3(G2_NT), 0, st, (const uint8_t*)X, x_stride, xs,
-                         xs_stride, topk, sorted_ids, tile_expert, (const uint8_t*)W, w_expert_stride, ws, N, K,
-                         (uint16_t*)Y, y_stride, act, alpha, limit, a_rows_are_slots, (const uint16_t*)bias);
-    else
-      hipLaunchKernelGGL(moe_gemm2_fp8_kernel<1>, grid2, dim3(G2_NT), 0, st, (const uint8_t*)X, x_stride, xs,
-                         xs_stride, topk, sorted_ids, tile_expert, (const uint8_t*)W, w_expert_stride, ws, N, K,
-                         (uint16_t*)Y, y_stride, act, alpha, limit, a_rows_are_slots, (const uint16_t*)bias);
+#define LLMD_G2F8(M, H)                                                                                           \
+  hipLaunchKernelGGL((moe_gemm2_fp8_kernel<M, H>), grid2, dim3(G2_NT), 0, st, (const uint8_t*)X, x_stride, xs,     \
+                     xs_stride, topk, sorted_ids, tile_expert, (const uint8_t*)W, w_expert_stride, ws, N, K,       \
+                     (uint16_t*)Y, y_stride, act, alpha, limit, a_rows_are_slots, (const uint16_t*)bias)
+    if (mode == 0) {
+      if (hws) LLMD_G2F8(0, true);
+      else LLMD_G2F8(0, false);
+    } else {
+      if (hws) LLMD_G2F8(1, true);
+      else LLMD_G2F8(1, false);
+    }
+#undef LLMD_G2F8
     return;
   }
   dim3 grid((N + BN - 1) / BN, num_tiles);

@@ -70,7 +70,7 @@ __global__ __launch_bounds__(NT) void quant_fp8_groups_kernel(const uint16_t* __
     for (int i = 0; i < 8; ++i) a = fmaxf(a, fabsf(f[i]));
 #pragma unroll
     for (int o = 8; o > 0; o >>= 1) a = fmaxf(a, __shfl_xor(a, o, 64));
-    const float s = fmaxf(a / FP8_MAX, floor_);
+    const float s = pow2_ceil(fmaxf(a / FP8_MAX, floor_));  // E8M0-exact (moe_gemm2_fp8_kernel)
     if (ok && (c & 15) == 0) scale[t * ss + c / 16] = s;
     const float inv = 1.f / s;
 #pragma unroll

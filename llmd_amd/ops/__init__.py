@@ -285,14 +285,23 @@ def fp8_linear(x, wq: torch.Tensor, w_scale: torch.Tensor, bias=None) -> torch.T
     return y.reshape(*lead, -1)
 
 
+def pow2_ceil(r: torch.Tensor) -> torch.Tensor:
+    """Smallest power of two >= r (f32, r > 0): the block scales of the fp8 MoE
+    path are powers of two so the grouped GEMM passes them to the MFMA as E8M0
+    exponents (csrc/include/llmd_common.h pow2_ceil)."""
+    m, e = torch.frexp(r.float())
+    return torch.ldexp(torch.ones_like(m), e - (m == 0.5).to(e.dtype))
+
+
 def quant_fp8_groups(x: torch.Tensor, group: int = 128):
-    """Per (token, 128-group) fp8: x [T, d] -> (q [T, d] e4m3fn, scale [T, ceil(d/128)] f32)."""
+    """Per (token, 128-group) fp8: x [T, d] -> (q [T, d] e4m3fn, scale [T, ceil(d/128)] f32).
+    Scales are powers of two (E8M0-exact)."""
     T, d = x.shape
     ng = (d + group - 1) // group
     if not _gpu(x):
         pad = ng * group - d
         xf = torch.nn.functional.pad(x.float(), (0, pad)).view(T, ng, group)
-        s = (xf.abs().amax(2) / FP8_MAX).clamp(min=1e-12)
+        s = pow2_ceil((xf.abs().amax(2) / FP8_MAX).clamp(min=1e-12))
         q = (xf / s[:, :, None]).clamp(-FP8_MAX, FP8_MAX).view(T, ng * group)[:, :d].to(FP8)
         return q, s
     assert group == 128
@@ -304,12 +313,16 @@ def quant_fp8_groups(x: torch.Tensor, group: int = 128):
 
 
 def quant_fp8_block_weight(w: torch.Tensor, block: int = 128):
-    """Expert weights [E, N, K] -> (e4m3fn, scales [E, ceil(N/128), ceil(K/128)]) per 128x128 block."""
+    """Expert weights [E, N, K] -> (e4m3fn, scales [E, ceil(N/128), ceil(K/128)]) per 128x128 block.
+    Scales are powers of two: the grouped GEMM hands them to the MFMA as E8M0
+    exponents. (Every block-fp8 expert weight of this code base is made here,
+    at load and on a weight update; a checkpoint's arbitrary fp32 block scales
+    would be re-quantised through this function.)"""
     E, N, K = w.shape
     nb, kb = (N + block - 1) // block, (K + block - 1) // block
     wf = torch.nn.functional.pad(w.float(), (0, kb * block - K, 0, nb * block - N))
     wf = wf.view(E, nb, block, kb, block)
-    s = (wf.abs().amax(dim=(2, 4)) / FP8_MAX).clamp(min=1e-12)
+    s = pow2_ceil((wf.abs().amax(dim=(2, 4)) / FP8_MAX).clamp(min=1e-12))
     q = (wf / s[:, :, None, :, None]).clamp(-FP8_MAX, FP8_MAX)
     q = q.view(E, nb * block, kb * block)[:, :N, :K].contiguous().to(FP8)
     return q, s.contiguous()
@@ -345,6 +358,10 @@ def dequant_fp8_block_weight(q: torch.Tensor, s: torch.Tensor, block: int = 128)
     return q.float() * full
 
 
+MOE_V3_MIN_ROWS = int(os.environ.get("LLMD_MOE_V3_MIN_ROWS", "96"))
+MOE_V3 = os.environ.get("LLMD_MOE_V3", "1") == "1"
+
+
 def moe_experts_fp8(x, ids, wts, w1q, w1s, w2q, w2s, act=0, alpha=1.702, limit=7.0, out=None, b1=None, b2=None):
     """Block-scaled FP8 routed experts (DeepGEMM role): activations quantised per
     (token, 128) group, grouped fp8 MFMA GEMMs with 128x128 weight-block scales,
@@ -364,7 +381,11 @@ def moe_experts_fp8(x, ids, wts, w1q, w1s, w2q, w2s, act=0, alpha=1.702, limit=7
     E, N1, Kp1 = w1q.shape
     F = N1 // 2
     Kp2 = w2q.shape[2]
-    bm = C.moe_tile_m()
+    # prefill-sized steps (>= MOE_V3_MIN_ROWS rows per local expert on average):
+    # 256-row expert tiles, one weight pass per expert (moe_gemm3_fp8_kernel);
+    # decode-sized steps keep the 64-row weight-streaming kernel
+    bm = C.moe_tile_m_prefill() if (T * k >= MOE_V3_MIN_ROWS * E and Kp1 % 128 == 0 and Kp2 % 128 == 0
+                                    and MOE_V3) else C.moe_tile_m()
     n = T * k
     max_p = ((n + E * (bm - 1)) + bm - 1) // bm * bm
     dev = x.device
@@ -373,14 +394,14 @@ def moe_experts_fp8(x, ids, wts, w1q, w1s, w2q, w2s, act=0, alpha=1.702, limit=7
     offs = torch.empty(E + 1, dtype=torch.int32, device=dev)
     total = torch.empty(1, dtype=torch.int32, device=dev)
     inv = torch.empty(n, dtype=torch.int32, device=dev)  # moe_align fills it (-1 = not on this rank)
-    C.moe_align(ids.contiguous().view(-1).to(torch.int32), E, sorted_ids, tile_e, offs, total, inv)
+    C.moe_align(ids.contiguous().view(-1).to(torch.int32), E, sorted_ids, tile_e, offs, total, inv, bm)
     xq, xs = _quant_groups_padded(x, Kp1)
     h = torch.empty(max_p, F, dtype=torch.bfloat16, device=dev)
-    C.moe_gemm_fp8(xq, xs, k, sorted_ids, tile_e, w1q, w1s, h, 1, act, alpha, limit, False, b1)
+    C.moe_gemm_fp8(xq, xs, k, sorted_ids, tile_e, w1q, w1s, h, 1, act, alpha, limit, False, b1, bm)
     hq, hs = _quant_groups_padded(h, Kp2)
     y = torch.empty(max_p, d, dtype=torch.bfloat16, device=dev)
     # second GEMM: A rows are the sorted slots themselves (row p of hq; a_rows_are_slots)
-    C.moe_gemm_fp8(hq, hs, 1, sorted_ids, tile_e, w2q, w2s, y, 0, 0, 0.0, 0.0, True, b2)
+    C.moe_gemm_fp8(hq, hs, 1, sorted_ids, tile_e, w2q, w2s, y, 0, 0, 0.0, 0.0, True, b2, bm)
     if out is None:
         out = torch.empty(T, d, dtype=torch.bfloat16, device=dev)
     C.moe_combine(y, inv, wts.contiguous().view(-1).float(), k, out)

@@ -239,6 +239,42 @@ def test_moe_experts_fp8_gpu(T, E, k, d, F, act):
         assert errp < 0.06 * r.float().abs().max().item() + 1e-3, errp
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("T,E,k,d,F,act,skew", [(512, 4, 4, 1024, 1024, 2, False), (600, 16, 8, 1024, 256, 0, True),
+                                                (700, 64, 4, 384, 256, 2, True), (5, 8, 2, 256, 128, 0, False)])
+def test_moe_fp8_prefill_tiles_gpu(T, E, k, d, F, act, skew, monkeypatch):
+    """256-row expert tiles (moe_gemm3_fp8_kernel, E8M0 hardware scales) vs the
+    64-row kernel and the CPU reference, incl. experts with no rows, partial
+    tiles (valid-row prefix) and multi-tile experts."""
+    torch.manual_seed(1)
+    dev = "cuda"
+    c128 = lambda n: (n + 127) // 128 * 128  # noqa: E731
+    x = torch.randn(T, d, device=dev, dtype=torch.bfloat16)
+    w1 = torch.randn(E, 2 * F, d, device=dev, dtype=torch.bfloat16) * 0.03
+    w2 = torch.randn(E, d, F, device=dev, dtype=torch.bfloat16) * 0.03
+    b1 = torch.randn(E, 2 * F, device=dev, dtype=torch.bfloat16) * 0.1
+    w1q, w1s = ops.quant_fp8_block_weight(w1)
+    w2q, w2s = ops.quant_fp8_block_weight(w2)
+    assert torch.equal(ops.pow2_ceil(w1s), w1s)  # E8M0-exact block scales
+    w1q, w2q = ops.pad_fp8_k(w1q, c128(d)), ops.pad_fp8_k(w2q, c128(F))
+    logits = torch.randn(T, E, device=dev)
+    if skew:  # a quarter of the experts take most tokens, the last ones (almost) none
+        logits[:, : E // 4] += 2.0
+        logits[:, -2:] -= 8.0
+    ids, wts = ops.moe_topk(logits, k, scoring=0)
+    monkeypatch.setattr(ops, "MOE_V3", True)
+    monkeypatch.setattr(ops, "MOE_V3_MIN_ROWS", 0)
+    y3 = ops.moe_experts_fp8(x, ids, wts, w1q, w1s, w2q, w2s, act, b1=b1)
+    monkeypatch.setattr(ops, "MOE_V3", False)
+    y2 = ops.moe_experts_fp8(x, ids, wts, w1q, w1s, w2q, w2s, act, b1=b1)
+    r = ops.moe_experts_fp8(x.cpu(), ids.cpu(), wts.cpu(), w1q.cpu()[..., :d], w1s.cpu(), w2q.cpu()[..., :F],
+                            w2s.cpu(), act, b1=b1.cpu())
+    m = r.float().abs().max().item()
+    assert torch.isfinite(y3).all()
+    assert (y3.float().cpu() - r.float()).abs().max().item() < 0.06 * m + 1e-3
+    assert (y3.float() - y2.float()).abs().max().item() < 0.02 * m + 1e-3
+
+
 def test_fused_norm_act_quant_cpu_matches_unfused():
     torch.manual_seed(0)
     x = torch.randn(6, 256).to(torch.bfloat16)
