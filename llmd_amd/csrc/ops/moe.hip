@@ -896,18 +896,21 @@ __global__ __launch_bounds__(G3_NT, 1) void moe_gemm3_fp8_kernel(
     g3_dma4(xsr + (kt >> 1), st + G3_A + G3_B + w * 256);
   };
   const float* wsr = ws + ((int64_t)e * nnb + (n0 + 64 * __builtin_amdgcn_readfirstlane(wn)) / 128) * nkb;
-  const int rb_live = min(4, max(0, (nvalid - 128 * wm + 31) / 32));  // live 32-row blocks of this wave
+  // wave wm owns the 32-row blocks {wm, wm + 2, wm + 4, wm + 6} (interleaved: an expert with
+  // ~160 rows gives the two halves 3 and 2 blocks, not 4 and 1); live = blocks before nvalid
+  const int nblk = (nvalid + 31) / 32;
+  const int rb_live = min(4, max(0, (nblk - wm + 1) / 2));
   // fragment reads: lane (l32, h) takes row l32 of a 32-row block, bytes [32h, 32h+32) = chunks 2h, 2h+1;
   // the swizzle key (row >> 2) & 3 is the same for every 32-row block
   const int sw_lo = g3r_swz(l32, 2 * h) * 16, sw_hi = g3r_swz(l32, 2 * h + 1) * 16;
-  const int a_off = (128 * wm + l32) * 64, b_off = G3_A + (64 * wn + l32) * 64;
-  const int s_off = G3_A + G3_B + (128 * wm / 32) * 256 + l32 * 4;  // scale of row 128*wm + 32i + l32: + i*256
+  const int a_off = (32 * wm + l32) * 64, b_off = G3_A + (64 * wn + l32) * 64;  // block i: + i * 4096
+  const int s_off = G3_A + G3_B + wm * 256 + l32 * 4;  // scale of row 32*(wm + 2i) + l32: + i * 512
   f32x16v_t acc[4][2];
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
     for (int j = 0; j < 2; ++j) acc[i][j] = f32x16v_t{};
-  auto compute = [&](int kt) {
+  auto compute = [&](int kt, bool refill) {
     const char* st = lds + (kt & (G3_NS - 1)) * G3_STAGE;
     const int we = e8m0_of(wsr[kt >> 1]);
     i32x8_t bfr[2];
@@ -920,16 +923,19 @@ __global__ __launch_bounds__(G3_NT, 1) void moe_gemm3_fp8_kernel(
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       if (i >= rb_live) break;  // wave-uniform: 32-row blocks past the expert's rows
-      const u32x4_t lo = *reinterpret_cast<const u32x4_t*>(st + a_off + i * 2048 + sw_lo);
-      const u32x4_t hi = *reinterpret_cast<const u32x4_t*>(st + a_off + i * 2048 + sw_hi);
+      const u32x4_t lo = *reinterpret_cast<const u32x4_t*>(st + a_off + i * 4096 + sw_lo);
+      const u32x4_t hi = *reinterpret_cast<const u32x4_t*>(st + a_off + i * 4096 + sw_hi);
       const i32x8_t af =
           i32x8_t{(int)lo[0], (int)lo[1], (int)lo[2], (int)lo[3], (int)hi[0], (int)hi[1], (int)hi[2], (int)hi[3]};
-      const int sa = e8m0_of(*reinterpret_cast<const float*>(st + s_off + i * 256));
+      const int sa = e8m0_of(*reinterpret_cast<const float*>(st + s_off + i * 512));
 #pragma unroll
       for (int j = 0; j < 2; ++j)
         acc[i][j] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(af, bfr[j], acc[i][j], 0, 0, 0, sa, 0, we);
       __builtin_amdgcn_sched_barrier(0);  // keep each block's fragment reads next to its MFMAs
+      // the next stage's DMA issues behind the first block's MFMAs (they start the matrix pipe at once)
+      if (i == 0 && refill) issue(kt + G3_NS - 1);
     }
+    if (rb_live == 0 && refill) issue(kt + G3_NS - 1);
   };
 #pragma unroll
   for (int s = 0; s < G3_NS - 1; ++s)
@@ -942,16 +948,15 @@ __global__ __launch_bounds__(G3_NT, 1) void moe_gemm3_fp8_kernel(
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
-    if (kt + G3_NS - 1 < nk) issue(kt + G3_NS - 1);
-    compute(kt);
+    compute(kt, kt + G3_NS - 1 < nk);
   }
-  // epilogue: acc[i][j][r] = C[row 128*wm + 32i + (r&3) + 8(r>>2) + 4h][col 64*wn + 32j + l32]
+  // epilogue: acc[i][j][r] = C[row 32*(wm + 2i) + (r&3) + 8(r>>2) + 4h][col 64*wn + 32j + l32]
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     if (i >= rb_live) break;
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
-      const int row = m0 + 128 * wm + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * h;
+      const int row = m0 + 32 * (wm + 2 * i) + (r & 3) + 8 * (r >> 2) + 4 * h;
       const bool live = sorted_ids[row] >= 0;
 #pragma unroll
       for (int j = 0; j < 2; ++j) {

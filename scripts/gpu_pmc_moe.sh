@@ -1,4 +1,4 @@
-# PMC counters of the block-fp8 grouped GEMM (moe_gemm2_fp8_kernel) at gpt-oss-120b and DeepSeek EP8 prefill shapes.
+# PMC counters of the block-fp8 grouped GEMM (moe_gemm3_fp8_kernel) at gpt-oss-120b and DeepSeek EP8 prefill shapes.
 set -o pipefail
 mkdir -p gpurun_out
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
@@ -16,7 +16,7 @@ for f in sorted(glob.glob("gpurun_out/pmc_moe/*counter_collection.csv")):
     n = collections.defaultdict(collections.Counter)
     for r in csv.DictReader(open(f)):
         kn = r.get("Kernel_Name", "")
-        if "moe_gemm2_fp8" not in kn:
+        if "moe_gemm3_fp8" not in kn:
             continue
         tag = "gemm1(act)" if "ILi1E" in kn else "gemm2"
         agg[tag][r["Counter_Name"]] += float(r["Counter_Value"])
