@@ -66,6 +66,12 @@ class LLMEngine:
 
         ep.set_backend(cfg.parallel.all2all_backend)
         self.dp_lockstep = ep.ep_active() and self.runner.mc.is_moe
+        if self.dp_lockstep:
+            from llmd_amd.parallel.state import get_state
+
+            st = get_state()
+            log.info("wide-EP: DP rank %d/%d, experts sharded over %d EP ranks (%s), lockstep steps",
+                     st.dp_rank, st.dp_size, st.ep_size, ep.backend())
         self.last_global_idle = False
         self.lora = None
         if cfg.enable_lora:

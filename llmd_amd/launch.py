@@ -16,7 +16,10 @@ A topology YAML names the model, the router and the engine roles::
     - name: prefill            # llm-d.ai/role label: prefill | decode | prefill-decode
       replicas: 6
       tp: 1                    # GPUs per replica (torchrun ranks for tp > 1)
-      port: 8200               # engine port of replica 0 (+1 per replica)
+      dp: 1                    # data-parallel ranks per replica (wide-EP: DP attention +
+                               # --enable-expert-parallel); rank r serves port + r and
+                               # is its own router endpoint (multi-port external LB)
+      port: 8200               # engine port of replica 0 (+ tp x dp ... see below)
       args: ["--max-num-batched-tokens", "8192"]
       kv_transfer: true        # kvx producer/consumer by role
     - name: decode
@@ -24,6 +27,14 @@ A topology YAML names the model, the router and the engine roles::
       tp: 1
       port: 8300
       sidecar_port: 8400       # routing sidecar in front of each decode engine
+
+  services:                    # router-side services of the well-lit paths
+    - {type: predictor, port: 8100}        # latency predictor (training + prediction);
+                                           # the router gets PREDICTION_SERVER_URL
+    - {type: render, port: 8300}           # tokenizer / render sidecar (token-producer)
+    - {type: batch-gateway, port: 8081}    # OpenAI Batch API -> router
+    - {type: async-processor}              # queue-driven async dispatch -> router
+    - {type: wva, port: 8080, config: {...}}   # workload variant autoscaler controller
 
 Every replica gets a disjoint GPU set (``HIP_VISIBLE_DEVICES``; TP replicas
 are packed onto neighbouring GPUs so TP traffic stays on direct xGMI links),
@@ -59,6 +70,7 @@ class ProcSpec:
     gpus: list[int] = field(default_factory=list)
     port: Optional[int] = None
     role: str = ""
+    health: str = "/health"  # readiness path polled by wait_ready
 
 
 def _kv_transfer(role: str) -> str:
@@ -75,27 +87,31 @@ def plan(topo: dict, workdir: str) -> tuple[list[ProcSpec], dict]:
     procs: list[ProcSpec] = []
     endpoints = []
     master_port = int(topo.get("master_port_base", 29600))
+    ev_next = 0  # KV-event ports handed out so far (one per engine process / DP rank)
     for role in topo.get("roles", []):
-        name, tp = role["name"], int(role.get("tp", 1))
+        name, tp, dp = role["name"], int(role.get("tp", 1)), int(role.get("dp", 1))
+        ranks = tp * dp
         for i in range(int(role.get("replicas", 1))):
             if cpu:
                 gpus = []
-            elif len(free) < tp:
-                raise ValueError(f"not enough GPUs for {name} replica {i} (tp={tp}, free={free})")
+            elif len(free) < ranks:
+                raise ValueError(f"not enough GPUs for {name} replica {i} (tp={tp}, dp={dp}, free={free})")
             else:
-                gpus, free = free[:tp], free[tp:]
-            port = int(role.get("port", 8200)) + i
+                gpus, free = free[:ranks], free[ranks:]
+            port = int(role.get("port", 8200)) + i * dp  # DP rank r of the replica serves port + r
             args = ["--model", model, "--port", str(port), "--tensor-parallel-size", str(tp)] + \
+                (["--data-parallel-size", str(dp)] if dp > 1 else []) + \
                 (["--device", "cpu"] if cpu else []) + [str(x) for x in role.get("args", [])]
             if role.get("kv_transfer", name in ("prefill", "decode")):
                 args += ["--kv-transfer-config", _kv_transfer(name)]
+            ev_port = int(role.get("kv_events_port", 5556)) + ev_next  # DP rank r publishes on ev_port + r
             if role.get("kv_events", False):
                 args += ["--kv-events-config", json.dumps(
-                    {"enable_kv_cache_events": True, "publisher": "zmq",
-                     "endpoint": f"tcp://*:{int(role.get('kv_events_port', 5556)) + len(procs)}"})]
+                    {"enable_kv_cache_events": True, "publisher": "zmq", "endpoint": f"tcp://*:{ev_port}"})]
+                ev_next += dp
             server = ["-m", "llmd_amd.serving.api_server"] + args
-            if tp > 1:
-                cmd = [PY, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={tp}",
+            if ranks > 1:
+                cmd = [PY, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={ranks}",
                        "--master-addr=127.0.0.1", f"--master-port={master_port}"] + server
                 master_port += 1
             else:
@@ -114,12 +130,25 @@ def plan(topo: dict, workdir: str) -> tuple[list[ProcSpec], dict]:
                                       {}, [], front, "sidecar"))
             labels = {"llm-d.ai/role": name if name in ("prefill", "decode", "encode") else "prefill-decode",
                       "llm-d.ai/model": model}
-            if role.get("kv_events", False):
-                labels["llm-d.ai/kv-events-port"] = str(int(role.get("kv_events_port", 5556)) + len(procs) - 1)
-            endpoints.append({"name": rid, "address": "127.0.0.1", "port": front, "labels": labels,
-                              "metricsPort": port})
+            for r in range(dp):  # one router endpoint per DP rank
+                lab = dict(labels)
+                if role.get("kv_events", False):
+                    lab["llm-d.ai/kv-events-port"] = str(ev_port + r)
+                ep_name = rid if dp == 1 else f"{rid}-dp{r}"
+                endpoints.append({"name": ep_name, "address": "127.0.0.1", "port": front + r, "labels": lab,
+                                  "metricsPort": port + r})
+                if r:
+                    procs.append(ProcSpec(ep_name, [], {}, [], port + r, name + "-dp-rank"))
     doc = {"endpoints": endpoints}
     r = topo.get("router")
+    router_env: dict[str, str] = {}
+    rport_http = int((r or {}).get("port", 8000))
+    for svc in topo.get("services", []) or []:
+        spec = _service(svc, model, workdir, rport_http)
+        procs.append(spec)
+        if svc["type"] == "predictor":
+            router_env["PREDICTION_SERVER_URL"] = f"http://127.0.0.1:{spec.port}"
+            router_env["TRAINING_SERVER_URL"] = f"http://127.0.0.1:{spec.port}"
     if r:
         ep_file = os.path.join(workdir, "endpoints.yaml")
         if r.get("mode", "proxy") == "extproc":
@@ -136,8 +165,50 @@ def plan(topo: dict, workdir: str) -> tuple[list[ProcSpec], dict]:
             else:
                 cmd += ["--config-text", conf if isinstance(conf, str) else yaml.safe_dump(conf)]
         rport = int(r.get("grpc_port", 9002)) if r.get("mode") == "extproc" else int(r.get("port", 8000))
-        procs.append(ProcSpec("router", cmd, {}, [], rport, "router"))
+        procs.append(ProcSpec("router", cmd, router_env, [], rport, "router"))
     return procs, doc
+
+
+SERVICES = {"predictor": "llmd_amd.router.predictor", "render": "llmd_amd.serving.render_server",
+            "batch-gateway": "llmd_amd.batch.gateway", "async-processor": "llmd_amd.batch.async_processor",
+            "wva": "llmd_amd.autoscale.controller"}
+
+
+def _service(svc: dict, model: str, workdir: str, router_port: int) -> ProcSpec:
+    """Router-side service of a well-lit path as a process spec."""
+    t = svc["type"]
+    if t not in SERVICES:
+        raise ValueError(f"unknown service type {t!r}; known: {sorted(SERVICES)}")
+    port = svc.get("port")
+    cmd = [PY, "-m", SERVICES[t]]
+    gw = f"http://127.0.0.1:{router_port}"
+    if t == "predictor":
+        port = int(port or 8100)
+        cmd += ["--port", str(port), "--role", svc.get("role", "combined")]
+        if svc.get("model_path"):
+            cmd += ["--model-path", str(svc["model_path"])]
+    elif t == "render":
+        port = int(port or 8300)
+        cmd += ["--port", str(port), "--model", model]
+    elif t == "batch-gateway":
+        port = int(port or 8081)
+        cmd += ["--port", str(port), "--gateway-url", gw, "--root", svc.get("root", os.path.join(workdir, "batch"))]
+    elif t == "async-processor":
+        port = None
+        cmd += ["--igw-base-url", gw, "--db", svc.get("db", os.path.join(workdir, "async-mq.db"))]
+    elif t == "wva":
+        port = int(port or 8080)
+        conf = dict(svc.get("config") or {})
+        conf.setdefault("endpointsFile", os.path.join(workdir, "endpoints.yaml"))
+        conf.setdefault("eppMetricsUrl", f"{gw}/metrics")
+        path = os.path.join(workdir, "wva-config.yaml")
+        if workdir and not workdir.startswith("<") and os.path.isdir(workdir):
+            with open(path, "w") as f:
+                yaml.safe_dump(conf, f)
+        cmd += ["--config", path, "--metrics-bind-address", f":{port}"]
+    cmd += [str(a) for a in svc.get("args", [])]
+    health = {"predictor": "/healthz", "batch-gateway": "/v1/batches", "wva": "/metrics"}.get(t, "/health")
+    return ProcSpec(svc.get("name", t), cmd, dict(svc.get("env") or {}), [], port, "service", health)
 
 
 class Launcher:
@@ -152,6 +223,8 @@ class Launcher:
         with open(os.path.join(self.workdir, "endpoints.yaml"), "w") as f:
             yaml.safe_dump(self.endpoints, f)
         for s in self.specs:
+            if not s.cmd:  # a DP rank > 0: served by its replica's torchrun group (started above)
+                continue
             env = dict(os.environ, **s.env)
             log = open(os.path.join(self.log_dir, f"{s.name}.log"), "w")
             p = subprocess.Popen(s.cmd, env=env, stdout=log, stderr=subprocess.STDOUT, start_new_session=True)
@@ -162,11 +235,11 @@ class Launcher:
         import urllib.request
 
         t0 = time.time()
-        pending = [s for s, _ in self.procs if s.port and s.role != "router"]
+        pending = [s for s in self.specs if s.port and s.role != "router"]
         while pending and time.time() - t0 < timeout:
             for s in list(pending):
                 try:
-                    with urllib.request.urlopen(f"http://127.0.0.1:{s.port}/health", timeout=2) as r:
+                    with urllib.request.urlopen(f"http://127.0.0.1:{s.port}{s.health}", timeout=2) as r:
                         if r.status == 200:
                             pending.remove(s)
                 except OSError:
@@ -205,7 +278,7 @@ def main(argv=None):
         specs, doc = plan(topo, "<workdir>")
         for s in specs:
             print(f"{s.name:18} gpus={s.gpus} port={s.port} env={s.env.get('HIP_VISIBLE_DEVICES', '')}\n"
-                  f"    {' '.join(s.cmd)}")
+                  f"    {' '.join(s.cmd) or '(DP rank of the replica above)'}")
         print(yaml.safe_dump(doc))
         return
     la = Launcher(topo, log_dir=a.log_dir).start()

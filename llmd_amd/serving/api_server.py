@@ -682,12 +682,19 @@ def main(argv=None):
     a = p.parse_args(argv)
     logging.basicConfig(level=a.log_level.upper(), format="%(asctime)s %(levelname)s %(name)s: %(message)s")
     cfg = engine_config_from_args(a)
-    if cfg.parallel.tensor_parallel_size > 1:
-        # one process per GPU under torchrun; TP rank 0 serves, the others follow
+    port = a.port
+    pc = cfg.parallel
+    if pc.tensor_parallel_size > 1 or pc.data_parallel_size > 1:
+        # one process per GPU under torchrun (WORLD_SIZE = tp x dp); TP rank 0 of
+        # each DP group serves, the others follow
         from llmd_amd.parallel.state import init_distributed
 
-        st = init_distributed(tp_size=cfg.parallel.tensor_parallel_size,
-                              backend=None if cfg.device == "cuda" else "gloo")
+        st = init_distributed(tp_size=pc.tensor_parallel_size, backend=None if cfg.device == "cuda" else "gloo")
+        if st.dp_size != pc.data_parallel_size:
+            raise SystemExit(f"WORLD_SIZE {st.world_size} != --tensor-parallel-size {pc.tensor_parallel_size} x "
+                             f"--data-parallel-size {pc.data_parallel_size}")
+        if pc.data_parallel_size > 1:
+            port = dp_rank_port(cfg, a.port, st.dp_rank)
         if st.tp_rank != 0:
             from llmd_amd.engine.tp_worker import run_follower
 
@@ -706,8 +713,24 @@ def main(argv=None):
     app.on_shutdown.append(on_shutdown)
     # keep-alive must exceed the sidecar's 90 s idle timeout (VLLM_HTTP_TIMEOUT_KEEP_ALIVE=120)
     keepalive = float(os.environ.get("VLLM_HTTP_TIMEOUT_KEEP_ALIVE", "120"))
-    web.run_app(app, host=a.host, port=a.port, keepalive_timeout=keepalive, access_log=None,
+    web.run_app(app, host=a.host, port=port, keepalive_timeout=keepalive, access_log=None,
                 shutdown_timeout=max(a.shutdown_timeout, 1.0))
+
+
+def dp_rank_port(cfg: EngineConfig, base_port: int, dp_rank: int) -> int:
+    """Data parallelism with an external load balancer (the reference's
+    multi-port DP-aware wide-EP: every DP rank is its own router endpoint,
+    guides/wide-ep-lws/experimental-dp-aware/README.md:1-29, router targetPorts
+    8000-8007): DP rank r serves the OpenAI API on ``base_port + r`` and
+    publishes KV events on its own port (endpoint port + r). Wide-EP ranks
+    (MoE + --enable-expert-parallel) step in lockstep (engine/engine.py)."""
+    cfg.parallel.data_parallel_rank = dp_rank
+    kc = cfg.kv_events_config
+    if kc and kc.get("endpoint"):
+        head, _, tail = kc["endpoint"].rpartition(":")
+        if tail.isdigit():
+            cfg.kv_events_config = dict(kc, endpoint=f"{head}:{int(tail) + dp_rank}")
+    return base_port + dp_rank
 
 
 if __name__ == "__main__":

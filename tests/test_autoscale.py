@@ -118,3 +118,92 @@ def test_process_actuator(tmp_path):
     act.scale(v, 1)
     assert v.current == 1 and act.free == [1, 2]
     act.shutdown()
+
+
+def test_wva_controller_scales_sim_replicas(tmp_path):
+    """The single-node WVA controller (autoscale/controller.py) closes the loop
+    the reference leaves to HPA: VariantAutoscaling objects + launch recipes ->
+    scrape replica /metrics -> saturation analyzer -> cost-aware optimizer ->
+    process actuation -> router endpoints file; here with simulator replicas
+    (llmd_amd/sim) as the engines: a queue builds on one replica -> scale to 2
+    (both in endpoints.yaml, wva_desired_replicas = 2); the load ends -> back
+    to minReplicas."""
+    import json
+    import socket
+    import sys
+    import threading
+    import time
+    import urllib.request
+
+    import yaml
+
+    from llmd_amd.autoscale.controller import WVAController
+
+    def free_port():
+        with socket.socket() as s:
+            s.bind(("127.0.0.1", 0))
+            return s.getsockname()[1]
+
+    base = free_port()
+    while True:  # two consecutive free ports
+        try:
+            with socket.socket() as s:
+                s.bind(("127.0.0.1", base + 1))
+            break
+        except OSError:
+            base = free_port()
+    ep_file = str(tmp_path / "endpoints.yaml")
+    cfg = {"interval": "0.5s", "gpus": 8, "endpointsFile": ep_file,
+           "scalingConfig": {"kvCacheThreshold": 0.8, "queueLengthThreshold": 5, "kvSpareTrigger": 0.1,
+                             "queueSpareTrigger": 3},
+           "variantAutoscalings": [{
+               "apiVersion": "llmd.ai/v1alpha1", "kind": "VariantAutoscaling", "metadata": {"name": "sim-tp1"},
+               "spec": {"modelID": "sim-model", "minReplicas": 1, "maxReplicas": 2, "variantCost": "5.0",
+                        "scaleTargetRef": {"kind": "EngineGroup", "name": "sim-tp1"}},
+               "launch": {"cpu": True, "portBase": base}}]}
+
+    def sim_cmd(v, ln, port):
+        return [sys.executable, "-m", "llmd_amd.sim.server", "--port", str(port), "--max-num-seqs", "2",
+                "--decode-step-ms", "40", "--model", "sim-model"]
+
+    ctl = WVAController(cfg, launch_cmd=sim_cmd)
+
+    def wait_for(pred, t=60):
+        t0 = time.time()
+        while time.time() - t0 < t:
+            if pred():
+                return True
+            time.sleep(0.2)
+        return False
+
+    def n_endpoints():
+        try:
+            return len(yaml.safe_load(open(ep_file))["endpoints"])
+        except (OSError, TypeError, KeyError):
+            return -1
+
+    ctl.start()
+    try:
+        v = ctl.variants["sim-tp1"]
+        assert v.current == 1
+        assert wait_for(lambda: n_endpoints() == 1), "replica 0 never became ready"
+
+        def req():
+            body = json.dumps({"model": "sim-model", "prompt": "hello " * 30, "max_tokens": 120}).encode()
+            r = urllib.request.Request(f"http://127.0.0.1:{base}/v1/completions", data=body,
+                                       headers={"content-type": "application/json"})
+            urllib.request.urlopen(r, timeout=120).read()
+
+        load = [threading.Thread(target=req, daemon=True) for _ in range(10)]
+        for t in load:
+            t.start()
+        assert wait_for(lambda: v.current == 2, 30), ctl.render_metrics()
+        assert wait_for(lambda: n_endpoints() == 2, 30)
+        assert 'wva_desired_replicas{variant_name="sim-tp1",exported_namespace="default",model_id="sim-model"} 2' \
+            in ctl.render_metrics()
+        for t in load:
+            t.join(timeout=120)
+        assert wait_for(lambda: v.current == 1, 60), ctl.render_metrics()
+        assert wait_for(lambda: n_endpoints() == 1, 10)
+    finally:
+        ctl.stop()
