@@ -77,7 +77,7 @@ void llmd_moe_gemm_fp8(const void*, int64_t, const float*, int64_t, int, const i
                        hipStream_t);
 int llmd_moe_gemm3_fp8(const void*, int64_t, const float*, int64_t, int, const int*, const int*, int, const void*,
                        int64_t, const float*, int, int, void*, int64_t, int, int, float, float, int, const void*,
-                       hipStream_t);
+                       void*, int64_t, float*, int64_t, hipStream_t);
 int llmd_moe_gemm3_tile_m();
 int llmd_symm_alloc(size_t, void**);
 int llmd_symm_free(void*);
@@ -675,7 +675,8 @@ void quant_fp8_groups(torch::Tensor x, torch::Tensor q, torch::Tensor scale) {
 
 void moe_gemm_fp8(torch::Tensor X, torch::Tensor xs, int64_t topk, torch::Tensor sorted_ids, torch::Tensor tile_expert,
                   torch::Tensor W, torch::Tensor ws, torch::Tensor Y, int64_t mode, int64_t act, double alpha,
-                  double limit, bool a_rows_are_slots, c10::optional<torch::Tensor> bias, int64_t tile_m) {
+                  double limit, bool a_rows_are_slots, c10::optional<torch::Tensor> bias, int64_t tile_m,
+                  c10::optional<torch::Tensor> hq, c10::optional<torch::Tensor> hs) {
   const c10::hip::OptionalHIPGuard device_guard(dev_of(X));
   CHECK_CUDA(X); CHECK_DT(X, at::kFloat8_e4m3fn); CHECK_DT(W, at::kFloat8_e4m3fn); CHECK_BF16(Y);
   CHECK_INNER(X); CHECK_INNER(Y); CHECK_DT(xs, at::kFloat); CHECK_DT(ws, at::kFloat);
@@ -690,20 +691,37 @@ void moe_gemm_fp8(torch::Tensor X, torch::Tensor xs, int64_t topk, torch::Tensor
   TORCH_CHECK(tile_m <= 0 || tile_m == llmd_moe_gemm_tile_m() || v3, "moe_gemm_fp8: tile_m");
   const int bm = v3 ? (int)tile_m : llmd_moe_gemm_tile_m();
   const int P = sorted_ids.numel();
-  TORCH_CHECK(P % bm == 0 && tile_expert.numel() >= P / bm && Y.size(0) >= P, "moe_gemm_fp8: rows");
-  TORCH_CHECK(Y.size(1) >= (mode == 1 ? N / 2 : N) && N % 2 == 0, "moe_gemm_fp8: Y width");
+  const bool fused = hq.has_value();  // the output is hq / hs; Y is unused
+  TORCH_CHECK(P % bm == 0 && tile_expert.numel() >= P / bm && (fused || Y.size(0) >= P), "moe_gemm_fp8: rows");
+  TORCH_CHECK((fused || Y.size(1) >= (mode == 1 ? N / 2 : N)) && N % 2 == 0, "moe_gemm_fp8: Y width");
   const void* bp = nullptr;
   if (bias.has_value()) {
     CHECK_BF16(bias.value());
     TORCH_CHECK(bias->is_contiguous() && bias->numel() == (int64_t)E * N, "bias [E, N]");
     bp = bias->data_ptr();
   }
+  void* hqp = nullptr;
+  float* hsp = nullptr;
+  int64_t hq_stride = 0, hs_stride = 0;
+  if (hq.has_value()) {  // fused activation quantisation (256-row tiles, mode 1)
+    TORCH_CHECK(v3 && mode == 1 && hs.has_value(), "fused quant: 256-row tiles, gated activation, hq + hs");
+    CHECK_DT(hq.value(), at::kFloat8_e4m3fn); CHECK_INNER(hq.value()); CHECK_DT(hs.value(), at::kFloat);
+    TORCH_CHECK(hq->size(0) >= P && hq->size(1) >= ((N / 2 + 127) / 128) * 128 && hq->size(1) % 128 == 0,
+                "hq [rows, F rounded up to 128]");
+    TORCH_CHECK(hs->dim() == 2 && hs->size(0) >= P && hs->size(1) >= (N + 255) / 256 && hs->stride(1) == 1,
+                "hs [rows, F / 128]");
+    hqp = hq->data_ptr();
+    hsp = hs->data_ptr<float>();
+    hq_stride = hq->stride(0);
+    hs_stride = hs->stride(0);
+  }
   if (v3) {  // 256-row expert tiles: power-of-two scales, K % 128 == 0, 16-B rows
     TORCH_CHECK(K % 128 == 0 && X.stride(0) % 16 == 0 && W.stride(0) % 16 == 0, "moe_gemm_fp8 (256-row tiles): K");
     const int rc = llmd_moe_gemm3_fp8(X.data_ptr(), X.stride(0), xs.data_ptr<float>(), xs.stride(0), topk,
                                       sorted_ids.data_ptr<int>(), tile_expert.data_ptr<int>(), P / bm, W.data_ptr(),
-                                      W.stride(0), ws.data_ptr<float>(), N, K, Y.data_ptr(), Y.stride(0), mode, act,
-                                      (float)alpha, (float)limit, a_rows_are_slots ? 1 : 0, bp, cur_stream());
+                                      W.stride(0), ws.data_ptr<float>(), N, K, fused ? nullptr : Y.data_ptr(),
+                                      fused ? 0 : Y.stride(0), mode, act, (float)alpha, (float)limit,
+                                      a_rows_are_slots ? 1 : 0, bp, hqp, hq_stride, hsp, hs_stride, cur_stream());
     TORCH_CHECK(rc == 0, "moe_gemm3_fp8 failed: ", rc);
     return;
   }
@@ -828,7 +846,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {  // _C, or _C_debug (llmd_amd/build.p
   m.def("gated_act_quant", &gated_act_quant);
   m.def("moe_gemm_fp8", &moe_gemm_fp8, py::arg("X"), py::arg("xs"), py::arg("topk"), py::arg("sorted_ids"),
         py::arg("tile_expert"), py::arg("W"), py::arg("ws"), py::arg("Y"), py::arg("mode"), py::arg("act"),
-        py::arg("alpha"), py::arg("limit"), py::arg("a_rows_are_slots"), py::arg("bias"), py::arg("tile_m") = 0);
+        py::arg("alpha"), py::arg("limit"), py::arg("a_rows_are_slots"), py::arg("bias"), py::arg("tile_m") = 0,
+        py::arg("hq") = py::none(), py::arg("hs") = py::none());
   m.def("moe_tile_m_prefill", &llmd_moe_gemm3_tile_m);
   m.def("symm_alloc", &symm_alloc);
   m.def("symm_error", &symm_error);

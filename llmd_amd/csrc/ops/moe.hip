@@ -846,12 +846,20 @@ __device__ __forceinline__ void g3_dma4(const void* src, char* lds_base) {
                                    (void __attribute__((address_space(3)))*)lds_base, 4, 0, 0);
 }
 
-template <int MODE>
+// FQ (MODE 1 only): the gated activation's output is quantised in the epilogue
+// straight to the second GEMM's fp8 operand - one workgroup's 256 gate/up
+// columns are exactly one 128-column activation-scale group, so the row amax
+// needs only the four N-waves' partials (exchanged through the then idle LDS
+// ring) - instead of a bf16 h round trip through HBM and a quant_fp8_groups
+// pass over every padded row. Same numerics as that pass: the bf16-rounded
+// value, power-of-two scale pow2_ceil(max(amax / 448, 1e-12)), saturating e4m3.
+template <int MODE, bool FQ>
 __global__ __launch_bounds__(G3_NT, 1) void moe_gemm3_fp8_kernel(
     const uint8_t* __restrict__ X, int64_t x_stride, const float* __restrict__ xs, int64_t xs_stride, int topk,
     const int* __restrict__ sorted_ids, const int* __restrict__ tile_expert, const uint8_t* __restrict__ W,
     int64_t w_expert_stride, const float* __restrict__ ws, int N, int K, uint16_t* __restrict__ Y, int64_t y_stride,
-    int act, float alpha, float limit, int a_rows_are_slots, const uint16_t* __restrict__ bias) {
+    int act, float alpha, float limit, int a_rows_are_slots, const uint16_t* __restrict__ bias,
+    uint8_t* __restrict__ hq, int64_t hq_stride, float* __restrict__ hs, int64_t hs_stride) {
   // ONE __shared__ array (a second LDS object can make hipcc drain vmcnt before every ds_read)
   __shared__ __attribute__((aligned(1024))) char lds[G3_NS * G3_STAGE];
   const int mt = blockIdx.y, nt = blockIdx.x;
@@ -951,6 +959,69 @@ __global__ __launch_bounds__(G3_NT, 1) void moe_gemm3_fp8_kernel(
     compute(kt, kt + G3_NS - 1 < nk);
   }
   // epilogue: acc[i][j][r] = C[row 32*(wm + 2i) + (r&3) + 8(r>>2) + 4h][col 64*wn + 32j + l32]
+  if constexpr (FQ && MODE == 1) {
+    // pass 1: bias + gated activation in place (even lanes hold o, odd lanes 0), per-row amax of
+    // this wave's 32 h columns, partials of the 4 N-waves through LDS
+    __syncthreads();  // every wave is out of the K loop: the ring is free
+    float* amax_lds = reinterpret_cast<float*>(lds);  // [256 rows][4 N-waves]
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        float a = 0.f;
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          const int col = n0 + 64 * wn + 32 * j + l32;
+          float v = acc[i][j][r];
+          if (bias && col < N) v += bf2f(bias[(int64_t)e * N + col]);
+          const float other = __shfl_xor(v, 1, 64);
+          float o = 0.f;
+          if ((l32 & 1) == 0 && col < N) {
+            float g = v, u = other;
+            if (act == 2) {
+              g = fminf(g, limit);
+              u = fminf(fmaxf(u, -limit), limit);
+              o = (u + 1.f) * g / (1.f + __expf(-alpha * g));
+            } else {
+              o = g / (1.f + __expf(-g)) * u;
+            }
+            o = bf2f(f2bf(o));  // the value the unfused path would have stored
+          }
+          acc[i][j][r] = o;
+          a = fmaxf(a, fabsf(o));
+        }
+#pragma unroll
+        for (int off = 1; off < 32; off <<= 1) a = fmaxf(a, __shfl_xor(a, off, 64));
+        if (l32 == 0) amax_lds[(32 * (wm + 2 * i) + (r & 3) + 8 * (r >> 2) + 4 * h) * 4 + wn] = a;
+      }
+    }
+    __syncthreads();
+    // pass 2: scale per row, e4m3 bytes of this workgroup's 128-column group (zeros past F)
+    const int hc0 = n0 / 2 + 32 * wn + l32 / 2;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      if (i >= rb_live) break;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int rl = 32 * (wm + 2 * i) + (r & 3) + 8 * (r >> 2) + 4 * h;
+        const int row = m0 + rl;
+        if (sorted_ids[row] < 0) continue;
+        const float* am = amax_lds + rl * 4;
+        const float s = pow2_ceil(fmaxf(fmaxf(fmaxf(am[0], am[1]), fmaxf(am[2], am[3])) / FP8_MAX, 1e-12f));
+        const float inv = 1.f / s;
+        if ((l32 & 1) == 0) {
+#pragma unroll
+          for (int j = 0; j < 2; ++j) {
+            const float c = fminf(fmaxf(acc[i][j][r] * inv, -FP8_MAX), FP8_MAX);
+            hq[(int64_t)row * hq_stride + hc0 + 16 * j] =
+                (uint8_t)(__builtin_amdgcn_cvt_pk_fp8_f32(c, 0.f, 0, false) & 0xff);
+          }
+        }
+        if (wn == 0 && l32 == 0) hs[(int64_t)row * hs_stride + nt] = s;
+      }
+    }
+    return;
+  }
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     if (i >= rb_live) break;
@@ -1071,21 +1142,26 @@ int llmd_moe_gemm3_tile_m() { return G3_BM; }
 
 // 256-row expert tiles (sorted by moe_align with bm = 256): the v3 kernel.
 // Needs power-of-two scales, K % 128 == 0 and 16-B aligned rows.
+// hq != nullptr (mode 1): fused e4m3 quantisation of the activation output into hq
+// [rows, >= N/2 rounded to 128] with power-of-two scales hs [rows, N/256 groups].
 int llmd_moe_gemm3_fp8(const void* X, int64_t x_stride, const float* xs, int64_t xs_stride, int topk,
                        const int* sorted_ids, const int* tile_expert, int num_tiles, const void* W,
                        int64_t w_expert_stride, const float* ws, int N, int K, void* Y, int64_t y_stride, int mode,
-                       int act, float alpha, float limit, int a_rows_are_slots, const void* bias, hipStream_t st) {
+                       int act, float alpha, float limit, int a_rows_are_slots, const void* bias, void* hq,
+                       int64_t hq_stride, float* hs, int64_t hs_stride, hipStream_t st) {
   if (K % 128 || x_stride % 16 || w_expert_stride % 16) return -1;
+  if (hq && mode != 1) return -2;
   if (num_tiles == 0) return 0;
   dim3 grid((N + G3_BN - 1) / G3_BN, num_tiles);
-  if (mode == 0)
-    hipLaunchKernelGGL(moe_gemm3_fp8_kernel<0>, grid, dim3(G3_NT), 0, st, (const uint8_t*)X, x_stride, xs, xs_stride,
-                       topk, sorted_ids, tile_expert, (const uint8_t*)W, w_expert_stride, ws, N, K, (uint16_t*)Y,
-                       y_stride, act, alpha, limit, a_rows_are_slots, (const uint16_t*)bias);
-  else
-    hipLaunchKernelGGL(moe_gemm3_fp8_kernel<1>, grid, dim3(G3_NT), 0, st, (const uint8_t*)X, x_stride, xs, xs_stride,
-                       topk, sorted_ids, tile_expert, (const uint8_t*)W, w_expert_stride, ws, N, K, (uint16_t*)Y,
-                       y_stride, act, alpha, limit, a_rows_are_slots, (const uint16_t*)bias);
+#define LLMD_G3F8(M, Q)                                                                                           \
+  hipLaunchKernelGGL((moe_gemm3_fp8_kernel<M, Q>), grid, dim3(G3_NT), 0, st, (const uint8_t*)X, x_stride, xs,      \
+                     xs_stride, topk, sorted_ids, tile_expert, (const uint8_t*)W, w_expert_stride, ws, N, K,       \
+                     (uint16_t*)Y, y_stride, act, alpha, limit, a_rows_are_slots, (const uint16_t*)bias,           \
+                     (uint8_t*)hq, hq_stride, hs, hs_stride)
+  if (mode == 0) LLMD_G3F8(0, false);
+  else if (hq) LLMD_G3F8(1, true);
+  else LLMD_G3F8(1, false);
+#undef LLMD_G3F8
   return (int)hipGetLastError();
 }
 

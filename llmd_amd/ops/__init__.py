@@ -360,6 +360,7 @@ def dequant_fp8_block_weight(q: torch.Tensor, s: torch.Tensor, block: int = 128)
 
 MOE_V3_MIN_ROWS = int(os.environ.get("LLMD_MOE_V3_MIN_ROWS", "96"))
 MOE_V3 = os.environ.get("LLMD_MOE_V3", "1") == "1"
+MOE_FUSED_QUANT = os.environ.get("LLMD_MOE_FUSED_QUANT", "0") == "1"
 
 
 def moe_experts_fp8(x, ids, wts, w1q, w1s, w2q, w2s, act=0, alpha=1.702, limit=7.0, out=None, b1=None, b2=None):
@@ -396,9 +397,18 @@ def moe_experts_fp8(x, ids, wts, w1q, w1s, w2q, w2s, act=0, alpha=1.702, limit=7
     inv = torch.empty(n, dtype=torch.int32, device=dev)  # moe_align fills it (-1 = not on this rank)
     C.moe_align(ids.contiguous().view(-1).to(torch.int32), E, sorted_ids, tile_e, offs, total, inv, bm)
     xq, xs = _quant_groups_padded(x, Kp1)
-    h = torch.empty(max_p, F, dtype=torch.bfloat16, device=dev)
-    C.moe_gemm_fp8(xq, xs, k, sorted_ids, tile_e, w1q, w1s, h, 1, act, alpha, limit, False, b1, bm)
-    hq, hs = _quant_groups_padded(h, Kp2)
+    if MOE_FUSED_QUANT and bm == C.moe_tile_m_prefill() and Kp2 == (N1 + 255) // 256 * 128:
+        # 256-row tiles: the first GEMM quantises its activation output itself (opt-in:
+        # measured slower - with one workgroup per CU the epilogue's amax exchange and
+        # byte stores are not hidden, profiles/moe_gemm_v3_fp8.txt)
+        hq = torch.empty(max_p, Kp2, dtype=FP8, device=dev)
+        hs = torch.empty(max_p, Kp2 // 128, dtype=torch.float32, device=dev)
+        C.moe_gemm_fp8(xq, xs, k, sorted_ids, tile_e, w1q, w1s, torch.empty(0, F, dtype=torch.bfloat16, device=dev),
+                       1, act, alpha, limit, False, b1, bm, hq, hs)
+    else:
+        h = torch.empty(max_p, F, dtype=torch.bfloat16, device=dev)
+        C.moe_gemm_fp8(xq, xs, k, sorted_ids, tile_e, w1q, w1s, h, 1, act, alpha, limit, False, b1, bm)
+        hq, hs = _quant_groups_padded(h, Kp2)
     y = torch.empty(max_p, d, dtype=torch.bfloat16, device=dev)
     # second GEMM: A rows are the sorted slots themselves (row p of hq; a_rows_are_slots)
     C.moe_gemm_fp8(hq, hs, 1, sorted_ids, tile_e, w2q, w2s, y, 0, 0, 0.0, 0.0, True, b2, bm)

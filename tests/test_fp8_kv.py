@@ -275,6 +275,44 @@ def test_moe_fp8_prefill_tiles_gpu(T, E, k, d, F, act, skew, monkeypatch):
     assert (y3.float() - y2.float()).abs().max().item() < 0.02 * m + 1e-3
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("T,E,k,d,F,act", [(700, 16, 4, 512, 2880, 2), (300, 8, 8, 256, 256, 0)])
+def test_moe_fp8_fused_act_quant_gpu(T, E, k, d, F, act):
+    """The 256-row first GEMM's fused epilogue quantisation (hq / hs) is bit
+    for bit the unfused path: bf16 h from the same kernel, then
+    quant_fp8_groups into K-padded rows (valid rows only; padding columns 0)."""
+    torch.manual_seed(2)
+    dev = "cuda"
+    C = ops.native()
+    c128 = lambda n: (n + 127) // 128 * 128  # noqa: E731
+    x = torch.randn(T, d, device=dev, dtype=torch.bfloat16)
+    w1q, w1s = ops.quant_fp8_block_weight(torch.randn(E, 2 * F, d, device=dev, dtype=torch.bfloat16) * 0.03)
+    w1q = ops.pad_fp8_k(w1q, c128(d))
+    b1 = torch.randn(E, 2 * F, device=dev, dtype=torch.bfloat16) * 0.1
+    ids, _ = ops.moe_topk(torch.randn(T, E, device=dev), k, scoring=0)
+    bm = C.moe_tile_m_prefill()
+    n = T * k
+    max_p = ((n + E * (bm - 1)) + bm - 1) // bm * bm
+    sorted_ids = torch.empty(max_p, dtype=torch.int32, device=dev)
+    tile_e = torch.empty(max_p // bm, dtype=torch.int32, device=dev)
+    offs = torch.empty(E + 1, dtype=torch.int32, device=dev)
+    total = torch.empty(1, dtype=torch.int32, device=dev)
+    inv = torch.empty(n, dtype=torch.int32, device=dev)
+    C.moe_align(ids.contiguous().view(-1).to(torch.int32), E, sorted_ids, tile_e, offs, total, inv, bm)
+    xq, xs = ops._quant_groups_padded(x, c128(d))
+    Kp2 = c128(F)
+    h = torch.empty(max_p, F, dtype=torch.bfloat16, device=dev)
+    C.moe_gemm_fp8(xq, xs, k, sorted_ids, tile_e, w1q, w1s, h, 1, act, 1.702, 7.0, False, b1, bm)
+    ref_q, ref_s = ops._quant_groups_padded(h, Kp2)
+    hq = torch.zeros(max_p, Kp2, dtype=ops.FP8, device=dev)
+    hs = torch.zeros(max_p, Kp2 // 128, dtype=torch.float32, device=dev)
+    C.moe_gemm_fp8(xq, xs, k, sorted_ids, tile_e, w1q, w1s, torch.empty(0, F, dtype=torch.bfloat16, device=dev),
+                   1, act, 1.702, 7.0, False, b1, bm, hq, hs)
+    valid = sorted_ids >= 0
+    assert torch.equal(hs[valid], ref_s[valid])
+    assert torch.equal(hq.view(torch.uint8)[valid], ref_q.view(torch.uint8)[valid])
+
+
 def test_fused_norm_act_quant_cpu_matches_unfused():
     torch.manual_seed(0)
     x = torch.randn(6, 256).to(torch.bfloat16)
