@@ -853,6 +853,10 @@ __device__ __forceinline__ void g3_dma4(const void* src, char* lds_base) {
 // ring) - instead of a bf16 h round trip through HBM and a quant_fp8_groups
 // pass over every padded row. Same numerics as that pass: the bf16-rounded
 // value, power-of-two scale pow2_ceil(max(amax / 448, 1e-12)), saturating e4m3.
+// Ablation switch for profiling (LLMD_MOE_ABLATE: 1 = no MFMA / fragment reads,
+// 2 = no DMA after the prologue); 0 in production.
+__device__ int g3_ablate = 0;
+
 template <int MODE, bool FQ>
 __global__ __launch_bounds__(G3_NT, 1) void moe_gemm3_fp8_kernel(
     const uint8_t* __restrict__ X, int64_t x_stride, const float* __restrict__ xs, int64_t xs_stride, int topk,
@@ -867,6 +871,7 @@ __global__ __launch_bounds__(G3_NT, 1) void moe_gemm3_fp8_kernel(
   if (e < 0) return;
   const int m0 = mt * G3_BM, n0 = nt * G3_BN;
   const int nk = K / 64, nkb = K / 128, nnb = (N + 127) / 128;
+
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
   const int wm = w >> 2, wn = w & 3;
   const int l32 = lane & 31, h = lane >> 5;
@@ -918,7 +923,13 @@ __global__ __launch_bounds__(G3_NT, 1) void moe_gemm3_fp8_kernel(
   for (int i = 0; i < 4; ++i)
 #pragma unroll
     for (int j = 0; j < 2; ++j) acc[i][j] = f32x16v_t{};
+  const int ablate = __builtin_amdgcn_readfirstlane(g3_ablate);
   auto compute = [&](int kt, bool refill) {
+    if (ablate) {
+      if (refill && !(ablate & 2)) issue(kt + G3_NS - 1);
+      if (ablate & 1) return;
+      refill = false;
+    }
     const char* st = lds + (kt & (G3_NS - 1)) * G3_STAGE;
     const int we = e8m0_of(wsr[kt >> 1]);
     i32x8_t bfr[2];
@@ -1151,6 +1162,13 @@ int llmd_moe_gemm3_fp8(const void* X, int64_t x_stride, const float* xs, int64_t
                        int64_t hq_stride, float* hs, int64_t hs_stride, hipStream_t st) {
   if (K % 128 || x_stride % 16 || w_expert_stride % 16) return -1;
   if (hq && mode != 1) return -2;
+  static const int ablate = [] {
+    const char* e = getenv("LLMD_MOE_ABLATE");
+    const int v = e ? atoi(e) : 0;
+    if (v) (void)hipMemcpyToSymbol(HIP_SYMBOL(g3_ablate), &v, sizeof v);
+    return v;
+  }();
+  (void)ablate;
   if (num_tiles == 0) return 0;
   dim3 grid((N + G3_BN - 1) / G3_BN, num_tiles);
 #define LLMD_G3F8(M, Q)                                                                                           \
