@@ -83,7 +83,6 @@ class WVAController:
                                           max_replicas=int(spec.get("maxReplicas", 2)),
                                           cost=float(spec.get("variantCost", "10.0")),
                                           gpus_per_replica=int(ln.get("tp", 1)) if not ln.get("cpu") else 0)
-        self.ports: dict[str, list[int]] = {n: [] for n in self.variants}
         self._launch_cmd = launch_cmd or self._engine_cmd
         self.actuator = ProcessActuator(int(cfg.get("gpus", 8)), self._launch, env=cfg.get("env") or {})
         self.engine = WVAEngine(cfg.get("scalingConfig") or {}, actuator=None,
@@ -106,29 +105,36 @@ class WVAController:
 
     def _launch(self, v: Variant, gpus: list[int], idx: int) -> list[str]:
         ln = self.launch[v.name]
-        port = int(ln.get("portBase", 8200)) + idx
-        ports = self.ports[v.name]
-        del ports[idx:]
-        ports.append(port)
+        # the lowest port of the variant's range that no running replica holds (replicas
+        # that died are pruned by the actuator, so indices and ports can diverge)
+        used = set(self.ports(v))
+        port = int(ln.get("portBase", 8200))
+        while port in used:
+            port += 1
         return self._launch_cmd(v, ln, port)
+
+    def ports(self, v: Variant) -> list[int]:
+        """Ports of the variant's live replicas, in start order (read back from
+        each process's ``--port`` argument, the single source of truth)."""
+        out = []
+        for p, _ in self.actuator.procs.get(v.name, []):
+            if p.poll() is None and "--port" in p.args:
+                out.append(int(p.args[p.args.index("--port") + 1]))
+        return out
 
     def scale(self, v: Variant, n: int):
         n = max(v.min_replicas, min(v.max_replicas, n))
         before = v.current
         if n < before:  # stop routing to the replicas first, then stop them
-            keep = self.ports[v.name][:n]
-            self._write_endpoints(exclude={(v.name, p) for p in self.ports[v.name][n:]})
-            self.actuator.scale(v, n)
-            self.ports[v.name] = keep
-        else:
-            self.actuator.scale(v, n)
+            self._write_endpoints(exclude={(v.name, p) for p in self.ports(v)[n:]})
+        self.actuator.scale(v, n)
         if n != before:
             log.info("variant %s: %d -> %d replicas", v.name, before, v.current)
 
     # ------------------------------------------------------------ observation
     def _observe(self, v: Variant):
         reps = []
-        for port in self.ports[v.name][:v.current]:
+        for port in self.ports(v):
             text = _get(f"http://127.0.0.1:{port}/metrics")
             if text is None:
                 reps.append(ReplicaMetrics(pod=f"{v.name}-{port}", ready=False))
@@ -222,7 +228,7 @@ class WVAController:
             return
         eps = []
         for v in self.variants.values():
-            for port in self.ports[v.name][:v.current]:
+            for port in self.ports(v):
                 if (v.name, port) in exclude or _get(f"http://127.0.0.1:{port}/health", 0.5) is None:
                     continue
                 eps.append({"name": f"{v.name}-{port}", "address": "127.0.0.1", "port": port,
