@@ -35,6 +35,9 @@ A topology YAML names the model, the router and the engine roles::
     - {type: batch-gateway, port: 8081}    # OpenAI Batch API -> router
     - {type: async-processor}              # queue-driven async dispatch -> router
     - {type: wva, port: 8080, config: {...}}   # workload variant autoscaler controller
+    - {type: iro, port: 8480}              # inference resilience operator; its rank
+                                           # topology map (engines, devices, DP groups,
+                                           # fault-event ports) is generated from the plan
 
 Every replica gets a disjoint GPU set (``HIP_VISIBLE_DEVICES``; TP replicas
 are packed onto neighbouring GPUs so TP traffic stays on direct xGMI links),
@@ -88,6 +91,8 @@ def plan(topo: dict, workdir: str) -> tuple[list[ProcSpec], dict]:
     endpoints = []
     master_port = int(topo.get("master_port_base", 29600))
     ev_next = 0  # KV-event ports handed out so far (one per engine process / DP rank)
+    node = str(topo.get("node_name", "localhost"))
+    iro_engines = []  # rank topology map for the resilience operator (nodeName + devices -> engine)
     for role in topo.get("roles", []):
         name, tp, dp = role["name"], int(role.get("tp", 1)), int(role.get("dp", 1))
         ranks = tp * dp
@@ -137,6 +142,14 @@ def plan(topo: dict, workdir: str) -> tuple[list[ProcSpec], dict]:
                 ep_name = rid if dp == 1 else f"{rid}-dp{r}"
                 endpoints.append({"name": ep_name, "address": "127.0.0.1", "port": front + r, "labels": lab,
                                   "metricsPort": port + r})
+                iro = {"name": ep_name, "url": f"http://127.0.0.1:{port + r}", "nodeName": node,
+                       "devices": gpus[r * tp:(r + 1) * tp],
+                       "endpoints": [{"address": "127.0.0.1", "port": front + r}]}
+                if dp > 1:  # wide-EP DP ranks step in lockstep: one recovery group
+                    iro["group"] = rid
+                if role.get("kv_events", False):
+                    iro["faultEvents"] = f"tcp://127.0.0.1:{ev_port + r}"
+                iro_engines.append(iro)
                 if r:
                     procs.append(ProcSpec(ep_name, [], {}, [], port + r, name + "-dp-rank"))
     doc = {"endpoints": endpoints}
@@ -144,7 +157,7 @@ def plan(topo: dict, workdir: str) -> tuple[list[ProcSpec], dict]:
     router_env: dict[str, str] = {}
     rport_http = int((r or {}).get("port", 8000))
     for svc in topo.get("services", []) or []:
-        spec = _service(svc, model, workdir, rport_http)
+        spec = _service(svc, model, workdir, rport_http, iro_engines)
         procs.append(spec)
         if svc["type"] == "predictor":
             router_env["PREDICTION_SERVER_URL"] = f"http://127.0.0.1:{spec.port}"
@@ -171,10 +184,10 @@ def plan(topo: dict, workdir: str) -> tuple[list[ProcSpec], dict]:
 
 SERVICES = {"predictor": "llmd_amd.router.predictor", "render": "llmd_amd.serving.render_server",
             "batch-gateway": "llmd_amd.batch.gateway", "async-processor": "llmd_amd.batch.async_processor",
-            "wva": "llmd_amd.autoscale.controller"}
+            "wva": "llmd_amd.autoscale.controller", "iro": "llmd_amd.resilience.operator"}
 
 
-def _service(svc: dict, model: str, workdir: str, router_port: int) -> ProcSpec:
+def _service(svc: dict, model: str, workdir: str, router_port: int, engines: Optional[list] = None) -> ProcSpec:
     """Router-side service of a well-lit path as a process spec."""
     t = svc["type"]
     if t not in SERVICES:
@@ -206,8 +219,20 @@ def _service(svc: dict, model: str, workdir: str, router_port: int) -> ProcSpec:
             with open(path, "w") as f:
                 yaml.safe_dump(conf, f)
         cmd += ["--config", path, "--metrics-bind-address", f":{port}"]
+    elif t == "iro":
+        port = int(port or 8480)
+        conf = dict(svc.get("config") or {})
+        conf.setdefault("recoveryRequestsDir", os.path.join(workdir, "recoveryrequests"))
+        conf.setdefault("endpointsFile", os.path.join(workdir, "endpoints.yaml"))
+        conf.setdefault("engines", list(engines or []))
+        path = os.path.join(workdir, "iro-config.yaml")
+        if workdir and not workdir.startswith("<") and os.path.isdir(workdir):
+            with open(path, "w") as f:
+                yaml.safe_dump(conf, f)
+        cmd += ["--config", path, "--port", str(port)]
     cmd += [str(a) for a in svc.get("args", [])]
-    health = {"predictor": "/healthz", "batch-gateway": "/v1/batches", "wva": "/metrics"}.get(t, "/health")
+    health = {"predictor": "/healthz", "batch-gateway": "/v1/batches", "wva": "/metrics",
+              "iro": "/healthz"}.get(t, "/health")
     return ProcSpec(svc.get("name", t), cmd, dict(svc.get("env") or {}), [], port, "service", health)
 
 

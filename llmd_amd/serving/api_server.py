@@ -104,6 +104,8 @@ class OpenAIServer:
         if self.mm is not None:
             r.add_post("/v1/encode", self.mm.http_encode)
             r.add_get("/v1/ec/{mm_hash}", self.mm.http_ec)
+        app.on_startup.append(self._start_fault_monitor)
+        app.on_cleanup.append(self._stop_fault_monitor)
         return app
 
     async def health(self, req):
@@ -597,6 +599,34 @@ class OpenAIServer:
                     out.append({"kind": "kv_peer_unreachable", "detail": peer})
         return out
 
+    def _publish_fault(self, action: str, faults: list[dict]):
+        pub = getattr(self, "kv_event_publisher", None)
+        if pub is not None:
+            pub.publish_batch({"ts": time.time(), "events": [{"type": "vllm_fault", "action": action,
+                                                              "faults": faults}]},
+                              topic=f"fault@{self.name}")
+
+    async def _fault_monitor(self):
+        """Engine-initiated fault notification (the ``vllm_fault`` PUB of
+        inference-resilience-operator.md:176-186): publish when the fault set
+        changes, so an operator reacts without polling ``/fault_tolerance/status``."""
+        last: list[dict] = []
+        period = float(os.environ.get("LLMD_FAULT_POLL_S", "1.0"))
+        while True:
+            await asyncio.sleep(period)
+            cur = self.faults()
+            if cur != last:
+                self._publish_fault("detected" if cur else "cleared", cur)
+                last = cur
+
+    async def _start_fault_monitor(self, _app):
+        self._fault_task = asyncio.get_running_loop().create_task(self._fault_monitor())
+
+    async def _stop_fault_monitor(self, _app):
+        t = getattr(self, "_fault_task", None)
+        if t is not None:
+            t.cancel()
+
     async def ft_status(self, req):
         faults = self.faults()
         eng = self.aeng.engine
@@ -606,11 +636,19 @@ class OpenAIServer:
                                   "num_waiting": eng.sched.num_waiting})
 
     async def ft_apply(self, req):
-        """Recovery actions: pause | resume | drain {timeout} | abort_all | reset_prefix_cache."""
+        """Recovery actions: pause | resume | retry | drain {timeout} | abort_all |
+        reset_prefix_cache. ``retry`` is the operator's answer to a transient,
+        engine-internal fault: re-probe the KV-transfer peers, then resume."""
         body = await req.json()
         act = body.get("action")
         if act == "pause":
             self.aeng.pause()
+        elif act == "retry":
+            ag = getattr(self.aeng.engine.connector, "agent", None)
+            if ag is not None:
+                await asyncio.get_running_loop().run_in_executor(None, ag.heartbeat_once)
+            self.aeng.accepting = True
+            self.aeng.resume()
         elif act == "resume":
             self.aeng.accepting = True
             self.aeng.resume()
@@ -623,11 +661,7 @@ class OpenAIServer:
             await self.aeng.call(lambda e: e.reset_prefix_cache())
         else:
             return _err(400, f"unknown action {act!r}")
-        pub = getattr(self, "kv_event_publisher", None)
-        if pub is not None:
-            pub.publish_batch({"ts": time.time(), "events": [{"type": "vllm_fault", "action": act,
-                                                              "faults": self.faults()}]},
-                              topic=f"fault@{self.name}")
+        self._publish_fault(act, self.faults())
         return web.json_response({"applied": act})
 
     async def is_paused(self, req):
