@@ -38,6 +38,7 @@ A topology YAML names the model, the router and the engine roles::
     - {type: iro, port: 8480}              # inference resilience operator; its rank
                                            # topology map (engines, devices, DP groups,
                                            # fault-event ports) is generated from the plan
+    - {type: timeslice, port: 8490}        # RL time-slicing orchestrator (llmd_amd.rl.timeslice)
 
 Every replica gets a disjoint GPU set (``HIP_VISIBLE_DEVICES``; TP replicas
 are packed onto neighbouring GPUs so TP traffic stays on direct xGMI links),
@@ -184,7 +185,8 @@ def plan(topo: dict, workdir: str) -> tuple[list[ProcSpec], dict]:
 
 SERVICES = {"predictor": "llmd_amd.router.predictor", "render": "llmd_amd.serving.render_server",
             "batch-gateway": "llmd_amd.batch.gateway", "async-processor": "llmd_amd.batch.async_processor",
-            "wva": "llmd_amd.autoscale.controller", "iro": "llmd_amd.resilience.operator"}
+            "wva": "llmd_amd.autoscale.controller", "iro": "llmd_amd.resilience.operator",
+            "timeslice": "llmd_amd.rl.timeslice"}
 
 
 def _service(svc: dict, model: str, workdir: str, router_port: int, engines: Optional[list] = None) -> ProcSpec:
@@ -230,9 +232,12 @@ def _service(svc: dict, model: str, workdir: str, router_port: int, engines: Opt
             with open(path, "w") as f:
                 yaml.safe_dump(conf, f)
         cmd += ["--config", path, "--port", str(port)]
+    elif t == "timeslice":
+        port = int(port or 8490)
+        cmd += ["--port", str(port)]
     cmd += [str(a) for a in svc.get("args", [])]
     health = {"predictor": "/healthz", "batch-gateway": "/v1/batches", "wva": "/metrics",
-              "iro": "/healthz"}.get(t, "/health")
+              "iro": "/healthz", "timeslice": "/healthz"}.get(t, "/health")
     return ProcSpec(svc.get("name", t), cmd, dict(svc.get("env") or {}), [], port, "service", health)
 
 
