@@ -129,6 +129,19 @@ class OpenAIServer:
         return web.Response(body=body, content_type="text/plain", charset="utf-8")
 
     # ------------------------------------------------------------ helpers
+    def _token_ids(self, ids) -> list[int]:
+        """Client-supplied token ids: integers inside the vocabulary (an
+        out-of-range id would fault the embedding gather inside the step)."""
+        v = self.cfg.model_config.vocab_size
+        out = []
+        for t in ids:
+            if isinstance(t, bool) or not isinstance(t, int):
+                raise ValueError(f"token ids must be integers, got {t!r}")
+            if not 0 <= t < v:
+                raise ValueError(f"Token id {t} is out of vocabulary (vocab size {v})")
+            out.append(t)
+        return out
+
     def _prompt_ids(self, body) -> list[list[int]]:
         p = body.get("prompt")
         if p is None:
@@ -136,11 +149,11 @@ class OpenAIServer:
         if isinstance(p, str):
             return [self.tok.encode(p)]
         if isinstance(p, list) and p and isinstance(p[0], int):
-            return [list(p)]
+            return [self._token_ids(p)]
         if isinstance(p, list) and p and isinstance(p[0], str):
             return [self.tok.encode(x) for x in p]
         if isinstance(p, list) and p and isinstance(p[0], list):
-            return [list(x) for x in p]
+            return [self._token_ids(x) for x in p]
         raise ValueError("unsupported prompt format")
 
     def _chat_ids(self, body) -> list[int]:
@@ -573,7 +586,10 @@ class OpenAIServer:
         router's vllmgrpc-style path): {"token_ids"|"prompt", "sampling_params"}."""
         body = await req.json()
         if "token_ids" in body:
-            ids = list(body["token_ids"])
+            try:
+                ids = self._token_ids(body["token_ids"])
+            except (ValueError, TypeError) as e:
+                return _err(400, str(e))
         elif isinstance(body.get("prompt"), str):
             ids = self.tok.encode(body["prompt"])
         else:

@@ -114,3 +114,35 @@ def test_embeddings_responses_messages_generate_endpoints():
     st, gen = out["gen"]
     assert st == 200 and len(gen["choices"][0]["token_ids"]) == 5
     assert gen["choices"][0]["token_ids"] == out["cmp"][1]["choices"][0]["token_ids"]
+
+
+def test_out_of_vocab_token_ids_rejected_engine_survives():
+    """Token-id prompts outside the vocabulary get a 400 instead of reaching
+    the embedding gather (which would take the engine loop down)."""
+    async def main():
+        eng = build_server(_cfg())
+        r1, port = await _serve(eng.app())
+        base = f"http://127.0.0.1:{port}"
+        v = eng.cfg.model_config.vocab_size
+        try:
+            async with aiohttp.ClientSession() as s:
+                out = {}
+                for tag, body, path in (
+                        ("comp", {"prompt": [1, 2, v + 5], "max_tokens": 2}, "/v1/completions"),
+                        ("batch", {"prompt": [[1, 2], [3, -1]], "max_tokens": 2}, "/v1/completions"),
+                        ("float", {"prompt": [1, 2.5], "max_tokens": 2}, "/v1/completions"),
+                        ("gen", {"token_ids": [v], "sampling_params": {"max_tokens": 2}}, "/inference/v1/generate"),
+                        ("ok", {"prompt": [1, 2, v - 1], "max_tokens": 2}, "/v1/completions")):
+                    async with s.post(base + path, json=dict(body, model="tiny-llama")) as r:
+                        out[tag] = (r.status, await r.json())
+            return out, eng.aeng.dead
+        finally:
+            await r1.cleanup()
+            eng.aeng.shutdown()
+
+    out, dead = asyncio.run(main())
+    for tag in ("comp", "batch", "float", "gen"):
+        assert out[tag][0] == 400, (tag, out[tag])
+    assert "out of vocabulary" in out["comp"][1]["error"]["message"]
+    assert out["ok"][0] == 200 and out["ok"][1]["usage"]["completion_tokens"] == 2
+    assert dead is None
