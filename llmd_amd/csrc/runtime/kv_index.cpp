@@ -219,13 +219,14 @@ class ApproxIndex {
   void insert(const std::string& server, const std::vector<uint64_t>& keys) {
     std::lock_guard<std::mutex> g(mu_);
     auto& s = servers_[server];
+    const int64_t cap = s.cap > 0 ? s.cap : cap_;
     for (uint64_t k : keys) {
       auto it = s.map.find(k);
       if (it != s.map.end()) {
         s.lru.splice(s.lru.begin(), s.lru, it->second);
         continue;
       }
-      if ((int64_t)s.map.size() >= cap_ && !s.lru.empty()) {
+      if ((int64_t)s.map.size() >= cap && !s.lru.empty()) {
         s.map.erase(s.lru.back());
         s.lru.pop_back();
       }
@@ -257,6 +258,23 @@ class ApproxIndex {
     std::lock_guard<std::mutex> g(mu_);
     servers_.erase(s);
   }
+  // Per-server LRU capacity (autoTune: the server's real KV capacity in
+  // producer blocks); shrinking evicts the least recently used keys at once.
+  void set_capacity(const std::string& server, int64_t cap) {
+    std::lock_guard<std::mutex> g(mu_);
+    auto& s = servers_[server];
+    s.cap = cap;
+    const int64_t c = cap > 0 ? cap : cap_;
+    while ((int64_t)s.map.size() > c && !s.lru.empty()) {
+      s.map.erase(s.lru.back());
+      s.lru.pop_back();
+    }
+  }
+  int64_t server_size(const std::string& server) {
+    std::lock_guard<std::mutex> g(mu_);
+    auto it = servers_.find(server);
+    return it == servers_.end() ? 0 : (int64_t)it->second.map.size();
+  }
   int64_t size() const {
     int64_t n = 0;
     for (auto& kv : servers_) n += (int64_t)kv.second.map.size();
@@ -265,6 +283,7 @@ class ApproxIndex {
 
  private:
   struct S {
+    int64_t cap = -1;  // < 0: the index-wide default
     std::list<uint64_t> lru;
     std::unordered_map<uint64_t, std::list<uint64_t>::iterator> map;
   };
@@ -314,6 +333,8 @@ void register_kv_index(py::module_& m) {
       .def("insert", &ApproxIndex::insert)
       .def("match", &ApproxIndex::match)
       .def("remove_server", &ApproxIndex::remove_server)
+      .def("set_capacity", &ApproxIndex::set_capacity, py::arg("server"), py::arg("cap"))
+      .def("server_size", &ApproxIndex::server_size)
       .def("size", &ApproxIndex::size);
   m.def("char_block_hashes", &char_block_hashes, py::arg("text"), py::arg("block_chars"),
         py::arg("seed") = 0, py::arg("max_blocks") = 0);

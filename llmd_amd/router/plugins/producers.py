@@ -14,7 +14,7 @@ from typing import Optional
 
 from llmd_amd import _rt_loader
 
-from ..types import KV_USAGE, RUNNING, WAITING, Endpoint, InferenceRequest
+from ..types import BLOCK_SIZE, KV_USAGE, NUM_GPU_BLOCKS, RUNNING, WAITING, Endpoint, InferenceRequest
 from .base import Admitter, DataProducer, PreRequest, ResponseProcessor, register
 
 log = logging.getLogger("llmd.router.producers")
@@ -26,7 +26,12 @@ CHARS_PER_TOKEN = 4
 class ApproxPrefixCacheProducer(DataProducer, PreRequest):
     """Character-block rolling hash chain + per-server LRU learned on route.
     Params: blockSizeTokens (default 64), maxPrefixBlocksToMatch (256),
-    maxPrefixTokensToMatch, lruCapacityPerServer (31250), autoTune."""
+    maxPrefixTokensToMatch, lruCapacityPerServer (31250), autoTune (true:
+    each server's LRU holds as many producer blocks as its KV pool holds
+    tokens - ``vllm:cache_config_info`` num_gpu_blocks x block_size /
+    blockSizeTokens - so the index forgets prefixes about when the engine
+    evicts them instead of crediting a server with everything ever routed
+    to it; configuration.md:380-390, agentic-serving.values.yaml:20-29)."""
 
     def __init__(self, *a, **k):
         super().__init__(*a, **k)
@@ -38,6 +43,19 @@ class ApproxPrefixCacheProducer(DataProducer, PreRequest):
             self.max_blocks = max(1, int(mt) // self.block_tokens)
         self.index = rt.ApproxIndex(int(self.p("lruCapacityPerServer", 31250)))
         self.rt = rt
+        at = self.p("autoTune", True)
+        self.auto_tune = at if isinstance(at, bool) else str(at).lower() == "true"
+        self._caps: dict[str, int] = {}
+
+    def _tune(self, eps):
+        for e in eps:
+            nb, bs = int(e.metric(NUM_GPU_BLOCKS, 0) or 0), int(e.metric(BLOCK_SIZE, 0) or 0)
+            if nb <= 0 or bs <= 0:
+                continue
+            cap = max(1, nb * bs // self.block_tokens)
+            if self._caps.get(e.key) != cap:
+                self._caps[e.key] = cap
+                self.index.set_capacity(e.key, cap)
 
     def _keys(self, req: InferenceRequest) -> list[int]:
         if req.token_ids:
@@ -46,6 +64,8 @@ class ApproxPrefixCacheProducer(DataProducer, PreRequest):
         return self.rt.char_block_hashes(req.prompt, self.block_tokens * CHARS_PER_TOKEN, 0, self.max_blocks)
 
     async def produce(self, req, eps):
+        if self.auto_tune:
+            self._tune(eps)
         keys = self._keys(req)
         req.data.setdefault("prefix_keys", {})[self.name] = keys
         if not keys:

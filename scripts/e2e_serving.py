@@ -6,8 +6,10 @@ prefix-cache-aware routing benchmark shape, guides/optimized-baseline and
 precise-prefix-cache-routing). The same load runs under several EPP
 configurations so the routing policy is the only variable:
 
-* ``prefix``  - approx prefix producer + prefix / queue / kv-util scorers
-  (the optimized-baseline default);
+* ``prefix``  - the reference's optimized-baseline EPP config (queue 2,
+  kv-util 2, prefix 3 over the approx producer, no-hit-LRU 2);
+* ``precise`` - the same scorers fed by the KV-event index (engines publish
+  BlockStored / BlockRemoved; precise-prefix-cache-routing);
 * ``load``    - queue + kv-util scorers only (no prefix affinity);
 * ``random``  - random picker.
 
@@ -42,12 +44,38 @@ from llmd_amd.router.datalayer import parse_prometheus  # noqa: E402
 from llmd_amd.tools import loadgen  # noqa: E402
 
 CONFIGS = {
+    # the reference's optimized-baseline EPP config verbatim
+    # (guides/optimized-baseline/router/optimized-baseline.values.yaml): the
+    # prefix-cache-scorer brings the approx producer with its defaults (autoTune)
     "prefix": """
 apiVersion: llm-d.ai/v1alpha1
 kind: EndpointPickerConfig
 plugins:
-- type: approx-prefix-cache-producer
-  parameters: {blockSize: 16}
+- type: queue-scorer
+- type: kv-cache-utilization-scorer
+- type: prefix-cache-scorer
+- type: no-hit-lru-scorer
+schedulingProfiles:
+- name: default
+  plugins:
+  - pluginRef: queue-scorer
+    weight: 2
+  - pluginRef: kv-cache-utilization-scorer
+    weight: 2
+  - pluginRef: prefix-cache-scorer
+    weight: 3
+  - pluginRef: no-hit-lru-scorer
+    weight: 2
+""",
+    "precise": """
+apiVersion: llm-d.ai/v1alpha1
+kind: EndpointPickerConfig
+plugins:
+- type: precise-prefix-cache-producer
+  parameters:
+    tokenProcessorConfig: {blockSize: 16}
+    speculativeIndexing: true
+    kvEventsConfig: {discoverPods: true}
 - type: prefix-cache-scorer
 - type: queue-scorer
 - type: kv-cache-utilization-scorer
@@ -55,7 +83,7 @@ plugins:
 schedulingProfiles:
 - name: default
   plugins:
-  - pluginRef: approx-prefix-cache-producer
+  - pluginRef: precise-prefix-cache-producer
   - pluginRef: prefix-cache-scorer
     weight: 3
   - pluginRef: queue-scorer
@@ -142,7 +170,8 @@ def main():
     ap.add_argument("--output-len", type=int, default=64)
     ap.add_argument("--concurrency", type=int, default=64)
     ap.add_argument("--requests", type=int, default=768)
-    ap.add_argument("--configs", default="prefix,load,random")
+    ap.add_argument("--configs", default="prefix,precise,load,random")
+    ap.add_argument("--kv-events-port-base", type=int, default=15556)
     ap.add_argument("--port-base", type=int, default=18200)
     ap.add_argument("--router-port", type=int, default=18100)
     ap.add_argument("--out", default=os.path.join(ROOT, "gpurun_out", "e2e_serving.json"))
@@ -161,13 +190,17 @@ def main():
         cmd = [sys.executable, "-m", "llmd_amd.serving.api_server", "--model", a.model, "--port", str(port),
                "--device", a.device, "--num-gpu-blocks-override", str(a.blocks), "--block-size", "16",
                "--max-num-seqs", str(max(8, a.concurrency)), "--max-num-batched-tokens", "8192",
-               "--max-model-len", str(a.system_len + a.question_len + a.output_len + 64)] + a.extra_engine_args.split()
+               "--max-model-len", str(a.system_len + a.question_len + a.output_len + 64),
+               "--kv-events-config", json.dumps({"enable_kv_cache_events": True, "publisher": "zmq",
+                                                 "endpoint": f"tcp://*:{a.kv_events_port_base + i}"})] + \
+            a.extra_engine_args.split()
         log = open(os.path.join(ROOT, "gpurun_out", f"e2e_engine{i}.log"), "w")
         logs.append(log)
         engines.append(subprocess.Popen(cmd, env=dict(env, POD_PORT=str(port)), stdout=log, stderr=subprocess.STDOUT,
                                         cwd=ROOT, start_new_session=True))
     eps = {"endpoints": [{"name": f"e{i}", "address": "127.0.0.1", "port": port,
-                          "labels": {"llm-d.ai/role": "prefill-decode", "llm-d.ai/model": a.model}}
+                          "labels": {"llm-d.ai/role": "prefill-decode", "llm-d.ai/model": a.model,
+                                     "llm-d.ai/kv-events-port": str(a.kv_events_port_base + i)}}
                          for i, port in enumerate(ports)]}
     ep_file = os.path.join(work, "endpoints.yaml")
     with open(ep_file, "w") as f:
@@ -190,7 +223,7 @@ def main():
             if not _wait(f"http://127.0.0.1:{port}/v1/models", engines, 600):
                 raise RuntimeError(f"engine on {port} not ready")
         print(f"[e2e] {a.replicas} engines ready", flush=True)
-        for name in a.configs.split(","):
+        for run_i, name in enumerate(a.configs.split(",")):
             for port in ports:
                 _post(f"http://127.0.0.1:{port}/reset_prefix_cache")
             rlog = open(os.path.join(ROOT, "gpurun_out", f"e2e_router_{name}.log"), "w")
@@ -223,7 +256,7 @@ def main():
                        "ttft_p90_s": s["latency"]["time_to_first_token"]["p90"],
                        "itl_p50_s": s["latency"]["inter_token_latency"]["p50"],
                        "prefix_hit_rate": (h1 - h0) / (q1 - q0) if q1 > q0 else None}
-                results["runs"][name] = out
+                results["runs"][name if name not in results["runs"] else f"{name}#{run_i}"] = out
                 print(f"[e2e] {name}: " + json.dumps(out), flush=True)
             finally:
                 os.killpg(router.pid, signal.SIGTERM)

@@ -3,7 +3,7 @@
 set -o pipefail
 mkdir -p gpurun_out
 timeout -k 10 1000 python -u scripts/e2e_serving.py --model llama-3-8b --device cuda --replicas 2 --blocks 4096 \
-  --groups 48 --per-group 16 --system-len 2048 --question-len 128 --output-len 64 --concurrency 64 --requests 768 \
+  --groups 48 --per-group 16 --system-len 2048 --question-len 128 --output-len 64 --concurrency 64 --requests 768 --configs prefix,precise,load,random,prefix,precise \
   --out gpurun_out/e2e_serving.json > gpurun_out/e2e_serving.log 2>&1
 rc=$?
 grep "^\[e2e\]" gpurun_out/e2e_serving.log | grep -v "\.\.\." | cut -c1-400

@@ -250,6 +250,33 @@ def test_approx_prefix_affinity_learns():
     assert picks == {first}
 
 
+def test_approx_prefix_autotune_forgets_evicted_prefixes():
+    """autoTune sizes each server's LRU from its KV pool (num_gpu_blocks x
+    block_size tokens): prefixes beyond that are forgotten like the engine
+    evicts them; with autoTune off the default 31250-block LRU keeps them."""
+    from llmd_amd.router.plugins.producers import ApproxPrefixCacheProducer
+    from llmd_amd.router.types import BLOCK_SIZE, NUM_GPU_BLOCKS
+
+    def run(auto):
+        prod = ApproxPrefixCacheProducer("p", {"blockSizeTokens": 16, "autoTune": auto})
+        e = ep(1, **{NUM_GPU_BLOCKS: 4, BLOCK_SIZE: 32})  # 128 tokens = 8 producer blocks
+        toks = lambda base: list(range(base, base + 64))  # noqa: E731  4 blocks per prompt
+
+        async def go():
+            out = []
+            for base in (1000, 2000, 3000, 1000):
+                r = req("")
+                r.token_ids = toks(base)
+                await prod.produce(r, [e])
+                out.append(r.data["prefix_match"]["p"][e.key])
+                prod.index.insert(e.key, r.data["prefix_keys"]["p"])  # routed there (PreRequest)
+            return out
+        return asyncio.run(go())
+
+    assert run(True) == [0.0, 0.0, 0.0, 0.0]    # prompt 1000 evicted by 2000 + 3000 (8-block LRU)
+    assert run(False) == [0.0, 0.0, 0.0, 1.0]
+
+
 # ------------------------------------------------------------------ flow control
 def test_flow_control_priority_capacity_ttl():
     c = load_config(FLOW)
