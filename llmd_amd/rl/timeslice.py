@@ -307,7 +307,15 @@ class Slicer:
     def gpu(self, yield_after: bool = False):
         """A GPU phase. ``yield_after``: swap out right away on exit (the job
         knows its next blocking phase is long) instead of staying resident."""
-        g = _post(self.url + "/acquire", {"job": self.job})
+        try:
+            g = _post(self.url + "/acquire", {"job": self.job})
+        except OSError:
+            # the grant may have happened with the reply lost: hand it back
+            try:
+                _post(self.url + "/release", {"job": self.job}, timeout=10)
+            except OSError:
+                pass
+            raise
         with self._lock:
             if not (g["warm"] and self.resident):
                 if self.swap_in_fn is not None:
