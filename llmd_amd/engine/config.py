@@ -432,12 +432,69 @@ def add_engine_args(p: argparse.ArgumentParser) -> argparse.ArgumentParser:
     p.add_argument("--max-loras", type=int, default=4)
     p.add_argument("--max-lora-rank", type=int, default=16)
     p.add_argument("--lora-modules", nargs="*", default=None, help="name=path adapters loaded at start-up")
+    # vLLM flags the reference's guides pass, mapped onto this engine
+    p.add_argument("--hf-overrides", type=_json_arg, default=None,
+                   help="JSON of model-config fields to override (HF names, e.g. num_hidden_layers)")
+    p.add_argument("--disable-sliding-window", action="store_true",
+                   help="full attention on every layer (sliding-window layers included)")
+    p.add_argument("--max-cudagraph-capture-size", type=int, default=None,
+                   help="largest decode batch captured as a hipGraph")
+    p.add_argument("--compilation-config", "-O", type=_json_arg, default=None,
+                   help="vLLM compilation config: cudagraph_capture_sizes / max_cudagraph_capture_size set the "
+                        "hipGraph buckets, cudagraph_mode NONE = --enforce-eager; other keys are ignored "
+                        "(no tracing compiler: the hot ops are HIP kernels)")
+    # accepted for command-line compatibility; no effect on this engine
+    for f in ("--trust-remote-code", "--enable-cumem-allocator", "--enable-ep-weight-filter",
+              "--enable-prefiller-sampling", "--async-scheduling", "--no-async-scheduling",
+              "--disable-hybrid-kv-cache-manager", "--no-disable-hybrid-kv-cache-manager",
+              "--data-parallel-hybrid-lb", "--data-parallel-multi-port-external-lb"):
+        p.add_argument(f, action="store_true", help=argparse.SUPPRESS)
+    for f in ("--tokenizer-mode", "--attention-backend", "--moe-backend", "--data-parallel-address",
+              "--data-parallel-rpc-port", "--data-parallel-supervisor-port"):
+        p.add_argument(f, default=None, help=argparse.SUPPRESS)
+    p.add_argument("--data-parallel-size-local", type=int, default=None,
+                   help="DP ranks on this node (must equal the local torchrun ranks / tp)")
+    p.add_argument("--data-parallel-start-rank", type=int, default=0,
+                   help="global DP rank of this node's first rank (multi-node DP)")
     return p
 
 
+def _model_config_from_args(a) -> Optional["ModelConfig"]:
+    ov = dict(getattr(a, "hf_overrides", None) or {})
+    if not ov and not getattr(a, "disable_sliding_window", False):
+        return None
+    mc = get_model_config(a.model)
+    unknown = [k for k in ov if not hasattr(mc, k)]
+    if unknown:
+        raise ValueError(f"--hf-overrides: unknown model-config fields {unknown}")
+    mc = dataclasses.replace(mc, **ov)
+    if getattr(a, "disable_sliding_window", False):
+        mc = dataclasses.replace(mc, sliding_window=0,
+                                 layer_types=["full_attention"] * mc.num_hidden_layers if mc.layer_types else
+                                 mc.layer_types)
+    return mc
+
+
+def _graph_max_bs(a) -> tuple[Optional[int], bool]:
+    """(largest captured decode batch, eager) from the vLLM graph flags."""
+    cc = getattr(a, "compilation_config", None) or {}
+    eager = a.enforce_eager or str(cc.get("cudagraph_mode", "")).upper() == "NONE"
+    bs = getattr(a, "max_cudagraph_capture_size", None) or cc.get("max_cudagraph_capture_size")
+    if bs is None and cc.get("cudagraph_capture_sizes"):
+        bs = max(int(x) for x in cc["cudagraph_capture_sizes"])
+    return (int(bs) if bs else None), eager
+
+
 def engine_config_from_args(a) -> EngineConfig:
+    graph_bs, eager = _graph_max_bs(a)
+    extra = {}
+    mc = _model_config_from_args(a)
+    if mc is not None:
+        extra["model_config"] = mc
+    if graph_bs is not None:
+        extra["cuda_graph_max_bs"] = graph_bs
     return EngineConfig.create(
-        a.model, served_model_name=a.served_model_name, tokenizer=a.tokenizer,
+        a.model, **extra, served_model_name=a.served_model_name, tokenizer=a.tokenizer,
         load_format=a.load_format, weights_path=a.weights_path, dtype=a.dtype, device=a.device,
         seed=a.seed, block_size=a.block_size, kv_cache_dtype=getattr(a, "kv_cache_dtype", "auto"),
         quantization=getattr(a, "quantization", None), gpu_memory_utilization=a.gpu_memory_utilization,
@@ -452,7 +509,7 @@ def engine_config_from_args(a) -> EngineConfig:
         enable_dbo=getattr(a, "enable_dbo", False),
         dbo_decode_token_threshold=getattr(a, "dbo_decode_token_threshold", 32),
         dbo_prefill_token_threshold=getattr(a, "dbo_prefill_token_threshold", 32),
-        enforce_eager=a.enforce_eager, kv_transfer_config=a.kv_transfer_config,
+        enforce_eager=eager, kv_transfer_config=a.kv_transfer_config,
         kv_events_config=a.kv_events_config, kv_offload_config=a.kv_offload_config,
         policy=a.scheduling_policy, prefill_token_align=getattr(a, "prefill_token_align", -1),
         enable_lora=getattr(a, "enable_lora", False),

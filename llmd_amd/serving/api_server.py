@@ -34,6 +34,7 @@ import logging
 import os
 import time
 import uuid
+from dataclasses import dataclass
 from typing import Optional
 
 from aiohttp import web
@@ -42,7 +43,9 @@ from llmd_amd.engine.config import EngineConfig, add_engine_args, engine_config_
 from llmd_amd.engine.request import SamplingParams
 
 from .async_engine import AsyncEngine, EngineDeadError
-from .tokenizer import load_tokenizer, render_chat
+from .chat_template import ChatTemplate, render_tools, style_for
+from .parsers import ChatOutputParser
+from .tokenizer import load_tokenizer
 
 log = logging.getLogger("llmd.api")
 
@@ -51,15 +54,33 @@ def _err(status: int, msg: str, typ: str = "invalid_request_error"):
     return web.json_response({"error": {"message": msg, "type": typ, "code": status}}, status=status)
 
 
+@dataclass
+class ServingOptions:
+    """Front-end options (vLLM flag names): chat template, output parsers,
+    streaming granularity, multimodal limits / roles."""
+    chat_template: Optional[str] = None
+    enable_auto_tool_choice: bool = False
+    tool_call_parser: Optional[str] = None
+    reasoning_parser: Optional[str] = None
+    stream_interval: int = 1
+    limit_mm_per_prompt: Optional[dict] = None
+    mm_encoder_only: bool = False
+
+
 class OpenAIServer:
-    def __init__(self, aeng: AsyncEngine, cfg: EngineConfig, tokenizer=None, lora_manager=None):
+    def __init__(self, aeng: AsyncEngine, cfg: EngineConfig, tokenizer=None, lora_manager=None,
+                 opts: Optional[ServingOptions] = None):
         self.aeng = aeng
         self.cfg = cfg
         self.name = cfg.served_name
         mc = cfg.model_config
         self.tok = tokenizer or load_tokenizer(cfg.tokenizer, mc.vocab_size, mc.bos_token_id, mc.eos_ids[0])
         self.lora = lora_manager
-        self.chat_style = "llama3" if mc.model_type == "llama" else "chatml"
+        self.opts = opts or ServingOptions()
+        self.template = ChatTemplate(style_for(mc.model_type), model_dir=cfg.tokenizer,
+                                     template=self.opts.chat_template)
+        self.parser = (ChatOutputParser(self.opts.reasoning_parser, self.opts.tool_call_parser)
+                       if self.opts.reasoning_parser or self.opts.tool_call_parser else None)
         self.ready = True
         self.extra_metrics = []  # callables returning bytes
         self.mm = None
@@ -156,13 +177,42 @@ class OpenAIServer:
             return [self._token_ids(x) for x in p]
         raise ValueError("unsupported prompt format")
 
+    def _tools_active(self, body) -> bool:
+        """OpenAI ``tools`` / ``tool_choice`` semantics (vLLM): ``auto`` needs
+        --enable-auto-tool-choice and a --tool-call-parser; ``none`` hides the
+        tools from the template; no tool_choice means auto when enabled."""
+        tools = body.get("tools")
+        if not tools:
+            return False
+        tc = body.get("tool_choice")
+        if tc == "none":
+            return False
+        enabled = self.opts.enable_auto_tool_choice and self.opts.tool_call_parser
+        if tc == "auto" and not enabled:
+            raise ValueError('"auto" tool choice requires --enable-auto-tool-choice and --tool-call-parser to be set')
+        if tc in ("required",) or isinstance(tc, dict):
+            if not self.opts.tool_call_parser:
+                raise ValueError("tool_choice 'required' / named functions need --tool-call-parser")
+            return True
+        return bool(enabled)
+
     def _chat_ids(self, body) -> list[int]:
         msgs = body.get("messages")
         if not isinstance(msgs, list) or not msgs:
             raise ValueError("messages is required")
         if self.mm is not None and self._has_images(body):
             raise ValueError("image inputs need the async multimodal path")
-        return self.tok.encode(render_chat(msgs, body.get("add_generation_prompt", True), self.chat_style))
+        self._tools_active(body)  # validates tool_choice
+        tools = render_tools(body, bool(self.opts.enable_auto_tool_choice and self.opts.tool_call_parser))
+        kw = dict(body.get("chat_template_kwargs") or {})
+        return self.tok.encode(self.template.render(msgs, body.get("add_generation_prompt", True), tools=tools,
+                                                    **kw))
+
+    @staticmethod
+    def _n_images(body) -> int:
+        from .multimodal import image_parts
+
+        return len(image_parts(body.get("messages") or []))
 
     @staticmethod
     def _has_images(body) -> bool:
@@ -177,7 +227,10 @@ class OpenAIServer:
         msgs = body.get("messages")
         if not isinstance(msgs, list) or not msgs:
             raise ValueError("messages is required")
-        text = render_chat(mark_images(msgs), body.get("add_generation_prompt", True), self.chat_style)
+        lim = (self.opts.limit_mm_per_prompt or {}).get("image")
+        if lim is not None and self._n_images(body) > int(lim):
+            raise ValueError(f"At most {lim} image(s) may be provided in one prompt (--limit-mm-per-prompt)")
+        text = self.template.render(mark_images(msgs), body.get("add_generation_prompt", True))
         return await self.mm.prepare(body, text, headers)
 
     def _lora_id(self, body) -> int:
@@ -217,6 +270,8 @@ class OpenAIServer:
             return await self._serve_inner(req, chat)
 
     async def _serve_inner(self, req: web.Request, chat: bool):
+        if self.opts.mm_encoder_only:
+            return _err(400, "this instance runs with --mm-encoder-only: it serves /v1/encode, not generation")
         try:
             body = await req.json()
         except Exception:  # noqa: BLE001
@@ -231,6 +286,7 @@ class OpenAIServer:
                 prompts = [ids0]
             else:
                 prompts = [self._chat_ids(body)] if chat else self._prompt_ids(body)
+            tools_on = chat and self._tools_active(body)
             params = SamplingParams.from_openai(body, default_max=16 if not chat else
                                                 max(1, self.cfg.sched.max_model_len - 1))
         except (ValueError, TypeError) as e:
@@ -255,7 +311,7 @@ class OpenAIServer:
         model_name = body.get("model") or self.name
         if stream:
             return await self._stream(req, rid_base, prompts[0], params, prio, ktp, lora, chat, include_usage,
-                                      created, model_name, mm)
+                                      created, model_name, mm, tools_on)
         # non-streaming: run all prompts concurrently
         async def one(i, ids):
             text_ids, lps, last = [], [], None
@@ -291,7 +347,15 @@ class OpenAIServer:
                 out_ktp = last.kv_transfer_params
             ch = {"index": i, "finish_reason": finish}
             if chat:
-                ch["message"] = {"role": "assistant", "content": text}
+                msg = {"role": "assistant", "content": text}
+                if self.parser is not None:
+                    r, c, calls = self.parser.extract(text, use_tools=tools_on)
+                    msg = {"role": "assistant", "content": c, "tool_calls": calls}
+                    if self.parser.reasoning is not None:
+                        msg["reasoning_content"] = r
+                    if calls:
+                        ch["finish_reason"] = "tool_calls"
+                ch["message"] = msg
             else:
                 ch["text"] = text
                 if params.logprobs:
@@ -308,7 +372,7 @@ class OpenAIServer:
         return web.json_response(resp)
 
     async def _stream(self, req, rid, ids, params, prio, ktp, lora, chat, include_usage, created, model_name,
-                      mm=None):
+                      mm=None, tools_on=False):
         resp = web.StreamResponse(headers={"Content-Type": "text/event-stream", "Cache-Control": "no-cache"})
         await resp.prepare(req)
         obj = "chat.completion.chunk" if chat else "text_completion"
@@ -325,11 +389,17 @@ class OpenAIServer:
                                      "finish_reason": None}]})
         finish = None
         last = None
+        st = self.parser.streamer(tools_on) if (chat and self.parser is not None) else None
+        every = max(1, int(self.opts.stream_interval))
+        n_emitted = 0
         try:
             async for o in self.aeng.generate(rid, ids, params, prio, ktp, lora, mm):
                 last = o
                 toks.extend(o.new_token_ids)
                 n_out = len(toks)
+                if not o.finished and n_out - n_emitted < every:  # --stream-interval
+                    continue
+                n_emitted = n_out
                 text = self.tok.decode(toks)
                 stop_hit = False
                 if params.stop:
@@ -340,6 +410,25 @@ class OpenAIServer:
                 delta = text[len(sent):] if text.startswith(sent) else text
                 sent = text
                 finish = "stop" if stop_hit else (o.finish_reason if o.finished else None)
+                if st is not None:  # reasoning / tool-call parsing: parsed deltas, then the final chunk
+                    deltas = st.feed(text)
+                    if finish is not None:
+                        tail, called = st.finish()
+                        deltas += tail
+                        if called:
+                            finish = "tool_calls"
+                    for k, dl in enumerate(deltas):
+                        last_one = k == len(deltas) - 1
+                        await send({"id": rid, "object": obj, "created": created, "model": model_name,
+                                    "choices": [{"index": 0, "delta": dl,
+                                                 "finish_reason": finish if last_one else None}]})
+                    if finish is not None and not deltas:
+                        await send({"id": rid, "object": obj, "created": created, "model": model_name,
+                                    "choices": [{"index": 0, "delta": {}, "finish_reason": finish}]})
+                    if stop_hit:
+                        self.aeng.abort(rid)
+                        break
+                    continue
                 ch = {"index": 0, "finish_reason": finish}
                 if chat:
                     ch["delta"] = {"content": delta}
@@ -513,7 +602,7 @@ class OpenAIServer:
                 msgs.append({"role": m.get("role", "user"), "content": c or ""})
         else:
             return _err(400, "input is required")
-        ids = self.tok.encode(render_chat(msgs, True, self.chat_style))
+        ids = self.tok.encode(self.template.render(msgs, True))
         params = SamplingParams.from_openai(dict(body, max_tokens=body.get("max_output_tokens")),
                                             default_max=max(1, self.cfg.sched.max_model_len - len(ids) - 1))
         toks, last = await self._run_one(req, ids, params, lora=self._lora_id(body))
@@ -705,12 +794,12 @@ class OpenAIServer:
         return web.Response(text=f"Success: LoRA adapter '{body['lora_name']}' removed successfully.")
 
 
-def build_server(cfg: EngineConfig, engine=None):
+def build_server(cfg: EngineConfig, engine=None, opts: Optional[ServingOptions] = None):
     from llmd_amd.engine.engine import LLMEngine
 
     eng = engine or LLMEngine(cfg)
     aeng = AsyncEngine(eng)
-    srv = OpenAIServer(aeng, cfg, lora_manager=eng.lora)
+    srv = OpenAIServer(aeng, cfg, lora_manager=eng.lora, opts=opts)
     if cfg.kv_events_config and cfg.kv_events_config.get("enable_kv_cache_events"):
         from .kv_events import KVEventPublisher
 
@@ -722,15 +811,97 @@ def build_server(cfg: EngineConfig, engine=None):
     return srv
 
 
+def add_serving_args(p: argparse.ArgumentParser) -> argparse.ArgumentParser:
+    """Front-end flags with vLLM's names (chat template, parsers, streaming,
+    multimodal roles, tracing), plus logging flags accepted for compatibility."""
+    p.add_argument("--chat-template", default=None, help="Jinja chat template (file or inline)")
+    p.add_argument("--enable-auto-tool-choice", action="store_true")
+    p.add_argument("--tool-call-parser", default=None, help="hermes | llama3_json | mistral | pythonic | openai")
+    p.add_argument("--reasoning-parser", default=None, help="deepseek_r1 | qwen3 | granite | openai_gptoss")
+    p.add_argument("--stream-interval", type=int, default=1, help="stream every N generated tokens")
+    p.add_argument("--limit-mm-per-prompt", type=_json_arg_safe, default=None, help='e.g. {"image": 4}')
+    p.add_argument("--mm-encoder-only", action="store_true",
+                   help="encode role: serve /v1/encode + /v1/ec only (E/PD encoder worker)")
+    p.add_argument("--language-model-only", action="store_true",
+                   help="never run the local vision tower: image embeddings come from encode workers")
+    p.add_argument("--ec-transfer-config", type=_json_arg_safe, default=None,
+                   help='{"ec_connector": ..., "ec_role": "ec_producer" | "ec_consumer"}')
+    p.add_argument("--mm-processor-cache-gb", type=float, default=None, help="encoder-cache size (GiB)")
+    p.add_argument("--otlp-traces-endpoint", default=None)
+    p.add_argument("--collect-detailed-traces", default=None,
+                   help="model / worker / all: also emit roctx ranges for the engine phases")
+    p.add_argument("--api-server-count", type=int, default=1)
+    p.add_argument("--numa-bind", action="store_true", help="pin this process to its GPU's NUMA node")
+    for f in ("--disable-access-log-for-endpoints", "--uvicorn-access-log-exclude-prefixes"):
+        p.add_argument(f, default=None, help=argparse.SUPPRESS)
+    p.add_argument("--disable-uvicorn-access-log", action="store_true", help=argparse.SUPPRESS)
+    return p
+
+
+def _json_arg_safe(s):
+    return json.loads(s) if s else None
+
+
+def serving_options_from_args(a) -> ServingOptions:
+    if a.tool_call_parser or a.reasoning_parser:
+        ChatOutputParser(a.reasoning_parser, a.tool_call_parser)  # validate names at start-up
+    if a.enable_auto_tool_choice and not a.tool_call_parser:
+        raise SystemExit("--enable-auto-tool-choice requires --tool-call-parser")
+    ec = a.ec_transfer_config or {}
+    if ec and ec.get("ec_role") not in (None, "ec_producer", "ec_consumer", "ec_both"):
+        raise SystemExit(f"--ec-transfer-config: unknown ec_role {ec.get('ec_role')!r}")
+    return ServingOptions(chat_template=a.chat_template, enable_auto_tool_choice=a.enable_auto_tool_choice,
+                          tool_call_parser=a.tool_call_parser, reasoning_parser=a.reasoning_parser,
+                          stream_interval=max(1, a.stream_interval), limit_mm_per_prompt=a.limit_mm_per_prompt,
+                          mm_encoder_only=a.mm_encoder_only)
+
+
+def _numa_bind(device_index: int):
+    """Pin the process to the CPUs of the GPU's NUMA node (sysfs; best effort)."""
+    import glob
+
+    try:
+        import torch
+
+        bus = torch.cuda.get_device_properties(device_index).pci_bus_id
+        node = int(open(glob.glob(f"/sys/bus/pci/devices/*{bus:02x}:00.0/numa_node")[0]).read())
+        if node < 0:
+            return
+        cpus = open(f"/sys/devices/system/node/node{node}/cpulist").read().strip()
+        sel = set()
+        for part in cpus.split(","):
+            lo, _, hi = part.partition("-")
+            sel.update(range(int(lo), int(hi or lo) + 1))
+        os.sched_setaffinity(0, sel)
+        log.info("numa-bind: GPU %d -> node %d (%d CPUs)", device_index, node, len(sel))
+    except Exception as e:  # noqa: BLE001
+        log.warning("numa-bind skipped: %s", e)
+
+
 def main(argv=None):
     p = argparse.ArgumentParser("llmd-amd serve")
     add_engine_args(p)
+    add_serving_args(p)
     p.add_argument("--host", default="0.0.0.0")
     p.add_argument("--port", type=int, default=8000)
     p.add_argument("--shutdown-timeout", type=float, default=0.0)
     p.add_argument("--log-level", default="info")
     a = p.parse_args(argv)
     logging.basicConfig(level=a.log_level.upper(), format="%(asctime)s %(levelname)s %(name)s: %(message)s")
+    opts = serving_options_from_args(a)
+    if a.otlp_traces_endpoint:
+        from llmd_amd.utils import tracing
+
+        tracing.configure_otlp(a.otlp_traces_endpoint)
+    if a.collect_detailed_traces:
+        os.environ.setdefault("LLMD_ROCTX", "1")
+    if a.api_server_count != 1:
+        log.warning("--api-server-count %d: one API server process per engine here (asyncio front end)",
+                    a.api_server_count)
+    for f in ("attention_backend", "moe_backend"):
+        if getattr(a, f, None):
+            log.info("--%s %s ignored: the attention / MoE kernels are this repo's HIP kernels",
+                     f.replace("_", "-"), getattr(a, f))
     cfg = engine_config_from_args(a)
     port = a.port
     pc = cfg.parallel
@@ -743,6 +914,10 @@ def main(argv=None):
         if st.dp_size != pc.data_parallel_size:
             raise SystemExit(f"WORLD_SIZE {st.world_size} != --tensor-parallel-size {pc.tensor_parallel_size} x "
                              f"--data-parallel-size {pc.data_parallel_size}")
+        local_dp = int(os.environ.get("LOCAL_WORLD_SIZE", st.world_size)) // pc.tensor_parallel_size
+        if a.data_parallel_size_local is not None and a.data_parallel_size_local != local_dp:
+            raise SystemExit(f"--data-parallel-size-local {a.data_parallel_size_local} != {local_dp} local DP "
+                             "ranks under torchrun")
         if pc.data_parallel_size > 1:
             port = dp_rank_port(cfg, a.port, st.dp_rank)
         if st.tp_rank != 0:
@@ -750,7 +925,16 @@ def main(argv=None):
 
             run_follower(cfg, capture_graphs=not cfg.enforce_eager)
             return
-    srv = build_server(cfg)
+    if a.numa_bind and cfg.device == "cuda":
+        import torch
+
+        _numa_bind(torch.cuda.current_device() if torch.cuda.is_initialized() else 0)
+    srv = build_server(cfg, opts=opts)
+    if srv.mm is not None:
+        if a.language_model_only:
+            srv.mm.has_tower = False
+        if a.mm_processor_cache_gb:
+            srv.mm.cache.max_bytes = int(a.mm_processor_cache_gb * (1 << 30))
     app = srv.app()
 
     async def on_shutdown(_app):

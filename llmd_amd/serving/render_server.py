@@ -23,20 +23,22 @@ from aiohttp import web
 
 from llmd_amd.engine.config import get_model_config
 
-from .tokenizer import load_tokenizer, render_chat
+from .chat_template import ChatTemplate, render_tools, style_for
+from .tokenizer import load_tokenizer
 
 log = logging.getLogger("llmd.render")
 
 
 class RenderServer:
     def __init__(self, model: str, tokenizer: str | None = None, served_name: str | None = None,
-                 max_model_len: int = 32768):
+                 max_model_len: int = 32768, chat_template: str | None = None, enable_auto_tool_choice: bool = False):
         mc = get_model_config(model)
         self.mc = mc
         self.name = served_name or model
         self.max_model_len = max_model_len
         self.tok = load_tokenizer(tokenizer, mc.vocab_size, mc.bos_token_id, mc.eos_ids[0])
-        self.style = "llama3" if mc.model_type in ("llama", "llava") else "chatml"
+        self.template = ChatTemplate(style_for(mc.model_type), model_dir=tokenizer, template=chat_template)
+        self.auto_tools = enable_auto_tool_choice
         self.n = 0
 
     def app(self) -> web.Application:
@@ -84,13 +86,15 @@ class RenderServer:
         msgs = body.get("messages")
         if not isinstance(msgs, list) or not msgs:
             return web.json_response({"error": {"message": "messages is required", "code": 400}}, status=400)
-        ids = self.tok.encode(render_chat(msgs, body.get("add_generation_prompt", True), self.style))
+        ids = self.tok.encode(self.template.render(msgs, body.get("add_generation_prompt", True),
+                                                   tools=render_tools(body, self.auto_tools)))
         return self._resp(body, ids)
 
     async def tokenize(self, req):
         body = await req.json()
         if "messages" in body:
-            ids = self.tok.encode(render_chat(body["messages"], body.get("add_generation_prompt", True), self.style))
+            ids = self.tok.encode(self.template.render(body["messages"], body.get("add_generation_prompt", True),
+                                                       tools=render_tools(body, self.auto_tools)))
         else:
             ids = self._prompt(body.get("prompt", ""))
         return web.json_response({"tokens": ids, "count": len(ids), "max_model_len": self.max_model_len})
@@ -106,11 +110,15 @@ def main(argv=None):
     p.add_argument("--tokenizer", default=None)
     p.add_argument("--served-model-name", default=None)
     p.add_argument("--max-model-len", type=int, default=32768)
+    p.add_argument("--chat-template", default=None)
+    p.add_argument("--enable-auto-tool-choice", action="store_true",
+                   help="render tools when a request omits tool_choice (match the engine's flag)")
     p.add_argument("--host", default="0.0.0.0")
     p.add_argument("--port", type=int, default=8300)
     a = p.parse_args(argv)
     logging.basicConfig(level="INFO")
-    srv = RenderServer(a.model, a.tokenizer, a.served_model_name, a.max_model_len)
+    srv = RenderServer(a.model, a.tokenizer, a.served_model_name, a.max_model_len, a.chat_template,
+                       a.enable_auto_tool_choice)
     web.run_app(srv.app(), host=a.host, port=a.port, access_log=None)
 
 

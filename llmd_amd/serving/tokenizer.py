@@ -71,25 +71,9 @@ def load_tokenizer(path: Optional[str], vocab_size: int, bos: int = 1, eos: int 
     return ByteTokenizer(vocab_size, bos_id=bos if bos < 3 else 1, eos_id=eos if eos < 3 else 2)
 
 
-def render_chat(messages: list[dict], add_generation_prompt: bool = True, style: str = "llama3") -> str:
-    """Minimal built-in chat templates (Jinja templates from tokenizer_config
-    are not evaluated: no jinja2 dependency)."""
-    out = []
-    if style == "llama3":
-        out.append("<|begin_of_text|>")
-        for m in messages:
-            content = m.get("content") or ""
-            if isinstance(content, list):
-                content = "".join(p.get("text", "") for p in content if isinstance(p, dict))
-            out.append(f"<|start_header_id|>{m['role']}<|end_header_id|>\n\n{content}<|eot_id|>")
-        if add_generation_prompt:
-            out.append("<|start_header_id|>assistant<|end_header_id|>\n\n")
-    else:
-        for m in messages:
-            content = m.get("content") or ""
-            if isinstance(content, list):
-                content = "".join(p.get("text", "") for p in content if isinstance(p, dict))
-            out.append(f"<|im_start|>{m['role']}\n{content}<|im_end|>\n")
-        if add_generation_prompt:
-            out.append("<|im_start|>assistant\n")
-    return "".join(out)
+def render_chat(messages: list[dict], add_generation_prompt: bool = True, style: str = "llama3",
+                tools=None) -> str:
+    """Built-in chat template of one model family (``serving/chat_template.py``)."""
+    from .chat_template import BUILTIN
+
+    return BUILTIN[style](messages, add_generation_prompt, tools)

@@ -29,13 +29,25 @@ SAMPLE_RATIO = float(os.environ.get("OTEL_TRACES_SAMPLER_ARG", "0.1"))
 ENABLED = os.environ.get("LLMD_TRACING", "1") != "0"
 
 _otel_tracer = None
-if os.environ.get("OTEL_EXPORTER_OTLP_ENDPOINT"):
+
+
+def configure_otlp(endpoint: Optional[str] = None):
+    """Export spans over OTLP (``--otlp-traces-endpoint`` / OTEL_EXPORTER_OTLP_ENDPOINT)
+    when the OpenTelemetry SDK is importable; the in-process ring always records."""
+    global _otel_tracer
+    if endpoint:
+        os.environ["OTEL_EXPORTER_OTLP_ENDPOINT"] = endpoint
+    if not os.environ.get("OTEL_EXPORTER_OTLP_ENDPOINT"):
+        return
     try:  # pragma: no cover - optional dependency
         from opentelemetry import trace as _ot
 
         _otel_tracer = _ot.get_tracer("llmd-amd")
     except Exception:  # noqa: BLE001
         _otel_tracer = None
+
+
+configure_otlp()
 
 
 @dataclass
