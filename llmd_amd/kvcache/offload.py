@@ -177,6 +177,21 @@ class OffloadManager:
     def after_step(self):
         self.poll()
 
+    def render_metrics(self, model: str) -> bytes:
+        """Tier traffic counters (blocks) and host-tier occupancy."""
+        lab = f'model_name="{model}"'
+        st = self.stats
+        lines = ["# HELP llmd:kv_offload_blocks_total KV blocks moved by the offload tiers",
+                 "# TYPE llmd:kv_offload_blocks_total counter",
+                 f'llmd:kv_offload_blocks_total{{{lab},op="store_cpu"}} {st["offloaded"]}',
+                 f'llmd:kv_offload_blocks_total{{{lab},op="load_cpu"}} {st["loaded_cpu"]}',
+                 f'llmd:kv_offload_blocks_total{{{lab},op="load_fs"}} {st["loaded_fs"]}',
+                 f'llmd:kv_offload_blocks_total{{{lab},op="evict_cpu"}} {st["evicted_cpu"]}',
+                 "# HELP llmd:kv_offload_cpu_usage_perc Host-tier slots in use",
+                 "# TYPE llmd:kv_offload_cpu_usage_perc gauge",
+                 f"llmd:kv_offload_cpu_usage_perc{{{lab}}} {len(self.slot_of) / max(1, self.n_slots):.6f}"]
+        return ("\n".join(lines) + "\n").encode()
+
     def take_events(self) -> list:
         out, self.events_out = self.events_out, []
         return out

@@ -808,6 +808,8 @@ def build_server(cfg: EngineConfig, engine=None, opts: Optional[ServingOptions] 
         srv.kv_event_publisher = pub
     if eng.connector is not None:
         srv.extra_metrics.append(eng.connector.render_metrics)
+    if eng.offload is not None:
+        srv.extra_metrics.append(lambda: eng.offload.render_metrics(cfg.served_name))
     return srv
 
 

@@ -147,6 +147,14 @@ def _wait(url, procs, timeout):
     return False
 
 
+def _offload_loads(ports):
+    n = 0.0
+    for port in ports:
+        m = parse_prometheus(_get(f"http://127.0.0.1:{port}/metrics", 5) or "")
+        n += sum(v for lab, v in m.get("llmd:kv_offload_blocks_total", []) if lab.get("op", "").startswith("load"))
+    return n
+
+
 def _prefix_counters(ports):
     hits = queries = 0.0
     for port in ports:
@@ -176,6 +184,7 @@ def main():
     ap.add_argument("--router-port", type=int, default=18100)
     ap.add_argument("--out", default=os.path.join(ROOT, "gpurun_out", "e2e_serving.json"))
     ap.add_argument("--extra-engine-args", default="")
+    ap.add_argument("--kv-offload-gb", type=float, default=0.0, help="host-DRAM KV tier per replica")
     a = ap.parse_args()
 
     from llmd_amd.engine.config import get_model_config
@@ -193,6 +202,8 @@ def main():
                "--max-model-len", str(a.system_len + a.question_len + a.output_len + 64),
                "--kv-events-config", json.dumps({"enable_kv_cache_events": True, "publisher": "zmq",
                                                  "endpoint": f"tcp://*:{a.kv_events_port_base + i}"})] + \
+            (["--kv-offload-config", json.dumps({"cpu_bytes_to_use": int(a.kv_offload_gb * (1 << 30))})]
+             if a.kv_offload_gb > 0 else []) + \
             a.extra_engine_args.split()
         log = open(os.path.join(ROOT, "gpurun_out", f"e2e_engine{i}.log"), "w")
         logs.append(log)
@@ -206,6 +217,7 @@ def main():
     with open(ep_file, "w") as f:
         yaml.safe_dump(eps, f)
     results = {"model": a.model, "replicas": a.replicas, "device": a.device, "blocks_per_replica": a.blocks,
+               "kv_offload_gb": a.kv_offload_gb,
                "workload": {"groups": a.groups, "per_group": a.per_group, "system_len": a.system_len,
                             "question_len": a.question_len, "output_len": a.output_len,
                             "concurrency": a.concurrency, "requests": a.requests}, "runs": {}}
@@ -235,6 +247,7 @@ def main():
                     raise RuntimeError("router not ready")
                 time.sleep(2)  # first metrics scrape of every endpoint
                 h0, q0 = _prefix_counters(ports)
+                l0 = _offload_loads(ports)
                 cfg = {"load": {"type": "concurrent", "stages": [{"concurrency": a.concurrency,
                                                                   "num_requests": a.requests}]},
                        "api": {"type": "completion"},
@@ -248,6 +261,7 @@ def main():
                 rep = asyncio.run(loadgen.run(cfg, vocab=vocab, seed=1))
                 wall = time.time() - t0
                 h1, q1 = _prefix_counters(ports)
+                l1 = _offload_loads(ports)
                 s = rep["summary"]
                 out = {"wall_s": wall, "requests": s["requests"]["total"], "failures": s["requests"]["failures"],
                        "output_tok_s": s["throughput"]["output_tokens_per_sec"],
@@ -255,7 +269,8 @@ def main():
                        "ttft_p50_s": s["latency"]["time_to_first_token"]["p50"],
                        "ttft_p90_s": s["latency"]["time_to_first_token"]["p90"],
                        "itl_p50_s": s["latency"]["inter_token_latency"]["p50"],
-                       "prefix_hit_rate": (h1 - h0) / (q1 - q0) if q1 > q0 else None}
+                       "prefix_hit_rate": (h1 - h0) / (q1 - q0) if q1 > q0 else None,
+                       "offload_blocks_loaded": l1 - l0}
                 results["runs"][name if name not in results["runs"] else f"{name}#{run_i}"] = out
                 print(f"[e2e] {name}: " + json.dumps(out), flush=True)
             finally:
