@@ -309,6 +309,13 @@ class Scheduler:
                         self._finish(r, Status.FINISHED_ERROR)
                         self.errored.append(r)
                         continue
+                else:
+                    # wait holding nothing: a waiting request that keeps its prefix (or
+                    # host-reloaded) blocks can starve a preempted request queued ahead
+                    # of it, and neither ever runs. Its next admission re-acquires the
+                    # prefix (GPU cache, then host tier).
+                    self.bm.free(r.seq_id)
+                    r.num_computed_tokens = 0
                 break
             self.waiting.pop()
             r.status = Status.RUNNING

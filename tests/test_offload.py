@@ -48,3 +48,27 @@ def test_fs_tier_survives_restart(tmp_path):
     eng2 = make_engine(kv_offload_config=cfg)  # fresh engine, empty GPU + host tiers
     assert _gen(eng2, _prompt(3)) == base
     assert eng2.offload.stats["loaded_fs"] >= 150 // 16 - 1
+
+
+def test_host_reload_retried_when_pool_was_full():
+    """A request whose prefix is in the host tier but arrives while the GPU
+    pool is full gets its reload when it is admitted later (not a from-scratch
+    prefill), and generates the same tokens."""
+    p, blocker = _prompt(11, 96), _prompt(12, 150)
+    sp = SamplingParams(max_tokens=8, temperature=0.0, ignore_eos=True)
+    base = _gen(make_engine(num_gpu_blocks=16), p)
+    eng = make_engine(num_gpu_blocks=16, kv_offload_config={"cpu_bytes_to_use": 64 << 20})
+    assert _gen(eng, p) == base                  # p's blocks are written through to the host tier
+    eng.reset_prefix_cache()
+    eng.add_request("blocker", blocker, SamplingParams(max_tokens=40, temperature=0.0, ignore_eos=True))
+    eng.step()                                   # blocker takes 10+ of the 16 blocks
+    eng.add_request("again", p, sp)
+    outs = {"again": [], "blocker": []}
+    for _ in range(500):
+        if not eng.has_unfinished():
+            break
+        for o in eng.step():
+            outs[o.request_id] += o.new_token_ids
+    assert not eng.has_unfinished()  # a waiting request holding blocks used to deadlock here
+    assert outs["again"] == base
+    assert eng.offload.stats["loaded_cpu"] >= 96 // 16 - 1
