@@ -186,7 +186,15 @@ def summarize(results: list[Result], duration: float) -> dict:
 
 
 # ------------------------------------------------------------------ runner
-async def run(cfg: dict, vocab: int = 32000, seed: int = 0) -> dict:
+def per_request(results: list[Result], stage: int) -> list[dict]:
+    """inference-perf style per-request lifecycle records."""
+    return [{"stage": stage, "start_time": r.t_start, "end_time": r.t_start + r.e2e, "ok": r.ok,
+             "error": r.err or None, "prompt_tokens": r.n_in, "output_tokens": r.n_out,
+             "time_to_first_token": r.ttft if r.ok else None, "inter_token_latencies": r.itls,
+             "request_latency": r.e2e if r.ok else None} for r in results]
+
+
+async def run(cfg: dict, vocab: int = 32000, seed: int = 0, records: bool = False) -> dict:
     import aiohttp
 
     load, server, api = cfg.get("load", {}), cfg["server"], cfg.get("api", {}).get("type", "completion")
@@ -196,6 +204,7 @@ async def run(cfg: dict, vocab: int = 32000, seed: int = 0) -> dict:
     data = make_data(cfg.get("data", {}), vocab, seed)
     rng = random.Random(seed)
     stages_out = []
+    recs: list[dict] = []
     all_res: list[Result] = []
     t_all = time.perf_counter()
     conn = aiohttp.TCPConnector(limit=0)
@@ -233,9 +242,14 @@ async def run(cfg: dict, vocab: int = 32000, seed: int = 0) -> dict:
                 await asyncio.gather(*tasks)
             dt = time.perf_counter() - t0
             stages_out.append({"stage": i, "config": st, **summarize(res, dt)})
+            if records:
+                recs += per_request(res, i)
             all_res += res
-    return {"version": "0.1", "harness": "llmd-loadgen", "scenario": cfg, "stages": stages_out,
-            "summary": summarize(all_res, time.perf_counter() - t_all)}
+    out = {"version": "0.1", "harness": "llmd-loadgen", "scenario": cfg, "stages": stages_out,
+           "summary": summarize(all_res, time.perf_counter() - t_all)}
+    if records:
+        out["per_request"] = recs
+    return out
 
 
 def main(argv=None):

@@ -91,3 +91,45 @@ def test_loadgen_random_and_shared_prefix(sim):
     assert st["requests"]["total"] == 12 and st["requests"]["failures"] == 0
     # multi-turn: second-round prompts carry the previous turn
     assert st["requests"]["input_length"]["max"] > 64 + 16
+
+
+def test_benchmark_cli_workspace_and_reports(sim, tmp_path):
+    """llmdbenchmark-style run against the simulator: every shipped profile
+    renders; a shared-prefix ladder (overridden to 2 short stages) writes the
+    reference's results layout with per-stage / summary / per-request files
+    and cross-harness benchmark reports."""
+    import json as _json
+
+    import yaml as _yaml
+
+    from llmd_amd.tools import benchmark
+
+    names = benchmark.list_workloads()
+    assert {"sanity_random.yaml", "shared_prefix_synthetic.yaml", "guide_optimized-baseline_1.yaml",
+            "guide_pd-disaggregation_1.yaml"} <= set(names)
+    for n in names:
+        cfg = benchmark.render(benchmark.load_profile(n)[1], "http://x:1", "m")
+        assert cfg["server"]["base_url"] == "http://x:1" and cfg["server"]["model_name"] == "m"
+        assert cfg["load"]["stages"] and cfg["data"]["type"] in ("random", "shared_prefix")
+    ov = benchmark.apply_overrides({"load": {"stages": [{"rate": 1}]}}, "load.stages.0.rate=5,data.x.y=true")
+    assert ov == {"load": {"stages": [{"rate": 5}]}, "data": {"x": {"y": True}}}
+    rc = benchmark.main(["--workspace", str(tmp_path), "--spec", "guides/optimized-baseline", "run",
+                         "--endpoint-url", f"http://127.0.0.1:{sim.port}", "--model", "m",
+                         "--workload", "shared_prefix_synthetic_short.yaml", "--vocab", "1000", "--analyze",
+                         "--overrides", "load.stages=[{rate: 20, duration: 1}, {rate: 40, duration: 1}],"
+                                        "data.shared_prefix.output_len=8"])
+    assert rc == 0
+    (runner,) = list(tmp_path.glob("runner-*"))
+    (res,) = list((runner / "results").iterdir())
+    files = {p.name for p in res.iterdir()}
+    assert {"stage_0_lifecycle_metrics.json", "stage_1_lifecycle_metrics.json", "summary_lifecycle_metrics.json",
+            "per_request_lifecycle_metrics.json", "benchmark_report,_stage_0.yaml", "benchmark_report,_stage_1.yaml",
+            "config.yaml", "stdout.log", "analysis"} <= files
+    rep = _yaml.safe_load((res / "benchmark_report,_stage_1.yaml").read_text())
+    assert rep["scenario"]["load"]["config"]["rate"] == 40
+    assert rep["metrics"]["requests"]["failures"] == 0 and rep["metrics"]["throughput"]["output_tokens_per_sec"] > 0
+    per = _json.loads((res / "per_request_lifecycle_metrics.json").read_text())
+    assert len(per) == rep["metrics"]["requests"]["total"] + _yaml.safe_load(
+        (res / "benchmark_report,_stage_0.yaml").read_text())["metrics"]["requests"]["total"]
+    assert all(r["output_tokens"] == 8 for r in per)
+    assert list((res / "analysis" / "distributions").glob("dist_ttft.png"))
