@@ -185,6 +185,8 @@ def main():
     ap.add_argument("--out", default=os.path.join(ROOT, "gpurun_out", "e2e_serving.json"))
     ap.add_argument("--extra-engine-args", default="")
     ap.add_argument("--kv-offload-gb", type=float, default=0.0, help="host-DRAM KV tier per replica")
+    ap.add_argument("--workload", default=None, help="benchmark profile (llmd_amd/tools/workloads) to run instead")
+    ap.add_argument("--overrides", default="", help="benchmark profile overrides (k=v,...)")
     a = ap.parse_args()
 
     from llmd_amd.engine.config import get_model_config
@@ -257,9 +259,24 @@ def main():
                                 "shared_prefix": {"num_groups": a.groups, "num_prompts_per_group": a.per_group,
                                                   "system_prompt_len": a.system_len,
                                                   "question_len": a.question_len, "output_len": a.output_len}}}
+                if a.workload:  # a shipped benchmark profile (llmd_amd.tools.benchmark) instead
+                    from llmd_amd.tools import benchmark
+
+                    _, text = benchmark.load_profile(a.workload)
+                    cfg = benchmark.apply_overrides(
+                        benchmark.render(text, f"http://127.0.0.1:{a.router_port}", a.model), a.overrides)
                 t0 = time.time()
                 rep = asyncio.run(loadgen.run(cfg, vocab=vocab, seed=1))
                 wall = time.time() - t0
+                if a.workload:
+                    results.setdefault("stages", {})[name] = [
+                        {"config": st["config"], "output_tok_s": st["throughput"]["output_tokens_per_sec"],
+                         "req_s": st["throughput"]["requests_per_sec"], "failures": st["requests"]["failures"],
+                         "ttft_mean_s": st["latency"]["time_to_first_token"]["mean"],
+                         "ttft_p90_s": st["latency"]["time_to_first_token"]["p90"],
+                         "itl_mean_s": st["latency"]["inter_token_latency"]["mean"]} for st in rep["stages"]]
+                    for st in results["stages"][name]:
+                        print(f"[e2e] {name} stage " + json.dumps(st), flush=True)
                 h1, q1 = _prefix_counters(ports)
                 l1 = _offload_loads(ports)
                 s = rep["summary"]
