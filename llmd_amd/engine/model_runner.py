@@ -436,10 +436,64 @@ class ModelRunner:
         self._last_hidden = hs if pl.get("embed") else None
         return self.model.compute_logits(hs)
 
+    def _penalize(self, logits, reqs):
+        """Presence / frequency / repetition penalties, logit bias and min-p for
+        the rows whose requests ask for them (one scatter per kind; rows
+        without them are untouched, so ordinary steps pay nothing)."""
+        logits = logits.float()
+        dev = logits.device
+        pr, pt, pv, rr, rt, rv = [], [], [], [], [], []
+        mp_rows, mp_vals, mp_temps = [], [], []
+        for i, r in enumerate(reqs):
+            sp = r.params
+            if not sp.penalized:
+                continue
+            out = np.asarray(r.output_token_ids, dtype=np.int64)
+            if (sp.presence_penalty or sp.frequency_penalty) and out.size:
+                toks, cnt = np.unique(out, return_counts=True)
+                pr.append(np.full(toks.size, i))
+                pt.append(toks)
+                pv.append(sp.frequency_penalty * cnt + sp.presence_penalty)
+            if sp.logit_bias:
+                toks = np.fromiter(sp.logit_bias.keys(), dtype=np.int64)
+                pr.append(np.full(toks.size, i))
+                pt.append(toks)
+                pv.append(-np.fromiter(sp.logit_bias.values(), dtype=np.float64))
+            if sp.repetition_penalty != 1.0:
+                seen = np.unique(np.concatenate([np.asarray(r.prompt_token_ids, dtype=np.int64), out]))
+                rr.append(np.full(seen.size, i))
+                rt.append(seen)
+                rv.append(np.full(seen.size, sp.repetition_penalty))
+            if sp.min_p > 0.0:
+                mp_rows.append(i)
+                mp_vals.append(sp.min_p)
+                mp_temps.append(max(sp.temperature, 1e-5))
+        if rr:
+            ri = torch.from_numpy(np.concatenate(rr)).to(dev)
+            ti = torch.from_numpy(np.concatenate(rt)).to(dev)
+            rp = torch.from_numpy(np.concatenate(rv)).to(dev, torch.float32)
+            cur = logits[ri, ti]
+            logits[ri, ti] = torch.where(cur > 0, cur / rp, cur * rp)
+        if pr:
+            ri = torch.from_numpy(np.concatenate(pr)).to(dev)
+            ti = torch.from_numpy(np.concatenate(pt)).to(dev)
+            logits.index_put_((ri, ti), -torch.from_numpy(np.concatenate(pv)).to(dev, torch.float32),
+                              accumulate=True)
+        if mp_rows:
+            rows = torch.tensor(mp_rows, device=dev)
+            sub = logits.index_select(0, rows) / torch.tensor(mp_temps, device=dev).unsqueeze(1)
+            pr_ = torch.softmax(sub, dim=-1)
+            thr = pr_.max(dim=-1, keepdim=True).values * torch.tensor(mp_vals, device=dev).unsqueeze(1)
+            keep = logits.index_select(0, rows).masked_fill(pr_ < thr, float("-inf"))
+            logits.index_copy_(0, rows, keep)
+        return logits
+
     def _sample(self, logits, reqs):
         temps, seeds, topk, topp, any_rand, any_k, any_p = self._sampling_tensors(reqs)
         want_lp = any(r.params.logprobs for r in reqs)
         dev = self.device
+        if any(r.params.penalized for r in reqs):
+            logits = self._penalize(logits, reqs)
         if any_k or any_p:
             logits = logits.float()
             ops.topk_topp_mask(logits, torch.from_numpy(topk).to(dev) if any_k else None,

@@ -22,6 +22,16 @@ class SamplingParams:
     logprobs: Optional[int] = None
     n: int = 1
     embed: bool = False  # /v1/embeddings: keep the final hidden state of the last prompt token
+    presence_penalty: float = 0.0      # OpenAI: - p for every token already generated
+    frequency_penalty: float = 0.0     # OpenAI: - f x count of the token in the output
+    repetition_penalty: float = 1.0    # vLLM/HF: logits of prompt+output tokens / r (if > 0) or x r
+    min_p: float = 0.0                 # drop tokens with prob < min_p x max prob
+    logit_bias: Optional[dict] = None  # token id -> additive bias
+
+    @property
+    def penalized(self) -> bool:
+        return bool(self.presence_penalty or self.frequency_penalty or self.repetition_penalty != 1.0
+                    or self.logit_bias or self.min_p > 0.0)
 
     @property
     def greedy(self) -> bool:
@@ -33,10 +43,14 @@ class SamplingParams:
         if isinstance(stop, str):
             stop = [stop]
         mt = body.get("max_completion_tokens", body.get("max_tokens"))
+
+        def g(k, d):
+            v = body.get(k)
+            return d if v is None else v
         return cls(
             max_tokens=int(mt) if mt is not None else default_max,
             temperature=float(body.get("temperature", 1.0) if body.get("temperature") is not None else 1.0),
-            top_p=float(body.get("top_p", 1.0) or 1.0),
+            top_p=float(g("top_p", 1.0)),
             top_k=int(body.get("top_k", 0) or 0),
             min_tokens=int(body.get("min_tokens", 0) or 0),
             seed=body.get("seed"),
@@ -45,7 +59,29 @@ class SamplingParams:
             ignore_eos=bool(body.get("ignore_eos", False)),
             logprobs=body.get("logprobs") if isinstance(body.get("logprobs"), int) else (
                 1 if body.get("logprobs") is True else None),
-        )
+            n=int(g("n", 1)),
+            presence_penalty=float(g("presence_penalty", 0.0)),
+            frequency_penalty=float(g("frequency_penalty", 0.0)),
+            repetition_penalty=float(g("repetition_penalty", 1.0)),
+            min_p=float(g("min_p", 0.0)),
+            logit_bias={int(k): float(v) for k, v in (body.get("logit_bias") or {}).items()} or None,
+        )._validated()
+
+    def _validated(self) -> "SamplingParams":
+        """OpenAI / vLLM ranges (ValueError -> HTTP 400)."""
+        if not -2.0 <= self.presence_penalty <= 2.0:
+            raise ValueError(f"presence_penalty must be in [-2, 2], got {self.presence_penalty}")
+        if not -2.0 <= self.frequency_penalty <= 2.0:
+            raise ValueError(f"frequency_penalty must be in [-2, 2], got {self.frequency_penalty}")
+        if self.repetition_penalty <= 0.0:
+            raise ValueError(f"repetition_penalty must be > 0, got {self.repetition_penalty}")
+        if not 0.0 <= self.min_p <= 1.0:
+            raise ValueError(f"min_p must be in [0, 1], got {self.min_p}")
+        if not 1 <= self.n <= 128:
+            raise ValueError(f"n must be in [1, 128], got {self.n}")
+        if self.max_tokens < 0 or self.temperature < 0 or not 0.0 < self.top_p <= 1.0:
+            raise ValueError("max_tokens and temperature must be >= 0 and top_p in (0, 1]")
+        return self
 
 
 class Status(enum.Enum):

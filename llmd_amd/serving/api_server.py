@@ -309,24 +309,29 @@ class OpenAIServer:
         include_usage = bool((body.get("stream_options") or {}).get("include_usage", False))
         created = int(time.time())
         model_name = body.get("model") or self.name
+        # one engine request per (prompt, sample): choice index = prompt * n + sample; the n
+        # samples of a prompt share its prefix blocks through prefix caching
+        jobs = [(ids, self._choice_params(params, j)) for ids in prompts for j in range(params.n)]
+        rids = [f"{rid_base}-{k}" if len(jobs) > 1 else rid_base for k in range(len(jobs))]
         if stream:
-            return await self._stream(req, rid_base, prompts[0], params, prio, ktp, lora, chat, include_usage,
-                                      created, model_name, mm, tools_on)
-        # non-streaming: run all prompts concurrently
-        async def one(i, ids):
+            if len(prompts) > 1:
+                return _err(400, "streaming supports a single prompt")
+            return await self._stream(req, rids, prompts[0], [pj for _, pj in jobs], prio, ktp, lora, chat,
+                                      include_usage, created, model_name, mm, tools_on, rid_base)
+
+        async def one(k, ids, pk):
             text_ids, lps, last = [], [], None
-            async for o in self.aeng.generate(f"{rid_base}-{i}" if len(prompts) > 1 else rid_base, ids, params,
-                                              prio, ktp, lora, mm):
+            async for o in self.aeng.generate(rids[k], ids, pk, prio, ktp, lora, mm):
                 text_ids.extend(o.new_token_ids)
                 lps.extend(o.new_logprobs)
                 last = o
                 text = self.tok.decode(text_ids)
-                if params.stop and any(s in text for s in params.stop):
-                    self.aeng.abort(f"{rid_base}-{i}" if len(prompts) > 1 else rid_base)
+                if pk.stop and any(s in text for s in pk.stop):
+                    self.aeng.abort(rids[k])
                     break
             return ids, text_ids, lps, last
         try:
-            results = await asyncio.gather(*[one(i, p) for i, p in enumerate(prompts)])
+            results = await asyncio.gather(*[one(k, ids, pk) for k, (ids, pk) in enumerate(jobs)])
         except EngineDeadError as e:
             return _err(503, str(e), "ServiceUnavailable")
         except Exception as e:  # noqa: BLE001
@@ -341,7 +346,8 @@ class OpenAIServer:
                     k = text.find(s)
                     if k >= 0:
                         text, finish = text[:k], "stop"
-            n_prompt += len(ids)
+            if i % params.n == 0:
+                n_prompt += len(ids)  # a prompt counts once however many samples it has
             n_out += len(toks)
             if last is not None and last.kv_transfer_params is not None:
                 out_ktp = last.kv_transfer_params
@@ -371,35 +377,49 @@ class OpenAIServer:
             resp["kv_transfer_params"] = out_ktp
         return web.json_response(resp)
 
-    async def _stream(self, req, rid, ids, params, prio, ktp, lora, chat, include_usage, created, model_name,
-                      mm=None, tools_on=False):
+    @staticmethod
+    def _choice_params(params: SamplingParams, j: int) -> SamplingParams:
+        """Sample j of an ``n > 1`` request: its own seed stream (seed + j when the
+        client fixed one, else a fresh random one per sample)."""
+        if params.n == 1:
+            return params
+        import dataclasses
+
+        return dataclasses.replace(params, seed=(params.seed + j) if params.seed is not None else None)
+
+    async def _stream(self, req, rids, ids, plist, prio, ktp, lora, chat, include_usage, created, model_name,
+                      mm=None, tools_on=False, rid=None):
+        """SSE stream of one prompt's ``n`` choices (chunks of different choices
+        interleave, each tagged with its ``index``)."""
+        rid = rid or rids[0]
         resp = web.StreamResponse(headers={"Content-Type": "text/event-stream", "Cache-Control": "no-cache"})
         await resp.prepare(req)
         obj = "chat.completion.chunk" if chat else "text_completion"
-        toks: list[int] = []
-        sent = ""
-        n_out = 0
+        wlock = asyncio.Lock()
+        n_outs = [0] * len(rids)
 
         async def send(d):
-            await resp.write(b"data: " + json.dumps(d).encode() + b"\n\n")
+            async with wlock:
+                await resp.write(b"data: " + json.dumps(d).encode() + b"\n\n")
 
-        if chat:
-            await send({"id": rid, "object": obj, "created": created, "model": model_name,
-                        "choices": [{"index": 0, "delta": {"role": "assistant", "content": ""},
-                                     "finish_reason": None}]})
-        finish = None
-        last = None
-        st = self.parser.streamer(tools_on) if (chat and self.parser is not None) else None
-        every = max(1, int(self.opts.stream_interval))
-        n_emitted = 0
-        try:
-            async for o in self.aeng.generate(rid, ids, params, prio, ktp, lora, mm):
-                last = o
+        def chunk(idx, body, finish):
+            return {"id": rid, "object": obj, "created": created, "model": model_name,
+                    "choices": [dict(body, index=idx, finish_reason=finish)]}
+
+        async def one_choice(idx, crid, params):
+            toks: list[int] = []
+            sent = ""
+            n_emitted = 0
+            if chat:
+                await send(chunk(idx, {"delta": {"role": "assistant", "content": ""}}, None))
+            st = self.parser.streamer(tools_on) if (chat and self.parser is not None) else None
+            every = max(1, int(self.opts.stream_interval))
+            async for o in self.aeng.generate(crid, ids, params, prio, ktp, lora, mm):
                 toks.extend(o.new_token_ids)
-                n_out = len(toks)
-                if not o.finished and n_out - n_emitted < every:  # --stream-interval
+                n_outs[idx] = len(toks)
+                if not o.finished and len(toks) - n_emitted < every:  # --stream-interval
                     continue
-                n_emitted = n_out
+                n_emitted = len(toks)
                 text = self.tok.decode(toks)
                 stop_hit = False
                 if params.stop:
@@ -418,35 +438,30 @@ class OpenAIServer:
                         if called:
                             finish = "tool_calls"
                     for k, dl in enumerate(deltas):
-                        last_one = k == len(deltas) - 1
-                        await send({"id": rid, "object": obj, "created": created, "model": model_name,
-                                    "choices": [{"index": 0, "delta": dl,
-                                                 "finish_reason": finish if last_one else None}]})
+                        await send(chunk(idx, {"delta": dl}, finish if k == len(deltas) - 1 else None))
                     if finish is not None and not deltas:
-                        await send({"id": rid, "object": obj, "created": created, "model": model_name,
-                                    "choices": [{"index": 0, "delta": {}, "finish_reason": finish}]})
-                    if stop_hit:
-                        self.aeng.abort(rid)
-                        break
-                    continue
-                ch = {"index": 0, "finish_reason": finish}
-                if chat:
-                    ch["delta"] = {"content": delta}
+                        await send(chunk(idx, {"delta": {}}, finish))
                 else:
-                    ch["text"] = delta
-                d = {"id": rid, "object": obj, "created": created, "model": model_name, "choices": [ch]}
-                if o.finished and o.kv_transfer_params is not None:
-                    d["kv_transfer_params"] = o.kv_transfer_params
-                await send(d)
+                    d = chunk(idx, {"delta": {"content": delta}} if chat else {"text": delta}, finish)
+                    if o.finished and o.kv_transfer_params is not None:
+                        d["kv_transfer_params"] = o.kv_transfer_params
+                    await send(d)
                 if stop_hit:
-                    self.aeng.abort(rid)
+                    self.aeng.abort(crid)
                     break
+
+        try:
+            await asyncio.gather(*[one_choice(i, crid, p) for i, (crid, p) in enumerate(zip(rids, plist))])
         except (ConnectionResetError, asyncio.CancelledError):
-            self.aeng.abort(rid)
+            for crid in rids:
+                self.aeng.abort(crid)
             raise
         except Exception as e:  # noqa: BLE001
+            for crid in rids:
+                self.aeng.abort(crid)
             await send({"error": {"message": str(e), "type": type(e).__name__}})
         if include_usage:
+            n_out = sum(n_outs)
             await send({"id": rid, "object": obj, "created": created, "model": model_name, "choices": [],
                         "usage": {"prompt_tokens": len(ids), "completion_tokens": n_out,
                                   "total_tokens": len(ids) + n_out}})
