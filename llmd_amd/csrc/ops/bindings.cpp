@@ -19,6 +19,7 @@ void llmd_layer_norm(void*, int64_t, void*, int64_t, void*, int64_t, const void*
                      hipStream_t);
 void llmd_fused_add_rms_norm(void*, int64_t, void*, int64_t, const void*, int, int, float,
                              hipStream_t);
+int llmd_qk_rms_norm(void*, int64_t, const void*, const void*, int, int, int, int, float, hipStream_t);
 void llmd_rope_cache(void*, int64_t, const int64_t*, const float*, int, int, int, int,
                      const int64_t*, void*, void*, int64_t, int, int, int, int, float, float, hipStream_t);
 void llmd_gated_act(void*, int64_t, const void*, int64_t, int, int, int, float, float, hipStream_t);
@@ -122,6 +123,20 @@ void rms_norm(torch::Tensor out, torch::Tensor x, torch::Tensor w, double eps) {
   TORCH_CHECK(x.stride(0) % 8 == 0 && out.stride(0) % 8 == 0, "rms_norm: 16-B aligned rows");
   llmd_rms_norm(out.data_ptr(), out.stride(0), x.data_ptr(), x.stride(0), w.data_ptr(), x.size(0), d,
                 (float)eps, cur_stream());
+}
+
+void qk_rms_norm(torch::Tensor qkv, torch::Tensor qw, torch::Tensor kw, int64_t Hq, int64_t Hkv, double eps) {
+  const c10::hip::OptionalHIPGuard device_guard(dev_of(qkv));
+  CHECK_CUDA(qkv); CHECK_BF16(qkv); CHECK_BF16(qw); CHECK_BF16(kw);
+  CHECK_INNER(qkv);
+  TORCH_CHECK(qkv.dim() == 2, "qk_rms_norm: qkv [T, (Hq+2Hkv)*D]");
+  const int64_t D = qw.numel();
+  TORCH_CHECK(kw.numel() == D && qw.is_contiguous() && kw.is_contiguous(), "qk_rms_norm: weights [D]");
+  TORCH_CHECK(D == 64 || D == 128 || D == 256, "qk_rms_norm: head dim 64 / 128 / 256");
+  TORCH_CHECK(qkv.size(1) >= (Hq + Hkv) * D, "qk_rms_norm: qkv narrower than (Hq + Hkv) * D");
+  const int rc = llmd_qk_rms_norm(qkv.data_ptr(), qkv.stride(0), qw.data_ptr(), kw.data_ptr(), qkv.size(0),
+                                  (int)Hq, (int)Hkv, (int)D, (float)eps, cur_stream());
+  TORCH_CHECK(rc == 0, "qk_rms_norm: unsupported head dim");
 }
 
 void fused_add_rms_norm(torch::Tensor x, torch::Tensor residual, torch::Tensor w, double eps) {
@@ -808,6 +823,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {  // _C, or _C_debug (llmd_amd/build.p
   m.doc() = "llmd_amd HIP/CDNA4 op library (gfx950)";
   m.def("rms_norm", &rms_norm);
   m.def("fused_add_rms_norm", &fused_add_rms_norm);
+  m.def("qk_rms_norm", &qk_rms_norm, "Qwen3 per-head q/k RMSNorm in place in the fused QKV output");
   m.def("layer_norm", &layer_norm);
   m.def("rope_cache", &rope_cache);
   m.def("gated_act", &gated_act);

@@ -257,9 +257,55 @@ void launch_ln(uint16_t* out, int64_t os, uint16_t* x, int64_t xs, uint16_t* res
 #undef L
 }
 
+// Qwen3 per-head RMSNorm of q and k, in place inside the fused QKV output
+// (qkv[T, (Hq + 2 Hkv) * D]; heads [0, Hq) use qw, [Hq, Hq + Hkv) use kw, V is
+// untouched). One wave per head: each lane owns E = D / 64 consecutive
+// elements, the sum of squares is a 64-lane shuffle reduction, and the head is
+// read and written once - no strided copies out of / back into the QKV buffer.
+template <int E>
+__global__ __launch_bounds__(NT) void qk_rmsnorm_kernel(uint16_t* __restrict__ qkv, int64_t stride,
+                                                        const uint16_t* __restrict__ qw,
+                                                        const uint16_t* __restrict__ kw, int Hq, int Hkv,
+                                                        float eps) {
+  constexpr int D = 64 * E;
+  const int t = blockIdx.x;
+  const int h = blockIdx.y * (NT / 64) + (threadIdx.x >> 6);
+  if (h >= Hq + Hkv) return;  // whole wave exits together
+  const int lane = threadIdx.x & 63;
+  uint16_t* hp = qkv + (int64_t)t * stride + (int64_t)h * D + lane * E;
+  const uint16_t* w = (h < Hq ? qw : kw) + lane * E;
+  float v[E];
+  float ss = 0.f;
+#pragma unroll
+  for (int j = 0; j < E; ++j) {
+    v[j] = bf2f(hp[j]);
+    ss += v[j] * v[j];
+  }
+  ss = wave_sum(ss);
+  const float inv = rsqrtf(ss / (float)D + eps);
+#pragma unroll
+  for (int j = 0; j < E; ++j) hp[j] = f2bf(v[j] * inv * bf2f(w[j]));
+}
+
 }  // namespace
 
 extern "C" {
+// qkv[:, :Hq*D] = rmsnorm_head(q) * qw, qkv[:, Hq*D:(Hq+Hkv)*D] = rmsnorm_head(k) * kw (in place)
+int llmd_qk_rms_norm(void* qkv, int64_t stride, const void* qw, const void* kw, int T, int Hq, int Hkv, int D,
+                     float eps, hipStream_t st) {
+  if (T == 0) return 0;
+  dim3 g(T, (Hq + Hkv + NT / 64 - 1) / (NT / 64)), b(NT);
+#define L(E)                                                                                             \
+  hipLaunchKernelGGL((qk_rmsnorm_kernel<E>), g, b, 0, st, (uint16_t*)qkv, stride, (const uint16_t*)qw, \
+                     (const uint16_t*)kw, Hq, Hkv, eps)
+  if (D == 64) L(1);
+  else if (D == 128) L(2);
+  else if (D == 256) L(4);
+  else return -1;
+#undef L
+  return 0;
+}
+
 // out = layernorm(x) * w + b; with residual: residual += x, x = layernorm(residual) * w + b (in place)
 void llmd_layer_norm(void* out, int64_t out_stride, void* x, int64_t x_stride, void* residual, int64_t res_stride,
                      const void* w, const void* b, int rows, int d, float eps, hipStream_t st) {

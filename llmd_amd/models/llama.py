@@ -55,11 +55,7 @@ class LlamaDecoderLayer(torch.nn.Module):
 
     def _apply_qk_norm(self, qkv):
         a = self.attn
-        T = qkv.shape[0]
-        q = qkv[:, : a.Hq * a.D].reshape(T * a.Hq, a.D)
-        k = qkv[:, a.Hq * a.D : (a.Hq + a.Hkv) * a.D].reshape(T * a.Hkv, a.D)
-        qkv[:, : a.Hq * a.D] = self.q_norm(q).view(T, -1)
-        qkv[:, a.Hq * a.D : (a.Hq + a.Hkv) * a.D] = self.k_norm(k).view(T, -1)
+        ops.qk_rms_norm(qkv, self.q_norm.weight, self.k_norm.weight, a.Hq, a.Hkv, self.q_norm.eps)
 
     def forward(self, x, residual, meta: AttnMeta):
         # W8A8: the norms emit fp8 + per-row scales straight into the fp8 GEMMs

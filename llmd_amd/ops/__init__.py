@@ -68,6 +68,21 @@ def fused_add_rms_norm(x: torch.Tensor, residual: torch.Tensor, w: torch.Tensor,
     native().fused_add_rms_norm(x, residual, w, eps)
 
 
+def qk_rms_norm(qkv: torch.Tensor, qw: torch.Tensor, kw: torch.Tensor, Hq: int, Hkv: int, eps: float):
+    """Qwen3 per-head RMSNorm of the q and k heads, in place in the fused QKV
+    projection output ``qkv[T, (Hq + 2 Hkv) * D]`` (one kernel, no strided copies)."""
+    if not _gpu(qkv):
+        D = qw.numel()
+        T = qkv.shape[0]
+        q = qkv[:, : Hq * D].reshape(T * Hq, D)
+        k = qkv[:, Hq * D: (Hq + Hkv) * D].reshape(T * Hkv, D)
+        qkv[:, : Hq * D] = ref.rms_norm(q, qw, eps).view(T, -1)
+        qkv[:, Hq * D: (Hq + Hkv) * D] = ref.rms_norm(k, kw, eps).view(T, -1)
+        return qkv
+    native().qk_rms_norm(qkv, qw, kw, Hq, Hkv, eps)
+    return qkv
+
+
 def layer_norm(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, eps: float):
     if not _gpu(x):
         return ref.layer_norm(x, w, b, eps)

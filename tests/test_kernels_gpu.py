@@ -35,6 +35,25 @@ def test_rms_norm(T, d):
     _close(x1, x2)
 
 
+@pytest.mark.parametrize("T,Hq,Hkv,D", [(1, 64, 8, 128), (37, 64, 8, 128), (5, 32, 4, 128), (9, 16, 2, 64),
+                                        (3, 8, 8, 256), (130, 40, 8, 128)])
+def test_qk_rms_norm_in_place(T, Hq, Hkv, D):
+    """Qwen3 per-head q/k RMSNorm inside the fused QKV buffer: q and k heads
+    match the fp32 reference, V is untouched."""
+    torch.manual_seed(0)
+    qkv = torch.randn(T, (Hq + 2 * Hkv) * D, device=DEV, dtype=torch.bfloat16) * 3
+    qw = torch.randn(D, device=DEV, dtype=torch.bfloat16)
+    kw = torch.randn(D, device=DEV, dtype=torch.bfloat16)
+    want = qkv.clone()
+    q = ref.rms_norm(want[:, : Hq * D].reshape(-1, D), qw, 1e-6).view(T, -1)
+    k = ref.rms_norm(want[:, Hq * D: (Hq + Hkv) * D].reshape(-1, D), kw, 1e-6).view(T, -1)
+    got = qkv.clone()
+    ops.qk_rms_norm(got, qw, kw, Hq, Hkv, 1e-6)
+    _close(got[:, : Hq * D], q)
+    _close(got[:, Hq * D: (Hq + Hkv) * D], k)
+    assert torch.equal(got[:, (Hq + Hkv) * D:], qkv[:, (Hq + Hkv) * D:])
+
+
 def _cache(nblk, Hkv, bs, D, L=1):
     kv = torch.zeros(nblk, L, 2, Hkv, bs, D, device=DEV, dtype=torch.bfloat16)
     return kv[:, 0, 0], kv[:, 0, 1]
