@@ -25,7 +25,8 @@ void llmd_rope_cache(void*, int64_t, const int64_t*, const float*, int, int, int
 void llmd_gated_act(void*, int64_t, const void*, int64_t, int, int, int, float, float, hipStream_t);
 int llmd_paged_decode(const void*, int64_t, const void*, const void*, int64_t, int, const int*, int,
                       const int*, int, int, int, int, float, int, const float*, int, int, void*,
-                      int64_t, float*, float*, int, float, float, hipStream_t);
+                      int64_t, float*, float*, int, float, float, const int*, const int*, const int*,
+                      const int*, int, int, int, hipStream_t);
 int llmd_paged_prefill(const void*, int64_t, const void*, const void*, int64_t, int, const int*, int,
                        const int*, const int*, const int*, const int*, int, int, int, int, float,
                        int, const float*, void*, int64_t, int, float, float, hipStream_t);
@@ -237,7 +238,8 @@ void paged_decode(torch::Tensor out, torch::Tensor q, torch::Tensor k_cache, tor
                   torch::Tensor block_tables, torch::Tensor seq_lens, int64_t Hq, int64_t Hkv,
                   int64_t D, double scale, int64_t window, c10::optional<torch::Tensor> sinks,
                   int64_t split_size, int64_t nsplit, torch::Tensor part_o, torch::Tensor part_ml,
-                  double k_scale, double v_scale) {
+                  double k_scale, double v_scale, c10::optional<torch::Tensor> cascade, int64_t np,
+                  int64_t nslot) {
   const c10::hip::OptionalHIPGuard device_guard(dev_of(out));
   CHECK_CUDA(q); CHECK_BF16(q); CHECK_BF16(out); CHECK_INNER(q); CHECK_INNER(out);
   check_cache(k_cache, v_cache, Hkv, D);
@@ -255,20 +257,42 @@ void paged_decode(torch::Tensor out, torch::Tensor q, torch::Tensor k_cache, tor
     TORCH_CHECK(sinks->numel() == Hq, "sinks [Hq]");
     sk = sinks->data_ptr<float>();
   }
-  if (nsplit > 1) {
+  // cascade: int32 [sstart(B) | pcount(B) | members(B) | work(nwork x 5)] (ops.cascade_tensors)
+  const int *sstart = nullptr, *pcount = nullptr, *members = nullptr, *work = nullptr;
+  int nwork = 0;
+  if (cascade.has_value()) {
+    CHECK_CUDA(cascade.value()); CHECK_DT(cascade.value(), at::kInt);
+    const int64_t n = cascade->numel();
+    TORCH_CHECK(n >= 3 * (int64_t)B && (n - 3 * (int64_t)B) % 5 == 0, "decode: cascade tensor layout");
+    TORCH_CHECK(cascade->is_contiguous(), "decode: cascade tensor contiguous");
+    sstart = cascade->data_ptr<int>();
+    pcount = sstart + B;
+    members = sstart + 2 * B;
+    work = sstart + 3 * B;
+    nwork = (int)((n - 3 * (int64_t)B) / 5);
+    const int64_t G = Hq / Hkv;
+    TORCH_CHECK(G <= 16 && 16 % G == 0 && np >= 1 && np <= 3, "decode: cascade needs 16 % G == 0, np in {1,2,3}");
+    TORCH_CHECK(np != 3 || (!is_fp8_cache(k_cache) && (G == 4 || G == 8) && k_cache.size(2) >= 8),
+                "decode: cascade kernel 3 needs a bf16 cache, G 4 or 8, block size >= 8");
+    TORCH_CHECK(nslot > nsplit, "decode: cascade needs prefix slots");
+  } else {
+    nslot = nsplit;
+  }
+  if (nsplit > 1 || nwork > 0) {
     CHECK_DT(part_o, at::kFloat); CHECK_DT(part_ml, at::kFloat);
-    TORCH_CHECK(part_o.numel() >= (int64_t)B * Hq * nsplit * D &&
-                    part_ml.numel() >= (int64_t)B * Hq * nsplit * 2, "decode workspace too small");
+    TORCH_CHECK(part_o.numel() >= (int64_t)B * Hq * nslot * D &&
+                    part_ml.numel() >= (int64_t)B * Hq * nslot * 2, "decode workspace too small");
   }
   // the host must guarantee ctx <= nsplit*split_size (checked by the caller, no sync here)
   int rc = llmd_paged_decode(q.data_ptr(), q.stride(0), k_cache.data_ptr(), v_cache.data_ptr(),
                              k_cache.stride(0), k_cache.size(2), block_tables.data_ptr<int>(),
                              block_tables.stride(0), seq_lens.data_ptr<int>(), B, Hq, Hkv, D,
                              (float)scale, (int)window, sk, split_size, nsplit, out.data_ptr(),
-                             out.stride(0), nsplit > 1 ? part_o.data_ptr<float>() : nullptr,
-                             nsplit > 1 ? part_ml.data_ptr<float>() : nullptr, is_fp8_cache(k_cache) ? 1 : 0,
-                             (float)k_scale, (float)v_scale, cur_stream());
-  TORCH_CHECK(rc == 0, "paged_decode: unsupported head dim");
+                             out.stride(0), (nsplit > 1 || nwork > 0) ? part_o.data_ptr<float>() : nullptr,
+                             (nsplit > 1 || nwork > 0) ? part_ml.data_ptr<float>() : nullptr,
+                             is_fp8_cache(k_cache) ? 1 : 0, (float)k_scale, (float)v_scale, sstart, pcount,
+                             members, work, nwork, (int)np, (int)nslot, cur_stream());
+  TORCH_CHECK(rc == 0, "paged_decode: unsupported head dim / cascade config, rc=", rc);
 }
 
 // MLA (absorbed form): q [R, H*576], cache [blocks, bs, 576] (block stride free),

@@ -25,6 +25,7 @@ class AttnMeta:
     d_split: Optional[tuple] = None                # (split_size, nsplit)
     d_workspace: Optional[tuple] = None            # (part_o, part_ml)
     d_max_ctx: int = 0
+    d_cascade: Optional[tuple] = None              # shared-prefix decode (ops.cascade_tensors)
     # prefill part
     num_prefill_tokens: int = 0
     p_block_tables: Optional[torch.Tensor] = None  # [Bp, W] int32

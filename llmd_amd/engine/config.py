@@ -292,6 +292,9 @@ class CacheConfig:
     num_gpu_blocks: Optional[int] = None
     enable_prefix_caching: bool = True
     kv_cache_dtype: str = "auto"
+    # decode attention reads a prefix shared by several running sequences once
+    # per group (ops.shared_prefix_plan; needs prefix caching to share blocks)
+    shared_prefix_decode: bool = True
 
     def __post_init__(self):
         # the attention kernels index blocks with shifts/masks
@@ -404,6 +407,8 @@ def add_engine_args(p: argparse.ArgumentParser) -> argparse.ArgumentParser:
     p.add_argument("--kv-cache-memory-bytes", type=int, default=None)
     p.add_argument("--num-gpu-blocks-override", type=int, default=None)
     p.add_argument("--no-enable-prefix-caching", action="store_true")
+    p.add_argument("--disable-shared-prefix-decode", action="store_true",
+                   help="read shared cached prefixes per sequence in decode attention (no cascade kernel)")
     p.add_argument("--max-num-seqs", type=int, default=256)
     p.add_argument("--max-num-batched-tokens", type=int, default=8192)
     p.add_argument("--max-model-len", type=int, default=32768)
@@ -500,6 +505,7 @@ def engine_config_from_args(a) -> EngineConfig:
         quantization=getattr(a, "quantization", None), gpu_memory_utilization=a.gpu_memory_utilization,
         kv_cache_memory_bytes=a.kv_cache_memory_bytes, num_gpu_blocks=a.num_gpu_blocks_override,
         enable_prefix_caching=not a.no_enable_prefix_caching, max_num_seqs=a.max_num_seqs,
+        shared_prefix_decode=not getattr(a, "disable_shared_prefix_decode", False),
         max_num_batched_tokens=a.max_num_batched_tokens, max_model_len=a.max_model_len,
         tensor_parallel_size=a.tensor_parallel_size, data_parallel_size=a.data_parallel_size,
         data_parallel_rank=a.data_parallel_rank, enable_expert_parallel=a.enable_expert_parallel,

@@ -104,6 +104,16 @@ class ModelRunner:
             self.kv_dtype = torch.float8_e4m3fn
         else:
             raise ValueError(f"unsupported --kv-cache-dtype {cfg.cache.kv_cache_dtype}")
+        # shared-prefix decode (ops.shared_prefix_plan): GQA kernels only, every
+        # layer full-context (a sliding-window layer needs the plain split plan)
+        G = self.Hq // self.Hkv
+        self.cascade_ok = (cfg.cache.shared_prefix_decode and cfg.cache.enable_prefix_caching and not self.is_mla
+                           and G <= 16 and 16 % G == 0 and not any(a.window for a in attn))
+        self.casc_variant = ops.cascade_variant(G, self.D, self.bs, self.kv_dtype != torch.bfloat16)
+        self.cascade_ok = self.cascade_ok and self.casc_variant is not None
+        self.casc_work = max(16, -(-512 // self.Hkv))  # prefix work units: ~2 workgroups per CU over kv heads
+        self.casc_slots = 16                           # prefix partial slots per sequence
+        self.cgraphs: dict[int, tuple] = {}
         self.lora = None  # engine/lora.py LoRAManager (set by the engine / TP follower)
         self.kv = None
         self.num_blocks = 0
@@ -528,8 +538,11 @@ class ModelRunner:
             meta.d_block_tables = torch.from_numpy(d_bt).to(dev, non_blocking=True)
             meta.d_seq_lens = torch.from_numpy(d_len).to(dev, non_blocking=True)
             meta.d_max_ctx = int(d_len.max())
-            w = [a.window for a in self.model.attention_layers()]
             mctx = meta.d_max_ctx
+            plan = self._cascade_plan(d_bt, d_len)
+            if plan is not None:
+                meta.d_cascade = ops.cascade_tensors(plan, dev)
+                mctx = int((d_len - plan.sstart[:nd]).max())  # splits cover the longest own suffix
             meta.d_split = ops.decode_split_plan(mctx, nd, self.Hkv, self.Hq // self.Hkv)
         if p_ql:
             meta.num_prefill_tokens = sum(p_ql)
@@ -546,6 +559,13 @@ class ModelRunner:
             meta.mm_rows = torch.tensor(rows, dtype=torch.long).to(dev, non_blocking=True)
             meta.mm_embeds = embs.to(dev)
         return hd[0], meta
+
+    def _cascade_plan(self, d_bt, d_len, max_work=None):
+        """Shared-prefix decode plan for this step's decode rows, or None."""
+        if not self.cascade_ok or len(d_len) < 2:
+            return None
+        return ops.shared_prefix_plan(d_bt, d_len, self.bs, self.Hq // self.Hkv, self.Hkv,
+                                      variant=self.casc_variant, max_slots=self.casc_slots, max_work=max_work)
 
     # ------------------------------------------------------------ dual-batch overlap
     def _forward_steps(self, ids, meta):
@@ -676,7 +696,10 @@ class ModelRunner:
         # big batches (2.6 TB/s KV read at batch 64 vs 4.7 with a sized plan)
         self.graph_plans = {B: ops.decode_split_plan(self.max_model_len, B, self.Hkv, self.Hq // self.Hkv)
                             for B in buckets}
-        ws_rows = max(B * p[1] for B, p in self.graph_plans.items())
+        extra = self.casc_slots if self.cascade_ok else 0
+        ws_rows = max(B * (p[1] + extra) for B, p in self.graph_plans.items())
+        # shared-prefix decode inputs [sstart | pcount | members | work] (ops.cascade_tensors)
+        self.g_casc = torch.zeros(3 * M + 5 * self.casc_work, dtype=torch.int32, device=dev)
         self.g_ids = torch.zeros(M, dtype=torch.long, device=dev)
         self.g_pos = torch.zeros(M, dtype=torch.long, device=dev)
         self.g_slots = torch.full((M,), -1, dtype=torch.long, device=dev)
@@ -710,11 +733,22 @@ class ModelRunner:
                 h = self.model(self.g_ids[:B], meta)
                 lg = self.model.compute_logits(h)
             self.graphs[B] = (g, lg)
+            if self.cascade_ok and B >= 2:
+                # variant with the shared-prefix kernel (all-padding work units while capturing)
+                meta.d_cascade = (self.g_casc[:3 * B + 5 * self.casc_work], self.casc_variant, self.casc_slots)
+                with torch.cuda.stream(s):
+                    self.model(self.g_ids[:B], meta)
+                torch.cuda.current_stream().wait_stream(s)
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g, pool=pool):
+                    h = self.model(self.g_ids[:B], meta)
+                    lg = self.model.compute_logits(h)
+                self.cgraphs[B] = (g, lg)
         if self._dbo_graphable():
             self._capture_dbo_graphs(buckets, pool)
         torch.cuda.synchronize()
-        log.info("captured %d decode graphs (+%d dual-batch) in %.1fs", len(buckets), len(self.dbo_graphs),
-                 time.time() - t0)
+        log.info("captured %d decode graphs (+%d shared-prefix, +%d dual-batch) in %.1fs", len(buckets),
+                 len(self.cgraphs), len(self.dbo_graphs), time.time() - t0)
 
     # ------------------------------------------------------------ dual-batch overlap under hipGraphs
     def _dbo_graphable(self) -> bool:
@@ -854,6 +888,11 @@ class ModelRunner:
         self.g_slots[:B].copy_(host[2], non_blocking=True)
         self.g_bt[:B].copy_(torch.from_numpy(d_bt).pin_memory(), non_blocking=True)
         self.g_len[:B].copy_(torch.from_numpy(d_len).pin_memory(), non_blocking=True)
+        if B in self.cgraphs:
+            plan = self._cascade_plan(d_bt, d_len, max_work=self.casc_work)
+            if plan is not None:
+                ops.cascade_tensors(plan, self.device, out=self.g_casc)
+                g, lg = self.cgraphs[B]
         g.replay()
         if len(rows) == B and rows == list(range(B)):
             return lg

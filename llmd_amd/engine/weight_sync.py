@@ -294,6 +294,7 @@ class WeightSync:
                 if t.device.type == "cuda":
                     t.untyped_storage().resize_(0)
             r.graphs.clear()
+            r.cgraphs.clear()
             r.dbo_graphs.clear()
             if r.kv is not None:
                 freed += r.kv.untyped_storage().nbytes()

@@ -154,9 +154,166 @@ def decode_split_plan(max_ctx: int, batch: int, Hkv: int, G: int, num_cus: int =
     return split, nsplit
 
 
+class SharedPrefixPlan:
+    """Shared-prefix ("cascade") decode plan for one step (SURVEY K01 on the
+    prefix-cache workloads: many running sequences whose first blocks are the
+    same physical KV blocks).
+
+    sstart[b]   end of sequence b's shared prefix (0 = none): its own decode
+                pass covers keys [sstart[b], L)
+    pcount[b]   prefix partial slots written for b (one per work unit of its item)
+    members     sequence indices, item by item (contiguous)
+    work        int32 [nwork, 5] = (first member, members, key lo, key hi, slot
+                offset); rows with 0 members are padding
+    items       number of prefix items (groups of <= CASCADE_MEMBERS[np](G) members)
+    np          prefix kernel variant (cascade_variant): 1 / 2 register kernel with
+                1 / 2 16-column passes, 3 LDS-DMA kernel
+    """
+
+    __slots__ = ("sstart", "pcount", "members", "work", "items", "np", "max_slots")
+
+    def __init__(self, sstart, pcount, members, work, items, np_, max_slots):
+        self.sstart, self.pcount, self.members, self.work = sstart, pcount, members, work
+        self.items, self.np, self.max_slots = items, np_, max_slots
+
+    @property
+    def work_units(self) -> int:
+        return int((self.work[:, 1] > 0).sum())
+
+
+def cascade_variant(G: int, D: int, bs: int, fp8: bool) -> Optional[int]:
+    """Shared-prefix kernel for this geometry: 3 = LDS-DMA kernel (bf16 cache,
+    G 4 or 8, D 64/128, block size >= 8; up to 128/G members per item),
+    1 = register kernel (16/G members), 2 = its two-pass form (G = 16: 2
+    members), None = no cascade (16 % G != 0)."""
+    if not fp8 and G in (4, 8) and D in (64, 128) and bs >= 8:
+        return 3
+    if G < 16 and 16 % G == 0:
+        return 1
+    if G == 16:
+        return 2  # one member per 16-column pass: two passes to pair sequences
+    return None
+
+
+CASCADE_MEMBERS = {1: lambda G: 16 // G, 2: lambda G: 32 // G, 3: lambda G: 128 // G}
+
+
+def shared_prefix_plan(block_tables, seq_lens, bs: int, G: int, Hkv: int = 8, *, variant: int = 1,
+                       max_slots: int = 16, min_prefix: int = 512, max_work: Optional[int] = None,
+                       min_chunk: int = 512) -> Optional[SharedPrefixPlan]:
+    """Group the decode batch by shared leading physical blocks.
+
+    Only FULL blocks strictly before a sequence's current token count (the
+    prefix cache shares full blocks; the current token's block is private).
+    Members of a group are sorted by how many blocks they share with the
+    group's first member and cut into items of at most the kernel variant's
+    member capacity (CASCADE_MEMBERS); an item's prefix is the shortest shared
+    run among its members. Items are split into work units of >= min_chunk
+    keys, one round of workgroups over the chip in total (512 / Hkv units; 256 /
+    Hkv for the one-workgroup-per-CU variant 2), at most `max_slots` per item.
+    Returns None when nothing is shared (the plain kernel runs)."""
+    import numpy as np
+
+    if G > 16 or 16 % G:
+        return None
+    lens = np.asarray(seq_lens, dtype=np.int64)
+    B = len(lens)
+    if B < 2:
+        return None
+    bt = np.asarray(block_tables)[:B]
+    cap = CASCADE_MEMBERS[variant](G)
+    nfull = np.maximum((lens - 1) // bs, 0)
+    min_blocks = max(1, -(-min_prefix // bs))
+    elig = np.nonzero(nfull >= min_blocks)[0]
+    if len(elig) < 2:
+        return None
+    groups: dict[int, list[int]] = {}
+    for i in elig.tolist():
+        groups.setdefault(int(bt[i, 0]), []).append(i)
+    items = []  # (prefix tokens, [members])
+    for mem in groups.values():
+        if len(mem) < 2:
+            continue
+        idx = np.asarray(mem)
+        w = int(nfull[idx].max())
+        rows = bt[idx, :w]
+        eq = rows == rows[0]
+        lcp = np.where(eq.all(1), w, eq.argmin(1))
+        lcp = np.minimum(lcp, nfull[idx])
+        order = np.argsort(-lcp, kind="stable")
+        keep = [(int(idx[o]), int(lcp[o])) for o in order if lcp[o] >= min_blocks]
+        n = len(keep)
+        if n < 2:
+            continue
+        nit = -(-n // cap)
+        sizes = [n // nit + (1 if k < n % nit else 0) for k in range(nit)]
+        pos = 0
+        for sz in sizes:
+            chunk = keep[pos:pos + sz]
+            pos += sz
+            if sz < 2:
+                continue
+            items.append((min(c[1] for c in chunk) * bs, [c[0] for c in chunk]))
+    if not items:
+        return None
+    # one round of workgroups over the chip: variant 2 holds two passes'
+    # accumulators (one workgroup per CU), the others run two per CU
+    target = max(8, -(-(256 if variant == 2 else 512) // max(1, Hkv)))
+    if max_work is not None:
+        target = min(target, max_work)
+    total = sum(p for p, _ in items)
+    sstart = np.zeros(B, np.int32)
+    pcount = np.zeros(B, np.int32)
+    members = np.zeros(B, np.int32)
+    work = []
+    mpos = 0
+    used_items = 0
+    for P, mem in sorted(items, key=lambda x: -x[0] * len(x[1])):
+        k = max(1, min(max_slots, round(target * P / total), -(-P // min_chunk)))
+        split = -(-P // k)
+        split = -(-split // 64) * 64
+        k = -(-P // split)
+        if max_work is not None and len(work) + k > max_work:
+            continue  # no capacity left in the captured grid: these members run the plain path
+        m0 = mpos
+        for b in mem:
+            members[mpos] = b
+            mpos += 1
+            sstart[b] = P
+            pcount[b] = k
+        for j in range(k):
+            work.append((m0, len(mem), j * split, min(P, (j + 1) * split), j))
+        used_items += 1
+    if not work:
+        return None
+    nwork = len(work) if max_work is None else max_work
+    wk = np.zeros((nwork, 5), np.int32)
+    wk[:len(work)] = np.asarray(work, np.int32)
+    return SharedPrefixPlan(sstart, pcount, members, wk, used_items, variant, max_slots)
+
+
+def cascade_tensors(plan: SharedPrefixPlan, device, out: Optional[torch.Tensor] = None):
+    """One int32 tensor [sstart | pcount | members | work] for paged_decode(cascade=...).
+    ``out``: a static (hipGraph) buffer of the same layout to copy into."""
+    import numpy as np
+
+    flat = np.concatenate([plan.sstart, plan.pcount, plan.members, plan.work.reshape(-1)]).astype(np.int32)
+    host = torch.from_numpy(flat)
+    if out is not None:
+        out[: host.numel()].copy_(host.pin_memory() if out.is_cuda else host, non_blocking=True)
+        return (out[: host.numel()], plan.np, plan.max_slots)
+    if torch.device(device).type == "cuda":
+        host = host.pin_memory()
+    return (host.to(device, non_blocking=True), plan.np, plan.max_slots)
+
+
 def paged_decode(q, k_cache, v_cache, block_tables, seq_lens, Hq, Hkv, D, scale, window=0,
-                 sinks=None, split=None, out=None, workspace=None, max_ctx=None, k_scale=1.0, v_scale=1.0):
-    """q: [B, >=Hq*D] -> out [B, Hq*D]. k/v caches bf16 or fp8 e4m3fn (dequant scales)."""
+                 sinks=None, split=None, out=None, workspace=None, max_ctx=None, k_scale=1.0, v_scale=1.0,
+                 cascade=None):
+    """q: [B, >=Hq*D] -> out [B, Hq*D]. k/v caches bf16 or fp8 e4m3fn (dequant scales).
+    cascade: (tensor, np, max_slots) from cascade_tensors(shared_prefix_plan(...)): shared
+    prefixes are read once per group by the prefix kernel; `split` must then cover the
+    longest suffix (L - sstart), and the workspace holds nsplit + max_slots slots per row."""
     if not _gpu(q):
         r = ref.paged_decode(q, k_cache, v_cache, block_tables, seq_lens, Hq, Hkv, D, scale,
                              window, sinks, k_scale, v_scale)
@@ -174,16 +331,21 @@ def paged_decode(q, k_cache, v_cache, block_tables, seq_lens, Hq, Hkv, D, scale,
             max_ctx = min(max_ctx, window)
         split = decode_split_plan(max_ctx, B, Hkv, Hq // Hkv)
     split_size, nsplit = split
-    if nsplit > 1:
+    ctens, cnp, nslot = None, 1, nsplit
+    if cascade is not None and not (window and window > 0):
+        ctens, cnp, extra = cascade
+        nslot = nsplit + extra
+    if nslot > 1:
         if workspace is None:
-            part_o = torch.empty(B * Hq * nsplit * D, dtype=torch.float32, device=q.device)
-            part_ml = torch.empty(B * Hq * nsplit * 2, dtype=torch.float32, device=q.device)
+            part_o = torch.empty(B * Hq * nslot * D, dtype=torch.float32, device=q.device)
+            part_ml = torch.empty(B * Hq * nslot * 2, dtype=torch.float32, device=q.device)
         else:
             part_o, part_ml = workspace
     else:
         part_o = part_ml = out.new_empty(0, dtype=torch.float32)
     native().paged_decode(out, q, k_cache, v_cache, block_tables, seq_lens, Hq, Hkv, D, scale,
-                          window, sinks, split_size, nsplit, part_o, part_ml, k_scale, v_scale)
+                          window, sinks, split_size, nsplit, part_o, part_ml, k_scale, v_scale,
+                          ctens, cnp, nslot)
     return out
 
 

@@ -133,6 +133,54 @@ def test_paged_decode_window_sinks():
             _close(o, r)
 
 
+@pytest.mark.parametrize("Hq,Hkv,D,bs,groups,fp8,variant", [
+    (64, 8, 128, 64, [(2048, 2), (1024, 3), (512, 4), (0, 3)], False, 2),   # 2 passes (4 members at G=8)
+    (64, 8, 128, 64, [(3072, 2), (1024, 2)], False, 1),                        # 1 pass
+    (32, 8, 128, 16, [(640, 7), (320, 2)], False, 2),                          # G 4: up to 8 members
+    (64, 8, 64, 64, [(1024, 3), (768, 2)], False, 1),
+    (16, 1, 128, 64, [(1536, 2), (512, 2)], False, 2),                         # G 16: one member per pass
+    (64, 8, 128, 64, [(2048, 3), (1024, 2)], True, 2),
+    (64, 8, 128, 64, [(2048, 17), (1088, 5), (512, 2), (0, 2)], False, 3),    # LDS-DMA: 16 members, partial tile
+    (32, 8, 128, 128, [(1536, 33), (640, 3)], False, 3),                       # G 4: 32 members
+    (64, 8, 64, 64, [(1024, 9), (704, 4)], False, 3),
+    (64, 8, 128, 16, [(1040, 5), (2048, 12)], False, 3),                      # 16-key blocks, partial tile
+    (64, 8, 64, 32, [(608, 3), (1024, 2)], False, 3),
+])
+def test_paged_decode_shared_prefix(Hq, Hkv, D, bs, groups, fp8, variant):
+    """Shared-prefix (cascade) decode: prefixes read once per group by the
+    prefix kernel, suffixes by the per-sequence kernel, merged by the reduce
+    kernel - against the fp32 reference and the plain kernel; with sinks."""
+    from shared_prefix_util import shared_tables
+
+    torch.manual_seed(4)
+    bt_np, lens_np, nb = shared_tables(groups, [1, 63, 64, 65, 300, 7], bs, seed=2)
+    kc, vc = _cache(nb + 2, Hkv, bs, D, L=2)
+    kc.normal_()
+    vc.normal_()
+    if fp8:
+        kc, vc = kc.to(torch.float8_e4m3fn), vc.to(torch.float8_e4m3fn)
+    B = len(lens_np)
+    bt = torch.from_numpy(bt_np).to(DEV)
+    sl = torch.from_numpy(lens_np).to(DEV)
+    q = torch.randn(B, (Hq + 2 * Hkv) * D, device=DEV, dtype=torch.bfloat16)
+    sinks = torch.randn(Hq, device=DEV)
+    scale = D ** -0.5
+    plan = ops.shared_prefix_plan(bt_np, lens_np, bs, G=Hq // Hkv, Hkv=Hkv, variant=variant, min_prefix=256,
+                                  min_chunk=256)
+    assert plan is not None and plan.items >= 2 and plan.np == variant
+    casc = ops.cascade_tensors(plan, DEV)
+    for sk in (None, sinks):
+        r = ref.paged_decode(q, kc, vc, bt, sl, Hq, Hkv, D, scale, 0, sk)
+        suffix = int((lens_np - plan.sstart).max())
+        for split in [None, (64, -(-suffix // 64)), (4096, 2)]:
+            if split is None:
+                split = ops.decode_split_plan(suffix, B, Hkv, Hq // Hkv)
+            o = ops.paged_decode(q, kc, vc, bt, sl, Hq, Hkv, D, scale, 0, sk, split=split, cascade=casc)
+            _close(o, r)
+        plain = ops.paged_decode(q, kc, vc, bt, sl, Hq, Hkv, D, scale, 0, sk, max_ctx=int(lens_np.max()))
+        _close(o, plain)
+
+
 @pytest.mark.parametrize("Hq,Hkv,D", [(64, 8, 128), (32, 8, 128), (8, 8, 128), (64, 8, 64), (16, 8, 128)])
 @pytest.mark.parametrize("bs", [16, 64])
 def test_paged_prefill(Hq, Hkv, D, bs):
