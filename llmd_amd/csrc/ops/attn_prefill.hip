@@ -299,7 +299,7 @@ __global__ __launch_bounds__(NT, 2) void prefill_kernel(
   }
 }
 
-// ---------------------------------------------------------------- v2 (bf16 cache, D = 64/128, block >= 64)
+// ---------------------------------------------------------------- v2 (bf16 cache, D = 64/128, block >= 16)
 // Same work decomposition and math as prefill_kernel; the tiles move
 // global -> LDS with global_load_lds_dwordx4 (no VGPR staging, no ds_write),
 // one vmcnt + barrier per tile, double-buffered. Images are unpadded 256-B rows
@@ -413,7 +413,7 @@ __global__ __launch_bounds__(NT, 2) void prefill_v2_kernel(
     const char* kb = reinterpret_cast<const char*>(kc) + tb;
     const char* vb = reinterpret_cast<const char*>(vc) + tb;
     const int rlim = ctx - 1 - ts;
-    if (rlim >= 63) {
+    if (rlim >= 63 && bs >= 64) {
 #pragma unroll
       for (int i = 0; i < NI / 4; ++i) {
         char* dst = base + 1024 * (ws + 4 * i);
@@ -422,12 +422,34 @@ __global__ __launch_bounds__(NT, 2) void prefill_v2_kernel(
         __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)(vb + voff[i]),
                                          (void __attribute__((address_space(3)))*)(dst + P2_IMG), 16, 0, 0);
       }
+    } else if (rlim >= 63) {
+      // blocks of 16 / 32 keys: a wave-instruction's RPI rows sit in one block
+      // (bs >= RPI), so one scalar block-table lookup per instruction
+      constexpr int RPI = 1024 / RB;
+#pragma unroll
+      for (int i = 0; i < NI / 4; ++i) {
+        const int r0 = RPI * (ws + 4 * i);
+        const int key0 = ts + r0;
+        const int64_t ib = 2 * ((int64_t)bt[key0 >> lbs] * block_stride + head_off + (int64_t)(key0 & (bs - 1)) * D) -
+                           (int64_t)r0 * RB;
+        char* dst = base + 1024 * (ws + 4 * i);
+        __builtin_amdgcn_global_load_lds(
+            (const void __attribute__((address_space(1)))*)(reinterpret_cast<const char*>(kc) + ib + koff[i]),
+            (void __attribute__((address_space(3)))*)dst, 16, 0, 0);
+        __builtin_amdgcn_global_load_lds(
+            (const void __attribute__((address_space(1)))*)(reinterpret_cast<const char*>(vc) + ib + voff[i]),
+            (void __attribute__((address_space(3)))*)(dst + P2_IMG), 16, 0, 0);
+      }
     } else {
 #pragma unroll
       for (int i = 0; i < NI / 4; ++i) {
         const int u = 64 * (w + 4 * i) + lane;
         const int row = u / (D / 8), sl = u % (D / 8);
-        const int64_t ro = (int64_t)min(row, rlim) * RB;
+        const int key = ts + min(row, rlim);
+        // row offset from the tile base when the tile is one block, else the key's own block
+        const int64_t ro = bs >= 64 ? (int64_t)min(row, rlim) * RB
+                                    : 2 * ((int64_t)bt[key >> lbs] * block_stride + head_off +
+                                           (int64_t)(key & (bs - 1)) * D) - tb;
         char* dst = base + 1024 * (ws + 4 * i);
         __builtin_amdgcn_global_load_lds(
             (const void __attribute__((address_space(1)))*)(kb + ro + 16 * (sl ^ p2_pk<D>(row))),
@@ -626,7 +648,7 @@ extern "C" int llmd_paged_prefill(const void* q, int64_t q_stride, const void* k
     const char* e = getenv("LLMD_PREFILL_XCD");
     return !(e && e[0] == '0');
   }();
-  if ((D == 128 || D == 64) && !fp8 && bs >= 64 && !v1_only) {
+  if ((D == 128 || D == 64) && !fp8 && bs >= 16 && !v1_only) {
     auto kern = D == 128 ? prefill_v2_kernel<128> : prefill_v2_kernel<64>;
     hipLaunchKernelGGL(kern, grid, blk, 0, st, (const uint16_t*)q, q_stride, (const uint16_t*)kc,
                        (const uint16_t*)vc, block_stride, bs, block_tables, bt_stride, q_start, q_len, ctx_len,
