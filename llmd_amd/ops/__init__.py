@@ -227,33 +227,38 @@ def shared_prefix_plan(block_tables, seq_lens, bs: int, G: int, Hkv: int = 8, *,
     elig = np.nonzero(nfull >= min_blocks)[0]
     if len(elig) < 2:
         return None
-    groups: dict[int, list[int]] = {}
-    for i in elig.tolist():
-        groups.setdefault(int(bt[i, 0]), []).append(i)
+    # group by first physical block (sorted), LCP of every row with its group's
+    # first row in one vectorised compare
+    first = bt[elig, 0]
+    order = np.argsort(first, kind="stable")
+    elig, first = elig[order], first[order]
+    _, gstart, gcount = np.unique(first, return_index=True, return_counts=True)
+    multi = gcount >= 2
+    if not multi.any():
+        return None
+    w = int(nfull[elig].max())
+    leader = np.repeat(gstart, gcount)
+    rows = bt[elig, :w]
+    eq = rows == rows[leader]
+    lcp = np.where(eq.all(1), w, eq.argmin(1))
+    lcp = np.minimum(lcp, nfull[elig])
     items = []  # (prefix tokens, [members])
-    for mem in groups.values():
-        if len(mem) < 2:
-            continue
-        idx = np.asarray(mem)
-        w = int(nfull[idx].max())
-        rows = bt[idx, :w]
-        eq = rows == rows[0]
-        lcp = np.where(eq.all(1), w, eq.argmin(1))
-        lcp = np.minimum(lcp, nfull[idx])
-        order = np.argsort(-lcp, kind="stable")
-        keep = [(int(idx[o]), int(lcp[o])) for o in order if lcp[o] >= min_blocks]
-        n = len(keep)
+    for g0, n0 in zip(gstart[multi].tolist(), gcount[multi].tolist()):
+        gl = lcp[g0:g0 + n0]
+        o = np.argsort(-gl, kind="stable")
+        o = o[gl[o] >= min_blocks]
+        n = len(o)
         if n < 2:
             continue
+        mem_sorted = elig[g0:g0 + n0][o].tolist()
+        lcp_sorted = gl[o].tolist()
         nit = -(-n // cap)
         sizes = [n // nit + (1 if k < n % nit else 0) for k in range(nit)]
         pos = 0
         for sz in sizes:
-            chunk = keep[pos:pos + sz]
+            if sz >= 2:
+                items.append((min(lcp_sorted[pos:pos + sz]) * bs, mem_sorted[pos:pos + sz]))
             pos += sz
-            if sz < 2:
-                continue
-            items.append((min(c[1] for c in chunk) * bs, [c[0] for c in chunk]))
     if not items:
         return None
     # one round of workgroups over the chip: variant 2 holds two passes'
