@@ -278,8 +278,9 @@ __global__ __launch_bounds__(NT, 2) void paged_decode_kernel(
     const void* __restrict__ vc, int64_t block_stride, int bs,
     const int* __restrict__ block_tables, int bt_stride, const int* __restrict__ seq_lens,
     const int* __restrict__ sstart, int Hq, int Hkv, int G, int NG, float scale_log2, int window,
-    const float* __restrict__ sinks, int split_size, int nslot, int direct, uint16_t* __restrict__ out,
-    int64_t out_stride, float* __restrict__ part_o, float* __restrict__ part_ml, float vscale) {
+    const float* __restrict__ sinks, int split_size, const int* __restrict__ split_dev, int nslot, int direct,
+    uint16_t* __restrict__ out, int64_t out_stride, float* __restrict__ part_o, float* __restrict__ part_ml,
+    float vscale) {
   constexpr int KS = D / 32;
   constexpr int NB = D / 16;
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -291,6 +292,7 @@ __global__ __launch_bounds__(NT, 2) void paged_decode_kernel(
   LLMD_DCHECK(L >= 0 && L <= bt_stride * bs);  // the block table covers the sequence
   int start = window > 0 ? max(0, L - window) : 0;
   if (sstart) start = max(start, sstart[b]);
+  if (split_dev) split_size = *split_dev;  // hipGraph replay: keys per split sized to this step's contexts
   const int s0 = start + sp * split_size;
   if (s0 >= L) return;
   const int s1 = min(s0 + split_size, L);
@@ -672,12 +674,13 @@ template <int D>
 __global__ __launch_bounds__(64) void decode_reduce_kernel(
     const float* __restrict__ part_o, const float* __restrict__ part_ml,
     const int* __restrict__ seq_lens, const int* __restrict__ sstart, const int* __restrict__ pcount,
-    int Hq, int nsplit, int nslot, int split_size, int window,
+    int Hq, int nsplit, int nslot, int split_size, const int* __restrict__ split_dev, int window,
     const float* __restrict__ sinks, uint16_t* __restrict__ out, int64_t out_stride) {
   const int hq = blockIdx.x, b = blockIdx.y;
   const int L = seq_lens[b];
   int start = window > 0 ? max(0, L - window) : 0;
   if (sstart) start = max(start, sstart[b]);
+  if (split_dev) split_size = *split_dev;
   const int nact = min(nsplit, (L - start + split_size - 1) / split_size);
   const int np = pcount ? pcount[b] : 0;
   const int64_t base = ((int64_t)b * Hq + hq) * nslot;
@@ -707,7 +710,7 @@ extern "C" int llmd_paged_decode(const void* q, int64_t q_stride, const void* kc
                                  int nsplit, void* out, int64_t out_stride, float* part_o,
                                  float* part_ml, int fp8, float k_scale, float v_scale,
                                  const int* sstart, const int* pcount, const int* members, const int* work,
-                                 int nwork, int np, int nslot, hipStream_t st) {
+                                 int nwork, int np, int nslot, const int* split_dev, hipStream_t st) {
   if (B == 0) return 0;
   const int G = Hq / Hkv;
   const int NG = (G + 15) / 16;
@@ -739,12 +742,14 @@ extern "C" int llmd_paged_decode(const void* q, int64_t q_stride, const void* kc
     }                                                                                                        \
     hipLaunchKernelGGL((paged_decode_kernel<DD, F8>), grid, blk, lds, st, (const uint16_t*)q, q_stride, kc,  \
                        vc, block_stride, bs, block_tables, bt_stride, seq_lens, cascade ? sstart : nullptr,  \
-                       Hq, Hkv, G, NG, scale_log2, window, sinks, split_size, direct ? nsplit : nslot,       \
+                       Hq, Hkv, G, NG, scale_log2, window, sinks, split_size, split_dev,                     \
+                       direct ? nsplit : nslot,                                                              \
                        direct, (uint16_t*)out, out_stride, part_o, part_ml, v_scale);                        \
     if (!direct)                                                                                             \
       hipLaunchKernelGGL(decode_reduce_kernel<DD>, dim3(Hq, B), dim3(64), 0, st, part_o, part_ml, seq_lens,  \
                          cascade ? sstart : nullptr, cascade ? pcount : nullptr, Hq, nsplit,                 \
-                         direct ? nsplit : nslot, split_size, window, sinks, (uint16_t*)out, out_stride);    \
+                         direct ? nsplit : nslot, split_size, split_dev, window, sinks, (uint16_t*)out,       \
+                         out_stride);                                                                        \
   } while (0)
   if (D == 128) {
     if (fp8) LAUNCH(128, true); else LAUNCH(128, false);

@@ -26,7 +26,7 @@ void llmd_gated_act(void*, int64_t, const void*, int64_t, int, int, int, float, 
 int llmd_paged_decode(const void*, int64_t, const void*, const void*, int64_t, int, const int*, int,
                       const int*, int, int, int, int, float, int, const float*, int, int, void*,
                       int64_t, float*, float*, int, float, float, const int*, const int*, const int*,
-                      const int*, int, int, int, hipStream_t);
+                      const int*, int, int, int, const int*, hipStream_t);
 int llmd_paged_prefill(const void*, int64_t, const void*, const void*, int64_t, int, const int*, int,
                        const int*, const int*, const int*, const int*, int, int, int, int, float,
                        int, const float*, void*, int64_t, int, float, float, hipStream_t);
@@ -239,7 +239,7 @@ void paged_decode(torch::Tensor out, torch::Tensor q, torch::Tensor k_cache, tor
                   int64_t D, double scale, int64_t window, c10::optional<torch::Tensor> sinks,
                   int64_t split_size, int64_t nsplit, torch::Tensor part_o, torch::Tensor part_ml,
                   double k_scale, double v_scale, c10::optional<torch::Tensor> cascade, int64_t np,
-                  int64_t nslot) {
+                  int64_t nslot, c10::optional<torch::Tensor> split_dev) {
   const c10::hip::OptionalHIPGuard device_guard(dev_of(out));
   CHECK_CUDA(q); CHECK_BF16(q); CHECK_BF16(out); CHECK_INNER(q); CHECK_INNER(out);
   check_cache(k_cache, v_cache, Hkv, D);
@@ -278,6 +278,14 @@ void paged_decode(torch::Tensor out, torch::Tensor q, torch::Tensor k_cache, tor
   } else {
     nslot = nsplit;
   }
+  // split_dev: int32 [1] on the device = keys per split, overriding split_size (hipGraph
+  // replay); the caller keeps split_dev * nsplit >= the longest (suffix) context
+  const int* sdev = nullptr;
+  if (split_dev.has_value()) {
+    CHECK_CUDA(split_dev.value()); CHECK_DT(split_dev.value(), at::kInt);
+    TORCH_CHECK(split_dev->numel() >= 1, "decode: split_dev [1]");
+    sdev = split_dev->data_ptr<int>();
+  }
   if (nsplit > 1 || nwork > 0) {
     CHECK_DT(part_o, at::kFloat); CHECK_DT(part_ml, at::kFloat);
     TORCH_CHECK(part_o.numel() >= (int64_t)B * Hq * nslot * D &&
@@ -291,7 +299,7 @@ void paged_decode(torch::Tensor out, torch::Tensor q, torch::Tensor k_cache, tor
                              out.stride(0), (nsplit > 1 || nwork > 0) ? part_o.data_ptr<float>() : nullptr,
                              (nsplit > 1 || nwork > 0) ? part_ml.data_ptr<float>() : nullptr,
                              is_fp8_cache(k_cache) ? 1 : 0, (float)k_scale, (float)v_scale, sstart, pcount,
-                             members, work, nwork, (int)np, (int)nslot, cur_stream());
+                             members, work, nwork, (int)np, (int)nslot, sdev, cur_stream());
   TORCH_CHECK(rc == 0, "paged_decode: unsupported head dim / cascade config, rc=", rc);
 }
 

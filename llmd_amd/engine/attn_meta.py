@@ -26,6 +26,7 @@ class AttnMeta:
     d_workspace: Optional[tuple] = None            # (part_o, part_ml)
     d_max_ctx: int = 0
     d_cascade: Optional[tuple] = None              # shared-prefix decode (ops.cascade_tensors)
+    d_split_dev: Optional[torch.Tensor] = None     # [1] int32 keys per split, set per graph replay
     # prefill part
     num_prefill_tokens: int = 0
     p_block_tables: Optional[torch.Tensor] = None  # [Bp, W] int32

@@ -700,6 +700,10 @@ class ModelRunner:
         ws_rows = max(B * (p[1] + extra) for B, p in self.graph_plans.items())
         # shared-prefix decode inputs [sstart | pcount | members | work] (ops.cascade_tensors)
         self.g_casc = torch.zeros(3 * M + 5 * self.casc_work, dtype=torch.int32, device=dev)
+        # keys per decode split, re-sized at every replay to the step's longest context (the
+        # bucket's split count stays the grid): a plan sized for max_model_len would leave most
+        # splits of a short-context batch empty and the chip underfilled
+        self.g_split = torch.full((1,), self.graph_plans[buckets[-1]][0], dtype=torch.int32, device=dev)
         self.g_ids = torch.zeros(M, dtype=torch.long, device=dev)
         self.g_pos = torch.zeros(M, dtype=torch.long, device=dev)
         self.g_slots = torch.full((M,), -1, dtype=torch.long, device=dev)
@@ -716,9 +720,11 @@ class ModelRunner:
         pool = torch.cuda.graph_pool_handle()
         t0 = time.time()
         for B in reversed(buckets):
+            self.g_split.fill_(self.graph_plans[B][0])  # warm-up / capture runs: the max_model_len plan
             meta = AttnMeta(num_tokens=B, positions=self.g_pos[:B], slot_mapping=self.g_slots[:B],
                             num_decode=B, d_block_tables=self.g_bt[:B], d_seq_lens=self.g_len[:B],
-                            d_split=self.graph_plans[B], d_workspace=self.g_ws, d_max_ctx=self.max_model_len)
+                            d_split=self.graph_plans[B], d_workspace=self.g_ws, d_max_ctx=self.max_model_len,
+                            d_split_dev=self.g_split)
             if self.is_mla:
                 meta.mla_d_rows, meta.mla_split, meta.mla_workspace = self.g_rows[:B], self.mla_plans[B], self.g_mla_ws
             s = torch.cuda.Stream()
@@ -888,11 +894,16 @@ class ModelRunner:
         self.g_slots[:B].copy_(host[2], non_blocking=True)
         self.g_bt[:B].copy_(torch.from_numpy(d_bt).pin_memory(), non_blocking=True)
         self.g_len[:B].copy_(torch.from_numpy(d_len).pin_memory(), non_blocking=True)
+        longest = int(d_len.max())
         if B in self.cgraphs:
             plan = self._cascade_plan(d_bt, d_len, max_work=self.casc_work)
             if plan is not None:
                 ops.cascade_tensors(plan, self.device, out=self.g_casc)
                 g, lg = self.cgraphs[B]
+                longest = int((d_len - plan.sstart).max())  # the per-sequence kernel covers suffixes only
+        nsplit = self.graph_plans[B][1]
+        split = max(64, -(-longest // (64 * nsplit)) * 64)
+        self.g_split.copy_(torch.tensor([split], dtype=torch.int32).pin_memory(), non_blocking=True)
         g.replay()
         if len(rows) == B and rows == list(range(B)):
             return lg

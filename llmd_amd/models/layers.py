@@ -225,7 +225,7 @@ class PagedAttention(torch.nn.Module):
                              meta.d_seq_lens, Hq, Hkv, D, self.scale, self.window, self.sinks,
                              split=meta.d_split, out=out[:nd], workspace=meta.d_workspace,
                              max_ctx=meta.d_max_ctx, k_scale=self.k_scale, v_scale=self.v_scale,
-                             cascade=meta.d_cascade)
+                             cascade=meta.d_cascade, split_dev=meta.d_split_dev)
         if meta.num_prefill_tokens:
             items = meta.p_items
             ops.paged_prefill(qkv[nd:], self.k_cache, self.v_cache, meta.p_block_tables,

@@ -314,11 +314,13 @@ def cascade_tensors(plan: SharedPrefixPlan, device, out: Optional[torch.Tensor] 
 
 def paged_decode(q, k_cache, v_cache, block_tables, seq_lens, Hq, Hkv, D, scale, window=0,
                  sinks=None, split=None, out=None, workspace=None, max_ctx=None, k_scale=1.0, v_scale=1.0,
-                 cascade=None):
+                 cascade=None, split_dev=None):
     """q: [B, >=Hq*D] -> out [B, Hq*D]. k/v caches bf16 or fp8 e4m3fn (dequant scales).
     cascade: (tensor, np, max_slots) from cascade_tensors(shared_prefix_plan(...)): shared
     prefixes are read once per group by the prefix kernel; `split` must then cover the
-    longest suffix (L - sstart), and the workspace holds nsplit + max_slots slots per row."""
+    longest suffix (L - sstart), and the workspace holds nsplit + max_slots slots per row.
+    split_dev: int32 [1] device tensor of keys per split read by the kernels instead of
+    split[0] (a captured hipGraph re-sizes its splits per step; nsplit stays the grid)."""
     if not _gpu(q):
         r = ref.paged_decode(q, k_cache, v_cache, block_tables, seq_lens, Hq, Hkv, D, scale,
                              window, sinks, k_scale, v_scale)
@@ -350,7 +352,7 @@ def paged_decode(q, k_cache, v_cache, block_tables, seq_lens, Hq, Hkv, D, scale,
         part_o = part_ml = out.new_empty(0, dtype=torch.float32)
     native().paged_decode(out, q, k_cache, v_cache, block_tables, seq_lens, Hq, Hkv, D, scale,
                           window, sinks, split_size, nsplit, part_o, part_ml, k_scale, v_scale,
-                          ctens, cnp, nslot)
+                          ctens, cnp, nslot, split_dev)
     return out
 
 

@@ -117,6 +117,10 @@ def test_paged_decode(Hq, Hkv, D, bs):
     for split in [None, (64, 79), (4096, 2), (5056, 1)]:
         o = ops.paged_decode(q, kc, vc, bt, sl, Hq, Hkv, D, scale, split=split, max_ctx=max(lens))
         _close(o, r)
+    # device-side split size (hipGraph replay): the grid's 8 splits re-sized to 640 keys
+    o = ops.paged_decode(q, kc, vc, bt, sl, Hq, Hkv, D, scale, split=(16384, 8), max_ctx=max(lens),
+                         split_dev=torch.tensor([640], dtype=torch.int32, device=DEV))
+    _close(o, r)
 
 
 def test_paged_decode_window_sinks():
