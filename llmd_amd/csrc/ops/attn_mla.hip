@@ -42,8 +42,8 @@ __global__ __launch_bounds__(NT, 1) void mla_kernel(
     const uint16_t* __restrict__ q, int64_t q_row_stride, const void* __restrict__ kcv,
     int64_t block_stride, int bs, const int* __restrict__ block_tables, int bt_stride,
     const int* __restrict__ row_seq, const int* __restrict__ row_len, int H, float scale_log2,
-    int split_size, int nsplit, uint16_t* __restrict__ out, int64_t out_row_stride,
-    float* __restrict__ part_o, float* __restrict__ part_ml, float kv_scale) {
+    int split_size, const int* __restrict__ split_dev, int nsplit, uint16_t* __restrict__ out,
+    int64_t out_row_stride, float* __restrict__ part_o, float* __restrict__ part_ml, float kv_scale) {
   // fp8 (e4m3fn) latent caches: 8-B loads widened to bf16 when written to LDS
   using CR = typename std::conditional<F8, u32x2_t, u32x4_t>::type;
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -53,6 +53,7 @@ __global__ __launch_bounds__(NT, 1) void mla_kernel(
 
   const int sp = blockIdx.x, hg = blockIdx.y, r = blockIdx.z;
   const int len = row_len[r];
+  if (split_dev) split_size = *split_dev;  // hipGraph replay: keys per split sized to this step's rows
   const int k0 = sp * split_size, k1 = min(len, k0 + split_size);
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, g = lane >> 4, c16 = lane & 15;
   const int head = hg * 16 + c16;
@@ -245,13 +246,14 @@ __global__ __launch_bounds__(64 * NW, 1) void mla_v2_kernel(
     const uint16_t* __restrict__ q, int64_t q_row_stride, const void* __restrict__ kcv,
     int64_t block_stride, int bs, const int* __restrict__ block_tables, int bt_stride,
     const int* __restrict__ row_seq, const int* __restrict__ row_len, int H, float scale_log2,
-    int split_size, int nsplit, uint16_t* __restrict__ out, int64_t out_row_stride,
-    float* __restrict__ part_o, float* __restrict__ part_ml, float kv_scale) {
+    int split_size, const int* __restrict__ split_dev, int nsplit, uint16_t* __restrict__ out,
+    int64_t out_row_stride, float* __restrict__ part_o, float* __restrict__ part_ml, float kv_scale) {
   __shared__ __attribute__((aligned(1024))) char buf0[V2_TILE];
   __shared__ __attribute__((aligned(1024))) char buf1[V2_TILE];
   const uint16_t* kc = reinterpret_cast<const uint16_t*>(kcv);
   const int sp = blockIdx.x, r = blockIdx.z;
   const int len = row_len[r];
+  if (split_dev) split_size = *split_dev;  // hipGraph replay: keys per split sized to this step's rows
   const int k0 = sp * split_size, k1 = min(len, k0 + split_size);
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, g = lane >> 4, c16 = lane & 15;
   const int h0 = 16 * (NW * blockIdx.y + w);  // this wave's first head
@@ -470,10 +472,11 @@ __global__ __launch_bounds__(64 * NW, 1) void mla_v2_kernel(
 __global__ __launch_bounds__(128) void mla_reduce_kernel(const float* __restrict__ part_o,
                                                          const float* __restrict__ part_ml,
                                                          const int* __restrict__ row_len, int H, int nsplit,
-                                                         int split_size, uint16_t* __restrict__ out,
-                                                         int64_t out_row_stride) {
+                                                         int split_size, const int* __restrict__ split_dev,
+                                                         uint16_t* __restrict__ out, int64_t out_row_stride) {
   const int hh = blockIdx.x, r = blockIdx.y;
   const int len = row_len[r];
+  if (split_dev) split_size = *split_dev;
   const int nact = min(nsplit, (len + split_size - 1) / split_size);
   const int64_t base = ((int64_t)r * H + hh) * nsplit;
   float M = NEG_INF;
@@ -526,7 +529,7 @@ extern "C" int llmd_mla_attention(const void* q, int64_t q_row_stride, const voi
                                   int bs, const int* block_tables, int bt_stride, const int* row_seq,
                                   const int* row_len, int R, int H, float scale, int split_size, int nsplit,
                                   void* out, int64_t out_row_stride, float* part_o, float* part_ml, int fp8,
-                                  float kv_scale, hipStream_t st) {
+                                  float kv_scale, const int* split_dev, hipStream_t st) {
   if (R == 0) return 0;
   if (split_size % 64 != 0 || nsplit < 1) return -1;
   const size_t lds = KTILE + PIMG + 128 * sizeof(float);
@@ -541,8 +544,8 @@ extern "C" int llmd_mla_attention(const void* q, int64_t q_row_stride, const voi
 #define V2(NW, BIG, F8)                                                                                        \
   hipLaunchKernelGGL((mla_v2_kernel<NW, BIG, F8>), dim3(nsplit, H / (16 * NW), R), dim3(64 * NW), 0, st,      \
                      (const uint16_t*)q, q_row_stride, kc, block_stride, bs, block_tables, bt_stride, row_seq, \
-                     row_len, H, scale_log2, split_size, nsplit, (uint16_t*)out, out_row_stride, part_o, part_ml, \
-                     kv_scale)
+                     row_len, H, scale_log2, split_size, split_dev, nsplit, (uint16_t*)out, out_row_stride,       \
+                     part_o, part_ml, kv_scale)
 #define V2NW(NW)                                   \
   if (fp8) {                                       \
     if (big) V2(NW, true, true); else V2(NW, false, true);   \
@@ -562,16 +565,16 @@ extern "C" int llmd_mla_attention(const void* q, int64_t q_row_stride, const voi
     if (fp8) {
       hipLaunchKernelGGL(mla_kernel<true>, grid, dim3(NT), lds, st, (const uint16_t*)q, q_row_stride, kc,
                          block_stride, bs, block_tables, bt_stride, row_seq, row_len, H, scale_log2, split_size,
-                         nsplit, (uint16_t*)out, out_row_stride, part_o, part_ml, kv_scale);
+                         split_dev, nsplit, (uint16_t*)out, out_row_stride, part_o, part_ml, kv_scale);
     } else {
       hipLaunchKernelGGL(mla_kernel<false>, grid, dim3(NT), lds, st, (const uint16_t*)q, q_row_stride, kc,
                          block_stride, bs, block_tables, bt_stride, row_seq, row_len, H, scale_log2, split_size,
-                         nsplit, (uint16_t*)out, out_row_stride, part_o, part_ml, kv_scale);
+                         split_dev, nsplit, (uint16_t*)out, out_row_stride, part_o, part_ml, kv_scale);
     }
   }
   if (nsplit > 1) {
     hipLaunchKernelGGL(mla_reduce_kernel, dim3(H, R), dim3(128), 0, st, part_o, part_ml, row_len, H, nsplit,
-                       split_size, (uint16_t*)out, out_row_stride);
+                       split_size, split_dev, (uint16_t*)out, out_row_stride);
   }
   return (int)hipGetLastError();
 }

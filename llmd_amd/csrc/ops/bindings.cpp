@@ -42,7 +42,7 @@ int llmd_kvx_ipc_open(const void*, void**);
 int llmd_kvx_ipc_close(void*);
 int llmd_mla_attention(const void*, int64_t, const void*, int64_t, int, const int*, int, const int*,
                        const int*, int, int, float, int, int, void*, int64_t, float*, float*, int, float,
-                       hipStream_t);
+                       const int*, hipStream_t);
 int llmd_mla_rope_cache(const void*, int64_t, void*, int64_t, const void*, int64_t, const void*, int64_t,
                         const int64_t*, const float*, int, int, const int64_t*, void*, int64_t, int, int, float,
                         hipStream_t);
@@ -307,10 +307,16 @@ void paged_decode(torch::Tensor out, torch::Tensor q, torch::Tensor k_cache, tor
 // out [R, H*512]; row r attends to keys [0, row_len[r]) of sequence row_seq[r].
 void mla_attention(torch::Tensor out, torch::Tensor q, torch::Tensor cache, torch::Tensor block_tables,
                    torch::Tensor row_seq, torch::Tensor row_len, int64_t H, double scale, int64_t split_size,
-                   int64_t nsplit, torch::Tensor part_o, torch::Tensor part_ml, double kv_scale) {
+                   int64_t nsplit, torch::Tensor part_o, torch::Tensor part_ml, double kv_scale,
+                   c10::optional<torch::Tensor> split_dev) {
   const c10::hip::OptionalHIPGuard device_guard(dev_of(out));
   CHECK_CUDA(q); CHECK_BF16(q); CHECK_BF16(out); CHECK_INNER(q); CHECK_INNER(out);
   const bool f8 = is_fp8_cache(cache);
+  const int* sdev = nullptr;  // int32 [1] keys per split (hipGraph replay), overrides split_size
+  if (split_dev.has_value()) {
+    CHECK_CUDA(split_dev.value()); CHECK_DT(split_dev.value(), at::kInt);
+    sdev = split_dev->data_ptr<int>();
+  }
   CHECK_DT(block_tables, at::kInt); CHECK_DT(row_seq, at::kInt); CHECK_DT(row_len, at::kInt);
   TORCH_CHECK(cache.dim() == 3 && cache.size(2) == 576 && cache.stride(2) == 1 && cache.stride(1) == 576,
               "mla cache [blocks, bs, 576] with contiguous rows");
@@ -331,7 +337,7 @@ void mla_attention(torch::Tensor out, torch::Tensor q, torch::Tensor cache, torc
                               row_len.data_ptr<int>(), R, H, (float)scale, split_size, nsplit, out.data_ptr(),
                               out.stride(0), nsplit > 1 ? part_o.data_ptr<float>() : nullptr,
                               nsplit > 1 ? part_ml.data_ptr<float>() : nullptr, f8 ? 1 : 0, (float)kv_scale,
-                              cur_stream());
+                              sdev, cur_stream());
   TORCH_CHECK(rc == 0, "mla_attention failed: ", rc);
 }
 

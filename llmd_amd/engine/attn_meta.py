@@ -39,6 +39,7 @@ class AttnMeta:
     mla_d_rows: Optional[torch.Tensor] = None      # [Bd] int32 = arange (row -> d_block_tables row)
     mla_split: Optional[tuple] = None              # fixed (split_size, nsplit) under graph capture
     mla_workspace: Optional[tuple] = None
+    mla_split_dev: Optional[torch.Tensor] = None   # [1] int32 keys per split, set per graph replay
     p_row_seq: Optional[torch.Tensor] = None       # [Tp] int32 prefill token -> p_block_tables row
     p_row_len: Optional[torch.Tensor] = None       # [Tp] int32 keys visible (= position + 1)
     p_max_ctx: int = 0

@@ -717,6 +717,7 @@ class ModelRunner:
             need = max(B * p[1] for B, p in self.mla_plans.items())
             self.g_mla_ws = (torch.empty(need * self.Hq * 512, dtype=torch.float32, device=dev),
                              torch.empty(need * self.Hq * 2, dtype=torch.float32, device=dev))
+            self.g_mla_split = torch.full((1,), self.mla_plans[buckets[-1]][0], dtype=torch.int32, device=dev)
         pool = torch.cuda.graph_pool_handle()
         t0 = time.time()
         for B in reversed(buckets):
@@ -727,6 +728,8 @@ class ModelRunner:
                             d_split_dev=self.g_split)
             if self.is_mla:
                 meta.mla_d_rows, meta.mla_split, meta.mla_workspace = self.g_rows[:B], self.mla_plans[B], self.g_mla_ws
+                self.g_mla_split.fill_(self.mla_plans[B][0])
+                meta.mla_split_dev = self.g_mla_split
             s = torch.cuda.Stream()
             s.wait_stream(torch.cuda.current_stream())
             with torch.cuda.stream(s):
@@ -901,9 +904,14 @@ class ModelRunner:
                 ops.cascade_tensors(plan, self.device, out=self.g_casc)
                 g, lg = self.cgraphs[B]
                 longest = int((d_len - plan.sstart).max())  # the per-sequence kernel covers suffixes only
-        nsplit = self.graph_plans[B][1]
-        split = max(64, -(-longest // (64 * nsplit)) * 64)
-        self.g_split.copy_(torch.tensor([split], dtype=torch.int32).pin_memory(), non_blocking=True)
+        if self.is_mla:  # latent attention: >= 4 key tiles per split (a split re-reads its rows' 128-head Q)
+            nsplit = self.mla_plans[B][1]
+            split = max(256, -(-int(d_len.max()) // (64 * nsplit)) * 64)
+            self.g_mla_split.copy_(torch.tensor([split], dtype=torch.int32).pin_memory(), non_blocking=True)
+        else:
+            nsplit = self.graph_plans[B][1]
+            split = max(64, -(-longest // (64 * nsplit)) * 64)
+            self.g_split.copy_(torch.tensor([split], dtype=torch.int32).pin_memory(), non_blocking=True)
         g.replay()
         if len(rows) == B and rows == list(range(B)):
             return lg

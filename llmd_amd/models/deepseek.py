@@ -98,7 +98,7 @@ class MLAAttention(torch.nn.Module):
         if nd:
             ops.mla_attention(q_lat[:nd], self.cache, meta.d_block_tables, meta.mla_d_rows, meta.d_seq_lens, H,
                               self.scale, max_len=meta.d_max_ctx, split=meta.mla_split, out=o_lat[:nd],
-                              workspace=meta.mla_workspace, kv_scale=self.kv_scale)
+                              workspace=meta.mla_workspace, kv_scale=self.kv_scale, split_dev=meta.mla_split_dev)
         if meta.num_prefill_tokens:
             ops.mla_attention(q_lat[nd:], self.cache, meta.p_block_tables, meta.p_row_seq, meta.p_row_len, H,
                               self.scale, max_len=meta.p_max_ctx, out=o_lat[nd:], kv_scale=self.kv_scale)

@@ -701,10 +701,11 @@ def mla_split_plan(max_len: int, rows: int, H: int, num_cus: int = 256) -> tuple
 
 
 def mla_attention(q, cache, block_tables, row_seq, row_len, H, scale, max_len=None, split=None, out=None,
-                  workspace=None, kv_scale=1.0):
+                  workspace=None, kv_scale=1.0, split_dev=None):
     """Absorbed-MLA attention over the paged latent cache (csrc/ops/attn_mla.hip).
     q [R, H*576] bf16, cache [blocks, bs, 576] bf16 or fp8 e4m3fn (dequant
-    x kv_scale) -> out [R, H*512]."""
+    x kv_scale) -> out [R, H*512]. split_dev: int32 [1] device keys per split
+    overriding split[0] (hipGraph replay; nsplit stays the grid)."""
     if not _gpu(q):
         r = ref.mla_attention(q, cache, block_tables, row_seq, row_len, H, scale, kv_scale)
         if out is not None:
@@ -728,7 +729,7 @@ def mla_attention(q, cache, block_tables, row_seq, row_len, H, scale, max_len=No
     else:
         part_o = part_ml = out.new_empty(0, dtype=torch.float32)
     native().mla_attention(out, q, cache, block_tables, row_seq, row_len, H, scale, split_size, nsplit,
-                           part_o, part_ml, kv_scale)
+                           part_o, part_ml, kv_scale, split_dev)
     return out
 
 

@@ -139,6 +139,11 @@ def test_mla_kernel_matches_reference():
             got = ops.mla_attention(q, cache, bt, rows, ln, H, scale, split=split)
             err = (got.float() - want.float()).abs().max().item()
             assert err < 2e-2, (H, lens, split, err)
+        # device-side split size (hipGraph replay): a 16k-key plan's 8 splits re-sized to the rows
+        dyn = torch.tensor([max(256, math.ceil(max(lens) / (64 * 8)) * 64)], dtype=torch.int32, device=dev)
+        got = ops.mla_attention(q, cache, bt, rows, ln, H, scale, split=(16384, 8), split_dev=dyn)
+        err = (got.float() - want.float()).abs().max().item()
+        assert err < 2e-2, (H, lens, "split_dev", err)
 
 
 @pytest.mark.gpu
