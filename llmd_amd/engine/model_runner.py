@@ -104,11 +104,13 @@ class ModelRunner:
             self.kv_dtype = torch.float8_e4m3fn
         else:
             raise ValueError(f"unsupported --kv-cache-dtype {cfg.cache.kv_cache_dtype}")
-        # shared-prefix decode (ops.shared_prefix_plan): GQA kernels only, every
-        # layer full-context (a sliding-window layer needs the plain split plan)
+        # shared-prefix decode (ops.shared_prefix_plan): GQA kernels only; sliding-window
+        # layers (gpt-oss) keep the plain kernel, so the step's split must also cover
+        # their window (self.max_window)
         G = self.Hq // self.Hkv
+        self.max_window = max((a.window for a in attn if a.window), default=0)
         self.cascade_ok = (cfg.cache.shared_prefix_decode and cfg.cache.enable_prefix_caching and not self.is_mla
-                           and G <= 16 and 16 % G == 0 and not any(a.window for a in attn))
+                           and G <= 16 and 16 % G == 0)
         self.casc_variant = ops.cascade_variant(G, self.D, self.bs, self.kv_dtype != torch.bfloat16)
         self.cascade_ok = self.cascade_ok and self.casc_variant is not None
         self.casc_work = max(16, -(-512 // self.Hkv))  # prefix work units: ~2 workgroups per CU over kv heads
@@ -542,7 +544,8 @@ class ModelRunner:
             plan = self._cascade_plan(d_bt, d_len)
             if plan is not None:
                 meta.d_cascade = ops.cascade_tensors(plan, dev)
-                mctx = int((d_len - plan.sstart[:nd]).max())  # splits cover the longest own suffix
+                # splits cover the longest own suffix (and a windowed layer's window)
+                mctx = max(int((d_len - plan.sstart[:nd]).max()), min(self.max_window, mctx))
             meta.d_split = ops.decode_split_plan(mctx, nd, self.Hkv, self.Hq // self.Hkv)
         if p_ql:
             meta.num_prefill_tokens = sum(p_ql)
@@ -903,7 +906,8 @@ class ModelRunner:
             if plan is not None:
                 ops.cascade_tensors(plan, self.device, out=self.g_casc)
                 g, lg = self.cgraphs[B]
-                longest = int((d_len - plan.sstart).max())  # the per-sequence kernel covers suffixes only
+                # the per-sequence kernel covers suffixes only (windowed layers: their window)
+                longest = max(int((d_len - plan.sstart).max()), min(self.max_window, longest))
         if self.is_mla:  # latent attention: >= 4 key tiles per split (a split re-reads its rows' 128-head Q)
             nsplit = self.mla_plans[B][1]
             split = max(256, -(-int(d_len.max()) // (64 * nsplit)) * 64)

@@ -172,10 +172,11 @@ def _shared_prefix_run(device, monkeypatch, model="tiny-llama", **kw):
     return eng, prompts, outs, any(calls)
 
 
-def test_engine_shared_prefix_decode_cpu(monkeypatch):
+@pytest.mark.parametrize("model", ["tiny-llama", "tiny-gpt-oss"])
+def test_engine_shared_prefix_decode_cpu(monkeypatch, model):
     """The engine groups the decode rows that share the cached prefix (CPU:
     the reference attention ignores the plan, so outputs are unchanged)."""
-    _, _, a, used = _shared_prefix_run("cpu", monkeypatch)
+    _, _, a, used = _shared_prefix_run("cpu", monkeypatch, model)
     assert used
-    _, _, b, used_off = _shared_prefix_run("cpu", monkeypatch, shared_prefix_decode=False)
+    _, _, b, used_off = _shared_prefix_run("cpu", monkeypatch, model, shared_prefix_decode=False)
     assert not used_off and a == b

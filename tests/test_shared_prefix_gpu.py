@@ -9,7 +9,8 @@ from test_shared_prefix import _shared_prefix_run
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("model,variant", [("tiny-llama", 1), ("small-llama", 3)])
+@pytest.mark.parametrize("model,variant", [("tiny-llama", 1), ("small-llama", 3),
+                                           ("tiny-gpt-oss", 3)])  # sliding-window layers + sinks
 @pytest.mark.parametrize("eager", [False, True])
 def test_engine_shared_prefix_decode_gpu(monkeypatch, eager, model, variant):
     eng, prompts, got, used = _shared_prefix_run("cuda", monkeypatch, model, enforce_eager=eager)
