@@ -364,6 +364,7 @@ __global__ __launch_bounds__(NT, NP == 1 ? 2 : 1) void shared_prefix_kernel(
   const int m0 = wk[0], nm = wk[1], s0 = wk[2], s1 = wk[3], slot = wk[4];
   if (nm <= 0 || s0 >= s1) return;
   const int spp = 16 / G;  // members per 16-column pass (host: 16 % G == 0, nm <= spp*NP)
+  LLMD_DCHECK(nm <= spp * NP && s1 <= bt_stride * bs);
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int g = lane >> 4, c16 = lane & 15;
   const int* bt = block_tables + (int64_t)members[m0] * bt_stride;
@@ -443,6 +444,7 @@ __global__ __launch_bounds__(NT, 2) void shared_prefix_v2_kernel(
   if (nm <= 0 || lo >= hi) return;
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, g = lane >> 4, c16 = lane & 15;
   const bool two_heads = G == 8;  // else G == 4 (host-checked)
+  LLMD_DCHECK(nm <= (two_heads ? 16 : 32) && lo % 64 == 0 && hi <= bt_stride * bs);
   const int* bt = block_tables + (int64_t)members[m0] * bt_stride;
   const int64_t head_off = (int64_t)kvh * bs * D;
   const int lbs = __builtin_ctz(bs);

@@ -37,6 +37,24 @@ ql = torch.tensor([ctx], dtype=torch.int32, device=dev)
 outp = ops.paged_prefill(qp, kc, vc, bt, qs, ql, sl, Hq, Hkv, D, D ** -0.5)
 wantp = ref.paged_prefill(qp, kc, vc, bt, qs, ql, sl, Hq, Hkv, D, D ** -0.5)
 assert (outp.float() - wantp.float()).abs().max().item() < 0.05
+# shared-prefix decode (both prefix kernels) + device-side split size: 4 sequences share 4 blocks
+import numpy as np
+nb2 = 24
+kc2 = torch.randn(nb2, Hkv, bs, D, device=dev).bfloat16()
+vc2 = torch.randn(nb2, Hkv, bs, D, device=dev).bfloat16()
+rows = [[0, 1, 2, 3, 4 + 2 * i, 5 + 2 * i] for i in range(4)]
+bt2 = np.array(rows, dtype=np.int32)
+ln2 = np.array([300, 330, 383, 290], dtype=np.int32)
+q2 = torch.randn(4, Hq * D, device=dev).bfloat16()
+btd, lnd = torch.from_numpy(bt2).to(dev), torch.from_numpy(ln2).to(dev)
+want2 = ref.paged_decode(q2, kc2, vc2, btd, lnd, Hq, Hkv, D, D ** -0.5)
+for variant in (1, 3):
+    plan = ops.shared_prefix_plan(bt2, ln2, bs, Hq // Hkv, Hkv, variant=variant, min_prefix=128, min_chunk=64)
+    assert plan is not None and plan.items == 1, plan
+    got2 = ops.paged_decode(q2, kc2, vc2, btd, lnd, Hq, Hkv, D, D ** -0.5, split=(256, 1),
+                            cascade=ops.cascade_tensors(plan, dev),
+                            split_dev=torch.tensor([128], dtype=torch.int32, device=dev))
+    assert (got2.float() - want2.float()).abs().max().item() < 0.05, variant
 # medium-M decode GEMM with split-K
 x = torch.randn(96, 1024, device=dev).bfloat16()
 w = (torch.randn(640, 1024, device=dev) * 0.05).bfloat16()
