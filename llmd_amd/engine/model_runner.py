@@ -912,9 +912,9 @@ class ModelRunner:
             nsplit = self.mla_plans[B][1]
             split = max(256, -(-int(d_len.max()) // (64 * nsplit)) * 64)
             self.g_mla_split.copy_(torch.tensor([split], dtype=torch.int32).pin_memory(), non_blocking=True)
-        else:
-            nsplit = self.graph_plans[B][1]
-            split = max(64, -(-longest // (64 * nsplit)) * 64)
+        else:  # the step's own split plan for its real rows, within the captured grid's splits
+            split, _ = ops.decode_split_plan(longest, max(1, n), self.Hkv, self.Hq // self.Hkv,
+                                             max_splits=self.graph_plans[B][1])
             self.g_split.copy_(torch.tensor([split], dtype=torch.int32).pin_memory(), non_blocking=True)
         g.replay()
         if len(rows) == B and rows == list(range(B)):

@@ -141,17 +141,33 @@ def prefill_tokens_per_item(Hq: int, Hkv: int, D: int = 128, block_size: int = 6
 
 
 def decode_split_plan(max_ctx: int, batch: int, Hkv: int, G: int, num_cus: int = 256,
-                      min_split: int = 256) -> tuple[int, int]:
-    """Pick (split_size, nsplit) for the decode kernel: enough workgroups to
-    fill 256 CUs at ~2 WGs/CU, splits a multiple of 64 keys."""
+                      min_split: int = 256, max_splits: Optional[int] = None) -> tuple[int, int]:
+    """Pick (split_size, nsplit) for the decode kernel by a makespan model:
+    batch x head-groups x nsplit workgroups run in rounds of two per CU, a
+    round lasts as long as one split (its keys), plus a small per-split cost
+    (partials + reduce). Splits are multiples of 64 keys and at least
+    `min_split` when there is more than one. Measured (profiles/decode_nsplit.txt):
+    batch 48 at 7.4k context 293 -> 264 us with 4 splits instead of 2 (1536
+    workgroups = 3 full rounds rather than 768 = 1.5)."""
     ng = (G + 15) // 16
     base = max(1, batch * Hkv * ng)
-    target = 2 * num_cus
-    nsplit = max(1, min(math.ceil(max_ctx / min_split), math.ceil(target / base)))
-    split = math.ceil(max_ctx / nsplit / 64) * 64
-    split = max(split, 64)
-    nsplit = math.ceil(max_ctx / split)
-    return split, nsplit
+    slots = 2 * num_cus
+    ctx = max(1, max_ctx)
+    hi = max(1, math.ceil(ctx / min_split))
+    if max_splits is not None:
+        hi = max(1, min(hi, max_splits))
+    best = None
+    for n in range(1, min(hi, 64) + 1):
+        split = max(64, math.ceil(ctx / n / 64) * 64)
+        n_eff = math.ceil(ctx / split)
+        w = base * n_eff
+        # up to two rounds the last one's idle slots are lost; beyond, workgroups of
+        # uneven sequences finish at different times and the tail shrinks
+        rounds = math.ceil(w / slots) if w <= 2 * slots else w / slots
+        cost = rounds * split + 16 * n_eff
+        if best is None or cost < best[0]:
+            best = (cost, split, n_eff)
+    return best[1], best[2]
 
 
 class SharedPrefixPlan:
