@@ -1,7 +1,13 @@
 import os
 import sys
 
-import pytest
+# CPU runs: engines, gloo ranks and reference ops each start an OpenMP pool; with
+# one pool per process sized to every core, multi-process tests oversubscribe the
+# CPUs and spin-waiting pools slow them ~10x. An explicit setting (the GPU box
+# exports 16) wins.
+os.environ.setdefault("OMP_NUM_THREADS", "2")
+
+import pytest  # noqa: E402
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 if ROOT not in sys.path:
