@@ -42,7 +42,13 @@ def main():
     from llmd_amd.ops.gemm_tuning import enable_lookup
     enable_lookup()
     nat = ops.native()
-    for name, (N, K) in SHAPES[a.model].items():
+    if a.model in SHAPES:
+        shapes = SHAPES[a.model]
+    else:  # any preset: its dense projection shapes at TP1
+        from llmd_amd.ops.gemm_tuning import model_gemm_shapes
+
+        shapes = {k: v for k, v in model_gemm_shapes(a.model).items() if k != "lm_head"}
+    for name, (N, K) in shapes.items():
         nw = max(2, -(-(1 << 30) // (N * K * 2)) + 1)
         ws = [(torch.randn(N, K, device="cuda") * 0.02).bfloat16() for _ in range(nw)]
         by = N * K * 2
