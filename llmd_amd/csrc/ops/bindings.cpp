@@ -54,6 +54,8 @@ int llmd_dgemm_supported(int, int, int);
 int llmd_mgemm(const void*, int64_t, const void*, int64_t, int, int, int, int, int, int, void*, int64_t, float*,
                hipStream_t);
 int llmd_mgemm_lds(int, int, int);
+int llmd_mgemm_fp8(const void*, int64_t, const float*, const void*, int64_t, const float*, int, int, int, int, int,
+                   int, void*, int64_t, float*, hipStream_t);
 int llmd_vmm_granularity(int, size_t*);
 int llmd_vmm_alloc(int, size_t, int, void**, uint64_t*);
 int llmd_vmm_export_fd(uint64_t, int*);
@@ -428,6 +430,32 @@ void mgemm(torch::Tensor y, torch::Tensor x, torch::Tensor w, int64_t wrb, int64
                       (int)stages, y.data_ptr(), y.stride(0), nsplit > 1 ? part.data_ptr<float>() : nullptr,
                       cur_stream());
   TORCH_CHECK(rc == 0, "mgemm failed: ", rc);
+}
+
+// fp8 W8A8 form: xq [M, K] e4m3fn with per-token scales xs [M, 1], wq [N, K] e4m3fn with
+// per-channel scales ws [1, N] (ops.fp8_linear's operands); K % 128 == 0
+void mgemm_fp8(torch::Tensor y, torch::Tensor xq, torch::Tensor xs, torch::Tensor wq, torch::Tensor ws, int64_t wrb,
+               int64_t nsplit, int64_t stages, torch::Tensor part) {
+  const c10::hip::OptionalHIPGuard device_guard(dev_of(y));
+  CHECK_CUDA(xq); CHECK_BF16(y); CHECK_INNER(xq); CHECK_INNER(wq); CHECK_INNER(y);
+  TORCH_CHECK(xq.scalar_type() == at::kFloat8_e4m3fn && wq.scalar_type() == at::kFloat8_e4m3fn, "mgemm_fp8: e4m3fn");
+  CHECK_DT(xs, at::kFloat); CHECK_DT(ws, at::kFloat);
+  TORCH_CHECK(xq.dim() == 2 && wq.dim() == 2 && y.dim() == 2, "mgemm_fp8: 2-D operands");
+  const int M = xq.size(0), K = xq.size(1), N = wq.size(0);
+  TORCH_CHECK(M >= 1 && M <= 128 && wq.size(1) == K && K % 128 == 0, "mgemm_fp8: M <= 128, K % 128 == 0");
+  TORCH_CHECK(N % 4 == 0 && y.size(0) == M && y.size(1) == N, "mgemm_fp8: output shape / N % 4");
+  TORCH_CHECK(xs.is_contiguous() && xs.numel() == M && ws.is_contiguous() && ws.numel() == N, "mgemm_fp8: scales");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(ws.data_ptr()) % 16 == 0, "mgemm_fp8: 16-B aligned weight scales");
+  TORCH_CHECK(xq.stride(0) % 16 == 0 && wq.stride(0) % 16 == 0 && y.stride(0) % 4 == 0, "mgemm_fp8: row alignment");
+  TORCH_CHECK(llmd_mgemm_lds(M, (int)wrb, (int)stages) > 0, "mgemm_fp8: no kernel for wrb=", wrb, " stages=", stages);
+  if (nsplit > 1) {
+    CHECK_DT(part, at::kFloat);
+    TORCH_CHECK(part.numel() >= nsplit * (int64_t)M * N, "mgemm_fp8: workspace");
+  }
+  int rc = llmd_mgemm_fp8(xq.data_ptr(), xq.stride(0), xs.data_ptr<float>(), wq.data_ptr(), wq.stride(0),
+                          ws.data_ptr<float>(), M, N, K, (int)wrb, (int)nsplit, (int)stages, y.data_ptr(), y.stride(0),
+                          nsplit > 1 ? part.data_ptr<float>() : nullptr, cur_stream());
+  TORCH_CHECK(rc == 0, "mgemm_fp8 failed: ", rc);
 }
 
 void paged_prefill(torch::Tensor out, torch::Tensor q, torch::Tensor k_cache,
@@ -881,6 +909,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {  // _C, or _C_debug (llmd_amd/build.p
   m.def("skinny_gemm", &skinny_gemm);
   m.def("skinny_supported", &skinny_supported);
   m.def("mgemm", &mgemm);
+  m.def("mgemm_fp8", &mgemm_fp8);
   m.def("mgemm_lds", [](int64_t M, int64_t wrb, int64_t stages) { return llmd_mgemm_lds((int)M, (int)wrb, (int)stages); });
   m.def("lora_bgmv", &lora_bgmv);
   m.def("mla_rope_cache", &mla_rope_cache);

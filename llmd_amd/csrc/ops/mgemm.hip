@@ -23,6 +23,13 @@
 // the 16 lanes of a ds_read_b128 pass (16 rows, one k chunk) hit 16 distinct
 // slots of the 256-B bank row.
 // Split-K partials: fp32 [split][M][N], summed and rounded by mgemm_reduce_kernel.
+//
+// fp8 (W8A8, e4m3fn, F8 = true): the same 128-B image rows hold 128 k per step;
+// a lane's 16-B fragment feeds two mfma_f32_16x16x32_fp8_fp8 (its low and high
+// 8 bytes - A and B lanes use the same k permutation, so each MFMA sums a
+// consistent 32-k subset), and the epilogue applies the per-token activation
+// scale and the per-channel weight scale (row-wise scales are constant over k,
+// so split-K partials are scaled before the reduce).
 #include "llmd_common.h"
 
 using namespace llmd;
@@ -46,12 +53,18 @@ struct Geo {
   static_assert(BM % 32 == 0, "MB must be even");
 };
 
-template <int MB, int WRB, int S>
-__global__ __launch_bounds__(NT, 1) void mgemm_kernel(const uint16_t* __restrict__ x, int64_t x_stride,
-                                                      const uint16_t* __restrict__ wt, int64_t w_stride, int M,
+template <int MB, int WRB, int S, bool F8 = false>
+__global__ __launch_bounds__(NT, 1) void mgemm_kernel(const void* __restrict__ xv, int64_t x_stride,
+                                                      const void* __restrict__ wv_, int64_t w_stride, int M,
                                                       int N, int K, int steps_per_split, uint16_t* __restrict__ y,
-                                                      int64_t y_stride, float* __restrict__ part) {
+                                                      int64_t y_stride, float* __restrict__ part,
+                                                      const float* __restrict__ xs, const float* __restrict__ wsc) {
   using G = Geo<MB, WRB, S>;
+  using E = typename std::conditional<F8, uint8_t, uint16_t>::type;
+  constexpr int CE = 16 / sizeof(E);  // elements per 16-B chunk
+  constexpr int KE = 8 * CE;          // k elements per step (one 128-B image row)
+  const E* x = reinterpret_cast<const E*>(xv);
+  const E* wt = reinterpret_cast<const E*>(wv_);
   __shared__ __attribute__((aligned(1024))) char st0[G::STAGE];
   __shared__ __attribute__((aligned(1024))) char st1[G::STAGE];
   __shared__ __attribute__((aligned(1024))) char st2[G::STAGE];
@@ -60,7 +73,7 @@ __global__ __launch_bounds__(NT, 1) void mgemm_kernel(const uint16_t* __restrict
   const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63, g = lane >> 4, c16 = lane & 15;
   const int ws = __builtin_amdgcn_readfirstlane(wv);
   const int row0 = tile * G::BN;
-  const int nk = K >> 6;
+  const int nk = K / KE;
   const int s0 = sp * steps_per_split;
   const int nsteps = min(nk, s0 + steps_per_split) - s0;  // >= 1: the host plans no empty split
   LLMD_DCHECK(nsteps >= 1 && M >= 1 && M <= 16 * MB);
@@ -73,20 +86,20 @@ __global__ __launch_bounds__(NT, 1) void mgemm_kernel(const uint16_t* __restrict
   for (int i = 0; i < G::NW; ++i) {
     const int r = 8 * (ws + 4 * i) + (lane >> 3);
     const int gr = min(row0 + r, N - 1);  // rows past N re-read the last row (result dropped)
-    woff[i] = (uint32_t)((int64_t)(gr - row0) * w_stride + 8 * ((lane & 7) ^ msw(r)));
+    woff[i] = (uint32_t)((int64_t)(gr - row0) * w_stride + CE * ((lane & 7) ^ msw(r)));
   }
 #pragma unroll
   for (int i = 0; i < G::NX; ++i) {
     const int r = 8 * (ws + 4 * i) + (lane >> 3);
-    xoff[i] = (uint32_t)((int64_t)min(r, M - 1) * x_stride + 8 * ((lane & 7) ^ msw(r)));
+    xoff[i] = (uint32_t)((int64_t)min(r, M - 1) * x_stride + CE * ((lane & 7) ^ msw(r)));
   }
-  const uint16_t* wbase = wt + (int64_t)row0 * w_stride;
+  const E* wbase = wt + (int64_t)row0 * w_stride;
   // each tile starts its K sweep at a rotated step so concurrent workgroups do
   // not stream the same k columns of W at once (DRAM channel spread)
   const int rot = nsteps > 0 ? (tile * 5) % nsteps : 0;
 
   auto issue = [&](char* stg, int t) {
-    const int k0 = (s0 + (t + rot) % nsteps) * 64;
+    const int k0 = (s0 + (t + rot) % nsteps) * KE;
 #pragma unroll
     for (int i = 0; i < G::NW; ++i)
       __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)(wbase + k0 + woff[i]),
@@ -124,16 +137,34 @@ __global__ __launch_bounds__(NT, 1) void mgemm_kernel(const uint16_t* __restrict
   auto compute = [&](const char* stg) {
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
-      bf16x8_t a[WRB], b[MB];
+      if constexpr (F8) {
+        u32x4_t a[WRB], b[MB];
 #pragma unroll
-      for (int rb = 0; rb < WRB; ++rb) a[rb] = *reinterpret_cast<const bf16x8_t*>(stg + aofs[rb][h]);
+        for (int rb = 0; rb < WRB; ++rb) a[rb] = *reinterpret_cast<const u32x4_t*>(stg + aofs[rb][h]);
 #pragma unroll
-      for (int mb = 0; mb < MB; ++mb) b[mb] = *reinterpret_cast<const bf16x8_t*>(stg + bofs[mb][h]);
+        for (int mb = 0; mb < MB; ++mb) b[mb] = *reinterpret_cast<const u32x4_t*>(stg + bofs[mb][h]);
 #pragma unroll
-      for (int rb = 0; rb < WRB; ++rb)
+        for (int hh = 0; hh < 2; ++hh)
 #pragma unroll
-        for (int mb = 0; mb < MB; ++mb)
-          acc[rb][mb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[rb], b[mb], acc[rb][mb], 0, 0, 0);
+          for (int rb = 0; rb < WRB; ++rb)
+#pragma unroll
+            for (int mb = 0; mb < MB; ++mb) {
+              const long av = (long)(((uint64_t)a[rb][2 * hh + 1] << 32) | a[rb][2 * hh]);
+              const long bv = (long)(((uint64_t)b[mb][2 * hh + 1] << 32) | b[mb][2 * hh]);
+              acc[rb][mb] = __builtin_amdgcn_mfma_f32_16x16x32_fp8_fp8(av, bv, acc[rb][mb], 0, 0, 0);
+            }
+      } else {
+        bf16x8_t a[WRB], b[MB];
+#pragma unroll
+        for (int rb = 0; rb < WRB; ++rb) a[rb] = *reinterpret_cast<const bf16x8_t*>(stg + aofs[rb][h]);
+#pragma unroll
+        for (int mb = 0; mb < MB; ++mb) b[mb] = *reinterpret_cast<const bf16x8_t*>(stg + bofs[mb][h]);
+#pragma unroll
+        for (int rb = 0; rb < WRB; ++rb)
+#pragma unroll
+          for (int mb = 0; mb < MB; ++mb)
+            acc[rb][mb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[rb], b[mb], acc[rb][mb], 0, 0, 0);
+      }
     }
   };
 
@@ -217,7 +248,13 @@ __global__ __launch_bounds__(NT, 1) void mgemm_kernel(const uint16_t* __restrict
     for (int rb = 0; rb < WRB; ++rb) {
       const int n = row0 + 16 * (WRB * wv + rb) + 4 * g;
       if (n >= N) continue;  // N % 4 == 0 (host check)
-      const f32x4_t v = acc[rb][mb];
+      f32x4_t v = acc[rb][mb];
+      if constexpr (F8) {  // row-wise scales: per-token activation x per-channel weight
+        const float sx = xs[m];
+        const f32x4_t sw = *reinterpret_cast<const f32x4_t*>(wsc + n);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) v[i] *= sx * sw[i];
+      }
       if (whole) {
         const uint32_t lo = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
         const uint32_t hi = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
@@ -242,25 +279,26 @@ __global__ __launch_bounds__(256) void mgemm_reduce_kernel(const float* __restri
   *reinterpret_cast<uint2*>(y + (int64_t)m * y_stride + n) = make_uint2(lo, hi);
 }
 
-typedef void (*mkern_t)(const uint16_t*, int64_t, const uint16_t*, int64_t, int, int, int, int, uint16_t*, int64_t,
-                        float*);
+typedef void (*mkern_t)(const void*, int64_t, const void*, int64_t, int, int, int, int, uint16_t*, int64_t,
+                        float*, const float*, const float*);
 
-template <int MB>
+template <int MB, bool F8>
 mkern_t pick_w(int wrb, int stages) {
-  if (wrb == 1) return stages == 3 ? mgemm_kernel<MB, 1, 3> : mgemm_kernel<MB, 1, 4>;
-  if (wrb == 2) return stages == 3 ? mgemm_kernel<MB, 2, 3> : mgemm_kernel<MB, 2, 4>;
+  if (wrb == 1) return stages == 3 ? mgemm_kernel<MB, 1, 3, F8> : mgemm_kernel<MB, 1, 4, F8>;
+  if (wrb == 2) return stages == 3 ? mgemm_kernel<MB, 2, 3, F8> : mgemm_kernel<MB, 2, 4, F8>;
   if (wrb == 4) {
-    if (stages == 3) return mgemm_kernel<MB, 4, 3>;
-    if constexpr (MB == 4) return mgemm_kernel<MB, 4, 4>;  // 160 KB: the only 4-stage ring of 256-row tiles that fits
+    if (stages == 3) return mgemm_kernel<MB, 4, 3, F8>;
+    if constexpr (MB == 4) return mgemm_kernel<MB, 4, 4, F8>;  // 160 KB: the only 4-stage ring of 256-row tiles that fits
   }
   return nullptr;
 }
 
+template <bool F8>
 mkern_t pick_m(int mb, int wrb, int stages) {
   switch (mb) {
-    case 4: return pick_w<4>(wrb, stages);
-    case 6: return pick_w<6>(wrb, stages);
-    case 8: return pick_w<8>(wrb, stages);
+    case 4: return pick_w<4, F8>(wrb, stages);
+    case 6: return pick_w<6, F8>(wrb, stages);
+    case 8: return pick_w<8, F8>(wrb, stages);
   }
   return nullptr;
 }
@@ -282,15 +320,40 @@ extern "C" int llmd_mgemm(const void* x, int64_t x_stride, const void* w, int64_
   if (M < 1 || M > 128 || K % 64 != 0 || N % 4 != 0 || nsplit < 1 || x_stride % 8 || w_stride % 8) return -1;
   if (llmd_mgemm_lds(M, wrb, stages) == 0) return -1;
   const int mb = M <= 64 ? 4 : M <= 96 ? 6 : 8;
-  mkern_t k = pick_m(mb, wrb, stages);
+  mkern_t k = pick_m<false>(mb, wrb, stages);
   if (k == nullptr) return -2;
   const int nk = K / 64;
   const int per = (nk + nsplit - 1) / nsplit;
   nsplit = (nk + per - 1) / per;  // no empty splits
   const int bn = 64 * wrb;
   dim3 grid((N + bn - 1) / bn, nsplit);
-  hipLaunchKernelGGL(k, grid, dim3(NT), 0, st, (const uint16_t*)x, x_stride, (const uint16_t*)w, w_stride, M, N, K,
-                     per, (uint16_t*)y, y_stride, part);
+  hipLaunchKernelGGL(k, grid, dim3(NT), 0, st, x, x_stride, w, w_stride, M, N, K, per, (uint16_t*)y, y_stride, part,
+                     (const float*)nullptr, (const float*)nullptr);
+  if (nsplit > 1) {
+    const int64_t total4 = (int64_t)M * N / 4;
+    hipLaunchKernelGGL(mgemm_reduce_kernel, dim3((unsigned)((total4 + 255) / 256)), dim3(256), 0, st, part, nsplit,
+                       M, N, (uint16_t*)y, y_stride);
+  }
+  return (int)hipGetLastError();
+}
+
+// fp8 W8A8: Y = (Xq sx) (Wq sw)^T, e4m3fn X [M, K] with per-row scales xs [M], e4m3fn
+// W [N, K] with per-channel scales ws [N]; K % 128 == 0 (128 k per 128-B image row).
+extern "C" int llmd_mgemm_fp8(const void* x, int64_t x_stride, const float* xs, const void* w, int64_t w_stride,
+                              const float* ws, int M, int N, int K, int wrb, int nsplit, int stages, void* y,
+                              int64_t y_stride, float* part, hipStream_t st) {
+  if (M < 1 || M > 128 || K % 128 != 0 || N % 4 != 0 || nsplit < 1 || x_stride % 16 || w_stride % 16) return -1;
+  if (llmd_mgemm_lds(M, wrb, stages) == 0) return -1;
+  const int mb = M <= 64 ? 4 : M <= 96 ? 6 : 8;
+  mkern_t k = pick_m<true>(mb, wrb, stages);
+  if (k == nullptr) return -2;
+  const int nk = K / 128;
+  const int per = (nk + nsplit - 1) / nsplit;
+  nsplit = (nk + per - 1) / per;
+  const int bn = 64 * wrb;
+  dim3 grid((N + bn - 1) / bn, nsplit);
+  hipLaunchKernelGGL(k, grid, dim3(NT), 0, st, x, x_stride, w, w_stride, M, N, K, per, (uint16_t*)y, y_stride, part,
+                     xs, ws);
   if (nsplit > 1) {
     const int64_t total4 = (int64_t)M * N / 4;
     hipLaunchKernelGGL(mgemm_reduce_kernel, dim3((unsigned)((total4 + 255) / 256)), dim3(256), 0, st, part, nsplit,

@@ -469,7 +469,7 @@ def fp8_linear(x, wq: torch.Tensor, w_scale: torch.Tensor, bias=None) -> torch.T
             return y.to(torch.bfloat16)
         if xq.shape[0] == 0:
             return torch.empty(0, wq.shape[0], dtype=torch.bfloat16, device=xq.device)
-        return torch._scaled_mm(xq, wq.t(), scale_a=xs, scale_b=w_scale, bias=bias, out_dtype=torch.bfloat16)
+        return _fp8_gemm(xq, xs, wq, w_scale, bias)
     lead = x.shape[:-1]
     x2 = x.reshape(-1, x.shape[-1])
     if not _gpu(x2):
@@ -481,8 +481,17 @@ def fp8_linear(x, wq: torch.Tensor, w_scale: torch.Tensor, bias=None) -> torch.T
     if x2.shape[0] == 0:
         return x2.new_empty(0, wq.shape[0]).reshape(*lead, -1)
     xq, xs = quant_fp8_rows(x2)
-    y = torch._scaled_mm(xq, wq.t(), scale_a=xs, scale_b=w_scale, bias=bias, out_dtype=torch.bfloat16)
-    return y.reshape(*lead, -1)
+    return _fp8_gemm(xq, xs, wq, w_scale, bias).reshape(*lead, -1)
+
+
+def _fp8_gemm(xq, xs, wq, w_scale, bias):
+    """Decode-sized M on the fp8 medium-M LDS-DMA GEMM where its measured table has it
+    ahead of hipBLASLt's (tuned) scaled GEMM, else torch._scaled_mm."""
+    if bias is None and _SKINNY and xq.is_contiguous() and wq.is_contiguous():
+        plan = mgemm_fp8_choice(xq.shape[0], wq.shape[0], wq.shape[1])
+        if plan is not None:
+            return mgemm_fp8(xq, xs, wq, w_scale, plan)
+    return torch._scaled_mm(xq, wq.t(), scale_a=xs, scale_b=w_scale, bias=bias, out_dtype=torch.bfloat16)
 
 
 def pow2_ceil(r: torch.Tensor) -> torch.Tensor:
@@ -856,6 +865,33 @@ def mgemm(x: torch.Tensor, w: torch.Tensor, plan: tuple[int, int, int]) -> torch
     part = torch.empty(ns * M * N if ns > 1 else 0, dtype=torch.float32, device=x.device)
     native().mgemm(y, x, w, wrb, ns, stages, part)
     return y
+
+
+def mgemm_fp8(xq: torch.Tensor, xs: torch.Tensor, wq: torch.Tensor, ws: torch.Tensor,
+              plan: tuple[int, int, int]) -> torch.Tensor:
+    """Y = (Xq sx)(Wq sw)^T on the medium-M GEMM's fp8 form (e4m3fn operands, per-token
+    scales xs [M, 1], per-channel scales ws [1, N]; K % 128 == 0), bf16 out."""
+    M = xq.shape[0]
+    N = wq.shape[0]
+    wrb, ns, stages = plan
+    y = torch.empty(M, N, dtype=torch.bfloat16, device=xq.device)
+    part = torch.empty(ns * M * N if ns > 1 else 0, dtype=torch.float32, device=xq.device)
+    native().mgemm_fp8(y, xq, xs, wq, ws, wrb, ns, stages, part)
+    return y
+
+
+def mgemm_fp8_choice(M: int, N: int, K: int) -> Optional[tuple[int, int, int]]:
+    """Plan of the fp8 medium-M GEMM for this shape (ops/mgemm_fp8_table.py,
+    winners over hipBLASLt's tuned scaled GEMM) at the smallest measured M >= M."""
+    from .mgemm_fp8_table import MGEMM_FP8_TABLE
+
+    if M < 33 or K % 128:
+        return None
+    for m in _MGEMM_MS:
+        if m >= M:
+            e = MGEMM_FP8_TABLE.get((m, N, K))
+            return e[0] if e is not None else None
+    return None
 
 
 def mgemm_ok(x: torch.Tensor, w: torch.Tensor) -> bool:

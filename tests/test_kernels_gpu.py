@@ -185,6 +185,26 @@ def test_paged_decode_shared_prefix(Hq, Hkv, D, bs, groups, fp8, variant):
         _close(o, plain)
 
 
+
+@pytest.mark.parametrize("M", [33, 64, 100, 128])
+@pytest.mark.parametrize("plan", [(1, 1, 3), (2, 3, 3), (4, 2, 3), (2, 5, 4)])
+def test_mgemm_fp8(M, plan):
+    """fp8 W8A8 medium-M GEMM (per-token x per-channel scales) vs the fp32 reference
+    of the dequantised operands, and against hipBLASLt's scaled GEMM."""
+    torch.manual_seed(7)
+    N, K = 1280, 1024
+    F8 = torch.float8_e4m3fn
+    xq = torch.randn(M, K, device=DEV).to(F8)
+    wq = (torch.randn(N, K, device=DEV) * 0.5).to(F8)
+    xs = torch.rand(M, 1, device=DEV) * 0.02 + 0.001
+    ws = torch.rand(1, N, device=DEV) * 0.02 + 0.001
+    want = (xq.float() * xs) @ (wq.float() * ws.view(-1, 1)).t()
+    got = ops.mgemm_fp8(xq, xs, wq, ws, plan)
+    _close(got, want, atol=2e-3, rtol=2e-2)
+    lib = torch._scaled_mm(xq, wq.t(), scale_a=xs, scale_b=ws, out_dtype=torch.bfloat16)
+    _close(got, lib, atol=2e-3, rtol=2e-2)
+
+
 @pytest.mark.parametrize("Hq,Hkv,D", [(64, 8, 128), (32, 8, 128), (8, 8, 128), (64, 8, 64), (16, 8, 128)])
 @pytest.mark.parametrize("bs", [16, 64])
 def test_paged_prefill(Hq, Hkv, D, bs):
