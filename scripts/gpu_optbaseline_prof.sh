@@ -1,13 +1,13 @@
-# kernel profile of the optimized-baseline ladder's rate-4 stage (one Qwen3-32B replica on one MI355X)
+# kernel profile of the optimized-baseline ladder's rate-8 stage (max-num-seqs 160) (one Qwen3-32B replica on one MI355X)
 set -o pipefail
 mkdir -p gpurun_out
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 rm -rf gpurun_out/ob_prof
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/ob_prof -o ob -- \
   python3 -u scripts/e2e_serving.py --model qwen3-32b --device cuda --replicas 1 --blocks 40000 \
-  --configs prefix --system-len 6000 --question-len 1200 --output-len 360 \
+  --configs prefix --system-len 6000 --question-len 1200 --output-len 360 --concurrency 160 \
   --workload guide_optimized-baseline_1.yaml \
-  --overrides "load.stages=[{rate: 4, duration: 40}],data.shared_prefix.num_groups=19" \
+  --overrides "load.stages=[{rate: 8, duration: 40}],data.shared_prefix.num_groups=19" \
   --out gpurun_out/ob_prof.json > gpurun_out/ob_prof.log 2>&1
 rc=$?
 grep "^\[e2e\]" gpurun_out/ob_prof.log | grep -v "\.\.\." | cut -c1-300
