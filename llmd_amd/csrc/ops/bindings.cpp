@@ -32,7 +32,8 @@ int llmd_paged_prefill(const void*, int64_t, const void*, const void*, int64_t, 
                        int, const float*, void*, int64_t, int, float, float, hipStream_t);
 int llmd_prefill_tokens_per_item(int, int, int, int, int);
 void llmd_sample(const void*, int64_t, int, int, int, const float*, const int64_t*, int64_t*, float*,
-                 hipStream_t);
+                 float*, int, hipStream_t);
+int llmd_sample_splits(int, int);
 void llmd_topk_topp_mask(float*, int64_t, int, int, const int*, const float*, const float*,
                          hipStream_t);
 int llmd_kvx_copy_blocks(void*, const void*, int64_t, int64_t, const int*, int, const int64_t*, int,
@@ -507,8 +508,12 @@ void sample(torch::Tensor logits, c10::optional<torch::Tensor> temps,
   if (temps.has_value()) { CHECK_DT(temps.value(), at::kFloat); TORCH_CHECK(temps->numel() >= B); t = temps->data_ptr<float>(); }
   if (seeds.has_value()) { CHECK_DT(seeds.value(), at::kLong); TORCH_CHECK(seeds->numel() >= B); s = seeds->data_ptr<int64_t>(); }
   if (out_logprob.has_value()) { CHECK_DT(out_logprob.value(), at::kFloat); lp = out_logprob->data_ptr<float>(); }
+  // small batches: each row split over several workgroups (partials merged by a second kernel)
+  const int nsp = llmd_sample_splits(B, V);
+  at::Tensor part;
+  if (nsp > 1) part = at::empty({(int64_t)B * nsp * 4}, logits.options().dtype(at::kFloat));
   llmd_sample(logits.data_ptr(), logits.stride(0), B, V, bf ? 1 : 0, t, s,
-              out_ids.data_ptr<int64_t>(), lp, cur_stream());
+              out_ids.data_ptr<int64_t>(), lp, nsp > 1 ? part.data_ptr<float>() : nullptr, nsp, cur_stream());
 }
 
 void topk_topp_mask(torch::Tensor logits, c10::optional<torch::Tensor> topk,

@@ -35,14 +35,19 @@ __device__ __forceinline__ Best better(Best a, Best b) {
   return (b.v > a.v || (b.v == a.v && b.i < a.i)) ? b : a;
 }
 
+// A row may be split over gridDim.y workgroups (batches smaller than the chip):
+// each takes a contiguous range of 8-element chunks and writes its (max, sum-exp,
+// best key, best index) to `part`; sample_merge_kernel folds them. The Gumbel
+// keys depend only on (seed, vocab index), so the pick is the same for any split.
 template <bool BF16>
 __global__ __launch_bounds__(NT) void sample_kernel(const void* __restrict__ logits,
                                                     int64_t stride, int V,
                                                     const float* __restrict__ temps,
                                                     const int64_t* __restrict__ seeds,
                                                     int64_t* __restrict__ out_ids,
-                                                    float* __restrict__ out_logprob) {
+                                                    float* __restrict__ out_logprob, float* __restrict__ part) {
   const int row = blockIdx.x;
+  const int nsp = gridDim.y, sp = blockIdx.y;
   const float T = temps ? temps[row] : 0.f;
   const bool greedy = !(T > 0.f);
   const float invT = greedy ? 1.f : 1.f / T;
@@ -65,23 +70,27 @@ __global__ __launch_bounds__(NT) void sample_kernel(const void* __restrict__ log
   };
   if (BF16) {
     const uint16_t* r = (const uint16_t*)logits + (int64_t)row * stride;
-    const int nchunk = V / 8;
-    for (int c = threadIdx.x; c < nchunk; c += NT) {
+    const int nchunk = V / 8, per = (nchunk + nsp - 1) / nsp;
+    const int c0 = sp * per, c1 = min(nchunk, c0 + per);
+    for (int c = c0 + threadIdx.x; c < c1; c += NT) {
       float f[8];
       unpack8(*reinterpret_cast<const u32x4_t*>(r + c * 8), f);
 #pragma unroll
       for (int j = 0; j < 8; ++j) consume(f[j], c * 8 + j);
     }
-    for (int i = nchunk * 8 + threadIdx.x; i < V; i += NT) consume(bf2f(r[i]), i);
+    if (sp == nsp - 1)
+      for (int i = nchunk * 8 + threadIdx.x; i < V; i += NT) consume(bf2f(r[i]), i);
   } else {
     const float* r = (const float*)logits + (int64_t)row * stride;
-    const int nchunk = V / 4;
-    for (int c = threadIdx.x; c < nchunk; c += NT) {
+    const int nchunk = V / 4, per = (nchunk + nsp - 1) / nsp;
+    const int c0 = sp * per, c1 = min(nchunk, c0 + per);
+    for (int c = c0 + threadIdx.x; c < c1; c += NT) {
       const f32x4_t v = *reinterpret_cast<const f32x4_t*>(r + c * 4);
 #pragma unroll
       for (int j = 0; j < 4; ++j) consume(v[j], c * 4 + j);
     }
-    for (int i = nchunk * 4 + threadIdx.x; i < V; i += NT) consume(r[i], i);
+    if (sp == nsp - 1)
+      for (int i = nchunk * 4 + threadIdx.x; i < V; i += NT) consume(r[i], i);
   }
   // wave reduce (max/sumexp and best)
 #pragma unroll
@@ -112,12 +121,44 @@ __global__ __launch_bounds__(NT) void sample_kernel(const void* __restrict__ log
       M = nm;
       B = better(B, Best{sbv[k], sbi[k]});
     }
+    if (nsp > 1) {
+      float* pp = part + ((int64_t)row * nsp + sp) * 4;
+      pp[0] = M;
+      pp[1] = S;
+      pp[2] = B.v;
+      pp[3] = __int_as_float(B.i);
+      return;
+    }
     out_ids[row] = B.i;
     if (out_logprob) {
       const float xc = BF16 ? bf2f(((const uint16_t*)logits)[(int64_t)row * stride + B.i])
                             : ((const float*)logits)[(int64_t)row * stride + B.i];
       out_logprob[row] = xc - M - __logf(S);
     }
+  }
+}
+
+template <bool BF16>
+__global__ __launch_bounds__(64) void sample_merge_kernel(const void* __restrict__ logits, int64_t stride, int nsp,
+                                                          const float* __restrict__ part, int64_t* __restrict__ out_ids,
+                                                          float* __restrict__ out_logprob, int B) {
+  const int row = blockIdx.x * 64 + threadIdx.x;
+  if (row >= B) return;
+  const float* pp = part + (int64_t)row * nsp * 4;
+  float M = NEG_INF, S = 0.f;
+  Best best{NEG_INF, 0x7fffffff};
+  for (int k = 0; k < nsp; ++k) {
+    const float mk = pp[4 * k], sk = pp[4 * k + 1];
+    const float nm = fmaxf(M, mk);
+    S = (M == NEG_INF ? 0.f : S * __expf(M - nm)) + (mk == NEG_INF ? 0.f : sk * __expf(mk - nm));
+    M = nm;
+    best = better(best, Best{pp[4 * k + 2], __float_as_int(pp[4 * k + 3])});
+  }
+  out_ids[row] = best.i;
+  if (out_logprob) {
+    const float xc = BF16 ? bf2f(((const uint16_t*)logits)[(int64_t)row * stride + best.i])
+                          : ((const float*)logits)[(int64_t)row * stride + best.i];
+    out_logprob[row] = xc - M - __logf(S);
   }
 }
 
@@ -212,16 +253,33 @@ __global__ __launch_bounds__(NT) void topk_topp_kernel(float* __restrict__ logit
 
 }  // namespace
 
+// rows split over nsp workgroups each (llmd_sample_splits), part: B * nsp * 4 floats
+extern "C" int llmd_sample_splits(int B, int V) {
+  if (B <= 0) return 1;
+  int nsp = (512 + B - 1) / B;                      // ~2 workgroups per CU in total
+  nsp = max(1, min(nsp, min(16, V / (8 * 2048))));  // keep >= 2k chunks of 8 per workgroup
+  return nsp;
+}
+
 extern "C" void llmd_sample(const void* logits, int64_t stride, int B, int V, int is_bf16,
                             const float* temps, const int64_t* seeds, int64_t* out_ids,
-                            float* out_logprob, hipStream_t st) {
+                            float* out_logprob, float* part, int nsp, hipStream_t st) {
   if (B == 0) return;
+  if (part == nullptr) nsp = 1;
   if (is_bf16)
-    hipLaunchKernelGGL(sample_kernel<true>, dim3(B), dim3(NT), 0, st, logits, stride, V, temps,
-                       seeds, out_ids, out_logprob);
+    hipLaunchKernelGGL(sample_kernel<true>, dim3(B, nsp), dim3(NT), 0, st, logits, stride, V, temps,
+                       seeds, out_ids, out_logprob, part);
   else
-    hipLaunchKernelGGL(sample_kernel<false>, dim3(B), dim3(NT), 0, st, logits, stride, V, temps,
-                       seeds, out_ids, out_logprob);
+    hipLaunchKernelGGL(sample_kernel<false>, dim3(B, nsp), dim3(NT), 0, st, logits, stride, V, temps,
+                       seeds, out_ids, out_logprob, part);
+  if (nsp > 1) {
+    if (is_bf16)
+      hipLaunchKernelGGL(sample_merge_kernel<true>, dim3((B + 63) / 64), dim3(64), 0, st, logits, stride, nsp, part,
+                         out_ids, out_logprob, B);
+    else
+      hipLaunchKernelGGL(sample_merge_kernel<false>, dim3((B + 63) / 64), dim3(64), 0, st, logits, stride, nsp, part,
+                         out_ids, out_logprob, B);
+  }
 }
 
 extern "C" void llmd_topk_topp_mask(float* logits, int64_t stride, int B, int V, const int* topk,

@@ -249,6 +249,20 @@ def test_sample_greedy_and_logprob():
     _close(lp, ref_lp, atol=1e-3, rtol=1e-3)
 
 
+def test_sample_split_rows_match_unsplit():
+    """Small batches split each row over several workgroups: the seeded Gumbel pick and
+    the log-prob equal those of the same rows inside a batch large enough to run unsplit."""
+    torch.manual_seed(9)
+    V = 151936
+    big = torch.randn(600, V, device=DEV).to(torch.bfloat16)
+    temps = torch.full((600,), 0.8, device=DEV)
+    seeds = torch.arange(600, device=DEV, dtype=torch.int64) * 31 + 5
+    ids_big, lp_big = ops.sample(big, temps, seeds, want_logprob=True)
+    ids_small, lp_small = ops.sample(big[:5].contiguous(), temps[:5], seeds[:5], want_logprob=True)
+    assert torch.equal(ids_small, ids_big[:5])
+    _close(lp_small, lp_big[:5], atol=1e-4, rtol=1e-4)
+
+
 def test_sample_temperature_distribution():
     V = 8
     logits = torch.tensor([[0.0, 1.0, 2.0, 0.5, -1.0, 0.0, 3.0, 1.5]], device=DEV).repeat(20000, 1)
