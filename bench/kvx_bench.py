@@ -61,7 +61,7 @@ def consumer(a, path):
         src_ids = torch.randperm(nblocks)[:nb]
         pairs = torch.stack([src_ids, torch.arange(nb)], 1).int().to(dst.device)
         segs = torch.tensor([[0, 0, block]], dtype=torch.int64, device=dst.device)
-        fn = lambda: _C.kvx_copy_blocks(dst, base, block, block, pairs, segs, block)  # noqa: E731
+        fn = lambda: _C.kvx_copy_blocks(dst, base, block, block, pairs, segs, block, a.engine)  # noqa: E731
         fn()
         torch.cuda.synchronize()
         ok = bool((dst[:nb] == src_ids.to(dst.device).int()[:, None]).all())
@@ -82,6 +82,7 @@ def main():
     ap.add_argument("--src-dev", type=int, default=0)
     ap.add_argument("--dst-dev", type=int, default=0)
     ap.add_argument("--block-mb", type=float, default=20.0)
+    ap.add_argument("--engine", type=int, default=1, help="1 = LDS-staged copy kernel, 0 = register-staged")
     ap.add_argument("--pool-gb", type=float, default=8.0)
     ap.add_argument("--role", default=None)
     ap.add_argument("--path", default=None)

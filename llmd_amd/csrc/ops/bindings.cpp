@@ -38,6 +38,8 @@ void llmd_topk_topp_mask(float*, int64_t, int, int, const int*, const float*, co
                          hipStream_t);
 int llmd_kvx_copy_blocks(void*, const void*, int64_t, int64_t, const int*, int, const int64_t*, int,
                          int64_t, hipStream_t);
+int llmd_kvx_copy_blocks2(void*, const void*, int64_t, int64_t, const int*, int, const int64_t*, int, int64_t, int,
+                          hipStream_t);
 int llmd_kvx_ipc_export(const void*, void*, int64_t*);
 int llmd_kvx_ipc_open(const void*, void**);
 int llmd_kvx_ipc_close(void*);
@@ -55,6 +57,7 @@ int llmd_dgemm_supported(int, int, int);
 int llmd_mgemm(const void*, int64_t, const void*, int64_t, int, int, int, int, int, int, void*, int64_t, float*,
                hipStream_t);
 int llmd_mgemm_lds(int, int, int);
+int llmd_pgemm(const void*, int64_t, const void*, int64_t, void*, int64_t, int, int, int, int, int, hipStream_t);
 int llmd_mgemm_fp8(const void*, int64_t, const float*, const void*, int64_t, const float*, int, int, int, int, int,
                    int, void*, int64_t, float*, hipStream_t);
 int llmd_vmm_granularity(int, size_t*);
@@ -433,6 +436,22 @@ void mgemm(torch::Tensor y, torch::Tensor x, torch::Tensor w, int64_t wrb, int64
   TORCH_CHECK(rc == 0, "mgemm failed: ", rc);
 }
 
+// y [M, N] = x [M, K] . w [N, K]^T for prefill-sized M on the 256 x 256 LDS-DMA MFMA
+// GEMM (csrc/ops/pgemm.hip); epi 1 = fused SiLU-and-mul over gate/up columns interleaved
+// per 256-column tile (y is then [M, N / 2])
+void pgemm(torch::Tensor y, torch::Tensor x, torch::Tensor w, int64_t epi, int64_t variant) {
+  const c10::hip::OptionalHIPGuard device_guard(dev_of(y));
+  CHECK_CUDA(x); CHECK_BF16(x); CHECK_BF16(w); CHECK_BF16(y); CHECK_INNER(x); CHECK_INNER(w); CHECK_INNER(y);
+  TORCH_CHECK(x.dim() == 2 && w.dim() == 2 && y.dim() == 2, "pgemm: 2-D operands");
+  const int64_t M = x.size(0), K = x.size(1), N = w.size(0);
+  TORCH_CHECK(w.size(1) == K && K % 64 == 0 && N % 256 == 0, "pgemm: N % 256 == 0, K % 64 == 0");
+  TORCH_CHECK(y.size(0) == M && y.size(1) == (epi == 1 ? N / 2 : N), "pgemm: output shape");
+  TORCH_CHECK(x.stride(0) % 8 == 0 && w.stride(0) % 8 == 0 && y.stride(0) % 8 == 0, "pgemm: 16-B row alignment");
+  int rc = llmd_pgemm(x.data_ptr(), x.stride(0), w.data_ptr(), w.stride(0), y.data_ptr(), y.stride(0), (int)M,
+                      (int)N, (int)K, (int)epi, (int)variant, cur_stream());
+  TORCH_CHECK(rc == 0, "pgemm failed: ", rc);
+}
+
 // fp8 W8A8 form: xq [M, K] e4m3fn with per-token scales xs [M, 1], wq [N, K] e4m3fn with
 // per-channel scales ws [1, N] (ops.fp8_linear's operands); K % 128 == 0
 void mgemm_fp8(torch::Tensor y, torch::Tensor xq, torch::Tensor xs, torch::Tensor wq, torch::Tensor ws, int64_t wrb,
@@ -533,16 +552,16 @@ void topk_topp_mask(torch::Tensor logits, c10::optional<torch::Tensor> topk,
 // ---------------------------------------------------------------- kvx
 // dst/src are base addresses of the two KV pools (src may be an IPC-mapped peer pointer)
 void kvx_copy_blocks(torch::Tensor dst, int64_t src_ptr, int64_t dst_stride, int64_t src_stride,
-                     torch::Tensor pairs, torch::Tensor segs, int64_t max_seg_bytes) {
+                     torch::Tensor pairs, torch::Tensor segs, int64_t max_seg_bytes, int64_t engine) {
   const c10::hip::OptionalHIPGuard device_guard(dev_of(dst));
   CHECK_CUDA(dst); CHECK_CUDA(pairs); CHECK_CUDA(segs);
   CHECK_DT(pairs, at::kInt); CHECK_DT(segs, at::kLong);
   TORCH_CHECK(pairs.is_contiguous() && pairs.dim() == 2 && pairs.size(1) == 2, "pairs [n,2] int32");
   TORCH_CHECK(segs.is_contiguous() && segs.dim() == 2 && segs.size(1) == 3, "segs [m,3] int64");
   TORCH_CHECK(src_ptr != 0, "null source pool");
-  int rc = llmd_kvx_copy_blocks(dst.data_ptr(), (const void*)src_ptr, dst_stride, src_stride,
-                                pairs.data_ptr<int>(), pairs.size(0), segs.data_ptr<int64_t>(),
-                                segs.size(0), max_seg_bytes, cur_stream());
+  int rc = llmd_kvx_copy_blocks2(dst.data_ptr(), (const void*)src_ptr, dst_stride, src_stride,
+                                 pairs.data_ptr<int>(), pairs.size(0), segs.data_ptr<int64_t>(),
+                                 segs.size(0), max_seg_bytes, (int)engine, cur_stream());
   TORCH_CHECK(rc == 0, "kvx_copy_blocks failed: ", rc);
 }
 
@@ -914,6 +933,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {  // _C, or _C_debug (llmd_amd/build.p
   m.def("skinny_gemm", &skinny_gemm);
   m.def("skinny_supported", &skinny_supported);
   m.def("mgemm", &mgemm);
+  m.def("pgemm", &pgemm, "prefill bf16 GEMM (256x256 LDS-DMA MFMA tiles), optional fused SiLU-and-mul");
   m.def("mgemm_fp8", &mgemm_fp8);
   m.def("mgemm_lds", [](int64_t M, int64_t wrb, int64_t stages) { return llmd_mgemm_lds((int)M, (int)wrb, (int)stages); });
   m.def("lora_bgmv", &lora_bgmv);

@@ -48,9 +48,67 @@ __global__ __launch_bounds__(NT) void copy_blocks_kernel(char* __restrict__ dst,
   for (; v < v1; v += NT) __builtin_nontemporal_store(s[v], d + v);
 }
 
+constexpr int CP_NT = 256, CP_CHUNK = 65536;  // 4 waves x 16 KB
+
+__device__ __forceinline__ void cp_dma16(const void* src, char* lds) {
+  __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)src,
+                                   (void __attribute__((address_space(3)))*)lds, 16, 0, 0);
+}
+
+__global__ __launch_bounds__(CP_NT) void copy_blocks_lds_kernel(char* __restrict__ dst, const char* __restrict__ src,
+                                                                int64_t dst_stride, int64_t src_stride,
+                                                                const int* __restrict__ pairs,
+                                                                const int64_t* __restrict__ segs) {
+  __shared__ __attribute__((aligned(1024))) char lds[CP_CHUNK];
+  const int pi = blockIdx.y, sj = blockIdx.z;
+  const int64_t sb = pairs[2 * pi], db = pairs[2 * pi + 1];
+  const int64_t so = segs[3 * sj], dof = segs[3 * sj + 1], len = segs[3 * sj + 2];
+  const int64_t c0 = (int64_t)blockIdx.x * CP_CHUNK;
+  if (c0 >= len) return;
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int64_t wb = c0 + w * 16384;  // this wave's 16 KB: 16 pieces of 64 lanes x 16 B
+  const char* s = src + sb * src_stride + so;
+  char* d = dst + db * dst_stride + dof;
+  char* lw = lds + w * 16384;         // lane-linear image: piece i at lw + i * 1024
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const int64_t off = wb + i * 1024 + lane * 16;
+    if (off < len) cp_dma16(s + off, lw + i * 1024);
+  }
+  // a wave reads back only what its own DMAs wrote: its vmcnt alone orders the reads
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const int64_t off = wb + i * 1024 + lane * 16;
+    if (off < len) {
+      const u32x4_t v = *reinterpret_cast<const u32x4_t*>(lw + i * 1024 + lane * 16);
+      __builtin_nontemporal_store(v, reinterpret_cast<u32x4_t*>(d + off));
+    }
+  }
+}
+
 }  // namespace
 
 extern "C" {
+
+int llmd_kvx_copy_blocks(void* dst, const void* src, int64_t dst_stride, int64_t src_stride, const int* pairs_dev,
+                         int npairs, const int64_t* segs_dev, int nseg, int64_t max_seg_bytes, hipStream_t st);
+
+// engine: 0 = register-staged, 1 = LDS-staged (default)
+int llmd_kvx_copy_blocks2(void* dst, const void* src, int64_t dst_stride, int64_t src_stride, const int* pairs_dev,
+                          int npairs, const int64_t* segs_dev, int nseg, int64_t max_seg_bytes, int engine,
+                          hipStream_t st) {
+  if (npairs == 0 || nseg == 0) return 0;
+  if (engine == 0)
+    return llmd_kvx_copy_blocks(dst, src, dst_stride, src_stride, pairs_dev, npairs, segs_dev, nseg, max_seg_bytes,
+                                st);
+  const int64_t nchunk = (max_seg_bytes + CP_CHUNK - 1) / CP_CHUNK;
+  if (nchunk > 65535 || npairs > 65535 || nseg > 65535) return -2;
+  dim3 grid((unsigned)nchunk, (unsigned)npairs, (unsigned)nseg);
+  hipLaunchKernelGGL(copy_blocks_lds_kernel, grid, dim3(CP_NT), 0, st, (char*)dst, (const char*)src, dst_stride,
+                     src_stride, pairs_dev, segs_dev);
+  return (int)hipGetLastError();
+}
 
 int llmd_kvx_copy_blocks(void* dst, const void* src, int64_t dst_stride, int64_t src_stride,
                          const int* pairs_dev, int npairs, const int64_t* segs_dev, int nseg,

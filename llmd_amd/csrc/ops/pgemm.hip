@@ -1,0 +1,533 @@
+// Prefill ("large-M") dense bf16 GEMM: C[M, N] = A[M, K] . W[N, K]^T, the
+// QKV / O / gate-up / down projections of a prefill chunk (the
+// hipBLASLt Cijk_* kernels that take ~68 % of the 70B serving bench).
+//
+// CDNA4 design (one 256 x 256 output tile per 512-thread workgroup, 1 per CU):
+//   * 8 waves as 2 (M) x 4 (N); a wave owns 128 x 64 of C, as four 64 x 32
+//     quadrants of 4 x 2 mfma_f32_16x16x32_bf16 tiles (128 accumulator regs);
+//   * K-steps of 64 through TWO LDS buffers of 64 KB (A 256 x 128 B, W 256 x
+//     128 B), each split into four 16 KB "halves" by the quadrant that reads
+//     them (A: rows of quadrant-row 0 / 1, W: columns of quadrant-col 0 / 1).
+//     A half is refilled by LDS-DMA (global_load_lds_dwordx4, no VGPR
+//     staging) one phase after its last fragment read, so each K-step's loads
+//     are in flight for ~6 phases, across the raw s_barriers, retired by
+//     COUNTED vmcnt waits (never 0 inside the loop);
+//   * 4 phases per K-step, one quadrant each (16 MFMA), fragment reads
+//     front-loaded (12 / 4 / 8 / 0 ds_read_b128): both W halves stay in
+//     registers for the whole K-step;
+//   * waves 4-7 run one barrier behind waves 0-3 (stagger): on every SIMD one
+//     wave's fragment reads + DMA issue overlap its partner's MFMA segment;
+//   * 16-B chunks XOR-swizzled by (row & 7) on the DMA source address and on
+//     the read (every ds_read_b128 lane group covers 16 distinct bank slots);
+//   * XCD-aware tile order (each XCD walks its own contiguous range of tiles,
+//     grouped 8 row-tiles deep so concurrently running tiles share A and W
+//     panels in that XCD's L2);
+//   * epilogue through the (then free) LDS: C is computed transposed (W frags
+//     as the MFMA's first operand) so each lane holds 4 consecutive columns,
+//     written as 8-B LDS stores, read back as 16-B rows and stored coalesced.
+//     EPI_SILU: gate/up columns interleaved per 256-column tile (128 gate then
+//     128 up, ops.pgemm_pack_gate_up) -> silu(g) * u is stored directly as the
+//     [M, N/2] activation (no separate act kernel, no [M, N] round trip).
+//
+// Requirements (checked by the host wrapper): N % 256 == 0, K % 64 == 0,
+// 16-B aligned rows; any M (rows past M are clamped on load, not stored).
+#include <type_traits>
+
+#include "llmd_common.h"
+
+using namespace llmd;
+
+namespace {
+
+constexpr int BM = 256, BN = 256, BK = 64, NT = 512;
+constexpr int HALF = 16384;         // bytes of one half (128 rows x 128 B)
+constexpr int BUF = 4 * HALF;       // one K-step: A q0, A q1, W q0, W q1
+constexpr int LDS_BYTES = 2 * BUF;  // 128 KB
+constexpr int GROUP_M = 8;
+
+enum { EPI_NONE = 0, EPI_SILU = 1 };
+
+__device__ __forceinline__ void dma16(const void* src, char* lds) {
+  __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)src,
+                                   (void __attribute__((address_space(3)))*)lds, 16, 0, 0);
+}
+
+// wait until at most n (wave-uniform, 0..10) VMEM ops of this wave are outstanding
+__device__ __forceinline__ void wait_vm(int n) {
+  switch (n) {
+    case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+    case 2: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
+    case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
+    case 6: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
+    case 8: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
+    default: asm volatile("s_waitcnt vmcnt(10)" ::: "memory"); break;
+  }
+}
+
+__device__ __forceinline__ void bar() {
+  __builtin_amdgcn_sched_barrier(0);
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+template <int EPI>
+__global__ __launch_bounds__(NT, 1) void pgemm_kernel(const uint16_t* __restrict__ A, int64_t lda,
+                                                      const uint16_t* __restrict__ W, int64_t ldw,
+                                                      uint16_t* __restrict__ C, int64_t ldc, int M, int N, int K) {
+  __shared__ __attribute__((aligned(1024))) char lds[LDS_BYTES];  // the ONLY LDS object (see moe.hip G3)
+  const int tiles_m = (M + BM - 1) / BM, tiles_n = N / BN;
+  const int ntiles = tiles_m * tiles_n;
+  // XCD-contiguous logical tile id, then GROUP_M-deep grouped order
+  const int L = xcd_remap(blockIdx.x, ntiles);
+  const int per_group = GROUP_M * tiles_n;
+  const int g = L / per_group, first_m = g * GROUP_M;
+  const int gm = min(tiles_m - first_m, GROUP_M);
+  const int tm = first_m + (L % per_group) % gm, tn = (L % per_group) / gm;
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int nk = K / BK;
+
+  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+  const int wr = w >> 2, wc = w & 3;
+
+  // ---- DMA sources: half row i = 8 * (2w + j) + (lane >> 3), LDS chunk slot lane & 7
+  // holds source chunk (lane & 7) ^ (i & 7); 32-bit element offsets from A / W
+  uint32_t aoff[2][2], woff[2][2];  // [half][j]
+#pragma unroll
+  for (int h = 0; h < 2; ++h)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int i = 8 * (2 * w + j) + (lane >> 3);
+      const int c = (lane & 7) ^ (i & 7);
+      const int ar = min(m0 + (i >> 6) * 128 + h * 64 + (i & 63), M - 1);
+      const int wn = n0 + (i >> 5) * 64 + h * 32 + (i & 31);
+      aoff[h][j] = (uint32_t)(ar * lda + c * 8);
+      woff[h][j] = (uint32_t)(wn * ldw + c * 8);
+    }
+  // half kinds in issue order: 0 = A q0, 1 = W q0, 2 = W q1, 3 = A q1; seq = 4 * ktile + kind
+  auto issue = [&](int seq) {
+    const int kt = seq >> 2, kind = seq & 3;
+    char* dst = lds + (kt & 1) * BUF + (2 * w) * 1024;
+    const int k0 = kt * BK;
+    if (kind == 0 || kind == 3) {
+      const int h = kind == 0 ? 0 : 1;
+      dst += h * HALF;
+      dma16(A + aoff[h][0] + k0, dst);
+      dma16(A + aoff[h][1] + k0, dst + 1024);
+    } else {
+      const int h = kind - 1;
+      dst += 2 * HALF + h * HALF;
+      dma16(W + woff[h][0] + k0, dst);
+      dma16(W + woff[h][1] + k0, dst + 1024);
+    }
+  };
+  const int nseq = 4 * nk;
+  int issued = 0;  // halves issued so far (wave-uniform)
+  auto issue_upto = [&](int seq) {
+    if (seq < nseq) {
+      issue(seq);
+      issued = seq + 1;
+    }
+  };
+  // wait until half `seq` landed: 2 DMAs per younger half may stay in flight
+  auto wait_seq = [&](int seq) { wait_vm(min(5, max(0, issued - seq - 1)) * 2); };
+
+  // ---- fragment read offsets (bytes inside a half): lane row l & 15, chunk 4s + (l >> 4)
+  const int fr = lane & 15, fq = lane >> 4;
+  int a_rd[4][2], w_rd[2][2];  // [mi][s], [ni][s]
+#pragma unroll
+  for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const int i = wr * 64 + mi * 16 + fr;
+      a_rd[mi][s] = i * 128 + (((4 * s + fq) ^ (i & 7)) * 16);
+    }
+#pragma unroll
+  for (int ni = 0; ni < 2; ++ni)
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const int i = wc * 32 + ni * 16 + fr;
+      w_rd[ni][s] = i * 128 + (((4 * s + fq) ^ (i & 7)) * 16);
+    }
+
+  f32x4_t acc[2][2][4][2];  // [qm][qn][mi][ni]: C^T tiles (row = n, col = m)
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int c = 0; c < 4; ++c)
+#pragma unroll
+        for (int d = 0; d < 2; ++d) acc[a][b][c][d] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  s16x8_t afr[4][2], wfr[2][2][2];  // [mi][s], [qn][ni][s]
+  auto read_a = [&](const char* hb) {
+#pragma unroll
+    for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+      for (int s = 0; s < 2; ++s) afr[mi][s] = *reinterpret_cast<const s16x8_t*>(hb + a_rd[mi][s]);
+  };
+  auto read_w = [&](const char* hb, int qn) {
+#pragma unroll
+    for (int ni = 0; ni < 2; ++ni)
+#pragma unroll
+      for (int s = 0; s < 2; ++s) wfr[qn][ni][s] = *reinterpret_cast<const s16x8_t*>(hb + w_rd[ni][s]);
+  };
+  auto mfma_q = [&](int qm, int qn) {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < 2; ++ni)
+          acc[qm][qn][mi][ni] =
+              __builtin_amdgcn_mfma_f32_16x16x32_bf16(wfr[qn][ni][s], afr[mi][s], acc[qm][qn][mi][ni], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+  };
+  // one phase: [reads + DMA issue + counted wait] -> lgkmcnt(0) -> barrier -> MFMA -> barrier
+  auto seg_end = [&]() {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    bar();
+  };
+
+  // ---- prologue: K-step 0 whole, K-step 1 but its A q1 half
+#pragma unroll
+  for (int s = 0; s < 7; ++s) issue_upto(s);
+  wait_seq(1);
+  bar();
+  if (__builtin_amdgcn_readfirstlane(wr) == 1) bar();  // stagger: waves 4-7 one segment behind
+
+  // one K-step: 4 phases of [fragment reads + DMA issue + counted wait] -> lgkmcnt(0) ->
+  // barrier -> 16 MFMA -> barrier. STEADY (kt + 2 < nk): every refill exists and exactly
+  // 5 younger halves (10 DMAs) stay in flight at each wait.
+  auto ktile = [&](int kt, auto steady_t) {
+    constexpr bool STEADY = decltype(steady_t)::value;
+    const char* bufp = lds + (kt & 1) * BUF;
+    // phase 1: A q0 + W q0 fragments; refill A q1 of K-step kt+1; W q1 (kt) lands for phase 2
+    read_a(bufp);
+    read_w(bufp + 2 * HALF, 0);
+    if constexpr (STEADY) {
+      issue(4 * (kt + 1) + 3);
+      wait_vm(10);
+    } else {
+      issue_upto(4 * (kt + 1) + 3);
+      wait_seq(4 * kt + 2);
+    }
+    seg_end();
+    mfma_q(0, 0);
+    bar();
+    // phase 2: W q1 fragments; refill A q0 of kt+2 (its kt copy was read in phase 1)
+    read_w(bufp + 3 * HALF, 1);
+    if constexpr (STEADY) {
+      issue(4 * (kt + 2) + 0);
+      wait_vm(10);
+    } else {
+      issue_upto(4 * (kt + 2) + 0);
+      wait_seq(4 * kt + 3);
+    }
+    seg_end();
+    mfma_q(0, 1);
+    bar();
+    // phase 3: A q1 fragments; refill W q0 of kt+2
+    read_a(bufp + HALF);
+    if constexpr (STEADY) issue(4 * (kt + 2) + 1);
+    else issue_upto(4 * (kt + 2) + 1);
+    seg_end();
+    mfma_q(1, 1);
+    bar();
+    // phase 4: no reads; refill W q1 of kt+2; A q0 + W q0 of kt+1 land for its phase 1
+    if constexpr (STEADY) {
+      issue(4 * (kt + 2) + 2);
+      issued = 4 * (kt + 2) + 3;
+      wait_vm(10);
+    } else {
+      issue_upto(4 * (kt + 2) + 2);
+      if (kt + 1 < nk) wait_seq(4 * (kt + 1) + 1);
+    }
+    seg_end();
+    mfma_q(1, 0);
+    bar();
+  };
+  int kt = 0;
+  for (; kt + 2 < nk; ++kt) ktile(kt, std::true_type{});
+  for (; kt < nk; ++kt) ktile(kt, std::false_type{});
+  if (__builtin_amdgcn_readfirstlane(wr) == 0) bar();  // balance the stagger
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+
+  // ---- epilogue: acc[qm][qn][mi][ni][r] = C[m][n] with
+  //   m = wr*128 + qm*64 + mi*16 + (lane & 15), n = wc*64 + qn*32 + ni*16 + (lane >> 4)*4 + r
+  // wave image in LDS: [128 rows (m)][64 cols (n)] bf16, 16-B chunks XOR-swizzled by row & 7
+  char* img = lds + w * 16384;
+#pragma unroll
+  for (int qm = 0; qm < 2; ++qm)
+#pragma unroll
+    for (int qn = 0; qn < 2; ++qn)
+#pragma unroll
+      for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < 2; ++ni) {
+          const int row = qm * 64 + mi * 16 + fr;
+          const int col = qn * 32 + ni * 16 + fq * 4;  // 4 consecutive bf16 = 8 B
+          const f32x4_t v = acc[qm][qn][mi][ni];
+          u32x2_t p;
+          p[0] = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
+          p[1] = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
+          const int chunk = (col >> 3) ^ (row & 7);
+          *reinterpret_cast<u32x2_t*>(img + row * 128 + chunk * 16 + (col & 7) * 2) = p;
+        }
+  __syncthreads();
+  if constexpr (EPI == EPI_NONE) {
+    // each wave stores its own 128 x 64 block: 8 rows x 128 B per instruction
+#pragma unroll 4
+    for (int it = 0; it < 16; ++it) {
+      const int row = it * 8 + (lane >> 3), c = lane & 7;
+      const int m = m0 + wr * 128 + row;
+      const u32x4_t v = *reinterpret_cast<const u32x4_t*>(img + row * 128 + ((c ^ (row & 7)) * 16));
+      if (m < M) *reinterpret_cast<u32x4_t*>(C + (int64_t)m * ldc + n0 + wc * 64 + c * 8) = v;
+    }
+  } else {
+    // EPI_SILU: tile columns [0,128) gate, [128,256) up -> 128 output columns at n0 / 2.
+    // Waves wc = 0,1 hold gate cols [0,128), wc = 2,3 the matching up cols; the
+    // wc < 2 waves combine their image with the partner wave's (wc + 2) image.
+    if (wc < 2) {
+      const char* up = lds + (w + 2) * 16384;
+#pragma unroll 4
+      for (int it = 0; it < 16; ++it) {
+        const int row = it * 8 + (lane >> 3), c = lane & 7;
+        const int m = m0 + wr * 128 + row;
+        const int off = row * 128 + ((c ^ (row & 7)) * 16);
+        float gf[8], uf[8], of[8];
+        unpack8(*reinterpret_cast<const u32x4_t*>(img + off), gf);
+        unpack8(*reinterpret_cast<const u32x4_t*>(up + off), uf);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) of[e] = gf[e] / (1.f + __expf(-gf[e])) * uf[e];
+        if (m < M) *reinterpret_cast<u32x4_t*>(C + (int64_t)m * ldc + n0 / 2 + wc * 64 + c * 8) = pack8(of);
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Variant 4W: 4 waves (one per SIMD), each 128 x 128 of C (8 x 8 tiles of
+// mfma_f32_16x16x32_bf16: 256 accumulator registers, AGPR-resident), the form
+// hipBLASLt's fastest MT256x256x64 kernels take. With one wave per SIMD the
+// wave itself must keep its matrix pipe fed, so fragment reads are software-
+// pipelined one k-substep (32) ahead in a second register set, interleaved
+// 1 ds_read : 4 MFMA, and there are only two barriers per 64-deep K-step.
+// LDS: 4 slots of 32 KB, slot (kt & 1) * 2 + h holds k-half h (32 wide) of
+// K-step kt for A and W ([256 rows][64 B], 16-B chunks swizzled by
+// F[(row >> 2) & 3], conflict-free for the 16x16x32 operand reads). A slot is
+// refilled right after the barrier that follows its last fragment read, so
+// every half has three substeps (~3000 cycles) to land; counted vmcnt(16).
+constexpr int NT4 = 256;
+constexpr int SLOT4 = 32768;  // one k-half of A (16 KB) + of W (16 KB)
+
+__device__ __forceinline__ int swz4(int row, int c) {
+  // F = {0, 2, 3, 1}: every ds_read_b128 lane group of a 16 x 4-chunk read hits 16 distinct slots
+  return c ^ ((0x1E >> (2 * ((row >> 2) & 3))) & 3);
+}
+
+template <int EPI>
+__global__ __launch_bounds__(NT4, 1) void pgemm4_kernel(const uint16_t* __restrict__ A, int64_t lda,
+                                                        const uint16_t* __restrict__ W, int64_t ldw,
+                                                        uint16_t* __restrict__ C, int64_t ldc, int M, int N, int K) {
+  __shared__ __attribute__((aligned(1024))) char lds[4 * SLOT4];  // the ONLY LDS object
+  const int tiles_m = (M + BM - 1) / BM, tiles_n = N / BN;
+  const int ntiles = tiles_m * tiles_n;
+  const int L = xcd_remap(blockIdx.x, ntiles);
+  const int per_group = GROUP_M * tiles_n;
+  const int g = L / per_group, first_m = g * GROUP_M;
+  const int gm = min(tiles_m - first_m, GROUP_M);
+  const int tm = first_m + (L % per_group) % gm, tn = (L % per_group) / gm;
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int nk = K / BK;
+
+  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+  const int wr = w >> 1, wc = w & 1;
+
+  // DMA: a k-half of A is 256 rows x 64 B = 16 pieces of 1 KB (16 rows each); wave w moves
+  // pieces 4w..4w+3 of A and of W. Lane: row 16 * piece + (lane >> 2), slot lane & 3.
+  uint32_t aoff[4], woff[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int row = 16 * (4 * w + j) + (lane >> 2);
+    const int c = swz4(row, lane & 3);
+    aoff[j] = (uint32_t)(min(m0 + row, M - 1) * lda + c * 8);
+    woff[j] = (uint32_t)((n0 + row) * ldw + c * 8);
+  }
+  // half index q = 2 * kt + h, slot (kt & 1) * 2 + h = q & 3
+  auto issue = [&](int q) {
+    char* dst = lds + (q & 3) * SLOT4 + (4 * w) * 1024;
+    const int k0 = (q >> 1) * BK + (q & 1) * 32;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) dma16(A + aoff[j] + k0, dst + j * 1024);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) dma16(W + woff[j] + k0, dst + 16384 + j * 1024);
+  };
+  const int nq = 2 * nk;
+
+  // fragment reads: tile row r = 16 * t + (lane & 15), chunk lane >> 4; (r >> 2) & 3 does not depend on t
+  const int fr = lane & 15, fq = lane >> 4;
+  const int rd = fr * 64 + swz4(fr, fq) * 16;
+  const int a_rd = (wr * 128) * 64 + rd, w_rd = 16384 + (wc * 128) * 64 + rd;
+
+  f32x4_t acc[8][8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  s16x8_t fa0[8], fw0[8], fa1[8], fw1[8];
+
+  // MFMAs of one substep on (fa, fw) with the next substep's 16 fragment reads from
+  // `nxt` interleaved (1 read per 4 MFMA) into (na, nw)
+#define PG4_SUBSTEP(fa, fw, na, nw, nxt, do_read)                                                          \
+  {                                                                                                        \
+    const char* nb_ = (nxt);                                                                               \
+    _Pragma("unroll") for (int i = 0; i < 8; ++i) {                                                        \
+      if (do_read) {                                                                                       \
+        na[i] = *reinterpret_cast<const s16x8_t*>(nb_ + a_rd + i * 1024);                                  \
+        nw[i] = *reinterpret_cast<const s16x8_t*>(nb_ + w_rd + i * 1024);                                  \
+      }                                                                                                    \
+      _Pragma("unroll") for (int j = 0; j < 8; ++j) acc[i][j] =                                            \
+          __builtin_amdgcn_mfma_f32_16x16x32_bf16(fw[j], fa[i], acc[i][j], 0, 0, 0);                        \
+      if (do_read) {                                                                                       \
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);                                                 \
+        __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);                                                 \
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);                                                 \
+        __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);                                                 \
+      }                                                                                                    \
+    }                                                                                                      \
+  }
+  // boundary: reads retired, the half read next has landed (every wave), then refill the slot whose
+  // fragments are now all in registers
+  auto boundary = [&](int wait_q, int issued_hi, int refill_q) {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    const int younger = min(2, max(0, issued_hi - wait_q - 1));
+    if (younger >= 2) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+    else if (younger == 1) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    bar();
+    if (refill_q < nq) issue(refill_q);
+  };
+
+  // prologue: halves 0..3 (K-steps 0, 1); read K-step 0 half 0 fragments
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+    if (q < nq) issue(q);
+  {
+    const int hi = min(4, nq);
+    const int younger = hi - 1;  // wait for half 0
+    if (younger >= 3) asm volatile("s_waitcnt vmcnt(24)" ::: "memory");
+    else if (younger == 1) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    bar();
+  }
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    fa0[i] = *reinterpret_cast<const s16x8_t*>(lds + a_rd + i * 1024);
+    fw0[i] = *reinterpret_cast<const s16x8_t*>(lds + w_rd + i * 1024);
+  }
+  // before half 1 of K-step 0 is read (during substep (0, 0)) it must have landed
+  {
+    const int hi = min(4, nq);
+    const int younger = hi - 2;
+    if (younger >= 2) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    bar();
+  }
+  int issued = min(4, nq);
+  // K-steps 0 .. nk-2: both substeps read ahead
+  for (int kt = 0; kt + 1 < nk; ++kt) {
+    const int q0 = 2 * kt;
+    // substep (kt, 0): compute half q0 (fa0/fw0), read half q0 + 1
+    PG4_SUBSTEP(fa0, fw0, fa1, fw1, lds + ((q0 + 1) & 3) * SLOT4, true);
+    // its slot is fully read -> refill with q0 + 1 + 4 = half 1 of K-step kt + 2; next read: half q0 + 2
+    boundary(q0 + 2, issued, q0 + 5);
+    if (q0 + 5 < nq) issued = q0 + 6;
+    // substep (kt, 1): compute half q0 + 1, read half q0 + 2 (K-step kt + 1, half 0)
+    PG4_SUBSTEP(fa1, fw1, fa0, fw0, lds + ((q0 + 2) & 3) * SLOT4, true);
+    // refill the slot of half q0 + 2 with q0 + 6; the next substep reads half q0 + 3
+    boundary(q0 + 3, issued, q0 + 6);
+    if (q0 + 6 < nq) issued = q0 + 7;
+  }
+  {  // last K-step: its second substep reads nothing
+    const int q0 = 2 * (nk - 1);
+    PG4_SUBSTEP(fa0, fw0, fa1, fw1, lds + ((q0 + 1) & 3) * SLOT4, true);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    PG4_SUBSTEP(fa1, fw1, fa0, fw0, lds, false);
+  }
+#undef PG4_SUBSTEP
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+
+  // epilogue: acc[i][j][r] = C[m][n], m = wr*128 + 16 i + (lane & 15), n = wc*128 + 16 j + 4 (lane >> 4) + r.
+  // wave image: [128 rows][128 cols] bf16 (256-B rows), 16-B chunks XOR-swizzled by row & 15
+  char* img = lds + w * 32768;
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int row = 16 * i + fr, col = 16 * j + 4 * fq;
+      const f32x4_t v = acc[i][j];
+      u32x2_t p;
+      p[0] = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
+      p[1] = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
+      *reinterpret_cast<u32x2_t*>(img + row * 256 + (((col >> 3) ^ (row & 15)) * 16) + (col & 7) * 2) = p;
+    }
+  __syncthreads();
+  if constexpr (EPI == EPI_NONE) {
+#pragma unroll 4
+    for (int it = 0; it < 32; ++it) {
+      const int row = it * 4 + (lane >> 4), c = lane & 15;
+      const int m = m0 + wr * 128 + row;
+      const u32x4_t v = *reinterpret_cast<const u32x4_t*>(img + row * 256 + ((c ^ (row & 15)) * 16));
+      if (m < M) *reinterpret_cast<u32x4_t*>(C + (int64_t)m * ldc + n0 + wc * 128 + c * 8) = v;
+    }
+  } else {
+    // gate = tile columns [0, 128) (waves wc = 0), up = [128, 256) (wc = 1): wave (wr, 0) combines
+    if (wc == 0) {
+      const char* up = lds + (w + 1) * 32768;
+#pragma unroll 4
+      for (int it = 0; it < 32; ++it) {
+        const int row = it * 4 + (lane >> 4), c = lane & 15;
+        const int m = m0 + wr * 128 + row;
+        const int off = row * 256 + ((c ^ (row & 15)) * 16);
+        float gf[8], uf[8], of[8];
+        unpack8(*reinterpret_cast<const u32x4_t*>(img + off), gf);
+        unpack8(*reinterpret_cast<const u32x4_t*>(up + off), uf);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) of[e] = gf[e] / (1.f + __expf(-gf[e])) * uf[e];
+        if (m < M) *reinterpret_cast<u32x4_t*>(C + (int64_t)m * ldc + n0 / 2 + c * 8) = pack8(of);
+      }
+    }
+  }
+}
+
+}  // namespace
+
+// variant 0: 8-wave staggered 4-phase kernel; 1: 4-wave 128 x 128-per-wave kernel
+extern "C" int llmd_pgemm(const void* A, int64_t lda, const void* W, int64_t ldw, void* C, int64_t ldc, int M, int N,
+                          int K, int epi, int variant, hipStream_t st) {
+  if (M <= 0) return 0;
+  if (N % BN || K % BK || lda % 8 || ldw % 8 || ldc % 8) return -1;
+  // 32-bit DMA offsets
+  if ((int64_t)(M - 1) * lda + K > 0x7fffffffLL || (int64_t)(N - 1) * ldw + K > 0x7fffffffLL) return -2;
+  const int ntiles = ((M + BM - 1) / BM) * (N / BN);
+  if (variant == 1) {
+    if (epi == EPI_SILU)
+      hipLaunchKernelGGL(pgemm4_kernel<EPI_SILU>, dim3(ntiles), dim3(NT4), 0, st, (const uint16_t*)A, lda,
+                         (const uint16_t*)W, ldw, (uint16_t*)C, ldc, M, N, K);
+    else
+      hipLaunchKernelGGL(pgemm4_kernel<EPI_NONE>, dim3(ntiles), dim3(NT4), 0, st, (const uint16_t*)A, lda,
+                         (const uint16_t*)W, ldw, (uint16_t*)C, ldc, M, N, K);
+    return (int)hipGetLastError();
+  }
+  if (epi == EPI_SILU)
+    hipLaunchKernelGGL(pgemm_kernel<EPI_SILU>, dim3(ntiles), dim3(NT), 0, st, (const uint16_t*)A, lda,
+                       (const uint16_t*)W, ldw, (uint16_t*)C, ldc, M, N, K);
+  else
+    hipLaunchKernelGGL(pgemm_kernel<EPI_NONE>, dim3(ntiles), dim3(NT), 0, st, (const uint16_t*)A, lda,
+                       (const uint16_t*)W, ldw, (uint16_t*)C, ldc, M, N, K);
+  return (int)hipGetLastError();
+}

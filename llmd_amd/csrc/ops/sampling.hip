@@ -55,10 +55,12 @@ __global__ __launch_bounds__(NT) void sample_kernel(const void* __restrict__ log
   float mx = NEG_INF, se = 0.f;
   Best best{NEG_INF, 0x7fffffff};
   auto consume = [&](float x, int i) {
+    // masked entries (-inf from top-k / top-p / min_p) add nothing; without the
+    // guard a thread whose first entries are masked computes exp(-inf - -inf) = NaN
     if (x > mx) {
       se = se * __expf(mx - x) + 1.f;
       mx = x;
-    } else {
+    } else if (x != NEG_INF) {
       se += __expf(x - mx);
     }
     float key = x;

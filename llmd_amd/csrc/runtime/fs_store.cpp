@@ -1,13 +1,25 @@
 // Filesystem KV tier (the llmd-fs-connector role). One file per
 // KV block under <root>/<key[0:2]>/<key>.kv, written by a native thread pool
 // (write to a temp file + fsync-less atomic rename, so readers never see a
-// torn block; "the directory is the index"). Reads are synchronous into a
-// caller-provided (pinned) buffer; blocks still queued for writing are served
-// from the queue. Survives engine restarts.
+// torn block; "the directory is the index"). Survives engine restarts.
+//
+// Asynchronous I/O on two pools (the reference offloader's n_read_threads /
+// n_write_threads, docs/architecture/advanced/kv-management/kv-offloader.md):
+//   * write_async(name, ptr, bytes, ticket): the worker writes straight from the
+//     caller's (pinned host-tier) buffer, no copy on the engine thread; the
+//     caller keeps the buffer unchanged until poll_writes() returns the ticket;
+//   * read_async(name, ptr, bytes, ticket): a read worker fills the caller's
+//     pinned buffer; poll_reads() returns (ticket, ok). Blocks still queued for
+//     writing are served from the writer's source buffer.
+// write()/read() are the synchronous forms. Per-direction byte and time
+// counters feed vllm:kv_offload_* metrics.
 #include <pybind11/numpy.h>
 #include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
 
 #include <atomic>
+#include <chrono>
+#include <functional>
 #include <condition_variable>
 #include <cstdio>
 #include <cstring>
@@ -29,9 +41,10 @@ namespace {
 
 class FsStore {
  public:
-  FsStore(const std::string& root, int threads) : root_(root) {
+  FsStore(const std::string& root, int threads, int read_threads) : root_(root) {
     ::mkdir(root_.c_str(), 0755);
-    for (int i = 0; i < std::max(1, threads); ++i) workers_.emplace_back([this] { run(); });
+    for (int i = 0; i < std::max(1, threads); ++i) workers_.emplace_back([this] { run_writes(); });
+    for (int i = 0; i < std::max(1, read_threads); ++i) workers_.emplace_back([this] { run_reads(); });
   }
   ~FsStore() {
     {
@@ -39,17 +52,26 @@ class FsStore {
       stop_ = true;
     }
     cv_.notify_all();
+    rcv_.notify_all();
     for (auto& t : workers_) t.join();
   }
 
+  // synchronous-source write: the bytes are copied now (small / test use)
   void write(const std::string& name, py::array_t<uint8_t, py::array::c_style> data) {
-    auto buf = std::make_shared<std::vector<uint8_t>>(data.data(), data.data() + data.size());
-    {
-      std::lock_guard<std::mutex> g(mu_);
-      pending_[name] = buf;
-      q_.push_back(name);
-    }
-    cv_.notify_one();
+    auto own = std::make_shared<std::vector<uint8_t>>(data.data(), data.data() + data.size());
+    enqueue_write(name, Job{own->data(), own->size(), -1, own});
+  }
+
+  // zero-copy write from a caller-owned buffer that stays valid until `ticket` is polled
+  void write_async(const std::string& name, uintptr_t ptr, int64_t bytes, int64_t ticket) {
+    enqueue_write(name, Job{reinterpret_cast<const uint8_t*>(ptr), (size_t)bytes, ticket, nullptr});
+  }
+
+  std::vector<int64_t> poll_writes() {
+    std::lock_guard<std::mutex> g(mu_);
+    std::vector<int64_t> out;
+    out.swap(wdone_);
+    return out;
   }
 
   bool exists(const std::string& name) {
@@ -62,67 +84,150 @@ class FsStore {
   }
 
   bool read(const std::string& name, py::array_t<uint8_t, py::array::c_style> out) {
+    uint8_t* dst = out.mutable_data();
+    const size_t n = (size_t)out.size();
+    py::gil_scoped_release nogil;
+    return read_into(name, dst, n);
+  }
+
+  void read_async(const std::string& name, uintptr_t ptr, int64_t bytes, int64_t ticket) {
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      rq_.push_back(RJob{name, reinterpret_cast<uint8_t*>(ptr), (size_t)bytes, ticket});
+    }
+    rcv_.notify_one();
+  }
+
+  std::vector<std::pair<int64_t, bool>> poll_reads() {
+    std::lock_guard<std::mutex> g(mu_);
+    std::vector<std::pair<int64_t, bool>> out;
+    out.swap(rdone_);
+    return out;
+  }
+
+  void flush() {
+    std::unique_lock<std::mutex> g(mu_);
+    done_cv_.wait(g, [this] { return q_.empty() && in_flight_ == 0 && rq_.empty() && r_in_flight_ == 0; });
+  }
+
+  bool remove(const std::string& name) { return ::unlink(path(name).c_str()) == 0; }
+
+  int64_t written() const { return written_.load(); }
+  // {bytes_written, write_seconds, bytes_read, read_seconds}
+  std::vector<double> io_stats() const {
+    return {(double)wbytes_.load(), wns_.load() * 1e-9, (double)rbytes_.load(), rns_.load() * 1e-9};
+  }
+
+ private:
+  struct Job {
+    const uint8_t* data;
+    size_t size;
+    int64_t ticket;                               // -1: synchronous-source write (owns its copy)
+    std::shared_ptr<std::vector<uint8_t>> own;
+  };
+  struct RJob {
+    std::string name;
+    uint8_t* dst;
+    size_t size;
+    int64_t ticket;
+  };
+
+  static int64_t now_ns() {
+    return std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now().time_since_epoch())
+        .count();
+  }
+
+  std::string path(const std::string& name) const {
+    const std::string d = root_ + "/" + name.substr(0, 2);
+    return d + "/" + name + ".kv";
+  }
+
+  void enqueue_write(const std::string& name, Job job) {
     {
       std::lock_guard<std::mutex> g(mu_);
       auto it = pending_.find(name);
-      if (it != pending_.end()) {
-        if ((py::ssize_t)it->second->size() != out.size()) return false;
-        std::memcpy(out.mutable_data(), it->second->data(), it->second->size());
+      if (it != pending_.end() && it->second.ticket >= 0) wdone_.push_back(it->second.ticket);  // superseded
+      pending_[name] = job;
+      q_.push_back(name);
+    }
+    cv_.notify_one();
+  }
+
+  bool read_into(const std::string& name, uint8_t* dst, size_t n) {
+    const int64_t t0 = now_ns();
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      auto it = pending_.find(name);
+      if (it != pending_.end()) {  // still queued for writing: copy from the writer's source
+        if (it->second.size != n) return false;
+        std::memcpy(dst, it->second.data, n);
         return true;
       }
     }
-    py::gil_scoped_release nogil;
     int fd = ::open(path(name).c_str(), O_RDONLY);
     if (fd < 0) return false;
-    size_t off = 0, n = (size_t)out.size();
-    uint8_t* dst = out.mutable_data();
+    size_t off = 0;
     while (off < n) {
       ssize_t r = ::read(fd, dst + off, n - off);
       if (r <= 0) break;
       off += (size_t)r;
     }
     ::close(fd);
+    if (off == n) {
+      rbytes_ += (int64_t)n;
+      rns_ += now_ns() - t0;
+    }
     return off == n;
   }
 
-  void flush() {
-    std::unique_lock<std::mutex> g(mu_);
-    done_cv_.wait(g, [this] { return q_.empty() && in_flight_ == 0; });
+  void run_reads() {
+    for (;;) {
+      RJob job;
+      {
+        std::unique_lock<std::mutex> g(mu_);
+        rcv_.wait(g, [this] { return stop_ || !rq_.empty(); });
+        if (stop_ && rq_.empty()) return;
+        job = rq_.front();
+        rq_.pop_front();
+        ++r_in_flight_;
+      }
+      const bool ok = read_into(job.name, job.dst, job.size);
+      {
+        std::lock_guard<std::mutex> g(mu_);
+        rdone_.emplace_back(job.ticket, ok);
+        --r_in_flight_;
+      }
+      done_cv_.notify_all();
+    }
   }
 
-  bool remove(const std::string& name) { return ::unlink(path(name).c_str()) == 0; }
-
-  int64_t written() const { return written_.load(); }
-
- private:
-  std::string path(const std::string& name) const {
-    const std::string d = root_ + "/" + name.substr(0, 2);
-    return d + "/" + name + ".kv";
-  }
-
-  void run() {
+  void run_writes() {
     for (;;) {
       std::string name;
-      std::shared_ptr<std::vector<uint8_t>> buf;
+      Job job;
       {
         std::unique_lock<std::mutex> g(mu_);
         cv_.wait(g, [this] { return stop_ || !q_.empty(); });
         if (stop_ && q_.empty()) return;
         name = q_.front();
         q_.pop_front();
-        buf = pending_[name];
+        auto it = pending_.find(name);
+        if (it == pending_.end()) continue;  // a later enqueue of the same name already wrote it
+        job = it->second;
         ++in_flight_;
       }
+      const int64_t t0 = now_ns();
       const std::string d = root_ + "/" + name.substr(0, 2);
       ::mkdir(d.c_str(), 0755);
       const std::string fin = path(name);
-      const std::string tmp = fin + ".tmp" + std::to_string((uintptr_t)buf.get());
+      const std::string tmp = fin + ".tmp" + std::to_string((uintptr_t)job.data) + "." +
+                              std::to_string((uintptr_t)std::hash<std::thread::id>{}(std::this_thread::get_id()));
       int fd = ::open(tmp.c_str(), O_WRONLY | O_CREAT | O_TRUNC, 0644);
       bool ok = fd >= 0;
       if (ok) {
         size_t off = 0;
-        while (off < buf->size()) {
-          ssize_t w = ::write(fd, buf->data() + off, buf->size() - off);
+        while (off < job.size) {
+          ssize_t w = ::write(fd, job.data + off, job.size - off);
           if (w <= 0) {
             ok = false;
             break;
@@ -136,9 +241,14 @@ class FsStore {
       {
         std::lock_guard<std::mutex> g(mu_);
         auto it = pending_.find(name);
-        if (it != pending_.end() && it->second == buf) pending_.erase(it);
+        if (it != pending_.end() && it->second.data == job.data && it->second.ticket == job.ticket) pending_.erase(it);
+        if (job.ticket >= 0) wdone_.push_back(job.ticket);
         --in_flight_;
-        if (ok) ++written_;
+        if (ok) {
+          ++written_;
+          wbytes_ += (int64_t)job.size;
+          wns_ += now_ns() - t0;
+        }
       }
       done_cv_.notify_all();
     }
@@ -146,23 +256,32 @@ class FsStore {
 
   std::string root_;
   std::mutex mu_;
-  std::condition_variable cv_, done_cv_;
+  std::condition_variable cv_, rcv_, done_cv_;
   std::deque<std::string> q_;
-  std::unordered_map<std::string, std::shared_ptr<std::vector<uint8_t>>> pending_;
+  std::deque<RJob> rq_;
+  std::unordered_map<std::string, Job> pending_;
+  std::vector<int64_t> wdone_;
+  std::vector<std::pair<int64_t, bool>> rdone_;
   std::vector<std::thread> workers_;
   bool stop_ = false;
-  int in_flight_ = 0;
-  std::atomic<int64_t> written_{0};
+  int in_flight_ = 0, r_in_flight_ = 0;
+  std::atomic<int64_t> written_{0}, wbytes_{0}, wns_{0}, rbytes_{0}, rns_{0};
 };
 
 }  // namespace
 
 void register_fs_store(py::module_& m) {
   py::class_<FsStore>(m, "FsStore")
-      .def(py::init<const std::string&, int>(), py::arg("root"), py::arg("threads") = 8)
+      .def(py::init<const std::string&, int, int>(), py::arg("root"), py::arg("threads") = 8,
+           py::arg("read_threads") = 8)
       .def("write", &FsStore::write)
+      .def("write_async", &FsStore::write_async)
+      .def("poll_writes", &FsStore::poll_writes)
       .def("exists", &FsStore::exists)
       .def("read", &FsStore::read)
+      .def("read_async", &FsStore::read_async)
+      .def("poll_reads", &FsStore::poll_reads)
+      .def("io_stats", &FsStore::io_stats)
       .def("flush", &FsStore::flush, py::call_guard<py::gil_scoped_release>())
       .def("remove", &FsStore::remove)
       .def_property_readonly("written", &FsStore::written);

@@ -90,6 +90,8 @@ class LLMEngine:
                     params: Optional[SamplingParams] = None, priority: int = 0,
                     kv_transfer_params: Optional[dict] = None, lora_id: int = 0,
                     arrival_time: Optional[float] = None, mm_inputs: Optional[list] = None) -> Request:
+        if params is not None and params.logit_bias:
+            params.check_vocab(self.cfg.model_config.vocab_size)
         r = Request(request_id, list(prompt_token_ids), params or SamplingParams(), priority=priority,
                     kv_transfer_params=kv_transfer_params, lora_id=lora_id, mm_inputs=mm_inputs or None)
         if arrival_time is not None:

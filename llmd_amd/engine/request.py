@@ -38,7 +38,7 @@ class SamplingParams:
         return self.temperature <= 0.0
 
     @classmethod
-    def from_openai(cls, body: dict, default_max: int = 16) -> "SamplingParams":
+    def from_openai(cls, body: dict, default_max: int = 16, vocab_size: Optional[int] = None) -> "SamplingParams":
         stop = body.get("stop") or []
         if isinstance(stop, str):
             stop = [stop]
@@ -47,7 +47,7 @@ class SamplingParams:
         def g(k, d):
             v = body.get(k)
             return d if v is None else v
-        return cls(
+        sp = cls(
             max_tokens=int(mt) if mt is not None else default_max,
             temperature=float(body.get("temperature", 1.0) if body.get("temperature") is not None else 1.0),
             top_p=float(g("top_p", 1.0)),
@@ -66,6 +66,7 @@ class SamplingParams:
             min_p=float(g("min_p", 0.0)),
             logit_bias={int(k): float(v) for k, v in (body.get("logit_bias") or {}).items()} or None,
         )._validated()
+        return sp.check_vocab(vocab_size) if vocab_size else sp
 
     def _validated(self) -> "SamplingParams":
         """OpenAI / vLLM ranges (ValueError -> HTTP 400)."""
@@ -81,6 +82,20 @@ class SamplingParams:
             raise ValueError(f"n must be in [1, 128], got {self.n}")
         if self.max_tokens < 0 or self.temperature < 0 or not 0.0 < self.top_p <= 1.0:
             raise ValueError("max_tokens and temperature must be >= 0 and top_p in (0, 1]")
+        for k, v in (self.logit_bias or {}).items():
+            if k < 0:
+                raise ValueError(f"logit_bias token id {k} is negative")
+            if not -100.0 <= v <= 100.0:  # OpenAI range; also rejects nan/inf
+                raise ValueError(f"logit_bias value for token {k} must be in [-100, 100], got {v}")
+        return self
+
+    def check_vocab(self, vocab_size: int) -> "SamplingParams":
+        """logit_bias keys index the logits row on the GPU and must lie in
+        [0, vocab_size): an out-of-range column in the penalty index_put_ would
+        fault the device for every in-flight request."""
+        for k in (self.logit_bias or {}):
+            if not 0 <= k < vocab_size:
+                raise ValueError(f"logit_bias token id {k} outside the vocabulary [0, {vocab_size})")
         return self
 
 

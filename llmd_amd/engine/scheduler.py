@@ -128,6 +128,8 @@ class Scheduler:
         self.waiting = _WaitQueue(self.sc.policy)
         self.running: list[Request] = []
         self.remote_wait: dict[str, Request] = {}
+        # reloading their prefix from the offload tiers (kvcache/offload.py start_load / poll_loads)
+        self.offload_wait: dict[str, Request] = {}
         # aborted while their KV pull was in flight: request id -> seq id whose
         # blocks stay allocated until the connector reports the pull finished
         self.aborted_remote: dict[str, int] = {}
@@ -157,6 +159,12 @@ class Scheduler:
             return None
         if r in self.running:
             self.running.remove(r)
+        elif request_id in self.offload_wait:
+            # the side stream may still be scattering into its blocks: they are freed
+            # when the load reports done (schedule -> poll_loads)
+            self.offload.cancel_load(request_id)
+            self._finish(r, Status.FINISHED_ABORTED, free_blocks=False)
+            return r
         elif self.remote_wait.pop(request_id, None) is not None:
             # the transfer worker may still be writing into this request's local
             # blocks: keep them allocated until the pull reports done
@@ -171,7 +179,7 @@ class Scheduler:
 
     @property
     def num_waiting(self) -> int:
-        return len(self.waiting) + len(self.remote_wait)
+        return len(self.waiting) + len(self.remote_wait) + len(self.offload_wait)
 
     @property
     def num_running(self) -> int:
@@ -179,7 +187,7 @@ class Scheduler:
 
     def has_work(self) -> bool:
         return (bool(self.running) or len(self.waiting) > 0 or bool(self.remote_wait)
-                or bool(self.aborted_remote))
+                or bool(self.aborted_remote) or bool(self.offload_wait))
 
     # ------------------------------------------------------------ helpers
     def _tokens(self, r: Request) -> np.ndarray:
@@ -243,6 +251,19 @@ class Scheduler:
                     r.status = Status.WAITING
                     r.kv_transfer_params = None
                     self.waiting.push(r, front=True)
+        # 0b. offload-tier reloads that landed: back to the head of the queue with the
+        # reloaded tokens counted as computed
+        if self.offload_wait:
+            for r, ntok in self.offload.poll_loads():
+                if self.offload_wait.pop(r.request_id, None) is None:
+                    continue
+                if r.status.finished:  # aborted while loading
+                    self.bm.free(r.seq_id)
+                    continue
+                r.num_computed_tokens += ntok
+                if r.num_preemptions == 0:
+                    r.num_cached_tokens = r.num_computed_tokens
+                self.waiting.push(r, front=True)
         # 1. running
         i = 0
         while i < len(self.running) and budget > 0:
@@ -289,11 +310,18 @@ class Scheduler:
             if not self.bm.has_seq(r.seq_id):
                 toks = self._tokens(r)
                 cached = self.bm.acquire(r.seq_id, toks, r.cache_extra)
-                if self.offload is not None and self.cfg.cache.enable_prefix_caching:
-                    cached += self.offload.load_prefix(r, toks, cached, self.bm)
                 r.num_computed_tokens = cached
                 if r.num_preemptions == 0:
                     r.num_cached_tokens = cached
+                if (self.offload is not None and self.cfg.cache.enable_prefix_caching
+                        and self.offload.start_load(r, toks, cached, self.bm)):
+                    # host / disk blocks continue the prefix: they load asynchronously
+                    # (side stream, native read pool) while the engine keeps stepping
+                    self.waiting.pop()
+                    self.offload_wait[r.request_id] = r
+                    if r.first_scheduled_time is None:
+                        r.first_scheduled_time = time.monotonic()
+                    continue
             n = r.num_tokens - r.num_computed_tokens
             if not self.sc.enable_chunked_prefill and n > budget:
                 break

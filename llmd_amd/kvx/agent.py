@@ -69,6 +69,8 @@ import torch
 from llmd_amd.utils import markers
 
 log = logging.getLogger("llmd.kvx")
+# peer-pull copy engine (csrc/ops/kvx_copy.hip): 1 = LDS-staged LDS-DMA kernel (default), 0 = register-staged
+COPY_ENGINE = int(os.environ.get("LLMD_KVX_COPY_ENGINE", "1"))
 
 
 def _send(sock, obj):
@@ -503,7 +505,7 @@ class KvxAgent:
             pairs = torch.tensor(list(zip(rblocks, lblocks)), dtype=torch.int32, device=self.kv.device)
             sg = torch.tensor(segs, dtype=torch.int64, device=self.kv.device)
             C.kvx_copy_blocks(self.kv, base, self.layer_block_bytes, int(rmeta["layer_block_bytes"]), pairs, sg,
-                              max(s[2] for s in segs))
+                              max(s[2] for s in segs), COPY_ENGINE)
             ev = torch.cuda.Event()
             ev.record(stream)
         ev.synchronize()

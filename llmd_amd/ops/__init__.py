@@ -904,6 +904,40 @@ def mgemm_ok(x: torch.Tensor, w: torch.Tensor) -> bool:
 _MGEMM_MS = (64, 96, 128)
 
 
+PGEMM_VARIANT = int(os.environ.get("LLMD_PGEMM_VARIANT", "1"))
+
+
+def pgemm(x: torch.Tensor, w: torch.Tensor, epi: int = 0, out: Optional[torch.Tensor] = None,
+          variant: Optional[int] = None) -> torch.Tensor:
+    """Y = X W^T on the prefill GEMM (csrc/ops/pgemm.hip: 256 x 256 LDS-DMA MFMA
+    tiles; N % 256 == 0, K % 64 == 0, any M). epi=1: ``w`` holds gate/up rows
+    interleaved per 256-row tile (pgemm_pack_gate_up) and the kernel stores
+    silu(gate) * up, [M, N / 2]."""
+    M = x.shape[0]
+    N = w.shape[0]
+    if out is None:
+        out = torch.empty(M, N // 2 if epi else N, dtype=x.dtype, device=x.device)
+    native().pgemm(out, x, w, epi, PGEMM_VARIANT if variant is None else variant)
+    return out
+
+
+def pgemm_pack_gate_up(w: torch.Tensor) -> torch.Tensor:
+    """[2F, K] (gate rows, then up rows) -> the fused-SiLU pgemm layout: per
+    256-row tile, 128 gate rows then the matching 128 up rows (F % 128 == 0)."""
+    F2, K = w.shape
+    F = F2 // 2
+    assert F % 128 == 0, F
+    g = w[:F].view(F // 128, 128, K)
+    u = w[F:].view(F // 128, 128, K)
+    return torch.stack((g, u), 1).reshape(F2, K).contiguous()
+
+
+def pgemm_ok(x: torch.Tensor, w: torch.Tensor) -> bool:
+    return (x.dim() == 2 and x.dtype == torch.bfloat16 and w.dtype == torch.bfloat16 and x.is_cuda
+            and w.shape[0] % 256 == 0 and w.shape[1] % 64 == 0 and x.stride(-1) == 1 and x.stride(0) % 8 == 0
+            and w.is_contiguous())
+
+
 def mgemm_choice(M: int, N: int, K: int) -> Optional[tuple[int, int, int]]:
     """Plan of the medium-M decode GEMM for this shape, or None: the measured
     table (ops/mgemm_table.py, winners over hipBLASLt and the small-M kernel)

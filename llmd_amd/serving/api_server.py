@@ -75,6 +75,7 @@ class OpenAIServer:
         self.name = cfg.served_name
         mc = cfg.model_config
         self.tok = tokenizer or load_tokenizer(cfg.tokenizer, mc.vocab_size, mc.bos_token_id, mc.eos_ids[0])
+        self._vocab = mc.vocab_size
         self.lora = lora_manager
         self.opts = opts or ServingOptions()
         self.template = ChatTemplate(style_for(mc.model_type), model_dir=cfg.tokenizer,
@@ -288,7 +289,7 @@ class OpenAIServer:
                 prompts = [self._chat_ids(body)] if chat else self._prompt_ids(body)
             tools_on = chat and self._tools_active(body)
             params = SamplingParams.from_openai(body, default_max=16 if not chat else
-                                                max(1, self.cfg.sched.max_model_len - 1))
+                                                max(1, self.cfg.sched.max_model_len - 1), vocab_size=self._vocab)
         except (ValueError, TypeError) as e:
             return _err(400, str(e))
         except RuntimeError as e:  # encoder (EC connector) failure
@@ -618,8 +619,12 @@ class OpenAIServer:
         else:
             return _err(400, "input is required")
         ids = self.tok.encode(self.template.render(msgs, True))
-        params = SamplingParams.from_openai(dict(body, max_tokens=body.get("max_output_tokens")),
-                                            default_max=max(1, self.cfg.sched.max_model_len - len(ids) - 1))
+        try:
+            params = SamplingParams.from_openai(dict(body, max_tokens=body.get("max_output_tokens")),
+                                                default_max=max(1, self.cfg.sched.max_model_len - len(ids) - 1),
+                                                vocab_size=self._vocab)
+        except (ValueError, TypeError) as e:
+            return _err(400, str(e))
         toks, last = await self._run_one(req, ids, params, lora=self._lora_id(body))
         text = self.tok.decode(toks)
         rid = f"resp_{uuid.uuid4().hex}"
@@ -667,7 +672,7 @@ class OpenAIServer:
                 ids, mm = await self._chat_mm(chat_body, req.headers)
             else:
                 ids = self._chat_ids(chat_body)
-            params = SamplingParams.from_openai(chat_body)
+            params = SamplingParams.from_openai(chat_body, vocab_size=self._vocab)
         except (ValueError, TypeError) as e:
             return _err(400, str(e))
         toks, last = await self._run_one(req, ids, params, lora=self._lora_id(body), mm=mm)
@@ -699,7 +704,7 @@ class OpenAIServer:
         else:
             return _err(400, "token_ids or prompt is required")
         sp = dict(body.get("sampling_params") or {})
-        params = SamplingParams.from_openai(sp, default_max=16)
+        params = SamplingParams.from_openai(sp, default_max=16, vocab_size=self._vocab)
         toks, last = await self._run_one(req, ids, params, lora=self._lora_id(body))
         return web.json_response({"request_id": req.headers.get("x-request-id"), "prompt_token_ids": ids,
                                   "choices": [{"index": 0, "token_ids": toks,

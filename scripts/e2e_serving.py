@@ -151,7 +151,7 @@ def _offload_loads(ports):
     n = 0.0
     for port in ports:
         m = parse_prometheus(_get(f"http://127.0.0.1:{port}/metrics", 5) or "")
-        n += sum(v for lab, v in m.get("llmd:kv_offload_blocks_total", []) if lab.get("op", "").startswith("load"))
+        n += sum(v for lab, v in m.get("vllm:kv_offload_blocks_total", []) if lab.get("op", "").startswith("load"))
     return n
 
 

@@ -49,7 +49,7 @@ def importer(gb, path):
     dst = torch.zeros(8, dtype=torch.bfloat16, device="cuda")
     pairs = torch.tensor([[0, 0]], dtype=torch.int32, device="cuda")
     seg = torch.tensor([[total - 16, 0, 16]], dtype=torch.int64, device="cuda")
-    _C.kvx_copy_blocks(dst, base, 16, 0, pairs, seg, 16)
+    _C.kvx_copy_blocks(dst, base, 16, 0, pairs, seg, 16, 1)
     torch.cuda.synchronize()
     print(f"[imp] tail copy ok={bool((dst == 5.0).all())}", flush=True)
     _C.vmm_release(base)

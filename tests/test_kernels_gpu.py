@@ -205,6 +205,23 @@ def test_mgemm_fp8(M, plan):
     _close(got, lib, atol=2e-3, rtol=2e-2)
 
 
+@pytest.mark.parametrize("M,N,K", [(1, 256, 64), (77, 512, 1024), (256, 768, 128), (1000, 1280, 2048),
+                                   (4608, 1024, 8192)])
+@pytest.mark.parametrize("variant", [0, 1])
+def test_pgemm(M, N, K, variant):
+    """Prefill GEMM (256 x 256 LDS-DMA tiles, counted-vmcnt pipeline) vs the fp32
+    reference; K = 64 and 128 exercise the prologue / tail waits without a steady state;
+    odd M the clamped rows. Fused SiLU-and-mul epilogue on the interleaved gate/up layout."""
+    torch.manual_seed(11)
+    x = (torch.rand(M, K, device=DEV) * 2 - 1).to(torch.bfloat16)
+    w = ((torch.rand(N, K, device=DEV) * 2 - 1) * 0.05).to(torch.bfloat16)
+    ref = x.float() @ w.float().t()
+    _close(ops.pgemm(x, w, variant=variant), ref, atol=2e-2, rtol=2e-2)
+    g, u = ref[:, : N // 2], ref[:, N // 2:]
+    _close(ops.pgemm(x, ops.pgemm_pack_gate_up(w), epi=1, variant=variant), g * torch.sigmoid(g) * u,
+           atol=2e-2, rtol=3e-2)
+
+
 @pytest.mark.parametrize("Hq,Hkv,D", [(64, 8, 128), (32, 8, 128), (8, 8, 128), (64, 8, 64), (16, 8, 128)])
 @pytest.mark.parametrize("bs", [16, 64])
 def test_paged_prefill(Hq, Hkv, D, bs):
@@ -263,6 +280,28 @@ def test_sample_split_rows_match_unsplit():
     _close(lp_small, lp_big[:5], atol=1e-4, rtol=1e-4)
 
 
+@pytest.mark.parametrize("B", [4, 600])   # split rows (small batch) and unsplit
+def test_sample_logprob_masked_rows(B):
+    """Rows with -inf entries (top-k / top-p / min_p masks): the log-prob of the
+    pick must be finite and match the masked log-softmax (a thread whose first
+    entries are masked used to turn its partial sum-exp into NaN)."""
+    torch.manual_seed(10)
+    V = 128256
+    x = torch.randn(B, V, device=DEV)
+    topk = torch.full((B,), 40, dtype=torch.int32, device=DEV)
+    temps = torch.full((B,), 0.9, device=DEV)
+    m = ops.topk_topp_mask(x.clone(), topk, None, temps)
+    m[1::2, ::3] = float("-inf")                       # and a min_p-like strided mask on odd rows
+    m[1::2, x.argmax(-1)[1]] = 5.0                     # keep one finite entry in those rows
+    seeds = torch.arange(B, device=DEV, dtype=torch.int64) * 13 + 1
+    for t in (None, temps):
+        ids, lp = ops.sample(m, t, seeds if t is not None else None, want_logprob=True)
+        assert torch.isfinite(lp).all()
+        assert torch.isfinite(m.gather(1, ids[:, None])).all()       # never picks a masked entry
+        want = torch.log_softmax(m, -1).gather(1, ids[:, None]).squeeze(1)
+        _close(lp, want, atol=1e-3, rtol=1e-3)
+
+
 def test_sample_temperature_distribution():
     V = 8
     logits = torch.tensor([[0.0, 1.0, 2.0, 0.5, -1.0, 0.0, 3.0, 1.5]], device=DEV).repeat(20000, 1)
@@ -289,7 +328,8 @@ def test_topk_topp_mask():
     assert torch.equal(torch.isinf(a), torch.isinf(b))
 
 
-def test_kvx_copy_blocks_and_reslice():
+@pytest.mark.parametrize("engine", [0, 1])   # register-staged, LDS-staged (LDS-DMA)
+def test_kvx_copy_blocks_and_reslice(engine):
     C = ops.native()
     L, H, bs, D = 3, 8, 16, 128
     src = torch.randn(10, L, 2, H, bs, D, device=DEV).to(torch.bfloat16)
@@ -297,7 +337,7 @@ def test_kvx_copy_blocks_and_reslice():
     bb = src[0].numel() * 2
     pairs = torch.tensor([[1, 5], [7, 0], [3, 11]], dtype=torch.int32, device=DEV)
     segs = torch.tensor([[0, 0, bb]], dtype=torch.int64, device=DEV)
-    C.kvx_copy_blocks(dst, src.data_ptr(), bb, bb, pairs, segs, bb)
+    C.kvx_copy_blocks(dst, src.data_ptr(), bb, bb, pairs, segs, bb, engine)
     torch.cuda.synchronize()
     for s_, d_ in [(1, 5), (7, 0), (3, 11)]:
         assert torch.equal(dst[d_], src[s_])
@@ -308,7 +348,7 @@ def test_kvx_copy_blocks_and_reslice():
     sg = [(((l * 2 + kv) * H + 2) * head, ((l * 2 + kv) * hl) * head, hl * head) for l in range(L) for kv in range(2)]
     C.kvx_copy_blocks(dst2, src.data_ptr(), dst2[0].numel() * 2, bb,
                       torch.tensor([[4, 2]], dtype=torch.int32, device=DEV),
-                      torch.tensor(sg, dtype=torch.int64, device=DEV), hl * head)
+                      torch.tensor(sg, dtype=torch.int64, device=DEV), hl * head, engine)
     torch.cuda.synchronize()
     assert torch.equal(dst2[2], src[4][:, :, 2:4])
     # SDMA path

@@ -72,3 +72,74 @@ def test_host_reload_retried_when_pool_was_full():
     assert not eng.has_unfinished()  # a waiting request holding blocks used to deadlock here
     assert outs["again"] == base
     assert eng.offload.stats["loaded_cpu"] >= 96 // 16 - 1
+
+
+def test_offload_metrics_use_vllm_names(tmp_path):
+    """Transfer metrics follow vLLM's offloading contract (vllm:kv_offload_*: bytes,
+    time and size distribution per transfer type; kv-offloader.md:211)."""
+    cfg = {"cpu_bytes_to_use": 64 << 20, "fs_root": str(tmp_path / "kv")}
+    eng = make_engine(kv_offload_config=cfg)
+    _gen(eng, _prompt(5))
+    eng.offload.fs.flush()
+    eng.reset_prefix_cache()
+    _gen(eng, _prompt(5))
+    text = eng.offload.render_metrics("m").decode()
+    assert "llmd:kv_offload" not in text
+    for t in ("GPU_to_CPU", "CPU_to_GPU", "CPU_to_FS"):
+        line = next(l for l in text.splitlines()
+                    if l.startswith("vllm:kv_offload_total_bytes") and f'transfer_type="{t}"' in l)
+        assert float(line.split()[-1]) > 0, line
+    assert 'vllm:kv_offload_size_bucket{model_name="m",transfer_type="GPU_to_CPU",le="+Inf"}' in text
+    assert 'vllm:kv_offload_total_time{model_name="m",transfer_type="CPU_to_GPU"}' in text
+
+
+def test_fs_reload_is_asynchronous(tmp_path):
+    """An FS-tier reload does not read the disk on the engine thread: the request
+    waits in offload_wait while the native read pool fills pinned buffers, and
+    other requests keep being scheduled meanwhile."""
+    cfg = {"cpu_bytes_to_use": 64 << 20, "fs_root": str(tmp_path / "kv")}
+    base = _gen(make_engine(), _prompt(9))
+    eng = make_engine(kv_offload_config=cfg)
+    _gen(eng, _prompt(9))
+    eng.offload.fs.flush()
+    eng2 = make_engine(kv_offload_config=cfg)
+    fs = eng2.offload.fs
+    reads = []
+    orig = fs.read
+    fs_read_sync = []
+
+    class Spy:  # the synchronous read must never be used by the engine
+        def __getattr__(self, k):
+            if k == "read":
+                fs_read_sync.append(1)
+            return getattr(fs, k)
+    eng2.offload.fs = Spy()
+    sp = SamplingParams(max_tokens=8, temperature=0.0, ignore_eos=True)
+    eng2.add_request("fs", _prompt(9), sp)
+    eng2.add_request("other", _prompt(10, 40), SamplingParams(max_tokens=4, temperature=0.0, ignore_eos=True))
+    outs = {"fs": [], "other": []}
+    for o in eng2.step():
+        outs[o.request_id] += o.new_token_ids
+    assert "fs" in eng2.sched.offload_wait or eng2.offload.stats["loaded_fs"] > 0
+    for _ in range(200):
+        if not eng2.has_unfinished():
+            break
+        for o in eng2.step():
+            outs[o.request_id] += o.new_token_ids
+    assert outs["fs"] == base and len(outs["other"]) == 4
+    assert eng2.offload.stats["loaded_fs"] >= 150 // 16 - 1
+    assert not fs_read_sync and not reads and orig
+
+
+def test_abort_while_loading_frees_blocks():
+    eng = make_engine(kv_offload_config={"cpu_bytes_to_use": 64 << 20})
+    _gen(eng, _prompt(13))
+    eng.reset_prefix_cache()
+    free0 = eng.bm.num_free()
+    eng.add_request("x", _prompt(13), SamplingParams(max_tokens=4, temperature=0.0, ignore_eos=True))
+    eng.sched.schedule()  # admission starts the reload (CPU engine: it completes at once)
+    if "x" in eng.sched.offload_wait:
+        eng.abort("x")
+        eng.sched.schedule()
+        assert "x" not in eng.sched.offload_wait
+        assert eng.bm.num_free() == free0

@@ -50,10 +50,12 @@ def test_min_p_masks_low_probability_tokens():
 
 
 @pytest.mark.parametrize("body", [{"presence_penalty": 3}, {"frequency_penalty": -2.5}, {"repetition_penalty": 0},
-                                  {"min_p": 1.5}, {"n": 0}, {"top_p": 0}, {"temperature": -1}])
+                                  {"min_p": 1.5}, {"n": 0}, {"top_p": 0}, {"temperature": -1},
+                                  {"logit_bias": {"-1": 1.0}}, {"logit_bias": {"5": 101.0}},
+                                  {"logit_bias": {"5": float("nan")}}, {"logit_bias": {"32000": 1.0}}])
 def test_validation(body):
     with pytest.raises(ValueError):
-        SamplingParams.from_openai(body)
+        SamplingParams.from_openai(body, vocab_size=32000)
 
 
 def _cfg():
@@ -97,6 +99,13 @@ def test_api_n_choices_bias_and_penalties():
                                      if l.startswith("data:") and "[DONE]" not in l]
                 async with s.post(base, json={"prompt": [5], "presence_penalty": 9}) as r:
                     out["bad"] = r.status
+                # a bias key outside the vocabulary would index past the logits row on the device
+                async with s.post(base, json={"prompt": [5], "logit_bias": {"10000000": 5}}) as r:
+                    out["bad_bias"] = r.status
+                async with s.post(base.replace("completions", "chat/completions"),
+                                  json={"messages": [{"role": "user", "content": "hi"}],
+                                        "logit_bias": {"-3": 5}}) as r:
+                    out["bad_bias_chat"] = r.status
             return out
         finally:
             await r1.cleanup()
@@ -118,3 +127,4 @@ def test_api_n_choices_bias_and_penalties():
     assert per[0] >= 1 and per[1] >= 1
     assert out["stream"][-1]["usage"]["completion_tokens"] == 8
     assert out["bad"] == 400
+    assert out["bad_bias"] == 400 and out["bad_bias_chat"] == 400
