@@ -27,12 +27,27 @@ Modes (default ``auto``: agg for N < 8, pd for N >= 8)
         reference tunes the P:D ratio per workload the same way
         (guides/pd-disaggregation/README.md:15-33).
 
+Multi-GPU robustness (N > 1): every process group has an explicit timeout
+(LLMD_DIST_TIMEOUT, default 1800 s) and, before any engine starts, a
+pre-flight (llmd_amd/parallel/preflight.py) proves peer access, IPC and VMM
+pulls, the symm all-reduce (vs RCCL, bit for bit) and the symm EP exchange (vs
+the RCCL all_to_all path) on this node; a failure exits non-zero with the
+failing check and ranks. Under the bench the kvx connector may not degrade a
+P/D pull to TCP (require_ipc): a failed IPC path is an error, never a silent
+1.6 GB msgpack per request.
+
+At N = 8 the P/D run is followed by BASELINE.json's literal split, 2P + 6D
+(``alt_split`` in the JSON; --alt-split none disables), and every result
+carries ``output_tok_s_per_gpu`` (whole job / N) next to the per-decode-GPU
+figure.
+
 Output: one JSON line on rank 0 (see README "bench.py contract").
 """
 from __future__ import annotations
 
 import argparse
 import collections
+import datetime
 import json
 import os
 import statistics
@@ -94,7 +109,15 @@ def parse():
     p.add_argument("--quantization", default=None, choices=[None, "fp8"],
                    help="fp8 = W8A8 linears (the reference AMD recipe serves Llama-3.3-70B-FP8); default bf16")
     p.add_argument("--kv-cache-dtype", default="auto", choices=["auto", "fp8"])
+    p.add_argument("--alt-split", default="auto",
+                   help="pd mode at N=8: also run this P:D split after the main one ('2p6d', BASELINE.json's "
+                        "literal config; 'auto' = 2p6d when N=8 and the main split differs; 'none' = skip)")
+    p.add_argument("--no-preflight", action="store_true", help="skip the N>1 cross-GPU pre-flight checks")
     return p.parse_args()
+
+
+def dist_timeout() -> datetime.timedelta:
+    return datetime.timedelta(seconds=int(os.environ.get("LLMD_DIST_TIMEOUT", "1800")))
 
 
 def _sync(a):
@@ -128,9 +151,22 @@ def main():
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         if forced is None:
-            dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", dev))
+            dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", dev),
+                                    timeout=dist_timeout())
         else:
-            dist.init_process_group("gloo", rank=rank, world_size=world)
+            dist.init_process_group("gloo", rank=rank, world_size=world, timeout=dist_timeout())
+        if a.device == "cuda" and not a.no_preflight:
+            from llmd_amd.parallel import preflight
+
+            # all ranks on one GPU (rehearsal): no peers, no RCCL - the IPC / VMM / symm paths only
+            checks = preflight.CHECKS if forced is None else ("ipc", "vmm")
+            try:
+                preflight.run(rank, world, torch.device("cuda", dev), checks=checks,
+                              cpu_group=dist.new_group(backend="gloo", timeout=datetime.timedelta(seconds=300)),
+                              log=lambda m: print(m, file=sys.stderr, flush=True))
+            except preflight.PreflightError as e:
+                print(f"[bench rank {rank}] PRE-FLIGHT FAILED: {e}", file=sys.stderr, flush=True)
+                sys.exit(3)
 
     if a.mode == "auto":
         a.mode = "pd" if world >= 8 else "agg"
@@ -138,6 +174,7 @@ def main():
         from llmd_amd.bench_pd import run_pd
 
         res = run_pd(a, rank, world, local_rank, log)
+        alt = _alt_split(a, rank, world, local_rank, log, res)
         if rank == 0 and res is not None:
             value = res["gen"] / res["elapsed"]
             out = {
@@ -154,9 +191,13 @@ def main():
                            "max_num_batched_tokens": a.max_num_batched_tokens, "block_size": a.block_size,
                            "kv_transfer": "kvx ipc over xGMI"},
                 "output_tok_s_per_decode_gpu": round(value / res["decode_ranks"], 2),
+                "output_tok_s_per_gpu": round(value / world, 2),
                 "p50_ttft_s": round(res["p50_ttft"], 4) if res["p50_ttft"] is not None else None,
+                "kv_transfer_failures": res.get("kv_failures", 0),
                 **_reference(a.model, value, world),
             }
+            if alt is not None:
+                out["alt_split"] = alt
             line = json.dumps(out)
             print(line, flush=True)
             if a.json_out:
@@ -297,6 +338,7 @@ def main():
                    "max_num_batched_tokens": a.max_num_batched_tokens, "block_size": a.block_size,
                    "graphs": not a.enforce_eager, "kv_cache_dtype": a.kv_cache_dtype},
         "output_tok_s_per_decode_gpu": round(value / max(1, n_decode_gpus), 2),
+        "output_tok_s_per_gpu": round(value / world, 2),
         "p50_ttft_s": round(p50, 4) if p50 is not None else None,
         "prefill_tok_s": round(ptoks / elapsed, 1),
         **_reference(a.model, value, world),
@@ -310,6 +352,46 @@ def main():
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def _alt_split(a, rank, world, local_rank, log, main_res):
+    """BASELINE.json's literal P/D split (2P + 6D at N = 8) after the main run, same
+    steps; failures are reported in the JSON, never lost with the main result."""
+    want = a.alt_split
+    if want == "auto":
+        want = "2p6d" if world == 8 else "none"
+    if want in ("none", ""):
+        return None
+    try:
+        p_n = int(want.split("p")[0])
+        d_n = int(want.split("p")[1].rstrip("d"))
+    except (ValueError, IndexError):
+        return {"error": f"bad --alt-split {want!r}"} if rank == 0 else None
+    if p_n + d_n != world or p_n == (a.prefill_gpus or (3 * world) // 4):
+        return None
+    import gc
+
+    from llmd_amd.bench_pd import run_pd
+
+    gc.collect()
+    if a.device == "cuda":
+        torch.cuda.empty_cache()
+    b = argparse.Namespace(**vars(a))
+    b.prefill_gpus, b.decode_tp = p_n, 0
+    os.environ["LLMD_PD_BASE_PORT"] = str(int(os.environ.get("LLMD_PD_BASE_PORT", "18200")) + 100)
+    try:
+        r = run_pd(b, rank, world, local_rank, log)
+    except Exception as e:  # noqa: BLE001 - the main result must survive
+        print(f"[bench rank {rank}] alt split {want} failed: {e!r}", file=sys.stderr, flush=True)
+        return {"split": want, "error": repr(e)} if rank == 0 else None
+    if rank != 0 or r is None:
+        return None
+    v = r["gen"] / r["elapsed"]
+    return {"split": want, "parallelism": f"pd{r['prefill_ranks']}p{r['decode_ranks']}d"
+                                          + (f"-dtp{r['decode_tp']}" if r.get("decode_tp", 1) > 1 else ""),
+            "value": round(v, 2), "output_tok_s_per_decode_gpu": round(v / r["decode_ranks"], 2),
+            "output_tok_s_per_gpu": round(v / world, 2), "ms_per_step": round(1000 * r["elapsed"] / a.steps, 3),
+            "p50_ttft_s": round(r["p50_ttft"], 4) if r["p50_ttft"] is not None else None}
 
 
 if __name__ == "__main__":

@@ -60,6 +60,64 @@ DASHBOARDS = {
         ("Request success rate", ["sum(rate(vllm:request_success_total[5m]))"], "reqps"),
         ("SLO violations", ["sum(rate(inference_objective_request_slo_violation_total[5m]))"], "ops"),
     ]),
+    # KV-cache performance (reference guides/recipes/observability/grafana/dashboards/
+    # llm-d-performance-kv-cache.json): latency vs cache hit rate, per pod, plus the offload tiers
+    "llmd-kv-cache": ("llm-d AMD / KV-cache performance", [
+        ("Time to first token p50 / p90", [
+            "histogram_quantile(0.5, sum by (le) (rate(vllm:time_to_first_token_seconds_bucket[5m])))",
+            "histogram_quantile(0.9, sum by (le) (rate(vllm:time_to_first_token_seconds_bucket[5m])))"], "s"),
+        ("Inter-token latency p50 / p90", [
+            "histogram_quantile(0.5, sum by (le) (rate(vllm:inter_token_latency_seconds_bucket[5m])))",
+            "histogram_quantile(0.9, sum by (le) (rate(vllm:inter_token_latency_seconds_bucket[5m])))"], "s"),
+        ("KV cache hit rate (pool)", ["sum(rate(vllm:prefix_cache_hits_total[5m])) / "
+                                      "clamp_min(sum(rate(vllm:prefix_cache_queries_total[5m])), 1)"], "percentunit"),
+        ("Per-pod cache hit rate", ["sum by (pod) (rate(vllm:prefix_cache_hits_total[5m])) / "
+                                    "clamp_min(sum by (pod) (rate(vllm:prefix_cache_queries_total[5m])), 1)"],
+         "percentunit"),
+        ("KV cache usage (pool max / mean)", ["max(vllm:kv_cache_usage_perc)", "avg(vllm:kv_cache_usage_perc)"],
+         "percentunit"),
+        ("Per-pod KV cache usage", ["max by (pod) (vllm:kv_cache_usage_perc)"], "percentunit"),
+        ("Request throughput", ["sum(rate(vllm:request_success_total[1m]))"], "reqps"),
+        ("Request queue (running / waiting)", ["sum(vllm:num_requests_running)", "sum(vllm:num_requests_waiting)"],
+         "short"),
+        ("EPP pool health & load", ["inference_pool_ready_pods", "inference_pool_average_queue_size"], "short"),
+        ("EPP pool KV utilisation", ["inference_pool_average_kv_cache_utilization"], "percentunit"),
+        ("Offload tier traffic (bytes/s)", ["sum by (transfer_type) (rate(vllm:kv_offload_total_bytes[1m]))"], "Bps"),
+        ("Offload transfer size p50", ["histogram_quantile(0.5, sum by (le, transfer_type) "
+                                       "(rate(vllm:kv_offload_size_bucket[5m])))"], "bytes"),
+        ("Host-tier occupancy", ["max by (pod) (vllm:kv_offload_cpu_usage_perc)"], "percentunit"),
+    ]),
+    # Diagnostic drill-down (reference llm-d-diagnostic-drilldown-dashboard.json): serving,
+    # routing, prefix caching and P/D sections
+    "llmd-drilldown": ("llm-d AMD / diagnostic drill-down", [
+        ("Model serving: running per pod", ["sum by (pod) (vllm:num_requests_running)"], "short"),
+        ("KV cache utilisation per pod", ["max by (pod) (vllm:kv_cache_usage_perc)"], "percentunit"),
+        ("Request queue lengths", ["sum by (pod) (vllm:num_requests_waiting)"], "short"),
+        ("Model throughput (req/s)", ["sum by (pod) (rate(vllm:request_success_total[1m]))"], "reqps"),
+        ("Generation token rate", ["sum by (pod) (rate(vllm:generation_tokens_total[1m]))"], "short"),
+        ("Queue utilisation (waiting / max-num-seqs)", [
+            "sum by (pod) (vllm:num_requests_waiting) / clamp_min(sum by (pod) (vllm:num_requests_running), 1)"],
+         "percentunit"),
+        ("Routing: request distribution", ["sum by (pod) (rate(vllm:prompt_tokens_total[1m])) / "
+                                           "clamp_min(sum(rate(vllm:prompt_tokens_total[1m])), 1)"], "percentunit"),
+        ("Token distribution (prompt tok/s by pod)", ["sum by (pod) (rate(vllm:prompt_tokens_total[1m]))"], "short"),
+        ("Idle GPU time (pods with no running requests)", ["count(sum by (pod) (vllm:num_requests_running) == 0)"],
+         "short"),
+        ("Routing decision latency p50 / p99", [
+            "histogram_quantile(0.5, sum by (le) (rate(inference_extension_scheduler_e2e_duration_seconds_bucket[5m])))",
+            "histogram_quantile(0.99, sum by (le) (rate(inference_extension_scheduler_e2e_duration_seconds_bucket[5m])))"],
+         "s"),
+        ("Prefix cache hit rate", ["sum(rate(vllm:prefix_cache_hits_total[5m])) / "
+                                   "clamp_min(sum(rate(vllm:prefix_cache_queries_total[5m])), 1)"], "percentunit"),
+        ("Per-instance hit rate", ["sum by (pod) (rate(vllm:prefix_cache_hits_total[5m])) / "
+                                   "clamp_min(sum by (pod) (rate(vllm:prefix_cache_queries_total[5m])), 1)"],
+         "percentunit"),
+        ("P/D: prefill worker utilisation", ["avg(vllm:num_requests_running{llm_d_ai_role=\"prefill\"})"], "short"),
+        ("P/D: decode worker utilisation", ["avg(vllm:kv_cache_usage_perc{llm_d_ai_role=\"decode\"})"],
+         "percentunit"),
+        ("P/D: prefill queue length", ["sum(vllm:num_requests_waiting{llm_d_ai_role=\"prefill\"})"], "short"),
+        ("P/D decisions", ["sum by (decision_type) (rate(llm_d_router_epp_pd_decision_total[5m]))"], "ops"),
+    ]),
 }
 
 

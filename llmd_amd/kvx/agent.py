@@ -119,8 +119,9 @@ class KvxAgent:
     def __init__(self, kv: torch.Tensor, engine_id: Optional[str] = None, host: Optional[str] = None,
                  port: int = 0, tp_rank: int = 0, tp_size: int = 1, abort_timeout: float = 480.0,
                  transport: str = "auto", metrics=None, vmm: Optional[dict] = None, exports: bool = True,
-                 workers: Optional[int] = None):
+                 workers: Optional[int] = None, require_ipc: bool = False):
         self.kv = kv                      # [L, num_blocks, planes, Hkv, bs, D] (layer-major)
+        self.require_ipc = require_ipc    # never degrade a GPU pull to TCP (bench / production P/D)
         self.vmm = vmm                    # chunked exportable pool (model_runner._alloc_cache)
         self.engine_id = engine_id or f"kvx-{uuid.uuid4().hex[:12]}"
         self.tp_rank, self.tp_size = tp_rank, tp_size
@@ -462,13 +463,21 @@ class KvxAgent:
                    and self.transport in ("auto", "ipc", "dma") and not p.get("no_ipc")
                    and rmeta.get("hostname") == socket.gethostname())
         nbytes = sum(s[2] for s in segs) * n
+        if self.require_ipc and self.is_gpu and not use_ipc and self.transport != "tcp":
+            raise RuntimeError(f"kvx: no IPC path to {rmeta.get('engine_id')} (host {rmeta.get('hostname')}, "
+                               f"handle {'ipc_handle' in rmeta or 'vmm' in rmeta}, degraded {bool(p.get('no_ipc'))}) "
+                               "and require_ipc is set")
         if use_ipc:
             try:
                 self._ipc_copy(rmeta, rblocks, lblocks, segs)
             except Exception as e:  # noqa: BLE001 - mapping failed: degrade this peer to TCP
+                if self.require_ipc:
+                    raise RuntimeError(f"kvx IPC pull from {rmeta.get('engine_id')} failed: {e}") from e
                 log.warning("kvx IPC path to %s failed (%s); using TCP for this peer", rmeta.get("engine_id"), e)
                 p["no_ipc"] = True
                 use_ipc = False
+                if self.metrics is not None and hasattr(self.metrics, "on_ipc_fallback"):
+                    self.metrics.on_ipc_fallback()
         if not use_ipc:
             data = self._rpc(p, {"op": "read", "blocks": rblocks, "request_id": prm.get("remote_request_id")})
             if isinstance(data, dict) and data.get("error"):

@@ -4,7 +4,9 @@ Config (vLLM-compatible keys): ``{"kv_connector": "KvxConnector" |
 "NixlConnector", "kv_role": "kv_producer" | "kv_consumer" | "kv_both",
 "kv_load_failure_policy": "recompute" | "fail", "kv_connector_extra_config":
 {"transport": "auto" | "ipc" | "dma" | "tcp", "side_channel_port": 5557,
-"abort_timeout": 480}}``.
+"abort_timeout": 480, "require_ipc": false}}``. ``require_ipc``: a GPU pull
+that cannot use the xGMI IPC/VMM path fails (counted in
+vllm:nixl_num_failed_transfers) instead of degrading to TCP; bench.py sets it.
 """
 from __future__ import annotations
 
@@ -35,15 +37,24 @@ class KvxMetrics:
         self.desc = Histogram("vllm:nixl_num_descriptors", "Descriptors (blocks) per transfer", L,
                               buckets=(1, 4, 16, 64, 256, 1024, 4096), registry=r)
         self.failed = Counter("vllm:nixl_num_failed_transfers", "Failed transfers", L, registry=r)
+        # pulls that left the xGMI IPC path for the TCP fallback (0 on a healthy node)
+        self.ipc_fallback = Counter("llmd:kvx_ipc_fallback", "Pulls degraded from IPC to TCP", L, registry=r)
+        self.n_failed = 0
+        self.n_ipc_fallback = 0
 
     def observe(self, ok: bool, dt: float, nbytes: int, nblocks: int):
         m = self.model
         if not ok:
             self.failed.labels(m).inc()
+            self.n_failed += 1
             return
         self.xfer.labels(m).observe(dt)
         self.bytes.labels(m).observe(nbytes)
         self.desc.labels(m).observe(nblocks)
+
+    def on_ipc_fallback(self):
+        self.ipc_fallback.labels(self.model).inc()
+        self.n_ipc_fallback += 1
 
     def render(self) -> bytes:
         return generate_latest(self.reg)
@@ -67,7 +78,8 @@ class KvxConnector:
                               abort_timeout=float(extra.get("abort_timeout",
                                                             os.environ.get("VLLM_NIXL_ABORT_REQUEST_TIMEOUT", 480))),
                               transport=extra.get("transport", "auto"), metrics=self.metrics,
-                              exports=self.role != "kv_consumer")
+                              exports=self.role != "kv_consumer",
+                              require_ipc=bool(extra.get("require_ipc", False)))
         self._results: dict[str, bool] = {}
         self._finished: list[str] = []
         self._outputs = []

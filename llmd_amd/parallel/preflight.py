@@ -171,8 +171,13 @@ def check_symm_ar(rank, world, dev, grp, devices, rccl=None) -> str:
             # small integers: every partial sum is exact in bf16, so any reduction order is bit-exact
             x = torch.randint(-8, 9, (n,), generator=g).to(torch.bfloat16).to(dev)
             got = ar.all_reduce(x, torch.empty_like(x))
-            ref = x.clone()
-            dist.all_reduce(ref, group=rccl)
+            if dist.get_backend(rccl) == "gloo":  # 1-GPU rehearsal: the sum on the host (exact, integers)
+                ref = x.float().cpu()
+                dist.all_reduce(ref, group=rccl)
+                ref = ref.to(torch.bfloat16).to(dev)
+            else:
+                ref = x.clone()
+                dist.all_reduce(ref, group=rccl)
             torch.cuda.synchronize(dev)
             if not torch.equal(got, ref):
                 raise PreflightError(f"custom all-reduce of {n} bf16 ({'one' if n * 2 <= ar.oneshot_max else 'two'}"

@@ -162,7 +162,11 @@ def load_config(text_or_dict, ctx=None) -> EPPConfig:
             raise ConfigError("multiple scheduling profiles require a profile handler plugin")
         handler = pb.create("single-profile-handler", "single-profile-handler", {}, ctx)
     # ---------------------------------------------------------- parser
-    pref = (raw.get("parser") or {}).get("pluginRef")
+    # parser: top-level ``parser.pluginRef``, or ``requestHandler.parser.pluginRef`` /
+    # ``requestHandler.parsers[].pluginRef`` (docs/api-reference/epp-grpc-apis.md:16-33)
+    rh = raw.get("requestHandler") or {}
+    pref = ((raw.get("parser") or {}).get("pluginRef") or (rh.get("parser") or {}).get("pluginRef")
+            or next((p.get("pluginRef") for p in (rh.get("parsers") or []) if isinstance(p, dict)), None))
     parser = ref(pref, "parser") if pref else pb.create("openai-parser", "openai-parser", {}, ctx)
     # ---------------------------------------------------------- flow control
     fc = raw.get("flowControl")

@@ -182,7 +182,8 @@ class EPP:
             hdrs.update(result.headers)
             hdrs.update(req.data.get("upstream_headers", {}))
             new_body = None
-            if req.target_model and req.target_model != req.model and isinstance(req.body, dict):
+            if (req.target_model and req.target_model != req.model and isinstance(req.body, dict)
+                    and not req.data.get("grpc")):
                 b = dict(req.body)
                 b["model"] = req.target_model
                 new_body = json.dumps(b).encode()

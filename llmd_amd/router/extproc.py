@@ -316,7 +316,11 @@ class _Stream:
             if self.first is None:
                 self.first = now
             self.last = now
-            self.tail = (self.tail + chunk)[-65536:]
+            if self.d is not None and self.d.req.data.get("grpc"):
+                # gRPC frames must stay whole for the usage parse (bounded)
+                self.tail = (self.tail + chunk) if len(self.tail) < (8 << 20) else self.tail
+            else:
+                self.tail = (self.tail + chunk)[-65536:]
             if self.d is not None and not self.done:
                 self.srv.epp.on_response_chunk(self.d, chunk, now)
         R = PB["ProcessingResponse"]()
@@ -334,7 +338,7 @@ class _Stream:
         self.done = True
         end = time.monotonic()
         info = {"status": None if aborted else self.status, "duration": end - self.t0, "ttft": None,
-                "usage": _find_usage(self.tail)}
+                "usage": _find_usage(self.tail, grpc=bool(self.d.req.data.get("grpc")))}
         if self.first is not None and (self.d.req.stream or self.status == 200):
             info["ttft"] = self.first - self.t0
         n = (info["usage"] or {}).get("completion_tokens") or 0

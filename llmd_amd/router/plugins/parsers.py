@@ -91,11 +91,47 @@ class PassthroughParser(Parser):
 
 @register("vllmgrpc-parser")
 class VllmGrpcParser(OpenAIParser):
-    """vLLM gRPC Generate/Embed (token-in): the HTTP bridge forwards the
-    decoded message as JSON with `token_ids`."""
+    """vLLM gRPC ``VllmEngine/Generate`` and ``/Embed``
+    (docs/api-reference/epp-grpc-apis.md:9-14): the body is the gRPC-framed
+    protobuf message (5-byte length prefix) of an h2c request, as the ext_proc
+    stream (Envoy) or the router's gRPC data plane (router/grpc_proxy.py) hands
+    it over. ``tokenized.input_ids`` become the request's exact tokens for
+    prefix scoring (``text`` input: the text); the body is forwarded unchanged
+    (no model rewrite: the message has no model field). Other paths: the
+    OpenAI parser, plus JSON ``token_ids`` (/inference/v1/generate)."""
 
     def parse(self, path, body, headers):
-        req = super().parse(path, body, headers)
-        if "token_ids" in req.body:
-            req.token_ids = list(req.body["token_ids"])
+        from llmd_amd.serving import vllm_grpc as vg
+
+        if path not in vg.PATHS:
+            req = super().parse(path, body, headers)
+            if "token_ids" in req.body:
+                req.token_ids = list(req.body["token_ids"])
+            return req
+        msgs = vg.unframe(bytes(body))
+        if len(msgs) != 1:
+            raise ValueError(f"expected one gRPC message, got {len(msgs)}")
+        h = headers if isinstance(headers, CIHeaders) else CIHeaders(dict(headers))
+        from google.protobuf.message import DecodeError
+
+        try:
+            if path == vg.GENERATE:
+                m = vg.PB["GenerateRequest"].FromString(msgs[0])
+            else:
+                m = vg.PB["EmbedRequest"].FromString(msgs[0])
+        except DecodeError as e:
+            raise ValueError(f"invalid {path} message: {e}") from e
+        req = InferenceRequest(path=path, body={"grpc_method": path.rsplit("/", 1)[1]}, headers=h,
+                               raw_size=len(body))
+        req.data["grpc"] = True
+        req.model = h.get("x-llm-d-model", "") or ""
+        req.target_model = req.model
+        if path == vg.GENERATE and m.WhichOneof("input") == "text":
+            req.prompt = m.text
+        else:
+            req.token_ids = list(m.tokenized.input_ids)
+            req.prompt = m.tokenized.original_text or " ".join(map(str, req.token_ids))
+        req.stream = bool(getattr(m, "stream", False))
+        if m.request_id:
+            req.request_id = m.request_id
         return req

@@ -40,7 +40,9 @@ from .types import SchedulingError
 log = logging.getLogger("llmd.router.proxy")
 
 INFERENCE_PATHS = {"/v1/completions", "/v1/chat/completions", "/v1/embeddings", "/v1/responses",
-                   "/v1/conversations", "/v1/messages", "/inference/v1/generate"}
+                   "/v1/conversations", "/v1/messages", "/inference/v1/generate",
+                   # h2c gRPC (vllmgrpc-parser): through Envoy's ext_proc or router/grpc_proxy.py
+                   "/vllm.grpc.engine.VllmEngine/Generate", "/vllm.grpc.engine.VllmEngine/Embed"}
 HOP = {"host", "content-length", "transfer-encoding", "connection", "keep-alive"}
 
 
@@ -180,8 +182,16 @@ class RouterProxy:
                 self.epp.on_response_complete(d, info)
 
 
-def _find_usage(buf: bytes) -> Optional[dict]:
-    """Usage from the tail of a JSON or SSE response (needs stream_options.include_usage)."""
+def _find_usage(buf: bytes, grpc: bool = False) -> Optional[dict]:
+    """Usage from the tail of a JSON or SSE response (needs stream_options.include_usage),
+    or from the gRPC Generate response frames (``complete`` / counted ``chunk`` tokens)."""
+    if grpc:
+        from llmd_amd.serving import vllm_grpc as vg
+
+        try:
+            return vg.usage_of_responses(vg.unframe(buf))
+        except Exception:  # noqa: BLE001 - a partial / foreign stream: no usage
+            return None
     txt = buf.decode("utf-8", errors="ignore")
     if txt.lstrip().startswith("{"):
         try:
@@ -218,6 +228,10 @@ def main(argv=None):
     p.add_argument("--ha-lease-duration", type=float, default=15.0)
     p.add_argument("--ha-renew-deadline", type=float, default=10.0)
     p.add_argument("--ha-retry-period", type=float, default=2.0)
+    p.add_argument("--grpc-port", type=int, default=0,
+                   help="also serve the vLLM gRPC engine API (h2c) through the EPP on this port")
+    p.add_argument("--grpc-upstream-port-offset", type=int, default=0,
+                   help="engine gRPC port = endpoint (HTTP) port + offset")
     p.add_argument("--v", type=int, default=1)
     a = p.parse_args(argv)
     logging.basicConfig(level=logging.DEBUG if a.v >= 3 else logging.INFO)
@@ -262,6 +276,10 @@ def main(argv=None):
         mr = web.AppRunner(mapp)
         await mr.setup()
         await web.TCPSite(mr, "0.0.0.0", a.metrics_port).start()
+        if a.grpc_port:
+            from .grpc_proxy import GrpcRouter, offset_target
+
+            await GrpcRouter(epp, offset_target(a.grpc_upstream_port_offset)).start(a.grpc_port)
         log.info("router listening on :%d (metrics :%d)", a.port, a.metrics_port)
         while True:
             await asyncio.sleep(3600)

@@ -637,11 +637,12 @@ class OpenAIServer:
             "usage": {"input_tokens": len(ids), "output_tokens": len(toks), "total_tokens": len(ids) + len(toks)}})
 
     async def messages(self, req: web.Request):
-        """Anthropic Messages API (non-streaming): system + messages with text
-        (and base64 image) blocks -> one assistant text block."""
+        """Anthropic Messages API: system + messages with text (and base64 image)
+        blocks -> one assistant text block; ``stream: true`` answers with the
+        Anthropic SSE event sequence (message_start, content_block_start,
+        content_block_delta x N, content_block_stop, message_delta, message_stop;
+        reference docs/api-reference/epp-http-apis.md:238-300)."""
         body = await req.json()
-        if body.get("stream"):
-            return _err(400, "streaming is not supported on /v1/messages; use /v1/chat/completions")
         msgs = []
         sysm = body.get("system")
         if isinstance(sysm, list):
@@ -675,6 +676,8 @@ class OpenAIServer:
             params = SamplingParams.from_openai(chat_body, vocab_size=self._vocab)
         except (ValueError, TypeError) as e:
             return _err(400, str(e))
+        if body.get("stream"):
+            return await self._stream_messages(req, body, ids, params, mm)
         toks, last = await self._run_one(req, ids, params, lora=self._lora_id(body), mm=mm)
         text = self.tok.decode(toks)
         stop_seq = None
@@ -689,6 +692,59 @@ class OpenAIServer:
                                   "content": [{"type": "text", "text": text}], "stop_reason": reason,
                                   "stop_sequence": stop_seq,
                                   "usage": {"input_tokens": len(ids), "output_tokens": len(toks)}})
+
+    async def _stream_messages(self, req, body, ids, params, mm):
+        rid = req.headers.get("x-request-id") or f"req-{uuid.uuid4().hex}"
+        mid = f"msg_{uuid.uuid4().hex}"
+        resp = web.StreamResponse(headers={"Content-Type": "text/event-stream", "Cache-Control": "no-cache"})
+        await resp.prepare(req)
+
+        async def event(name, data):
+            await resp.write(f"event: {name}\ndata: {json.dumps(data)}\n\n".encode())
+
+        await event("message_start", {"type": "message_start", "message": {
+            "id": mid, "type": "message", "role": "assistant", "model": body.get("model") or self.name,
+            "content": [], "stop_reason": None, "stop_sequence": None,
+            "usage": {"input_tokens": len(ids), "output_tokens": 0}}})
+        await event("content_block_start", {"type": "content_block_start", "index": 0,
+                                            "content_block": {"type": "text", "text": ""}})
+        await event("ping", {"type": "ping"})
+        toks: list[int] = []
+        sent, stop_seq, last = "", None, None
+        try:
+            async for o in self.aeng.generate(rid, ids, params, 0, None, self._lora_id(body), mm):
+                toks.extend(o.new_token_ids)
+                last = o
+                text = self.tok.decode(toks)
+                for s in params.stop:
+                    k = text.find(s)
+                    if k >= 0:
+                        text, stop_seq = text[:k], s
+                delta = text[len(sent):] if text.startswith(sent) else ""
+                sent = text
+                if delta:
+                    await event("content_block_delta", {"type": "content_block_delta", "index": 0,
+                                                        "delta": {"type": "text_delta", "text": delta}})
+                if stop_seq is not None:
+                    self.aeng.abort(rid)
+                    break
+        except (ConnectionResetError, asyncio.CancelledError):
+            self.aeng.abort(rid)
+            raise
+        except Exception as e:  # noqa: BLE001
+            self.aeng.abort(rid)
+            await event("error", {"type": "error", "error": {"type": "api_error", "message": str(e)}})
+            await resp.write_eof()
+            return resp
+        reason = "stop_sequence" if stop_seq else ("max_tokens" if last and last.finish_reason == "length"
+                                                   else "end_turn")
+        await event("content_block_stop", {"type": "content_block_stop", "index": 0})
+        await event("message_delta", {"type": "message_delta",
+                                      "delta": {"stop_reason": reason, "stop_sequence": stop_seq},
+                                      "usage": {"output_tokens": len(toks)}})
+        await event("message_stop", {"type": "message_stop"})
+        await resp.write_eof()
+        return resp
 
     async def generate_tokens(self, req: web.Request):
         """vLLM token-in / token-out generate API (`/inference/v1/generate`, the
@@ -857,6 +913,8 @@ def add_serving_args(p: argparse.ArgumentParser) -> argparse.ArgumentParser:
     for f in ("--disable-access-log-for-endpoints", "--uvicorn-access-log-exclude-prefixes"):
         p.add_argument(f, default=None, help=argparse.SUPPRESS)
     p.add_argument("--disable-uvicorn-access-log", action="store_true", help=argparse.SUPPRESS)
+    p.add_argument("--grpc-port", type=int, default=0,
+                   help="also serve the vLLM gRPC engine API (vllm.grpc.engine.VllmEngine) on this port (h2c)")
     return p
 
 
@@ -967,6 +1025,19 @@ def main(argv=None):
         srv.aeng.shutdown()
 
     app.on_shutdown.append(on_shutdown)
+    if a.grpc_port:
+        from . import vllm_grpc
+
+        grpc_box = {}
+
+        async def grpc_start(_app):
+            grpc_box["s"], _ = await vllm_grpc.start_server(srv, a.grpc_port, a.host)
+
+        async def grpc_stop(_app):
+            if "s" in grpc_box:
+                await grpc_box["s"].stop(grace=1.0)
+        app.on_startup.append(grpc_start)
+        app.on_shutdown.insert(0, grpc_stop)
     # keep-alive must exceed the sidecar's 90 s idle timeout (VLLM_HTTP_TIMEOUT_KEEP_ALIVE=120)
     keepalive = float(os.environ.get("VLLM_HTTP_TIMEOUT_KEEP_ALIVE", "120"))
     web.run_app(app, host=a.host, port=port, keepalive_timeout=keepalive, access_log=None,

@@ -146,3 +146,45 @@ def test_out_of_vocab_token_ids_rejected_engine_survives():
     assert "out of vocabulary" in out["comp"][1]["error"]["message"]
     assert out["ok"][0] == 200 and out["ok"][1]["usage"]["completion_tokens"] == 2
     assert dead is None
+
+
+def test_messages_streaming_event_sequence():
+    """Anthropic /v1/messages with stream=true: message_start, content_block_start,
+    deltas, content_block_stop, message_delta (stop_reason, usage), message_stop;
+    the concatenated deltas equal the non-streaming answer."""
+    body = {"model": "tiny-llama", "max_tokens": 6, "temperature": 0, "system": "s",
+            "messages": [{"role": "user", "content": "hello there"}]}
+
+    async def main():
+        eng = build_server(_cfg())
+        r1, p1 = await _serve(eng.app())
+        base = f"http://127.0.0.1:{p1}/v1/messages"
+        try:
+            async with aiohttp.ClientSession() as s:
+                async with s.post(base, json=body) as r:
+                    full = await r.json()
+                async with s.post(base, json=dict(body, stream=True)) as r:
+                    ctype = r.headers.get("Content-Type", "")
+                    raw = await r.text()
+        finally:
+            await r1.cleanup()
+            eng.aeng.shutdown()
+        return full, ctype, raw
+
+    import json
+
+    full, ctype, raw = asyncio.run(main())
+    assert ctype.startswith("text/event-stream")
+    events = []
+    for block in raw.strip().split("\n\n"):
+        lines = dict(l.split(": ", 1) for l in block.splitlines() if ": " in l)
+        events.append((lines["event"], json.loads(lines["data"])))
+    names = [e for e, _ in events]
+    assert names[0] == "message_start" and names[1] == "content_block_start"
+    assert names[-3:] == ["content_block_stop", "message_delta", "message_stop"]
+    text = "".join(d["delta"]["text"] for e, d in events if e == "content_block_delta")
+    assert text == full["content"][0]["text"]
+    md = dict(events)["message_delta"]
+    assert md["delta"]["stop_reason"] == full["stop_reason"] == "max_tokens"
+    assert md["usage"]["output_tokens"] == full["usage"]["output_tokens"] == 6
+    assert dict(events)["message_start"]["message"]["usage"]["input_tokens"] == full["usage"]["input_tokens"]
