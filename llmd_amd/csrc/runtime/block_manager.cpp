@@ -9,6 +9,14 @@
 //   * every store / eviction / reset emits an event (BlockStored with parent
 //     hash + tokens, BlockRemoved, AllBlocksCleared) drained by the publisher;
 //   * evicted blocks are reported so an offload tier can save them first.
+// Sliding-window groups (engine/hybrid_kv.py, the hybrid KV-cache manager):
+//   * `reserved` leading blocks are never handed out; block 0 then serves as
+//     the null block that replaces released table entries;
+//   * release_before() drops a sequence's blocks that lie entirely before the
+//     first key any future query can attend (they stay cached / evictable);
+//   * acquire_window() takes a cached prefix whose LAST window of blocks is
+//     resident (earlier entries are null): a windowed layer never reads older
+//     keys, so they need not be cached.
 // Single-threaded by design: the engine scheduler owns it.
 #include <pybind11/numpy.h>
 #include <pybind11/pybind11.h>
@@ -41,6 +49,7 @@ struct Seq {
   int32_t committed = 0;  // number of leading blocks already hashed/registered
   uint64_t last_hash = kRootHash;
   uint64_t extra = 0;
+  int32_t released = 0;   // leading entries replaced by the null block
 };
 
 struct Event {
@@ -53,18 +62,20 @@ struct Event {
 
 class BlockManager {
  public:
-  BlockManager(int num_blocks, int block_size, bool prefix_caching, bool emit_events)
-      : bs_(block_size), caching_(prefix_caching), events_on_(emit_events), blocks_(num_blocks) {
-    if (num_blocks <= 0 || block_size <= 0) throw std::invalid_argument("bad pool");
+  BlockManager(int num_blocks, int block_size, bool prefix_caching, bool emit_events, int reserved = 0)
+      : bs_(block_size), caching_(prefix_caching), events_on_(emit_events), reserved_(reserved),
+        blocks_(num_blocks) {
+    if (num_blocks <= reserved || block_size <= 0 || reserved < 0) throw std::invalid_argument("bad pool");
     free_.reserve(num_blocks);
-    for (int i = num_blocks - 1; i >= 0; --i) free_.push_back(i);
+    for (int i = num_blocks - 1; i >= reserved; --i) free_.push_back(i);
+    for (int i = 0; i < reserved; ++i) blocks_[i].ref = 1;  // pinned forever
   }
 
   int block_size() const { return bs_; }
-  int num_blocks() const { return (int)blocks_.size(); }
+  int num_blocks() const { return (int)blocks_.size() - reserved_; }
   int num_free() const { return (int)(free_.size() + lru_.size()); }
   int num_cached() const { return (int)cache_.size(); }
-  double usage() const { return 1.0 - (double)num_free() / (double)blocks_.size(); }
+  double usage() const { return 1.0 - (double)num_free() / (double)num_blocks(); }
 
   // Number of leading prompt tokens already in the cache (multiple of bs).
   // Never matches the whole prompt: at least one token must be computed.
@@ -84,9 +95,10 @@ class BlockManager {
     return hit;
   }
 
-  // Register a new sequence and take references on its cached prefix blocks.
+  // Register a new sequence and take references on its cached prefix blocks
+  // (at most max_tokens of them when max_tokens >= 0).
   int acquire(int64_t seq_id, py::array_t<int32_t, py::array::c_style | py::array::forcecast> toks,
-              uint64_t extra) {
+              uint64_t extra, int max_tokens = -1) {
     if (seqs_.count(seq_id)) throw std::runtime_error("acquire: sequence exists");
     Seq s;
     s.extra = extra;
@@ -94,7 +106,7 @@ class BlockManager {
     const int32_t* p = toks.data();
     if (caching_) {
       uint64_t h = kRootHash;
-      for (int b = 0; (b + 1) * bs_ <= n - 1; ++b) {
+      for (int b = 0; (b + 1) * bs_ <= n - 1 && (max_tokens < 0 || (b + 1) * bs_ <= max_tokens); ++b) {
         const uint64_t nh = hash_block(h, extra, p + b * bs_, bs_);
         auto it = cache_.find(nh);
         if (it == cache_.end()) break;
@@ -110,6 +122,74 @@ class BlockManager {
     const int hit = (int)s.blocks.size() * bs_;
     seqs_.emplace(seq_id, std::move(s));
     return hit;
+  }
+
+  // Windowed group: the longest cached prefix of at most max_tokens tokens
+  // (multiple of bs) whose blocks [lo, k) are all cached, lo = first block a
+  // query at position k*bs can reach with a `window`-token window; entries
+  // before lo become the null block (block 0, requires reserved >= 1).
+  int acquire_window(int64_t seq_id, py::array_t<int32_t, py::array::c_style | py::array::forcecast> toks,
+                     uint64_t extra, int max_tokens, int window) {
+    if (seqs_.count(seq_id)) throw std::runtime_error("acquire_window: sequence exists");
+    if (reserved_ < 1) throw std::runtime_error("acquire_window needs a reserved null block");
+    Seq s;
+    s.extra = extra;
+    const int n = (int)toks.shape(0);
+    const int32_t* p = toks.data();
+    int best = 0;
+    std::vector<uint64_t> hs;
+    if (caching_) {
+      uint64_t h = kRootHash;
+      for (int b = 0; (b + 1) * bs_ <= n - 1 && (b + 1) * bs_ <= max_tokens; ++b) {
+        h = hash_block(h, extra, p + b * bs_, bs_);
+        hs.push_back(h);
+      }
+      // candidate k from the longest down: blocks [lo(k), k) must be cached
+      for (int k = (int)hs.size(); k > 0; --k) {
+        const int lo = std::max(0, (k * bs_ - window + 1) / bs_);
+        bool ok = true;
+        for (int b = lo; b < k && ok; ++b) ok = cache_.count(hs[b]) > 0;
+        if (ok) {
+          best = k;
+          break;
+        }
+      }
+      if (best > 0) {
+        const int lo = std::max(0, (best * bs_ - window + 1) / bs_);
+        for (int b = 0; b < lo; ++b) s.blocks.push_back(0);
+        for (int b = lo; b < best; ++b) {
+          const int32_t blk = cache_.find(hs[b])->second;
+          take_ref(blk);
+          s.blocks.push_back(blk);
+        }
+        s.released = lo;
+        s.committed = best;
+        s.last_hash = hs[best - 1];
+      }
+      hits_ += (int64_t)best * bs_;
+    }
+    queries_ += n;
+    seqs_.emplace(seq_id, std::move(s));
+    return best * bs_;
+  }
+
+  // Release every block of the sequence that lies entirely before token
+  // position `first_needed` (never attended again by a windowed layer); the
+  // table entries become the null block. Returns the number released.
+  int release_before(int64_t seq_id, int first_needed) {
+    if (reserved_ < 1) throw std::runtime_error("release_before needs a reserved null block");
+    Seq& s = get(seq_id);
+    const int upto = std::min<int>((int)s.blocks.size(), std::max(0, first_needed) / bs_);
+    int n = 0;
+    for (int b = s.released; b < upto; ++b) {
+      if (s.blocks[b] != 0) {
+        drop_ref(s.blocks[b]);
+        s.blocks[b] = 0;
+        ++n;
+      }
+    }
+    s.released = std::max(s.released, upto);
+    return n;
   }
 
   // Can `extra_blocks` more blocks be obtained right now?
@@ -138,6 +218,11 @@ class BlockManager {
       const uint64_t h = hash_block(s.last_hash, s.extra, p + b * bs_, bs_);
       const int32_t blk = s.blocks[b];
       auto it = cache_.find(h);
+      if (blk < reserved_) {  // a released (null) entry: keep the hash chain, register nothing
+        s.last_hash = h;
+        s.committed = b + 1;
+        continue;
+      }
       if (it == cache_.end()) {
         Block& B = blocks_[blk];
         B.hash = h;
@@ -155,7 +240,9 @@ class BlockManager {
     auto it = seqs_.find(seq_id);
     if (it == seqs_.end()) return;
     // release in reverse so the tail of a prefix is evicted before its head
-    for (auto b = it->second.blocks.rbegin(); b != it->second.blocks.rend(); ++b) drop_ref(*b);
+    const int rel = it->second.released;
+    const auto& bl = it->second.blocks;
+    for (int b = (int)bl.size() - 1; b >= rel; --b) drop_ref(bl[b]);
     seqs_.erase(it);
   }
 
@@ -240,9 +327,9 @@ class BlockManager {
   // `commit` (its committed index still points before them).
   void check_invariants() const {
     int refd = 0;
-    for (size_t i = 0; i < blocks_.size(); ++i)
+    for (size_t i = (size_t)reserved_; i < blocks_.size(); ++i)
       if (blocks_[i].ref > 0) ++refd;
-    if ((size_t)(refd + free_.size() + lru_.size()) != blocks_.size())
+    if ((size_t)(refd + free_.size() + lru_.size() + reserved_) != blocks_.size())
       throw std::runtime_error("block conservation violated");
   }
 
@@ -298,6 +385,7 @@ class BlockManager {
 
   int bs_;
   bool caching_, events_on_;
+  int reserved_ = 0;
   std::vector<Block> blocks_;
   std::vector<int32_t> free_;
   std::list<int32_t> lru_;
@@ -334,15 +422,18 @@ void register_block_manager(py::module_& m) {
   m.def("hash_blocks", &py_hash_blocks, py::arg("tokens"), py::arg("block_size"),
         py::arg("extra") = 0, "chained keys of every full block of a token sequence");
   py::class_<BlockManager>(m, "BlockManager")
-      .def(py::init<int, int, bool, bool>(), py::arg("num_blocks"), py::arg("block_size"),
-           py::arg("prefix_caching") = true, py::arg("emit_events") = false)
+      .def(py::init<int, int, bool, bool, int>(), py::arg("num_blocks"), py::arg("block_size"),
+           py::arg("prefix_caching") = true, py::arg("emit_events") = false, py::arg("reserved") = 0)
       .def_property_readonly("block_size", &BlockManager::block_size)
       .def_property_readonly("num_blocks", &BlockManager::num_blocks)
       .def("num_free", &BlockManager::num_free)
       .def("num_cached", &BlockManager::num_cached)
       .def("usage", &BlockManager::usage)
       .def("lookup", &BlockManager::lookup)
-      .def("acquire", &BlockManager::acquire)
+      .def("acquire", &BlockManager::acquire, py::arg("seq_id"), py::arg("tokens"), py::arg("extra"),
+           py::arg("max_tokens") = -1)
+      .def("acquire_window", &BlockManager::acquire_window)
+      .def("release_before", &BlockManager::release_before)
       .def("can_allocate", &BlockManager::can_allocate)
       .def("grow", &BlockManager::grow)
       .def("commit", &BlockManager::commit)

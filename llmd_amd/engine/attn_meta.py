@@ -46,6 +46,9 @@ class AttnMeta:
     # multimodal: step rows that are image placeholders and their embeddings
     mm_rows: Optional[torch.Tensor] = None         # [n] int64
     mm_embeds: Optional[torch.Tensor] = None       # [n, d_model]
+    # hybrid KV cache (engine/hybrid_kv.py): the windowed layers' own slot mapping and
+    # block tables (everything else shared), or None
+    swa: Optional["AttnMeta"] = None
 
     @property
     def has_prefill(self) -> bool:

@@ -295,6 +295,10 @@ class CacheConfig:
     # decode attention reads a prefix shared by several running sequences once
     # per group (ops.shared_prefix_plan; needs prefix caching to share blocks)
     shared_prefix_decode: bool = True
+    # hybrid KV-cache manager (engine/hybrid_kv.py): None = on for models with sliding-window
+    # layers unless a KV connector needs whole-model blocks; False = off
+    # (--disable-hybrid-kv-cache-manager); True = requested (--no-disable-hybrid-kv-cache-manager)
+    hybrid_kv_cache_manager: Optional[bool] = None
 
     def __post_init__(self):
         # the attention kernels index blocks with shifts/masks
@@ -451,9 +455,12 @@ def add_engine_args(p: argparse.ArgumentParser) -> argparse.ArgumentParser:
     # accepted for command-line compatibility; no effect on this engine
     for f in ("--trust-remote-code", "--enable-cumem-allocator", "--enable-ep-weight-filter",
               "--enable-prefiller-sampling", "--async-scheduling", "--no-async-scheduling",
-              "--disable-hybrid-kv-cache-manager", "--no-disable-hybrid-kv-cache-manager",
               "--data-parallel-hybrid-lb", "--data-parallel-multi-port-external-lb"):
         p.add_argument(f, action="store_true", help=argparse.SUPPRESS)
+    p.add_argument("--disable-hybrid-kv-cache-manager", action="store_true",
+                   help="every layer keeps full-length KV (no separate sliding-window pool)")
+    p.add_argument("--no-disable-hybrid-kv-cache-manager", action="store_true",
+                   help="request the hybrid KV-cache manager (sliding-window layers in their own pool)")
     for f in ("--tokenizer-mode", "--attention-backend", "--moe-backend", "--data-parallel-address",
               "--data-parallel-rpc-port", "--data-parallel-supervisor-port"):
         p.add_argument(f, default=None, help=argparse.SUPPRESS)
@@ -506,6 +513,8 @@ def engine_config_from_args(a) -> EngineConfig:
         kv_cache_memory_bytes=a.kv_cache_memory_bytes, num_gpu_blocks=a.num_gpu_blocks_override,
         enable_prefix_caching=not a.no_enable_prefix_caching, max_num_seqs=a.max_num_seqs,
         shared_prefix_decode=not getattr(a, "disable_shared_prefix_decode", False),
+        hybrid_kv_cache_manager=(False if getattr(a, "disable_hybrid_kv_cache_manager", False) else
+                                 True if getattr(a, "no_disable_hybrid_kv_cache_manager", False) else None),
         max_num_batched_tokens=a.max_num_batched_tokens, max_model_len=a.max_model_len,
         tensor_parallel_size=a.tensor_parallel_size, data_parallel_size=a.data_parallel_size,
         data_parallel_rank=a.data_parallel_rank, enable_expert_parallel=a.enable_expert_parallel,

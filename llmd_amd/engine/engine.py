@@ -45,8 +45,14 @@ class LLMEngine:
         nb = self.runner.profile_and_allocate() if self.runner.kv is None else self.runner.num_blocks
         rt = _rt_loader.rt()
         ev_on = bool(cfg.kv_events_config and cfg.kv_events_config.get("enable_kv_cache_events"))
-        self.bm = rt.BlockManager(nb, cfg.cache.block_size, cfg.cache.enable_prefix_caching,
-                                  ev_on or bool(cfg.kv_offload_config))
+        if self.runner.hybrid:
+            from .hybrid_kv import HybridBlockManager
+
+            self.bm = HybridBlockManager(rt, nb, self.runner.num_swa_blocks, cfg.cache.block_size,
+                                         self.runner.max_window, cfg.cache.enable_prefix_caching, ev_on)
+        else:
+            self.bm = rt.BlockManager(nb, cfg.cache.block_size, cfg.cache.enable_prefix_caching,
+                                      ev_on or bool(cfg.kv_offload_config))
         self.connector = None
         if cfg.kv_transfer_config:
             from llmd_amd.kvx.connector import make_connector
@@ -109,7 +115,12 @@ class LLMEngine:
         return self.sched.has_work()
 
     def block_tables(self, so: SchedulerOutput) -> dict[int, list[int]]:
-        return {sr.req.seq_id: self.bm.block_table(sr.req.seq_id) for sr in so.all()}
+        full = {sr.req.seq_id: self.bm.block_table(sr.req.seq_id) for sr in so.all()}
+        if self.runner.hybrid:
+            from .hybrid_kv import HybridTables
+
+            return HybridTables(full, {sr.req.seq_id: self.bm.block_table_swa(sr.req.seq_id) for sr in so.all()})
+        return full
 
     def step(self) -> list[RequestOutput]:
         # asleep, or woken from level 2 with the trainer's weights not yet sent:

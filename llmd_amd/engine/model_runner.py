@@ -9,6 +9,11 @@ decode kernel 5-11 % (203-208 vs 219-227 us per 70B layer at batch 64 ctx
 sit 20 MB apart across a 100+ GB range. Transfers instead move a block as 2 L
 per-layer segments (kvx copy kernel segment lists, offload gathers).
 
+Hybrid KV cache (engine/hybrid_kv.py; models with sliding-window layers):
+the full-attention layers keep ``kv`` ([L_full, num_blocks, ...]) and the
+windowed layers get their own small pool ``kv_swa`` ([L_swa, num_swa_blocks,
+...]) with separate block tables and slot mappings (``AttnMeta.swa``).
+
 Decode-only steps replay a captured hipGraph per batch bucket:
 all inputs live in static device buffers, padded rows have ``slot = -1`` and
 ``seq_len = 1`` so they neither write the cache nor read past it. Mixed
@@ -16,6 +21,7 @@ steps (chunked prefill + decodes) run eagerly.
 """
 from __future__ import annotations
 
+import dataclasses
 import logging
 import math
 import os
@@ -119,6 +125,15 @@ class ModelRunner:
         self.lora = None  # engine/lora.py LoRAManager (set by the engine / TP follower)
         self.kv = None
         self.num_blocks = 0
+        # hybrid KV cache: windowed layers in their own pool (engine/hybrid_kv.py)
+        self.swa_layers = [i for i, a in enumerate(attn) if getattr(a, "window", 0)]
+        self.full_layers = [i for i in range(self.L) if i not in set(self.swa_layers)]
+        self.hybrid = self._want_hybrid()
+        self.kv_swa = None
+        self.num_swa_blocks = 0
+        if self.hybrid:
+            log.info("hybrid KV cache: %d full-attention layers, %d window-%d layers in their own pool",
+                     len(self.full_layers), len(self.swa_layers), self.max_window)
         self.graphs: dict[int, tuple] = {}
         self.dbo_graphs: dict[int, tuple] = {}  # bucket -> (graph, logits) of two B/2 micro-batches
         self._rng = np.random.default_rng(cfg.seed)
@@ -170,9 +185,40 @@ class ModelRunner:
                       topk=self.mc.num_experts_per_tok, micro_batches=2 if pc.enable_dbo else 1)
 
     # ------------------------------------------------------------ KV cache
-    def block_bytes(self) -> int:
+    def _want_hybrid(self) -> bool:
+        """Hybrid manager: on by default for models mixing windowed and full layers
+        (vLLM's default); off with --disable-hybrid-kv-cache-manager, and when a KV
+        transfer / offload connector needs whole-model blocks."""
+        flag = self.cfg.cache.hybrid_kv_cache_manager
+        if not self.swa_layers or not self.full_layers or self.is_mla or flag is False:
+            return False
+        if self.cfg.parallel.enable_dbo:
+            return False  # dual-batch graphs carry one set of tables
+        if self.cfg.kv_transfer_config or self.cfg.kv_offload_config:
+            if flag:
+                log.warning("hybrid KV cache manager not available with a KV transfer / offload connector: "
+                            "every layer keeps full-length KV")
+            return False
+        return True
+
+    def layer_bytes_per_block(self) -> int:
         planes, heads, dim = self.kv_spec
-        return self.L * planes * heads * self.bs * dim * torch.empty(0, dtype=self.kv_dtype).element_size()
+        return planes * heads * self.bs * dim * torch.empty(0, dtype=self.kv_dtype).element_size()
+
+    def block_bytes(self) -> int:
+        """Bytes of one block of the main pool (all layers, or the full-attention
+        layers of a hybrid cache)."""
+        n = len(self.full_layers) if self.hybrid else self.L
+        return n * self.layer_bytes_per_block()
+
+    def swa_block_bytes(self) -> int:
+        return len(self.swa_layers) * self.layer_bytes_per_block()
+
+    def _swa_pool_blocks(self) -> int:
+        from .hybrid_kv import swa_blocks
+
+        sc = self.cfg.sched
+        return swa_blocks(sc.max_num_seqs, sc.max_num_batched_tokens, self.max_window, self.bs)
 
     def _wants_vmm(self) -> bool:
         """KV producers export their pool to other processes (kvx); a single
@@ -184,7 +230,10 @@ class ModelRunner:
 
     def _alloc_cache(self, num_blocks: int, scratch: bool = False) -> torch.Tensor:
         planes, heads, dim = self.kv_spec
-        shape = (self.L, num_blocks, planes, heads, self.bs, dim)
+        shape = (len(self.full_layers) if self.hybrid else self.L, num_blocks, planes, heads, self.bs, dim)
+        if self.hybrid:
+            self.kv_swa = torch.zeros((len(self.swa_layers), num_blocks if scratch else self.num_swa_blocks,
+                                       planes, heads, self.bs, dim), dtype=self.kv_dtype, device=self.device)
         self.vmm = None
         if not scratch and self._wants_vmm():
             C = ops.native()
@@ -202,12 +251,20 @@ class ModelRunner:
         return kv
 
     def _bind(self, kv: Optional[torch.Tensor]):
+        if kv is None:
+            self.kv_swa = None
+        slot = {}
+        if self.hybrid:
+            slot.update({li: ("full", j) for j, li in enumerate(self.full_layers)})
+            slot.update({li: ("swa", j) for j, li in enumerate(self.swa_layers)})
         for i, a in enumerate(self.model.attention_layers()):
+            pool, j = slot.get(i, ("full", i))
+            src = kv if pool == "full" else self.kv_swa
             if hasattr(a, "bind_cache"):
-                a.bind_cache(kv[i]) if kv is not None else setattr(a, "cache", None)
+                a.bind_cache(src[j]) if src is not None else setattr(a, "cache", None)
             else:
-                a.k_cache = kv[i, :, 0] if kv is not None else None
-                a.v_cache = kv[i, :, 1] if kv is not None else None
+                a.k_cache = src[j, :, 0] if src is not None else None
+                a.v_cache = src[j, :, 1] if src is not None else None
 
     def _mla_rows(self, meta: AttnMeta, nd: int, p_ql, p_ctx):
         """Row metadata of the latent-attention kernel (decode rows + one row per
@@ -231,7 +288,10 @@ class ModelRunner:
         if cc.num_gpu_blocks:
             nb = cc.num_gpu_blocks
         elif not self.is_gpu:
-            nb = max(64, (cc.kv_cache_memory_bytes or (256 << 20)) // self.block_bytes())
+            budget = cc.kv_cache_memory_bytes or (256 << 20)
+            if self.hybrid:
+                budget -= self._swa_pool_blocks() * self.swa_block_bytes()
+            nb = max(64, budget // self.block_bytes())
         else:
             # dummy max-size step on a scratch cache to measure activation peak
             T = self.cfg.sched.max_num_batched_tokens
@@ -252,12 +312,19 @@ class ModelRunner:
             else:
                 used = total - free
                 budget = int(total * cc.gpu_memory_utilization) - used - act_peak - (2 << 30)
+            if self.hybrid:  # the windowed pool first, the full-attention layers get the rest
+                self.num_swa_blocks = self._swa_pool_blocks()
+                budget -= self.num_swa_blocks * self.swa_block_bytes()
             nb = max(16, budget // self.block_bytes())
             log.info("kv cache: %d blocks x %d tokens (%.1f GiB), activation peak %.2f GiB",
                      nb, self.bs, nb * self.block_bytes() / 2**30, act_peak / 2**30)
         if self.tp_size > 1:
             nb = tp_min_int(int(nb))  # every TP rank must hold the same block pool
         self.num_blocks = int(nb)
+        if self.hybrid:
+            self.num_swa_blocks = self._swa_pool_blocks()
+            log.info("hybrid KV cache: %d full-layer blocks (%d tokens of context) + %d windowed blocks",
+                     self.num_blocks, self.num_blocks * self.bs, self.num_swa_blocks)
         self.kv = self._alloc_cache(self.num_blocks)
         return self.num_blocks
 
@@ -323,6 +390,26 @@ class ModelRunner:
             p_ql.append(sr.num_new_tokens)
             p_ctx.append(sr.start + sr.num_new_tokens)
         return ids, pos, slots, d_bt, d_len, p_ql, p_ctx, p_bt
+
+    def _group_tables(self, so: SchedulerOutput, tables: dict):
+        """Slot mapping and block tables of one KV group (the windowed pool of a
+        hybrid cache): same token layout as _prepare."""
+        bs = self.bs
+        slots = []
+        d_bt = np.zeros((len(so.decodes), self.width), dtype=np.int32)
+        for i, sr in enumerate(so.decodes):
+            bt = tables[sr.req.seq_id]
+            p = sr.start
+            slots.append(bt[p // bs] * bs + p % bs)
+            d_bt[i, : len(bt)] = bt
+        p_bt = np.zeros((len(so.prefills), self.width), dtype=np.int32)
+        for i, sr in enumerate(so.prefills):
+            bt = tables[sr.req.seq_id]
+            ps = np.arange(sr.start, sr.start + sr.num_new_tokens)
+            bta = np.asarray(bt, dtype=np.int64)
+            slots.extend((bta[ps // bs] * bs + ps % bs).tolist())
+            p_bt[i, : len(bt)] = bt
+        return slots, d_bt, p_bt
 
     def _sample_rows(self, so: SchedulerOutput):
         """Rows (token index) that produce a sampled token, and their requests."""
@@ -399,6 +486,8 @@ class ModelRunner:
         graph = not so.prefills and self._graph_ok(len(so.decodes))
         pl = {"graph": graph, "nd": len(so.decodes), "ids": ids, "pos": pos, "slots": slots, "d_bt": d_bt,
               "d_len": d_len, "p_ql": p_ql, "p_ctx": p_ctx, "p_bt": p_bt, "rows": rows}
+        if self.hybrid:
+            pl["swa"] = self._group_tables(so, block_tables.swa)
         if self.lora is not None:
             lo = [sr.req.lora_id for sr in so.decodes]
             for sr in so.prefills:
@@ -531,7 +620,8 @@ class ModelRunner:
         dev = self.device
         nd = pl["nd"]
         T = len(ids)
-        host = torch.tensor([ids, pos, slots], dtype=torch.long)
+        swa = pl.get("swa")
+        host = torch.tensor([ids, pos, slots] + ([swa[0]] if swa is not None else []), dtype=torch.long)
         if self.is_gpu:
             host = host.pin_memory()
         hd = host.to(dev, non_blocking=True)
@@ -561,6 +651,11 @@ class ModelRunner:
             rows, embs = pl["mm"]
             meta.mm_rows = torch.tensor(rows, dtype=torch.long).to(dev, non_blocking=True)
             meta.mm_embeds = embs.to(dev)
+        if swa is not None:  # windowed layers: their own pool's slots and block tables
+            meta.swa = dataclasses.replace(
+                meta, slot_mapping=hd[3], d_cascade=None,
+                d_block_tables=torch.from_numpy(swa[1]).to(dev, non_blocking=True) if nd else None,
+                p_block_tables=torch.from_numpy(swa[2]).to(dev, non_blocking=True) if p_ql else None)
         return hd[0], meta
 
     def _cascade_plan(self, d_bt, d_len, max_work=None):
@@ -712,6 +807,9 @@ class ModelRunner:
         self.g_slots = torch.full((M,), -1, dtype=torch.long, device=dev)
         self.g_bt = torch.zeros(M, self.width, dtype=torch.int32, device=dev)
         self.g_len = torch.ones(M, dtype=torch.int32, device=dev)
+        if self.hybrid:  # the windowed pool's slots / tables (block 0 = null block)
+            self.g_slots_swa = torch.full((M,), -1, dtype=torch.long, device=dev)
+            self.g_bt_swa = torch.zeros(M, self.width, dtype=torch.int32, device=dev)
         self.g_ws = (torch.empty(ws_rows * self.Hq * self.D, dtype=torch.float32, device=dev),
                      torch.empty(ws_rows * self.Hq * 2, dtype=torch.float32, device=dev))
         if self.is_mla:  # fixed per-bucket latent-attention split plans + one shared workspace
@@ -729,6 +827,9 @@ class ModelRunner:
                             num_decode=B, d_block_tables=self.g_bt[:B], d_seq_lens=self.g_len[:B],
                             d_split=self.graph_plans[B], d_workspace=self.g_ws, d_max_ctx=self.max_model_len,
                             d_split_dev=self.g_split)
+            if self.hybrid:
+                meta.swa = dataclasses.replace(meta, slot_mapping=self.g_slots_swa[:B],
+                                               d_block_tables=self.g_bt_swa[:B])
             if self.is_mla:
                 meta.mla_d_rows, meta.mla_split, meta.mla_workspace = self.g_rows[:B], self.mla_plans[B], self.g_mla_ws
                 self.g_mla_split.fill_(self.mla_plans[B][0])
@@ -748,6 +849,8 @@ class ModelRunner:
             if self.cascade_ok and B >= 2:
                 # variant with the shared-prefix kernel (all-padding work units while capturing)
                 meta.d_cascade = (self.g_casc[:3 * B + 5 * self.casc_work], self.casc_variant, self.casc_slots)
+                if self.hybrid:
+                    meta.swa = dataclasses.replace(meta.swa, d_cascade=None)
                 with torch.cuda.stream(s):
                     self.model(self.g_ids[:B], meta)
                 torch.cuda.current_stream().wait_stream(s)
@@ -900,6 +1003,13 @@ class ModelRunner:
         self.g_slots[:B].copy_(host[2], non_blocking=True)
         self.g_bt[:B].copy_(torch.from_numpy(d_bt).pin_memory(), non_blocking=True)
         self.g_len[:B].copy_(torch.from_numpy(d_len).pin_memory(), non_blocking=True)
+        if self.hybrid:
+            s_slots, s_bt, _ = pl.get("swa") or ([], np.zeros((0, self.width), np.int32), None)
+            if B > n:
+                s_slots = list(s_slots) + [-1] * (B - n)
+                s_bt = np.concatenate([s_bt, np.zeros((B - n, self.width), dtype=np.int32)])
+            self.g_slots_swa[:B].copy_(torch.tensor(s_slots, dtype=torch.long).pin_memory(), non_blocking=True)
+            self.g_bt_swa[:B].copy_(torch.from_numpy(s_bt).pin_memory(), non_blocking=True)
         longest = int(d_len.max())
         if B in self.cgraphs:
             plan = self._cascade_plan(d_bt, d_len, max_work=self.casc_work)

@@ -137,6 +137,7 @@ class Scheduler:
         self.eos = set(cfg.model_config.eos_ids)
         self.num_preemptions_total = 0
         self.errored: list[Request] = []  # finished by the scheduler itself (not via update)
+        self._window_release = hasattr(block_manager, "after_compute")
         self._tok_arrays: dict[str, np.ndarray] = {}
 
     # ------------------------------------------------------------ admission
@@ -396,6 +397,9 @@ class Scheduler:
             if (self.cfg.cache.enable_prefix_caching and r.num_computed_tokens // bs > sr.start // bs
                     and self.bm.has_seq(r.seq_id)):
                 self.bm.commit(r.seq_id, self._tokens(r), r.num_computed_tokens)
+            if self._window_release and self.bm.has_seq(r.seq_id):
+                # hybrid KV cache: windowed blocks no future query can reach go back to the pool
+                self.bm.after_compute(r.seq_id, r.num_computed_tokens)
             if r.seq_id in sampled:
                 tok, lp = sampled[r.seq_id]
                 r.output_token_ids.append(tok)

@@ -216,6 +216,8 @@ class PagedAttention(torch.nn.Module):
     def forward(self, qkv: torch.Tensor, meta: AttnMeta) -> torch.Tensor:
         T = qkv.shape[0]
         Hq, Hkv, D = self.Hq, self.Hkv, self.D
+        if self.window and meta.swa is not None:  # hybrid KV cache: this layer's pool has its own tables
+            meta = meta.swa
         ops.rope_cache(qkv, meta.positions, self.cos_sin, Hq, Hkv, D, meta.slot_mapping,
                        self.k_cache, self.v_cache, self.neox, self.k_scale, self.v_scale)
         out = torch.empty(T, Hq * D, dtype=qkv.dtype, device=qkv.device)
