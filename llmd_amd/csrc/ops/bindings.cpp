@@ -98,7 +98,7 @@ int llmd_symm_clear_error(void*);
 int llmd_symm_all_reduce(const int64_t*, int, int, int, int, int64_t, int64_t, const void*, void*, int64_t,
                          hipStream_t);
 int llmd_symm_ep_dispatch(const int64_t*, int, int, int, const int64_t*, const void*, int64_t, const int*,
-                          const float*, int, int, int, int, int, hipStream_t);
+                          const float*, int, int, int, int, int, int, hipStream_t);
 int llmd_symm_ep_combine(const int64_t*, int, int, int, const int64_t*, const void*, int64_t, const int*, int, int,
                          int, int, int, void*, int64_t, hipStream_t);
 }
@@ -875,11 +875,12 @@ void symm_all_reduce(std::vector<int64_t> bases, int64_t rank, int64_t ch, int64
 }
 
 void symm_ep_dispatch(std::vector<int64_t> bases, int64_t rank, int64_t ch, std::vector<int64_t> layout,
-                      torch::Tensor x, torch::Tensor ids, torch::Tensor w, int64_t R, int64_t E_local) {
+                      torch::Tensor x, torch::Tensor ids, torch::Tensor w, int64_t R, int64_t E_local, bool fp8) {
   const c10::hip::OptionalHIPGuard device_guard(dev_of(x));
   check_bases(bases, rank);
   CHECK_CUDA(x); CHECK_BF16(x); CHECK_INNER(x); CHECK_DT(ids, at::kInt); CHECK_DT(w, at::kFloat);
-  TORCH_CHECK(layout.size() == 5, "ep layout");
+  TORCH_CHECK(layout.size() == 7, "ep layout");
+  TORCH_CHECK(!fp8 || (layout[5] >= 0 && layout[6] >= 0), "ep_dispatch: heap has no fp8 receive area");
   const int T = x.size(0), d = x.size(1);
   TORCH_CHECK(ids.dim() == 2 && ids.is_contiguous() && w.sizes() == ids.sizes() && w.is_contiguous() &&
                   ids.size(0) == T, "ep_dispatch: ids/w [T, k]");
@@ -887,7 +888,7 @@ void symm_ep_dispatch(std::vector<int64_t> bases, int64_t rank, int64_t ch, std:
   TORCH_CHECK(T <= R && d % 8 == 0 && k <= 64 && x.stride(0) % 8 == 0, "ep_dispatch shape");
   int rc = llmd_symm_ep_dispatch(bases.data(), (int)bases.size(), (int)rank, (int)ch, layout.data(), x.data_ptr(),
                                  x.stride(0), ids.data_ptr<int>(), w.data_ptr<float>(), T, (int)R, d, k, (int)E_local,
-                                 cur_stream());
+                                 (int)fp8, cur_stream());
   TORCH_CHECK(rc == 0, "symm_ep_dispatch failed: ", rc);
 }
 
@@ -896,7 +897,7 @@ void symm_ep_combine(std::vector<int64_t> bases, int64_t rank, int64_t ch, std::
   const c10::hip::OptionalHIPGuard device_guard(dev_of(y));
   check_bases(bases, rank);
   CHECK_CUDA(y); CHECK_BF16(y); CHECK_BF16(out); CHECK_INNER(y); CHECK_INNER(out); CHECK_DT(ids, at::kInt);
-  TORCH_CHECK(layout.size() == 5, "ep layout");
+  TORCH_CHECK(layout.size() == 7, "ep layout");
   const int T = out.size(0), d = out.size(1);
   TORCH_CHECK(ids.dim() == 2 && ids.is_contiguous() && ids.size(0) == T, "ep_combine: ids [T, k]");
   TORCH_CHECK(y.size(0) == (int64_t)bases.size() * R && y.size(1) >= d && d % 8 == 0 && T <= R, "ep_combine shape");
@@ -963,6 +964,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {  // _C, or _C_debug (llmd_amd/build.p
   m.def("symm_grid", &llmd_symm_grid);
   m.def("symm_channels", &llmd_symm_channels);
   m.def("symm_all_reduce", &symm_all_reduce);
-  m.def("symm_ep_dispatch", &symm_ep_dispatch);
+  m.def("symm_ep_dispatch", &symm_ep_dispatch, py::arg("bases"), py::arg("rank"), py::arg("ch"), py::arg("layout"),
+        py::arg("x"), py::arg("ids"), py::arg("w"), py::arg("R"), py::arg("E_local"), py::arg("fp8") = false);
   m.def("symm_ep_combine", &symm_ep_combine);
 }

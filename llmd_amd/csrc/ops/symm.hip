@@ -201,6 +201,7 @@ __global__ __launch_bounds__(NT) void ar_twoshot_kernel(Peers P, int nranks, int
 struct EpLayout {
   int64_t rx, rid, rw, cb;  // byte offsets of the four areas (parity 0)
   int64_t par_stride;       // bytes between parity 0 and 1
+  int64_t rxq, rxs;         // fp8 dispatch: e4m3 rows [src][R][dp] + group scales [src][R][dp/128] (or -1)
 };
 
 __global__ __launch_bounds__(NT) void ep_dispatch_kernel(Peers P, int nranks, int rank, int ch, EpLayout L,
@@ -238,6 +239,71 @@ __global__ __launch_bounds__(NT) void ep_dispatch_kernel(Peers P, int nranks, in
       const u32x4_t* src = reinterpret_cast<const u32x4_t*>(x + t * xs);
       u32x4_t* dst = reinterpret_cast<u32x4_t*>(pb + L.rx + po) + ((int64_t)rank * R + t) * (d / 8);
       for (int c = ln; c < d / 8; c += 64) dst[c] = src[c];
+    }
+  }
+  block_barrier(P, nranks, rank, ch, 0, epoch);
+}
+
+// FP8 dispatch (DeepEP-LL with fp8 fused in): the same exchange, but a token
+// row travels as e4m3fn with one power-of-two (E8M0-exact) scale per 128
+// columns - quantised in registers by the sending wave, the same numerics as
+// ops.quant_fp8_groups - into rxq [src][R][dp] / rxs [src][R][dp / 128]
+// (dp = d rounded up to 128, zero padded): half the xGMI bytes of bf16, and the
+// block-fp8 grouped GEMM consumes the rows without a quantisation pass.
+__global__ __launch_bounds__(NT) void ep_dispatch_fp8_kernel(Peers P, int nranks, int rank, int ch, EpLayout L,
+                                                             const uint16_t* __restrict__ x, int64_t xs,
+                                                             const int* __restrict__ ids,
+                                                             const float* __restrict__ w, int T, int R, int d,
+                                                             int k, int E_local) {
+  const uint32_t epoch = next_epoch(P.base[rank], ch);
+  const int64_t po = (int64_t)(epoch & 1) * L.par_stride;
+  const int wv = threadIdx.x >> 6, ln = threadIdx.x & 63;
+  constexpr int NW = NT / 64;
+  const int ng = (d + 127) / 128, dp = ng * 128;
+  for (int64_t i = wv;; i += NW) {
+    const int64_t t = blockIdx.x + (int64_t)G * (i / nranks);
+    const int p = (int)(i % nranks);
+    if (t >= R) break;
+    char* pb = P.base[p];
+    const int64_t row = (int64_t)rank * R + t;
+    int* rid = reinterpret_cast<int*>(pb + L.rid + po) + row * k;
+    float* rw = reinterpret_cast<float*>(pb + L.rw + po) + row * k;
+    int lid = -1;
+    float lw = 0.f;
+    if (t < T && ln < k) {
+      const int e = ids[t * k + ln];
+      if (e >= p * E_local && e < (p + 1) * E_local) {
+        lid = e - p * E_local;
+        lw = w[t * k + ln];
+      }
+    }
+    const bool any = __any(lid >= 0);
+    if (ln < k) {
+      rid[ln] = lid;
+      rw[ln] = lw;
+    }
+    if (!any) continue;
+    const uint16_t* src = x + t * xs;
+    uint8_t* dq = reinterpret_cast<uint8_t*>(pb + L.rxq + po) + row * dp;
+    float* ds = reinterpret_cast<float*>(pb + L.rxs + po) + row * ng;
+    // 16 lanes x 8 columns per 128-column group, 4 groups per wave pass
+    for (int g0 = 0; g0 < ng; g0 += 4) {
+      const int g = g0 + (ln >> 4), c = g * 128 + (ln & 15) * 8;
+      float f[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+      if (g < ng && c < d) unpack8(*reinterpret_cast<const u32x4_t*>(src + c), f);
+      float a = 0.f;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) a = fmaxf(a, fabsf(f[j]));
+#pragma unroll
+      for (int o = 8; o > 0; o >>= 1) a = fmaxf(a, __shfl_xor(a, o, 64));
+      const float s = pow2_ceil(fmaxf(a / FP8_MAX, 1e-12f));
+      const float inv = 1.f / s;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) f[j] *= inv;
+      if (g < ng) {
+        *reinterpret_cast<u32x2_t*>(dq + c) = f32x8_to_fp8(f);
+        if ((ln & 15) == 0) ds[g] = s;
+      }
     }
   }
   block_barrier(P, nranks, rank, ch, 0, epoch);
@@ -347,9 +413,15 @@ int llmd_symm_all_reduce(const int64_t* bases, int nranks, int rank, int ch, int
 
 int llmd_symm_ep_dispatch(const int64_t* bases, int nranks, int rank, int ch, const int64_t* lay,
                           const void* x, int64_t xs, const int* ids, const float* w, int T, int R, int d, int k,
-                          int E_local, hipStream_t st) {
+                          int E_local, int fp8, hipStream_t st) {
   if (nranks < 1 || nranks > MAXR || k > 64 || d % 8) return -1;
-  EpLayout L{lay[0], lay[1], lay[2], lay[3], lay[4]};
+  EpLayout L{lay[0], lay[1], lay[2], lay[3], lay[4], lay[5], lay[6]};
+  if (fp8) {
+    if (L.rxq < 0 || L.rxs < 0) return -3;
+    hipLaunchKernelGGL(ep_dispatch_fp8_kernel, dim3(G), dim3(NT), 0, st, make_peers(bases, nranks), nranks, rank,
+                       ch, L, (const uint16_t*)x, xs, ids, w, T, R, d, k, E_local);
+    return (int)hipGetLastError();
+  }
   hipLaunchKernelGGL(ep_dispatch_kernel, dim3(G), dim3(NT), 0, st, make_peers(bases, nranks), nranks, rank, ch, L,
                      (const uint16_t*)x, xs, ids, w, T, R, d, k, E_local);
   return (int)hipGetLastError();
@@ -359,7 +431,7 @@ int llmd_symm_ep_combine(const int64_t* bases, int nranks, int rank, int ch, con
                          int64_t ys, const int* ids, int T, int R, int d, int k, int E_local, void* out, int64_t os,
                          hipStream_t st) {
   if (nranks < 1 || nranks > MAXR || k > 64 || d % 8) return -1;
-  EpLayout L{lay[0], lay[1], lay[2], lay[3], lay[4]};
+  EpLayout L{lay[0], lay[1], lay[2], lay[3], lay[4], lay[5], lay[6]};
   hipLaunchKernelGGL(ep_combine_kernel, dim3(G), dim3(NT), 0, st, make_peers(bases, nranks), nranks, rank, ch, L,
                      (const uint16_t*)y, ys, ids, T, R, d, k, E_local, (uint16_t*)out, os);
   return (int)hipGetLastError();

@@ -181,8 +181,12 @@ class ModelRunner:
         elif (ep_mod.canonical(pc.all2all_backend) == "symm_ll" and st.dp_size > 1 and st.tp_size == 1
               and self.mc.is_moe):
             rows = max(self.cfg.cuda_graph_max_bs, 256)
+            # block-fp8 experts: quantise in the dispatch kernel (DeepEP-LL use_fp8)
+            fp8 = (os.environ.get("LLMD_EP_FP8_DISPATCH", "1") == "1"
+                   and any(getattr(m, "w1_scale", None) is not None and m.w1.dtype == torch.float8_e4m3fn
+                           for m in self.model.modules()))
             symm.init(st.ep_rank, st.ep_size, group=st.cpu_group, ep_rows=rows, hidden=self.mc.hidden_size,
-                      topk=self.mc.num_experts_per_tok, micro_batches=2 if pc.enable_dbo else 1)
+                      topk=self.mc.num_experts_per_tok, micro_batches=2 if pc.enable_dbo else 1, ep_fp8=fp8)
 
     # ------------------------------------------------------------ KV cache
     def _want_hybrid(self) -> bool:

@@ -73,6 +73,8 @@ def run_experts(mod, x, ids, w, act, alpha=1.702, limit=7.0, b1=None, b2=None):
     if mod.w1.dtype == torch.float8_e4m3fn:
         return ops.moe_experts_fp8(x, ids, w, mod.w1, mod.w1_scale, mod.w2, mod.w2_scale, act, alpha, limit,
                                    b1=b1, b2=b2)
+    if isinstance(x, ops.Fp8Rows):
+        x = x.dequant()
     return ops.moe_experts(x, ids, w, mod.w1, mod.w2, act, alpha, limit, b1=b1, b2=b2)
 
 

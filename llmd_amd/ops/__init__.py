@@ -572,11 +572,39 @@ MOE_V3 = os.environ.get("LLMD_MOE_V3", "1") == "1"
 MOE_FUSED_QUANT = os.environ.get("LLMD_MOE_FUSED_QUANT", "0") == "1"
 
 
+class Fp8Rows:
+    """Activation rows already quantised to block fp8 (e4m3 ``q`` [T, dp] with
+    dp = d padded to 128 and zeros past d, fp32 group scales ``s`` [T, dp/128]):
+    what the fp8 EP dispatch kernel delivers (parallel/symm.py)."""
+
+    def __init__(self, q: torch.Tensor, s: torch.Tensor, d: int):
+        self.q, self.s, self.d = q, s, d
+
+    @property
+    def shape(self):
+        return torch.Size((self.q.shape[0], self.d))
+
+    @property
+    def device(self):
+        return self.q.device
+
+    @property
+    def is_cuda(self):
+        return self.q.is_cuda
+
+    def dequant(self) -> torch.Tensor:
+        f = self.q.float() * self.s.repeat_interleave(128, 1)[:, :self.q.shape[1]]
+        return f[:, :self.d].to(torch.bfloat16)
+
+
 def moe_experts_fp8(x, ids, wts, w1q, w1s, w2q, w2s, act=0, alpha=1.702, limit=7.0, out=None, b1=None, b2=None):
     """Block-scaled FP8 routed experts (DeepGEMM role): activations quantised per
     (token, 128) group, grouped fp8 MFMA GEMMs with 128x128 weight-block scales,
-    the gated activation fused into GEMM 1, bf16 weighted combine."""
-    if not _gpu(x):
+    the gated activation fused into GEMM 1, bf16 weighted combine. ``x`` may be
+    ``Fp8Rows`` (quantised by the EP dispatch kernel): no quantisation pass."""
+    if isinstance(x, Fp8Rows) and not (x.is_cuda and x.q.shape[1] == w1q.shape[2]):
+        x = x.dequant()
+    if not isinstance(x, Fp8Rows) and not _gpu(x):
         xq, xs = quant_fp8_groups(x)
         xd = (xq.float().view(x.shape[0], -1) * xs.repeat_interleave(128, 1)[:, :x.shape[1]]).to(torch.bfloat16)
         r = ref.moe_forward(xd, ids, wts, dequant_fp8_block_weight(w1q, w1s).to(torch.bfloat16),
@@ -605,7 +633,10 @@ def moe_experts_fp8(x, ids, wts, w1q, w1s, w2q, w2s, act=0, alpha=1.702, limit=7
     total = torch.empty(1, dtype=torch.int32, device=dev)
     inv = torch.empty(n, dtype=torch.int32, device=dev)  # moe_align fills it (-1 = not on this rank)
     C.moe_align(ids.contiguous().view(-1).to(torch.int32), E, sorted_ids, tile_e, offs, total, inv, bm)
-    xq, xs = _quant_groups_padded(x, Kp1)
+    if isinstance(x, Fp8Rows):
+        xq, xs = x.q, x.s
+    else:
+        xq, xs = _quant_groups_padded(x, Kp1)
     if MOE_FUSED_QUANT and bm == C.moe_tile_m_prefill() and Kp2 == (N1 + 255) // 256 * 128:
         # 256-row tiles: the first GEMM quantises its activation output itself (opt-in:
         # measured slower - with one workgroup per CU the epilogue's amax exchange and

@@ -17,7 +17,10 @@ host round trip, no NIC, hipGraph-capturable.
   each token row is written only to the ranks owning one of its top-k experts
   (fixed [N, R] receive layout, -1 expert rows elsewhere), the local grouped
   GEMM runs on the received rows, the weighted partial outputs are pushed
-  back and summed by the token's owner.
+  back and summed by the token's owner. With ``fp8=True`` (block-fp8 expert
+  weights) the dispatch kernel quantises each row to e4m3 + per-128 scales on
+  the way out (DeepEP-LL's fused fp8 dispatch, ``use_fp8``): half the bytes
+  over xGMI and no quantisation pass before the grouped GEMM.
 
 Handles are exchanged with ``all_gather_object`` over a gloo/cpu group, so the
 same code runs with RCCL ranks on 8 GPUs or with several processes sharing one
@@ -135,15 +138,23 @@ class SymmEP:
     """Low-latency wide-EP token exchange (DeepEP-LL role) for steps of at most
     ``max_rows`` tokens per rank; the caller falls back to RCCL beyond that."""
 
-    def __init__(self, heap: SymmHeap, max_rows: int, hidden: int, topk: int, channel: int = CH_EP):
+    def __init__(self, heap: SymmHeap, max_rows: int, hidden: int, topk: int, channel: int = CH_EP,
+                 fp8: bool = False):
         self.heap, self.ch = heap, channel
         n = heap.world
         self.R_max, self.d, self.k = max_rows, hidden, topk
+        self.fp8 = fp8
+        # fp8 dispatch: e4m3 rows padded to 128 columns + one fp32 scale per group
+        self.dp = (hidden + 127) // 128 * 128
+        self.ng = self.dp // 128
         rx = n * max_rows * hidden * 2
         rid = n * max_rows * topk * 4
         rw = rid
         cb = rx
-        per = _align(rx, 256) + _align(rid, 256) + _align(rw, 256) + _align(cb, 256)
+        rxq = n * max_rows * self.dp if fp8 else 0
+        rxs = n * max_rows * self.ng * 4 if fp8 else 0
+        per = (_align(rx, 256) + _align(rid, 256) + _align(rw, 256) + _align(cb, 256) + _align(rxq, 256)
+               + _align(rxs, 256))
         # Single-buffered: dispatch and combine barriers interlock (a peer's
         # dispatch e+1 needs our combine-e signal, issued after our expert GEMM
         # consumed the rows), so the receive views have fixed addresses and a
@@ -153,13 +164,21 @@ class SymmEP:
         o_rid = o_rx + _align(rx, 256)
         o_rw = o_rid + _align(rid, 256)
         o_cb = o_rw + _align(rw, 256)
-        self.layout = [o_rx, o_rid, o_rw, o_cb, 0]
+        o_rxq = o_cb + _align(cb, 256)
+        o_rxs = o_rxq + _align(rxq, 256)
+        self.layout = [o_rx, o_rid, o_rw, o_cb, 0, o_rxq if fp8 else -1, o_rxs if fp8 else -1]
+        if fp8:  # padding columns are never written by the kernel: zero them once
+            self.heap.heap[o_rxq:o_rxq + rxq].zero_()
 
     @staticmethod
-    def heap_bytes(world: int, max_rows: int, hidden: int, topk: int) -> int:
+    def heap_bytes(world: int, max_rows: int, hidden: int, topk: int, fp8: bool = False) -> int:
         rx = world * max_rows * hidden * 2
         rid = world * max_rows * topk * 4
-        return 2 * _align(rx, 256) + 2 * _align(rid, 256) + 4096
+        extra = 0
+        if fp8:
+            dp = (hidden + 127) // 128 * 128
+            extra = _align(world * max_rows * dp, 256) + _align(world * max_rows * (dp // 128) * 4, 256)
+        return 2 * _align(rx, 256) + 2 * _align(rid, 256) + extra + 4096
 
     def views(self, R: int):
         """Local receive views (rows of all src ranks) for a step of R rows per rank."""
@@ -169,6 +188,13 @@ class SymmEP:
         rx = h[o_rx:o_rx + n * R * self.d * 2].view(torch.bfloat16).view(n * R, self.d)
         rid = h[o_rid:o_rid + n * R * self.k * 4].view(torch.int32).view(n * R, self.k)
         rw = h[o_rw:o_rw + n * R * self.k * 4].view(torch.float32).view(n * R, self.k)
+        if self.fp8:
+            from llmd_amd.ops import Fp8Rows
+
+            o_q, o_s = self.layout[5], self.layout[6]
+            q = h[o_q:o_q + n * R * self.dp].view(torch.float8_e4m3fn).view(n * R, self.dp)
+            s = h[o_s:o_s + n * R * self.ng * 4].view(torch.float32).view(n * R, self.ng)
+            rx = Fp8Rows(q, s, self.d)
         return rx, rid, rw
 
     def moe(self, x: torch.Tensor, ids: torch.Tensor, w: torch.Tensor, E_local: int, R: int,
@@ -183,7 +209,7 @@ class SymmEP:
         C = _C()
         ids = ids.to(torch.int32).contiguous()
         w = w.to(torch.float32).contiguous()
-        C.symm_ep_dispatch(self.heap.bases, self.heap.rank, self.ch, self.layout, x, ids, w, R, E_local)
+        C.symm_ep_dispatch(self.heap.bases, self.heap.rank, self.ch, self.layout, x, ids, w, R, E_local, self.fp8)
         rx, rid, rw = self.views(R)
         y = expert_fn(rx, rid, rw)
         out = torch.empty_like(x)
@@ -198,25 +224,26 @@ _active_mb = 0  # dual-batch overlap: micro-batch m uses EP channel CH_EP + m an
 
 
 def init(rank: int, world: int, group=None, tp_allreduce: bool = False, ep_rows: int = 0, hidden: int = 0,
-         topk: int = 0, ar_max_bytes: int = 16 << 20, micro_batches: int = 1) -> SymmHeap:
+         topk: int = 0, ar_max_bytes: int = 16 << 20, micro_batches: int = 1, ep_fp8: bool = False) -> SymmHeap:
     """Create the process-wide heap and install the users that were asked for.
-    ``micro_batches=2`` (DBO) gives each micro-batch its own EP channel/buffers."""
+    ``micro_batches=2`` (DBO) gives each micro-batch its own EP channel/buffers;
+    ``ep_fp8`` quantises dispatched rows to block-fp8 in the dispatch kernel."""
     global _heap, _eps
     n = 1 << 20
     if tp_allreduce:
         slot = _align(max(512 << 10, ar_max_bytes // max(world, 1) + 16), 256)
         n += 4 * world * slot + 4096
     if ep_rows:
-        n += micro_batches * SymmEP.heap_bytes(world, ep_rows, hidden, topk)
+        n += micro_batches * SymmEP.heap_bytes(world, ep_rows, hidden, topk, ep_fp8)
     _heap = SymmHeap(n + (1 << 20), rank, world, group)
     if tp_allreduce:
         from .comm import set_custom_allreduce
 
         set_custom_allreduce(CustomAllReduce(_heap, max_bytes=ar_max_bytes))
     if ep_rows:
-        _eps = [SymmEP(_heap, ep_rows, hidden, topk, channel=CH_EP + m) for m in range(micro_batches)]
-    log.info("symm heap %.1f MiB on rank %d/%d (allreduce=%s, ep_rows=%d)", _heap.nbytes / 2**20, rank, world,
-             tp_allreduce, ep_rows)
+        _eps = [SymmEP(_heap, ep_rows, hidden, topk, channel=CH_EP + m, fp8=ep_fp8) for m in range(micro_batches)]
+    log.info("symm heap %.1f MiB on rank %d/%d (allreduce=%s, ep_rows=%d, fp8 dispatch=%s)", _heap.nbytes / 2**20,
+             rank, world, tp_allreduce, ep_rows, ep_fp8)
     return _heap
 
 

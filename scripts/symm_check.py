@@ -10,7 +10,11 @@ Checks (vs fp32 torch references):
   * custom all-reduce, one-shot and two-shot, odd sizes, in place and out of
     place, and replayed from a captured hipGraph with changing inputs;
   * EP low-latency dispatch -> expert fn -> combine with random top-k routing,
-    padded rows (T < R) and a captured-graph replay.
+    padded rows (T < R) and a captured-graph replay;
+  * fp8 dispatch (rows quantised in the dispatch kernel): received e4m3 bytes
+    and scales bit-identical to ops.quant_fp8_groups of the sender's rows
+    (hidden 320: a padded last group), and the block-fp8 grouped GEMM on the
+    received rows vs the same experts run without EP.
 Prints one JSON line per rank-0 result; exit code != 0 on any mismatch.
 """
 from __future__ import annotations
@@ -44,9 +48,12 @@ def main():
     ok = True
     res = {"world": world}
     E_local, k, d, R = 4, 4, 256, 96
-    heap = symm.SymmHeap((64 << 20) + symm.SymmEP.heap_bytes(world, R, d, k), rank, world)
+    d8 = 320
+    heap = symm.SymmHeap((64 << 20) + symm.SymmEP.heap_bytes(world, R, d, k)
+                         + symm.SymmEP.heap_bytes(world, R, d8, k, fp8=True), rank, world)
     ar = symm.CustomAllReduce(heap, max_bytes=8 << 20, oneshot_max=256 << 10)
     sep = symm.SymmEP(heap, R, d, k)
+    sep8 = symm.SymmEP(heap, R, d8, k, channel=symm.CH_EP + 1, fp8=True)
 
     # ---------------- all-reduce
     errs = {}
@@ -154,6 +161,67 @@ def main():
             ok = False
             print(f"[rank {rank}] ep graph replay {it} mismatch {err}", flush=True)
         dist.barrier()
+
+    # ---------------- fp8 dispatch
+    from llmd_amd import ops
+
+    def inputs(src, T, dd):
+        gen = torch.Generator().manual_seed(500 + src * 31 + T)
+        x = (torch.randn(T, dd, generator=gen) * (1 + 4 * torch.rand(T, 1, generator=gen))).to(torch.bfloat16)
+        ids = torch.stack([torch.randperm(E, generator=gen)[:k] for _ in range(T)]).to(torch.int32)
+        w = torch.rand(T, k, generator=gen)
+        return x, ids, w
+
+    for T in (R, 29):
+        seen = {}
+
+        def grab(rx, rid, rw):
+            seen["q"] = rx.q.view(torch.uint8).clone().cpu()
+            seen["s"] = rx.s.clone().cpu()
+            seen["rid"] = rid.clone().cpu()
+            return torch.zeros(rx.shape[0], d8, dtype=torch.bfloat16, device="cuda")
+
+        x, ids, w = inputs(rank, T, d8)
+        sep8.moe(x.cuda(), ids.cuda(), w.cuda(), E_local, R, grab)
+        torch.cuda.synchronize()
+        bad = 0
+        for src in range(world):
+            xs_, ids_, _ = inputs(src, T, d8)
+            rq, rs = ops.quant_fp8_groups(xs_.cuda())
+            rq = torch.nn.functional.pad(rq.view(torch.uint8), (0, sep8.dp - d8)).cpu()
+            mine = ((ids_ >= rank * E_local) & (ids_ < (rank + 1) * E_local)).any(1)
+            rows = torch.arange(T)[mine] + src * R
+            bad += int((seen["q"][rows] != rq[mine]).sum()) + int((seen["s"][rows] != rs.cpu()[mine]).sum())
+        if bad:
+            ok = False
+            print(f"[rank {rank}] fp8 dispatch T={T}: {bad} bytes/scales differ from quant_fp8_groups", flush=True)
+        res[f"ep_fp8_bad_T{T}"] = bad
+
+    # real block-fp8 experts on the received rows vs no EP
+    F8 = 256
+    gw = torch.Generator().manual_seed(4242)
+    w1 = (torch.randn(E, 2 * F8, d8, generator=gw) * 0.05).cuda()
+    w2 = (torch.randn(E, d8, F8, generator=gw) * 0.05).cuda()
+    w1q, w1s = ops.quant_fp8_block_weight(w1)
+    w2q, w2s = ops.quant_fp8_block_weight(w2)
+    w1q = ops.pad_fp8_k(w1q, sep8.dp)
+    lo = rank * E_local
+    loc = (w1q[lo:lo + E_local].contiguous(), w1s[lo:lo + E_local].contiguous(),
+           w2q[lo:lo + E_local].contiguous(), w2s[lo:lo + E_local].contiguous())
+
+    def fp8_experts(rx, rid, rw):
+        return ops.moe_experts_fp8(rx, rid, rw, *loc, 0)
+
+    x, ids, w = inputs(rank, 53, d8)
+    x, ids, w = x.cuda(), ids.cuda(), w.cuda()
+    got = sep8.moe(x, ids, w, E_local, R, fp8_experts)
+    want = ops.moe_experts_fp8(x, ids, w, w1q, w1s, w2q, w2s, 0)
+    torch.cuda.synchronize()
+    err = (got.float() - want.float()).abs().max().item()
+    res["ep_fp8_moe_err"] = err
+    if not err < 0.02 * want.float().abs().max().item() + 1e-3:
+        ok = False
+        print(f"[rank {rank}] fp8 EP moe mismatch {err} (max {want.float().abs().max().item()})", flush=True)
 
     e = heap.error()
     if e:

@@ -77,13 +77,20 @@ def test_dashboards_reference_exported_metrics():
 
     names = set(re.findall(r"^# TYPE (\S+)", EngineMetrics("m", 16, 100).render().decode(), re.M))
     names |= set(re.findall(r"^# TYPE (\S+)", EPPMetrics().render().decode(), re.M))
+    from llmd_amd.kvcache.offload import _XferStats
+
+    names |= set(re.findall(r"^# TYPE (\S+)", "\n".join(_XferStats().render('model_name="m"')), re.M))
+    import llmd_amd.kvcache.offload as off  # the tier's own gauges / counters (rendered per engine)
+
+    names |= set(re.findall(r"# TYPE (vllm:[a-z_]+)", open(off.__file__).read()))
     names |= {"vllm:nixl_xfer_time_seconds", "vllm:nixl_bytes_transferred", "vllm:nixl_num_failed_transfers"}
     files = glob.glob(os.path.join(ROOT, "deploy/observability/grafana/dashboards/*.json"))
-    assert len(files) == 4
+    assert len(files) == 6
     for f in files:
         for p in json.load(open(f))["panels"]:
             for t in p["targets"]:
-                for m in re.findall(r"(vllm:[a-z_]+|inference_[a-z_]+|llm_d_[a-z_]+)", t["expr"]):
+                for m in re.findall(r"(vllm:[a-z0-9_]+|inference_[a-z0-9_]+|llm_d_[a-z0-9_]+)",
+                                   re.sub(r"\{[^}]*\}", "", t["expr"])):  # metric names, not labels
                     base = re.sub(r"_(bucket|sum|count|total)$", "", m)
                     assert base in names or m in names, (f, m)
 

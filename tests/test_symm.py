@@ -36,6 +36,55 @@ def test_ep_heap_bytes_cover_layout():
             assert need >= 2 * rx + 2 * rid
 
 
+class _FakeHeap:
+    """SymmHeap stand-in on the CPU: a byte tensor carved like the real one."""
+
+    def __init__(self, nbytes, world):
+        import torch
+
+        self.world, self.rank = world, 0
+        self.heap = torch.full((nbytes,), 0xAB, dtype=torch.uint8)
+        self._next = 4096
+        self.nbytes = nbytes
+
+    carve = symm.SymmHeap.carve
+
+
+@pytest.mark.parametrize("world,rows,d,k", [(1, 16, 320, 4), (8, 256, 7168, 8), (4, 64, 2880, 4)])
+def test_ep_fp8_layout_fits_and_views(world, rows, d, k):
+    import torch
+
+    need = symm.SymmEP.heap_bytes(world, rows, d, k, fp8=True)
+    h = _FakeHeap(need + 4096, world)
+    sep = symm.SymmEP(h, rows, d, k, fp8=True)
+    lay = sep.layout
+    assert len(lay) == 7 and lay[5] > lay[3] and lay[6] > lay[5]
+    dp = (d + 127) // 128 * 128
+    assert lay[6] + world * rows * (dp // 128) * 4 <= h.nbytes
+    rx, rid, rw = sep.views(rows)
+    assert rx.q.dtype == torch.float8_e4m3fn and tuple(rx.q.shape) == (world * rows, dp)
+    assert tuple(rx.s.shape) == (world * rows, dp // 128) and tuple(rx.shape) == (world * rows, d)
+    assert bool((rx.q.view(torch.uint8) == 0).all())  # padding zeroed at construction
+    # bf16 layouts keep the fp8 areas disabled
+    h2 = _FakeHeap(symm.SymmEP.heap_bytes(world, rows, d, k) + 4096, world)
+    assert symm.SymmEP(h2, rows, d, k).layout[5:] == [-1, -1]
+
+
+def test_fp8_rows_dequant_feeds_bf16_experts():
+    import torch
+
+    from llmd_amd import ops
+
+    x = torch.randn(5, 200).to(torch.bfloat16)
+    q, s = ops.quant_fp8_groups(x)
+    q = torch.nn.functional.pad(q.view(torch.uint8), (0, 56)).view(torch.float8_e4m3fn)
+    r = ops.Fp8Rows(q, s, 200)
+    assert tuple(r.shape) == (5, 200)
+    dq = r.dequant()
+    assert dq.shape == (5, 200)
+    assert (dq.float() - x.float()).abs().max() <= x.float().abs().max() / 8
+
+
 def test_symm_ll_falls_back_on_cpu():
     """On CPU tensors the symm backend must take the RCCL/gloo path (no heap)."""
     import torch
