@@ -421,7 +421,7 @@ def add_engine_args(p: argparse.ArgumentParser) -> argparse.ArgumentParser:
     p.add_argument("--data-parallel-rank", type=int, default=0)
     p.add_argument("--enable-expert-parallel", action="store_true")
     p.add_argument("--all2all-backend", default="allgather_reducescatter",
-                   choices=["allgather_reducescatter", "alltoall", "symm_ll", "deepep_low_latency",
+                   choices=["allgather_reducescatter", "alltoall", "symm_ll", "symm_ht", "deepep_low_latency",
                             "deepep_high_throughput"])
     p.add_argument("--disable-custom-all-reduce", action="store_true")
     p.add_argument("--enable-eplb", action="store_true")

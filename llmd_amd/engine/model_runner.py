@@ -178,9 +178,12 @@ class ModelRunner:
 
             if tp_min_int(ok) == 0:
                 symm.shutdown()
-        elif (ep_mod.canonical(pc.all2all_backend) == "symm_ll" and st.dp_size > 1 and st.tp_size == 1
-              and self.mc.is_moe):
+        elif (ep_mod.canonical(pc.all2all_backend) in ("symm_ll", "symm_ht") and st.dp_size > 1
+              and st.tp_size == 1 and self.mc.is_moe):
+            # LL: decode-sized steps in one exchange; HT: prefill steps in chunks of this many rows
             rows = max(self.cfg.cuda_graph_max_bs, 256)
+            if ep_mod.canonical(pc.all2all_backend) == "symm_ht":
+                rows = max(rows, int(os.environ.get("LLMD_EP_HT_ROWS", "1024")))
             # block-fp8 experts: quantise in the dispatch kernel (DeepEP-LL use_fp8)
             fp8 = (os.environ.get("LLMD_EP_FP8_DISPATCH", "1") == "1"
                    and any(getattr(m, "w1_scale", None) is not None and m.w1.dtype == torch.float8_e4m3fn

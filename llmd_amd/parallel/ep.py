@@ -20,8 +20,15 @@ Each rank owns E / EP experts and its own tokens. Two exchange backends:
   kernels over the symmetric IPC heap (parallel/symm.py) for steps of at most
   the heap's row capacity: each token row is pushed straight into the
   owning ranks' receive buffers over xGMI (7 links at once), fixed shapes, so
-  decode graphs capture it. Larger (prefill) steps fall back to ``alltoall``
-  eagerly - the reference's LL-for-decode / HT-for-prefill split.
+  decode graphs capture it.
+* ``symm_ht`` (alias ``deepep_high_throughput``): prefill-sized steps through
+  the same kernels in chunks of the heap's row capacity. The chunk count comes
+  from the step's agreed max rows (DP coordinator), so no per-layer count
+  exchange or host sync is needed (the RCCL ``alltoall`` backend needs
+  ``.tolist()`` of the split sizes), the exchange stays on the GPU and the
+  whole prefill MoE is graph-capturable. Each chunk's grouped GEMM still sees
+  world x chunk rows. Without a heap (CPU, multi-node) it degrades to
+  ``alltoall``.
 
 ``expert_fn(x, local_ids, weights) -> y`` computes the weighted sum over the
 given local experts (-1 ids are skipped).
@@ -33,8 +40,8 @@ import torch.distributed as dist
 
 from .state import get_state
 
-BACKENDS = ("allgather_reducescatter", "alltoall", "symm_ll")
-ALIASES = {"deepep_low_latency": "symm_ll", "deepep_high_throughput": "alltoall"}
+BACKENDS = ("allgather_reducescatter", "alltoall", "symm_ll", "symm_ht")
+ALIASES = {"deepep_low_latency": "symm_ll", "deepep_high_throughput": "symm_ht"}
 _backend = "allgather_reducescatter"
 _step_rows = 0  # max token rows of this step over the EP group (DP coordinator)
 
@@ -67,16 +74,39 @@ def ep_active() -> bool:
 
 def moe_ep(x: torch.Tensor, ids: torch.Tensor, w: torch.Tensor, E_local: int, expert_fn) -> torch.Tensor:
     capturing = x.is_cuda and torch.cuda.is_current_stream_capturing()
-    if _backend == "symm_ll" and x.is_cuda:
+    if _backend in ("symm_ll", "symm_ht") and x.is_cuda:
         from . import symm
 
         sep = symm.ep()
         R = max(x.shape[0], _step_rows)
         if sep is not None and R <= sep.R_max:
             return sep.moe(x, ids, w, E_local, R, expert_fn)
-    if _backend in ("alltoall", "symm_ll") and not capturing:
+        if sep is not None and _step_rows >= x.shape[0]:
+            # the chunk count must agree over the EP group: only from the agreed step rows
+            return symm_chunked(sep, x, ids, w, E_local, _step_rows, expert_fn)
+    if _backend in ("alltoall", "symm_ll", "symm_ht") and not capturing:
         return _alltoall(x, ids, w, E_local, expert_fn)
     return _allgather(x, ids, w, E_local, expert_fn)
+
+
+def chunk_plan(R: int, cap: int) -> tuple[int, int]:
+    """(chunks, rows per chunk) covering R rows with chunks of at most ``cap``,
+    balanced so the last chunk is not nearly empty."""
+    n = -(-R // cap)
+    return n, -(-R // n)
+
+
+def symm_chunked(sep, x, ids, w, E_local, R, expert_fn):
+    """HT exchange: ``R`` (agreed over the group) rows in equal chunks through
+    the symm dispatch/combine kernels; ranks whose own rows run out still take
+    part in every chunk with empty slices."""
+    T = x.shape[0]
+    n, rc = chunk_plan(R, sep.R_max)
+    outs = []
+    for c in range(n):
+        a, b = min(c * rc, T), min((c + 1) * rc, T)
+        outs.append(sep.moe(x[a:b], ids[a:b], w[a:b], E_local, rc, expert_fn))
+    return torch.cat(outs) if len(outs) > 1 else outs[0]
 
 
 def _allgather(x, ids, w, E_local, expert_fn):

@@ -117,7 +117,7 @@ class EPP:
         else:
             tgt, rule = self.control.rewrite(req.model)
             if rule is not None:
-                self.metrics.rewrite.labels(rule, req.model, tgt).inc()
+                self.metrics.child(self.metrics.rewrite, rule, req.model, tgt).inc()
             req.target_model = tgt
         req.objective = H.lookup(req.headers, H.OBJECTIVE)
         req.priority = self.control.priority_of(req.objective)
@@ -136,8 +136,8 @@ class EPP:
 
     async def schedule_request(self, req: InferenceRequest, body: bytes) -> Decision:
         m = self.metrics
-        m.req_total.labels(req.model, req.target_model, str(req.priority)).inc()
-        m.req_sizes.labels(req.model, req.target_model).observe(req.raw_size)
+        m.child(m.req_total, req.model, req.target_model, str(req.priority)).inc()
+        m.child(m.req_sizes, req.model, req.target_model).observe(req.raw_size)
         try:
             # ---- flow control / saturation shedding
             if self.flow is not None:
@@ -157,7 +157,7 @@ class EPP:
             for p in self.cfg.producers:
                 t0 = time.perf_counter()
                 await p.produce(req, eps)
-                m.plugin_dur.labels("DataProducer", p.plugin_type, p.name).observe(time.perf_counter() - t0)
+                m.child(m.plugin_dur, "DataProducer", p.plugin_type, p.name).observe(time.perf_counter() - t0)
             # ---- admitters
             for a in self.cfg.admitters:
                 rej = a.admit(req, eps)
@@ -169,15 +169,15 @@ class EPP:
             m.sched_e2e.observe(time.perf_counter() - t0)
             tgt = result.target
             if tgt is None:
-                m.sched_attempts.labels("failure", req.target_model, "", "", "").inc()
+                m.child(m.sched_attempts, "failure", req.target_model, "", "", "").inc()
                 raise SchedulingError(503, "no endpoint satisfied the scheduling profiles")
-            m.sched_attempts.labels("success", req.target_model, tgt.name, tgt.namespace, str(tgt.port)).inc()
+            m.child(m.sched_attempts, "success", req.target_model, tgt.name, tgt.namespace, str(tgt.port)).inc()
             # ---- pre-request hooks
             for p in self.cfg.pre_request:
                 p.pre_request(req, result)
             self.ctx.inflight_requests[tgt.key] = self.ctx.inflight_requests.get(tgt.key, 0) + 1
             if "pd_decision" in req.data:
-                m.pd_decisions.labels(req.target_model, req.data["pd_decision"]).inc()
+                m.child(m.pd_decisions, req.target_model, req.data["pd_decision"]).inc()
             hdrs = {H.DESTINATION: tgt.key}
             hdrs.update(result.headers)
             hdrs.update(req.data.get("upstream_headers", {}))
@@ -187,10 +187,10 @@ class EPP:
                 b = dict(req.body)
                 b["model"] = req.target_model
                 new_body = json.dumps(b).encode()
-            m.running.labels(req.model).inc()
+            m.child(m.running, req.model).inc()
             return Decision(req, tgt, hdrs, new_body, result)
         except SchedulingError as e:
-            m.req_err.labels(req.model, req.target_model, str(e.status)).inc()
+            m.child(m.req_err, req.model, req.target_model, str(e.status)).inc()
             raise
 
     def schedule(self, req: InferenceRequest, eps: list[Endpoint]) -> SchedulingResult:
@@ -214,20 +214,20 @@ class EPP:
         for f in prof.filters:
             t0 = time.perf_counter()
             cand = f.filter(req, cand)
-            m.plugin_dur.labels("Filter", f.plugin_type, f.name).observe(time.perf_counter() - t0)
+            m.child(m.plugin_dur, "Filter", f.plugin_type, f.name).observe(time.perf_counter() - t0)
             if not cand:
                 return ProfileRunResult([], {})
         total = {e.key: 0.0 for e in cand}
         for s, w in prof.scorers:
             t0 = time.perf_counter()
             sc = s.score(req, cand)
-            m.plugin_dur.labels("Scorer", s.plugin_type, s.name).observe(time.perf_counter() - t0)
+            m.child(m.plugin_dur, "Scorer", s.plugin_type, s.name).observe(time.perf_counter() - t0)
             for k in total:
                 total[k] += w * max(0.0, min(1.0, float(sc.get(k, 0.0))))
         scored = [(e, total[e.key]) for e in cand]
         t0 = time.perf_counter()
         picked = prof.picker.pick(req, scored)
-        m.plugin_dur.labels("Picker", prof.picker.plugin_type, prof.picker.name).observe(time.perf_counter() - t0)
+        m.child(m.plugin_dur, "Picker", prof.picker.plugin_type, prof.picker.name).observe(time.perf_counter() - t0)
         return ProfileRunResult(picked, total)
 
     # ------------------------------------------------------------ response path
@@ -244,25 +244,25 @@ class EPP:
         req = d.req
         k = d.endpoint.key
         self.ctx.inflight_requests[k] = max(0, self.ctx.inflight_requests.get(k, 0) - 1)
-        m.running.labels(req.model).dec()
+        m.child(m.running, req.model).dec()
         if info.get("duration") is not None:
-            m.duration.labels(req.model, req.target_model).observe(info["duration"])
+            m.child(m.duration, req.model, req.target_model).observe(info["duration"])
         if info.get("ttft") is not None:
-            m.ttft.labels(req.model, req.target_model).observe(info["ttft"])
+            m.child(m.ttft, req.model, req.target_model).observe(info["ttft"])
             if req.slo_ttft_ms and info["ttft"] * 1000 > req.slo_ttft_ms:
-                m.slo_viol.labels(req.model, req.target_model, "ttft").inc()
+                m.child(m.slo_viol, req.model, req.target_model, "ttft").inc()
         usage = info.get("usage") or {}
         if usage:
-            m.in_toks.labels(req.model, req.target_model).observe(usage.get("prompt_tokens", 0))
-            m.out_toks.labels(req.model, req.target_model).observe(usage.get("completion_tokens", 0))
+            m.child(m.in_toks, req.model, req.target_model).observe(usage.get("prompt_tokens", 0))
+            m.child(m.out_toks, req.model, req.target_model).observe(usage.get("completion_tokens", 0))
             ct = (usage.get("prompt_tokens_details") or {}).get("cached_tokens")
             if ct is not None:
-                m.cached_toks.labels(req.model, req.target_model).observe(ct)
+                m.child(m.cached_toks, req.model, req.target_model).observe(ct)
             n = usage.get("completion_tokens", 0)
             if n and info.get("duration"):
-                m.ntpot.labels(req.model, req.target_model).observe(info["duration"] / n)
+                m.child(m.ntpot, req.model, req.target_model).observe(info["duration"] / n)
         if info.get("tpot") is not None and req.slo_tpot_ms and info["tpot"] * 1000 > req.slo_tpot_ms:
-            m.slo_viol.labels(req.model, req.target_model, "tpot").inc()
+            m.child(m.slo_viol, req.model, req.target_model, "tpot").inc()
         for p in self.cfg.response_processors:
             p.on_response_complete(req, d.endpoint, info)
         if self.flow is not None:

@@ -55,7 +55,7 @@ def _get(headers, k):
         return None
     try:
         v = headers.get(k)
-        if v is None:
+        if v is None and not getattr(headers, "case_insensitive", False):
             low = k.lower()
             for hk, hv in headers.items():
                 if hk.lower() == low:

@@ -17,6 +17,7 @@ TOKS = (1, 8, 16, 32, 64, 128, 256, 512, 1024, 2048, 4096, 8192, 16384, 32778, 6
 
 class EPPMetrics:
     def __init__(self, pool: str = "pool"):
+        self._children: dict = {}
         self.reg = r = CollectorRegistry()
         self.pool = pool
         ml = ["model_name", "target_model_name"]
@@ -103,6 +104,15 @@ class EPPMetrics:
                 self.pool_pod_queue.labels(e.name, self.pool).set(float(e.metric(WAITING, 0)))
         if sat is not None:
             self.fc_sat.labels(self.pool).set(sat)
+
+    def child(self, metric, *labels):
+        """Cached labelled child: prometheus ``labels()`` costs a few microseconds and
+        the request path touches ~15 children per request."""
+        key = (id(metric), labels)
+        c = self._children.get(key)
+        if c is None:
+            c = self._children[key] = metric.labels(*labels)
+        return c
 
     def render(self) -> bytes:
         return generate_latest(self.reg)

@@ -153,7 +153,7 @@ class RouterProxy:
                 self.epp.on_response_headers(d, r.status, out_h)
                 resp = web.StreamResponse(status=r.status, headers=out_h)
                 await resp.prepare(req)
-                buf = b""
+                buf = bytearray()  # response tail for the usage block (trimmed in amortised O(1))
                 async for chunk in r.content.iter_any():
                     now = time.monotonic()
                     if first is None:
@@ -161,10 +161,12 @@ class RouterProxy:
                     last_tok = now
                     n_chunks += 1
                     self.epp.on_response_chunk(d, chunk, now)
-                    buf = (buf + chunk)[-65536:]
+                    buf += chunk
+                    if len(buf) > 131072:
+                        del buf[:-65536]
                     await resp.write(chunk)
                 await resp.write_eof()
-                info["usage"] = _find_usage(buf)
+                info["usage"] = _find_usage(bytes(buf))
                 return resp
         except (aiohttp.ClientError, asyncio.TimeoutError) as e:
             info["status"] = 502

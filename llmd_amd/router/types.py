@@ -24,8 +24,8 @@ class Attributes:
         self._lock = threading.Lock()
 
     def get(self, k: str, default=None):
-        with self._lock:
-            return self._d.get(k, default)
+        # a single dict read is atomic under the GIL; writers still lock
+        return self._d.get(k, default)
 
     def put(self, k: str, v: Any):
         with self._lock:
@@ -63,9 +63,10 @@ class Endpoint:
     attrs: Attributes = field(default_factory=Attributes)
     healthy: bool = True
 
-    @property
-    def key(self) -> str:
-        return f"{self.address}:{self.port}"
+    key: str = field(init=False, repr=False)  # "ip:port", read per scorer per endpoint: a plain attribute
+
+    def __post_init__(self):
+        self.key = f"{self.address}:{self.port}"
 
     @property
     def role(self) -> str:
@@ -83,6 +84,8 @@ class Endpoint:
 
 class CIHeaders(dict):
     """Case-insensitive header mapping (keys stored lower-case)."""
+
+    case_insensitive = True  # headers._get: a miss is final, no scan
 
     def __init__(self, d=None):
         super().__init__()

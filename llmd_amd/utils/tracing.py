@@ -16,7 +16,6 @@ import contextlib
 import contextvars
 import os
 import random
-import secrets
 import threading
 import time
 from dataclasses import dataclass, field
@@ -78,6 +77,12 @@ def parse_traceparent(tp: Optional[str]) -> Optional[tuple[str, str, bool]]:
     return parts[1], parts[2], bool(int(parts[3], 16) & 1)
 
 
+def _hex(bits: int) -> str:
+    """Random trace / span id (W3C ids need uniqueness, not secrecy; secrets.token_hex
+    costs ~3x more on the per-request router path)."""
+    return "%0*x" % (bits // 4, random.getrandbits(bits))
+
+
 def current() -> Optional[Span]:
     return _current.get()
 
@@ -95,8 +100,8 @@ def span(name: str, attrs: Optional[dict] = None, traceparent: Optional[str] = N
         if ext:
             tid, pid, sampled = ext
         else:
-            tid, pid, sampled = secrets.token_hex(16), None, random.random() < SAMPLE_RATIO
-    s = Span(name, tid, secrets.token_hex(8), pid, sampled, attrs=dict(attrs or {}))
+            tid, pid, sampled = _hex(128), None, random.random() < SAMPLE_RATIO
+    s = Span(name, tid, _hex(64), pid, sampled, attrs=dict(attrs or {}))
     tok = _current.set(s)
     try:
         if _otel_tracer is not None and sampled:  # pragma: no cover

@@ -162,6 +162,25 @@ def main():
             print(f"[rank {rank}] ep graph replay {it} mismatch {err}", flush=True)
         dist.barrier()
 
+    # ---------------- HT: a prefill-sized step in chunks of the heap capacity
+    from llmd_amd.parallel import ep as ep_mod
+
+    Rstep = 250
+    T = Rstep - 40 * rank  # ranks hold different row counts; chunk count agreed from Rstep
+    gen = torch.Generator().manual_seed(77 + rank)
+    x = torch.randn(T, d, generator=gen).to(torch.bfloat16)
+    ids = torch.stack([torch.randperm(E, generator=gen)[:k] for _ in range(T)]).to(torch.int32)
+    w = torch.rand(T, k, generator=gen)
+    got = ep_mod.symm_chunked(sep, x.cuda(), ids.cuda(), w.cuda(), E_local, Rstep, expert_fn_for(rank))
+    torch.cuda.synchronize()
+    want = expert_ref(x, ids, w, scale)
+    err = (got.float().cpu() - want).abs().max().item()
+    res["ep_ht_chunks"] = ep_mod.chunk_plan(Rstep, R)[0]
+    res["ep_ht_err"] = err
+    if got.shape[0] != T or not err < 0.05 + 0.02 * want.abs().max().item():
+        ok = False
+        print(f"[rank {rank}] ep HT chunked mismatch {err} shape {tuple(got.shape)}", flush=True)
+
     # ---------------- fp8 dispatch
     from llmd_amd import ops
 

@@ -18,12 +18,21 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 def test_backend_aliases():
     assert ep.canonical("deepep_low_latency") == "symm_ll"
-    assert ep.canonical("deepep_high_throughput") == "alltoall"
+    assert ep.canonical("deepep_high_throughput") == "symm_ht"
     ep.set_backend("deepep_low_latency")
     assert ep.backend() == "symm_ll"
     ep.set_backend("allgather_reducescatter")
     with pytest.raises(ValueError):
         ep.set_backend("nvshmem")
+
+
+def test_ht_chunk_plan():
+    assert ep.chunk_plan(4096, 1024) == (4, 1024)
+    assert ep.chunk_plan(1025, 1024) == (2, 513)
+    assert ep.chunk_plan(10, 1024) == (1, 10)
+    for R in range(1, 3000, 37):
+        n, rc = ep.chunk_plan(R, 256)
+        assert rc <= 256 and n * rc >= R and (n - 1) * rc < R
 
 
 def test_ep_heap_bytes_cover_layout():
