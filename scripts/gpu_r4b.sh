@@ -1,0 +1,12 @@
+# round 4 (b): production-shape attention numerics, then the one-EP-rank DeepSeek-R1
+# projection (fp8 dispatch kernels in loopback + the 61-layer decode step)
+set -o pipefail
+mkdir -p gpurun_out
+timeout -k 10 500 python -u -m pytest tests/test_kernels_prod_shapes.py -q -x --timeout 240 --timeout-method thread -p no:cacheprovider > gpurun_out/r4b_prod_shapes.log 2>&1
+rc=$?
+tail -4 gpurun_out/r4b_prod_shapes.log
+[ $rc -ne 0 ] && { grep -E "Error|error|FAILED|assert|Mismatch" gpurun_out/r4b_prod_shapes.log | head -30; exit $rc; }
+timeout -k 10 900 python -u scripts/bench_wide_ep_rank.py --steps 20 --out gpurun_out/wide_ep_rank_r1.json > gpurun_out/wide_ep_rank.log 2>&1
+rc=$?
+grep -v amdgpu.ids gpurun_out/wide_ep_rank.log | tail -12
+exit $rc
