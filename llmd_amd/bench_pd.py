@@ -85,6 +85,11 @@ def run_pd(a, rank: int, world: int, local_rank: int, log) -> dict | None:
                                         tp_rank=rank - d, tp_group=tg, tp_cpu_group=tgc, cpu_group=tgc,
                                         backend=dist.get_backend(), tp_src=d))
                 is_follower = rank != d
+    if os.environ.get("LLMD_KVX_TRANSPORT", "auto") == "rccl":
+        # two-sided RCCL send/recv KV transport: a group used by kvx only (collective creation)
+        from llmd_amd.kvx.agent import set_p2p_group
+
+        set_p2p_group(dist.new_group(timeout=to))
     base_port = int(os.environ.get("LLMD_PD_BASE_PORT", "18200"))
     max_len = a.isl + a.osl + 64
     kt = {"kv_connector": "KvxConnector", "kv_role": "kv_producer" if is_prefill else "kv_consumer",
@@ -92,7 +97,7 @@ def run_pd(a, rank: int, world: int, local_rank: int, log) -> dict | None:
           "kv_connector_extra_config": {"transport": os.environ.get("LLMD_KVX_TRANSPORT", "auto"),
                                         # a GPU bench never silently degrades a pull to TCP
                                         "require_ipc": a.device == "cuda"
-                                        and os.environ.get("LLMD_KVX_TRANSPORT", "auto") != "tcp"}}
+                                        and os.environ.get("LLMD_KVX_TRANSPORT", "auto") == "auto"}}
     conc = a.concurrency * (1 if is_prefill else dtp)  # --concurrency is per GPU
     cfg = EngineConfig.create(
         a.model, device=a.device, block_size=a.block_size,

@@ -17,6 +17,16 @@ Roles and protocol (vLLM NixlConnector-compatible ``kv_transfer_params``):
       heterogeneous-TP head re-slicing via copy segments; the layer-major pools
       make a block 2 L pieces, so the transfer is always the copy kernel and
       "dma" is kept only as an alias of "ipc");
+    - ``rccl`` (two-sided): when both engines sit in one torch.distributed
+      world (``set_p2p_group``: a group made for kvx only, so transfers never
+      interleave with the engines' own collectives), the decoder asks the
+      prefiller to ``push`` the blocks; the prefiller's single sender thread
+      gathers them into a contiguous block-major buffer on its own stream and
+      ``send``s it over RCCL (xGMI between GPUs of one node, the network
+      otherwise), the decoder ``recv``s into a staging buffer and scatters it
+      into its pool (TP head re-slicing by wire segments). Per prefiller the
+      decoder issues push + recv under one lock and the prefiller sends in
+      arrival order, so every send meets its recv;
     - ``tcp``  (CPU CI / fallback): block bytes streamed over the side channel.
   Completion -> ``free`` notification to the prefiller.
 Side channel: length-prefixed msgpack request/response over TCP
@@ -114,6 +124,58 @@ class LoadJob:
 
 LEGACY_IPC_MAX = 4 << 30  # hipIpcOpenMemHandle hangs importing larger allocations
 
+_P2P_GROUP = None  # torch.distributed group spanning prefill + decode engines (rccl transport)
+
+
+def set_p2p_group(group):
+    """Register the process group the ``rccl`` transport sends over. Every rank of
+    the world must create it (``dist.new_group``) before the engines start; it
+    must not be used for anything else."""
+    global _P2P_GROUP
+    _P2P_GROUP = group
+
+
+def p2p_group():
+    return _P2P_GROUP
+
+
+class _P2PSender:
+    """Prefiller side of the rccl transport: ONE thread owns every send, in the
+    order the pushes arrived (per decoder that is the order of its recvs)."""
+
+    def __init__(self, agent: "KvxAgent"):
+        self.agent = agent
+        self.q: "queue.Queue[Optional[tuple]]" = queue.Queue()
+        self.t = threading.Thread(target=self._run, daemon=True, name="kvx-p2p-send")
+        self.t.start()
+
+    def _run(self):
+        import torch.distributed as dist
+
+        a = self.agent
+        stream = None
+        while True:
+            item = self.q.get()
+            if item is None:
+                return
+            blocks, dst = item
+            try:
+                if a.is_gpu:
+                    if stream is None:
+                        torch.cuda.set_device(a.kv.device)
+                        stream = torch.cuda.Stream(device=a.kv.device)
+                    with torch.cuda.stream(stream):
+                        buf = a.pack_blocks(blocks)
+                        dist.send(buf, dst=dst, group=_P2P_GROUP)
+                    stream.synchronize()
+                else:
+                    dist.send(a.pack_blocks(blocks), dst=dst, group=_P2P_GROUP)
+            except Exception as e:  # noqa: BLE001 - the decoder's recv fails / times out in turn
+                log.warning("kvx p2p send of %d blocks to rank %d failed: %s", len(blocks), dst, e)
+
+    def close(self):
+        self.q.put(None)
+
 
 class KvxAgent:
     def __init__(self, kv: torch.Tensor, engine_id: Optional[str] = None, host: Optional[str] = None,
@@ -146,6 +208,15 @@ class KvxAgent:
         self.peers: dict[tuple, dict] = {}
         self.ipc_maps: dict[str, int] = {}
         self.ipc_handle = None
+        self.p2p_rank = None
+        self.p2p_sender = None
+        if _P2P_GROUP is not None:
+            import torch.distributed as dist
+
+            self.p2p_rank = dist.get_rank()
+            if exports:
+                self.p2p_sender = _P2PSender(self)
+        self.p2p_lock = threading.Lock()  # decoder: one push + recv in flight per process
         self.uds_name = None
         if self.is_gpu and transport in ("auto", "ipc", "dma"):
             if vmm is not None:
@@ -248,6 +319,8 @@ class KvxAgent:
              "pid": os.getpid(), "num_blocks": k.shape[1]}
         if self.ipc_handle is not None:
             m["ipc_handle"], m["ipc_offset"] = self.ipc_handle
+        if self.p2p_sender is not None:
+            m["p2p_rank"] = self.p2p_rank
         if self.uds_name is not None:
             off = self.kv.data_ptr() - self.vmm["pool"].data_ptr()
             m["vmm"] = {"uds": self.uds_name, "chunk": self.vmm["chunk"], "n": self.vmm["n"], "offset": off}
@@ -285,11 +358,16 @@ class KvxAgent:
                 out.append(self.held.pop(rid))
         return out
 
-    def read_blocks(self, blocks: list) -> bytes:
-        """Wire format (TCP path): each block's bytes block-major [L, planes, H, bs, D]."""
+    def pack_blocks(self, blocks: list) -> torch.Tensor:
+        """Wire format: each block's bytes block-major [L, planes, H, bs, D], as one
+        contiguous uint8 tensor on the pool's device."""
         idx = torch.tensor(blocks, dtype=torch.long, device=self.kv.device)
         g = self.kv.index_select(1, idx).transpose(0, 1).contiguous()
-        return g.cpu().view(torch.uint8).numpy().tobytes()
+        return g.view(torch.uint8).view(-1)
+
+    def read_blocks(self, blocks: list) -> bytes:
+        """Wire format (TCP path), as bytes."""
+        return self.pack_blocks(blocks).cpu().numpy().tobytes()
 
     # ------------------------------------------------------------ decode side
     def start_load(self, request_id: str, params: dict, local_blocks: list, report: Optional[tuple] = None):
@@ -463,7 +541,14 @@ class KvxAgent:
                    and self.transport in ("auto", "ipc", "dma") and not p.get("no_ipc")
                    and rmeta.get("hostname") == socket.gethostname())
         nbytes = sum(s[2] for s in segs) * n
-        if self.require_ipc and self.is_gpu and not use_ipc and self.transport != "tcp":
+        use_p2p = (self.transport == "rccl" and _P2P_GROUP is not None and rmeta.get("p2p_rank") is not None)
+        if self.transport == "rccl" and not use_p2p:
+            raise RuntimeError(f"kvx: rccl transport to {rmeta.get('engine_id')} needs a shared p2p group "
+                               f"(set_p2p_group) and a sending peer (peer p2p rank {rmeta.get('p2p_rank')})")
+        if use_p2p:
+            self._p2p_pull(p, prm, rblocks, lblocks)
+            use_ipc = False
+        elif self.require_ipc and self.is_gpu and not use_ipc and self.transport != "tcp":
             raise RuntimeError(f"kvx: no IPC path to {rmeta.get('engine_id')} (host {rmeta.get('hostname')}, "
                                f"handle {'ipc_handle' in rmeta or 'vmm' in rmeta}, degraded {bool(p.get('no_ipc'))}) "
                                "and require_ipc is set")
@@ -478,17 +563,12 @@ class KvxAgent:
                 use_ipc = False
                 if self.metrics is not None and hasattr(self.metrics, "on_ipc_fallback"):
                     self.metrics.on_ipc_fallback()
-        if not use_ipc:
+        if not use_ipc and not use_p2p:
             data = self._rpc(p, {"op": "read", "blocks": rblocks, "request_id": prm.get("remote_request_id")})
             if isinstance(data, dict) and data.get("error"):
                 raise RuntimeError(data["error"])
             src = torch.frombuffer(bytearray(data), dtype=torch.uint8).view(n, -1)
-            dst_idx = torch.tensor(lblocks, dtype=torch.long, device=self.kv.device)
-            rows = torch.empty(n, self.block_bytes, dtype=torch.uint8)
-            for so, do, ln in self._wire_segments(rmeta):
-                rows[:, do:do + ln] = src[:, so:so + ln]
-            blk = rows.view(self.kv.dtype).view((n,) + tuple(self.kv.shape[:1]) + tuple(self.kv.shape[2:]))
-            self.kv.index_copy_(1, dst_idx, blk.transpose(0, 1).to(self.kv.device))
+            self._scatter_wire(rmeta, src, lblocks)
             if self.is_gpu:
                 torch.cuda.current_stream().synchronize()
         if fault == "corrupt":
@@ -497,6 +577,50 @@ class KvxAgent:
         # release the prefiller's blocks (this rank's share)
         self._rpc(p, self._free_msg(prm))
         return True, nbytes
+
+    def _scatter_wire(self, rmeta, src: torch.Tensor, lblocks: list):
+        """Write wire-format blocks ``src`` [n, remote block bytes] (any device) into the
+        local pool at ``lblocks`` (this rank's head slice)."""
+        n = len(lblocks)
+        dst_idx = torch.tensor(lblocks, dtype=torch.long, device=self.kv.device)
+        segs = self._wire_segments(rmeta)
+        if len(segs) == 1 and segs[0][2] == src.shape[1]:
+            rows = src
+        else:
+            rows = torch.empty(n, self.block_bytes, dtype=torch.uint8, device=src.device)
+            for so, do, ln in segs:
+                rows[:, do:do + ln] = src[:, so:so + ln]
+        blk = rows.view(self.kv.dtype).view((n,) + tuple(self.kv.shape[:1]) + tuple(self.kv.shape[2:]))
+        self.kv.index_copy_(1, dst_idx, blk.transpose(0, 1).to(self.kv.device))
+
+    def _p2p_pull(self, p, prm, rblocks, lblocks):
+        """rccl transport: push request, then the matching recv, then the scatter."""
+        import torch.distributed as dist
+
+        rmeta = p["meta"]
+        rbb = int(rmeta["block_bytes"])
+        n = len(rblocks)
+        stream = None
+        if self.is_gpu:
+            stream = getattr(self._tls, "stream", None)
+            if stream is None:
+                torch.cuda.set_device(self.kv.device)
+                stream = self._tls.stream = torch.cuda.Stream(device=self.kv.device)
+        with self.p2p_lock:
+            r = self._rpc(p, {"op": "push", "blocks": rblocks, "request_id": prm.get("remote_request_id"),
+                              "dst": self.p2p_rank})
+            if not (isinstance(r, dict) and r.get("ok")):
+                raise RuntimeError(f"kvx push refused: {r}")
+            if stream is not None:
+                with torch.cuda.stream(stream):
+                    buf = torch.empty(n * rbb, dtype=torch.uint8, device=self.kv.device)
+                    dist.recv(buf, src=int(rmeta["p2p_rank"]), group=_P2P_GROUP)
+                    self._scatter_wire(rmeta, buf.view(n, rbb), lblocks)
+                stream.synchronize()
+            else:
+                buf = torch.empty(n * rbb, dtype=torch.uint8)
+                dist.recv(buf, src=int(rmeta["p2p_rank"]), group=_P2P_GROUP)
+                self._scatter_wire(rmeta, buf.view(n, rbb), lblocks)
 
     def _ipc_copy(self, rmeta, rblocks, lblocks, segs):
         from llmd_amd.ops import native
@@ -550,6 +674,8 @@ class KvxAgent:
 
     def close(self):
         self._stop.set()
+        if self.p2p_sender is not None:
+            self.p2p_sender.close()
         for _ in self.workers:
             self.jobs.put(None)
         self.server.shutdown()
@@ -584,6 +710,17 @@ class _Handler(socketserver.BaseRequestHandler):
                         _send(s, {"error": "blocks not held for request"})
                         continue
                     _send(s, agent.read_blocks(msg["blocks"]))
+                elif op == "push":  # rccl transport: queue the send, the decoder posts the recv
+                    rid = msg.get("request_id")
+                    with agent.held_lock:
+                        held = agent.held.get(rid)
+                    if agent.p2p_sender is None:
+                        _send(s, {"error": "no p2p group on this agent"})
+                    elif held is not None and not set(msg["blocks"]) <= set(held.blocks):
+                        _send(s, {"error": "blocks not held for request"})
+                    else:
+                        agent.p2p_sender.q.put((list(msg["blocks"]), int(msg["dst"])))
+                        _send(s, {"ok": True})
                 elif op == "free":
                     agent.free_requests.put((msg.get("request_id"), int(msg.get("rank", 0)),
                                              int(msg.get("of", 1))))
