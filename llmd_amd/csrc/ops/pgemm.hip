@@ -186,7 +186,7 @@ __global__ __launch_bounds__(NT, 1) void pgemm_kernel(const uint16_t* __restrict
   };
   // one phase: [reads + DMA issue + counted wait] -> lgkmcnt(0) -> barrier -> MFMA -> barrier
   auto seg_end = [&]() {
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0), visible to hipcc's waitcnt pass
     bar();
   };
 
@@ -323,6 +323,19 @@ __global__ __launch_bounds__(NT, 1) void pgemm_kernel(const uint16_t* __restrict
 constexpr int NT4 = 256;
 constexpr int SLOT4 = 32768;  // one k-half of A (16 KB) + of W (16 KB)
 
+// The 64 accumulators (256 registers) fill the accumulator file exactly; through the
+// builtin, hipcc's register allocator re-homes loop-carried accumulators every
+// iteration (~100-450 v_accvgpr moves per 64 MFMAs, with MFMA-result read stalls).
+// As an asm statement with the accumulator TIED in an AGPR ("+a") every tile stays
+// in place (0 moves). Hazards the compiler cannot see: an MFMA result read by a
+// non-MFMA instruction needs 12 wait states (8-pass XDL) -> mfma_drain() before the
+// epilogue; the A/B operands come straight from ds_read (lgkmcnt-ordered by hipcc,
+// which tracks the asm's "v" inputs), never from a VALU write in the 2 states before.
+__device__ __forceinline__ void mfma16_acc(f32x4_t& acc, const s16x8_t& a, const s16x8_t& b) {
+  asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(a), "v"(b));
+}
+__device__ __forceinline__ void mfma_drain() { asm volatile("s_nop 7\n\ts_nop 7" ::: "memory"); }
+
 __device__ __forceinline__ int swz4(int row, int c) {
   // F = {0, 2, 3, 1}: every ds_read_b128 lane group of a 16 x 4-chunk read hits 16 distinct slots
   return c ^ ((0x1E >> (2 * ((row >> 2) & 3))) & 3);
@@ -378,6 +391,9 @@ __global__ __launch_bounds__(NT4, 1) void pgemm4_kernel(const uint16_t* __restri
 #pragma unroll
     for (int j = 0; j < 8; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
   s16x8_t fa0[8], fw0[8], fa1[8], fw1[8];
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_nop 4" ::: "memory");  // v_accvgpr_write (zero init) -> MFMA srcC
+  __builtin_amdgcn_sched_barrier(0);
 
   // MFMAs of one substep on (fa, fw) with the next substep's 16 fragment reads from
   // `nxt` interleaved (1 read per 4 MFMA) into (na, nw)
@@ -389,8 +405,7 @@ __global__ __launch_bounds__(NT4, 1) void pgemm4_kernel(const uint16_t* __restri
         na[i] = *reinterpret_cast<const s16x8_t*>(nb_ + a_rd + i * 1024);                                  \
         nw[i] = *reinterpret_cast<const s16x8_t*>(nb_ + w_rd + i * 1024);                                  \
       }                                                                                                    \
-      _Pragma("unroll") for (int j = 0; j < 8; ++j) acc[i][j] =                                            \
-          __builtin_amdgcn_mfma_f32_16x16x32_bf16(fw[j], fa[i], acc[i][j], 0, 0, 0);                        \
+      _Pragma("unroll") for (int j = 0; j < 8; ++j) mfma16_acc(acc[i][j], fw[j], fa[i]);                   \
       if (do_read) {                                                                                       \
         __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);                                                 \
         __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);                                                 \
@@ -402,7 +417,10 @@ __global__ __launch_bounds__(NT4, 1) void pgemm4_kernel(const uint16_t* __restri
   // boundary: reads retired, the half read next has landed (every wave), then refill the slot whose
   // fragments are now all in registers
   auto boundary = [&](int wait_q, int issued_hi, int refill_q) {
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    // lgkmcnt(0) as the builtin, so hipcc's waitcnt pass sees the fragment reads retired
+    // (after an asm wait it re-waits before the next substep's first MFMA, stalling on
+    // that substep's first reads)
+    __builtin_amdgcn_s_waitcnt(0xC07F);
     const int younger = min(2, max(0, issued_hi - wait_q - 1));
     if (younger >= 2) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
     else if (younger == 1) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
@@ -434,11 +452,14 @@ __global__ __launch_bounds__(NT4, 1) void pgemm4_kernel(const uint16_t* __restri
     const int younger = hi - 2;
     if (younger >= 2) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // the prologue fragments, visibly to hipcc (else it re-waits in the loop)
     bar();
   }
   int issued = min(4, nq);
-  // K-steps 0 .. nk-2: both substeps read ahead
-  for (int kt = 0; kt + 1 < nk; ++kt) {
+  // every K-step in one loop body (a peeled last step makes hipcc re-home the
+  // accumulators through VGPRs): the last step's read-ahead of the nonexistent next
+  // half reads a stale slot into registers nothing consumes, its waits drain to 0
+  for (int kt = 0; kt < nk; ++kt) {
     const int q0 = 2 * kt;
     // substep (kt, 0): compute half q0 (fa0/fw0), read half q0 + 1
     PG4_SUBSTEP(fa0, fw0, fa1, fw1, lds + ((q0 + 1) & 3) * SLOT4, true);
@@ -451,14 +472,10 @@ __global__ __launch_bounds__(NT4, 1) void pgemm4_kernel(const uint16_t* __restri
     boundary(q0 + 3, issued, q0 + 6);
     if (q0 + 6 < nq) issued = q0 + 7;
   }
-  {  // last K-step: its second substep reads nothing
-    const int q0 = 2 * (nk - 1);
-    PG4_SUBSTEP(fa0, fw0, fa1, fw1, lds + ((q0 + 1) & 3) * SLOT4, true);
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    PG4_SUBSTEP(fa1, fw1, fa0, fw0, lds, false);
-  }
 #undef PG4_SUBSTEP
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  mfma_drain();  // the last MFMA results before the epilogue reads them (asm MFMAs are opaque to hipcc)
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
   __syncthreads();
 
   // epilogue: acc[i][j][r] = C[m][n], m = wr*128 + 16 i + (lane & 15), n = wc*128 + 16 j + 4 (lane >> 4) + r.
