@@ -57,7 +57,9 @@ int llmd_dgemm_supported(int, int, int);
 int llmd_mgemm(const void*, int64_t, const void*, int64_t, int, int, int, int, int, int, void*, int64_t, float*,
                hipStream_t);
 int llmd_mgemm_lds(int, int, int);
-int llmd_pgemm(const void*, int64_t, const void*, int64_t, void*, int64_t, int, int, int, int, int, hipStream_t);
+int llmd_pgemm(const void*, int64_t, const void*, int64_t, void*, int64_t, int, int, int, int, int, void*,
+               hipStream_t);
+int64_t llmd_pgemm_ws_bytes(int, int, int, int, int);
 int llmd_mgemm_fp8(const void*, int64_t, const float*, const void*, int64_t, const float*, int, int, int, int, int,
                    int, void*, int64_t, float*, hipStream_t);
 int llmd_vmm_granularity(int, size_t*);
@@ -439,7 +441,9 @@ void mgemm(torch::Tensor y, torch::Tensor x, torch::Tensor w, int64_t wrb, int64
 // y [M, N] = x [M, K] . w [N, K]^T for prefill-sized M on the 256 x 256 LDS-DMA MFMA
 // GEMM (csrc/ops/pgemm.hip); epi 1 = fused SiLU-and-mul over gate/up columns interleaved
 // per 256-column tile (y is then [M, N / 2])
-void pgemm(torch::Tensor y, torch::Tensor x, torch::Tensor w, int64_t epi, int64_t variant) {
+// variant 1 with split_k: a mostly idle last wave of tiles runs split over K into an fp32
+// workspace (allocated here from the caching allocator) and is reduced by a second kernel
+void pgemm(torch::Tensor y, torch::Tensor x, torch::Tensor w, int64_t epi, int64_t variant, bool split_k) {
   const c10::hip::OptionalHIPGuard device_guard(dev_of(y));
   CHECK_CUDA(x); CHECK_BF16(x); CHECK_BF16(w); CHECK_BF16(y); CHECK_INNER(x); CHECK_INNER(w); CHECK_INNER(y);
   TORCH_CHECK(x.dim() == 2 && w.dim() == 2 && y.dim() == 2, "pgemm: 2-D operands");
@@ -447,8 +451,11 @@ void pgemm(torch::Tensor y, torch::Tensor x, torch::Tensor w, int64_t epi, int64
   TORCH_CHECK(w.size(1) == K && K % 64 == 0 && N % 256 == 0, "pgemm: N % 256 == 0, K % 64 == 0");
   TORCH_CHECK(y.size(0) == M && y.size(1) == (epi == 1 ? N / 2 : N), "pgemm: output shape");
   TORCH_CHECK(x.stride(0) % 8 == 0 && w.stride(0) % 8 == 0 && y.stride(0) % 8 == 0, "pgemm: 16-B row alignment");
+  torch::Tensor ws;
+  const int64_t wsb = split_k ? llmd_pgemm_ws_bytes((int)M, (int)N, (int)K, (int)epi, (int)variant) : 0;
+  if (wsb > 0) ws = torch::empty({wsb / 4}, x.options().dtype(torch::kFloat));
   int rc = llmd_pgemm(x.data_ptr(), x.stride(0), w.data_ptr(), w.stride(0), y.data_ptr(), y.stride(0), (int)M,
-                      (int)N, (int)K, (int)epi, (int)variant, cur_stream());
+                      (int)N, (int)K, (int)epi, (int)variant, wsb > 0 ? ws.data_ptr() : nullptr, cur_stream());
   TORCH_CHECK(rc == 0, "pgemm failed: ", rc);
 }
 
@@ -934,7 +941,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {  // _C, or _C_debug (llmd_amd/build.p
   m.def("skinny_gemm", &skinny_gemm);
   m.def("skinny_supported", &skinny_supported);
   m.def("mgemm", &mgemm);
-  m.def("pgemm", &pgemm, "prefill bf16 GEMM (256x256 LDS-DMA MFMA tiles), optional fused SiLU-and-mul");
+  m.def("pgemm", &pgemm, "prefill bf16 GEMM (256x256 LDS-DMA MFMA tiles), optional fused SiLU-and-mul",
+        py::arg("y"), py::arg("x"), py::arg("w"), py::arg("epi"), py::arg("variant"), py::arg("split_k") = true);
   m.def("mgemm_fp8", &mgemm_fp8);
   m.def("mgemm_lds", [](int64_t M, int64_t wrb, int64_t stages) { return llmd_mgemm_lds((int)M, (int)wrb, (int)stages); });
   m.def("lora_bgmv", &lora_bgmv);

@@ -31,6 +31,7 @@
 //
 // Requirements (checked by the host wrapper): N % 256 == 0, K % 64 == 0,
 // 16-B aligned rows; any M (rows past M are clamped on load, not stored).
+#include <algorithm>
 #include <type_traits>
 
 #include "llmd_common.h"
@@ -45,7 +46,7 @@ constexpr int BUF = 4 * HALF;       // one K-step: A q0, A q1, W q0, W q1
 constexpr int LDS_BYTES = 2 * BUF;  // 128 KB
 constexpr int GROUP_M = 8;
 
-enum { EPI_NONE = 0, EPI_SILU = 1 };
+enum { EPI_NONE = 0, EPI_SILU = 1, EPI_F32 = 2 };
 
 __device__ __forceinline__ void dma16(const void* src, char* lds) {
   __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)src,
@@ -341,20 +342,39 @@ __device__ __forceinline__ int swz4(int row, int c) {
   return c ^ ((0x1E >> (2 * ((row >> 2) & 3))) & 3);
 }
 
-template <int EPI>
-__global__ __launch_bounds__(NT4, 1) void pgemm4_kernel(const uint16_t* __restrict__ A, int64_t lda,
-                                                        const uint16_t* __restrict__ W, int64_t ldw,
-                                                        uint16_t* __restrict__ C, int64_t ldc, int M, int N, int K) {
-  __shared__ __attribute__((aligned(1024))) char lds[4 * SLOT4];  // the ONLY LDS object
-  const int tiles_m = (M + BM - 1) / BM, tiles_n = N / BN;
-  const int ntiles = tiles_m * tiles_n;
-  const int L = xcd_remap(blockIdx.x, ntiles);
+// logical tile L (XCD-contiguous, GROUP_M-deep grouped order) -> (row tile, column tile)
+__device__ __forceinline__ void tile_mn(int L, int tiles_m, int tiles_n, int& tm, int& tn) {
   const int per_group = GROUP_M * tiles_n;
   const int g = L / per_group, first_m = g * GROUP_M;
   const int gm = min(tiles_m - first_m, GROUP_M);
-  const int tm = first_m + (L % per_group) % gm, tn = (L % per_group) / gm;
+  tm = first_m + (L % per_group) % gm;
+  tn = (L % per_group) / gm;
+}
+
+// Launch forms (host: llmd_pgemm): nsplit == 1 -> tiles [tile0, tile0 + grid) over the whole K
+// (data-parallel); nsplit > 1 (EPI_F32) -> the grid covers `tail` tiles from tile0 x nsplit
+// K-ranges, each block writing its fp32 partial tile to ws[split][tile][256][256]
+// (pgemm_splitk_reduce sums them). The tail split turns a last, mostly idle wave of tiles
+// (e.g. 576 tiles = 2.25 waves over 256 CUs at M 4608, N 8192) into one short full wave.
+template <int EPI>
+__global__ __launch_bounds__(NT4, 1) void pgemm4_kernel(const uint16_t* __restrict__ A, int64_t lda,
+                                                        const uint16_t* __restrict__ W, int64_t ldw,
+                                                        uint16_t* __restrict__ C, int64_t ldc, int M, int N, int K,
+                                                        int tile0, int nsplit, float* __restrict__ ws) {
+  __shared__ __attribute__((aligned(1024))) char lds[4 * SLOT4];  // the ONLY LDS object
+  const int tiles_m = (M + BM - 1) / BM, tiles_n = N / BN;
+  const int b = xcd_remap(blockIdx.x, gridDim.x);
+  const int tail = gridDim.x / nsplit;
+  const int t_local = b % tail, split = b / tail;
+  const int nk_all = K / BK;
+  const int chunk = (nk_all + nsplit - 1) / nsplit;
+  const int kbeg = split * chunk;
+  const int nk = min(chunk, nk_all - kbeg);
+  int tm, tn;
+  tile_mn(tile0 + t_local, tiles_m, tiles_n, tm, tn);
   const int m0 = tm * BM, n0 = tn * BN;
-  const int nk = K / BK;
+  A += (int64_t)kbeg * BK;
+  W += (int64_t)kbeg * BK;
 
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
   const int wr = w >> 1, wc = w & 1;
@@ -476,6 +496,18 @@ __global__ __launch_bounds__(NT4, 1) void pgemm4_kernel(const uint16_t* __restri
   mfma_drain();  // the last MFMA results before the epilogue reads them (asm MFMAs are opaque to hipcc)
   __builtin_amdgcn_sched_barrier(0);
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  if constexpr (EPI == EPI_F32) {
+    // fp32 partial tile, row-major [256][256]: 4 consecutive columns per lane -> 16-B stores
+    float* wt = ws + ((int64_t)split * tail + t_local) * (BM * BN);
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int row = wr * 128 + 16 * i + fr, col = wc * 128 + 16 * j + 4 * fq;
+        *reinterpret_cast<f32x4_t*>(wt + row * BN + col) = acc[i][j];
+      }
+    return;
+  }
   __syncthreads();
 
   // epilogue: acc[i][j][r] = C[m][n], m = wr*128 + 16 i + (lane & 15), n = wc*128 + 16 j + 4 (lane >> 4) + r.
@@ -521,23 +553,84 @@ __global__ __launch_bounds__(NT4, 1) void pgemm4_kernel(const uint16_t* __restri
   }
 }
 
+// ws [nsplit][tail][256][256] fp32 partials -> C tiles tile0 .. tile0 + tail - 1 (bf16, rows < M)
+__global__ __launch_bounds__(256) void pgemm_splitk_reduce(const float* __restrict__ ws, int nsplit, int tail,
+                                                           int tile0, uint16_t* __restrict__ C, int64_t ldc, int M,
+                                                           int N) {
+  const int t = blockIdx.x / (BM / 8), rblk = blockIdx.x % (BM / 8);  // 8 rows per block
+  int tm, tn;
+  tile_mn(tile0 + t, (M + BM - 1) / BM, N / BN, tm, tn);
+  const int row = rblk * 8 + (threadIdx.x >> 5), col = (threadIdx.x & 31) * 8;
+  const int m = tm * BM + row;
+  if (m >= M) return;
+  float f[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  for (int s = 0; s < nsplit; ++s) {
+    const float* p = ws + ((int64_t)s * tail + t) * (BM * BN) + row * BN + col;
+    const f32x4_t a = *reinterpret_cast<const f32x4_t*>(p), b = *reinterpret_cast<const f32x4_t*>(p + 4);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      f[e] += a[e];
+      f[4 + e] += b[e];
+    }
+  }
+  *reinterpret_cast<u32x4_t*>(C + (int64_t)m * ldc + tn * BN + col) = pack8(f);
+}
+
+constexpr int PG_CUS = 256;  // MI355X compute units: one 256 x 256 tile per CU per wave
+
+// tail split plan of the 4-wave kernel: (tiles run data-parallel, tail tiles, splits) or splits 1
+__host__ inline void pgemm_plan(int M, int N, int K, int epi, int& full, int& tail, int& nsplit) {
+  const int ntiles = ((M + BM - 1) / BM) * (N / BN), nk = K / BK;
+  full = ntiles;
+  tail = 0;
+  nsplit = 1;
+  const int t = ntiles % PG_CUS;
+  // a last wave at most half full, and K long enough that a quarter of it still pipelines
+  if (epi != EPI_NONE || t == 0 || 2 * t > PG_CUS || nk < 32) return;
+  int s = PG_CUS / t;
+  s = std::min(s, nk / 8);
+  if (s < 2) return;
+  full = ntiles - t;
+  tail = t;
+  nsplit = s;
+}
+
 }  // namespace
 
-// variant 0: 8-wave staggered 4-phase kernel; 1: 4-wave 128 x 128-per-wave kernel
+extern "C" int64_t llmd_pgemm_ws_bytes(int M, int N, int K, int epi, int variant) {
+  if (variant != 1 || M <= 0 || N % BN || K % BK) return 0;
+  int full, tail, nsplit;
+  pgemm_plan(M, N, K, epi, full, tail, nsplit);
+  return nsplit > 1 ? (int64_t)nsplit * tail * BM * BN * 4 : 0;
+}
+
+// variant 0: 8-wave staggered 4-phase kernel; 1: 4-wave 128 x 128-per-wave kernel (+ split-K tail when
+// ws is given: see pgemm_plan)
 extern "C" int llmd_pgemm(const void* A, int64_t lda, const void* W, int64_t ldw, void* C, int64_t ldc, int M, int N,
-                          int K, int epi, int variant, hipStream_t st) {
+                          int K, int epi, int variant, void* ws, hipStream_t st) {
   if (M <= 0) return 0;
   if (N % BN || K % BK || lda % 8 || ldw % 8 || ldc % 8) return -1;
   // 32-bit DMA offsets
   if ((int64_t)(M - 1) * lda + K > 0x7fffffffLL || (int64_t)(N - 1) * ldw + K > 0x7fffffffLL) return -2;
   const int ntiles = ((M + BM - 1) / BM) * (N / BN);
   if (variant == 1) {
+    int full = ntiles, tail = 0, nsplit = 1;
+    if (ws != nullptr) pgemm_plan(M, N, K, epi, full, tail, nsplit);
+    const auto* a = (const uint16_t*)A;
+    const auto* w = (const uint16_t*)W;
+    auto* c = (uint16_t*)C;
     if (epi == EPI_SILU)
-      hipLaunchKernelGGL(pgemm4_kernel<EPI_SILU>, dim3(ntiles), dim3(NT4), 0, st, (const uint16_t*)A, lda,
-                         (const uint16_t*)W, ldw, (uint16_t*)C, ldc, M, N, K);
-    else
-      hipLaunchKernelGGL(pgemm4_kernel<EPI_NONE>, dim3(ntiles), dim3(NT4), 0, st, (const uint16_t*)A, lda,
-                         (const uint16_t*)W, ldw, (uint16_t*)C, ldc, M, N, K);
+      hipLaunchKernelGGL(pgemm4_kernel<EPI_SILU>, dim3(full), dim3(NT4), 0, st, a, lda, w, ldw, c, ldc, M, N, K, 0, 1,
+                         nullptr);
+    else if (full > 0)
+      hipLaunchKernelGGL(pgemm4_kernel<EPI_NONE>, dim3(full), dim3(NT4), 0, st, a, lda, w, ldw, c, ldc, M, N, K, 0, 1,
+                         nullptr);
+    if (nsplit > 1) {
+      hipLaunchKernelGGL(pgemm4_kernel<EPI_F32>, dim3(tail * nsplit), dim3(NT4), 0, st, a, lda, w, ldw, c, ldc, M, N,
+                         K, full, nsplit, (float*)ws);
+      hipLaunchKernelGGL(pgemm_splitk_reduce, dim3(tail * (BM / 8)), dim3(256), 0, st, (const float*)ws, nsplit,
+                         tail, full, c, ldc, M, N);
+    }
     return (int)hipGetLastError();
   }
   if (epi == EPI_SILU)

@@ -359,11 +359,15 @@ class Scheduler:
 
     def _align_tokens(self, out: SchedulerOutput) -> None:
         """Trim prefill chunks, newest first, so the step's token count is a
-        multiple of ``prefill_token_align`` (GEMM-friendly M). Each trimmed chunk
-        keeps at least two tokens (a one-token chunk would read as a decode);
-        steps below two alignment units, or whose chunks cannot give up the
-        whole remainder, run as scheduled. Trimmed tokens go in the next step
-        (their blocks stay allocated, so the next ``grow`` is a no-op)."""
+        multiple of ``prefill_token_align`` (GEMM-friendly M). Only chunks that
+        do not finish their prompt give tokens up: those continue next step
+        anyway, while trimming a FINAL chunk would add a whole extra step for
+        its tail (measured: a 5000-token prompt beside 64 decodes became 4608-
+        and 518-token steps, 509 + 103 ms, instead of one 5064-token step). Each
+        trimmed chunk keeps at least two tokens (a one-token chunk would read as
+        a decode); steps below two alignment units, or whose chunks cannot give
+        up the whole remainder, run as scheduled. Trimmed tokens go in the next
+        step (their blocks stay allocated, so the next ``grow`` is a no-op)."""
         a = self.sc.prefill_token_align
         if a <= 0 or not out.prefills:
             return
@@ -371,10 +375,16 @@ class Scheduler:
         rem = total % a
         if total < 2 * a or rem == 0:
             return
-        if sum(max(sr.num_new_tokens - 2, 0) for sr in out.prefills) < rem:
+
+        def slack(sr):
+            if sr.start + sr.num_new_tokens >= sr.req.num_tokens:  # final chunk: keep whole
+                return 0
+            return max(sr.num_new_tokens - 2, 0)
+
+        if sum(slack(sr) for sr in out.prefills) < rem:
             return
         for sr in reversed(out.prefills):
-            take = min(rem, max(sr.num_new_tokens - 2, 0))
+            take = min(rem, slack(sr))
             sr.num_new_tokens -= take
             rem -= take
             if rem == 0:

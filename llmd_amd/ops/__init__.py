@@ -939,16 +939,17 @@ PGEMM_VARIANT = int(os.environ.get("LLMD_PGEMM_VARIANT", "1"))
 
 
 def pgemm(x: torch.Tensor, w: torch.Tensor, epi: int = 0, out: Optional[torch.Tensor] = None,
-          variant: Optional[int] = None) -> torch.Tensor:
+          variant: Optional[int] = None, split_k: bool = True) -> torch.Tensor:
     """Y = X W^T on the prefill GEMM (csrc/ops/pgemm.hip: 256 x 256 LDS-DMA MFMA
     tiles; N % 256 == 0, K % 64 == 0, any M). epi=1: ``w`` holds gate/up rows
     interleaved per 256-row tile (pgemm_pack_gate_up) and the kernel stores
-    silu(gate) * up, [M, N / 2]."""
+    silu(gate) * up, [M, N / 2]. ``split_k`` (variant 1, epi 0): a last wave of
+    tiles at most half full runs split over K (fp32 partials + reduce)."""
     M = x.shape[0]
     N = w.shape[0]
     if out is None:
         out = torch.empty(M, N // 2 if epi else N, dtype=x.dtype, device=x.device)
-    native().pgemm(out, x, w, epi, PGEMM_VARIANT if variant is None else variant)
+    native().pgemm(out, x, w, epi, PGEMM_VARIANT if variant is None else variant, split_k)
     return out
 
 

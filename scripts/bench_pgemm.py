@@ -31,7 +31,7 @@ def timeit(fn, iters):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--rounds", type=int, default=3)
-    ap.add_argument("--ms", default="4608,8192,2048")
+    ap.add_argument("--ms", default="4608,5064,8192,2048")
     ap.add_argument("--shapes", default=",".join(SHAPES))
     a = ap.parse_args()
     dev = "cuda"
@@ -53,6 +53,7 @@ def main():
             print(f"check v{v} M={M} N={N} K={K}: rel err {err:.2e}  silu rel err {serr:.2e}", flush=True)
             assert err < 1e-2 and serr < 2e-2
     ms = [int(m) for m in a.ms.split(",")]
+    # M = 5064: a whole 5000-token prompt beside 64 decode rows (no chunk trim)
     for M in ms:
         for name in a.shapes.split(","):
             N, K = SHAPES[name]
@@ -61,11 +62,12 @@ def main():
             y = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
             flops = 2.0 * M * N * K
             it = max(3, int(2e13 / flops))
-            res = {"blas": [], "v0": [], "v1": []}
+            res = {"blas": [], "v0": [], "v1": [], "v1sk": []}
             for _ in range(a.rounds):
                 res["blas"].append(timeit(lambda: F.linear(x, w), it))
                 res["v0"].append(timeit(lambda: ops.pgemm(x, w, out=y, variant=0), it))
-                res["v1"].append(timeit(lambda: ops.pgemm(x, w, out=y, variant=1), it))
+                res["v1"].append(timeit(lambda: ops.pgemm(x, w, out=y, variant=1, split_k=False), it))
+                res["v1sk"].append(timeit(lambda: ops.pgemm(x, w, out=y, variant=1), it))
             d = max((ops.pgemm(x, w, variant=v).float() - F.linear(x, w).float()).abs().max().item() for v in (0, 1))
             line = f"M={M:5d} {name:10s} N={N:6d} K={K:6d}:"
             for k, v in res.items():
