@@ -21,6 +21,7 @@ from __future__ import annotations
 
 import heapq
 import itertools
+import os
 import time
 from collections import deque
 from dataclasses import dataclass, field
@@ -30,6 +31,9 @@ import numpy as np
 
 from .config import EngineConfig
 from .request import Request, Status
+
+# GEMM alignment may not trim a chunk that finishes its prompt (engine/scheduler._align_tokens)
+KEEP_FINAL_CHUNK = os.environ.get("LLMD_ALIGN_KEEP_FINAL", "0") == "1"
 
 
 @dataclass
@@ -359,11 +363,12 @@ class Scheduler:
 
     def _align_tokens(self, out: SchedulerOutput) -> None:
         """Trim prefill chunks, newest first, so the step's token count is a
-        multiple of ``prefill_token_align`` (GEMM-friendly M). Only chunks that
-        do not finish their prompt give tokens up: those continue next step
-        anyway, while trimming a FINAL chunk would add a whole extra step for
-        its tail (measured: a 5000-token prompt beside 64 decodes became 4608-
-        and 518-token steps, 509 + 103 ms, instead of one 5064-token step). Each
+        multiple of ``prefill_token_align`` (GEMM-friendly M). With
+        ``LLMD_ALIGN_KEEP_FINAL=1`` only chunks that do not finish their prompt
+        give tokens up (trimming a FINAL chunk adds a whole extra step for its
+        tail: a 5000-token prompt beside 64 decodes becomes 4608- and 518-token
+        steps, 509 + 103 ms); off by default because hipBLASLt runs the unaligned
+        5064-row GEMMs ~20 % slower per token (profiles/gemm_prefill_odd_m.txt). Each
         trimmed chunk keeps at least two tokens (a one-token chunk would read as
         a decode); steps below two alignment units, or whose chunks cannot give
         up the whole remainder, run as scheduled. Trimmed tokens go in the next
@@ -377,7 +382,7 @@ class Scheduler:
             return
 
         def slack(sr):
-            if sr.start + sr.num_new_tokens >= sr.req.num_tokens:  # final chunk: keep whole
+            if KEEP_FINAL_CHUNK and sr.start + sr.num_new_tokens >= sr.req.num_tokens:  # final: keep whole
                 return 0
             return max(sr.num_new_tokens - 2, 0)
 

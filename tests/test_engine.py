@@ -98,8 +98,7 @@ def test_prefill_token_align_trims_steps_and_keeps_outputs():
         if so.prefills:
             # the trim keeps >= 2 tokens per chunk: a step is left unaligned
             # only when its chunks could not give up the remainder
-            slack = sum(sr.num_new_tokens - 2 for sr in so.prefills
-                        if sr.start + sr.num_new_tokens < sr.req.num_tokens)  # final chunks stay whole
+            slack = sum(sr.num_new_tokens - 2 for sr in so.prefills)
             seen.append((so.num_tokens, slack))
         return so
 
