@@ -268,14 +268,21 @@ class BlockManager {
   }
 
   // Blocks for an externally produced KV (P/D): allocate `n` fresh blocks for a
-  // new sequence without any prefix reuse (the sender fills them).
-  std::vector<int32_t> allocate_remote(int64_t seq_id, int num_tokens, uint64_t extra) {
+  // new sequence without any prefix reuse (the sender fills them). window > 0
+  // (windowed group of a hybrid cache): only the blocks the next query can reach
+  // (keys >= num_tokens - window + 1) are allocated, earlier entries are the null
+  // block (requires reserved >= 1).
+  std::vector<int32_t> allocate_remote(int64_t seq_id, int num_tokens, uint64_t extra, int window) {
     if (seqs_.count(seq_id)) throw std::runtime_error("allocate_remote: sequence exists");
-    const int need = (num_tokens + bs_ - 1) / bs_;
-    if (need > num_free()) return {};
+    if (window > 0 && reserved_ < 1) throw std::runtime_error("allocate_remote(window) needs a reserved null block");
+    const int nb = (num_tokens + bs_ - 1) / bs_;
+    const int lo = window > 0 ? std::min(nb, std::max(0, num_tokens - window + 1) / bs_) : 0;
+    if (nb - lo > num_free()) return {};
     Seq s;
     s.extra = extra;
-    for (int i = 0; i < need; ++i) s.blocks.push_back(pop_free());
+    for (int i = 0; i < lo; ++i) s.blocks.push_back(0);
+    for (int i = lo; i < nb; ++i) s.blocks.push_back(pop_free());
+    s.released = lo;
     auto out = s.blocks;
     seqs_.emplace(seq_id, std::move(s));
     return out;
@@ -442,7 +449,8 @@ void register_block_manager(py::module_& m) {
       .def("block_table", &BlockManager::block_table)
       .def("num_seq_blocks", &BlockManager::num_seq_blocks)
       .def("fill_block_tables", &BlockManager::fill_block_tables)
-      .def("allocate_remote", &BlockManager::allocate_remote)
+      .def("allocate_remote", &BlockManager::allocate_remote, py::arg("seq_id"), py::arg("num_tokens"),
+           py::arg("extra"), py::arg("window") = 0)
       .def("reset_prefix_cache", &BlockManager::reset_prefix_cache)
       .def("take_events", &BlockManager::take_events)
       .def("take_evicted", &BlockManager::take_evicted)

@@ -17,7 +17,11 @@ Without it every layer keeps the whole context, so a windowed layer holds
   the null block, which the window-limited attention kernels never read;
 * released blocks stay content-addressed in the windowed pool's LRU, so a
   prefix-cache hit needs only the LAST window of the prefix there
-  (``acquire_window``); the hit is the longest prefix both groups hold.
+  (``acquire_window``); the hit is the longest prefix both groups hold;
+* P/D (kvx): the prefiller holds both groups' tables (``transfer_tables``; the
+  windowed one is null before the last window), the decoder allocates the full
+  prompt in the full group and the last window in the windowed group
+  (``allocate_remote``), and the pull copies each group's non-null blocks.
 
 The windowed pool is sized for every sequence's window plus one step's prefill
 chunks (``swa_blocks``); the full pool gets the rest of the KV budget, so
@@ -79,8 +83,21 @@ class HybridBlockManager:
         self.swa.free(seq_id)
 
     def allocate_remote(self, seq_id, num_tokens, extra):
-        raise NotImplementedError("P/D KV pulls into a hybrid KV cache are not supported; "
-                                  "run the decoder with --disable-hybrid-kv-cache-manager")
+        """P/D decode side: fresh blocks for the whole prompt in the full group, and
+        in the windowed group only for the last window (earlier entries null) -
+        the prefiller holds exactly those (it released the rest after its step)."""
+        full = self.full.allocate_remote(seq_id, num_tokens, extra)
+        if not full:
+            return []
+        swa = self.swa.allocate_remote(seq_id, num_tokens, extra, self.window)
+        if not swa and num_tokens > 0:
+            self.full.free(seq_id)
+            return []
+        return HybridBlocks(full, swa)
+
+    def transfer_tables(self, seq_id):
+        """Both groups' tables of a finished prefill (P side of P/D)."""
+        return HybridBlocks(self.full.block_table(seq_id), self.swa.block_table(seq_id))
 
     # ---- tables
     def has_seq(self, seq_id) -> bool:
@@ -135,3 +152,12 @@ class HybridTables(dict):
     def __init__(self, full: dict, swa: dict):
         super().__init__(full)
         self.swa = swa
+
+
+class HybridBlocks(list):
+    """A full-group block list carrying the windowed group's list in ``swa``
+    (null entries = block 0): what kvx moves for one request of a hybrid cache."""
+
+    def __init__(self, full, swa):
+        super().__init__(full)
+        self.swa = list(swa)

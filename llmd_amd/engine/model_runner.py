@@ -194,16 +194,16 @@ class ModelRunner:
     # ------------------------------------------------------------ KV cache
     def _want_hybrid(self) -> bool:
         """Hybrid manager: on by default for models mixing windowed and full layers
-        (vLLM's default); off with --disable-hybrid-kv-cache-manager, and when a KV
-        transfer / offload connector needs whole-model blocks."""
+        (vLLM's default); off with --disable-hybrid-kv-cache-manager, and with the
+        tiered offload connector (whole-model blocks). kvx P/D moves both pools."""
         flag = self.cfg.cache.hybrid_kv_cache_manager
         if not self.swa_layers or not self.full_layers or self.is_mla or flag is False:
             return False
         if self.cfg.parallel.enable_dbo:
             return False  # dual-batch graphs carry one set of tables
-        if self.cfg.kv_transfer_config or self.cfg.kv_offload_config:
+        if self.cfg.kv_offload_config:
             if flag:
-                log.warning("hybrid KV cache manager not available with a KV transfer / offload connector: "
+                log.warning("hybrid KV cache manager not available with the KV offload connector: "
                             "every layer keeps full-length KV")
             return False
         return True

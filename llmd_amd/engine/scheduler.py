@@ -452,7 +452,11 @@ class Scheduler:
         ktp = r.kv_transfer_params or {}
         if ktp.get("do_remote_decode") and self.connector is not None and status != Status.FINISHED_ABORTED:
             # P side: keep blocks for the remote reader; the connector frees them
-            self.connector.hold_for_remote(r, self.bm.block_table(r.seq_id) if self.bm.has_seq(r.seq_id) else [])
+            tables = []
+            if self.bm.has_seq(r.seq_id):
+                tables = (self.bm.transfer_tables(r.seq_id) if hasattr(self.bm, "transfer_tables")
+                          else self.bm.block_table(r.seq_id))
+            self.connector.hold_for_remote(r, tables)
         elif free_blocks:
             self.bm.free(r.seq_id)
         self.requests.pop(r.request_id, None)

@@ -45,6 +45,12 @@ every ``LLMD_KVX_HEARTBEAT_S`` (5 s) on a fresh connection; after
 its cached connection and mapping are dropped, and pulls from it fail at once
 (-> kv_load_failure_policy) instead of hanging on a dead socket. A later
 successful ping revives it.
+Hybrid KV caches (engine/hybrid_kv.py; gpt-oss with the hybrid manager): the
+sliding-window layers live in a second pool (``kv_swa``) with their own block
+tables; the prefiller holds both tables (windowed entries null before the last
+window), the decoder allocated the full prompt in one group and the last
+window in the other, and every transport moves each pool's non-null pairs
+with that pool's own segments (``pool="swa"`` on the wire).
 Tensor-parallel decoders (the reference's ``D TP4`` P/D deployments,
 guides/pd-disaggregation/README.md:336-460): every TP rank of a decode
 replica owns a slice of the KV heads and pulls that slice itself, straight
@@ -111,6 +117,7 @@ class Held:
     expiry: float
     num_tokens: int
     frees: set = field(default_factory=set)  # consumer TP ranks done reading
+    swa_blocks: Optional[list] = None        # windowed pool of a hybrid cache
 
 
 @dataclass
@@ -120,6 +127,14 @@ class LoadJob:
     local_blocks: list
     t0: float = field(default_factory=time.monotonic)
     report: Optional[tuple] = None  # TP follower: the driver's side channel
+    local_swa: Optional[list] = None  # hybrid cache: the windowed pool's destination blocks
+
+
+def _pool_info(t: torch.Tensor) -> dict:
+    """Geometry of a layer-major pool [L, num_blocks, planes, H, bs, D] in bytes."""
+    esz = t.element_size()
+    return {"shape": list(t.shape), "block_bytes": t[:, 0].numel() * esz,
+            "layer_block_bytes": t[0, 0].numel() * esz, "layer_stride": t.stride(0) * esz}
 
 
 LEGACY_IPC_MAX = 4 << 30  # hipIpcOpenMemHandle hangs importing larger allocations
@@ -158,18 +173,18 @@ class _P2PSender:
             item = self.q.get()
             if item is None:
                 return
-            blocks, dst = item
+            blocks, dst, pool = item
             try:
                 if a.is_gpu:
                     if stream is None:
                         torch.cuda.set_device(a.kv.device)
                         stream = torch.cuda.Stream(device=a.kv.device)
                     with torch.cuda.stream(stream):
-                        buf = a.pack_blocks(blocks)
+                        buf = a.pack_blocks(blocks, pool)
                         dist.send(buf, dst=dst, group=_P2P_GROUP)
                     stream.synchronize()
                 else:
-                    dist.send(a.pack_blocks(blocks), dst=dst, group=_P2P_GROUP)
+                    dist.send(a.pack_blocks(blocks, pool), dst=dst, group=_P2P_GROUP)
             except Exception as e:  # noqa: BLE001 - the decoder's recv fails / times out in turn
                 log.warning("kvx p2p send of %d blocks to rank %d failed: %s", len(blocks), dst, e)
 
@@ -181,8 +196,9 @@ class KvxAgent:
     def __init__(self, kv: torch.Tensor, engine_id: Optional[str] = None, host: Optional[str] = None,
                  port: int = 0, tp_rank: int = 0, tp_size: int = 1, abort_timeout: float = 480.0,
                  transport: str = "auto", metrics=None, vmm: Optional[dict] = None, exports: bool = True,
-                 workers: Optional[int] = None, require_ipc: bool = False):
+                 workers: Optional[int] = None, require_ipc: bool = False, kv_swa: Optional[torch.Tensor] = None):
         self.kv = kv                      # [L, num_blocks, planes, Hkv, bs, D] (layer-major)
+        self.kv_swa = kv_swa              # hybrid cache: the windowed layers' pool (same layout)
         self.require_ipc = require_ipc    # never degrade a GPU pull to TCP (bench / production P/D)
         self.vmm = vmm                    # chunked exportable pool (model_runner._alloc_cache)
         self.engine_id = engine_id or f"kvx-{uuid.uuid4().hex[:12]}"
@@ -208,6 +224,7 @@ class KvxAgent:
         self.peers: dict[tuple, dict] = {}
         self.ipc_maps: dict[str, int] = {}
         self.ipc_handle = None
+        self.ipc_handle_swa = None
         self.p2p_rank = None
         self.p2p_sender = None
         if _P2P_GROUP is not None:
@@ -237,6 +254,14 @@ class KvxAgent:
             elif exports:  # a pure consumer only pulls, nobody maps its pool
                 log.warning("KV pool of %.1f GiB is not VMM-chunked; hipIpc cannot import >4 GiB, "
                             "kvx falls back to TCP", kv.numel() * kv.element_size() / 2**30)
+            if kv_swa is not None and exports and kv_swa.numel() * kv_swa.element_size() <= LEGACY_IPC_MAX:
+                try:
+                    from llmd_amd.ops import native
+
+                    h, off = native().kvx_ipc_export(kv_swa)
+                    self.ipc_handle_swa = (h, off)
+                except Exception as e:  # noqa: BLE001
+                    log.warning("IPC export of the windowed pool unavailable (%s)", e)
         self.host = host or os.environ.get("VLLM_NIXL_SIDE_CHANNEL_HOST", "127.0.0.1")
         self.server = _Server(("0.0.0.0" if self.host not in ("127.0.0.1", "localhost") else self.host,
                                port or int(os.environ.get("VLLM_NIXL_SIDE_CHANNEL_PORT", "0") or 0)), self)
@@ -321,18 +346,28 @@ class KvxAgent:
             m["ipc_handle"], m["ipc_offset"] = self.ipc_handle
         if self.p2p_sender is not None:
             m["p2p_rank"] = self.p2p_rank
+        if self.kv_swa is not None:
+            m["swa"] = _pool_info(self.kv_swa)
+            if self.ipc_handle_swa is not None:
+                m["swa"]["ipc_handle"], m["swa"]["ipc_offset"] = self.ipc_handle_swa
         if self.uds_name is not None:
             off = self.kv.data_ptr() - self.vmm["pool"].data_ptr()
             m["vmm"] = {"uds": self.uds_name, "chunk": self.vmm["chunk"], "n": self.vmm["n"], "offset": off}
         return m
 
     # ------------------------------------------------------------ prefill side
-    def hold(self, request_id: str, seq_id: int, blocks: list, num_tokens: int) -> dict:
+    def hold(self, request_id: str, seq_id: int, blocks: list, num_tokens: int,
+             swa_blocks: Optional[list] = None) -> dict:
+        swa = list(swa_blocks) if swa_blocks is not None else None
         with self.held_lock:
-            self.held[request_id] = Held(seq_id, list(blocks), time.monotonic() + self.abort_timeout, num_tokens)
-        return {"do_remote_prefill": True, "do_remote_decode": False, "remote_engine_id": self.engine_id,
-                "remote_host": self.host, "remote_port": self.port, "remote_block_ids": list(blocks),
-                "remote_request_id": request_id, "remote_tp_size": self.tp_size, "num_tokens": num_tokens}
+            self.held[request_id] = Held(seq_id, list(blocks), time.monotonic() + self.abort_timeout, num_tokens,
+                                         swa_blocks=swa)
+        out = {"do_remote_prefill": True, "do_remote_decode": False, "remote_engine_id": self.engine_id,
+               "remote_host": self.host, "remote_port": self.port, "remote_block_ids": list(blocks),
+               "remote_request_id": request_id, "remote_tp_size": self.tp_size, "num_tokens": num_tokens}
+        if swa is not None:
+            out["remote_swa_block_ids"] = swa
+        return out
 
     def expired_or_freed(self) -> list[Held]:
         """Held entries to release now (engine thread)."""
@@ -358,25 +393,38 @@ class KvxAgent:
                 out.append(self.held.pop(rid))
         return out
 
-    def pack_blocks(self, blocks: list) -> torch.Tensor:
+    def _pool(self, pool: str = "full") -> torch.Tensor:
+        if pool == "swa":
+            if self.kv_swa is None:
+                raise RuntimeError("kvx: no windowed pool on this agent")
+            return self.kv_swa
+        return self.kv
+
+    def pack_blocks(self, blocks: list, pool: str = "full") -> torch.Tensor:
         """Wire format: each block's bytes block-major [L, planes, H, bs, D], as one
         contiguous uint8 tensor on the pool's device."""
-        idx = torch.tensor(blocks, dtype=torch.long, device=self.kv.device)
-        g = self.kv.index_select(1, idx).transpose(0, 1).contiguous()
+        kv = self._pool(pool)
+        idx = torch.tensor(blocks, dtype=torch.long, device=kv.device)
+        g = kv.index_select(1, idx).transpose(0, 1).contiguous()
         return g.view(torch.uint8).view(-1)
 
-    def read_blocks(self, blocks: list) -> bytes:
+    def read_blocks(self, blocks: list, pool: str = "full") -> bytes:
         """Wire format (TCP path), as bytes."""
-        return self.pack_blocks(blocks).cpu().numpy().tobytes()
+        return self.pack_blocks(blocks, pool).cpu().numpy().tobytes()
 
     # ------------------------------------------------------------ decode side
-    def start_load(self, request_id: str, params: dict, local_blocks: list, report: Optional[tuple] = None):
+    def start_load(self, request_id: str, params: dict, local_blocks: list, report: Optional[tuple] = None,
+                   local_swa: Optional[list] = None):
         """Queue a pull. ``report`` (TP followers) is the driver's side-channel
-        address: completion goes there instead of this agent's ``done``."""
+        address: completion goes there instead of this agent's ``done``.
+        ``local_swa`` (or ``local_blocks.swa``): windowed-pool destinations."""
+        if local_swa is None:
+            local_swa = getattr(local_blocks, "swa", None)
         if self.tp_size > 1 and report is None:
             with self.tp_lock:
                 self.tp_wait[request_id] = [0, True]
-        self.jobs.put(LoadJob(request_id, dict(params), list(local_blocks), report=report))
+        self.jobs.put(LoadJob(request_id, dict(params), list(local_blocks), report=report,
+                              local_swa=list(local_swa) if local_swa is not None else None))
 
     def _complete(self, job: LoadJob, ok: bool):
         if job.report is not None:
@@ -454,6 +502,13 @@ class KvxAgent:
             raise RuntimeError(f"kvx layout mismatch local {ls} remote {rs}")
         if m["dtype"] != str(self.kv.dtype).replace("torch.", ""):
             raise RuntimeError("kvx dtype mismatch")
+        if ("swa" in m) != (self.kv_swa is not None):
+            raise RuntimeError("kvx: hybrid (windowed-pool) KV cache on one side only; run both engines with "
+                               "the same --disable-hybrid-kv-cache-manager setting")
+        if "swa" in m:
+            rw, lw = m["swa"]["shape"], list(self.kv_swa.shape)
+            if rw[0] != lw[0] or rw[2] != lw[2] or rw[4] != lw[4] or rw[5] != lw[5]:
+                raise RuntimeError(f"kvx windowed-pool layout mismatch local {lw} remote {rw}")
         if rs[3] % ls[3] and ls[3] % rs[3]:
             raise RuntimeError("kvx: KV head counts not TP-compatible")
 
@@ -469,27 +524,36 @@ class KvxAgent:
             raise RuntimeError("kvx: decoder holds more KV heads than the prefiller (unsupported pull)")
         return hr, hl, (self.tp_rank * hl) % hr  # prefiller has all heads of a group of decoder ranks
 
-    def _segments(self, rmeta) -> list[tuple[int, int, int]]:
+    @staticmethod
+    def _rinfo(rmeta, pool: str = "full") -> dict:
+        return rmeta["swa"] if pool == "swa" else rmeta
+
+    def _segments(self, rmeta, pool: str = "full") -> list[tuple[int, int, int]]:
         """IPC copy segments (src_off, dst_off, len) of one block, relative to
         block * layer_block_bytes in each pool: one per layer (per layer and
         plane when TP re-slices heads) - a block is 2 L pieces of the
         layer-major pools."""
-        L, _, planes, _, bs, D = self.kv.shape
+        kv = self._pool(pool)
+        ri = self._rinfo(rmeta, pool)
+        L, _, planes, _, bs, D = kv.shape
         hr, hl, h0 = self._head_slice(rmeta)
-        lsr, lsl = int(rmeta["layer_stride"]), self.layer_stride
+        esz = kv.element_size()
+        lsr, lsl = int(ri["layer_stride"]), kv.stride(0) * esz
+        lbb = kv[0, 0].numel() * esz
         if hr == hl:
-            return [(l * lsr, l * lsl, self.layer_block_bytes) for l in range(L)]
-        head = bs * D * self.kv.element_size()
+            return [(l * lsr, l * lsl, lbb) for l in range(L)]
+        head = bs * D * esz
         return [(l * lsr + (p * hr + h0) * head, l * lsl + p * hl * head, hl * head)
                 for l in range(L) for p in range(planes)]
 
-    def _wire_segments(self, rmeta) -> list[tuple[int, int, int]]:
-        """TCP path: segments inside one block-major wire block (read_blocks)."""
-        L, _, planes, _, bs, D = self.kv.shape
+    def _wire_segments(self, rmeta, pool: str = "full") -> list[tuple[int, int, int]]:
+        """TCP / rccl paths: segments inside one block-major wire block (read_blocks)."""
+        kv = self._pool(pool)
+        L, _, planes, _, bs, D = kv.shape
         hr, hl, h0 = self._head_slice(rmeta)
         if hr == hl:
-            return [(0, 0, self.block_bytes)]
-        head = bs * D * self.kv.element_size()
+            return [(0, 0, kv[:, 0].numel() * kv.element_size())]
+        head = bs * D * kv.element_size()
         return [(((l * planes + p) * hr + h0) * head, ((l * planes + p) * hl) * head, hl * head)
                 for l in range(L) for p in range(planes)]
 
@@ -535,18 +599,28 @@ class KvxAgent:
         rmeta = p["meta"]
         rblocks = list(prm["remote_block_ids"])
         n = min(len(rblocks), len(job.local_blocks))
-        rblocks, lblocks = rblocks[:n], job.local_blocks[:n]
-        segs = self._segments(rmeta)
+        # (pool, remote blocks, local blocks): the windowed pool of a hybrid cache moves
+        # only the pairs both sides hold (null = block 0 before the last window)
+        work = [("full", rblocks[:n], job.local_blocks[:n])]
+        rs, ls = prm.get("remote_swa_block_ids"), job.local_swa
+        if self.kv_swa is not None and rs is not None and ls is not None:
+            pairs = [(r, l) for r, l in zip(rs, ls) if r and l]
+            if pairs:
+                work.append(("swa", [r for r, _ in pairs], [l for _, l in pairs]))
+        elif (self.kv_swa is not None) != (rs is not None):
+            raise RuntimeError("kvx: request and KV cache disagree on the hybrid (windowed) pool")
         use_ipc = (self.is_gpu and ("ipc_handle" in rmeta or "vmm" in rmeta)
                    and self.transport in ("auto", "ipc", "dma") and not p.get("no_ipc")
-                   and rmeta.get("hostname") == socket.gethostname())
-        nbytes = sum(s[2] for s in segs) * n
+                   and rmeta.get("hostname") == socket.gethostname()
+                   and (len(work) == 1 or "ipc_handle" in rmeta.get("swa", {})))
+        nbytes = sum(sum(sg[2] for sg in self._segments(rmeta, pool)) * len(lb) for pool, _, lb in work)
         use_p2p = (self.transport == "rccl" and _P2P_GROUP is not None and rmeta.get("p2p_rank") is not None)
         if self.transport == "rccl" and not use_p2p:
             raise RuntimeError(f"kvx: rccl transport to {rmeta.get('engine_id')} needs a shared p2p group "
                                f"(set_p2p_group) and a sending peer (peer p2p rank {rmeta.get('p2p_rank')})")
         if use_p2p:
-            self._p2p_pull(p, prm, rblocks, lblocks)
+            for pool, rb, lb in work:
+                self._p2p_pull(p, prm, rb, lb, pool)
             use_ipc = False
         elif self.require_ipc and self.is_gpu and not use_ipc and self.transport != "tcp":
             raise RuntimeError(f"kvx: no IPC path to {rmeta.get('engine_id')} (host {rmeta.get('hostname')}, "
@@ -554,7 +628,8 @@ class KvxAgent:
                                "and require_ipc is set")
         if use_ipc:
             try:
-                self._ipc_copy(rmeta, rblocks, lblocks, segs)
+                for pool, rb, lb in work:
+                    self._ipc_copy(rmeta, rb, lb, self._segments(rmeta, pool), pool)
             except Exception as e:  # noqa: BLE001 - mapping failed: degrade this peer to TCP
                 if self.require_ipc:
                     raise RuntimeError(f"kvx IPC pull from {rmeta.get('engine_id')} failed: {e}") from e
@@ -564,41 +639,45 @@ class KvxAgent:
                 if self.metrics is not None and hasattr(self.metrics, "on_ipc_fallback"):
                     self.metrics.on_ipc_fallback()
         if not use_ipc and not use_p2p:
-            data = self._rpc(p, {"op": "read", "blocks": rblocks, "request_id": prm.get("remote_request_id")})
-            if isinstance(data, dict) and data.get("error"):
-                raise RuntimeError(data["error"])
-            src = torch.frombuffer(bytearray(data), dtype=torch.uint8).view(n, -1)
-            self._scatter_wire(rmeta, src, lblocks)
+            for pool, rb, lb in work:
+                data = self._rpc(p, {"op": "read", "blocks": rb, "request_id": prm.get("remote_request_id"),
+                                     "pool": pool})
+                if isinstance(data, dict) and data.get("error"):
+                    raise RuntimeError(data["error"])
+                src = torch.frombuffer(bytearray(data), dtype=torch.uint8).view(len(rb), -1)
+                self._scatter_wire(rmeta, src, lb, pool)
             if self.is_gpu:
                 torch.cuda.current_stream().synchronize()
         if fault == "corrupt":
-            idx = torch.tensor(lblocks[:1], dtype=torch.long, device=self.kv.device)
+            idx = torch.tensor(work[0][2][:1], dtype=torch.long, device=self.kv.device)
             self.kv.index_fill_(1, idx, 0)
         # release the prefiller's blocks (this rank's share)
         self._rpc(p, self._free_msg(prm))
         return True, nbytes
 
-    def _scatter_wire(self, rmeta, src: torch.Tensor, lblocks: list):
+    def _scatter_wire(self, rmeta, src: torch.Tensor, lblocks: list, pool: str = "full"):
         """Write wire-format blocks ``src`` [n, remote block bytes] (any device) into the
         local pool at ``lblocks`` (this rank's head slice)."""
+        kv = self._pool(pool)
         n = len(lblocks)
-        dst_idx = torch.tensor(lblocks, dtype=torch.long, device=self.kv.device)
-        segs = self._wire_segments(rmeta)
+        dst_idx = torch.tensor(lblocks, dtype=torch.long, device=kv.device)
+        segs = self._wire_segments(rmeta, pool)
+        bb = kv[:, 0].numel() * kv.element_size()
         if len(segs) == 1 and segs[0][2] == src.shape[1]:
             rows = src
         else:
-            rows = torch.empty(n, self.block_bytes, dtype=torch.uint8, device=src.device)
+            rows = torch.empty(n, bb, dtype=torch.uint8, device=src.device)
             for so, do, ln in segs:
                 rows[:, do:do + ln] = src[:, so:so + ln]
-        blk = rows.view(self.kv.dtype).view((n,) + tuple(self.kv.shape[:1]) + tuple(self.kv.shape[2:]))
-        self.kv.index_copy_(1, dst_idx, blk.transpose(0, 1).to(self.kv.device))
+        blk = rows.view(kv.dtype).view((n,) + tuple(kv.shape[:1]) + tuple(kv.shape[2:]))
+        kv.index_copy_(1, dst_idx, blk.transpose(0, 1).to(kv.device))
 
-    def _p2p_pull(self, p, prm, rblocks, lblocks):
+    def _p2p_pull(self, p, prm, rblocks, lblocks, pool: str = "full"):
         """rccl transport: push request, then the matching recv, then the scatter."""
         import torch.distributed as dist
 
         rmeta = p["meta"]
-        rbb = int(rmeta["block_bytes"])
+        rbb = int(self._rinfo(rmeta, pool)["block_bytes"])
         n = len(rblocks)
         stream = None
         if self.is_gpu:
@@ -608,43 +687,52 @@ class KvxAgent:
                 stream = self._tls.stream = torch.cuda.Stream(device=self.kv.device)
         with self.p2p_lock:
             r = self._rpc(p, {"op": "push", "blocks": rblocks, "request_id": prm.get("remote_request_id"),
-                              "dst": self.p2p_rank})
+                              "dst": self.p2p_rank, "pool": pool})
             if not (isinstance(r, dict) and r.get("ok")):
                 raise RuntimeError(f"kvx push refused: {r}")
             if stream is not None:
                 with torch.cuda.stream(stream):
                     buf = torch.empty(n * rbb, dtype=torch.uint8, device=self.kv.device)
                     dist.recv(buf, src=int(rmeta["p2p_rank"]), group=_P2P_GROUP)
-                    self._scatter_wire(rmeta, buf.view(n, rbb), lblocks)
+                    self._scatter_wire(rmeta, buf.view(n, rbb), lblocks, pool)
                 stream.synchronize()
             else:
                 buf = torch.empty(n * rbb, dtype=torch.uint8)
                 dist.recv(buf, src=int(rmeta["p2p_rank"]), group=_P2P_GROUP)
-                self._scatter_wire(rmeta, buf.view(n, rbb), lblocks)
+                self._scatter_wire(rmeta, buf.view(n, rbb), lblocks, pool)
 
-    def _ipc_copy(self, rmeta, rblocks, lblocks, segs):
+    def _ipc_copy(self, rmeta, rblocks, lblocks, segs, pool: str = "full"):
         from llmd_amd.ops import native
 
         C = native()
         eid = rmeta["engine_id"]
+        kv = self._pool(pool)
+        ri = self._rinfo(rmeta, pool)
         stream = getattr(self._tls, "stream", None)
         if stream is None:
             torch.cuda.set_device(self.kv.device)
             stream = self._tls.stream = torch.cuda.Stream(device=self.kv.device)
         with self.peer_lock:
-            base = self._map_peer(C, eid, rmeta)
+            base = self._map_peer(C, eid, rmeta, pool)
         with torch.cuda.stream(stream):
             # block b of layer l sits at pool + l * layer_stride + b * layer_block_bytes
-            pairs = torch.tensor(list(zip(rblocks, lblocks)), dtype=torch.int32, device=self.kv.device)
-            sg = torch.tensor(segs, dtype=torch.int64, device=self.kv.device)
-            C.kvx_copy_blocks(self.kv, base, self.layer_block_bytes, int(rmeta["layer_block_bytes"]), pairs, sg,
-                              max(s[2] for s in segs), COPY_ENGINE)
+            pairs = torch.tensor(list(zip(rblocks, lblocks)), dtype=torch.int32, device=kv.device)
+            sg = torch.tensor(segs, dtype=torch.int64, device=kv.device)
+            C.kvx_copy_blocks(kv, base, kv[0, 0].numel() * kv.element_size(), int(ri["layer_block_bytes"]), pairs,
+                              sg, max(x[2] for x in segs), COPY_ENGINE)
             ev = torch.cuda.Event()
             ev.record(stream)
         ev.synchronize()
 
-    def _map_peer(self, C, eid, rmeta) -> int:
+    def _map_peer(self, C, eid, rmeta, pool: str = "full") -> int:
         """Base pointer of a peer's KV pool in this process (mapped once)."""
+        if pool == "swa":
+            key = eid + ":swa"
+            base = self.ipc_maps.get(key)
+            if base is None:
+                sw = rmeta["swa"]
+                base = self.ipc_maps[key] = C.kvx_ipc_open(sw["ipc_handle"]) + int(sw["ipc_offset"])
+            return base
         base = self.ipc_maps.get(eid)
         if base is None:
             if "vmm" in rmeta:
@@ -688,6 +776,16 @@ class KvxAgent:
         # process exit: a pull kernel may still reference them on another stream
 
 
+def _held_ok(agent: KvxAgent, msg: dict, pool: str) -> bool:
+    """A read / push may only name blocks the request holds (of that pool)."""
+    with agent.held_lock:
+        held = agent.held.get(msg.get("request_id"))
+    if held is None:
+        return True
+    have = held.swa_blocks if pool == "swa" else held.blocks
+    return have is not None and set(msg["blocks"]) <= set(have)
+
+
 class _Handler(socketserver.BaseRequestHandler):
     def handle(self):
         agent: KvxAgent = self.server.agent
@@ -703,23 +801,19 @@ class _Handler(socketserver.BaseRequestHandler):
                 if op == "meta":
                     _send(s, agent.meta())
                 elif op == "read":
-                    rid = msg.get("request_id")
-                    with agent.held_lock:
-                        held = agent.held.get(rid)
-                    if held is not None and not set(msg["blocks"]) <= set(held.blocks):
+                    pool = msg.get("pool", "full")
+                    if not _held_ok(agent, msg, pool):
                         _send(s, {"error": "blocks not held for request"})
                         continue
-                    _send(s, agent.read_blocks(msg["blocks"]))
+                    _send(s, agent.read_blocks(msg["blocks"], pool))
                 elif op == "push":  # rccl transport: queue the send, the decoder posts the recv
-                    rid = msg.get("request_id")
-                    with agent.held_lock:
-                        held = agent.held.get(rid)
+                    pool = msg.get("pool", "full")
                     if agent.p2p_sender is None:
                         _send(s, {"error": "no p2p group on this agent"})
-                    elif held is not None and not set(msg["blocks"]) <= set(held.blocks):
+                    elif not _held_ok(agent, msg, pool):
                         _send(s, {"error": "blocks not held for request"})
                     else:
-                        agent.p2p_sender.q.put((list(msg["blocks"]), int(msg["dst"])))
+                        agent.p2p_sender.q.put((list(msg["blocks"]), int(msg["dst"]), pool))
                         _send(s, {"ok": True})
                 elif op == "free":
                     agent.free_requests.put((msg.get("request_id"), int(msg.get("rank", 0)),

@@ -72,6 +72,7 @@ class KvxConnector:
 
         st = get_state()
         self.agent = KvxAgent(engine.runner.kv, vmm=getattr(engine.runner, "vmm", None),
+                              kv_swa=getattr(engine.runner, "kv_swa", None),
                               host=extra.get("side_channel_host"),
                               port=int(extra.get("side_channel_port", 0) or 0),
                               tp_rank=st.tp_rank, tp_size=st.tp_size,
@@ -89,9 +90,10 @@ class KvxConnector:
     # ---------------- decode side (scheduler hooks)
     def start_load(self, req, local_blocks: list):
         prm = req.kv_transfer_params or {}
-        self.agent.start_load(req.request_id, prm, local_blocks)
+        swa = getattr(local_blocks, "swa", None)
+        self.agent.start_load(req.request_id, prm, local_blocks, local_swa=swa)
         if self.tp_size > 1:
-            self._tp_cmds.append(("load", req.request_id, dict(prm), list(local_blocks)))
+            self._tp_cmds.append(("load", req.request_id, dict(prm), list(local_blocks), swa))
 
     def cancel_load(self, request_id: str):
         """The request was aborted while its pull is queued or running. A queued
@@ -130,7 +132,8 @@ class KvxConnector:
             self.engine.bm.free(req.seq_id)
             return
         req.extra["kv_transfer_params_out"] = self.agent.hold(req.request_id, req.seq_id, blocks,
-                                                              req.num_prompt_tokens)
+                                                              req.num_prompt_tokens,
+                                                              swa_blocks=getattr(blocks, "swa", None))
 
     def tick(self):
         for h in self.agent.expired_or_freed():
@@ -160,6 +163,7 @@ class KvxFollower:
         if kt.get("kv_role", "kv_both") != "kv_consumer":
             raise NotImplementedError("kvx with TP > 1 is supported on the decode (kv_consumer) side")
         self.agent = KvxAgent(runner.kv, vmm=getattr(runner, "vmm", None), host=extra.get("side_channel_host"),
+                              kv_swa=getattr(runner, "kv_swa", None),
                               tp_rank=st.tp_rank, tp_size=st.tp_size,
                               abort_timeout=float(extra.get("abort_timeout", 480)),
                               transport=extra.get("transport", "auto"), exports=False)
@@ -168,7 +172,7 @@ class KvxFollower:
         drv = tuple(pl["driver"])
         for c in pl["kvx_cmd"]:
             if c[0] == "load":
-                self.agent.start_load(c[1], c[2], c[3], report=drv)
+                self.agent.start_load(c[1], c[2], c[3], report=drv, local_swa=c[4] if len(c) > 4 else None)
             elif c[0] == "cancel":
                 self.agent.cancel(c[1])
 

@@ -135,3 +135,52 @@ def test_hybrid_gpu_graphs_match_full_kv():
     prompts = [rng.integers(3, 500, size=n).tolist() for n in (300, 129, 17, 64)]
     assert _run(hyb, prompts, n=40) == _run(ref, prompts, n=40)
     hyb.bm.check_invariants()
+
+
+def _pd_engine(kt, **kw):
+    return _engine(None, kv_transfer_config=kt, **kw)
+
+
+@pytest.mark.parametrize("transport", ["tcp"])
+def test_hybrid_pd_transfer_matches_aggregated(transport):
+    """P/D between two hybrid caches (kvx moves the full pool's blocks and the
+    windowed pool's last-window blocks): the decoder's tokens equal an aggregated
+    full-KV engine's; the windowed table is null before the window on both sides;
+    the prefiller frees both pools after the read."""
+    import time
+
+    kt = {"kv_connector": "KvxConnector", "kv_role": "kv_both",
+          "kv_connector_extra_config": {"transport": transport}}
+    P, D = _pd_engine(kt), _pd_engine(kt)
+    assert P.runner.hybrid and D.runner.hybrid
+    ref = _engine(False)
+    prompt = np.random.default_rng(11).integers(3, 500, size=150).tolist()
+
+    def run(eng, rid, sp, ktp=None):
+        r = eng.add_request(rid, prompt, sp, kv_transfer_params=ktp)
+        for _ in range(20000):
+            for o in eng.step():
+                if o.request_id == rid and o.finished:
+                    return r, o
+            if eng.last_step_empty:
+                time.sleep(0.001)
+        raise AssertionError("request did not finish")
+
+    _, op = run(P, "p", SamplingParams(max_tokens=1, temperature=0.0, ignore_eos=True), {"do_remote_decode": True})
+    ktp = op.kv_transfer_params
+    nb = -(-150 // 16)
+    assert len(ktp["remote_block_ids"]) == nb
+    swa = ktp["remote_swa_block_ids"]
+    lo = (150 - 16 + 1) // 16  # window 16 in tiny-gpt-oss: only the last window is held
+    assert swa[:lo] == [0] * lo and 0 not in swa[lo:]
+    sp = SamplingParams(max_tokens=12, temperature=0.0, ignore_eos=True)
+    rd, od = run(D, "d", sp, ktp)
+    want = ref.generate([prompt], sp)[0].output_token_ids
+    assert rd.output_token_ids == want
+    for _ in range(300):
+        P.step()
+        if P.bm.num_free() == P.bm.num_blocks and P.bm.swa.num_free() == P.bm.swa.num_blocks:
+            break
+    assert P.bm.num_free() == P.bm.num_blocks and P.bm.swa.num_free() == P.bm.swa.num_blocks
+    P.bm.check_invariants()
+    D.bm.check_invariants()
