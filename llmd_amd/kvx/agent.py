@@ -85,8 +85,9 @@ import torch
 from llmd_amd.utils import markers
 
 log = logging.getLogger("llmd.kvx")
-# peer-pull copy engine (csrc/ops/kvx_copy.hip): 1 = LDS-staged LDS-DMA kernel (default), 0 = register-staged
-COPY_ENGINE = int(os.environ.get("LLMD_KVX_COPY_ENGINE", "1"))
+# peer-pull copy engine (csrc/ops/kvx_copy.hip): 0 = register-staged (default until the LDS-staged
+# kernel's numerics test has run on the GPU), 1 = LDS-staged through global_load_lds
+COPY_ENGINE = int(os.environ.get("LLMD_KVX_COPY_ENGINE", "0"))
 
 
 def _send(sock, obj):

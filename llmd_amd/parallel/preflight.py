@@ -7,8 +7,8 @@ Checks, each collective over the job's ranks (one process per GPU):
 
   peer     hipDeviceCanAccessPeer for every ordered pair of the job's devices
            (xGMI peer access is what IPC / VMM mappings and the symm heap use);
-  ipc      hipIpc export -> import of a neighbour's buffer + an LDS-staged
-           kvx_copy_blocks pull of it, compared byte for byte (the P/D KV pull);
+  ipc      hipIpc export -> import of a neighbour's buffer + a kvx_copy_blocks
+           pull of it (the kvx copy engine), compared byte for byte (the P/D KV pull);
   vmm      the chunked VMM (dmabuf fd over a Unix socket) export -> import of
            a neighbour's pool + the same pull (the decode pool's export path);
   symm_ar  the symm heap's one-shot and two-shot custom all-reduce vs RCCL
@@ -58,7 +58,9 @@ def _pattern(rank: int, n: int, device) -> torch.Tensor:
 def _pull(C, dst: torch.Tensor, src_ptr: int, nbytes: int):
     pairs = torch.tensor([[0, 0]], dtype=torch.int32, device=dst.device)
     segs = torch.tensor([[0, 0, nbytes]], dtype=torch.int64, device=dst.device)
-    C.kvx_copy_blocks(dst, src_ptr, nbytes, nbytes, pairs, segs, nbytes, 1)
+    from llmd_amd.kvx.agent import COPY_ENGINE  # the engine the P/D pulls will use
+
+    C.kvx_copy_blocks(dst, src_ptr, nbytes, nbytes, pairs, segs, nbytes, COPY_ENGINE)
     torch.cuda.synchronize(dst.device)
 
 
