@@ -38,6 +38,16 @@ Concurrency (the UCCL multi-path role, SURVEY N04, on one node): pulls run on
 stream, so KV from different prefillers - different xGMI links - lands in
 parallel instead of queueing behind one copy; a peer's connection, metadata
 and pool mapping are set up once under a lock and shared by the workers.
+Multi-link striping (the UCCL multi-path role; docs/infrastructure/
+rdma/README.md:36-70): on one node every GPU pair has its own xGMI link, so a
+single P->D pull over the direct link uses 1 of D's 7 links. With ``relays``
+(other kvx agents on the node, e.g. the other decoders) a pull of at least
+``stripe_min_bytes`` is split over 1 + k paths: the direct one, and per relay
+R the two-hop P->R->D path - R copies its share of blocks from P's mapped pool
+into its own IPC-exported staging buffer (one kernel, P->R link), D copies them
+from R's staging into its pool (R->D link), double-buffered in chunks so the two
+hops overlap. The shares run concurrently, so the pull spreads over 1 + k links
+(and 1 + k of P's links).
 Prefiller liveness (SGLang-style heartbeat, SURVEY M13,
 operations-sglang.md:93-98): the decode side pings every known prefiller
 every ``LLMD_KVX_HEARTBEAT_S`` (5 s) on a fresh connection; after
@@ -139,6 +149,27 @@ def _pool_info(t: torch.Tensor) -> dict:
 
 
 LEGACY_IPC_MAX = 4 << 30  # hipIpcOpenMemHandle hangs importing larger allocations
+RELAY_MB = int(os.environ.get("LLMD_KVX_RELAY_MB", "128"))  # staging per client decoder, two halves
+
+
+def _hostport(x) -> tuple:
+    if isinstance(x, (tuple, list)):
+        return (str(x[0]), int(x[1]))
+    h, p = str(x).rsplit(":", 1)
+    return (h, int(p))
+
+
+def stripe_plan(n: int, k: int) -> list[tuple[int, int]]:
+    """Split n block pairs over 1 + k paths: [start, end) of the direct path first,
+    then one range per relay (as equal as possible; empty ranges dropped)."""
+    paths = 1 + k
+    base, extra = divmod(n, paths)
+    out, a = [], 0
+    for i in range(paths):
+        b = a + base + (1 if i < extra else 0)
+        out.append((a, b))
+        a = b
+    return out
 
 _P2P_GROUP = None  # torch.distributed group spanning prefill + decode engines (rccl transport)
 
@@ -197,10 +228,18 @@ class KvxAgent:
     def __init__(self, kv: torch.Tensor, engine_id: Optional[str] = None, host: Optional[str] = None,
                  port: int = 0, tp_rank: int = 0, tp_size: int = 1, abort_timeout: float = 480.0,
                  transport: str = "auto", metrics=None, vmm: Optional[dict] = None, exports: bool = True,
-                 workers: Optional[int] = None, require_ipc: bool = False, kv_swa: Optional[torch.Tensor] = None):
+                 workers: Optional[int] = None, require_ipc: bool = False, kv_swa: Optional[torch.Tensor] = None,
+                 relays: Optional[list] = None, stripe_min_bytes: Optional[int] = None):
         self.kv = kv                      # [L, num_blocks, planes, Hkv, bs, D] (layer-major)
         self.kv_swa = kv_swa              # hybrid cache: the windowed layers' pool (same layout)
         self.require_ipc = require_ipc    # never degrade a GPU pull to TCP (bench / production P/D)
+        env_relays = [x for x in os.environ.get("LLMD_KVX_RELAYS", "").split(",") if x]
+        self.relays = [_hostport(r) for r in (relays if relays is not None else env_relays)]
+        self.stripe_min = int(stripe_min_bytes if stripe_min_bytes is not None
+                              else os.environ.get("LLMD_KVX_STRIPE_MIN_BYTES", str(64 << 20)))
+        self.relay_bufs: dict[str, tuple] = {}  # relay role: per client engine, IPC-exported staging
+        self.relay_lock = threading.Lock()
+        self.relay_use: dict[tuple, threading.Lock] = {}  # decoder role: one pull at a time per relay
         self.vmm = vmm                    # chunked exportable pool (model_runner._alloc_cache)
         self.engine_id = engine_id or f"kvx-{uuid.uuid4().hex[:12]}"
         self.tp_rank, self.tp_size = tp_rank, tp_size
@@ -347,6 +386,8 @@ class KvxAgent:
             m["ipc_handle"], m["ipc_offset"] = self.ipc_handle
         if self.p2p_sender is not None:
             m["p2p_rank"] = self.p2p_rank
+        if self.is_gpu and RELAY_MB > 0:
+            m["relay"] = {"bytes": RELAY_MB << 20}
         if self.kv_swa is not None:
             m["swa"] = _pool_info(self.kv_swa)
             if self.ipc_handle_swa is not None:
@@ -630,7 +671,10 @@ class KvxAgent:
         if use_ipc:
             try:
                 for pool, rb, lb in work:
-                    self._ipc_copy(rmeta, rb, lb, self._segments(rmeta, pool), pool)
+                    sg = self._segments(rmeta, pool)
+                    if pool == "full" and self._striped_ipc_copy(rmeta, rb, lb, sg):
+                        continue
+                    self._ipc_copy(rmeta, rb, lb, sg, pool)
             except Exception as e:  # noqa: BLE001 - mapping failed: degrade this peer to TCP
                 if self.require_ipc:
                     raise RuntimeError(f"kvx IPC pull from {rmeta.get('engine_id')} failed: {e}") from e
@@ -701,6 +745,135 @@ class KvxAgent:
                 buf = torch.empty(n * rbb, dtype=torch.uint8)
                 dist.recv(buf, src=int(rmeta["p2p_rank"]), group=_P2P_GROUP)
                 self._scatter_wire(rmeta, buf.view(n, rbb), lblocks, pool)
+
+    # ------------------------------------------------------------ relay (multi-link striping)
+    def _relay_staging(self, client: str) -> tuple:
+        """(staging tensor, (ipc handle, offset)) of one client decoder, created on first
+        use (clients never share a staging buffer, so their chunks cannot collide)."""
+        with self.relay_lock:
+            st = self.relay_bufs.get(client)
+            if st is None:
+                from llmd_amd.ops import native
+
+                buf = torch.empty(RELAY_MB << 20, dtype=torch.uint8, device=self.kv.device)
+                h, off = native().kvx_ipc_export(buf)
+                st = self.relay_bufs[client] = (buf, (bytes(h), int(off)))
+            return st
+
+    def relay_copy(self, src_meta: dict, pairs: list, segs: list, slot_bytes: int, half: int,
+                   client: str = "") -> dict:
+        """Relay side: copy blocks of a peer's pool (mapped here) into the client's
+        staging half ``half``, packed at ``slot_bytes`` per block (one kernel, src ->
+        this GPU)."""
+        from llmd_amd.ops import native
+
+        C = native()
+        buf, (h, off) = self._relay_staging(client)
+        halfb = buf.numel() // 2
+        if len(pairs) * slot_bytes > halfb:
+            raise RuntimeError(f"relay chunk of {len(pairs)} x {slot_bytes} B exceeds the staging half ({halfb} B)")
+        stream = getattr(self._tls, "rstream", None)
+        if stream is None:
+            torch.cuda.set_device(self.kv.device)
+            stream = self._tls.rstream = torch.cuda.Stream(device=self.kv.device)
+        with self.peer_lock:
+            base = self._map_peer(C, src_meta["engine_id"], src_meta)
+        dst = buf[half * halfb:(half + 1) * halfb]
+        with torch.cuda.stream(stream):
+            pr = torch.tensor(pairs, dtype=torch.int32, device=self.kv.device)
+            sg = torch.tensor(segs, dtype=torch.int64, device=self.kv.device)
+            C.kvx_copy_blocks(dst, base, slot_bytes, int(src_meta["layer_block_bytes"]), pr, sg,
+                              max(x[2] for x in segs), COPY_ENGINE)
+        stream.synchronize()
+        return {"ok": True, "ipc_handle": h, "ipc_offset": off, "half_bytes": halfb}
+
+    def _relay_pull(self, relay: tuple, rmeta: dict, rblocks: list, lblocks: list, segs: list):
+        """Decoder side of one relay path: chunks alternate between the relay's two
+        staging halves; the relay's copy of chunk i+1 (P -> R) overlaps ours of chunk i
+        (R -> D)."""
+        from llmd_amd.ops import native
+
+        C = native()
+        rp = self._peer(*relay)
+        # packed layout inside the staging: each block's segments back to back
+        slot = sum(x[2] for x in segs)
+        leg1, leg2, o = [], [], 0
+        for so, do, ln in segs:
+            leg1.append((so, o, ln))
+            leg2.append((o, do, ln))
+            o += ln
+        half_bytes = (int(rp["meta"].get("relay", {}).get("bytes", RELAY_MB << 20)) // 2)
+        per = max(1, half_bytes // slot)
+        stream = getattr(self._tls, "stream", None)
+        if stream is None:
+            torch.cuda.set_device(self.kv.device)
+            stream = self._tls.stream = torch.cuda.Stream(device=self.kv.device)
+        src_meta = {k: v for k, v in rmeta.items() if k != "swa"}
+        pending = [None, None]  # per half: event of our last copy out of it
+        base = None
+        with self.peer_lock:
+            use = self.relay_use.setdefault(relay, threading.Lock())
+        with use:  # one pull at a time through our staging on this relay
+            self._relay_chunks(C, rp, relay, src_meta, rblocks, lblocks, leg1, leg2, slot, per, stream, pending)
+
+    def _relay_chunks(self, C, rp, relay, src_meta, rblocks, lblocks, leg1, leg2, slot, per, stream, pending):
+        base = None
+        for ci, a in enumerate(range(0, len(rblocks), per)):
+            b = min(len(rblocks), a + per)
+            half = ci & 1
+            if pending[half] is not None:
+                pending[half].synchronize()  # the relay may overwrite this half only once we read it
+            r = self._rpc(rp, {"op": "relay_copy", "src": src_meta, "segs": leg1, "slot_bytes": slot, "half": half,
+                               "pairs": [[rb, i] for i, rb in enumerate(rblocks[a:b])], "client": self.engine_id})
+            if not (isinstance(r, dict) and r.get("ok")):
+                raise RuntimeError(f"kvx relay {relay[0]}:{relay[1]} failed: {r}")
+            if base is None:
+                key = f"relay:{r['ipc_handle'].hex()}"
+                with self.peer_lock:
+                    base = self.ipc_maps.get(key)
+                    if base is None:
+                        base = self.ipc_maps[key] = C.kvx_ipc_open(r["ipc_handle"]) + int(r["ipc_offset"])
+            with torch.cuda.stream(stream):
+                pr = torch.tensor([[i, lb] for i, lb in enumerate(lblocks[a:b])], dtype=torch.int32,
+                                  device=self.kv.device)
+                sg = torch.tensor(leg2, dtype=torch.int64, device=self.kv.device)
+                C.kvx_copy_blocks(self.kv, base + half * int(r["half_bytes"]), self.layer_block_bytes, slot, pr, sg,
+                                  max(x[2] for x in leg2), COPY_ENGINE)
+                ev = torch.cuda.Event()
+                ev.record(stream)
+            pending[half] = ev
+        for ev in pending:
+            if ev is not None:
+                ev.synchronize()
+
+    def _striped_ipc_copy(self, rmeta, rblocks, lblocks, segs) -> bool:
+        """Full-pool pull over the direct link + every relay, concurrently. False if
+        striping does not apply (no relays, small pull)."""
+        nbytes = sum(x[2] for x in segs) * len(rblocks)
+        if not self.relays or nbytes < self.stripe_min or len(rblocks) < 2:
+            return False
+        plan = stripe_plan(len(rblocks), len(self.relays))
+        errs = []
+
+        def leg(i, a, b):
+            try:
+                if i == 0:
+                    self._ipc_copy(rmeta, rblocks[a:b], lblocks[a:b], segs)
+                else:
+                    self._relay_pull(self.relays[i - 1], rmeta, rblocks[a:b], lblocks[a:b], segs)
+            except Exception as e:  # noqa: BLE001 - reported below
+                errs.append(e)
+
+        ts = [threading.Thread(target=leg, args=(i, a, b), daemon=True) for i, (a, b) in enumerate(plan) if b > a]
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join()
+        if errs:
+            raise RuntimeError(f"striped pull failed: {errs[0]}")
+        if self.metrics is not None and hasattr(self.metrics, "on_striped"):
+            self.metrics.on_striped(len(ts))
+        return True
 
     def _ipc_copy(self, rmeta, rblocks, lblocks, segs, pool: str = "full"):
         from llmd_amd.ops import native
@@ -820,6 +993,12 @@ class _Handler(socketserver.BaseRequestHandler):
                     agent.free_requests.put((msg.get("request_id"), int(msg.get("rank", 0)),
                                              int(msg.get("of", 1))))
                     _send(s, {"ok": True})
+                elif op == "relay_copy":  # multi-link striping: this agent relays a share of a pull
+                    try:
+                        _send(s, agent.relay_copy(msg["src"], msg["pairs"], msg["segs"], int(msg["slot_bytes"]),
+                                                  int(msg["half"]), str(msg.get("client", ""))))
+                    except Exception as e:  # noqa: BLE001 - the decoder fails the pull (-> failure policy)
+                        _send(s, {"error": f"relay: {e}"})
                 elif op == "tp_done":
                     agent.tp_report(msg["request_id"], bool(msg.get("ok")))
                     _send(s, {"ok": True})

@@ -39,6 +39,9 @@ class KvxMetrics:
         self.failed = Counter("vllm:nixl_num_failed_transfers", "Failed transfers", L, registry=r)
         # pulls that left the xGMI IPC path for the TCP fallback (0 on a healthy node)
         self.ipc_fallback = Counter("llmd:kvx_ipc_fallback", "Pulls degraded from IPC to TCP", L, registry=r)
+        self.striped = Counter("llmd:kvx_striped_pulls", "Pulls striped over the direct link + relays", L,
+                               registry=r)
+        self.n_striped = 0
         self.n_failed = 0
         self.n_ipc_fallback = 0
 
@@ -51,6 +54,10 @@ class KvxMetrics:
         self.xfer.labels(m).observe(dt)
         self.bytes.labels(m).observe(nbytes)
         self.desc.labels(m).observe(nblocks)
+
+    def on_striped(self, paths: int):
+        self.striped.labels(self.model).inc()
+        self.n_striped += 1
 
     def on_ipc_fallback(self):
         self.ipc_fallback.labels(self.model).inc()
@@ -80,7 +87,8 @@ class KvxConnector:
                                                             os.environ.get("VLLM_NIXL_ABORT_REQUEST_TIMEOUT", 480))),
                               transport=extra.get("transport", "auto"), metrics=self.metrics,
                               exports=self.role != "kv_consumer",
-                              require_ipc=bool(extra.get("require_ipc", False)))
+                              require_ipc=bool(extra.get("require_ipc", False)),
+                              relays=extra.get("relays"), stripe_min_bytes=extra.get("stripe_min_bytes"))
         self._results: dict[str, bool] = {}
         self._finished: list[str] = []
         self._outputs = []
