@@ -39,6 +39,8 @@ log = logging.getLogger("llmd.symm")
 
 CH_ALLREDUCE = 0
 CH_EP = 1
+# copy received EP rows out of the uncached heap before the expert GEMM (LLMD_EP_RECV_COPY=0: read in place)
+RECV_COPY = os.environ.get("LLMD_EP_RECV_COPY", "1") == "1"
 
 
 def _C():
@@ -211,6 +213,17 @@ class SymmEP:
         w = w.to(torch.float32).contiguous()
         C.symm_ep_dispatch(self.heap.bases, self.heap.rank, self.ch, self.layout, x, ids, w, R, E_local, self.fp8)
         rx, rid, rw = self.views(R)
+        if RECV_COPY:
+            # the heap is uncached (peers' stores must be visible without flushes): the
+            # grouped GEMM re-reads each row once per N-tile of its expert, so move the
+            # rows into cached memory once (one streaming copy) instead of re-fetching
+            # them from HBM every time
+            if self.fp8:
+                from llmd_amd.ops import Fp8Rows
+
+                rx = Fp8Rows(rx.q.clone(), rx.s.clone(), rx.d)
+            else:
+                rx = rx.clone()
         y = expert_fn(rx, rid, rw)
         out = torch.empty_like(x)
         C.symm_ep_combine(self.heap.bases, self.heap.rank, self.ch, self.layout, y.contiguous(), ids, R, E_local,

@@ -6,6 +6,10 @@ timeout -k 10 500 python -u -m pytest tests/test_kernels_prod_shapes.py -q -x --
 rc=$?
 tail -4 gpurun_out/r4b_prod_shapes.log
 [ $rc -ne 0 ] && { grep -E "Error|error|FAILED|assert|Mismatch" gpurun_out/r4b_prod_shapes.log | head -30; exit $rc; }
+timeout -k 10 200 python -u scripts/bench_ep_recv.py > gpurun_out/ep_recv.log 2>&1
+rc=$?
+grep -v amdgpu.ids gpurun_out/ep_recv.log | tail -4
+[ $rc -ne 0 ] && exit $rc
 timeout -k 10 900 python -u scripts/bench_wide_ep_rank.py --steps 20 --out gpurun_out/wide_ep_rank_r1.json > gpurun_out/wide_ep_rank.log 2>&1
 rc=$?
 grep -v amdgpu.ids gpurun_out/wide_ep_rank.log | tail -12
