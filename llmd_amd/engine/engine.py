@@ -49,7 +49,8 @@ class LLMEngine:
             from .hybrid_kv import HybridBlockManager
 
             self.bm = HybridBlockManager(rt, nb, self.runner.num_swa_blocks, cfg.cache.block_size,
-                                         self.runner.max_window, cfg.cache.enable_prefix_caching, ev_on)
+                                         self.runner.max_window, cfg.cache.enable_prefix_caching,
+                                         ev_on or bool(cfg.kv_offload_config), swa_events=bool(cfg.kv_offload_config))
         else:
             self.bm = rt.BlockManager(nb, cfg.cache.block_size, cfg.cache.enable_prefix_caching,
                                       ev_on or bool(cfg.kv_offload_config))
@@ -64,9 +65,9 @@ class LLMEngine:
         self.event_sink = None  # set by serving.kv_events.KVEventPublisher
         self.offload = None
         if cfg.kv_offload_config:
-            from llmd_amd.kvcache.offload import OffloadManager
+            from llmd_amd.kvcache.offload import HybridOffload, OffloadManager
 
-            self.offload = OffloadManager(cfg, self)
+            self.offload = HybridOffload(cfg, self) if self.runner.hybrid else OffloadManager(cfg, self)
             self.sched.offload = self.offload
         from llmd_amd.parallel import ep
 
@@ -266,6 +267,8 @@ class LLMEngine:
         evs = self.bm.take_events() if (self.offload is not None or self.event_sink is not None) else []
         if self.offload is not None:
             self.offload.on_block_events(evs)
+            if hasattr(self.offload, "on_swa_events"):
+                self.offload.on_swa_events(self.bm.take_swa_events())
             self.offload.after_step()
             evs = list(evs) + self.offload.take_events()
         if self.event_sink is not None and evs:

@@ -46,9 +46,10 @@ def swa_blocks(max_num_seqs: int, max_num_batched_tokens: int, window: int, bloc
 
 class HybridBlockManager:
     def __init__(self, rt, num_full_blocks: int, num_swa_blocks: int, block_size: int, window: int,
-                 prefix_caching: bool, emit_events: bool):
+                 prefix_caching: bool, emit_events: bool, swa_events: bool = False):
         self.full = rt.BlockManager(num_full_blocks, block_size, prefix_caching, emit_events)
-        self.swa = rt.BlockManager(num_swa_blocks, block_size, prefix_caching, False, 1)
+        # windowed-group events feed the offload tier only (never published to the router)
+        self.swa = rt.BlockManager(num_swa_blocks, block_size, prefix_caching, swa_events, 1)
         self.window = window
         self.block_size = block_size
         self.num_blocks = self.full.num_blocks
@@ -131,6 +132,9 @@ class HybridBlockManager:
 
     def take_events(self):
         return self.full.take_events()
+
+    def take_swa_events(self):
+        return self.swa.take_events()
 
     def take_evicted(self):
         return self.full.take_evicted()

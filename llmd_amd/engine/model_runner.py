@@ -194,18 +194,13 @@ class ModelRunner:
     # ------------------------------------------------------------ KV cache
     def _want_hybrid(self) -> bool:
         """Hybrid manager: on by default for models mixing windowed and full layers
-        (vLLM's default); off with --disable-hybrid-kv-cache-manager, and with the
-        tiered offload connector (whole-model blocks). kvx P/D moves both pools."""
+        (vLLM's default); off with --disable-hybrid-kv-cache-manager. kvx P/D and the
+        tiered offload move / store both pools."""
         flag = self.cfg.cache.hybrid_kv_cache_manager
         if not self.swa_layers or not self.full_layers or self.is_mla or flag is False:
             return False
         if self.cfg.parallel.enable_dbo:
             return False  # dual-batch graphs carry one set of tables
-        if self.cfg.kv_offload_config:
-            if flag:
-                log.warning("hybrid KV cache manager not available with the KV offload connector: "
-                            "every layer keeps full-length KV")
-            return False
         return True
 
     def layer_bytes_per_block(self) -> int:

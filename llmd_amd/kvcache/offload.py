@@ -110,13 +110,14 @@ class _LoadJob:
 
 
 class OffloadManager:
-    def __init__(self, cfg, engine):
+    def __init__(self, cfg, engine, pool: str = "full", cpu_share: float = 1.0):
         oc = dict(cfg.kv_offload_config or {})
         extra = oc.get("kv_connector_extra_config", oc)
         self.engine = engine
-        self.kv = engine.runner.kv
+        self.pool = pool  # "full": the main pool; "swa": the windowed pool of a hybrid cache
+        self.kv = engine.runner.kv if pool == "full" else engine.runner.kv_swa
         self._layout(self.kv)
-        cpu_bytes = int(extra.get("cpu_bytes_to_use", extra.get("cpu_bytes", 1 << 30)))
+        cpu_bytes = int(int(extra.get("cpu_bytes_to_use", extra.get("cpu_bytes", 1 << 30))) * cpu_share)
         self.n_slots = max(1, cpu_bytes // self.block_bytes)
         pin = self.kv.is_cuda
         self.host = torch.empty(self.n_slots, self.block_bytes, dtype=torch.uint8, pin_memory=pin)
@@ -169,7 +170,7 @@ class OffloadManager:
         return hashlib.sha256(weights_id.encode()).hexdigest()[:12]
 
     def _fs_key(self, h: int) -> str:
-        return f"{h:016x}-{self.ns}"
+        return f"{h:016x}-{self.ns}" + ("-swa" if self.pool == "swa" else "")
 
     # ------------------------------------------------------------ slab pack / unpack
     def _seg_tensors(self):
@@ -275,10 +276,16 @@ class OffloadManager:
                 ev0 = torch.cuda.Event(enable_timing=True)
                 ev0.record(self.stream)
                 stage, pairs = self._pack(blocks)
+                packed = torch.cuda.Event()
+                packed.record(self.stream)
                 for i, (h, b, slot) in enumerate(assign):
                     self.host[slot].copy_(stage[i], non_blocking=True)
                 ev = torch.cuda.Event(enable_timing=True)
                 ev.record(self.stream)
+            # a committed block can be released and re-filled by the very next step (the
+            # windowed pool recycles blocks every step): that step may write only after the
+            # gather read it (the slow D2H copies run on behind)
+            torch.cuda.current_stream().wait_event(packed)
             # the staging slab and the pair list stay referenced until the copies land, so the
             # caching allocator cannot hand their memory to the compute stream early
             self.pending.append((ev, [(h, s) for h, _, s in assign], (stage, pairs), ev0, nbytes))
@@ -391,20 +398,9 @@ class OffloadManager:
         if self.kv is None:
             return 0
         bs = bm.block_size
-        rt = _rt_loader.rt()
-        keys = rt.hash_blocks(tokens[: max(0, len(tokens) - 1)], bs, req.cache_extra)
+        keys = self.block_keys(req, tokens, bs)
         first = cached // bs
-        found = []
-        for i in range(first, len(keys)):
-            k = int(keys[i])
-            s = self.slot_of.get(k)
-            if s is not None:
-                found.append(("cpu", k, s))
-                continue
-            if self.fs is not None and self.fs.exists(self._fs_key(k)):
-                found.append(("fs", k, None))
-                continue
-            break
+        found = self.lookup_chain(keys, first)
         if not found:
             return 0
         # the reloaded prefix plus the block of the next token must fit in what is free
@@ -416,7 +412,34 @@ class OffloadManager:
             return 0
         if not bm.grow(req.seq_id, (first + n) * bs):
             return 0
-        dst = list(bm.block_table(req.seq_id)[first:first + n])
+        self.launch(req, first, list(bm.block_table(req.seq_id)[first:first + n]), found)
+        return n * bs
+
+    @staticmethod
+    def block_keys(req, tokens: np.ndarray, bs: int):
+        return _rt_loader.rt().hash_blocks(tokens[: max(0, len(tokens) - 1)], bs, req.cache_extra)
+
+    def locate(self, k: int):
+        """(tier, key, slot) of one block key in the host / disk tiers, or None."""
+        s = self.slot_of.get(k)
+        if s is not None:
+            return ("cpu", k, s)
+        if self.fs is not None and self.fs.exists(self._fs_key(k)):
+            return ("fs", k, None)
+        return None
+
+    def lookup_chain(self, keys, first: int) -> list:
+        """The consecutive run of tier-resident blocks continuing block ``first``."""
+        found = []
+        for i in range(first, len(keys)):
+            it = self.locate(int(keys[i]))
+            if it is None:
+                break
+            found.append(it)
+        return found
+
+    def launch(self, req, first: int, dst: list, found: list):
+        """Start the reload of ``found`` (locate() results) into pool blocks ``dst``."""
         job = _LoadJob(req, first, dst, [], t0=time.perf_counter())
         for tier, k, s in found:
             if tier == "cpu":
@@ -433,7 +456,6 @@ class OffloadManager:
         self.loads[req.request_id] = job
         if not job.fs_tickets:
             self._launch_copy(job)
-        return n * bs
 
     def _launch_copy(self, job: _LoadJob):
         n = len(job.items) if job.n_ok < 0 else job.n_ok
@@ -510,3 +532,130 @@ class OffloadManager:
             if r is req:
                 return ntok
         return 0
+
+
+class HybridOffload:
+    """Tiered offload of a hybrid KV cache (engine/hybrid_kv.py): one
+    OffloadManager per pool - the full-attention pool and the windowed pool,
+    each with its own host slots and FS keys (``-swa``). Both store
+    write-through on their group's BlockStored events. A reload extends a
+    prefix to block k only if the full pool's blocks [first, k) are in the tiers
+    AND the windowed pool holds (on the GPU, or in its tiers) every block of the
+    last window before k; both pools' copies run on the side stream and the
+    request continues once both landed. The windowed table is grown with real
+    blocks up to k (the ones before the window are released right after the
+    load), so a partly failed reload simply reports 0 tokens and the request
+    recomputes from its GPU-cached prefix."""
+
+    def __init__(self, cfg, engine):
+        r = engine.runner
+        fb, sb = r.block_bytes(), r.swa_block_bytes()
+        share = fb / (fb + sb)
+        self.full = OffloadManager(cfg, engine, "full", share)
+        self.swa = OffloadManager(cfg, engine, "swa", 1.0 - share)
+        self.engine = engine
+        self.window = engine.bm.window
+        self.pending: dict[str, dict] = {}  # request id -> {"req", "first", "k", "done": {pool: ntok}}
+
+    # ---- store / housekeeping: both pools
+    def on_block_events(self, events: list):
+        self.full.on_block_events(events)
+
+    def on_swa_events(self, events: list):
+        self.swa.on_block_events(events)
+
+    def before_step(self, so):
+        self.full.before_step(so)
+        self.swa.before_step(so)
+
+    def after_step(self):
+        self.full.after_step()
+        self.swa.after_step()
+
+    def take_events(self) -> list:
+        self.swa.take_events()  # windowed-pool tier changes are not published (the router indexes full blocks)
+        return self.full.take_events()
+
+    def render_metrics(self, model: str) -> bytes:
+        return self.full.render_metrics(model)
+
+    def invalidate(self, weights_id: str):
+        self.full.invalidate(weights_id)
+        self.swa.invalidate(weights_id)
+
+    def rebind(self, kv):
+        self.full.rebind(kv)
+        self.swa.rebind(None if kv is None else self.engine.runner.kv_swa)
+
+    @property
+    def stats(self):
+        return self.full.stats
+
+    # ---- reload
+    def start_load(self, req, tokens, cached: int, bm) -> int:
+        if self.full.kv is None or self.swa.kv is None:
+            return 0
+        bs = bm.block_size
+        keys = OffloadManager.block_keys(req, tokens, bs)
+        first = cached // bs
+        found = self.full.lookup_chain(keys, first)
+        if not found:
+            return 0
+        swa_tab = bm.block_table_swa(req.seq_id)
+        resident = {p for p, b in enumerate(swa_tab) if b}
+        k = first + len(found)
+        while k > first:  # longest extension whose last window is available for the windowed pool
+            lo = max(0, k * bs - self.window + 1) // bs
+            need = [p for p in range(lo, k) if p not in resident]
+            locs = [self.swa.locate(int(keys[p])) for p in need]
+            if all(x is not None for x in locs):
+                break
+            k -= 1
+        if k <= first:
+            return 0
+        n = k - first
+        need_full = -(-min(req.num_tokens, k * bs + 1) // bs) - bm.full.num_seq_blocks(req.seq_id)
+        need_swa = -(-min(req.num_tokens, k * bs + 1) // bs) - bm.swa.num_seq_blocks(req.seq_id)
+        if bm.full.num_free() < need_full or bm.swa.num_free() < need_swa:
+            return 0
+        if not bm.grow(req.seq_id, k * bs):
+            return 0
+        self.full.launch(req, first, list(bm.block_table(req.seq_id)[first:k]), found[:n])
+        swa_tab = bm.block_table_swa(req.seq_id)
+        self.pending[req.request_id] = {"req": req, "n": n * bs, "ok": True, "wait": {"full"}}
+        if need:
+            self.swa.launch(req, need[0], [swa_tab[p] for p in need], locs)
+            self.pending[req.request_id]["wait"].add("swa")
+            self.pending[req.request_id]["swa_n"] = len(need) * bs
+        return n * bs
+
+    def poll_loads(self) -> list:
+        out = []
+        for name, mgr in (("full", self.full), ("swa", self.swa)):
+            for req, ntok in mgr.poll_loads():
+                st = self.pending.get(req.request_id)
+                if st is None:
+                    continue
+                want = st["n"] if name == "full" else st.get("swa_n", 0)
+                st["ok"] = st["ok"] and ntok == want
+                st["wait"].discard(name)
+        for rid, st in list(self.pending.items()):
+            if st["wait"]:
+                continue
+            del self.pending[rid]
+            req = st["req"]
+            ntok = st["n"] if st["ok"] else 0
+            if ntok and not req.status.finished:
+                # blocks before the window of the next query were grown only to keep the
+                # table dense: release them now
+                self.engine.bm.after_compute(req.seq_id, req.num_computed_tokens + ntok)
+            out.append((req, ntok))
+        return out
+
+    def cancel_load(self, request_id: str):
+        self.full.cancel_load(request_id)
+        self.swa.cancel_load(request_id)
+
+    @property
+    def loads(self):
+        return {**self.swa.loads, **self.full.loads}

@@ -184,3 +184,36 @@ def test_hybrid_pd_transfer_matches_aggregated(transport):
     assert P.bm.num_free() == P.bm.num_blocks and P.bm.swa.num_free() == P.bm.swa.num_blocks
     P.bm.check_invariants()
     D.bm.check_invariants()
+
+
+@pytest.mark.parametrize("tier", ["cpu", "fs"])
+def test_hybrid_tiered_offload_reload(tier, tmp_path):
+    """Tiered offload of a hybrid cache: both pools store write-through (host slots
+    split by block bytes, FS keys of the windowed pool suffixed), a reload after the
+    GPU prefix cache is dropped brings back the full pool's prefix and the windowed
+    pool's last window, and the tokens equal a full-KV engine's."""
+    kw = {"cpu_bytes_to_use": 64 << 20}
+    if tier == "fs":
+        kw["fs_root"] = str(tmp_path / "kv")
+    prompt = np.random.default_rng(21).integers(3, 500, size=150).tolist()
+    sp = SamplingParams(max_tokens=10, temperature=0.0, ignore_eos=True)
+    want = _engine(False).generate([prompt], sp)[0].output_token_ids
+    eng = _engine(None, kv_offload_config=kw)
+    assert eng.runner.hybrid
+    assert eng.generate([prompt], sp)[0].output_token_ids == want
+    off = eng.offload
+    off.full.poll()
+    off.swa.poll()
+    assert off.full.stats["offloaded"] >= 150 // 16 and off.swa.stats["offloaded"] >= 150 // 16
+    if tier == "fs":
+        off.full.fs.flush()
+        off.swa.fs.flush()
+        eng = _engine(None, kv_offload_config=kw)  # fresh engine: empty GPU + host tiers
+        off = eng.offload
+    else:
+        eng.reset_prefix_cache()
+    assert eng.generate([prompt], sp)[0].output_token_ids == want
+    key = "loaded_cpu" if tier == "cpu" else "loaded_fs"
+    assert off.full.stats[key] >= 150 // 16 - 1
+    assert 1 <= off.swa.stats[key] <= 3  # only the last window of the windowed pool
+    eng.bm.check_invariants()
