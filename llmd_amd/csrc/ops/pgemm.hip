@@ -475,7 +475,10 @@ __global__ __launch_bounds__(NT4, 1) void pgemm4_kernel(const uint16_t* __restri
     __builtin_amdgcn_s_waitcnt(0xC07F);  // the prologue fragments, visibly to hipcc (else it re-waits in the loop)
     bar();
   }
-  int issued = min(4, nq);
+  // every wave has read half 0 out of slot 0: refill it with half 4 (K-step 2, half 0) - the
+  // loop's boundaries refill only the slots their own substeps read
+  if (4 < nq) issue(4);
+  int issued = min(5, nq);
   // every K-step in one loop body (a peeled last step makes hipcc re-home the
   // accumulators through VGPRs): the last step's read-ahead of the nonexistent next
   // half reads a stale slot into registers nothing consumes, its waits drain to 0
