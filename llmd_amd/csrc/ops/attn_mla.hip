@@ -251,12 +251,32 @@ __global__ __launch_bounds__(64 * NW, 1) void mla_v2_kernel(
   __shared__ __attribute__((aligned(1024))) char buf0[V2_TILE];
   __shared__ __attribute__((aligned(1024))) char buf1[V2_TILE];
   const uint16_t* kc = reinterpret_cast<const uint16_t*>(kcv);
-  const int sp = blockIdx.x, r = blockIdx.z;
+  // Two head groups (NW = 4 at H = 128) read the same K/V tiles. Workgroups are
+  // handed to the 8 XCDs round-robin in id order, so the natural ids (x = split
+  // fastest) put the two groups of one (split, row) on different XCDs and every
+  // tile crosses HBM twice. Re-pair them: ids L and L + 8 (same XCD, one dispatch
+  // round apart) are the two groups of one (split, row), so the second group's
+  // tiles come out of that XCD's L2 (speed only: any placement stays correct).
+  int sp = blockIdx.x, hgrp = blockIdx.y, r = blockIdx.z;
+  if (gridDim.y == 2) {
+    const int L = blockIdx.x + gridDim.x * (blockIdx.y + 2 * blockIdx.z);
+    const int total = gridDim.x * 2 * gridDim.z, full = total / 16 * 16;
+    int pidx;
+    if (L < full) {
+      hgrp = (L & 15) >> 3;
+      pidx = (L >> 4) * 8 + (L & 7);
+    } else {
+      hgrp = (L - full) & 1;
+      pidx = full / 2 + ((L - full) >> 1);
+    }
+    sp = pidx % gridDim.x;
+    r = pidx / gridDim.x;
+  }
   const int len = row_len[r];
   if (split_dev) split_size = *split_dev;  // hipGraph replay: keys per split sized to this step's rows
   const int k0 = sp * split_size, k1 = min(len, k0 + split_size);
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, g = lane >> 4, c16 = lane & 15;
-  const int h0 = 16 * (NW * blockIdx.y + w);  // this wave's first head
+  const int h0 = 16 * (NW * hgrp + w);  // this wave's first head
   const int head = h0 + c16;
   const int* bt = block_tables + (int64_t)row_seq[r] * bt_stride;
   const int lbs = __builtin_ctz(bs);

@@ -164,9 +164,11 @@ def check_vmm(rank, world, dev, grp, devices) -> str:
 def check_symm_ar(rank, world, dev, grp, devices, rccl=None) -> str:
     from llmd_amd.parallel import symm
 
-    heap = symm.SymmHeap(32 << 20, rank, world, grp, device=dev)
+    max_bytes = 8 << 20
+    slot = symm._align(max(256 << 10, max_bytes // world + 16), 256)  # CustomAllReduce's slot size
+    heap = symm.SymmHeap(4 * world * slot + (2 << 20), rank, world, grp, device=dev)
     try:
-        ar = symm.CustomAllReduce(heap, max_bytes=8 << 20, oneshot_max=256 << 10)
+        ar = symm.CustomAllReduce(heap, max_bytes=max_bytes, oneshot_max=256 << 10)
         out = []
         for n in (4096, 96 * 1024, 1 << 20, 3 * (1 << 20) + 8 * 5):  # one-shot and two-shot sizes
             g = torch.Generator(device="cpu").manual_seed(31 * rank + n)

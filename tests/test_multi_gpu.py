@@ -78,7 +78,7 @@ def test_preflight_two_ranks_one_gpu():
     """1-GPU rehearsal: IPC + VMM pulls and the symm all-reduce (vs gloo's sum, bit for bit)."""
     res = _run_ranks(2, "0", ["ipc", "vmm", "symm_ar"], "gloo")
     for k in ("ipc", "vmm", "symm_ar"):
-        assert res["preflight"][k]["ok"], res
+        assert res["preflight"][k]["ok"], (k, res["preflight"][k])
 
 
 @pytest.mark.skipif(NGPU < 2, reason="needs 2 GPUs")
