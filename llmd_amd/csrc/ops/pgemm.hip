@@ -389,14 +389,17 @@ __global__ __launch_bounds__(NT4, 1) void pgemm4_kernel(const uint16_t* __restri
     aoff[j] = (uint32_t)(min(m0 + row, M - 1) * lda + c * 8);
     woff[j] = (uint32_t)((n0 + row) * ldw + c * 8);
   }
-  // half index q = 2 * kt + h, slot (kt & 1) * 2 + h = q & 3
-  auto issue = [&](int q) {
+  // half index q = 2 * kt + h, slot (kt & 1) * 2 + h = q & 3; a half is 8 LDS-DMA pieces per wave
+  // (A rows 0..3, W rows 4..7)
+  auto issue_piece = [&](int q, int p) {
     char* dst = lds + (q & 3) * SLOT4 + (4 * w) * 1024;
     const int k0 = (q >> 1) * BK + (q & 1) * 32;
+    if (p < 4) dma16(A + aoff[p] + k0, dst + p * 1024);
+    else dma16(W + woff[p - 4] + k0, dst + 16384 + (p - 4) * 1024);
+  };
+  auto issue = [&](int q) {
 #pragma unroll
-    for (int j = 0; j < 4; ++j) dma16(A + aoff[j] + k0, dst + j * 1024);
-#pragma unroll
-    for (int j = 0; j < 4; ++j) dma16(W + woff[j] + k0, dst + 16384 + j * 1024);
+    for (int p = 0; p < 8; ++p) issue_piece(q, p);
   };
   const int nq = 2 * nk;
 
@@ -415,38 +418,34 @@ __global__ __launch_bounds__(NT4, 1) void pgemm4_kernel(const uint16_t* __restri
   asm volatile("s_nop 4" ::: "memory");  // v_accvgpr_write (zero init) -> MFMA srcC
   __builtin_amdgcn_sched_barrier(0);
 
-  // MFMAs of one substep on (fa, fw) with the next substep's 16 fragment reads from
-  // `nxt` interleaved (1 read per 4 MFMA) into (na, nw)
-#define PG4_SUBSTEP(fa, fw, na, nw, nxt, do_read)                                                          \
+  // One substep = 64 MFMAs on (fa, fw), row i of 8 at a time. Around each row: the next
+  // substep's two fragment reads of row i (from `nxt` into na / nw) before it, and one of
+  // the 8 LDS-DMA pieces of half `dq` (the refill of the slot the PREVIOUS substep read)
+  // after it - DMA issue costs ~60-180 cycles each, so it must ride inside the MFMA stream,
+  // not stall the wave at the boundary.
+#define PG4_SUBSTEP(fa, fw, na, nw, nxt, dq)                                                               \
   {                                                                                                        \
     const char* nb_ = (nxt);                                                                               \
+    const bool dma_ = (dq) < nq;                                                                           \
     _Pragma("unroll") for (int i = 0; i < 8; ++i) {                                                        \
-      if (do_read) {                                                                                       \
-        na[i] = *reinterpret_cast<const s16x8_t*>(nb_ + a_rd + i * 1024);                                  \
-        nw[i] = *reinterpret_cast<const s16x8_t*>(nb_ + w_rd + i * 1024);                                  \
-      }                                                                                                    \
+      na[i] = *reinterpret_cast<const s16x8_t*>(nb_ + a_rd + i * 1024);                                    \
+      nw[i] = *reinterpret_cast<const s16x8_t*>(nb_ + w_rd + i * 1024);                                    \
       _Pragma("unroll") for (int j = 0; j < 8; ++j) mfma16_acc(acc[i][j], fw[j], fa[i]);                   \
-      if (do_read) {                                                                                       \
-        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);                                                 \
-        __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);                                                 \
-        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);                                                 \
-        __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);                                                 \
-      }                                                                                                    \
+      if (dma_) issue_piece((dq), i);                                                                      \
+      __builtin_amdgcn_sched_barrier(0);                                                                   \
     }                                                                                                      \
   }
-  // boundary: reads retired, the half read next has landed (every wave), then refill the slot whose
-  // fragments are now all in registers
-  auto boundary = [&](int wait_q, int issued_hi, int refill_q) {
+  // boundary: this wave's fragment reads retired, the half read next has landed (every wave,
+  // after the barrier)
+  auto boundary = [&](int wait_q, int issued_hi) {
     // lgkmcnt(0) as the builtin, so hipcc's waitcnt pass sees the fragment reads retired
-    // (after an asm wait it re-waits before the next substep's first MFMA, stalling on
-    // that substep's first reads)
+    // (after an asm wait it re-waits before the next substep's first MFMA)
     __builtin_amdgcn_s_waitcnt(0xC07F);
     const int younger = min(2, max(0, issued_hi - wait_q - 1));
     if (younger >= 2) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
     else if (younger == 1) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     bar();
-    if (refill_q < nq) issue(refill_q);
   };
 
   // prologue: halves 0..3 (K-steps 0, 1); read K-step 0 half 0 fragments
@@ -475,25 +474,20 @@ __global__ __launch_bounds__(NT4, 1) void pgemm4_kernel(const uint16_t* __restri
     __builtin_amdgcn_s_waitcnt(0xC07F);  // the prologue fragments, visibly to hipcc (else it re-waits in the loop)
     bar();
   }
-  // every wave has read half 0 out of slot 0: refill it with half 4 (K-step 2, half 0) - the
-  // loop's boundaries refill only the slots their own substeps read
-  if (4 < nq) issue(4);
-  int issued = min(5, nq);
-  // every K-step in one loop body (a peeled last step makes hipcc re-home the
-  // accumulators through VGPRs): the last step's read-ahead of the nonexistent next
-  // half reads a stale slot into registers nothing consumes, its waits drain to 0
+  int issued = min(4, nq);
+  // Substep u = 2 kt + s computes half u, reads half u + 1 and refills with half u + 4 the
+  // slot of half u (read by substep u - 1, retired by the boundary before u). Every K-step
+  // in one loop body (a peeled last step makes hipcc re-home the accumulators): the last
+  // step's read-ahead of the nonexistent next half reads a stale slot into registers nothing
+  // consumes, its waits drain to 0.
   for (int kt = 0; kt < nk; ++kt) {
     const int q0 = 2 * kt;
-    // substep (kt, 0): compute half q0 (fa0/fw0), read half q0 + 1
-    PG4_SUBSTEP(fa0, fw0, fa1, fw1, lds + ((q0 + 1) & 3) * SLOT4, true);
-    // its slot is fully read -> refill with q0 + 1 + 4 = half 1 of K-step kt + 2; next read: half q0 + 2
-    boundary(q0 + 2, issued, q0 + 5);
+    PG4_SUBSTEP(fa0, fw0, fa1, fw1, lds + ((q0 + 1) & 3) * SLOT4, q0 + 4);
+    if (q0 + 4 < nq) issued = q0 + 5;
+    boundary(q0 + 2, issued);
+    PG4_SUBSTEP(fa1, fw1, fa0, fw0, lds + ((q0 + 2) & 3) * SLOT4, q0 + 5);
     if (q0 + 5 < nq) issued = q0 + 6;
-    // substep (kt, 1): compute half q0 + 1, read half q0 + 2 (K-step kt + 1, half 0)
-    PG4_SUBSTEP(fa1, fw1, fa0, fw0, lds + ((q0 + 2) & 3) * SLOT4, true);
-    // refill the slot of half q0 + 2 with q0 + 6; the next substep reads half q0 + 3
-    boundary(q0 + 3, issued, q0 + 6);
-    if (q0 + 6 < nq) issued = q0 + 7;
+    boundary(q0 + 3, issued);
   }
 #undef PG4_SUBSTEP
   mfma_drain();  // the last MFMA results before the epilogue reads them (asm MFMAs are opaque to hipcc)

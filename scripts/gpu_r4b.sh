@@ -6,6 +6,10 @@ timeout -k 10 500 python -u -m pytest tests/test_kernels_prod_shapes.py -q -x --
 rc=$?
 tail -4 gpurun_out/r4b_prod_shapes.log
 [ $rc -ne 0 ] && { grep -E "Error|error|FAILED|assert|Mismatch" gpurun_out/r4b_prod_shapes.log | head -30; exit $rc; }
+timeout -k 10 200 python -u scripts/bench_attn.py --mla --ctx 4096 > gpurun_out/mla_pair.log 2>&1
+rc=$?
+grep -v amdgpu.ids gpurun_out/mla_pair.log | tail -6
+[ $rc -ne 0 ] && exit $rc
 timeout -k 10 200 python -u scripts/bench_ep_recv.py > gpurun_out/ep_recv.log 2>&1
 rc=$?
 grep -v amdgpu.ids gpurun_out/ep_recv.log | tail -4
