@@ -71,21 +71,40 @@ __device__ __forceinline__ void bar() {
   __builtin_amdgcn_sched_barrier(0);
 }
 
-template <int EPI>
-__global__ __launch_bounds__(NT, 1) void pgemm_kernel(const uint16_t* __restrict__ A, int64_t lda,
-                                                      const uint16_t* __restrict__ W, int64_t ldw,
-                                                      uint16_t* __restrict__ C, int64_t ldc, int M, int N, int K) {
-  __shared__ __attribute__((aligned(1024))) char lds[LDS_BYTES];  // the ONLY LDS object (see moe.hip G3)
-  const int tiles_m = (M + BM - 1) / BM, tiles_n = N / BN;
-  const int ntiles = tiles_m * tiles_n;
-  // XCD-contiguous logical tile id, then GROUP_M-deep grouped order
-  const int L = xcd_remap(blockIdx.x, ntiles);
+// logical tile L (XCD-contiguous, GROUP_M-deep grouped order) -> (row tile, column tile)
+__device__ __forceinline__ void tile_mn(int L, int tiles_m, int tiles_n, int& tm, int& tn) {
   const int per_group = GROUP_M * tiles_n;
   const int g = L / per_group, first_m = g * GROUP_M;
   const int gm = min(tiles_m - first_m, GROUP_M);
-  const int tm = first_m + (L % per_group) % gm, tn = (L % per_group) / gm;
+  tm = first_m + (L % per_group) % gm;
+  tn = (L % per_group) / gm;
+}
+
+// Launch forms (host: llmd_pgemm, both variants): nsplit == 1 -> tiles [tile0, tile0 + grid)
+// over the whole K (data-parallel); nsplit > 1 (EPI_F32) -> the grid covers `tail` tiles from
+// tile0 x nsplit K-ranges, each block writing its fp32 partial tile to ws[split][tile][256][256]
+// (pgemm_splitk_reduce sums them). The tail split turns a last, mostly idle wave of tiles
+// (e.g. 576 tiles = 2.25 waves over 256 CUs at M 4608, N 8192) into one short full wave.
+template <int EPI>
+__global__ __launch_bounds__(NT, 1) void pgemm_kernel(const uint16_t* __restrict__ A, int64_t lda,
+                                                      const uint16_t* __restrict__ W, int64_t ldw,
+                                                      uint16_t* __restrict__ C, int64_t ldc, int M, int N, int K,
+                                                      int tile0, int nsplit, float* __restrict__ ws) {
+  __shared__ __attribute__((aligned(1024))) char lds[LDS_BYTES];  // the ONLY LDS object (see moe.hip G3)
+  const int tiles_m = (M + BM - 1) / BM, tiles_n = N / BN;
+  // XCD-contiguous logical tile id, then GROUP_M-deep grouped order
+  const int b = xcd_remap(blockIdx.x, gridDim.x);
+  const int tail = gridDim.x / nsplit;
+  const int t_local = b % tail, split = b / tail;
+  const int nk_all = K / BK;
+  const int chunk = (nk_all + nsplit - 1) / nsplit;
+  const int kbeg = split * chunk;
+  const int nk = min(chunk, nk_all - kbeg);
+  int tm, tn;
+  tile_mn(tile0 + t_local, tiles_m, tiles_n, tm, tn);
   const int m0 = tm * BM, n0 = tn * BN;
-  const int nk = K / BK;
+  A += (int64_t)kbeg * BK;
+  W += (int64_t)kbeg * BK;
 
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
   const int wr = w >> 2, wc = w & 3;
@@ -254,6 +273,22 @@ __global__ __launch_bounds__(NT, 1) void pgemm_kernel(const uint16_t* __restrict
   for (; kt < nk; ++kt) ktile(kt, std::false_type{});
   if (__builtin_amdgcn_readfirstlane(wr) == 0) bar();  // balance the stagger
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if constexpr (EPI == EPI_F32) {
+    float* wt = ws + ((int64_t)split * tail + t_local) * (BM * BN);
+#pragma unroll
+    for (int qm = 0; qm < 2; ++qm)
+#pragma unroll
+      for (int qn = 0; qn < 2; ++qn)
+#pragma unroll
+        for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+          for (int ni = 0; ni < 2; ++ni) {
+            const int row = wr * 128 + qm * 64 + mi * 16 + (lane & 15);
+            const int col = wc * 64 + qn * 32 + ni * 16 + (lane >> 4) * 4;
+            *reinterpret_cast<f32x4_t*>(wt + row * BN + col) = acc[qm][qn][mi][ni];
+          }
+    return;
+  }
   __syncthreads();
 
   // ---- epilogue: acc[qm][qn][mi][ni][r] = C[m][n] with
@@ -342,20 +377,7 @@ __device__ __forceinline__ int swz4(int row, int c) {
   return c ^ ((0x1E >> (2 * ((row >> 2) & 3))) & 3);
 }
 
-// logical tile L (XCD-contiguous, GROUP_M-deep grouped order) -> (row tile, column tile)
-__device__ __forceinline__ void tile_mn(int L, int tiles_m, int tiles_n, int& tm, int& tn) {
-  const int per_group = GROUP_M * tiles_n;
-  const int g = L / per_group, first_m = g * GROUP_M;
-  const int gm = min(tiles_m - first_m, GROUP_M);
-  tm = first_m + (L % per_group) % gm;
-  tn = (L % per_group) / gm;
-}
-
-// Launch forms (host: llmd_pgemm): nsplit == 1 -> tiles [tile0, tile0 + grid) over the whole K
-// (data-parallel); nsplit > 1 (EPI_F32) -> the grid covers `tail` tiles from tile0 x nsplit
-// K-ranges, each block writing its fp32 partial tile to ws[split][tile][256][256]
-// (pgemm_splitk_reduce sums them). The tail split turns a last, mostly idle wave of tiles
-// (e.g. 576 tiles = 2.25 waves over 256 CUs at M 4608, N 8192) into one short full wave.
+// Same launch forms as pgemm_kernel (tile0 / nsplit / ws).
 template <int EPI>
 __global__ __launch_bounds__(NT4, 1) void pgemm4_kernel(const uint16_t* __restrict__ A, int64_t lda,
                                                         const uint16_t* __restrict__ W, int64_t ldw,
@@ -595,7 +617,7 @@ __host__ inline void pgemm_plan(int M, int N, int K, int epi, int& full, int& ta
 }  // namespace
 
 extern "C" int64_t llmd_pgemm_ws_bytes(int M, int N, int K, int epi, int variant) {
-  if (variant != 1 || M <= 0 || N % BN || K % BK) return 0;
+  if (M <= 0 || N % BN || K % BK) return 0;
   int full, tail, nsplit;
   pgemm_plan(M, N, K, epi, full, tail, nsplit);
   return nsplit > 1 ? (int64_t)nsplit * tail * BM * BN * 4 : 0;
@@ -630,11 +652,22 @@ extern "C" int llmd_pgemm(const void* A, int64_t lda, const void* W, int64_t ldw
     }
     return (int)hipGetLastError();
   }
+  int full = ntiles, tail = 0, nsplit = 1;
+  if (ws != nullptr) pgemm_plan(M, N, K, epi, full, tail, nsplit);
+  const auto* a = (const uint16_t*)A;
+  const auto* w = (const uint16_t*)W;
+  auto* c = (uint16_t*)C;
   if (epi == EPI_SILU)
-    hipLaunchKernelGGL(pgemm_kernel<EPI_SILU>, dim3(ntiles), dim3(NT), 0, st, (const uint16_t*)A, lda,
-                       (const uint16_t*)W, ldw, (uint16_t*)C, ldc, M, N, K);
-  else
-    hipLaunchKernelGGL(pgemm_kernel<EPI_NONE>, dim3(ntiles), dim3(NT), 0, st, (const uint16_t*)A, lda,
-                       (const uint16_t*)W, ldw, (uint16_t*)C, ldc, M, N, K);
+    hipLaunchKernelGGL(pgemm_kernel<EPI_SILU>, dim3(full), dim3(NT), 0, st, a, lda, w, ldw, c, ldc, M, N, K, 0, 1,
+                       nullptr);
+  else if (full > 0)
+    hipLaunchKernelGGL(pgemm_kernel<EPI_NONE>, dim3(full), dim3(NT), 0, st, a, lda, w, ldw, c, ldc, M, N, K, 0, 1,
+                       nullptr);
+  if (nsplit > 1) {
+    hipLaunchKernelGGL(pgemm_kernel<EPI_F32>, dim3(tail * nsplit), dim3(NT), 0, st, a, lda, w, ldw, c, ldc, M, N, K,
+                       full, nsplit, (float*)ws);
+    hipLaunchKernelGGL(pgemm_splitk_reduce, dim3(tail * (BM / 8)), dim3(256), 0, st, (const float*)ws, nsplit, tail,
+                       full, c, ldc, M, N);
+  }
   return (int)hipGetLastError();
 }

@@ -935,7 +935,7 @@ def mgemm_ok(x: torch.Tensor, w: torch.Tensor) -> bool:
 _MGEMM_MS = (64, 96, 128)
 
 
-PGEMM_VARIANT = int(os.environ.get("LLMD_PGEMM_VARIANT", "1"))
+PGEMM_VARIANT = int(os.environ.get("LLMD_PGEMM_VARIANT", "0"))
 
 
 def pgemm(x: torch.Tensor, w: torch.Tensor, epi: int = 0, out: Optional[torch.Tensor] = None,

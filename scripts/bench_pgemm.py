@@ -62,10 +62,11 @@ def main():
             y = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
             flops = 2.0 * M * N * K
             it = max(3, int(2e13 / flops))
-            res = {"blas": [], "v0": [], "v1": [], "v1sk": []}
+            res = {"blas": [], "v0": [], "v0sk": [], "v1": [], "v1sk": []}
             for _ in range(a.rounds):
                 res["blas"].append(timeit(lambda: F.linear(x, w), it))
-                res["v0"].append(timeit(lambda: ops.pgemm(x, w, out=y, variant=0), it))
+                res["v0"].append(timeit(lambda: ops.pgemm(x, w, out=y, variant=0, split_k=False), it))
+                res["v0sk"].append(timeit(lambda: ops.pgemm(x, w, out=y, variant=0), it))
                 res["v1"].append(timeit(lambda: ops.pgemm(x, w, out=y, variant=1, split_k=False), it))
                 res["v1sk"].append(timeit(lambda: ops.pgemm(x, w, out=y, variant=1), it))
             d = max((ops.pgemm(x, w, variant=v).float() - F.linear(x, w).float()).abs().max().item() for v in (0, 1))

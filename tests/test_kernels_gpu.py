@@ -212,7 +212,7 @@ def test_pgemm(M, N, K, variant):
     """Prefill GEMM (256 x 256 LDS-DMA tiles, counted-vmcnt pipeline) vs the fp32
     reference; K = 64 and 128 exercise the prologue / tail waits without a steady state;
     odd M the clamped rows. Fused SiLU-and-mul epilogue on the interleaved gate/up layout.
-    Variant 1 with and without the split-K tail: (1000, 1280, 2048) = 20 tiles in 4 splits,
+    Both variants with and without the split-K tail: (1000, 1280, 2048) = 20 tiles in 4 splits,
     (300, 512, 8192) = tail only (16 splits), (4608, 8192, 8192) = 512 data-parallel tiles +
     64 tail tiles in 4 splits (the 70B o-projection at a 4608-token step)."""
     torch.manual_seed(11)
@@ -220,8 +220,7 @@ def test_pgemm(M, N, K, variant):
     w = ((torch.rand(N, K, device=DEV) * 2 - 1) * 0.05).to(torch.bfloat16)
     ref = x.float() @ w.float().t()
     _close(ops.pgemm(x, w, variant=variant), ref, atol=2e-2, rtol=2e-2)
-    if variant == 1:
-        _close(ops.pgemm(x, w, variant=1, split_k=False), ref, atol=2e-2, rtol=2e-2)
+    _close(ops.pgemm(x, w, variant=variant, split_k=False), ref, atol=2e-2, rtol=2e-2)
     g, u = ref[:, : N // 2], ref[:, N // 2:]
     _close(ops.pgemm(x, ops.pgemm_pack_gate_up(w), epi=1, variant=variant), g * torch.sigmoid(g) * u,
            atol=2e-2, rtol=3e-2)
