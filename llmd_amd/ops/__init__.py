@@ -6,6 +6,7 @@ on a GPU host the call raises (no silent eager fallback). CPU tensors use
 """
 from __future__ import annotations
 
+import logging
 import math
 import os
 from typing import Optional
@@ -13,6 +14,8 @@ from typing import Optional
 import torch
 
 from . import reference as ref
+
+log = logging.getLogger("llmd.ops")
 
 _C = None
 _C_ERR: Exception | None = None
@@ -983,12 +986,54 @@ def mgemm_choice(M: int, N: int, K: int) -> Optional[tuple[int, int, int]]:
     return None
 
 
+# Prefill-sized GEMMs: the hand-written prefill GEMM (pgemm, v0 + split-K tail) where it
+# beats hipBLASLt ON THIS SHAPE. hipBLASLt's kernel choice swings with M (profiles/
+# pgemm_r4_v0_v1_blas.txt: at M 5064 its o / down projections run at ~1.0 PF/s, pgemm at
+# 1.34 / 1.38; Llama-3-8B's down projection at M 4608: 0.77 vs 0.42 ms) while it wins most
+# aligned shapes, so the choice is measured once per (M bucket of 256 rows, N, K) on the
+# operands themselves - two timed runs each, outside graph capture - and cached.
+PGEMM_AUTO = os.environ.get("LLMD_PGEMM_AUTO", "1") == "1"
+PGEMM_MIN_M = int(os.environ.get("LLMD_PGEMM_MIN_M", "1024"))
+_pgemm_pick: dict = {}
+
+
+def _time_ms(fn, reps: int = 2) -> float:
+    fn()
+    st, en = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    st.record()
+    for _ in range(reps):
+        fn()
+    en.record()
+    en.synchronize()
+    return st.elapsed_time(en) / reps
+
+
+def pgemm_wins(x: torch.Tensor, w: torch.Tensor) -> bool:
+    M, (N, K) = x.shape[0], w.shape
+    key = ((M + 255) // 256, N, K)
+    c = _pgemm_pick.get(key)
+    if c is None:
+        if torch.cuda.is_current_stream_capturing():
+            return False
+        y = torch.empty(M, N, dtype=x.dtype, device=x.device)
+        t_pg = _time_ms(lambda: pgemm(x, w, out=y))
+        t_bl = _time_ms(lambda: torch.nn.functional.linear(x, w))
+        c = _pgemm_pick[key] = t_pg < 0.97 * t_bl
+        log.debug("prefill GEMM M~%d N=%d K=%d: pgemm %.3f ms, hipBLASLt %.3f ms -> %s", M, N, K, t_pg, t_bl,
+                  "pgemm" if c else "hipBLASLt")
+    return c
+
+
 def linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None) -> torch.Tensor:
     """Dense projection: decode-sized M on our decode GEMM kernels where their
     measured dispatch tables have them ahead of hipBLASLt - the medium-M LDS-DMA
     kernel (csrc/ops/mgemm.hip, M 33..128, ops/mgemm_table.py) first, then the
     stream kernel (csrc/ops/skinny_gemm.hip, M <= 64, ops/dgemm_table.py) -
-    everything else on hipBLASLt."""
+    prefill-sized M on the prefill GEMM where it measured faster for the shape
+    (pgemm_wins) - everything else on hipBLASLt."""
+    if PGEMM_AUTO and x.dim() == 2 and x.shape[0] >= PGEMM_MIN_M and pgemm_ok(x, w) and pgemm_wins(x, w):
+        y = pgemm(x, w)
+        return y if bias is None else y.add_(bias)
     if _SKINNY:
         M = x.shape[0] if x.dim() == 2 else 0
         if 33 <= M <= 128 and mgemm_ok(x, w):
