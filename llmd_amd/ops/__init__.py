@@ -1019,8 +1019,13 @@ def pgemm_wins(x: torch.Tensor, w: torch.Tensor) -> bool:
         t_pg = _time_ms(lambda: pgemm(x, w, out=y))
         t_bl = _time_ms(lambda: torch.nn.functional.linear(x, w))
         c = _pgemm_pick[key] = t_pg < 0.97 * t_bl
-        log.debug("prefill GEMM M~%d N=%d K=%d: pgemm %.3f ms, hipBLASLt %.3f ms -> %s", M, N, K, t_pg, t_bl,
-                  "pgemm" if c else "hipBLASLt")
+        msg = (f"prefill GEMM M~{M} N={N} K={K}: pgemm {t_pg:.3f} ms, hipBLASLt {t_bl:.3f} ms -> "
+               f"{'pgemm' if c else 'hipBLASLt'}")
+        log.debug(msg)
+        if os.environ.get("LLMD_PGEMM_VERBOSE") == "1":
+            import sys
+
+            print(msg, file=sys.stderr, flush=True)
     return c
 
 
