@@ -993,7 +993,7 @@ def mgemm_choice(M: int, N: int, K: int) -> Optional[tuple[int, int, int]]:
 # aligned shapes, so the choice is measured once per (M bucket of 256 rows, N, K) on the
 # operands themselves - two timed runs each, outside graph capture - and cached.
 PGEMM_AUTO = os.environ.get("LLMD_PGEMM_AUTO", "1") == "1"
-PGEMM_MIN_M = int(os.environ.get("LLMD_PGEMM_MIN_M", "1024"))
+PGEMM_MIN_M = int(os.environ.get("LLMD_PGEMM_MIN_M", "256"))
 _pgemm_pick: dict = {}
 
 

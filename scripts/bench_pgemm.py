@@ -31,7 +31,7 @@ def timeit(fn, iters):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--rounds", type=int, default=3)
-    ap.add_argument("--ms", default="4608,5064,8192,2048")
+    ap.add_argument("--ms", default="4608,5064,8192,2048,518")
     ap.add_argument("--shapes", default=",".join(SHAPES))
     a = ap.parse_args()
     dev = "cuda"
