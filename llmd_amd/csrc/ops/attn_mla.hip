@@ -489,6 +489,283 @@ __global__ __launch_bounds__(64 * NW, 1) void mla_v2_kernel(
   }
 }
 
+// ---------------------------------------------------------------- v3: 32 heads per wave
+// H = 128 in ONE workgroup of 4 waves, wave w owning heads 32w..32w+31 as two
+// 16-head blocks: every K fragment (S^T A operand) and every V fragment (PV B
+// operand) read from LDS feeds two MFMAs, so LDS traffic per FLOP is half of
+// v2's (whose LDS-array time about equalled its MFMA time per tile) and each
+// K/V tile crosses HBM once per row (v2 with 4-wave workgroups: twice).
+// Registers at 1 wave/SIMD (512): O = 256 accumulators held in AGPRs by asm
+// MFMAs, Q = 144 VGPRs; fragment reads are software-pipelined 4 ahead with a
+// sched_barrier per step, so the scheduler cannot hoist a tile's 200 reads
+// (hipcc's own schedule of this loop spills ~750 registers).
+// Same LDS tile image, DMA and fp8 staging as v2.
+__device__ __forceinline__ void mla_mfma2(f32x4_t& o0, f32x4_t& o1, const bf16x8_t& p0, const bf16x8_t& p1,
+                                          const bf16x8_t& v) {
+  asm volatile(
+      "v_mfma_f32_16x16x32_bf16 %0, %2, %4, %0\n\t"
+      "v_mfma_f32_16x16x32_bf16 %1, %3, %4, %1"
+      : "+a"(o0), "+a"(o1)
+      : "v"(p0), "v"(p1), "v"(v));
+}
+
+template <bool BIG, bool F8>
+__global__ __launch_bounds__(256, 1) void mla_v3_kernel(
+    const uint16_t* __restrict__ q, int64_t q_row_stride, const void* __restrict__ kcv,
+    int64_t block_stride, int bs, const int* __restrict__ block_tables, int bt_stride,
+    const int* __restrict__ row_seq, const int* __restrict__ row_len, int H, float scale_log2,
+    int split_size, const int* __restrict__ split_dev, int nsplit, uint16_t* __restrict__ out,
+    int64_t out_row_stride, float* __restrict__ part_o, float* __restrict__ part_ml, float kv_scale) {
+  constexpr int NW = 4;
+  __shared__ __attribute__((aligned(1024))) char buf0[V2_TILE];
+  __shared__ __attribute__((aligned(1024))) char buf1[V2_TILE];
+  const uint16_t* kc = reinterpret_cast<const uint16_t*>(kcv);
+  const int sp = blockIdx.x, r = blockIdx.z;
+  const int len = row_len[r];
+  if (split_dev) split_size = *split_dev;  // hipGraph replay: keys per split sized to this step's rows
+  const int k0 = sp * split_size, k1 = min(len, k0 + split_size);
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, g = lane >> 4, c16 = lane & 15;
+  const int h0 = 32 * w;  // head block hb: heads h0 + 16 hb + (0..15)
+  const int* bt = block_tables + (int64_t)row_seq[r] * bt_stride;
+  const int lbs = __builtin_ctz(bs);
+
+  float m[2] = {NEG_INF, NEG_INF}, l[2] = {0.f, 0.f};  // stats of head h0 + 16 hb + c16
+  f32x4_t o[2][32];
+#pragma unroll
+  for (int hb = 0; hb < 2; ++hb)
+#pragma unroll
+    for (int n = 0; n < 32; ++n) o[hb][n] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  asm volatile("s_nop 4" ::: "memory");  // zeroed accumulators -> asm MFMA srcC
+
+  if (k0 < k1) {
+    bf16x8_t qf[2][18];
+#pragma unroll
+    for (int hb = 0; hb < 2; ++hb) {
+      const uint16_t* qr = q + (int64_t)r * q_row_stride + (int64_t)(h0 + 16 * hb + c16) * DQK;
+#pragma unroll
+      for (int s = 0; s < 18; ++s) qf[hb][s] = *reinterpret_cast<const bf16x8_t*>(qr + 32 * s + 8 * g);
+    }
+    auto issue = [&](char* base, int ts) {
+      int64_t tile_off = 0;
+      if constexpr (BIG) tile_off = (int64_t)bt[ts >> lbs] * block_stride + (int64_t)(ts & (bs - 1)) * DQK;
+#pragma unroll
+      for (int k = 0; k < 72 / NW; ++k) {
+        int ln = lane;  // opaque: keep the per-lane DMA addressing out of the loop-invariant (spilled) set
+        asm volatile("" : "+v"(ln));
+        const int u = 64 * (w + NW * k) + ln;
+        const int row = u / CPR, ch = (u - row * CPR) ^ mla_swz(row);
+        const int key = min(ts + row, k1 - 1);
+        int64_t off;
+        if constexpr (BIG) {
+          off = tile_off + (int64_t)(key - ts) * DQK;
+        } else {
+          off = (int64_t)bt[key >> lbs] * block_stride + (int64_t)(key & (bs - 1)) * DQK;
+        }
+        __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)(kc + off + ch * 8),
+                                         (void __attribute__((address_space(3)))*)(base + 1024 * (w + NW * k)),
+                                         16, 0, 0);
+      }
+    };
+    // per-lane LDS offsets: as v2
+    const int qq = c16 >> 2, pp = c16 & 3;
+    const int srow = rowoff(c16 >> 2) + (c16 & 3), ssw = mla_swz(srow);
+    const int gx = g ^ (ssw & 2);
+    const int offE = srow * V2_ROWB + 16 * (gx + (ssw & 4));
+    const int offO = srow * V2_ROWB + 16 * (gx - (ssw & 4));
+    const int vrow = rowoff(g) + qq, vk = mla_swz(vrow) >> 1;
+    int voff[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) voff[j] = vrow * V2_ROWB + 8 * (pp & 1) + 16 * (pp >> 1) + 32 * (j ^ vk);
+    auto compute = [&](const char* kt, int ts) {
+      // K fragment j = 18 b4 + s (keys 16 b4.., k-step s); V fragment j = 32 t2 + n
+      auto kread = [&](int j) -> bf16x8_t {
+        const int b4 = j / 18, s = j % 18;
+        return *reinterpret_cast<const bf16x8_t*>(kt + ((s & 1) ? offO : offE) + b4 * 16 * V2_ROWB + 64 * s);
+      };
+      auto vread = [&](int j) -> bf16x8_t {
+        const int t2 = j >> 5, n = j & 31;
+        const char* p0 = kt + voff[n & 3] + 32 * t2 * V2_ROWB + 32 * (n & ~3);
+        s16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4_t*)p0);
+        s16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            (__attribute__((address_space(3))) s16x4_t*)(p0 + 16 * V2_ROWB));
+        return __builtin_bit_cast(bf16x8_t, s16x8_t{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]});
+      };
+      // ---- S^T[key][head] = K . Q^T over 576 dims, two head blocks per K fragment
+      f32x4_t sc[2][4];
+      bf16x8_t kr[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) kr[j] = kread(j);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int b4 = 0; b4 < 4; ++b4) {
+        f32x4_t a0 = {0.f, 0.f, 0.f, 0.f}, a1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int s = 0; s < 18; ++s) {
+          const int j = 18 * b4 + s;
+          const bf16x8_t ka = kr[j & 3];
+          if (j + 4 < 72) kr[j & 3] = kread(j + 4);
+          a0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ka, qf[0][s], a0, 0, 0, 0);
+          a1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ka, qf[1][s], a1, 0, 0, 0);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+        sc[0][b4] = a0;
+        sc[1][b4] = a1;
+      }
+      // the first V fragments load under the softmax
+      bf16x8_t vr[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) vr[j] = vread(j);
+      // rows of sc[hb][b4]: keys ts + 16 b4 + rowoff(g) + i, column: head h0 + 16 hb + c16
+      if (ts + 64 > k1) {
+#pragma unroll
+        for (int hb = 0; hb < 2; ++hb)
+#pragma unroll
+          for (int b4 = 0; b4 < 4; ++b4)
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+              if (ts + 16 * b4 + rowoff(g) + i >= k1) sc[hb][b4][i] = NEG_INF;
+      }
+      bf16x8_t pa[2][2];
+#pragma unroll
+      for (int hb = 0; hb < 2; ++hb) {
+        float mx = NEG_INF;
+#pragma unroll
+        for (int b4 = 0; b4 < 4; ++b4)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) mx = fmaxf(mx, sc[hb][b4][i]);
+        const float tl = mx * scale_log2;
+        if (__ballot(tl > m[hb] + 8.f) != 0) {  // lazy rescale (threshold 2^8), wave-uniform
+          float tm = fmaxf(tl, __shfl_xor(tl, 16, 64));
+          tm = fmaxf(tm, __shfl_xor(tm, 32, 64));
+          const float mnew = fmaxf(m[hb], tm);
+          const float alpha = (mnew == NEG_INF) ? 1.f : __builtin_amdgcn_exp2f(m[hb] - mnew);
+          l[hb] *= alpha;
+          m[hb] = mnew;
+          asm volatile("s_nop 7\n\ts_nop 7" ::: "memory");  // asm MFMA results settled before the reads
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const float a = __shfl(alpha, 4 * g + i, 64);
+#pragma unroll
+            for (int n = 0; n < 32; ++n) o[hb][n][i] *= a;
+          }
+          asm volatile("s_nop 4" ::: "memory");  // accumulator writes -> MFMA srcC
+        }
+        const float msub = (m[hb] == NEG_INF) ? 0.f : m[hb];
+        float ps = 0.f;
+#pragma unroll
+        for (int b4 = 0; b4 < 4; ++b4)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const float p = __builtin_amdgcn_exp2f(fmaf(sc[hb][b4][i], scale_log2, -msub));
+            sc[hb][b4][i] = p;
+            ps += p;
+          }
+        l[hb] += ps;
+#pragma unroll
+        for (int t2 = 0; t2 < 2; ++t2)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            pa[hb][t2][j] = (__bf16)sc[hb][2 * t2][j];
+            pa[hb][t2][4 + j] = (__bf16)sc[hb][2 * t2 + 1][j];
+          }
+      }
+      asm volatile("s_nop 1" ::: "memory");  // pa (VALU) -> asm MFMA operand
+      __builtin_amdgcn_sched_barrier(0);
+      // ---- O[head][dim] += P[head][key] . V[key][dim]   (V = first 512 dims of the key row)
+#pragma unroll
+      for (int j = 0; j < 64; ++j) {
+        const bf16x8_t vb = vr[j & 3];
+        if (j + 4 < 64) vr[j & 3] = vread(j + 4);
+        const int t2 = j >> 5, n = j & 31;
+        mla_mfma2(o[0][n], o[1][n], pa[0][t2], pa[1][t2], vb);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    };
+    const int nt = (k1 - k0 + 63) >> 6;
+    if constexpr (F8) {
+      const uint8_t* k8 = reinterpret_cast<const uint8_t*>(kcv);
+      auto issue8 = [&](char* base, int ts) {
+        int64_t tile_off = 0;
+        if constexpr (BIG) tile_off = (int64_t)bt[ts >> lbs] * block_stride + (int64_t)(ts & (bs - 1)) * DQK;
+#pragma unroll
+        for (int k = 0; k < 9; ++k) {
+          const int j = w + NW * k;
+          const int u = 64 * j + lane;
+          const int row = u / 36, c = u - row * 36;
+          const int key = min(ts + row, k1 - 1);
+          int64_t off;
+          if constexpr (BIG) {
+            off = tile_off + (int64_t)(key - ts) * DQK;
+          } else {
+            off = (int64_t)bt[key >> lbs] * block_stride + (int64_t)(key & (bs - 1)) * DQK;
+          }
+          __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)(k8 + off + c * 16),
+                                           (void __attribute__((address_space(3)))*)(base + 1024 * j), 16, 0, 0);
+        }
+      };
+      issue8(buf1, k0);
+      for (int t = 0; t < nt; ++t) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();  // stage t landed; tile of t-1 fully consumed
+        if (t + 1 < nt) issue8(buf1 + ((t + 1) & 1) * V2_STAGE, k0 + 64 * (t + 1));
+        const char* st8 = buf1 + (t & 1) * V2_STAGE;
+#pragma unroll
+        for (int i = 0; i < 72 / NW; ++i) {
+          const int v = threadIdx.x + 64 * NW * i;
+          const int row = v / CPR, ch = v - row * CPR;
+          const u32x2_t f = *reinterpret_cast<const u32x2_t*>(st8 + row * DQK + ch * 8);
+          *reinterpret_cast<u32x4_t*>(buf0 + row * V2_ROWB + 16 * (ch ^ mla_swz(row))) = fp8x8_to_bf16x8(f);
+        }
+        __syncthreads();
+        compute(buf0, k0 + 64 * t);
+      }
+    } else {
+      issue(buf0, k0);
+      for (int t = 0; t < nt; t += 2) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (t + 1 < nt) issue(buf1, k0 + 64 * (t + 1));
+        compute(buf0, k0 + 64 * t);
+        if (t + 1 >= nt) break;
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (t + 2 < nt) issue(buf0, k0 + 64 * (t + 2));
+        compute(buf1, k0 + 64 * (t + 1));
+      }
+    }
+  }
+  asm volatile("s_nop 7\n\ts_nop 7" ::: "memory");  // last asm MFMAs -> epilogue reads
+  // ---- epilogue: O rows are heads h0 + 16 hb + 4g + i (stats in lane 4g + i), columns dims 16n + c16
+#pragma unroll
+  for (int hb = 0; hb < 2; ++hb) {
+    const int hh = h0 + 16 * hb;
+    float lt = l[hb] + __shfl_xor(l[hb], 16, 64);  // the head's 4 lane partials
+    lt += __shfl_xor(lt, 32, 64);
+    if (nsplit == 1) {
+      const float inv = lt > 0.f ? kv_scale / lt : 0.f;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float f = __shfl(inv, 4 * g + i, 64);
+        uint16_t* orow = out + (int64_t)r * out_row_stride + (int64_t)(hh + 4 * g + i) * DV;
+#pragma unroll
+        for (int n = 0; n < 32; ++n) orow[16 * n + c16] = f2bf(o[hb][n][i] * f);
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        float* po = part_o + (((int64_t)r * H + hh + 4 * g + i) * nsplit + sp) * DV;
+#pragma unroll
+        for (int n = 0; n < 32; ++n) po[16 * n + c16] = o[hb][n][i] * kv_scale;
+      }
+      if (g == 0) {
+        float* pm = part_ml + (((int64_t)r * H + hh + c16) * nsplit + sp) * 2;
+        pm[0] = m[hb];
+        pm[1] = lt;
+      }
+    }
+  }
+}
+
 __global__ __launch_bounds__(128) void mla_reduce_kernel(const float* __restrict__ part_o,
                                                          const float* __restrict__ part_ml,
                                                          const int* __restrict__ row_len, int H, int nsplit,
@@ -520,20 +797,24 @@ __global__ __launch_bounds__(128) void mla_reduce_kernel(const float* __restrict
 
 }  // namespace
 
-// v2 waves per workgroup for H = 128: 8 (all heads, 2 waves/SIMD, register
-// budget 256: the 128 accumulators + 72 Q registers spill a few dozen values)
-// or 4 (two 64-head workgroups, 1 wave/SIMD, 512 registers, no spills, each
-// K/V tile fetched twice). Measured (profiles/mla_v2.txt, round 2): 4 wins
-// bf16 decode (rows 64: 0.18 vs 0.21 ms, rows 8: 0.058 vs 0.073) and tiny fp8
-// batches, 8 wins prefill (596 vs 508 TF/s) and fp8 decode at 64 rows.
-// LLMD_MLA_NW=4|8 forces one.
-extern "C" int llmd_mla_v2_waves(int R, int fp8) {
+// Kernel shape for H = 128, as 10 * waves + head blocks per wave:
+//   81: v2, 8 waves x 16 heads (2 waves/SIMD, register budget 256: the 128
+//       accumulators + 72 Q registers spill a few dozen values);
+//   41: v2, two 64-head workgroups of 4 waves x 16 heads (1 wave/SIMD, no
+//       spills, each K/V tile fetched by both);
+//   42: v3, one workgroup of 4 waves x 32 heads.
+// Round 2 (profiles/mla_v2.txt): 41 beat 81 on bf16 decode (rows 64: 0.18 vs
+// 0.21 ms) and tiny fp8 batches, 81 won prefill and fp8 decode at 64 rows.
+// LLMD_MLA_SHAPE=41|42|81 forces one (LLMD_MLA_NW=4|8 is 41|81).
+extern "C" int llmd_mla_v2_shape(int R, int fp8) {
   static const int forced = [] {
-    const char* e = getenv("LLMD_MLA_NW");
-    return e ? atoi(e) : 0;
+    const char* e = getenv("LLMD_MLA_SHAPE");
+    if (e) return atoi(e);
+    e = getenv("LLMD_MLA_NW");
+    return e ? 10 * atoi(e) + 1 : 0;
   }();
-  if (forced == 4 || forced == 8) return forced;
-  return R <= (fp8 ? 16 : 256) ? 4 : 8;
+  if (forced == 41 || forced == 42 || forced == 81) return forced;
+  return R <= (fp8 ? 16 : 256) ? 41 : 81;
 }
 
 // v2 (64-head groups per workgroup) for 64 or 128 heads; LLMD_MLA_V1=1 forces v1
@@ -572,12 +853,24 @@ extern "C" int llmd_mla_attention(const void* q, int64_t q_row_stride, const voi
   } else {                                         \
     if (big) V2(NW, true, false); else V2(NW, false, false); \
   }
+#define V3(BIG, F8)                                                                                            \
+  hipLaunchKernelGGL((mla_v3_kernel<BIG, F8>), dim3(nsplit, 1, R), dim3(256), 0, st, (const uint16_t*)q,        \
+                     q_row_stride, kc, block_stride, bs, block_tables, bt_stride, row_seq, row_len, H, scale_log2, \
+                     split_size, split_dev, nsplit, (uint16_t*)out, out_row_stride, part_o, part_ml, kv_scale)
     const bool big = bs >= 64;
-    if (H == 128 && llmd_mla_v2_waves(R, fp8) == 8) {
+    const int shape = H == 128 ? llmd_mla_v2_shape(R, fp8) : 41;
+    if (shape == 81) {
       V2NW(8)
+    } else if (shape == 42) {
+      if (fp8) {
+        if (big) V3(true, true); else V3(false, true);
+      } else {
+        if (big) V3(true, false); else V3(false, false);
+      }
     } else {
       V2NW(4)
     }
+#undef V3
 #undef V2NW
 #undef V2
   } else {

@@ -413,6 +413,9 @@ void skinny_gemm(torch::Tensor y, torch::Tensor x, torch::Tensor w, int64_t rb, 
   TORCH_CHECK(rc == 0, "skinny_gemm failed: ", rc);
 }
 
+extern "C" int llmd_mla_v2_shape(int R, int fp8);
+int64_t mla_v2_shape(int64_t R, bool fp8) { return llmd_mla_v2_shape((int)R, fp8 ? 1 : 0); }
+
 bool skinny_supported(int64_t M, int64_t rb, int64_t occ) { return llmd_dgemm_supported((int)M, (int)rb, (int)occ); }
 
 // y [M, N] = x [M, K] . w [N, K]^T for 33 <= M <= 128 (decode batches of a P/D
@@ -938,6 +941,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {  // _C, or _C_debug (llmd_amd/build.p
   m.def("kvx_ipc_open", &kvx_ipc_open);
   m.def("kvx_ipc_close", &kvx_ipc_close);
   m.def("mla_attention", &mla_attention);
+  m.def("mla_v2_shape", &mla_v2_shape, "H=128 MLA kernel shape: 10 * waves + head blocks per wave");
   m.def("skinny_gemm", &skinny_gemm);
   m.def("skinny_supported", &skinny_supported);
   m.def("mgemm", &mgemm);

@@ -816,7 +816,8 @@ class ModelRunner:
                      torch.empty(ws_rows * self.Hq * 2, dtype=torch.float32, device=dev))
         if self.is_mla:  # fixed per-bucket latent-attention split plans + one shared workspace
             self.g_rows = torch.arange(M, dtype=torch.int32, device=dev)
-            self.mla_plans = {B: ops.mla_split_plan(self.max_model_len, B, self.Hq) for B in buckets}
+            f8 = self.kv_dtype == torch.float8_e4m3fn
+            self.mla_plans = {B: ops.mla_split_plan(self.max_model_len, B, self.Hq, fp8=f8) for B in buckets}
             need = max(B * p[1] for B, p in self.mla_plans.items())
             self.g_mla_ws = (torch.empty(need * self.Hq * 512, dtype=torch.float32, device=dev),
                              torch.empty(need * self.Hq * 2, dtype=torch.float32, device=dev))

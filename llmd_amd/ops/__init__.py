@@ -740,7 +740,7 @@ def moe_experts(x, ids, wts, w1, w2, act=0, alpha=1.702, limit=7.0, out=None, b1
     return out
 
 
-def mla_split_plan(max_len: int, rows: int, H: int, num_cus: int = 256) -> tuple[int, int]:
+def mla_split_plan(max_len: int, rows: int, H: int, num_cus: int = 256, fp8: bool = False) -> tuple[int, int]:
     """(split_size, nsplit) so rows x head-groups x splits fills ~2 WGs per CU
     (the v2 kernel runs all 64/128 heads of a row in one workgroup)."""
     v2 = H in (64, 128) and os.environ.get("LLMD_MLA_V1", "0") != "1"
@@ -748,7 +748,12 @@ def mla_split_plan(max_len: int, rows: int, H: int, num_cus: int = 256) -> tuple
         # one 147 KB-LDS workgroup per CU; a split re-loads the row's 128-head Q
         # (147 KB), so keep >= 4 tiles per split (scripts/bench_mla_split.py sweep:
         # rows 1/8/32/64/128 at ctx 4096 best at 256/256/512/1024/2048 keys)
-        groups = 1 if (H == 64 or os.environ.get("LLMD_MLA_NW", "8") != "4") else 2
+        groups = 1
+        if H == 128:
+            try:
+                groups = 2 if native().mla_v2_shape(rows, fp8) == 41 else 1
+            except (RuntimeError, ImportError, AttributeError):  # no extension (CPU planning)
+                groups = 2 if rows <= (16 if fp8 else 256) else 1
         want = max(1, min(math.ceil(max_len / 256), math.ceil(num_cus / max(1, rows * groups))))
         split = max(64, math.ceil(math.ceil(max_len / want) / 64) * 64)
         return split, math.ceil(max(1, max_len) / split)
@@ -777,7 +782,7 @@ def mla_attention(q, cache, block_tables, row_seq, row_len, H, scale, max_len=No
     if split is None:
         if max_len is None:
             max_len = int(row_len.max().item()) if R else 1
-        split = mla_split_plan(max_len, R, H)
+        split = mla_split_plan(max_len, R, H, fp8=cache.dtype == torch.float8_e4m3fn)
     split_size, nsplit = split
     if nsplit > 1:
         if workspace is None:

@@ -142,6 +142,8 @@ def main():
     ap.add_argument("--D", type=int, default=128)
     ap.add_argument("--so", default=None)
     ap.add_argument("--mla", action="store_true")
+    ap.add_argument("--mla-only", action="store_true", help="only the MLA cases")
+    ap.add_argument("--rows", type=int, default=0, help="--mla-only: just this decode batch")
     ap.add_argument("--kv-dtype", default="bf16", choices=["bf16", "fp8"])
     ap.add_argument("--decode-layout", action="store_true",
                     help="decode only: per-layer pool vs the engine's [blocks, layers, 2, ...] layout")
@@ -153,6 +155,14 @@ def main():
             decode(a.ctx, 64, 64, 8, a.D, 64)
             decode(a.ctx, 64, 64, 8, a.D, 64, layers=80)
             torch.cuda.empty_cache()
+        return
+    if a.mla_only:
+        if a.rows:
+            mla(4096, a.rows, 128)
+            return
+        mla(4096, 64, 128)
+        mla(4096, 8, 128)
+        mla(4096, 2048, 128, prefill=True)
         return
     if a.check:
         prefill(700, 300, 16, 2, a.D, 64, check=True)
