@@ -241,6 +241,21 @@ __device__ __forceinline__ int mla_swz(int r) { return (r & 2) | ((r >> 1) & 4);
 // scale and the output normalisation.
 constexpr int V2_STAGE = 64 * DQK;        // fp8 tile bytes
 
+// LDS-DMA of one 16-B piece per lane in inline asm: hipcc then keeps counting its
+// own LDS reads with lgkmcnt(N) (a global_load_lds it can see in the loop makes it
+// fall back to lgkmcnt(0) at every wait, exposing each fragment read's latency).
+// The kernel waits for these itself (vmcnt(0) before the tile barrier).
+__device__ __forceinline__ void mla_glds16(const void* gsrc, unsigned lds_dst) {
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(gsrc), "s"(lds_dst)
+               : "memory");
+}
+__device__ __forceinline__ unsigned lds_addr(const void* p) {
+  return (unsigned)(uintptr_t)(const __attribute__((address_space(3))) char*)p;
+}
+
 template <int NW, bool BIG, bool F8>
 __global__ __launch_bounds__(64 * NW, 1) void mla_v2_kernel(
     const uint16_t* __restrict__ q, int64_t q_row_stride, const void* __restrict__ kcv,
@@ -275,7 +290,8 @@ __global__ __launch_bounds__(64 * NW, 1) void mla_v2_kernel(
   const int len = row_len[r];
   if (split_dev) split_size = *split_dev;  // hipGraph replay: keys per split sized to this step's rows
   const int k0 = sp * split_size, k1 = min(len, k0 + split_size);
-  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, g = lane >> 4, c16 = lane & 15;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63, g = lane >> 4,
+            c16 = lane & 15;
   const int h0 = 16 * (NW * hgrp + w);  // this wave's first head
   const int head = h0 + c16;
   const int* bt = block_tables + (int64_t)row_seq[r] * bt_stride;
@@ -308,9 +324,7 @@ __global__ __launch_bounds__(64 * NW, 1) void mla_v2_kernel(
         } else {
           off = (int64_t)bt[key >> lbs] * block_stride + (int64_t)(key & (bs - 1)) * DQK;
         }
-        __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)(kc + off + ch * 8),
-                                         (void __attribute__((address_space(3)))*)(base + 1024 * (w + NW * k)),
-                                         16, 0, 0);
+        mla_glds16(kc + off + ch * 8, lds_addr(base) + 1024 * (w + NW * k));
       }
     };
     // Per-lane LDS offsets. The swizzle depends on row & 15 only, so every read
@@ -495,18 +509,32 @@ __global__ __launch_bounds__(64 * NW, 1) void mla_v2_kernel(
 // operand) read from LDS feeds two MFMAs, so LDS traffic per FLOP is half of
 // v2's (whose LDS-array time about equalled its MFMA time per tile) and each
 // K/V tile crosses HBM once per row (v2 with 4-wave workgroups: twice).
-// Registers at 1 wave/SIMD (512): O = 256 accumulators held in AGPRs by asm
-// MFMAs, Q = 144 VGPRs; fragment reads are software-pipelined 4 ahead with a
-// sched_barrier per step, so the scheduler cannot hoist a tile's 200 reads
-// (hipcc's own schedule of this loop spills ~750 registers).
+// Registers at 1 wave/SIMD (512): O = the 256 AGPRs, owned outright by the
+// generated asm of mla_v3_agpr.inc (gen_mla_v3.py: literal a[..] operands and
+// clobbers; hipcc's own allocation of 256 accumulators + 144 Q registers
+// re-homed and spilled hundreds of registers), Q = 144 VGPRs, scores in VGPRs
+// via asm MFMAs. Fragment reads are software-pipelined 4 ahead with a
+// sched_barrier per step, so the scheduler cannot hoist a tile's 200 reads.
 // Same LDS tile image, DMA and fp8 staging as v2.
-__device__ __forceinline__ void mla_mfma2(f32x4_t& o0, f32x4_t& o1, const bf16x8_t& p0, const bf16x8_t& p1,
-                                          const bf16x8_t& v) {
+#include "mla_v3_agpr.inc"
+
+// S^T accumulators in VGPRs (the 256 AGPRs hold O): a chain's first MFMA takes
+// C = 0 (no zeroing VALU write ahead of it), later ones accumulate in place.
+__device__ __forceinline__ void mla_mfma2_first(f32x4_t& s0, f32x4_t& s1, const bf16x8_t& k, const bf16x8_t& q0,
+                                                const bf16x8_t& q1) {
   asm volatile(
-      "v_mfma_f32_16x16x32_bf16 %0, %2, %4, %0\n\t"
-      "v_mfma_f32_16x16x32_bf16 %1, %3, %4, %1"
-      : "+a"(o0), "+a"(o1)
-      : "v"(p0), "v"(p1), "v"(v));
+      "v_mfma_f32_16x16x32_bf16 %0, %2, %3, 0\n\t"
+      "v_mfma_f32_16x16x32_bf16 %1, %2, %4, 0"
+      : "=&v"(s0), "=&v"(s1)
+      : "v"(k), "v"(q0), "v"(q1));
+}
+__device__ __forceinline__ void mla_mfma2_acc(f32x4_t& s0, f32x4_t& s1, const bf16x8_t& k, const bf16x8_t& q0,
+                                              const bf16x8_t& q1) {
+  asm volatile(
+      "v_mfma_f32_16x16x32_bf16 %0, %2, %3, %0\n\t"
+      "v_mfma_f32_16x16x32_bf16 %1, %2, %4, %1"
+      : "+v"(s0), "+v"(s1)
+      : "v"(k), "v"(q0), "v"(q1));
 }
 
 template <bool BIG, bool F8>
@@ -524,18 +552,15 @@ __global__ __launch_bounds__(256, 1) void mla_v3_kernel(
   const int len = row_len[r];
   if (split_dev) split_size = *split_dev;  // hipGraph replay: keys per split sized to this step's rows
   const int k0 = sp * split_size, k1 = min(len, k0 + split_size);
-  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, g = lane >> 4, c16 = lane & 15;
+  // wave index as a scalar: the DMA's LDS destinations stay in SGPRs
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63, g = lane >> 4,
+            c16 = lane & 15;
   const int h0 = 32 * w;  // head block hb: heads h0 + 16 hb + (0..15)
   const int* bt = block_tables + (int64_t)row_seq[r] * bt_stride;
   const int lbs = __builtin_ctz(bs);
 
   float m[2] = {NEG_INF, NEG_INF}, l[2] = {0.f, 0.f};  // stats of head h0 + 16 hb + c16
-  f32x4_t o[2][32];
-#pragma unroll
-  for (int hb = 0; hb < 2; ++hb)
-#pragma unroll
-    for (int n = 0; n < 32; ++n) o[hb][n] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-  asm volatile("s_nop 4" ::: "memory");  // zeroed accumulators -> asm MFMA srcC
+  MLA3_ZERO_ACC();  // O = a[0:255]
 
   if (k0 < k1) {
     bf16x8_t qf[2][18];
@@ -545,25 +570,35 @@ __global__ __launch_bounds__(256, 1) void mla_v3_kernel(
 #pragma unroll
       for (int s = 0; s < 18; ++s) qf[hb][s] = *reinterpret_cast<const bf16x8_t*>(qr + 32 * s + 8 * g);
     }
+    // this lane's element offset inside a 64-key tile for each of its 18 DMA pieces
+    // (slot u = 64 (w + NW k) + lane of the swizzled tile image)
+    // (< 36,864: two 16-bit offsets per register, 9 VGPRs)
+    unsigned poff[72 / NW / 2];
+#pragma unroll
+    for (int k = 0; k < 72 / NW; ++k) {
+      const int u = 64 * (w + NW * k) + lane;
+      const int row = u / CPR, ch = (u - row * CPR) ^ mla_swz(row);
+      const unsigned o = row * DQK + ch * 8;
+      if (k & 1) poff[k >> 1] |= o << 16; else poff[k >> 1] = o;
+    }
     auto issue = [&](char* base, int ts) {
-      int64_t tile_off = 0;
-      if constexpr (BIG) tile_off = (int64_t)bt[ts >> lbs] * block_stride + (int64_t)(ts & (bs - 1)) * DQK;
+      const unsigned l0 = lds_addr(base) + 1024 * w;
+      if (BIG && ts + 64 <= k1) {  // a whole tile inside one cache block
+        const uint16_t* tb = kc + (int64_t)bt[ts >> lbs] * block_stride + (int64_t)(ts & (bs - 1)) * DQK;
+#pragma unroll
+        for (int k = 0; k < 72 / NW; ++k)
+          mla_glds16(tb + ((k & 1) ? (poff[k >> 1] >> 16) : (poff[k >> 1] & 0xffffu)), l0 + 1024 * NW * k);
+        return;
+      }
 #pragma unroll
       for (int k = 0; k < 72 / NW; ++k) {
-        int ln = lane;  // opaque: keep the per-lane DMA addressing out of the loop-invariant (spilled) set
+        int ln = lane;  // opaque: this (last-tile) path's addressing is recomputed, not hoisted and spilled
         asm volatile("" : "+v"(ln));
         const int u = 64 * (w + NW * k) + ln;
         const int row = u / CPR, ch = (u - row * CPR) ^ mla_swz(row);
         const int key = min(ts + row, k1 - 1);
-        int64_t off;
-        if constexpr (BIG) {
-          off = tile_off + (int64_t)(key - ts) * DQK;
-        } else {
-          off = (int64_t)bt[key >> lbs] * block_stride + (int64_t)(key & (bs - 1)) * DQK;
-        }
-        __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)(kc + off + ch * 8),
-                                         (void __attribute__((address_space(3)))*)(base + 1024 * (w + NW * k)),
-                                         16, 0, 0);
+        const int64_t off = (int64_t)bt[key >> lbs] * block_stride + (int64_t)(key & (bs - 1)) * DQK;
+        mla_glds16(kc + off + ch * 8, l0 + 1024 * NW * k);
       }
     };
     // per-lane LDS offsets: as v2
@@ -598,23 +633,19 @@ __global__ __launch_bounds__(256, 1) void mla_v3_kernel(
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int b4 = 0; b4 < 4; ++b4) {
-        f32x4_t a0 = {0.f, 0.f, 0.f, 0.f}, a1 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int s = 0; s < 18; ++s) {
           const int j = 18 * b4 + s;
           const bf16x8_t ka = kr[j & 3];
           if (j + 4 < 72) kr[j & 3] = kread(j + 4);
-          a0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ka, qf[0][s], a0, 0, 0, 0);
-          a1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ka, qf[1][s], a1, 0, 0, 0);
+          if (s == 0)
+            mla_mfma2_first(sc[0][b4], sc[1][b4], ka, qf[0][s], qf[1][s]);
+          else
+            mla_mfma2_acc(sc[0][b4], sc[1][b4], ka, qf[0][s], qf[1][s]);
           __builtin_amdgcn_sched_barrier(0);
         }
-        sc[0][b4] = a0;
-        sc[1][b4] = a1;
       }
-      // the first V fragments load under the softmax
-      bf16x8_t vr[4];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) vr[j] = vread(j);
+      asm volatile("s_nop 7\n\ts_nop 7" ::: "memory");  // score MFMAs (asm) -> softmax VALU reads
       // rows of sc[hb][b4]: keys ts + 16 b4 + rowoff(g) + i, column: head h0 + 16 hb + c16
       if (ts + 64 > k1) {
 #pragma unroll
@@ -641,14 +672,13 @@ __global__ __launch_bounds__(256, 1) void mla_v3_kernel(
           const float alpha = (mnew == NEG_INF) ? 1.f : __builtin_amdgcn_exp2f(m[hb] - mnew);
           l[hb] *= alpha;
           m[hb] = mnew;
-          asm volatile("s_nop 7\n\ts_nop 7" ::: "memory");  // asm MFMA results settled before the reads
-#pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            const float a = __shfl(alpha, 4 * g + i, 64);
-#pragma unroll
-            for (int n = 0; n < 32; ++n) o[hb][n][i] *= a;
+          const float a0 = __shfl(alpha, 4 * g, 64), a1 = __shfl(alpha, 4 * g + 1, 64),
+                      a2 = __shfl(alpha, 4 * g + 2, 64), a3 = __shfl(alpha, 4 * g + 3, 64);
+          if (hb == 0) {
+            MLA3_RESCALE0(a0, a1, a2, a3);
+          } else {
+            MLA3_RESCALE1(a0, a1, a2, a3);
           }
-          asm volatile("s_nop 4" ::: "memory");  // accumulator writes -> MFMA srcC
         }
         const float msub = (m[hb] == NEG_INF) ? 0.f : m[hb];
         float ps = 0.f;
@@ -669,17 +699,14 @@ __global__ __launch_bounds__(256, 1) void mla_v3_kernel(
             pa[hb][t2][4 + j] = (__bf16)sc[hb][2 * t2 + 1][j];
           }
       }
+      bf16x8_t vr[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) vr[j] = vread(j);
+      __builtin_amdgcn_sched_barrier(0);
       asm volatile("s_nop 1" ::: "memory");  // pa (VALU) -> asm MFMA operand
       __builtin_amdgcn_sched_barrier(0);
       // ---- O[head][dim] += P[head][key] . V[key][dim]   (V = first 512 dims of the key row)
-#pragma unroll
-      for (int j = 0; j < 64; ++j) {
-        const bf16x8_t vb = vr[j & 3];
-        if (j + 4 < 64) vr[j & 3] = vread(j + 4);
-        const int t2 = j >> 5, n = j & 31;
-        mla_mfma2(o[0][n], o[1][n], pa[0][t2], pa[1][t2], vb);
-        __builtin_amdgcn_sched_barrier(0);
-      }
+      MLA3_PV_BLOCK
     };
     const int nt = (k1 - k0 + 63) >> 6;
     if constexpr (F8) {
@@ -734,34 +761,39 @@ __global__ __launch_bounds__(256, 1) void mla_v3_kernel(
       }
     }
   }
-  asm volatile("s_nop 7\n\ts_nop 7" ::: "memory");  // last asm MFMAs -> epilogue reads
+  MLA3_DRAIN();  // last MFMAs -> accumulator reads
   // ---- epilogue: O rows are heads h0 + 16 hb + 4g + i (stats in lane 4g + i), columns dims 16n + c16
 #pragma unroll
   for (int hb = 0; hb < 2; ++hb) {
     const int hh = h0 + 16 * hb;
     float lt = l[hb] + __shfl_xor(l[hb], 16, 64);  // the head's 4 lane partials
     lt += __shfl_xor(lt, 32, 64);
-    if (nsplit == 1) {
-      const float inv = lt > 0.f ? kv_scale / lt : 0.f;
+    const float inv = lt > 0.f ? kv_scale / lt : 0.f;
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
+    for (int i = 0; i < 4; ++i) {
+      float x[32];
+      if (hb == 0) {
+        if (i == 0) { MLA3_READ_0_0(x) } else if (i == 1) { MLA3_READ_0_1(x) }
+        else if (i == 2) { MLA3_READ_0_2(x) } else { MLA3_READ_0_3(x) }
+      } else {
+        if (i == 0) { MLA3_READ_1_0(x) } else if (i == 1) { MLA3_READ_1_1(x) }
+        else if (i == 2) { MLA3_READ_1_2(x) } else { MLA3_READ_1_3(x) }
+      }
+      if (nsplit == 1) {
         const float f = __shfl(inv, 4 * g + i, 64);
         uint16_t* orow = out + (int64_t)r * out_row_stride + (int64_t)(hh + 4 * g + i) * DV;
 #pragma unroll
-        for (int n = 0; n < 32; ++n) orow[16 * n + c16] = f2bf(o[hb][n][i] * f);
-      }
-    } else {
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
+        for (int n = 0; n < 32; ++n) orow[16 * n + c16] = f2bf(x[n] * f);
+      } else {
         float* po = part_o + (((int64_t)r * H + hh + 4 * g + i) * nsplit + sp) * DV;
 #pragma unroll
-        for (int n = 0; n < 32; ++n) po[16 * n + c16] = o[hb][n][i] * kv_scale;
+        for (int n = 0; n < 32; ++n) po[16 * n + c16] = x[n] * kv_scale;
       }
-      if (g == 0) {
-        float* pm = part_ml + (((int64_t)r * H + hh + c16) * nsplit + sp) * 2;
-        pm[0] = m[hb];
-        pm[1] = lt;
-      }
+    }
+    if (nsplit > 1 && g == 0) {
+      float* pm = part_ml + (((int64_t)r * H + hh + c16) * nsplit + sp) * 2;
+      pm[0] = m[hb];
+      pm[1] = lt;
     }
   }
 }

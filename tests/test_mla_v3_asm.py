@@ -1,0 +1,56 @@
+"""Static check of the MLA v3 kernel's register discipline (csrc/ops/attn_mla.hip,
+gen_mla_v3.py): the output accumulators are the literal AGPRs a[0:255], touched
+only by generated inline asm, so the compiled bf16 variants must have no
+hipcc-emitted v_accvgpr_* instruction, no scratch spills, and a generated
+include that matches its generator."""
+import os
+import re
+import shutil
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+OPS = os.path.join(ROOT, "llmd_amd", "csrc", "ops")
+HIPCC = "/opt/rocm/bin/hipcc"
+
+
+def test_generated_include_is_current(tmp_path):
+    gen = os.path.join(OPS, "gen_mla_v3.py")
+    inc = os.path.join(OPS, "mla_v3_agpr.inc")
+    before = open(inc).read()
+    env = dict(os.environ)
+    out = tmp_path / "copy"
+    out.mkdir()
+    shutil.copy(gen, out / "gen_mla_v3.py")
+    subprocess.run([sys.executable, str(out / "gen_mla_v3.py")], check=True, capture_output=True, env=env)
+    assert (out / "mla_v3_agpr.inc").read_text() == before
+
+
+@pytest.mark.skipif(not os.path.exists(HIPCC), reason="hipcc not installed")
+def test_v3_accumulators_only_in_asm(tmp_path):
+    s_path = tmp_path / "attn_mla.s"
+    subprocess.run([HIPCC, "--offload-arch=gfx950", "-O3", "-std=c++17",
+                    f"-I{os.path.join(ROOT, 'llmd_amd', 'csrc', 'include')}", "--cuda-device-only", "-S",
+                    os.path.join(OPS, "attn_mla.hip"), "-o", str(s_path)], check=True, capture_output=True)
+    s = s_path.read_text()
+    names = re.findall(r"^(_ZN\S*mla_v3_kernelILb[01]ELb0E\S*):", s, re.M)  # bf16 caches (F8 = false)
+    assert len(names) == 2
+    for name in names:
+        i = s.index(name + ":")
+        j = s.index(".Lfunc_end", i)
+        in_asm, stray, scratch = False, [], 0
+        for line in s[i:j].split("\n"):
+            if ";;#ASMSTART" in line:
+                in_asm = True
+            elif ";;#ASMEND" in line:
+                in_asm = False
+            elif not in_asm:
+                op = line.strip().split(" ")[0]
+                if "accvgpr" in op:
+                    stray.append(line.strip())
+                if op.startswith("scratch_"):
+                    scratch += 1
+        assert not stray, (name, stray[:5])
+        assert scratch == 0, (name, scratch)
