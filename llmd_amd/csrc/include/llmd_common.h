@@ -162,6 +162,24 @@ __device__ __forceinline__ int xcd_remap(int orig, int nwg) {
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + orig / 8;
 }
 
+// LDS-DMA of one 16-B piece per lane (global_load_lds_dwordx4) written as inline
+// asm. A global_load_lds that hipcc can see anywhere in a loop makes its waitcnt
+// pass give up on counting LDS reads (every wait becomes lgkmcnt(0), exposing
+// each fragment read's latency); issued from asm, the DMA is invisible to it and
+// the reads keep counted lgkmcnt(N) waits. The caller waits for the DMA itself
+// (s_waitcnt vmcnt(..) before the barrier that publishes the tile): hipcc emits
+// no wait for it, and __syncthreads() does not drain it.
+__device__ __forceinline__ unsigned lds_addr(const void* p) {
+  return (unsigned)(uintptr_t)(const __attribute__((address_space(3))) char*)p;
+}
+__device__ __forceinline__ void glds16(const void* gsrc, unsigned lds_dst) {
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(gsrc), "s"(__builtin_amdgcn_readfirstlane(lds_dst))
+               : "memory");
+}
+
 }  // namespace llmd
 
 #define LLMD_CHECK_LAUNCH() \

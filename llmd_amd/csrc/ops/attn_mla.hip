@@ -241,20 +241,8 @@ __device__ __forceinline__ int mla_swz(int r) { return (r & 2) | ((r >> 1) & 4);
 // scale and the output normalisation.
 constexpr int V2_STAGE = 64 * DQK;        // fp8 tile bytes
 
-// LDS-DMA of one 16-B piece per lane in inline asm: hipcc then keeps counting its
-// own LDS reads with lgkmcnt(N) (a global_load_lds it can see in the loop makes it
-// fall back to lgkmcnt(0) at every wait, exposing each fragment read's latency).
-// The kernel waits for these itself (vmcnt(0) before the tile barrier).
-__device__ __forceinline__ void mla_glds16(const void* gsrc, unsigned lds_dst) {
-  unsigned keep;
-  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
-               : "=&s"(keep)
-               : "v"(gsrc), "s"(lds_dst)
-               : "memory");
-}
-__device__ __forceinline__ unsigned lds_addr(const void* p) {
-  return (unsigned)(uintptr_t)(const __attribute__((address_space(3))) char*)p;
-}
+// LDS-DMA from inline asm (llmd_common.h glds16): hipcc keeps counted lgkmcnt waits.
+__device__ __forceinline__ void mla_glds16(const void* gsrc, unsigned lds_dst) { glds16(gsrc, lds_dst); }
 
 template <int NW, bool BIG, bool F8>
 __global__ __launch_bounds__(64 * NW, 1) void mla_v2_kernel(
@@ -835,8 +823,10 @@ __global__ __launch_bounds__(128) void mla_reduce_kernel(const float* __restrict
 //   41: v2, two 64-head workgroups of 4 waves x 16 heads (1 wave/SIMD, no
 //       spills, each K/V tile fetched by both);
 //   42: v3, one workgroup of 4 waves x 32 heads.
-// Round 2 (profiles/mla_v2.txt): 41 beat 81 on bf16 decode (rows 64: 0.18 vs
-// 0.21 ms) and tiny fp8 batches, 81 won prefill and fp8 decode at 64 rows.
+// Round 4 (profiles/mla_r4_shapes.txt, ctx 4096): 42 takes bf16 decode rows=64
+// 0.150 -> 0.113 ms and prefill rows=2048 2.68 -> 1.49 ms (81: 2.83), fp8
+// prefill 2.85 -> 2.41; at <= 16 rows 41 is as fast or faster (fp8 rows=8:
+// 0.055 vs 0.069 ms).
 // LLMD_MLA_SHAPE=41|42|81 forces one (LLMD_MLA_NW=4|8 is 41|81).
 extern "C" int llmd_mla_v2_shape(int R, int fp8) {
   static const int forced = [] {
@@ -846,7 +836,7 @@ extern "C" int llmd_mla_v2_shape(int R, int fp8) {
     return e ? 10 * atoi(e) + 1 : 0;
   }();
   if (forced == 41 || forced == 42 || forced == 81) return forced;
-  return R <= (fp8 ? 16 : 256) ? 41 : 81;
+  return R <= 16 ? 41 : 42;
 }
 
 // v2 (64-head groups per workgroup) for 64 or 128 heads; LLMD_MLA_V1=1 forces v1

@@ -417,10 +417,8 @@ __global__ __launch_bounds__(NT, 2) void prefill_v2_kernel(
 #pragma unroll
       for (int i = 0; i < NI / 4; ++i) {
         char* dst = base + 1024 * (ws + 4 * i);
-        __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)(kb + koff[i]),
-                                         (void __attribute__((address_space(3)))*)dst, 16, 0, 0);
-        __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)(vb + voff[i]),
-                                         (void __attribute__((address_space(3)))*)(dst + P2_IMG), 16, 0, 0);
+        glds16(kb + koff[i], lds_addr(dst));
+        glds16(vb + voff[i], lds_addr(dst + P2_IMG));
       }
     } else if (rlim >= 63) {
       // blocks of 16 / 32 keys: a wave-instruction's RPI rows sit in one block
@@ -433,12 +431,8 @@ __global__ __launch_bounds__(NT, 2) void prefill_v2_kernel(
         const int64_t ib = 2 * ((int64_t)bt[key0 >> lbs] * block_stride + head_off + (int64_t)(key0 & (bs - 1)) * D) -
                            (int64_t)r0 * RB;
         char* dst = base + 1024 * (ws + 4 * i);
-        __builtin_amdgcn_global_load_lds(
-            (const void __attribute__((address_space(1)))*)(reinterpret_cast<const char*>(kc) + ib + koff[i]),
-            (void __attribute__((address_space(3)))*)dst, 16, 0, 0);
-        __builtin_amdgcn_global_load_lds(
-            (const void __attribute__((address_space(1)))*)(reinterpret_cast<const char*>(vc) + ib + voff[i]),
-            (void __attribute__((address_space(3)))*)(dst + P2_IMG), 16, 0, 0);
+        glds16(reinterpret_cast<const char*>(kc) + ib + koff[i], lds_addr(dst));
+        glds16(reinterpret_cast<const char*>(vc) + ib + voff[i], lds_addr(dst + P2_IMG));
       }
     } else {
 #pragma unroll
@@ -451,12 +445,8 @@ __global__ __launch_bounds__(NT, 2) void prefill_v2_kernel(
                                     : 2 * ((int64_t)bt[key >> lbs] * block_stride + head_off +
                                            (int64_t)(key & (bs - 1)) * D) - tb;
         char* dst = base + 1024 * (ws + 4 * i);
-        __builtin_amdgcn_global_load_lds(
-            (const void __attribute__((address_space(1)))*)(kb + ro + 16 * (sl ^ p2_pk<D>(row))),
-            (void __attribute__((address_space(3)))*)dst, 16, 0, 0);
-        __builtin_amdgcn_global_load_lds(
-            (const void __attribute__((address_space(1)))*)(vb + ro + 16 * (sl ^ p2_pv<D>(row))),
-            (void __attribute__((address_space(3)))*)(dst + P2_IMG), 16, 0, 0);
+        glds16(kb + ro + 16 * (sl ^ p2_pk<D>(row)), lds_addr(dst));
+        glds16(vb + ro + 16 * (sl ^ p2_pv<D>(row)), lds_addr(dst + P2_IMG));
       }
     }
   };

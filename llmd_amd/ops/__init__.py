@@ -753,7 +753,7 @@ def mla_split_plan(max_len: int, rows: int, H: int, num_cus: int = 256, fp8: boo
             try:
                 groups = 2 if native().mla_v2_shape(rows, fp8) == 41 else 1
             except (RuntimeError, ImportError, AttributeError):  # no extension (CPU planning)
-                groups = 2 if rows <= (16 if fp8 else 256) else 1
+                groups = 2 if rows <= 16 else 1
         want = max(1, min(math.ceil(max_len / 256), math.ceil(num_cus / max(1, rows * groups))))
         split = max(64, math.ceil(math.ceil(max_len / want) / 64) * 64)
         return split, math.ceil(max(1, max_len) / split)

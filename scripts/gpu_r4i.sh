@@ -1,0 +1,16 @@
+# round 4 (i): numerics after the asm LDS-DMA change (prefill v2, MLA v2/v3), MLA split sweep
+# with the v3 default, kernel-level MLA breakdown, GQA prefill/decode timing
+set -o pipefail
+mkdir -p gpurun_out
+R=$GRAFT_REPO_ROOT
+timeout -k 10 400 python -u -m pytest tests/test_kernels_gpu.py tests/test_deepseek.py tests/test_kernels_prod_shapes.py -q -x --timeout 240 --timeout-method thread -p no:cacheprovider > gpurun_out/r4i_tests.log 2>&1
+rc=$?
+tail -3 gpurun_out/r4i_tests.log
+[ $rc -ne 0 ] && { grep -E "^E |Error|FAILED" gpurun_out/r4i_tests.log | head -20; exit $rc; }
+timeout -k 10 300 python -u scripts/bench_mla_split.py > gpurun_out/mla_split_v3.log 2>&1 || exit $?
+grep rows gpurun_out/mla_split_v3.log
+timeout -k 10 200 python -u scripts/bench_attn.py > gpurun_out/attn_r4i.log 2>&1 || exit $?
+grep -E "^(prefill|decode)" gpurun_out/attn_r4i.log
+cd /tmp && export TMPDIR=/tmp
+timeout -k 10 120 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/prof_mla_v3 -- python3 $R/scripts/bench_attn.py --mla-only --rows 64 > $R/gpurun_out/prof_mla_v3.log 2>&1 || exit $?
+echo prof done
