@@ -699,23 +699,31 @@ __global__ __launch_bounds__(256, 1) void mla_v3_kernel(
     const int nt = (k1 - k0 + 63) >> 6;
     if constexpr (F8) {
       const uint8_t* k8 = reinterpret_cast<const uint8_t*>(kcv);
+      // this lane's byte offset inside a 64-key fp8 tile for each of its 9 DMA pieces (rows of 576 B)
+      int p8[9];
+#pragma unroll
+      for (int k = 0; k < 9; ++k) {
+        const int u = 64 * (w + NW * k) + lane;
+        const int row = u / 36, c = u - row * 36;
+        p8[k] = row * DQK + c * 16;
+      }
       auto issue8 = [&](char* base, int ts) {
-        int64_t tile_off = 0;
-        if constexpr (BIG) tile_off = (int64_t)bt[ts >> lbs] * block_stride + (int64_t)(ts & (bs - 1)) * DQK;
+        const unsigned l0 = lds_addr(base) + 1024 * w;
+        if (BIG && ts + 64 <= k1) {
+          const uint8_t* tb = k8 + (int64_t)bt[ts >> lbs] * block_stride + (int64_t)(ts & (bs - 1)) * DQK;
+#pragma unroll
+          for (int k = 0; k < 9; ++k) mla_glds16(tb + p8[k], l0 + 1024 * NW * k);
+          return;
+        }
 #pragma unroll
         for (int k = 0; k < 9; ++k) {
-          const int j = w + NW * k;
-          const int u = 64 * j + lane;
+          int ln = lane;  // opaque: the last tile's addressing is recomputed, not hoisted
+          asm volatile("" : "+v"(ln));
+          const int u = 64 * (w + NW * k) + ln;
           const int row = u / 36, c = u - row * 36;
           const int key = min(ts + row, k1 - 1);
-          int64_t off;
-          if constexpr (BIG) {
-            off = tile_off + (int64_t)(key - ts) * DQK;
-          } else {
-            off = (int64_t)bt[key >> lbs] * block_stride + (int64_t)(key & (bs - 1)) * DQK;
-          }
-          __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)(k8 + off + c * 16),
-                                           (void __attribute__((address_space(3)))*)(base + 1024 * j), 16, 0, 0);
+          const int64_t off = (int64_t)bt[key >> lbs] * block_stride + (int64_t)(key & (bs - 1)) * DQK;
+          mla_glds16(k8 + off + c * 16, l0 + 1024 * NW * k);
         }
       };
       issue8(buf1, k0);
@@ -724,9 +732,11 @@ __global__ __launch_bounds__(256, 1) void mla_v3_kernel(
         __syncthreads();  // stage t landed; tile of t-1 fully consumed
         if (t + 1 < nt) issue8(buf1 + ((t + 1) & 1) * V2_STAGE, k0 + 64 * (t + 1));
         const char* st8 = buf1 + (t & 1) * V2_STAGE;
+        int tid = threadIdx.x;  // opaque: the widening addresses are recomputed per tile (no hoisted set)
+        asm volatile("" : "+v"(tid));
 #pragma unroll
         for (int i = 0; i < 72 / NW; ++i) {
-          const int v = threadIdx.x + 64 * NW * i;
+          const int v = tid + 64 * NW * i;
           const int row = v / CPR, ch = v - row * CPR;
           const u32x2_t f = *reinterpret_cast<const u32x2_t*>(st8 + row * DQK + ch * 8);
           *reinterpret_cast<u32x4_t*>(buf0 + row * V2_ROWB + 16 * (ch ^ mla_swz(row))) = fp8x8_to_bf16x8(f);

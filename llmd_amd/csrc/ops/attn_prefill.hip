@@ -466,15 +466,28 @@ __global__ __launch_bounds__(NT, 2) void prefill_v2_kernel(
     const int ts = t * 64;
     const bool active = ntok > 0 && ts <= p_hi && (window <= 0 || ts + 63 > p_lo - window);
     if (!active) return;
+    // S^T: K fragment j = KS b4 + s, read PF ahead of its two MFMAs (a ring with a
+    // sched_barrier per step: hipcc's own schedule hoists every read and waits lgkmcnt(0))
+    constexpr int PF = 4;
+    auto kread = [&](int j) {
+      return *reinterpret_cast<const bf16x8_t*>(img + kofs[j % KS] + (j / KS) * 16 * RB);
+    };
     f32x4_t sc[4][2];
+    bf16x8_t kr[PF];
+#pragma unroll
+    for (int j = 0; j < PF; ++j) kr[j] = kread(j);
+    __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int b4 = 0; b4 < 4; ++b4) {
       f32x4_t a0 = {0.f, 0.f, 0.f, 0.f}, a1 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int s = 0; s < KS; ++s) {
-        const bf16x8_t ka = *reinterpret_cast<const bf16x8_t*>(img + kofs[s] + b4 * 16 * RB);
+        const int j = KS * b4 + s;
+        const bf16x8_t ka = kr[j % PF];
+        if (j + PF < 4 * KS) kr[j % PF] = kread(j + PF);
         a0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ka, qf[0][s], a0, 0, 0, 0);
         a1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ka, qf[1][s], a1, 0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
       }
       sc[b4][0] = a0;
       sc[b4][1] = a1;
@@ -544,27 +557,35 @@ __global__ __launch_bounds__(NT, 2) void prefill_v2_kernel(
         }
       lsum[nb] += ps;  // lane-partial: summed over the row's 4 lanes once, in the epilogue
     }
+    bf16x8_t pa[2][2];
 #pragma unroll
-    for (int t2 = 0; t2 < 2; ++t2) {
-      bf16x8_t pa[2];
+    for (int t2 = 0; t2 < 2; ++t2)
 #pragma unroll
       for (int nb = 0; nb < 2; ++nb)
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-          pa[nb][j] = (__bf16)sc[2 * t2][nb][j];
-          pa[nb][4 + j] = (__bf16)sc[2 * t2 + 1][nb][j];
+          pa[t2][nb][j] = (__bf16)sc[2 * t2][nb][j];
+          pa[t2][nb][4 + j] = (__bf16)sc[2 * t2 + 1][nb][j];
         }
+    // PV: V fragment j = NB t2 + n (two transposed reads), PF ahead of its two MFMAs
+    auto vread = [&](int j) {
+      const char* p0 = img + vofs[j % NB] + 32 * (j / NB) * RB;
+      s16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4_t*)p0);
+      s16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4_t*)(p0 + 16 * RB));
+      return __builtin_bit_cast(bf16x8_t, s16x8_t{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]});
+    };
+    bf16x8_t vr[PF];
 #pragma unroll
-      for (int n = 0; n < NB; ++n) {
-        const char* p0 = img + vofs[n] + 32 * t2 * RB;
-        s16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4_t*)p0);
-        s16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-            (__attribute__((address_space(3))) s16x4_t*)(p0 + 16 * RB));
-        const bf16x8_t vb = __builtin_bit_cast(
-            bf16x8_t, s16x8_t{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]});
-        o[0][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pa[0], vb, o[0][n], 0, 0, 0);
-        o[1][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pa[1], vb, o[1][n], 0, 0, 0);
-      }
+    for (int j = 0; j < PF; ++j) vr[j] = vread(j);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int j = 0; j < 2 * NB; ++j) {
+      const int t2 = j / NB, n = j % NB;
+      const bf16x8_t vb = vr[j % PF];
+      if (j + PF < 2 * NB) vr[j % PF] = vread(j + PF);
+      o[0][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pa[t2][0], vb, o[0][n], 0, 0, 0);
+      o[1][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pa[t2][1], vb, o[1][n], 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
     }
   };
 

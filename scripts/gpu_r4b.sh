@@ -17,4 +17,9 @@ grep -v amdgpu.ids gpurun_out/ep_recv.log | tail -4
 timeout -k 10 900 python -u scripts/bench_wide_ep_rank.py --steps 20 --out gpurun_out/wide_ep_rank_r1.json > gpurun_out/wide_ep_rank.log 2>&1
 rc=$?
 grep -v amdgpu.ids gpurun_out/wide_ep_rank.log | tail -12
-exit $rc
+[ $rc -ne 0 ] && exit $rc
+# kernel-level breakdown of the one-rank decode step (MLA, grouped GEMMs, symm dispatch/combine)
+R=$GRAFT_REPO_ROOT
+cd /tmp && export TMPDIR=/tmp
+timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/prof_wide_ep_rank -- python3 $R/scripts/bench_wide_ep_rank.py --steps 5 --out $R/gpurun_out/wide_ep_rank_prof.json > $R/gpurun_out/prof_wide_ep_rank.log 2>&1
+echo "prof rc=$?"

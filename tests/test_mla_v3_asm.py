@@ -1,7 +1,7 @@
 """Static check of the MLA v3 kernel's register discipline (csrc/ops/attn_mla.hip,
 gen_mla_v3.py): the output accumulators are the literal AGPRs a[0:255], touched
-only by generated inline asm, so the compiled bf16 variants must have no
-hipcc-emitted v_accvgpr_* instruction, no scratch spills, and a generated
+only by generated inline asm, so the compiled variants must have no
+hipcc-emitted v_accvgpr_* instruction, no scratch spills (bf16 and fp8 caches), and a generated
 include that matches its generator."""
 import os
 import re
@@ -35,8 +35,8 @@ def test_v3_accumulators_only_in_asm(tmp_path):
                     f"-I{os.path.join(ROOT, 'llmd_amd', 'csrc', 'include')}", "--cuda-device-only", "-S",
                     os.path.join(OPS, "attn_mla.hip"), "-o", str(s_path)], check=True, capture_output=True)
     s = s_path.read_text()
-    names = re.findall(r"^(_ZN\S*mla_v3_kernelILb[01]ELb0E\S*):", s, re.M)  # bf16 caches (F8 = false)
-    assert len(names) == 2
+    names = re.findall(r"^(_ZN\S*mla_v3_kernelILb[01]ELb[01]E\S*):", s, re.M)  # BIG x fp8-cache variants
+    assert len(names) == 4
     for name in names:
         i = s.index(name + ":")
         j = s.index(".Lfunc_end", i)
