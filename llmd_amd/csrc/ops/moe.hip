@@ -349,6 +349,9 @@ __device__ __forceinline__ void g2_dma(const void* src, char* lds_base) {
   __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)src,
                                    (void __attribute__((address_space(3)))*)lds_base, 16, 0, 0);
 }
+// LDS-DMA from inline asm (llmd_common.h glds16 / glds4) for the v3 kernel: hipcc then keeps
+// counted lgkmcnt(N) waits for its fragment reads; the K loop's counted vmcnt covers them
+__device__ __forceinline__ void g3_dma16(const void* src, char* lds_base) { glds16(src, lds_addr(lds_base)); }
 
 template <int MODE>
 __global__ __launch_bounds__(G2_NT, 2) void moe_gemm2_kernel(
@@ -841,10 +844,7 @@ typedef float f32x16v_t __attribute__((ext_vector_type(16)));
 
 __device__ __forceinline__ int g3r_swz(int row, int c) { return c ^ ((row >> 2) & 3); }
 
-__device__ __forceinline__ void g3_dma4(const void* src, char* lds_base) {
-  __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)src,
-                                   (void __attribute__((address_space(3)))*)lds_base, 4, 0, 0);
-}
+__device__ __forceinline__ void g3_dma4(const void* src, char* lds_base) { glds4(src, lds_addr(lds_base)); }
 
 // FQ (MODE 1 only): the gated activation's output is quantised in the epilogue
 // straight to the second GEMM's fp8 operand - one workgroup's 256 gate/up
@@ -903,9 +903,9 @@ __global__ __launch_bounds__(G3_NT, 1) void moe_gemm3_fp8_kernel(
     char* st = lds + (kt & (G3_NS - 1)) * G3_STAGE;
     const int k0 = kt * 64;
 #pragma unroll
-    for (int i = 0; i < 2; ++i) g2_dma(X + aoff[i] + k0, st + (2 * w + i) * 1024);
+    for (int i = 0; i < 2; ++i) g3_dma16(X + aoff[i] + k0, st + (2 * w + i) * 1024);
 #pragma unroll
-    for (int i = 0; i < 2; ++i) g2_dma(We + boff[i] + k0, st + G3_A + (2 * w + i) * 1024);
+    for (int i = 0; i < 2; ++i) g3_dma16(We + boff[i] + k0, st + G3_A + (2 * w + i) * 1024);
     g3_dma4(xsr + (kt >> 1), st + G3_A + G3_B + w * 256);
   };
   const float* wsr = ws + ((int64_t)e * nnb + (n0 + 64 * __builtin_amdgcn_readfirstlane(wn)) / 128) * nkb;
@@ -939,20 +939,30 @@ __global__ __launch_bounds__(G3_NT, 1) void moe_gemm3_fp8_kernel(
       const u32x4_t hi = *reinterpret_cast<const u32x4_t*>(st + b_off + j * 2048 + sw_hi);
       bfr[j] = i32x8_t{(int)lo[0], (int)lo[1], (int)lo[2], (int)lo[3], (int)hi[0], (int)hi[1], (int)hi[2], (int)hi[3]};
     }
+    auto aread = [&](int i, i32x8_t& af, float& sc) {
+      const u32x4_t lo = *reinterpret_cast<const u32x4_t*>(st + a_off + i * 4096 + sw_lo);
+      const u32x4_t hi = *reinterpret_cast<const u32x4_t*>(st + a_off + i * 4096 + sw_hi);
+      af = i32x8_t{(int)lo[0], (int)lo[1], (int)lo[2], (int)lo[3], (int)hi[0], (int)hi[1], (int)hi[2], (int)hi[3]};
+      sc = *reinterpret_cast<const float*>(st + s_off + i * 512);
+    };
+    // block i's A fragment is read one block ahead of its MFMAs (counted lgkmcnt waits:
+    // the DMA is asm, g2_dma), so a read's latency hides behind the previous block's MFMAs
+    i32x8_t af_cur, af_nxt;
+    float sc_cur = 0.f, sc_nxt = 0.f;
+    if (rb_live > 0) aread(0, af_cur, sc_cur);
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       if (i >= rb_live) break;  // wave-uniform: 32-row blocks past the expert's rows
-      const u32x4_t lo = *reinterpret_cast<const u32x4_t*>(st + a_off + i * 4096 + sw_lo);
-      const u32x4_t hi = *reinterpret_cast<const u32x4_t*>(st + a_off + i * 4096 + sw_hi);
-      const i32x8_t af =
-          i32x8_t{(int)lo[0], (int)lo[1], (int)lo[2], (int)lo[3], (int)hi[0], (int)hi[1], (int)hi[2], (int)hi[3]};
-      const int sa = e8m0_of(*reinterpret_cast<const float*>(st + s_off + i * 512));
+      if (i + 1 < rb_live) aread(i + 1, af_nxt, sc_nxt);
+      const int sa = e8m0_of(sc_cur);
 #pragma unroll
       for (int j = 0; j < 2; ++j)
-        acc[i][j] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(af, bfr[j], acc[i][j], 0, 0, 0, sa, 0, we);
-      __builtin_amdgcn_sched_barrier(0);  // keep each block's fragment reads next to its MFMAs
+        acc[i][j] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(af_cur, bfr[j], acc[i][j], 0, 0, 0, sa, 0, we);
+      __builtin_amdgcn_sched_barrier(0);
       // the next stage's DMA issues behind the first block's MFMAs (they start the matrix pipe at once)
       if (i == 0 && refill) issue(kt + G3_NS - 1);
+      af_cur = af_nxt;
+      sc_cur = sc_nxt;
     }
     if (rb_live == 0 && refill) issue(kt + G3_NS - 1);
   };

@@ -14,3 +14,8 @@ grep -E "^(prefill|decode)" gpurun_out/attn_r4i.log
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 120 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/prof_mla_v3 -- python3 $R/scripts/bench_attn.py --mla-only --rows 64 > $R/gpurun_out/prof_mla_v3.log 2>&1 || exit $?
 echo prof done
+cd $R
+timeout -k 10 400 python -u -m pytest tests/test_fp8_kv.py tests/test_kernels_gpu.py -x -q --timeout 120 --timeout-method thread -k "moe" -p no:cacheprovider > gpurun_out/moe_r4i_tests.log 2>&1 || { echo "moe tests failed"; grep -E "^E |FAILED" gpurun_out/moe_r4i_tests.log | head; exit 1; }
+tail -1 gpurun_out/moe_r4i_tests.log
+timeout -k 10 300 python -u scripts/bench_moe.py > gpurun_out/moe_r4i_bench.txt 2>&1 || { echo bench failed; tail -20 gpurun_out/moe_r4i_bench.txt; exit 1; }
+grep -v amdgpu.ids gpurun_out/moe_r4i_bench.txt
