@@ -623,7 +623,315 @@ __global__ __launch_bounds__(NT, 2) void prefill_v2_kernel(
   }
 }
 
+// ---------------------------------------------------------------- v3 (bf16 cache, D = 128, block >= 64, G % 4 == 0)
+// One 4-wave workgroup per CU (512 registers per wave) runs 4 query heads of a
+// GQA group x 64 query tokens; each wave owns one head x 4 token blocks of 16,
+// so every K fragment (S^T A operand) and every V fragment (PV B operand) read
+// from LDS feeds four MFMAs (v2: two) and each K/V tile serves 256 query rows.
+// O (4 x 8 f32x4 = 128 accumulators) lives in the literal AGPRs a[0:127],
+// touched only by the generated asm of prefill_v3_agpr.inc (gen_prefill_v3.py);
+// scores accumulate in VGPRs through asm MFMAs; K and V fragments are read 4
+// steps ahead with a sched_barrier per step; the LDS-DMA is issued from asm
+// (glds16) so hipcc's waitcnt pass keeps counted lgkmcnt(N) waits. Same tile
+// images, swizzles, masking, lazy rescale and sinks as v2.
+#include "prefill_v3_agpr.inc"
+
+__device__ __forceinline__ void pf3_mfma4(f32x4_t& s0, f32x4_t& s1, f32x4_t& s2, f32x4_t& s3, const bf16x8_t& k,
+                                          const bf16x8_t& q0, const bf16x8_t& q1, const bf16x8_t& q2,
+                                          const bf16x8_t& q3, bool first) {
+  if (first) {
+    asm volatile(
+        "v_mfma_f32_16x16x32_bf16 %0, %4, %5, 0\n\t"
+        "v_mfma_f32_16x16x32_bf16 %1, %4, %6, 0\n\t"
+        "v_mfma_f32_16x16x32_bf16 %2, %4, %7, 0\n\t"
+        "v_mfma_f32_16x16x32_bf16 %3, %4, %8, 0"
+        : "=&v"(s0), "=&v"(s1), "=&v"(s2), "=&v"(s3)
+        : "v"(k), "v"(q0), "v"(q1), "v"(q2), "v"(q3));
+  } else {
+    asm volatile(
+        "v_mfma_f32_16x16x32_bf16 %0, %4, %5, %0\n\t"
+        "v_mfma_f32_16x16x32_bf16 %1, %4, %6, %1\n\t"
+        "v_mfma_f32_16x16x32_bf16 %2, %4, %7, %2\n\t"
+        "v_mfma_f32_16x16x32_bf16 %3, %4, %8, %3"
+        : "+v"(s0), "+v"(s1), "+v"(s2), "+v"(s3)
+        : "v"(k), "v"(q0), "v"(q1), "v"(q2), "v"(q3));
+  }
+}
+
+__global__ __launch_bounds__(NT, 1) void prefill_v3_kernel(
+    const uint16_t* __restrict__ q, int64_t q_stride, const uint16_t* __restrict__ kc,
+    const uint16_t* __restrict__ vc, int64_t block_stride, int bs,
+    const int* __restrict__ block_tables, int bt_stride, const int* __restrict__ q_start,
+    const int* __restrict__ q_len, const int* __restrict__ ctx_len, const int* __restrict__ items,
+    int Hq, int Hkv, int G, float scale_log2, int window, const float* __restrict__ sinks,
+    uint16_t* __restrict__ out, int64_t out_stride, float vscale, int xcd) {
+  constexpr int D = 128, KS = D / 32, NB = D / 16, RB = 2 * D;
+  constexpr int P2_IMG = 64 * RB;  // one 64-key bf16 image (16 KB)
+  constexpr int NI = 64 * (D / 8) / 64;  // 16 DMA wave-instructions per image
+  __shared__ __attribute__((aligned(1024))) char buf0[2 * P2_IMG];  // K | V of even tiles
+  __shared__ __attribute__((aligned(1024))) char buf1[2 * P2_IMG];  // K | V of odd tiles
+
+  int bx = blockIdx.x, by = blockIdx.y;
+  if (xcd) {
+    const int l = xcd_remap(by * gridDim.x + bx, gridDim.x * gridDim.y);
+    bx = l % gridDim.x;
+    by = l / gridDim.x;
+  }
+  const int seq = items[2 * bx], tok0 = items[2 * bx + 1];
+  const int NHG = G / 4;
+  const int kvh = by / NHG, hg = by % NHG;
+  const int qs = q_start[seq], ql = q_len[seq], ctx = ctx_len[seq];
+  const int pbase = ctx - ql;
+  const int* bt = block_tables + (int64_t)seq * bt_stride;
+  const int64_t head_off = (int64_t)kvh * bs * D;
+  const int lbs = __builtin_ctz(bs);
+
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63, g = lane >> 4,
+            c16 = lane & 15;
+  const int head = kvh * G + hg * 4 + w;
+  const int ntok = max(0, min(64, ql - tok0));
+  const int p_lo = pbase + tok0, p_hi = pbase + tok0 + max(ntok, 1) - 1;
+  const int kmin = window > 0 ? max(0, p_lo - window + 1) : 0;
+  const int t_first = kmin >> 6, t_last = p_hi >> 6;
+
+  bf16x8_t qf[4][KS];
+#pragma unroll
+  for (int nb = 0; nb < 4; ++nb) {
+    const int tk = tok0 + 16 * nb + c16;
+    const uint16_t* qr = q + (int64_t)(qs + tk) * q_stride + (int64_t)head * D;
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      u32x4_t v = {0, 0, 0, 0};
+      if (tk < ql) v = *reinterpret_cast<const u32x4_t*>(qr + (4 * s + g) * 8);
+      qf[nb][s] = __builtin_bit_cast(bf16x8_t, v);
+    }
+  }
+  float m[4] = {NEG_INF, NEG_INF, NEG_INF, NEG_INF}, lsum[4] = {0.f, 0.f, 0.f, 0.f};
+  PF3_ZERO_ACC();  // O = a[0:127]
+
+  uint32_t koff[NI / 4], voff[NI / 4];
+#pragma unroll
+  for (int i = 0; i < NI / 4; ++i) {
+    const int u = 64 * (w + 4 * i) + lane;
+    const int row = u / (D / 8), sl = u % (D / 8);
+    koff[i] = (uint32_t)(row * RB + 16 * (sl ^ p2_pk<D>(row)));
+    voff[i] = (uint32_t)(row * RB + 16 * (sl ^ p2_pv<D>(row)));
+  }
+  auto issue = [&](char* base, int t) {
+    const int ts = t * 64;
+    LLMD_DCHECK(ts < ctx && bt[ts >> lbs] >= 0 && ctx <= bt_stride * bs);
+    const int64_t tb = 2 * ((int64_t)bt[ts >> lbs] * block_stride + head_off + (int64_t)(ts & (bs - 1)) * D);
+    const char* kb = reinterpret_cast<const char*>(kc) + tb;
+    const char* vb = reinterpret_cast<const char*>(vc) + tb;
+    const int rlim = ctx - 1 - ts;
+    const unsigned lk = lds_addr(base) + 1024 * w, lv = lk + P2_IMG;
+    if (rlim >= 63) {
+#pragma unroll
+      for (int i = 0; i < NI / 4; ++i) {
+        glds16(kb + koff[i], lk + 4096 * i);
+        glds16(vb + voff[i], lv + 4096 * i);
+      }
+    } else {
+      // a sequence's last, partial tile: rows past the end re-read the last key (finite V)
+#pragma unroll
+      for (int i = 0; i < NI / 4; ++i) {
+        int ln = lane;  // opaque: recomputed here, not hoisted
+        asm volatile("" : "+v"(ln));
+        const int u = 64 * (w + 4 * i) + ln;
+        const int row = u / (D / 8), sl = u % (D / 8);
+        const int64_t ro = (int64_t)min(row, rlim) * RB;
+        glds16(kb + ro + 16 * (sl ^ p2_pk<D>(row)), lk + 4096 * i);
+        glds16(vb + ro + 16 * (sl ^ p2_pv<D>(row)), lv + 4096 * i);
+      }
+    }
+  };
+  const int qq = c16 >> 2, pp = c16 & 3;
+  const int srow = rowoff(c16 >> 2) + (c16 & 3), kp = p2_pk<D>(srow);
+  int kofs[KS];
+#pragma unroll
+  for (int s = 0; s < KS; ++s) kofs[s] = srow * RB + 16 * ((4 * s + g) ^ kp);
+  const int vrow = rowoff(g) + qq, vp = p2_pv<D>(vrow);
+  int vofs[NB];
+#pragma unroll
+  for (int n = 0; n < NB; ++n) vofs[n] = P2_IMG + vrow * RB + 16 * ((2 * n + (pp >> 1)) ^ vp) + 8 * (pp & 1);
+
+  auto compute = [&](const char* img, int t) {
+    const int ts = t * 64;
+    const bool active = ntok > 0 && ts <= p_hi && (window <= 0 || ts + 63 > p_lo - window);
+    if (!active) return;
+    auto kread = [&](int j) {
+      return *reinterpret_cast<const bf16x8_t*>(img + kofs[j % KS] + (j / KS) * 16 * RB);
+    };
+    auto vread = [&](int j) {
+      const char* p0 = img + vofs[j % NB] + 32 * (j / NB) * RB;
+      s16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4_t*)p0);
+      s16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4_t*)(p0 + 16 * RB));
+      return __builtin_bit_cast(bf16x8_t, s16x8_t{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]});
+    };
+    // ---- S^T[key][token] for the 4 token blocks: K fragment j = KS b4 + s
+    f32x4_t sc[4][4];  // [b4][nb]
+    bf16x8_t kr[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) kr[j] = kread(j);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int b4 = 0; b4 < 4; ++b4) {
+#pragma unroll
+      for (int s = 0; s < KS; ++s) {
+        const int j = KS * b4 + s;
+        const bf16x8_t ka = kr[j & 3];
+        if (j + 4 < 4 * KS) kr[j & 3] = kread(j + 4);
+        pf3_mfma4(sc[b4][0], sc[b4][1], sc[b4][2], sc[b4][3], ka, qf[0][s], qf[1][s], qf[2][s], qf[3][s], s == 0);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+    asm volatile("s_nop 7\n\ts_nop 7" ::: "memory");  // score MFMAs (asm) -> VALU reads
+    __builtin_amdgcn_sched_barrier(0);
+    const bool need_mask = (ts + 63 > p_lo) || (window > 0 && ts <= p_hi - window);
+    if (need_mask) {
+#pragma unroll
+      for (int nb = 0; nb < 4; ++nb) {
+        const int qp = p_lo + 16 * nb + c16;
+#pragma unroll
+        for (int b4 = 0; b4 < 4; ++b4)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const int key = ts + 16 * b4 + rowoff(g) + i;
+            bool ok = key <= qp;
+            if (window > 0) ok = ok && key > qp - window;
+            sc[b4][nb][i] = ok ? sc[b4][nb][i] : NEG_INF;
+          }
+      }
+    }
+    float mt[4];
+    bool grow = false;
+#pragma unroll
+    for (int nb = 0; nb < 4; ++nb) {
+      float mx = NEG_INF;
+#pragma unroll
+      for (int b4 = 0; b4 < 4; ++b4)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) mx = fmaxf(mx, sc[b4][nb][i]);
+      mt[nb] = mx * scale_log2;
+      grow = grow || (mt[nb] > m[nb] + 8.f);
+    }
+    if (__ballot(grow) != 0) {  // wave-uniform, rare after the first tiles
+#pragma unroll
+      for (int nb = 0; nb < 4; ++nb) {
+        float mx = fmaxf(mt[nb], __shfl_xor(mt[nb], 16, 64));
+        mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+        const float mnew = fmaxf(m[nb], mx);
+        const float alpha = (mnew == NEG_INF) ? 1.f : __builtin_amdgcn_exp2f(m[nb] - mnew);
+        lsum[nb] *= alpha;
+        m[nb] = mnew;
+        const float a0 = __shfl(alpha, 4 * g, 64), a1 = __shfl(alpha, 4 * g + 1, 64),
+                    a2 = __shfl(alpha, 4 * g + 2, 64), a3 = __shfl(alpha, 4 * g + 3, 64);
+        if (nb == 0) {
+          PF3_RESCALE0(a0, a1, a2, a3);
+        } else if (nb == 1) {
+          PF3_RESCALE1(a0, a1, a2, a3);
+        } else if (nb == 2) {
+          PF3_RESCALE2(a0, a1, a2, a3);
+        } else {
+          PF3_RESCALE3(a0, a1, a2, a3);
+        }
+      }
+    }
+    bf16x8_t pa[2][4];
+#pragma unroll
+    for (int nb = 0; nb < 4; ++nb) {
+      const float msub = (m[nb] == NEG_INF) ? 0.f : m[nb];
+      float ps = 0.f;
+#pragma unroll
+      for (int b4 = 0; b4 < 4; ++b4)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const float p = __builtin_amdgcn_exp2f(fmaf(sc[b4][nb][i], scale_log2, -msub));
+          sc[b4][nb][i] = p;
+          ps += p;
+        }
+      lsum[nb] += ps;
+#pragma unroll
+      for (int t2 = 0; t2 < 2; ++t2)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          pa[t2][nb][j] = (__bf16)sc[2 * t2][nb][j];
+          pa[t2][nb][4 + j] = (__bf16)sc[2 * t2 + 1][nb][j];
+        }
+    }
+    // ---- O[token][dim] += P[token][key] . V[key][dim]: V fragment j = NB t2 + n feeds the 4 token blocks
+    bf16x8_t vr[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) vr[j] = vread(j);
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_nop 1" ::: "memory");  // pa (VALU) -> asm MFMA operand
+    __builtin_amdgcn_sched_barrier(0);
+    PF3_PV_BLOCK
+  };
+
+  issue(buf0, t_first);
+  for (int t = t_first; t <= t_last; t += 2) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (t + 1 <= t_last) issue(buf1, t + 1);
+    compute(buf0, t);
+    if (t + 1 > t_last) break;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (t + 2 <= t_last) issue(buf0, t + 2);
+    compute(buf1, t + 1);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no DMA left in flight at exit
+
+  if (ntok == 0) return;
+  PF3_DRAIN();
+  const float sink = sinks ? sinks[head] * 1.4426950408889634f : NEG_INF;
+#pragma unroll
+  for (int nb = 0; nb < 4; ++nb) {
+    float den = lsum[nb] + __shfl_xor(lsum[nb], 16, 64);
+    den += __shfl_xor(den, 32, 64);
+    if (sinks) den += exp2f(sink - (m[nb] == NEG_INF ? 0.f : m[nb]));
+    const float inv = den > 0.f ? vscale / den : 0.f;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      float x[NB];
+      if (nb == 0) {
+        if (i == 0) { PF3_READ_0_0(x) } else if (i == 1) { PF3_READ_0_1(x) } else if (i == 2) { PF3_READ_0_2(x) } else { PF3_READ_0_3(x) }
+      } else if (nb == 1) {
+        if (i == 0) { PF3_READ_1_0(x) } else if (i == 1) { PF3_READ_1_1(x) } else if (i == 2) { PF3_READ_1_2(x) } else { PF3_READ_1_3(x) }
+      } else if (nb == 2) {
+        if (i == 0) { PF3_READ_2_0(x) } else if (i == 1) { PF3_READ_2_1(x) } else if (i == 2) { PF3_READ_2_2(x) } else { PF3_READ_2_3(x) }
+      } else {
+        if (i == 0) { PF3_READ_3_0(x) } else if (i == 1) { PF3_READ_3_1(x) } else if (i == 2) { PF3_READ_3_2(x) } else { PF3_READ_3_3(x) }
+      }
+      const float f = __shfl(inv, 4 * g + i, 64);
+      const int tk = tok0 + 16 * nb + 4 * g + i;
+      if (tk < ql) {
+        uint16_t* orow = out + (int64_t)(qs + tk) * out_stride + (int64_t)head * D;
+#pragma unroll
+        for (int n = 0; n < NB; ++n) orow[16 * n + c16] = f2bf(x[n] * f);
+      }
+    }
+  }
+}
+
 }  // namespace
+
+// v3 for D = 128 bf16 caches with blocks of >= 64 keys and whole groups of 4 query
+// heads per KV head (LLMD_PREFILL_V3=0 keeps v2); the single source of the item shape
+static bool prefill_v3_ok(int Hq, int Hkv, int D, int bs, int fp8) {
+  static const bool off = [] {
+    const char* e = getenv("LLMD_PREFILL_V3");
+    return e && e[0] == '0';
+  }();
+  static const bool v1_only = [] {
+    const char* e = getenv("LLMD_PREFILL_V1");
+    return e && e[0] == '1';
+  }();
+  return !off && !v1_only && D == 128 && !fp8 && bs >= 64 && Hkv > 0 && (Hq / Hkv) % 4 == 0;
+}
+
+
 
 extern "C" int llmd_paged_prefill(const void* q, int64_t q_stride, const void* kc, const void* vc,
                                   int64_t block_stride, int bs, const int* block_tables,
@@ -659,7 +967,13 @@ extern "C" int llmd_paged_prefill(const void* q, int64_t q_stride, const void* k
     const char* e = getenv("LLMD_PREFILL_XCD");
     return !(e && e[0] == '0');
   }();
-  if ((D == 128 || D == 64) && !fp8 && bs >= 16 && !v1_only) {
+  if (prefill_v3_ok(Hq, Hkv, D, bs, fp8)) {
+    const dim3 grid3(n_items, Hkv * (G / 4));
+    hipLaunchKernelGGL(prefill_v3_kernel, grid3, blk, 0, st, (const uint16_t*)q, q_stride, (const uint16_t*)kc,
+                       (const uint16_t*)vc, block_stride, bs, block_tables, bt_stride, q_start, q_len, ctx_len,
+                       items, Hq, Hkv, G, scale_log2, window, sinks, (uint16_t*)out, out_stride, v_scale,
+                       xcd_map && (int64_t)n_items * grid3.y >= 1024 ? 1 : 0);
+  } else if ((D == 128 || D == 64) && !fp8 && bs >= 16 && !v1_only) {
     auto kern = D == 128 ? prefill_v2_kernel<128> : prefill_v2_kernel<64>;
     hipLaunchKernelGGL(kern, grid, blk, 0, st, (const uint16_t*)q, q_stride, (const uint16_t*)kc,
                        (const uint16_t*)vc, block_stride, bs, block_tables, bt_stride, q_start, q_len, ctx_len,
@@ -677,10 +991,10 @@ extern "C" int llmd_paged_prefill(const void* q, int64_t q_stride, const void* k
 }
 
 // tokens per work item (host helper, mirrors the kernel llmd_paged_prefill
-// dispatches: 32 query tokens per wave, 4 / HPW waves stacked along the
-// tokens for every variant; D, block size and fp8 select among v1 / v2 but
-// not the item shape)
-extern "C" int llmd_prefill_tokens_per_item(int Hq, int Hkv, int /*D*/, int /*bs*/, int /*fp8*/) {
+// dispatches: v3 64; v1 / v2 32 query tokens per wave, 4 / HPW waves stacked
+// along the tokens)
+extern "C" int llmd_prefill_tokens_per_item(int Hq, int Hkv, int D, int bs, int fp8) {
+  if (prefill_v3_ok(Hq, Hkv, D, bs, fp8)) return 64;  // v3: 64 tokens x 4 heads per workgroup
   const int G = Hq / Hkv;
   const int HPW = (G % 4 == 0) ? 4 : ((G % 2 == 0) ? 2 : 1);
   return 32 * (4 / HPW);

@@ -9,8 +9,10 @@ tail -3 gpurun_out/r4i_tests.log
 [ $rc -ne 0 ] && { grep -E "^E |Error|FAILED" gpurun_out/r4i_tests.log | head -20; exit $rc; }
 timeout -k 10 300 python -u scripts/bench_mla_split.py > gpurun_out/mla_split_v3.log 2>&1 || exit $?
 grep rows gpurun_out/mla_split_v3.log
-timeout -k 10 200 python -u scripts/bench_attn.py > gpurun_out/attn_r4i.log 2>&1 || exit $?
-grep -E "^(prefill|decode)" gpurun_out/attn_r4i.log
+timeout -k 10 200 python -u scripts/bench_attn.py --check > gpurun_out/attn_r4i.log 2>&1 || exit $?
+grep -E "^(prefill|decode|  prefill check)" gpurun_out/attn_r4i.log
+LLMD_PREFILL_V3=0 timeout -k 10 200 python -u scripts/bench_attn.py > gpurun_out/attn_r4i_v2.log 2>&1 || exit $?
+grep -E "^prefill" gpurun_out/attn_r4i_v2.log | sed "s/^/v2: /"
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 120 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/prof_mla_v3 -- python3 $R/scripts/bench_attn.py --mla-only --rows 64 > $R/gpurun_out/prof_mla_v3.log 2>&1 || exit $?
 echo prof done
