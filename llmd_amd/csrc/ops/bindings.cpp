@@ -89,6 +89,8 @@ int llmd_moe_gemm3_fp8(const void*, int64_t, const float*, int64_t, int, const i
                        int64_t, const float*, int, int, void*, int64_t, int, int, float, float, int, const void*,
                        void*, int64_t, float*, int64_t, hipStream_t);
 int llmd_moe_gemm3_tile_m();
+int llmd_moe_gemm3_bf16(const void*, int64_t, int, const int*, const int*, int, const void*, int64_t, int, int, void*,
+                        int64_t, int, int, float, float, int, const void*, hipStream_t);
 int llmd_symm_alloc(size_t, void**);
 int llmd_symm_free(void*);
 int64_t llmd_symm_sig_bytes();
@@ -695,13 +697,15 @@ void moe_align(torch::Tensor ids, int64_t E, torch::Tensor sorted_ids, torch::Te
 
 void moe_gemm(torch::Tensor X, int64_t topk, torch::Tensor sorted_ids, torch::Tensor tile_expert,
               torch::Tensor W, torch::Tensor Y, int64_t mode, int64_t act, double alpha, double limit,
-              bool a_rows_are_slots, c10::optional<torch::Tensor> bias) {
+              bool a_rows_are_slots, c10::optional<torch::Tensor> bias, int64_t tile_m) {
   const c10::hip::OptionalHIPGuard device_guard(dev_of(X));
   CHECK_CUDA(X); CHECK_BF16(X); CHECK_BF16(W); CHECK_BF16(Y); CHECK_INNER(X); CHECK_INNER(Y);
   TORCH_CHECK(W.dim() == 3 && W.is_contiguous(), "W [E, N, K] contiguous");
   const int N = W.size(1), K = W.size(2);
   TORCH_CHECK(X.size(1) == K && K % 8 == 0, "moe_gemm: K");
-  const int bm = llmd_moe_gemm_tile_m();
+  const bool v3 = tile_m == llmd_moe_gemm3_tile_m();
+  TORCH_CHECK(tile_m == 0 || tile_m == llmd_moe_gemm_tile_m() || v3, "moe_gemm: tile_m");
+  const int bm = v3 ? llmd_moe_gemm3_tile_m() : llmd_moe_gemm_tile_m();
   const int P = sorted_ids.numel();
   TORCH_CHECK(P % bm == 0 && tile_expert.numel() >= P / bm && Y.size(0) >= P, "moe_gemm: rows");
   TORCH_CHECK(Y.size(1) >= (mode == 1 ? N / 2 : N) && N % 2 == 0, "moe_gemm: Y width");
@@ -711,6 +715,15 @@ void moe_gemm(torch::Tensor X, int64_t topk, torch::Tensor sorted_ids, torch::Te
     CHECK_BF16(bias.value());
     TORCH_CHECK(bias->is_contiguous() && bias->numel() == (int64_t)W.size(0) * N, "bias [E, N]");
     bp = bias->data_ptr();
+  }
+  if (v3) {
+    TORCH_CHECK(K % 32 == 0, "moe_gemm v3: K % 32");
+    const int rc = llmd_moe_gemm3_bf16(X.data_ptr(), X.stride(0), topk, sorted_ids.data_ptr<int>(),
+                                       tile_expert.data_ptr<int>(), P / bm, W.data_ptr(), W.stride(0), N, K,
+                                       Y.data_ptr(), Y.stride(0), mode, act, (float)alpha, (float)limit,
+                                       a_rows_are_slots ? 1 : 0, bp, cur_stream());
+    TORCH_CHECK(rc == 0, "moe_gemm v3 failed: ", rc);
+    return;
   }
   llmd_moe_gemm(X.data_ptr(), X.stride(0), topk, sorted_ids.data_ptr<int>(), tile_expert.data_ptr<int>(), P / bm,
                 W.data_ptr(), W.stride(0), N, K, Y.data_ptr(), Y.stride(0), mode, act, (float)alpha, (float)limit,
@@ -958,7 +971,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {  // _C, or _C_debug (llmd_amd/build.p
   m.def("moe_topk", &moe_topk);
   m.def("moe_align", &moe_align, py::arg("ids"), py::arg("E"), py::arg("sorted_ids"), py::arg("tile_expert"),
         py::arg("expert_offsets"), py::arg("total_p"), py::arg("inv"), py::arg("tile_m") = 0);
-  m.def("moe_gemm", &moe_gemm);
+  m.def("moe_gemm", &moe_gemm, py::arg("X"), py::arg("topk"), py::arg("sorted_ids"), py::arg("tile_expert"),
+        py::arg("W"), py::arg("Y"), py::arg("mode"), py::arg("act"), py::arg("alpha"), py::arg("limit"),
+        py::arg("a_rows_are_slots"), py::arg("bias"), py::arg("tile_m") = 0);
   m.def("moe_combine", &moe_combine);
   m.def("moe_tile_m", &llmd_moe_gemm_tile_m);
   m.def("quant_fp8_rows", &quant_fp8_rows);

@@ -835,6 +835,10 @@ __global__ __launch_bounds__(G2_NT, 2) void moe_gemm2_fp8_kernel(
 //     loaded (from token 0, L2 hits: the DMA count per stage stays fixed for
 //     the counted waits) but not multiplied or stored: the valid rows are a
 //     prefix, each wave skips its 32-row blocks past it (wave-uniform).
+// BF (bf16 operands, round 4): the same 64-B image rows hold 32 bf16 = one
+// K-step of two v_mfma_f32_32x32x16_bf16 per 32x32 tile (lane half h reads
+// chunks h and 2 + h, conflict-free under the same swizzle), no scales, four
+// DMA pieces per wave per stage.
 constexpr int G3_BM = 256, G3_BN = 256, G3_NT = 512, G3_NS = 4;
 constexpr int G3_A = G3_BM * 64, G3_B = G3_BN * 64, G3_SC = 8 * 256;
 constexpr int G3_STAGE = G3_A + G3_B + G3_SC;  // 34 KB
@@ -857,7 +861,7 @@ __device__ __forceinline__ void g3_dma4(const void* src, char* lds_base) { glds4
 // 2 = no DMA after the prologue); 0 in production.
 __device__ int g3_ablate = 0;
 
-template <int MODE, bool FQ>
+template <int MODE, bool FQ, bool BF = false>
 __global__ __launch_bounds__(G3_NT, 1) void moe_gemm3_fp8_kernel(
     const uint8_t* __restrict__ X, int64_t x_stride, const float* __restrict__ xs, int64_t xs_stride, int topk,
     const int* __restrict__ sorted_ids, const int* __restrict__ tile_expert, const uint8_t* __restrict__ W,
@@ -869,8 +873,10 @@ __global__ __launch_bounds__(G3_NT, 1) void moe_gemm3_fp8_kernel(
   const int mt = blockIdx.y, nt = blockIdx.x;
   const int e = tile_expert[mt];
   if (e < 0) return;
+  static_assert(!(FQ && BF), "fused quantisation is an fp8-path epilogue");
   const int m0 = mt * G3_BM, n0 = nt * G3_BN;
-  const int nk = K / 64, nkb = K / 128, nnb = (N + 127) / 128;
+  constexpr int EB = BF ? 2 : 1;  // bytes per element; a K-step is 64 B of every row
+  const int nk = K * EB / 64, nkb = K / 128, nnb = (N + 127) / 128;
 
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
   const int wm = w >> 2, wn = w & 3;
@@ -893,12 +899,12 @@ __global__ __launch_bounds__(G3_NT, 1) void moe_gemm3_fp8_kernel(
   for (int i = 0; i < 2; ++i) {
     const int row = 16 * (2 * w + i) + lr;
     const int tok = tok_of(m0 + row);
-    aoff[i] = (tok < 0 ? 0 : tok) * (int)x_stride + g3r_swz(row, lp) * 16;
-    boff[i] = min(n0 + row, N - 1) * K + g3r_swz(row, lp) * 16;  // tail columns: a valid row, never stored
+    aoff[i] = (tok < 0 ? 0 : tok) * (int)x_stride * EB + g3r_swz(row, lp) * 16;
+    boff[i] = min(n0 + row, N - 1) * K * EB + g3r_swz(row, lp) * 16;  // tail columns: a valid row, never stored
   }
   const int stok = tok_of(m0 + 32 * w + l32);
   const float* xsr = xs + (int64_t)(stok < 0 ? 0 : stok) * xs_stride;
-  const uint8_t* We = W + (int64_t)e * w_expert_stride;
+  const uint8_t* We = W + (int64_t)e * w_expert_stride * EB;
   auto issue = [&](int kt) {
     char* st = lds + (kt & (G3_NS - 1)) * G3_STAGE;
     const int k0 = kt * 64;
@@ -906,16 +912,17 @@ __global__ __launch_bounds__(G3_NT, 1) void moe_gemm3_fp8_kernel(
     for (int i = 0; i < 2; ++i) g3_dma16(X + aoff[i] + k0, st + (2 * w + i) * 1024);
 #pragma unroll
     for (int i = 0; i < 2; ++i) g3_dma16(We + boff[i] + k0, st + G3_A + (2 * w + i) * 1024);
-    g3_dma4(xsr + (kt >> 1), st + G3_A + G3_B + w * 256);
+    if constexpr (!BF) g3_dma4(xsr + (kt >> 1), st + G3_A + G3_B + w * 256);
   };
-  const float* wsr = ws + ((int64_t)e * nnb + (n0 + 64 * __builtin_amdgcn_readfirstlane(wn)) / 128) * nkb;
+  const float* wsr = BF ? nullptr : ws + ((int64_t)e * nnb + (n0 + 64 * __builtin_amdgcn_readfirstlane(wn)) / 128) * nkb;
   // wave wm owns the 32-row blocks {wm, wm + 2, wm + 4, wm + 6} (interleaved: an expert with
   // ~160 rows gives the two halves 3 and 2 blocks, not 4 and 1); live = blocks before nvalid
   const int nblk = (nvalid + 31) / 32;
   const int rb_live = min(4, max(0, (nblk - wm + 1) / 2));
   // fragment reads: lane (l32, h) takes row l32 of a 32-row block, bytes [32h, 32h+32) = chunks 2h, 2h+1;
   // the swizzle key (row >> 2) & 3 is the same for every 32-row block
-  const int sw_lo = g3r_swz(l32, 2 * h) * 16, sw_hi = g3r_swz(l32, 2 * h + 1) * 16;
+  // (bf16: k-substep 0 reads chunk h, k-substep 1 chunk 2 + h)
+  const int sw_lo = g3r_swz(l32, BF ? h : 2 * h) * 16, sw_hi = g3r_swz(l32, BF ? 2 + h : 2 * h + 1) * 16;
   const int a_off = (32 * wm + l32) * 64, b_off = G3_A + (64 * wn + l32) * 64;  // block i: + i * 4096
   const int s_off = G3_A + G3_B + wm * 256 + l32 * 4;  // scale of row 32*(wm + 2i) + l32: + i * 512
   f32x16v_t acc[4][2];
@@ -931,38 +938,69 @@ __global__ __launch_bounds__(G3_NT, 1) void moe_gemm3_fp8_kernel(
       refill = false;
     }
     const char* st = lds + (kt & (G3_NS - 1)) * G3_STAGE;
-    const int we = e8m0_of(wsr[kt >> 1]);
-    i32x8_t bfr[2];
+    if constexpr (BF) {
+      bf16x8_t bfr[2][2];  // [col block][k-substep]
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const u32x4_t lo = *reinterpret_cast<const u32x4_t*>(st + b_off + j * 2048 + sw_lo);
-      const u32x4_t hi = *reinterpret_cast<const u32x4_t*>(st + b_off + j * 2048 + sw_hi);
-      bfr[j] = i32x8_t{(int)lo[0], (int)lo[1], (int)lo[2], (int)lo[3], (int)hi[0], (int)hi[1], (int)hi[2], (int)hi[3]};
-    }
-    auto aread = [&](int i, i32x8_t& af, float& sc) {
-      const u32x4_t lo = *reinterpret_cast<const u32x4_t*>(st + a_off + i * 4096 + sw_lo);
-      const u32x4_t hi = *reinterpret_cast<const u32x4_t*>(st + a_off + i * 4096 + sw_hi);
-      af = i32x8_t{(int)lo[0], (int)lo[1], (int)lo[2], (int)lo[3], (int)hi[0], (int)hi[1], (int)hi[2], (int)hi[3]};
-      sc = *reinterpret_cast<const float*>(st + s_off + i * 512);
-    };
-    // block i's A fragment is read one block ahead of its MFMAs (counted lgkmcnt waits:
-    // the DMA is asm, g2_dma), so a read's latency hides behind the previous block's MFMAs
-    i32x8_t af_cur, af_nxt;
-    float sc_cur = 0.f, sc_nxt = 0.f;
-    if (rb_live > 0) aread(0, af_cur, sc_cur);
+      for (int j = 0; j < 2; ++j) {
+        bfr[j][0] = *reinterpret_cast<const bf16x8_t*>(st + b_off + j * 2048 + sw_lo);
+        bfr[j][1] = *reinterpret_cast<const bf16x8_t*>(st + b_off + j * 2048 + sw_hi);
+      }
+      bf16x8_t a_cur[2], a_nxt[2];
+      if (rb_live > 0) {
+        a_cur[0] = *reinterpret_cast<const bf16x8_t*>(st + a_off + sw_lo);
+        a_cur[1] = *reinterpret_cast<const bf16x8_t*>(st + a_off + sw_hi);
+      }
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      if (i >= rb_live) break;  // wave-uniform: 32-row blocks past the expert's rows
-      if (i + 1 < rb_live) aread(i + 1, af_nxt, sc_nxt);
-      const int sa = e8m0_of(sc_cur);
+      for (int i = 0; i < 4; ++i) {
+        if (i >= rb_live) break;  // wave-uniform: 32-row blocks past the expert's rows
+        if (i + 1 < rb_live) {
+          a_nxt[0] = *reinterpret_cast<const bf16x8_t*>(st + a_off + (i + 1) * 4096 + sw_lo);
+          a_nxt[1] = *reinterpret_cast<const bf16x8_t*>(st + a_off + (i + 1) * 4096 + sw_hi);
+        }
 #pragma unroll
-      for (int j = 0; j < 2; ++j)
-        acc[i][j] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(af_cur, bfr[j], acc[i][j], 0, 0, 0, sa, 0, we);
-      __builtin_amdgcn_sched_barrier(0);
-      // the next stage's DMA issues behind the first block's MFMAs (they start the matrix pipe at once)
-      if (i == 0 && refill) issue(kt + G3_NS - 1);
-      af_cur = af_nxt;
-      sc_cur = sc_nxt;
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+          for (int ks = 0; ks < 2; ++ks)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a_cur[ks], bfr[j][ks], acc[i][j], 0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
+        if (i == 0 && refill) issue(kt + G3_NS - 1);
+        a_cur[0] = a_nxt[0];
+        a_cur[1] = a_nxt[1];
+      }
+    } else {
+      const int we = e8m0_of(wsr[kt >> 1]);
+      i32x8_t bfr[2];
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const u32x4_t lo = *reinterpret_cast<const u32x4_t*>(st + b_off + j * 2048 + sw_lo);
+        const u32x4_t hi = *reinterpret_cast<const u32x4_t*>(st + b_off + j * 2048 + sw_hi);
+        bfr[j] = i32x8_t{(int)lo[0], (int)lo[1], (int)lo[2], (int)lo[3], (int)hi[0], (int)hi[1], (int)hi[2], (int)hi[3]};
+      }
+      auto aread = [&](int i, i32x8_t& af, float& sc) {
+        const u32x4_t lo = *reinterpret_cast<const u32x4_t*>(st + a_off + i * 4096 + sw_lo);
+        const u32x4_t hi = *reinterpret_cast<const u32x4_t*>(st + a_off + i * 4096 + sw_hi);
+        af = i32x8_t{(int)lo[0], (int)lo[1], (int)lo[2], (int)lo[3], (int)hi[0], (int)hi[1], (int)hi[2], (int)hi[3]};
+        sc = *reinterpret_cast<const float*>(st + s_off + i * 512);
+      };
+      // block i's A fragment is read one block ahead of its MFMAs (counted lgkmcnt waits:
+      // the DMA is asm, g3_dma16), so a read's latency hides behind the previous block's MFMAs
+      i32x8_t af_cur, af_nxt;
+      float sc_cur = 0.f, sc_nxt = 0.f;
+      if (rb_live > 0) aread(0, af_cur, sc_cur);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        if (i >= rb_live) break;  // wave-uniform: 32-row blocks past the expert's rows
+        if (i + 1 < rb_live) aread(i + 1, af_nxt, sc_nxt);
+        const int sa = e8m0_of(sc_cur);
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(af_cur, bfr[j], acc[i][j], 0, 0, 0, sa, 0, we);
+        __builtin_amdgcn_sched_barrier(0);
+        // the next stage's DMA issues behind the first block's MFMAs (they start the matrix pipe at once)
+        if (i == 0 && refill) issue(kt + G3_NS - 1);
+        af_cur = af_nxt;
+        sc_cur = sc_nxt;
+      }
     }
     if (rb_live == 0 && refill) issue(kt + G3_NS - 1);
   };
@@ -972,9 +1010,16 @@ __global__ __launch_bounds__(G3_NT, 1) void moe_gemm3_fp8_kernel(
   for (int kt = 0; kt < nk; ++kt) {
     // stage kt landed (this wave's DMAs; the barrier extends it to every wave's), and every
     // wave is done reading the stage that issue(kt + 3) overwrites (it was read in step kt - 1)
-    if (kt + 2 < nk) asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
-    else if (kt + 1 < nk) asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    // G3_OPS (fp8) or 4 (bf16, no scale piece) DMA ops per wave per stage
+    if (kt + 2 < nk) {
+      if constexpr (BF) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
+    } else if (kt + 1 < nk) {
+      if constexpr (BF) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
     compute(kt, kt + G3_NS - 1 < nk);
@@ -1190,6 +1235,25 @@ int llmd_moe_gemm3_fp8(const void* X, int64_t x_stride, const float* xs, int64_t
   else if (hq) LLMD_G3F8(1, true);
   else LLMD_G3F8(1, false);
 #undef LLMD_G3F8
+  return (int)hipGetLastError();
+}
+
+// bf16 operands on the v3 tiles (256-row expert tiles from moe_align with bm = 256)
+int llmd_moe_gemm3_bf16(const void* X, int64_t x_stride, int topk, const int* sorted_ids, const int* tile_expert,
+                        int num_tiles, const void* W, int64_t w_expert_stride, int N, int K, void* Y, int64_t y_stride,
+                        int mode, int act, float alpha, float limit, int a_rows_are_slots, const void* bias,
+                        hipStream_t st) {
+  if (K % 32 || x_stride % 8 || w_expert_stride % 8) return -1;
+  if (num_tiles == 0) return 0;
+  dim3 grid((N + G3_BN - 1) / G3_BN, num_tiles);
+#define LLMD_G3BF(M)                                                                                              \
+  hipLaunchKernelGGL((moe_gemm3_fp8_kernel<M, false, true>), grid, dim3(G3_NT), 0, st, (const uint8_t*)X, x_stride, \
+                     nullptr, 0, topk, sorted_ids, tile_expert, (const uint8_t*)W, w_expert_stride, nullptr, N, K,  \
+                     (uint16_t*)Y, y_stride, act, alpha, limit, a_rows_are_slots, (const uint16_t*)bias, nullptr, 0, \
+                     nullptr, 0)
+  if (mode == 0) LLMD_G3BF(0);
+  else LLMD_G3BF(1);
+#undef LLMD_G3BF
   return (int)hipGetLastError();
 }
 

@@ -572,6 +572,8 @@ def dequant_fp8_block_weight(q: torch.Tensor, s: torch.Tensor, block: int = 128)
 
 MOE_V3_MIN_ROWS = int(os.environ.get("LLMD_MOE_V3_MIN_ROWS", "96"))
 MOE_V3 = os.environ.get("LLMD_MOE_V3", "1") == "1"
+# bf16 experts on the same 256-row tiles (moe_gemm3 with bf16 operands); LLMD_MOE_V3_BF16=0 keeps v2
+MOE_V3_BF16 = os.environ.get("LLMD_MOE_V3_BF16", "1") == "1"
 MOE_FUSED_QUANT = os.environ.get("LLMD_MOE_FUSED_QUANT", "0") == "1"
 
 
@@ -717,9 +719,11 @@ def moe_experts(x, ids, wts, w1, w2, act=0, alpha=1.702, limit=7.0, out=None, b1
     C = native()
     T, d = x.shape
     k = ids.shape[1]
-    E, N1, _ = w1.shape
+    E, N1, K1 = w1.shape
     F = N1 // 2
-    bm = C.moe_tile_m()
+    # prefill-sized steps: 256-row expert tiles on the v3 kernel (bf16 form), as moe_experts_fp8
+    v3 = T * k >= MOE_V3_MIN_ROWS * E and K1 % 32 == 0 and F % 32 == 0 and MOE_V3 and MOE_V3_BF16
+    bm = C.moe_tile_m_prefill() if v3 else C.moe_tile_m()
     n = T * k
     max_p = ((n + E * (bm - 1)) + bm - 1) // bm * bm
     dev = x.device
@@ -728,12 +732,12 @@ def moe_experts(x, ids, wts, w1, w2, act=0, alpha=1.702, limit=7.0, out=None, b1
     offs = torch.empty(E + 1, dtype=torch.int32, device=dev)
     total = torch.empty(1, dtype=torch.int32, device=dev)
     inv = torch.empty(n, dtype=torch.int32, device=dev)  # moe_align fills it (-1 = not on this rank)
-    C.moe_align(ids.contiguous().view(-1), E, sorted_ids, tile_e, offs, total, inv)
+    C.moe_align(ids.contiguous().view(-1), E, sorted_ids, tile_e, offs, total, inv, bm)
     h = torch.empty(max_p, F, dtype=x.dtype, device=dev)
-    C.moe_gemm(x, k, sorted_ids, tile_e, w1, h, 1, act, alpha, limit, False, b1)
+    C.moe_gemm(x, k, sorted_ids, tile_e, w1, h, 1, act, alpha, limit, False, b1, bm)
     y = torch.empty(max_p, d, dtype=x.dtype, device=dev)
     # second GEMM: A rows are the sorted slots themselves (row p of h; a_rows_are_slots)
-    C.moe_gemm(h, 1, sorted_ids, tile_e, w2, y, 0, 0, 0.0, 0.0, True, b2)
+    C.moe_gemm(h, 1, sorted_ids, tile_e, w2, y, 0, 0, 0.0, 0.0, True, b2, bm)
     if out is None:
         out = torch.empty(T, d, dtype=x.dtype, device=dev)
     C.moe_combine(y, inv, wts.contiguous().view(-1), k, out)

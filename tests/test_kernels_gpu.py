@@ -379,7 +379,10 @@ def test_moe_topk(E, k, scoring, ng, tg, renorm):
 
 
 @pytest.mark.parametrize("T,E,k,d,F,act", [(1, 8, 2, 256, 128, 2), (37, 32, 4, 2880, 2880, 2),
-                                            (19, 128, 4, 512, 256, 2), (64, 16, 2, 1024, 512, 0)])
+                                            (19, 128, 4, 512, 256, 2), (64, 16, 2, 1024, 512, 0),
+                                            # prefill-sized: 256-row tiles of the bf16 v3 kernel (>= 96 rows
+                                            # per expert), experts spanning several tiles, gpt-oss widths
+                                            (1024, 8, 2, 1024, 512, 0), (800, 16, 4, 2880, 2880, 2)])
 def test_moe_experts(T, E, k, d, F, act):
     torch.manual_seed(10)
     x = torch.randn(T, d, device=DEV, dtype=torch.bfloat16)
