@@ -525,7 +525,7 @@ __device__ __forceinline__ void mla_mfma2_acc(f32x4_t& s0, f32x4_t& s1, const bf
       : "v"(k), "v"(q0), "v"(q1));
 }
 
-template <bool BIG, bool F8>
+template <bool BIG, bool F8, bool PBF = false>
 __global__ __launch_bounds__(256, 1) void mla_v3_kernel(
     const uint16_t* __restrict__ q, int64_t q_row_stride, const void* __restrict__ kcv,
     int64_t block_stride, int bs, const int* __restrict__ block_tables, int bt_stride,
@@ -782,6 +782,10 @@ __global__ __launch_bounds__(256, 1) void mla_v3_kernel(
         uint16_t* orow = out + (int64_t)r * out_row_stride + (int64_t)(hh + 4 * g + i) * DV;
 #pragma unroll
         for (int n = 0; n < 32; ++n) orow[16 * n + c16] = f2bf(x[n] * f);
+      } else if constexpr (PBF) {  // bf16 partials: half the split-K round trip through memory
+        uint16_t* po = reinterpret_cast<uint16_t*>(part_o) + (((int64_t)r * H + hh + 4 * g + i) * nsplit + sp) * DV;
+#pragma unroll
+        for (int n = 0; n < 32; ++n) po[16 * n + c16] = f2bf(x[n] * kv_scale);
       } else {
         float* po = part_o + (((int64_t)r * H + hh + 4 * g + i) * nsplit + sp) * DV;
 #pragma unroll
@@ -796,6 +800,7 @@ __global__ __launch_bounds__(256, 1) void mla_v3_kernel(
   }
 }
 
+template <bool PBF>
 __global__ __launch_bounds__(128) void mla_reduce_kernel(const float* __restrict__ part_o,
                                                          const float* __restrict__ part_ml,
                                                          const int* __restrict__ row_len, int H, int nsplit,
@@ -819,7 +824,11 @@ __global__ __launch_bounds__(128) void mla_reduce_kernel(const float* __restrict
     float acc = 0.f;
     for (int s = 0; s < nact; ++s) {
       const float ms = part_ml[(base + s) * 2];
-      if (ms != NEG_INF) acc += exp2f(ms - M) * part_o[(base + s) * DV + d];
+      if (ms != NEG_INF) {
+        const float pv = PBF ? bf2f(reinterpret_cast<const uint16_t*>(part_o)[(base + s) * DV + d])
+                             : part_o[(base + s) * DV + d];
+        acc += exp2f(ms - M) * pv;
+      }
     }
     orow[d] = f2bf(acc * inv);
   }
@@ -849,6 +858,14 @@ extern "C" int llmd_mla_v2_shape(int R, int fp8) {
   return R <= 16 ? 41 : 42;
 }
 
+static bool mla_partial_bf16() {
+  static const bool on = [] {
+    const char* e = getenv("LLMD_MLA_PARTIAL_BF16");
+    return e && e[0] == '1';
+  }();
+  return on;
+}
+
 // v2 (64-head groups per workgroup) for 64 or 128 heads; LLMD_MLA_V1=1 forces v1
 extern "C" int llmd_mla_uses_v2(int H) {
   static const int force_v1 = [] {
@@ -873,6 +890,7 @@ extern "C" int llmd_mla_attention(const void* q, int64_t q_row_stride, const voi
     attr_done = true;
   }
   const float scale_log2 = scale * kv_scale * 1.4426950408889634f;
+  bool pbf = false;  // v3 split partials in bf16 (LLMD_MLA_PARTIAL_BF16=1)
   if (llmd_mla_uses_v2(H)) {
 #define V2(NW, BIG, F8)                                                                                        \
   hipLaunchKernelGGL((mla_v2_kernel<NW, BIG, F8>), dim3(nsplit, H / (16 * NW), R), dim3(64 * NW), 0, st,      \
@@ -886,11 +904,14 @@ extern "C" int llmd_mla_attention(const void* q, int64_t q_row_stride, const voi
     if (big) V2(NW, true, false); else V2(NW, false, false); \
   }
 #define V3(BIG, F8)                                                                                            \
-  hipLaunchKernelGGL((mla_v3_kernel<BIG, F8>), dim3(nsplit, 1, R), dim3(256), 0, st, (const uint16_t*)q,        \
+  if (pbf) V3P(BIG, F8, true); else V3P(BIG, F8, false)
+#define V3P(BIG, F8, P)                                                                                        \
+  hipLaunchKernelGGL((mla_v3_kernel<BIG, F8, P>), dim3(nsplit, 1, R), dim3(256), 0, st, (const uint16_t*)q,     \
                      q_row_stride, kc, block_stride, bs, block_tables, bt_stride, row_seq, row_len, H, scale_log2, \
                      split_size, split_dev, nsplit, (uint16_t*)out, out_row_stride, part_o, part_ml, kv_scale)
     const bool big = bs >= 64;
     const int shape = H == 128 ? llmd_mla_v2_shape(R, fp8) : 41;
+    pbf = shape == 42 && nsplit > 1 && mla_partial_bf16();
     if (shape == 81) {
       V2NW(8)
     } else if (shape == 42) {
@@ -903,6 +924,7 @@ extern "C" int llmd_mla_attention(const void* q, int64_t q_row_stride, const voi
       V2NW(4)
     }
 #undef V3
+#undef V3P
 #undef V2NW
 #undef V2
   } else {
@@ -918,7 +940,8 @@ extern "C" int llmd_mla_attention(const void* q, int64_t q_row_stride, const voi
     }
   }
   if (nsplit > 1) {
-    hipLaunchKernelGGL(mla_reduce_kernel, dim3(H, R), dim3(128), 0, st, part_o, part_ml, row_len, H, nsplit,
+    hipLaunchKernelGGL(pbf ? mla_reduce_kernel<true> : mla_reduce_kernel<false>, dim3(H, R), dim3(128), 0, st,
+                       part_o, part_ml, row_len, H, nsplit,
                        split_size, split_dev, (uint16_t*)out, out_row_stride);
   }
   return (int)hipGetLastError();

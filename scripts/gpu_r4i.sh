@@ -9,6 +9,11 @@ tail -3 gpurun_out/r4i_tests.log
 [ $rc -ne 0 ] && { grep -E "^E |Error|FAILED" gpurun_out/r4i_tests.log | head -20; exit $rc; }
 timeout -k 10 300 python -u scripts/bench_mla_split.py > gpurun_out/mla_split_v3.log 2>&1 || exit $?
 grep rows gpurun_out/mla_split_v3.log
+LLMD_MLA_PARTIAL_BF16=1 timeout -k 10 200 python -u -m pytest tests/test_deepseek.py -q -x -k mla_kernel --timeout 150 --timeout-method thread -p no:cacheprovider > gpurun_out/mla_pbf16_test.log 2>&1 || { tail -5 gpurun_out/mla_pbf16_test.log; exit 1; }
+LLMD_MLA_PARTIAL_BF16=1 timeout -k 10 150 python -u scripts/bench_attn.py --mla-only > gpurun_out/mla_pbf16.log 2>&1 || exit $?
+grep "^mla" gpurun_out/mla_pbf16.log | sed "s/^/partial bf16: /"
+timeout -k 10 150 python -u scripts/bench_attn.py --mla-only > gpurun_out/mla_pf32.log 2>&1 || exit $?
+grep "^mla" gpurun_out/mla_pf32.log | sed "s/^/partial f32: /"
 timeout -k 10 200 python -u scripts/bench_attn.py --check > gpurun_out/attn_r4i.log 2>&1 || exit $?
 grep -E "^(prefill|decode|  prefill check)" gpurun_out/attn_r4i.log
 LLMD_PREFILL_V3=0 timeout -k 10 200 python -u scripts/bench_attn.py > gpurun_out/attn_r4i_v2.log 2>&1 || exit $?

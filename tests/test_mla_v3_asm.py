@@ -35,8 +35,8 @@ def test_v3_accumulators_only_in_asm(tmp_path):
                     f"-I{os.path.join(ROOT, 'llmd_amd', 'csrc', 'include')}", "--cuda-device-only", "-S",
                     os.path.join(OPS, "attn_mla.hip"), "-o", str(s_path)], check=True, capture_output=True)
     s = s_path.read_text()
-    names = re.findall(r"^(_ZN\S*mla_v3_kernelILb[01]ELb[01]E\S*):", s, re.M)  # BIG x fp8-cache variants
-    assert len(names) == 4
+    names = re.findall(r"^(_ZN\S*mla_v3_kernelILb[01]ELb[01]ELb[01]E\S*):", s, re.M)  # BIG x fp8 x bf16-partials
+    assert len(names) == 8
     for name in names:
         i = s.index(name + ":")
         j = s.index(".Lfunc_end", i)
