@@ -99,7 +99,7 @@ def build_ops(jobs: int = 8, verbose: bool = False, debug: bool = False) -> Path
     out_dir = BUILD / ("ops_debug" if debug else "ops")
     out_dir.mkdir(parents=True, exist_ok=True)
     inc = CSRC / "include"
-    deps = _headers(inc)
+    deps = _headers(inc) + sorted(str(p) for p in (CSRC / "ops").glob("*.inc"))  # + generated asm includes
     hip_srcs = sorted((CSRC / "ops").glob("*.hip"))
     hip_flags = [
         f"--offload-arch={ARCH}", "-O1" if debug else "-O3", "-fPIC", "-std=c++17", f"-I{inc}",
