@@ -918,11 +918,12 @@ __global__ __launch_bounds__(NT, 1) void prefill_v3_kernel(
 }  // namespace
 
 // v3 for D = 128 bf16 caches with blocks of >= 64 keys and whole groups of 4 query
-// heads per KV head (LLMD_PREFILL_V3=0 keeps v2); the single source of the item shape
+// heads per KV head (LLMD_PREFILL_V3=1 until its GPU numerics have run on the
+// driver's box; v2 otherwise); the single source of the item shape
 static bool prefill_v3_ok(int Hq, int Hkv, int D, int bs, int fp8) {
   static const bool off = [] {
     const char* e = getenv("LLMD_PREFILL_V3");
-    return e && e[0] == '0';
+    return !(e && e[0] == '1');
   }();
   static const bool v1_only = [] {
     const char* e = getenv("LLMD_PREFILL_V1");

@@ -2,6 +2,8 @@
 # with the v3 default, kernel-level MLA breakdown, GQA prefill/decode timing
 set -o pipefail
 mkdir -p gpurun_out
+# the round-4 kernels under test (opt-in until these numerics pass)
+export LLMD_PREFILL_V3=1 LLMD_MOE_V3_BF16=1
 R=$GRAFT_REPO_ROOT
 timeout -k 10 400 python -u -m pytest tests/test_kernels_gpu.py tests/test_deepseek.py tests/test_kernels_prod_shapes.py -q -x --timeout 240 --timeout-method thread -p no:cacheprovider > gpurun_out/r4i_tests.log 2>&1
 rc=$?
@@ -26,3 +28,5 @@ timeout -k 10 400 python -u -m pytest tests/test_fp8_kv.py tests/test_kernels_gp
 tail -1 gpurun_out/moe_r4i_tests.log
 timeout -k 10 300 python -u scripts/bench_moe.py > gpurun_out/moe_r4i_bench.txt 2>&1 || { echo bench failed; tail -20 gpurun_out/moe_r4i_bench.txt; exit 1; }
 grep -v amdgpu.ids gpurun_out/moe_r4i_bench.txt
+LLMD_MOE_V3_BF16=0 timeout -k 10 300 python -u scripts/bench_moe.py > gpurun_out/moe_r4i_bench_v2bf16.txt 2>&1 || exit $?
+grep -v amdgpu.ids gpurun_out/moe_r4i_bench_v2bf16.txt | sed "s/^/bf16 v2: /"
