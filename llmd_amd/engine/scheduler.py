@@ -318,6 +318,13 @@ class Scheduler:
                 r.num_computed_tokens = cached
                 if r.num_preemptions == 0:
                     r.num_cached_tokens = cached
+                if (self.offload is not None and self.cfg.cache.enable_prefix_caching and self.running
+                        and self._reload_cannot_fit(r, cached, budget)):
+                    # it would have to give the reloaded blocks back at once (below) and
+                    # reload them again next step: wait holding nothing until blocks free up
+                    self.bm.free(r.seq_id)
+                    r.num_computed_tokens = 0
+                    break
                 if (self.offload is not None and self.cfg.cache.enable_prefix_caching
                         and self.offload.start_load(r, toks, cached, self.bm)):
                     # host / disk blocks continue the prefix: they load asynchronously
@@ -360,6 +367,14 @@ class Scheduler:
             budget -= n
         self._align_tokens(out)
         return out
+
+    def _reload_cannot_fit(self, r, cached: int, budget: int) -> bool:
+        """True when the pool cannot hold this request's first chunk even after a
+        tier reload (the blocks it holds now plus the free ones): reloading host /
+        disk blocks it must release in the same step only repeats every step."""
+        bs = self.bm.block_size
+        want = -(-min(r.num_tokens, cached + max(budget, 1)) // bs)
+        return want - self.bm.num_seq_blocks(r.seq_id) > self.bm.num_free()
 
     def _align_tokens(self, out: SchedulerOutput) -> None:
         """Trim prefill chunks, newest first, so the step's token count is a

@@ -73,6 +73,9 @@ def test_host_reload_retried_when_pool_was_full():
     assert not eng.has_unfinished()  # a waiting request holding blocks used to deadlock here
     assert outs["again"] == base
     assert eng.offload.stats["loaded_cpu"] >= 96 // 16 - 1
+    # while the pool cannot hold it, the waiting request does not reload (and give back)
+    # its host prefix every step: one reload, not one per blocked step
+    assert eng.offload.stats["loaded_cpu"] <= 2 * (96 // 16)
 
 
 def test_offload_metrics_use_vllm_names(tmp_path):
