@@ -498,12 +498,8 @@ __global__ __launch_bounds__(NT, 2) void shared_prefix_v2_kernel(
         const int64_t tb = 2 * ((int64_t)bt[key0 >> lbs] * block_stride + head_off +
                                 (int64_t)(key0 & (bs - 1)) * D) - (int64_t)r0 * RB;
         char* dst = base + 1024 * (ws + 4 * i);
-        __builtin_amdgcn_global_load_lds(
-            (const void __attribute__((address_space(1)))*)(reinterpret_cast<const char*>(kc) + tb + koff[i]),
-            (void __attribute__((address_space(3)))*)dst, 16, 0, 0);
-        __builtin_amdgcn_global_load_lds(
-            (const void __attribute__((address_space(1)))*)(reinterpret_cast<const char*>(vc) + tb + voff[i]),
-            (void __attribute__((address_space(3)))*)(dst + IMG), 16, 0, 0);
+        glds16(reinterpret_cast<const char*>(kc) + tb + koff[i], lds_addr(dst));  // asm DMA: counted lgkmcnt
+        glds16(reinterpret_cast<const char*>(vc) + tb + voff[i], lds_addr(dst + IMG));
       }
     } else {  // last partial tile: rows past the prefix re-read key hi - 1 (finite; masked below)
 #pragma unroll
@@ -513,14 +509,8 @@ __global__ __launch_bounds__(NT, 2) void shared_prefix_v2_kernel(
         const int key = ts + min(row, rlim);
         const int64_t ro = 2 * ((int64_t)bt[key >> lbs] * block_stride + head_off + (int64_t)(key & (bs - 1)) * D);
         char* dst = base + 1024 * (ws + 4 * i);
-        __builtin_amdgcn_global_load_lds(
-            (const void __attribute__((address_space(1)))*)(reinterpret_cast<const char*>(kc) + ro +
-                                                            16 * (sl ^ sp_pk<D>(row))),
-            (void __attribute__((address_space(3)))*)dst, 16, 0, 0);
-        __builtin_amdgcn_global_load_lds(
-            (const void __attribute__((address_space(1)))*)(reinterpret_cast<const char*>(vc) + ro +
-                                                            16 * (sl ^ sp_pv<D>(row))),
-            (void __attribute__((address_space(3)))*)(dst + IMG), 16, 0, 0);
+        glds16(reinterpret_cast<const char*>(kc) + ro + 16 * (sl ^ sp_pk<D>(row)), lds_addr(dst));
+        glds16(reinterpret_cast<const char*>(vc) + ro + 16 * (sl ^ sp_pv<D>(row)), lds_addr(dst + IMG));
       }
     }
   };

@@ -5,7 +5,7 @@ mkdir -p gpurun_out
 # the round-4 kernels under test (opt-in until these numerics pass)
 export LLMD_PREFILL_V3=1 LLMD_MOE_V3_BF16=1
 R=$GRAFT_REPO_ROOT
-timeout -k 10 400 python -u -m pytest tests/test_kernels_gpu.py tests/test_deepseek.py tests/test_kernels_prod_shapes.py -q -x --timeout 240 --timeout-method thread -p no:cacheprovider > gpurun_out/r4i_tests.log 2>&1
+timeout -k 10 500 python -u -m pytest tests/test_kernels_gpu.py tests/test_deepseek.py tests/test_kernels_prod_shapes.py tests/test_shared_prefix_gpu.py -q -x --timeout 240 --timeout-method thread -p no:cacheprovider > gpurun_out/r4i_tests.log 2>&1
 rc=$?
 tail -3 gpurun_out/r4i_tests.log
 [ $rc -ne 0 ] && { grep -E "^E |Error|FAILED" gpurun_out/r4i_tests.log | head -20; exit $rc; }
@@ -30,3 +30,5 @@ timeout -k 10 300 python -u scripts/bench_moe.py > gpurun_out/moe_r4i_bench.txt 
 grep -v amdgpu.ids gpurun_out/moe_r4i_bench.txt
 LLMD_MOE_V3_BF16=0 timeout -k 10 300 python -u scripts/bench_moe.py > gpurun_out/moe_r4i_bench_v2bf16.txt 2>&1 || exit $?
 grep -v amdgpu.ids gpurun_out/moe_r4i_bench_v2bf16.txt | sed "s/^/bf16 v2: /"
+timeout -k 10 200 python -u scripts/bench_shared_prefix.py > gpurun_out/shared_prefix_r4i.txt 2>&1 || exit $?
+grep -v amdgpu.ids gpurun_out/shared_prefix_r4i.txt | tail -12
