@@ -172,7 +172,15 @@ __device__ __forceinline__ int xcd_remap(int orig, int nwg) {
 __device__ __forceinline__ unsigned lds_addr(const void* p) {
   return (unsigned)(uintptr_t)(const __attribute__((address_space(3))) char*)p;
 }
+#ifndef LLMD_ASM_DMA
+#define LLMD_ASM_DMA 1  // 0: the builtin (hipcc-visible) DMA, for A/B runs
+#endif
 __device__ __forceinline__ void glds16(const void* gsrc, unsigned lds_dst) {
+#if !LLMD_ASM_DMA
+  __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)gsrc,
+                                   (void __attribute__((address_space(3)))*)(uintptr_t)lds_dst, 16, 0, 0);
+  return;
+#endif
   unsigned keep;
   asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
                : "=&s"(keep)
@@ -182,6 +190,11 @@ __device__ __forceinline__ void glds16(const void* gsrc, unsigned lds_dst) {
 
 // 4-byte-per-lane form (global_load_lds_dword), same contract as glds16
 __device__ __forceinline__ void glds4(const void* gsrc, unsigned lds_dst) {
+#if !LLMD_ASM_DMA
+  __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)gsrc,
+                                   (void __attribute__((address_space(3)))*)(uintptr_t)lds_dst, 4, 0, 0);
+  return;
+#endif
   unsigned keep;
   asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off\n\ts_mov_b32 m0, %0"
                : "=&s"(keep)
