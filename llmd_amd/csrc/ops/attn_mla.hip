@@ -834,6 +834,54 @@ __global__ __launch_bounds__(128) void mla_reduce_kernel(const float* __restrict
   }
 }
 
+// Split merge, one wave per (row, head): lane l owns dims 8l..8l+7 (16-B partial
+// loads, bf16 or fp32), the split weights exp2(m_s - M) / sum are wave-uniform.
+// 4 heads per 256-thread workgroup.
+template <bool PBF>
+__global__ __launch_bounds__(256) void mla_reduce2_kernel(const float* __restrict__ part_o,
+                                                          const float* __restrict__ part_ml,
+                                                          const int* __restrict__ row_len, int H, int nsplit,
+                                                          int split_size, const int* __restrict__ split_dev,
+                                                          uint16_t* __restrict__ out, int64_t out_row_stride) {
+  const int hh = blockIdx.x * 4 + (threadIdx.x >> 6), r = blockIdx.y, lane = threadIdx.x & 63;
+  if (hh >= H) return;
+  const int len = row_len[r];
+  if (split_dev) split_size = *split_dev;
+  const int nact = min(nsplit, (len + split_size - 1) / split_size);
+  const int64_t base = ((int64_t)r * H + hh) * nsplit;
+  float M = NEG_INF;
+  for (int s = 0; s < nact; ++s) M = fmaxf(M, part_ml[(base + s) * 2]);
+  float den = 0.f;
+  for (int s = 0; s < nact; ++s) {
+    const float ms = part_ml[(base + s) * 2];
+    if (ms != NEG_INF) den += exp2f(ms - M) * part_ml[(base + s) * 2 + 1];
+  }
+  const float inv = den > 0.f ? 1.f / den : 0.f;
+  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  for (int s = 0; s < nact; ++s) {
+    const float ms = part_ml[(base + s) * 2];
+    if (ms == NEG_INF) continue;
+    const float wgt = exp2f(ms - M) * inv;
+    if constexpr (PBF) {
+      const u32x4_t v = *reinterpret_cast<const u32x4_t*>(reinterpret_cast<const uint16_t*>(part_o) +
+                                                           (base + s) * DV + 8 * lane);
+      float f[8];
+      unpack8(v, f);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) acc[k] += wgt * f[k];
+    } else {
+      const f32x4_t* pv = reinterpret_cast<const f32x4_t*>(part_o + (base + s) * DV + 8 * lane);
+      const f32x4_t a = pv[0], b = pv[1];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        acc[k] += wgt * a[k];
+        acc[4 + k] += wgt * b[k];
+      }
+    }
+  }
+  *reinterpret_cast<u32x4_t*>(out + (int64_t)r * out_row_stride + (int64_t)hh * DV + 8 * lane) = pack8(acc);
+}
+
 }  // namespace
 
 // Kernel shape for H = 128, as 10 * waves + head blocks per wave:
@@ -858,10 +906,12 @@ extern "C" int llmd_mla_v2_shape(int R, int fp8) {
   return R <= 16 ? 41 : 42;
 }
 
+// v3 split partials in bf16 (default; LLMD_MLA_PARTIAL_BF16=0 keeps fp32): rows=64
+// ctx 4k 0.112 -> 0.108 ms, MLA numerics tests pass (profiles/mla_r4_shapes.txt)
 static bool mla_partial_bf16() {
   static const bool on = [] {
     const char* e = getenv("LLMD_MLA_PARTIAL_BF16");
-    return e && e[0] == '1';
+    return !(e && e[0] == '0');
   }();
   return on;
 }
@@ -940,9 +990,10 @@ extern "C" int llmd_mla_attention(const void* q, int64_t q_row_stride, const voi
     }
   }
   if (nsplit > 1) {
-    hipLaunchKernelGGL(pbf ? mla_reduce_kernel<true> : mla_reduce_kernel<false>, dim3(H, R), dim3(128), 0, st,
-                       part_o, part_ml, row_len, H, nsplit,
-                       split_size, split_dev, (uint16_t*)out, out_row_stride);
+    // the vectorised merge needs 16-B aligned output rows (out_row_stride % 8: the op checks it)
+    hipLaunchKernelGGL(pbf ? mla_reduce2_kernel<true> : mla_reduce2_kernel<false>, dim3((H + 3) / 4, R), dim3(256),
+                       0, st, part_o, part_ml, row_len, H, nsplit, split_size, split_dev, (uint16_t*)out,
+                       out_row_stride);
   }
   return (int)hipGetLastError();
 }

@@ -573,7 +573,7 @@ def dequant_fp8_block_weight(q: torch.Tensor, s: torch.Tensor, block: int = 128)
 MOE_V3_MIN_ROWS = int(os.environ.get("LLMD_MOE_V3_MIN_ROWS", "96"))
 MOE_V3 = os.environ.get("LLMD_MOE_V3", "1") == "1"
 # bf16 experts on the same 256-row tiles (moe_gemm3 with bf16 operands); LLMD_MOE_V3_BF16=0 keeps v2
-MOE_V3_BF16 = os.environ.get("LLMD_MOE_V3_BF16", "0") == "1"  # on once its GPU numerics have run
+MOE_V3_BF16 = os.environ.get("LLMD_MOE_V3_BF16", "1") == "1"  # DeepSeek EP8 T=4096 701 -> 789 TF/s, gpt-oss T=5120 369 -> 529
 MOE_FUSED_QUANT = os.environ.get("LLMD_MOE_FUSED_QUANT", "0") == "1"
 
 
