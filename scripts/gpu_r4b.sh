@@ -18,8 +18,12 @@ timeout -k 10 900 python -u scripts/bench_wide_ep_rank.py --steps 20 --out gpuru
 rc=$?
 grep -v amdgpu.ids gpurun_out/wide_ep_rank.log | tail -12
 [ $rc -ne 0 ] && exit $rc
-# kernel-level breakdown of the one-rank decode step (MLA, grouped GEMMs, symm dispatch/combine)
+# kernel-level breakdown of the one-rank decode step (MLA, grouped GEMMs, symm dispatch/combine);
+# the full trace stays in /tmp (it exceeds gpurun_out's 64 MiB), only the stats are copied back
 R=$GRAFT_REPO_ROOT
 cd /tmp && export TMPDIR=/tmp
-timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/prof_wide_ep_rank -- python3 $R/scripts/bench_wide_ep_rank.py --steps 5 --out $R/gpurun_out/wide_ep_rank_prof.json > $R/gpurun_out/prof_wide_ep_rank.log 2>&1
-echo "prof rc=$?"
+timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d /tmp/prof_wide_ep_rank -- python3 $R/scripts/bench_wide_ep_rank.py --steps 5 --out /tmp/wide_ep_rank_prof.json > $R/gpurun_out/prof_wide_ep_rank.log 2>&1
+rc=$?
+echo "prof rc=$rc"
+mkdir -p $R/gpurun_out/prof_wide_ep_rank && cp /tmp/prof_wide_ep_rank/*/*kernel_stats.csv $R/gpurun_out/prof_wide_ep_rank/ 2>/dev/null
+exit $rc
