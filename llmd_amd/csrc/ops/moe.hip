@@ -861,7 +861,9 @@ __device__ __forceinline__ void g3_dma4(const void* src, char* lds_base) { glds4
 // 2 = no DMA after the prologue); 0 in production.
 __device__ int g3_ablate = 0;
 
-template <int MODE, bool FQ, bool BF = false>
+// V (fp8 A/B switch, round 4): bit 0 = A fragments read one row block ahead,
+// bit 1 = LDS-DMA from asm (glds16/glds4) instead of the builtin
+template <int MODE, bool FQ, bool BF = false, int V = 3>
 __global__ __launch_bounds__(G3_NT, 1) void moe_gemm3_fp8_kernel(
     const uint8_t* __restrict__ X, int64_t x_stride, const float* __restrict__ xs, int64_t xs_stride, int topk,
     const int* __restrict__ sorted_ids, const int* __restrict__ tile_expert, const uint8_t* __restrict__ W,
@@ -909,10 +911,21 @@ __global__ __launch_bounds__(G3_NT, 1) void moe_gemm3_fp8_kernel(
     char* st = lds + (kt & (G3_NS - 1)) * G3_STAGE;
     const int k0 = kt * 64;
 #pragma unroll
-    for (int i = 0; i < 2; ++i) g3_dma16(X + aoff[i] + k0, st + (2 * w + i) * 1024);
+    for (int i = 0; i < 2; ++i) {
+      if constexpr (V & 2) g3_dma16(X + aoff[i] + k0, st + (2 * w + i) * 1024);
+      else g2_dma(X + aoff[i] + k0, st + (2 * w + i) * 1024);
+    }
 #pragma unroll
-    for (int i = 0; i < 2; ++i) g3_dma16(We + boff[i] + k0, st + G3_A + (2 * w + i) * 1024);
-    if constexpr (!BF) g3_dma4(xsr + (kt >> 1), st + G3_A + G3_B + w * 256);
+    for (int i = 0; i < 2; ++i) {
+      if constexpr (V & 2) g3_dma16(We + boff[i] + k0, st + G3_A + (2 * w + i) * 1024);
+      else g2_dma(We + boff[i] + k0, st + G3_A + (2 * w + i) * 1024);
+    }
+    if constexpr (!BF) {
+      if constexpr (V & 2) g3_dma4(xsr + (kt >> 1), st + G3_A + G3_B + w * 256);
+      else __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)(xsr + (kt >> 1)),
+                                            (void __attribute__((address_space(3)))*)(st + G3_A + G3_B + w * 256),
+                                            4, 0, 0);
+    }
   };
   const float* wsr = BF ? nullptr : ws + ((int64_t)e * nnb + (n0 + 64 * __builtin_amdgcn_readfirstlane(wn)) / 128) * nkb;
   // wave wm owns the 32-row blocks {wm, wm + 2, wm + 4, wm + 6} (interleaved: an expert with
@@ -986,11 +999,15 @@ __global__ __launch_bounds__(G3_NT, 1) void moe_gemm3_fp8_kernel(
       // the DMA is asm, g3_dma16), so a read's latency hides behind the previous block's MFMAs
       i32x8_t af_cur, af_nxt;
       float sc_cur = 0.f, sc_nxt = 0.f;
-      if (rb_live > 0) aread(0, af_cur, sc_cur);
+      if ((V & 1) && rb_live > 0) aread(0, af_cur, sc_cur);
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         if (i >= rb_live) break;  // wave-uniform: 32-row blocks past the expert's rows
-        if (i + 1 < rb_live) aread(i + 1, af_nxt, sc_nxt);
+        if constexpr (V & 1) {
+          if (i + 1 < rb_live) aread(i + 1, af_nxt, sc_nxt);
+        } else {
+          aread(i, af_cur, sc_cur);  // read right before its MFMAs (round-3 schedule)
+        }
         const int sa = e8m0_of(sc_cur);
 #pragma unroll
         for (int j = 0; j < 2; ++j)
@@ -998,8 +1015,10 @@ __global__ __launch_bounds__(G3_NT, 1) void moe_gemm3_fp8_kernel(
         __builtin_amdgcn_sched_barrier(0);
         // the next stage's DMA issues behind the first block's MFMAs (they start the matrix pipe at once)
         if (i == 0 && refill) issue(kt + G3_NS - 1);
-        af_cur = af_nxt;
-        sc_cur = sc_nxt;
+        if constexpr (V & 1) {
+          af_cur = af_nxt;
+          sc_cur = sc_nxt;
+        }
       }
     }
     if (rb_live == 0 && refill) issue(kt + G3_NS - 1);
@@ -1226,8 +1245,18 @@ int llmd_moe_gemm3_fp8(const void* X, int64_t x_stride, const float* xs, int64_t
   (void)ablate;
   if (num_tiles == 0) return 0;
   dim3 grid((N + G3_BN - 1) / G3_BN, num_tiles);
+  static const int g3v = [] {
+    const char* e = getenv("LLMD_MOE_V3_VARIANT");  // A/B of the round-4 fp8 v3 schedule (V above)
+    return e ? (atoi(e) & 3) : 3;
+  }();
 #define LLMD_G3F8(M, Q)                                                                                           \
-  hipLaunchKernelGGL((moe_gemm3_fp8_kernel<M, Q>), grid, dim3(G3_NT), 0, st, (const uint8_t*)X, x_stride, xs,      \
+  do {                                                                                                            \
+    if (g3v == 0) LLMD_G3F8V(M, Q, 0); else if (g3v == 1) LLMD_G3F8V(M, Q, 1);                                  \
+    else if (g3v == 2) LLMD_G3F8V(M, Q, 2); else LLMD_G3F8V(M, Q, 3);                                           \
+  } while (0)
+#define LLMD_G3F8V(M, Q, VV)                                                                                      \
+  hipLaunchKernelGGL((moe_gemm3_fp8_kernel<M, Q, false, VV>), grid, dim3(G3_NT), 0, st, (const uint8_t*)X,       \
+                     x_stride, xs,                                                                                 \
                      xs_stride, topk, sorted_ids, tile_expert, (const uint8_t*)W, w_expert_stride, ws, N, K,       \
                      (uint16_t*)Y, y_stride, act, alpha, limit, a_rows_are_slots, (const uint16_t*)bias,           \
                      (uint8_t*)hq, hq_stride, hs, hs_stride)
@@ -1235,6 +1264,7 @@ int llmd_moe_gemm3_fp8(const void* X, int64_t x_stride, const float* xs, int64_t
   else if (hq) LLMD_G3F8(1, true);
   else LLMD_G3F8(1, false);
 #undef LLMD_G3F8
+#undef LLMD_G3F8V
   return (int)hipGetLastError();
 }
 
