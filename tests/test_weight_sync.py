@@ -219,7 +219,13 @@ def test_sleep_with_kv_offload_gpu_releases_pool(tmp_path):
     assert used0 - used1 >= 0.9 * res["freed_bytes"] > kv_bytes, (used0, used1, res, kv_bytes)
     eng.weight_sync_cmd({"op": "wake_up"})
     assert eng.offload.kv is eng.runner.kv
-    assert _run(eng) == ref
+    # after wake-up the prompts' prefixes come back from the host tier, so only their
+    # tails are recomputed: same tokens, logprobs equal up to the GEMM path chosen for
+    # the smaller prefill batch (ops.linear autotunes per M bucket)
+    got = _run(eng)
+    assert [t for t, _ in got] == [t for t, _ in ref]
+    for (_, lp), (_, lr) in zip(got, ref):
+        assert np.allclose(lp, lr, atol=2e-3), (lp, lr)
 
 
 @pytest.mark.gpu
