@@ -325,7 +325,9 @@ __device__ __forceinline__ int p2_pv(int r) {
   else return (r & 2) | ((r >> 1) & 4);
 }
 
-template <int D>
+// V (round-4 A/B switch): bit 0 = K/V fragment reads ring-pipelined with a sched_barrier
+// per step, bit 1 = LDS-DMA from asm (glds16) instead of the builtin
+template <int D, int V = 3>
 __global__ __launch_bounds__(NT, 2) void prefill_v2_kernel(
     const uint16_t* __restrict__ q, int64_t q_stride, const uint16_t* __restrict__ kc,
     const uint16_t* __restrict__ vc, int64_t block_stride, int bs,
@@ -406,6 +408,11 @@ __global__ __launch_bounds__(NT, 2) void prefill_v2_kernel(
     koff[i] = (uint32_t)(row * RB + 16 * (sl ^ p2_pk<D>(row)));
     voff[i] = (uint32_t)(row * RB + 16 * (sl ^ p2_pv<D>(row)));
   }
+  auto dma = [&](const char* src, char* dst) {
+    if constexpr (V & 2) glds16(src, lds_addr(dst));
+    else __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)src,
+                                          (void __attribute__((address_space(3)))*)dst, 16, 0, 0);
+  };
   auto issue = [&](char* base, int t) {
     const int ts = t * 64;
     LLMD_DCHECK(ts < ctx && bt[ts >> lbs] >= 0 && ctx <= bt_stride * bs);
@@ -417,8 +424,8 @@ __global__ __launch_bounds__(NT, 2) void prefill_v2_kernel(
 #pragma unroll
       for (int i = 0; i < NI / 4; ++i) {
         char* dst = base + 1024 * (ws + 4 * i);
-        glds16(kb + koff[i], lds_addr(dst));
-        glds16(vb + voff[i], lds_addr(dst + P2_IMG));
+        dma(kb + koff[i], dst);
+        dma(vb + voff[i], dst + P2_IMG);
       }
     } else if (rlim >= 63) {
       // blocks of 16 / 32 keys: a wave-instruction's RPI rows sit in one block
@@ -431,8 +438,8 @@ __global__ __launch_bounds__(NT, 2) void prefill_v2_kernel(
         const int64_t ib = 2 * ((int64_t)bt[key0 >> lbs] * block_stride + head_off + (int64_t)(key0 & (bs - 1)) * D) -
                            (int64_t)r0 * RB;
         char* dst = base + 1024 * (ws + 4 * i);
-        glds16(reinterpret_cast<const char*>(kc) + ib + koff[i], lds_addr(dst));
-        glds16(reinterpret_cast<const char*>(vc) + ib + voff[i], lds_addr(dst + P2_IMG));
+        dma(reinterpret_cast<const char*>(kc) + ib + koff[i], dst);
+        dma(reinterpret_cast<const char*>(vc) + ib + voff[i], dst + P2_IMG);
       }
     } else {
 #pragma unroll
@@ -445,8 +452,8 @@ __global__ __launch_bounds__(NT, 2) void prefill_v2_kernel(
                                     : 2 * ((int64_t)bt[key >> lbs] * block_stride + head_off +
                                            (int64_t)(key & (bs - 1)) * D) - tb;
         char* dst = base + 1024 * (ws + 4 * i);
-        glds16(kb + ro + 16 * (sl ^ p2_pk<D>(row)), lds_addr(dst));
-        glds16(vb + ro + 16 * (sl ^ p2_pv<D>(row)), lds_addr(dst + P2_IMG));
+        dma(kb + ro + 16 * (sl ^ p2_pk<D>(row)), dst);
+        dma(vb + ro + 16 * (sl ^ p2_pv<D>(row)), dst + P2_IMG);
       }
     }
   };
@@ -476,7 +483,7 @@ __global__ __launch_bounds__(NT, 2) void prefill_v2_kernel(
     bf16x8_t kr[PF];
 #pragma unroll
     for (int j = 0; j < PF; ++j) kr[j] = kread(j);
-    __builtin_amdgcn_sched_barrier(0);
+    if constexpr (V & 1) __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int b4 = 0; b4 < 4; ++b4) {
       f32x4_t a0 = {0.f, 0.f, 0.f, 0.f}, a1 = {0.f, 0.f, 0.f, 0.f};
@@ -487,7 +494,7 @@ __global__ __launch_bounds__(NT, 2) void prefill_v2_kernel(
         if (j + PF < 4 * KS) kr[j % PF] = kread(j + PF);
         a0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ka, qf[0][s], a0, 0, 0, 0);
         a1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ka, qf[1][s], a1, 0, 0, 0);
-        __builtin_amdgcn_sched_barrier(0);
+        if constexpr (V & 1) __builtin_amdgcn_sched_barrier(0);
       }
       sc[b4][0] = a0;
       sc[b4][1] = a1;
@@ -577,7 +584,7 @@ __global__ __launch_bounds__(NT, 2) void prefill_v2_kernel(
     bf16x8_t vr[PF];
 #pragma unroll
     for (int j = 0; j < PF; ++j) vr[j] = vread(j);
-    __builtin_amdgcn_sched_barrier(0);
+    if constexpr (V & 1) __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int j = 0; j < 2 * NB; ++j) {
       const int t2 = j / NB, n = j % NB;
@@ -585,7 +592,7 @@ __global__ __launch_bounds__(NT, 2) void prefill_v2_kernel(
       if (j + PF < 2 * NB) vr[j % PF] = vread(j + PF);
       o[0][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pa[t2][0], vb, o[0][n], 0, 0, 0);
       o[1][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pa[t2][1], vb, o[1][n], 0, 0, 0);
-      __builtin_amdgcn_sched_barrier(0);
+      if constexpr (V & 1) __builtin_amdgcn_sched_barrier(0);
     }
   };
 
@@ -975,7 +982,17 @@ extern "C" int llmd_paged_prefill(const void* q, int64_t q_stride, const void* k
                        items, Hq, Hkv, G, scale_log2, window, sinks, (uint16_t*)out, out_stride, v_scale,
                        xcd_map && (int64_t)n_items * grid3.y >= 1024 ? 1 : 0);
   } else if ((D == 128 || D == 64) && !fp8 && bs >= 16 && !v1_only) {
-    auto kern = D == 128 ? prefill_v2_kernel<128> : prefill_v2_kernel<64>;
+    static const int pv = [] {
+      const char* e = getenv("LLMD_PREFILL_V2_VARIANT");  // A/B of the round-4 schedule (V above)
+      return e ? (atoi(e) & 3) : 3;
+    }();
+    auto pick = [](int v, bool d128) {
+      if (d128) return v == 0 ? prefill_v2_kernel<128, 0> : v == 1 ? prefill_v2_kernel<128, 1>
+                     : v == 2 ? prefill_v2_kernel<128, 2> : prefill_v2_kernel<128, 3>;
+      return v == 0 ? prefill_v2_kernel<64, 0> : v == 1 ? prefill_v2_kernel<64, 1>
+             : v == 2 ? prefill_v2_kernel<64, 2> : prefill_v2_kernel<64, 3>;
+    };
+    auto kern = pick(pv, D == 128);
     hipLaunchKernelGGL(kern, grid, blk, 0, st, (const uint16_t*)q, q_stride, (const uint16_t*)kc,
                        (const uint16_t*)vc, block_stride, bs, block_tables, bt_stride, q_start, q_len, ctx_len,
                        items, Hq, Hkv, G, HPW, scale_log2, window, sinks, (uint16_t*)out, out_stride, v_scale,

@@ -1246,8 +1246,10 @@ int llmd_moe_gemm3_fp8(const void* X, int64_t x_stride, const float* xs, int64_t
   if (num_tiles == 0) return 0;
   dim3 grid((N + G3_BN - 1) / G3_BN, num_tiles);
   static const int g3v = [] {
-    const char* e = getenv("LLMD_MOE_V3_VARIANT");  // A/B of the round-4 fp8 v3 schedule (V above)
-    return e ? (atoi(e) & 3) : 3;
+    // A/B of the round-4 fp8 v3 schedule (V above; profiles/moe_gemm_v3_r4_ab.txt): the A prefetch
+    // lost 6 % (DeepSeek EP8 T=4096 2.20 -> 2.35 ms), the asm DMA alone is at parity or better -> 2
+    const char* e = getenv("LLMD_MOE_V3_VARIANT");
+    return e ? (atoi(e) & 3) : 2;
   }();
 #define LLMD_G3F8(M, Q)                                                                                           \
   do {                                                                                                            \
