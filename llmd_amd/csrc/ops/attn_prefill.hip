@@ -983,8 +983,10 @@ extern "C" int llmd_paged_prefill(const void* q, int64_t q_stride, const void* k
                        xcd_map && (int64_t)n_items * grid3.y >= 1024 ? 1 : 0);
   } else if ((D == 128 || D == 64) && !fp8 && bs >= 16 && !v1_only) {
     static const int pv = [] {
-      const char* e = getenv("LLMD_PREFILL_V2_VARIANT");  // A/B of the round-4 schedule (V above)
-      return e ? (atoi(e) & 3) : 3;
+      // A/B of the round-4 schedule (V above; profiles/attn_prefill_r4_ab.txt): the ring wins everywhere,
+      // the asm DMA only at full ISL and loses 12 % on one-wave grids (5000 x 512 chunk) -> 1
+      const char* e = getenv("LLMD_PREFILL_V2_VARIANT");
+      return e ? (atoi(e) & 3) : 1;
     }();
     auto pick = [](int v, bool d128) {
       if (d128) return v == 0 ? prefill_v2_kernel<128, 0> : v == 1 ? prefill_v2_kernel<128, 1>

@@ -959,16 +959,21 @@ __global__ __launch_bounds__(G3_NT, 1) void moe_gemm3_fp8_kernel(
         bfr[j][1] = *reinterpret_cast<const bf16x8_t*>(st + b_off + j * 2048 + sw_hi);
       }
       bf16x8_t a_cur[2], a_nxt[2];
-      if (rb_live > 0) {
+      if ((V & 1) && rb_live > 0) {
         a_cur[0] = *reinterpret_cast<const bf16x8_t*>(st + a_off + sw_lo);
         a_cur[1] = *reinterpret_cast<const bf16x8_t*>(st + a_off + sw_hi);
       }
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         if (i >= rb_live) break;  // wave-uniform: 32-row blocks past the expert's rows
-        if (i + 1 < rb_live) {
-          a_nxt[0] = *reinterpret_cast<const bf16x8_t*>(st + a_off + (i + 1) * 4096 + sw_lo);
-          a_nxt[1] = *reinterpret_cast<const bf16x8_t*>(st + a_off + (i + 1) * 4096 + sw_hi);
+        if constexpr (V & 1) {
+          if (i + 1 < rb_live) {
+            a_nxt[0] = *reinterpret_cast<const bf16x8_t*>(st + a_off + (i + 1) * 4096 + sw_lo);
+            a_nxt[1] = *reinterpret_cast<const bf16x8_t*>(st + a_off + (i + 1) * 4096 + sw_hi);
+          }
+        } else {
+          a_cur[0] = *reinterpret_cast<const bf16x8_t*>(st + a_off + i * 4096 + sw_lo);
+          a_cur[1] = *reinterpret_cast<const bf16x8_t*>(st + a_off + i * 4096 + sw_hi);
         }
 #pragma unroll
         for (int j = 0; j < 2; ++j)
@@ -977,8 +982,10 @@ __global__ __launch_bounds__(G3_NT, 1) void moe_gemm3_fp8_kernel(
             acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a_cur[ks], bfr[j][ks], acc[i][j], 0, 0, 0);
         __builtin_amdgcn_sched_barrier(0);
         if (i == 0 && refill) issue(kt + G3_NS - 1);
-        a_cur[0] = a_nxt[0];
-        a_cur[1] = a_nxt[1];
+        if constexpr (V & 1) {
+          a_cur[0] = a_nxt[0];
+          a_cur[1] = a_nxt[1];
+        }
       }
     } else {
       const int we = e8m0_of(wsr[kt >> 1]);
@@ -1278,14 +1285,24 @@ int llmd_moe_gemm3_bf16(const void* X, int64_t x_stride, int topk, const int* so
   if (K % 32 || x_stride % 8 || w_expert_stride % 8) return -1;
   if (num_tiles == 0) return 0;
   dim3 grid((N + G3_BN - 1) / G3_BN, num_tiles);
+  static const int bfv = [] {  // schedule variant for bf16 (bits as V; LLMD_MOE_V3_BF16_VARIANT)
+    const char* e = getenv("LLMD_MOE_V3_BF16_VARIANT");
+    return e ? (atoi(e) & 3) : 3;
+  }();
 #define LLMD_G3BF(M)                                                                                              \
-  hipLaunchKernelGGL((moe_gemm3_fp8_kernel<M, false, true>), grid, dim3(G3_NT), 0, st, (const uint8_t*)X, x_stride, \
+  do {                                                                                                            \
+    if (bfv == 0) LLMD_G3BFV(M, 0); else if (bfv == 1) LLMD_G3BFV(M, 1);                                        \
+    else if (bfv == 2) LLMD_G3BFV(M, 2); else LLMD_G3BFV(M, 3);                                                 \
+  } while (0)
+#define LLMD_G3BFV(M, VV)                                                                                         \
+  hipLaunchKernelGGL((moe_gemm3_fp8_kernel<M, false, true, VV>), grid, dim3(G3_NT), 0, st, (const uint8_t*)X, x_stride, \
                      nullptr, 0, topk, sorted_ids, tile_expert, (const uint8_t*)W, w_expert_stride, nullptr, N, K,  \
                      (uint16_t*)Y, y_stride, act, alpha, limit, a_rows_are_slots, (const uint16_t*)bias, nullptr, 0, \
                      nullptr, 0)
   if (mode == 0) LLMD_G3BF(0);
   else LLMD_G3BF(1);
 #undef LLMD_G3BF
+#undef LLMD_G3BFV
   return (int)hipGetLastError();
 }
 
