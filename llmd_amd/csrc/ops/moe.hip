@@ -1286,8 +1286,9 @@ int llmd_moe_gemm3_bf16(const void* X, int64_t x_stride, int topk, const int* so
   if (num_tiles == 0) return 0;
   dim3 grid((N + G3_BN - 1) / G3_BN, num_tiles);
   static const int bfv = [] {  // schedule variant for bf16 (bits as V; LLMD_MOE_V3_BF16_VARIANT)
+    // A/B (profiles/moe_gemm_v3_r4_ab.txt): without the A prefetch DeepSeek EP8 T=4096 794 -> 821 TF/s
     const char* e = getenv("LLMD_MOE_V3_BF16_VARIANT");
-    return e ? (atoi(e) & 3) : 3;
+    return e ? (atoi(e) & 3) : 2;
   }();
 #define LLMD_G3BF(M)                                                                                              \
   do {                                                                                                            \
