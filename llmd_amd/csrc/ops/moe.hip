@@ -860,6 +860,7 @@ __device__ __forceinline__ void g3_dma4(const void* src, char* lds_base) { glds4
 // Ablation switch for profiling (LLMD_MOE_ABLATE: 1 = no MFMA / fragment reads,
 // 2 = no DMA after the prologue); 0 in production.
 __device__ int g3_ablate = 0;
+__device__ int g3_xcd = 0;
 
 // V (fp8 A/B switch, round 4): bit 0 = A fragments read one row block ahead,
 // bit 1 = LDS-DMA from asm (glds16/glds4) instead of the builtin
@@ -872,7 +873,14 @@ __global__ __launch_bounds__(G3_NT, 1) void moe_gemm3_fp8_kernel(
     uint8_t* __restrict__ hq, int64_t hq_stride, float* __restrict__ hs, int64_t hs_stride) {
   // ONE __shared__ array (a second LDS object can make hipcc drain vmcnt before every ds_read)
   __shared__ __attribute__((aligned(1024))) char lds[G3_NS * G3_STAGE];
-  const int mt = blockIdx.y, nt = blockIdx.x;
+  // g3_xcd (LLMD_MOE_V3_XCD=1): deal tiles to XCDs in contiguous runs (xcd_remap) so the N tiles
+  // of one 256-row A panel share that XCD's L2 instead of every XCD fetching the panel
+  int mt = blockIdx.y, nt = blockIdx.x;
+  if (g3_xcd) {
+    const int l = xcd_remap(blockIdx.y * gridDim.x + blockIdx.x, gridDim.x * gridDim.y);
+    nt = l % gridDim.x;
+    mt = l / gridDim.x;
+  }
   const int e = tile_expert[mt];
   if (e < 0) return;
   static_assert(!(FQ && BF), "fused quantisation is an fp8-path epilogue");
@@ -1232,6 +1240,20 @@ void llmd_moe_gemm(const void* X, int64_t x_stride, int topk, const int* sorted_
 
 int llmd_moe_gemm3_tile_m() { return G3_BM; }
 
+// device-side switches of the v3 kernels, read from the environment once per process
+static void g3_env() {
+  static const bool done = [] {
+    const char* e = getenv("LLMD_MOE_ABLATE");
+    const int v = e ? atoi(e) : 0;
+    if (v) (void)hipMemcpyToSymbol(HIP_SYMBOL(g3_ablate), &v, sizeof v);
+    const char* x = getenv("LLMD_MOE_V3_XCD");
+    const int xv = x ? atoi(x) : 0;
+    if (xv) (void)hipMemcpyToSymbol(HIP_SYMBOL(g3_xcd), &xv, sizeof xv);
+    return true;
+  }();
+  (void)done;
+}
+
 // 256-row expert tiles (sorted by moe_align with bm = 256): the v3 kernel.
 // Needs power-of-two scales, K % 128 == 0 and 16-B aligned rows.
 // hq != nullptr (mode 1): fused e4m3 quantisation of the activation output into hq
@@ -1243,13 +1265,7 @@ int llmd_moe_gemm3_fp8(const void* X, int64_t x_stride, const float* xs, int64_t
                        int64_t hq_stride, float* hs, int64_t hs_stride, hipStream_t st) {
   if (K % 128 || x_stride % 16 || w_expert_stride % 16) return -1;
   if (hq && mode != 1) return -2;
-  static const int ablate = [] {
-    const char* e = getenv("LLMD_MOE_ABLATE");
-    const int v = e ? atoi(e) : 0;
-    if (v) (void)hipMemcpyToSymbol(HIP_SYMBOL(g3_ablate), &v, sizeof v);
-    return v;
-  }();
-  (void)ablate;
+  g3_env();
   if (num_tiles == 0) return 0;
   dim3 grid((N + G3_BN - 1) / G3_BN, num_tiles);
   static const int g3v = [] {
@@ -1283,6 +1299,7 @@ int llmd_moe_gemm3_bf16(const void* X, int64_t x_stride, int topk, const int* so
                         int mode, int act, float alpha, float limit, int a_rows_are_slots, const void* bias,
                         hipStream_t st) {
   if (K % 32 || x_stride % 8 || w_expert_stride % 8) return -1;
+  g3_env();
   if (num_tiles == 0) return 0;
   dim3 grid((N + G3_BN - 1) / G3_BN, num_tiles);
   static const int bfv = [] {  // schedule variant for bf16 (bits as V; LLMD_MOE_V3_BF16_VARIANT)
