@@ -558,6 +558,7 @@ __global__ __launch_bounds__(256, 1) void mla_v3_kernel(
 #pragma unroll
       for (int s = 0; s < 18; ++s) qf[hb][s] = *reinterpret_cast<const bf16x8_t*>(qr + 32 * s + 8 * g);
     }
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): Q landed (see mla_v4_kernel)
     // this lane's element offset inside a 64-key tile for each of its 18 DMA pieces
     // (slot u = 64 (w + NW k) + lane of the swizzled tile image)
     // (< 36,864: two 16-bit offsets per register, 9 VGPRs)
@@ -834,6 +835,235 @@ __global__ __launch_bounds__(128) void mla_reduce_kernel(const float* __restrict
   }
 }
 
+// ---------------------------------------------------------------- v4: v3 on a 4-deep ring of 32-key tiles
+// v3's decode at rows=64 spends over half its time waiting for the next 72 KB
+// tile (one tile in flight per CU, one workgroup per CU). v4 keeps v3's
+// registers and math (4 waves x 32 heads, O in a[0:255], scores via VGPR asm
+// MFMAs) but stages 32-key tiles (36,864 B) through a 4-slot ring: three tiles
+// (108 KB) in flight while one is computed, counted vmcnt waits (9 LDS-DMA
+// pieces per wave per tile) and a raw s_barrier per tile. bf16 latent caches.
+constexpr int V4_TILE = 32 * V2_ROWB;  // 36,864 B
+constexpr int V4_NS = 4;
+
+template <bool BIG, bool PBF>
+__global__ __launch_bounds__(256, 1) void mla_v4_kernel(
+    const uint16_t* __restrict__ q, int64_t q_row_stride, const void* __restrict__ kcv,
+    int64_t block_stride, int bs, const int* __restrict__ block_tables, int bt_stride,
+    const int* __restrict__ row_seq, const int* __restrict__ row_len, int H, float scale_log2,
+    int split_size, const int* __restrict__ split_dev, int nsplit, uint16_t* __restrict__ out,
+    int64_t out_row_stride, float* __restrict__ part_o, float* __restrict__ part_ml, float kv_scale) {
+  constexpr int NW = 4, NP = 9;  // DMA pieces per wave per tile (32 rows x 72 chunks / 256 lanes)
+  __shared__ __attribute__((aligned(1024))) char ring[V4_NS * V4_TILE];
+  const uint16_t* kc = reinterpret_cast<const uint16_t*>(kcv);
+  const int sp = blockIdx.x, r = blockIdx.z;
+  const int len = row_len[r];
+  if (split_dev) split_size = *split_dev;
+  const int k0 = sp * split_size, k1 = min(len, k0 + split_size);
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63, g = lane >> 4,
+            c16 = lane & 15;
+  const int h0 = 32 * w;
+  const int* bt = block_tables + (int64_t)row_seq[r] * bt_stride;
+  const int lbs = __builtin_ctz(bs);
+
+  float m[2] = {NEG_INF, NEG_INF}, l[2] = {0.f, 0.f};
+  MLA3_ZERO_ACC();
+
+  if (k0 < k1) {
+    bf16x8_t qf[2][18];
+#pragma unroll
+    for (int hb = 0; hb < 2; ++hb) {
+      const uint16_t* qr = q + (int64_t)r * q_row_stride + (int64_t)(h0 + 16 * hb + c16) * DQK;
+#pragma unroll
+      for (int s = 0; s < 18; ++s) qf[hb][s] = *reinterpret_cast<const bf16x8_t*>(qr + 32 * s + 8 * g);
+    }
+    // Q landed before the first DMA: waited here with the builtin (hipcc sees it), its own
+    // count-based waits for Q would otherwise also drain the asm DMAs issued after the loads
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+    unsigned poff[(NP + 1) / 2];  // two 16-bit element offsets per register
+#pragma unroll
+    for (int k = 0; k < NP; ++k) {
+      const int u = 64 * (w + NW * k) + lane;
+      const int row = u / CPR, ch = (u - row * CPR) ^ mla_swz(row);
+      const unsigned o = row * DQK + ch * 8;
+      if (k & 1) poff[k >> 1] |= o << 16; else poff[k >> 1] = o;
+    }
+    const unsigned ring0 = lds_addr(ring);
+    auto issue = [&](int t) {  // tile t (keys k0 + 32 t ..) into slot t % 4: NP pieces per wave
+      const int ts = k0 + 32 * t;
+      const unsigned l0 = ring0 + (t & (V4_NS - 1)) * V4_TILE + 1024 * w;
+      if (BIG && ts + 32 <= k1) {
+        const uint16_t* tb = kc + (int64_t)bt[ts >> lbs] * block_stride + (int64_t)(ts & (bs - 1)) * DQK;
+#pragma unroll
+        for (int k = 0; k < NP; ++k)
+          glds16(tb + ((k & 1) ? (poff[k >> 1] >> 16) : (poff[k >> 1] & 0xffffu)), l0 + 1024 * NW * k);
+        return;
+      }
+#pragma unroll
+      for (int k = 0; k < NP; ++k) {
+        int ln = lane;
+        asm volatile("" : "+v"(ln));
+        const int u = 64 * (w + NW * k) + ln;
+        const int row = u / CPR, ch = (u - row * CPR) ^ mla_swz(row);
+        const int key = min(ts + row, k1 - 1);
+        const int64_t off = (int64_t)bt[key >> lbs] * block_stride + (int64_t)(key & (bs - 1)) * DQK;
+        glds16(kc + off + ch * 8, l0 + 1024 * NW * k);
+      }
+    };
+    const int qq = c16 >> 2, pp = c16 & 3;
+    const int srow = rowoff(c16 >> 2) + (c16 & 3), ssw = mla_swz(srow);
+    const int gx = g ^ (ssw & 2);
+    const int offE = srow * V2_ROWB + 16 * (gx + (ssw & 4));
+    const int offO = srow * V2_ROWB + 16 * (gx - (ssw & 4));
+    const int vrow = rowoff(g) + qq, vk = mla_swz(vrow) >> 1;
+    int voff[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) voff[j] = vrow * V2_ROWB + 8 * (pp & 1) + 16 * (pp >> 1) + 32 * (j ^ vk);
+    auto compute = [&](const char* kt, int ts) {
+      auto kread = [&](int j) -> bf16x8_t {  // j = 18 b4 + s, b4 in {0, 1}
+        const int b4 = j / 18, s = j % 18;
+        return *reinterpret_cast<const bf16x8_t*>(kt + ((s & 1) ? offO : offE) + b4 * 16 * V2_ROWB + 64 * s);
+      };
+      auto vread = [&](int j) -> bf16x8_t {  // j = n (one 32-key block)
+        const int n = j & 31;
+        const char* p0 = kt + voff[n & 3] + 32 * (n & ~3);
+        s16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4_t*)p0);
+        s16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            (__attribute__((address_space(3))) s16x4_t*)(p0 + 16 * V2_ROWB));
+        return __builtin_bit_cast(bf16x8_t, s16x8_t{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]});
+      };
+      f32x4_t sc[2][2];
+      bf16x8_t kr[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) kr[j] = kread(j);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int b4 = 0; b4 < 2; ++b4) {
+#pragma unroll
+        for (int s = 0; s < 18; ++s) {
+          const int j = 18 * b4 + s;
+          const bf16x8_t ka = kr[j & 3];
+          if (j + 4 < 36) kr[j & 3] = kread(j + 4);
+          if (s == 0)
+            mla_mfma2_first(sc[0][b4], sc[1][b4], ka, qf[0][s], qf[1][s]);
+          else
+            mla_mfma2_acc(sc[0][b4], sc[1][b4], ka, qf[0][s], qf[1][s]);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      }
+      asm volatile("s_nop 7\n\ts_nop 7" ::: "memory");
+      if (ts + 32 > k1) {
+#pragma unroll
+        for (int hb = 0; hb < 2; ++hb)
+#pragma unroll
+          for (int b4 = 0; b4 < 2; ++b4)
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+              if (ts + 16 * b4 + rowoff(g) + i >= k1) sc[hb][b4][i] = NEG_INF;
+      }
+      bf16x8_t pa[2][1];
+#pragma unroll
+      for (int hb = 0; hb < 2; ++hb) {
+        float mx = NEG_INF;
+#pragma unroll
+        for (int b4 = 0; b4 < 2; ++b4)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) mx = fmaxf(mx, sc[hb][b4][i]);
+        const float tl = mx * scale_log2;
+        if (__ballot(tl > m[hb] + 8.f) != 0) {
+          float tm = fmaxf(tl, __shfl_xor(tl, 16, 64));
+          tm = fmaxf(tm, __shfl_xor(tm, 32, 64));
+          const float mnew = fmaxf(m[hb], tm);
+          const float alpha = (mnew == NEG_INF) ? 1.f : __builtin_amdgcn_exp2f(m[hb] - mnew);
+          l[hb] *= alpha;
+          m[hb] = mnew;
+          const float a0 = __shfl(alpha, 4 * g, 64), a1 = __shfl(alpha, 4 * g + 1, 64),
+                      a2 = __shfl(alpha, 4 * g + 2, 64), a3 = __shfl(alpha, 4 * g + 3, 64);
+          if (hb == 0) {
+            MLA3_RESCALE0(a0, a1, a2, a3);
+          } else {
+            MLA3_RESCALE1(a0, a1, a2, a3);
+          }
+        }
+        const float msub = (m[hb] == NEG_INF) ? 0.f : m[hb];
+        float ps = 0.f;
+#pragma unroll
+        for (int b4 = 0; b4 < 2; ++b4)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const float p = __builtin_amdgcn_exp2f(fmaf(sc[hb][b4][i], scale_log2, -msub));
+            sc[hb][b4][i] = p;
+            ps += p;
+          }
+        l[hb] += ps;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          pa[hb][0][j] = (__bf16)sc[hb][0][j];
+          pa[hb][0][4 + j] = (__bf16)sc[hb][1][j];
+        }
+      }
+      bf16x8_t vr[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) vr[j] = vread(j);
+      __builtin_amdgcn_sched_barrier(0);
+      asm volatile("s_nop 1" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+      MLA3_PV_BLOCK32
+    };
+    const int nt = (k1 - k0 + 31) >> 5;
+#pragma unroll
+    for (int t = 0; t < V4_NS - 1; ++t)
+      if (t < nt) issue(t);
+    for (int t = 0; t < nt; ++t) {
+      // tile t landed for this wave (tiles issued after it may stay in flight), the raw
+      // barrier extends that to every wave and retires the reads of slot (t + 3) % 4 (tile t - 1)
+      if (t + 2 < nt) asm volatile("s_waitcnt vmcnt(18)" ::: "memory");
+      else if (t + 1 < nt) asm volatile("s_waitcnt vmcnt(9)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      if (t + V4_NS - 1 < nt) issue(t + V4_NS - 1);
+      compute(ring + (t & (V4_NS - 1)) * V4_TILE, k0 + 32 * t);
+    }
+  }
+  MLA3_DRAIN();
+#pragma unroll
+  for (int hb = 0; hb < 2; ++hb) {
+    const int hh = h0 + 16 * hb;
+    float lt = l[hb] + __shfl_xor(l[hb], 16, 64);
+    lt += __shfl_xor(lt, 32, 64);
+    const float inv = lt > 0.f ? kv_scale / lt : 0.f;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      float x[32];
+      if (hb == 0) {
+        if (i == 0) { MLA3_READ_0_0(x) } else if (i == 1) { MLA3_READ_0_1(x) }
+        else if (i == 2) { MLA3_READ_0_2(x) } else { MLA3_READ_0_3(x) }
+      } else {
+        if (i == 0) { MLA3_READ_1_0(x) } else if (i == 1) { MLA3_READ_1_1(x) }
+        else if (i == 2) { MLA3_READ_1_2(x) } else { MLA3_READ_1_3(x) }
+      }
+      if (nsplit == 1) {
+        const float f = __shfl(inv, 4 * g + i, 64);
+        uint16_t* orow = out + (int64_t)r * out_row_stride + (int64_t)(hh + 4 * g + i) * DV;
+#pragma unroll
+        for (int n = 0; n < 32; ++n) orow[16 * n + c16] = f2bf(x[n] * f);
+      } else if constexpr (PBF) {
+        uint16_t* po = reinterpret_cast<uint16_t*>(part_o) + (((int64_t)r * H + hh + 4 * g + i) * nsplit + sp) * DV;
+#pragma unroll
+        for (int n = 0; n < 32; ++n) po[16 * n + c16] = f2bf(x[n] * kv_scale);
+      } else {
+        float* po = part_o + (((int64_t)r * H + hh + 4 * g + i) * nsplit + sp) * DV;
+#pragma unroll
+        for (int n = 0; n < 32; ++n) po[16 * n + c16] = x[n] * kv_scale;
+      }
+    }
+    if (nsplit > 1 && g == 0) {
+      float* pm = part_ml + (((int64_t)r * H + hh + c16) * nsplit + sp) * 2;
+      pm[0] = m[hb];
+      pm[1] = lt;
+    }
+  }
+}
+
 // Split merge, one wave per (row, head): lane l owns dims 8l..8l+7 (16-B partial
 // loads, bf16 or fp32), the split weights exp2(m_s - M) / sum are wave-uniform.
 // 4 heads per 256-thread workgroup.
@@ -902,7 +1132,7 @@ extern "C" int llmd_mla_v2_shape(int R, int fp8) {
     e = getenv("LLMD_MLA_NW");
     return e ? 10 * atoi(e) + 1 : 0;
   }();
-  if (forced == 41 || forced == 42 || forced == 81) return forced;
+  if (forced == 41 || forced == 42 || forced == 43 || forced == 81) return forced;
   return R <= 16 ? 41 : 42;
 }
 
@@ -953,6 +1183,14 @@ extern "C" int llmd_mla_attention(const void* q, int64_t q_row_stride, const voi
   } else {                                         \
     if (big) V2(NW, true, false); else V2(NW, false, false); \
   }
+#define V4(BIG)                                                                                                \
+  do {                                                                                                         \
+    if (pbf) V4P(BIG, true); else V4P(BIG, false);                                                             \
+  } while (0)
+#define V4P(BIG, P)                                                                                            \
+  hipLaunchKernelGGL((mla_v4_kernel<BIG, P>), dim3(nsplit, 1, R), dim3(256), 0, st, (const uint16_t*)q,          \
+                     q_row_stride, kc, block_stride, bs, block_tables, bt_stride, row_seq, row_len, H, scale_log2, \
+                     split_size, split_dev, nsplit, (uint16_t*)out, out_row_stride, part_o, part_ml, kv_scale)
 #define V3(BIG, F8)                                                                                            \
   if (pbf) V3P(BIG, F8, true); else V3P(BIG, F8, false)
 #define V3P(BIG, F8, P)                                                                                        \
@@ -961,10 +1199,12 @@ extern "C" int llmd_mla_attention(const void* q, int64_t q_row_stride, const voi
                      split_size, split_dev, nsplit, (uint16_t*)out, out_row_stride, part_o, part_ml, kv_scale)
     const bool big = bs >= 64;
     const int shape = H == 128 ? llmd_mla_v2_shape(R, fp8) : 41;
-    pbf = shape == 42 && nsplit > 1 && mla_partial_bf16();
+    pbf = (shape == 42 || shape == 43) && nsplit > 1 && mla_partial_bf16();
     if (shape == 81) {
       V2NW(8)
-    } else if (shape == 42) {
+    } else if (shape == 43 && !fp8) {
+      if (big) V4(true); else V4(false);
+    } else if (shape == 42 || shape == 43) {
       if (fp8) {
         if (big) V3(true, true); else V3(false, true);
       } else {
@@ -975,6 +1215,8 @@ extern "C" int llmd_mla_attention(const void* q, int64_t q_row_stride, const voi
     }
 #undef V3
 #undef V3P
+#undef V4
+#undef V4P
 #undef V2NW
 #undef V2
   } else {

@@ -37,6 +37,9 @@ def test_v3_accumulators_only_in_asm(tmp_path):
     s = s_path.read_text()
     names = re.findall(r"^(_ZN\S*mla_v3_kernelILb[01]ELb[01]ELb[01]E\S*):", s, re.M)  # BIG x fp8 x bf16-partials
     assert len(names) == 8
+    v4 = re.findall(r"^(_ZN\S*mla_v4_kernelILb[01]ELb[01]E\S*):", s, re.M)  # the 32-key ring form
+    assert len(v4) == 4
+    names += v4
     for name in names:
         i = s.index(name + ":")
         j = s.index(".Lfunc_end", i)
