@@ -475,10 +475,18 @@ __global__ __launch_bounds__(NT, 2) void prefill_v2_kernel(
     if (!active) return;
     // S^T: K fragment j = KS b4 + s, read PF ahead of its two MFMAs (a ring with a
     // sched_barrier per step: hipcc's own schedule hoists every read and waits lgkmcnt(0))
-    constexpr int PF = 4;
+    constexpr int PF = (V & 4) ? 6 : 4;  // fragments read ahead (V bit 2: 6)
     auto kread = [&](int j) {
       return *reinterpret_cast<const bf16x8_t*>(img + kofs[j % KS] + (j / KS) * 16 * RB);
     };
+    // PV: V fragment j = NB t2 + n (two transposed reads), PF ahead of its two MFMAs
+    auto vread = [&](int j) {
+      const char* p0 = img + vofs[j % NB] + 32 * (j / NB) * RB;
+      s16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4_t*)p0);
+      s16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4_t*)(p0 + 16 * RB));
+      return __builtin_bit_cast(bf16x8_t, s16x8_t{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]});
+    };
+    bf16x8_t vr[PF];
     f32x4_t sc[4][2];
     bf16x8_t kr[PF];
 #pragma unroll
@@ -498,6 +506,10 @@ __global__ __launch_bounds__(NT, 2) void prefill_v2_kernel(
       }
       sc[b4][0] = a0;
       sc[b4][1] = a1;
+    }
+    if constexpr (V & 8) {  // the first V fragments load under the mask + softmax (V bit 3)
+#pragma unroll
+      for (int j = 0; j < PF; ++j) vr[j] = vread(j);
     }
     const bool need_mask = (ts + 63 > p_lo) || (window > 0 && ts <= p_hi - window);
     if (need_mask) {
@@ -574,16 +586,10 @@ __global__ __launch_bounds__(NT, 2) void prefill_v2_kernel(
           pa[t2][nb][j] = (__bf16)sc[2 * t2][nb][j];
           pa[t2][nb][4 + j] = (__bf16)sc[2 * t2 + 1][nb][j];
         }
-    // PV: V fragment j = NB t2 + n (two transposed reads), PF ahead of its two MFMAs
-    auto vread = [&](int j) {
-      const char* p0 = img + vofs[j % NB] + 32 * (j / NB) * RB;
-      s16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4_t*)p0);
-      s16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4_t*)(p0 + 16 * RB));
-      return __builtin_bit_cast(bf16x8_t, s16x8_t{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]});
-    };
-    bf16x8_t vr[PF];
+    if constexpr (!(V & 8)) {
 #pragma unroll
-    for (int j = 0; j < PF; ++j) vr[j] = vread(j);
+      for (int j = 0; j < PF; ++j) vr[j] = vread(j);
+    }
     if constexpr (V & 1) __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int j = 0; j < 2 * NB; ++j) {
@@ -986,13 +992,17 @@ extern "C" int llmd_paged_prefill(const void* q, int64_t q_stride, const void* k
       // A/B of the round-4 schedule (V above; profiles/attn_prefill_r4_ab.txt): the ring wins everywhere,
       // the asm DMA only at full ISL and loses 12 % on one-wave grids (5000 x 512 chunk) -> 1
       const char* e = getenv("LLMD_PREFILL_V2_VARIANT");
-      return e ? (atoi(e) & 3) : 1;
+      return e ? (atoi(e) & 15) : 1;
     }();
-    auto pick = [](int v, bool d128) {
-      if (d128) return v == 0 ? prefill_v2_kernel<128, 0> : v == 1 ? prefill_v2_kernel<128, 1>
-                     : v == 2 ? prefill_v2_kernel<128, 2> : prefill_v2_kernel<128, 3>;
-      return v == 0 ? prefill_v2_kernel<64, 0> : v == 1 ? prefill_v2_kernel<64, 1>
-             : v == 2 ? prefill_v2_kernel<64, 2> : prefill_v2_kernel<64, 3>;
+    auto pick = [](int v, bool d128) {  // instantiated: 0-3, 5 (PF 6), 9 (early V), 13 (both)
+      if (d128) return v == 0 ? prefill_v2_kernel<128, 0> : v == 2 ? prefill_v2_kernel<128, 2>
+                     : v == 3 ? prefill_v2_kernel<128, 3> : v == 5 ? prefill_v2_kernel<128, 5>
+                     : v == 9 ? prefill_v2_kernel<128, 9> : v == 13 ? prefill_v2_kernel<128, 13>
+                     : prefill_v2_kernel<128, 1>;
+      return v == 0 ? prefill_v2_kernel<64, 0> : v == 2 ? prefill_v2_kernel<64, 2>
+             : v == 3 ? prefill_v2_kernel<64, 3> : v == 5 ? prefill_v2_kernel<64, 5>
+             : v == 9 ? prefill_v2_kernel<64, 9> : v == 13 ? prefill_v2_kernel<64, 13>
+             : prefill_v2_kernel<64, 1>;
     };
     auto kern = pick(pv, D == 128);
     hipLaunchKernelGGL(kern, grid, blk, 0, st, (const uint16_t*)q, q_stride, (const uint16_t*)kc,
