@@ -990,9 +990,10 @@ extern "C" int llmd_paged_prefill(const void* q, int64_t q_stride, const void* k
   } else if ((D == 128 || D == 64) && !fp8 && bs >= 16 && !v1_only) {
     static const int pv = [] {
       // A/B of the round-4 schedule (V above; profiles/attn_prefill_r4_ab.txt): the ring wins everywhere,
-      // the asm DMA only at full ISL and loses 12 % on one-wave grids (5000 x 512 chunk) -> 1
+      // the asm DMA only at full ISL and loses 12 % on one-wave grids (5000 x 512 chunk); reading
+      // 6 fragments ahead (bit 2) adds ~1 % -> 5
       const char* e = getenv("LLMD_PREFILL_V2_VARIANT");
-      return e ? (atoi(e) & 15) : 1;
+      return e ? (atoi(e) & 15) : 5;
     }();
     auto pick = [](int v, bool d128) {  // instantiated: 0-3, 5 (PF 6), 9 (early V), 13 (both)
       if (d128) return v == 0 ? prefill_v2_kernel<128, 0> : v == 2 ? prefill_v2_kernel<128, 2>
