@@ -378,8 +378,7 @@ class Scheduler:
 
     def _align_tokens(self, out: SchedulerOutput) -> None:
         """Trim prefill chunks, newest first, so the step's token count is a
-        multiple of ``prefill_token_align`` (GEMM-friendly M; between one and two units only
-        when the step also carries decodes). With
+        multiple of ``prefill_token_align`` (GEMM-friendly M). With
         ``LLMD_ALIGN_KEEP_FINAL=1`` only chunks that do not finish their prompt
         give tokens up (trimming a FINAL chunk adds a whole extra step for its
         tail: a 5000-token prompt beside 64 decodes becomes 4608- and 518-token
@@ -394,13 +393,7 @@ class Scheduler:
             return
         total = out.num_tokens
         rem = total % a
-        if rem == 0 or total < a:
-            return
-        if total < 2 * a and not out.decodes:
-            # a one-unit prefill-only step would leave its tail as an extra step; with decodes
-            # in the step the tail rides along with the next decode step (a 455-token prompt
-            # remainder + 63 decodes = 518 -> 512: the 70B layer's GEMMs 0.86 -> 0.76 ms,
-            # profiles/gemm_m518_r4.txt)
+        if total < 2 * a or rem == 0:
             return
 
         def slack(sr):
