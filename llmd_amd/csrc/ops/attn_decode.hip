@@ -59,12 +59,19 @@ template <>
 struct CacheReg<true> {
   using T = u32x2_t;
 };
-template <bool F8>
+// NTL: non-temporal (nt) loads - the K/V of a decode step is read once, and a
+// layer's cache (1.3 GB at 64 x 5000 tokens for 70B) never fits the 256 MB MALL
+template <bool F8, bool NTL = false>
 __device__ __forceinline__ typename CacheReg<F8>::T ld_cache(const void* base, int64_t off) {
-  if constexpr (F8)
-    return *reinterpret_cast<const u32x2_t*>(reinterpret_cast<const uint8_t*>(base) + off);
-  else
-    return *reinterpret_cast<const u32x4_t*>(reinterpret_cast<const uint16_t*>(base) + off);
+  if constexpr (F8) {
+    const u32x2_t* p = reinterpret_cast<const u32x2_t*>(reinterpret_cast<const uint8_t*>(base) + off);
+    if constexpr (NTL) return __builtin_nontemporal_load(p);
+    return *p;
+  } else {
+    const u32x4_t* p = reinterpret_cast<const u32x4_t*>(reinterpret_cast<const uint16_t*>(base) + off);
+    if constexpr (NTL) return __builtin_nontemporal_load(p);
+    return *p;
+  }
 }
 template <bool F8>
 __device__ __forceinline__ u32x4_t widen(const typename CacheReg<F8>::T v) {
@@ -84,7 +91,7 @@ struct TileState {
   float m[NP], lsum[NP];
 };
 
-template <int D, bool F8, int NP>
+template <int D, bool F8, int NP, bool NTL = false>
 __device__ __forceinline__ void attend_tiles(TileState<D, F8, NP>& st, const void* __restrict__ kc,
                                              const void* __restrict__ vc, int64_t block_stride, int bs,
                                              const int* __restrict__ bt, int64_t head_off, int s0, int s1,
@@ -114,7 +121,7 @@ __device__ __forceinline__ void attend_tiles(TileState<D, F8, NP>& st, const voi
       LLMD_DCHECK(phys >= 0);
       const int64_t kr = (int64_t)phys * block_stride + head_off + (int64_t)(key & (bs - 1)) * D;
 #pragma unroll
-      for (int s = 0; s < KS; ++s) kf[b4][s] = ld_cache<F8>(kc, kr + (4 * s + g) * 8);
+      for (int s = 0; s < KS; ++s) kf[b4][s] = ld_cache<F8, NTL>(kc, kr + (4 * s + g) * 8);
     }
   };
   if (w < ntile) load_k(w);
@@ -129,7 +136,7 @@ __device__ __forceinline__ void attend_tiles(TileState<D, F8, NP>& st, const voi
       key = key < s1 ? key : s0;
       const int phys = bt[key >> lbs];
       const int64_t vp = (int64_t)phys * block_stride + head_off + (int64_t)(key & (bs - 1)) * D;
-      vr[i] = ld_cache<F8>(vc, vp + (lane % CPR) * 8);
+      vr[i] = ld_cache<F8, NTL>(vc, vp + (lane % CPR) * 8);
     }
     // ---- S^T = K Q^T for every pass
     f32x4_t sc[NP][4];
@@ -272,7 +279,7 @@ __device__ __forceinline__ void merge_waves(const TileState<D, F8, NP>& st, int 
 // its shared prefix `sstart[b]` when the shared-prefix kernel covers the rest).
 // direct: one split and no shared prefix - normalise and write `out` here;
 // otherwise partial slot `sp` of nslot per (seq, head).
-template <int D, bool F8>
+template <int D, bool F8, bool NTL = false>
 __global__ __launch_bounds__(NT, 2) void paged_decode_kernel(
     const uint16_t* __restrict__ q, int64_t q_stride, const void* __restrict__ kc,
     const void* __restrict__ vc, int64_t block_stride, int bs,
@@ -319,7 +326,7 @@ __global__ __launch_bounds__(NT, 2) void paged_decode_kernel(
 #pragma unroll
   for (int n = 0; n < NB; ++n) st.o[0][n] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 
-  attend_tiles<D, F8, 1>(st, kc, vc, block_stride, bs, bt, head_off, s0, s1, scale_log2,
+  attend_tiles<D, F8, 1, NTL>(st, kc, vc, block_stride, bs, bt, head_off, s0, s1, scale_log2,
                          smem + w * (64 * D * 2), w, lane);
 
   merge_waves<D, F8, 1>(st, 0, smem, w, lane, [&](int h, int d, float acc, float M, float Ls) {
@@ -715,6 +722,11 @@ extern "C" int llmd_paged_decode(const void* q, int64_t q_stride, const void* kc
   if (!direct && nslot < nsplit) return -3;
   dim3 grid(nsplit, Hkv * NG, B), blk(NT);
   const size_t lds = (size_t)4 * 64 * D * 2;
+  static const bool nt_env = [] {  // non-temporal K/V loads by default (LLMD_DECODE_NT=0 for A/B): with the
+    const char* e = getenv("LLMD_DECODE_NT");  // nt weight stream, 70B decode 44.1 -> 43.5 ms/step
+    return !(e && e[0] == '0');                 // (profiles/decode_nt_r4.txt)
+  }();
+  auto decode_nt = [] { return nt_env; };
 #define LAUNCH(DD, F8)                                                                                       \
   do {                                                                                                       \
     if (cascade) {                                                                                           \
@@ -732,7 +744,8 @@ extern "C" int llmd_paged_decode(const void* q, int64_t q_stride, const void* kc
                            (const uint16_t*)q, q_stride, kc, vc, block_stride, bs, block_tables, bt_stride,  \
                            members, work, Hq, G, scale_log2, nslot, nsplit, part_o, part_ml, v_scale);               \
     }                                                                                                        \
-    hipLaunchKernelGGL((paged_decode_kernel<DD, F8>), grid, blk, lds, st, (const uint16_t*)q, q_stride, kc,  \
+    hipLaunchKernelGGL((decode_nt() ? paged_decode_kernel<DD, F8, true> : paged_decode_kernel<DD, F8, false>), \
+                       grid, blk, lds, st, (const uint16_t*)q, q_stride, kc,                                 \
                        vc, block_stride, bs, block_tables, bt_stride, seq_lens, cascade ? sstart : nullptr,  \
                        Hq, Hkv, G, NG, scale_log2, window, sinks, split_size, split_dev,                     \
                        direct ? nsplit : nslot,                                                              \

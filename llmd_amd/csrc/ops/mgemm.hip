@@ -53,7 +53,7 @@ struct Geo {
   static_assert(BM % 32 == 0, "MB must be even");
 };
 
-template <int MB, int WRB, int S, bool F8 = false>
+template <int MB, int WRB, int S, bool F8 = false, int POL = 0>
 __global__ __launch_bounds__(NT, 1) void mgemm_kernel(const void* __restrict__ xv, int64_t x_stride,
                                                       const void* __restrict__ wv_, int64_t w_stride, int M,
                                                       int N, int K, int steps_per_split, uint16_t* __restrict__ y,
@@ -104,7 +104,7 @@ __global__ __launch_bounds__(NT, 1) void mgemm_kernel(const void* __restrict__ x
     for (int i = 0; i < G::NW; ++i)
       __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)(wbase + k0 + woff[i]),
                                        (void __attribute__((address_space(3)))*)(stg + 1024 * (ws + 4 * i)), 16, 0,
-                                       0);
+                                       POL);  // POL 2 = nt: every W byte is read once per step
 #pragma unroll
     for (int i = 0; i < G::NX; ++i)
       __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)(x + k0 + xoff[i]),
@@ -282,25 +282,41 @@ __global__ __launch_bounds__(256) void mgemm_reduce_kernel(const float* __restri
 typedef void (*mkern_t)(const void*, int64_t, const void*, int64_t, int, int, int, int, uint16_t*, int64_t,
                         float*, const float*, const float*);
 
-template <int MB, bool F8>
+template <int MB, bool F8, int POL>
 mkern_t pick_w(int wrb, int stages) {
-  if (wrb == 1) return stages == 3 ? mgemm_kernel<MB, 1, 3, F8> : mgemm_kernel<MB, 1, 4, F8>;
-  if (wrb == 2) return stages == 3 ? mgemm_kernel<MB, 2, 3, F8> : mgemm_kernel<MB, 2, 4, F8>;
+  if (wrb == 1) return stages == 3 ? mgemm_kernel<MB, 1, 3, F8, POL> : mgemm_kernel<MB, 1, 4, F8, POL>;
+  if (wrb == 2) return stages == 3 ? mgemm_kernel<MB, 2, 3, F8, POL> : mgemm_kernel<MB, 2, 4, F8, POL>;
   if (wrb == 4) {
-    if (stages == 3) return mgemm_kernel<MB, 4, 3, F8>;
-    if constexpr (MB == 4) return mgemm_kernel<MB, 4, 4, F8>;  // 160 KB: the only 4-stage ring of 256-row tiles that fits
+    if (stages == 3) return mgemm_kernel<MB, 4, 3, F8, POL>;
+    if constexpr (MB == 4) return mgemm_kernel<MB, 4, 4, F8, POL>;  // 160 KB: the only 4-stage ring of 256-row tiles that fits
+  }
+  return nullptr;
+}
+
+// The W stream's LDS-DMA with the nt policy by default (LLMD_MGEMM_NT=0: default policy, for A/B).
+// 70B decode batch 64 ctx 5000: 46.6-47.2 -> 44.1 ms/step (profiles/decode_nt_r4.txt): every W
+// byte is read once per step and a layer's weights (1.7 GB) never fit the MALL
+bool mgemm_nt() {
+  static const bool v = [] {
+    const char* e = getenv("LLMD_MGEMM_NT");
+    return !(e && e[0] == '0');
+  }();
+  return v;
+}
+
+template <bool F8, int POL>
+mkern_t pick_m_pol(int mb, int wrb, int stages) {
+  switch (mb) {
+    case 4: return pick_w<4, F8, POL>(wrb, stages);
+    case 6: return pick_w<6, F8, POL>(wrb, stages);
+    case 8: return pick_w<8, F8, POL>(wrb, stages);
   }
   return nullptr;
 }
 
 template <bool F8>
 mkern_t pick_m(int mb, int wrb, int stages) {
-  switch (mb) {
-    case 4: return pick_w<4, F8>(wrb, stages);
-    case 6: return pick_w<6, F8>(wrb, stages);
-    case 8: return pick_w<8, F8>(wrb, stages);
-  }
-  return nullptr;
+  return mgemm_nt() ? pick_m_pol<F8, 2>(mb, wrb, stages) : pick_m_pol<F8, 0>(mb, wrb, stages);
 }
 
 }  // namespace
