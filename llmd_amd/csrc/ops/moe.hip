@@ -345,15 +345,27 @@ constexpr int G2_AB = G2_BM * 128, G2_BB = G2_BN * 128, G2_BUF = G2_AB + G2_BB;
 
 __device__ __forceinline__ int g2_swz(int row, int c) { return c ^ ((row >> 1) & 7); }
 
+template <int POL = 0>  // POL 2: nt policy (the expert-weight stream of decode-sized steps)
 __device__ __forceinline__ void g2_dma(const void* src, char* lds_base) {
   __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)src,
-                                   (void __attribute__((address_space(3)))*)lds_base, 16, 0, 0);
+                                   (void __attribute__((address_space(3)))*)lds_base, 16, 0, POL);
+}
+// Expert weights of the v2 kernels (the steps below the v3 row threshold: decode, small mixed
+// steps - an expert's panel is read by one or two row tiles) with the nt policy by default
+// (LLMD_MOE_NT=0: default policy, for A/B). gpt-oss-120b decode: fp8 batch 256 38.9 -> 36.8 ms,
+// bf16 batch 112 44.4 -> 41.7 ms (profiles/decode_nt_r4.txt)
+static bool moe_nt() {
+  static const bool v = [] {
+    const char* e = getenv("LLMD_MOE_NT");
+    return !(e && e[0] == '0');
+  }();
+  return v;
 }
 // LDS-DMA from inline asm (llmd_common.h glds16 / glds4) for the v3 kernel: hipcc then keeps
 // counted lgkmcnt(N) waits for its fragment reads; the K loop's counted vmcnt covers them
 __device__ __forceinline__ void g3_dma16(const void* src, char* lds_base) { glds16(src, lds_addr(lds_base)); }
 
-template <int MODE>
+template <int MODE, int POL = 0>
 __global__ __launch_bounds__(G2_NT, 2) void moe_gemm2_kernel(
     const uint16_t* __restrict__ X, int64_t x_stride, int topk, const int* __restrict__ sorted_ids,
     const int* __restrict__ tile_expert, const uint16_t* __restrict__ W, int64_t w_expert_stride, int N, int K,
@@ -388,7 +400,7 @@ __global__ __launch_bounds__(G2_NT, 2) void moe_gemm2_kernel(
 #pragma unroll
     for (int i = 0; i < 2; ++i) g2_dma(asrc[i] + k0, base + (2 * w + i) * 1024);
 #pragma unroll
-    for (int i = 0; i < 8; ++i) g2_dma(bsrc[i] + k0, base + G2_AB + (8 * w + i) * 1024);
+    for (int i = 0; i < 8; ++i) g2_dma<POL>(bsrc[i] + k0, base + G2_AB + (8 * w + i) * 1024);
   };
   f32x4_t acc[4][4];
 #pragma unroll
@@ -653,7 +665,7 @@ typedef int i32x8_t __attribute__((ext_vector_type(8)));
 // value (probed: scripts/probes/mfma_scale_map2.hip) - and the product is
 // accumulated in place: no per-step block accumulator, no VALU re-scaling
 // (~10 VALU per MFMA before), MFMAs back to back.
-template <int MODE, bool HWS>
+template <int MODE, bool HWS, int POL = 0>
 __global__ __launch_bounds__(G2_NT, 2) void moe_gemm2_fp8_kernel(
     const uint8_t* __restrict__ X, int64_t x_stride, const float* __restrict__ xs, int64_t xs_stride, int topk,
     const int* __restrict__ sorted_ids, const int* __restrict__ tile_expert, const uint8_t* __restrict__ W,
@@ -702,7 +714,7 @@ __global__ __launch_bounds__(G2_NT, 2) void moe_gemm2_fp8_kernel(
 #pragma unroll
     for (int i = 0; i < 2; ++i) g2_dma(asrc[i] + k0, base + (2 * w + i) * 1024);
 #pragma unroll
-    for (int i = 0; i < 8; ++i) g2_dma(We + boff[i] + k0, base + G2_AB + (8 * w + i) * 1024);
+    for (int i = 0; i < 8; ++i) g2_dma<POL>(We + boff[i] + k0, base + G2_AB + (8 * w + i) * 1024);
   };
   const int r16 = lane & 15, kq = lane >> 4;
   f32x4_t acc[4][4];
@@ -1217,12 +1229,13 @@ void llmd_moe_gemm(const void* X, int64_t x_stride, int topk, const int* sorted_
   }();
   if (v2 && K % 64 == 0 && (x_stride % 8) == 0 && (w_expert_stride % 8) == 0) {
     dim3 grid2((N + G2_BN - 1) / G2_BN, num_tiles);
+    const bool nt = moe_nt();
     if (mode == 0)
-      hipLaunchKernelGGL(moe_gemm2_kernel<0>, grid2, dim3(G2_NT), 0, st, (const uint16_t*)X, x_stride, topk,
+      hipLaunchKernelGGL((nt ? moe_gemm2_kernel<0, 2> : moe_gemm2_kernel<0, 0>), grid2, dim3(G2_NT), 0, st, (const uint16_t*)X, x_stride, topk,
                          sorted_ids, tile_expert, (const uint16_t*)W, w_expert_stride, N, K, (uint16_t*)Y, y_stride,
                          act, alpha, limit, a_rows_are_slots, (const uint16_t*)bias);
     else
-      hipLaunchKernelGGL(moe_gemm2_kernel<1>, grid2, dim3(G2_NT), 0, st, (const uint16_t*)X, x_stride, topk,
+      hipLaunchKernelGGL((nt ? moe_gemm2_kernel<1, 2> : moe_gemm2_kernel<1, 0>), grid2, dim3(G2_NT), 0, st, (const uint16_t*)X, x_stride, topk,
                          sorted_ids, tile_expert, (const uint16_t*)W, w_expert_stride, N, K, (uint16_t*)Y, y_stride,
                          act, alpha, limit, a_rows_are_slots, (const uint16_t*)bias);
     return;
@@ -1341,8 +1354,9 @@ void llmd_moe_gemm_fp8(const void* X, int64_t x_stride, const float* xs, int64_t
   }();
   if (v2 && K % 128 == 0 && K / 128 <= G2_MAX_KB && x_stride % 16 == 0 && w_expert_stride % 16 == 0) {
     dim3 grid2((N + G2_BN - 1) / G2_BN, num_tiles);
+    const bool nt = moe_nt();
 #define LLMD_G2F8(M, H)                                                                                           \
-  hipLaunchKernelGGL((moe_gemm2_fp8_kernel<M, H>), grid2, dim3(G2_NT), 0, st, (const uint8_t*)X, x_stride, xs,     \
+  hipLaunchKernelGGL((nt ? moe_gemm2_fp8_kernel<M, H, 2> : moe_gemm2_fp8_kernel<M, H, 0>), grid2, dim3(G2_NT), 0, st, (const uint8_t*)X, x_stride, xs,     \
                      xs_stride, topk, sorted_ids, tile_expert, (const uint8_t*)W, w_expert_stride, ws, N, K,       \
                      (uint16_t*)Y, y_stride, act, alpha, limit, a_rows_are_slots, (const uint16_t*)bias)
     if (mode == 0) {
