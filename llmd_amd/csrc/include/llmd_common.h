@@ -188,6 +188,20 @@ __device__ __forceinline__ void glds16(const void* gsrc, unsigned lds_dst) {
                : "memory");
 }
 
+// glds16 with the nt cache policy (a stream read once per launch)
+__device__ __forceinline__ void glds16_nt(const void* gsrc, unsigned lds_dst) {
+#if !LLMD_ASM_DMA
+  __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)gsrc,
+                                   (void __attribute__((address_space(3)))*)(uintptr_t)lds_dst, 16, 0, 2);
+  return;
+#endif
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off nt\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(gsrc), "s"(__builtin_amdgcn_readfirstlane(lds_dst))
+               : "memory");
+}
+
 // 4-byte-per-lane form (global_load_lds_dword), same contract as glds16
 __device__ __forceinline__ void glds4(const void* gsrc, unsigned lds_dst) {
 #if !LLMD_ASM_DMA

@@ -937,7 +937,8 @@ __global__ __launch_bounds__(G3_NT, 1) void moe_gemm3_fp8_kernel(
     }
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
-      if constexpr (V & 2) g3_dma16(We + boff[i] + k0, st + G3_A + (2 * w + i) * 1024);
+      if constexpr ((V & 6) == 6) glds16_nt(We + boff[i] + k0, lds_addr(st + G3_A + (2 * w + i) * 1024));
+      else if constexpr (V & 2) g3_dma16(We + boff[i] + k0, st + G3_A + (2 * w + i) * 1024);
       else g2_dma(We + boff[i] + k0, st + G3_A + (2 * w + i) * 1024);
     }
     if constexpr (!BF) {
@@ -1253,6 +1254,15 @@ void llmd_moe_gemm(const void* X, int64_t x_stride, int topk, const int* sorted_
 
 int llmd_moe_gemm3_tile_m() { return G3_BM; }
 
+// LLMD_MOE_V3_NT=1: the v3 expert-weight DMA with the nt policy (schedule variant 2 only; A/B)
+static bool g3_nt() {
+  static const bool v = [] {
+    const char* e = getenv("LLMD_MOE_V3_NT");
+    return e && e[0] == '1';
+  }();
+  return v;
+}
+
 // device-side switches of the v3 kernels, read from the environment once per process
 static void g3_env() {
   static const bool done = [] {
@@ -1289,6 +1299,7 @@ int llmd_moe_gemm3_fp8(const void* X, int64_t x_stride, const float* xs, int64_t
   }();
 #define LLMD_G3F8(M, Q)                                                                                           \
   do {                                                                                                            \
+    if (g3v == 2 && g3_nt()) LLMD_G3F8V(M, Q, 6); else                                                          \
     if (g3v == 0) LLMD_G3F8V(M, Q, 0); else if (g3v == 1) LLMD_G3F8V(M, Q, 1);                                  \
     else if (g3v == 2) LLMD_G3F8V(M, Q, 2); else LLMD_G3F8V(M, Q, 3);                                           \
   } while (0)
@@ -1322,6 +1333,7 @@ int llmd_moe_gemm3_bf16(const void* X, int64_t x_stride, int topk, const int* so
   }();
 #define LLMD_G3BF(M)                                                                                              \
   do {                                                                                                            \
+    if (bfv == 2 && g3_nt()) LLMD_G3BFV(M, 6); else                                                             \
     if (bfv == 0) LLMD_G3BFV(M, 0); else if (bfv == 1) LLMD_G3BFV(M, 1);                                        \
     else if (bfv == 2) LLMD_G3BFV(M, 2); else LLMD_G3BFV(M, 3);                                                 \
   } while (0)
