@@ -99,6 +99,7 @@ int llmd_symm_max_ranks();
 int llmd_symm_channels();
 int llmd_symm_error(const void*, uint32_t*);
 int llmd_symm_clear_error(void*);
+int llmd_symm_host_err(int64_t*);
 int llmd_symm_all_reduce(const int64_t*, int, int, int, int, int64_t, int64_t, const void*, void*, int64_t,
                          hipStream_t);
 int llmd_symm_ep_dispatch(const int64_t*, int, int, int, const int64_t*, const void*, int64_t, const int*,
@@ -878,6 +879,13 @@ int64_t symm_error(torch::Tensor heap, bool clear) {
   return (int64_t)e;
 }
 
+// address of the process's host-mapped symm failure word (allocated on first use)
+int64_t symm_host_err() {
+  int64_t p = 0;
+  TORCH_CHECK(llmd_symm_host_err(&p) == 0, "symm_host_err: hipHostMalloc failed");
+  return p;
+}
+
 void check_bases(const std::vector<int64_t>& bases, int64_t rank) {
   TORCH_CHECK((int)bases.size() >= 1 && (int)bases.size() <= llmd_symm_max_ranks(), "symm: 1..8 ranks");
   TORCH_CHECK(rank >= 0 && rank < (int64_t)bases.size(), "symm: rank");
@@ -987,6 +995,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {  // _C, or _C_debug (llmd_amd/build.p
   m.def("moe_tile_m_prefill", &llmd_moe_gemm3_tile_m);
   m.def("symm_alloc", &symm_alloc);
   m.def("symm_error", &symm_error);
+  m.def("symm_host_err", &symm_host_err);
   m.def("symm_sig_bytes", &llmd_symm_sig_bytes);
   m.def("symm_grid", &llmd_symm_grid);
   m.def("symm_channels", &llmd_symm_channels);

@@ -572,6 +572,211 @@ __global__ __launch_bounds__(NT4, 1) void pgemm4_kernel(const uint16_t* __restri
   }
 }
 
+// ---------------------------------------------------------------------------
+// Variant 2 ("RS4"): the 4-wave / 128 x 128-per-wave form of variant 1, but the
+// operands are REGISTER-staged (global_load_dwordx4 -> VGPR -> ds_write_b128)
+// instead of LDS-DMA. Why: with one wave per SIMD there is no partner wave to
+// hide an instruction's issue cost behind, and an LDS-DMA piece costs ~60-180
+// cycles of issue among MFMAs (MI355X_MICROARCH.md, LDS-DMA piece row) - 8 per
+// 64 MFMA (1024 cycles) in variant 1 - while a global_load / ds_write issues in
+// a few cycles. One wave per SIMD has 512 registers (256 AGPR accumulators +
+// 256 VGPR), so the staging ring that would not fit at two waves per SIMD fits.
+//
+// Per 64-deep K-step kt (LDS buffer cur = kt & 1, 2 x 64 KB):
+//   substep 0: 64 MFMA on fragment set 0 (k 0..31); between MFMA rows: the 16
+//              fragment reads of set 1 (k 32..63) from buf cur and the 16
+//              ds_write_b128 of step kt+1's staged tile into buf cur ^ 1;
+//   lgkmcnt(0) + s_barrier (the ONE barrier per K-step);
+//   substep 1: 64 MFMA on set 1; between rows: the 16 fragment reads of step
+//              kt+1's set 0 from buf cur ^ 1 and the 16 global loads of step
+//              kt+2 into the staging registers.
+// Buffer cur ^ 1 was last read in step kt-1's substep 0, before step kt-1's
+// barrier, so substep 0 of kt may overwrite it; it is read again only after
+// step kt's barrier. W fragments are read before A fragments in each set (every
+// MFMA row needs all 8 W fragments). LDS image: [256 rows][64 k] bf16 per
+// operand, 16-B chunk c of row r at chunk c ^ ((r >> 1) & 7): conflict-free for
+// the ds_read_b128 lane groups of the 16 x 16 x 32 operand reads and for the
+// 8-lane ds_write_b128 groups (one 128-B row each).
+constexpr int NT5 = 256;
+constexpr int OPB5 = BM * BK * 2;  // one operand of one K-step: 32 KB
+constexpr int BUF5 = 2 * OPB5;     // A + W
+
+__device__ __forceinline__ int swz5(int row, int c) { return c ^ ((row >> 1) & 7); }
+
+template <int EPI>
+__global__ __launch_bounds__(NT5, 1) void pgemm5_kernel(const uint16_t* __restrict__ A, int64_t lda,
+                                                        const uint16_t* __restrict__ W, int64_t ldw,
+                                                        uint16_t* __restrict__ C, int64_t ldc, int M, int N, int K,
+                                                        int tile0, int nsplit, float* __restrict__ ws) {
+  __shared__ __attribute__((aligned(1024))) char lds[2 * BUF5];  // the ONLY LDS object
+  const int tiles_m = (M + BM - 1) / BM, tiles_n = N / BN;
+  const int b = xcd_remap(blockIdx.x, gridDim.x);
+  const int tail = gridDim.x / nsplit;
+  const int t_local = b % tail, split = b / tail;
+  const int nk_all = K / BK;
+  const int chunk = (nk_all + nsplit - 1) / nsplit;
+  const int kbeg = split * chunk;
+  const int nk = min(chunk, nk_all - kbeg);
+  int tm, tn;
+  tile_mn(tile0 + t_local, tiles_m, tiles_n, tm, tn);
+  const int m0 = tm * BM, n0 = tn * BN;
+  A += (int64_t)kbeg * BK;
+  W += (int64_t)kbeg * BK;
+
+  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+  const int wr = w >> 1, wc = w & 1;
+
+  // staging: load i (0..7) of an operand = row 32 i + (tid >> 3), chunk tid & 7
+  const int srow = tid >> 3, sc = tid & 7;
+  uint32_t aoff[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) aoff[i] = (uint32_t)(min(m0 + 32 * i + srow, M - 1) * lda + sc * 8);
+  const uint32_t woff0 = (uint32_t)((n0 + srow) * ldw + sc * 8);
+  const uint32_t wstep = (uint32_t)(32 * ldw);
+  // LDS byte offset of this thread's chunk in row 32 i + srow ((32 i + srow) >> 1 & 7 == (srow >> 1) & 7)
+  const int st_off = srow * 128 + swz5(srow, sc) * 16;
+
+  // fragment reads: row 16 t + (lane & 15), chunk 4 s + (lane >> 4)
+  const int fr = lane & 15, fq = lane >> 4;
+  const int rd0 = fr * 128 + swz5(fr, fq) * 16, rd1 = fr * 128 + swz5(fr, 4 + fq) * 16;
+  const int a_rd = (wr * 128) * 128, w_rd = OPB5 + (wc * 128) * 128;
+
+  f32x4_t acc[8][8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  s16x8_t fa0[8], fw0[8], fa1[8], fw1[8];
+  u32x4_t ga[8], gw[8];
+
+  auto gload = [&](int kt, int i) {  // loads i of A and of W, K-step kt
+    const int k0 = min(kt, nk - 1) * BK;
+    ga[i] = *reinterpret_cast<const u32x4_t*>(A + aoff[i] + k0);
+    gw[i] = *reinterpret_cast<const u32x4_t*>(W + woff0 + i * wstep + k0);
+  };
+  auto swrite = [&](char* buf, int i) {
+    *reinterpret_cast<u32x4_t*>(buf + i * 4096 + st_off) = ga[i];
+    *reinterpret_cast<u32x4_t*>(buf + OPB5 + i * 4096 + st_off) = gw[i];
+  };
+
+  // prologue: step 0 -> buf 0, step 1 -> staging, set 0 of step 0 -> registers
+#pragma unroll
+  for (int i = 0; i < 8; ++i) gload(0, i);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) swrite(lds, i);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) gload(1, i);
+  __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this wave's ds_writes done
+  bar();
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    fw0[i] = *reinterpret_cast<const s16x8_t*>(lds + w_rd + i * 2048 + rd0);
+    fa0[i] = *reinterpret_cast<const s16x8_t*>(lds + a_rd + i * 2048 + rd0);
+  }
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_nop 4" ::: "memory");  // v_accvgpr_write (zero init) -> MFMA srcC
+  __builtin_amdgcn_sched_barrier(0);
+
+  // one MFMA row i (8 MFMA on acc[i][*]) with two "side" instructions after it
+#define PG5_ROW(fa, fw, i, SIDE)                                                       \
+  {                                                                                    \
+    _Pragma("unroll") for (int j = 0; j < 8; ++j) mfma16_acc(acc[i][j], fw[j], fa[i]); \
+    SIDE;                                                                              \
+    __builtin_amdgcn_sched_barrier(0);                                                 \
+  }
+  for (int kt = 0; kt < nk; ++kt) {
+    char* cur = lds + (kt & 1) * BUF5;
+    char* nxt = lds + ((kt & 1) ^ 1) * BUF5;
+    // substep 0: set 0; read set 1 (W first) from cur, write step kt+1 into nxt
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      PG5_ROW(fa0, fw0, i, {
+        if (i < 4) {
+          fw1[2 * i] = *reinterpret_cast<const s16x8_t*>(cur + w_rd + (2 * i) * 2048 + rd1);
+          fw1[2 * i + 1] = *reinterpret_cast<const s16x8_t*>(cur + w_rd + (2 * i + 1) * 2048 + rd1);
+        } else {
+          fa1[2 * i - 8] = *reinterpret_cast<const s16x8_t*>(cur + a_rd + (2 * i - 8) * 2048 + rd1);
+          fa1[2 * i - 7] = *reinterpret_cast<const s16x8_t*>(cur + a_rd + (2 * i - 7) * 2048 + rd1);
+        }
+        swrite(nxt, i);
+      });
+    }
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): set-1 reads and the nxt writes retired
+    bar();
+    // substep 1: set 1; read step kt+1's set 0 (W first) from nxt, load step kt+2
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      PG5_ROW(fa1, fw1, i, {
+        if (i < 4) {
+          fw0[2 * i] = *reinterpret_cast<const s16x8_t*>(nxt + w_rd + (2 * i) * 2048 + rd0);
+          fw0[2 * i + 1] = *reinterpret_cast<const s16x8_t*>(nxt + w_rd + (2 * i + 1) * 2048 + rd0);
+        } else {
+          fa0[2 * i - 8] = *reinterpret_cast<const s16x8_t*>(nxt + a_rd + (2 * i - 8) * 2048 + rd0);
+          fa0[2 * i - 7] = *reinterpret_cast<const s16x8_t*>(nxt + a_rd + (2 * i - 7) * 2048 + rd0);
+        }
+        gload(kt + 2, i);
+      });
+    }
+  }
+#undef PG5_ROW
+  mfma_drain();
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  if constexpr (EPI == EPI_F32) {
+    float* wt = ws + ((int64_t)split * tail + t_local) * (BM * BN);
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int row = wr * 128 + 16 * i + fr, col = wc * 128 + 16 * j + 4 * fq;
+        *reinterpret_cast<f32x4_t*>(wt + row * BN + col) = acc[i][j];
+      }
+    return;
+  }
+  __syncthreads();
+  // epilogue (as variant 1): acc[i][j][r] = C[m][n], m = wr*128 + 16 i + (lane & 15),
+  // n = wc*128 + 16 j + 4 (lane >> 4) + r; per-wave [128][128] bf16 image, chunks XOR row & 15
+  char* img = lds + w * 32768;
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int row = 16 * i + fr, col = 16 * j + 4 * fq;
+      const f32x4_t v = acc[i][j];
+      u32x2_t p;
+      p[0] = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
+      p[1] = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
+      *reinterpret_cast<u32x2_t*>(img + row * 256 + (((col >> 3) ^ (row & 15)) * 16) + (col & 7) * 2) = p;
+    }
+  __syncthreads();
+  if constexpr (EPI == EPI_NONE) {
+#pragma unroll 4
+    for (int it = 0; it < 32; ++it) {
+      const int row = it * 4 + (lane >> 4), c = lane & 15;
+      const int m = m0 + wr * 128 + row;
+      const u32x4_t v = *reinterpret_cast<const u32x4_t*>(img + row * 256 + ((c ^ (row & 15)) * 16));
+      if (m < M) *reinterpret_cast<u32x4_t*>(C + (int64_t)m * ldc + n0 + wc * 128 + c * 8) = v;
+    }
+  } else {
+    // gate = tile columns [0, 128) (waves wc = 0), up = [128, 256) (wc = 1): both waves of a row
+    // half store 64 rows each of silu(g) * u
+    const char* gimg = lds + (wr * 2) * 32768;
+    const char* uimg = gimg + 32768;
+#pragma unroll 4
+    for (int it = 0; it < 16; ++it) {
+      const int row = wc * 64 + it * 4 + (lane >> 4), c = lane & 15;
+      const int m = m0 + wr * 128 + row;
+      const int off = row * 256 + ((c ^ (row & 15)) * 16);
+      float gf[8], uf[8], of[8];
+      unpack8(*reinterpret_cast<const u32x4_t*>(gimg + off), gf);
+      unpack8(*reinterpret_cast<const u32x4_t*>(uimg + off), uf);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) of[e] = gf[e] / (1.f + __expf(-gf[e])) * uf[e];
+      if (m < M) *reinterpret_cast<u32x4_t*>(C + (int64_t)m * ldc + n0 / 2 + c * 8) = pack8(of);
+    }
+  }
+}
+
 // ws [nsplit][tail][256][256] fp32 partials -> C tiles tile0 .. tile0 + tail - 1 (bf16, rows < M)
 __global__ __launch_bounds__(256) void pgemm_splitk_reduce(const float* __restrict__ ws, int nsplit, int tail,
                                                            int tile0, uint16_t* __restrict__ C, int64_t ldc, int M,
@@ -632,6 +837,26 @@ extern "C" int llmd_pgemm(const void* A, int64_t lda, const void* W, int64_t ldw
   // 32-bit DMA offsets
   if ((int64_t)(M - 1) * lda + K > 0x7fffffffLL || (int64_t)(N - 1) * ldw + K > 0x7fffffffLL) return -2;
   const int ntiles = ((M + BM - 1) / BM) * (N / BN);
+  if (variant == 2) {
+    int full = ntiles, tail = 0, nsplit = 1;
+    if (ws != nullptr) pgemm_plan(M, N, K, epi, full, tail, nsplit);
+    const auto* a = (const uint16_t*)A;
+    const auto* w = (const uint16_t*)W;
+    auto* c = (uint16_t*)C;
+    if (epi == EPI_SILU)
+      hipLaunchKernelGGL(pgemm5_kernel<EPI_SILU>, dim3(full), dim3(NT5), 0, st, a, lda, w, ldw, c, ldc, M, N, K, 0, 1,
+                         nullptr);
+    else if (full > 0)
+      hipLaunchKernelGGL(pgemm5_kernel<EPI_NONE>, dim3(full), dim3(NT5), 0, st, a, lda, w, ldw, c, ldc, M, N, K, 0, 1,
+                         nullptr);
+    if (nsplit > 1) {
+      hipLaunchKernelGGL(pgemm5_kernel<EPI_F32>, dim3(tail * nsplit), dim3(NT5), 0, st, a, lda, w, ldw, c, ldc, M, N,
+                         K, full, nsplit, (float*)ws);
+      hipLaunchKernelGGL(pgemm_splitk_reduce, dim3(tail * (BM / 8)), dim3(256), 0, st, (const float*)ws, nsplit,
+                         tail, full, c, ldc, M, N);
+    }
+    return (int)hipGetLastError();
+  }
   if (variant == 1) {
     int full = ntiles, tail = 0, nsplit = 1;
     if (ws != nullptr) pgemm_plan(M, N, K, epi, full, tail, nsplit);

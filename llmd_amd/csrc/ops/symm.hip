@@ -25,8 +25,16 @@
 // peers' receive areas with 16-B stores, all 7 xGMI links in flight at once;
 // the reduction then reads local HBM only.
 //
-// Every wait is bounded (~2 s); on timeout the err word is set and the kernel
-// finishes (with garbage) instead of hanging the GPU. symm_error() reports it.
+// Every wait is bounded (LLMD_SYMM_TIMEOUT_S, default 20 s, on the 100 MHz
+// s_memrealtime clock); on timeout the err word is set and the kernel
+// finishes (with garbage) instead of hanging the GPU. symm_error() reports it,
+// and the same timeout also sets a HOST-mapped word (fine-grained pinned host
+// memory, llmd_symm_host_err) that the engine reads after every step with a
+// plain load - no device sync - and turns into a fatal error before any token
+// computed from a broken collective is emitted (parallel/symm.py check_health).
+#include <cstdlib>
+#include <cstring>
+
 #include "llmd_common.h"
 
 using namespace llmd;
@@ -42,6 +50,8 @@ constexpr int64_t SIG_BYTES = 1 << 20;
 
 struct Peers {
   char* base[MAXR];
+  uint32_t* herr;        // host-mapped failure word (device address), or null
+  uint64_t wait_ticks;   // barrier timeout in s_memrealtime ticks (100 MHz)
 };
 
 __device__ __forceinline__ uint32_t* flag_ptr(char* base, int ch, int ph, int b, int src) {
@@ -89,11 +99,13 @@ __device__ __forceinline__ void block_barrier(const Peers& P, int nranks, int ra
   }
   if (t < nranks && t != rank) {
     uint32_t* f = flag_ptr(P.base[rank], ch, ph, blockIdx.x, t);
-    for (int64_t it = 0;; ++it) {
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    for (;;) {
       uint32_t v = __hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
       if ((int32_t)(v - epoch) >= 0) break;
-      if (it > (1 << 24)) {
+      if (__builtin_amdgcn_s_memrealtime() - t0 > P.wait_ticks) {
         __hip_atomic_store(err_ptr(P.base[rank]), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        if (P.herr != nullptr) __hip_atomic_store(P.herr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         break;
       }
       __builtin_amdgcn_s_sleep(2);
@@ -387,9 +399,48 @@ int llmd_symm_clear_error(void* self) {
   return (int)hipMemset((char*)self + (NCH * NPH * G * MAXR + NCH * G) * 4, 0, 4);
 }
 
+// One fine-grained (coherent) mapped host word per process: every symm launch
+// carries its device address, so it must exist before any graph is captured
+// (SymmHeap creates it).
+static uint32_t* g_herr_host = nullptr;
+static uint32_t* g_herr_dev = nullptr;
+
+int llmd_symm_host_err(int64_t* host_ptr) {
+  if (g_herr_host == nullptr) {
+    void* h = nullptr;
+    hipError_t e = hipHostMalloc(&h, 64, hipHostMallocMapped | hipHostMallocCoherent);
+    if (e != hipSuccess) return (int)e;
+    std::memset(h, 0, 64);
+    void* d = nullptr;
+    e = hipHostGetDevicePointer(&d, h, 0);
+    if (e != hipSuccess) return (int)e;
+    g_herr_host = (uint32_t*)h;
+    g_herr_dev = (uint32_t*)d;
+  }
+  *host_ptr = (int64_t)(uintptr_t)g_herr_host;
+  return 0;
+}
+
+// Barrier timeout: LLMD_SYMM_TIMEOUT_S (default 20 s, the order of the reference's
+// NCCL heartbeat timeout of 15 s) - long enough for any lock-step skew between
+// ranks (a long prefill chunk on one DP rank), short enough to fail a wedged
+// replica quickly.
+static uint64_t wait_ticks() {
+  static uint64_t t = 0;
+  if (t == 0) {
+    const char* e = std::getenv("LLMD_SYMM_TIMEOUT_S");
+    double sec = e != nullptr ? std::atof(e) : 20.0;
+    if (!(sec > 0.0)) sec = 20.0;
+    t = (uint64_t)(sec * 1e8);  // s_memrealtime runs at 100 MHz
+  }
+  return t;
+}
+
 static Peers make_peers(const int64_t* bases, int n) {
   Peers P = {};
   for (int i = 0; i < n; ++i) P.base[i] = (char*)bases[i];
+  P.herr = g_herr_dev;
+  P.wait_ticks = wait_ticks();
   return P;
 }
 

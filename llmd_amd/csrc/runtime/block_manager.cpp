@@ -269,14 +269,16 @@ class BlockManager {
 
   // Blocks for an externally produced KV (P/D): allocate `n` fresh blocks for a
   // new sequence without any prefix reuse (the sender fills them). window > 0
-  // (windowed group of a hybrid cache): only the blocks the next query can reach
-  // (keys >= num_tokens - window + 1) are allocated, earlier entries are the null
-  // block (requires reserved >= 1).
+  // (windowed group of a hybrid cache): only the blocks the decoder's first query
+  // can reach are allocated. That query RECOMPUTES the last prompt token (position
+  // num_tokens - 1, scheduler.py: num_computed = prompt_len - 1), so it attends keys
+  // >= num_tokens - window, one more than a query at num_tokens would; earlier
+  // entries are the null block (requires reserved >= 1).
   std::vector<int32_t> allocate_remote(int64_t seq_id, int num_tokens, uint64_t extra, int window) {
     if (seqs_.count(seq_id)) throw std::runtime_error("allocate_remote: sequence exists");
     if (window > 0 && reserved_ < 1) throw std::runtime_error("allocate_remote(window) needs a reserved null block");
     const int nb = (num_tokens + bs_ - 1) / bs_;
-    const int lo = window > 0 ? std::min(nb, std::max(0, num_tokens - window + 1) / bs_) : 0;
+    const int lo = window > 0 ? std::min(nb, std::max(0, num_tokens - window) / bs_) : 0;
     if (nb - lo > num_free()) return {};
     Seq s;
     s.extra = extra;

@@ -142,13 +142,21 @@ class FsStore {
     return d + "/" + name + ".kv";
   }
 
+  // Per name at most one job is QUEUED (not yet picked by a worker) and at most
+  // one RUNNING. A new write replaces only the queued one, whose ticket is then
+  // reported as done (superseded: no worker ever read its buffer); a running job
+  // keeps its buffer until its own worker reports its ticket. Writes of one name
+  // are serialized (the finishing worker re-queues the name), so renames land in
+  // enqueue order and an older block can never overwrite a newer one.
   void enqueue_write(const std::string& name, Job job) {
     {
       std::lock_guard<std::mutex> g(mu_);
-      auto it = pending_.find(name);
-      if (it != pending_.end() && it->second.ticket >= 0) wdone_.push_back(it->second.ticket);  // superseded
-      pending_[name] = job;
-      q_.push_back(name);
+      Entry& e = pending_[name];
+      const bool queued = e.has_queued;
+      if (queued && e.queued.ticket >= 0) wdone_.push_back(e.queued.ticket);  // superseded, never read
+      e.queued = job;
+      e.has_queued = true;
+      if (!queued && !e.running) q_.push_back(name);
     }
     cv_.notify_one();
   }
@@ -158,9 +166,10 @@ class FsStore {
     {
       std::lock_guard<std::mutex> g(mu_);
       auto it = pending_.find(name);
-      if (it != pending_.end()) {  // still queued for writing: copy from the writer's source
-        if (it->second.size != n) return false;
-        std::memcpy(dst, it->second.data, n);
+      if (it != pending_.end()) {  // queued or being written: copy from the newest source buffer
+        const Job& j = it->second.has_queued ? it->second.queued : it->second.running_job;
+        if (j.size != n) return false;
+        std::memcpy(dst, j.data, n);
         return true;
       }
     }
@@ -212,8 +221,12 @@ class FsStore {
         name = q_.front();
         q_.pop_front();
         auto it = pending_.find(name);
-        if (it == pending_.end()) continue;  // a later enqueue of the same name already wrote it
-        job = it->second;
+        if (it == pending_.end() || !it->second.has_queued || it->second.running) continue;
+        Entry& e = it->second;
+        job = e.queued;
+        e.running_job = e.queued;
+        e.has_queued = false;
+        e.running = true;
         ++in_flight_;
       }
       const int64_t t0 = now_ns();
@@ -241,7 +254,13 @@ class FsStore {
       {
         std::lock_guard<std::mutex> g(mu_);
         auto it = pending_.find(name);
-        if (it != pending_.end() && it->second.data == job.data && it->second.ticket == job.ticket) pending_.erase(it);
+        bool requeue = false;
+        if (it != pending_.end()) {
+          it->second.running = false;
+          if (it->second.has_queued) requeue = true;  // a newer block arrived while this one was written
+          else pending_.erase(it);
+        }
+        if (requeue) q_.push_back(name);
         if (job.ticket >= 0) wdone_.push_back(job.ticket);
         --in_flight_;
         if (ok) {
@@ -251,6 +270,7 @@ class FsStore {
         }
       }
       done_cv_.notify_all();
+      cv_.notify_one();
     }
   }
 
@@ -259,7 +279,12 @@ class FsStore {
   std::condition_variable cv_, rcv_, done_cv_;
   std::deque<std::string> q_;
   std::deque<RJob> rq_;
-  std::unordered_map<std::string, Job> pending_;
+  struct Entry {
+    Job queued{nullptr, 0, -1, nullptr};
+    Job running_job{nullptr, 0, -1, nullptr};
+    bool has_queued = false, running = false;
+  };
+  std::unordered_map<std::string, Entry> pending_;
   std::vector<int64_t> wdone_;
   std::vector<std::pair<int64_t, bool>> rdone_;
   std::vector<std::thread> workers_;

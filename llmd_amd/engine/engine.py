@@ -14,6 +14,7 @@ from typing import Iterable, Optional
 import torch
 
 from llmd_amd import _rt_loader
+from llmd_amd.parallel import symm as _symm
 from llmd_amd.utils import markers
 
 from .config import EngineConfig
@@ -236,6 +237,9 @@ class LLMEngine:
         return bool(v.item())
 
     def _finish_step(self, so, sampled, err_outs, t0) -> list[RequestOutput]:
+        # a timed-out symm collective (stalled peer) makes this step's tokens garbage:
+        # fail loudly before any of them reaches a client (one host load, no sync)
+        _symm.check_health("emitting step %d" % self.step_count)
         touched = self.sched.update(so, sampled)
         dt = time.monotonic() - t0
         self.step_count += 1

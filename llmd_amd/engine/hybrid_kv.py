@@ -28,8 +28,10 @@ chunks (``swa_blocks``); the full pool gets the rest of the KV budget, so
 capacity in tokens grows by ~ L / L_full (1.9x for gpt-oss at
 --gpu-memory-utilization fixed).
 
-The scheduler sees the BlockManager interface (the full group's block counts
-drive admission and preemption); ``grow`` fails if either group cannot grow.
+The scheduler sees the BlockManager interface: ``grow`` is all-or-nothing over
+both groups (it fails, changing neither, if either cannot grow, so preemption
+follows whichever pool is exhausted) and ``can_allocate`` checks both; block
+counts reported to metrics / the router are the full group's.
 """
 from __future__ import annotations
 
@@ -66,10 +68,22 @@ class HybridBlockManager:
         return hit
 
     def can_allocate(self, n: int) -> bool:
-        return self.full.can_allocate(n)
+        # a new sequence's first blocks come from BOTH pools (the windowed table
+        # grows with the sequence and nulls its head only after each step)
+        return self.full.can_allocate(n) and self.swa.can_allocate(n)
 
     def grow(self, seq_id, total_tokens: int) -> bool:
-        return self.full.grow(seq_id, total_tokens) and self.swa.grow(seq_id, total_tokens)
+        """All or nothing over both pools: when either cannot grow, neither does,
+        so the scheduler preempts on whichever pool is exhausted (a failed
+        windowed grow must not leave the full pool's new blocks behind)."""
+        nb = -(-total_tokens // self.block_size)
+        need_full = nb - self.full.num_seq_blocks(seq_id)
+        need_swa = nb - self.swa.num_seq_blocks(seq_id)
+        if need_full > self.full.num_free() or need_swa > self.swa.num_free():
+            return False
+        ok = self.full.grow(seq_id, total_tokens) and self.swa.grow(seq_id, total_tokens)
+        assert ok, "hybrid grow: pool changed between the check and the grow"
+        return True
 
     def commit(self, seq_id, toks, num_computed: int):
         self.full.commit(seq_id, toks, num_computed)

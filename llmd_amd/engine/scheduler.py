@@ -428,8 +428,13 @@ class Scheduler:
                     and self.bm.has_seq(r.seq_id)):
                 self.bm.commit(r.seq_id, self._tokens(r), r.num_computed_tokens)
             if self._window_release and self.bm.has_seq(r.seq_id):
-                # hybrid KV cache: windowed blocks no future query can reach go back to the pool
-                self.bm.after_compute(r.seq_id, r.num_computed_tokens)
+                # hybrid KV cache: windowed blocks no future query can reach go back to the pool.
+                # A P/D prefill keeps one key more: the decoder recomputes the last prompt
+                # token, whose query reaches back to position n - window (allocate_remote).
+                n_keep = r.num_computed_tokens
+                if (r.kv_transfer_params or {}).get("do_remote_decode"):
+                    n_keep -= 1
+                self.bm.after_compute(r.seq_id, n_keep)
             if r.seq_id in sampled:
                 tok, lp = sampled[r.seq_id]
                 r.output_token_ids.append(tok)

@@ -18,6 +18,7 @@ import logging
 
 import torch
 
+from llmd_amd.parallel import symm as _symm
 from llmd_amd.parallel.comm import tp_broadcast_plan, tp_recv_plan
 
 from .config import EngineConfig
@@ -70,6 +71,7 @@ def run_follower(cfg: EngineConfig, capture_graphs: bool = True, on_ready=None) 
                 kvx.apply(pl)
                 continue
             runner.run_plan(pl)
+            _symm.check_health("follower plan %d" % n)  # a stalled peer: exit non-zero, never continue
             n += 1
     if kvx is not None:
         kvx.close()

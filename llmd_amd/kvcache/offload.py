@@ -107,6 +107,21 @@ class _LoadJob:
     t0: float = 0.0
     ev0: object = None
     aborted: bool = False
+    released: bool = False          # host-slot references given back (poll_loads / cancel)
+
+
+def _slot_runs(slots: list):
+    """(first index, first slot, length) of each run of consecutive host slots, so a
+    multi-block transfer is one copy per run instead of one per block."""
+    out = []
+    i = 0
+    while i < len(slots):
+        r = 1
+        while i + r < len(slots) and slots[i + r] == slots[i] + r:
+            r += 1
+        out.append((i, slots[i], r))
+        i += r
+    return out
 
 
 class OffloadManager:
@@ -229,6 +244,9 @@ class OffloadManager:
         tier (removal events for the router's index) and move FS keys to the new
         weights' namespace, so files of the old weights are never read again."""
         self._drain()
+        # reloads still in flight carry KV of the old weights: they report 0 tokens (the
+        # scheduler recomputes) and give their slot references back before the reset
+        self._cancel_inflight_loads()
         for key in list(self.slot_of):
             self.events_out.append((1, key, 0, -1, [], "cpu"))
         self.slot_of.clear()
@@ -244,12 +262,26 @@ class OffloadManager:
         lost) before the pool can be freed; in-flight reloads write into the old
         pool and are finished the same way."""
         self._drain()
-        for job in list(self.loads.values()):
-            if job.event is not None:
-                job.event.synchronize()
+        # a reload in flight scattered into the OLD pool (or was never copied when the
+        # pool is gone): none of its tokens are resident in the pool used from now on
+        self._cancel_inflight_loads()
         self.kv = kv
         if kv is not None:
             self._layout(kv)
+
+    def _cancel_inflight_loads(self):
+        """Wait for every reload's FS reads and copies, then make it report 0 tokens
+        and release the host slots it holds (poll_loads still returns the request,
+        so the scheduler recomputes its prefix instead of trusting the blocks)."""
+        if self.fs is not None:
+            while any(job.fs_tickets for job in self.loads.values()):
+                self.fs.flush()
+                self._poll_fs()
+        for job in self.loads.values():
+            if job.event is not None:
+                job.event.synchronize()
+            job.n_ok = 0
+            self._release_job_slots(job, loaded=False)
 
     # ------------------------------------------------------------ write-through
     def on_block_events(self, events: list):
@@ -278,8 +310,8 @@ class OffloadManager:
                 stage, pairs = self._pack(blocks)
                 packed = torch.cuda.Event()
                 packed.record(self.stream)
-                for i, (h, b, slot) in enumerate(assign):
-                    self.host[slot].copy_(stage[i], non_blocking=True)
+                for i, s0, r in _slot_runs([slot for _, _, slot in assign]):
+                    self.host[s0:s0 + r].copy_(stage[i:i + r], non_blocking=True)
                 ev = torch.cuda.Event(enable_timing=True)
                 ev.record(self.stream)
             # a committed block can be released and re-filled by the very next step (the
@@ -441,31 +473,49 @@ class OffloadManager:
     def launch(self, req, first: int, dst: list, found: list):
         """Start the reload of ``found`` (locate() results) into pool blocks ``dst``."""
         job = _LoadJob(req, first, dst, [], t0=time.perf_counter())
+        # host-tier blocks of the chain are pinned BEFORE any FS block takes a slot, so
+        # the slot allocation below cannot evict a block this same reload reads
         for tier, k, s in found:
             if tier == "cpu":
                 self.slot_of.move_to_end(k)
                 self.slot_busy[s] += 1
+        for tier, k, s in found:
+            if tier == "cpu":
                 job.items.append(("cpu", k, s, None))
-            else:
-                buf = torch.empty(self.block_bytes, dtype=torch.uint8, pin_memory=self.kv.is_cuda)
-                t = next(self._ticket)
-                job.fs_tickets.add(t)
-                self._fs_read_job[t] = job
-                job.items.append(("fs", k, buf, t))
-                self.fs.read_async(self._fs_key(k), buf.data_ptr(), self.block_bytes, t)
+                continue
+            # an FS block is read into a host-tier slot (the pinned slab allocated once at
+            # start-up; no per-block pinned allocation on the engine thread) and joins the
+            # host tier once the read succeeded; with every slot busy it is not reloaded
+            slot = self._alloc_slot()
+            if slot is None:
+                break
+            self.slot_busy[slot] += 1
+            t = next(self._ticket)
+            job.fs_tickets.add(t)
+            self._fs_read_job[t] = job
+            job.items.append(("fs", k, slot, t))
+            self.fs.read_async(self._fs_key(k), self.host[slot].data_ptr(), self.block_bytes, t)
+        if len(job.items) < len(found):  # the chain is truncated at the first block without a slot
+            for tier, k, s in found[len(job.items):]:
+                if tier == "cpu":
+                    self.slot_busy[s] -= 1
+            job.n_ok = len(job.items)
         self.loads[req.request_id] = job
         if not job.fs_tickets:
             self._launch_copy(job)
 
     def _launch_copy(self, job: _LoadJob):
         n = len(job.items) if job.n_ok < 0 else job.n_ok
+        if self.kv is None:  # the pool is released (sleep): nothing can be scattered
+            n = 0
         job.n_ok = n
-        if n == 0 or self.kv is None:
+        if n == 0:
             job.event = None
             return
         nbytes = n * self.block_bytes
+        slots = [it[2] for it in job.items[:n]]
         if self.stream is None:  # CPU engine: synchronous
-            stage = torch.stack([self.host[it[2]] if it[0] == "cpu" else it[2] for it in job.items[:n]])
+            stage = self.host[torch.tensor(slots, dtype=torch.long)]
             self._unpack(stage, job.dst[:n])
             job.event = None
             self.xfer.add("CPU_to_GPU", nbytes, time.perf_counter() - job.t0)
@@ -474,8 +524,8 @@ class OffloadManager:
             job.ev0 = torch.cuda.Event(enable_timing=True)
             job.ev0.record(self.stream)
             stage = torch.empty(n, self.block_bytes, dtype=torch.uint8, device=self.kv.device)
-            for j, it in enumerate(job.items[:n]):
-                stage[j].copy_(self.host[it[2]] if it[0] == "cpu" else it[2], non_blocking=True)
+            for j, s0, r in _slot_runs(slots):  # one H2D copy per run of consecutive host slots
+                stage[j:j + r].copy_(self.host[s0:s0 + r], non_blocking=True)
             # the destination blocks may have been freed by a request whose last step is still
             # on the compute stream: scatter only behind it
             self.stream.wait_stream(torch.cuda.current_stream())
@@ -499,15 +549,31 @@ class OffloadManager:
                 continue
             del self.loads[rid]
             n = max(0, job.n_ok)
-            for tier, k, s, _t in job.items:
-                if tier == "cpu":
-                    self.slot_busy[s] -= 1
+            self._release_job_slots(job, loaded=True)
             for tier, *_ in job.items[:n]:
                 self.stats["loaded_cpu" if tier == "cpu" else "loaded_fs"] += 1
             if job.event is not None:
                 self.xfer.add("CPU_to_GPU", n * self.block_bytes, job.ev0.elapsed_time(job.event) * 1e-3)
             out.append((job.req, n * self.block_size_of(job)))
         return out
+
+    def _release_job_slots(self, job: _LoadJob, loaded: bool):
+        """Drop a reload's host-slot references (once). FS blocks that were read
+        successfully (``loaded``, within n_ok) stay in their slot as host-tier
+        entries; the other FS slots go back to the free list."""
+        if job.released:
+            return
+        job.released = True
+        n = max(0, job.n_ok) if loaded else 0
+        for j, (tier, k, s, _t) in enumerate(job.items):
+            self.slot_busy[s] -= 1
+            if tier != "fs":
+                continue
+            if j < n and k not in self.slot_of:
+                self.slot_of[k] = s
+                self.events_out.append((0, k, 0, -1, [], "cpu"))
+            else:
+                self.free_slots.append(s)
 
     def block_size_of(self, job) -> int:
         return self.engine.bm.block_size

@@ -49,6 +49,45 @@ def _C():
     return ops.native()
 
 
+class CollectiveFailure(RuntimeError):
+    """A symm collective's bounded barrier wait timed out (a peer never arrived):
+    every all-reduce / EP result of that step is garbage. Fatal - the engine must
+    not emit a token computed from it (the role NCCL's watchdog plays for the
+    reference, TORCH_NCCL_HEARTBEAT_TIMEOUT_SEC, docker/Dockerfile.cuda:607-608)."""
+
+
+_herr_word = None  # ctypes view of the process's host-mapped failure word
+
+
+def _host_err_word():
+    global _herr_word
+    if _herr_word is None:
+        import ctypes
+
+        _herr_word = ctypes.c_uint32.from_address(_C().symm_host_err())
+    return _herr_word
+
+
+def host_error() -> int:
+    """The host-mapped failure word: non-zero once any symm kernel of this process
+    timed out in a barrier. A plain host load, no device synchronisation."""
+    return 0 if _herr_word is None else int(_herr_word.value)
+
+
+def clear_host_error():
+    if _herr_word is not None:
+        _herr_word.value = 0
+
+
+def check_health(where: str = "step"):
+    """Raise CollectiveFailure if a symm barrier timed out. Called by the engine
+    after every step (before its tokens are emitted) and by TP followers after
+    every plan; costs one host load."""
+    if _herr_word is not None and _herr_word.value:
+        raise CollectiveFailure(f"symm collective timed out (a peer rank stalled or died) before {where}: "
+                                "all-reduce / EP results are invalid, refusing to continue")
+
+
 def _align(n: int, a: int = 4096) -> int:
     return (n + a - 1) // a * a
 
@@ -68,6 +107,7 @@ class SymmHeap:
         self.nbytes = _align(nbytes)
         if self.nbytes > (4 << 30):
             raise ValueError("hipIpc imports of >4 GiB allocations hang on this stack; keep the heap <= 4 GiB")
+        _host_err_word()  # every symm launch carries the failure word's address: create it first
         self.heap = C.symm_alloc(self.nbytes, self.device.index)
         handle, off = C.kvx_ipc_export(self.heap)
         recs = [None] * world
@@ -98,7 +138,10 @@ class SymmHeap:
 
     def error(self, clear: bool = False) -> int:
         """Non-zero if a barrier wait timed out (a peer never arrived)."""
-        return int(_C().symm_error(self.heap, clear))
+        e = int(_C().symm_error(self.heap, clear))
+        if clear:
+            clear_host_error()
+        return e
 
     def close(self):
         C = _C()

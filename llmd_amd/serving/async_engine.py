@@ -11,6 +11,7 @@ from __future__ import annotations
 
 import asyncio
 import logging
+import os
 import queue
 import threading
 import time
@@ -20,6 +21,7 @@ import torch
 
 from llmd_amd.engine.engine import LLMEngine
 from llmd_amd.engine.request import RequestOutput, SamplingParams
+from llmd_amd.parallel.symm import CollectiveFailure
 
 log = logging.getLogger("llmd.async")
 
@@ -76,6 +78,13 @@ class AsyncEngine:
             self.dead = e
             for rid, (loop, q) in list(self.streams.items()):
                 loop.call_soon_threadsafe(q.put_nowait, e)
+            if isinstance(e, CollectiveFailure) and os.environ.get("LLMD_EXIT_ON_COLLECTIVE_FAILURE", "1") == "1":
+                # like NCCL's watchdog abort: the peers are wedged in the same collective, so a
+                # restart of the whole replica (the pod) is the only recovery; exit non-zero
+                # once the failing streams have been told
+                time.sleep(0.5)
+                log.critical("exiting: %s", e)
+                os._exit(70)
 
     def _apply_cmds(self):
         while True:

@@ -33,6 +33,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--ms", default="4608,5064,8192,2048,518")
     ap.add_argument("--shapes", default=",".join(SHAPES))
+    ap.add_argument("--variants", default="0,1,2", help="pgemm variants to time (each also with split-K tail)")
     a = ap.parse_args()
     dev = "cuda"
     torch.manual_seed(0)
@@ -42,7 +43,7 @@ def main():
         x = torch.rand(M, K, device=dev).mul_(2).sub_(1).to(torch.bfloat16)
         w = torch.rand(N, K, device=dev).mul_(2).sub_(1).mul_(0.05).to(torch.bfloat16)
         ref = x.float() @ w.float().t()
-        for v in (0, 1):
+        for v in (0, 1, 2):
             got = ops.pgemm(x, w, variant=v).float()
             err = (got - ref).abs().max().item() / ref.abs().max().item()
             wp = ops.pgemm_pack_gate_up(w)
@@ -62,20 +63,35 @@ def main():
             y = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
             flops = 2.0 * M * N * K
             it = max(3, int(2e13 / flops))
-            res = {"blas": [], "v0": [], "v0sk": [], "v1": [], "v1sk": []}
+            vs = [int(v) for v in a.variants.split(",")]
+            res = {"blas": []}
+            for v in vs:
+                res[f"v{v}"], res[f"v{v}sk"] = [], []
+            fused = name.endswith("gate_up")
+            if fused:
+                wp = ops.pgemm_pack_gate_up(w)
+                ya = torch.empty(M, N // 2, device=dev, dtype=torch.bfloat16)
+                res["blas+act"] = []
+                for v in vs:
+                    res[f"v{v}silu"] = []
             for _ in range(a.rounds):
                 res["blas"].append(timeit(lambda: F.linear(x, w), it))
-                res["v0"].append(timeit(lambda: ops.pgemm(x, w, out=y, variant=0, split_k=False), it))
-                res["v0sk"].append(timeit(lambda: ops.pgemm(x, w, out=y, variant=0), it))
-                res["v1"].append(timeit(lambda: ops.pgemm(x, w, out=y, variant=1, split_k=False), it))
-                res["v1sk"].append(timeit(lambda: ops.pgemm(x, w, out=y, variant=1), it))
-            d = max((ops.pgemm(x, w, variant=v).float() - F.linear(x, w).float()).abs().max().item() for v in (0, 1))
+                for v in vs:
+                    res[f"v{v}"].append(timeit(lambda: ops.pgemm(x, w, out=y, variant=v, split_k=False), it))
+                    res[f"v{v}sk"].append(timeit(lambda: ops.pgemm(x, w, out=y, variant=v), it))
+                if fused:
+                    res["blas+act"].append(timeit(lambda: ops.gated_act(F.linear(x, w), ops.ACT_SILU), it))
+                    for v in vs:
+                        res[f"v{v}silu"].append(timeit(lambda: ops.pgemm(x, wp, epi=1, out=ya, variant=v), it))
+            d = max((ops.pgemm(x, w, variant=v).float() - F.linear(x, w).float()).abs().max().item() for v in vs)
             line = f"M={M:5d} {name:10s} N={N:6d} K={K:6d}:"
             for k, v in res.items():
                 t = sorted(v)[len(v) // 2]
                 line += f"  {k} {t:.3f} ms {flops / t / 1e9:7.1f} TF/s"
             print(line + f"  max|diff| {d:.3f}", flush=True)
             del x, w, y
+            if fused:
+                del wp, ya
 
 
 if __name__ == "__main__":

@@ -137,9 +137,46 @@ def stress_fs_store(rt, seed=3):
     return len(blobs)
 
 
+def stress_fs_overwrite(rt, seed=4, keys=3, rounds=300):
+    """Zero-copy writes of the SAME names in quick succession (the offload tier
+    re-storing a block): a ticket comes back exactly once, and once it is back
+    the caller scribbles over its buffer (the host slot is reused) - that must
+    never reach the file. The last write of each name wins."""
+    import time
+
+    rng = np.random.default_rng(seed)
+    with tempfile.TemporaryDirectory() as d:
+        st = rt.FsStore(d, 4)
+        names = [f"{i:02x}{int(rng.integers(1, 2**40)):010x}" for i in range(keys)]
+        bufs, live, last = {}, set(), {}
+        for t in range(rounds):
+            name = names[t % keys]
+            b = np.full(4096 + 64 * (t % 7), t % 251, dtype=np.uint8)
+            bufs[t] = b
+            live.add(t)
+            last[name] = b.copy()
+            st.write_async(name, b.ctypes.data, b.nbytes, t)
+            for done in st.poll_writes():
+                assert done in live, done
+                live.discard(done)
+                bufs[done][:] = 255  # slot reused after the ticket came back
+            if t % 37 == 0:
+                time.sleep(0.001)
+        st.flush()
+        for done in st.poll_writes():
+            assert done in live, done
+            live.discard(done)
+        assert not live, sorted(live)[:5]
+        for name, want in last.items():
+            out = np.zeros_like(want)
+            assert st.read(name, out)
+            assert (out == want).all(), name
+    return rounds
+
+
 def run_all(rt):
     return {"bm": stress_block_manager(rt), "kv_index": stress_kv_index(rt), "gbdt_mae": stress_gbdt(rt),
-            "fs": stress_fs_store(rt)}
+            "fs": stress_fs_store(rt), "fs_overwrite": stress_fs_overwrite(rt)}
 
 
 if __name__ == "__main__":

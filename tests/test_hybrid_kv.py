@@ -142,11 +142,15 @@ def _pd_engine(kt, **kw):
 
 
 @pytest.mark.parametrize("transport", ["tcp"])
-def test_hybrid_pd_transfer_matches_aggregated(transport):
+@pytest.mark.parametrize("n_prompt", [150, 143])
+def test_hybrid_pd_transfer_matches_aggregated(transport, n_prompt):
     """P/D between two hybrid caches (kvx moves the full pool's blocks and the
     windowed pool's last-window blocks): the decoder's tokens equal an aggregated
     full-KV engine's; the windowed table is null before the window on both sides;
-    the prefiller frees both pools after the read."""
+    the prefiller frees both pools after the read. n_prompt 143 is the boundary
+    case (n - window + 1) % bs == 0: the decoder's recomputed last prompt token
+    attends key n - window, which lies in the block just below the one a query
+    at position n would first need."""
     import time
 
     kt = {"kv_connector": "KvxConnector", "kv_role": "kv_both",
@@ -154,7 +158,7 @@ def test_hybrid_pd_transfer_matches_aggregated(transport):
     P, D = _pd_engine(kt), _pd_engine(kt)
     assert P.runner.hybrid and D.runner.hybrid
     ref = _engine(False)
-    prompt = np.random.default_rng(11).integers(3, 500, size=150).tolist()
+    prompt = np.random.default_rng(11).integers(3, 500, size=n_prompt).tolist()
 
     def run(eng, rid, sp, ktp=None):
         r = eng.add_request(rid, prompt, sp, kv_transfer_params=ktp)
@@ -168,10 +172,10 @@ def test_hybrid_pd_transfer_matches_aggregated(transport):
 
     _, op = run(P, "p", SamplingParams(max_tokens=1, temperature=0.0, ignore_eos=True), {"do_remote_decode": True})
     ktp = op.kv_transfer_params
-    nb = -(-150 // 16)
+    nb = -(-n_prompt // 16)
     assert len(ktp["remote_block_ids"]) == nb
     swa = ktp["remote_swa_block_ids"]
-    lo = (150 - 16 + 1) // 16  # window 16 in tiny-gpt-oss: only the last window is held
+    lo = (n_prompt - 16) // 16  # window 16 in tiny-gpt-oss: the last window + the recomputed token's key
     assert swa[:lo] == [0] * lo and 0 not in swa[lo:]
     sp = SamplingParams(max_tokens=12, temperature=0.0, ignore_eos=True)
     rd, od = run(D, "d", sp, ktp)
@@ -217,3 +221,29 @@ def test_hybrid_tiered_offload_reload(tier, tmp_path):
     assert off.full.stats[key] >= 150 // 16 - 1
     assert 1 <= off.swa.stats[key] <= 3  # only the last window of the windowed pool
     eng.bm.check_invariants()
+
+
+def test_hybrid_grow_is_all_or_nothing_when_windowed_pool_exhausted():
+    """A windowed pool smaller than the full one runs out first: grow fails
+    without keeping the full pool's new blocks, can_allocate sees the windowed
+    pool, and freeing a sequence makes the grow succeed."""
+    from llmd_amd.engine.hybrid_kv import HybridBlockManager
+
+    rt = _rt_loader.rt()
+    bm = HybridBlockManager(rt, num_full_blocks=64, num_swa_blocks=6, block_size=16, window=16,
+                            prefix_caching=False, emit_events=False)
+    toks = np.arange(3, 200, dtype=np.int32)
+    assert bm.acquire(1, toks, 0) == 0 and bm.acquire(2, toks, 0) == 0
+    assert bm.grow(1, 64)                      # 4 blocks in each pool (swa: 5 usable after the null)
+    free_full, free_swa = bm.full.num_free(), bm.swa.num_free()
+    assert free_swa == 1
+    assert not bm.can_allocate(2)              # the full pool could, the windowed pool cannot
+    assert not bm.grow(2, 32)                  # needs 2 windowed blocks, 1 free
+    assert bm.full.num_free() == free_full and bm.swa.num_free() == free_swa
+    assert bm.full.num_seq_blocks(2) == 0
+    bm.after_compute(1, 64)                    # window 16: blocks below (64-16+1)//16 = 3 go back
+    assert bm.swa.num_free() == 4
+    assert bm.grow(2, 32) and bm.full.num_seq_blocks(2) == 2 and bm.swa.num_seq_blocks(2) == 2
+    bm.free(1)
+    bm.free(2)
+    bm.check_invariants()

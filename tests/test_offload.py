@@ -135,6 +135,55 @@ def test_fs_reload_is_asynchronous(tmp_path):
     assert not fs_read_sync and not reads and orig
 
 
+def test_fs_reload_joins_host_tier(tmp_path):
+    """An FS reload reads into host-tier slots (no per-block pinned buffers) and
+    those blocks stay in the host tier: the next reload of the same prefix is
+    served from host memory, not from disk."""
+    cfg = {"cpu_bytes_to_use": 64 << 20, "fs_root": str(tmp_path / "kv")}
+    base = _gen(make_engine(), _prompt(14))
+    eng = make_engine(kv_offload_config=cfg)
+    _gen(eng, _prompt(14))
+    eng.offload.fs.flush()
+    eng2 = make_engine(kv_offload_config=cfg)
+    assert _gen(eng2, _prompt(14)) == base
+    off = eng2.offload
+    n_fs = off.stats["loaded_fs"]
+    assert n_fs >= 150 // 16 - 1
+    assert len(off.slot_of) >= n_fs and not any(off.slot_busy.values())
+    eng2.reset_prefix_cache()
+    assert _gen(eng2, _prompt(14)) == base
+    assert off.stats["loaded_fs"] == n_fs and off.stats["loaded_cpu"] >= n_fs
+
+
+def test_invalidate_cancels_inflight_reload(tmp_path):
+    """A weight update while an FS reload is in flight: the reload
+    reports 0 tokens (the request recomputes its prefix), its host-slot
+    references are released exactly once (no negative busy counts, every slot
+    can be recycled), and the request still completes with the right tokens."""
+    cfg = {"cpu_bytes_to_use": 64 << 20, "fs_root": str(tmp_path / "kv")}
+    base = _gen(make_engine(), _prompt(15))
+    eng = make_engine(kv_offload_config=cfg)
+    _gen(eng, _prompt(15))
+    eng.offload.fs.flush()
+    eng2 = make_engine(kv_offload_config=cfg)
+    off = eng2.offload
+    eng2.add_request("x", _prompt(15), SamplingParams(max_tokens=8, temperature=0.0, ignore_eos=True))
+    eng2.sched.schedule()
+    assert "x" in eng2.sched.offload_wait and off.loads
+    off.invalidate("new-weights")
+    assert all(v == 0 for v in off.slot_busy.values())
+    out = []
+    for _ in range(300):
+        if not eng2.has_unfinished():
+            break
+        for o in eng2.step():
+            out += o.new_token_ids
+    assert out == base
+    assert off.stats["loaded_fs"] == 0
+    assert all(v >= 0 for v in off.slot_busy.values())
+    assert len(off.free_slots) + len(off.slot_of) == off.n_slots
+
+
 def test_abort_while_loading_frees_blocks():
     eng = make_engine(kv_offload_config={"cpu_bytes_to_use": 64 << 20})
     _gen(eng, _prompt(13))
