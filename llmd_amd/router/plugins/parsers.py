@@ -46,6 +46,8 @@ def _flatten_prompt(body: dict, est: TokenEstimator = _DEFAULT_EST, assets: list
         if p and isinstance(p[0], int):
             return " ".join(map(str, p))
         return "".join(x if isinstance(x, str) else " ".join(map(str, x)) for x in p)
+    if p is not None and not isinstance(p, str):  # a malformed request is the client's error (400)
+        raise ValueError(f"prompt must be a string or a list, got {type(p).__name__}")
     return p or ""
 
 

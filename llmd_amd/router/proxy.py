@@ -234,6 +234,9 @@ def main(argv=None):
                    help="also serve the vLLM gRPC engine API (h2c) through the EPP on this port")
     p.add_argument("--grpc-upstream-port-offset", type=int, default=0,
                    help="engine gRPC port = endpoint (HTTP) port + offset")
+    p.add_argument("--workers", type=int, default=1,
+                   help="proxy worker processes (SO_REUSEPORT) in front of one EPP process; 1 = all in-process "
+                        "(the reference's --concurrency, guides/no-kubernetes-deployment/README.md:211)")
     p.add_argument("--v", type=int, default=1)
     a = p.parse_args(argv)
     logging.basicConfig(level=logging.DEBUG if a.v >= 3 else logging.INFO)
@@ -266,6 +269,18 @@ def main(argv=None):
                 eps.append({"name": f"ep{i}", "address": parts[0], "port": int(parts[1]), "labels": labels})
             for e in endpoints_from_yaml({"endpoints": eps}):
                 await store.add(e)
+
+    if a.workers > 1:
+        from .workers import run_multi
+
+        async def seed_multi():
+            class _App(dict):
+                pass
+            await seed(_App())
+
+        run_multi(epp, elector, "0.0.0.0", a.port, a.metrics_port, a.workers, a.failure_mode, seed=seed_multi,
+                  grpc_port=a.grpc_port, grpc_offset=a.grpc_upstream_port_offset)
+        return
 
     app.on_startup.insert(0, seed)
 

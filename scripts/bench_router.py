@@ -13,7 +13,12 @@ B. End to end: E simulator processes, the router (llmd_amd.router.proxy) in its
    TTFT p50/p99 through the router vs the same load sent straight to the engines
    (round robin) - the difference is the router's added latency.
 
-  python scripts/bench_router.py [--endpoints 8] [--conc 64,256] [--secs 8] [--out profiles/router_overhead.json]
+  python scripts/bench_router.py [--endpoints 8] [--conc 64,256] [--secs 8] [--workers 1,4]
+      [--out profiles/router_overhead.json]
+
+``--workers``: the router runs with that many proxy worker processes in front
+of one EPP process (router/workers.py); each count is measured against the same
+direct baseline.
 """
 from __future__ import annotations
 
@@ -157,41 +162,57 @@ def _wait_port(port, timeout=60):
     raise RuntimeError(f"port {port} never opened")
 
 
-def bench_e2e(n_endpoints, concs, secs, max_tokens, procs) -> list:
+def _start_router(env, ports, workers):
+    rport, mport = _free_port(), _free_port()
+    router = subprocess.Popen([sys.executable, "-m", "llmd_amd.router.proxy", "--port", str(rport),
+                               "--metrics-port", str(mport), "--workers", str(workers),
+                               "--endpoints", ",".join(f"127.0.0.1:{p}" for p in ports), "--v", "0"],
+                              env=env, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
+    return router, rport
+
+
+def _stop(procs):
+    for p in procs:
+        p.terminate()
+    for p in procs:
+        try:
+            p.wait(timeout=10)
+        except subprocess.TimeoutExpired:
+            p.kill()
+
+
+def bench_e2e(n_endpoints, concs, secs, max_tokens, procs, workers=(1,)) -> list:
     env = dict(os.environ, PYTHONPATH=ROOT)
     ports = [_free_port() for _ in range(n_endpoints)]
     sims = [subprocess.Popen([sys.executable, "-m", "llmd_amd.sim.server", "--port", str(p), "--max-num-seqs", "4096",
                               "--prefill-tps", "1e9", "--decode-step-ms", "1"], env=env,
                              stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL) for p in ports]
-    rport, mport = _free_port(), _free_port()
-    router = subprocess.Popen([sys.executable, "-m", "llmd_amd.router.proxy", "--port", str(rport),
-                               "--metrics-port", str(mport),
-                               "--endpoints", ",".join(f"127.0.0.1:{p}" for p in ports), "--v", "0"],
-                              env=env, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
     out = []
     try:
-        for p in ports + [rport]:
+        for p in ports:
             _wait_port(p)
-        time.sleep(2.0)  # first metrics scrape
         direct = [f"http://127.0.0.1:{p}/v1/completions" for p in ports]
-        routed = [f"http://127.0.0.1:{rport}/v1/completions"]
-        for c in concs:
-            d = _load(direct, c, secs, max_tokens, procs)
-            r = _load(routed, c, secs, max_tokens, procs)
-            row = {"endpoints": n_endpoints, "conc": c, "max_tokens": max_tokens, "direct": d, "routed": r,
-                   "added_ttft_p50_ms": round(r["ttft_p50_ms"] - d["ttft_p50_ms"], 2),
-                   "added_ttft_p99_ms": round(r["ttft_p99_ms"] - d["ttft_p99_ms"], 2),
-                   "routed_vs_direct_req_s": round(r["req_s"] / max(d["req_s"], 1e-9), 3)}
-            print(json.dumps(row), flush=True)
-            out.append(row)
-    finally:
-        for p in sims + [router]:
-            p.terminate()
-        for p in sims + [router]:
+        base = {c: _load(direct, c, secs, max_tokens, procs) for c in concs}
+        for w in workers:
+            router, rport = _start_router(env, ports, w)
             try:
-                p.wait(timeout=10)
-            except subprocess.TimeoutExpired:
-                p.kill()
+                _wait_port(rport)
+                time.sleep(2.0)  # first metrics scrape, workers up
+                routed = [f"http://127.0.0.1:{rport}/v1/completions"]
+                for c in concs:
+                    d = base[c]
+                    r = _load(routed, c, secs, max_tokens, procs)
+                    row = {"endpoints": n_endpoints, "router_workers": w, "conc": c, "max_tokens": max_tokens,
+                           "direct": d, "routed": r,
+                           "added_ttft_p50_ms": round(r["ttft_p50_ms"] - d["ttft_p50_ms"], 2),
+                           "added_ttft_p99_ms": round(r["ttft_p99_ms"] - d["ttft_p99_ms"], 2),
+                           "routed_vs_direct_req_s": round(r["req_s"] / max(d["req_s"], 1e-9), 3)}
+                    print(json.dumps(row), flush=True)
+                    out.append(row)
+            finally:
+                _stop([router])
+    finally:
+        _stop(sims)
     return out
 
 
@@ -203,13 +224,15 @@ def main():
     ap.add_argument("--max-tokens", type=int, default=32)
     ap.add_argument("--procs", type=int, default=3, help="client processes")
     ap.add_argument("--skip-e2e", action="store_true")
+    ap.add_argument("--workers", default="1,4", help="router proxy worker processes to compare")
     ap.add_argument("--out", default=None)
     a = ap.parse_args()
     res = {"cpus": os.cpu_count(), "epp": [bench_epp(n) for n in (a.endpoints, 4 * a.endpoints)]}
     for r in res["epp"]:
         print(json.dumps({"epp_decision": r}), flush=True)
     if not a.skip_e2e:
-        res["e2e"] = bench_e2e(a.endpoints, [int(c) for c in a.conc.split(",")], a.secs, a.max_tokens, a.procs)
+        res["e2e"] = bench_e2e(a.endpoints, [int(c) for c in a.conc.split(",")], a.secs, a.max_tokens, a.procs,
+                               [int(w) for w in a.workers.split(",")])
     if a.out:
         with open(a.out, "w") as f:
             json.dump(res, f, indent=1)
