@@ -446,7 +446,8 @@ void mgemm(torch::Tensor y, torch::Tensor x, torch::Tensor w, int64_t wrb, int64
 
 // y [M, N] = x [M, K] . w [N, K]^T for prefill-sized M on the 256 x 256 LDS-DMA MFMA
 // GEMM (csrc/ops/pgemm.hip); epi 1 = fused SiLU-and-mul over gate/up columns interleaved
-// per 256-column tile (y is then [M, N / 2])
+// per 256-column tile, epi 3 = the same on the plain [gate; up] weight (variants 3-5); y is
+// then [M, N / 2]
 // variant 1 with split_k: a mostly idle last wave of tiles runs split over K into an fp32
 // workspace (allocated here from the caching allocator) and is reduced by a second kernel
 void pgemm(torch::Tensor y, torch::Tensor x, torch::Tensor w, int64_t epi, int64_t variant, bool split_k) {
@@ -455,7 +456,8 @@ void pgemm(torch::Tensor y, torch::Tensor x, torch::Tensor w, int64_t epi, int64
   TORCH_CHECK(x.dim() == 2 && w.dim() == 2 && y.dim() == 2, "pgemm: 2-D operands");
   const int64_t M = x.size(0), K = x.size(1), N = w.size(0);
   TORCH_CHECK(w.size(1) == K && K % 64 == 0 && N % 256 == 0, "pgemm: N % 256 == 0, K % 64 == 0");
-  TORCH_CHECK(y.size(0) == M && y.size(1) == (epi == 1 ? N / 2 : N), "pgemm: output shape");
+  TORCH_CHECK(y.size(0) == M && y.size(1) == ((epi == 1 || epi == 3) ? N / 2 : N), "pgemm: output shape");
+  TORCH_CHECK(epi != 3 || (variant >= 3 && variant <= 5), "pgemm: epi 3 (SiLU on the [gate; up] weight) needs variant 3-5");
   TORCH_CHECK(x.stride(0) % 8 == 0 && w.stride(0) % 8 == 0 && y.stride(0) % 8 == 0, "pgemm: 16-B row alignment");
   torch::Tensor ws;
   const int64_t wsb = split_k ? llmd_pgemm_ws_bytes((int)M, (int)N, (int)K, (int)epi, (int)variant) : 0;

@@ -46,7 +46,10 @@ constexpr int BUF = 4 * HALF;       // one K-step: A q0, A q1, W q0, W q1
 constexpr int LDS_BYTES = 2 * BUF;  // 128 KB
 constexpr int GROUP_M = 8;
 
-enum { EPI_NONE = 0, EPI_SILU = 1, EPI_F32 = 2 };
+// EPI_SILU_STD (variants 3-5 only): the fused SiLU-and-mul on the model's own [gate; up] weight
+// ([2F, K], F % 128 == 0): tile tn's W rows are gate rows [128 tn, +128) then up rows
+// [F + 128 tn, +128) - the same tile image as EPI_SILU on a packed weight, no repacking.
+enum { EPI_NONE = 0, EPI_SILU = 1, EPI_F32 = 2, EPI_SILU_STD = 3 };
 
 __device__ __forceinline__ void dma16(const void* src, char* lds) {
   __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)src,
@@ -777,6 +780,435 @@ __global__ __launch_bounds__(NT5, 1) void pgemm5_kernel(const uint16_t* __restri
   }
 }
 
+// ---------------------------------------------------------------------------
+// Variant 3 ("PGR2"): 4 waves x (128 x 128 of C) as variant 1, restructured so
+// that each 64-deep K-step's fragments (both 32-deep halves, 32 ds_read_b128 =
+// 128 VGPR) are read into registers BEFORE its LDS buffer is refilled. With the
+// whole step register-resident, two 64 KB LDS buffers carry a global prefetch
+// two K-steps deep (step kt+2 streams into the buffer step kt was read from),
+// so every LDS-DMA piece has ~1.5 K-steps (~3000 cycles) to land.
+//
+// Per K-step kt (buffer b = kt & 1), 128 MFMA in two halves of 64:
+//   half 0 (set 0, k 0..31): MFMA 0-15 each followed by one ds_read of set 1
+//     (k 32..63 of step kt, W fragments first); at MFMA 40 lgkmcnt(0) +
+//     barrier (every wave has read ALL of buffer b); MFMA 41-63 carry the 8
+//     A-tile LDS-DMA pieces of step kt+2 into buffer b, one per 3 MFMA;
+//   half 1 (set 1): MFMA 0-35 carry the 8 W-tile pieces (one per 5 MFMA); at
+//     MFMA 36 vmcnt(16) (step kt+1's pieces, issued one K-step ago, landed;
+//     this step's 16 stay in flight) + barrier; MFMA 37-52 each followed by one
+//     ds_read of step kt+1's set 0 from buffer b ^ 1 (11 MFMA of slack before
+//     the next step's first MFMA needs them).
+// LDS-DMA through buffer_load_dwordx4 ... lds: one scalar buffer descriptor per
+// operand, a 32-bit per-lane offset fixed for the whole loop, the K offset in
+// soffset and the LDS base in m0 - a handful of scalar instructions per piece,
+// no per-piece 64-bit address math, no branch (the step index is clamped; the
+// two surplus steps at the end reload the last tile into a buffer nobody reads).
+// LDS image per operand: [256 rows][64 k] bf16, each 1 KB DMA piece = 8 rows;
+// 16-B chunk c of row r sits at slot c ^ ((r >> 1) & 7) (source-side swizzle,
+// conflict-free for the 16 x 16 x 32 operand reads).
+constexpr int NT6 = 256;
+// RB6: half-1 MFMA index of the first read of the next step (its barrier one before);
+// AUX6: cache-policy bits of the LDS-DMA loads (0, or 16 = sc1 as hipBLASLt's kernels use)
+constexpr int OPB6 = BM * BK * 2;  // 32 KB per operand per K-step
+constexpr int BUF6 = 2 * OPB6;     // 64 KB
+
+template <int EPI, int RB6 = 37, int AUX6 = 0>
+__global__ __launch_bounds__(NT6, 1) void pgemm6_kernel(const uint16_t* __restrict__ A, int64_t lda,
+                                                        const uint16_t* __restrict__ W, int64_t ldw,
+                                                        uint16_t* __restrict__ C, int64_t ldc, int M, int N, int K,
+                                                        int tile0, int nsplit, float* __restrict__ ws) {
+  __shared__ __attribute__((aligned(1024))) char lds[2 * BUF6];  // the ONLY LDS object
+  const int tiles_m = (M + BM - 1) / BM, tiles_n = N / BN;
+  const int b = xcd_remap(blockIdx.x, gridDim.x);
+  const int tail = gridDim.x / nsplit;
+  const int t_local = b % tail, split = b / tail;
+  const int nk_all = K / BK;
+  const int chunk = (nk_all + nsplit - 1) / nsplit;
+  const int kbeg = split * chunk;
+  const int nk = min(chunk, nk_all - kbeg);
+  int tm, tn;
+  tile_mn(tile0 + t_local, tiles_m, tiles_n, tm, tn);
+  const int m0 = tm * BM, n0 = tn * BN;
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: LDS bases stay scalar
+  const int wr = w >> 1, wc = w & 1;
+
+  // buffer descriptors over the K-range of this split (byte offsets must fit 31 bits: host-checked)
+  const __amdgpu_buffer_rsrc_t ra =
+      __builtin_amdgcn_make_buffer_rsrc((void*)(A + (int64_t)kbeg * BK), 0, 0x7fffffff, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rw =
+      __builtin_amdgcn_make_buffer_rsrc((void*)(W + (int64_t)kbeg * BK), 0, 0x7fffffff, 0x00020000);
+  // DMA piece j of this wave: rows 64 w + 8 j + (lane >> 3), LDS slot lane & 7 <- chunk (lane & 7) ^ f(row)
+  uint32_t va[8], vw[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int row = 64 * w + 8 * j + (lane >> 3);
+    const int c = (lane & 7) ^ ((row >> 1) & 7);
+    va[j] = (uint32_t)((min(m0 + row, M - 1) * lda + c * 8) * 2);
+    const int wrow = EPI == EPI_SILU_STD ? (row < 128 ? 0 : N / 2 - 128) + tn * 128 + row : n0 + row;
+    vw[j] = (uint32_t)((wrow * ldw + c * 8) * 2);
+  }
+  auto dma = [&](int kt, int j, bool wop) {  // piece j of operand A (wop = false) or W, K-step kt
+    const uint32_t so = (uint32_t)(min(kt, nk - 1) * BK * 2);
+    char* dst = lds + (kt & 1) * BUF6 + (wop ? OPB6 : 0) + (8 * w + j) * 1024;
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(wop ? rw : ra, (__attribute__((address_space(3))) void*)dst, 16,
+                                             wop ? vw[j] : va[j], so, 0, AUX6);
+  };
+
+  // fragment reads: row 16 t + (lane & 15), chunk 4 h + (lane >> 4) at slot chunk ^ ((lane >> 1) & 7)
+  const int fr = lane & 15, fq = lane >> 4;
+  const int rd0 = fr * 128 + ((fq ^ ((fr >> 1) & 7)) * 16);
+  const int rd1 = fr * 128 + (((4 + fq) ^ ((fr >> 1) & 7)) * 16);
+  const int a_rd = (wr * 128) * 128, w_rd = OPB6 + (wc * 128) * 128;
+
+  f32x4_t acc[8][8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  s16x8_t fa0[8], fw0[8], fa1[8], fw1[8];
+
+  // prologue: steps 0 and 1 in flight, step 0 landed, its set 0 in registers
+#pragma unroll
+  for (int j = 0; j < 8; ++j) dma(0, j, false);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) dma(0, j, true);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) dma(1, j, false);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) dma(1, j, true);
+  asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+  bar();
+  // read order of a set (everywhere): A row 0, the 8 W fragments, A rows 1..7 - MFMA (0, j) then
+  // needs only the first j + 2 reads, so the waits before the first MFMA row are progressive
+  fa0[0] = *reinterpret_cast<const s16x8_t*>(lds + a_rd + rd0);
+  __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    fw0[i] = *reinterpret_cast<const s16x8_t*>(lds + w_rd + i * 2048 + rd0);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+#pragma unroll
+  for (int i = 1; i < 8; ++i) {
+    fa0[i] = *reinterpret_cast<const s16x8_t*>(lds + a_rd + i * 2048 + rd0);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  // nothing pending on the loop's entry edge: hipcc's waitcnt pass then keeps the counted
+  // waits of the back edge at the loop head instead of merging to lgkmcnt(0) every K-step
+  __builtin_amdgcn_s_waitcnt(0xC07F);
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_nop 4" ::: "memory");  // v_accvgpr_write (zero init) -> MFMA srcC
+  __builtin_amdgcn_sched_barrier(0);
+
+  for (int kt = 0; kt < nk; ++kt) {
+    const char* cur = lds + (kt & 1) * BUF6;
+    const char* nxt = lds + ((kt & 1) ^ 1) * BUF6;
+    // ---- half 0: set 0; reads of set 1; barrier; A pieces of step kt + 2
+#pragma unroll
+    for (int t = 0; t < 64; ++t) {
+      const int i = t >> 3, j = t & 7;
+      // explicit progressive waits for set 0 (hipcc's own pass waits lgkmcnt(0) at the loop head):
+      // MFMA (0, j) needs the first j + 2 of set 0's 16 reads, (i, 0) the first i + 9; the set-1
+      // reads issued after MFMA 0 .. t - 1 are younger still
+      // (row 1: 7 - 1 + 8 = 14; from row 2 on at least 15 younger reads, nothing to wait for)
+      if (t <= 8) __builtin_amdgcn_s_waitcnt(0xC07F | (14 << 8));
+      mfma16_acc(acc[i][j], fw0[j], fa0[i]);
+      if (t == 0) {
+        fa1[0] = *reinterpret_cast<const s16x8_t*>(cur + a_rd + rd1);
+      } else if (t < 9) {
+        fw1[t - 1] = *reinterpret_cast<const s16x8_t*>(cur + w_rd + (t - 1) * 2048 + rd1);
+      } else if (t < 16) {
+        fa1[t - 8] = *reinterpret_cast<const s16x8_t*>(cur + a_rd + (t - 8) * 2048 + rd1);
+      } else if (t == 40) {
+        __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this wave's reads of buffer b retired
+        bar();
+      } else if (t > 40 && (t - 41) % 3 == 0) {
+        dma(kt + 2, (t - 41) / 3, false);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    // ---- half 1: set 1; W pieces of step kt + 2; wait step kt + 1; reads of its set 0
+#pragma unroll
+    for (int t = 0; t < 64; ++t) {
+      const int i = t >> 3, j = t & 7;
+      mfma16_acc(acc[i][j], fw1[j], fa1[i]);
+      if (t < 36 && t % 5 == 0) {
+        dma(kt + 2, t / 5, true);
+      } else if (t == RB6 - 1) {
+        asm volatile("s_waitcnt vmcnt(16)" ::: "memory");  // step kt+1 landed (this step's 16 in flight)
+        bar();
+      } else if (t == RB6) {
+        fa0[0] = *reinterpret_cast<const s16x8_t*>(nxt + a_rd + rd0);
+      } else if (t > RB6 && t < RB6 + 9) {
+        fw0[t - RB6 - 1] = *reinterpret_cast<const s16x8_t*>(nxt + w_rd + (t - RB6 - 1) * 2048 + rd0);
+      } else if (t >= RB6 + 9 && t < RB6 + 16) {
+        fa0[t - RB6 - 8] = *reinterpret_cast<const s16x8_t*>(nxt + a_rd + (t - RB6 - 8) * 2048 + rd0);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+  mfma_drain();
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  if constexpr (EPI == EPI_F32) {
+    float* wt = ws + ((int64_t)split * tail + t_local) * (BM * BN);
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int row = wr * 128 + 16 * i + fr, col = wc * 128 + 16 * j + 4 * fq;
+        *reinterpret_cast<f32x4_t*>(wt + row * BN + col) = acc[i][j];
+      }
+    return;
+  }
+  __syncthreads();
+  char* img = lds + w * 32768;
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int row = 16 * i + fr, col = 16 * j + 4 * fq;
+      const f32x4_t v = acc[i][j];
+      u32x2_t p;
+      p[0] = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
+      p[1] = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
+      *reinterpret_cast<u32x2_t*>(img + row * 256 + (((col >> 3) ^ (row & 15)) * 16) + (col & 7) * 2) = p;
+    }
+  __syncthreads();
+  if constexpr (EPI == EPI_NONE) {
+#pragma unroll 4
+    for (int it = 0; it < 32; ++it) {
+      const int row = it * 4 + (lane >> 4), c = lane & 15;
+      const int m = m0 + wr * 128 + row;
+      const u32x4_t v = *reinterpret_cast<const u32x4_t*>(img + row * 256 + ((c ^ (row & 15)) * 16));
+      if (m < M) *reinterpret_cast<u32x4_t*>(C + (int64_t)m * ldc + n0 + wc * 128 + c * 8) = v;
+    }
+  } else {
+    const char* gimg = lds + (wr * 2) * 32768;
+    const char* uimg = gimg + 32768;
+#pragma unroll 4
+    for (int it = 0; it < 16; ++it) {
+      const int row = wc * 64 + it * 4 + (lane >> 4), c = lane & 15;
+      const int m = m0 + wr * 128 + row;
+      const int off = row * 256 + ((c ^ (row & 15)) * 16);
+      float gf[8], uf[8], of[8];
+      unpack8(*reinterpret_cast<const u32x4_t*>(gimg + off), gf);
+      unpack8(*reinterpret_cast<const u32x4_t*>(uimg + off), uf);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) of[e] = gf[e] / (1.f + __expf(-gf[e])) * uf[e];
+      if (m < M) *reinterpret_cast<u32x4_t*>(C + (int64_t)m * ldc + n0 / 2 + c * 8) = pack8(of);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Variant 6 ("persistent PGR2"): variant 3's K-loop, but each workgroup walks a
+// list of tiles (tile b, b + P, b + 2P, ... of the data-parallel range; P = min(#tiles,
+// 256) workgroups) as ONE continuous stream of K-steps: the LDS-DMA of step g + 2
+// and the fragment reads of step g + 1 run straight across tile boundaries, so the
+// next tile's first two K-steps load while the current tile finishes - no per-tile
+// prologue wait (an HBM round trip, ~2-4 % of a 128-step tile). The epilogue stores
+// straight from the accumulators (no LDS: both LDS buffers hold the next tile then):
+// each lane owns 4 consecutive columns of a row, 8-B stores. EPI_SILU_STD maps
+// each wave to 64 gate + the matching 64 up columns (W fragments 0-3 from gate rows,
+// 4-7 from up rows), so silu(g) * u is formed in registers.
+template <int EPI>
+__global__ __launch_bounds__(NT6, 1) void pgemm7_kernel(const uint16_t* __restrict__ A, int64_t lda,
+                                                        const uint16_t* __restrict__ W, int64_t ldw,
+                                                        uint16_t* __restrict__ C, int64_t ldc, int M, int N, int K,
+                                                        int ntiles) {
+  constexpr int RB = 37;
+  __shared__ __attribute__((aligned(1024))) char lds[2 * BUF6];  // the ONLY LDS object
+  const int tiles_m = (M + BM - 1) / BM, tiles_n = N / BN;
+  const int P = gridDim.x;
+  const int b = xcd_remap(blockIdx.x, P);
+  const int nt = (ntiles - b + P - 1) / P;  // tiles of this workgroup: b, b + P, ...
+  const int nk = K / BK;
+  const int S = nt * nk;                    // K-steps of this workgroup, all tiles
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = w >> 1, wc = w & 1;
+  const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc((void*)A, 0, 0x7fffffff, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc((void*)W, 0, 0x7fffffff, 0x00020000);
+
+  // per-lane DMA offsets of the tile being LOADED (advances two K-steps ahead of compute)
+  uint32_t va[8], vw[8];
+  auto set_dma_tile = [&](int r) {
+    int tm, tn;
+    tile_mn(b + min(r, nt - 1) * P, tiles_m, tiles_n, tm, tn);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int row = 64 * w + 8 * j + (lane >> 3);
+      const int c = (lane & 7) ^ ((row >> 1) & 7);
+      va[j] = (uint32_t)((min(tm * BM + row, M - 1) * lda + c * 8) * 2);
+      const int wrow = EPI == EPI_SILU_STD ? (row < 128 ? 0 : N / 2 - 128) + tn * 128 + row : tn * BN + row;
+      vw[j] = (uint32_t)((wrow * ldw + c * 8) * 2);
+    }
+  };
+  // piece j of operand A or W of global K-step g, whose step within its tile is kt_of_g (the
+  // offsets of that tile are set by set_dma_tile)
+  auto dma = [&](int g, int kt_of_g, int j, bool wop) {
+    const uint32_t so = (uint32_t)(kt_of_g * BK * 2);
+    char* dst = lds + (g & 1) * BUF6 + (wop ? OPB6 : 0) + (8 * w + j) * 1024;
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(wop ? rw : ra, (__attribute__((address_space(3))) void*)dst, 16,
+                                             wop ? vw[j] : va[j], so, 0, 0);
+  };
+
+  const int fr = lane & 15, fq = lane >> 4;
+  const int rd0 = fr * 128 + ((fq ^ ((fr >> 1) & 7)) * 16);
+  const int rd1 = fr * 128 + (((4 + fq) ^ ((fr >> 1) & 7)) * 16);
+  const int a_rd = (wr * 128) * 128;
+  // W fragment j of this wave: rows wc*128 + 16 j (EPI_NONE); gate rows wc*64 + 16 j (j < 4) and
+  // up rows 128 + wc*64 + 16 (j - 4) (EPI_SILU_STD)
+  auto w_off = [&](int j) {
+    return OPB6 + (EPI == EPI_SILU_STD ? (j < 4 ? wc * 64 + 16 * j : 128 + wc * 64 + 16 * (j - 4))
+                                       : wc * 128 + 16 * j) * 128;
+  };
+
+  f32x4_t acc[8][8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  s16x8_t fa0[8], fw0[8], fa1[8], fw1[8];
+
+  set_dma_tile(0);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) dma(0, 0, j, false);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) dma(0, 0, j, true);
+  if (nk == 1) set_dma_tile(1);
+  const int kt1 = nk == 1 ? 0 : 1;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) dma(1, kt1, j, false);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) dma(1, kt1, j, true);
+  asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+  bar();
+  fa0[0] = *reinterpret_cast<const s16x8_t*>(lds + a_rd + rd0);
+  __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    fw0[i] = *reinterpret_cast<const s16x8_t*>(lds + w_off(i) + rd0);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+#pragma unroll
+  for (int i = 1; i < 8; ++i) {
+    fa0[i] = *reinterpret_cast<const s16x8_t*>(lds + a_rd + i * 2048 + rd0);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  __builtin_amdgcn_s_waitcnt(0xC07F);
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_nop 4" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+
+  for (int r = 0; r < nt; ++r) {
+  for (int kt = 0; kt < nk; ++kt) {
+    const int g = r * nk + kt;
+    const char* cur = lds + (g & 1) * BUF6;
+    const char* nxt = lds + ((g & 1) ^ 1) * BUF6;
+    // the DMA of this step loads global step g + 2 = step kt2 of tile r2 (scalar bookkeeping, no
+    // division); past the last step it re-loads the last one into a buffer nobody reads
+    int kt2 = kt + 2;
+    if (nk == 1) {
+      kt2 = 0;
+      set_dma_tile(r + 2);
+    } else if (kt2 >= nk) {
+      kt2 -= nk;
+      if (kt2 == 0) set_dma_tile(r + 1);
+    }
+    if (g + 2 >= S) kt2 = nk - 1;
+#pragma unroll
+    for (int t = 0; t < 64; ++t) {
+      const int i = t >> 3, j = t & 7;
+      if (t <= 8) __builtin_amdgcn_s_waitcnt(0xC07F | (14 << 8));
+      mfma16_acc(acc[i][j], fw0[j], fa0[i]);
+      if (t == 0) {
+        fa1[0] = *reinterpret_cast<const s16x8_t*>(cur + a_rd + rd1);
+      } else if (t < 9) {
+        fw1[t - 1] = *reinterpret_cast<const s16x8_t*>(cur + w_off(t - 1) + rd1);
+      } else if (t < 16) {
+        fa1[t - 8] = *reinterpret_cast<const s16x8_t*>(cur + a_rd + (t - 8) * 2048 + rd1);
+      } else if (t == 40) {
+        __builtin_amdgcn_s_waitcnt(0xC07F);
+        bar();
+      } else if (t > 40 && (t - 41) % 3 == 0) {
+        dma(g + 2, kt2, (t - 41) / 3, false);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+#pragma unroll
+    for (int t = 0; t < 64; ++t) {
+      const int i = t >> 3, j = t & 7;
+      mfma16_acc(acc[i][j], fw1[j], fa1[i]);
+      if (t < 36 && t % 5 == 0) {
+        dma(g + 2, kt2, t / 5, true);
+      } else if (t == RB - 1) {
+        asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+        bar();
+      } else if (t == RB) {
+        fa0[0] = *reinterpret_cast<const s16x8_t*>(nxt + a_rd + rd0);
+      } else if (t > RB && t < RB + 9) {
+        fw0[t - RB - 1] = *reinterpret_cast<const s16x8_t*>(nxt + w_off(t - RB - 1) + rd0);
+      } else if (t >= RB + 9 && t < RB + 16) {
+        fa0[t - RB - 8] = *reinterpret_cast<const s16x8_t*>(nxt + a_rd + (t - RB - 8) * 2048 + rd0);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+    {
+      // tile r done: store it straight from the accumulators, then restart them
+      int tm, tn;
+      tile_mn(b + r * P, tiles_m, tiles_n, tm, tn);
+      mfma_drain();
+      __builtin_amdgcn_sched_barrier(0);
+      const int mrow = tm * BM + wr * 128 + fr;
+      if constexpr (EPI == EPI_NONE) {
+        uint16_t* cb = C + (int64_t)tn * BN + wc * 128 + 4 * fq;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          const int m = mrow + 16 * i;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const f32x4_t v = acc[i][j];
+            u32x2_t p;
+            p[0] = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
+            p[1] = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
+            if (m < M) *reinterpret_cast<u32x2_t*>(cb + (int64_t)m * ldc + 16 * j) = p;
+          }
+        }
+      } else {
+        uint16_t* cb = C + (int64_t)tn * 128 + wc * 64 + 4 * fq;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          const int m = mrow + 16 * i;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const f32x4_t gv = acc[i][j], uv = acc[i][j + 4];
+            float o[4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) o[e] = gv[e] / (1.f + __expf(-gv[e])) * uv[e];
+            u32x2_t p;
+            p[0] = (uint32_t)f2bf(o[0]) | ((uint32_t)f2bf(o[1]) << 16);
+            p[1] = (uint32_t)f2bf(o[2]) | ((uint32_t)f2bf(o[3]) << 16);
+            if (m < M) *reinterpret_cast<u32x2_t*>(cb + (int64_t)m * ldc + 16 * j) = p;
+          }
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+      __builtin_amdgcn_sched_barrier(0);
+      asm volatile("s_nop 4" ::: "memory");  // v_accvgpr_write -> MFMA srcC
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+}
+
 // ws [nsplit][tail][256][256] fp32 partials -> C tiles tile0 .. tile0 + tail - 1 (bf16, rows < M)
 __global__ __launch_bounds__(256) void pgemm_splitk_reduce(const float* __restrict__ ws, int nsplit, int tail,
                                                            int tile0, uint16_t* __restrict__ C, int64_t ldc, int M,
@@ -834,9 +1266,66 @@ extern "C" int llmd_pgemm(const void* A, int64_t lda, const void* W, int64_t ldw
                           int K, int epi, int variant, void* ws, hipStream_t st) {
   if (M <= 0) return 0;
   if (N % BN || K % BK || lda % 8 || ldw % 8 || ldc % 8) return -1;
+  if (epi == EPI_SILU_STD && (variant < 3 || variant > 6)) return -3;
   // 32-bit DMA offsets
   if ((int64_t)(M - 1) * lda + K > 0x7fffffffLL || (int64_t)(N - 1) * ldw + K > 0x7fffffffLL) return -2;
   const int ntiles = ((M + BM - 1) / BM) * (N / BN);
+  if (variant == 6) {
+    if (((int64_t)(M - 1) * lda + K) * 2 > 0x7fffffffLL || ((int64_t)(N - 1) * ldw + K) * 2 > 0x7fffffffLL) return -2;
+    int full = ntiles, tail = 0, nsplit = 1;
+    if (ws != nullptr) pgemm_plan(M, N, K, epi == EPI_SILU_STD ? EPI_SILU : epi, full, tail, nsplit);
+    const auto* a = (const uint16_t*)A;
+    const auto* w = (const uint16_t*)W;
+    auto* c = (uint16_t*)C;
+    const int P = std::min(full, PG_CUS);
+    if (epi == EPI_SILU_STD)
+      hipLaunchKernelGGL(pgemm7_kernel<EPI_SILU_STD>, dim3(P), dim3(NT6), 0, st, a, lda, w, ldw, c, ldc, M, N, K, full);
+    else if (epi == EPI_NONE && full > 0)
+      hipLaunchKernelGGL(pgemm7_kernel<EPI_NONE>, dim3(P), dim3(NT6), 0, st, a, lda, w, ldw, c, ldc, M, N, K, full);
+    else if (epi != EPI_NONE)
+      return -3;
+    if (nsplit > 1) {
+      hipLaunchKernelGGL((pgemm6_kernel<EPI_F32, 37, 0>), dim3(tail * nsplit), dim3(NT6), 0, st, a, lda, w, ldw, c, ldc,
+                         M, N, K, full, nsplit, (float*)ws);
+      hipLaunchKernelGGL(pgemm_splitk_reduce, dim3(tail * (BM / 8)), dim3(256), 0, st, (const float*)ws, nsplit,
+                         tail, full, c, ldc, M, N);
+    }
+    return (int)hipGetLastError();
+  }
+  if (variant >= 3 && variant <= 5) {
+    // buffer offsets are 31-bit byte offsets
+    if (((int64_t)(M - 1) * lda + K) * 2 > 0x7fffffffLL || ((int64_t)(N - 1) * ldw + K) * 2 > 0x7fffffffLL) return -2;
+    int full = ntiles, tail = 0, nsplit = 1;
+    if (ws != nullptr) pgemm_plan(M, N, K, epi, full, tail, nsplit);
+    const auto* a = (const uint16_t*)A;
+    const auto* w = (const uint16_t*)W;
+    auto* c = (uint16_t*)C;
+    // 3: reads of the next step from half-1 MFMA 37; 4: + sc1 LDS-DMA loads; 5: reads from MFMA 44
+    auto launch = [&](auto k_silu, auto k_std, auto k_none, auto k_f32) {
+      if (epi == EPI_SILU)
+        hipLaunchKernelGGL(k_silu, dim3(full), dim3(NT6), 0, st, a, lda, w, ldw, c, ldc, M, N, K, 0, 1, nullptr);
+      else if (epi == EPI_SILU_STD)
+        hipLaunchKernelGGL(k_std, dim3(full), dim3(NT6), 0, st, a, lda, w, ldw, c, ldc, M, N, K, 0, 1, nullptr);
+      else if (full > 0)
+        hipLaunchKernelGGL(k_none, dim3(full), dim3(NT6), 0, st, a, lda, w, ldw, c, ldc, M, N, K, 0, 1, nullptr);
+      if (nsplit > 1) {
+        hipLaunchKernelGGL(k_f32, dim3(tail * nsplit), dim3(NT6), 0, st, a, lda, w, ldw, c, ldc, M, N, K, full,
+                           nsplit, (float*)ws);
+        hipLaunchKernelGGL(pgemm_splitk_reduce, dim3(tail * (BM / 8)), dim3(256), 0, st, (const float*)ws, nsplit,
+                           tail, full, c, ldc, M, N);
+      }
+    };
+    if (variant == 3)
+      launch(pgemm6_kernel<EPI_SILU, 37, 0>, pgemm6_kernel<EPI_SILU_STD, 37, 0>, pgemm6_kernel<EPI_NONE, 37, 0>,
+             pgemm6_kernel<EPI_F32, 37, 0>);
+    else if (variant == 4)
+      launch(pgemm6_kernel<EPI_SILU, 37, 16>, pgemm6_kernel<EPI_SILU_STD, 37, 16>, pgemm6_kernel<EPI_NONE, 37, 16>,
+             pgemm6_kernel<EPI_F32, 37, 16>);
+    else
+      launch(pgemm6_kernel<EPI_SILU, 44, 0>, pgemm6_kernel<EPI_SILU_STD, 44, 0>, pgemm6_kernel<EPI_NONE, 44, 0>,
+             pgemm6_kernel<EPI_F32, 44, 0>);
+    return (int)hipGetLastError();
+  }
   if (variant == 2) {
     int full = ntiles, tail = 0, nsplit = 1;
     if (ws != nullptr) pgemm_plan(M, N, K, epi, full, tail, nsplit);

@@ -25,7 +25,15 @@ class LlamaMLP(torch.nn.Module):
         self.down = RowLinear(cfg.intermediate_size, cfg.hidden_size, device=device)
 
     def forward(self, x):
-        h = self.gate_up(x)
+        gu = self.gate_up
+        if (gu.lora is None and gu.bias is None and not wants_fp8_input(self.down) and x.dim() == 2
+                and gu.weight.dtype == torch.bfloat16):
+            # prefill: gate/up GEMM with the SiLU-and-mul in its epilogue (csrc/ops/pgemm.hip
+            # EPI_SILU_STD) where the shipped table has it ahead of hipBLASLt + the act kernel
+            v = ops.pgemm_silu_plan(x, gu.weight)
+            if v is not None:
+                return self.down(ops.pgemm_silu(x, gu.weight, variant=v))
+        h = gu(x)
         if wants_fp8_input(self.down):  # SiLU*up fused with the down proj's fp8 activation quant
             return self.down(ops.gated_act_quant(h, ops.ACT_SILU))
         return self.down(ops.gated_act(h, ops.ACT_SILU))

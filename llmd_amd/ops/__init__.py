@@ -960,9 +960,16 @@ def pgemm(x: torch.Tensor, w: torch.Tensor, epi: int = 0, out: Optional[torch.Te
     M = x.shape[0]
     N = w.shape[0]
     if out is None:
-        out = torch.empty(M, N // 2 if epi else N, dtype=x.dtype, device=x.device)
+        out = torch.empty(M, N // 2 if epi in (1, 3) else N, dtype=x.dtype, device=x.device)
     native().pgemm(out, x, w, epi, PGEMM_VARIANT if variant is None else variant, split_k)
     return out
+
+
+def pgemm_silu(x: torch.Tensor, w: torch.Tensor, variant: int = 3, out: Optional[torch.Tensor] = None):
+    """silu(x W_gate^T) * (x W_up^T) in ONE prefill GEMM on the model's own fused [gate; up]
+    weight ([2F, K], F % 128 == 0): each 256-column tile loads 128 gate rows and the matching
+    128 up rows, the epilogue stores the activation [M, F] (no [M, 2F] round trip, no act kernel)."""
+    return pgemm(x, w, epi=3, out=out, variant=variant, split_k=False)
 
 
 def pgemm_pack_gate_up(w: torch.Tensor) -> torch.Tensor:
@@ -995,13 +1002,12 @@ def mgemm_choice(M: int, N: int, K: int) -> Optional[tuple[int, int, int]]:
     return None
 
 
-# Prefill-sized GEMMs: the hand-written prefill GEMM (pgemm, v0 + split-K tail) where it
-# beats hipBLASLt ON THIS SHAPE. hipBLASLt's kernel choice swings with M (profiles/
-# pgemm_r4_v0_v1_blas.txt: at M 5064 its o / down projections run at ~1.0 PF/s, pgemm at
-# 1.34 / 1.38; Llama-3-8B's down projection at M 4608: 0.77 vs 0.42 ms) while it wins most
-# aligned shapes, so the choice is measured once per (M bucket of 256 rows, N, K) on the
-# operands themselves - two timed runs each, outside graph capture - and cached.
-PGEMM_AUTO = os.environ.get("LLMD_PGEMM_AUTO", "1") == "1"
+# Prefill-sized GEMMs: the hand-written prefill GEMM (pgemm) where it beats hipBLASLt ON THIS
+# SHAPE. The choice is a STATIC table measured offline (ops/pgemm_table.py, written by
+# scripts/make_pgemm_table.py): keyed by (M bucket of 256 rows, N, K), so every run and every
+# TP / EP rank picks the same kernel and no forward ever stalls on a timing run.
+# LLMD_PGEMM_AUTO=measure restores the old first-sight timing (tuning only); =0 disables pgemm.
+PGEMM_AUTO = os.environ.get("LLMD_PGEMM_AUTO", "table")
 PGEMM_MIN_M = int(os.environ.get("LLMD_PGEMM_MIN_M", "256"))
 _pgemm_pick: dict = {}
 
@@ -1017,17 +1023,40 @@ def _time_ms(fn, reps: int = 2) -> float:
     return st.elapsed_time(en) / reps
 
 
-def pgemm_wins(x: torch.Tensor, w: torch.Tensor) -> bool:
+def pgemm_plan(M: int, N: int, K: int) -> Optional[tuple[int, bool]]:
+    """(variant, split_k) of the prefill GEMM for this shape from the shipped table, or None
+    (hipBLASLt)."""
+    from .pgemm_table import PGEMM_TABLE
+
+    e = PGEMM_TABLE.get(((M + 255) // 256, N, K))
+    return None if e is None else e[0]
+
+
+def pgemm_silu_plan(x: torch.Tensor, w: torch.Tensor) -> Optional[int]:
+    """Variant of the fused gate/up + SiLU prefill GEMM (pgemm_silu) for this shape from the
+    shipped table (entries keyed ("silu", M bucket, N, K)), or None: hipBLASLt + act kernel."""
+    if PGEMM_AUTO == "0" or x.shape[0] < PGEMM_MIN_M or not pgemm_ok(x, w) or (w.shape[0] // 2) % 128:
+        return None
+    from .pgemm_table import PGEMM_TABLE
+
+    e = PGEMM_TABLE.get(("silu", (x.shape[0] + 255) // 256, w.shape[0], w.shape[1]))
+    return None if e is None or e[0] is None else e[0][0]
+
+
+def pgemm_wins(x: torch.Tensor, w: torch.Tensor) -> Optional[tuple[int, bool]]:
+    """The pgemm plan for this GEMM, or None for hipBLASLt."""
     M, (N, K) = x.shape[0], w.shape
+    if PGEMM_AUTO != "measure":
+        return pgemm_plan(M, N, K)
     key = ((M + 255) // 256, N, K)
-    c = _pgemm_pick.get(key)
-    if c is None:
+    c = _pgemm_pick.get(key, False)
+    if c is False:
         if torch.cuda.is_current_stream_capturing():
-            return False
+            return None
         y = torch.empty(M, N, dtype=x.dtype, device=x.device)
         t_pg = _time_ms(lambda: pgemm(x, w, out=y))
         t_bl = _time_ms(lambda: torch.nn.functional.linear(x, w))
-        c = _pgemm_pick[key] = t_pg < 0.97 * t_bl
+        c = _pgemm_pick[key] = (PGEMM_VARIANT, True) if t_pg < 0.97 * t_bl else None
         msg = (f"prefill GEMM M~{M} N={N} K={K}: pgemm {t_pg:.3f} ms, hipBLASLt {t_bl:.3f} ms -> "
                f"{'pgemm' if c else 'hipBLASLt'}")
         log.debug(msg)
@@ -1043,11 +1072,13 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None
     measured dispatch tables have them ahead of hipBLASLt - the medium-M LDS-DMA
     kernel (csrc/ops/mgemm.hip, M 33..128, ops/mgemm_table.py) first, then the
     stream kernel (csrc/ops/skinny_gemm.hip, M <= 64, ops/dgemm_table.py) -
-    prefill-sized M on the prefill GEMM where it measured faster for the shape
-    (pgemm_wins) - everything else on hipBLASLt."""
-    if PGEMM_AUTO and x.dim() == 2 and x.shape[0] >= PGEMM_MIN_M and pgemm_ok(x, w) and pgemm_wins(x, w):
-        y = pgemm(x, w)
-        return y if bias is None else y.add_(bias)
+    prefill-sized M on the prefill GEMM where the shipped table (ops/pgemm_table.py)
+    has it ahead of hipBLASLt - everything else on hipBLASLt."""
+    if PGEMM_AUTO != "0" and x.dim() == 2 and x.shape[0] >= PGEMM_MIN_M and pgemm_ok(x, w):
+        plan = pgemm_wins(x, w)
+        if plan is not None:
+            y = pgemm(x, w, variant=plan[0], split_k=plan[1])
+            return y if bias is None else y.add_(bias)
     if _SKINNY:
         M = x.shape[0] if x.dim() == 2 else 0
         if 33 <= M <= 128 and mgemm_ok(x, w):

@@ -43,13 +43,13 @@ def main():
         x = torch.rand(M, K, device=dev).mul_(2).sub_(1).to(torch.bfloat16)
         w = torch.rand(N, K, device=dev).mul_(2).sub_(1).mul_(0.05).to(torch.bfloat16)
         ref = x.float() @ w.float().t()
-        for v in (0, 1, 2):
+        for v in sorted({0} | {int(t) for t in a.variants.split(",")}):
             got = ops.pgemm(x, w, variant=v).float()
             err = (got - ref).abs().max().item() / ref.abs().max().item()
             wp = ops.pgemm_pack_gate_up(w)
             g, u = ref[:, : N // 2], ref[:, N // 2:]
             sref = g * torch.sigmoid(g) * u
-            sgot = ops.pgemm(x, wp, epi=1, variant=v).float()
+            sgot = (ops.pgemm_silu(x, w, variant=v) if v >= 3 else ops.pgemm(x, wp, epi=1, variant=v)).float()
             serr = (sgot - sref).abs().max().item() / sref.abs().max().item()
             print(f"check v{v} M={M} N={N} K={K}: rel err {err:.2e}  silu rel err {serr:.2e}", flush=True)
             assert err < 1e-2 and serr < 2e-2
@@ -82,7 +82,9 @@ def main():
                 if fused:
                     res["blas+act"].append(timeit(lambda: ops.gated_act(F.linear(x, w), ops.ACT_SILU), it))
                     for v in vs:
-                        res[f"v{v}silu"].append(timeit(lambda: ops.pgemm(x, wp, epi=1, out=ya, variant=v), it))
+                        res[f"v{v}silu"].append(timeit(
+                            (lambda: ops.pgemm_silu(x, w, variant=v, out=ya)) if v >= 3 else
+                            (lambda: ops.pgemm(x, wp, epi=1, out=ya, variant=v)), it))
             d = max((ops.pgemm(x, w, variant=v).float() - F.linear(x, w).float()).abs().max().item() for v in vs)
             line = f"M={M:5d} {name:10s} N={N:6d} K={K:6d}:"
             for k, v in res.items():

@@ -12,7 +12,12 @@ timeout -s KILL 120 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT
 python3 - <<'PY'
 import csv, glob, collections
 def kind(n):
-    return "blas" if "Cijk" in n else ("pgemm5" if "pgemm5" in n else ("pgemm4" if "pgemm4" in n else ("pgemm0" if "pgemm_kernel" in n else None)))
+    if "Cijk" in n:
+        return "blas"
+    for v in ("pgemm6", "pgemm5", "pgemm4"):
+        if v in n:
+            return v
+    return "pgemm0" if "pgemm_kernel" in n else None
 agg = collections.defaultdict(lambda: collections.defaultdict(float))
 cnt = collections.defaultdict(lambda: collections.defaultdict(int))
 for f in sorted(glob.glob("gpurun_out/pmc_pgemm/*counter_collection.csv")):

@@ -207,7 +207,7 @@ def test_mgemm_fp8(M, plan):
 
 @pytest.mark.parametrize("M,N,K", [(1, 256, 64), (77, 512, 1024), (256, 768, 128), (1000, 1280, 2048),
                                    (4608, 1024, 8192), (300, 512, 8192), (4608, 8192, 8192)])
-@pytest.mark.parametrize("variant", [0, 1])
+@pytest.mark.parametrize("variant", [0, 1, 3, 6])
 def test_pgemm(M, N, K, variant):
     """Prefill GEMM (256 x 256 LDS-DMA tiles, counted-vmcnt pipeline) vs the fp32
     reference; K = 64 and 128 exercise the prologue / tail waits without a steady state;
@@ -222,8 +222,27 @@ def test_pgemm(M, N, K, variant):
     _close(ops.pgemm(x, w, variant=variant), ref, atol=2e-2, rtol=2e-2)
     _close(ops.pgemm(x, w, variant=variant, split_k=False), ref, atol=2e-2, rtol=2e-2)
     g, u = ref[:, : N // 2], ref[:, N // 2:]
-    _close(ops.pgemm(x, ops.pgemm_pack_gate_up(w), epi=1, variant=variant), g * torch.sigmoid(g) * u,
-           atol=2e-2, rtol=3e-2)
+    if variant != 6:  # the persistent variant has no packed-layout (epi 1) form
+        _close(ops.pgemm(x, ops.pgemm_pack_gate_up(w), epi=1, variant=variant), g * torch.sigmoid(g) * u,
+               atol=2e-2, rtol=3e-2)
+    if variant in (3, 6):  # fused SiLU on the plain [gate; up] weight (the engine's layout)
+        _close(ops.pgemm_silu(x, w, variant=variant), g * torch.sigmoid(g) * u, atol=2e-2, rtol=3e-2)
+
+
+@pytest.mark.parametrize("variant", [3, 4, 5, 6])
+def test_pgemm_v3_schedules_and_silu_std(variant):
+    """Variants 3-5 (4 waves x 128 x 128, the whole K-step register-resident, LDS-DMA two steps
+    ahead) at a 70B-like prefill shape with an odd M, split-K tail on and off, and the fused
+    SiLU on the plain [gate; up] weight (F = 1408: 11 tiles of 128) vs the fp32 reference."""
+    torch.manual_seed(12)
+    M, K = 1030, 4096
+    x = (torch.rand(M, K, device=DEV) * 2 - 1).to(torch.bfloat16)
+    w = ((torch.rand(2816, K, device=DEV) * 2 - 1) * 0.05).to(torch.bfloat16)
+    ref = x.float() @ w.float().t()
+    _close(ops.pgemm(x, w, variant=variant), ref, atol=2e-2, rtol=2e-2)
+    _close(ops.pgemm(x, w, variant=variant, split_k=False), ref, atol=2e-2, rtol=2e-2)
+    g, u = ref[:, :1408], ref[:, 1408:]
+    _close(ops.pgemm_silu(x, w, variant=variant), g * torch.sigmoid(g) * u, atol=2e-2, rtol=3e-2)
 
 
 @pytest.mark.parametrize("Hq,Hkv,D", [(64, 8, 128), (32, 8, 128), (8, 8, 128), (64, 8, 64), (16, 8, 128)])
