@@ -457,7 +457,7 @@ void pgemm(torch::Tensor y, torch::Tensor x, torch::Tensor w, int64_t epi, int64
   const int64_t M = x.size(0), K = x.size(1), N = w.size(0);
   TORCH_CHECK(w.size(1) == K && K % 64 == 0 && N % 256 == 0, "pgemm: N % 256 == 0, K % 64 == 0");
   TORCH_CHECK(y.size(0) == M && y.size(1) == ((epi == 1 || epi == 3) ? N / 2 : N), "pgemm: output shape");
-  TORCH_CHECK(epi != 3 || (variant >= 3 && variant <= 5), "pgemm: epi 3 (SiLU on the [gate; up] weight) needs variant 3-5");
+  TORCH_CHECK(epi != 3 || (variant >= 3 && variant <= 6), "pgemm: epi 3 (SiLU on the [gate; up] weight) needs variant 3-6");
   TORCH_CHECK(x.stride(0) % 8 == 0 && w.stride(0) % 8 == 0 && y.stride(0) % 8 == 0, "pgemm: 16-B row alignment");
   torch::Tensor ws;
   const int64_t wsb = split_k ? llmd_pgemm_ws_bytes((int)M, (int)N, (int)K, (int)epi, (int)variant) : 0;

@@ -31,6 +31,7 @@ from typing import Optional
 import numpy as np
 import torch
 
+from llmd_amd.kvx.agent import p2p_step_guard
 from llmd_amd import ops
 from llmd_amd.models import build_model
 from llmd_amd.parallel.comm import tp_broadcast_plan, tp_min_int
@@ -523,6 +524,13 @@ class ModelRunner:
 
     @torch.no_grad()
     def run_plan(self, pl: dict):
+        # rccl kvx transport: KV sends / recvs are enqueued only between forward passes, so on every
+        # rank the p2p communicator's operations and this step's TP / EP collectives are issued in
+        # one fixed order (kvx/agent.py p2p_step_guard; a no-op without the rccl transport)
+        with p2p_step_guard():
+            return self._run_plan(pl)
+
+    def _run_plan(self, pl: dict):
         rows = pl["rows"]
         if self.lora is not None:
             lo = pl.get("lora") or [0] * len(pl["ids"])

@@ -172,6 +172,28 @@ def stripe_plan(n: int, k: int) -> list[tuple[int, int]]:
     return out
 
 _P2P_GROUP = None  # torch.distributed group spanning prefill + decode engines (rccl transport)
+# Held by the engine thread while it enqueues a forward pass (ModelRunner.run_plan) and by the
+# kvx threads while they enqueue an rccl send / recv: the p2p communicator's operations are
+# issued only between forward passes, never interleaved with a step's TP / EP collectives from
+# another thread, so every rank issues its communicators' operations in one fixed order
+# (two communicators driven from two threads in racing orders can deadlock).
+_P2P_STEP_LOCK = threading.RLock()
+
+
+class _NoGuard:
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        return False
+
+
+_NO_GUARD = _NoGuard()
+
+
+def p2p_step_guard():
+    """Context held around forward-pass enqueue; a no-op unless the rccl transport is set up."""
+    return _P2P_STEP_LOCK if _P2P_GROUP is not None else _NO_GUARD
 
 
 def set_p2p_group(group):
@@ -211,12 +233,13 @@ class _P2PSender:
                     if stream is None:
                         torch.cuda.set_device(a.kv.device)
                         stream = torch.cuda.Stream(device=a.kv.device)
-                    with torch.cuda.stream(stream):
+                    with _P2P_STEP_LOCK, torch.cuda.stream(stream):  # enqueue between forward passes
                         buf = a.pack_blocks(blocks, pool)
                         dist.send(buf, dst=dst, group=_P2P_GROUP)
                     stream.synchronize()
                 else:
-                    dist.send(a.pack_blocks(blocks, pool), dst=dst, group=_P2P_GROUP)
+                    with _P2P_STEP_LOCK:
+                        dist.send(a.pack_blocks(blocks, pool), dst=dst, group=_P2P_GROUP)
             except Exception as e:  # noqa: BLE001 - the decoder's recv fails / times out in turn
                 log.warning("kvx p2p send of %d blocks to rank %d failed: %s", len(blocks), dst, e)
 
@@ -736,14 +759,15 @@ class KvxAgent:
             if not (isinstance(r, dict) and r.get("ok")):
                 raise RuntimeError(f"kvx push refused: {r}")
             if stream is not None:
-                with torch.cuda.stream(stream):
+                with _P2P_STEP_LOCK, torch.cuda.stream(stream):  # enqueue between forward passes
                     buf = torch.empty(n * rbb, dtype=torch.uint8, device=self.kv.device)
                     dist.recv(buf, src=int(rmeta["p2p_rank"]), group=_P2P_GROUP)
                     self._scatter_wire(rmeta, buf.view(n, rbb), lblocks, pool)
                 stream.synchronize()
             else:
                 buf = torch.empty(n * rbb, dtype=torch.uint8)
-                dist.recv(buf, src=int(rmeta["p2p_rank"]), group=_P2P_GROUP)
+                with _P2P_STEP_LOCK:
+                    dist.recv(buf, src=int(rmeta["p2p_rank"]), group=_P2P_GROUP)
                 self._scatter_wire(rmeta, buf.view(n, rbb), lblocks, pool)
 
     # ------------------------------------------------------------ relay (multi-link striping)

@@ -30,6 +30,11 @@ def main():
     ap.add_argument("--weights", default=None)
     ap.add_argument("--dbo-eager", action="store_true", help="drop the captured dual-batch graphs")
     ap.add_argument("--eager", action="store_true", help="no decode graphs at all")
+    ap.add_argument("--backend", default="symm_ll", choices=["symm_ll", "symm_ht"],
+                    help="symm_ht: prefill-sized steps go through the chunked high-throughput exchange")
+    ap.add_argument("--quantization", default=None, choices=[None, "fp8"],
+                    help="fp8: block-fp8 experts, rows quantised to e4m3 in the dispatch kernel (the reference "
+                         "engine is quantised the same way)")
     ap.add_argument("--seed", type=int, default=0, help="seed of the random checkpoint")
     ap.add_argument("--router-scale", type=float, default=8.0,
                     help="scale the router weights of the random checkpoint: with flat routers (random init "
@@ -54,7 +59,8 @@ def main():
     def cfg(**kw):
         return EngineConfig.create(a.model, device="cuda", block_size=64, num_gpu_blocks=96,
                                    max_num_batched_tokens=256, max_num_seqs=8, max_model_len=1024,
-                                   cuda_graph_max_bs=8, load_format="safetensors", weights_path=a.weights, **kw)
+                                   cuda_graph_max_bs=8, load_format="safetensors", weights_path=a.weights,
+                                   quantization=a.quantization, **kw)
 
     if rank == 0 and not os.path.exists(a.weights):
         from llmd_amd.models import build_model
@@ -80,8 +86,10 @@ def main():
         extra.update(enable_eplb=True, eplb_config={"num_redundant_experts": 2 * world, "step_interval": 3})
     if a.eager:
         extra.update(enforce_eager=True)
-    eng = LLMEngine(cfg(data_parallel_size=world, enable_expert_parallel=True, all2all_backend="symm_ll", **extra))
+    eng = LLMEngine(cfg(data_parallel_size=world, enable_expert_parallel=True, all2all_backend=a.backend, **extra))
     assert eng.dp_lockstep and symm.ep() is not None
+    if a.quantization == "fp8":
+        assert symm.ep().fp8, "block-fp8 experts must use the fp8 dispatch kernel"
     if a.dbo_eager:
         eng.runner.dbo_graphs.clear()
     dbo_graphs = sorted(eng.runner.dbo_graphs)

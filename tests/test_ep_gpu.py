@@ -12,8 +12,14 @@ pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-@pytest.mark.parametrize("model,flags,port", [("tiny-gpt-oss", [], 29751),
-                                               ("tiny-deepseek", ["--dbo", "--eplb"], 29752)])
+@pytest.mark.parametrize("model,flags,port", [
+    ("tiny-gpt-oss", [], 29751),
+    ("tiny-deepseek", ["--dbo", "--eplb"], 29752),
+    # the engine path (graphs, DBO) with the chunked HT exchange and with
+    # block-fp8 experts (rows quantised to e4m3 inside the dispatch kernel)
+    ("tiny-deepseek", ["--backend", "symm_ht", "--dbo"], 29753),
+    ("tiny-deepseek", ["--quantization", "fp8", "--dbo"], 29754),
+    ("tiny-gpt-oss", ["--backend", "symm_ht", "--quantization", "fp8"], 29755)])
 def test_wide_ep_symm_gpu(model, flags, port, tmp_path):
     env = dict(os.environ, LLMD_SYMM_DEVICE="0", HSA_ENABLE_IPC_MODE_LEGACY="0")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",

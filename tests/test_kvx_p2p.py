@@ -133,3 +133,31 @@ def test_rccl_transport_needs_group():
     finally:
         p.close()
         d.close()
+
+
+def test_p2p_enqueue_waits_for_forward_pass():
+    """rccl transport: kvx sends / recvs are enqueued only between forward passes
+    (ModelRunner.run_plan holds p2p_step_guard), so each rank issues the p2p
+    communicator's operations and a step's TP / EP collectives in one fixed order."""
+    import threading
+    import time
+
+    from llmd_amd.kvx import agent as A
+
+    old = A.p2p_group()
+    try:
+        A.set_p2p_group(None)
+        assert A.p2p_step_guard() is A._NO_GUARD
+        A.set_p2p_group(object())
+        g = A.p2p_step_guard()
+        order = []
+        with g:  # the engine thread is enqueueing a forward pass
+            t = threading.Thread(target=lambda: (A._P2P_STEP_LOCK.acquire(), order.append("p2p"),
+                                                 A._P2P_STEP_LOCK.release()))
+            t.start()
+            time.sleep(0.05)
+            order.append("forward done")
+        t.join(5)
+        assert order == ["forward done", "p2p"]
+    finally:
+        A.set_p2p_group(old)

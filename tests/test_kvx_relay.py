@@ -42,10 +42,10 @@ def _pool(seed, heads=H):
     return torch.randn(L, NB, PL, heads, BS, D, generator=g).to(torch.bfloat16)
 
 
-def _proc(role, q_out, q_in, heads):
+def _proc(role, q_out, q_in, heads, dev=0):
     os.environ["LLMD_KVX_HEARTBEAT_S"] = "0"
     os.environ["HSA_ENABLE_IPC_MODE_LEGACY"] = "0"
-    torch.cuda.set_device(0)
+    torch.cuda.set_device(dev)
     from llmd_amd.kvx import agent as A
 
     try:
@@ -85,13 +85,19 @@ def _proc(role, q_out, q_in, heads):
         q_out.put((role, f"error: {e!r}"))
 
 
+NGPU = torch.cuda.device_count() if torch.cuda.is_available() else 0
+
+
 @pytest.mark.gpu
 @pytest.mark.timeout(240)
+@pytest.mark.parametrize("devices", [(0, 0, 0), pytest.param((0, 1, 2), marks=pytest.mark.skipif(
+    NGPU < 3, reason="needs 3 GPUs: P, relay and D on their own devices (two-hop xGMI path)"))])
 @pytest.mark.parametrize("heads", [H, H // 2])
-def test_striped_pull_through_relay(heads):
+def test_striped_pull_through_relay(heads, devices):
     ctx = mp.get_context("spawn")
     q_out, qp, qr, qd = ctx.Queue(), ctx.Queue(), ctx.Queue(), ctx.Queue()
-    procs = [ctx.Process(target=_proc, args=(r, q_out, qi, heads)) for r, qi in (("P", qp), ("R", qr), ("D", qd))]
+    procs = [ctx.Process(target=_proc, args=(r, q_out, qi, heads, d))
+             for (r, qi), d in zip((("P", qp), ("R", qr), ("D", qd)), devices)]
     for p in procs:
         p.start()
     try:
