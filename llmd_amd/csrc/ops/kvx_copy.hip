@@ -94,7 +94,7 @@ extern "C" {
 int llmd_kvx_copy_blocks(void* dst, const void* src, int64_t dst_stride, int64_t src_stride, const int* pairs_dev,
                          int npairs, const int64_t* segs_dev, int nseg, int64_t max_seg_bytes, hipStream_t st);
 
-// engine: 0 = register-staged, 1 = LDS-staged (default)
+// engine: 0 = register-staged, 1 = LDS-staged (the Python default, kvx/agent.py COPY_ENGINE)
 int llmd_kvx_copy_blocks2(void* dst, const void* src, int64_t dst_stride, int64_t src_stride, const int* pairs_dev,
                           int npairs, const int64_t* segs_dev, int nseg, int64_t max_seg_bytes, int engine,
                           hipStream_t st) {

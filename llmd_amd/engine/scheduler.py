@@ -33,7 +33,7 @@ from .config import EngineConfig
 from .request import Request, Status
 
 # GEMM alignment may not trim a chunk that finishes its prompt (engine/scheduler._align_tokens)
-KEEP_FINAL_CHUNK = os.environ.get("LLMD_ALIGN_KEEP_FINAL", "0") == "1"
+KEEP_FINAL_CHUNK = os.environ.get("LLMD_ALIGN_KEEP_FINAL", "1") == "1"
 
 
 @dataclass
@@ -382,8 +382,12 @@ class Scheduler:
         ``LLMD_ALIGN_KEEP_FINAL=1`` only chunks that do not finish their prompt
         give tokens up (trimming a FINAL chunk adds a whole extra step for its
         tail: a 5000-token prompt beside 64 decodes becomes 4608- and 518-token
-        steps, 509 + 103 ms); off by default because hipBLASLt runs the unaligned
-        5064-row GEMMs ~20 % slower per token (profiles/gemm_prefill_odd_m.txt). Each
+        steps, 509 + 103 ms). On by default since round 5: the unaligned 5064-row GEMMs
+        that hipBLASLt runs ~20 % slower per token (profiles/gemm_prefill_odd_m.txt) go
+        to the hand-written prefill GEMM through ops/pgemm_table.py (o / down 28-38 %,
+        qkv 11 %, fused gate/up + SiLU 6 % faster than hipBLASLt there,
+        profiles/pgemm_r5_v3_v6_5064.txt), so one 5064-token step replaces the 4608 + 518
+        pair. LLMD_ALIGN_KEEP_FINAL=0 restores trimming final chunks too. Each
         trimmed chunk keeps at least two tokens (a one-token chunk would read as
         a decode); steps below two alignment units, or whose chunks cannot give
         up the whole remainder, run as scheduled. Trimmed tokens go in the next

@@ -95,9 +95,11 @@ import torch
 from llmd_amd.utils import markers
 
 log = logging.getLogger("llmd.kvx")
-# peer-pull copy engine (csrc/ops/kvx_copy.hip): 0 = register-staged (default until the LDS-staged
-# kernel's numerics test has run on the GPU), 1 = LDS-staged through global_load_lds
-COPY_ENGINE = int(os.environ.get("LLMD_KVX_COPY_ENGINE", "0"))
+# block-copy engine (csrc/ops/kvx_copy.hip) of P/D pulls and the offload pack / unpack: 1 =
+# LDS-staged through global_load_lds (default: 8-20 % faster than the register-staged kernel on
+# 16-128-block pulls, TP re-slices and slab packs of 70B blocks, profiles/kvx_copy_engine_ab_r5.txt),
+# 0 = register-staged
+COPY_ENGINE = int(os.environ.get("LLMD_KVX_COPY_ENGINE", "1"))
 
 
 def _send(sock, obj):

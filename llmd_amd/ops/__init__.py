@@ -574,6 +574,9 @@ MOE_V3_MIN_ROWS = int(os.environ.get("LLMD_MOE_V3_MIN_ROWS", "96"))
 MOE_V3 = os.environ.get("LLMD_MOE_V3", "1") == "1"
 # bf16 experts on the same 256-row tiles (moe_gemm3 with bf16 operands); LLMD_MOE_V3_BF16=0 keeps v2
 MOE_V3_BF16 = os.environ.get("LLMD_MOE_V3_BF16", "1") == "1"  # DeepSeek EP8 T=4096 701 -> 789 TF/s, gpt-oss T=5120 369 -> 529
+# bf16 prefill-sized steps on the v4 grouped GEMM (csrc/ops/moe4.hip, the PGR2 structure of the dense
+# prefill GEMM); off until its A/B on the GPU (scripts/bench_moe.py)
+MOE_BF16_V4 = os.environ.get("LLMD_MOE_BF16_V4", "0") == "1"
 MOE_FUSED_QUANT = os.environ.get("LLMD_MOE_FUSED_QUANT", "0") == "1"
 
 
@@ -734,10 +737,15 @@ def moe_experts(x, ids, wts, w1, w2, act=0, alpha=1.702, limit=7.0, out=None, b1
     inv = torch.empty(n, dtype=torch.int32, device=dev)  # moe_align fills it (-1 = not on this rank)
     C.moe_align(ids.contiguous().view(-1), E, sorted_ids, tile_e, offs, total, inv, bm)
     h = torch.empty(max_p, F, dtype=x.dtype, device=dev)
-    C.moe_gemm(x, k, sorted_ids, tile_e, w1, h, 1, act, alpha, limit, False, b1, bm)
     y = torch.empty(max_p, d, dtype=x.dtype, device=dev)
-    # second GEMM: A rows are the sorted slots themselves (row p of h; a_rows_are_slots)
-    C.moe_gemm(h, 1, sorted_ids, tile_e, w2, y, 0, 0, 0.0, 0.0, True, b2, bm)
+    if v3 and MOE_BF16_V4 and K1 % 64 == 0 and F % 64 == 0 and N1 % 16 == 0 and d % 8 == 0:
+        # v4: the dense prefill GEMM's 4-wave PGR2 structure, rows gathered by the LDS-DMA (csrc/ops/moe4.hip)
+        C.moe_gemm4(x, k, sorted_ids, tile_e, w1, h, 1, act, alpha, limit, False, b1)
+        C.moe_gemm4(h, 1, sorted_ids, tile_e, w2, y, 0, 0, 0.0, 0.0, True, b2)
+    else:
+        C.moe_gemm(x, k, sorted_ids, tile_e, w1, h, 1, act, alpha, limit, False, b1, bm)
+        # second GEMM: A rows are the sorted slots themselves (row p of h; a_rows_are_slots)
+        C.moe_gemm(h, 1, sorted_ids, tile_e, w2, y, 0, 0, 0.0, 0.0, True, b2, bm)
     if out is None:
         out = torch.empty(T, d, dtype=x.dtype, device=dev)
     C.moe_combine(y, inv, wts.contiguous().view(-1), k, out)

@@ -420,3 +420,25 @@ def test_moe_experts(T, E, k, d, F, act):
     o2 = ops.moe_experts(x, ids2, w, w1, w2, act, b1=b1, b2=b2)
     r2 = ref.moe_forward(x, ids2, w, w1, w2, act, b1=b1, b2=b2)
     _close(o2, r2, atol=3e-2, rtol=3e-2)
+
+
+@pytest.mark.parametrize("T,E,k,d,F,act", [(1024, 8, 2, 1024, 512, 0), (800, 16, 4, 2880, 2880, 2),
+                                            (2048, 32, 8, 1024, 768, 0)])
+def test_moe_experts_bf16_v4(T, E, k, d, F, act, monkeypatch):
+    """The v4 bf16 grouped GEMM (csrc/ops/moe4.hip: 4-wave PGR2 tiles, A rows gathered by the
+    LDS-DMA, gated activation in registers) vs the fp32 reference, with biases, gpt-oss widths
+    (N = 5760 and 2880: partial last column tiles) and EP-style masked experts."""
+    monkeypatch.setattr(ops, "MOE_BF16_V4", True)
+    torch.manual_seed(13)
+    x = torch.randn(T, d, device=DEV, dtype=torch.bfloat16)
+    w1 = (torch.randn(E, 2 * F, d, device=DEV) * d ** -0.5).to(torch.bfloat16)
+    w2 = (torch.randn(E, d, F, device=DEV) * F ** -0.5).to(torch.bfloat16)
+    b1 = (torch.randn(E, 2 * F, device=DEV) * 0.1).to(torch.bfloat16)
+    b2 = (torch.randn(E, d, device=DEV) * 0.1).to(torch.bfloat16)
+    ids, w = ops.moe_topk(torch.randn(T, E, device=DEV), k, 2)
+    _close(ops.moe_experts(x, ids, w, w1, w2, act, b1=b1, b2=b2),
+           ref.moe_forward(x, ids, w, w1, w2, act, b1=b1, b2=b2), atol=3e-2, rtol=3e-2)
+    ids2 = ids.clone()
+    ids2[ids2 >= E // 2] = -1
+    _close(ops.moe_experts(x, ids2, w, w1, w2, act), ref.moe_forward(x, ids2, w, w1, w2, act),
+           atol=3e-2, rtol=3e-2)
