@@ -225,6 +225,248 @@ __global__ __launch_bounds__(M4_NT, 1) void moe_gemm4_bf16_kernel(
   }
 }
 
+// ---------------------------------------------------------------------------
+// Block-scaled fp8 form (DeepGEMM role): e4m3 X [rows, Kp] with power-of-two
+// per-(row, 128) scales xs, e4m3 W [E, N, Kp] with per-(128 x 128) scales ws
+// [E, N / 128, Kp / 128]; v_mfma_scale_f32_32x32x64_f8f6f4 applies both as
+// E8M0 exponents in hardware. A 64 KB K-step holds 128 fp8 of every row (the
+// same 256 x 128-B images as the bf16 form), computed as 2 k-substeps of 4 x 4
+// 32 x 32 x 64 MFMA per wave (64 cycles each: the step's 2048 MFMA cycles, with
+// twice the bf16 FLOPs). The product is C^T (W fragments as the MFMA's A
+// operand): the weight scale is one value per wave and K-step, the activation
+// scale travels per lane (its token column), and a lane's accumulator holds 4
+// consecutive N columns (one (g, u) pair per two). Activation scales ride the
+// LDS-DMA (one 4-B piece per wave per step: 17 pieces, counted vmcnt(17)); the
+// tile's weight scales are DMA'd once in the prologue.
+constexpr int M8_S = 256 * 4;                        // act scales of one K-step
+constexpr int M8_BUF = 2 * M4_OPB + M8_S;            // 66560 B
+constexpr int M8_WS = 2 * M8_BUF;                    // weight scales [2 col blocks][64 k-blocks]
+constexpr int M8_LDS = M8_WS + 2 * 64 * 4;
+
+typedef int i32x8_t __attribute__((ext_vector_type(8)));
+typedef float f32x16_t __attribute__((ext_vector_type(16)));
+
+__device__ __forceinline__ void m8_mfma(f32x16_t& acc, const i32x8_t& a, const i32x8_t& b, int sa, int sb) {
+  asm volatile("v_mfma_scale_f32_32x32x64_f8f6f4 %0, %1, %2, %0, %3, %4 op_sel_hi:[0,0,0]"
+               : "+a"(acc) : "v"(a), "v"(b), "v"(sa), "v"(sb));
+}
+
+template <int MODE>
+__global__ __launch_bounds__(M4_NT, 1) void moe_gemm4_fp8_kernel(
+    const uint8_t* __restrict__ X, int64_t x_stride, const float* __restrict__ xs, int64_t xs_stride, int topk,
+    const int* __restrict__ sorted_ids, const int* __restrict__ tile_expert, const uint8_t* __restrict__ W,
+    int64_t w_expert_stride, const float* __restrict__ ws, int N, int K, uint16_t* __restrict__ Y,
+    int64_t y_stride, int act, float alpha, float limit, int a_rows_are_slots, const uint16_t* __restrict__ bias) {
+  __shared__ __attribute__((aligned(1024))) char lds[M8_LDS];  // the ONLY LDS object
+  const int nt_ = blockIdx.x, mt = blockIdx.y;
+  const int e = tile_expert[mt];
+  if (e < 0) return;
+  const int m0 = mt * M4_BM, n0 = nt_ * M4_BN;
+  const int nk = K / 128, nnb = (N + 127) / 128;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = w >> 1, wc = w & 1;
+  const int l32 = lane & 31, h = lane >> 5;
+
+  const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc((void*)X, 0, 0x7fffffff, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)xs, 0, 0x7fffffff, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(W + (int64_t)e * w_expert_stride), 0, 0x7fffffff, 0x00020000);
+  uint32_t va[8], vw[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int row = 64 * w + 8 * j + (lane >> 3);
+    const int c = (lane & 7) ^ ((row >> 1) & 7);
+    const int sid = sorted_ids[m0 + row];
+    const int tok = sid < 0 ? 0 : (a_rows_are_slots ? m0 + row : sid / topk);
+    va[j] = (uint32_t)((int64_t)tok * x_stride + c * 16);
+    vw[j] = (uint32_t)((int64_t)min(n0 + row, N - 1) * K + c * 16);
+  }
+  uint32_t vs;  // this lane's act-scale row 64 w + lane
+  {
+    const int row = 64 * w + lane;
+    const int sid = sorted_ids[m0 + row];
+    const int tok = sid < 0 ? 0 : (a_rows_are_slots ? m0 + row : sid / topk);
+    vs = (uint32_t)((int64_t)tok * xs_stride * 4);
+  }
+  auto dma = [&](int kt, int j, int op) {  // op 0 = A piece j, 1 = W piece j, 2 = act scales
+    const int kc = min(kt, nk - 1);
+    char* buf = lds + (kt & 1) * M8_BUF;
+    if (op == 2)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)(buf + 2 * M4_OPB + w * 256),
+                                               4, vs, (uint32_t)(kc * 4), 0, 0);
+    else
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(op ? rw : ra,
+                                               (__attribute__((address_space(3))) void*)(buf + op * M4_OPB + (8 * w + j) * 1024),
+                                               16, op ? vw[j] : va[j], (uint32_t)(kc * 128), 0, 0);
+  };
+  // fragment of 32-row block b, k-substep s: lane row 32 b + l32, chunks 4 s + 2 h and 4 s + 2 h + 1
+  auto frag = [&](const char* base, int b, int s) {
+    const int row = 32 * b + l32;
+    const int f = (row >> 1) & 7;
+    const char* rp = base + row * 128;
+    const u32x4_t lo = *reinterpret_cast<const u32x4_t*>(rp + (((4 * s + 2 * h) ^ f) * 16));
+    const u32x4_t hi = *reinterpret_cast<const u32x4_t*>(rp + (((4 * s + 2 * h + 1) ^ f) * 16));
+    return i32x8_t{(int)lo[0], (int)lo[1], (int)lo[2], (int)lo[3], (int)hi[0], (int)hi[1], (int)hi[2], (int)hi[3]};
+  };
+  const int a_base = wr * 128 * 128, w_base = M4_OPB + wc * 128 * 128;
+
+  f32x16_t acc[4][4];  // [W n-block j][A m-block i]
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) acc[j][i] = f32x16_t{};
+  i32x8_t fw0[4], fa0[4], fw1[4], fa1[4];
+  int sa[4];  // E8M0 act scales of this lane's token column in each m-block (current step)
+  int swt;    // E8M0 weight scale of this wave's 128-column block (current step)
+  float nsf[4], nwf;  // the next step's raw scales
+
+  // prologue: the tile's weight scales (waves 0 / 1: column blocks n0 / 128 + 0 / 1), steps 0 and 1
+  if (w < 2) {
+    const int cb = min(n0 / 128 + w, nnb - 1);
+    const __amdgpu_buffer_rsrc_t rws = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(ws + ((int64_t)e * nnb + cb) * nk), 0, 0x7fffffff, 0x00020000);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rws, (__attribute__((address_space(3))) void*)(lds + M8_WS + w * 256), 4,
+                                             (uint32_t)(min(lane, nk - 1) * 4), 0, 0, 0);
+  }
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) dma(s, j, 0);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) dma(s, j, 1);
+    dma(s, 0, 2);
+  }
+  asm volatile("s_waitcnt vmcnt(17)" ::: "memory");  // step 0 (and the weight scales) landed
+  m4_bar();
+#pragma unroll
+  for (int b = 0; b < 4; ++b) {
+    fw0[b] = frag(lds + w_base, b, 0);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+#pragma unroll
+  for (int b = 0; b < 4; ++b) {
+    fa0[b] = frag(lds + a_base, b, 0);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+#pragma unroll
+  for (int b = 0; b < 4; ++b)
+    sa[b] = e8m0_of(*reinterpret_cast<const float*>(lds + 2 * M4_OPB + (wr * 128 + 32 * b + l32) * 4));
+  swt = e8m0_of(*reinterpret_cast<const float*>(lds + M8_WS + wc * 256));
+  __builtin_amdgcn_s_waitcnt(0xC07F);
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_nop 4" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+
+  for (int kt = 0; kt < nk; ++kt) {
+    const char* cur = lds + (kt & 1) * M8_BUF;
+    const char* nxt = lds + ((kt & 1) ^ 1) * M8_BUF;
+    // half 0 (k-substep 0): 16 MFMA; reads of substep 1 (W then A, 2 ds_read_b128 per fragment) after
+    // MFMA 0-7; barrier after MFMA 9; A pieces + the act-scale piece of step kt + 2 after MFMA 10-15
+#pragma unroll
+    for (int t = 0; t < 16; ++t) {
+      const int j = t >> 2, i = t & 3;
+      m8_mfma(acc[j][i], fw0[j], fa0[i], swt, sa[i]);
+      if (t < 4) {
+        fw1[t] = frag(cur + w_base, t, 1);
+      } else if (t < 8) {
+        fa1[t - 4] = frag(cur + a_base, t - 4, 1);
+      } else if (t == 9) {
+        __builtin_amdgcn_s_waitcnt(0xC07F);
+        m4_bar();
+      } else if (t >= 10 && t < 14) {  // A pieces 0-7, two per MFMA gap (64-cycle MFMAs)
+        dma(kt + 2, 2 * (t - 10), 0);
+        dma(kt + 2, 2 * (t - 10) + 1, 0);
+      } else if (t == 14) {
+        dma(kt + 2, 0, 2);  // the act-scale piece: 17 DMA per wave per step
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    // half 1 (k-substep 1): W pieces after MFMA 0-7; step kt+1 landed (vmcnt 17) + barrier after
+    // MFMA 8; its substep-0 fragments and scales after MFMA 9-15
+#pragma unroll
+    for (int t = 0; t < 16; ++t) {
+      const int j = t >> 2, i = t & 3;
+      m8_mfma(acc[j][i], fw1[j], fa1[i], swt, sa[i]);
+      if (t < 8) {
+        dma(kt + 2, t, 1);
+      } else if (t == 8) {
+        asm volatile("s_waitcnt vmcnt(17)" ::: "memory");
+        m4_bar();
+      } else if (t < 13) {
+        if (t == 9) {  // the next step's raw scales, early (converted after the last MFMA)
+#pragma unroll
+          for (int b = 0; b < 4; ++b)
+            nsf[b] = *reinterpret_cast<const float*>(nxt + 2 * M4_OPB + (wr * 128 + 32 * b + l32) * 4);
+          nwf = *reinterpret_cast<const float*>(lds + M8_WS + wc * 256 + min(kt + 1, nk - 1) * 4);
+        }
+        fw0[t - 9] = frag(nxt + w_base, t - 9, 0);
+      } else if (t < 15) {
+        fa0[2 * (t - 13)] = frag(nxt + a_base, 2 * (t - 13), 0);
+        fa0[2 * (t - 13) + 1] = frag(nxt + a_base, 2 * (t - 13) + 1, 0);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    // the next step's scales (swapped in after this step's last MFMA used the current ones)
+#pragma unroll
+    for (int b = 0; b < 4; ++b) sa[b] = e8m0_of(nsf[b]);
+    swt = e8m0_of(nwf);
+  }
+  asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  __syncthreads();
+
+  // epilogue: acc[j][i][4 g + q] = C[m][n], m = wr*128 + 32 i + l32, n = wc*128 + 32 j + 8 g + 4 h + q
+  char* img = lds + w * 32768;
+  const int ncol0 = n0 + wc * 128;
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int row = 32 * i + l32, col = 32 * j + 8 * g + 4 * h;
+        float v[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          v[q] = acc[j][i][4 * g + q];
+          if (bias != nullptr) v[q] += bf2f(bias[(int64_t)e * N + min(ncol0 + col + q, N - 1)]);
+        }
+        if constexpr (MODE == 0) {
+          u32x2_t p;
+          p[0] = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
+          p[1] = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
+          *reinterpret_cast<u32x2_t*>(img + row * 256 + (((col >> 3) ^ (row & 15)) * 16) + (col & 7) * 2) = p;
+        } else {
+          const float o0 = m4_act(v[0], v[1], act, alpha, limit), o1 = m4_act(v[2], v[3], act, alpha, limit);
+          const uint32_t p = (uint32_t)f2bf(o0) | ((uint32_t)f2bf(o1) << 16);
+          const int hc = col >> 1;
+          *reinterpret_cast<uint32_t*>(img + row * 128 + (((hc >> 3) ^ (row & 7)) * 16) + (hc & 7) * 2) = p;
+        }
+      }
+  __syncthreads();
+  if constexpr (MODE == 0) {
+#pragma unroll 4
+    for (int it = 0; it < 32; ++it) {
+      const int row = it * 4 + (lane >> 4), c = lane & 15;
+      const int p = m0 + wr * 128 + row;
+      const int n = ncol0 + c * 8;
+      const u32x4_t v = *reinterpret_cast<const u32x4_t*>(img + row * 256 + ((c ^ (row & 15)) * 16));
+      if (sorted_ids[p] >= 0 && n < N) *reinterpret_cast<u32x4_t*>(Y + (int64_t)p * y_stride + n) = v;
+    }
+  } else {
+#pragma unroll 4
+    for (int it = 0; it < 16; ++it) {
+      const int row = it * 8 + (lane >> 3), c = lane & 7;
+      const int p = m0 + wr * 128 + row;
+      const int n = ncol0 / 2 + c * 8;
+      const u32x4_t v = *reinterpret_cast<const u32x4_t*>(img + row * 128 + ((c ^ (row & 7)) * 16));
+      if (sorted_ids[p] >= 0 && 2 * n < N) *reinterpret_cast<u32x4_t*>(Y + (int64_t)p * y_stride + n) = v;
+    }
+  }
+}
+
 }  // namespace
 
 extern "C" int llmd_moe_gemm4_bf16(const void* X, int64_t x_stride, int topk, const int* sorted_ids,
@@ -245,5 +487,27 @@ extern "C" int llmd_moe_gemm4_bf16(const void* X, int64_t x_stride, int topk, co
     hipLaunchKernelGGL(moe_gemm4_bf16_kernel<1>, grid, dim3(M4_NT), 0, st, (const uint16_t*)X, x_stride, topk,
                        sorted_ids, tile_expert, (const uint16_t*)W, w_expert_stride, N, K, (uint16_t*)Y, y_stride, act,
                        alpha, limit, a_rows_are_slots, (const uint16_t*)bias);
+  return (int)hipGetLastError();
+}
+
+extern "C" int llmd_moe_gemm4_fp8(const void* X, int64_t x_stride, const float* xs, int64_t xs_stride, int topk,
+                                  const int* sorted_ids, const int* tile_expert, int num_tiles, const void* W,
+                                  int64_t w_expert_stride, const float* ws, int N, int K, void* Y, int64_t y_stride,
+                                  int mode, int act, float alpha, float limit, int a_rows_are_slots, const void* bias,
+                                  int64_t x_rows, hipStream_t st) {
+  // K: Kp (padded to 128), at most 64 k-blocks (the weight-scale row of a tile is one 64-lane DMA)
+  if (K % 128 || K / 128 > 64 || x_stride % 16 || w_expert_stride % 16 || N % 8 || (mode == 1 && N % 16)) return -1;
+  if (x_rows * x_stride + K > 0x7fffffffLL || (int64_t)N * K > 0x7fffffffLL || x_rows * xs_stride * 4 > 0x7fffffffLL)
+    return -2;
+  if (num_tiles == 0) return 0;
+  dim3 grid((N + M4_BN - 1) / M4_BN, num_tiles);
+  if (mode == 0)
+    hipLaunchKernelGGL(moe_gemm4_fp8_kernel<0>, grid, dim3(M4_NT), 0, st, (const uint8_t*)X, x_stride, xs, xs_stride,
+                       topk, sorted_ids, tile_expert, (const uint8_t*)W, w_expert_stride, ws, N, K, (uint16_t*)Y,
+                       y_stride, act, alpha, limit, a_rows_are_slots, (const uint16_t*)bias);
+  else
+    hipLaunchKernelGGL(moe_gemm4_fp8_kernel<1>, grid, dim3(M4_NT), 0, st, (const uint8_t*)X, x_stride, xs, xs_stride,
+                       topk, sorted_ids, tile_expert, (const uint8_t*)W, w_expert_stride, ws, N, K, (uint16_t*)Y,
+                       y_stride, act, alpha, limit, a_rows_are_slots, (const uint16_t*)bias);
   return (int)hipGetLastError();
 }

@@ -578,6 +578,9 @@ MOE_V3_BF16 = os.environ.get("LLMD_MOE_V3_BF16", "1") == "1"  # DeepSeek EP8 T=4
 # prefill GEMM); off until its A/B on the GPU (scripts/bench_moe.py)
 MOE_BF16_V4 = os.environ.get("LLMD_MOE_BF16_V4", "0") == "1"
 MOE_FUSED_QUANT = os.environ.get("LLMD_MOE_FUSED_QUANT", "0") == "1"
+# block-fp8 prefill-sized steps on the v4 grouped GEMM (moe4.hip moe_gemm4_fp8_kernel: 4-wave PGR2,
+# scaled 32x32x64 MFMA with the E8M0 block scales as operands); off until its A/B (scripts/bench_moe.py)
+MOE_FP8_V4 = os.environ.get("LLMD_MOE_FP8_V4", "0") == "1"
 
 
 class Fp8Rows:
@@ -653,6 +656,18 @@ def moe_experts_fp8(x, ids, wts, w1q, w1s, w2q, w2s, act=0, alpha=1.702, limit=7
         hs = torch.empty(max_p, Kp2 // 128, dtype=torch.float32, device=dev)
         C.moe_gemm_fp8(xq, xs, k, sorted_ids, tile_e, w1q, w1s, torch.empty(0, F, dtype=torch.bfloat16, device=dev),
                        1, act, alpha, limit, False, b1, bm, hq, hs)
+    elif bm == C.moe_tile_m_prefill() and MOE_FP8_V4 and Kp1 <= 8192 and Kp2 <= 8192 and N1 % 16 == 0 \
+            and d % 8 == 0:
+        # v4: PGR2 4-wave tiles, A rows and their act scales gathered by the LDS-DMA (csrc/ops/moe4.hip)
+        h = torch.empty(max_p, F, dtype=torch.bfloat16, device=dev)
+        C.moe_gemm4_fp8(xq, xs, k, sorted_ids, tile_e, w1q, w1s, h, 1, act, alpha, limit, False, b1)
+        hq, hs = _quant_groups_padded(h, Kp2)
+        y = torch.empty(max_p, d, dtype=torch.bfloat16, device=dev)
+        C.moe_gemm4_fp8(hq, hs, 1, sorted_ids, tile_e, w2q, w2s, y, 0, 0, 0.0, 0.0, True, b2)
+        if out is None:
+            out = torch.empty(T, d, dtype=torch.bfloat16, device=dev)
+        C.moe_combine(y, inv, wts.contiguous().view(-1).float(), k, out)
+        return out
     else:
         h = torch.empty(max_p, F, dtype=torch.bfloat16, device=dev)
         C.moe_gemm_fp8(xq, xs, k, sorted_ids, tile_e, w1q, w1s, h, 1, act, alpha, limit, False, b1, bm)

@@ -276,6 +276,44 @@ def test_moe_fp8_prefill_tiles_gpu(T, E, k, d, F, act, skew, monkeypatch):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("T,E,k,d,F,act,skew", [(512, 4, 4, 1024, 1024, 2, False), (600, 16, 8, 1024, 256, 0, True),
+                                                (800, 16, 4, 2880, 2880, 2, False), (300, 8, 8, 7168, 2048, 0, True),
+                                                (5, 8, 2, 256, 128, 0, False)])
+def test_moe_fp8_v4_gpu(T, E, k, d, F, act, skew, monkeypatch):
+    """The v4 block-fp8 grouped GEMM (csrc/ops/moe4.hip moe_gemm4_fp8_kernel: 4-wave PGR2 tiles,
+    A rows and their act scales gathered by the LDS-DMA, scaled 32x32x64 MFMA) vs the v3 256-row
+    kernel and the CPU reference: gpt-oss widths (partial column tiles), K = 7168 (56 k-blocks),
+    empty and multi-tile experts, biases."""
+    torch.manual_seed(3)
+    dev = "cuda"
+    c128 = lambda n: (n + 127) // 128 * 128  # noqa: E731
+    x = torch.randn(T, d, device=dev, dtype=torch.bfloat16)
+    w1q, w1s = ops.quant_fp8_block_weight(torch.randn(E, 2 * F, d, device=dev, dtype=torch.bfloat16) * 0.03)
+    w2q, w2s = ops.quant_fp8_block_weight(torch.randn(E, d, F, device=dev, dtype=torch.bfloat16) * 0.03)
+    b1 = torch.randn(E, 2 * F, device=dev, dtype=torch.bfloat16) * 0.1
+    b2 = torch.randn(E, d, device=dev, dtype=torch.bfloat16) * 0.1
+    w1q, w2q = ops.pad_fp8_k(w1q, c128(d)), ops.pad_fp8_k(w2q, c128(F))
+    logits = torch.randn(T, E, device=dev)
+    if skew:
+        logits[:, : E // 4] += 2.0
+        logits[:, -2:] -= 8.0
+    ids, wts = ops.moe_topk(logits, k, scoring=0)
+    monkeypatch.setattr(ops, "MOE_V3", True)
+    monkeypatch.setattr(ops, "MOE_V3_MIN_ROWS", 0)
+    monkeypatch.setattr(ops, "MOE_FUSED_QUANT", False)
+    monkeypatch.setattr(ops, "MOE_FP8_V4", False)
+    y3 = ops.moe_experts_fp8(x, ids, wts, w1q, w1s, w2q, w2s, act, b1=b1, b2=b2)
+    monkeypatch.setattr(ops, "MOE_FP8_V4", True)
+    y4 = ops.moe_experts_fp8(x, ids, wts, w1q, w1s, w2q, w2s, act, b1=b1, b2=b2)
+    r = ops.moe_experts_fp8(x.cpu(), ids.cpu(), wts.cpu(), w1q.cpu()[..., :d], w1s.cpu(), w2q.cpu()[..., :F],
+                            w2s.cpu(), act, b1=b1.cpu(), b2=b2.cpu())
+    m = r.float().abs().max().item()
+    assert torch.isfinite(y4).all()
+    assert (y4.float().cpu() - r.float()).abs().max().item() < 0.06 * m + 1e-3
+    assert (y4.float() - y3.float()).abs().max().item() < 0.02 * m + 1e-3
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("T,E,k,d,F,act", [(700, 16, 4, 512, 2880, 2), (300, 8, 8, 256, 256, 0)])
 def test_moe_fp8_fused_act_quant_gpu(T, E, k, d, F, act):
     """The 256-row first GEMM's fused epilogue quantisation (hq / hs) is bit
