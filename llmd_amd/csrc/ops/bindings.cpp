@@ -10,6 +10,7 @@
 #include <pybind11/stl.h>
 
 #include <map>
+#include <mutex>
 #include <memory>
 #include <vector>
 
@@ -55,13 +56,14 @@ int llmd_skinny_gemm(const void*, int64_t, const void*, int64_t, int, int, int, 
                      float*, hipStream_t);
 int llmd_dgemm_supported(int, int, int);
 int llmd_mgemm(const void*, int64_t, const void*, int64_t, int, int, int, int, int, int, void*, int64_t, float*,
-               hipStream_t);
+               int*, hipStream_t);
 int llmd_mgemm_lds(int, int, int);
+int llmd_mgemm_silu(const void*, int64_t, const void*, int64_t, int, int, int, int, int, void*, int64_t, hipStream_t);
 int llmd_pgemm(const void*, int64_t, const void*, int64_t, void*, int64_t, int, int, int, int, int, void*,
                hipStream_t);
 int64_t llmd_pgemm_ws_bytes(int, int, int, int, int);
 int llmd_mgemm_fp8(const void*, int64_t, const float*, const void*, int64_t, const float*, int, int, int, int, int,
-                   int, void*, int64_t, float*, hipStream_t);
+                   int, void*, int64_t, float*, int*, hipStream_t);
 int llmd_vmm_granularity(int, size_t*);
 int llmd_vmm_alloc(int, size_t, int, void**, uint64_t*);
 int llmd_vmm_export_fd(uint64_t, int*);
@@ -429,6 +431,30 @@ bool skinny_supported(int64_t M, int64_t rb, int64_t occ) { return llmd_dgemm_su
 // y [M, N] = x [M, K] . w [N, K]^T for 33 <= M <= 128 (decode batches of a P/D
 // decode replica): LDS-DMA staged tiles of 64 wrb W rows x all M, nsplit-way
 // split-K, 3- or 4-stage ring (csrc/ops/mgemm.hip)
+// Split-K fixup counters of mgemm (csrc/ops/mgemm.hip): per device 256 slabs of 1024 zeroed ints, handed
+// out round-robin so kernels in flight on different streams (DBO, TP overlap) never share a slab; each
+// launch leaves its slab zeroed. Created outside stream capture (a capture before the first eager call
+// falls back to the reduce kernel); LLMD_MGEMM_FIXUP=0 keeps the reduce kernel.
+int* mgemm_counters(const torch::Device& d, int64_t tiles) {
+  static const bool on = [] {
+    const char* e = getenv("LLMD_MGEMM_FIXUP");
+    return !(e && e[0] == '0');
+  }();
+  if (!on || tiles > 1024) return nullptr;
+  static std::mutex mu;
+  static std::map<int, torch::Tensor> pools;
+  static std::map<int, uint32_t> next;
+  std::lock_guard<std::mutex> g(mu);
+  auto& t = pools[d.index()];
+  if (!t.defined()) {
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(cur_stream(), &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return nullptr;
+    t = torch::zeros({256 * 1024}, torch::dtype(torch::kInt32).device(d));
+  }
+  const uint32_t i = next[d.index()]++ % 256;
+  return t.data_ptr<int>() + (int64_t)i * 1024;
+}
+
 void mgemm(torch::Tensor y, torch::Tensor x, torch::Tensor w, int64_t wrb, int64_t nsplit, int64_t stages,
            torch::Tensor part) {
   const c10::hip::OptionalHIPGuard device_guard(dev_of(y));
@@ -445,6 +471,7 @@ void mgemm(torch::Tensor y, torch::Tensor x, torch::Tensor w, int64_t wrb, int64
   }
   int rc = llmd_mgemm(x.data_ptr(), x.stride(0), w.data_ptr(), w.stride(0), M, N, K, (int)wrb, (int)nsplit,
                       (int)stages, y.data_ptr(), y.stride(0), nsplit > 1 ? part.data_ptr<float>() : nullptr,
+                      nsplit > 1 ? mgemm_counters(y.device(), (N + 64 * wrb - 1) / (64 * wrb)) : nullptr,
                       cur_stream());
   TORCH_CHECK(rc == 0, "mgemm failed: ", rc);
 }
@@ -472,6 +499,19 @@ void pgemm(torch::Tensor y, torch::Tensor x, torch::Tensor w, int64_t epi, int64
   TORCH_CHECK(rc == 0, "pgemm failed: ", rc);
 }
 
+// y [M, F] = silu(x wg^T) * (x wu^T), w = [gate; up] [2F, K] (mgemm ACT form, whole K per workgroup)
+void mgemm_silu(torch::Tensor y, torch::Tensor x, torch::Tensor w, int64_t wrb, int64_t stages) {
+  const c10::hip::OptionalHIPGuard device_guard(dev_of(y));
+  CHECK_CUDA(x); CHECK_BF16(x); CHECK_BF16(w); CHECK_BF16(y); CHECK_INNER(x); CHECK_INNER(w); CHECK_INNER(y);
+  TORCH_CHECK(x.dim() == 2 && w.dim() == 2 && y.dim() == 2, "mgemm_silu: 2-D operands");
+  const int M = x.size(0), K = x.size(1), N = w.size(0);
+  TORCH_CHECK(M >= 1 && M <= 128 && w.size(1) == K && K % 64 == 0 && N % 8 == 0, "mgemm_silu: shapes");
+  TORCH_CHECK(y.size(0) == M && y.size(1) == N / 2, "mgemm_silu: y [M, N / 2]");
+  int rc = llmd_mgemm_silu(x.data_ptr(), x.stride(0), w.data_ptr(), w.stride(0), M, N, K, (int)wrb, (int)stages,
+                           y.data_ptr(), y.stride(0), cur_stream());
+  TORCH_CHECK(rc == 0, "mgemm_silu failed: ", rc);
+}
+
 // fp8 W8A8 form: xq [M, K] e4m3fn with per-token scales xs [M, 1], wq [N, K] e4m3fn with
 // per-channel scales ws [1, N] (ops.fp8_linear's operands); K % 128 == 0
 void mgemm_fp8(torch::Tensor y, torch::Tensor xq, torch::Tensor xs, torch::Tensor wq, torch::Tensor ws, int64_t wrb,
@@ -494,7 +534,9 @@ void mgemm_fp8(torch::Tensor y, torch::Tensor xq, torch::Tensor xs, torch::Tenso
   }
   int rc = llmd_mgemm_fp8(xq.data_ptr(), xq.stride(0), xs.data_ptr<float>(), wq.data_ptr(), wq.stride(0),
                           ws.data_ptr<float>(), M, N, K, (int)wrb, (int)nsplit, (int)stages, y.data_ptr(), y.stride(0),
-                          nsplit > 1 ? part.data_ptr<float>() : nullptr, cur_stream());
+                          nsplit > 1 ? part.data_ptr<float>() : nullptr,
+                          nsplit > 1 ? mgemm_counters(y.device(), (N + 64 * wrb - 1) / (64 * wrb)) : nullptr,
+                          cur_stream());
   TORCH_CHECK(rc == 0, "mgemm_fp8 failed: ", rc);
 }
 
@@ -1060,6 +1102,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {  // _C, or _C_debug (llmd_amd/build.p
   m.def("moe_tile_m_prefill", &llmd_moe_gemm3_tile_m);
   m.def("symm_alloc", &symm_alloc);
   m.def("moe_gemm4", &moe_gemm4);
+  m.def("mgemm_silu", &mgemm_silu);
   m.def("moe_gemm4_fp8", &moe_gemm4_fp8);
   m.def("symm_error", &symm_error);
   m.def("symm_host_err", &symm_host_err);

@@ -22,7 +22,9 @@
 // (swizzle applied on the DMA source address; destination stays lane-linear):
 // the 16 lanes of a ds_read_b128 pass (16 rows, one k chunk) hit 16 distinct
 // slots of the 256-B bank row.
-// Split-K partials: fp32 [split][M][N], summed and rounded by mgemm_reduce_kernel.
+// Split-K partials: fp32 [split][M][N], summed and rounded in the kernel by the last split of
+// each column tile to finish (an atomic counter per tile; LLMD_MGEMM_FIXUP=0: by
+// mgemm_reduce_kernel, one more launch and one more pass over the partials).
 //
 // fp8 (W8A8, e4m3fn, F8 = true): the same 128-B image rows hold 128 k per step;
 // a lane's 16-B fragment feeds two mfma_f32_16x16x32_fp8_fp8 (its low and high
@@ -53,12 +55,17 @@ struct Geo {
   static_assert(BM % 32 == 0, "MB must be even");
 };
 
-template <int MB, int WRB, int S, bool F8 = false, int POL = 0>
+// ACT: gate/up GEMM with the SiLU-and-mul in the epilogue on the plain [gate; up] weight
+// (N = 2F rows): a wave's 16 WRB image rows are F-rows f0 .. f0 + 8 WRB - 1 of gate
+// (rb < WRB / 2) then the same F-rows of up, so acc[rb] and acc[rb + WRB / 2] pair
+// lane-locally; Y [M, F]; whole-K tiles only (nsplit 1).
+template <int MB, int WRB, int S, bool F8 = false, int POL = 0, bool ACT = false>
 __global__ __launch_bounds__(NT, 1) void mgemm_kernel(const void* __restrict__ xv, int64_t x_stride,
                                                       const void* __restrict__ wv_, int64_t w_stride, int M,
                                                       int N, int K, int steps_per_split, uint16_t* __restrict__ y,
                                                       int64_t y_stride, float* __restrict__ part,
-                                                      const float* __restrict__ xs, const float* __restrict__ wsc) {
+                                                      const float* __restrict__ xs, const float* __restrict__ wsc,
+                                                      int* __restrict__ cnt) {
   using G = Geo<MB, WRB, S>;
   using E = typename std::conditional<F8, uint8_t, uint16_t>::type;
   constexpr int CE = 16 / sizeof(E);  // elements per 16-B chunk
@@ -85,15 +92,23 @@ __global__ __launch_bounds__(NT, 1) void mgemm_kernel(const void* __restrict__ x
 #pragma unroll
   for (int i = 0; i < G::NW; ++i) {
     const int r = 8 * (ws + 4 * i) + (lane >> 3);
-    const int gr = min(row0 + r, N - 1);  // rows past N re-read the last row (result dropped)
-    woff[i] = (uint32_t)((int64_t)(gr - row0) * w_stride + CE * ((lane & 7) ^ msw(r)));
+    int gr;
+    if constexpr (ACT) {
+      constexpr int HB = 8 * WRB;  // half of a wave's rows
+      const int q = r / (2 * HB), j = r % (2 * HB), F = N / 2;
+      const int f = min(row0 / 2 + HB * q + (j < HB ? j : j - HB), F - 1);  // past F: dropped
+      gr = (j < HB ? 0 : F) + f;
+    } else {
+      gr = min(row0 + r, N - 1);  // rows past N re-read the last row (result dropped)
+    }
+    woff[i] = (uint32_t)((int64_t)(ACT ? gr : gr - row0) * w_stride + CE * ((lane & 7) ^ msw(r)));
   }
 #pragma unroll
   for (int i = 0; i < G::NX; ++i) {
     const int r = 8 * (ws + 4 * i) + (lane >> 3);
     xoff[i] = (uint32_t)((int64_t)min(r, M - 1) * x_stride + CE * ((lane & 7) ^ msw(r)));
   }
-  const E* wbase = wt + (int64_t)row0 * w_stride;
+  const E* wbase = ACT ? wt : wt + (int64_t)row0 * w_stride;
   // each tile starts its K sweep at a rotated step so concurrent workgroups do
   // not stream the same k columns of W at once (DRAM channel spread)
   const int rot = nsteps > 0 ? (tile * 5) % nsteps : 0;
@@ -239,6 +254,28 @@ __global__ __launch_bounds__(NT, 1) void mgemm_kernel(const void* __restrict__ x
 #undef MG_LGKM0
 
   // acc[rb][mb][i] = Y^T[row0 + 16 (WRB wv + rb) + 4 g + i][16 mb + c16]
+  if constexpr (ACT) {
+    constexpr int HW = WRB / 2;
+    const int F = N / 2;
+#pragma unroll
+    for (int mb = 0; mb < MB; ++mb) {
+      const int m = 16 * mb + c16;
+      if (m >= M) continue;
+#pragma unroll
+      for (int rb = 0; rb < HW; ++rb) {
+        const int f = row0 / 2 + 8 * WRB * wv + 16 * rb + 4 * g;
+        if (f >= F) continue;  // F % 4 == 0 (host check)
+        const f32x4_t gt = acc[rb][mb], up = acc[rb + HW][mb];
+        float o[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) o[i] = gt[i] / (1.f + __expf(-gt[i])) * up[i];
+        const uint32_t lo = (uint32_t)f2bf(o[0]) | ((uint32_t)f2bf(o[1]) << 16);
+        const uint32_t hi = (uint32_t)f2bf(o[2]) | ((uint32_t)f2bf(o[3]) << 16);
+        *reinterpret_cast<uint2*>(y + (int64_t)m * y_stride + f) = make_uint2(lo, hi);
+      }
+    }
+    return;
+  }
   const bool whole = gridDim.y == 1;
 #pragma unroll
   for (int mb = 0; mb < MB; ++mb) {
@@ -254,6 +291,7 @@ __global__ __launch_bounds__(NT, 1) void mgemm_kernel(const void* __restrict__ x
         const f32x4_t sw = *reinterpret_cast<const f32x4_t*>(wsc + n);
 #pragma unroll
         for (int i = 0; i < 4; ++i) v[i] *= sx * sw[i];
+        acc[rb][mb] = v;
       }
       if (whole) {
         const uint32_t lo = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
@@ -264,6 +302,36 @@ __global__ __launch_bounds__(NT, 1) void mgemm_kernel(const void* __restrict__ x
       }
     }
   }
+  if (whole || cnt == nullptr) return;
+  // split-K fixup in the kernel (no reduce launch): the last split of this column tile to
+  // finish sums the others' partials into its registers and writes bf16 Y. Release: the
+  // agent-scope fence writes this XCD's L2 back so another XCD's acquire sees the partials.
+  // (the flag lives in stage 0: every wave is past its last LDS read at the first barrier; the
+  // 4-stage 256-row ring fills all 160 KB)
+  int* last = reinterpret_cast<int*>(st0);
+  __threadfence();
+  __syncthreads();
+  if (threadIdx.x == 0) *last = atomicAdd(cnt + tile, 1) == (int)gridDim.y - 1;
+  __syncthreads();
+  if (!*last) return;
+  __threadfence();  // acquire: this XCD's stale L2 lines are invalidated
+#pragma unroll
+  for (int mb = 0; mb < MB; ++mb) {
+    const int m = 16 * mb + c16;
+    if (m >= M) continue;
+#pragma unroll
+    for (int rb = 0; rb < WRB; ++rb) {
+      const int n = row0 + 16 * (WRB * wv + rb) + 4 * g;
+      if (n >= N) continue;
+      f32x4_t v = acc[rb][mb];
+      for (int s2 = 0; s2 < (int)gridDim.y; ++s2)
+        if (s2 != sp) v += *reinterpret_cast<const f32x4_t*>(part + ((int64_t)s2 * M + m) * N + n);
+      const uint32_t lo = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
+      const uint32_t hi = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
+      *reinterpret_cast<uint2*>(y + (int64_t)m * y_stride + n) = make_uint2(lo, hi);
+    }
+  }
+  if (threadIdx.x == 0) cnt[tile] = 0;  // ready for the next launch on this slab (stream order)
 }
 
 __global__ __launch_bounds__(256) void mgemm_reduce_kernel(const float* __restrict__ part, int nsplit, int M, int N,
@@ -280,7 +348,7 @@ __global__ __launch_bounds__(256) void mgemm_reduce_kernel(const float* __restri
 }
 
 typedef void (*mkern_t)(const void*, int64_t, const void*, int64_t, int, int, int, int, uint16_t*, int64_t,
-                        float*, const float*, const float*);
+                        float*, const float*, const float*, int*);
 
 template <int MB, bool F8, int POL>
 mkern_t pick_w(int wrb, int stages) {
@@ -319,6 +387,26 @@ mkern_t pick_m(int mb, int wrb, int stages) {
   return mgemm_nt() ? pick_m_pol<F8, 2>(mb, wrb, stages) : pick_m_pol<F8, 0>(mb, wrb, stages);
 }
 
+template <int MB, int POL>
+mkern_t pick_act_w(int wrb, int stages) {
+  if (wrb == 2) return stages == 3 ? mgemm_kernel<MB, 2, 3, false, POL, true> : mgemm_kernel<MB, 2, 4, false, POL, true>;
+  if (wrb == 4) {
+    if (stages == 3) return mgemm_kernel<MB, 4, 3, false, POL, true>;
+    if constexpr (MB == 4) return mgemm_kernel<MB, 4, 4, false, POL, true>;
+  }
+  return nullptr;
+}
+
+template <int POL>
+mkern_t pick_act_pol(int mb, int wrb, int stages) {
+  switch (mb) {
+    case 4: return pick_act_w<4, POL>(wrb, stages);
+    case 6: return pick_act_w<6, POL>(wrb, stages);
+    case 8: return pick_act_w<8, POL>(wrb, stages);
+  }
+  return nullptr;
+}
+
 }  // namespace
 
 // LDS bytes of one (M, wrb, stages) configuration; 0 if not instantiated
@@ -331,8 +419,11 @@ extern "C" int llmd_mgemm_lds(int M, int wrb, int stages) {
 
 // Y = X W^T, M <= 128, K % 64 == 0, N % 4 == 0; wrb: 64-row W tiles per workgroup
 // (1, 2 or 4), nsplit K splits (part: nsplit * M * N fp32 when > 1), stages 3 or 4.
+// cnt: nullptr = split-K partials summed by mgemm_reduce_kernel; else a zeroed int slab of >= N / (64 wrb)
+// counters for the in-kernel fixup (left zeroed again)
 extern "C" int llmd_mgemm(const void* x, int64_t x_stride, const void* w, int64_t w_stride, int M, int N, int K,
-                          int wrb, int nsplit, int stages, void* y, int64_t y_stride, float* part, hipStream_t st) {
+                          int wrb, int nsplit, int stages, void* y, int64_t y_stride, float* part, int* cnt,
+                          hipStream_t st) {
   if (M < 1 || M > 128 || K % 64 != 0 || N % 4 != 0 || nsplit < 1 || x_stride % 8 || w_stride % 8) return -1;
   if (llmd_mgemm_lds(M, wrb, stages) == 0) return -1;
   const int mb = M <= 64 ? 4 : M <= 96 ? 6 : 8;
@@ -344,8 +435,8 @@ extern "C" int llmd_mgemm(const void* x, int64_t x_stride, const void* w, int64_
   const int bn = 64 * wrb;
   dim3 grid((N + bn - 1) / bn, nsplit);
   hipLaunchKernelGGL(k, grid, dim3(NT), 0, st, x, x_stride, w, w_stride, M, N, K, per, (uint16_t*)y, y_stride, part,
-                     (const float*)nullptr, (const float*)nullptr);
-  if (nsplit > 1) {
+                     (const float*)nullptr, (const float*)nullptr, nsplit > 1 ? cnt : nullptr);
+  if (nsplit > 1 && cnt == nullptr) {
     const int64_t total4 = (int64_t)M * N / 4;
     hipLaunchKernelGGL(mgemm_reduce_kernel, dim3((unsigned)((total4 + 255) / 256)), dim3(256), 0, st, part, nsplit,
                        M, N, (uint16_t*)y, y_stride);
@@ -357,7 +448,7 @@ extern "C" int llmd_mgemm(const void* x, int64_t x_stride, const void* w, int64_
 // W [N, K] with per-channel scales ws [N]; K % 128 == 0 (128 k per 128-B image row).
 extern "C" int llmd_mgemm_fp8(const void* x, int64_t x_stride, const float* xs, const void* w, int64_t w_stride,
                               const float* ws, int M, int N, int K, int wrb, int nsplit, int stages, void* y,
-                              int64_t y_stride, float* part, hipStream_t st) {
+                              int64_t y_stride, float* part, int* cnt, hipStream_t st) {
   if (M < 1 || M > 128 || K % 128 != 0 || N % 4 != 0 || nsplit < 1 || x_stride % 16 || w_stride % 16) return -1;
   if (llmd_mgemm_lds(M, wrb, stages) == 0) return -1;
   const int mb = M <= 64 ? 4 : M <= 96 ? 6 : 8;
@@ -369,11 +460,29 @@ extern "C" int llmd_mgemm_fp8(const void* x, int64_t x_stride, const float* xs, 
   const int bn = 64 * wrb;
   dim3 grid((N + bn - 1) / bn, nsplit);
   hipLaunchKernelGGL(k, grid, dim3(NT), 0, st, x, x_stride, w, w_stride, M, N, K, per, (uint16_t*)y, y_stride, part,
-                     xs, ws);
-  if (nsplit > 1) {
+                     xs, ws, nsplit > 1 ? cnt : nullptr);
+  if (nsplit > 1 && cnt == nullptr) {
     const int64_t total4 = (int64_t)M * N / 4;
     hipLaunchKernelGGL(mgemm_reduce_kernel, dim3((unsigned)((total4 + 255) / 256)), dim3(256), 0, st, part, nsplit,
                        M, N, (uint16_t*)y, y_stride);
   }
+  return (int)hipGetLastError();
+}
+
+// Y [M, F] = silu(X Wg^T) * (X Wu^T) on the plain [gate; up] weight W [N = 2F, K] (the decode
+// step's gate/up projection with the activation fused: no [M, 2F] intermediate, no act launch);
+// wrb 2 or 4, whole K per workgroup.
+extern "C" int llmd_mgemm_silu(const void* x, int64_t x_stride, const void* w, int64_t w_stride, int M, int N,
+                               int K, int wrb, int stages, void* y, int64_t y_stride, hipStream_t st) {
+  if (M < 1 || M > 128 || K % 64 != 0 || N % 8 != 0 || x_stride % 8 || w_stride % 8 || y_stride % 4) return -1;
+  if ((wrb != 2 && wrb != 4) || llmd_mgemm_lds(M, wrb, stages) == 0) return -1;
+  if ((int64_t)N * w_stride >= 0x7fffffffLL) return -2;  // 32-bit DMA offsets from the weight base
+  const int mb = M <= 64 ? 4 : M <= 96 ? 6 : 8;
+  mkern_t k = mgemm_nt() ? pick_act_pol<2>(mb, wrb, stages) : pick_act_pol<0>(mb, wrb, stages);
+  if (k == nullptr) return -2;
+  const int bn = 64 * wrb;
+  dim3 grid((N + bn - 1) / bn, 1);
+  hipLaunchKernelGGL(k, grid, dim3(NT), 0, st, x, x_stride, w, w_stride, M, N, K, K / 64, (uint16_t*)y, y_stride,
+                     (float*)nullptr, (const float*)nullptr, (const float*)nullptr, (int*)nullptr);
   return (int)hipGetLastError();
 }

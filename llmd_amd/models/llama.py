@@ -33,6 +33,10 @@ class LlamaMLP(torch.nn.Module):
             v = ops.pgemm_silu_plan(x, gu.weight)
             if v is not None:
                 return self.down(ops.pgemm_silu(x, gu.weight, variant=v))
+            # decode: the same fusion in the medium-M GEMM (csrc/ops/mgemm.hip ACT form)
+            p = ops.mgemm_silu_plan(x, gu.weight)
+            if p is not None:
+                return self.down(ops.mgemm_silu(x, gu.weight, p))
         h = gu(x)
         if wants_fp8_input(self.down):  # SiLU*up fused with the down proj's fp8 activation quant
             return self.down(ops.gated_act_quant(h, ops.ACT_SILU))

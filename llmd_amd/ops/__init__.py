@@ -933,6 +933,29 @@ def mgemm(x: torch.Tensor, w: torch.Tensor, plan: tuple[int, int, int]) -> torch
     return y
 
 
+# decode gate/up projection with the SiLU-and-mul in the medium-M GEMM's epilogue (LLMD_MGEMM_SILU=0:
+# the plain GEMM + act kernel)
+MGEMM_SILU = os.environ.get("LLMD_MGEMM_SILU", "1") == "1"
+
+
+def mgemm_silu_plan(x: torch.Tensor, w: torch.Tensor) -> Optional[tuple[int, int, int]]:
+    """The shipped medium-M plan of the [gate; up] GEMM when it runs whole-K tiles of 2 or 4
+    W row blocks (the fused form's shape), else None."""
+    if not (MGEMM_SILU and x.dim() == 2 and 33 <= x.shape[0] <= 128 and mgemm_ok(x, w) and w.shape[0] % 8 == 0):
+        return None
+    plan = mgemm_choice(x.shape[0], w.shape[0], w.shape[1])
+    if plan is None or plan[1] != 1 or plan[0] not in (2, 4):
+        return None
+    return plan
+
+
+def mgemm_silu(x: torch.Tensor, w: torch.Tensor, plan: tuple[int, int, int]) -> torch.Tensor:
+    """silu(x Wg^T) * (x Wu^T) for w = [gate; up] [2F, K], M 33..128 (csrc/ops/mgemm.hip ACT form)."""
+    y = torch.empty(x.shape[0], w.shape[0] // 2, dtype=x.dtype, device=x.device)
+    native().mgemm_silu(y, x, w, plan[0], plan[2])
+    return y
+
+
 def mgemm_fp8(xq: torch.Tensor, xs: torch.Tensor, wq: torch.Tensor, ws: torch.Tensor,
               plan: tuple[int, int, int]) -> torch.Tensor:
     """Y = (Xq sx)(Wq sw)^T on the medium-M GEMM's fp8 form (e4m3fn operands, per-token

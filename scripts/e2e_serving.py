@@ -170,7 +170,7 @@ def main():
     ap.add_argument("--model", default="llama-3-8b")
     ap.add_argument("--device", default="cuda")
     ap.add_argument("--replicas", type=int, default=2)
-    ap.add_argument("--blocks", type=int, default=4096, help="KV blocks (16 tokens) per replica")
+    ap.add_argument("--blocks", type=int, default=4096, help="KV blocks (16 tokens) per replica (0: sized by the engine, e.g. --kv-cache-memory-bytes)")
     ap.add_argument("--groups", type=int, default=48)
     ap.add_argument("--per-group", type=int, default=16)
     ap.add_argument("--system-len", type=int, default=2048)
@@ -199,7 +199,8 @@ def main():
     logs = []
     for i, port in enumerate(ports):
         cmd = [sys.executable, "-m", "llmd_amd.serving.api_server", "--model", a.model, "--port", str(port),
-               "--device", a.device, "--num-gpu-blocks-override", str(a.blocks), "--block-size", "16",
+               "--device", a.device] + (["--num-gpu-blocks-override", str(a.blocks)] if a.blocks > 0 else []) + [
+               "--block-size", "16",
                "--max-num-seqs", str(max(8, a.concurrency)), "--max-num-batched-tokens", "8192",
                "--max-model-len", str(a.system_len + a.question_len + a.output_len + 64),
                "--kv-events-config", json.dumps({"enable_kv_cache_events": True, "publisher": "zmq",

@@ -63,3 +63,49 @@ def test_mgemm_graph_capture():
         torch.cuda.synchronize()
         want = _ref(x, w)
         assert (y.float() - want).abs().max().item() <= 2e-2 * max(1.0, want.abs().max().item())
+
+
+def test_mgemm_split_fixup_many_launches_two_streams():
+    """The in-kernel split-K fixup (per-tile counters on round-robin slabs, left zeroed by each
+    launch): > 256 back-to-back launches (every slab reused) interleaved on two streams at once,
+    and a split count that leaves the last split short."""
+    from llmd_amd import ops
+
+    torch.manual_seed(5)
+    ws = [(torch.randn(1536, 2560, device="cuda") * 0.05).bfloat16() for _ in range(2)]
+    xs = [torch.randn(64, 2560, device="cuda").bfloat16() for _ in range(6)]
+    want = [[_ref(x, w) for w in ws] for x in xs]
+    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+    outs = []
+    torch.cuda.synchronize()
+    for i in range(300):
+        s = streams[i % 2]
+        with torch.cuda.stream(s):
+            outs.append((i % 6, i % 2, ops.mgemm(xs[i % 6], ws[i % 2], (2, 3 + i % 5, 3))))
+    torch.cuda.synchronize()
+    for xi, wi, y in outs:
+        ref = want[xi][wi]
+        assert (y.float() - ref).abs().max().item() <= 2e-2 * max(1.0, ref.abs().max().item()), (xi, wi)
+
+
+@pytest.mark.parametrize("M", [33, 64, 100, 128])
+@pytest.mark.parametrize("F,K", [(1536, 1024), (2004, 2048)])
+def test_mgemm_silu_matches_fp32(M, F, K):
+    """The ACT form (SiLU-and-mul in the epilogue on the plain [gate; up] weight) vs fp32:
+    every wrb / stage ring it instantiates, F not a multiple of the tile's half (dropped rows)."""
+    from llmd_amd import ops
+
+    torch.manual_seed(M + F)
+    x = torch.randn(M, K, device="cuda").bfloat16()
+    w = (torch.randn(2 * F, K, device="cuda") * 0.05).bfloat16()
+    h = _ref(x, w)
+    want = torch.nn.functional.silu(h[:, :F]) * h[:, F:]
+    tol = 2e-2 * max(1.0, want.abs().max().item())
+    for wrb in (2, 4):
+        for stages in (3, 4):
+            if not ops.native().mgemm_lds(M, wrb, stages):
+                continue
+            y = ops.mgemm_silu(x, w, (wrb, 1, stages))
+            assert y.shape == (M, F)
+            err = (y.float() - want).abs().max().item()
+            assert err <= tol, (M, F, K, wrb, stages, err)
