@@ -168,6 +168,9 @@ __global__ __launch_bounds__(M4_NT, 1) void moe_gemm4_bf16_kernel(
       }
       __builtin_amdgcn_sched_barrier(0);
     }
+    // drain the asm MFMAs inside the last iteration: hipcc cannot see their latency, and the
+    // register allocator may place accumulator copies (epilogue spills) right at the loop exit
+    if (kt + 1 == nk) asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 3" ::: "memory");
   }
   asm volatile("s_nop 7\n\ts_nop 7" ::: "memory");  // asm MFMA results -> VALU reads
   __builtin_amdgcn_sched_barrier(0);
@@ -411,6 +414,8 @@ __global__ __launch_bounds__(M4_NT, 1) void moe_gemm4_fp8_kernel(
 #pragma unroll
     for (int b = 0; b < 4; ++b) sa[b] = e8m0_of(nsf[b]);
     swt = e8m0_of(nwf);
+    // drain inside the last iteration (see the bf16 form): 16-pass MFMAs
+    if (kt + 1 == nk) asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
   }
   asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
   __builtin_amdgcn_sched_barrier(0);
