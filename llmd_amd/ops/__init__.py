@@ -575,12 +575,13 @@ MOE_V3 = os.environ.get("LLMD_MOE_V3", "1") == "1"
 # bf16 experts on the same 256-row tiles (moe_gemm3 with bf16 operands); LLMD_MOE_V3_BF16=0 keeps v2
 MOE_V3_BF16 = os.environ.get("LLMD_MOE_V3_BF16", "1") == "1"  # DeepSeek EP8 T=4096 701 -> 789 TF/s, gpt-oss T=5120 369 -> 529
 # bf16 prefill-sized steps on the v4 grouped GEMM (csrc/ops/moe4.hip, the PGR2 structure of the dense
-# prefill GEMM); off until its A/B on the GPU (scripts/bench_moe.py)
-MOE_BF16_V4 = os.environ.get("LLMD_MOE_BF16_V4", "0") == "1"
+# prefill GEMM): DeepSeek EP8 T=4096 807 -> 1011 TF/s, gpt-oss T=5120 534 -> 586 (profiles/moe_gemm_v4_r5.txt)
+MOE_BF16_V4 = os.environ.get("LLMD_MOE_BF16_V4", "1") == "1"
 MOE_FUSED_QUANT = os.environ.get("LLMD_MOE_FUSED_QUANT", "0") == "1"
 # block-fp8 prefill-sized steps on the v4 grouped GEMM (moe4.hip moe_gemm4_fp8_kernel: 4-wave PGR2,
-# scaled 32x32x64 MFMA with the E8M0 block scales as operands); off until its A/B (scripts/bench_moe.py)
-MOE_FP8_V4 = os.environ.get("LLMD_MOE_FP8_V4", "0") == "1"
+# scaled 32x32x64 MFMA with the E8M0 block scales as operands): DeepSeek EP8 T=4096 1307 -> 1496 TF/s,
+# gpt-oss T=5120 757 -> 782 (profiles/moe_gemm_v4_r5.txt)
+MOE_FP8_V4 = os.environ.get("LLMD_MOE_FP8_V4", "1") == "1"
 
 
 class Fp8Rows:
