@@ -928,6 +928,283 @@ __global__ __launch_bounds__(NT, 1) void prefill_v3_kernel(
   }
 }
 
+
+// ---------------------------------------------------------------- v4 (bf16 cache, D = 128): 32x32x16 MFMAs
+// The work decomposition, items, K/V tiles and the double-buffered LDS-DMA ring of v2; the two
+// products run on v_mfma_f32_32x32x16_bf16. An MFMA holds its SIMD's vector issue for 8 of its 32
+// cycles (16x16x32: 8 of 16), so per MFMA-cycle there is three times the room for the softmax
+// VALU and the LDS reads that share the issue port (MI355X_MICROARCH 'vector-instruction ISSUE
+// cost'; v2 is issue-bound beside its MFMAs).
+//   S^T[key][q] = K . Q^T: A = 32 K rows (ds_read_b128), B = the wave's 32 queries (registers);
+//     lane l holds query l & 31's scores of keys (r & 3) + 8 (r >> 2) + 4 (l >> 5) of a 32-key
+//     block (r = 0..15): row max and sum are lane-local plus one permlane32_swap.
+//   O^T[d][q] += V^T . P^T: P^T is S^T's accumulator used in place as the B operand (cvt_pk per
+//     register pair; its k order is the accumulator's permuted key order), A = V^T read with two
+//     ds_read_b64_tr_b16 per fragment in that same key order.
+// O^T's column is the query, so the online-softmax rescale is a lane-local multiply.
+// Images: 256-B rows, 16-B chunk ch of row r at slot ch ^ (((r & 3) << 2) | ((r >> 2) & 3))
+// (vimg_off<128>): conflict-free for the 32-row b128 reads and the transposed reads alike.
+__device__ __forceinline__ int p4_sw(int r) { return ((r & 3) << 2) | ((r >> 2) & 3); }
+
+template <int V4 = 1>
+__global__ __launch_bounds__(NT, 2) void prefill_v4_kernel(
+    const uint16_t* __restrict__ q, int64_t q_stride, const uint16_t* __restrict__ kc,
+    const uint16_t* __restrict__ vc, int64_t block_stride, int bs,
+    const int* __restrict__ block_tables, int bt_stride, const int* __restrict__ q_start,
+    const int* __restrict__ q_len, const int* __restrict__ ctx_len, const int* __restrict__ items,
+    int Hq, int Hkv, int G, int HPW, float scale_log2, int window,
+    const float* __restrict__ sinks, uint16_t* __restrict__ out, int64_t out_stride, float vscale, int xcd) {
+  constexpr int D = 128, RB = 256, IMG = 64 * RB, NI = 16;
+  __shared__ __attribute__((aligned(1024))) char buf0[2 * IMG];  // K | V of even tiles
+  __shared__ __attribute__((aligned(1024))) char buf1[2 * IMG];  // K | V of odd tiles
+
+  int bx = blockIdx.x, by = blockIdx.y;
+  if (xcd) {
+    const int l = xcd_remap(by * gridDim.x + bx, gridDim.x * gridDim.y);
+    bx = l % gridDim.x;
+    by = l / gridDim.x;
+  }
+  const int seq = items[2 * bx], qb = items[2 * bx + 1];
+  const int NHG = G / HPW;
+  const int kvh = by / NHG, hg = by % NHG;
+  const int TPW = 4 / HPW;
+  const int qs = q_start[seq], ql = q_len[seq], ctx = ctx_len[seq];
+  const int pbase = ctx - ql;
+  const int* bt = block_tables + (int64_t)seq * bt_stride;
+  const int64_t head_off = (int64_t)kvh * bs * D;
+  const int lbs = __builtin_ctz(bs);
+
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, l32 = lane & 31, h = lane >> 5;
+  const int head = kvh * G + hg * HPW + (w % HPW);
+  const int tok0 = qb + (w / HPW) * 32;
+  const int ntok = max(0, min(32, ql - tok0));
+  const int p_lo = pbase + tok0, p_hi = pbase + tok0 + max(ntok, 1) - 1;
+  const int wg_tok_end = min(ql, qb + 32 * TPW);
+  const int wg_p_lo = pbase + qb, wg_p_hi = pbase + wg_tok_end - 1;
+  const int kmin = window > 0 ? max(0, wg_p_lo - window + 1) : 0;
+  const int t_first = kmin >> 6, t_last = wg_p_hi >> 6;
+
+  // Q^T fragments (B operand): lane l holds Q[tok0 + l32][16 ks + 8 h + j]
+  bf16x8_t qf[8];
+  {
+    const int tk = tok0 + l32;
+    const uint16_t* qr = q + (int64_t)(qs + min(tk, ql - 1)) * q_stride + (int64_t)head * D;
+#pragma unroll
+    for (int ks = 0; ks < 8; ++ks) {
+      u32x4_t v = {0, 0, 0, 0};
+      if (tk < ql) v = *reinterpret_cast<const u32x4_t*>(qr + (2 * ks + h) * 8);
+      qf[ks] = __builtin_bit_cast(bf16x8_t, v);
+    }
+  }
+  const int qp = p_lo + l32;  // this lane's query position
+  float m = NEG_INF, lsum = 0.f;
+  f32x16_t o[4];
+#pragma unroll
+  for (int db = 0; db < 4; ++db) o[db] = f32x16_t{};
+
+  // DMA (v2's): wave w issues 1-KB pieces j = w + 4 i of K and V; lane -> row u / 16, slot u % 16
+  const int ws = __builtin_amdgcn_readfirstlane(w);
+  uint32_t koff[NI / 4];
+#pragma unroll
+  for (int i = 0; i < NI / 4; ++i) {
+    const int u = 64 * (w + 4 * i) + lane;
+    const int row = u / 16, sl = u % 16;
+    koff[i] = (uint32_t)(row * RB + 16 * (sl ^ p4_sw(row)));
+  }
+  auto dma = [&](const char* src, char* dst) {
+    __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)src,
+                                     (void __attribute__((address_space(3)))*)dst, 16, 0, 0);
+  };
+  auto issue = [&](char* base, int t) {
+    const int ts = t * 64;
+    LLMD_DCHECK(ts < ctx && bt[ts >> lbs] >= 0 && ctx <= bt_stride * bs);
+    const int64_t tb = 2 * ((int64_t)bt[ts >> lbs] * block_stride + head_off + (int64_t)(ts & (bs - 1)) * D);
+    const char* kb = reinterpret_cast<const char*>(kc) + tb;
+    const char* vb = reinterpret_cast<const char*>(vc) + tb;
+    const int rlim = ctx - 1 - ts;
+    if (rlim >= 63 && bs >= 64) {
+#pragma unroll
+      for (int i = 0; i < NI / 4; ++i) {
+        char* dst = base + 1024 * (ws + 4 * i);
+        dma(kb + koff[i], dst);
+        dma(vb + koff[i], dst + IMG);
+      }
+    } else if (rlim >= 63) {
+      // blocks of 16 / 32 keys: a piece's 4 rows sit in one block
+#pragma unroll
+      for (int i = 0; i < NI / 4; ++i) {
+        const int r0 = 4 * (ws + 4 * i);
+        const int key0 = ts + r0;
+        const int64_t ib = 2 * ((int64_t)bt[key0 >> lbs] * block_stride + head_off + (int64_t)(key0 & (bs - 1)) * D) -
+                           (int64_t)r0 * RB;
+        char* dst = base + 1024 * (ws + 4 * i);
+        dma(reinterpret_cast<const char*>(kc) + ib + koff[i], dst);
+        dma(reinterpret_cast<const char*>(vc) + ib + koff[i], dst + IMG);
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < NI / 4; ++i) {
+        const int u = 64 * (w + 4 * i) + lane;
+        const int row = u / 16, sl = u % 16;
+        const int key = ts + min(row, rlim);  // rows past the end re-read the last key (finite V, P = 0)
+        const int64_t ro = bs >= 64 ? (int64_t)min(row, rlim) * RB
+                                    : 2 * ((int64_t)bt[key >> lbs] * block_stride + head_off +
+                                           (int64_t)(key & (bs - 1)) * D) - tb;
+        char* dst = base + 1024 * (ws + 4 * i);
+        dma(kb + ro + 16 * (sl ^ p4_sw(row)), dst);
+        dma(vb + ro + 16 * (sl ^ p4_sw(row)), dst + IMG);
+      }
+    }
+  };
+  // K (A operand) row reads: row 32 kb + l32, chunk 2 ks + h; the swizzle depends on l32 & 15 only
+  const int swk = p4_sw(l32);
+  int kofs[8];
+#pragma unroll
+  for (int ks = 0; ks < 8; ++ks) kofs[ks] = l32 * RB + 16 * ((2 * ks + h) ^ swk);
+  // V^T (A operand) transposed reads: 16-lane group gr = lane >> 4 (column half gr & 1, key half h),
+  // lane 4 qq + pp supplies row r0 + qq, columns 32 db + 16 (gr & 1) + 4 pp .. + 3; two reads per
+  // fragment at key rows 4 h + qq and 8 + 4 h + qq (+ 16 s + 32 kb: multiples of 16, same swizzle)
+  const int qq = (lane & 15) >> 2, pp = lane & 3, gc = (lane >> 4) & 1;
+  int vofs[4][2];
+#pragma unroll
+  for (int db = 0; db < 4; ++db)
+#pragma unroll
+    for (int hh = 0; hh < 2; ++hh) {
+      const int r = 8 * hh + 4 * h + qq, ch = 4 * db + 2 * gc + (pp >> 1);
+      vofs[db][hh] = IMG + r * RB + 16 * (ch ^ p4_sw(r)) + 8 * (pp & 1);
+    }
+
+  auto compute = [&](const char* img, int t) {
+    const int ts = t * 64;
+    const bool active = ntok > 0 && ts <= p_hi && (window <= 0 || ts + 63 > p_lo - window);
+    if (!active) return;
+    constexpr int PF = 4;
+    auto kread = [&](int j) {  // fragment j = 8 kb + ks
+      return *reinterpret_cast<const bf16x8_t*>(img + kofs[j % 8] + (j / 8) * 32 * RB);
+    };
+    auto vread = [&](int j) {  // fragment j = 4 db + ks2 (keys 16 ks2 ..)
+      const char* p0 = img + vofs[j / 4][0] + 16 * (j % 4) * RB;
+      const char* p1 = img + vofs[j / 4][1] + 16 * (j % 4) * RB;
+      s16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4_t*)p0);
+      s16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4_t*)p1);
+      return __builtin_bit_cast(bf16x8_t, s16x8_t{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]});
+    };
+    f32x16_t sc[2];
+    bf16x8_t kr[PF];
+#pragma unroll
+    for (int j = 0; j < PF; ++j) kr[j] = kread(j);
+    if constexpr (V4 & 1) __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb) {
+      f32x16_t a;
+#pragma unroll
+      for (int ks = 0; ks < 8; ++ks) {
+        const int j = 8 * kb + ks;
+        const bf16x8_t ka = kr[j % PF];
+        if (j + PF < 16) kr[j % PF] = kread(j + PF);
+        a = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ka, qf[ks], ks == 0 ? f32x16_t{} : a, 0, 0, 0);
+        if constexpr (V4 & 1) __builtin_amdgcn_sched_barrier(0);
+      }
+      sc[kb] = a;
+    }
+    bf16x8_t vr[PF];
+#pragma unroll
+    for (int j = 0; j < PF; ++j) vr[j] = vread(j);
+    const bool need_mask = (ts + 63 > p_lo) || (window > 0 && ts <= p_hi - window);
+    if (need_mask) {
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int key = ts + 32 * kb + (r & 3) + 8 * (r >> 2) + 4 * h;
+          bool ok = key <= qp;
+          if (window > 0) ok = ok && key > qp - window;
+          sc[kb][r] = ok ? sc[kb][r] : NEG_INF;
+        }
+    }
+    float mx = NEG_INF;
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) mx = fmaxf(mx, sc[kb][r]);
+    {
+      const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(mx), __float_as_uint(mx), false, false);
+      mx = fmaxf(__uint_as_float(sw[0]), __uint_as_float(sw[1]));
+    }
+    const float mt = mx * scale_log2;
+    if (__ballot(mt > m + 8.f) != 0) {  // lazy rescale (v2's threshold), wave-uniform branch
+      const float mnew = fmaxf(m, mt);
+      const float alpha = (mnew == NEG_INF) ? 1.f : __builtin_amdgcn_exp2f(m - mnew);
+      lsum *= alpha;
+      m = mnew;
+#pragma unroll
+      for (int db = 0; db < 4; ++db) o[db] *= alpha;
+    }
+    const float msub = (m == NEG_INF) ? 0.f : m;
+    float ps = 0.f;
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const float p = __builtin_amdgcn_exp2f(fmaf(sc[kb][r], scale_log2, -msub));
+        sc[kb][r] = p;
+        ps += p;
+      }
+    lsum += ps;  // lane-partial (this half's keys): the halves are summed once, in the epilogue
+    bf16x8_t pb[4];  // P^T fragments of key steps 2 kb + s2: registers 8 s2 .. 8 s2 + 7 of sc[kb]
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) pb[2 * kb + s2][j] = (__bf16)sc[kb][8 * s2 + j];
+    if constexpr (V4 & 1) __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const int db = j / 4, ks2 = j % 4;
+      const bf16x8_t va = vr[j % PF];
+      if (j + PF < 16) vr[j % PF] = vread(j + PF);
+      o[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(va, pb[ks2], o[db], 0, 0, 0);
+      if constexpr (V4 & 1) __builtin_amdgcn_sched_barrier(0);
+    }
+  };
+
+  issue(buf0, t_first);
+  for (int t = t_first; t <= t_last; t += 2) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (t + 1 <= t_last) issue(buf1, t + 1);
+    compute(buf0, t);
+    if (t + 1 > t_last) break;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (t + 2 <= t_last) issue(buf0, t + 2);
+    compute(buf1, t + 1);
+  }
+
+  if (ntok == 0) return;
+  const float sink = sinks ? sinks[head] * 1.4426950408889634f : NEG_INF;
+  float den;
+  {
+    const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(lsum), __float_as_uint(lsum), false, false);
+    den = __uint_as_float(sw[0]) + __uint_as_float(sw[1]);
+  }
+  if (sinks) den += exp2f(sink - (m == NEG_INF ? 0.f : m));
+  const float inv = den > 0.f ? vscale / den : 0.f;
+  const int tk = tok0 + l32;
+  if (tk < ql) {
+    uint16_t* orow = out + (int64_t)(qs + tk) * out_stride + (int64_t)head * D;
+#pragma unroll
+    for (int db = 0; db < 4; ++db)
+#pragma unroll
+      for (int g4 = 0; g4 < 4; ++g4) {  // d = 32 db + 8 g4 + 4 h + (0..3)
+        u32x2_t p;
+        p[0] = (uint32_t)f2bf(o[db][4 * g4] * inv) | ((uint32_t)f2bf(o[db][4 * g4 + 1] * inv) << 16);
+        p[1] = (uint32_t)f2bf(o[db][4 * g4 + 2] * inv) | ((uint32_t)f2bf(o[db][4 * g4 + 3] * inv) << 16);
+        *reinterpret_cast<u32x2_t*>(orow + 32 * db + 8 * g4 + 4 * h) = p;
+      }
+  }
+}
 }  // namespace
 
 // v3 for D = 128 bf16 caches with blocks of >= 64 keys and whole groups of 4 query
@@ -946,6 +1223,13 @@ static bool prefill_v3_ok(int Hq, int Hkv, int D, int bs, int fp8) {
 }
 
 
+
+// v4 (32x32x16 MFMAs) for D = 128 bf16 caches: LLMD_PREFILL_V4=1 (off until its GPU A/B); read per
+// launch so one process can A/B both (v4 and v2 share the item shape)
+static bool prefill_v4_on() {
+  const char* e = getenv("LLMD_PREFILL_V4");
+  return e && e[0] == '1';
+}
 
 extern "C" int llmd_paged_prefill(const void* q, int64_t q_stride, const void* kc, const void* vc,
                                   int64_t block_stride, int bs, const int* block_tables,
@@ -987,6 +1271,11 @@ extern "C" int llmd_paged_prefill(const void* q, int64_t q_stride, const void* k
                        (const uint16_t*)vc, block_stride, bs, block_tables, bt_stride, q_start, q_len, ctx_len,
                        items, Hq, Hkv, G, scale_log2, window, sinks, (uint16_t*)out, out_stride, v_scale,
                        xcd_map && (int64_t)n_items * grid3.y >= 1024 ? 1 : 0);
+  } else if (D == 128 && !fp8 && bs >= 16 && !v1_only && prefill_v4_on()) {
+    hipLaunchKernelGGL(prefill_v4_kernel<1>, grid, blk, 0, st, (const uint16_t*)q, q_stride, (const uint16_t*)kc,
+                       (const uint16_t*)vc, block_stride, bs, block_tables, bt_stride, q_start, q_len, ctx_len,
+                       items, Hq, Hkv, G, HPW, scale_log2, window, sinks, (uint16_t*)out, out_stride, v_scale,
+                       xcd_map && (int64_t)n_items * grid.y >= 1024 ? 1 : 0);
   } else if ((D == 128 || D == 64) && !fp8 && bs >= 16 && !v1_only) {
     static const int pv = [] {
       // A/B of the round-4 schedule (V above; profiles/attn_prefill_r4_ab.txt): the ring wins everywhere,

@@ -6,6 +6,11 @@ mkdir -p gpurun_out
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 timeout -k 10 300 python -u -m pytest tests/test_mgemm.py tests/test_kernels_gpu.py -q -x --timeout 120 --timeout-method thread -p no:cacheprovider -k "mgemm" > gpurun_out/r5j_tests.log 2>&1
 rc=$?; tail -3 gpurun_out/r5j_tests.log; [ $rc -ne 0 ] && exit $rc
+# prefill attention v4 (32x32x16): numerics, then the A/B against v2
+timeout -k 10 300 python -u -m pytest tests/test_prefill_v4.py -q -x --timeout 120 --timeout-method thread -p no:cacheprovider > gpurun_out/r5j_attn_tests.log 2>&1
+rc=$?; tail -15 gpurun_out/r5j_attn_tests.log; [ $rc -ne 0 ] && exit $rc
+timeout -k 10 300 python -u scripts/attn_v4_ab.py > gpurun_out/r5j_attn_ab.log 2>&1
+rc=$?; grep -v amdgpu.ids gpurun_out/r5j_attn_ab.log | grep "AB\|check"; [ $rc -ne 0 ] && exit $rc
 for cfg in "0 0" "1 0" "1 1"; do
   set -- $cfg
   LLMD_MGEMM_FIXUP=$1 LLMD_MGEMM_SILU=$2 timeout -k 10 400 python -u scripts/bench_decode.py --steps 40 > gpurun_out/r5j_dec_$1$2.log 2>&1
