@@ -434,11 +434,12 @@ bool skinny_supported(int64_t M, int64_t rb, int64_t occ) { return llmd_dgemm_su
 // Split-K fixup counters of mgemm (csrc/ops/mgemm.hip): per device 256 slabs of 1024 zeroed ints, handed
 // out round-robin so kernels in flight on different streams (DBO, TP overlap) never share a slab; each
 // launch leaves its slab zeroed. Created outside stream capture (a capture before the first eager call
-// falls back to the reduce kernel); LLMD_MGEMM_FIXUP=0 keeps the reduce kernel.
+// falls back to the reduce kernel). Opt-in (LLMD_MGEMM_FIXUP=1): with agent-scope fences in every
+// workgroup it measured slower than the reduce launch (profiles/decode_r5.txt).
 int* mgemm_counters(const torch::Device& d, int64_t tiles) {
   static const bool on = [] {
     const char* e = getenv("LLMD_MGEMM_FIXUP");
-    return !(e && e[0] == '0');
+    return e && e[0] == '1';
   }();
   if (!on || tiles > 1024) return nullptr;
   static std::mutex mu;

@@ -22,9 +22,9 @@
 // (swizzle applied on the DMA source address; destination stays lane-linear):
 // the 16 lanes of a ds_read_b128 pass (16 rows, one k chunk) hit 16 distinct
 // slots of the 256-B bank row.
-// Split-K partials: fp32 [split][M][N], summed and rounded in the kernel by the last split of
-// each column tile to finish (an atomic counter per tile; LLMD_MGEMM_FIXUP=0: by
-// mgemm_reduce_kernel, one more launch and one more pass over the partials).
+// Split-K partials: fp32 [split][M][N], summed and rounded by mgemm_reduce_kernel, or (opt-in,
+// LLMD_MGEMM_FIXUP=1) in the kernel by the last split of each column tile to finish (an atomic
+// counter per tile; agent-scope fences for the cross-XCD hand-off).
 //
 // fp8 (W8A8, e4m3fn, F8 = true): the same 128-B image rows hold 128 k per step;
 // a lane's 16-B fragment feeds two mfma_f32_16x16x32_fp8_fp8 (its low and high
@@ -309,12 +309,14 @@ __global__ __launch_bounds__(NT, 1) void mgemm_kernel(const void* __restrict__ x
   // (the flag lives in stage 0: every wave is past its last LDS read at the first barrier; the
   // 4-stage 256-row ring fills all 160 KB)
   int* last = reinterpret_cast<int*>(st0);
-  __threadfence();
+  // release only (L2 write-back, no invalidate: a seq_cst fence in every workgroup also dropped the
+  // XCD's L2 under its neighbours' X reads - 43.3 -> 53.7 ms per 70B decode step, profiles/decode_r5.txt)
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
   __syncthreads();
   if (threadIdx.x == 0) *last = atomicAdd(cnt + tile, 1) == (int)gridDim.y - 1;
   __syncthreads();
   if (!*last) return;
-  __threadfence();  // acquire: this XCD's stale L2 lines are invalidated
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // the last split only: other XCDs' partials
 #pragma unroll
   for (int mb = 0; mb < MB; ++mb) {
     const int m = 16 * mb + c16;
