@@ -22,9 +22,9 @@
 // (swizzle applied on the DMA source address; destination stays lane-linear):
 // the 16 lanes of a ds_read_b128 pass (16 rows, one k chunk) hit 16 distinct
 // slots of the 256-B bank row.
-// Split-K partials: fp32 [split][M][N], summed and rounded by mgemm_reduce_kernel, or (opt-in,
-// LLMD_MGEMM_FIXUP=1) in the kernel by the last split of each column tile to finish (an atomic
-// counter per tile; agent-scope fences for the cross-XCD hand-off).
+// Split-K partials: fp32 [split][M][N], summed and rounded by mgemm_reduce_kernel, or (LLMD_MGEMM_FIXUP,
+// column-tile counts that are multiples of 8) in the kernel by the last split of each column tile
+// to finish (an atomic counter per tile; the splits of a tile share an XCD, see the epilogue).
 //
 // fp8 (W8A8, e4m3fn, F8 = true): the same 128-B image rows hold 128 k per step;
 // a lane's 16-B fragment feeds two mfma_f32_16x16x32_fp8_fp8 (its low and high
@@ -308,15 +308,19 @@ __global__ __launch_bounds__(NT, 1) void mgemm_kernel(const void* __restrict__ x
   // agent-scope fence writes this XCD's L2 back so another XCD's acquire sees the partials.
   // (the flag lives in stage 0: every wave is past its last LDS read at the first barrier; the
   // 4-stage 256-row ring fills all 160 KB)
+  // The host passes counters only when the column-tile count is a multiple of 8: workgroups are
+  // dealt round-robin over the 8 XCDs in linear order (sp * tiles + tile), so every split of a
+  // tile runs on the same XCD and meets the others in that XCD's L2 - no agent-scope fence (an
+  // L2 write-back per workgroup cost 8-10 ms per 70B decode step, profiles/decode_r5.txt). The
+  // vector L1 writes through; this workgroup's stores are acknowledged (vmcnt 0, stores count on
+  // CDNA4) before its arrival is counted, and the last split's loads miss its L1 (it never read
+  // those lines) and hit L2.
   int* last = reinterpret_cast<int*>(st0);
-  // release only (L2 write-back, no invalidate: a seq_cst fence in every workgroup also dropped the
-  // XCD's L2 under its neighbours' X reads - 43.3 -> 53.7 ms per 70B decode step, profiles/decode_r5.txt)
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (threadIdx.x == 0) *last = atomicAdd(cnt + tile, 1) == (int)gridDim.y - 1;
   __syncthreads();
   if (!*last) return;
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // the last split only: other XCDs' partials
 #pragma unroll
   for (int mb = 0; mb < MB; ++mb) {
     const int m = 16 * mb + c16;
@@ -436,6 +440,7 @@ extern "C" int llmd_mgemm(const void* x, int64_t x_stride, const void* w, int64_
   nsplit = (nk + per - 1) / per;  // no empty splits
   const int bn = 64 * wrb;
   dim3 grid((N + bn - 1) / bn, nsplit);
+  if (grid.x % 8) cnt = nullptr;  // the fixup needs every split of a tile on one XCD
   hipLaunchKernelGGL(k, grid, dim3(NT), 0, st, x, x_stride, w, w_stride, M, N, K, per, (uint16_t*)y, y_stride, part,
                      (const float*)nullptr, (const float*)nullptr, nsplit > 1 ? cnt : nullptr);
   if (nsplit > 1 && cnt == nullptr) {
@@ -461,6 +466,7 @@ extern "C" int llmd_mgemm_fp8(const void* x, int64_t x_stride, const float* xs, 
   nsplit = (nk + per - 1) / per;
   const int bn = 64 * wrb;
   dim3 grid((N + bn - 1) / bn, nsplit);
+  if (grid.x % 8) cnt = nullptr;
   hipLaunchKernelGGL(k, grid, dim3(NT), 0, st, x, x_stride, w, w_stride, M, N, K, per, (uint16_t*)y, y_stride, part,
                      xs, ws, nsplit > 1 ? cnt : nullptr);
   if (nsplit > 1 && cnt == nullptr) {

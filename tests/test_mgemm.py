@@ -66,13 +66,14 @@ def test_mgemm_graph_capture():
 
 
 def test_mgemm_split_fixup_many_launches_two_streams():
-    """The in-kernel split-K fixup (per-tile counters on round-robin slabs, left zeroed by each
-    launch): > 256 back-to-back launches (every slab reused) interleaved on two streams at once,
-    and a split count that leaves the last split short."""
+    """The in-kernel split-K fixup (LLMD_MGEMM_FIXUP=1; per-tile counters on round-robin slabs, left
+    zeroed by each launch; column-tile counts that are multiples of 8): > 256 back-to-back launches
+    (every slab reused) interleaved on two streams at once, split counts that leave the last split
+    short. Without the switch the same calls run the reduce kernel."""
     from llmd_amd import ops
 
     torch.manual_seed(5)
-    ws = [(torch.randn(1536, 2560, device="cuda") * 0.05).bfloat16() for _ in range(2)]
+    ws = [(torch.randn(2048, 2560, device="cuda") * 0.05).bfloat16() for _ in range(2)]  # 16 column tiles
     xs = [torch.randn(64, 2560, device="cuda").bfloat16() for _ in range(6)]
     want = [[_ref(x, w) for w in ws] for x in xs]
     streams = [torch.cuda.Stream(), torch.cuda.Stream()]
