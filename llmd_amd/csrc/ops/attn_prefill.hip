@@ -1012,8 +1012,11 @@ __global__ __launch_bounds__(NT, 2) void prefill_v4_kernel(
     koff[i] = (uint32_t)(row * RB + 16 * (sl ^ p4_sw(row)));
   }
   auto dma = [&](const char* src, char* dst) {
-    __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)src,
-                                     (void __attribute__((address_space(3)))*)dst, 16, 0, 0);
+    // V4 bit 1: the DMA from asm (glds16), so hipcc's waitcnt pass keeps counting LDS reads
+    // (a visible global_load_lds in the loop turns every fragment wait into lgkmcnt(0))
+    if constexpr (V4 & 2) glds16(src, lds_addr(dst));
+    else __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)src,
+                                          (void __attribute__((address_space(3)))*)dst, 16, 0, 0);
   };
   auto issue = [&](char* base, int t) {
     const int ts = t * 64;
@@ -1272,7 +1275,9 @@ extern "C" int llmd_paged_prefill(const void* q, int64_t q_stride, const void* k
                        items, Hq, Hkv, G, scale_log2, window, sinks, (uint16_t*)out, out_stride, v_scale,
                        xcd_map && (int64_t)n_items * grid3.y >= 1024 ? 1 : 0);
   } else if (D == 128 && !fp8 && bs >= 16 && !v1_only && prefill_v4_on()) {
-    hipLaunchKernelGGL(prefill_v4_kernel<1>, grid, blk, 0, st, (const uint16_t*)q, q_stride, (const uint16_t*)kc,
+    const char* e4 = getenv("LLMD_PREFILL_V4_VARIANT");  // 1: builtin DMA, 3: asm DMA
+    auto kern4 = (e4 && e4[0] == '1') ? prefill_v4_kernel<1> : prefill_v4_kernel<3>;
+    hipLaunchKernelGGL(kern4, grid, blk, 0, st, (const uint16_t*)q, q_stride, (const uint16_t*)kc,
                        (const uint16_t*)vc, block_stride, bs, block_tables, bt_stride, q_start, q_len, ctx_len,
                        items, Hq, Hkv, G, HPW, scale_log2, window, sinks, (uint16_t*)out, out_stride, v_scale,
                        xcd_map && (int64_t)n_items * grid.y >= 1024 ? 1 : 0);

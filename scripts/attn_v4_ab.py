@@ -18,19 +18,20 @@ def main():
     a = ap.parse_args()
     cases = [(5000, 5000), (8192, 8192), (8192, 4096), (2048, 2048)]
     res = {}
+    arms = {"v2": ("0", "3"), "v4-builtin-dma": ("1", "1"), "v4-asm-dma": ("1", "3")}
     for r in range(a.rounds):
         for ctx, ql in cases:
-            for v in ("0", "1"):
-                os.environ["LLMD_PREFILL_V4"] = v
+            for name, (on, var) in arms.items():
+                os.environ["LLMD_PREFILL_V4"] = on
+                os.environ["LLMD_PREFILL_V4_VARIANT"] = var
                 t = prefill(ctx, ql, 64, 8, 128, 64, check=(r == 0 and ctx == 2048))
-                res.setdefault((ctx, ql, v), []).append(t)
+                res.setdefault((ctx, ql, name), []).append(t)
     for ctx, ql in cases:
         vis = sum(ctx - ql + i + 1 for i in range(ql))
         fl = 4 * 64 * 128 * vis
-        t2 = sorted(res[(ctx, ql, "0")])[a.rounds // 2]
-        t4 = sorted(res[(ctx, ql, "1")])[a.rounds // 2]
-        print(f"AB ctx={ctx} q={ql}: v2 {t2 * 1e3:.3f} ms {fl / t2 / 1e12:.0f} TF/s | v4 {t4 * 1e3:.3f} ms "
-              f"{fl / t4 / 1e12:.0f} TF/s | v4/v2 speedup {t2 / t4:.3f}", flush=True)
+        med = {n: sorted(res[(ctx, ql, n)])[a.rounds // 2] for n in arms}
+        print(f"AB ctx={ctx} q={ql}: " + " | ".join(f"{n} {t * 1e3:.3f} ms {fl / t / 1e12:.0f} TF/s"
+                                                   for n, t in med.items()), flush=True)
 
 
 if __name__ == "__main__":

@@ -46,10 +46,12 @@ def _run(shapes, Hq, Hkv, bs, window=0, sinks=None, seed=5):
     return q, kc, vc, bt, args
 
 
+@pytest.mark.parametrize("variant", ["1", "3"])  # 1: builtin LDS-DMA, 3: asm LDS-DMA
 @pytest.mark.parametrize("Hq,Hkv", [(64, 8), (32, 8), (8, 8), (16, 8)])
 @pytest.mark.parametrize("bs", [16, 64])
-def test_prefill_v4_matches_reference(Hq, Hkv, bs, monkeypatch):
+def test_prefill_v4_matches_reference(Hq, Hkv, bs, variant, monkeypatch):
     monkeypatch.setenv("LLMD_PREFILL_V4", "1")
+    monkeypatch.setenv("LLMD_PREFILL_V4_VARIANT", variant)
     shapes = [(1, 1), (37, 37), (200, 200), (130, 1000), (64, 64), (513, 700)]
     q, kc, vc, bt, args = _run(shapes, Hq, Hkv, bs)
     r = ref.paged_prefill(q, kc, vc, bt, *args, Hq, Hkv, 128, 1 / math.sqrt(128))
