@@ -1172,17 +1172,124 @@ __global__ __launch_bounds__(NT, 2) void prefill_v4_kernel(
     }
   };
 
+  // V4 bit 2: the two 32-key halves of a tile software-pipelined inside the wave - the MFMAs of
+  // S^T half 1 run beside the mask / max VALU of half 0, and the PV MFMAs of half 0 beside the exp /
+  // cvt VALU of half 1 (sched_group_barrier interleave: one MFMA, then its share of VALU and LDS
+  // reads), so the softmax no longer sits serially between the two products.
+  auto compute_p = [&](const char* img, int t) {
+    const int ts = t * 64;
+    const bool active = ntok > 0 && ts <= p_hi && (window <= 0 || ts + 63 > p_lo - window);
+    if (!active) return;
+    auto kread = [&](int kb, int ks) {
+      return *reinterpret_cast<const bf16x8_t*>(img + kofs[ks] + kb * 32 * RB);
+    };
+    auto vread = [&](int db, int ks2) {
+      const char* p0 = img + vofs[db][0] + 16 * ks2 * RB;
+      const char* p1 = img + vofs[db][1] + 16 * ks2 * RB;
+      s16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4_t*)p0);
+      s16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4_t*)p1);
+      return __builtin_bit_cast(bf16x8_t, s16x8_t{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]});
+    };
+    const bool need_mask = (ts + 63 > p_lo) || (window > 0 && ts <= p_hi - window);
+    auto mask = [&](f32x16_t& x, int kb) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int key = ts + 32 * kb + (r & 3) + 8 * (r >> 2) + 4 * h;
+        bool ok = key <= qp;
+        if (window > 0) ok = ok && key > qp - window;
+        x[r] = ok ? x[r] : NEG_INF;
+      }
+    };
+    // S^T half 0, with the half-1 K fragments read beside it
+    bf16x8_t k0[8], k1[8];
+#pragma unroll
+    for (int ks = 0; ks < 8; ++ks) k0[ks] = kread(0, ks);
+    f32x16_t s0, s1;
+#pragma unroll
+    for (int ks = 0; ks < 8; ++ks) {
+      s0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(k0[ks], qf[ks], ks == 0 ? f32x16_t{} : s0, 0, 0, 0);
+      k1[ks] = kread(1, ks);
+    }
+    if (need_mask) mask(s0, 0);
+    // region A: S^T half 1 beside the max of half 0 and the half-0 V fragment reads
+    bf16x8_t v0[8];
+    float mx = NEG_INF;
+#pragma unroll
+    for (int ks = 0; ks < 8; ++ks) {
+      s1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(k1[ks], qf[ks], ks == 0 ? f32x16_t{} : s1, 0, 0, 0);
+      mx = fmaxf(mx, fmaxf(s0[2 * ks], s0[2 * ks + 1]));
+      v0[ks] = vread(ks >> 1, ks & 1);
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
+      __builtin_amdgcn_sched_group_barrier(0x002, 1, 0);  // VALU
+      __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);  // DS read
+    }
+    if (need_mask) mask(s1, 1);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) mx = fmaxf(mx, s1[r]);
+    {
+      const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(mx), __float_as_uint(mx), false, false);
+      mx = fmaxf(__uint_as_float(sw[0]), __uint_as_float(sw[1]));
+    }
+    const float mt = mx * scale_log2;
+    if (__ballot(mt > m + 8.f) != 0) {
+      const float mnew = fmaxf(m, mt);
+      const float alpha = (mnew == NEG_INF) ? 1.f : __builtin_amdgcn_exp2f(m - mnew);
+      lsum *= alpha;
+      m = mnew;
+#pragma unroll
+      for (int db = 0; db < 4; ++db) o[db] *= alpha;
+    }
+    const float msub = (m == NEG_INF) ? 0.f : m;
+    float ps = 0.f;
+    bf16x8_t p0[2], p1[2];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const float p = __builtin_amdgcn_exp2f(fmaf(s0[r], scale_log2, -msub));
+      ps += p;
+      p0[r >> 3][r & 7] = (__bf16)p;
+    }
+    // region B: PV half 0 beside the exp / cvt of half 1 and the half-1 V fragment reads
+    bf16x8_t v1[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int db = j >> 1, s2 = j & 1;
+      o[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(v0[j], p0[s2], o[db], 0, 0, 0);
+      v1[j] = vread(db, 2 + s2);
+#pragma unroll
+      for (int r = 2 * j; r < 2 * j + 2; ++r) {
+        const float p = __builtin_amdgcn_exp2f(fmaf(s1[r], scale_log2, -msub));
+        ps += p;
+        p1[r >> 3][r & 7] = (__bf16)p;
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 1);  // MFMA
+      __builtin_amdgcn_sched_group_barrier(0x002, 6, 1);  // VALU
+      __builtin_amdgcn_sched_group_barrier(0x100, 2, 1);  // DS read
+    }
+    lsum += ps;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int db = j >> 1, s2 = j & 1;
+      o[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(v1[j], p1[s2], o[db], 0, 0, 0);
+    }
+  };
+
   issue(buf0, t_first);
   for (int t = t_first; t <= t_last; t += 2) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (t + 1 <= t_last) issue(buf1, t + 1);
-    compute(buf0, t);
+    if constexpr (V4 & 4) compute_p(buf0, t); else compute(buf0, t);
     if (t + 1 > t_last) break;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (t + 2 <= t_last) issue(buf0, t + 2);
-    compute(buf1, t + 1);
+    if constexpr (V4 & 4) compute_p(buf1, t + 1); else compute(buf1, t + 1);
   }
 
   if (ntok == 0) return;
@@ -1275,8 +1382,9 @@ extern "C" int llmd_paged_prefill(const void* q, int64_t q_stride, const void* k
                        items, Hq, Hkv, G, scale_log2, window, sinks, (uint16_t*)out, out_stride, v_scale,
                        xcd_map && (int64_t)n_items * grid3.y >= 1024 ? 1 : 0);
   } else if (D == 128 && !fp8 && bs >= 16 && !v1_only && prefill_v4_on()) {
-    const char* e4 = getenv("LLMD_PREFILL_V4_VARIANT");  // 1: builtin DMA, 3: asm DMA
-    auto kern4 = (e4 && e4[0] == '1') ? prefill_v4_kernel<1> : prefill_v4_kernel<3>;
+    const char* e4 = getenv("LLMD_PREFILL_V4_VARIANT");  // 1: builtin DMA, 3: asm DMA, 7: asm DMA + pipelined halves
+    auto kern4 = (e4 && e4[0] == '1') ? prefill_v4_kernel<1> : (e4 && e4[0] == '7') ? prefill_v4_kernel<7>
+                                                                                     : prefill_v4_kernel<3>;
     hipLaunchKernelGGL(kern4, grid, blk, 0, st, (const uint16_t*)q, q_stride, (const uint16_t*)kc,
                        (const uint16_t*)vc, block_stride, bs, block_tables, bt_stride, q_start, q_len, ctx_len,
                        items, Hq, Hkv, G, HPW, scale_log2, window, sinks, (uint16_t*)out, out_stride, v_scale,
