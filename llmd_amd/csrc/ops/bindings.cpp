@@ -92,10 +92,10 @@ int llmd_moe_gemm3_fp8(const void*, int64_t, const float*, int64_t, int, const i
                        void*, int64_t, float*, int64_t, hipStream_t);
 int llmd_moe_gemm3_tile_m();
 int llmd_moe_gemm4_bf16(const void*, int64_t, int, const int*, const int*, int, const void*, int64_t, int, int, void*,
-                        int64_t, int, int, float, float, int, const void*, int64_t, hipStream_t);
+                        int64_t, int, int, float, float, int, const void*, int64_t, int, hipStream_t);
 int llmd_moe_gemm4_fp8(const void*, int64_t, const float*, int64_t, int, const int*, const int*, int, const void*,
                        int64_t, const float*, int, int, void*, int64_t, int, int, float, float, int, const void*,
-                       int64_t, hipStream_t);
+                       int64_t, int, hipStream_t);
 int llmd_moe_gemm3_bf16(const void*, int64_t, int, const int*, const int*, int, const void*, int64_t, int, int, void*,
                         int64_t, int, int, float, float, int, const void*, hipStream_t);
 int llmd_symm_alloc(size_t, void**);
@@ -735,7 +735,7 @@ void moe_align(torch::Tensor ids, int64_t E, torch::Tensor sorted_ids, torch::Te
   CHECK_CUDA(ids); CHECK_DT(ids, at::kInt); CHECK_DT(sorted_ids, at::kInt); CHECK_DT(tile_expert, at::kInt);
   const int n = ids.numel();
   const int bm = tile_m > 0 ? (int)tile_m : llmd_moe_gemm_tile_m();
-  TORCH_CHECK(bm == llmd_moe_gemm_tile_m() || bm == llmd_moe_gemm3_tile_m(), "moe_align: tile_m");
+  TORCH_CHECK(bm == llmd_moe_gemm_tile_m() || bm == llmd_moe_gemm3_tile_m() || bm == 192, "moe_align: tile_m");
   const int max_p = sorted_ids.numel();
   TORCH_CHECK(max_p % bm == 0 && max_p >= n + E * (bm - 1), "sorted_ids too small");
   TORCH_CHECK(tile_expert.numel() >= max_p / bm && expert_offsets.numel() >= E + 1 && inv.numel() >= n,
@@ -784,13 +784,14 @@ void moe_gemm(torch::Tensor X, int64_t topk, torch::Tensor sorted_ids, torch::Te
 // bf16 grouped GEMM v4 (csrc/ops/moe4.hip) on the 256-row expert tiles of moe_align(bm = 256)
 void moe_gemm4(torch::Tensor X, int64_t topk, torch::Tensor sorted_ids, torch::Tensor tile_expert, torch::Tensor W,
                torch::Tensor Y, int64_t mode, int64_t act, double alpha, double limit, bool a_rows_are_slots,
-               c10::optional<torch::Tensor> bias) {
+               c10::optional<torch::Tensor> bias, int64_t tile_m) {
   const c10::hip::OptionalHIPGuard device_guard(dev_of(X));
   CHECK_CUDA(X); CHECK_BF16(X); CHECK_BF16(W); CHECK_BF16(Y); CHECK_INNER(X); CHECK_INNER(Y);
   TORCH_CHECK(W.dim() == 3 && W.is_contiguous(), "W [E, N, K] contiguous");
   const int N = W.size(1), K = W.size(2);
   TORCH_CHECK(X.size(1) == K && K % 64 == 0, "moe_gemm4: K % 64");
-  const int bm = llmd_moe_gemm3_tile_m();
+  TORCH_CHECK(tile_m == 256 || tile_m == 192, "moe_gemm4: tile_m 256 or 192");
+  const int bm = (int)tile_m;
   const int P = sorted_ids.numel();
   TORCH_CHECK(P % bm == 0 && tile_expert.numel() >= P / bm && Y.size(0) >= P, "moe_gemm4: rows");
   TORCH_CHECK(Y.size(1) >= (mode == 1 ? N / 2 : N), "moe_gemm4: Y width");
@@ -804,25 +805,27 @@ void moe_gemm4(torch::Tensor X, int64_t topk, torch::Tensor sorted_ids, torch::T
   const int rc = llmd_moe_gemm4_bf16(X.data_ptr(), X.stride(0), topk, sorted_ids.data_ptr<int>(),
                                      tile_expert.data_ptr<int>(), P / bm, W.data_ptr(), W.stride(0), N, K,
                                      Y.data_ptr(), Y.stride(0), mode, act, (float)alpha, (float)limit,
-                                     a_rows_are_slots ? 1 : 0, bp, X.size(0), cur_stream());
+                                     a_rows_are_slots ? 1 : 0, bp, X.size(0), bm, cur_stream());
   TORCH_CHECK(rc == 0, "moe_gemm4 failed: ", rc);
 }
 
 // block-fp8 grouped GEMM v4 (csrc/ops/moe4.hip) on 256-row expert tiles: power-of-two scales, K % 128 == 0
 void moe_gemm4_fp8(torch::Tensor X, torch::Tensor xs, int64_t topk, torch::Tensor sorted_ids,
                    torch::Tensor tile_expert, torch::Tensor W, torch::Tensor ws, torch::Tensor Y, int64_t mode,
-                   int64_t act, double alpha, double limit, bool a_rows_are_slots, c10::optional<torch::Tensor> bias) {
+                   int64_t act, double alpha, double limit, bool a_rows_are_slots, c10::optional<torch::Tensor> bias,
+                   int64_t tile_m) {
   const c10::hip::OptionalHIPGuard device_guard(dev_of(X));
   CHECK_CUDA(X); CHECK_DT(X, at::kFloat8_e4m3fn); CHECK_DT(W, at::kFloat8_e4m3fn); CHECK_BF16(Y);
   CHECK_INNER(X); CHECK_INNER(Y); CHECK_DT(xs, at::kFloat); CHECK_DT(ws, at::kFloat);
   TORCH_CHECK(W.dim() == 3 && W.is_contiguous() && ws.is_contiguous(), "W [E, N, K] / ws contiguous");
   const int E = W.size(0), N = W.size(1), K = W.size(2);
   TORCH_CHECK(X.size(1) == K && K % 128 == 0 && K / 128 <= 64 && X.stride(0) % 16 == 0, "moe_gemm4_fp8: K");
+  TORCH_CHECK(tile_m == 256 || tile_m == 192, "moe_gemm4_fp8: tile_m 256 or 192");
   TORCH_CHECK(ws.dim() == 3 && ws.size(0) == E && ws.size(1) == (N + 127) / 128 && ws.size(2) == K / 128,
               "ws [E, ceil(N/128), K/128]");
   TORCH_CHECK(xs.dim() == 2 && xs.size(0) >= X.size(0) && xs.size(1) >= K / 128 && xs.stride(1) == 1,
               "xs [rows, K/128]");
-  const int bm = llmd_moe_gemm3_tile_m();
+  const int bm = (int)tile_m;
   const int P = sorted_ids.numel();
   TORCH_CHECK(P % bm == 0 && tile_expert.numel() >= P / bm && Y.size(0) >= P, "moe_gemm4_fp8: rows");
   TORCH_CHECK(Y.size(1) >= (mode == 1 ? N / 2 : N) && Y.stride(0) % 8 == 0, "moe_gemm4_fp8: Y width");
@@ -835,7 +838,8 @@ void moe_gemm4_fp8(torch::Tensor X, torch::Tensor xs, int64_t topk, torch::Tenso
   const int rc = llmd_moe_gemm4_fp8(X.data_ptr(), X.stride(0), xs.data_ptr<float>(), xs.stride(0), topk,
                                     sorted_ids.data_ptr<int>(), tile_expert.data_ptr<int>(), P / bm, W.data_ptr(),
                                     W.stride(0), ws.data_ptr<float>(), N, K, Y.data_ptr(), Y.stride(0), mode, act,
-                                    (float)alpha, (float)limit, a_rows_are_slots ? 1 : 0, bp, X.size(0), cur_stream());
+                                    (float)alpha, (float)limit, a_rows_are_slots ? 1 : 0, bp, X.size(0), bm,
+                                    cur_stream());
   TORCH_CHECK(rc == 0, "moe_gemm4_fp8 failed: ", rc);
 }
 
@@ -1102,9 +1106,13 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {  // _C, or _C_debug (llmd_amd/build.p
         py::arg("hq") = py::none(), py::arg("hs") = py::none());
   m.def("moe_tile_m_prefill", &llmd_moe_gemm3_tile_m);
   m.def("symm_alloc", &symm_alloc);
-  m.def("moe_gemm4", &moe_gemm4);
+  m.def("moe_gemm4", &moe_gemm4, py::arg("X"), py::arg("topk"), py::arg("sorted_ids"), py::arg("tile_expert"),
+        py::arg("W"), py::arg("Y"), py::arg("mode"), py::arg("act"), py::arg("alpha"), py::arg("limit"),
+        py::arg("a_rows_are_slots"), py::arg("bias"), py::arg("tile_m") = 256);
   m.def("mgemm_silu", &mgemm_silu);
-  m.def("moe_gemm4_fp8", &moe_gemm4_fp8);
+  m.def("moe_gemm4_fp8", &moe_gemm4_fp8, py::arg("X"), py::arg("xs"), py::arg("topk"), py::arg("sorted_ids"),
+        py::arg("tile_expert"), py::arg("W"), py::arg("ws"), py::arg("Y"), py::arg("mode"), py::arg("act"),
+        py::arg("alpha"), py::arg("limit"), py::arg("a_rows_are_slots"), py::arg("bias"), py::arg("tile_m") = 256);
   m.def("symm_error", &symm_error);
   m.def("symm_host_err", &symm_host_err);
   m.def("symm_sig_bytes", &llmd_symm_sig_bytes);

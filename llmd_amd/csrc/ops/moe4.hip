@@ -53,17 +53,30 @@ __device__ __forceinline__ float m4_act(float g, float u, int act, float alpha, 
   return g / (1.f + __expf(-g)) * u;
 }
 
-template <int MODE>
+// TBM: expert-tile rows, 256 or 192 (gpt-oss: ~160 rows per expert at a 5120-token step, so a
+// 256-row tile is 62 % useful rows, a 192-row one 83 %). A wave owns TBM / 2 rows x 128 columns:
+// MI = TBM / 32 A fragments of 16 rows; A DMA pieces per wave = MI, W pieces 8.
+template <int MODE, int TBM = 256>
 __global__ __launch_bounds__(M4_NT, 1) void moe_gemm4_bf16_kernel(
     const uint16_t* __restrict__ X, int64_t x_stride, int topk, const int* __restrict__ sorted_ids,
     const int* __restrict__ tile_expert, const uint16_t* __restrict__ W, int64_t w_expert_stride, int N, int K,
     uint16_t* __restrict__ Y, int64_t y_stride, int act, float alpha, float limit, int a_rows_are_slots,
     const uint16_t* __restrict__ bias) {
-  __shared__ __attribute__((aligned(1024))) char lds[2 * M4_BUF];  // the ONLY LDS object
+  constexpr int MI = TBM / 32;             // 16-row A fragments per wave (8 / 6)
+  constexpr int OPA = TBM * M4_BK * 2;     // A bytes per K-step
+  constexpr int BUF = OPA + M4_OPB;        // A | W of one K-step
+  constexpr int NPC = MI + 8;              // DMA pieces per wave per K-step (= fragment reads per half)
+  constexpr int NMF = 8 * MI;              // MFMAs per half
+  constexpr int TB = 8 * MI - 24;          // half 0: barrier MFMA index (A pieces of step kt + 2 after it)
+  constexpr int WP = MI == 8 ? 5 : 4;      // half 1: one W piece every WP MFMAs
+  constexpr int RB = MI == 8 ? M4_RB : 30; // half 1: first next-step read
+  static_assert(TBM == 256 || TBM == 192, "tile rows");
+  static_assert(TB + 1 + 3 * (MI - 1) < NMF && 8 + MI <= TB && 7 * WP < RB - 1 && RB + NPC <= NMF, "schedule");
+  __shared__ __attribute__((aligned(1024))) char lds[2 * BUF];  // the ONLY LDS object
   const int nt_ = blockIdx.x, mt = blockIdx.y;
   const int e = tile_expert[mt];
   if (e < 0) return;
-  const int m0 = mt * M4_BM, n0 = nt_ * M4_BN;
+  const int m0 = mt * TBM, n0 = nt_ * M4_BN;
   const int nk = K / M4_BK;
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -72,44 +85,50 @@ __global__ __launch_bounds__(M4_NT, 1) void moe_gemm4_bf16_kernel(
   const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc((void*)X, 0, 0x7fffffff, 0x00020000);
   const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc(
       (void*)(W + (int64_t)e * w_expert_stride), 0, 0x7fffffff, 0x00020000);
-  // DMA piece j of this wave: tile rows 64 w + 8 j + (lane >> 3); LDS slot lane & 7 <- chunk (lane & 7) ^ f(row)
-  uint32_t va[8], vw[8];
+  // DMA piece j: A rows 8 (MI w + j) + (lane >> 3), W rows 64 w + 8 j + (lane >> 3);
+  // LDS slot lane & 7 <- chunk (lane & 7) ^ f(row)
+  uint32_t va[MI], vw[8];
 #pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    const int row = 64 * w + 8 * j + (lane >> 3);
+  for (int j = 0; j < MI; ++j) {
+    const int row = 8 * (MI * w + j) + (lane >> 3);
     const int c = (lane & 7) ^ ((row >> 1) & 7);
     const int sid = sorted_ids[m0 + row];
     const int tok = sid < 0 ? 0 : (a_rows_are_slots ? m0 + row : sid / topk);
     va[j] = (uint32_t)(((int64_t)tok * x_stride + c * 8) * 2);
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int row = 64 * w + 8 * j + (lane >> 3);
+    const int c = (lane & 7) ^ ((row >> 1) & 7);
     vw[j] = (uint32_t)(((int64_t)min(n0 + row, N - 1) * K + c * 8) * 2);
   }
   auto dma = [&](int kt, int j, bool wop) {
     const uint32_t so = (uint32_t)(min(kt, nk - 1) * M4_BK * 2);
-    char* dst = lds + (kt & 1) * M4_BUF + (wop ? M4_OPB : 0) + (8 * w + j) * 1024;
+    char* dst = lds + (kt & 1) * BUF + (wop ? OPA + (8 * w + j) * 1024 : (MI * w + j) * 1024);
     __builtin_amdgcn_raw_ptr_buffer_load_lds(wop ? rw : ra, (__attribute__((address_space(3))) void*)dst, 16,
                                              wop ? vw[j] : va[j], so, 0, 0);
   };
   const int fr = lane & 15, fq = lane >> 4;
   const int rd0 = fr * 128 + ((fq ^ ((fr >> 1) & 7)) * 16);
   const int rd1 = fr * 128 + (((4 + fq) ^ ((fr >> 1) & 7)) * 16);
-  const int a_rd = (wr * 128) * 128, w_rd = M4_OPB + (wc * 128) * 128;
+  const int a_rd = (wr * (TBM / 2)) * 128, w_rd = OPA + (wc * 128) * 128;
 
-  f32x4_t acc[8][8];
+  f32x4_t acc[MI][8];
 #pragma unroll
-  for (int i = 0; i < 8; ++i)
+  for (int i = 0; i < MI; ++i)
 #pragma unroll
     for (int j = 0; j < 8; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-  s16x8_t fa0[8], fw0[8], fa1[8], fw1[8];
+  s16x8_t fa0[MI], fw0[8], fa1[MI], fw1[8];
 
 #pragma unroll
-  for (int j = 0; j < 8; ++j) dma(0, j, false);
+  for (int s2 = 0; s2 < 2; ++s2) {
 #pragma unroll
-  for (int j = 0; j < 8; ++j) dma(0, j, true);
+    for (int j = 0; j < MI; ++j) dma(s2, j, false);
 #pragma unroll
-  for (int j = 0; j < 8; ++j) dma(1, j, false);
-#pragma unroll
-  for (int j = 0; j < 8; ++j) dma(1, j, true);
-  asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+    for (int j = 0; j < 8; ++j) dma(s2, j, true);
+  }
+  if constexpr (NPC == 16) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+  else asm volatile("s_waitcnt vmcnt(14)" ::: "memory");
   m4_bar();
   fa0[0] = *reinterpret_cast<const s16x8_t*>(lds + a_rd + rd0);
   __builtin_amdgcn_sched_barrier(0);
@@ -119,7 +138,7 @@ __global__ __launch_bounds__(M4_NT, 1) void moe_gemm4_bf16_kernel(
     __builtin_amdgcn_sched_barrier(0);
   }
 #pragma unroll
-  for (int i = 1; i < 8; ++i) {
+  for (int i = 1; i < MI; ++i) {
     fa0[i] = *reinterpret_cast<const s16x8_t*>(lds + a_rd + i * 2048 + rd0);
     __builtin_amdgcn_sched_barrier(0);
   }
@@ -129,42 +148,45 @@ __global__ __launch_bounds__(M4_NT, 1) void moe_gemm4_bf16_kernel(
   __builtin_amdgcn_sched_barrier(0);
 
   for (int kt = 0; kt < nk; ++kt) {
-    const char* cur = lds + (kt & 1) * M4_BUF;
-    const char* nxt = lds + ((kt & 1) ^ 1) * M4_BUF;
+    const char* cur = lds + (kt & 1) * BUF;
+    const char* nxt = lds + ((kt & 1) ^ 1) * BUF;
 #pragma unroll
-    for (int t = 0; t < 64; ++t) {
+    for (int t = 0; t < NMF; ++t) {
       const int i = t >> 3, j = t & 7;
-      if (t <= 8) __builtin_amdgcn_s_waitcnt(0xC07F | (14 << 8));
+      // MFMA (0, j) needs the first j + 2 of this set's NPC reads, (1, 0) the first 10; the next
+      // set's reads issued after MFMA 0 .. t - 1 are younger
+      if (t <= 8) __builtin_amdgcn_s_waitcnt(0xC07F | ((NPC - 2) << 8));
       m4_mfma(acc[i][j], fw0[j], fa0[i]);
       if (t == 0) {
         fa1[0] = *reinterpret_cast<const s16x8_t*>(cur + a_rd + rd1);
       } else if (t < 9) {
         fw1[t - 1] = *reinterpret_cast<const s16x8_t*>(cur + w_rd + (t - 1) * 2048 + rd1);
-      } else if (t < 16) {
+      } else if (t < 8 + MI) {
         fa1[t - 8] = *reinterpret_cast<const s16x8_t*>(cur + a_rd + (t - 8) * 2048 + rd1);
-      } else if (t == 40) {
+      } else if (t == TB) {
         __builtin_amdgcn_s_waitcnt(0xC07F);
         m4_bar();
-      } else if (t > 40 && (t - 41) % 3 == 0) {
-        dma(kt + 2, (t - 41) / 3, false);
+      } else if (t > TB && (t - TB - 1) % 3 == 0 && (t - TB - 1) / 3 < MI) {
+        dma(kt + 2, (t - TB - 1) / 3, false);
       }
       __builtin_amdgcn_sched_barrier(0);
     }
 #pragma unroll
-    for (int t = 0; t < 64; ++t) {
+    for (int t = 0; t < NMF; ++t) {
       const int i = t >> 3, j = t & 7;
       m4_mfma(acc[i][j], fw1[j], fa1[i]);
-      if (t < 36 && t % 5 == 0) {
-        dma(kt + 2, t / 5, true);
-      } else if (t == M4_RB - 1) {
-        asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+      if (t < 8 * WP && t % WP == 0) {
+        dma(kt + 2, t / WP, true);
+      } else if (t == RB - 1) {
+        if constexpr (NPC == 16) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(14)" ::: "memory");
         m4_bar();
-      } else if (t == M4_RB) {
+      } else if (t == RB) {
         fa0[0] = *reinterpret_cast<const s16x8_t*>(nxt + a_rd + rd0);
-      } else if (t > M4_RB && t < M4_RB + 9) {
-        fw0[t - M4_RB - 1] = *reinterpret_cast<const s16x8_t*>(nxt + w_rd + (t - M4_RB - 1) * 2048 + rd0);
-      } else if (t >= M4_RB + 9 && t < M4_RB + 16) {
-        fa0[t - M4_RB - 8] = *reinterpret_cast<const s16x8_t*>(nxt + a_rd + (t - M4_RB - 8) * 2048 + rd0);
+      } else if (t > RB && t < RB + 9) {
+        fw0[t - RB - 1] = *reinterpret_cast<const s16x8_t*>(nxt + w_rd + (t - RB - 1) * 2048 + rd0);
+      } else if (t >= RB + 9 && t < RB + 8 + MI) {
+        fa0[t - RB - 8] = *reinterpret_cast<const s16x8_t*>(nxt + a_rd + (t - RB - 8) * 2048 + rd0);
       }
       __builtin_amdgcn_sched_barrier(0);
     }
@@ -177,11 +199,12 @@ __global__ __launch_bounds__(M4_NT, 1) void moe_gemm4_bf16_kernel(
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
   __syncthreads();
 
-  // epilogue: acc[i][j][r] = C[m][n], m = wr*128 + 16 i + (lane & 15), n = wc*128 + 16 j + 4 (lane >> 4) + r
-  char* img = lds + w * 32768;
+  // epilogue: acc[i][j][r] = C[m][n], m = wr*TBM/2 + 16 i + (lane & 15), n = wc*128 + 16 j + 4 (lane >> 4) + r
+  constexpr int WROWS = TBM / 2;
+  char* img = lds + w * (WROWS * 256);
   const int ncol0 = n0 + wc * 128;
 #pragma unroll
-  for (int i = 0; i < 8; ++i)
+  for (int i = 0; i < MI; ++i)
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const int row = 16 * i + fr, col = 16 * j + 4 * fq;
@@ -199,7 +222,7 @@ __global__ __launch_bounds__(M4_NT, 1) void moe_gemm4_bf16_kernel(
         p[1] = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
         *reinterpret_cast<u32x2_t*>(img + row * 256 + (((col >> 3) ^ (row & 15)) * 16) + (col & 7) * 2) = p;
       } else {
-        // two (g, u) pairs -> 2 outputs at half-columns col / 2, col / 2 + 1 of a [128][64] image (128-B rows)
+        // two (g, u) pairs -> 2 outputs at half-columns col / 2, col / 2 + 1 of a [rows][64] image (128-B rows)
         const float o0 = m4_act(v[0], v[1], act, alpha, limit), o1 = m4_act(v[2], v[3], act, alpha, limit);
         const uint32_t p = (uint32_t)f2bf(o0) | ((uint32_t)f2bf(o1) << 16);
         const int hc = col >> 1;  // 0..62, even
@@ -209,18 +232,18 @@ __global__ __launch_bounds__(M4_NT, 1) void moe_gemm4_bf16_kernel(
   __syncthreads();
   if constexpr (MODE == 0) {
 #pragma unroll 4
-    for (int it = 0; it < 32; ++it) {
+    for (int it = 0; it < WROWS / 4; ++it) {
       const int row = it * 4 + (lane >> 4), c = lane & 15;
-      const int p = m0 + wr * 128 + row;
+      const int p = m0 + wr * WROWS + row;
       const int n = ncol0 + c * 8;
       const u32x4_t v = *reinterpret_cast<const u32x4_t*>(img + row * 256 + ((c ^ (row & 15)) * 16));
       if (sorted_ids[p] >= 0 && n < N) *reinterpret_cast<u32x4_t*>(Y + (int64_t)p * y_stride + n) = v;
     }
   } else {
 #pragma unroll 4
-    for (int it = 0; it < 16; ++it) {
+    for (int it = 0; it < WROWS / 8; ++it) {
       const int row = it * 8 + (lane >> 3), c = lane & 7;
-      const int p = m0 + wr * 128 + row;
+      const int p = m0 + wr * WROWS + row;
       const int n = ncol0 / 2 + c * 8;
       const u32x4_t v = *reinterpret_cast<const u32x4_t*>(img + row * 128 + ((c ^ (row & 7)) * 16));
       if (sorted_ids[p] >= 0 && 2 * n < N) *reinterpret_cast<u32x4_t*>(Y + (int64_t)p * y_stride + n) = v;
@@ -241,11 +264,6 @@ __global__ __launch_bounds__(M4_NT, 1) void moe_gemm4_bf16_kernel(
 // consecutive N columns (one (g, u) pair per two). Activation scales ride the
 // LDS-DMA (one 4-B piece per wave per step: 17 pieces, counted vmcnt(17)); the
 // tile's weight scales are DMA'd once in the prologue.
-constexpr int M8_S = 256 * 4;                        // act scales of one K-step
-constexpr int M8_BUF = 2 * M4_OPB + M8_S;            // 66560 B
-constexpr int M8_WS = 2 * M8_BUF;                    // weight scales [2 col blocks][64 k-blocks]
-constexpr int M8_LDS = M8_WS + 2 * 64 * 4;
-
 typedef int i32x8_t __attribute__((ext_vector_type(8)));
 typedef float f32x16_t __attribute__((ext_vector_type(16)));
 
@@ -254,17 +272,31 @@ __device__ __forceinline__ void m8_mfma(f32x16_t& acc, const i32x8_t& a, const i
                : "+a"(acc) : "v"(a), "v"(b), "v"(sa), "v"(sb));
 }
 
-template <int MODE>
+// TBM 256 or 192 (as the bf16 form): a wave owns TBM / 2 rows = MB 32-row blocks (4 / 3); A DMA pieces
+// per wave MB * 2 (8 / 6), act-scale piece: rows TBM / 4 * w + lane (clamped; 192: lanes 48-63 re-write
+// the next wave's first rows with the same values).
+template <int MODE, int TBM = 256>
 __global__ __launch_bounds__(M4_NT, 1) void moe_gemm4_fp8_kernel(
     const uint8_t* __restrict__ X, int64_t x_stride, const float* __restrict__ xs, int64_t xs_stride, int topk,
     const int* __restrict__ sorted_ids, const int* __restrict__ tile_expert, const uint8_t* __restrict__ W,
     int64_t w_expert_stride, const float* __restrict__ ws, int N, int K, uint16_t* __restrict__ Y,
     int64_t y_stride, int act, float alpha, float limit, int a_rows_are_slots, const uint16_t* __restrict__ bias) {
-  __shared__ __attribute__((aligned(1024))) char lds[M8_LDS];  // the ONLY LDS object
+  constexpr int MB = TBM / 64;                 // 32-row A blocks per wave
+  constexpr int NA = 2 * MB;                   // A DMA pieces per wave per K-step
+  constexpr int OPA = TBM * 128;               // A bytes per K-step (128 fp8 per row)
+  constexpr int SCB = TBM * 4 + 256;           // act scales of a K-step (+ the 192 form's overhang)
+  constexpr int BUF = OPA + M4_OPB + SCB;
+  constexpr int WSO = 2 * BUF;                 // weight scales [2 col blocks][64 k-blocks]
+  constexpr int LDSB = WSO + 2 * 64 * 4;
+  constexpr int NPC = NA + 8 + 1;              // DMA pieces per wave per K-step (17 / 15)
+  constexpr int NMF = 4 * MB;                  // MFMAs per k-substep
+  constexpr int SROWS = TBM / 4;               // act-scale rows per wave
+  static_assert(TBM == 256 || TBM == 192, "tile rows");
+  __shared__ __attribute__((aligned(1024))) char lds[LDSB];  // the ONLY LDS object
   const int nt_ = blockIdx.x, mt = blockIdx.y;
   const int e = tile_expert[mt];
   if (e < 0) return;
-  const int m0 = mt * M4_BM, n0 = nt_ * M4_BN;
+  const int m0 = mt * TBM, n0 = nt_ * M4_BN;
   const int nk = K / 128, nnb = (N + 127) / 128;
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -275,32 +307,37 @@ __global__ __launch_bounds__(M4_NT, 1) void moe_gemm4_fp8_kernel(
   const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)xs, 0, 0x7fffffff, 0x00020000);
   const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc(
       (void*)(W + (int64_t)e * w_expert_stride), 0, 0x7fffffff, 0x00020000);
-  uint32_t va[8], vw[8];
+  uint32_t va[NA], vw[8];
 #pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    const int row = 64 * w + 8 * j + (lane >> 3);
+  for (int j = 0; j < NA; ++j) {
+    const int row = 8 * (NA * w + j) + (lane >> 3);
     const int c = (lane & 7) ^ ((row >> 1) & 7);
     const int sid = sorted_ids[m0 + row];
     const int tok = sid < 0 ? 0 : (a_rows_are_slots ? m0 + row : sid / topk);
     va[j] = (uint32_t)((int64_t)tok * x_stride + c * 16);
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int row = 64 * w + 8 * j + (lane >> 3);
+    const int c = (lane & 7) ^ ((row >> 1) & 7);
     vw[j] = (uint32_t)((int64_t)min(n0 + row, N - 1) * K + c * 16);
   }
-  uint32_t vs;  // this lane's act-scale row 64 w + lane
+  uint32_t vs;  // this lane's act-scale row SROWS w + lane (clamped to the tile)
   {
-    const int row = 64 * w + lane;
+    const int row = min(SROWS * w + lane, TBM - 1);
     const int sid = sorted_ids[m0 + row];
     const int tok = sid < 0 ? 0 : (a_rows_are_slots ? m0 + row : sid / topk);
     vs = (uint32_t)((int64_t)tok * xs_stride * 4);
   }
   auto dma = [&](int kt, int j, int op) {  // op 0 = A piece j, 1 = W piece j, 2 = act scales
     const int kc = min(kt, nk - 1);
-    char* buf = lds + (kt & 1) * M8_BUF;
+    char* buf = lds + (kt & 1) * BUF;
     if (op == 2)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)(buf + 2 * M4_OPB + w * 256),
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)(buf + OPA + M4_OPB + w * SROWS * 4),
                                                4, vs, (uint32_t)(kc * 4), 0, 0);
     else
       __builtin_amdgcn_raw_ptr_buffer_load_lds(op ? rw : ra,
-                                               (__attribute__((address_space(3))) void*)(buf + op * M4_OPB + (8 * w + j) * 1024),
+                                               (__attribute__((address_space(3))) void*)(buf + (op ? OPA + (8 * w + j) * 1024 : (NA * w + j) * 1024)),
                                                16, op ? vw[j] : va[j], (uint32_t)(kc * 128), 0, 0);
   };
   // fragment of 32-row block b, k-substep s: lane row 32 b + l32, chunks 4 s + 2 h and 4 s + 2 h + 1
@@ -312,35 +349,37 @@ __global__ __launch_bounds__(M4_NT, 1) void moe_gemm4_fp8_kernel(
     const u32x4_t hi = *reinterpret_cast<const u32x4_t*>(rp + (((4 * s + 2 * h + 1) ^ f) * 16));
     return i32x8_t{(int)lo[0], (int)lo[1], (int)lo[2], (int)lo[3], (int)hi[0], (int)hi[1], (int)hi[2], (int)hi[3]};
   };
-  const int a_base = wr * 128 * 128, w_base = M4_OPB + wc * 128 * 128;
+  const int a_base = wr * (TBM / 2) * 128, w_base = OPA + wc * 128 * 128;
+  const int s_base = OPA + M4_OPB + wr * (TBM / 2) * 4;
 
-  f32x16_t acc[4][4];  // [W n-block j][A m-block i]
+  f32x16_t acc[4][MB];  // [W n-block j][A m-block i]
 #pragma unroll
   for (int j = 0; j < 4; ++j)
 #pragma unroll
-    for (int i = 0; i < 4; ++i) acc[j][i] = f32x16_t{};
-  i32x8_t fw0[4], fa0[4], fw1[4], fa1[4];
-  int sa[4];  // E8M0 act scales of this lane's token column in each m-block (current step)
-  int swt;    // E8M0 weight scale of this wave's 128-column block (current step)
-  float nsf[4], nwf;  // the next step's raw scales
+    for (int i = 0; i < MB; ++i) acc[j][i] = f32x16_t{};
+  i32x8_t fw0[4], fa0[MB], fw1[4], fa1[MB];
+  int sa[MB];  // E8M0 act scales of this lane's token column in each m-block (current step)
+  int swt;     // E8M0 weight scale of this wave's 128-column block (current step)
+  float nsf[MB], nwf;  // the next step's raw scales
 
   // prologue: the tile's weight scales (waves 0 / 1: column blocks n0 / 128 + 0 / 1), steps 0 and 1
   if (w < 2) {
     const int cb = min(n0 / 128 + w, nnb - 1);
     const __amdgpu_buffer_rsrc_t rws = __builtin_amdgcn_make_buffer_rsrc(
         (void*)(ws + ((int64_t)e * nnb + cb) * nk), 0, 0x7fffffff, 0x00020000);
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(rws, (__attribute__((address_space(3))) void*)(lds + M8_WS + w * 256), 4,
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rws, (__attribute__((address_space(3))) void*)(lds + WSO + w * 256), 4,
                                              (uint32_t)(min(lane, nk - 1) * 4), 0, 0, 0);
   }
 #pragma unroll
   for (int s = 0; s < 2; ++s) {
 #pragma unroll
-    for (int j = 0; j < 8; ++j) dma(s, j, 0);
+    for (int j = 0; j < NA; ++j) dma(s, j, 0);
 #pragma unroll
     for (int j = 0; j < 8; ++j) dma(s, j, 1);
     dma(s, 0, 2);
   }
-  asm volatile("s_waitcnt vmcnt(17)" ::: "memory");  // step 0 (and the weight scales) landed
+  if constexpr (NPC == 17) asm volatile("s_waitcnt vmcnt(17)" ::: "memory");  // step 0 (and the weight scales) landed
+  else asm volatile("s_waitcnt vmcnt(15)" ::: "memory");
   m4_bar();
 #pragma unroll
   for (int b = 0; b < 4; ++b) {
@@ -348,71 +387,88 @@ __global__ __launch_bounds__(M4_NT, 1) void moe_gemm4_fp8_kernel(
     __builtin_amdgcn_sched_barrier(0);
   }
 #pragma unroll
-  for (int b = 0; b < 4; ++b) {
+  for (int b = 0; b < MB; ++b) {
     fa0[b] = frag(lds + a_base, b, 0);
     __builtin_amdgcn_sched_barrier(0);
   }
 #pragma unroll
-  for (int b = 0; b < 4; ++b)
-    sa[b] = e8m0_of(*reinterpret_cast<const float*>(lds + 2 * M4_OPB + (wr * 128 + 32 * b + l32) * 4));
-  swt = e8m0_of(*reinterpret_cast<const float*>(lds + M8_WS + wc * 256));
+  for (int b = 0; b < MB; ++b) sa[b] = e8m0_of(*reinterpret_cast<const float*>(lds + s_base + (32 * b + l32) * 4));
+  swt = e8m0_of(*reinterpret_cast<const float*>(lds + WSO + wc * 256));
   __builtin_amdgcn_s_waitcnt(0xC07F);
   __builtin_amdgcn_sched_barrier(0);
   asm volatile("s_nop 4" ::: "memory");
   __builtin_amdgcn_sched_barrier(0);
 
   for (int kt = 0; kt < nk; ++kt) {
-    const char* cur = lds + (kt & 1) * M8_BUF;
-    const char* nxt = lds + ((kt & 1) ^ 1) * M8_BUF;
-    // half 0 (k-substep 0): 16 MFMA; reads of substep 1 (W then A, 2 ds_read_b128 per fragment) after
-    // MFMA 0-7; barrier after MFMA 9; A pieces + the act-scale piece of step kt + 2 after MFMA 10-15
+    const char* cur = lds + (kt & 1) * BUF;
+    const char* nxt = lds + ((kt & 1) ^ 1) * BUF;
+    // half 0 (k-substep 0): NMF MFMAs; reads of substep 1 (W then A) after the first 4 + MB; barrier
+    // after them; A pieces (two per 64-cycle MFMA gap) + the act-scale piece of step kt + 2 to the end
 #pragma unroll
-    for (int t = 0; t < 16; ++t) {
-      const int j = t >> 2, i = t & 3;
+    for (int t = 0; t < NMF; ++t) {
+      const int j = t / MB, i = t % MB;
       m8_mfma(acc[j][i], fw0[j], fa0[i], swt, sa[i]);
       if (t < 4) {
         fw1[t] = frag(cur + w_base, t, 1);
-      } else if (t < 8) {
+      } else if (t < 4 + MB) {
         fa1[t - 4] = frag(cur + a_base, t - 4, 1);
-      } else if (t == 9) {
+      } else if (t == 4 + MB + 1) {
         __builtin_amdgcn_s_waitcnt(0xC07F);
         m4_bar();
-      } else if (t >= 10 && t < 14) {  // A pieces 0-7, two per MFMA gap (64-cycle MFMAs)
-        dma(kt + 2, 2 * (t - 10), 0);
-        dma(kt + 2, 2 * (t - 10) + 1, 0);
-      } else if (t == 14) {
-        dma(kt + 2, 0, 2);  // the act-scale piece: 17 DMA per wave per step
+      } else if (t > 4 + MB + 1 && t < 4 + MB + 2 + MB) {  // MB gaps x 2 A pieces
+        const int q = t - (4 + MB + 2);
+        dma(kt + 2, 2 * q, 0);
+        dma(kt + 2, 2 * q + 1, 0);
+        if (4 + 2 * MB + 2 >= NMF && t == NMF - 1) dma(kt + 2, 0, 2);  // 192 rows: the act-scale piece here
+      } else if (t == 4 + 2 * MB + 2) {
+        dma(kt + 2, 0, 2);  // the act-scale piece
       }
       __builtin_amdgcn_sched_barrier(0);
     }
-    // half 1 (k-substep 1): W pieces after MFMA 0-7; step kt+1 landed (vmcnt 17) + barrier after
-    // MFMA 8; its substep-0 fragments and scales after MFMA 9-15
+    // half 1 (k-substep 1): W pieces of step kt + 2 after MFMA 0-7; step kt+1 landed + barrier after
+    // MFMA 8; its substep-0 fragments and scales after
 #pragma unroll
-    for (int t = 0; t < 16; ++t) {
-      const int j = t >> 2, i = t & 3;
+    for (int t = 0; t < NMF; ++t) {
+      const int j = t / MB, i = t % MB;
       m8_mfma(acc[j][i], fw1[j], fa1[i], swt, sa[i]);
       if (t < 8) {
         dma(kt + 2, t, 1);
       } else if (t == 8) {
-        asm volatile("s_waitcnt vmcnt(17)" ::: "memory");
+        if constexpr (NPC == 17) asm volatile("s_waitcnt vmcnt(17)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(15)" ::: "memory");
         m4_bar();
-      } else if (t < 13) {
+      } else if constexpr (MB == 4) {  // 16 MFMAs: one W fragment per gap, then A pairs
         if (t == 9) {  // the next step's raw scales, early (converted after the last MFMA)
 #pragma unroll
-          for (int b = 0; b < 4; ++b)
-            nsf[b] = *reinterpret_cast<const float*>(nxt + 2 * M4_OPB + (wr * 128 + 32 * b + l32) * 4);
-          nwf = *reinterpret_cast<const float*>(lds + M8_WS + wc * 256 + min(kt + 1, nk - 1) * 4);
+          for (int b = 0; b < MB; ++b) nsf[b] = *reinterpret_cast<const float*>(nxt + s_base + (32 * b + l32) * 4);
+          nwf = *reinterpret_cast<const float*>(lds + WSO + wc * 256 + min(kt + 1, nk - 1) * 4);
         }
-        fw0[t - 9] = frag(nxt + w_base, t - 9, 0);
-      } else if (t < 15) {
-        fa0[2 * (t - 13)] = frag(nxt + a_base, 2 * (t - 13), 0);
-        fa0[2 * (t - 13) + 1] = frag(nxt + a_base, 2 * (t - 13) + 1, 0);
+        if (t >= 9 && t < 13) {
+          fw0[t - 9] = frag(nxt + w_base, t - 9, 0);
+        } else if (t >= 13 && t < 15) {
+          fa0[2 * (t - 13)] = frag(nxt + a_base, 2 * (t - 13), 0);
+          fa0[2 * (t - 13) + 1] = frag(nxt + a_base, 2 * (t - 13) + 1, 0);
+        }
+      } else {  // 12 MFMAs: the next set in the last three gaps
+        if (t == 9) {
+#pragma unroll
+          for (int b = 0; b < MB; ++b) nsf[b] = *reinterpret_cast<const float*>(nxt + s_base + (32 * b + l32) * 4);
+          nwf = *reinterpret_cast<const float*>(lds + WSO + wc * 256 + min(kt + 1, nk - 1) * 4);
+          fw0[0] = frag(nxt + w_base, 0, 0);
+          fw0[1] = frag(nxt + w_base, 1, 0);
+        } else if (t == 10) {
+          fw0[2] = frag(nxt + w_base, 2, 0);
+          fw0[3] = frag(nxt + w_base, 3, 0);
+        } else if (t == 11) {
+#pragma unroll
+          for (int b = 0; b < MB; ++b) fa0[b] = frag(nxt + a_base, b, 0);
+        }
       }
       __builtin_amdgcn_sched_barrier(0);
     }
     // the next step's scales (swapped in after this step's last MFMA used the current ones)
 #pragma unroll
-    for (int b = 0; b < 4; ++b) sa[b] = e8m0_of(nsf[b]);
+    for (int b = 0; b < MB; ++b) sa[b] = e8m0_of(nsf[b]);
     swt = e8m0_of(nwf);
     // drain inside the last iteration (see the bf16 form): 16-pass MFMAs
     if (kt + 1 == nk) asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
@@ -422,13 +478,14 @@ __global__ __launch_bounds__(M4_NT, 1) void moe_gemm4_fp8_kernel(
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
   __syncthreads();
 
-  // epilogue: acc[j][i][4 g + q] = C[m][n], m = wr*128 + 32 i + l32, n = wc*128 + 32 j + 8 g + 4 h + q
-  char* img = lds + w * 32768;
+  // epilogue: acc[j][i][4 g + q] = C[m][n], m = wr*TBM/2 + 32 i + l32, n = wc*128 + 32 j + 8 g + 4 h + q
+  constexpr int WROWS = TBM / 2;
+  char* img = lds + w * (WROWS * 256);
   const int ncol0 = n0 + wc * 128;
 #pragma unroll
   for (int j = 0; j < 4; ++j)
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < MB; ++i)
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
         const int row = 32 * i + l32, col = 32 * j + 8 * g + 4 * h;
@@ -453,18 +510,18 @@ __global__ __launch_bounds__(M4_NT, 1) void moe_gemm4_fp8_kernel(
   __syncthreads();
   if constexpr (MODE == 0) {
 #pragma unroll 4
-    for (int it = 0; it < 32; ++it) {
+    for (int it = 0; it < WROWS / 4; ++it) {
       const int row = it * 4 + (lane >> 4), c = lane & 15;
-      const int p = m0 + wr * 128 + row;
+      const int p = m0 + wr * WROWS + row;
       const int n = ncol0 + c * 8;
       const u32x4_t v = *reinterpret_cast<const u32x4_t*>(img + row * 256 + ((c ^ (row & 15)) * 16));
       if (sorted_ids[p] >= 0 && n < N) *reinterpret_cast<u32x4_t*>(Y + (int64_t)p * y_stride + n) = v;
     }
   } else {
 #pragma unroll 4
-    for (int it = 0; it < 16; ++it) {
+    for (int it = 0; it < WROWS / 8; ++it) {
       const int row = it * 8 + (lane >> 3), c = lane & 7;
-      const int p = m0 + wr * 128 + row;
+      const int p = m0 + wr * WROWS + row;
       const int n = ncol0 / 2 + c * 8;
       const u32x4_t v = *reinterpret_cast<const u32x4_t*>(img + row * 128 + ((c ^ (row & 7)) * 16));
       if (sorted_ids[p] >= 0 && 2 * n < N) *reinterpret_cast<u32x4_t*>(Y + (int64_t)p * y_stride + n) = v;
@@ -477,21 +534,24 @@ __global__ __launch_bounds__(M4_NT, 1) void moe_gemm4_fp8_kernel(
 extern "C" int llmd_moe_gemm4_bf16(const void* X, int64_t x_stride, int topk, const int* sorted_ids,
                                    const int* tile_expert, int num_tiles, const void* W, int64_t w_expert_stride,
                                    int N, int K, void* Y, int64_t y_stride, int mode, int act, float alpha,
-                                   float limit, int a_rows_are_slots, const void* bias, int64_t x_rows,
+                                   float limit, int a_rows_are_slots, const void* bias, int64_t x_rows, int tile_m,
                                    hipStream_t st) {
   if (K % M4_BK || x_stride % 8 || w_expert_stride % 8 || N % 8 || (mode == 1 && N % 16)) return -1;
+  if (tile_m != 256 && tile_m != 192) return -1;
   // 31-bit byte offsets of the gathered rows and of one expert's weights
   if ((x_rows * x_stride + K) * 2 > 0x7fffffffLL || ((int64_t)N * K) * 2 > 0x7fffffffLL) return -2;
   if (num_tiles == 0) return 0;
   dim3 grid((N + M4_BN - 1) / M4_BN, num_tiles);
-  if (mode == 0)
-    hipLaunchKernelGGL(moe_gemm4_bf16_kernel<0>, grid, dim3(M4_NT), 0, st, (const uint16_t*)X, x_stride, topk,
-                       sorted_ids, tile_expert, (const uint16_t*)W, w_expert_stride, N, K, (uint16_t*)Y, y_stride, act,
-                       alpha, limit, a_rows_are_slots, (const uint16_t*)bias);
-  else
-    hipLaunchKernelGGL(moe_gemm4_bf16_kernel<1>, grid, dim3(M4_NT), 0, st, (const uint16_t*)X, x_stride, topk,
-                       sorted_ids, tile_expert, (const uint16_t*)W, w_expert_stride, N, K, (uint16_t*)Y, y_stride, act,
-                       alpha, limit, a_rows_are_slots, (const uint16_t*)bias);
+#define M4_LAUNCH(MODE_, TBM_)                                                                                    \
+  hipLaunchKernelGGL((moe_gemm4_bf16_kernel<MODE_, TBM_>), grid, dim3(M4_NT), 0, st, (const uint16_t*)X, x_stride, \
+                     topk, sorted_ids, tile_expert, (const uint16_t*)W, w_expert_stride, N, K, (uint16_t*)Y,        \
+                     y_stride, act, alpha, limit, a_rows_are_slots, (const uint16_t*)bias)
+  if (tile_m == 256) {
+    if (mode == 0) M4_LAUNCH(0, 256); else M4_LAUNCH(1, 256);
+  } else {
+    if (mode == 0) M4_LAUNCH(0, 192); else M4_LAUNCH(1, 192);
+  }
+#undef M4_LAUNCH
   return (int)hipGetLastError();
 }
 
@@ -499,20 +559,23 @@ extern "C" int llmd_moe_gemm4_fp8(const void* X, int64_t x_stride, const float* 
                                   const int* sorted_ids, const int* tile_expert, int num_tiles, const void* W,
                                   int64_t w_expert_stride, const float* ws, int N, int K, void* Y, int64_t y_stride,
                                   int mode, int act, float alpha, float limit, int a_rows_are_slots, const void* bias,
-                                  int64_t x_rows, hipStream_t st) {
+                                  int64_t x_rows, int tile_m, hipStream_t st) {
   // K: Kp (padded to 128), at most 64 k-blocks (the weight-scale row of a tile is one 64-lane DMA)
   if (K % 128 || K / 128 > 64 || x_stride % 16 || w_expert_stride % 16 || N % 8 || (mode == 1 && N % 16)) return -1;
+  if (tile_m != 256 && tile_m != 192) return -1;
   if (x_rows * x_stride + K > 0x7fffffffLL || (int64_t)N * K > 0x7fffffffLL || x_rows * xs_stride * 4 > 0x7fffffffLL)
     return -2;
   if (num_tiles == 0) return 0;
   dim3 grid((N + M4_BN - 1) / M4_BN, num_tiles);
-  if (mode == 0)
-    hipLaunchKernelGGL(moe_gemm4_fp8_kernel<0>, grid, dim3(M4_NT), 0, st, (const uint8_t*)X, x_stride, xs, xs_stride,
-                       topk, sorted_ids, tile_expert, (const uint8_t*)W, w_expert_stride, ws, N, K, (uint16_t*)Y,
-                       y_stride, act, alpha, limit, a_rows_are_slots, (const uint16_t*)bias);
-  else
-    hipLaunchKernelGGL(moe_gemm4_fp8_kernel<1>, grid, dim3(M4_NT), 0, st, (const uint8_t*)X, x_stride, xs, xs_stride,
-                       topk, sorted_ids, tile_expert, (const uint8_t*)W, w_expert_stride, ws, N, K, (uint16_t*)Y,
-                       y_stride, act, alpha, limit, a_rows_are_slots, (const uint16_t*)bias);
+#define M8_LAUNCH(MODE_, TBM_)                                                                                    \
+  hipLaunchKernelGGL((moe_gemm4_fp8_kernel<MODE_, TBM_>), grid, dim3(M4_NT), 0, st, (const uint8_t*)X, x_stride, xs, \
+                     xs_stride, topk, sorted_ids, tile_expert, (const uint8_t*)W, w_expert_stride, ws, N, K,         \
+                     (uint16_t*)Y, y_stride, act, alpha, limit, a_rows_are_slots, (const uint16_t*)bias)
+  if (tile_m == 256) {
+    if (mode == 0) M8_LAUNCH(0, 256); else M8_LAUNCH(1, 256);
+  } else {
+    if (mode == 0) M8_LAUNCH(0, 192); else M8_LAUNCH(1, 192);
+  }
+#undef M8_LAUNCH
   return (int)hipGetLastError();
 }

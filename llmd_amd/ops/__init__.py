@@ -578,6 +578,17 @@ MOE_V3_BF16 = os.environ.get("LLMD_MOE_V3_BF16", "1") == "1"  # DeepSeek EP8 T=4
 # prefill GEMM): DeepSeek EP8 T=4096 807 -> 1011 TF/s, gpt-oss T=5120 534 -> 586 (profiles/moe_gemm_v4_r5.txt)
 MOE_BF16_V4 = os.environ.get("LLMD_MOE_BF16_V4", "1") == "1"
 MOE_FUSED_QUANT = os.environ.get("LLMD_MOE_FUSED_QUANT", "0") == "1"
+# v4 expert-tile rows: "auto" picks 192 or 256 by the expected padding at T*k/E rows per expert (gpt-oss
+# at a 5120-token step: 160 rows -> a 256-row tile is 62 % useful rows, a 192-row one 83 %)
+MOE4_TILE = os.environ.get("LLMD_MOE4_TILE", "auto")
+
+
+def moe4_tile_rows(n_rows: int, E: int) -> int:
+    if MOE4_TILE in ("192", "256"):
+        return int(MOE4_TILE)
+    r = n_rows / max(1, E)
+    waste = {t: math.ceil(r / t) * t - r for t in (256, 192)}
+    return 192 if waste[192] < waste[256] else 256
 # block-fp8 prefill-sized steps on the v4 grouped GEMM (moe4.hip moe_gemm4_fp8_kernel: 4-wave PGR2,
 # scaled 32x32x64 MFMA with the E8M0 block scales as operands): DeepSeek EP8 T=4096 1307 -> 1496 TF/s,
 # gpt-oss T=5120 757 -> 782 (profiles/moe_gemm_v4_r5.txt)
@@ -636,6 +647,10 @@ def moe_experts_fp8(x, ids, wts, w1q, w1s, w2q, w2s, act=0, alpha=1.702, limit=7
     # decode-sized steps keep the 64-row weight-streaming kernel
     bm = C.moe_tile_m_prefill() if (T * k >= MOE_V3_MIN_ROWS * E and Kp1 % 128 == 0 and Kp2 % 128 == 0
                                     and MOE_V3) else C.moe_tile_m()
+    v4 = (bm == C.moe_tile_m_prefill() and MOE_FP8_V4 and not MOE_FUSED_QUANT and Kp1 <= 8192 and Kp2 <= 8192
+          and N1 % 16 == 0 and d % 8 == 0)
+    if v4:
+        bm = moe4_tile_rows(T * k, E)
     n = T * k
     max_p = ((n + E * (bm - 1)) + bm - 1) // bm * bm
     dev = x.device
@@ -657,14 +672,13 @@ def moe_experts_fp8(x, ids, wts, w1q, w1s, w2q, w2s, act=0, alpha=1.702, limit=7
         hs = torch.empty(max_p, Kp2 // 128, dtype=torch.float32, device=dev)
         C.moe_gemm_fp8(xq, xs, k, sorted_ids, tile_e, w1q, w1s, torch.empty(0, F, dtype=torch.bfloat16, device=dev),
                        1, act, alpha, limit, False, b1, bm, hq, hs)
-    elif bm == C.moe_tile_m_prefill() and MOE_FP8_V4 and Kp1 <= 8192 and Kp2 <= 8192 and N1 % 16 == 0 \
-            and d % 8 == 0:
+    elif v4:
         # v4: PGR2 4-wave tiles, A rows and their act scales gathered by the LDS-DMA (csrc/ops/moe4.hip)
         h = torch.empty(max_p, F, dtype=torch.bfloat16, device=dev)
-        C.moe_gemm4_fp8(xq, xs, k, sorted_ids, tile_e, w1q, w1s, h, 1, act, alpha, limit, False, b1)
+        C.moe_gemm4_fp8(xq, xs, k, sorted_ids, tile_e, w1q, w1s, h, 1, act, alpha, limit, False, b1, bm)
         hq, hs = _quant_groups_padded(h, Kp2)
         y = torch.empty(max_p, d, dtype=torch.bfloat16, device=dev)
-        C.moe_gemm4_fp8(hq, hs, 1, sorted_ids, tile_e, w2q, w2s, y, 0, 0, 0.0, 0.0, True, b2)
+        C.moe_gemm4_fp8(hq, hs, 1, sorted_ids, tile_e, w2q, w2s, y, 0, 0, 0.0, 0.0, True, b2, bm)
         if out is None:
             out = torch.empty(T, d, dtype=torch.bfloat16, device=dev)
         C.moe_combine(y, inv, wts.contiguous().view(-1).float(), k, out)
@@ -743,6 +757,9 @@ def moe_experts(x, ids, wts, w1, w2, act=0, alpha=1.702, limit=7.0, out=None, b1
     # prefill-sized steps: 256-row expert tiles on the v3 kernel (bf16 form), as moe_experts_fp8
     v3 = T * k >= MOE_V3_MIN_ROWS * E and K1 % 32 == 0 and F % 32 == 0 and MOE_V3 and MOE_V3_BF16
     bm = C.moe_tile_m_prefill() if v3 else C.moe_tile_m()
+    v4 = v3 and MOE_BF16_V4 and K1 % 64 == 0 and F % 64 == 0 and N1 % 16 == 0 and d % 8 == 0
+    if v4:
+        bm = moe4_tile_rows(T * k, E)
     n = T * k
     max_p = ((n + E * (bm - 1)) + bm - 1) // bm * bm
     dev = x.device
@@ -754,10 +771,10 @@ def moe_experts(x, ids, wts, w1, w2, act=0, alpha=1.702, limit=7.0, out=None, b1
     C.moe_align(ids.contiguous().view(-1), E, sorted_ids, tile_e, offs, total, inv, bm)
     h = torch.empty(max_p, F, dtype=x.dtype, device=dev)
     y = torch.empty(max_p, d, dtype=x.dtype, device=dev)
-    if v3 and MOE_BF16_V4 and K1 % 64 == 0 and F % 64 == 0 and N1 % 16 == 0 and d % 8 == 0:
+    if v4:
         # v4: the dense prefill GEMM's 4-wave PGR2 structure, rows gathered by the LDS-DMA (csrc/ops/moe4.hip)
-        C.moe_gemm4(x, k, sorted_ids, tile_e, w1, h, 1, act, alpha, limit, False, b1)
-        C.moe_gemm4(h, 1, sorted_ids, tile_e, w2, y, 0, 0, 0.0, 0.0, True, b2)
+        C.moe_gemm4(x, k, sorted_ids, tile_e, w1, h, 1, act, alpha, limit, False, b1, bm)
+        C.moe_gemm4(h, 1, sorted_ids, tile_e, w2, y, 0, 0, 0.0, 0.0, True, b2, bm)
     else:
         C.moe_gemm(x, k, sorted_ids, tile_e, w1, h, 1, act, alpha, limit, False, b1, bm)
         # second GEMM: A rows are the sorted slots themselves (row p of h; a_rows_are_slots)

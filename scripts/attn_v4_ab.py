@@ -18,7 +18,7 @@ def main():
     a = ap.parse_args()
     cases = [(5000, 5000), (8192, 8192), (8192, 4096), (2048, 2048)]
     res = {}
-    arms = {"v2": ("0", "3"), "v4-builtin-dma": ("1", "1"), "v4-asm-dma": ("1", "3")}
+    arms = {"v2": ("0", "3"), "v4-builtin-dma": ("1", "1"), "v4-asm-dma": ("1", "3"), "v4-pipelined": ("1", "7")}
     for r in range(a.rounds):
         for ctx, ql in cases:
             for name, (on, var) in arms.items():

@@ -1,0 +1,12 @@
+# MoE v4 192-row expert tiles: numerics (bf16 + fp8, both tile sizes), A/B (scripts/bench_moe.py), then the
+# prefill attention 4-arm A/B.
+set -o pipefail
+mkdir -p gpurun_out
+timeout -k 10 400 python -u -m pytest tests/test_kernels_gpu.py tests/test_fp8_kv.py -q -x --timeout 150 --timeout-method thread -p no:cacheprovider -k "moe" > gpurun_out/r5p_tests.log 2>&1
+rc=$?; tail -3 gpurun_out/r5p_tests.log; [ $rc -ne 0 ] && exit $rc
+timeout -k 10 600 python -u scripts/bench_moe.py > gpurun_out/r5p_moe.log 2>&1
+rc=$?; grep -v amdgpu.ids gpurun_out/r5p_moe.log; [ $rc -ne 0 ] && exit $rc
+timeout -k 10 300 python -u -m pytest tests/test_prefill_v4.py -q -x --timeout 120 --timeout-method thread -p no:cacheprovider > gpurun_out/r5p_attn_tests.log 2>&1
+rc=$?; tail -3 gpurun_out/r5p_attn_tests.log; [ $rc -ne 0 ] && exit $rc
+timeout -k 10 400 python -u scripts/attn_v4_ab.py > gpurun_out/r5p_attn_ab.log 2>&1
+rc=$?; grep -v amdgpu.ids gpurun_out/r5p_attn_ab.log | grep "AB\|check"; exit $rc

@@ -279,7 +279,8 @@ def test_moe_fp8_prefill_tiles_gpu(T, E, k, d, F, act, skew, monkeypatch):
 @pytest.mark.parametrize("T,E,k,d,F,act,skew", [(512, 4, 4, 1024, 1024, 2, False), (600, 16, 8, 1024, 256, 0, True),
                                                 (800, 16, 4, 2880, 2880, 2, False), (300, 8, 8, 7168, 2048, 0, True),
                                                 (5, 8, 2, 256, 128, 0, False)])
-def test_moe_fp8_v4_gpu(T, E, k, d, F, act, skew, monkeypatch):
+@pytest.mark.parametrize("tile", ["256", "192"])
+def test_moe_fp8_v4_gpu(T, E, k, d, F, act, skew, tile, monkeypatch):
     """The v4 block-fp8 grouped GEMM (csrc/ops/moe4.hip moe_gemm4_fp8_kernel: 4-wave PGR2 tiles,
     A rows and their act scales gathered by the LDS-DMA, scaled 32x32x64 MFMA) vs the v3 256-row
     kernel and the CPU reference: gpt-oss widths (partial column tiles), K = 7168 (56 k-blocks),
@@ -304,6 +305,7 @@ def test_moe_fp8_v4_gpu(T, E, k, d, F, act, skew, monkeypatch):
     monkeypatch.setattr(ops, "MOE_FP8_V4", False)
     y3 = ops.moe_experts_fp8(x, ids, wts, w1q, w1s, w2q, w2s, act, b1=b1, b2=b2)
     monkeypatch.setattr(ops, "MOE_FP8_V4", True)
+    monkeypatch.setattr(ops, "MOE4_TILE", tile)
     y4 = ops.moe_experts_fp8(x, ids, wts, w1q, w1s, w2q, w2s, act, b1=b1, b2=b2)
     r = ops.moe_experts_fp8(x.cpu(), ids.cpu(), wts.cpu(), w1q.cpu()[..., :d], w1s.cpu(), w2q.cpu()[..., :F],
                             w2s.cpu(), act, b1=b1.cpu(), b2=b2.cpu())

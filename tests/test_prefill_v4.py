@@ -46,7 +46,7 @@ def _run(shapes, Hq, Hkv, bs, window=0, sinks=None, seed=5):
     return q, kc, vc, bt, args
 
 
-@pytest.mark.parametrize("variant", ["1", "3"])  # 1: builtin LDS-DMA, 3: asm LDS-DMA
+@pytest.mark.parametrize("variant", ["1", "3", "7"])  # 1: builtin LDS-DMA, 3: asm LDS-DMA, 7: + pipelined halves
 @pytest.mark.parametrize("Hq,Hkv", [(64, 8), (32, 8), (8, 8), (16, 8)])
 @pytest.mark.parametrize("bs", [16, 64])
 def test_prefill_v4_matches_reference(Hq, Hkv, bs, variant, monkeypatch):
