@@ -2,6 +2,8 @@
 # prefill attention 4-arm A/B.
 set -o pipefail
 mkdir -p gpurun_out
+timeout -k 10 400 python -u -m pytest tests/test_pd_cross_device.py -q -x --timeout 200 --timeout-method thread -p no:cacheprovider > gpurun_out/r5p_pd.log 2>&1
+rc=$?; tail -3 gpurun_out/r5p_pd.log; [ $rc -ne 0 ] && exit $rc
 timeout -k 10 400 python -u -m pytest tests/test_kernels_gpu.py tests/test_fp8_kv.py -q -x --timeout 150 --timeout-method thread -p no:cacheprovider -k "moe" > gpurun_out/r5p_tests.log 2>&1
 rc=$?; tail -3 gpurun_out/r5p_tests.log; [ $rc -ne 0 ] && exit $rc
 timeout -k 10 600 python -u scripts/bench_moe.py > gpurun_out/r5p_moe.log 2>&1
