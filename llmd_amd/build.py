@@ -119,9 +119,24 @@ def build_ops(jobs: int = 8, verbose: bool = False, debug: bool = False) -> Path
         "-ltorch_python", "-lamdhip64", f"-Wl,-rpath,{tlib}",
     ]
     out = _link(objs, PKG / f"{name}{EXT}", libs)
+    _check_launch_stubs(out)
     if verbose:
         print(f"[llmd build] {out}")
     return out
+
+
+def _check_launch_stubs(lib: Path) -> None:
+    """Fail the build when a kernel's host launch stub is missing from the library: the link of a
+    shared object leaves it undefined and the failure would only show at import time on the GPU box
+    (hipcc's host pass drops the stub of a kernel template whose DMA lambda reads an array of
+    template-dependent size - seen in moe4.hip)."""
+    try:
+        r = subprocess.run(["nm", "-D", "--undefined-only", str(lib)], capture_output=True, text=True, check=True)
+    except (OSError, subprocess.CalledProcessError):
+        return  # no binutils: the import check of __graft_entry__.build() still catches it
+    missing = [l.split()[-1] for l in r.stdout.splitlines() if "__device_stub__" in l]
+    if missing:
+        raise RuntimeError(f"{lib.name}: {len(missing)} kernel launch stubs undefined, e.g. {missing[0]}")
 
 
 def build_runtime(jobs: int = 8, verbose: bool = False) -> Path:

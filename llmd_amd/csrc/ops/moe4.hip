@@ -87,7 +87,9 @@ __global__ __launch_bounds__(M4_NT, 1) void moe_gemm4_bf16_kernel(
       (void*)(W + (int64_t)e * w_expert_stride), 0, 0x7fffffff, 0x00020000);
   // DMA piece j: A rows 8 (MI w + j) + (lane >> 3), W rows 64 w + 8 j + (lane >> 3);
   // LDS slot lane & 7 <- chunk (lane & 7) ^ f(row)
-  uint32_t va[MI], vw[8];
+  // fixed-size offset arrays: a template-dependent array size read by the DMA lambda makes hipcc's host
+  // pass drop this kernel's launch stub (undefined symbol at load time)
+  uint32_t va[8], vw[8];
 #pragma unroll
   for (int j = 0; j < MI; ++j) {
     const int row = 8 * (MI * w + j) + (lane >> 3);
@@ -307,7 +309,7 @@ __global__ __launch_bounds__(M4_NT, 1) void moe_gemm4_fp8_kernel(
   const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)xs, 0, 0x7fffffff, 0x00020000);
   const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc(
       (void*)(W + (int64_t)e * w_expert_stride), 0, 0x7fffffff, 0x00020000);
-  uint32_t va[NA], vw[8];
+  uint32_t va[8], vw[8];  // fixed size: see the bf16 form
 #pragma unroll
   for (int j = 0; j < NA; ++j) {
     const int row = 8 * (NA * w + j) + (lane >> 3);

@@ -7,7 +7,9 @@ runs in the hand-written HIP kernels of ``llmd_amd.ops``.
 """
 from __future__ import annotations
 
+import contextlib
 import math
+import os
 from typing import Optional
 
 import torch
@@ -190,6 +192,20 @@ class LMHead(torch.nn.Module):
         return logits[:, : self.vocab]
 
 
+_ATTN_OVERLAP = os.environ.get("LLMD_ATTN_OVERLAP", "1") == "1"
+_SIDE_STREAMS: dict = {}
+
+
+def _overlap_stream(t: torch.Tensor):
+    """The per-device side stream of mixed-step attention, or None (off, CPU, or under graph capture)."""
+    if not (_ATTN_OVERLAP and t.is_cuda) or torch.cuda.is_current_stream_capturing():
+        return None
+    s = _SIDE_STREAMS.get(t.device.index)
+    if s is None:
+        s = _SIDE_STREAMS[t.device.index] = torch.cuda.Stream(device=t.device)
+    return s
+
+
 class PagedAttention(torch.nn.Module):
     """QKV projection output -> rope + cache write -> decode/prefill attention."""
 
@@ -224,16 +240,25 @@ class PagedAttention(torch.nn.Module):
                        self.k_cache, self.v_cache, self.neox, self.k_scale, self.v_scale)
         out = torch.empty(T, Hq * D, dtype=qkv.dtype, device=qkv.device)
         nd = meta.num_decode
+        # a mixed step (eager): the memory-bound decode rows run on a side stream beside the compute-bound
+        # prefill attention (the decode kernel streams the running sequences' KV while the prefill's
+        # MFMAs run; back to back they serialise)
+        side = _overlap_stream(qkv) if nd and meta.num_prefill_tokens else None
         if nd:
-            ops.paged_decode(qkv[:nd], self.k_cache, self.v_cache, meta.d_block_tables,
-                             meta.d_seq_lens, Hq, Hkv, D, self.scale, self.window, self.sinks,
-                             split=meta.d_split, out=out[:nd], workspace=meta.d_workspace,
-                             max_ctx=meta.d_max_ctx, k_scale=self.k_scale, v_scale=self.v_scale,
-                             cascade=meta.d_cascade, split_dev=meta.d_split_dev)
+            if side is not None:
+                side.wait_stream(torch.cuda.current_stream(qkv.device))
+            with torch.cuda.stream(side) if side is not None else contextlib.nullcontext():
+                ops.paged_decode(qkv[:nd], self.k_cache, self.v_cache, meta.d_block_tables,
+                                 meta.d_seq_lens, Hq, Hkv, D, self.scale, self.window, self.sinks,
+                                 split=meta.d_split, out=out[:nd], workspace=meta.d_workspace,
+                                 max_ctx=meta.d_max_ctx, k_scale=self.k_scale, v_scale=self.v_scale,
+                                 cascade=meta.d_cascade, split_dev=meta.d_split_dev)
         if meta.num_prefill_tokens:
             items = meta.p_items
             ops.paged_prefill(qkv[nd:], self.k_cache, self.v_cache, meta.p_block_tables,
                               meta.p_q_start, meta.p_q_len, meta.p_ctx_len, Hq, Hkv, D, self.scale,
                               self.window, self.sinks, items=items, out=out[nd:], k_scale=self.k_scale,
                               v_scale=self.v_scale)
+        if side is not None:
+            torch.cuda.current_stream(qkv.device).wait_stream(side)
         return out

@@ -1,0 +1,5 @@
+# P/D same-device check, printed in full
+set -o pipefail
+mkdir -p gpurun_out
+LLMD_PD_DEVICES=0,0 LLMD_KV_VMM=1 timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node=2 --master-addr=127.0.0.1 --master-port=29611 scripts/pd_check.py --model small-llama --transport ipc > gpurun_out/r5q_pd.out 2> gpurun_out/r5q_pd.err
+rc=$?; grep PDCHECK gpurun_out/r5q_pd.out; grep -v "Gloo\|amdgpu.ids" gpurun_out/r5q_pd.err | tail -30; exit $rc
