@@ -19,7 +19,7 @@ def main():
     x = torch.randn(T, d, device=dev, dtype=torch.bfloat16)
     w1 = (torch.randn(E, 2 * F, d, device=dev) * d ** -0.5).to(torch.bfloat16)
     ids, _ = ops.moe_topk(torch.randn(T, E, device=dev), k, 2)
-    bm = C.moe_tile_m_prefill()
+    bm = int(sys.argv[1]) if len(sys.argv) > 1 else C.moe_tile_m_prefill()
     n = T * k
     max_p = ((n + E * (bm - 1)) + bm - 1) // bm * bm
     sorted_ids = torch.empty(max_p, dtype=torch.int32, device=dev)
@@ -42,7 +42,7 @@ def main():
     for name, src, slots in (("gather", x, False), ("slots", None, True)):
         xs = src if src is not None else x[tok.to(dev)].contiguous()
         y = torch.full((max_p, 2 * F), float("nan"), device=dev, dtype=torch.bfloat16)
-        C.moe_gemm4(xs, k, sorted_ids, tile_e, w1, y, 0, 0, 0.0, 0.0, slots, None)
+        C.moe_gemm4(xs, k, sorted_ids, tile_e, w1, y, 0, 0, 0.0, 0.0, slots, None, bm)
         torch.cuda.synchronize()
         err = (y.float().cpu() - want).abs()
         err[~valid] = 0
@@ -51,9 +51,15 @@ def main():
         print(f"{name}: max err {err.max().item():.4f} tol {tol:.4f} bad {int(bad.sum())} of {int(valid.sum()) * 2 * F}")
         if bad.any():
             eb = err.view(max_p // bm, bm // 32, 32, 2 * F // 32, 32).amax(dim=(2, 4))
-            for t_, rb, cb in (eb > tol).nonzero().tolist()[:40]:
+            for t_, rb, cb in (eb > tol).nonzero().tolist()[:4]:
                 print(f"  tile {t_} (expert {int(te[t_])}) rows {32 * rb}-{32 * rb + 31} cols {32 * cb}-{32 * cb + 31} "
                       f"err {eb[t_, rb, cb].item():.3f}")
+            nt_ = max_p // bm
+            frac = bad.view(nt_, bm // 16, 16, -1).float().mean(dim=(2, 3))
+            for t_ in range(min(nt_, 6)):
+                print(f"  tile {t_} bad fraction per 16-row block:", " ".join(f"{v:.2f}" for v in frac[t_].tolist()))
+            cfrac = bad.view(max_p, -1, 16).float().mean(dim=(0, 2))
+            print("  bad fraction per 16-col block:", " ".join(f"{v:.2f}" for v in cfrac.tolist()[:32]))
             rows = bad.any(1).nonzero().view(-1)
             print("  bad rows (first 40):", rows[:40].tolist())
             cols = bad.any(0).nonzero().view(-1)
@@ -71,7 +77,7 @@ def main():
                     h = h + bf[ex[p]]
                 want_h[p] = torch.nn.functional.silu(h[0::2]) * h[1::2]
         hh = torch.full((max_p, F), float("nan"), device=dev, dtype=torch.bfloat16)
-        C.moe_gemm4(x, k, sorted_ids, tile_e, w1, hh, 1, 0, 1.702, 7.0, False, bias)
+        C.moe_gemm4(x, k, sorted_ids, tile_e, w1, hh, 1, 0, 1.702, 7.0, False, bias, bm)
         torch.cuda.synchronize()
         err = (hh.float().cpu() - want_h).abs()
         err[~valid] = 0
@@ -88,14 +94,20 @@ def main():
     w1q = ops.pad_fp8_k(w1q, c128(d))
     xq, xs = ops._quant_groups_padded(x, w1q.shape[2])
     y3 = torch.zeros(max_p, 2 * F, device=dev, dtype=torch.bfloat16)
-    C.moe_gemm_fp8(xq, xs, k, sorted_ids, tile_e, w1q, w1s, y3, 0, 0, 0.0, 0.0, False, None, bm)
+    C.moe_gemm_fp8(xq, xs, k, sorted_ids, tile_e, w1q, w1s, y3, 0, 0, 0.0, 0.0, False, None, bm) if bm == 256 else None
     y4 = torch.zeros(max_p, 2 * F, device=dev, dtype=torch.bfloat16)
-    C.moe_gemm4_fp8(xq, xs, k, sorted_ids, tile_e, w1q, w1s, y4, 0, 0, 0.0, 0.0, False, None)
+    C.moe_gemm4_fp8(xq, xs, k, sorted_ids, tile_e, w1q, w1s, y4, 0, 0, 0.0, 0.0, False, None, bm)
+    if bm != 256:  # the v3 kernel has 256-row tiles only: compare against torch on the dequantised operands
+        xd = (xq.float() * xs.repeat_interleave(128, 1)[:, :xq.shape[1]]).cpu()
+        wd = ops.dequant_fp8_block_weight(w1q, w1s).float().cpu()
+        for p in range(max_p):
+            if valid[p]:
+                y3[p] = (wd[ex[p]][:, :xd.shape[1]] @ xd[tok[p]]).to(torch.bfloat16).to(dev)
     torch.cuda.synchronize()
-    err = (y4.float() - y3.float()).abs().cpu()
+    err = (y4.float() - y3.float()).abs().cpu()  # v4 vs v3 (256) or vs torch (192)
     err[~valid] = 0
     tol = 2e-2 * y3.float().abs().max().item()
-    print(f"fp8 v4 vs v3: max err {err.max().item():.4f} tol {tol:.4f} bad {int((err > tol).sum())}")
+    print(f"fp8 v4 (tile {bm}) vs reference: max err {err.max().item():.4f} tol {tol:.4f} bad {int((err > tol).sum())}")
     if (err > tol).any():
         eb = err.view(max_p // bm, bm // 32, 32, 2 * F // 32, 32).amax(dim=(2, 4))
         for t_, rb, cb in (eb > tol).nonzero().tolist()[:40]:

@@ -42,7 +42,7 @@ def _run(nproc, args, devices=None, env_extra=None, timeout=420):
            "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.join(ROOT, "scripts", "pd_check.py")]
     r = subprocess.run(cmd + args, env=env, cwd=ROOT, capture_output=True, text=True, timeout=timeout)
     lines = [l for l in r.stdout.splitlines() if l.startswith("PDCHECK ")]
-    assert r.returncode == 0 and lines, (r.returncode, r.stdout[-3000:], r.stderr[-3000:])
+    assert r.returncode == 0 and lines, (r.returncode, lines[-1] if lines else r.stdout[-2000:], r.stderr[-2000:])
     d = json.loads(lines[-1][8:])
     assert d["ok"] and d["decoder"]["all_remote"] and d["decoder"]["finished"], d
     return d
