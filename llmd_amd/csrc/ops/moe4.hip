@@ -56,6 +56,9 @@ __device__ __forceinline__ float m4_act(float g, float u, int act, float alpha, 
 // TBM: expert-tile rows, 256 or 192 (gpt-oss: ~160 rows per expert at a 5120-token step, so a
 // 256-row tile is 62 % useful rows, a 192-row one 83 %). A wave owns TBM / 2 rows x 128 columns:
 // MI = TBM / 32 A fragments of 16 rows; A DMA pieces per wave = MI, W pieces 8.
+// The 192 form is NOT validated: one K-step is exact, from the second on the rows of fragments
+// 1..5 of each wave go wrong (scripts/moe4_diag.py 192, DIAG_D=64 / 128); not the buffer
+// placement, not the fragment waits. ops keeps 256 (LLMD_MOE4_TILE).
 template <int MODE, int TBM = 256>
 __global__ __launch_bounds__(M4_NT, 1) void moe_gemm4_bf16_kernel(
     const uint16_t* __restrict__ X, int64_t x_stride, int topk, const int* __restrict__ sorted_ids,

@@ -1,6 +1,9 @@
-"""Scan a hipcc --save-temps .s file for accumulator reads that follow an asm MFMA writing the
-same AGPRs too closely (hipcc does not model the latency of MFMAs issued from inline asm, so
-register-allocator copies can land inside their shadow). Prints each suspect and a count.
+"""Scan a hipcc --save-temps .s file for two hazards of MFMAs issued from inline asm, which
+hipcc does not model: accumulator reads that follow an asm MFMA writing the same AGPRs too
+closely (register-allocator copies in its shadow), and VALU writes of a VGPR that an asm MFMA
+issued shortly before still reads as SrcA / SrcB (the allocator reuses an operand register
+right after its last asm use - moe4.hip's 192-row form computed wrong rows from it). Prints each
+suspect and the counts.
   python scripts/mfma_hazard_scan.py file.s [min_wait_states=20]"""
 import re
 import sys
@@ -37,7 +40,36 @@ def main():
                 print(f"{func[:90]}: line {i + 1}: {t} {n} states after {l.strip()[:50]}")
                 bad += 1
                 break
-    print(f"{path}: {bad} suspects")
+    # WAR: a VALU write of a VGPR that an asm MFMA issued shortly before still reads as SrcA / SrcB
+    func, war, in_asm = None, 0, False
+    for i, l in enumerate(lines):
+        if re.match(r"^_Z\S*:", l):
+            func = l.split(":")[0]
+        if ";;#ASMSTART" in l:
+            in_asm = True
+        elif ";;#ASMEND" in l:
+            in_asm = False
+        m = re.search(r"v_mfma\S*\s+a\[\d+:\d+\],\s*v\[(\d+):(\d+)\],\s*v\[(\d+):(\d+)\]", l)
+        if not m or not in_asm:
+            continue
+        srcs = set(range(int(m.group(1)), int(m.group(2)) + 1)) | set(range(int(m.group(3)), int(m.group(4)) + 1))
+        n = 0
+        for l2 in lines[i + 1:i + 60]:
+            t = l2.strip()
+            if not t or t.startswith(";") or t.endswith(":") or t.startswith("."):
+                continue
+            n += int(t.split()[1]) + 1 if t.startswith("s_nop") else 1
+            if n >= need:
+                break
+            w = re.match(r"(v_(?!mfma|accvgpr_read)\S+)\s+v\[?(\d+)(?::(\d+))?\]?", t)
+            if w:
+                lo = int(w.group(2))
+                hi = int(w.group(3)) if w.group(3) else lo
+                if srcs & set(range(lo, hi + 1)):
+                    print(f"{func[:90]}: line {i + 1}: WAR {t} {n} states after {l.strip()[:60]}")
+                    war += 1
+                    break
+    print(f"{path}: {bad} accumulator suspects, {war} operand WAR suspects")
 
 
 if __name__ == "__main__":

@@ -15,7 +15,7 @@ def main():
     torch.manual_seed(13)
     C = ops.native()
     dev = "cuda"
-    T, E, k, d, F = 1024, 8, 2, 1024, 512
+    T, E, k, d, F = 1024, 8, 2, int(os.environ.get("DIAG_D", "1024")), 512
     x = torch.randn(T, d, device=dev, dtype=torch.bfloat16)
     w1 = (torch.randn(E, 2 * F, d, device=dev) * d ** -0.5).to(torch.bfloat16)
     ids, _ = ops.moe_topk(torch.randn(T, E, device=dev), k, 2)
