@@ -20,7 +20,7 @@ for f in sorted(glob.glob("gpurun_out/pmc_moe4/*counter_collection.csv")):
         kn = r.get("Kernel_Name", "")
         if "moe_gemm4" not in kn:
             continue
-        tag = ("fp8 " if "fp8" in kn else "bf16 ") + ("gemm1(act)" if "ILi1E" in kn else "gemm2")
+        tag = ("fp8 " if "fp8" in kn else "bf16 ") + ("gemm1(act)" if ("<1," in kn or "ILi1E" in kn) else "gemm2")
         agg[tag][r["Counter_Name"]] += float(r["Counter_Value"])
         n[tag][r["Counter_Name"]] += 1
     for tag in sorted(agg):
