@@ -56,9 +56,9 @@ __device__ __forceinline__ float m4_act(float g, float u, int act, float alpha, 
 // TBM: expert-tile rows, 256 or 192 (gpt-oss: ~160 rows per expert at a 5120-token step, so a
 // 256-row tile is 62 % useful rows, a 192-row one 83 %). A wave owns TBM / 2 rows x 128 columns:
 // MI = TBM / 32 A fragments of 16 rows; A DMA pieces per wave = MI, W pieces 8.
-// The 192 form is NOT validated: one K-step is exact, from the second on the rows of fragments
-// 1..5 of each wave go wrong (scripts/moe4_diag.py 192, DIAG_D=64 / 128); not the buffer
-// placement, not the fragment waits. ops keeps 256 (LLMD_MOE4_TILE).
+// (The 192 form first computed wrong rows from the second K-step on: hipcc had peeled the last
+// iteration around a conditional drain and re-homed the accumulators right behind the loop's last
+// asm MFMA - see the drain at the end of the K loop.)
 template <int MODE, int TBM = 256>
 __global__ __launch_bounds__(M4_NT, 1) void moe_gemm4_bf16_kernel(
     const uint16_t* __restrict__ X, int64_t x_stride, int topk, const int* __restrict__ sorted_ids,
@@ -195,9 +195,12 @@ __global__ __launch_bounds__(M4_NT, 1) void moe_gemm4_bf16_kernel(
       }
       __builtin_amdgcn_sched_barrier(0);
     }
-    // drain the asm MFMAs inside the last iteration: hipcc cannot see their latency, and the
-    // register allocator may place accumulator copies (epilogue spills) right at the loop exit
-    if (kt + 1 == nk) asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 3" ::: "memory");
+    // drain the asm MFMAs at the end of EVERY iteration (~19 cycles of ~4000): hipcc cannot see
+    // their latency, and accumulator copies can land right at the loop exit (epilogue spills). A
+    // drain only in the last iteration made hipcc peel that iteration, with the accumulators
+    // re-homed to other AGPRs by v_accvgpr_read / mov right behind the loop's last MFMA - stale
+    // values (the 192-row form's wrong rows)
+    asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 3" ::: "memory");
   }
   asm volatile("s_nop 7\n\ts_nop 7" ::: "memory");  // asm MFMA results -> VALU reads
   __builtin_amdgcn_sched_barrier(0);
@@ -475,8 +478,8 @@ __global__ __launch_bounds__(M4_NT, 1) void moe_gemm4_fp8_kernel(
 #pragma unroll
     for (int b = 0; b < MB; ++b) sa[b] = e8m0_of(nsf[b]);
     swt = e8m0_of(nwf);
-    // drain inside the last iteration (see the bf16 form): 16-pass MFMAs
-    if (kt + 1 == nk) asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
+    // drain at the end of every iteration (see the bf16 form): 16-pass MFMAs
+    asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
   }
   asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
   __builtin_amdgcn_sched_barrier(0);

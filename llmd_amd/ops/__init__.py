@@ -580,8 +580,7 @@ MOE_BF16_V4 = os.environ.get("LLMD_MOE_BF16_V4", "1") == "1"
 MOE_FUSED_QUANT = os.environ.get("LLMD_MOE_FUSED_QUANT", "0") == "1"
 # v4 expert-tile rows: "auto" picks 192 or 256 by the expected padding at T*k/E rows per expert (gpt-oss
 # at a 5120-token step: 160 rows -> a 256-row tile is 62 % useful rows, a 192-row one 83 %)
-# NOT validated: the 192-row kernels compute wrong rows (scripts/moe4_diag.py 192) - 256 stays the default
-MOE4_TILE = os.environ.get("LLMD_MOE4_TILE", "256")
+MOE4_TILE = os.environ.get("LLMD_MOE4_TILE", "auto")
 
 
 def moe4_tile_rows(n_rows: int, E: int) -> int:

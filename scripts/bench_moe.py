@@ -42,11 +42,19 @@ def run(name, T, E, k, d, F, act):
     tb3 = t_it(lambda: ops.moe_experts(x, ids, wts, w1, w2, act))
     ops.MOE_BF16_V4 = old_v4
     ops.MOE_BF16_V4 = old_v4
+    ops.MOE4_TILE = "192"  # 192-row expert tiles forced on (auto picks them where they pad less)
+    ops.MOE_BF16_V4, ops.MOE_FP8_V4 = True, True
+    tb4b = t_it(lambda: ops.moe_experts(x, ids, wts, w1, w2, act))
+    tf4b = t_it(lambda: ops.moe_experts_fp8(x, ids, wts, w1q, w1s, w2q, w2s, act))
+    ops.MOE4_TILE = "256"
+    tb4 = t_it(lambda: ops.moe_experts(x, ids, wts, w1, w2, act))
+    ops.MOE_BF16_V4 = old_v4
     ops.MOE_FP8_V4 = True  # the v4 block-fp8 grouped GEMM (moe4.hip moe_gemm4_fp8_kernel), 256-row tiles
     tf4 = t_it(lambda: ops.moe_experts_fp8(x, ids, wts, w1q, w1s, w2q, w2s, act))
     ops.MOE_FP8_V4 = False
     tf3 = t_it(lambda: ops.moe_experts_fp8(x, ids, wts, w1q, w1s, w2q, w2s, act))
     ops.MOE_FP8_V4 = old_f4
+    ops.MOE4_TILE = "auto"
     active = min(E, T * k)
     flops = 2 * T * k * (2 * F * d + d * F)
     wbytes_bf = active * 3 * F * d * 2
@@ -54,7 +62,8 @@ def run(name, T, E, k, d, F, act):
           f"fp8 {tf * 1e3:.3f} ms ({flops / tf / 1e12:.0f} TF/s, {wbytes_bf / 2 / tf / 1e9:.0f} GB/s w) "
           f"speedup {tb / tf:.2f}x | bf16 v3 {tb3 * 1e3:.3f} ms ({flops / tb3 / 1e12:.0f} TF/s) "
           f"v4 {tb4 * 1e3:.3f} ms ({flops / tb4 / 1e12:.0f} TF/s) | fp8 v3 {tf3 * 1e3:.3f} ms "
-          f"({flops / tf3 / 1e12:.0f} TF/s) v4 {tf4 * 1e3:.3f} ms ({flops / tf4 / 1e12:.0f} TF/s)", flush=True)
+          f"({flops / tf3 / 1e12:.0f} TF/s) v4 {tf4 * 1e3:.3f} ms ({flops / tf4 / 1e12:.0f} TF/s) | v4 192-row tiles: "
+          f"bf16 {flops / tb4b / 1e12:.0f} fp8 {flops / tf4b / 1e12:.0f} TF/s", flush=True)
 
 
 if __name__ == "__main__":

@@ -279,7 +279,7 @@ def test_moe_fp8_prefill_tiles_gpu(T, E, k, d, F, act, skew, monkeypatch):
 @pytest.mark.parametrize("T,E,k,d,F,act,skew", [(512, 4, 4, 1024, 1024, 2, False), (600, 16, 8, 1024, 256, 0, True),
                                                 (800, 16, 4, 2880, 2880, 2, False), (300, 8, 8, 7168, 2048, 0, True),
                                                 (5, 8, 2, 256, 128, 0, False)])
-@pytest.mark.parametrize("tile", ["256"])  # the 192-row form fails its error map (scripts/moe4_diag.py 192)
+@pytest.mark.parametrize("tile", ["256", "192"])
 def test_moe_fp8_v4_gpu(T, E, k, d, F, act, skew, tile, monkeypatch):
     """The v4 block-fp8 grouped GEMM (csrc/ops/moe4.hip moe_gemm4_fp8_kernel: 4-wave PGR2 tiles,
     A rows and their act scales gathered by the LDS-DMA, scaled 32x32x64 MFMA) vs the v3 256-row
