@@ -25,7 +25,7 @@ from .config import EPPConfig, load_config
 from .datalayer import EndpointStore, MetricsDataSource
 from .flow_control import DISPATCHED, OUTCOME_HTTP, OUTCOME_REASON, FlowController
 from .metrics import EPPMetrics
-from .tracing import span
+from ..utils.tracing import span
 from .types import Endpoint, InferenceRequest, ProfileRunResult, SchedulingError, SchedulingResult
 
 log = logging.getLogger("llmd.router.epp")

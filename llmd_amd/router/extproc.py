@@ -50,7 +50,7 @@ from google.protobuf import descriptor_pb2, descriptor_pool, message_factory, st
 from . import headers as H
 from .epp import EPP, Decision
 from .proxy import INFERENCE_PATHS, _find_usage
-from .tracing import span
+from ..utils.tracing import span
 from .types import CIHeaders, InferenceRequest, SchedulingError
 
 log = logging.getLogger("llmd.router.extproc")

@@ -34,7 +34,7 @@ from . import headers as H
 from .api import ControlPlane
 from .datalayer import EndpointStore, FileDiscovery, endpoints_from_yaml
 from .epp import EPP, Decision
-from .tracing import inject, span
+from ..utils.tracing import inject, span
 from .types import SchedulingError
 
 log = logging.getLogger("llmd.router.proxy")
