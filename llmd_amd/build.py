@@ -184,8 +184,31 @@ def build_sanitized_runtime(verbose: bool = False) -> Path:
     return out
 
 
+RELAY = PKG / "bin" / "llmd-relay"
+
+
+def build_relay(verbose: bool = False) -> Path:
+    """The router's native data plane (``csrc/relay/relay.cpp``, router/relay.py): a
+    standalone epoll executable, no Python / torch / HIP."""
+    src = CSRC / "relay" / "relay.cpp"
+    flags = ["-O2", "-std=c++17", "-pthread", "-Wall"]
+    key = _hash([src], flags)
+    stamp = RELAY.with_name(RELAY.name + ".stamp")
+    if RELAY.exists() and stamp.exists() and stamp.read_text() == key:
+        return RELAY
+    RELAY.parent.mkdir(parents=True, exist_ok=True)
+    tmp = RELAY.with_name(RELAY.name + ".tmp")
+    _run(["g++"] + flags + [str(src), "-o", str(tmp)])
+    os.replace(tmp, RELAY)
+    stamp.write_text(key)
+    if verbose:
+        print(f"[llmd build] {RELAY}")
+    return RELAY
+
+
 def build_all(jobs: int | None = None, verbose: bool = True):
     jobs = jobs or min(8, os.cpu_count() or 4)
+    build_relay(verbose)
     rt = build_runtime(jobs, verbose)
     ops = build_ops(jobs, verbose)
     if verbose:
@@ -199,6 +222,8 @@ if __name__ == "__main__":
         build_ops(verbose=True)
     elif what == "rt":
         build_runtime(verbose=True)
+    elif what == "relay":
+        build_relay(verbose=True)
     elif what == "sanitize":
         build_sanitized_runtime(verbose=True)
     elif what == "debug":

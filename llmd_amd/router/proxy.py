@@ -237,6 +237,9 @@ def main(argv=None):
     p.add_argument("--workers", type=int, default=1,
                    help="proxy worker processes (SO_REUSEPORT) in front of one EPP process; 1 = all in-process "
                         "(the reference's --concurrency, guides/no-kubernetes-deployment/README.md:211)")
+    p.add_argument("--data-plane", default="native", choices=["native", "python"],
+                   help="with --workers > 1: native = one llmd-relay process with that many epoll threads "
+                        "(csrc/relay/relay.cpp, the Envoy role), python = aiohttp worker processes")
     p.add_argument("--v", type=int, default=1)
     a = p.parse_args(argv)
     logging.basicConfig(level=logging.DEBUG if a.v >= 3 else logging.INFO)
@@ -279,7 +282,7 @@ def main(argv=None):
             await seed(_App())
 
         run_multi(epp, elector, "0.0.0.0", a.port, a.metrics_port, a.workers, a.failure_mode, seed=seed_multi,
-                  grpc_port=a.grpc_port, grpc_offset=a.grpc_upstream_port_offset)
+                  grpc_port=a.grpc_port, grpc_offset=a.grpc_upstream_port_offset, data_plane=a.data_plane)
         return
 
     app.on_startup.insert(0, seed)

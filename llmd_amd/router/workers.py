@@ -335,15 +335,24 @@ def worker_main(uds: str, host: str, port: int, failure_mode: str):
 
 
 def run_multi(epp, elector, host: str, port: int, metrics_port: int, workers: int, failure_mode: str,
-              seed=None, grpc_port: int = 0, grpc_offset: int = 0):
+              seed=None, grpc_port: int = 0, grpc_offset: int = 0, data_plane: str = "native"):
     """Parent process: the EPP (+ its metrics port, discovery, the h2c gRPC router)
-    and an EppServer on a Unix socket; ``workers`` proxy processes serve ``port``.
-    A worker that exits is restarted; the parent exits non-zero if it cannot keep
-    them up."""
+    and an EppServer on a Unix socket; the data plane serves ``port``:
+    ``native`` = one llmd-relay process with ``workers`` epoll threads
+    (router/relay.py, csrc/relay/relay.cpp), ``python`` = ``workers`` aiohttp
+    WorkerProxy processes. A data-plane process that exits is restarted; the
+    parent exits non-zero if it cannot keep them up."""
     import multiprocessing as mp
 
     uds = f"/tmp/llmd-epp-{os.getpid()}-{port}.sock"
     ctx = mp.get_context("spawn")
+    relay_bin = None
+    if data_plane == "native":
+        from .relay import relay_binary
+
+        relay_bin = relay_binary()
+        if relay_bin is None:
+            log.warning("native relay unavailable: falling back to %d Python proxy workers", workers)
 
     async def run():
         if seed is not None:
@@ -366,6 +375,29 @@ def run_multi(epp, elector, host: str, port: int, metrics_port: int, workers: in
             from .grpc_proxy import GrpcRouter, offset_target
 
             await GrpcRouter(epp, offset_target(grpc_offset)).start(grpc_port)
+        if relay_bin is not None:
+            from .relay import spawn
+
+            relay = [spawn(uds, host, port, workers, failure_mode, relay_bin)]
+            log.info("router: EPP pid %d, native relay pid %d with %d threads on :%d (metrics :%d)", os.getpid(),
+                     relay[0].pid, workers, port, metrics_port)
+            try:
+                restarts = 0
+                while True:
+                    await asyncio.sleep(1.0)
+                    if relay[0].poll() is not None:
+                        restarts += 1
+                        if restarts > 10:
+                            raise SystemExit("router relay keeps dying")
+                        log.warning("router relay exited (%s): restarting", relay[0].returncode)
+                        relay[0] = spawn(uds, host, port, workers, failure_mode, relay_bin)
+            finally:
+                if relay[0].poll() is None:
+                    relay[0].terminate()
+                    try:
+                        relay[0].wait(5)
+                    except Exception:  # noqa: BLE001
+                        relay[0].kill()
         procs = []
         for i in range(workers):
             p = ctx.Process(target=worker_main, args=(uds, host, port, failure_mode), daemon=True)
@@ -386,6 +418,12 @@ def run_multi(epp, elector, host: str, port: int, metrics_port: int, workers: in
                     q.start()
                     procs[i] = q
 
+    import signal
+
+    def _term(*_):
+        raise SystemExit(0)  # unwinds run(): the relay child is terminated in its finally
+
+    signal.signal(signal.SIGTERM, _term)
     try:
         asyncio.run(run())
     finally:

@@ -13,12 +13,13 @@ B. End to end: E simulator processes, the router (llmd_amd.router.proxy) in its
    TTFT p50/p99 through the router vs the same load sent straight to the engines
    (round robin) - the difference is the router's added latency.
 
-  python scripts/bench_router.py [--endpoints 8] [--conc 64,256] [--secs 8] [--workers 1,4]
+  python scripts/bench_router.py [--endpoints 8] [--conc 64,256] [--secs 8] [--workers 1,py4,native4]
       [--out profiles/router_overhead.json]
 
-``--workers``: the router runs with that many proxy worker processes in front
-of one EPP process (router/workers.py); each count is measured against the same
-direct baseline.
+``--workers``: data planes in front of one EPP process (router/workers.py):
+``1`` the in-process Python proxy, ``pyN`` N aiohttp worker processes,
+``nativeN`` the llmd-relay executable with N epoll threads
+(csrc/relay/relay.cpp); each is measured against the same direct baseline.
 """
 from __future__ import annotations
 
@@ -162,11 +163,23 @@ def _wait_port(port, timeout=60):
     raise RuntimeError(f"port {port} never opened")
 
 
-def _start_router(env, ports, workers):
+def _plane(spec: str):
+    """'1' -> in-process Python proxy; 'pyN' -> N Python worker processes; 'nativeN' -> the
+    llmd-relay data plane with N threads (csrc/relay/relay.cpp)."""
+    if spec.startswith("native"):
+        return "native", int(spec[6:])
+    if spec.startswith("py"):
+        return "python", int(spec[2:])
+    return ("python" if int(spec) > 1 else "inproc"), int(spec)
+
+
+def _start_router(env, ports, spec):
+    plane, workers = _plane(spec)
     rport, mport = _free_port(), _free_port()
+    extra = ["--data-plane", plane] if plane != "inproc" else []
     router = subprocess.Popen([sys.executable, "-m", "llmd_amd.router.proxy", "--port", str(rport),
                                "--metrics-port", str(mport), "--workers", str(workers),
-                               "--endpoints", ",".join(f"127.0.0.1:{p}" for p in ports), "--v", "0"],
+                               "--endpoints", ",".join(f"127.0.0.1:{p}" for p in ports), "--v", "0"] + extra,
                               env=env, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
     return router, rport
 
@@ -181,7 +194,7 @@ def _stop(procs):
             p.kill()
 
 
-def bench_e2e(n_endpoints, concs, secs, max_tokens, procs, workers=(1,)) -> list:
+def bench_e2e(n_endpoints, concs, secs, max_tokens, procs, workers=("1",)) -> list:
     env = dict(os.environ, PYTHONPATH=ROOT)
     ports = [_free_port() for _ in range(n_endpoints)]
     sims = [subprocess.Popen([sys.executable, "-m", "llmd_amd.sim.server", "--port", str(p), "--max-num-seqs", "4096",
@@ -202,7 +215,8 @@ def bench_e2e(n_endpoints, concs, secs, max_tokens, procs, workers=(1,)) -> list
                 for c in concs:
                     d = base[c]
                     r = _load(routed, c, secs, max_tokens, procs)
-                    row = {"endpoints": n_endpoints, "router_workers": w, "conc": c, "max_tokens": max_tokens,
+                    row = {"endpoints": n_endpoints, "router_workers": _plane(w)[1], "data_plane": _plane(w)[0],
+                           "conc": c, "max_tokens": max_tokens,
                            "direct": d, "routed": r,
                            "added_ttft_p50_ms": round(r["ttft_p50_ms"] - d["ttft_p50_ms"], 2),
                            "added_ttft_p99_ms": round(r["ttft_p99_ms"] - d["ttft_p99_ms"], 2),
@@ -224,7 +238,9 @@ def main():
     ap.add_argument("--max-tokens", type=int, default=32)
     ap.add_argument("--procs", type=int, default=3, help="client processes")
     ap.add_argument("--skip-e2e", action="store_true")
-    ap.add_argument("--workers", default="1,4", help="router proxy worker processes to compare")
+    ap.add_argument("--workers", default="1,py4,native4",
+                    help="data planes to compare: 1 (in-process Python proxy), pyN (N Python worker "
+                         "processes), nativeN (llmd-relay with N threads)")
     ap.add_argument("--out", default=None)
     a = ap.parse_args()
     res = {"cpus": os.cpu_count(), "epp": [bench_epp(n) for n in (a.endpoints, 4 * a.endpoints)]}
@@ -232,7 +248,7 @@ def main():
         print(json.dumps({"epp_decision": r}), flush=True)
     if not a.skip_e2e:
         res["e2e"] = bench_e2e(a.endpoints, [int(c) for c in a.conc.split(",")], a.secs, a.max_tokens, a.procs,
-                               [int(w) for w in a.workers.split(",")])
+                               a.workers.split(","))
     if a.out:
         with open(a.out, "w") as f:
             json.dump(res, f, indent=1)
