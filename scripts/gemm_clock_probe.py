@@ -6,7 +6,7 @@ Each arm loops one GEMM for ~5 s; a side thread samples ``rocm-smi -c -P``
 power, and TF/s per GHz (the clock-normalised efficiency: the bf16 dense peak
 is 2.5 PF/s at 2.4 GHz = 1042 TF/s per GHz).
 
-  python scripts/gemm_clock_probe.py
+  python scripts/gemm_clock_probe.py [gemm,attn,moe]
 """
 import os
 import re
@@ -63,9 +63,66 @@ def arm(name, fn, flops, secs=5.0):
           f"{tf / (sk / 1000):6.0f} TF/s per GHz  ({len(samples)} samples)", flush=True)
 
 
+def attn_arms():
+    """GQA prefill attention (70B heads, one 5000-token causal prompt) and paged decode (B=64, ctx 5000)."""
+    import math
+
+    dev = "cuda"
+    Hq, Hkv, D, bs, ctx = 64, 8, 128, 64, 5000
+    nb = math.ceil(ctx / bs) * 64 + 1
+    kc = torch.randn(nb, Hkv, bs, D, device=dev, dtype=torch.bfloat16)
+    vc = torch.randn(nb, Hkv, bs, D, device=dev, dtype=torch.bfloat16)
+    per = math.ceil(ctx / bs)
+    bt = torch.randperm(nb - 1, device=dev)[:per].view(1, per).int()
+    q = torch.randn(ctx, Hq * D, device=dev, dtype=torch.bfloat16)
+    i32 = lambda v: torch.tensor([v], dtype=torch.int32, device=dev)  # noqa: E731
+    tpi = ops.prefill_tokens_per_item(Hq, Hkv, D, bs, False)
+    items = torch.tensor(ops.build_prefill_items([ctx], [ctx], tpi), dtype=torch.int32, device=dev).view(-1, 2)
+    out = torch.empty(ctx, Hq * D, device=dev, dtype=torch.bfloat16)
+    fl = 4 * Hq * D * sum(i + 1 for i in range(ctx))
+    arm("prefill attention v2 ISL 5000", lambda: ops.paged_prefill(q, kc, vc, bt, i32(0), i32(ctx), i32(ctx), Hq, Hkv,
+                                                                    D, D ** -0.5, 0, None, items=items, out=out), fl)
+    B = 64
+    btd = torch.randperm(nb - 1, device=dev)[:B * per].view(B, per).int()
+    qd = torch.randn(B, Hq * D, device=dev, dtype=torch.bfloat16)
+    sl = torch.full((B,), ctx, dtype=torch.int32, device=dev)
+    od = torch.empty(B, Hq * D, device=dev, dtype=torch.bfloat16)
+    split = ops.decode_split_plan(ctx, B, Hkv, Hq // Hkv)
+    arm("paged decode B=64 ctx 5000 (flops col = GB/s)",
+        lambda: ops.paged_decode(qd, kc, vc, btd, sl, Hq, Hkv, D, D ** -0.5, 0, None, split=split, out=od,
+                                 max_ctx=ctx), B * ctx * Hkv * D * 2 * 2 * 1000)
+
+
+def moe_arms():
+    """Block-fp8 and bf16 grouped expert GEMMs (moe4) at DeepSeek EP8 T=4096 and gpt-oss-120b T=5120."""
+    dev = "cuda"
+    for name, (T, E, k, d, F, act) in {"deepseek-ep8 T=4096": (4096, 32, 8, 7168, 2048, 0),
+                                       "gpt-oss-120b T=5120": (5120, 128, 4, 2880, 2880, 2)}.items():
+        x = torch.randn(T, d, device=dev, dtype=torch.bfloat16)
+        c128 = lambda n: (n + 127) // 128 * 128  # noqa: E731
+        w1 = (torch.randn(E, 2 * F, d, device=dev) * 0.02).to(torch.bfloat16)
+        w2 = (torch.randn(E, d, F, device=dev) * 0.02).to(torch.bfloat16)
+        w1q, w1s = ops.quant_fp8_block_weight(w1)
+        w2q, w2s = ops.quant_fp8_block_weight(w2)
+        w1q, w2q = ops.pad_fp8_k(w1q, c128(d)), ops.pad_fp8_k(w2q, c128(F))
+        ids, wts = ops.moe_topk(torch.randn(T, E, device=dev), k, scoring=0)
+        fl = 2 * T * k * 3 * F * d
+        arm(f"MoE fp8 {name}", lambda: ops.moe_experts_fp8(x, ids, wts, w1q, w1s, w2q, w2s, act), fl)
+        arm(f"MoE bf16 {name}", lambda: ops.moe_experts(x, ids, wts, w1, w2, act), fl)
+        del w1, w2, w1q, w2q
+        torch.cuda.empty_cache()
+
+
 def main():
     dev = "cuda"
     torch.manual_seed(0)
+    arms = sys.argv[1].split(",") if len(sys.argv) > 1 else ["gemm"]
+    if "attn" in arms:
+        attn_arms()
+    if "moe" in arms:
+        moe_arms()
+    if "gemm" not in arms:
+        return
     K = 8192
     for M in (5063, 4608):
         x = torch.randn(M, K, device=dev, dtype=torch.bfloat16)
