@@ -172,6 +172,8 @@ def plan(topo: dict, workdir: str) -> tuple[list[ProcSpec], dict]:
         else:
             cmd = [PY, "-m", "llmd_amd.router.proxy", "--port", str(r.get("port", 8000)),
                    "--endpoints-file", ep_file]
+            if int(r.get("workers", 1)) > 1:  # native relay threads in front of one EPP process
+                cmd += ["--workers", str(int(r["workers"])), "--metrics-port", str(r.get("metrics_port", 9090))]
         conf = r.get("config")
         if conf:
             if os.path.exists(str(conf)):
