@@ -33,6 +33,11 @@ constexpr int M4_BM = 256, M4_BN = 256, M4_BK = 64, M4_NT = 256;
 constexpr int M4_OPB = M4_BM * M4_BK * 2;  // 32 KB per operand per K-step
 constexpr int M4_BUF = 2 * M4_OPB;         // 64 KB
 constexpr int M4_RB = 37;                  // half-1 MFMA index of the next step's first read
+// Per-lane DMA offset past the buffer descriptors' 0x7fffffff-byte range: the load is out of bounds
+// and returns zeros. Padding slots and W rows past N (never stored) read it instead of a clamped
+// real row, so their MFMAs multiply zeros: with the kernels at the 1400 W package cap, operand bits
+// that do not toggle are clock (profiles/gemm_clock_power_r5.txt).
+constexpr uint32_t M4_OOB = 0x80000000u;
 
 __device__ __forceinline__ void m4_bar() {
   __builtin_amdgcn_sched_barrier(0);
@@ -98,14 +103,14 @@ __global__ __launch_bounds__(M4_NT, 1) void moe_gemm4_bf16_kernel(
     const int row = 8 * (MI * w + j) + (lane >> 3);
     const int c = (lane & 7) ^ ((row >> 1) & 7);
     const int sid = sorted_ids[m0 + row];
-    const int tok = sid < 0 ? 0 : (a_rows_are_slots ? m0 + row : sid / topk);
-    va[j] = (uint32_t)(((int64_t)tok * x_stride + c * 8) * 2);
+    const int tok = a_rows_are_slots ? m0 + row : sid / topk;
+    va[j] = sid < 0 ? M4_OOB : (uint32_t)(((int64_t)tok * x_stride + c * 8) * 2);
   }
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     const int row = 64 * w + 8 * j + (lane >> 3);
     const int c = (lane & 7) ^ ((row >> 1) & 7);
-    vw[j] = (uint32_t)(((int64_t)min(n0 + row, N - 1) * K + c * 8) * 2);
+    vw[j] = n0 + row < N ? (uint32_t)(((int64_t)(n0 + row) * K + c * 8) * 2) : M4_OOB;
   }
   auto dma = [&](int kt, int j, bool wop) {
     const uint32_t so = (uint32_t)(min(kt, nk - 1) * M4_BK * 2);
@@ -321,14 +326,14 @@ __global__ __launch_bounds__(M4_NT, 1) void moe_gemm4_fp8_kernel(
     const int row = 8 * (NA * w + j) + (lane >> 3);
     const int c = (lane & 7) ^ ((row >> 1) & 7);
     const int sid = sorted_ids[m0 + row];
-    const int tok = sid < 0 ? 0 : (a_rows_are_slots ? m0 + row : sid / topk);
-    va[j] = (uint32_t)((int64_t)tok * x_stride + c * 16);
+    const int tok = a_rows_are_slots ? m0 + row : sid / topk;
+    va[j] = sid < 0 ? M4_OOB : (uint32_t)((int64_t)tok * x_stride + c * 16);
   }
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     const int row = 64 * w + 8 * j + (lane >> 3);
     const int c = (lane & 7) ^ ((row >> 1) & 7);
-    vw[j] = (uint32_t)((int64_t)min(n0 + row, N - 1) * K + c * 16);
+    vw[j] = n0 + row < N ? (uint32_t)((int64_t)(n0 + row) * K + c * 16) : M4_OOB;
   }
   uint32_t vs;  // this lane's act-scale row SROWS w + lane (clamped to the tile)
   {

@@ -845,7 +845,7 @@ __global__ __launch_bounds__(NT6, 1) void pgemm6_kernel(const uint16_t* __restri
   for (int j = 0; j < 8; ++j) {
     const int row = 64 * w + 8 * j + (lane >> 3);
     const int c = (lane & 7) ^ ((row >> 1) & 7);
-    va[j] = (uint32_t)((min(m0 + row, M - 1) * lda + c * 8) * 2);
+    va[j] = m0 + row < M ? (uint32_t)(((m0 + row) * lda + c * 8) * 2) : 0x80000000u;  // past M: OOB zeros
     const int wrow = EPI == EPI_SILU_STD ? (row < 128 ? 0 : N / 2 - 128) + tn * 128 + row : n0 + row;
     vw[j] = (uint32_t)((wrow * ldw + c * 8) * 2);
   }
@@ -1042,7 +1042,7 @@ __global__ __launch_bounds__(NT6, 1) void pgemm7_kernel(const uint16_t* __restri
     for (int j = 0; j < 8; ++j) {
       const int row = 64 * w + 8 * j + (lane >> 3);
       const int c = (lane & 7) ^ ((row >> 1) & 7);
-      va[j] = (uint32_t)((min(tm * BM + row, M - 1) * lda + c * 8) * 2);
+      va[j] = tm * BM + row < M ? (uint32_t)(((tm * BM + row) * lda + c * 8) * 2) : 0x80000000u;
       const int wrow = EPI == EPI_SILU_STD ? (row < 128 ? 0 : N / 2 - 128) + tn * 128 + row : tn * BN + row;
       vw[j] = (uint32_t)((wrow * ldw + c * 8) * 2);
     }
