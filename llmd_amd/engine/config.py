@@ -384,7 +384,8 @@ class EngineConfig:
         cfg = cls(model=model, model_config=mc, **parts, **top)
         cfg.sched.max_model_len = min(cfg.sched.max_model_len, mc.max_position_embeddings)
         if cfg.sched.prefill_token_align < 0:
-            cfg.sched.prefill_token_align = 512 if str(cfg.device).startswith("cuda") else 0
+            cfg.sched.prefill_token_align = (int(os.environ.get("LLMD_PREFILL_ALIGN", "512"))
+                                             if str(cfg.device).startswith("cuda") else 0)
         return cfg
 
 
