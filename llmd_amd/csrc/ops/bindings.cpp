@@ -58,6 +58,8 @@ int llmd_dgemm_supported(int, int, int);
 int llmd_mgemm(const void*, int64_t, const void*, int64_t, int, int, int, int, int, int, void*, int64_t, float*,
                int*, hipStream_t);
 int llmd_mgemm_lds(int, int, int);
+int llmd_mgemm_add_rmsnorm(const void*, int64_t, const void*, int64_t, int, int, int, int, int, int, float*, void*,
+                           int64_t, const void*, float, void*, int64_t, hipStream_t);
 int llmd_mgemm_silu(const void*, int64_t, const void*, int64_t, int, int, int, int, int, void*, int64_t, hipStream_t);
 int llmd_pgemm(const void*, int64_t, const void*, int64_t, void*, int64_t, int, int, int, int, int, void*,
                hipStream_t);
@@ -475,6 +477,26 @@ void mgemm(torch::Tensor y, torch::Tensor x, torch::Tensor w, int64_t wrb, int64
                       nsplit > 1 ? mgemm_counters(y.device(), (N + 64 * wrb - 1) / (64 * wrb)) : nullptr,
                       cur_stream());
   TORCH_CHECK(rc == 0, "mgemm failed: ", rc);
+}
+
+// out = rmsnorm(residual + x w^T) * gamma with residual updated in place: the decode step's o / down
+// projection on the split-K medium-M GEMM with the residual-add + RMSNorm in its reduce (csrc/ops/mgemm.hip)
+void mgemm_add_rmsnorm(torch::Tensor out, torch::Tensor x, torch::Tensor w, int64_t wrb, int64_t nsplit,
+                       int64_t stages, torch::Tensor part, torch::Tensor residual, torch::Tensor gamma, double eps) {
+  const c10::hip::OptionalHIPGuard device_guard(dev_of(out));
+  CHECK_CUDA(x); CHECK_BF16(x); CHECK_BF16(w); CHECK_BF16(out); CHECK_BF16(residual); CHECK_BF16(gamma);
+  CHECK_INNER(x); CHECK_INNER(w); CHECK_INNER(out); CHECK_INNER(residual); CHECK_DT(part, at::kFloat);
+  TORCH_CHECK(x.dim() == 2 && w.dim() == 2 && out.dim() == 2 && residual.dim() == 2, "mgemm_add_rmsnorm: 2-D operands");
+  const int M = x.size(0), K = x.size(1), N = w.size(0);
+  TORCH_CHECK(M >= 1 && M <= 128 && w.size(1) == K && K % 64 == 0 && N % 8 == 0, "mgemm_add_rmsnorm: shapes");
+  TORCH_CHECK(out.size(0) == M && out.size(1) == N && residual.size(0) == M && residual.size(1) == N &&
+              gamma.numel() == N, "mgemm_add_rmsnorm: output / residual / gamma shape");
+  TORCH_CHECK(nsplit > 1 && part.numel() >= nsplit * (int64_t)M * N, "mgemm_add_rmsnorm: split-K workspace");
+  int rc = llmd_mgemm_add_rmsnorm(x.data_ptr(), x.stride(0), w.data_ptr(), w.stride(0), M, N, K, (int)wrb,
+                                  (int)nsplit, (int)stages, part.data_ptr<float>(), residual.data_ptr(),
+                                  residual.stride(0), gamma.data_ptr(), (float)eps, out.data_ptr(), out.stride(0),
+                                  cur_stream());
+  TORCH_CHECK(rc == 0, "mgemm_add_rmsnorm failed: ", rc);
 }
 
 // y [M, N] = x [M, K] . w [N, K]^T for prefill-sized M on the 256 x 256 LDS-DMA MFMA
@@ -1078,6 +1100,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {  // _C, or _C_debug (llmd_amd/build.p
   m.def("skinny_gemm", &skinny_gemm);
   m.def("skinny_supported", &skinny_supported);
   m.def("mgemm", &mgemm);
+  m.def("mgemm_add_rmsnorm", &mgemm_add_rmsnorm, "decode o / down projection with residual-add + RMSNorm in its split-K reduce");
   m.def("pgemm", &pgemm, "prefill bf16 GEMM (256x256 LDS-DMA MFMA tiles), optional fused SiLU-and-mul",
         py::arg("y"), py::arg("x"), py::arg("w"), py::arg("epi"), py::arg("variant"), py::arg("split_k") = true);
   m.def("mgemm_fp8", &mgemm_fp8);

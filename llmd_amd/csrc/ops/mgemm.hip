@@ -353,6 +353,79 @@ __global__ __launch_bounds__(256) void mgemm_reduce_kernel(const float* __restri
   *reinterpret_cast<uint2*>(y + (int64_t)m * y_stride + n) = make_uint2(lo, hi);
 }
 
+// The o / down projection's split-K partials -> y = bf16(sum); residual += y (rounded to bf16);
+// out = rmsnorm(residual) * gamma. One workgroup per row with 256 * VPT threads, one 8-column chunk
+// each (thread t: chunk t), so a row's partials stream with 4x the loads in flight of a 256-thread
+// row. Bit-identical to mgemm_reduce_kernel + rmsnorm.hip's fused_add_rms_norm (256 threads, thread i
+// owning chunks i, i + 256, ..): the same roundings, and the sum of squares is formed the unfused way -
+// the rounded values go through LDS and thread i accumulates its chunks c = 0 .. VPT-1 sequentially
+// (same FMA chain), then the same wave sums; the extra waves add exact zeros to the block sum.
+template <int VPT>
+__global__ __launch_bounds__(256 * VPT) void mgemm_reduce_norm_kernel(const float* __restrict__ part, int nsplit,
+                                                                      int M, int N, uint16_t* __restrict__ residual,
+                                                                      int64_t res_stride,
+                                                                      const uint16_t* __restrict__ gamma, float eps,
+                                                                      uint16_t* __restrict__ out, int64_t out_stride) {
+  constexpr int NTR = 256 * VPT;
+  __shared__ float red[NTR / 64];
+  __shared__ float vs[VPT > 1 ? NTR * 8 : 1];
+  const int row = blockIdx.x;
+  const int nchunk = N >> 3;
+  const int64_t total = (int64_t)M * N;
+  const int ci = threadIdx.x;
+  uint16_t* rr = residual + (int64_t)row * res_stride;
+  float v[8];
+  float ss = 0.f;
+  if (ci < nchunk) {
+    const float* p = part + (int64_t)row * N + ci * 8;
+    f32x4_t s0 = *reinterpret_cast<const f32x4_t*>(p), s1 = *reinterpret_cast<const f32x4_t*>(p + 4);
+    for (int k = 1; k < nsplit; ++k) {
+      s0 += *reinterpret_cast<const f32x4_t*>(p + (int64_t)k * total);
+      s1 += *reinterpret_cast<const f32x4_t*>(p + (int64_t)k * total + 4);
+    }
+    const float y[8] = {s0[0], s0[1], s0[2], s0[3], s1[0], s1[1], s1[2], s1[3]};
+    unpack8(pack8(y), v);  // the GEMM output as bf16
+    float rf[8];
+    unpack8(*reinterpret_cast<const u32x4_t*>(rr + ci * 8), rf);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] += rf[j];
+    const u32x4_t pr = pack8(v);  // the residual rounded once; normalise the rounded value
+    *reinterpret_cast<u32x4_t*>(rr + ci * 8) = pr;
+    unpack8(pr, v);
+  }
+  if constexpr (VPT == 1) {
+    if (ci < nchunk) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) ss += v[j] * v[j];
+    }
+  } else {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) vs[j * NTR + ci] = v[j];  // [j][chunk]: conflict-free writes and reads
+    __syncthreads();
+    if (ci < 256) {
+#pragma unroll
+      for (int c = 0; c < VPT; ++c) {
+        if (ci + 256 * c < nchunk) {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const float t = vs[j * NTR + ci + 256 * c];
+            ss += t * t;
+          }
+        }
+      }
+    }
+  }
+  ss = block_sum<NTR>(ss, red);
+  const float inv = rsqrtf(ss / (float)N + eps);
+  if (ci < nchunk) {
+    float wf[8], o[8];
+    unpack8(*reinterpret_cast<const u32x4_t*>(gamma + ci * 8), wf);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = v[j] * inv * wf[j];
+    *reinterpret_cast<u32x4_t*>(out + (int64_t)row * out_stride + ci * 8) = pack8(o);
+  }
+}
+
 typedef void (*mkern_t)(const void*, int64_t, const void*, int64_t, int, int, int, int, uint16_t*, int64_t,
                         float*, const float*, const float*, int*);
 
@@ -448,6 +521,39 @@ extern "C" int llmd_mgemm(const void* x, int64_t x_stride, const void* w, int64_
     hipLaunchKernelGGL(mgemm_reduce_kernel, dim3((unsigned)((total4 + 255) / 256)), dim3(256), 0, st, part, nsplit,
                        M, N, (uint16_t*)y, y_stride);
   }
+  return (int)hipGetLastError();
+}
+
+// out = rmsnorm(residual + X W^T) * gamma, residual updated in place (the decode step's o / down
+// projection with the next residual-add + RMSNorm fused into its split-K reduce); nsplit must stay > 1
+// after the no-empty-split clamp (else -3: the caller runs the plain GEMM + norm).
+extern "C" int llmd_mgemm_add_rmsnorm(const void* x, int64_t x_stride, const void* w, int64_t w_stride, int M, int N,
+                                      int K, int wrb, int nsplit, int stages, float* part, void* residual,
+                                      int64_t res_stride, const void* gamma, float eps, void* out, int64_t out_stride,
+                                      hipStream_t st) {
+  if (M < 1 || M > 128 || K % 64 != 0 || N % 8 != 0 || N > 8 * 1024 || nsplit < 2 || x_stride % 8 ||
+      w_stride % 8 || res_stride % 8 || out_stride % 8)
+    return -1;
+  if (llmd_mgemm_lds(M, wrb, stages) == 0) return -1;
+  const int mb = M <= 64 ? 4 : M <= 96 ? 6 : 8;
+  mkern_t k = pick_m<false>(mb, wrb, stages);
+  if (k == nullptr) return -2;
+  const int nk = K / 64;
+  const int per = (nk + nsplit - 1) / nsplit;
+  nsplit = (nk + per - 1) / per;
+  if (nsplit < 2) return -3;
+  const int bn = 64 * wrb;
+  dim3 grid((N + bn - 1) / bn, nsplit);
+  hipLaunchKernelGGL(k, grid, dim3(NT), 0, st, x, x_stride, w, w_stride, M, N, K, per, (uint16_t*)out, out_stride,
+                     part, (const float*)nullptr, (const float*)nullptr, (int*)nullptr);
+  const int vpt = (N / 8 + 255) / 256;  // the unfused norm's chunks per thread (its launch rounds to 1, 2, 4)
+#define RN(V)                                                                                                   \
+  hipLaunchKernelGGL((mgemm_reduce_norm_kernel<V>), dim3(M), dim3(256 * V), 0, st, (const float*)part, nsplit, M, \
+                     N, (uint16_t*)residual, res_stride, (const uint16_t*)gamma, eps, (uint16_t*)out, out_stride)
+  if (vpt <= 1) RN(1);
+  else if (vpt <= 2) RN(2);
+  else RN(4);
+#undef RN
   return (int)hipGetLastError();
 }
 

@@ -8,6 +8,8 @@ Residual stream is carried separately so every norm fuses the residual add.
 """
 from __future__ import annotations
 
+from typing import Optional
+
 import torch
 
 from llmd_amd import ops
@@ -25,6 +27,10 @@ class LlamaMLP(torch.nn.Module):
         self.down = RowLinear(cfg.intermediate_size, cfg.hidden_size, device=device)
 
     def forward(self, x):
+        return self.down(self.hidden(x))
+
+    def hidden(self, x):
+        """silu(x Wg^T) * (x Wu^T): the down projection's input (fp8 (q, scale) for an fp8 down)."""
         gu = self.gate_up
         if (gu.lora is None and gu.bias is None and not wants_fp8_input(self.down) and x.dim() == 2
                 and gu.weight.dtype == torch.bfloat16):
@@ -32,15 +38,25 @@ class LlamaMLP(torch.nn.Module):
             # EPI_SILU_STD) where the shipped table has it ahead of hipBLASLt + the act kernel
             v = ops.pgemm_silu_plan(x, gu.weight)
             if v is not None:
-                return self.down(ops.pgemm_silu(x, gu.weight, variant=v))
+                return ops.pgemm_silu(x, gu.weight, variant=v)
             # decode: the same fusion in the medium-M GEMM (csrc/ops/mgemm.hip ACT form)
             p = ops.mgemm_silu_plan(x, gu.weight)
             if p is not None:
-                return self.down(ops.mgemm_silu(x, gu.weight, p))
+                return ops.mgemm_silu(x, gu.weight, p)
         h = gu(x)
         if wants_fp8_input(self.down):  # SiLU*up fused with the down proj's fp8 activation quant
-            return self.down(ops.gated_act_quant(h, ops.ACT_SILU))
-        return self.down(ops.gated_act(h, ops.ACT_SILU))
+            return ops.gated_act_quant(h, ops.ACT_SILU)
+        return ops.gated_act(h, ops.ACT_SILU)
+
+
+def norm_fused_plan(lin, x):
+    """Medium-M GEMM plan for ``lin(x)`` with the following residual-add + RMSNorm fused into its
+    split-K reduce (ops.mgemm_add_rmsnorm), or None: bf16 TP1 row-parallel linears without bias or
+    LoRA at decode-sized M (33..128) whose shipped plan splits K."""
+    if (not isinstance(x, torch.Tensor) or lin.bias is not None or lin.lora is not None
+            or lin.weight.dtype != torch.bfloat16 or (lin.reduce and get_state().tp_size > 1)):
+        return None
+    return ops.mgemm_norm_plan(x, lin.weight)
 
 
 class LlamaDecoderLayer(torch.nn.Module):
@@ -70,9 +86,22 @@ class LlamaDecoderLayer(torch.nn.Module):
         ops.qk_rms_norm(qkv, self.q_norm.weight, self.k_norm.weight, a.Hq, a.Hkv, self.q_norm.eps)
 
     def forward(self, x, residual, meta: AttnMeta):
+        x, residual, _ = self.run(x, residual, meta)
+        return x, residual
+
+    def run(self, x, residual, meta: AttnMeta, normed: bool = False, next_norm: Optional[RMSNorm] = None):
+        """The layer with decode-step norm fusions. ``normed``: x already is this layer's
+        input_layernorm output (fused into the previous layer's down projection). ``next_norm``:
+        the RMSNorm that follows this layer (the next layer's input norm or the model's final
+        norm); where the decode GEMM plan allows, the down projection's split-K reduce applies
+        it and the third return value is True. The o projection always takes the
+        post-attention norm this way when it can (csrc/ops/mgemm.hip mgemm_reduce_norm_kernel:
+        bit-identical to GEMM + reduce + fused_add_rms_norm, two launches fewer)."""
         # W8A8: the norms emit fp8 + per-row scales straight into the fp8 GEMMs
         q_in = wants_fp8_input(self.qkv)
-        if residual is None:
+        if normed:
+            pass
+        elif residual is None:
             residual = x.clone()
             x = self.input_layernorm(x, quant=q_in)
         else:
@@ -80,10 +109,23 @@ class LlamaDecoderLayer(torch.nn.Module):
         qkv = self.qkv(x)
         if self.qk_norm:
             self._apply_qk_norm(qkv)
-        x = self.o_proj(self.attn(qkv, meta))
+        a = self.attn(qkv, meta)
         q_mlp = isinstance(self.mlp, LlamaMLP) and wants_fp8_input(self.mlp.gate_up)
-        x, residual = self.post_attention_layernorm(x, residual, quant=q_mlp)
-        return self.mlp(x), residual
+        p = None if q_mlp else norm_fused_plan(self.o_proj, a)
+        if p is not None:
+            pn = self.post_attention_layernorm
+            x = ops.mgemm_add_rmsnorm(a, self.o_proj.weight, p, residual, pn.weight, pn.eps)
+        else:
+            x = self.o_proj(a)
+            x, residual = self.post_attention_layernorm(x, residual, quant=q_mlp)
+        if next_norm is not None and type(self.mlp) is LlamaMLP:
+            h = self.mlp.hidden(x)
+            p = norm_fused_plan(self.mlp.down, h)
+            if p is not None:
+                return ops.mgemm_add_rmsnorm(h, self.mlp.down.weight, p, residual, next_norm.weight,
+                                             next_norm.eps), residual, True
+            return self.mlp.down(h), residual, False
+        return self.mlp(x), residual, False
 
 
 class LlamaForCausalLM(torch.nn.Module):
@@ -146,8 +188,25 @@ class LlamaForCausalLM(torch.nn.Module):
     def forward(self, input_ids: torch.Tensor, meta: AttnMeta) -> torch.Tensor:
         x = self.embed(input_ids)
         residual = None
-        for layer in self.layers:
-            x, residual = layer(x, residual, meta)
+        normed = False
+        n = len(self.layers)
+        for i, layer in enumerate(self.layers):
+            if not isinstance(layer, LlamaDecoderLayer) or type(layer).forward is not LlamaDecoderLayer.forward:
+                x, residual = layer(x, residual, meta)
+                normed = False
+                continue
+            # the norm after this layer, for the decode down projection's fused reduce
+            nxt = self.layers[i + 1] if i + 1 < n else None
+            if nxt is None:
+                nn = self.norm
+            elif (isinstance(nxt, LlamaDecoderLayer) and type(nxt).forward is LlamaDecoderLayer.forward
+                  and not wants_fp8_input(nxt.qkv)):
+                nn = nxt.input_layernorm
+            else:
+                nn = None
+            x, residual, normed = layer.run(x, residual, meta, normed, nn)
+        if normed:
+            return x
         x, _ = self.norm(x, residual)
         return x
 

@@ -951,6 +951,35 @@ def mgemm(x: torch.Tensor, w: torch.Tensor, plan: tuple[int, int, int]) -> torch
     return y
 
 
+# decode o / down projection with the following residual-add + RMSNorm in the medium-M GEMM's split-K
+# reduce (LLMD_MGEMM_NORM=0: the plain GEMM + reduce + fused_add_rms_norm kernels)
+MGEMM_NORM = os.environ.get("LLMD_MGEMM_NORM", "1") == "1"
+
+
+def mgemm_norm_plan(x: torch.Tensor, w: torch.Tensor) -> Optional[tuple[int, int, int]]:
+    """The shipped medium-M plan of this projection when it is split over K (so its partials can be
+    reduced together with the residual-add + RMSNorm), else None."""
+    if not (MGEMM_NORM and _SKINNY and x.dim() == 2 and 33 <= x.shape[0] <= 128 and mgemm_ok(x, w)
+            and w.shape[0] % 8 == 0 and w.shape[0] <= 8192 and w.shape[1] >= 128):
+        return None
+    plan = mgemm_choice(x.shape[0], w.shape[0], w.shape[1])
+    if plan is None or plan[1] < 2:
+        return None
+    return plan
+
+
+def mgemm_add_rmsnorm(x: torch.Tensor, w: torch.Tensor, plan: tuple[int, int, int], residual: torch.Tensor,
+                      gamma: torch.Tensor, eps: float) -> torch.Tensor:
+    """residual += x W^T (rounded to bf16); returns rmsnorm(residual) * gamma - bit-identical to
+    ``linear`` + ``fused_add_rms_norm`` (csrc/ops/mgemm.hip mgemm_reduce_norm_kernel)."""
+    M, N = x.shape[0], w.shape[0]
+    wrb, ns, stages = plan
+    out = torch.empty(M, N, dtype=x.dtype, device=x.device)
+    part = torch.empty(ns * M * N, dtype=torch.float32, device=x.device)
+    native().mgemm_add_rmsnorm(out, x, w, wrb, ns, stages, part, residual, gamma, eps)
+    return out
+
+
 # decode gate/up projection with the SiLU-and-mul in the medium-M GEMM's epilogue (LLMD_MGEMM_SILU=0:
 # the plain GEMM + act kernel)
 MGEMM_SILU = os.environ.get("LLMD_MGEMM_SILU", "1") == "1"

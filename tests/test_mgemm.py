@@ -110,3 +110,69 @@ def test_mgemm_silu_matches_fp32(M, F, K):
             assert y.shape == (M, F)
             err = (y.float() - want).abs().max().item()
             assert err <= tol, (M, F, K, wrb, stages, err)
+
+
+@pytest.mark.parametrize("M", [33, 64, 128])
+@pytest.mark.parametrize("N,K,plan", [(8192, 8192, (1, 2, 4)), (8192, 28672, (4, 6, 3)), (1032, 1024, (2, 3, 3))])
+def test_mgemm_add_rmsnorm_bit_identical(M, N, K, plan):
+    """The o / down projection with the residual-add + RMSNorm in its split-K reduce
+    (ops.mgemm_add_rmsnorm) against the two-kernel path it replaces (mgemm + fused_add_rms_norm):
+    bit-identical output AND residual, and close to an fp32 reference; N not a multiple of 2048
+    (partial per-thread chunks), the 70B o / down shapes and plans."""
+    from llmd_amd import ops
+
+    if not ops.native().mgemm_lds(M, plan[0], plan[2]):
+        pytest.skip("no ring for this M")
+    torch.manual_seed(M + N + K)
+    x = torch.randn(M, K, device="cuda").bfloat16()
+    w = (torch.randn(N, K, device="cuda") * 0.02).bfloat16()
+    res0 = torch.randn(M, N, device="cuda").bfloat16()
+    g = (1 + 0.1 * torch.randn(N, device="cuda")).bfloat16()
+    eps = 1e-5
+    # two-kernel path
+    y = ops.mgemm(x, w, plan)
+    r_ref = res0.clone()
+    ops.fused_add_rms_norm(y, r_ref, g, eps)
+    # fused
+    r = res0.clone()
+    out = ops.mgemm_add_rmsnorm(x, w, plan, r, g, eps)
+    torch.cuda.synchronize()
+    assert torch.equal(r, r_ref)
+    assert torch.equal(out, y)
+    # and against fp32
+    h = res0.float() + _ref(x, w)
+    want = h * torch.rsqrt(h.pow(2).mean(-1, keepdim=True) + eps) * g.float()
+    assert (out.float() - want).abs().max().item() < 5e-2 * max(1.0, want.abs().max().item())
+
+
+def test_llama_decode_norm_fusion_greedy_equal(monkeypatch):
+    """small-llama (40 sequences: decode M = 40, hipGraphs) decodes the same greedy tokens with
+    the decode-GEMM norm fusions on and off. Its o / down shapes are not in the shipped medium-M
+    table, so a split-K plan is supplied for them in both runs; the fused reduce is bit-identical,
+    so the logits and tokens are too."""
+    from llmd_amd import ops
+    from llmd_amd.engine.config import EngineConfig
+    from llmd_amd.engine.engine import LLMEngine
+    from llmd_amd.engine.request import SamplingParams
+
+    base = ops.mgemm_choice
+    monkeypatch.setattr(ops, "mgemm_choice", lambda M, N, K: (1, 2, 3) if N == 1024 else base(M, N, K))
+    calls = []
+    fused = ops.mgemm_add_rmsnorm
+    monkeypatch.setattr(ops, "mgemm_add_rmsnorm", lambda *a, **k: calls.append(1) or fused(*a, **k))
+    sp = SamplingParams(max_tokens=6, temperature=0.0, ignore_eos=True)
+    prompts = [[(7 * i + j) % 1000 + 5 for j in range(40 + i)] for i in range(40)]
+
+    def run():
+        cfg = EngineConfig.create("small-llama", device="cuda", block_size=64, num_gpu_blocks=256,
+                                  max_num_batched_tokens=4096, max_num_seqs=40, max_model_len=1024,
+                                  cuda_graph_max_bs=64)
+        return [r.output_token_ids for r in LLMEngine(cfg).generate(prompts, sp)]
+
+    on = run()
+    assert calls, "the fused o / down path never ran"
+    monkeypatch.setattr(ops, "MGEMM_NORM", False)
+    calls.clear()
+    off = run()
+    assert not calls
+    assert on == off and all(len(t) == 6 for t in on)
