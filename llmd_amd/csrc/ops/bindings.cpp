@@ -58,6 +58,9 @@ int llmd_dgemm_supported(int, int, int);
 int llmd_mgemm(const void*, int64_t, const void*, int64_t, int, int, int, int, int, int, void*, int64_t, float*,
                int*, hipStream_t);
 int llmd_mgemm_lds(int, int, int);
+int llmd_mgemm_partials(const void*, int64_t, const void*, int64_t, int, int, int, int, int, int, float*, hipStream_t);
+int llmd_reduce_rope_cache(const float*, int, int, void*, int64_t, const int64_t*, const float*, int, int, int, int,
+                           const int64_t*, void*, void*, int64_t, int, int, int, int, float, float, hipStream_t);
 int llmd_mgemm_add_rmsnorm(const void*, int64_t, const void*, int64_t, int, int, int, int, int, int, float*, void*,
                            int64_t, const void*, float, void*, int64_t, hipStream_t);
 int llmd_mgemm_silu(const void*, int64_t, const void*, int64_t, int, int, int, int, int, void*, int64_t, hipStream_t);
@@ -230,6 +233,48 @@ void rope_cache(torch::Tensor qkv, torch::Tensor positions, torch::Tensor cos_si
                   cos_sin.data_ptr<float>(), rot, Hq, Hkv, D, slots.data_ptr<int64_t>(),
                   k_cache.data_ptr(), v_cache.data_ptr(), k_cache.stride(0), k_cache.size(2), T,
                   neox ? 1 : 0, f8 ? 1 : 0, (float)(1.0 / k_scale), (float)(1.0 / v_scale), cur_stream());
+}
+
+// The decode QKV projection's split-K partials (mgemm_partials) reduced, rotated and written to the paged
+// cache in one kernel: qkv [T, W] receives the projection (Q rotated), K / V go to the cache.
+void reduce_rope_cache(torch::Tensor part, int64_t nsplit, torch::Tensor qkv, torch::Tensor positions,
+                       torch::Tensor cos_sin, int64_t Hq, int64_t Hkv, int64_t D, torch::Tensor slots,
+                       torch::Tensor k_cache, torch::Tensor v_cache, bool neox, double k_scale, double v_scale) {
+  const c10::hip::OptionalHIPGuard device_guard(dev_of(qkv));
+  CHECK_CUDA(qkv); CHECK_BF16(qkv); CHECK_INNER(qkv); CHECK_DT(part, at::kFloat);
+  CHECK_DT(positions, at::kLong); CHECK_DT(slots, at::kLong); CHECK_DT(cos_sin, at::kFloat);
+  TORCH_CHECK(qkv.dim() == 2 && qkv.size(1) >= (Hq + 2 * Hkv) * D, "reduce_rope_cache: qkv width");
+  const int T = qkv.size(0), W = qkv.size(1);
+  TORCH_CHECK(part.numel() >= nsplit * (int64_t)T * W, "reduce_rope_cache: partials");
+  TORCH_CHECK(positions.numel() == T && slots.numel() == T, "reduce_rope_cache: T mismatch");
+  TORCH_CHECK(cos_sin.dim() == 2 && cos_sin.is_contiguous(), "cos_sin 2-D contiguous");
+  const int rot = cos_sin.size(1);
+  TORCH_CHECK(rot % 16 == 0 && rot <= D && D % 8 == 0, "reduce_rope_cache: rotary dim");
+  const bool f8 = is_fp8_cache(k_cache);
+  TORCH_CHECK(v_cache.scalar_type() == k_cache.scalar_type(), "k/v cache dtype");
+  TORCH_CHECK(k_cache.dim() == 4 && k_cache.size(1) == Hkv && k_cache.size(3) == D &&
+              k_cache.stride(3) == 1 && k_cache.stride(2) == D && k_cache.stride(1) == k_cache.size(2) * D &&
+              v_cache.sizes() == k_cache.sizes() && v_cache.strides() == k_cache.strides(), "k/v cache layout");
+  int rc = llmd_reduce_rope_cache(part.data_ptr<float>(), (int)nsplit, W, qkv.data_ptr(), qkv.stride(0),
+                                  positions.data_ptr<int64_t>(), cos_sin.data_ptr<float>(), rot, Hq, Hkv, D,
+                                  slots.data_ptr<int64_t>(), k_cache.data_ptr(), v_cache.data_ptr(), k_cache.stride(0),
+                                  k_cache.size(2), T, neox ? 1 : 0, f8 ? 1 : 0, (float)(1.0 / k_scale),
+                                  (float)(1.0 / v_scale), cur_stream());
+  TORCH_CHECK(rc == 0, "reduce_rope_cache failed: ", rc);
+}
+
+// split-K partials of y = x w^T (csrc/ops/mgemm.hip) for a consumer that fuses the reduce; returns nsplit
+int64_t mgemm_partials(torch::Tensor x, torch::Tensor w, int64_t wrb, int64_t nsplit, int64_t stages,
+                       torch::Tensor part) {
+  const c10::hip::OptionalHIPGuard device_guard(dev_of(x));
+  CHECK_CUDA(x); CHECK_BF16(x); CHECK_BF16(w); CHECK_INNER(x); CHECK_INNER(w); CHECK_DT(part, at::kFloat);
+  TORCH_CHECK(x.dim() == 2 && w.dim() == 2 && w.size(1) == x.size(1), "mgemm_partials: shapes");
+  const int M = x.size(0), K = x.size(1), N = w.size(0);
+  TORCH_CHECK(part.numel() >= nsplit * (int64_t)M * N, "mgemm_partials: workspace");
+  int rc = llmd_mgemm_partials(x.data_ptr(), x.stride(0), w.data_ptr(), w.stride(0), M, N, K, (int)wrb, (int)nsplit,
+                               (int)stages, part.data_ptr<float>(), cur_stream());
+  TORCH_CHECK(rc >= 2, "mgemm_partials failed: ", rc);
+  return rc;
 }
 
 void gated_act(torch::Tensor out, torch::Tensor x, int64_t mode, double alpha, double limit) {
@@ -1100,6 +1145,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {  // _C, or _C_debug (llmd_amd/build.p
   m.def("skinny_gemm", &skinny_gemm);
   m.def("skinny_supported", &skinny_supported);
   m.def("mgemm", &mgemm);
+  m.def("mgemm_partials", &mgemm_partials, "split-K partials of the medium-M GEMM (no reduce); returns nsplit");
+  m.def("reduce_rope_cache", &reduce_rope_cache, "QKV split-K reduce + RoPE + paged cache write");
   m.def("mgemm_add_rmsnorm", &mgemm_add_rmsnorm, "decode o / down projection with residual-add + RMSNorm in its split-K reduce");
   m.def("pgemm", &pgemm, "prefill bf16 GEMM (256x256 LDS-DMA MFMA tiles), optional fused SiLU-and-mul",
         py::arg("y"), py::arg("x"), py::arg("w"), py::arg("epi"), py::arg("variant"), py::arg("split_k") = true);

@@ -524,6 +524,28 @@ extern "C" int llmd_mgemm(const void* x, int64_t x_stride, const void* w, int64_
   return (int)hipGetLastError();
 }
 
+// The split-K partials of Y = X W^T only (fp32 [nsplit][M][N] in part, no reduce): their consumer fuses
+// the reduce (rope_cache.hip reduce_rope_cache_kernel for the QKV projection). Returns the split count
+// after the no-empty-split clamp (>= 2), or a negative error.
+extern "C" int llmd_mgemm_partials(const void* x, int64_t x_stride, const void* w, int64_t w_stride, int M, int N,
+                                   int K, int wrb, int nsplit, int stages, float* part, hipStream_t st) {
+  if (M < 1 || M > 128 || K % 64 != 0 || N % 8 != 0 || nsplit < 2 || x_stride % 8 || w_stride % 8) return -1;
+  if (llmd_mgemm_lds(M, wrb, stages) == 0) return -1;
+  const int mb = M <= 64 ? 4 : M <= 96 ? 6 : 8;
+  mkern_t k = pick_m<false>(mb, wrb, stages);
+  if (k == nullptr) return -2;
+  const int nk = K / 64;
+  const int per = (nk + nsplit - 1) / nsplit;
+  nsplit = (nk + per - 1) / per;
+  if (nsplit < 2) return -3;
+  const int bn = 64 * wrb;
+  dim3 grid((N + bn - 1) / bn, nsplit);
+  hipLaunchKernelGGL(k, grid, dim3(NT), 0, st, x, x_stride, w, w_stride, M, N, K, per, (uint16_t*)nullptr,
+                     (int64_t)0, part, (const float*)nullptr, (const float*)nullptr, (int*)nullptr);
+  const hipError_t e = hipGetLastError();
+  return e == hipSuccess ? nsplit : -(int)e - 100;
+}
+
 // out = rmsnorm(residual + X W^T) * gamma, residual updated in place (the decode step's o / down
 // projection with the next residual-add + RMSNorm fused into its split-K reduce); nsplit must stay > 1
 // after the no-empty-split clamp (else -3: the caller runs the plain GEMM + norm).

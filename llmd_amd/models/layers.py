@@ -231,13 +231,20 @@ class PagedAttention(torch.nn.Module):
         self.k_scale = 1.0
         self.v_scale = 1.0
 
-    def forward(self, qkv: torch.Tensor, meta: AttnMeta) -> torch.Tensor:
+    def forward(self, qkv: torch.Tensor, meta: AttnMeta, parts=None) -> torch.Tensor:
+        """``parts`` = (fp32 split-K partials, nsplit) of the QKV projection whose reduce is fused
+        with RoPE + the cache write (``qkv`` is then the allocated, unwritten output)."""
         T = qkv.shape[0]
         Hq, Hkv, D = self.Hq, self.Hkv, self.D
         if self.window and meta.swa is not None:  # hybrid KV cache: this layer's pool has its own tables
             meta = meta.swa
-        ops.rope_cache(qkv, meta.positions, self.cos_sin, Hq, Hkv, D, meta.slot_mapping,
-                       self.k_cache, self.v_cache, self.neox, self.k_scale, self.v_scale)
+        if parts is not None:
+            ops.reduce_rope_cache(parts[0], parts[1], qkv, meta.positions, self.cos_sin, Hq, Hkv, D,
+                                  meta.slot_mapping, self.k_cache, self.v_cache, self.neox, self.k_scale,
+                                  self.v_scale)
+        else:
+            ops.rope_cache(qkv, meta.positions, self.cos_sin, Hq, Hkv, D, meta.slot_mapping,
+                           self.k_cache, self.v_cache, self.neox, self.k_scale, self.v_scale)
         out = torch.empty(T, Hq * D, dtype=qkv.dtype, device=qkv.device)
         nd = meta.num_decode
         # a mixed step (eager): the memory-bound decode rows run on a side stream beside the compute-bound

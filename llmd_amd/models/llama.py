@@ -5,6 +5,10 @@ Per layer (dense TP=k):
   -> O GEMM (+TP all-reduce) -> fused_add_rmsnorm -> gate_up GEMM
   -> SiLU*mul -> down GEMM (+TP all-reduce)
 Residual stream is carried separately so every norm fuses the residual add.
+Decode steps on the split-K medium-M GEMM (csrc/ops/mgemm.hip) fold the
+kernels after each projection into its reduce: QKV reduce + RoPE + cache write
+(rope_cache.hip reduce_rope_cache_kernel), o / down reduce + residual add +
+the next RMSNorm (mgemm_reduce_norm_kernel), bit-identical to the unfused path.
 """
 from __future__ import annotations
 
@@ -47,6 +51,20 @@ class LlamaMLP(torch.nn.Module):
         if wants_fp8_input(self.down):  # SiLU*up fused with the down proj's fp8 activation quant
             return ops.gated_act_quant(h, ops.ACT_SILU)
         return ops.gated_act(h, ops.ACT_SILU)
+
+
+def qkv_fused_plan(lin, x):
+    """Medium-M GEMM plan of the QKV projection when its split-K reduce can be fused with RoPE + the
+    cache write (ops.reduce_rope_cache), or None: bf16 weights without bias or LoRA, decode-sized M,
+    a shipped plan that splits K."""
+    if (not isinstance(x, torch.Tensor) or lin.bias is not None or lin.lora is not None
+            or lin.weight.dtype != torch.bfloat16 or not (ops.MGEMM_NORM and ops._SKINNY)
+            or lin.weight.shape[0] > 24576):
+        return None
+    if not (x.dim() == 2 and 33 <= x.shape[0] <= 128 and ops.mgemm_ok(x, lin.weight)):
+        return None
+    plan = ops.mgemm_choice(x.shape[0], lin.weight.shape[0], lin.weight.shape[1])
+    return plan if plan is not None and plan[1] >= 2 and lin.weight.shape[1] // 64 >= 2 else None
 
 
 def norm_fused_plan(lin, x):
@@ -106,10 +124,16 @@ class LlamaDecoderLayer(torch.nn.Module):
             x = self.input_layernorm(x, quant=q_in)
         else:
             x, residual = self.input_layernorm(x, residual, quant=q_in)
-        qkv = self.qkv(x)
-        if self.qk_norm:
-            self._apply_qk_norm(qkv)
-        a = self.attn(qkv, meta)
+        p = None if (self.qk_norm or q_in) else qkv_fused_plan(self.qkv, x)
+        if p is not None:  # decode: the QKV split-K reduce fused with RoPE + the cache write
+            parts = ops.mgemm_partials(x, self.qkv.weight, p)
+            a = self.attn(torch.empty(x.shape[0], self.qkv.weight.shape[0], dtype=x.dtype, device=x.device), meta,
+                          parts=parts)
+        else:
+            qkv = self.qkv(x)
+            if self.qk_norm:
+                self._apply_qk_norm(qkv)
+            a = self.attn(qkv, meta)
         q_mlp = isinstance(self.mlp, LlamaMLP) and wants_fp8_input(self.mlp.gate_up)
         p = None if q_mlp else norm_fused_plan(self.o_proj, a)
         if p is not None:

@@ -968,6 +968,24 @@ def mgemm_norm_plan(x: torch.Tensor, w: torch.Tensor) -> Optional[tuple[int, int
     return plan
 
 
+def mgemm_partials(x: torch.Tensor, w: torch.Tensor, plan: tuple[int, int, int]):
+    """Split-K partials of x W^T on the medium-M GEMM, for a consumer that fuses the reduce:
+    returns (fp32 partials [nsplit * M * N], nsplit)."""
+    M, N = x.shape[0], w.shape[0]
+    part = torch.empty(plan[1] * M * N, dtype=torch.float32, device=x.device)
+    ns = native().mgemm_partials(x, w, plan[0], plan[1], plan[2], part)
+    return part, int(ns)
+
+
+def reduce_rope_cache(part: torch.Tensor, nsplit: int, qkv: torch.Tensor, positions, cos_sin, Hq, Hkv, D, slots,
+                      k_cache, v_cache, neox=True, k_scale=1.0, v_scale=1.0):
+    """The QKV projection's split-K reduce + RoPE + paged KV write in one kernel (rope_cache.hip):
+    ``qkv`` [T, W] (allocated, unwritten) receives the projection with Q rotated - bit-identical to
+    mgemm + rope_cache."""
+    native().reduce_rope_cache(part, nsplit, qkv, positions, cos_sin, Hq, Hkv, D, slots, k_cache, v_cache, neox,
+                               k_scale, v_scale)
+
+
 def mgemm_add_rmsnorm(x: torch.Tensor, w: torch.Tensor, plan: tuple[int, int, int], residual: torch.Tensor,
                       gamma: torch.Tensor, eps: float) -> torch.Tensor:
     """residual += x W^T (rounded to bf16); returns rmsnorm(residual) * gamma - bit-identical to

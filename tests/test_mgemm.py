@@ -147,19 +147,20 @@ def test_mgemm_add_rmsnorm_bit_identical(M, N, K, plan):
 
 def test_llama_decode_norm_fusion_greedy_equal(monkeypatch):
     """small-llama (40 sequences: decode M = 40, hipGraphs) decodes the same greedy tokens with
-    the decode-GEMM norm fusions on and off. Its o / down shapes are not in the shipped medium-M
-    table, so a split-K plan is supplied for them in both runs; the fused reduce is bit-identical,
-    so the logits and tokens are too."""
+    the decode-GEMM reduce fusions (o / down + RMSNorm, QKV + RoPE + cache write) on and off. Its
+    shapes are not in the shipped medium-M table, so a split-K plan is supplied for them in both
+    runs; the fused reduces are bit-identical, so the logits and tokens are too."""
     from llmd_amd import ops
     from llmd_amd.engine.config import EngineConfig
     from llmd_amd.engine.engine import LLMEngine
     from llmd_amd.engine.request import SamplingParams
 
     base = ops.mgemm_choice
-    monkeypatch.setattr(ops, "mgemm_choice", lambda M, N, K: (1, 2, 3) if N == 1024 else base(M, N, K))
+    monkeypatch.setattr(ops, "mgemm_choice", lambda M, N, K: (1, 2, 3) if N in (1024, 1536) else base(M, N, K))
     calls = []
-    fused = ops.mgemm_add_rmsnorm
+    fused, fused_rope = ops.mgemm_add_rmsnorm, ops.reduce_rope_cache
     monkeypatch.setattr(ops, "mgemm_add_rmsnorm", lambda *a, **k: calls.append(1) or fused(*a, **k))
+    monkeypatch.setattr(ops, "reduce_rope_cache", lambda *a, **k: calls.append(2) or fused_rope(*a, **k))
     sp = SamplingParams(max_tokens=6, temperature=0.0, ignore_eos=True)
     prompts = [[(7 * i + j) % 1000 + 5 for j in range(40 + i)] for i in range(40)]
 
@@ -170,9 +171,47 @@ def test_llama_decode_norm_fusion_greedy_equal(monkeypatch):
         return [r.output_token_ids for r in LLMEngine(cfg).generate(prompts, sp)]
 
     on = run()
-    assert calls, "the fused o / down path never ran"
+    assert 1 in calls and 2 in calls, "the fused o / down / QKV paths never ran"
     monkeypatch.setattr(ops, "MGEMM_NORM", False)
     calls.clear()
     off = run()
     assert not calls
     assert on == off and all(len(t) == 6 for t in on)
+
+
+@pytest.mark.parametrize("neox,fp8", [(True, False), (False, False), (True, True)])
+@pytest.mark.parametrize("M,Hq,Hkv,K,plan", [(64, 64, 8, 8192, (2, 3, 3)), (40, 8, 2, 1024, (1, 2, 3))])
+def test_reduce_rope_cache_bit_identical(M, Hq, Hkv, K, plan, neox, fp8):
+    """The decode QKV projection's split-K reduce fused with RoPE + the paged cache write
+    (ops.mgemm_partials + ops.reduce_rope_cache) against mgemm + rope_cache: the same qkv rows
+    (Q rotated, K / V as projected) and the same K / V cache bytes; padded rows (slot -1) skipped."""
+    from llmd_amd import ops
+
+    D, bs = 128, 64
+    W = (Hq + 2 * Hkv) * D
+    if not ops.native().mgemm_lds(M, plan[0], plan[2]):
+        pytest.skip("no ring for this M")
+    torch.manual_seed(M + Hq + K + int(neox) + 2 * int(fp8))
+    x = torch.randn(M, K, device="cuda").bfloat16()
+    w = (torch.randn(W, K, device="cuda") * 0.02).bfloat16()
+    pos = torch.randint(0, 4000, (M,), device="cuda", dtype=torch.int64)
+    inv = 1.0 / (10000 ** (torch.arange(0, D, 2, device="cuda").float() / D))
+    ang = torch.arange(4096, device="cuda").float()[:, None] * inv[None]
+    cos_sin = torch.cat([ang.cos(), ang.sin()], 1).contiguous()
+    nblk = 64
+    slots = torch.randperm(nblk * bs, device="cuda")[:M].to(torch.int64)
+    slots[3] = -1
+    dt = torch.float8_e4m3fn if fp8 else torch.bfloat16
+    caches = [torch.zeros(nblk, Hkv, bs, D, device="cuda").to(dt) for _ in range(4)]
+    ks, vs = (0.5, 0.25) if fp8 else (1.0, 1.0)
+    # two-kernel path
+    q1 = ops.mgemm(x, w, plan)
+    ops.rope_cache(q1, pos, cos_sin, Hq, Hkv, D, slots, caches[0], caches[1], neox, ks, vs)
+    # fused
+    part, ns = ops.mgemm_partials(x, w, plan)
+    q2 = torch.empty(M, W, device="cuda", dtype=torch.bfloat16)
+    ops.reduce_rope_cache(part, ns, q2, pos, cos_sin, Hq, Hkv, D, slots, caches[2], caches[3], neox, ks, vs)
+    torch.cuda.synchronize()
+    assert torch.equal(q1, q2)
+    assert torch.equal(caches[0].view(torch.uint8), caches[2].view(torch.uint8))
+    assert torch.equal(caches[1].view(torch.uint8), caches[3].view(torch.uint8))
