@@ -180,7 +180,8 @@ def test_llama_decode_norm_fusion_greedy_equal(monkeypatch):
 
 
 @pytest.mark.parametrize("neox,fp8", [(True, False), (False, False), (True, True)])
-@pytest.mark.parametrize("M,Hq,Hkv,K,plan", [(64, 64, 8, 8192, (2, 3, 3)), (40, 8, 2, 1024, (1, 2, 3))])
+@pytest.mark.parametrize("M,Hq,Hkv,K,plan", [(64, 64, 8, 8192, (2, 3, 3)), (40, 8, 2, 1024, (1, 2, 3)),
+                                             (128, 32, 4, 8192, (2, 6, 3))])  # 70B TP1 / small / 70B TP2 shard
 def test_reduce_rope_cache_bit_identical(M, Hq, Hkv, K, plan, neox, fp8):
     """The decode QKV projection's split-K reduce fused with RoPE + the paged cache write
     (ops.mgemm_partials + ops.reduce_rope_cache) against mgemm + rope_cache: the same qkv rows
