@@ -8,6 +8,7 @@ Also keeps in-process summaries (TTFT/ITL lists) for the benchmark harness.
 """
 from __future__ import annotations
 
+import collections
 import time
 from typing import Optional
 
@@ -67,24 +68,33 @@ class EngineMetrics:
                                      buckets=TOK_BUCKETS, registry=r)
         self._last_prefix = (0, 0)
         self._last_preempt = 0
-        # in-process summaries for benchmarks
-        self.ttfts: list[float] = []
-        self.itls: list[float] = []
+        # in-process summaries for benchmarks (bounded: a long-running server must not grow them forever)
+        self.ttfts: collections.deque = collections.deque(maxlen=1 << 16)
+        self.itls: collections.deque = collections.deque(maxlen=1 << 16)
         self.n_gen = 0
         self.n_prompt = 0
         self._last_tok_time: dict[str, float] = {}
         self.running.labels(model_name).set(0)
         self.waiting.labels(model_name).set(0)
         self.kv_usage.labels(model_name).set(0)
+        # label children of the per-step / per-token series, resolved once (labels() locks and
+        # hashes on every call; on_step touches every running request each step)
+        self._c_itl = self.itl.labels(model_name)
+        self._c_ttft = self.ttft.labels(model_name)
+        self._c_iter = self.iter_tokens.labels(model_name)
+        self._c_gen = self.gen_tokens.labels(model_name)
+        self._c_running = self.running.labels(model_name)
+        self._c_waiting = self.waiting.labels(model_name)
+        self._c_kv = self.kv_usage.labels(model_name)
 
     def on_arrival(self, r):
         pass
 
     def on_step(self, so, touched, dt, n_running, n_waiting, usage, prefix_stats):
         m = self.model
-        self.running.labels(m).set(n_running)
-        self.waiting.labels(m).set(n_waiting)
-        self.kv_usage.labels(m).set(usage)
+        self._c_running.set(n_running)
+        self._c_waiting.set(n_waiting)
+        self._c_kv.set(usage)
         hits, queries = prefix_stats
         dh, dq = hits - self._last_prefix[0], queries - self._last_prefix[1]
         if dh > 0:
@@ -98,24 +108,24 @@ class EngineMetrics:
         if ptoks:
             self.prompt_tokens.labels(m).inc(ptoks)
             self.n_prompt += ptoks
-        self.iter_tokens.labels(m).observe(so.num_tokens)
+        self._c_iter.observe(so.num_tokens)
         ng = len(touched)
         if ng:
-            self.gen_tokens.labels(m).inc(ng)
+            self._c_gen.inc(ng)
             self.n_gen += ng
         now = time.monotonic()
+        itl, last_tok = self._c_itl, self._last_tok_time
         for r in touched:
-            n = len(r.output_token_ids)
-            if n == 1 and r.first_token_time is not None:
+            if len(r.output_token_ids) == 1 and r.first_token_time is not None:
                 t = r.first_token_time - r.arrival_time
-                self.ttft.labels(m).observe(t)
+                self._c_ttft.observe(t)
                 self.ttfts.append(t)
             else:
-                last = self._last_tok_time.get(r.request_id)
+                last = last_tok.get(r.request_id)
                 if last is not None:
-                    self.itl.labels(m).observe(now - last)
+                    itl.observe(now - last)
                     self.itls.append(now - last)
-            self._last_tok_time[r.request_id] = now
+            last_tok[r.request_id] = now
 
     def on_finish(self, r):
         m = self.model
