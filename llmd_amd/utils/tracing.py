@@ -18,7 +18,6 @@ import os
 import random
 import threading
 import time
-from dataclasses import dataclass, field
 from typing import Optional
 
 _current: contextvars.ContextVar = contextvars.ContextVar("llmd_span", default=None)
@@ -49,16 +48,29 @@ def configure_otlp(endpoint: Optional[str] = None):
 configure_otlp()
 
 
-@dataclass
 class Span:
-    name: str
-    trace_id: str
-    span_id: str
-    parent_id: Optional[str]
-    sampled: bool
-    start: float = field(default_factory=time.time)
-    end: Optional[float] = None
-    attrs: dict = field(default_factory=dict)
+    """One span. ``span_id`` is drawn lazily (the first time it is read: a child span,
+    ``traceparent`` injection, an exporter), so the unsampled majority of spans on the
+    router's per-request path cost no id generation."""
+
+    __slots__ = ("name", "trace_id", "_span_id", "parent_id", "sampled", "start", "end", "attrs")
+
+    def __init__(self, name: str, trace_id: str, span_id: Optional[str], parent_id: Optional[str], sampled: bool,
+                 start: Optional[float] = None, end: Optional[float] = None, attrs: Optional[dict] = None):
+        self.name = name
+        self.trace_id = trace_id
+        self._span_id = span_id
+        self.parent_id = parent_id
+        self.sampled = sampled
+        self.start = time.time() if start is None else start
+        self.end = end
+        self.attrs = {} if attrs is None else attrs
+
+    @property
+    def span_id(self) -> str:
+        if self._span_id is None:
+            self._span_id = _hex(64)
+        return self._span_id
 
     def set(self, k, v):
         self.attrs[k] = v
@@ -66,6 +78,9 @@ class Span:
     @property
     def traceparent(self) -> str:
         return f"00-{self.trace_id}-{self.span_id}-{'01' if self.sampled else '00'}"
+
+    def __repr__(self):
+        return f"Span({self.name!r}, trace={self.trace_id}, span={self.span_id}, parent={self.parent_id})"
 
 
 def parse_traceparent(tp: Optional[str]) -> Optional[tuple[str, str, bool]]:
@@ -87,34 +102,54 @@ def current() -> Optional[Span]:
     return _current.get()
 
 
-@contextlib.contextmanager
-def span(name: str, attrs: Optional[dict] = None, traceparent: Optional[str] = None):
-    if not ENABLED:
-        yield None
-        return
-    parent = _current.get()
-    if parent is not None:
-        tid, pid, sampled = parent.trace_id, parent.span_id, parent.sampled
-    else:
-        ext = parse_traceparent(traceparent)
-        if ext:
-            tid, pid, sampled = ext
+_TRACE_ALL = os.environ.get("LLMD_TRACE_ALL") == "1"
+
+
+class _SpanCtx:
+    """``with span(...) as s``: a plain context-manager object (a generator-based
+    contextmanager costs several microseconds per use; the EPP opens ~6 spans per request)."""
+
+    __slots__ = ("name", "attrs", "tp", "s", "tok", "ot")
+
+    def __init__(self, name, attrs, tp):
+        self.name, self.attrs, self.tp = name, attrs, tp
+        self.s = self.tok = self.ot = None
+
+    def __enter__(self):
+        if not ENABLED:
+            return None
+        parent = _current.get()
+        if parent is not None:
+            tid, pid, sampled = parent.trace_id, parent.span_id, parent.sampled
         else:
-            tid, pid, sampled = _hex(128), None, random.random() < SAMPLE_RATIO
-    s = Span(name, tid, _hex(64), pid, sampled, attrs=dict(attrs or {}))
-    tok = _current.set(s)
-    try:
+            ext = parse_traceparent(self.tp)
+            if ext:
+                tid, pid, sampled = ext
+            else:
+                tid, pid, sampled = _hex(128), None, random.random() < SAMPLE_RATIO
+        s = self.s = Span(self.name, tid, None, pid, sampled, attrs=dict(self.attrs) if self.attrs else None)
+        self.tok = _current.set(s)
         if _otel_tracer is not None and sampled:  # pragma: no cover
-            with _otel_tracer.start_as_current_span(name, attributes=s.attrs):
-                yield s
-        else:
-            yield s
-    finally:
+            self.ot = _otel_tracer.start_as_current_span(self.name, attributes=s.attrs)
+            self.ot.__enter__()
+        return s
+
+    def __exit__(self, et, ev, tb):
+        s = self.s
+        if s is None:
+            return False
+        if self.ot is not None:  # pragma: no cover
+            self.ot.__exit__(et, ev, tb)
         s.end = time.time()
-        _current.reset(tok)
-        if sampled or os.environ.get("LLMD_TRACE_ALL") == "1":
+        _current.reset(self.tok)
+        if s.sampled or _TRACE_ALL:
             with _lock:
                 _ring.append(s)
+        return False
+
+
+def span(name: str, attrs: Optional[dict] = None, traceparent: Optional[str] = None) -> _SpanCtx:
+    return _SpanCtx(name, attrs, traceparent)
 
 
 def recent_spans(name: Optional[str] = None) -> list[Span]:
