@@ -89,6 +89,8 @@ void llmd_rms_norm_quant(void*, int64_t, float*, const void*, int64_t, void*, in
                          hipStream_t);
 void llmd_gated_act_quant(void*, int64_t, float*, const void*, int64_t, int, int, int, float, float, hipStream_t);
 int llmd_quant_fp8_groups(const void*, int64_t, void*, int64_t, float*, int64_t, int, int, hipStream_t);
+int llmd_quant_fp8_groups_padded(const void*, int64_t, void*, int64_t, float*, int64_t, int, int, int, const int*,
+                                 hipStream_t);
 void llmd_moe_gemm_fp8(const void*, int64_t, const float*, int64_t, int, const int*, const int*, int, const void*,
                        int64_t, const float*, int, int, void*, int64_t, int, int, float, float, int, const void*,
                        hipStream_t);
@@ -981,6 +983,28 @@ void quant_fp8_groups(torch::Tensor x, torch::Tensor q, torch::Tensor scale) {
   TORCH_CHECK(rc == 0, "quant_fp8_groups failed: ", rc);
 }
 
+// x [T, d] bf16 -> q [T, kp] e4m3 (zeros past d) + per-128 scales; rows >= row_limit[0] skipped when given
+void quant_fp8_groups_padded(torch::Tensor x, torch::Tensor q, torch::Tensor scale, c10::optional<torch::Tensor> row_limit) {
+  const c10::hip::OptionalHIPGuard device_guard(dev_of(x));
+  CHECK_CUDA(x); CHECK_BF16(x); CHECK_INNER(x); CHECK_INNER(q); CHECK_DT(q, at::kFloat8_e4m3fn);
+  CHECK_DT(scale, at::kFloat);
+  const int d = x.size(1), kp = q.size(1);
+  TORCH_CHECK(x.dim() == 2 && q.dim() == 2 && q.size(0) == x.size(0) && d % 8 == 0 && kp % 8 == 0 && kp >= d,
+              "quant_fp8_groups_padded shapes");
+  TORCH_CHECK(scale.dim() == 2 && scale.size(0) >= x.size(0) && scale.size(1) >= (d + 127) / 128 &&
+                  scale.stride(1) == 1, "quant_fp8_groups_padded: scale [T, ceil(d/128)]");
+  TORCH_CHECK(x.stride(0) % 8 == 0 && q.stride(0) % 8 == 0, "16-B rows");
+  const int* lim = nullptr;
+  if (row_limit.has_value()) {
+    CHECK_DT((*row_limit), at::kInt);
+    lim = row_limit->data_ptr<int>();
+  }
+  int rc = llmd_quant_fp8_groups_padded(x.data_ptr(), x.stride(0), q.data_ptr(), q.stride(0),
+                                        scale.data_ptr<float>(), scale.stride(0), x.size(0), d, kp, lim,
+                                        cur_stream());
+  TORCH_CHECK(rc == 0, "quant_fp8_groups_padded failed: ", rc);
+}
+
 void moe_gemm_fp8(torch::Tensor X, torch::Tensor xs, int64_t topk, torch::Tensor sorted_ids, torch::Tensor tile_expert,
                   torch::Tensor W, torch::Tensor ws, torch::Tensor Y, int64_t mode, int64_t act, double alpha,
                   double limit, bool a_rows_are_slots, c10::optional<torch::Tensor> bias, int64_t tile_m,
@@ -1168,6 +1192,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {  // _C, or _C_debug (llmd_amd/build.p
   m.def("moe_tile_m", &llmd_moe_gemm_tile_m);
   m.def("quant_fp8_rows", &quant_fp8_rows);
   m.def("quant_fp8_groups", &quant_fp8_groups);
+  m.def("quant_fp8_groups_padded", &quant_fp8_groups_padded, py::arg("x"), py::arg("q"), py::arg("scale"),
+        py::arg("row_limit") = py::none());
   m.def("rms_norm_quant", &rms_norm_quant);
   m.def("gated_act_quant", &gated_act_quant);
   m.def("moe_gemm_fp8", &moe_gemm_fp8, py::arg("X"), py::arg("xs"), py::arg("topk"), py::arg("sorted_ids"),

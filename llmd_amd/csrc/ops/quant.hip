@@ -51,11 +51,16 @@ __global__ __launch_bounds__(NT) void quant_fp8_rows_kernel(const uint16_t* __re
 // Per (row, 128-element group) scales (DeepSeek / DeepGEMM activation format):
 // 16 consecutive lanes own one group's 16 packets; the group amax is a 16-lane
 // xor-shuffle reduction. s[t][g] = amax / 448.
+// kp > d: q rows are kp bytes wide and columns [d, kp) are zero-filled (the K-padded operand of the
+// grouped GEMM); row_limit (device scalar, nullable): rows at or past it are left untouched - the
+// grouped GEMM's padded-slot rows beyond the last real expert tile, which it never reads.
 __global__ __launch_bounds__(NT) void quant_fp8_groups_kernel(const uint16_t* __restrict__ x, int64_t xs,
                                                               uint8_t* __restrict__ q, int64_t qs,
                                                               float* __restrict__ scale, int64_t ss, int d,
+                                                              int kp, const int* __restrict__ row_limit,
                                                               float floor_) {
   const int64_t t = blockIdx.x;
+  if (row_limit != nullptr && t >= *row_limit) return;
   const u32x4_t* xr = reinterpret_cast<const u32x4_t*>(x + t * xs);
   u32x2_t* qr = reinterpret_cast<u32x2_t*>(q + t * qs);
   const int nc = d / 8;
@@ -77,6 +82,7 @@ __global__ __launch_bounds__(NT) void quant_fp8_groups_kernel(const uint16_t* __
     for (int i = 0; i < 8; ++i) f[i] *= inv;
     if (ok) qr[c] = f32x8_to_fp8(f);
   }
+  for (int c = d / 8 + threadIdx.x; c < kp / 8; c += NT) qr[c] = u32x2_t{0u, 0u};
 }
 
 }  // namespace
@@ -86,7 +92,18 @@ extern "C" int llmd_quant_fp8_groups(const void* x, int64_t xs, void* q, int64_t
   if (T == 0) return 0;
   if (d % 8) return -1;
   hipLaunchKernelGGL(quant_fp8_groups_kernel, dim3(T), dim3(NT), 0, st, (const uint16_t*)x, xs, (uint8_t*)q, qs,
-                     scale, ss, d, 1e-12f);
+                     scale, ss, d, d, (const int*)nullptr, 1e-12f);
+  return (int)hipGetLastError();
+}
+
+// rows of kp >= d bytes (zeros past d), rows >= *row_limit skipped (row_limit nullable)
+extern "C" int llmd_quant_fp8_groups_padded(const void* x, int64_t xs, void* q, int64_t qs, float* scale,
+                                            int64_t ss, int T, int d, int kp, const int* row_limit,
+                                            hipStream_t st) {
+  if (T == 0) return 0;
+  if (d % 8 || kp % 8 || kp < d || qs < kp) return -1;
+  hipLaunchKernelGGL(quant_fp8_groups_kernel, dim3(T), dim3(NT), 0, st, (const uint16_t*)x, xs, (uint8_t*)q, qs,
+                     scale, ss, d, kp, row_limit, 1e-12f);
   return (int)hipGetLastError();
 }
 

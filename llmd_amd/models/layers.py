@@ -120,12 +120,14 @@ class RowLinear(torch.nn.Module):
     lora = None
 
     def forward(self, x):
-        y = _linear(self, x, None)
+        # one rank (no reduce to follow): the bias rides in the GEMM epilogue instead of a separate add
+        fold = self.bias is not None and self.lora is None and (not self.reduce or get_state().tp_size == 1)
+        y = _linear(self, x, self.bias if fold else None)
         if self.lora is not None:  # partial sums join the layer's all-reduce
             self.lora.apply(y, x)
         if self.reduce:
             y = tp_all_reduce(y)
-        if self.bias is not None:
+        if self.bias is not None and not fold:
             y = y + self.bias
         return y
 

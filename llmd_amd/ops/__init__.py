@@ -540,16 +540,17 @@ def quant_fp8_block_weight(w: torch.Tensor, block: int = 128):
     return q, s.contiguous()
 
 
-def _quant_groups_padded(x: torch.Tensor, kp: int):
-    """quant_fp8_groups into rows of ``kp`` >= d columns, zeros past d (GPU)."""
+def _quant_groups_padded(x: torch.Tensor, kp: int, row_limit: Optional[torch.Tensor] = None):
+    """quant_fp8_groups into rows of ``kp`` >= d columns, zeros past d, in one kernel (GPU).
+    ``row_limit`` (int32 device scalar, e.g. moe_align's padded-slot total): rows at or past it
+    are skipped - the grouped GEMM never reads them."""
     T, d = x.shape
-    if kp == d:
+    if kp == d and row_limit is None:
         return quant_fp8_groups(x)
     x = x if x.stride(-1) == 1 and x.stride(0) % 8 == 0 else x.contiguous()
     q = torch.empty(T, kp, dtype=FP8, device=x.device)
-    q.view(torch.uint8)[:, d:].zero_()
     s = torch.empty(T, (kp + 127) // 128, dtype=torch.float32, device=x.device)
-    native().quant_fp8_groups(x, q[:, :d], s)
+    native().quant_fp8_groups_padded(x, q, s, row_limit)
     return q, s
 
 
@@ -676,7 +677,7 @@ def moe_experts_fp8(x, ids, wts, w1q, w1s, w2q, w2s, act=0, alpha=1.702, limit=7
         # v4: PGR2 4-wave tiles, A rows and their act scales gathered by the LDS-DMA (csrc/ops/moe4.hip)
         h = torch.empty(max_p, F, dtype=torch.bfloat16, device=dev)
         C.moe_gemm4_fp8(xq, xs, k, sorted_ids, tile_e, w1q, w1s, h, 1, act, alpha, limit, False, b1, bm)
-        hq, hs = _quant_groups_padded(h, Kp2)
+        hq, hs = _quant_groups_padded(h, Kp2, total)  # slots past the last real tile are never read
         y = torch.empty(max_p, d, dtype=torch.bfloat16, device=dev)
         C.moe_gemm4_fp8(hq, hs, 1, sorted_ids, tile_e, w2q, w2s, y, 0, 0, 0.0, 0.0, True, b2, bm)
         if out is None:
@@ -686,7 +687,7 @@ def moe_experts_fp8(x, ids, wts, w1q, w1s, w2q, w2s, act=0, alpha=1.702, limit=7
     else:
         h = torch.empty(max_p, F, dtype=torch.bfloat16, device=dev)
         C.moe_gemm_fp8(xq, xs, k, sorted_ids, tile_e, w1q, w1s, h, 1, act, alpha, limit, False, b1, bm)
-        hq, hs = _quant_groups_padded(h, Kp2)
+        hq, hs = _quant_groups_padded(h, Kp2, total)
     y = torch.empty(max_p, d, dtype=torch.bfloat16, device=dev)
     # second GEMM: A rows are the sorted slots themselves (row p of hq; a_rows_are_slots)
     C.moe_gemm_fp8(hq, hs, 1, sorted_ids, tile_e, w2q, w2s, y, 0, 0, 0.0, 0.0, True, b2, bm)
