@@ -216,6 +216,21 @@ __global__ __launch_bounds__(M4_NT, 1) void moe_gemm4_bf16_kernel(
   constexpr int WROWS = TBM / 2;
   char* img = lds + w * (WROWS * 256);
   const int ncol0 = n0 + wc * 128;
+  // the expert bias of this lane's 8 x 4 columns, loaded once per tile (4 consecutive bf16 = one 8-B load;
+  // N % 8 == 0 so a group is wholly in or out; columns past N are never stored)
+  float bv[8][4];
+  if (bias != nullptr) {
+    const uint16_t* bp = bias + (int64_t)e * N;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int n = ncol0 + 16 * j + 4 * fq;
+      const u32x2_t raw = n < N ? *reinterpret_cast<const u32x2_t*>(bp + n) : u32x2_t{0u, 0u};
+      bv[j][0] = __uint_as_float(raw[0] << 16);
+      bv[j][1] = __uint_as_float(raw[0] & 0xffff0000u);
+      bv[j][2] = __uint_as_float(raw[1] << 16);
+      bv[j][3] = __uint_as_float(raw[1] & 0xffff0000u);
+    }
+  }
 #pragma unroll
   for (int i = 0; i < MI; ++i)
 #pragma unroll
@@ -224,10 +239,7 @@ __global__ __launch_bounds__(M4_NT, 1) void moe_gemm4_bf16_kernel(
       f32x4_t v = acc[i][j];
       if (bias != nullptr) {
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int n = min(ncol0 + col + r, N - 1);
-          v[r] += bf2f(bias[(int64_t)e * N + n]);
-        }
+        for (int r = 0; r < 4; ++r) v[r] += bv[j][r];
       }
       if constexpr (MODE == 0) {
         u32x2_t p;
@@ -495,6 +507,22 @@ __global__ __launch_bounds__(M4_NT, 1) void moe_gemm4_fp8_kernel(
   constexpr int WROWS = TBM / 2;
   char* img = lds + w * (WROWS * 256);
   const int ncol0 = n0 + wc * 128;
+  // the expert bias of this lane's 4 x 4 x 4 columns, loaded once per tile (one 8-B load per 4 columns)
+  float bv[4][4][4];
+  if (bias != nullptr) {
+    const uint16_t* bp = bias + (int64_t)e * N;
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int n = ncol0 + 32 * j + 8 * g + 4 * h;
+        const u32x2_t raw = n < N ? *reinterpret_cast<const u32x2_t*>(bp + n) : u32x2_t{0u, 0u};
+        bv[j][g][0] = __uint_as_float(raw[0] << 16);
+        bv[j][g][1] = __uint_as_float(raw[0] & 0xffff0000u);
+        bv[j][g][2] = __uint_as_float(raw[1] << 16);
+        bv[j][g][3] = __uint_as_float(raw[1] & 0xffff0000u);
+      }
+  }
 #pragma unroll
   for (int j = 0; j < 4; ++j)
 #pragma unroll
@@ -506,7 +534,7 @@ __global__ __launch_bounds__(M4_NT, 1) void moe_gemm4_fp8_kernel(
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
           v[q] = acc[j][i][4 * g + q];
-          if (bias != nullptr) v[q] += bf2f(bias[(int64_t)e * N + min(ncol0 + col + q, N - 1)]);
+          if (bias != nullptr) v[q] += bv[j][g][q];
         }
         if constexpr (MODE == 0) {
           u32x2_t p;
