@@ -295,6 +295,13 @@ __global__ __launch_bounds__(NT, 2) void moe_gemm_kernel(
     }
   }
   // epilogue: C[row = 4*kq + r][col = r16] within each 16x16 fragment
+  // the expert bias of this lane's columns, loaded once (not once per accumulator element)
+  float bvj[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int col = n0 + wn * 64 + j * 16 + r16;
+    bvj[j] = (bias && col < N) ? bf2f(bias[(int64_t)e * N + col]) : 0.f;
+  }
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
 #pragma unroll
@@ -305,7 +312,7 @@ __global__ __launch_bounds__(NT, 2) void moe_gemm_kernel(
       for (int j = 0; j < 4; ++j) {
         const int col = n0 + wn * 64 + j * 16 + r16;
         float v = acc[i][j][r];
-        if (bias && col < N) v += bf2f(bias[(int64_t)e * N + col]);
+        v += bvj[j];
         if (MODE == 0) {
           if (col < N) Y[(int64_t)row * y_stride + col] = f2bf(v);
         } else {
@@ -445,6 +452,13 @@ __global__ __launch_bounds__(G2_NT, 2) void moe_gemm2_kernel(
     compute(buf1);
   }
   // epilogue: C[row = 16i + 4kq + r][col = 64w + 16j + r16]
+  // the expert bias of this lane's columns, loaded once (not once per accumulator element)
+  float bvj[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int col = n0 + 64 * w + 16 * j + r16;
+    bvj[j] = (bias && col < N) ? bf2f(bias[(int64_t)e * N + col]) : 0.f;
+  }
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
 #pragma unroll
@@ -455,7 +469,7 @@ __global__ __launch_bounds__(G2_NT, 2) void moe_gemm2_kernel(
       for (int j = 0; j < 4; ++j) {
         const int col = n0 + 64 * w + 16 * j + r16;
         float v = acc[i][j][r];
-        if (bias && col < N) v += bf2f(bias[(int64_t)e * N + col]);
+        v += bvj[j];
         if (MODE == 0) {
           if (col < N) Y[(int64_t)row * y_stride + col] = f2bf(v);
         } else {
@@ -603,6 +617,13 @@ __global__ __launch_bounds__(NT, 2) void moe_gemm_fp8_kernel(
       __syncthreads();
     }
   }
+  // the expert bias of this lane's columns, loaded once (not once per accumulator element)
+  float bvj[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int col = n0 + wn * 64 + j * 16 + r16;
+    bvj[j] = (bias && col < N) ? bf2f(bias[(int64_t)e * N + col]) : 0.f;
+  }
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
 #pragma unroll
@@ -613,7 +634,7 @@ __global__ __launch_bounds__(NT, 2) void moe_gemm_fp8_kernel(
       for (int j = 0; j < 4; ++j) {
         const int col = n0 + wn * 64 + j * 16 + r16;
         float v = acc[i][j][r];
-        if (bias && col < N) v += bf2f(bias[(int64_t)e * N + col]);
+        v += bvj[j];
         if (MODE == 0) {
           if (col < N) Y[(int64_t)row * y_stride + col] = f2bf(v);
         } else {
@@ -791,6 +812,13 @@ __global__ __launch_bounds__(G2_NT, 2) void moe_gemm2_fp8_kernel(
     }
     compute(buf1, xv1, wv1);
   }
+  // the expert bias of this lane's columns, loaded once (not once per accumulator element)
+  float bvj[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int col = n0 + 64 * w + 16 * j + r16;
+    bvj[j] = (bias && col < N) ? bf2f(bias[(int64_t)e * N + col]) : 0.f;
+  }
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
 #pragma unroll
@@ -801,7 +829,7 @@ __global__ __launch_bounds__(G2_NT, 2) void moe_gemm2_fp8_kernel(
       for (int j = 0; j < 4; ++j) {
         const int col = n0 + 64 * w + 16 * j + r16;
         float v = acc[i][j][r];
-        if (bias && col < N) v += bf2f(bias[(int64_t)e * N + col]);
+        v += bvj[j];
         if (MODE == 0) {
           if (col < N) Y[(int64_t)row * y_stride + col] = f2bf(v);
         } else {
@@ -1077,6 +1105,13 @@ __global__ __launch_bounds__(G3_NT, 1) void moe_gemm3_fp8_kernel(
     // this wave's 32 h columns, partials of the 4 N-waves through LDS
     __syncthreads();  // every wave is out of the K loop: the ring is free
     float* amax_lds = reinterpret_cast<float*>(lds);  // [256 rows][4 N-waves]
+    // the expert bias of this lane's columns, loaded once (not once per accumulator element)
+    float bvj[2];
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int col = n0 + 64 * wn + 32 * j + l32;
+      bvj[j] = (bias && col < N) ? bf2f(bias[(int64_t)e * N + col]) : 0.f;
+    }
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
 #pragma unroll
@@ -1086,7 +1121,7 @@ __global__ __launch_bounds__(G3_NT, 1) void moe_gemm3_fp8_kernel(
         for (int j = 0; j < 2; ++j) {
           const int col = n0 + 64 * wn + 32 * j + l32;
           float v = acc[i][j][r];
-          if (bias && col < N) v += bf2f(bias[(int64_t)e * N + col]);
+          v += bvj[j];
           const float other = __shfl_xor(v, 1, 64);
           float o = 0.f;
           if ((l32 & 1) == 0 && col < N) {
@@ -1135,6 +1170,13 @@ __global__ __launch_bounds__(G3_NT, 1) void moe_gemm3_fp8_kernel(
     }
     return;
   }
+  // the expert bias of this lane's columns, loaded once (not once per accumulator element)
+  float bvj[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int col = n0 + 64 * wn + 32 * j + l32;
+    bvj[j] = (bias && col < N) ? bf2f(bias[(int64_t)e * N + col]) : 0.f;
+  }
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     if (i >= rb_live) break;
@@ -1146,7 +1188,7 @@ __global__ __launch_bounds__(G3_NT, 1) void moe_gemm3_fp8_kernel(
       for (int j = 0; j < 2; ++j) {
         const int col = n0 + 64 * wn + 32 * j + l32;
         float v = acc[i][j][r];
-        if (bias && col < N) v += bf2f(bias[(int64_t)e * N + col]);
+        v += bvj[j];
         if (MODE == 0) {
           if (live && col < N) Y[(int64_t)row * y_stride + col] = f2bf(v);
         } else {
