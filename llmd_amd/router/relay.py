@@ -12,6 +12,7 @@ remain the fallback when the executable cannot be built.
 from __future__ import annotations
 
 import logging
+import os
 import shutil
 import subprocess
 from pathlib import Path
@@ -21,9 +22,12 @@ log = logging.getLogger("llmd.router.relay")
 
 
 def relay_binary(build: bool = True) -> Optional[Path]:
-    """Path of the built relay (building it with g++ if needed and allowed), or None."""
+    """Path of the built relay (building it with g++ if needed and allowed), or None.
+    ``LLMD_RELAY_BIN`` overrides it (e.g. an ASan + UBSan build, tests/test_relay_sanitize.py)."""
     from llmd_amd import build as B
 
+    if os.environ.get("LLMD_RELAY_BIN"):
+        return Path(os.environ["LLMD_RELAY_BIN"])
     if B.RELAY.exists():
         try:
             return B.build_relay() if build and shutil.which("g++") else B.RELAY
