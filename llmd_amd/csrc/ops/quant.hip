@@ -54,19 +54,23 @@ __global__ __launch_bounds__(NT) void quant_fp8_rows_kernel(const uint16_t* __re
 // kp > d: q rows are kp bytes wide and columns [d, kp) are zero-filled (the K-padded operand of the
 // grouped GEMM); row_limit (device scalar, nullable): rows at or past it are left untouched - the
 // grouped GEMM's padded-slot rows beyond the last real expert tile, which it never reads.
+// One wave per row (4 rows per 256-thread workgroup): a row of a few thousand columns is a few
+// 8-column chunks per lane, and a 128-column group is 16 lanes, so the group amax is a 16-lane
+// shuffle reduction inside the wave (a workgroup per row left most of its lanes idle).
 __global__ __launch_bounds__(NT) void quant_fp8_groups_kernel(const uint16_t* __restrict__ x, int64_t xs,
                                                               uint8_t* __restrict__ q, int64_t qs,
-                                                              float* __restrict__ scale, int64_t ss, int d,
-                                                              int kp, const int* __restrict__ row_limit,
+                                                              float* __restrict__ scale, int64_t ss, int T,
+                                                              int d, int kp, const int* __restrict__ row_limit,
                                                               float floor_) {
-  const int64_t t = blockIdx.x;
-  if (row_limit != nullptr && t >= *row_limit) return;
+  const int64_t t = (int64_t)blockIdx.x * (NT / 64) + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (t >= T || (row_limit != nullptr && t >= *row_limit)) return;
   const u32x4_t* xr = reinterpret_cast<const u32x4_t*>(x + t * xs);
   u32x2_t* qr = reinterpret_cast<u32x2_t*>(q + t * qs);
   const int nc = d / 8;
-  const int span = (nc + 15) / 16 * 16;
-  for (int c0 = 0; c0 < span; c0 += NT) {
-    const int c = c0 + threadIdx.x;
+  const int span = (nc + 15) / 16 * 16;  // whole 16-lane groups (a partial last group reads zeros)
+  for (int c0 = 0; c0 < span; c0 += 64) {
+    const int c = c0 + lane;
     const bool ok = c < nc;
     float f[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     if (ok) unpack8(xr[c], f);
@@ -75,14 +79,14 @@ __global__ __launch_bounds__(NT) void quant_fp8_groups_kernel(const uint16_t* __
     for (int i = 0; i < 8; ++i) a = fmaxf(a, fabsf(f[i]));
 #pragma unroll
     for (int o = 8; o > 0; o >>= 1) a = fmaxf(a, __shfl_xor(a, o, 64));
-    const float s = pow2_ceil(fmaxf(a / FP8_MAX, floor_));  // E8M0-exact (moe_gemm2_fp8_kernel)
-    if (ok && (c & 15) == 0) scale[t * ss + c / 16] = s;
-    const float inv = 1.f / s;
+    const float sc = pow2_ceil(fmaxf(a / FP8_MAX, floor_));  // E8M0-exact (moe_gemm2_fp8_kernel)
+    if (ok && (c & 15) == 0) scale[t * ss + c / 16] = sc;
+    const float inv = 1.f / sc;
 #pragma unroll
     for (int i = 0; i < 8; ++i) f[i] *= inv;
     if (ok) qr[c] = f32x8_to_fp8(f);
   }
-  for (int c = d / 8 + threadIdx.x; c < kp / 8; c += NT) qr[c] = u32x2_t{0u, 0u};
+  for (int c = nc + lane; c < kp / 8; c += 64) qr[c] = u32x2_t{0u, 0u};
 }
 
 }  // namespace
@@ -91,8 +95,8 @@ extern "C" int llmd_quant_fp8_groups(const void* x, int64_t xs, void* q, int64_t
                                      int T, int d, hipStream_t st) {
   if (T == 0) return 0;
   if (d % 8) return -1;
-  hipLaunchKernelGGL(quant_fp8_groups_kernel, dim3(T), dim3(NT), 0, st, (const uint16_t*)x, xs, (uint8_t*)q, qs,
-                     scale, ss, d, d, (const int*)nullptr, 1e-12f);
+  hipLaunchKernelGGL(quant_fp8_groups_kernel, dim3((T + NT / 64 - 1) / (NT / 64)), dim3(NT), 0, st,
+                     (const uint16_t*)x, xs, (uint8_t*)q, qs, scale, ss, T, d, d, (const int*)nullptr, 1e-12f);
   return (int)hipGetLastError();
 }
 
@@ -102,8 +106,8 @@ extern "C" int llmd_quant_fp8_groups_padded(const void* x, int64_t xs, void* q, 
                                             hipStream_t st) {
   if (T == 0) return 0;
   if (d % 8 || kp % 8 || kp < d || qs < kp) return -1;
-  hipLaunchKernelGGL(quant_fp8_groups_kernel, dim3(T), dim3(NT), 0, st, (const uint16_t*)x, xs, (uint8_t*)q, qs,
-                     scale, ss, d, kp, row_limit, 1e-12f);
+  hipLaunchKernelGGL(quant_fp8_groups_kernel, dim3((T + NT / 64 - 1) / (NT / 64)), dim3(NT), 0, st,
+                     (const uint16_t*)x, xs, (uint8_t*)q, qs, scale, ss, T, d, kp, row_limit, 1e-12f);
   return (int)hipGetLastError();
 }
 
