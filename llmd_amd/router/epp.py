@@ -217,14 +217,20 @@ class EPP:
             m.child(m.plugin_dur, "Filter", f.plugin_type, f.name).observe(time.perf_counter() - t0)
             if not cand:
                 return ProfileRunResult([], {})
-        total = {e.key: 0.0 for e in cand}
+        keys = [e.key for e in cand]
+        acc = [0.0] * len(keys)
         for s, w in prof.scorers:
             t0 = time.perf_counter()
             sc = s.score(req, cand)
             m.child(m.plugin_dur, "Scorer", s.plugin_type, s.name).observe(time.perf_counter() - t0)
-            for k in total:
-                total[k] += w * max(0.0, min(1.0, float(sc.get(k, 0.0))))
-        scored = [(e, total[e.key]) for e in cand]
+            get = sc.get
+            for i, k in enumerate(keys):  # clamp to [0, 1], weight, sum (per endpoint per scorer)
+                v = get(k)
+                if v:
+                    v = float(v)
+                    acc[i] += w * (1.0 if v > 1.0 else (v if v > 0.0 else 0.0))
+        total = dict(zip(keys, acc))
+        scored = list(zip(cand, acc))
         t0 = time.perf_counter()
         picked = prof.picker.pick(req, scored)
         m.child(m.plugin_dur, "Picker", prof.picker.plugin_type, prof.picker.name).observe(time.perf_counter() - t0)

@@ -46,10 +46,16 @@ class ApproxPrefixCacheProducer(DataProducer, PreRequest):
         at = self.p("autoTune", True)
         self.auto_tune = at if isinstance(at, bool) else str(at).lower() == "true"
         self._caps: dict[str, int] = {}
+        self._seen: dict[str, tuple] = {}
 
     def _tune(self, eps):
+        seen = self._seen
         for e in eps:
-            nb, bs = int(e.metric(NUM_GPU_BLOCKS, 0) or 0), int(e.metric(BLOCK_SIZE, 0) or 0)
+            raw = (e.metric(NUM_GPU_BLOCKS, 0), e.metric(BLOCK_SIZE, 0))
+            if seen.get(e.key) == raw:  # per request per endpoint: skip unchanged pool sizes
+                continue
+            seen[e.key] = raw
+            nb, bs = int(raw[0] or 0), int(raw[1] or 0)
             if nb <= 0 or bs <= 0:
                 continue
             cap = max(1, nb * bs // self.block_tokens)
@@ -84,6 +90,8 @@ class ApproxPrefixCacheProducer(DataProducer, PreRequest):
 
     def on_endpoint_removed(self, ep: Endpoint):
         self.index.remove_server(ep.key)
+        self._caps.pop(ep.key, None)
+        self._seen.pop(ep.key, None)
 
 
 @register("token-producer", "tokenizer")

@@ -134,7 +134,11 @@ class QueueScorer(Scorer):
 @register("kv-cache-utilization-scorer", "kv-cache-scorer")
 class KVCacheUtilizationScorer(Scorer):
     def score(self, req, eps):
-        return {e.key: max(0.0, min(1.0, 1.0 - float(e.metric(KV_USAGE, 0.0)))) for e in eps}
+        out = {}
+        for e in eps:
+            v = 1.0 - float(e.metric(KV_USAGE, 0.0))
+            out[e.key] = 1.0 if v > 1.0 else (v if v > 0.0 else 0.0)
+        return out
 
 
 @register("running-requests-size-scorer")

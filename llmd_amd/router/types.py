@@ -73,7 +73,7 @@ class Endpoint:
         return self.labels.get("llm-d.ai/role", "prefill-decode")
 
     def metric(self, k: str, default=0.0):
-        return self.attrs.get(k, default)
+        return self.attrs._d.get(k, default)  # scorers call this per endpoint: skip one frame
 
     def __repr__(self):
         return f"Endpoint({self.name}@{self.key})"

@@ -1,0 +1,43 @@
+"""EPP metrics batch Counter/Histogram children (router/metrics.py _Deferred):
+the exposition must equal what per-call prometheus observe/inc would give."""
+import random
+
+from prometheus_client import CollectorRegistry, Counter, Histogram, generate_latest
+
+from llmd_amd.router.metrics import SMALL, EPPMetrics
+
+
+def _samples(text: bytes, family: str) -> dict:
+    out = {}
+    for line in text.decode().splitlines():
+        if line.startswith(family) and not line.startswith("#") and "_created" not in line:
+            k, v = line.rsplit(" ", 1)
+            out[k] = float(v)
+    return out
+
+
+def test_deferred_histogram_and_counter_match_prometheus():
+    m = EPPMetrics()
+    reg = CollectorRegistry()
+    h = Histogram("inference_extension_plugin_duration_seconds", "Plugin latency",
+                  ["extension_point", "plugin_type", "plugin_name"], buckets=SMALL, registry=reg)
+    c = Counter("inference_objective_request", "Requests", ["model_name", "target_model_name", "priority"],
+                registry=reg)
+    rnd = random.Random(0)
+    # bucket bounds exactly, values between, beyond the last bound, and more than one flush batch
+    vals = list(SMALL) + [rnd.random() * 0.02 for _ in range(5000)] + [1e4, 0.0]
+    for v in vals:
+        m.child(m.plugin_dur, "Scorer", "queue-scorer", "q").observe(v)
+        h.labels("Scorer", "queue-scorer", "q").observe(v)
+    for i in range(3000):
+        m.child(m.req_total, "m", "m", "0").inc()
+        c.labels("m", "m", "0").inc()
+    mine = _samples(m.render(), "inference_extension_plugin_duration_seconds")
+    ref = _samples(generate_latest(reg), "inference_extension_plugin_duration_seconds")
+    assert mine.keys() == ref.keys() and mine
+    for k in ref:
+        assert abs(mine[k] - ref[k]) <= 1e-9 * max(1.0, abs(ref[k])), k
+    assert _samples(m.render(), "inference_objective_request_total") == \
+        _samples(generate_latest(reg), "inference_objective_request_total")
+    # a second render without new observations is unchanged (nothing counted twice)
+    assert _samples(m.render(), "inference_extension_plugin_duration_seconds") == mine
