@@ -14,6 +14,8 @@ from typing import Optional
 
 from prometheus_client import CollectorRegistry, Counter, Gauge, Histogram, generate_latest
 
+from ..utils.prom import Deferred, Flusher
+
 TTFT_BUCKETS = (0.001, 0.005, 0.01, 0.02, 0.04, 0.06, 0.08, 0.1, 0.25, 0.5, 0.75, 1.0, 2.5, 5.0,
                 7.5, 10.0, 20.0, 40.0, 80.0, 160.0, 640.0, 2560.0)
 ITL_BUCKETS = (0.001, 0.0025, 0.005, 0.01, 0.015, 0.02, 0.025, 0.03, 0.04, 0.05, 0.075, 0.1, 0.15,
@@ -27,6 +29,7 @@ class EngineMetrics:
     def __init__(self, model_name: str, block_size: int, num_gpu_blocks: int,
                  registry: Optional[CollectorRegistry] = None, max_lora: int = 0):
         self.reg = registry or CollectorRegistry()
+        self.reg.register(Flusher(self))  # before the families: a scrape sees the batched per-token series
         L = ["model_name"]
         self.model = model_name
         r = self.reg
@@ -79,13 +82,20 @@ class EngineMetrics:
         self.kv_usage.labels(model_name).set(0)
         # label children of the per-step / per-token series, resolved once (labels() locks and
         # hashes on every call; on_step touches every running request each step)
-        self._c_itl = self.itl.labels(model_name)
-        self._c_ttft = self.ttft.labels(model_name)
+        # per-token series batched (utils/prom.py Deferred): on_step runs between decode graph
+        # replays, one ITL observation per running request
+        self._c_itl = Deferred(self.itl.labels(model_name))
+        self._c_ttft = Deferred(self.ttft.labels(model_name))
         self._c_iter = self.iter_tokens.labels(model_name)
         self._c_gen = self.gen_tokens.labels(model_name)
+        self._deferred = (self._c_itl, self._c_ttft)
         self._c_running = self.running.labels(model_name)
         self._c_waiting = self.waiting.labels(model_name)
         self._c_kv = self.kv_usage.labels(model_name)
+
+    def flush(self):
+        for c in self._deferred:
+            c.flush()
 
     def on_arrival(self, r):
         pass

@@ -6,74 +6,16 @@ under the legacy ``inference_*`` names the dashboards/PromQL cookbook use.
 """
 from __future__ import annotations
 
-import collections
-from bisect import bisect_left
-
 from prometheus_client import CollectorRegistry, Counter, Gauge, Histogram, generate_latest
+
+from ..utils.prom import Deferred as _Deferred
+from ..utils.prom import Flusher as _Flusher
 
 LAT = (0.005, 0.025, 0.05, 0.1, 0.2, 0.4, 0.6, 0.8, 1.0, 1.25, 1.5, 2, 3, 4, 5, 6, 8, 10, 15, 20, 30, 45,
        60, 120, 180, 240, 300, 360, 480, 600, 900, 1200, 1800, 2700, 3600)
 SMALL = (0.0001, 0.0002, 0.0005, 0.001, 0.002, 0.005, 0.01, 0.02, 0.05, 0.1)
 SMALL_LAT = tuple(sorted(set(SMALL + (0.25, 0.5, 1, 2, 5, 10, 30, 60, 120, 300, 600))))
 TOKS = (1, 8, 16, 32, 64, 128, 256, 512, 1024, 2048, 4096, 8192, 16384, 32778, 65536, 131072)
-
-
-class _Deferred:
-    """Batched labelled child of a Counter or Histogram. ``inc``/``observe`` only
-    append to a deque (~0.1 us); ``flush`` folds the batch into the prometheus
-    child: one bisect per observation and one locked ``inc`` per touched bucket,
-    instead of prometheus' lock + bucket scan per call (~2.5 us; a decision
-    makes ~15 such calls). Every scrape flushes first (``_Flusher``), so the
-    exposition is exact; deque appends/pops keep a scrape thread safe."""
-
-    __slots__ = ("c", "ub", "q")
-
-    def __init__(self, c):
-        self.c = c
-        self.ub = list(getattr(c, "_upper_bounds", ()))
-        self.q = collections.deque()
-
-    def observe(self, v):
-        self.q.append(v)
-        if len(self.q) >= 4096:
-            self.flush()
-
-    def inc(self, v=1):
-        self.q.append(v)
-        if len(self.q) >= 4096:
-            self.flush()
-
-    def flush(self):
-        q = self.q
-        n = len(q)
-        if not n:
-            return
-        vals = [q.popleft() for _ in range(n)]
-        if not self.ub:  # counter
-            self.c.inc(sum(vals))
-            return
-        cnt = [0] * len(self.ub)
-        ub = self.ub
-        for v in vals:
-            cnt[bisect_left(ub, v)] += 1  # first bound >= v: prometheus' ``v <= bound``
-        bk = self.c._buckets
-        for i, k in enumerate(cnt):
-            if k:
-                bk[i].inc(k)
-        self.c._sum.inc(sum(vals))
-
-
-class _Flusher:
-    """Registered first in the EPP registry: every collect (render, a scrape of
-    the registry by anyone) flushes the deferred children before the families
-    are read."""
-
-    def __init__(self, m: "EPPMetrics"):
-        self.m = m
-
-    def collect(self):
-        self.m.flush()
-        return []
 
 
 class EPPMetrics:

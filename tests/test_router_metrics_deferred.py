@@ -41,3 +41,22 @@ def test_deferred_histogram_and_counter_match_prometheus():
         _samples(generate_latest(reg), "inference_objective_request_total")
     # a second render without new observations is unchanged (nothing counted twice)
     assert _samples(m.render(), "inference_extension_plugin_duration_seconds") == mine
+
+
+def test_engine_batched_itl_ttft_exposed_on_scrape():
+    from llmd_amd.engine.request import SamplingParams
+    from tests.test_engine import make_engine
+
+    eng = make_engine()
+    for i, n in enumerate((5, 9, 14)):
+        eng.add_request(f"r{i}", list(range(3, 3 + n)), SamplingParams(max_tokens=5, temperature=0.0,
+                                                                      ignore_eos=True))
+    while eng.has_unfinished():
+        eng.step()
+    text = eng.metrics.render().decode()
+
+    def count(name):
+        return sum(float(ln.rsplit(" ", 1)[1]) for ln in text.splitlines() if ln.startswith(name + "_count"))
+
+    assert count("vllm:inter_token_latency_seconds") == len(eng.metrics.itls) > 0
+    assert count("vllm:time_to_first_token_seconds") == len(eng.metrics.ttfts) == 3
