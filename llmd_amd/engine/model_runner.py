@@ -812,30 +812,11 @@ class ModelRunner:
         # bucket's split count stays the grid): a plan sized for max_model_len would leave most
         # splits of a short-context batch empty and the chip underfilled
         self.g_split = torch.full((1,), self.graph_plans[buckets[-1]][0], dtype=torch.int32, device=dev)
-        # the replay inputs live in ONE device buffer with a pinned host mirror of the same layout,
-        # [ids | pos | slots] int64 x M, then [split, pad | len x M | block table x M x width] int32,
-        # so a step fills numpy views and issues one H2D copy (not six copies of freshly pinned tensors)
-        o32 = 24 * M
-        self._in_bytes = (o32 + 8 + 4 * M, 4 * self.width)  # prefix before the table, bytes per table row
-        nbytes = o32 + 8 + 4 * M + 4 * M * self.width
-        self.g_in = torch.zeros(nbytes, dtype=torch.uint8, device=dev)
-        self.h_in = torch.zeros(nbytes, dtype=torch.uint8).pin_memory()
-        self._in_ev = None
-
-        def views(b):
-            return (b[:8 * M].view(torch.long), b[8 * M:16 * M].view(torch.long), b[16 * M:o32].view(torch.long),
-                    b[o32:o32 + 4].view(torch.int32), b[o32 + 8:o32 + 8 + 4 * M].view(torch.int32),
-                    b[o32 + 8 + 4 * M:].view(torch.int32).view(M, self.width))
-        self.g_ids, self.g_pos, self.g_slots, g_split, self.g_len, self.g_bt = views(self.g_in)
-        self.h_ids, self.h_pos, self.h_slots, self.h_split, self.h_len, self.h_bt = (
-            t.numpy() for t in views(self.h_in))
-        g_split.copy_(self.g_split)
-        self.g_split = g_split
-        self.g_slots.fill_(-1)
-        self.g_len.fill_(1)
-        self.h_split[0] = self.graph_plans[buckets[-1]][0]
-        self.h_slots[:] = -1
-        self.h_len[:] = 1
+        self.g_ids = torch.zeros(M, dtype=torch.long, device=dev)
+        self.g_pos = torch.zeros(M, dtype=torch.long, device=dev)
+        self.g_slots = torch.full((M,), -1, dtype=torch.long, device=dev)
+        self.g_bt = torch.zeros(M, self.width, dtype=torch.int32, device=dev)
+        self.g_len = torch.ones(M, dtype=torch.int32, device=dev)
         if self.hybrid:  # the windowed pool's slots / tables (block 0 = null block)
             self.g_slots_swa = torch.full((M,), -1, dtype=torch.long, device=dev)
             self.g_bt_swa = torch.zeros(M, self.width, dtype=torch.int32, device=dev)
@@ -1027,13 +1008,12 @@ class ModelRunner:
             slots = slots + [-1] * pad
             d_bt = np.concatenate([d_bt, np.zeros((pad, self.width), dtype=np.int32)])
             d_len = np.concatenate([d_len, np.ones(pad, dtype=np.int32)])
-        if self._in_ev is not None:  # the previous step's copy has read the pinned mirror
-            self._in_ev.synchronize()
-        self.h_ids[:B] = ids
-        self.h_pos[:B] = pos
-        self.h_slots[:B] = slots
-        self.h_bt[:B] = d_bt
-        self.h_len[:B] = d_len
+        host = torch.tensor([ids, pos, slots], dtype=torch.long).pin_memory()
+        self.g_ids[:B].copy_(host[0], non_blocking=True)
+        self.g_pos[:B].copy_(host[1], non_blocking=True)
+        self.g_slots[:B].copy_(host[2], non_blocking=True)
+        self.g_bt[:B].copy_(torch.from_numpy(d_bt).pin_memory(), non_blocking=True)
+        self.g_len[:B].copy_(torch.from_numpy(d_len).pin_memory(), non_blocking=True)
         if self.hybrid:
             s_slots, s_bt, _ = pl.get("swa") or ([], np.zeros((0, self.width), np.int32), None)
             if B > n:
@@ -1056,13 +1036,7 @@ class ModelRunner:
         else:  # the step's own split plan for its real rows, within the captured grid's splits
             split, _ = ops.decode_split_plan(longest, max(1, n), self.Hkv, self.Hq // self.Hkv,
                                              max_splits=self.graph_plans[B][1])
-            self.h_split[0] = split
-        pre, row = self._in_bytes
-        nb = pre + row * B
-        self.g_in[:nb].copy_(self.h_in[:nb], non_blocking=True)
-        if self._in_ev is None:
-            self._in_ev = torch.cuda.Event()
-        self._in_ev.record()
+            self.g_split.copy_(torch.tensor([split], dtype=torch.int32).pin_memory(), non_blocking=True)
         g.replay()
         if len(rows) == B and rows == list(range(B)):
             return lg
