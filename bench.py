@@ -58,6 +58,8 @@ import numpy as np
 import torch
 import torch.distributed as dist
 
+from llmd_amd.tools import steady
+
 METRIC = "output tok/s per decode GPU + p50 TTFT, Llama-3-70B P/D-disagg on 8×MI355X"
 REF_CONTEXT = ("reference publishes no Llama-3-70B number; its P/D headline is gpt-oss-120b on 16xH200 "
                "(8 P TP1 + 2 D TP4): 12236.6 output tok/s total = 1529.6 per decode GPU, p50 TTFT 1.264 s "
@@ -211,7 +213,9 @@ def main():
     from llmd_amd.engine.engine import LLMEngine
     from llmd_amd.engine.request import SamplingParams
 
-    max_len = a.isl + a.osl + 64
+    # prompt + up to 2 x OSL: the steady-state re-stagger (tools/steady.py) gives
+    # a request that already generated g tokens during setup up to OSL more
+    max_len = a.isl + 2 * a.osl + 64
     cfg = EngineConfig.create(
         a.model, device=a.device, block_size=a.block_size, max_num_seqs=a.concurrency,
         max_num_batched_tokens=a.max_num_batched_tokens, max_model_len=max_len,
@@ -262,8 +266,15 @@ def main():
         if eng.sched.num_waiting <= (added if may_wait else 0) and \
                 all(r.output_token_ids for r in eng.sched.running):
             break
+    # Steady-state phase: the admission ramp bunches the remaining output
+    # lengths, so completions (and the replacement prefills) would arrive late
+    # and the window would under-sample prefill steps. Re-space them to exactly
+    # C/OSL per step (tools/steady.py).
+    longest = steady.restagger(eng.sched.running, a.osl, a.concurrency)
+    assert a.isl + longest <= max_len, (longest, max_len)
     _sync(a)
-    log(rank, f"setup: {setup_steps} steps in {time.time() - ts:.1f}s (batch filled to {a.concurrency})")
+    log(rank, f"setup: {setup_steps} steps in {time.time() - ts:.1f}s (batch filled to {a.concurrency}, "
+              f"completions re-spaced to {a.concurrency}/{a.osl} per step)")
 
     step_tokens = []
     step_ms = collections.defaultdict(list)  # step size -> wall ms (a step ends in a host sync on sampling)
@@ -306,6 +317,7 @@ def main():
     stats = torch.tensor([elapsed, gen, ptoks, len(ttfts)], dtype=torch.float64,
                          device="cuda" if forced is None else "cpu")
     all_ttft = ttfts
+    n_prefills = len(ttfts)  # requests whose first token (prefill end) fell in the window
     if world > 1:
         mx = stats.clone()
         dist.all_reduce(mx, op=dist.ReduceOp.MAX)
@@ -313,6 +325,7 @@ def main():
         dist.all_reduce(sm, op=dist.ReduceOp.SUM)
         elapsed = float(mx[0])
         gen, ptoks = float(sm[1]), float(sm[2])
+        n_prefills = int(sm[3])
         gathered = [None] * world
         dist.all_gather_object(gathered, ttfts)
         all_ttft = [t for g in gathered for t in g]
@@ -341,6 +354,8 @@ def main():
         "output_tok_s_per_gpu": round(value / world, 2),
         "p50_ttft_s": round(p50, 4) if p50 is not None else None,
         "prefill_tok_s": round(ptoks / elapsed, 1),
+        # conservation check: a steady-state window of K steps holds K*C/OSL prefills per replica
+        "steady_state": steady.window_report(n_prefills, a.steps * world, a.concurrency, a.osl),
         **_reference(a.model, value, world),
     }
     if rank == 0:

@@ -99,10 +99,15 @@ __device__ __forceinline__ void block_barrier(const Peers& P, int nranks, int ra
   }
   if (t < nranks && t != rank) {
     uint32_t* f = flag_ptr(P.base[rank], ch, ph, blockIdx.x, t);
+    uint32_t* ew = err_ptr(P.base[rank]);
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
     for (;;) {
       uint32_t v = __hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
       if ((int32_t)(v - epoch) >= 0) break;
+      // A barrier of this rank already timed out (a dead peer): give up at
+      // once, so only the first collective of a step or graph replay pays the
+      // timeout and check_health fires after ~1x LLMD_SYMM_TIMEOUT_S, not Nx.
+      if (__hip_atomic_load(ew, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0u) break;
       if (__builtin_amdgcn_s_memrealtime() - t0 > P.wait_ticks) {
         __hip_atomic_store(err_ptr(P.base[rank]), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         if (P.herr != nullptr) __hip_atomic_store(P.herr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);

@@ -434,7 +434,18 @@ bool hop_header(const std::string& k) {
          ieq(k, "keep-alive");
 }
 
-// parse "Name: value\r\n" lines of [p, e) (the head without its first line)
+// RFC 9110 tchar: the only bytes a field name may hold
+bool tchar(unsigned char ch) {
+  if (ch >= '0' && ch <= '9') return true;
+  if ((ch | 0x20) >= 'a' && (ch | 0x20) <= 'z') return true;
+  return strchr("!#$%&'*+-.^_`|~", ch) != nullptr && ch != 0;
+}
+
+// parse "Name: value\r\n" lines of [p, e) (the head without its first line).
+// Strict per RFC 9112: the name is a non-empty token with nothing
+// between it and the colon ("Content-Length :" would slip past hop_header and
+// reach the upstream as a second framing header), no obs-fold continuation
+// lines, and no bare CR or NUL in a value. Any of those -> 400.
 bool parse_headers(const char* p, const char* e, Headers& out) {
   while (p < e) {
     const char* nl = (const char*)memchr(p, '\n', e - p);
@@ -442,7 +453,11 @@ bool parse_headers(const char* p, const char* e, Headers& out) {
     const char* ln_end = (le > p && le[-1] == '\r') ? le - 1 : le;
     if (ln_end > p) {
       const char* colon = (const char*)memchr(p, ':', ln_end - p);
-      if (!colon) return false;
+      if (!colon || colon == p) return false;
+      for (const char* q = p; q < colon; ++q)
+        if (!tchar((unsigned char)*q)) return false;
+      for (const char* q = colon + 1; q < ln_end; ++q)
+        if (*q == '\r' || *q == '\0') return false;
       const char* v = colon + 1;
       while (v < ln_end && (*v == ' ' || *v == '\t')) ++v;
       const char* ve = ln_end;
@@ -581,6 +596,11 @@ struct Client : Ev {
   bool close_after = false;
   bool dead = false;
   bool sent_continue = false;
+  // chunked request body: parser state kept across reads, so each byte is
+  // decoded once (not re-parsed from the start whenever more data arrives)
+  Chunked req_ck;
+  std::string req_body;
+  size_t req_fed = 0;  // bytes after the head already given to req_ck
 };
 
 struct Upstream : Ev {
@@ -824,7 +844,10 @@ class Loop {
         Up up{(const uint8_t*)epp_->in.data() + off + 4, (const uint8_t*)epp_->in.data() + off + 4 + n};
         up.read(msg);
         off += 4 + n;
-        if (up.ok) on_epp_msg(msg);
+        // An undecodable frame may have been a decision: its client would wait
+        // in pending_ forever. Treat it as a lost EPP (fails every pick over).
+        if (!up.ok) return epp_lost();
+        on_epp_msg(msg);
         if (epp_ == nullptr) return;
       }
       epp_->in.erase(0, off);
@@ -1024,14 +1047,23 @@ class Loop {
     size_t body_at = he + 4;
     const std::string* te = hget(x->hdrs, "transfer-encoding");
     if (te && lower(*te).find("chunked") != std::string::npos) {
-      Chunked ck;
-      std::string body;
-      long used = ck.feed(c->in.data() + body_at, c->in.data() + c->in.size(),
-                          [&](const char* d, size_t n) { body.append(d, n); });
+      long used = c->req_ck.feed(c->in.data() + body_at + c->req_fed, c->in.data() + c->in.size(),
+                                 [&](const char* d, size_t n) { c->req_body.append(d, n); });
       if (used < 0) { respond_simple_close(c, 400, "bad chunked body"); return false; }
-      if (ck.st != Chunked::DONE) return true;  // wait for the rest
-      x->body = std::move(body);
-      c->in.erase(0, body_at + (size_t)used);
+      c->req_fed += (size_t)used;
+      // the same 256 MB cap as a Content-Length body, on the decoded body and
+      // on what is buffered (chunk-size lines and extensions count too)
+      // (a declared chunk size that would pass it is refused at once)
+      if (c->req_body.size() + c->req_ck.left > (256u << 20) || c->req_fed > (256u << 20) + (1u << 20)) {
+        respond_simple_close(c, 413, "body too large");
+        return false;
+      }
+      if (c->req_ck.st != Chunked::DONE) return true;  // wait for the rest
+      x->body = std::move(c->req_body);
+      c->in.erase(0, body_at + c->req_fed);
+      c->req_ck = Chunked();
+      c->req_body.clear();
+      c->req_fed = 0;
     } else {
       const std::string* cl = hget(x->hdrs, "content-length");
       size_t n = cl ? strtoull(cl->c_str(), nullptr, 10) : 0;

@@ -33,11 +33,19 @@ class Deferred:
             self.flush()
 
     def flush(self):
+        # The engine thread (inc/observe at 4096 items) and a /metrics scrape
+        # (Flusher.collect on the asyncio thread) can flush at once: pop until
+        # empty instead of popping a length read earlier.
         q = self.q
-        n = len(q)
-        if not n:
+        vals = []
+        pop = q.popleft
+        try:
+            while True:
+                vals.append(pop())
+        except IndexError:
+            pass
+        if not vals:
             return
-        vals = [q.popleft() for _ in range(n)]
         if not self.ub:  # counter
             self.c.inc(sum(vals))
             return

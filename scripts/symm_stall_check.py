@@ -23,6 +23,9 @@ import torch.distributed as dist
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
+N_MORE = 16
+
+
 def main():
     rank = int(os.environ["RANK"])
     world = int(os.environ["WORLD_SIZE"])
@@ -45,6 +48,15 @@ def main():
         ar.all_reduce(x)                 # rank 1 never joins: the barrier must time out
         torch.cuda.synchronize()
         res["kernel_s"] = round(time.time() - t0, 2)
+        # A step issues many collectives: once one barrier timed out, the rest
+        # must give up at once (the err word is read inside the wait), so N
+        # more stalled all-reduces cost ~0, not N x LLMD_SYMM_TIMEOUT_S.
+        t0 = time.time()
+        for _ in range(N_MORE):
+            ar.all_reduce(x)
+        torch.cuda.synchronize()
+        res["n_more"] = N_MORE
+        res["more_s"] = round(time.time() - t0, 2)
         res["host_word"] = symm.host_error()
         res["device_word"] = heap.error()
         try:

@@ -12,8 +12,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 def _bench(*args):
     env = dict(os.environ, LLMD_BENCH_DEVICE="cpu")
-    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--model", "tiny-llama", "--enforce-eager",
-                        "--block-size", "16", "--max-num-batched-tokens", "512", *args],
+    base = ["--model", "tiny-llama", "--enforce-eager", "--block-size", "16", "--max-num-batched-tokens", "512"]
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), *base, *args],
                        env=env, cwd=ROOT, capture_output=True, text=True, timeout=240)
     assert r.returncode == 0, r.stderr[-3000:]
     lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
@@ -34,3 +34,22 @@ def test_bench_json_line_contract():
 def test_bench_setup_ends_with_more_in_flight_than_output_tokens():
     d, err = _bench("--isl", "16", "--osl", "4", "--concurrency", "24", "--steps", "4", "--warmup", "1")
     assert "batch filled to 24" in err and d["value"] > 0
+
+
+import pytest  # noqa: E402
+
+
+@pytest.mark.parametrize("model,conc,mnbt", [
+    ("tiny-llama", 64, 144),      # Llama-3-70B bench: R 64, one ISL-5000 prompt per 8192-token step
+    ("tiny-llama", 256, 333),     # Llama-3-8B at 256 in flight: R > OSL, two prompts overflow a step
+    ("tiny-gpt-oss", 256, 333),   # gpt-oss-120b at 256 in flight (hybrid sliding-window KV)
+])
+def test_bench_window_is_steady_state(model, conc, mnbt):
+    """the timed window's prefills match conservation
+    (steps * C / OSL) within one, at the driver's --steps 20 --warmup 5, for
+    the bench shapes scaled to a CPU model (ISL:budget ratio kept)."""
+    d, err = _bench("--model", model, "--isl", "48", "--osl", "250", "--concurrency", str(conc),
+                    "--max-num-batched-tokens", str(mnbt), "--steps", "20", "--warmup", "5")
+    ss = d["steady_state"]
+    assert abs(ss["conservation_prefills"] - 20 * conc / 250) < 0.01
+    assert ss["within_one"], (ss, err[-800:])

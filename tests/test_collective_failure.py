@@ -95,3 +95,5 @@ def test_stalled_peer_fails_loudly_2proc():
     d = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
     assert d["ok"] and d["raised"] and d["host_word"] == 1
     assert 1.5 <= d["kernel_s"] < 30, d
+    # later collectives of the same step must not each pay the timeout
+    assert d["more_s"] < 1.5, d

@@ -60,3 +60,46 @@ def test_engine_batched_itl_ttft_exposed_on_scrape():
 
     assert count("vllm:inter_token_latency_seconds") == len(eng.metrics.itls) > 0
     assert count("vllm:time_to_first_token_seconds") == len(eng.metrics.ttfts) == 3
+
+
+def test_concurrent_flush_and_observe_is_exact():
+    """the engine thread's 4096-item flush and a scrape's flush can
+    run at once; neither may raise and no observation may be lost."""
+    import threading
+
+    from llmd_amd.utils.prom import Deferred
+
+    reg = CollectorRegistry()
+    h = Histogram("t_h", "h", registry=reg, buckets=(1.0, 2.0, 4.0))
+    d = Deferred(h)
+    errors = []
+    n_per, n_thr = 20000, 3
+
+    def produce():
+        try:
+            for i in range(n_per):
+                d.observe(float(i % 5))
+        except Exception as e:  # noqa: BLE001
+            errors.append(e)
+
+    def scrape(stop):
+        try:
+            while not stop.is_set():
+                d.flush()
+        except Exception as e:  # noqa: BLE001
+            errors.append(e)
+
+    stop = threading.Event()
+    scr = [threading.Thread(target=scrape, args=(stop,)) for _ in range(2)]
+    prod = [threading.Thread(target=produce) for _ in range(n_thr)]
+    for t in scr + prod:
+        t.start()
+    for t in prod:
+        t.join()
+    stop.set()
+    for t in scr:
+        t.join()
+    d.flush()
+    assert not errors, errors
+    total = sum(b.get() for b in h._buckets)
+    assert total == n_per * n_thr

@@ -183,6 +183,26 @@ def test_native_relay_contract(tmp_path):
             resp = await _raw(port, req)
             assert resp.startswith(b"HTTP/1.1 200"), resp[:200]
             assert seen[-1]["body"]["prompt"] == "chunked"
+            # the same body delivered in small pieces (incremental chunked parse)
+            r, w = await asyncio.open_connection("127.0.0.1", port)
+            for i in range(0, len(req), 7):
+                w.write(req[i:i + 7])
+                await w.drain()
+                await asyncio.sleep(0.002)
+            resp = await asyncio.wait_for(r.readuntil(b"\r\n\r\n"), 5)
+            assert resp.startswith(b"HTTP/1.1 200"), resp[:200]
+            w.close()
+            # request smuggling shapes are refused (RFC 9112): whitespace before
+            # the colon, bare CR inside a value, an obs-fold continuation line
+            for bad in (b"Content-Length : 5\r\n", b"X-A: a\rb\r\n", b"X-A: a\r\n folded\r\n",
+                        b"Transfer-Encoding\t: chunked\r\n"):
+                resp = await _raw(port, b"POST /v1/completions HTTP/1.1\r\nHost: x\r\n" + bad +
+                                  b"Content-Length: 2\r\n\r\n{}", read_until=b"\r\n\r\n")
+                assert resp.startswith(b"HTTP/1.1 400"), (bad, resp[:200])
+            # a chunked body past the 256 MB cap is a 413 (not unbounded buffering)
+            resp = await _raw(port, b"POST /v1/completions HTTP/1.1\r\nHost: x\r\nTransfer-Encoding: chunked\r\n\r\n"
+                              b"%x\r\n" % (300 << 20) + b"x" * 1024, read_until=b"\r\n\r\n")
+            assert resp.startswith(b"HTTP/1.1 413"), resp[:200]
             r, w = await asyncio.open_connection("127.0.0.1", port)
             w.write(b"POST /v1/completions HTTP/1.1\r\nHost: x\r\nContent-Type: application/json\r\n"
                     b"Expect: 100-continue\r\nContent-Length: %d\r\n\r\n" % len(payload))
@@ -287,4 +307,47 @@ def test_native_relay_dead_endpoint_502(tmp_path):
             relay.wait(5)
             await srv.stop()
             await epp.stop()
+    asyncio.run(main())
+
+
+def test_native_relay_bad_epp_frame_fails_over(tmp_path):
+    """an EPP frame that does not decode must not leave its pick
+    pending forever - the relay treats it as a lost EPP (FailClose -> 503)."""
+    import struct
+
+    import msgpack
+
+    async def main():
+        uds = str(tmp_path / "bad.sock")
+
+        async def serve(reader, writer):
+            try:
+                while True:
+                    n = struct.unpack(">I", await reader.readexactly(4))[0]
+                    m = msgpack.unpackb(await reader.readexactly(n), raw=False)
+                    if m.get("op") == "state":
+                        out = msgpack.packb({"id": m["id"], "eps": ["127.0.0.1:9"], "health": [200, "ok"]})
+                    elif m.get("op") == "pick":
+                        out = b"\xc1"  # the one byte msgpack never uses
+                    else:
+                        continue
+                    writer.write(struct.pack(">I", len(out)) + out)
+                    await writer.drain()
+            except (asyncio.IncompleteReadError, ConnectionError):
+                pass
+
+        srv = await asyncio.start_unix_server(serve, uds)
+        port = _free_port()
+        relay = spawn(uds, "127.0.0.1", port, 1, "FailClose")
+        try:
+            await _up(port, relay)
+            t0 = time.monotonic()
+            resp = await _raw(port, b"POST /v1/completions HTTP/1.1\r\nHost: x\r\nContent-Length: 2\r\n\r\n{}",
+                              read_until=b"}}", timeout=10)
+            assert resp.startswith(b"HTTP/1.1 503"), resp[:200]
+            assert time.monotonic() - t0 < 5
+        finally:
+            relay.terminate()
+            relay.wait(5)
+            srv.close()
     asyncio.run(main())
