@@ -67,6 +67,8 @@ int llmd_mgemm_silu(const void*, int64_t, const void*, int64_t, int, int, int, i
 int llmd_pgemm(const void*, int64_t, const void*, int64_t, void*, int64_t, int, int, int, int, int, void*,
                hipStream_t);
 int64_t llmd_pgemm_ws_bytes(int, int, int, int, int);
+int llmd_pgemm_fp8(const void*, int64_t, const float*, const void*, int64_t, const float*, void*, int64_t, int, int,
+                   int, int, hipStream_t);
 int llmd_mgemm_fp8(const void*, int64_t, const float*, const void*, int64_t, const float*, int, int, int, int, int,
                    int, void*, int64_t, float*, int*, hipStream_t);
 int llmd_vmm_granularity(int, size_t*);
@@ -567,6 +569,28 @@ void pgemm(torch::Tensor y, torch::Tensor x, torch::Tensor w, int64_t epi, int64
   int rc = llmd_pgemm(x.data_ptr(), x.stride(0), w.data_ptr(), w.stride(0), y.data_ptr(), y.stride(0), (int)M,
                       (int)N, (int)K, (int)epi, (int)variant, wsb > 0 ? ws.data_ptr() : nullptr, cur_stream());
   TORCH_CHECK(rc == 0, "pgemm failed: ", rc);
+}
+
+// y = (xs . xq) (ws . wq)^T for prefill-sized M on the fp8 256 x 256 LDS-DMA GEMM (csrc/ops/pgemm8.hip,
+// v_mfma_scale_f32_16x16x128_f8f6f4): xq [M, K] / wq [N, K] e4m3fn, xs [M] or [M, 1] and ws [N] or
+// [1, N] fp32; epi 3 = silu(gate) * up on wq = [gate; up], y [M, N / 2]
+void pgemm_fp8(torch::Tensor y, torch::Tensor xq, torch::Tensor xs, torch::Tensor wq, torch::Tensor ws, int64_t epi) {
+  const c10::hip::OptionalHIPGuard device_guard(dev_of(y));
+  CHECK_CUDA(xq); CHECK_BF16(y); CHECK_INNER(xq); CHECK_INNER(wq); CHECK_INNER(y);
+  TORCH_CHECK(xq.scalar_type() == at::kFloat8_e4m3fn && wq.scalar_type() == at::kFloat8_e4m3fn, "pgemm_fp8: e4m3fn");
+  TORCH_CHECK(xs.scalar_type() == at::kFloat && ws.scalar_type() == at::kFloat, "pgemm_fp8: fp32 scales");
+  TORCH_CHECK(xs.is_contiguous() && ws.is_contiguous(), "pgemm_fp8: contiguous scales");
+  TORCH_CHECK(xq.dim() == 2 && wq.dim() == 2 && y.dim() == 2, "pgemm_fp8: 2-D operands");
+  const int64_t M = xq.size(0), K = xq.size(1), N = wq.size(0);
+  TORCH_CHECK(wq.size(1) == K && K % 128 == 0 && N % 256 == 0, "pgemm_fp8: N % 256 == 0, K % 128 == 0");
+  TORCH_CHECK(xs.numel() == M && ws.numel() == N, "pgemm_fp8: per-token / per-channel scales");
+  TORCH_CHECK(epi == 0 || epi == 3, "pgemm_fp8: epi 0 or 3");
+  TORCH_CHECK(y.size(0) == M && y.size(1) == (epi == 3 ? N / 2 : N), "pgemm_fp8: output shape");
+  TORCH_CHECK(xq.stride(0) % 16 == 0 && wq.stride(0) % 16 == 0 && y.stride(0) % 8 == 0, "pgemm_fp8: 16-B rows");
+  int rc = llmd_pgemm_fp8(xq.data_ptr(), xq.stride(0), xs.data_ptr<float>(), wq.data_ptr(), wq.stride(0),
+                          ws.data_ptr<float>(), y.data_ptr(), y.stride(0), (int)M, (int)N, (int)K, (int)epi,
+                          cur_stream());
+  TORCH_CHECK(rc == 0, "pgemm_fp8 failed: ", rc);
 }
 
 // y [M, F] = silu(x wg^T) * (x wu^T), w = [gate; up] [2F, K] (mgemm ACT form, whole K per workgroup)
@@ -1172,6 +1196,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {  // _C, or _C_debug (llmd_amd/build.p
   m.def("mgemm_partials", &mgemm_partials, "split-K partials of the medium-M GEMM (no reduce); returns nsplit");
   m.def("reduce_rope_cache", &reduce_rope_cache, "QKV split-K reduce + RoPE + paged cache write");
   m.def("mgemm_add_rmsnorm", &mgemm_add_rmsnorm, "decode o / down projection with residual-add + RMSNorm in its split-K reduce");
+  m.def("pgemm_fp8", &pgemm_fp8, "prefill fp8 W8A8 GEMM (256x256 LDS-DMA tiles on 16x16x128 f8f6f4 MFMA), "
+        "per-token x per-channel scales, optional fused SiLU-and-mul");
   m.def("pgemm", &pgemm, "prefill bf16 GEMM (256x256 LDS-DMA MFMA tiles), optional fused SiLU-and-mul",
         py::arg("y"), py::arg("x"), py::arg("w"), py::arg("epi"), py::arg("variant"), py::arg("split_k") = true);
   m.def("mgemm_fp8", &mgemm_fp8);

@@ -1,0 +1,275 @@
+// Prefill ("large-M") fp8 W8A8 GEMM: C[M, N] = (xs . A[M, K]) (ws . W[N, K])^T,
+// A and W e4m3fn, xs per-token and ws per-output-channel fp32 scales, bf16 C
+// (SURVEY K08 + K16; the role of hipBLASLt's row-wise-scaled F8 GEMM behind
+// torch._scaled_mm, which the reference's AMD P/D recipe runs for
+// amd/Llama-3.3-70B-Instruct-FP8-KV, guides/pd-disaggregation/modelserver/amd/
+// vllm/base/patch-decode.yaml:13).
+//
+// CDNA4 design - the bf16 PGR2 kernel (pgemm.hip variant 3) re-cut for the
+// block-scaled MFMA, whose e4m3 form runs at twice the bf16 rate per clock:
+//   * one 256 x 256 output tile per 4-wave workgroup, a wave owns 128 x 128 as
+//     8 x 8 v_mfma_scale_f32_16x16x128_f8f6f4 tiles (256 AGPR accumulators);
+//     the E8M0 scale operands are 1.0 and the fp32 scales are applied in the
+//     epilogue, so the operands are exactly hipBLASLt's;
+//   * a K-step is 128 fp8 = 128 B per row, i.e. byte-for-byte the bf16 PGR2
+//     LDS image: 2 x 64 KB buffers, 1 KB LDS-DMA pieces (buffer_load ... lds,
+//     K offset in soffset), 16-B chunks XOR-swizzled by row on the source side;
+//   * one 16x16x128 MFMA consumes a whole K-step per fragment pair (32 B per
+//     lane = 2 ds_read_b128), so there is no second k-half to pipeline
+//     against. The schedule instead pipelines ACROSS steps: the W fragments
+//     of step kt+1 go to a second register set (named statically by a 2-step
+//     unroll), an A fragment is refilled in place once its row of 8 MFMAs is
+//     done; per step (64 MFMA slots of 32 cycles):
+//       t 1-2   A fragment 7 of THIS step (its register was busy until the end
+//               of the previous step)
+//       t 5     lgkmcnt(0) + barrier: every wave is done with this buffer
+//       t 6-21  the 16 DMA pieces of step kt+2 into it
+//       t 27    vmcnt(16) + barrier: step kt+1 landed
+//       t 28-43 W fragments of step kt+1 (second set), t 44-55 A fragments
+//               0-5 of step kt+1, t 57-58 A fragment 6
+//     so a DMA piece has ~1.3 steps to land and LDS traffic is ~96 B/clk/CU;
+//   * XCD-aware grouped tile order as pgemm.hip;
+//   * epilogue through the free LDS (C^T: W fragments are the MFMA's A
+//     operand, a lane holds 4 consecutive N columns of one token row), scaled
+//     by xs[m] * ws[n] in fp32; EPI_SILU_STD fuses silu(gate) * up on the
+//     model's plain [gate; up] weight (tile tn: gate rows [128 tn, +128),
+//     up rows [F + 128 tn, +128)).
+//
+// Requirements (host-checked): N % 256 == 0, K % 128 == 0, 16-B aligned rows,
+// byte offsets within 31 bits; any M (rows past M read zeros, not stored).
+#include <algorithm>
+#include <type_traits>
+
+#include "llmd_common.h"
+
+using namespace llmd;
+
+namespace {
+
+constexpr int P8_BM = 256, P8_BN = 256, P8_BK = 128, P8_NT = 256;
+constexpr int P8_OPB = P8_BM * P8_BK;  // 32 KB per operand per K-step
+constexpr int P8_BUF = 2 * P8_OPB;     // 64 KB
+constexpr int P8_GROUP_M = 8;
+constexpr uint32_t P8_OOB = 0x80000000u;  // past the 0x7fffffff buffer range: reads zeros
+
+enum { P8_EPI_NONE = 0, P8_EPI_SILU_STD = 3 };
+
+typedef int i32x8_t __attribute__((ext_vector_type(8)));
+
+// D(16x16, f32) += A(16x128 e4m3) . B(128x16 e4m3), E8M0 scales 127 = 1.0
+__device__ __forceinline__ void mfma8(f32x4_t& acc, const i32x8_t& a, const i32x8_t& b, int one) {
+  asm volatile("v_mfma_scale_f32_16x16x128_f8f6f4 %0, %1, %2, %0, %3, %3 op_sel_hi:[0,0,0]"
+               : "+a"(acc)
+               : "v"(a), "v"(b), "v"(one));
+}
+
+__device__ __forceinline__ void p8_bar() {
+  __builtin_amdgcn_sched_barrier(0);
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+__device__ __forceinline__ void p8_tile_mn(int L, int tiles_m, int tiles_n, int& tm, int& tn) {
+  const int per_group = P8_GROUP_M * tiles_n;
+  const int g = L / per_group, first_m = g * P8_GROUP_M;
+  const int gm = min(tiles_m - first_m, P8_GROUP_M);
+  tm = first_m + (L % per_group) % gm;
+  tn = (L % per_group) / gm;
+}
+
+template <int EPI>
+__global__ __launch_bounds__(P8_NT, 1) void pgemm8_kernel(const uint8_t* __restrict__ A, int64_t lda,
+                                                          const float* __restrict__ xs,
+                                                          const uint8_t* __restrict__ W, int64_t ldw,
+                                                          const float* __restrict__ wsc,
+                                                          uint16_t* __restrict__ C, int64_t ldc, int M, int N,
+                                                          int K) {
+  __shared__ __attribute__((aligned(1024))) char lds[2 * P8_BUF];  // the ONLY LDS object
+  const int tiles_m = (M + P8_BM - 1) / P8_BM, tiles_n = N / P8_BN;
+  int tm, tn;
+  p8_tile_mn(xcd_remap(blockIdx.x, gridDim.x), tiles_m, tiles_n, tm, tn);
+  const int m0 = tm * P8_BM, n0 = tn * P8_BN;
+  const int nk = K / P8_BK;
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: LDS bases stay scalar
+  const int wr = w >> 1, wc = w & 1;
+
+  const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc((void*)A, 0, 0x7fffffff, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc((void*)W, 0, 0x7fffffff, 0x00020000);
+  // DMA piece j of this wave: rows 64 w + 8 j + (lane >> 3); LDS slot lane & 7 <- chunk (lane & 7) ^ f(row)
+  uint32_t va[8], vw[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int row = 64 * w + 8 * j + (lane >> 3);
+    const int c = (lane & 7) ^ ((row >> 1) & 7);
+    va[j] = m0 + row < M ? (uint32_t)((int64_t)(m0 + row) * lda + c * 16) : P8_OOB;
+    const int wrow = EPI == P8_EPI_SILU_STD ? (row < 128 ? 0 : N / 2 - 128) + tn * 128 + row : n0 + row;
+    vw[j] = (uint32_t)((int64_t)wrow * ldw + c * 16);
+  }
+  auto dma = [&](int kt, int j) {  // piece j < 8: A, j >= 8: W piece j - 8, K-step kt (clamped)
+    const uint32_t so = (uint32_t)(min(kt, nk - 1) * P8_BK);
+    char* dst = lds + (kt & 1) * P8_BUF + (j >= 8 ? P8_OPB : 0) + (8 * w + (j & 7)) * 1024;
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(j >= 8 ? rw : ra, (__attribute__((address_space(3))) void*)dst, 16,
+                                             j >= 8 ? vw[j - 8] : va[j], so, 0, 0);
+  };
+  // fragment t (16 rows): row 16 t + (lane & 15), k 32 (lane >> 4) .. +31 = chunks 2q, 2q + 1
+  const int fr = lane & 15, fq = lane >> 4;
+  const int sw = (fr >> 1) & 7;
+  const int rd0 = fr * 128 + (((2 * fq) ^ sw) * 16), rd1 = fr * 128 + (((2 * fq + 1) ^ sw) * 16);
+  const int a_rd = (wr * 128) * 128, w_rd = P8_OPB + (wc * 128) * 128;
+  auto frag = [&](const char* buf, int base, int t) {
+    const char* p = buf + base + t * 2048;
+    const u32x4_t lo = *reinterpret_cast<const u32x4_t*>(p + rd0);
+    const u32x4_t hi = *reinterpret_cast<const u32x4_t*>(p + rd1);
+    return i32x8_t{(int)lo[0], (int)lo[1], (int)lo[2], (int)lo[3], (int)hi[0], (int)hi[1], (int)hi[2], (int)hi[3]};
+  };
+  const int one = 127;  // E8M0 1.0
+
+  f32x4_t acc[8][8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  i32x8_t fa[8], fw[2][8];
+
+  // prologue: steps 0 and 1 in flight, step 0 landed, its W set and A fragments 0-6 in registers
+#pragma unroll
+  for (int j = 0; j < 16; ++j) dma(0, j);
+#pragma unroll
+  for (int j = 0; j < 16; ++j) dma(1, j);
+  asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+  p8_bar();
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    fw[0][j] = frag(lds, w_rd, j);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+#pragma unroll
+  for (int i = 0; i < 7; ++i) {
+    fa[i] = frag(lds, a_rd, i);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_nop 4" ::: "memory");  // accumulator zero-init -> MFMA srcC
+  __builtin_amdgcn_sched_barrier(0);
+
+  // one K-step on W set S (the next step's W fragments go to set S ^ 1)
+  auto step = [&](auto S_, int kt) {
+    constexpr int S = decltype(S_)::value;
+    const char* cur = lds + (kt & 1) * P8_BUF;
+    const char* nxt = lds + ((kt & 1) ^ 1) * P8_BUF;
+#pragma unroll
+    for (int t = 0; t < 64; ++t) {
+      const int i = t >> 3, j = t & 7;
+      mfma8(acc[i][j], fw[S][j], fa[i], one);
+      if (t == 1) {
+        fa[7] = frag(cur, a_rd, 7);
+      } else if (t == 5) {
+        __builtin_amdgcn_s_waitcnt(0xC07F);  // this wave's reads of the current buffer retired
+        p8_bar();
+      } else if (t >= 6 && t < 22) {
+        dma(kt + 2, t - 6);
+      } else if (t == 27) {
+        asm volatile("s_waitcnt vmcnt(16)" ::: "memory");  // step kt+1 landed (kt+2's 16 in flight)
+        p8_bar();
+      } else if (t >= 28 && t < 36) {
+        fw[S ^ 1][t - 28] = frag(nxt, w_rd, t - 28);
+      } else if (t >= 44 && t < 50) {
+        fa[t - 44] = frag(nxt, a_rd, t - 44);
+      } else if (t == 57) {
+        fa[6] = frag(nxt, a_rd, 6);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    // drain at the end of every step (asm MFMAs: hipcc does not model their latency)
+    asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  int kt = 0;
+  for (; kt + 1 < nk; kt += 2) {
+    step(std::integral_constant<int, 0>{}, kt);
+    step(std::integral_constant<int, 1>{}, kt + 1);
+  }
+  if (kt < nk) step(std::integral_constant<int, 0>{}, kt);
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+
+  // ---- epilogue: acc[i][j][r] = C[m = 16 i + fr][n = 16 j + 4 fq + r] (wave-relative), x xs[m] ws[n]
+  float sx[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int m = m0 + wr * 128 + 16 * i + fr;
+    sx[i] = m < M ? xs[m] : 0.f;
+  }
+  f32x4_t sn[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int nl = wc * 128 + 16 * j + 4 * fq;  // tile-relative column
+    const int n = EPI == P8_EPI_SILU_STD ? (nl < 128 ? 0 : N / 2 - 128) + tn * 128 + nl : n0 + nl;
+    sn[j] = *reinterpret_cast<const f32x4_t*>(wsc + n);
+  }
+  __syncthreads();
+  char* img = lds + w * 32768;
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int row = 16 * i + fr, col = 16 * j + 4 * fq;
+      const f32x4_t v = acc[i][j];
+      u32x2_t p;
+      p[0] = (uint32_t)f2bf(v[0] * sx[i] * sn[j][0]) | ((uint32_t)f2bf(v[1] * sx[i] * sn[j][1]) << 16);
+      p[1] = (uint32_t)f2bf(v[2] * sx[i] * sn[j][2]) | ((uint32_t)f2bf(v[3] * sx[i] * sn[j][3]) << 16);
+      *reinterpret_cast<u32x2_t*>(img + row * 256 + (((col >> 3) ^ (row & 15)) * 16) + (col & 7) * 2) = p;
+    }
+  __syncthreads();
+  if constexpr (EPI == P8_EPI_NONE) {
+#pragma unroll 4
+    for (int it = 0; it < 32; ++it) {
+      const int row = it * 4 + (lane >> 4), c = lane & 15;
+      const int m = m0 + wr * 128 + row;
+      const u32x4_t v = *reinterpret_cast<const u32x4_t*>(img + row * 256 + ((c ^ (row & 15)) * 16));
+      if (m < M) *reinterpret_cast<u32x4_t*>(C + (int64_t)m * ldc + n0 + wc * 128 + c * 8) = v;
+    }
+  } else {
+    // gate image of row-half wr: wave (wr, 0); up: wave (wr, 1); this wave stores 64 of its 128 rows
+    const char* gimg = lds + (wr * 2) * 32768;
+    const char* uimg = gimg + 32768;
+#pragma unroll 4
+    for (int it = 0; it < 16; ++it) {
+      const int row = wc * 64 + it * 4 + (lane >> 4), c = lane & 15;
+      const int m = m0 + wr * 128 + row;
+      const int off = row * 256 + ((c ^ (row & 15)) * 16);
+      float gf[8], uf[8], of[8];
+      unpack8(*reinterpret_cast<const u32x4_t*>(gimg + off), gf);
+      unpack8(*reinterpret_cast<const u32x4_t*>(uimg + off), uf);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) of[e] = gf[e] / (1.f + __expf(-gf[e])) * uf[e];
+      if (m < M) *reinterpret_cast<u32x4_t*>(C + (int64_t)m * ldc + tn * 128 + c * 8) = pack8(of);
+    }
+  }
+}
+
+}  // namespace
+
+// epi 0: C [M, N]; epi 3: C [M, N / 2] = silu(gate) * up on W = [gate; up] ([N, K], N / 2 % 128 == 0)
+extern "C" int llmd_pgemm_fp8(const void* A, int64_t lda, const float* xs, const void* W, int64_t ldw,
+                              const float* ws, void* C, int64_t ldc, int M, int N, int K, int epi, hipStream_t st) {
+  if (M <= 0) return 0;
+  if (N % P8_BN || K % P8_BK || lda % 16 || ldw % 16 || ldc % 8) return -1;
+  if (epi != P8_EPI_NONE && epi != P8_EPI_SILU_STD) return -3;
+  if (epi == P8_EPI_SILU_STD && (N / 2) % 128) return -3;
+  if ((int64_t)(M - 1) * lda + K > 0x7fffffffLL || (int64_t)(N - 1) * ldw + K > 0x7fffffffLL) return -2;
+  const int ntiles = ((M + P8_BM - 1) / P8_BM) * (N / P8_BN);
+  const auto* a = (const uint8_t*)A;
+  const auto* w = (const uint8_t*)W;
+  auto* c = (uint16_t*)C;
+  if (epi == P8_EPI_SILU_STD)
+    hipLaunchKernelGGL(pgemm8_kernel<P8_EPI_SILU_STD>, dim3(ntiles), dim3(P8_NT), 0, st, a, lda, xs, w, ldw, ws, c,
+                       ldc, M, N, K);
+  else
+    hipLaunchKernelGGL(pgemm8_kernel<P8_EPI_NONE>, dim3(ntiles), dim3(P8_NT), 0, st, a, lda, xs, w, ldw, ws, c, ldc,
+                       M, N, K);
+  return (int)hipGetLastError();
+}

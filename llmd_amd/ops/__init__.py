@@ -497,6 +497,25 @@ def _fp8_gemm(xq, xs, wq, w_scale, bias):
     return torch._scaled_mm(xq, wq.t(), scale_a=xs, scale_b=w_scale, bias=bias, out_dtype=torch.bfloat16)
 
 
+def pgemm_fp8(xq: torch.Tensor, xs: torch.Tensor, wq: torch.Tensor, ws: torch.Tensor, epi: int = 0,
+              out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Prefill fp8 W8A8 GEMM (csrc/ops/pgemm8.hip): (xs . xq) (ws . wq)^T in bf16,
+    per-token xs [M(, 1)] and per-channel ws [(1, )N] fp32 scales; epi 3 =
+    silu(gate) * up on wq = [gate; up] (output [M, N / 2]). N % 256 == 0,
+    K % 128 == 0. Fails loudly without the native library."""
+    M, N = xq.shape[0], wq.shape[0]
+    if out is None:
+        out = torch.empty(M, N // 2 if epi == 3 else N, dtype=torch.bfloat16, device=xq.device)
+    native().pgemm_fp8(out, xq, xs, wq, ws, epi)
+    return out
+
+
+def pgemm_fp8_ok(xq: torch.Tensor, wq: torch.Tensor) -> bool:
+    """Shapes / layouts the fp8 prefill GEMM takes."""
+    return (xq.dim() == 2 and wq.dim() == 2 and wq.shape[0] % 256 == 0 and xq.shape[1] % 128 == 0
+            and xq.stride(-1) == 1 and wq.stride(-1) == 1 and xq.stride(0) % 16 == 0 and wq.stride(0) % 16 == 0)
+
+
 def pow2_ceil(r: torch.Tensor) -> torch.Tensor:
     """Smallest power of two >= r (f32, r > 0): the block scales of the fp8 MoE
     path are powers of two so the grouped GEMM passes them to the MFMA as E8M0
