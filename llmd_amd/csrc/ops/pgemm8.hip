@@ -52,7 +52,7 @@ constexpr int P8_BUF = 2 * P8_OPB;     // 64 KB
 constexpr int P8_GROUP_M = 8;
 constexpr uint32_t P8_OOB = 0x80000000u;  // past the 0x7fffffff buffer range: reads zeros
 
-enum { P8_EPI_NONE = 0, P8_EPI_SILU_STD = 3 };
+enum { P8_EPI_NONE = 0, P8_EPI_F32 = 2, P8_EPI_SILU_STD = 3 };
 
 typedef int i32x8_t __attribute__((ext_vector_type(8)));
 
@@ -83,13 +83,23 @@ __global__ __launch_bounds__(P8_NT, 1) void pgemm8_kernel(const uint8_t* __restr
                                                           const uint8_t* __restrict__ W, int64_t ldw,
                                                           const float* __restrict__ wsc,
                                                           uint16_t* __restrict__ C, int64_t ldc, int M, int N,
-                                                          int K) {
+                                                          int K, int tile0, int nsplit, float* __restrict__ ws) {
   __shared__ __attribute__((aligned(1024))) char lds[2 * P8_BUF];  // the ONLY LDS object
   const int tiles_m = (M + P8_BM - 1) / P8_BM, tiles_n = N / P8_BN;
+  // nsplit > 1 (EPI_F32): the grid covers `tail` tiles from tile0 x nsplit K-ranges, each block
+  // writing its scaled fp32 partial tile to ws[split][tile][256][256] (pgemm8_splitk_reduce sums)
+  const int b = xcd_remap(blockIdx.x, gridDim.x);
+  const int tail = gridDim.x / nsplit;
+  const int t_local = b % tail, split = b / tail;
+  const int nk_all = K / P8_BK;
+  const int chunk = (nk_all + nsplit - 1) / nsplit;
+  const int kbeg = split * chunk;
+  const int nk = min(chunk, nk_all - kbeg);
   int tm, tn;
-  p8_tile_mn(xcd_remap(blockIdx.x, gridDim.x), tiles_m, tiles_n, tm, tn);
+  p8_tile_mn(tile0 + t_local, tiles_m, tiles_n, tm, tn);
   const int m0 = tm * P8_BM, n0 = tn * P8_BN;
-  const int nk = K / P8_BK;
+  A += (int64_t)kbeg * P8_BK;
+  W += (int64_t)kbeg * P8_BK;
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: LDS bases stay scalar
@@ -210,6 +220,19 @@ __global__ __launch_bounds__(P8_NT, 1) void pgemm8_kernel(const uint8_t* __restr
     const int n = EPI == P8_EPI_SILU_STD ? (nl < 128 ? 0 : N / 2 - 128) + tn * 128 + nl : n0 + nl;
     sn[j] = *reinterpret_cast<const f32x4_t*>(wsc + n);
   }
+  if constexpr (EPI == P8_EPI_F32) {
+    float* wt = ws + ((int64_t)split * tail + t_local) * (P8_BM * P8_BN);
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int row = wr * 128 + 16 * i + fr, col = wc * 128 + 16 * j + 4 * fq;
+        const f32x4_t v = acc[i][j];
+        *reinterpret_cast<f32x4_t*>(wt + row * P8_BN + col) =
+            f32x4_t{v[0] * sx[i] * sn[j][0], v[1] * sx[i] * sn[j][1], v[2] * sx[i] * sn[j][2], v[3] * sx[i] * sn[j][3]};
+      }
+    return;
+  }
   __syncthreads();
   char* img = lds + w * 32768;
 #pragma unroll
@@ -251,25 +274,81 @@ __global__ __launch_bounds__(P8_NT, 1) void pgemm8_kernel(const uint8_t* __restr
   }
 }
 
+// sum of the nsplit scaled fp32 partials of tail tile t -> bf16 C (8 rows x 256 columns per block)
+__global__ __launch_bounds__(256) void pgemm8_splitk_reduce(const float* __restrict__ ws, int nsplit, int tail,
+                                                            int tile0, uint16_t* __restrict__ C, int64_t ldc, int M,
+                                                            int N) {
+  const int t = blockIdx.x / (P8_BM / 8), rblk = blockIdx.x % (P8_BM / 8);
+  int tm, tn;
+  p8_tile_mn(tile0 + t, (M + P8_BM - 1) / P8_BM, N / P8_BN, tm, tn);
+  const int row = rblk * 8 + (threadIdx.x >> 5), col = (threadIdx.x & 31) * 8;
+  const int m = tm * P8_BM + row;
+  if (m >= M) return;
+  float f[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  for (int s = 0; s < nsplit; ++s) {
+    const float* src = ws + ((int64_t)s * tail + t) * (P8_BM * P8_BN) + row * P8_BN + col;
+    const f32x4_t a = *reinterpret_cast<const f32x4_t*>(src);
+    const f32x4_t b = *reinterpret_cast<const f32x4_t*>(src + 4);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      f[e] += a[e];
+      f[4 + e] += b[e];
+    }
+  }
+  *reinterpret_cast<u32x4_t*>(C + (int64_t)m * ldc + tn * P8_BN + col) = pack8(f);
+}
+
+constexpr int P8_CUS = 256;  // MI355X compute units: one 256 x 256 tile per CU per wave
+
+// tail split plan: a last wave at most half full, and a K long enough that each split keeps >= 8 steps
+__host__ inline void pgemm8_plan(int M, int N, int K, int epi, int& full, int& tail, int& nsplit) {
+  const int ntiles = ((M + P8_BM - 1) / P8_BM) * (N / P8_BN), nk = K / P8_BK;
+  full = ntiles;
+  tail = 0;
+  nsplit = 1;
+  const int t = ntiles % P8_CUS;
+  if (epi != P8_EPI_NONE || t == 0 || 2 * t > P8_CUS) return;
+  int s = std::min(P8_CUS / t, nk / 8);
+  if (s < 2) return;
+  full = ntiles - t;
+  tail = t;
+  nsplit = s;
+}
+
 }  // namespace
+
+extern "C" int64_t llmd_pgemm_fp8_ws_bytes(int M, int N, int K, int epi) {
+  if (M <= 0 || N % P8_BN || K % P8_BK) return 0;
+  int full, tail, nsplit;
+  pgemm8_plan(M, N, K, epi, full, tail, nsplit);
+  return nsplit > 1 ? (int64_t)nsplit * tail * P8_BM * P8_BN * 4 : 0;
+}
 
 // epi 0: C [M, N]; epi 3: C [M, N / 2] = silu(gate) * up on W = [gate; up] ([N, K], N / 2 % 128 == 0)
 extern "C" int llmd_pgemm_fp8(const void* A, int64_t lda, const float* xs, const void* W, int64_t ldw,
-                              const float* ws, void* C, int64_t ldc, int M, int N, int K, int epi, hipStream_t st) {
+                              const float* ws, void* C, int64_t ldc, int M, int N, int K, int epi, void* wsp,
+                              hipStream_t st) {
   if (M <= 0) return 0;
   if (N % P8_BN || K % P8_BK || lda % 16 || ldw % 16 || ldc % 8) return -1;
   if (epi != P8_EPI_NONE && epi != P8_EPI_SILU_STD) return -3;
   if (epi == P8_EPI_SILU_STD && (N / 2) % 128) return -3;
   if ((int64_t)(M - 1) * lda + K > 0x7fffffffLL || (int64_t)(N - 1) * ldw + K > 0x7fffffffLL) return -2;
-  const int ntiles = ((M + P8_BM - 1) / P8_BM) * (N / P8_BN);
+  int full = ((M + P8_BM - 1) / P8_BM) * (N / P8_BN), tail = 0, nsplit = 1;
+  if (wsp != nullptr) pgemm8_plan(M, N, K, epi, full, tail, nsplit);
   const auto* a = (const uint8_t*)A;
   const auto* w = (const uint8_t*)W;
   auto* c = (uint16_t*)C;
   if (epi == P8_EPI_SILU_STD)
-    hipLaunchKernelGGL(pgemm8_kernel<P8_EPI_SILU_STD>, dim3(ntiles), dim3(P8_NT), 0, st, a, lda, xs, w, ldw, ws, c,
-                       ldc, M, N, K);
-  else
-    hipLaunchKernelGGL(pgemm8_kernel<P8_EPI_NONE>, dim3(ntiles), dim3(P8_NT), 0, st, a, lda, xs, w, ldw, ws, c, ldc,
-                       M, N, K);
+    hipLaunchKernelGGL(pgemm8_kernel<P8_EPI_SILU_STD>, dim3(full), dim3(P8_NT), 0, st, a, lda, xs, w, ldw, ws, c,
+                       ldc, M, N, K, 0, 1, nullptr);
+  else if (full > 0)
+    hipLaunchKernelGGL(pgemm8_kernel<P8_EPI_NONE>, dim3(full), dim3(P8_NT), 0, st, a, lda, xs, w, ldw, ws, c, ldc,
+                       M, N, K, 0, 1, nullptr);
+  if (nsplit > 1) {
+    hipLaunchKernelGGL(pgemm8_kernel<P8_EPI_F32>, dim3(tail * nsplit), dim3(P8_NT), 0, st, a, lda, xs, w, ldw, ws, c,
+                       ldc, M, N, K, full, nsplit, (float*)wsp);
+    hipLaunchKernelGGL(pgemm8_splitk_reduce, dim3(tail * (P8_BM / 8)), dim3(256), 0, st, (const float*)wsp, nsplit,
+                       tail, full, c, ldc, M, N);
+  }
   return (int)hipGetLastError();
 }

@@ -47,6 +47,14 @@ class LlamaMLP(torch.nn.Module):
             p = ops.mgemm_silu_plan(x, gu.weight)
             if p is not None:
                 return ops.mgemm_silu(x, gu.weight, p)
+        x0 = x[0] if isinstance(x, tuple) else x
+        if (wants_fp8_input(self.down) and wants_fp8_input(gu) and gu.bias is None and x0.dim() == 2
+                and ops._gpu(x0) and ops.pgemm8_silu_planned(x0.shape[0], gu.weight.shape[0], gu.weight.shape[1])):
+            # fp8 prefill: SiLU-and-mul in the fp8 gate/up GEMM's epilogue (csrc/ops/pgemm8.hip), then
+            # the per-token quant of the [M, F] activation (half the bytes of the act-quant's input)
+            xq, xs = x if isinstance(x, tuple) else ops.quant_fp8_rows(x)
+            if ops.pgemm_fp8_ok(xq, gu.weight):
+                return ops.quant_fp8_rows(ops.pgemm_fp8(xq, xs, gu.weight, gu.weight_scale, epi=3))
         h = gu(x)
         if wants_fp8_input(self.down):  # SiLU*up fused with the down proj's fp8 activation quant
             return ops.gated_act_quant(h, ops.ACT_SILU)

@@ -487,26 +487,54 @@ def fp8_linear(x, wq: torch.Tensor, w_scale: torch.Tensor, bias=None) -> torch.T
     return _fp8_gemm(xq, xs, wq, w_scale, bias).reshape(*lead, -1)
 
 
+def pgemm8_plan(M: int, N: int, K: int) -> Optional[bool]:
+    """split_k of the fp8 prefill GEMM for this shape from the shipped table
+    (ops/pgemm8_table.py), or None: hipBLASLt's scaled GEMM."""
+    if PGEMM_AUTO == "0" or M < PGEMM_MIN_M:
+        return None
+    from .pgemm8_table import PGEMM8_TABLE
+
+    e = PGEMM8_TABLE.get(((M + 255) // 256, N, K))
+    return None if e is None else e[0]
+
+
+def pgemm8_silu_planned(M: int, N: int, K: int) -> bool:
+    """True where the shipped table has the SiLU-epilogue fp8 gate/up GEMM + a row
+    quant ahead of GEMM + the fused act-quant kernel."""
+    if PGEMM_AUTO == "0" or M < PGEMM_MIN_M:
+        return False
+    from .pgemm8_table import PGEMM8_TABLE
+
+    e = PGEMM8_TABLE.get(("silu", (M + 255) // 256, N, K))
+    return e is not None and e[0] is not None
+
+
 def _fp8_gemm(xq, xs, wq, w_scale, bias):
     """Decode-sized M on the fp8 medium-M LDS-DMA GEMM where its measured table has it
-    ahead of hipBLASLt's (tuned) scaled GEMM, else torch._scaled_mm."""
+    ahead of hipBLASLt's (tuned) scaled GEMM, prefill-sized M on the fp8 256 x 256
+    tile GEMM (pgemm8) where its table does, else torch._scaled_mm."""
     if bias is None and _SKINNY and xq.is_contiguous() and wq.is_contiguous():
         plan = mgemm_fp8_choice(xq.shape[0], wq.shape[0], wq.shape[1])
         if plan is not None:
             return mgemm_fp8(xq, xs, wq, w_scale, plan)
+        if pgemm_fp8_ok(xq, wq):
+            sk = pgemm8_plan(xq.shape[0], wq.shape[0], wq.shape[1])
+            if sk is not None:
+                return pgemm_fp8(xq, xs, wq, w_scale, split_k=sk)
     return torch._scaled_mm(xq, wq.t(), scale_a=xs, scale_b=w_scale, bias=bias, out_dtype=torch.bfloat16)
 
 
 def pgemm_fp8(xq: torch.Tensor, xs: torch.Tensor, wq: torch.Tensor, ws: torch.Tensor, epi: int = 0,
-              out: Optional[torch.Tensor] = None) -> torch.Tensor:
+              out: Optional[torch.Tensor] = None, split_k: bool = True) -> torch.Tensor:
     """Prefill fp8 W8A8 GEMM (csrc/ops/pgemm8.hip): (xs . xq) (ws . wq)^T in bf16,
     per-token xs [M(, 1)] and per-channel ws [(1, )N] fp32 scales; epi 3 =
     silu(gate) * up on wq = [gate; up] (output [M, N / 2]). N % 256 == 0,
-    K % 128 == 0. Fails loudly without the native library."""
+    K % 128 == 0; ``split_k`` runs a last wave at most half full split over K
+    (fp32 partials + a reduce). Fails loudly without the native library."""
     M, N = xq.shape[0], wq.shape[0]
     if out is None:
         out = torch.empty(M, N // 2 if epi == 3 else N, dtype=torch.bfloat16, device=xq.device)
-    native().pgemm_fp8(out, xq, xs, wq, ws, epi)
+    native().pgemm_fp8(out, xq, xs, wq, ws, epi, split_k)
     return out
 
 

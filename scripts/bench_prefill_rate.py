@@ -27,10 +27,13 @@ def main():
     ap.add_argument("--warmup", type=int, default=4)
     ap.add_argument("--max-num-batched-tokens", type=int, default=8192)
     ap.add_argument("--inflight", type=int, default=6)
+    ap.add_argument("--quantization", default=None, choices=[None, "fp8"])
+    ap.add_argument("--kv-cache-dtype", default="auto", choices=["auto", "fp8"])
     a = ap.parse_args()
     cfg = EngineConfig.create(a.model, device="cuda", block_size=64, max_num_seqs=64,
                               max_num_batched_tokens=a.max_num_batched_tokens, max_model_len=a.isl + 64,
-                              enforce_eager=True, kv_cache_memory_bytes=40 << 30)
+                              enforce_eager=True, kv_cache_memory_bytes=40 << 30,
+                              quantization=a.quantization, kv_cache_dtype=a.kv_cache_dtype)
     eng = LLMEngine(cfg)
     rng = np.random.default_rng(0)
     sp = SamplingParams(max_tokens=1, temperature=0.0, ignore_eos=True)
@@ -58,7 +61,7 @@ def main():
     dt = time.perf_counter() - t0
     pt = eng.metrics.n_prompt - p0
     rate = pt / dt
-    print(f"{a.model} prefill ISL {a.isl}: {pt} prompt tokens in {dt:.2f}s = {rate:.0f} tok/s "
+    print(f"{a.model} ({a.quantization or 'bf16'}, kv {a.kv_cache_dtype}) prefill ISL {a.isl}: {pt} prompt tokens in {dt:.2f}s = {rate:.0f} tok/s "
           f"({1000 * dt / a.steps:.0f} ms/step) -> feeds {rate / a.isl * a.osl:.0f} output tok/s at OSL {a.osl}",
           flush=True)
 

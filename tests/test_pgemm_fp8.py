@@ -17,7 +17,7 @@ def _q(shape, gen, scale=1.0):
 
 
 def _ref(xq, xs, wq, ws):
-    return (xq.float() * xs.view(-1, 1)) @ (wq.float() * ws.view(1, -1)).t()
+    return (xq.float() * xs.view(-1, 1)) @ (wq.float() * ws.view(-1, 1)).t()
 
 
 @pytest.mark.parametrize("M,N,K", [(1, 256, 128), (300, 512, 384), (513, 768, 1024), (1030, 1280, 640),
@@ -63,3 +63,18 @@ def test_pgemm_fp8_exact_integers():
     torch.cuda.synchronize()
     # |r| <= 9 * 384 = 3456: exact in bf16 only up to 256, so compare after rounding r to bf16
     assert torch.equal(y.float(), r.to(torch.bfloat16).float())
+
+
+@pytest.mark.parametrize("M,N,K", [(300, 512, 2048), (513, 256, 4096)])
+def test_pgemm_fp8_split_k_tail(M, N, K):
+    """A last wave at most half full runs split over K (fp32 partials + reduce): same result."""
+    g = torch.Generator(device="cuda").manual_seed(K)
+    xq, xs = _q((M, K), g)
+    wq, ws = ops.quant_fp8_weight(torch.randn(N, K, generator=g, device="cuda") * 0.05)
+    y0 = ops.pgemm_fp8(xq, xs, wq, ws, split_k=False)
+    y1 = ops.pgemm_fp8(xq, xs, wq, ws, split_k=True)
+    r = _ref(xq, xs, wq, ws)
+    torch.cuda.synchronize()
+    for y in (y0, y1):
+        err = (y.float() - r).abs().max().item()
+        assert err <= 1e-2 * r.abs().max().item() + 1e-3, err
