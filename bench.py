@@ -115,6 +115,10 @@ def parse():
                    help="pd mode at N=8: also run this P:D split after the main one ('2p6d', BASELINE.json's "
                         "literal config; 'auto' = 2p6d when N=8 and the main split differs; 'none' = skip)")
     p.add_argument("--no-preflight", action="store_true", help="skip the N>1 cross-GPU pre-flight checks")
+    p.add_argument("--fp8-extra", default="auto", choices=["auto", "off"],
+                   help="agg mode, 1 GPU, bf16 run: also measure the reference AMD recipe's precision (W8A8 fp8 "
+                        "linears + fp8 KV) in a child process and report it under 'fp8' (the bf16 figure stays "
+                        "the value)")
     return p.parse_args()
 
 
@@ -358,6 +362,14 @@ def main():
         "steady_state": steady.window_report(n_prefills, a.steps * world, a.concurrency, a.osl),
         **_reference(a.model, value, world),
     }
+    if rank == 0 and world == 1 and a.device == "cuda" and a.quantization is None and a.fp8_extra == "auto":
+        del eng
+        import gc
+
+        gc.collect()
+        torch.cuda.empty_cache()
+        log(rank, f"bf16 engine released: {torch.cuda.memory_reserved() / 2**30:.1f} GiB still reserved")
+        result["fp8"] = _fp8_extra(a)
     if rank == 0:
         line = json.dumps(result)
         print(line, flush=True)
@@ -367,6 +379,44 @@ def main():
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def _fp8_extra(a) -> dict:
+    """The same bench at the reference AMD P/D recipe's precision (amd/Llama-3.3-70B-Instruct-FP8-KV:
+    W8A8 fp8 linears, fp8 KV cache; guides/pd-disaggregation/modelserver/amd/vllm/base/patch-decode.yaml:13),
+    run as a CHILD process (clean GPU memory; a failure or timeout is reported, never loses the bf16
+    result). Same steps / warmup / shapes."""
+    import subprocess
+    import tempfile
+
+    with tempfile.NamedTemporaryFile(suffix=".json", delete=False) as tf:
+        out = tf.name
+    cmd = [sys.executable, os.path.abspath(__file__), "--gpus", "1", "--steps", str(a.steps), "--warmup",
+           str(a.warmup), "--model", a.model, "--isl", str(a.isl), "--osl", str(a.osl), "--concurrency",
+           str(a.concurrency), "--max-num-batched-tokens", str(a.max_num_batched_tokens), "--block-size",
+           str(a.block_size), "--quantization", "fp8", "--kv-cache-dtype", "fp8", "--fp8-extra", "off",
+           "--json-out", out] + (["--enforce-eager"] if a.enforce_eager else [])
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "LOCAL_RANK", "WORLD_SIZE")}
+    t0 = time.time()
+    try:
+        r = subprocess.run(cmd, env=env, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, text=True,
+                           timeout=float(os.environ.get("LLMD_BENCH_FP8_TIMEOUT", "420")))
+        if r.returncode != 0:
+            return {"error": f"exit {r.returncode}", "stderr_tail": r.stderr[-400:]}
+        with open(out) as f:
+            d = json.loads(f.read())
+    except (subprocess.TimeoutExpired, OSError, ValueError) as e:
+        return {"error": repr(e)[:300]}
+    finally:
+        try:
+            os.unlink(out)
+        except OSError:
+            pass
+    log(0, f"fp8 extra: {d['value']} tok/s in {time.time() - t0:.0f}s")
+    return {"value": d["value"], "ms_per_step": d["ms_per_step"], "p50_ttft_s": d["p50_ttft_s"],
+            "prefill_tok_s": d["prefill_tok_s"], "steady_state": d["steady_state"], "dtype": "fp8",
+            "kv_cache_dtype": "fp8", "quantization": "W8A8 fp8 linears (per-token x per-channel), fp8 KV",
+            **({k: d[k] for k in ("output_tok_s_per_gpu_vs_reference",) if k in d})}
 
 
 def _alt_split(a, rank, world, local_rank, log, main_res):
