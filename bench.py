@@ -111,6 +111,8 @@ def parse():
     p.add_argument("--quantization", default=None, choices=[None, "fp8"],
                    help="fp8 = W8A8 linears (the reference AMD recipe serves Llama-3.3-70B-FP8); default bf16")
     p.add_argument("--kv-cache-dtype", default="auto", choices=["auto", "fp8"])
+    p.add_argument("--no-async-scheduling", action="store_true",
+                   help="step synchronously (default: step N+1 launched before step N's tokens reach the host)")
     p.add_argument("--alt-split", default="auto",
                    help="pd mode at N=8: also run this P:D split after the main one ('2p6d', BASELINE.json's "
                         "literal config; 'auto' = 2p6d when N=8 and the main split differs; 'none' = skip)")
@@ -226,9 +228,11 @@ def main():
         enforce_eager=a.enforce_eager, seed=a.seed + rank, enable_prefix_caching=True,
         cuda_graph_max_bs=a.concurrency, gpu_memory_utilization=a.gpu_memory_utilization,
         kv_cache_memory_bytes=int(a.kv_cache_gb * 2**30) if a.kv_cache_gb else None,
-        quantization=a.quantization, kv_cache_dtype=a.kv_cache_dtype)
+        quantization=a.quantization, kv_cache_dtype=a.kv_cache_dtype,
+        async_scheduling=not a.no_async_scheduling)
     t0 = time.time()
     eng = LLMEngine(cfg)
+    eng_async = eng.async_sched
     _sync(a)
     log(rank, f"engine up in {time.time() - t0:.1f}s: {cfg.model_config.name}, "
               f"{eng.runner.num_blocks} KV blocks x {a.block_size}")
@@ -353,7 +357,8 @@ def main():
                    "global_batch": a.concurrency * world, "seq_len": a.isl, "isl": a.isl, "osl": a.osl,
                    "parallelism": f"dp{world}" if a.mode == "agg" else f"pd{a.prefill_gpus}p{world - a.prefill_gpus}d",
                    "max_num_batched_tokens": a.max_num_batched_tokens, "block_size": a.block_size,
-                   "graphs": not a.enforce_eager, "kv_cache_dtype": a.kv_cache_dtype},
+                   "graphs": not a.enforce_eager, "kv_cache_dtype": a.kv_cache_dtype,
+                   "async_scheduling": eng_async},
         "output_tok_s_per_decode_gpu": round(value / max(1, n_decode_gpus), 2),
         "output_tok_s_per_gpu": round(value / world, 2),
         "p50_ttft_s": round(p50, 4) if p50 is not None else None,

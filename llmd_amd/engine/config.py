@@ -312,6 +312,10 @@ class SchedulerConfig:
     max_num_batched_tokens: int = 8192
     max_model_len: int = 32768
     enable_chunked_prefill: bool = True
+    # step N+1 is scheduled and launched before step N's sampled tokens reach the host (its decode
+    # inputs are gathered on the device); the host turns step N into outputs while N+1 runs.
+    # Applies to single-rank engines (TP / DP-lockstep / P/D-connector engines step synchronously).
+    async_scheduling: bool = True
     policy: str = "fcfs"  # or "priority"
     long_prefill_token_threshold: int = 0
     # Steps carrying a prefill chunk are trimmed so their token count (the M of
@@ -455,9 +459,12 @@ def add_engine_args(p: argparse.ArgumentParser) -> argparse.ArgumentParser:
                         "(no tracing compiler: the hot ops are HIP kernels)")
     # accepted for command-line compatibility; no effect on this engine
     for f in ("--trust-remote-code", "--enable-cumem-allocator", "--enable-ep-weight-filter",
-              "--enable-prefiller-sampling", "--async-scheduling", "--no-async-scheduling",
+              "--enable-prefiller-sampling",
               "--data-parallel-hybrid-lb", "--data-parallel-multi-port-external-lb"):
         p.add_argument(f, action="store_true", help=argparse.SUPPRESS)
+    p.add_argument("--async-scheduling", dest="async_scheduling", action="store_true", default=True,
+                   help="launch step N+1 before step N's tokens reach the host (default on)")
+    p.add_argument("--no-async-scheduling", dest="async_scheduling", action="store_false")
     p.add_argument("--disable-hybrid-kv-cache-manager", action="store_true",
                    help="every layer keeps full-length KV (no separate sliding-window pool)")
     p.add_argument("--no-disable-hybrid-kv-cache-manager", action="store_true",
@@ -528,6 +535,7 @@ def engine_config_from_args(a) -> EngineConfig:
         enforce_eager=eager, kv_transfer_config=a.kv_transfer_config,
         kv_events_config=a.kv_events_config, kv_offload_config=a.kv_offload_config,
         policy=a.scheduling_policy, prefill_token_align=getattr(a, "prefill_token_align", -1),
+        async_scheduling=getattr(a, "async_scheduling", True),
         enable_lora=getattr(a, "enable_lora", False),
         max_loras=getattr(a, "max_loras", 4), max_lora_rank=getattr(a, "max_lora_rank", 16),
         lora_modules=dict(m.split("=", 1) for m in (getattr(a, "lora_modules", None) or [])) or None)

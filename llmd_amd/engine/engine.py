@@ -92,6 +92,10 @@ class LLMEngine:
         self.step_count = 0
         self.last_step_empty = False
         self.last_num_tokens = 0
+        # async scheduling: the launched step whose tokens are still on the device
+        self._pending = None  # (SchedulerOutput, DeferredSample, t0)
+        self.async_sched = bool(cfg.sched.async_scheduling and not self.dp_lockstep and self.runner.tp_size == 1
+                                and self.connector is None)
 
     # ------------------------------------------------------------ API
     def add_request(self, request_id: str, prompt_token_ids: list[int],
@@ -114,7 +118,7 @@ class LLMEngine:
             self.metrics.on_finish(r)
 
     def has_unfinished(self) -> bool:
-        return self.sched.has_work()
+        return self.sched.has_work() or self._pending is not None
 
     def block_tables(self, so: SchedulerOutput) -> dict[int, list[int]]:
         full = {sr.req.seq_id: self.bm.block_table(sr.req.seq_id) for sr in so.all()}
@@ -128,7 +132,9 @@ class LLMEngine:
         # asleep, or woken from level 2 with the trainer's weights not yet sent:
         # new requests queue until the weights are real again
         if self.paused or self.sleeping or self.weights_pending:
-            return []
+            return self.drain()
+        if self.async_sched:
+            return self._step_async()
         if self.connector is not None:
             self.connector.tick()
         t0 = time.monotonic()
@@ -153,6 +159,67 @@ class LLMEngine:
         sampled = self.runner.execute(so, self.block_tables(so))
         with markers.range("llmd.update"):
             return self._finish_step(so, sampled, err_outs, t0)
+
+    # ------------------------------------------------------------ async scheduling
+    def drain(self) -> list[RequestOutput]:
+        """Outputs of the step still in flight (async scheduling), or []: called before
+        anything that must see settled request state (pause, sleep, weight updates)."""
+        pend, self._pending = self._pending, None
+        return self._resolve(*pend) if pend is not None else []
+
+    def _needs_settled(self, so) -> bool:
+        """Steps whose planning reads output-token VALUES must wait for the step in flight:
+        penalties / logit bias / min-p, embeddings, and a recompute chunk that re-reads a
+        placeholder (a request preempted while its last token was in flight)."""
+        for sr in so.decodes:
+            sp = sr.req.params
+            if sp.penalized or sp.embed:
+                return True
+        for sr in so.prefills:
+            r = sr.req
+            if r.params.penalized or r.params.embed or (r.async_pending and sr.start + sr.num_new_tokens >= r.num_tokens):
+                return True
+        return False
+
+    def _step_async(self) -> list[RequestOutput]:
+        """schedule N+1 (state advanced over step N's placeholders) -> launch N+1 (its decode
+        inputs gathered on the device from N's samples) -> wait for N's tokens (N+1 is queued
+        behind N, so the GPU never idles on the host) -> emit N's outputs. A request whose
+        last token is in flight is not scheduled again; one stopped by EOS / a stop token
+        costs one discarded row in the step launched before its token was seen."""
+        t0 = time.monotonic()
+        with markers.range("llmd.schedule"):
+            so = self.sched.schedule()
+        if self.lora is not None:
+            nm = self.lora.name_of
+            self.metrics.set_lora(sorted({nm(r.lora_id) for r in self.sched.running if r.lora_id} - {None}),
+                                  sorted({nm(r.lora_id) for r in self.sched.waiting if r.lora_id} - {None}))
+        outs = self._error_outputs()
+        self.last_step_empty = so.empty
+        self.last_num_tokens = so.num_tokens
+        if so.empty:
+            outs += self.drain()
+            if self._pending is None and not outs:
+                self._flush_events()
+            return outs
+        if self._pending is not None and self._needs_settled(so):
+            outs += self.drain()
+        if self.offload is not None:
+            self.offload.before_step(so)
+        prev = self._pending[1] if self._pending is not None else None
+        handle = self.runner.execute(so, self.block_tables(so), prev=prev, defer=True)
+        if self._pending is not None:
+            with markers.range("llmd.update"):
+                outs += self.drain()
+        self.sched.advance(so, set(handle.seq_ids))
+        self._pending = (so, handle, t0)
+        return outs
+
+    def _resolve(self, so, handle, t0) -> list[RequestOutput]:
+        sampled = handle.host()
+        _symm.check_health("emitting step %d" % self.step_count)
+        touched = self.sched.resolve(so, sampled)
+        return self._outputs(so, touched, [], t0)
 
     # ------------------------------------------------------------ DP lockstep
     def _lockstep_step(self, so, err_outs, t0) -> list[RequestOutput]:
@@ -241,6 +308,9 @@ class LLMEngine:
         # fail loudly before any of them reaches a client (one host load, no sync)
         _symm.check_health("emitting step %d" % self.step_count)
         touched = self.sched.update(so, sampled)
+        return self._outputs(so, touched, err_outs, t0)
+
+    def _outputs(self, so, touched, err_outs, t0) -> list[RequestOutput]:
         dt = time.monotonic() - t0
         self.step_count += 1
         outs = err_outs

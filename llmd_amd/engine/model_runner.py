@@ -45,6 +45,43 @@ from .scheduler import ScheduledReq, SchedulerOutput
 log = logging.getLogger("llmd.runner")
 
 
+class DeferredSample:
+    """A step's sampled tokens still on the device (async scheduling): the ids stay there
+    for the next step's decode inputs; a non-blocking copy to pinned host memory plus an
+    event let ``host()`` wait for exactly this step, not for the step launched after it."""
+
+    __slots__ = ("ids", "lp", "seq_ids", "row_of", "_h_ids", "_h_lp", "_ev")
+
+    def __init__(self, ids, lp, seq_ids, gpu: bool):
+        self.ids, self.lp, self.seq_ids = ids, lp, seq_ids
+        self.row_of = {s: i for i, s in enumerate(seq_ids)}
+        self._ev = None
+        if gpu and ids is not None:
+            self._h_ids = torch.empty(ids.shape, dtype=ids.dtype, pin_memory=True)
+            self._h_ids.copy_(ids, non_blocking=True)
+            self._h_lp = None
+            if lp is not None:
+                self._h_lp = torch.empty(lp.shape, dtype=lp.dtype, pin_memory=True)
+                self._h_lp.copy_(lp, non_blocking=True)
+            self._ev = torch.cuda.Event()
+            self._ev.record()
+        else:
+            self._h_ids, self._h_lp = ids, lp
+
+    @classmethod
+    def empty(cls) -> "DeferredSample":
+        return cls(None, None, [], False)
+
+    def host(self) -> dict[int, tuple[int, float]]:
+        if not self.seq_ids:
+            return {}
+        if self._ev is not None:
+            self._ev.synchronize()
+        ids = self._h_ids.tolist()
+        lp = self._h_lp.tolist() if self._h_lp is not None else [0.0] * len(ids)
+        return {s: (int(ids[i]), float(lp[i])) for i, s in enumerate(self.seq_ids)}
+
+
 def _mix64(z: int) -> int:
     z &= (1 << 64) - 1
     z = ((z ^ (z >> 30)) * 0xBF58476D1CE4E5B9) & ((1 << 64) - 1)
@@ -455,23 +492,33 @@ class ModelRunner:
     # ------------------------------------------------------------ execution
     @torch.no_grad()
     def execute(self, so: SchedulerOutput, block_tables: dict[int, list[int]], force_eager: bool = False,
-                bucket: Optional[int] = None) -> dict[int, tuple[int, float]]:
+                bucket: Optional[int] = None, prev: Optional["DeferredSample"] = None, defer: bool = False):
         """force_eager / bucket: DP-lockstep overrides (every EP rank must run the
-        same kind of step with the same collective shapes)."""
+        same kind of step with the same collective shapes).
+
+        Async scheduling (engine.py): ``prev`` is the previous step, still in flight, whose
+        sampled tokens are the inputs of this step's decode rows - they are gathered on the
+        device (the host holds placeholders); ``defer`` returns a DeferredSample instead of
+        waiting for this step's tokens."""
         if so.empty:
-            return {}
+            return DeferredSample.empty() if defer else {}
         with markers.range("llmd.plan"):
             pl, reqs = self.plan(so, block_tables)
             if force_eager:
                 pl["graph"] = False
             elif bucket is not None and pl["graph"]:
                 pl["bucket"] = bucket
+            if prev is not None:
+                g = self._gather_from(so, prev)
+                if g is not None:
+                    pl["gather"] = g
             if self.tp_size > 1:
+                assert "gather" not in pl, "async scheduling is single-rank only"
                 tp_broadcast_plan(pl)  # TP followers run the same plan (engine/tp_worker.py)
         with markers.range("llmd.forward"):
             logits = self.run_plan(pl)
         if not reqs:
-            return {}
+            return DeferredSample.empty() if defer else {}
         if pl.get("embed") and getattr(self, "_last_hidden", None) is not None:
             # pooling for /v1/embeddings: last-token final hidden state, L2-normalised
             e = torch.nn.functional.normalize(self._last_hidden.float(), dim=-1).cpu()
@@ -479,7 +526,24 @@ class ModelRunner:
                 if r.params.embed:
                     r.extra["embedding"] = e[i].tolist()
         with markers.range("llmd.sample"):
-            return self._sample(logits, reqs)
+            ids, lp = self._sample_dev(logits, reqs)
+            if defer:
+                return DeferredSample(ids, lp, [r.seq_id for r in reqs], self.is_gpu)
+            return self._to_host(ids, lp, reqs)
+
+    def _gather_from(self, so: SchedulerOutput, prev: "DeferredSample"):
+        """(dst rows, src rows) device index tensors: decode rows whose input token is the
+        previous step's sampled token (a host placeholder), or None."""
+        dst, src = [], []
+        for i, sr in enumerate(so.decodes):
+            r = sr.req
+            if r.async_pending and sr.start == r.num_tokens - 1:
+                dst.append(i)
+                src.append(prev.row_of[r.seq_id])
+        if not dst:
+            return None
+        return (torch.tensor(dst, dtype=torch.long).to(self.device, non_blocking=True),
+                torch.tensor(src, dtype=torch.long).to(self.device, non_blocking=True), prev.ids)
 
     def plan(self, so: SchedulerOutput, block_tables: dict[int, list[int]]) -> tuple[dict, list]:
         """Host-side step description: everything a (TP) rank needs to run the
@@ -600,6 +664,16 @@ class ModelRunner:
         return logits
 
     def _sample(self, logits, reqs):
+        ids, lp = self._sample_dev(logits, reqs)
+        return self._to_host(ids, lp, reqs)
+
+    @staticmethod
+    def _to_host(ids, lp, reqs):
+        ids_h = ids.cpu().tolist()
+        lp_h = lp.cpu().tolist() if lp is not None else [0.0] * len(ids_h)
+        return {r.seq_id: (int(ids_h[i]), float(lp_h[i])) for i, r in enumerate(reqs)}
+
+    def _sample_dev(self, logits, reqs):
         temps, seeds, topk, topp, any_rand, any_k, any_p = self._sampling_tensors(reqs)
         want_lp = any(r.params.logprobs for r in reqs)
         dev = self.device
@@ -615,10 +689,7 @@ class ModelRunner:
         gen = None
         if not self.is_gpu and any_rand:
             gen = torch.Generator().manual_seed(int(seeds[0]) & 0x7FFFFFFF)
-        ids, lp = ops.sample(logits, t, s, want_logprob=want_lp, generator=gen)
-        ids_h = ids.cpu().tolist()
-        lp_h = lp.cpu().tolist() if lp is not None else [0.0] * len(ids_h)
-        return {r.seq_id: (int(ids_h[i]), float(lp_h[i])) for i, r in enumerate(reqs)}
+        return ops.sample(logits, t, s, want_logprob=want_lp, generator=gen)
 
     def _run_eager(self, pl: dict):
         ids, meta = self._eager_meta(pl)
@@ -666,7 +737,11 @@ class ModelRunner:
                 meta, slot_mapping=hd[3], d_cascade=None,
                 d_block_tables=torch.from_numpy(swa[1]).to(dev, non_blocking=True) if nd else None,
                 p_block_tables=torch.from_numpy(swa[2]).to(dev, non_blocking=True) if p_ql else None)
-        return hd[0], meta
+        ids = hd[0]
+        if pl.get("gather") is not None:  # async: decode inputs sampled by the step still in flight
+            dst, src, prev_ids = pl["gather"]
+            ids.index_copy_(0, dst, prev_ids.index_select(0, src).to(ids.dtype))
+        return ids, meta
 
     def _cascade_plan(self, d_bt, d_len, max_work=None):
         """Shared-prefix decode plan for this step's decode rows, or None."""
@@ -1010,6 +1085,9 @@ class ModelRunner:
             d_len = np.concatenate([d_len, np.ones(pad, dtype=np.int32)])
         host = torch.tensor([ids, pos, slots], dtype=torch.long).pin_memory()
         self.g_ids[:B].copy_(host[0], non_blocking=True)
+        if pl.get("gather") is not None:  # async: decode inputs sampled by the step still in flight
+            dst, src, prev_ids = pl["gather"]
+            self.g_ids.index_copy_(0, dst, prev_ids.index_select(0, src).to(self.g_ids.dtype))
         self.g_pos[:B].copy_(host[1], non_blocking=True)
         self.g_slots[:B].copy_(host[2], non_blocking=True)
         self.g_bt[:B].copy_(torch.from_numpy(d_bt).pin_memory(), non_blocking=True)

@@ -150,6 +150,11 @@ class Request:
     extra: dict = field(default_factory=dict)
     # multimodal inputs (models/vision.py MMInput): image placeholder runs + embeddings
     mm_inputs: Optional[list] = None
+    # async scheduling (engine.py): the last output token is a placeholder whose value is
+    # still on the device (its step is in flight); final_pending = that token is the last one
+    # (max_tokens / max_model_len reached), so the request is not scheduled again
+    async_pending: bool = False
+    final_pending: bool = False
 
     @property
     def cache_extra(self) -> int:

@@ -274,7 +274,7 @@ class Scheduler:
         while i < len(self.running) and budget > 0:
             r = self.running[i]
             n = r.num_tokens - r.num_computed_tokens
-            if n <= 0:
+            if n <= 0 or r.final_pending:  # final_pending: its last token is in flight (async)
                 i += 1
                 continue
             n = min(n, budget)
@@ -450,6 +450,61 @@ class Scheduler:
                 touched.append(r)
         return touched
 
+    # ------------------------------------------------------------ async scheduling
+    # A step's update split in two (engine.py async path): ``advance`` when the step is
+    # launched - positions move on, completed blocks are committed, windowed blocks released,
+    # and every sampling request gets a placeholder output token, so the next step can be
+    # scheduled before this one's tokens reach the host; ``resolve`` once they have -
+    # placeholders become the real tokens and stop conditions are checked.
+    PLACEHOLDER = -1
+
+    def advance(self, out: SchedulerOutput, sampling: set) -> None:
+        """Called once the previous step is resolved, so every INPUT token of this step is
+        real: blocks this step completes are committed here (hashes over their tokens),
+        before the windowed pool releases anything (write-through offload sees them)."""
+        bs = self.cfg.cache.block_size
+        for sr in out.all():
+            r = sr.req
+            if r.status.finished:
+                continue
+            r.num_computed_tokens = sr.start + sr.num_new_tokens
+            if (self.cfg.cache.enable_prefix_caching and r.num_computed_tokens // bs > sr.start // bs
+                    and self.bm.has_seq(r.seq_id)):
+                self.bm.commit(r.seq_id, self._tokens(r)[:r.num_computed_tokens], r.num_computed_tokens)
+            if self._window_release and self.bm.has_seq(r.seq_id):
+                # windowed blocks no later query reaches: released now (token values not needed;
+                # a step launched after this one reuses them only after this one ran - one stream)
+                n_keep = r.num_computed_tokens
+                if (r.kv_transfer_params or {}).get("do_remote_decode"):
+                    n_keep -= 1
+                self.bm.after_compute(r.seq_id, n_keep)
+            if r.seq_id in sampling:
+                r.output_token_ids.append(self.PLACEHOLDER)
+                r.output_logprobs.append(0.0)
+                r.async_pending = True
+                # the token in flight is the last one whatever its value: do not schedule again
+                if len(r.output_token_ids) >= r.params.max_tokens or r.num_tokens >= self.sc.max_model_len:
+                    r.final_pending = True
+
+    def resolve(self, out: SchedulerOutput, sampled: dict[int, tuple[int, float]]) -> list[Request]:
+        touched = []
+        now = time.monotonic()
+        for sr in out.all():
+            r = sr.req
+            if r.status.finished:
+                continue
+            if r.seq_id in sampled and r.async_pending:
+                tok, lp = sampled[r.seq_id]
+                r.output_token_ids[-1] = tok
+                r.output_logprobs[-1] = lp
+                r.async_pending = False
+                if r.first_token_time is None:
+                    r.first_token_time = now
+                r.last_token_time = now
+                self._check_stop(r)
+                touched.append(r)
+        return touched
+
     def _check_stop(self, r: Request):
         p = r.params
         n_out = len(r.output_token_ids)
@@ -468,6 +523,8 @@ class Scheduler:
     def _finish_running(self, r: Request, status: Status):
         if r in self.running:
             self.running.remove(r)
+        elif r.status == Status.PREEMPTED:  # async: preempted while its last token was in flight
+            self.waiting.remove(r)
         self._finish(r, status)
 
     def _finish(self, r: Request, status: Status, free_blocks: bool = True):

@@ -67,6 +67,9 @@ class AsyncEngine:
                         for o in eng.connector.take_outputs():
                             self._emit(o)
                 else:
+                    if getattr(eng, "_pending", None) is not None:  # async: the step in flight's outputs
+                        for o in eng.drain():
+                            self._emit(o)
                     if eng.connector is not None:
                         eng.connector.tick()
                         for o in eng.connector.take_outputs():

@@ -39,6 +39,9 @@ def restagger(running, osl: int, concurrency: int) -> int:
     longest = 0
     for r, left in zip(reqs, remaining_schedule(len(reqs), osl, concurrency)):
         r.params.max_tokens = len(r.output_token_ids) + left
+        # async scheduling: a request whose in-flight token was its last under the old length
+        # is scheduled again under the new one
+        r.final_pending = len(r.output_token_ids) >= r.params.max_tokens
         longest = max(longest, r.params.max_tokens)
     return longest
 

@@ -29,6 +29,7 @@ def main():
                     help="emulate one rank of a TP-N replica on one GPU: heads, FFN and vocab divided by N "
                          "(the rank's GEMM/attention/KV work; the TP all-reduces are not included)")
     ap.add_argument("--kv-cache-gb", type=float, default=None)
+    ap.add_argument("--no-async-scheduling", action="store_true")
     a = ap.parse_args()
     if a.tp_shard > 1:
         import dataclasses
@@ -49,7 +50,7 @@ def main():
     cfg = EngineConfig.create(a.model, device="cuda", block_size=64, max_num_seqs=a.batch,
                               max_num_batched_tokens=8192, max_model_len=a.isl + mt + 64,
                               cuda_graph_max_bs=a.batch, quantization=a.quantization,
-                              kv_cache_dtype=a.kv_cache_dtype,
+                              kv_cache_dtype=a.kv_cache_dtype, async_scheduling=not a.no_async_scheduling,
                               kv_cache_memory_bytes=int(a.kv_cache_gb * 2**30) if a.kv_cache_gb else None)
     eng = LLMEngine(cfg)
     tstart = time.perf_counter()
@@ -82,7 +83,7 @@ def main():
         torch.cuda.synchronize()
         pr.disable()
         pstats.Stats(pr).sort_stats("tottime").print_stats(25)
-    print(f"{a.model} q={a.quantization} kv={a.kv_cache_dtype} decode batch={a.batch} ctx~{a.isl}: "
+    print(f"{a.model} q={a.quantization} kv={a.kv_cache_dtype} async={not a.no_async_scheduling} decode batch={a.batch} ctx~{a.isl}: "
           f"{dt * 1e3:.2f} ms/step  {ran / dt:.0f} tok/s (running {ran:.0f}) (prefill phase {t0 - tstart:.1f}s)", flush=True)
 
 

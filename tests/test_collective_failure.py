@@ -34,7 +34,7 @@ def fake_word(monkeypatch):
 def test_engine_step_raises_before_emitting(fake_word):
     from tests.test_engine import make_engine
 
-    eng = make_engine()
+    eng = make_engine(async_scheduling=False)
     prompt = np.random.default_rng(1).integers(3, 500, size=40).tolist()
     eng.add_request("a", prompt, SamplingParams(max_tokens=8, temperature=0.0, ignore_eos=True))
     outs = eng.step()  # healthy: the prefill step emits the first token
@@ -44,6 +44,24 @@ def test_engine_step_raises_before_emitting(fake_word):
     with pytest.raises(symm.CollectiveFailure):
         eng.step()
     assert len(eng.sched.requests["a"].output_token_ids) == n_tok  # nothing from the bad step
+    fake_word.value = 0
+    symm.clear_host_error()
+
+
+def test_async_engine_step_raises_before_emitting(fake_word):
+    """Async scheduling: a step's tokens are emitted one call later, and the health check
+    runs before they are - a broken step's tokens never reach a client there either."""
+    from tests.test_engine import make_engine
+
+    eng = make_engine(async_scheduling=True)
+    prompt = np.random.default_rng(1).integers(3, 500, size=40).tolist()
+    eng.add_request("a", prompt, SamplingParams(max_tokens=8, temperature=0.0, ignore_eos=True))
+    assert eng.step() == []               # prefill launched, its token still in flight
+    outs = eng.step()                     # next step launched, the prefill's token emitted
+    assert [o.request_id for o in outs] == ["a"]
+    fake_word.value = 1                   # a symm kernel timed out during the step in flight
+    with pytest.raises(symm.CollectiveFailure):
+        eng.step()
     fake_word.value = 0
     symm.clear_host_error()
 
