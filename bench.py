@@ -287,14 +287,20 @@ def main():
     step_tokens = []
     step_ms = collections.defaultdict(list)  # step size -> wall ms (a step ends in a host sync on sampling)
 
+    prev_n = [0]
+
     def run_steps(n):
         for _ in range(n):
             ts0 = time.perf_counter()
             for o in eng.step():
                 if o.finished:
                     new_request(a.osl)
+            # async scheduling: a call returns once the PREVIOUS step finished on the device
+            # (the one it launched is still running), so its wall time is that step's
+            k = prev_n[0] if eng_async else eng.last_num_tokens
+            prev_n[0] = eng.last_num_tokens
             step_tokens.append(eng.last_num_tokens)
-            step_ms[eng.last_num_tokens].append(1000 * (time.perf_counter() - ts0))
+            step_ms[k].append(1000 * (time.perf_counter() - ts0))
 
     # warmup
     tw = time.time()
@@ -318,7 +324,8 @@ def main():
     elapsed = time.perf_counter() - t1
     hist = collections.Counter(step_tokens)
     log(rank, "timed step sizes (tokens: steps, mean ms): " + ", ".join(
-        f"{k}: {v} x {statistics.mean(step_ms[k]):.1f}" for k, v in sorted(hist.items())))
+        f"{k}: {v} x {statistics.mean(step_ms[k]) if step_ms.get(k) else float('nan'):.1f}"
+        for k, v in sorted(hist.items())))
     gen = eng.metrics.n_gen - gen0
     ptoks = eng.metrics.n_prompt - prompt0
     ttfts = list(eng.metrics.ttfts)
