@@ -117,6 +117,15 @@ def parse():
                    help="pd mode at N=8: also run this P:D split after the main one ('2p6d', BASELINE.json's "
                         "literal config; 'auto' = 2p6d when N=8 and the main split differs; 'none' = skip)")
     p.add_argument("--no-preflight", action="store_true", help="skip the N>1 cross-GPU pre-flight checks")
+    p.add_argument("--pd-route", default="router", choices=["router", "direct"],
+                   help="pd mode: requests go client -> router (EPP, the reference's P/D config) -> decode "
+                        "routing sidecar -> prefill + kvx pull (router), or through an in-process sidecar loop "
+                        "on each decode driver (direct)")
+    p.add_argument("--pd-decider", default="always", choices=["always", "load-aware"],
+                   help="pd mode, routed: the EPP's P/D decider (always-disagg = the reference config)")
+    p.add_argument("--open-loop-rate", type=float, default=0.0,
+                   help="pd mode, routed: Poisson request rate of the open-loop phase (0 = 0.9 x closed-loop rate)")
+    p.add_argument("--open-loop-requests", type=int, default=0)
     p.add_argument("--fp8-extra", default="auto", choices=["auto", "off"],
                    help="agg mode, 1 GPU, bf16 run: also measure the reference AMD recipe's precision (W8A8 fp8 "
                         "linears + fp8 KV) in a child process and report it under 'fp8' (the bf16 figure stays "
@@ -202,8 +211,12 @@ def main():
                 "output_tok_s_per_gpu": round(value / world, 2),
                 "p50_ttft_s": round(res["p50_ttft"], 4) if res["p50_ttft"] is not None else None,
                 "kv_transfer_failures": res.get("kv_failures", 0),
+                **{k: res[k] for k in ("route", "open_loop", "router_pd_decisions", "sidecar_pd_requests",
+                                       "sidecar_fallbacks", "steady_state") if k in res},
                 **_reference(a.model, value, world),
             }
+            if "ttft_p90" in res:
+                out["p90_ttft_s"] = round(res["ttft_p90"], 4)
             if alt is not None:
                 out["alt_split"] = alt
             line = json.dumps(out)
@@ -455,6 +468,9 @@ def _alt_split(a, rank, world, local_rank, log, main_res):
         torch.cuda.empty_cache()
     b = argparse.Namespace(**vars(a))
     b.prefill_gpus, b.decode_tp = p_n, 0
+    # few prefill GPUs: the load-aware decider lets decoders prefill locally while every
+    # prefill queue is deep (router/plugins/scheduling.py LoadAwarePDDecider)
+    b.pd_decider = os.environ.get("LLMD_ALT_PD_DECIDER", "load-aware")
     os.environ["LLMD_PD_BASE_PORT"] = str(int(os.environ.get("LLMD_PD_BASE_PORT", "18200")) + 100)
     try:
         r = run_pd(b, rank, world, local_rank, log)
@@ -468,7 +484,9 @@ def _alt_split(a, rank, world, local_rank, log, main_res):
                                           + (f"-dtp{r['decode_tp']}" if r.get("decode_tp", 1) > 1 else ""),
             "value": round(v, 2), "output_tok_s_per_decode_gpu": round(v / r["decode_ranks"], 2),
             "output_tok_s_per_gpu": round(v / world, 2), "ms_per_step": round(1000 * r["elapsed"] / a.steps, 3),
-            "p50_ttft_s": round(r["p50_ttft"], 4) if r["p50_ttft"] is not None else None}
+            "p50_ttft_s": round(r["p50_ttft"], 4) if r["p50_ttft"] is not None else None,
+            "pd_decider": b.pd_decider,
+            **{k: r[k] for k in ("open_loop", "router_pd_decisions", "sidecar_pd_requests") if k in r}}
 
 
 if __name__ == "__main__":
