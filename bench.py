@@ -212,7 +212,7 @@ def main():
                 "p50_ttft_s": round(res["p50_ttft"], 4) if res["p50_ttft"] is not None else None,
                 "kv_transfer_failures": res.get("kv_failures", 0),
                 **{k: res[k] for k in ("route", "open_loop", "router_pd_decisions", "sidecar_pd_requests",
-                                       "sidecar_fallbacks", "steady_state") if k in res},
+                                       "sidecar_fallbacks", "steady_state", "ttft_source") if k in res},
                 **_reference(a.model, value, world),
             }
             if "ttft_p90" in res:

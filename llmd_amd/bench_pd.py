@@ -233,7 +233,7 @@ def _summarize(gathered, P, world, dtp=1):
            "prefill_ranks": P, "decode_ranks": world - P, "decode_tp": dtp, "n_ttft": len(tt),
            "kv_failures": sum(g.get("kv_failures", 0) for g in dec)}
     for g in gathered:  # routed path: rank 0 carries the client / router view
-        for k in ("route", "open_loop", "router_pd_decisions", "ttft_p90", "steady_state"):
+        for k in ("route", "open_loop", "router_pd_decisions", "ttft_p90", "steady_state", "ttft_source"):
             if k in g:
                 out[k] = g[k]
     if any("sidecar_pd" in g for g in dec):
@@ -606,6 +606,13 @@ def _run_routed(a, rank, world, P, dtp, drivers, is_prefill, eng, cfg, world_ctl
                                 "ttft_p90_s": round(float(np.percentile(tt, 90)), 4) if tt else None,
                                 "output_tok_s": round(toks / dur, 1) if dur > 0 else None,
                                 "errors": sum(1 for e in evs if not e[4])}
+        # p50 TTFT: the closed-loop window's when it saw enough first tokens, else the open loop's
+        # (the reference's TTFT comes from its rate-driven run)
+        out["ttft_source"] = "closed-loop window"
+        if out.get("n_ttft", 0) < 5 and out.get("open_loop", {}).get("ttft_p50_s") is not None:
+            out["p50_ttft"] = out["open_loop"]["ttft_p50_s"]
+            out["ttft_p90"] = out["open_loop"]["ttft_p90_s"]
+            out["ttft_source"] = "open-loop phase"
         try:
             m = _scrape(f"http://127.0.0.1:{base + 1001}/metrics")
             out["router_pd_decisions"] = {k: _counter_sum(m, "llm_d_router_epp_pd_decision", f'decision_type="{k}"')
