@@ -8,6 +8,7 @@ void register_kv_index(py::module_& m);
 void register_gbdt(py::module_& m);
 void register_fs_store(py::module_& m);
 void register_shm_ring(py::module_& m);
+void register_epp_score(py::module_& m);
 
 PYBIND11_MODULE(_rt, m) {
   m.doc() = "llmd_amd native host runtime";
@@ -16,4 +17,5 @@ PYBIND11_MODULE(_rt, m) {
   register_gbdt(m);
   register_fs_store(m);
   register_shm_ring(m);
+  register_epp_score(m);
 }

@@ -13,8 +13,10 @@ latency samples and metrics.
 from __future__ import annotations
 
 import asyncio
+import functools
 import json
 import logging
+import random
 import time
 from dataclasses import dataclass, field
 from typing import Optional
@@ -27,6 +29,10 @@ from .flow_control import DISPATCHED, OUTCOME_HTTP, OUTCOME_REASON, FlowControll
 from .metrics import EPPMetrics
 from ..utils.tracing import span
 from .types import Endpoint, InferenceRequest, ProfileRunResult, SchedulingError, SchedulingResult
+from .. import _rt_loader
+
+_RT = _rt_loader.rt()
+_rand64 = functools.partial(random.getrandbits, 64)  # Python's random: seeding it keeps picks reproducible
 
 log = logging.getLogger("llmd.router.epp")
 
@@ -218,23 +224,33 @@ class EPP:
             if not cand:
                 return ProfileRunResult([], {})
         keys = [e.key for e in cand]
-        acc = [0.0] * len(keys)
+        cols, ws = [], []
         for s, w in prof.scorers:
             t0 = time.perf_counter()
-            sc = s.score(req, cand)
+            vec = getattr(s, "score_vec", None)
+            if vec is not None:  # a list aligned with the candidates
+                col = vec(req, cand)
+            else:
+                get = s.score(req, cand).get
+                col = [float(get(k) or 0.0) for k in keys]
             m.child(m.plugin_dur, "Scorer", s.plugin_type, s.name).observe(time.perf_counter() - t0)
-            get = sc.get
-            for i, k in enumerate(keys):  # clamp to [0, 1], weight, sum (per endpoint per scorer)
-                v = get(k)
-                if v:
-                    v = float(v)
-                    acc[i] += w * (1.0 if v > 1.0 else (v if v > 0.0 else 0.0))
-        total = dict(zip(keys, acc))
-        scored = list(zip(cand, acc))
+            cols.append(col)
+            ws.append(float(w))
+        # clamp to [0, 1], weight, sum, and the stock pickers: one native call (csrc/runtime/epp_score.cpp)
+        picker = prof.picker
+        kind = getattr(type(picker), "native_kind", None)
         t0 = time.perf_counter()
-        picked = prof.picker.pick(req, scored)
-        m.child(m.plugin_dur, "Picker", prof.picker.plugin_type, prof.picker.name).observe(time.perf_counter() - t0)
-        return ProfileRunResult(picked, total)
+        if not cols:
+            cols = [[0.0] * len(keys)]
+            ws = [0.0]
+        n_pick = int(picker.p("maxNumOfEndpoints", 1))
+        acc, idx = _RT.combine_pick(cols, ws, n_pick if kind is not None else 0, kind or 0, _rand64())
+        if kind is not None:
+            picked = [cand[i] for i in idx]
+        else:
+            picked = picker.pick(req, list(zip(cand, acc)))
+        m.child(m.plugin_dur, "Picker", picker.plugin_type, picker.name).observe(time.perf_counter() - t0)
+        return ProfileRunResult(picked, dict(zip(keys, acc)))
 
     # ------------------------------------------------------------ response path
     def on_response_headers(self, d: Decision, status: int, headers: dict):

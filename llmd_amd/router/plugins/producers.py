@@ -14,7 +14,7 @@ from typing import Optional
 
 from llmd_amd import _rt_loader
 
-from ..types import BLOCK_SIZE, KV_USAGE, NUM_GPU_BLOCKS, RUNNING, WAITING, Endpoint, InferenceRequest
+from ..types import ATTR_VERSION, BLOCK_SIZE, KV_USAGE, NUM_GPU_BLOCKS, RUNNING, WAITING, Endpoint, InferenceRequest
 from .base import Admitter, DataProducer, PreRequest, ResponseProcessor, register
 
 log = logging.getLogger("llmd.router.producers")
@@ -47,8 +47,13 @@ class ApproxPrefixCacheProducer(DataProducer, PreRequest):
         self.auto_tune = at if isinstance(at, bool) else str(at).lower() == "true"
         self._caps: dict[str, int] = {}
         self._seen: dict[str, tuple] = {}
+        self._ver, self._n_eps = -1, -1
 
     def _tune(self, eps):
+        v = ATTR_VERSION[0]
+        if v == self._ver and len(eps) == self._n_eps:  # no endpoint attribute written since the last scan
+            return
+        self._ver, self._n_eps = v, len(eps)
         seen = self._seen
         for e in eps:
             raw = (e.metric(NUM_GPU_BLOCKS, 0), e.metric(BLOCK_SIZE, 0))

@@ -125,26 +125,42 @@ class SloHeadroomTierFilter(Filter):
 
 
 # ======================================================================= scorers
+def _minmax_inverse_vec(vals: list) -> list:
+    """_minmax_inverse over a list aligned with the candidates."""
+    if not vals:
+        return []
+    lo, hi = min(vals), max(vals)
+    if hi <= lo:
+        return [1.0] * len(vals)
+    d = hi - lo
+    return [(hi - v) / d for v in vals]
+
+
 @register("queue-scorer", "queue-depth-scorer")
 class QueueScorer(Scorer):
     def score(self, req, eps):
-        return _minmax_inverse({e.key: float(e.metric(WAITING, 0)) for e in eps})
+        return dict(zip([e.key for e in eps], self.score_vec(req, eps)))
+
+    def score_vec(self, req, eps):
+        return _minmax_inverse_vec([float(e.attrs._d.get(WAITING, 0)) for e in eps])
 
 
 @register("kv-cache-utilization-scorer", "kv-cache-scorer")
 class KVCacheUtilizationScorer(Scorer):
     def score(self, req, eps):
-        out = {}
-        for e in eps:
-            v = 1.0 - float(e.metric(KV_USAGE, 0.0))
-            out[e.key] = 1.0 if v > 1.0 else (v if v > 0.0 else 0.0)
-        return out
+        return {e.key: min(1.0, max(0.0, v)) for e, v in zip(eps, self.score_vec(req, eps))}
+
+    def score_vec(self, req, eps):  # 1 - usage; the combiner (_rt.combine_pick) clamps to [0, 1]
+        return [1.0 - e.attrs._d.get(KV_USAGE, 0.0) for e in eps]
 
 
 @register("running-requests-size-scorer")
 class RunningRequestsScorer(Scorer):
     def score(self, req, eps):
-        return _minmax_inverse({e.key: float(e.metric(RUNNING, 0)) for e in eps})
+        return dict(zip([e.key for e in eps], self.score_vec(req, eps)))
+
+    def score_vec(self, req, eps):
+        return _minmax_inverse_vec([float(e.attrs._d.get(RUNNING, 0)) for e in eps])
 
 
 @register("active-request-scorer")
@@ -214,6 +230,10 @@ class PrefixCacheScorer(Scorer):
         info = _prefix_info(req, self.p("prefixMatchInfoProducerName"))
         return {e.key: float(info.get(e.key, 0.0)) for e in eps}
 
+    def score_vec(self, req, eps):
+        get = _prefix_info(req, self.p("prefixMatchInfoProducerName")).get
+        return [get(e.key, 0.0) for e in eps]
+
 
 @register("no-hit-lru-scorer")
 class NoHitLRUScorer(Scorer, PreRequest):
@@ -226,7 +246,13 @@ class NoHitLRUScorer(Scorer, PreRequest):
 
     def _cold(self, req):
         info = _prefix_info(req, self.p("prefixMatchInfoProducerName"))
-        return not any(v > 0 for v in info.values())
+        return max(info.values(), default=0.0) <= 0
+
+    def score_vec(self, req, eps):
+        if not self._cold(req):
+            return [1.0] * len(eps)
+        sc = self.score(req, eps)
+        return [sc[e.key] for e in eps]
 
     def score(self, req, eps):
         if not self._cold(req):
@@ -327,6 +353,8 @@ class LatencyScorer(Scorer):
 # ======================================================================= pickers
 @register("max-score-picker")
 class MaxScorePicker(Picker):
+    native_kind = 0  # epp.run_profile picks natively (_rt.combine_pick) with the same semantics
+
     def pick(self, req, scored):
         n = int(self.p("maxNumOfEndpoints", 1))
         if not scored:
@@ -338,6 +366,8 @@ class MaxScorePicker(Picker):
 
 @register("random-picker")
 class RandomPicker(Picker):
+    native_kind = 2
+
     def pick(self, req, scored):
         n = int(self.p("maxNumOfEndpoints", 1))
         eps = [e for e, _ in scored]
@@ -348,6 +378,8 @@ class RandomPicker(Picker):
 @register("weighted-random-picker")
 class WeightedRandomPicker(Picker):
     """Lottery scheduling: probability proportional to score."""
+
+    native_kind = 1
 
     def pick(self, req, scored):
         n = int(self.p("maxNumOfEndpoints", 1))

@@ -30,15 +30,21 @@ class Attributes:
     def put(self, k: str, v: Any):
         with self._lock:
             self._d[k] = v
+            ATTR_VERSION[0] += 1
 
     def update(self, d: dict):
         with self._lock:
             self._d.update(d)
+            ATTR_VERSION[0] += 1
 
     def snapshot(self) -> dict:
         with self._lock:
             return dict(self._d)
 
+
+# bumped by every Attributes write: per-request consumers of slowly changing endpoint attributes
+# (the prefix producer's LRU auto-tune) skip their scan while nothing changed
+ATTR_VERSION = [0]
 
 # standard metric attribute keys (core-metrics-extractor output)
 WAITING = "WaitingQueueSize"
