@@ -68,7 +68,7 @@ int llmd_pgemm(const void*, int64_t, const void*, int64_t, void*, int64_t, int, 
                hipStream_t);
 int64_t llmd_pgemm_ws_bytes(int, int, int, int, int);
 int llmd_pgemm_fp8(const void*, int64_t, const float*, const void*, int64_t, const float*, void*, int64_t, int, int,
-                   int, int, void*, hipStream_t);
+                   int, int, void*, int, hipStream_t);
 int64_t llmd_pgemm_fp8_ws_bytes(int, int, int, int);
 int llmd_mgemm_fp8(const void*, int64_t, const float*, const void*, int64_t, const float*, int, int, int, int, int,
                    int, void*, int64_t, float*, int*, hipStream_t);
@@ -576,7 +576,7 @@ void pgemm(torch::Tensor y, torch::Tensor x, torch::Tensor w, int64_t epi, int64
 // v_mfma_scale_f32_16x16x128_f8f6f4): xq [M, K] / wq [N, K] e4m3fn, xs [M] or [M, 1] and ws [N] or
 // [1, N] fp32; epi 3 = silu(gate) * up on wq = [gate; up], y [M, N / 2]
 void pgemm_fp8(torch::Tensor y, torch::Tensor xq, torch::Tensor xs, torch::Tensor wq, torch::Tensor ws, int64_t epi,
-               bool split_k) {
+               bool split_k, bool persistent) {
   const c10::hip::OptionalHIPGuard device_guard(dev_of(y));
   CHECK_CUDA(xq); CHECK_BF16(y); CHECK_INNER(xq); CHECK_INNER(wq); CHECK_INNER(y);
   TORCH_CHECK(xq.scalar_type() == at::kFloat8_e4m3fn && wq.scalar_type() == at::kFloat8_e4m3fn, "pgemm_fp8: e4m3fn");
@@ -591,11 +591,12 @@ void pgemm_fp8(torch::Tensor y, torch::Tensor xq, torch::Tensor xs, torch::Tenso
   TORCH_CHECK(xq.stride(0) % 16 == 0 && wq.stride(0) % 16 == 0 && y.stride(0) % 8 == 0, "pgemm_fp8: 16-B rows");
   // split_k: a mostly idle last wave of tiles runs split over K into an fp32 workspace
   torch::Tensor wsp;
-  const int64_t wsb = split_k ? llmd_pgemm_fp8_ws_bytes((int)M, (int)N, (int)K, (int)epi) : 0;
+  const int64_t wsb = (split_k && !(persistent && epi == 0)) ? llmd_pgemm_fp8_ws_bytes((int)M, (int)N, (int)K, (int)epi)
+                                                            : 0;
   if (wsb > 0) wsp = torch::empty({wsb / 4}, xs.options());
   int rc = llmd_pgemm_fp8(xq.data_ptr(), xq.stride(0), xs.data_ptr<float>(), wq.data_ptr(), wq.stride(0),
                           ws.data_ptr<float>(), y.data_ptr(), y.stride(0), (int)M, (int)N, (int)K, (int)epi,
-                          wsb > 0 ? wsp.data_ptr() : nullptr, cur_stream());
+                          wsb > 0 ? wsp.data_ptr() : nullptr, persistent ? 1 : 0, cur_stream());
   TORCH_CHECK(rc == 0, "pgemm_fp8 failed: ", rc);
 }
 

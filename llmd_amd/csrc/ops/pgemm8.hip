@@ -315,6 +315,193 @@ __host__ inline void pgemm8_plan(int M, int N, int K, int epi, int& full, int& t
   nsplit = s;
 }
 
+
+// ---------------------------------------------------------------------------
+// Persistent form (EPI_NONE): each workgroup walks tiles b, b + P, b + 2P, ... (P = min(#tiles,
+// 256) workgroups) as ONE stream of K-steps g = 0 .. nt * nk - 1 with the schedule above, so the
+// next tile's first two K-steps (and its 2 KB of scales) are DMA'd while the current tile's last
+// steps compute - no per-tile prologue wait. The epilogue stores straight from the accumulators
+// (both LDS buffers already hold the next tile): each lane writes 4 consecutive bf16 columns of a
+// row (8 B); the tile's token / channel scales come from a small double-buffered LDS slot filled
+// by the same LDS-DMA (a global load here would make hipcc wait vmcnt(0) on the DMAs in flight).
+constexpr int P8_SCB = 2 * 256 * 4;             // one tile's xs (256 rows) + ws (256 columns)
+constexpr int P8_LDS_P = 2 * P8_BUF + 2 * P8_SCB;
+
+__global__ __launch_bounds__(P8_NT, 1) void pgemm8p_kernel(const uint8_t* __restrict__ A, int64_t lda,
+                                                           const float* __restrict__ xs,
+                                                           const uint8_t* __restrict__ W, int64_t ldw,
+                                                           const float* __restrict__ wsc,
+                                                           uint16_t* __restrict__ C, int64_t ldc, int M, int N,
+                                                           int K, int ntiles) {
+  __shared__ __attribute__((aligned(1024))) char lds[P8_LDS_P];  // the ONLY LDS object
+  const int tiles_m = (M + P8_BM - 1) / P8_BM, tiles_n = N / P8_BN;
+  const int P = gridDim.x;
+  const int b = xcd_remap(blockIdx.x, P);
+  const int nt = (ntiles - b + P - 1) / P;  // this workgroup's tiles: b, b + P, ...
+  const int nk = K / P8_BK;
+  const int S = nt * nk;                    // K-steps of this workgroup, all tiles
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = w >> 1, wc = w & 1;
+  const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc((void*)A, 0, 0x7fffffff, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc((void*)W, 0, 0x7fffffff, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rxs = __builtin_amdgcn_make_buffer_rsrc((void*)xs, 0, 0x7fffffff, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rws = __builtin_amdgcn_make_buffer_rsrc((void*)wsc, 0, 0x7fffffff, 0x00020000);
+
+  // DMA offsets of the tile being LOADED (two K-steps ahead of compute)
+  uint32_t va[8], vw[8], vxs, vws;
+  auto set_dma_tile = [&](int r) {
+    int tm, tn;
+    p8_tile_mn(b + min(r, nt - 1) * P, tiles_m, tiles_n, tm, tn);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int row = 64 * w + 8 * j + (lane >> 3);
+      const int c = (lane & 7) ^ ((row >> 1) & 7);
+      va[j] = tm * P8_BM + row < M ? (uint32_t)((int64_t)(tm * P8_BM + row) * lda + c * 16) : P8_OOB;
+      vw[j] = (uint32_t)((int64_t)(tn * P8_BN + row) * ldw + c * 16);
+    }
+    const int m = tm * P8_BM + 64 * w + lane;
+    vxs = m < M ? (uint32_t)(m * 4) : P8_OOB;
+    vws = (uint32_t)((tn * P8_BN + 64 * w + lane) * 4);
+  };
+  // piece j (< 8: A, >= 8: W) of global step g, whose step within its tile is kt
+  auto dma = [&](int g, int kt, int j) {
+    char* dst = lds + (g & 1) * P8_BUF + (j >= 8 ? P8_OPB : 0) + (8 * w + (j & 7)) * 1024;
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(j >= 8 ? rw : ra, (__attribute__((address_space(3))) void*)dst, 16,
+                                             j >= 8 ? vw[j - 8] : va[j], (uint32_t)(kt * P8_BK), 0, 0);
+  };
+  auto dma_scales = [&](int r) {  // tile r's scales into slot r & 1 (issued with its step-0 pieces)
+    char* base = lds + 2 * P8_BUF + (r & 1) * P8_SCB;
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rxs, (__attribute__((address_space(3))) void*)(base + w * 256), 4, vxs,
+                                             0, 0, 0);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rws, (__attribute__((address_space(3))) void*)(base + 1024 + w * 256),
+                                             4, vws, 0, 0, 0);
+  };
+  const int fr = lane & 15, fq = lane >> 4;
+  const int sw = (fr >> 1) & 7;
+  const int rd0 = fr * 128 + (((2 * fq) ^ sw) * 16), rd1 = fr * 128 + (((2 * fq + 1) ^ sw) * 16);
+  const int a_rd = (wr * 128) * 128, w_rd = P8_OPB + (wc * 128) * 128;
+  auto frag = [&](const char* buf, int base, int t) {
+    const char* p = buf + base + t * 2048;
+    const u32x4_t lo = *reinterpret_cast<const u32x4_t*>(p + rd0);
+    const u32x4_t hi = *reinterpret_cast<const u32x4_t*>(p + rd1);
+    return i32x8_t{(int)lo[0], (int)lo[1], (int)lo[2], (int)lo[3], (int)hi[0], (int)hi[1], (int)hi[2], (int)hi[3]};
+  };
+  const int one = 127;
+
+  f32x4_t acc[8][8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  i32x8_t fa[8], fw[2][8];
+
+  // prologue: global steps 0 and 1 (+ tile 0's scales) in flight, step 0 landed
+  set_dma_tile(0);
+  dma_scales(0);
+#pragma unroll
+  for (int j = 0; j < 16; ++j) dma(0, 0, j);
+  if (nk == 1) set_dma_tile(1);
+  if (nk == 1 && S > 1) dma_scales(1);
+#pragma unroll
+  for (int j = 0; j < 16; ++j) dma(1, nk == 1 ? 0 : 1, j);
+  asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+  p8_bar();
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    fw[0][j] = frag(lds, w_rd, j);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+#pragma unroll
+  for (int i = 0; i < 7; ++i) {
+    fa[i] = frag(lds, a_rd, i);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  __builtin_amdgcn_s_waitcnt(0xC07F);
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_nop 4" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+
+  // one K-step on W set SET; nk is even (host-checked), so every tile starts on set 0 and its
+  // last step runs on set 1 (after which set 1 is dead: room for the epilogue's registers)
+  auto step = [&](auto S_, int g, int kt) {
+    constexpr int SET = decltype(S_)::value;
+    const char* cur = lds + (g & 1) * P8_BUF;
+    const char* nxt = lds + ((g & 1) ^ 1) * P8_BUF;
+    const int g2 = g + 2;
+    int kt2 = kt + 2;  // step of g + 2 within its tile (scalar bookkeeping, no division)
+    if (kt2 >= nk) kt2 -= nk;
+#pragma clang loop unroll(full)
+    for (int t = 0; t < 64; ++t) {
+      const int i = t >> 3, j = t & 7;
+      mfma8(acc[i][j], fw[SET][j], fa[i], one);
+      if (t == 1) {
+        fa[7] = frag(cur, a_rd, 7);
+      } else if (t == 5) {
+        __builtin_amdgcn_s_waitcnt(0xC07F);
+        p8_bar();
+      } else if (t == 6) {
+        if (kt2 == 0 && g2 < S) {  // g + 2 starts the next tile: its offsets and its scales
+          set_dma_tile(g2 / nk);
+          dma_scales(g2 / nk);
+        }
+        dma(g2, kt2, 0);
+      } else if (t > 6 && t < 22) {
+        dma(g2, kt2, t - 6);
+      } else if (t == 27) {
+        asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+        p8_bar();
+      } else if (t >= 28 && t < 36) {
+        fw[SET ^ 1][t - 28] = frag(nxt, w_rd, t - 28);
+      } else if (t >= 44 && t < 50) {
+        fa[t - 44] = frag(nxt, a_rd, t - 44);
+      } else if (t == 57) {
+        fa[6] = frag(nxt, a_rd, 6);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  for (int r = 0; r < nt; ++r) {
+    for (int kt = 0; kt < nk; kt += 2) {
+      const int g = r * nk + kt;
+      step(std::integral_constant<int, 0>{}, g, kt);
+      step(std::integral_constant<int, 1>{}, g + 1, kt + 1);
+    }
+    {  // tile r done: scale + store straight from the accumulators, then restart them
+      int tm, tn;
+      p8_tile_mn(b + r * P, tiles_m, tiles_n, tm, tn);
+      const char* sb = lds + 2 * P8_BUF + (r & 1) * P8_SCB;
+      const int mrow = tm * P8_BM + wr * 128 + fr;
+      uint16_t* cb = C + (int64_t)tn * P8_BN + wc * 128 + 4 * fq;
+#pragma unroll
+      for (int i2 = 0; i2 < 8; ++i2) {
+        const float sx = *reinterpret_cast<const float*>(sb + (wr * 128 + 16 * i2 + fr) * 4);
+        const int m = mrow + 16 * i2;
+#pragma unroll
+        for (int j2 = 0; j2 < 8; ++j2) {
+          const f32x4_t sn = *reinterpret_cast<const f32x4_t*>(sb + 1024 + (wc * 128 + 16 * j2 + 4 * fq) * 4);
+          const f32x4_t v = acc[i2][j2];
+          u32x2_t o;
+          o[0] = (uint32_t)f2bf(v[0] * sx * sn[0]) | ((uint32_t)f2bf(v[1] * sx * sn[1]) << 16);
+          o[1] = (uint32_t)f2bf(v[2] * sx * sn[2]) | ((uint32_t)f2bf(v[3] * sx * sn[3]) << 16);
+          if (m < M) *reinterpret_cast<u32x2_t*>(cb + (int64_t)m * ldc + 16 * j2) = o;
+        }
+      }
+#pragma unroll
+      for (int i2 = 0; i2 < 8; ++i2)
+#pragma unroll
+        for (int j2 = 0; j2 < 8; ++j2) acc[i2][j2] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+      __builtin_amdgcn_sched_barrier(0);
+      asm volatile("s_nop 4" ::: "memory");  // v_accvgpr_write -> MFMA srcC
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+}
+
 }  // namespace
 
 extern "C" int64_t llmd_pgemm_fp8_ws_bytes(int M, int N, int K, int epi) {
@@ -327,13 +514,19 @@ extern "C" int64_t llmd_pgemm_fp8_ws_bytes(int M, int N, int K, int epi) {
 // epi 0: C [M, N]; epi 3: C [M, N / 2] = silu(gate) * up on W = [gate; up] ([N, K], N / 2 % 128 == 0)
 extern "C" int llmd_pgemm_fp8(const void* A, int64_t lda, const float* xs, const void* W, int64_t ldw,
                               const float* ws, void* C, int64_t ldc, int M, int N, int K, int epi, void* wsp,
-                              hipStream_t st) {
+                              int persistent, hipStream_t st) {
   if (M <= 0) return 0;
   if (N % P8_BN || K % P8_BK || lda % 16 || ldw % 16 || ldc % 8) return -1;
   if (epi != P8_EPI_NONE && epi != P8_EPI_SILU_STD) return -3;
   if (epi == P8_EPI_SILU_STD && (N / 2) % 128) return -3;
   if ((int64_t)(M - 1) * lda + K > 0x7fffffffLL || (int64_t)(N - 1) * ldw + K > 0x7fffffffLL) return -2;
   int full = ((M + P8_BM - 1) / P8_BM) * (N / P8_BN), tail = 0, nsplit = 1;
+  if (persistent && epi == P8_EPI_NONE) {
+    if ((int64_t)M * 4 > 0x7fffffffLL || (K / P8_BK) % 2) return -2;
+    hipLaunchKernelGGL(pgemm8p_kernel, dim3(std::min(full, P8_CUS)), dim3(P8_NT), 0, st, (const uint8_t*)A, lda, xs,
+                       (const uint8_t*)W, ldw, ws, (uint16_t*)C, ldc, M, N, K, full);
+    return (int)hipGetLastError();
+  }
   if (wsp != nullptr) pgemm8_plan(M, N, K, epi, full, tail, nsplit);
   const auto* a = (const uint8_t*)A;
   const auto* w = (const uint8_t*)W;

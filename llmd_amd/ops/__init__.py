@@ -525,16 +525,17 @@ def _fp8_gemm(xq, xs, wq, w_scale, bias):
 
 
 def pgemm_fp8(xq: torch.Tensor, xs: torch.Tensor, wq: torch.Tensor, ws: torch.Tensor, epi: int = 0,
-              out: Optional[torch.Tensor] = None, split_k: bool = True) -> torch.Tensor:
+              out: Optional[torch.Tensor] = None, split_k: bool = True, persistent: bool = False) -> torch.Tensor:
     """Prefill fp8 W8A8 GEMM (csrc/ops/pgemm8.hip): (xs . xq) (ws . wq)^T in bf16,
     per-token xs [M(, 1)] and per-channel ws [(1, )N] fp32 scales; epi 3 =
     silu(gate) * up on wq = [gate; up] (output [M, N / 2]). N % 256 == 0,
     K % 128 == 0; ``split_k`` runs a last wave at most half full split over K
-    (fp32 partials + a reduce). Fails loudly without the native library."""
+    (fp32 partials + a reduce); ``persistent`` (epi 0) walks the tiles as one K-step stream per
+    workgroup (no per-tile prologue wait). Fails loudly without the native library."""
     M, N = xq.shape[0], wq.shape[0]
     if out is None:
         out = torch.empty(M, N // 2 if epi == 3 else N, dtype=torch.bfloat16, device=xq.device)
-    native().pgemm_fp8(out, xq, xs, wq, ws, epi, split_k)
+    native().pgemm_fp8(out, xq, xs, wq, ws, epi, split_k, persistent)
     return out
 
 

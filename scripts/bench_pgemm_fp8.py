@@ -52,17 +52,24 @@ def main():
             rel = ((y1.float() - y2.float()).abs().max() / y2.float().abs().max()).item()
             t1 = timeit(lambda: ops.pgemm_fp8(xq, xs, wq, ws, out=y1))
             t2 = timeit(lambda: torch._scaled_mm(xq, wq.t(), scale_a=xs, scale_b=ws, out_dtype=torch.bfloat16))
+            yp = ops.pgemm_fp8(xq, xs, wq, ws, persistent=True)
+            relp = ((yp.float() - y2.float()).abs().max() / y2.float().abs().max()).item()
+            t3 = timeit(lambda: ops.pgemm_fp8(xq, xs, wq, ws, out=yp, persistent=True))
             tot["pgemm8"] += t1
             tot["scaled_mm"] += t2
+            tot["persistent"] = tot.get("persistent", 0.0) + t3
             line = (f"M={M:5d} {name:8s} N={N:5d} K={K:5d}: pgemm8 {t1:8.1f} us {flops / t1 / 1e6:6.0f} TF/s | "
-                    f"scaled_mm {t2:8.1f} us {flops / t2 / 1e6:6.0f} TF/s | speedup {t2 / t1:5.3f} | max rel diff {rel:.2e}")
+                    f"persistent {t3:8.1f} us {flops / t3 / 1e6:6.0f} TF/s | "
+                    f"scaled_mm {t2:8.1f} us {flops / t2 / 1e6:6.0f} TF/s | speedup {t2 / min(t1, t3):5.3f} | "
+                    f"max rel diff {max(rel, relp):.2e}")
             print(line, flush=True)
             if a.power:  # arm() prints: us, TF/s, sclk, package power, TF/s per GHz
                 arm(f"  pgemm8 M={M} {name}", lambda: ops.pgemm_fp8(xq, xs, wq, ws, out=y1), flops, secs=3.0)
                 arm(f"  scaled_mm M={M} {name}", lambda: torch._scaled_mm(
                     xq, wq.t(), scale_a=xs, scale_b=ws, out_dtype=torch.bfloat16), flops, secs=3.0)
             del wq, ws, y1, y2
-    print(f"total: pgemm8 {tot['pgemm8']:.0f} us, scaled_mm {tot['scaled_mm']:.0f} us", flush=True)
+    print(f"total: pgemm8 {tot['pgemm8']:.0f} us, persistent {tot.get('persistent', 0):.0f} us, "
+          f"scaled_mm {tot['scaled_mm']:.0f} us", flush=True)
 
 
 if __name__ == "__main__":

@@ -78,3 +78,18 @@ def test_pgemm_fp8_split_k_tail(M, N, K):
     for y in (y0, y1):
         err = (y.float() - r).abs().max().item()
         assert err <= 1e-2 * r.abs().max().item() + 1e-3, err
+
+
+@pytest.mark.parametrize("M,N,K", [(1030, 16384, 256), (300, 1024, 2048), (2100, 8192, 512)])
+def test_pgemm_fp8_persistent(M, N, K):
+    """Persistent form: tiles walked as one K-step stream per workgroup (more tiles than
+    workgroups in the first and last shapes), epilogue from the accumulators with the
+    LDS-staged scales; same result as the oracle."""
+    g = torch.Generator(device="cuda").manual_seed(N + K)
+    xq, xs = _q((M, K), g)
+    wq, ws = ops.quant_fp8_weight(torch.randn(N, K, generator=g, device="cuda") * 0.05)
+    y = ops.pgemm_fp8(xq, xs, wq, ws, persistent=True)
+    r = _ref(xq, xs, wq, ws)
+    torch.cuda.synchronize()
+    err = (y.float() - r).abs().max().item()
+    assert err <= 1e-2 * r.abs().max().item() + 1e-3, err
