@@ -480,7 +480,7 @@ int64_t mla_v2_shape(int64_t R, bool fp8) { return llmd_mla_v2_shape((int)R, fp8
 
 bool skinny_supported(int64_t M, int64_t rb, int64_t occ) { return llmd_dgemm_supported((int)M, (int)rb, (int)occ); }
 
-// y [M, N] = x [M, K] . w [N, K]^T for 33 <= M <= 128 (decode batches of a P/D
+// y [M, N] = x [M, K] . w [N, K]^T for 33 <= M <= 256 (decode batches of a P/D
 // decode replica): LDS-DMA staged tiles of 64 wrb W rows x all M, nsplit-way
 // split-K, 3- or 4-stage ring (csrc/ops/mgemm.hip)
 // Split-K fixup counters of mgemm (csrc/ops/mgemm.hip): per device 256 slabs of 1024 zeroed ints, handed
@@ -514,7 +514,7 @@ void mgemm(torch::Tensor y, torch::Tensor x, torch::Tensor w, int64_t wrb, int64
   CHECK_CUDA(x); CHECK_BF16(x); CHECK_BF16(w); CHECK_BF16(y); CHECK_INNER(x); CHECK_INNER(w); CHECK_INNER(y);
   TORCH_CHECK(x.dim() == 2 && w.dim() == 2 && y.dim() == 2, "mgemm: 2-D operands");
   const int M = x.size(0), K = x.size(1), N = w.size(0);
-  TORCH_CHECK(M >= 1 && M <= 128 && w.size(1) == K && K % 64 == 0, "mgemm: M <= 128, K % 64 == 0");
+  TORCH_CHECK(M >= 1 && M <= 256 && w.size(1) == K && K % 64 == 0, "mgemm: M <= 256, K % 64 == 0");
   TORCH_CHECK(N % 4 == 0 && y.size(0) == M && y.size(1) == N, "mgemm: output shape / N % 4");
   TORCH_CHECK(x.stride(0) % 8 == 0 && w.stride(0) % 8 == 0 && y.stride(0) % 4 == 0, "mgemm: row alignment");
   TORCH_CHECK(llmd_mgemm_lds(M, (int)wrb, (int)stages) > 0, "mgemm: no kernel for wrb=", wrb, " stages=", stages);
@@ -606,7 +606,7 @@ void mgemm_silu(torch::Tensor y, torch::Tensor x, torch::Tensor w, int64_t wrb, 
   CHECK_CUDA(x); CHECK_BF16(x); CHECK_BF16(w); CHECK_BF16(y); CHECK_INNER(x); CHECK_INNER(w); CHECK_INNER(y);
   TORCH_CHECK(x.dim() == 2 && w.dim() == 2 && y.dim() == 2, "mgemm_silu: 2-D operands");
   const int M = x.size(0), K = x.size(1), N = w.size(0);
-  TORCH_CHECK(M >= 1 && M <= 128 && w.size(1) == K && K % 64 == 0 && N % 8 == 0, "mgemm_silu: shapes");
+  TORCH_CHECK(M >= 1 && M <= 256 && w.size(1) == K && K % 64 == 0 && N % 8 == 0, "mgemm_silu: shapes");
   TORCH_CHECK(y.size(0) == M && y.size(1) == N / 2, "mgemm_silu: y [M, N / 2]");
   int rc = llmd_mgemm_silu(x.data_ptr(), x.stride(0), w.data_ptr(), w.stride(0), M, N, K, (int)wrb, (int)stages,
                            y.data_ptr(), y.stride(0), cur_stream());
@@ -623,7 +623,7 @@ void mgemm_fp8(torch::Tensor y, torch::Tensor xq, torch::Tensor xs, torch::Tenso
   CHECK_DT(xs, at::kFloat); CHECK_DT(ws, at::kFloat);
   TORCH_CHECK(xq.dim() == 2 && wq.dim() == 2 && y.dim() == 2, "mgemm_fp8: 2-D operands");
   const int M = xq.size(0), K = xq.size(1), N = wq.size(0);
-  TORCH_CHECK(M >= 1 && M <= 128 && wq.size(1) == K && K % 128 == 0, "mgemm_fp8: M <= 128, K % 128 == 0");
+  TORCH_CHECK(M >= 1 && M <= 256 && wq.size(1) == K && K % 128 == 0, "mgemm_fp8: M <= 256, K % 128 == 0");
   TORCH_CHECK(N % 4 == 0 && y.size(0) == M && y.size(1) == N, "mgemm_fp8: output shape / N % 4");
   TORCH_CHECK(xs.is_contiguous() && xs.numel() == M && ws.is_contiguous() && ws.numel() == N, "mgemm_fp8: scales");
   TORCH_CHECK(reinterpret_cast<uintptr_t>(ws.data_ptr()) % 16 == 0, "mgemm_fp8: 16-B aligned weight scales");

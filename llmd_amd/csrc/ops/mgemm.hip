@@ -429,15 +429,26 @@ __global__ __launch_bounds__(256 * VPT) void mgemm_reduce_norm_kernel(const floa
 typedef void (*mkern_t)(const void*, int64_t, const void*, int64_t, int, int, int, int, uint16_t*, int64_t,
                         float*, const float*, const float*, int*);
 
+// X row blocks (16 rows) of the tile for M rows: 64 / 96 / 128 rows as before, and 192 / 256 (the
+// 129-256-row decode batches: 256 in flight, SURVEY K08 "M <= 256"; only 1- and 2-row-block W
+// tiles fit the LDS with the 32 KB X image of 256 rows)
+__host__ inline int mgemm_mb(int M) { return M <= 64 ? 4 : M <= 96 ? 6 : M <= 128 ? 8 : M <= 192 ? 12 : 16; }
+
 template <int MB, bool F8, int POL>
 mkern_t pick_w(int wrb, int stages) {
-  if (wrb == 1) return stages == 3 ? mgemm_kernel<MB, 1, 3, F8, POL> : mgemm_kernel<MB, 1, 4, F8, POL>;
-  if (wrb == 2) return stages == 3 ? mgemm_kernel<MB, 2, 3, F8, POL> : mgemm_kernel<MB, 2, 4, F8, POL>;
-  if (wrb == 4) {
-    if (stages == 3) return mgemm_kernel<MB, 4, 3, F8, POL>;
-    if constexpr (MB == 4) return mgemm_kernel<MB, 4, 4, F8, POL>;  // 160 KB: the only 4-stage ring of 256-row tiles that fits
+  if constexpr (MB > 8) {  // 192 / 256 rows: W tiles of 64 or 128 rows, 3 stages (4 with 64-row tiles)
+    if (wrb == 1) return stages == 3 ? mgemm_kernel<MB, 1, 3, F8, POL> : mgemm_kernel<MB, 1, 4, F8, POL>;
+    if (wrb == 2 && stages == 3) return mgemm_kernel<MB, 2, 3, F8, POL>;
+    return nullptr;
+  } else {
+    if (wrb == 1) return stages == 3 ? mgemm_kernel<MB, 1, 3, F8, POL> : mgemm_kernel<MB, 1, 4, F8, POL>;
+    if (wrb == 2) return stages == 3 ? mgemm_kernel<MB, 2, 3, F8, POL> : mgemm_kernel<MB, 2, 4, F8, POL>;
+    if (wrb == 4) {
+      if (stages == 3) return mgemm_kernel<MB, 4, 3, F8, POL>;
+      if constexpr (MB == 4) return mgemm_kernel<MB, 4, 4, F8, POL>;  // 160 KB: the only 4-stage ring of 256-row tiles that fits
+    }
+    return nullptr;
   }
-  return nullptr;
 }
 
 // The W stream's LDS-DMA with the nt policy by default (LLMD_MGEMM_NT=0: default policy, for A/B).
@@ -457,6 +468,8 @@ mkern_t pick_m_pol(int mb, int wrb, int stages) {
     case 4: return pick_w<4, F8, POL>(wrb, stages);
     case 6: return pick_w<6, F8, POL>(wrb, stages);
     case 8: return pick_w<8, F8, POL>(wrb, stages);
+    case 12: return pick_w<12, F8, POL>(wrb, stages);
+    case 16: return pick_w<16, F8, POL>(wrb, stages);
   }
   return nullptr;
 }
@@ -468,12 +481,17 @@ mkern_t pick_m(int mb, int wrb, int stages) {
 
 template <int MB, int POL>
 mkern_t pick_act_w(int wrb, int stages) {
-  if (wrb == 2) return stages == 3 ? mgemm_kernel<MB, 2, 3, false, POL, true> : mgemm_kernel<MB, 2, 4, false, POL, true>;
-  if (wrb == 4) {
-    if (stages == 3) return mgemm_kernel<MB, 4, 3, false, POL, true>;
-    if constexpr (MB == 4) return mgemm_kernel<MB, 4, 4, false, POL, true>;
+  if constexpr (MB > 8) {
+    if (wrb == 2 && stages == 3) return mgemm_kernel<MB, 2, 3, false, POL, true>;
+    return nullptr;
+  } else {
+    if (wrb == 2) return stages == 3 ? mgemm_kernel<MB, 2, 3, false, POL, true> : mgemm_kernel<MB, 2, 4, false, POL, true>;
+    if (wrb == 4) {
+      if (stages == 3) return mgemm_kernel<MB, 4, 3, false, POL, true>;
+      if constexpr (MB == 4) return mgemm_kernel<MB, 4, 4, false, POL, true>;
+    }
+    return nullptr;
   }
-  return nullptr;
 }
 
 template <int POL>
@@ -482,6 +500,8 @@ mkern_t pick_act_pol(int mb, int wrb, int stages) {
     case 4: return pick_act_w<4, POL>(wrb, stages);
     case 6: return pick_act_w<6, POL>(wrb, stages);
     case 8: return pick_act_w<8, POL>(wrb, stages);
+    case 12: return pick_act_w<12, POL>(wrb, stages);
+    case 16: return pick_act_w<16, POL>(wrb, stages);
   }
   return nullptr;
 }
@@ -490,8 +510,9 @@ mkern_t pick_act_pol(int mb, int wrb, int stages) {
 
 // LDS bytes of one (M, wrb, stages) configuration; 0 if not instantiated
 extern "C" int llmd_mgemm_lds(int M, int wrb, int stages) {
-  if (M < 1 || M > 128 || (wrb != 1 && wrb != 2 && wrb != 4) || (stages != 3 && stages != 4)) return 0;
-  const int mb = M <= 64 ? 4 : M <= 96 ? 6 : 8;
+  if (M < 1 || M > 256 || (wrb != 1 && wrb != 2 && wrb != 4) || (stages != 3 && stages != 4)) return 0;
+  const int mb = mgemm_mb(M);
+  if (mb > 8 && !(wrb == 1 || (wrb == 2 && stages == 3))) return 0;  // the instantiated 192 / 256-row forms
   const int lds = stages * (64 * wrb * 128 + 16 * mb * 128);
   return lds <= 160 * 1024 ? lds : 0;
 }
@@ -503,9 +524,9 @@ extern "C" int llmd_mgemm_lds(int M, int wrb, int stages) {
 extern "C" int llmd_mgemm(const void* x, int64_t x_stride, const void* w, int64_t w_stride, int M, int N, int K,
                           int wrb, int nsplit, int stages, void* y, int64_t y_stride, float* part, int* cnt,
                           hipStream_t st) {
-  if (M < 1 || M > 128 || K % 64 != 0 || N % 4 != 0 || nsplit < 1 || x_stride % 8 || w_stride % 8) return -1;
+  if (M < 1 || M > 256 || K % 64 != 0 || N % 4 != 0 || nsplit < 1 || x_stride % 8 || w_stride % 8) return -1;
   if (llmd_mgemm_lds(M, wrb, stages) == 0) return -1;
-  const int mb = M <= 64 ? 4 : M <= 96 ? 6 : 8;
+  const int mb = mgemm_mb(M);
   mkern_t k = pick_m<false>(mb, wrb, stages);
   if (k == nullptr) return -2;
   const int nk = K / 64;
@@ -531,7 +552,7 @@ extern "C" int llmd_mgemm_partials(const void* x, int64_t x_stride, const void* 
                                    int K, int wrb, int nsplit, int stages, float* part, hipStream_t st) {
   if (M < 1 || M > 128 || K % 64 != 0 || N % 8 != 0 || nsplit < 2 || x_stride % 8 || w_stride % 8) return -1;
   if (llmd_mgemm_lds(M, wrb, stages) == 0) return -1;
-  const int mb = M <= 64 ? 4 : M <= 96 ? 6 : 8;
+  const int mb = mgemm_mb(M);
   mkern_t k = pick_m<false>(mb, wrb, stages);
   if (k == nullptr) return -2;
   const int nk = K / 64;
@@ -557,7 +578,7 @@ extern "C" int llmd_mgemm_add_rmsnorm(const void* x, int64_t x_stride, const voi
       w_stride % 8 || res_stride % 8 || out_stride % 8)
     return -1;
   if (llmd_mgemm_lds(M, wrb, stages) == 0) return -1;
-  const int mb = M <= 64 ? 4 : M <= 96 ? 6 : 8;
+  const int mb = mgemm_mb(M);
   mkern_t k = pick_m<false>(mb, wrb, stages);
   if (k == nullptr) return -2;
   const int nk = K / 64;
@@ -584,9 +605,9 @@ extern "C" int llmd_mgemm_add_rmsnorm(const void* x, int64_t x_stride, const voi
 extern "C" int llmd_mgemm_fp8(const void* x, int64_t x_stride, const float* xs, const void* w, int64_t w_stride,
                               const float* ws, int M, int N, int K, int wrb, int nsplit, int stages, void* y,
                               int64_t y_stride, float* part, int* cnt, hipStream_t st) {
-  if (M < 1 || M > 128 || K % 128 != 0 || N % 4 != 0 || nsplit < 1 || x_stride % 16 || w_stride % 16) return -1;
+  if (M < 1 || M > 256 || K % 128 != 0 || N % 4 != 0 || nsplit < 1 || x_stride % 16 || w_stride % 16) return -1;
   if (llmd_mgemm_lds(M, wrb, stages) == 0) return -1;
-  const int mb = M <= 64 ? 4 : M <= 96 ? 6 : 8;
+  const int mb = mgemm_mb(M);
   mkern_t k = pick_m<true>(mb, wrb, stages);
   if (k == nullptr) return -2;
   const int nk = K / 128;
@@ -610,10 +631,10 @@ extern "C" int llmd_mgemm_fp8(const void* x, int64_t x_stride, const float* xs, 
 // wrb 2 or 4, whole K per workgroup.
 extern "C" int llmd_mgemm_silu(const void* x, int64_t x_stride, const void* w, int64_t w_stride, int M, int N,
                                int K, int wrb, int stages, void* y, int64_t y_stride, hipStream_t st) {
-  if (M < 1 || M > 128 || K % 64 != 0 || N % 8 != 0 || x_stride % 8 || w_stride % 8 || y_stride % 4) return -1;
+  if (M < 1 || M > 256 || K % 64 != 0 || N % 8 != 0 || x_stride % 8 || w_stride % 8 || y_stride % 4) return -1;
   if ((wrb != 2 && wrb != 4) || llmd_mgemm_lds(M, wrb, stages) == 0) return -1;
   if ((int64_t)N * w_stride >= 0x7fffffffLL) return -2;  // 32-bit DMA offsets from the weight base
-  const int mb = M <= 64 ? 4 : M <= 96 ? 6 : 8;
+  const int mb = mgemm_mb(M);
   mkern_t k = mgemm_nt() ? pick_act_pol<2>(mb, wrb, stages) : pick_act_pol<0>(mb, wrb, stages);
   if (k == nullptr) return -2;
   const int bn = 64 * wrb;

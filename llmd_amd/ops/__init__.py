@@ -988,7 +988,7 @@ def dgemm_choice(M: int, N: int, K: int) -> Optional[tuple[int, int, int]]:
 
 
 def mgemm(x: torch.Tensor, w: torch.Tensor, plan: tuple[int, int, int]) -> torch.Tensor:
-    """Y = X W^T for 33 <= M <= 128 on the LDS-DMA medium-M decode GEMM
+    """Y = X W^T for 33 <= M <= 256 on the LDS-DMA medium-M decode GEMM
     (csrc/ops/mgemm.hip); plan = (wrb: 64-row W tiles per workgroup, nsplit,
     stages)."""
     M, K = x.shape
@@ -1055,16 +1055,18 @@ MGEMM_SILU = os.environ.get("LLMD_MGEMM_SILU", "1") == "1"
 def mgemm_silu_plan(x: torch.Tensor, w: torch.Tensor) -> Optional[tuple[int, int, int]]:
     """The shipped medium-M plan of the [gate; up] GEMM when it runs whole-K tiles of 2 or 4
     W row blocks (the fused form's shape), else None."""
-    if not (MGEMM_SILU and x.dim() == 2 and 33 <= x.shape[0] <= 128 and mgemm_ok(x, w) and w.shape[0] % 8 == 0):
+    if not (MGEMM_SILU and x.dim() == 2 and 33 <= x.shape[0] <= 256 and mgemm_ok(x, w) and w.shape[0] % 8 == 0):
         return None
     plan = mgemm_choice(x.shape[0], w.shape[0], w.shape[1])
     if plan is None or plan[1] != 1 or plan[0] not in (2, 4):
+        return None
+    if x.shape[0] > 128 and (plan[0], plan[2]) != (2, 3):  # the only ACT form of the 192 / 256-row tiles
         return None
     return plan
 
 
 def mgemm_silu(x: torch.Tensor, w: torch.Tensor, plan: tuple[int, int, int]) -> torch.Tensor:
-    """silu(x Wg^T) * (x Wu^T) for w = [gate; up] [2F, K], M 33..128 (csrc/ops/mgemm.hip ACT form)."""
+    """silu(x Wg^T) * (x Wu^T) for w = [gate; up] [2F, K], M 33..256 (csrc/ops/mgemm.hip ACT form)."""
     y = torch.empty(x.shape[0], w.shape[0] // 2, dtype=x.dtype, device=x.device)
     native().mgemm_silu(y, x, w, plan[0], plan[2])
     return y
@@ -1097,14 +1099,16 @@ def mgemm_fp8_choice(M: int, N: int, K: int) -> Optional[tuple[int, int, int]]:
     return None
 
 
-def mgemm_ok(x: torch.Tensor, w: torch.Tensor) -> bool:
+def mgemm_ok(x: torch.Tensor, w: torch.Tensor, max_m: int = 256) -> bool:
+    """Shapes the medium-M kernel takes (plain / fp8 / SiLU forms up to 256 rows; the forms with a
+    fused split-K reduce pass max_m=128)."""
     M = x.shape[0] if x.dim() == 2 else -1
-    return (_gpu(x) and 1 <= M <= 128 and x.shape[1] % 64 == 0 and x.dtype == torch.bfloat16
+    return (_gpu(x) and 1 <= M <= max_m and x.shape[1] % 64 == 0 and x.dtype == torch.bfloat16
             and w.dtype == torch.bfloat16 and w.shape[0] % 4 == 0 and x.stride(-1) == 1 and x.stride(0) % 8 == 0
             and w.is_contiguous())
 
 
-_MGEMM_MS = (64, 96, 128)
+_MGEMM_MS = (64, 96, 128, 192, 256)
 
 
 PGEMM_VARIANT = int(os.environ.get("LLMD_PGEMM_VARIANT", "0"))
@@ -1241,7 +1245,7 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None
             return y if bias is None else y.add_(bias)
     if _SKINNY:
         M = x.shape[0] if x.dim() == 2 else 0
-        if 33 <= M <= 128 and mgemm_ok(x, w):
+        if 33 <= M <= 256 and mgemm_ok(x, w):
             plan = mgemm_choice(M, w.shape[0], w.shape[1])
             if plan is not None:
                 y = mgemm(x, w, plan)

@@ -186,8 +186,9 @@ def test_paged_decode_shared_prefix(Hq, Hkv, D, bs, groups, fp8, variant):
 
 
 
-@pytest.mark.parametrize("M", [33, 64, 100, 128])
-@pytest.mark.parametrize("plan", [(1, 1, 3), (2, 3, 3), (4, 2, 3), (2, 5, 4)])
+@pytest.mark.parametrize("M,plan", [(m, p) for m in (33, 64, 100, 128)
+                                    for p in ((1, 1, 3), (2, 3, 3), (4, 2, 3), (2, 5, 4))] +
+                         [(m, p) for m in (150, 256) for p in ((1, 1, 3), (1, 4, 4), (2, 3, 3))])
 def test_mgemm_fp8(M, plan):
     """fp8 W8A8 medium-M GEMM (per-token x per-channel scales) vs the fp32 reference
     of the dequantised operands, and against hipBLASLt's scaled GEMM."""

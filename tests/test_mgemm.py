@@ -1,5 +1,5 @@
 """Medium-M decode GEMM (csrc/ops/mgemm.hip) against an fp32 PyTorch
-reference: M 33..128 (row clamping, partial token blocks), N not a multiple of
+reference: M 33..256 (row clamping, partial token blocks), N not a multiple of
 the tile (row clamping + dropped rows), K splits that do not divide the k-steps,
 3- and 4-stage rings, split-K partials + reduce, hipGraph capture."""
 import pytest
@@ -12,7 +12,7 @@ def _ref(x, w):
     return (x.float() @ w.float().T)
 
 
-@pytest.mark.parametrize("M", [33, 64, 80, 96, 128])
+@pytest.mark.parametrize("M", [33, 64, 80, 96, 128, 160, 192, 200, 256])
 @pytest.mark.parametrize("N,K", [(640, 1024), (1028, 4160), (8192, 512)])
 def test_mgemm_matches_fp32(M, N, K):
     from llmd_amd import ops
@@ -89,7 +89,7 @@ def test_mgemm_split_fixup_many_launches_two_streams():
         assert (y.float() - ref).abs().max().item() <= 2e-2 * max(1.0, ref.abs().max().item()), (xi, wi)
 
 
-@pytest.mark.parametrize("M", [33, 64, 100, 128])
+@pytest.mark.parametrize("M", [33, 64, 100, 128, 176, 256])
 @pytest.mark.parametrize("F,K", [(1536, 1024), (2004, 2048)])
 def test_mgemm_silu_matches_fp32(M, F, K):
     """The ACT form (SiLU-and-mul in the epilogue on the plain [gate; up] weight) vs fp32:
