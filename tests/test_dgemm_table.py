@@ -34,15 +34,18 @@ def test_mgemm_table_entries_and_buckets():
     from llmd_amd.ops.mgemm_table import MGEMM_TABLE
 
     for (M, N, K), (plan, t_ours, t_other) in MGEMM_TABLE.items():
-        assert M in (64, 96, 128) and K % 64 == 0 and N % 4 == 0
+        assert M in (64, 96, 128, 192, 256) and K % 64 == 0 and N % 4 == 0
         if plan is not None:
             wrb, ns, stages = plan
             assert wrb in (1, 2, 4) and 1 <= ns <= K // 64 and stages in (3, 4)
-            mb = 4 if M <= 64 else 6 if M <= 96 else 8
+            mb = 4 if M <= 64 else 6 if M <= 96 else 8 if M <= 128 else 12 if M <= 192 else 16
             assert stages * (64 * wrb * 128 + 16 * mb * 128) <= 160 * 1024  # LDS of the instantiation
+            if mb > 8:  # the instantiated 192 / 256-row forms
+                assert wrb == 1 or (wrb, stages) == (2, 3)
             assert t_ours < 0.95 * t_other
-    # M 65..96 use the 96 row, 97..128 the 128 row; unmeasured M/shape -> None
+    # M 65..96 use the 96 row, 97..128 the 128 row, 129..192 the 192 row; unmeasured M/shape -> None
     assert ops.mgemm_choice(80, 5120, 8192) == MGEMM_TABLE[(96, 5120, 8192)][0]
     assert ops.mgemm_choice(100, 5120, 8192) == MGEMM_TABLE[(128, 5120, 8192)][0]
-    assert ops.mgemm_choice(129, 5120, 8192) is None
+    assert ops.mgemm_choice(129, 5120, 8192) == MGEMM_TABLE[(192, 5120, 8192)][0]
+    assert ops.mgemm_choice(257, 5120, 8192) is None
     assert ops.mgemm_choice(64, 1234, 4096) is None
