@@ -15,12 +15,14 @@ void register_block_manager(py::module_& m);
 void register_kv_index(py::module_& m);
 void register_gbdt(py::module_& m);
 void register_fs_store(py::module_& m);
+void register_epp_score(py::module_& m);
 
 PYBIND11_EMBEDDED_MODULE(_rt_san, m) {
   register_block_manager(m);
   register_kv_index(m);
   register_gbdt(m);
   register_fs_store(m);
+  register_epp_score(m);
 }
 
 int main(int argc, char** argv) {

@@ -174,9 +174,28 @@ def stress_fs_overwrite(rt, seed=4, keys=3, rounds=300):
     return rounds
 
 
+def stress_epp_score(rt, seed=5, iters=3000):
+    """EPP combine_pick: ragged-free random columns, every picker, n_pick past the candidate count."""
+    rng = random.Random(seed)
+    picks = 0
+    for _ in range(iters):
+        n = rng.randint(0, 40)
+        cols = [[rng.uniform(-1, 2) for _ in range(n)] for _ in range(rng.randint(1, 6))]
+        tot, idx = rt.combine_pick(cols, [rng.uniform(0, 3) for _ in cols], rng.randint(0, 3), rng.randint(0, 2),
+                                   rng.getrandbits(64))
+        assert len(tot) == n and len(set(idx)) == len(idx) and all(0 <= i < n for i in idx)
+        picks += len(idx)
+    try:
+        rt.combine_pick([[1.0, 2.0], [1.0]], [1.0, 1.0], 1, 0, 1)
+        raise AssertionError("ragged columns accepted")
+    except ValueError:
+        pass
+    return picks
+
+
 def run_all(rt):
     return {"bm": stress_block_manager(rt), "kv_index": stress_kv_index(rt), "gbdt_mae": stress_gbdt(rt),
-            "fs": stress_fs_store(rt), "fs_overwrite": stress_fs_overwrite(rt)}
+            "fs": stress_fs_store(rt), "fs_overwrite": stress_fs_overwrite(rt), "epp_score": stress_epp_score(rt)}
 
 
 if __name__ == "__main__":
