@@ -106,6 +106,9 @@ int llmd_moe_gemm4_bf16(const void*, int64_t, int, const int*, const int*, int, 
 int llmd_moe_gemm4_fp8(const void*, int64_t, const float*, int64_t, int, const int*, const int*, int, const void*,
                        int64_t, const float*, int, int, void*, int64_t, int, int, float, float, int, const void*,
                        int64_t, int, hipStream_t);
+int llmd_moe_gemm8_fp8(const void*, int64_t, const float*, int64_t, int, const int*, const int*, const int*, int,
+                       const void*, int64_t, const float*, int, int, void*, int64_t, int, int, float, float, int,
+                       const void*, int64_t, int, hipStream_t);
 int llmd_moe_gemm3_bf16(const void*, int64_t, int, const int*, const int*, int, const void*, int64_t, int, int, void*,
                         int64_t, int, int, float, float, int, const void*, hipStream_t);
 int llmd_symm_alloc(size_t, void**);
@@ -909,12 +912,15 @@ void moe_gemm4(torch::Tensor X, int64_t topk, torch::Tensor sorted_ids, torch::T
   TORCH_CHECK(rc == 0, "moe_gemm4 failed: ", rc);
 }
 
-// block-fp8 grouped GEMM v4 (csrc/ops/moe4.hip) on 256-row expert tiles: power-of-two scales, K % 128 == 0
+// block-fp8 grouped GEMM v4 (csrc/ops/moe4.hip) or v8 (csrc/ops/moe8.hip, version = 8) on 256 / 192-row expert
+// tiles: power-of-two scales, K % 128 == 0
 void moe_gemm4_fp8(torch::Tensor X, torch::Tensor xs, int64_t topk, torch::Tensor sorted_ids,
                    torch::Tensor tile_expert, torch::Tensor W, torch::Tensor ws, torch::Tensor Y, int64_t mode,
                    int64_t act, double alpha, double limit, bool a_rows_are_slots, c10::optional<torch::Tensor> bias,
-                   int64_t tile_m) {
+                   int64_t tile_m, int64_t version, c10::optional<torch::Tensor> total) {
   const c10::hip::OptionalHIPGuard device_guard(dev_of(X));
+  TORCH_CHECK(version == 4 || (version == 8 && total.has_value()),
+              "moe_gemm4_fp8: version 4 (moe4.hip) or 8 (moe8.hip, needs moe_align's total)");
   CHECK_CUDA(X); CHECK_DT(X, at::kFloat8_e4m3fn); CHECK_DT(W, at::kFloat8_e4m3fn); CHECK_BF16(Y);
   CHECK_INNER(X); CHECK_INNER(Y); CHECK_DT(xs, at::kFloat); CHECK_DT(ws, at::kFloat);
   TORCH_CHECK(W.dim() == 3 && W.is_contiguous() && ws.is_contiguous(), "W [E, N, K] / ws contiguous");
@@ -935,11 +941,20 @@ void moe_gemm4_fp8(torch::Tensor X, torch::Tensor xs, int64_t topk, torch::Tenso
     TORCH_CHECK(bias->is_contiguous() && bias->numel() == (int64_t)E * N, "bias [E, N]");
     bp = bias->data_ptr();
   }
-  const int rc = llmd_moe_gemm4_fp8(X.data_ptr(), X.stride(0), xs.data_ptr<float>(), xs.stride(0), topk,
-                                    sorted_ids.data_ptr<int>(), tile_expert.data_ptr<int>(), P / bm, W.data_ptr(),
-                                    W.stride(0), ws.data_ptr<float>(), N, K, Y.data_ptr(), Y.stride(0), mode, act,
-                                    (float)alpha, (float)limit, a_rows_are_slots ? 1 : 0, bp, X.size(0), bm,
-                                    cur_stream());
+  int rc;
+  if (version == 8) {
+    CHECK_CUDA(total.value()); CHECK_DT(total.value(), at::kInt);
+    rc = llmd_moe_gemm8_fp8(X.data_ptr(), X.stride(0), xs.data_ptr<float>(), xs.stride(0), topk,
+                            sorted_ids.data_ptr<int>(), tile_expert.data_ptr<int>(), total->data_ptr<int>(), P / bm,
+                            W.data_ptr(), W.stride(0), ws.data_ptr<float>(), N, K, Y.data_ptr(), Y.stride(0), mode,
+                            act, (float)alpha, (float)limit, a_rows_are_slots ? 1 : 0, bp, X.size(0), bm,
+                            cur_stream());
+  } else {
+    rc = llmd_moe_gemm4_fp8(X.data_ptr(), X.stride(0), xs.data_ptr<float>(), xs.stride(0), topk,
+                            sorted_ids.data_ptr<int>(), tile_expert.data_ptr<int>(), P / bm, W.data_ptr(),
+                            W.stride(0), ws.data_ptr<float>(), N, K, Y.data_ptr(), Y.stride(0), mode, act,
+                            (float)alpha, (float)limit, a_rows_are_slots ? 1 : 0, bp, X.size(0), bm, cur_stream());
+  }
   TORCH_CHECK(rc == 0, "moe_gemm4_fp8 failed: ", rc);
 }
 
@@ -1241,7 +1256,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {  // _C, or _C_debug (llmd_amd/build.p
   m.def("mgemm_silu", &mgemm_silu);
   m.def("moe_gemm4_fp8", &moe_gemm4_fp8, py::arg("X"), py::arg("xs"), py::arg("topk"), py::arg("sorted_ids"),
         py::arg("tile_expert"), py::arg("W"), py::arg("ws"), py::arg("Y"), py::arg("mode"), py::arg("act"),
-        py::arg("alpha"), py::arg("limit"), py::arg("a_rows_are_slots"), py::arg("bias"), py::arg("tile_m") = 256);
+        py::arg("alpha"), py::arg("limit"), py::arg("a_rows_are_slots"), py::arg("bias"), py::arg("tile_m") = 256,
+        py::arg("version") = 4, py::arg("total") = py::none());
   m.def("symm_error", &symm_error);
   m.def("symm_host_err", &symm_host_err);
   m.def("symm_sig_bytes", &llmd_symm_sig_bytes);

@@ -642,6 +642,11 @@ def moe4_tile_rows(n_rows: int, E: int) -> int:
 # scaled 32x32x64 MFMA with the E8M0 block scales as operands): DeepSeek EP8 T=4096 1307 -> 1496 TF/s,
 # gpt-oss T=5120 757 -> 782 (profiles/moe_gemm_v4_r5.txt)
 MOE_FP8_V4 = os.environ.get("LLMD_MOE_FP8_V4", "1") == "1"
+# v8: the persistent form of those tiles (csrc/ops/moe8.hip: one workgroup per CU walks XCD-local
+# tile chunks, the LDS-DMA stream runs across tile edges, epilogue stored from the accumulators)
+# gpt-oss T=5120 gate/up 1053-1069 -> 1175-1191 TF/s, down 993 -> 1140; DeepSeek EP8 T=4096 down 1535 -> 1868
+# (profiles/moe_gemm_v8_r6.txt)
+MOE_FP8_V8 = os.environ.get("LLMD_MOE_FP8_V8", "1") == "1"
 
 
 class Fp8Rows:
@@ -724,10 +729,13 @@ def moe_experts_fp8(x, ids, wts, w1q, w1s, w2q, w2s, act=0, alpha=1.702, limit=7
     elif v4:
         # v4: PGR2 4-wave tiles, A rows and their act scales gathered by the LDS-DMA (csrc/ops/moe4.hip)
         h = torch.empty(max_p, F, dtype=torch.bfloat16, device=dev)
-        C.moe_gemm4_fp8(xq, xs, k, sorted_ids, tile_e, w1q, w1s, h, 1, act, alpha, limit, False, b1, bm)
+        # v8: the persistent form (K-step stream across tiles, epilogue from registers; >= 4 K-steps)
+        v1 = 8 if MOE_FP8_V8 and Kp1 >= 512 else 4
+        v2 = 8 if MOE_FP8_V8 and Kp2 >= 512 else 4
+        C.moe_gemm4_fp8(xq, xs, k, sorted_ids, tile_e, w1q, w1s, h, 1, act, alpha, limit, False, b1, bm, v1, total)
         hq, hs = _quant_groups_padded(h, Kp2, total)  # slots past the last real tile are never read
         y = torch.empty(max_p, d, dtype=torch.bfloat16, device=dev)
-        C.moe_gemm4_fp8(hq, hs, 1, sorted_ids, tile_e, w2q, w2s, y, 0, 0, 0.0, 0.0, True, b2, bm)
+        C.moe_gemm4_fp8(hq, hs, 1, sorted_ids, tile_e, w2q, w2s, y, 0, 0, 0.0, 0.0, True, b2, bm, v2, total)
         if out is None:
             out = torch.empty(T, d, dtype=torch.bfloat16, device=dev)
         C.moe_combine(y, inv, wts.contiguous().view(-1).float(), k, out)

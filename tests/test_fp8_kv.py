@@ -316,6 +316,93 @@ def test_moe_fp8_v4_gpu(T, E, k, d, F, act, skew, tile, monkeypatch):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("T,E,k,d,F,act,skew", [(512, 4, 4, 1024, 1024, 2, False), (600, 16, 8, 1024, 256, 0, True),
+                                                (800, 16, 4, 2880, 2880, 2, False), (300, 8, 8, 7168, 2048, 0, True),
+                                                (5, 8, 2, 256, 128, 0, False)])
+@pytest.mark.parametrize("tile", ["256", "192"])
+def test_moe_fp8_v8_gpu(T, E, k, d, F, act, skew, tile, monkeypatch):
+    """The v8 block-fp8 grouped GEMM (csrc/ops/moe8.hip: v4's tile loop made persistent - the
+    LDS-DMA stream crosses tile edges, the epilogue stores from the accumulators) vs the v4 kernel on
+    the same tiles and the CPU reference: gpt-oss widths (partial column tiles, a 2880 = 22.5 x 128 N),
+    K = 7168 (56 k-blocks), empty and multi-tile experts, biases, both tile heights."""
+    torch.manual_seed(3)
+    dev = "cuda"
+    c128 = lambda n: (n + 127) // 128 * 128  # noqa: E731
+    x = torch.randn(T, d, device=dev, dtype=torch.bfloat16)
+    w1q, w1s = ops.quant_fp8_block_weight(torch.randn(E, 2 * F, d, device=dev, dtype=torch.bfloat16) * 0.03)
+    w2q, w2s = ops.quant_fp8_block_weight(torch.randn(E, d, F, device=dev, dtype=torch.bfloat16) * 0.03)
+    b1 = torch.randn(E, 2 * F, device=dev, dtype=torch.bfloat16) * 0.1
+    b2 = torch.randn(E, d, device=dev, dtype=torch.bfloat16) * 0.1
+    w1q, w2q = ops.pad_fp8_k(w1q, c128(d)), ops.pad_fp8_k(w2q, c128(F))
+    logits = torch.randn(T, E, device=dev)
+    if skew:
+        logits[:, : E // 4] += 2.0
+        logits[:, -2:] -= 8.0
+    ids, wts = ops.moe_topk(logits, k, scoring=0)
+    monkeypatch.setattr(ops, "MOE_V3", True)
+    monkeypatch.setattr(ops, "MOE_V3_MIN_ROWS", 0)
+    monkeypatch.setattr(ops, "MOE_FUSED_QUANT", False)
+    monkeypatch.setattr(ops, "MOE_FP8_V4", True)
+    monkeypatch.setattr(ops, "MOE4_TILE", tile)
+    monkeypatch.setattr(ops, "MOE_FP8_V8", False)
+    y4 = ops.moe_experts_fp8(x, ids, wts, w1q, w1s, w2q, w2s, act, b1=b1, b2=b2)
+    monkeypatch.setattr(ops, "MOE_FP8_V8", True)
+    y8 = ops.moe_experts_fp8(x, ids, wts, w1q, w1s, w2q, w2s, act, b1=b1, b2=b2)
+    r = ops.moe_experts_fp8(x.cpu(), ids.cpu(), wts.cpu(), w1q.cpu()[..., :d], w1s.cpu(), w2q.cpu()[..., :F],
+                            w2s.cpu(), act, b1=b1.cpu(), b2=b2.cpu())
+    m = r.float().abs().max().item()
+    assert torch.isfinite(y8).all()
+    assert (y8.float().cpu() - r.float()).abs().max().item() < 0.06 * m + 1e-3
+    assert (y8.float() - y4.float()).abs().max().item() < 0.02 * m + 1e-3
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", [0, 1])
+@pytest.mark.parametrize("tile", [256, 192])
+def test_moe_gemm8_fp8_kernel_matches_fp32(mode, tile):
+    """One v8 grouped GEMM on its own against the fp32 PyTorch oracle of the same op (dequantised
+    operands, gathered rows, expert bias, gpt-oss activation in mode 1); padding slots stay unwritten."""
+    torch.manual_seed(5)
+    dev = "cuda"
+    C = ops.native()
+    T, E, k, K, N = 400, 8, 4, 2944, 5760 if mode == 1 else 2880
+    x = torch.randn(T, K, device=dev, dtype=torch.bfloat16)
+    xq, xs = ops._quant_groups_padded(x, K)
+    wq, ws = ops.quant_fp8_block_weight(torch.randn(E, N, K, device=dev, dtype=torch.bfloat16) * 0.03)
+    bias = torch.randn(E, N, device=dev, dtype=torch.bfloat16) * 0.1
+    ids, _ = ops.moe_topk(torch.randn(T, E, device=dev), k, scoring=0)
+    n = T * k
+    max_p = ((n + E * (tile - 1)) + tile - 1) // tile * tile
+    sorted_ids = torch.empty(max_p, dtype=torch.int32, device=dev)
+    tile_e = torch.empty(max_p // tile, dtype=torch.int32, device=dev)
+    offs = torch.empty(E + 1, dtype=torch.int32, device=dev)
+    total = torch.empty(1, dtype=torch.int32, device=dev)
+    inv = torch.empty(n, dtype=torch.int32, device=dev)
+    C.moe_align(ids.contiguous().view(-1).to(torch.int32), E, sorted_ids, tile_e, offs, total, inv, tile)
+    width = N // 2 if mode == 1 else N
+    y = torch.full((max_p, width), 7.0, device=dev, dtype=torch.bfloat16)
+    C.moe_gemm4_fp8(xq, xs, k, sorted_ids, tile_e, wq, ws, y, mode, 2, 1.702, 7.0, False, bias, tile, 8, total)
+    torch.cuda.synchronize()
+    xd = xq.float() * xs.repeat_interleave(128, 1)[:, :K]
+    wd = ops.dequant_fp8_block_weight(wq, ws).float()
+    sid = sorted_ids.long()
+    live = sid >= 0
+    te = tile_e.long().repeat_interleave(tile)[:max_p]
+    ref = torch.zeros(max_p, N, device=dev)
+    for e in range(E):
+        rows = live & (te == e)
+        if rows.any():
+            ref[rows] = xd[sid[rows] // k] @ wd[e].T + bias[e].float()
+    if mode == 1:
+        g, u = ref[:, 0::2].clamp(max=7.0), ref[:, 1::2].clamp(-7.0, 7.0)
+        ref = (u + 1) * g * torch.sigmoid(1.702 * g)
+    got = y.float()
+    m = ref[live].abs().max().item()
+    assert (got[live] - ref[live]).abs().max().item() < 0.01 * m + 1e-2
+    assert (got[~live] == 7.0).all()
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("T,E,k,d,F,act", [(700, 16, 4, 512, 2880, 2), (300, 8, 8, 256, 256, 0)])
 def test_moe_fp8_fused_act_quant_gpu(T, E, k, d, F, act):
     """The 256-row first GEMM's fused epilogue quantisation (hq / hs) is bit
