@@ -619,7 +619,10 @@ def dequant_fp8_block_weight(q: torch.Tensor, s: torch.Tensor, block: int = 128)
     return q.float() * full
 
 
-MOE_V3_MIN_ROWS = int(os.environ.get("LLMD_MOE_V3_MIN_ROWS", "96"))
+# rows per local expert from which the tile GEMMs (v4 bf16 / v8 fp8) replace the 64-row streaming kernels:
+# they win from 64 rows on (gpt-oss 1.21-1.25x, DeepSeek EP8 1.29-1.35x) and lose at <= 48
+# (profiles/moe_tile_threshold_r6.txt)
+MOE_V3_MIN_ROWS = int(os.environ.get("LLMD_MOE_V3_MIN_ROWS", "56"))
 MOE_V3 = os.environ.get("LLMD_MOE_V3", "1") == "1"
 # bf16 experts on the same 256-row tiles (moe_gemm3 with bf16 operands); LLMD_MOE_V3_BF16=0 keeps v2
 MOE_V3_BF16 = os.environ.get("LLMD_MOE_V3_BF16", "1") == "1"  # DeepSeek EP8 T=4096 701 -> 789 TF/s, gpt-oss T=5120 369 -> 529
