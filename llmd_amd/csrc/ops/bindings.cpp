@@ -103,6 +103,8 @@ int llmd_moe_gemm3_fp8(const void*, int64_t, const float*, int64_t, int, const i
 int llmd_moe_gemm3_tile_m();
 int llmd_moe_gemm4_bf16(const void*, int64_t, int, const int*, const int*, int, const void*, int64_t, int, int, void*,
                         int64_t, int, int, float, float, int, const void*, int64_t, int, hipStream_t);
+int llmd_moe_gemm8_bf16(const void*, int64_t, int, const int*, const int*, const int*, int, const void*, int64_t, int,
+                        int, void*, int64_t, int, int, float, float, int, const void*, int64_t, int, hipStream_t);
 int llmd_moe_gemm4_fp8(const void*, int64_t, const float*, int64_t, int, const int*, const int*, int, const void*,
                        int64_t, const float*, int, int, void*, int64_t, int, int, float, float, int, const void*,
                        int64_t, int, hipStream_t);
@@ -887,8 +889,10 @@ void moe_gemm(torch::Tensor X, int64_t topk, torch::Tensor sorted_ids, torch::Te
 // bf16 grouped GEMM v4 (csrc/ops/moe4.hip) on the 256-row expert tiles of moe_align(bm = 256)
 void moe_gemm4(torch::Tensor X, int64_t topk, torch::Tensor sorted_ids, torch::Tensor tile_expert, torch::Tensor W,
                torch::Tensor Y, int64_t mode, int64_t act, double alpha, double limit, bool a_rows_are_slots,
-               c10::optional<torch::Tensor> bias, int64_t tile_m) {
+               c10::optional<torch::Tensor> bias, int64_t tile_m, int64_t version, c10::optional<torch::Tensor> total) {
   const c10::hip::OptionalHIPGuard device_guard(dev_of(X));
+  TORCH_CHECK(version == 4 || (version == 8 && total.has_value()),
+              "moe_gemm4: version 4 (moe4.hip) or 8 (moe8.hip, needs moe_align's total)");
   CHECK_CUDA(X); CHECK_BF16(X); CHECK_BF16(W); CHECK_BF16(Y); CHECK_INNER(X); CHECK_INNER(Y);
   TORCH_CHECK(W.dim() == 3 && W.is_contiguous(), "W [E, N, K] contiguous");
   const int N = W.size(1), K = W.size(2);
@@ -905,10 +909,18 @@ void moe_gemm4(torch::Tensor X, int64_t topk, torch::Tensor sorted_ids, torch::T
     TORCH_CHECK(bias->is_contiguous() && bias->numel() == (int64_t)W.size(0) * N, "bias [E, N]");
     bp = bias->data_ptr();
   }
-  const int rc = llmd_moe_gemm4_bf16(X.data_ptr(), X.stride(0), topk, sorted_ids.data_ptr<int>(),
-                                     tile_expert.data_ptr<int>(), P / bm, W.data_ptr(), W.stride(0), N, K,
-                                     Y.data_ptr(), Y.stride(0), mode, act, (float)alpha, (float)limit,
-                                     a_rows_are_slots ? 1 : 0, bp, X.size(0), bm, cur_stream());
+  int rc;
+  if (version == 8) {
+    CHECK_CUDA(total.value()); CHECK_DT(total.value(), at::kInt);
+    rc = llmd_moe_gemm8_bf16(X.data_ptr(), X.stride(0), topk, sorted_ids.data_ptr<int>(), tile_expert.data_ptr<int>(),
+                             total->data_ptr<int>(), P / bm, W.data_ptr(), W.stride(0), N, K, Y.data_ptr(),
+                             Y.stride(0), mode, act, (float)alpha, (float)limit, a_rows_are_slots ? 1 : 0, bp,
+                             X.size(0), bm, cur_stream());
+  } else {
+    rc = llmd_moe_gemm4_bf16(X.data_ptr(), X.stride(0), topk, sorted_ids.data_ptr<int>(), tile_expert.data_ptr<int>(),
+                             P / bm, W.data_ptr(), W.stride(0), N, K, Y.data_ptr(), Y.stride(0), mode, act,
+                             (float)alpha, (float)limit, a_rows_are_slots ? 1 : 0, bp, X.size(0), bm, cur_stream());
+  }
   TORCH_CHECK(rc == 0, "moe_gemm4 failed: ", rc);
 }
 
@@ -1252,7 +1264,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {  // _C, or _C_debug (llmd_amd/build.p
   m.def("symm_alloc", &symm_alloc);
   m.def("moe_gemm4", &moe_gemm4, py::arg("X"), py::arg("topk"), py::arg("sorted_ids"), py::arg("tile_expert"),
         py::arg("W"), py::arg("Y"), py::arg("mode"), py::arg("act"), py::arg("alpha"), py::arg("limit"),
-        py::arg("a_rows_are_slots"), py::arg("bias"), py::arg("tile_m") = 256);
+        py::arg("a_rows_are_slots"), py::arg("bias"), py::arg("tile_m") = 256, py::arg("version") = 4,
+        py::arg("total") = py::none());
   m.def("mgemm_silu", &mgemm_silu);
   m.def("moe_gemm4_fp8", &moe_gemm4_fp8, py::arg("X"), py::arg("xs"), py::arg("topk"), py::arg("sorted_ids"),
         py::arg("tile_expert"), py::arg("W"), py::arg("ws"), py::arg("Y"), py::arg("mode"), py::arg("act"),

@@ -61,6 +61,10 @@ __device__ __forceinline__ void p8_mfma(f32x16_t& acc, const i32x8_t& a, const i
                : "+a"(acc) : "v"(a), "v"(b), "v"(sa), "v"(sb));
 }
 
+__device__ __forceinline__ void m4b_mfma(f32x4_t& acc, const s16x8_t& a, const s16x8_t& b) {
+  asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(a), "v"(b));
+}
+
 __device__ __forceinline__ float p8_act(float g, float u, int act, float alpha, float limit) {
   if (act == 2) {  // gpt-oss: clamp, (u + 1) * g * sigmoid(alpha * g)
     g = fminf(g, limit);
@@ -409,6 +413,290 @@ __global__ __launch_bounds__(P8_NT, 1) void moe_gemm8_fp8_kernel(
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
 }
 
+
+// bf16 form: the v4 bf16 tile loop (moe4.hip moe_gemm4_bf16_kernel: 16x16x32 bf16 MFMA, 64-deep
+// K-steps, MI = TBM / 32 A fragments per wave, NPC = MI + 8 DMA pieces per wave and step) in the
+// same persistent frame. No scales; the side DMA is the bias only (waves 2 / 3). Epilogue layout:
+// acc[i][j][r] = C[m][n], m = wr*TBM/2 + 16 i + (lane & 15), n = wc*128 + 16 j + 4 (lane >> 4) + r;
+// lanes l and l ^ 16 exchange one column group so a lane holds 8 consecutive columns.
+template <int MODE, int TBM>
+__global__ __launch_bounds__(P8_NT, 1) void moe_gemm8_bf16_kernel(
+    const uint16_t* __restrict__ X, int64_t x_stride, int topk, const int* __restrict__ sorted_ids,
+    const int* __restrict__ tile_expert, const int* __restrict__ total_p, int max_mtiles, int ntn, int order,
+    const uint16_t* __restrict__ W, int64_t w_expert_stride, int N, int K, uint16_t* __restrict__ Y,
+    int64_t y_stride, int act, float alpha, float limit, int a_rows_are_slots, const uint16_t* __restrict__ bias) {
+  static_assert(TBM == 256 || TBM == 192, "tile rows");
+  constexpr int MI = TBM / 32;             // 16-row A fragments per wave (8 / 6)
+  constexpr int OPA = TBM * 128;           // A bytes per K-step (64 bf16 per row)
+  constexpr int BUF = OPA + P8_OPB;        // A | W of one K-step
+  constexpr int BSO = 2 * BUF;             // bias [2 tile slots][256 columns] bf16
+  constexpr int LDSB = BSO + 2 * 512;
+  constexpr int NPC = MI + 8;              // DMA pieces per wave per K-step (= fragment reads per half)
+  constexpr int NMF = 8 * MI;              // MFMAs per half
+  constexpr int TB = 8 * MI - 24;          // half 0: barrier MFMA index (A pieces of step kt + 2 after it)
+  constexpr int WP = MI == 8 ? 5 : 4;      // half 1: one W piece every WP MFMAs
+  constexpr int RB = MI == 8 ? 37 : 30;    // half 1: first next-step read
+  constexpr int NQ = TBM / 64;
+  static_assert(TB + 1 + 3 * (MI - 1) < NMF && 8 + MI <= TB && 7 * WP < RB - 1 && RB + NPC <= NMF, "schedule");
+  __shared__ __attribute__((aligned(1024))) char lds[LDSB];  // the ONLY LDS object
+
+  const int nk = K / 64;
+  const int n_items = min(__builtin_amdgcn_readfirstlane(total_p[0]) / TBM, max_mtiles) * ntn;
+  const int xcd = blockIdx.x & 7;
+  const int S = order ? (int)gridDim.x : (int)(gridDim.x >> 3);
+  const int c0 = order ? 0 : (int)((int64_t)n_items * xcd / 8);
+  const int c1 = order ? n_items : (int)((int64_t)n_items * (xcd + 1) / 8);
+  int item = c0 + (int)(order ? blockIdx.x : blockIdx.x >> 3);
+  if (item >= c1) return;
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = w >> 1, wc = w & 1;
+  const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc((void*)X, 0, 0x7fffffff, 0x00020000);
+
+  int m0 = 0, n0 = 0, e = 0, nvalid = 0;
+  __amdgpu_buffer_rsrc_t rw;
+  uint32_t va[8], vw[8];
+  int sid_a[8], sid_v[4], e_ld;
+  auto meta_load = [&](int it) {
+    const int mm = (it / ntn) * TBM;
+    e_ld = tile_expert[it / ntn];
+#pragma unroll
+    for (int j = 0; j < MI; ++j) sid_a[j] = sorted_ids[mm + 8 * (MI * w + j) + (lane >> 3)];
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) sid_v[q] = sorted_ids[mm + 64 * q + lane];
+  };
+  auto build = [&](int it) {
+    const int mt = it / ntn;
+    m0 = mt * TBM;
+    n0 = (it - mt * ntn) * P8_BN;
+    e = __builtin_amdgcn_readfirstlane(e_ld);
+    int nv = 0;
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) nv += __popcll(__ballot(sid_v[q] >= 0));
+    nvalid = __builtin_amdgcn_readfirstlane(nv);
+    if (e < 0) {
+      e = 0;
+      nvalid = 0;
+    }
+    rw = __builtin_amdgcn_make_buffer_rsrc((void*)(W + (int64_t)e * w_expert_stride), 0, 0x7fffffff, 0x00020000);
+#pragma unroll
+    for (int j = 0; j < MI; ++j) {
+      const int row = 8 * (MI * w + j) + (lane >> 3);
+      const int c = (lane & 7) ^ ((row >> 1) & 7);
+      const int sid = sid_a[j];
+      const int tok = a_rows_are_slots ? m0 + row : sid / topk;
+      va[j] = sid < 0 || nvalid == 0 ? P8_OOB : (uint32_t)(((int64_t)tok * x_stride + c * 8) * 2);
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int row = 64 * w + 8 * j + (lane >> 3);
+      const int c = (lane & 7) ^ ((row >> 1) & 7);
+      vw[j] = n0 + row < N ? (uint32_t)(((int64_t)(n0 + row) * K + c * 8) * 2) : P8_OOB;
+    }
+  };
+  auto side_dma = [&](int sl) {  // bias columns n0 + 128 (w - 2) + [0, 128) (waves 2 / 3)
+    if (w >= 2 && bias != nullptr) {
+      const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc(
+          (void*)(bias + (int64_t)e * N), 0, (uint32_t)N * 2, 0x00020000);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(
+          rb, (__attribute__((address_space(3))) void*)(lds + BSO + sl * 512 + (w - 2) * 256), 4,
+          (uint32_t)((n0 + 128 * (w - 2) + 2 * lane) * 2), 0, 0, 0);
+    }
+  };
+  auto dma = [&](int bsel, int kc, int j, bool wop) {
+    char* dst = lds + bsel * BUF + (wop ? OPA + (8 * w + j) * 1024 : (MI * w + j) * 1024);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(wop ? rw : ra, (__attribute__((address_space(3))) void*)dst, 16,
+                                             wop ? vw[j] : va[j], (uint32_t)(kc * 128), 0, 0);
+  };
+  const int fr = lane & 15, fq = lane >> 4;
+  const int rd0 = fr * 128 + ((fq ^ ((fr >> 1) & 7)) * 16);
+  const int rd1 = fr * 128 + (((4 + fq) ^ ((fr >> 1) & 7)) * 16);
+  const int a_rd = (wr * (TBM / 2)) * 128, w_rd = OPA + (wc * 128) * 128;
+
+  f32x4_t acc[MI][8];
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  s16x8_t fa0[MI], fw0[8], fa1[MI], fw1[8];
+
+  meta_load(item);
+  build(item);
+  int slot = 0;
+  side_dma(0);
+#pragma unroll
+  for (int s2 = 0; s2 < 2; ++s2) {
+#pragma unroll
+    for (int j = 0; j < MI; ++j) dma(s2, s2, j, false);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) dma(s2, s2, j, true);
+  }
+  if constexpr (NPC == 16) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+  else asm volatile("s_waitcnt vmcnt(14)" ::: "memory");
+  p8_bar();
+  fa0[0] = *reinterpret_cast<const s16x8_t*>(lds + a_rd + rd0);
+  __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    fw0[i] = *reinterpret_cast<const s16x8_t*>(lds + w_rd + i * 2048 + rd0);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+#pragma unroll
+  for (int i = 1; i < MI; ++i) {
+    fa0[i] = *reinterpret_cast<const s16x8_t*>(lds + a_rd + i * 2048 + rd0);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  __builtin_amdgcn_s_waitcnt(0xC07F);
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_nop 4" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+
+  int gs = 0;
+  auto step = [&](auto PH_, int kt, int nx) {
+    constexpr int PH = decltype(PH_)::value;  // as the fp8 form
+    const int bsel = gs & 1;
+    const char* cur = lds + bsel * BUF;
+    const char* nxt = lds + (bsel ^ 1) * BUF;
+    const int kc = PH <= 1 ? kt + 2 : PH - 2;
+    if constexpr (PH == 1) meta_load(nx);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int t = 0; t < NMF; ++t) {
+      const int i = t >> 3, j = t & 7;
+      if (t <= 8) __builtin_amdgcn_s_waitcnt(0xC07F | ((NPC - 2) << 8));
+      m4b_mfma(acc[i][j], fw0[j], fa0[i]);
+      if (t == 0) {
+        fa1[0] = *reinterpret_cast<const s16x8_t*>(cur + a_rd + rd1);
+      } else if (t < 9) {
+        fw1[t - 1] = *reinterpret_cast<const s16x8_t*>(cur + w_rd + (t - 1) * 2048 + rd1);
+      } else if (t < 8 + MI) {
+        fa1[t - 8] = *reinterpret_cast<const s16x8_t*>(cur + a_rd + (t - 8) * 2048 + rd1);
+      } else if (t == TB) {
+        __builtin_amdgcn_s_waitcnt(0xC07F);
+        p8_bar();
+        if constexpr (PH == 2) side_dma(slot ^ 1);  // older than this step's DMAs
+      } else if (t > TB && (t - TB - 1) % 3 == 0 && (t - TB - 1) / 3 < MI) {
+        dma(bsel, kc, (t - TB - 1) / 3, false);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+#pragma unroll
+    for (int t = 0; t < NMF; ++t) {
+      const int i = t >> 3, j = t & 7;
+      m4b_mfma(acc[i][j], fw1[j], fa1[i]);
+      if (t < 8 * WP && t % WP == 0) {
+        dma(bsel, kc, t / WP, true);
+      } else if (t == RB - 1) {
+        if constexpr (NPC == 16) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(14)" ::: "memory");
+        p8_bar();
+      } else if (t == RB) {
+        fa0[0] = *reinterpret_cast<const s16x8_t*>(nxt + a_rd + rd0);
+      } else if (t > RB && t < RB + 9) {
+        fw0[t - RB - 1] = *reinterpret_cast<const s16x8_t*>(nxt + w_rd + (t - RB - 1) * 2048 + rd0);
+      } else if (t >= RB + 9 && t < RB + 8 + MI) {
+        fa0[t - RB - 8] = *reinterpret_cast<const s16x8_t*>(nxt + a_rd + (t - RB - 8) * 2048 + rd0);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    if constexpr (PH == 1) build(nx);
+    asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 3" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    ++gs;
+  };
+  while (true) {
+    const int nxt_item = item + S;
+    const bool has_next = nxt_item < c1;
+    const int nx = has_next ? nxt_item : item;
+    const int cm0 = m0, cn0 = n0, cnv = nvalid, cslot = slot;
+    for (int kt = 0; kt < nk - 3; ++kt) step(std::integral_constant<int, 0>{}, kt, nx);
+    step(std::integral_constant<int, 1>{}, nk - 3, nx);
+    step(std::integral_constant<int, 2>{}, nk - 2, nx);
+    step(std::integral_constant<int, 3>{}, nk - 1, nx);
+    asm volatile("s_nop 7\n\ts_nop 7" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+
+    const int ncol0 = cn0 + wc * 128;
+    const char* bl = lds + BSO + cslot * 512 + wc * 256;
+    const int odd = fq & 1;
+#pragma unroll
+    for (int jp = 0; jp < 4; ++jp) {
+      float bv[2][4];
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+        u32x2_t raw = u32x2_t{0u, 0u};
+        if (bias != nullptr) raw = *reinterpret_cast<const u32x2_t*>(bl + (32 * jp + 16 * s2 + 4 * fq) * 2);
+        bv[s2][0] = __uint_as_float(raw[0] << 16);
+        bv[s2][1] = __uint_as_float(raw[0] & 0xffff0000u);
+        bv[s2][2] = __uint_as_float(raw[1] << 16);
+        bv[s2][3] = __uint_as_float(raw[1] & 0xffff0000u);
+      }
+#pragma unroll
+      for (int i = 0; i < MI; ++i) {
+        const int m = wr * (TBM / 2) + 16 * i + fr;
+        const bool live = m < cnv;
+        uint16_t* yrow = Y + (int64_t)(cm0 + m) * y_stride;
+        float v0[4], v1[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          v0[r] = acc[i][2 * jp][r] + bv[0][r];
+          v1[r] = acc[i][2 * jp + 1][r] + bv[1][r];
+        }
+        if constexpr (MODE == 0) {
+          const uint32_t a0 = p8_pack(v0[0], v0[1]), a1 = p8_pack(v0[2], v0[3]);
+          const uint32_t b0 = p8_pack(v1[0], v1[1]), b1 = p8_pack(v1[2], v1[3]);
+          // even fq keeps column block 2 jp (its 4 columns + the partner's 4), odd fq block 2 jp + 1
+          const uint32_t r0 = (uint32_t)__shfl_xor((int)(odd ? a0 : b0), 16, 64);
+          const uint32_t r1 = (uint32_t)__shfl_xor((int)(odd ? a1 : b1), 16, 64);
+          const u32x4_t o = odd ? u32x4_t{r0, r1, b0, b1} : u32x4_t{a0, a1, r0, r1};
+          const int n = ncol0 + 16 * (2 * jp + odd) + 4 * (fq - odd);
+          if (live && n < N) *reinterpret_cast<u32x4_t*>(yrow + n) = o;
+        } else {
+          const uint32_t oa = p8_pack(p8_act(v0[0], v0[1], act, alpha, limit), p8_act(v0[2], v0[3], act, alpha, limit));
+          const uint32_t ob = p8_pack(p8_act(v1[0], v1[1], act, alpha, limit), p8_act(v1[2], v1[3], act, alpha, limit));
+          const uint32_t r = (uint32_t)__shfl_xor((int)(odd ? oa : ob), 16, 64);
+          const u32x2_t o = odd ? u32x2_t{r, ob} : u32x2_t{oa, r};
+          const int hc = ncol0 / 2 + 8 * (2 * jp + odd) + 2 * (fq - odd);
+          if (live && 2 * hc < N) *reinterpret_cast<u32x2_t*>(yrow + hc) = o;
+        }
+      }
+    }
+    if (!has_next) break;
+    item = nxt_item;
+    slot ^= 1;
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_nop 4" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+}
+
+}  // namespace
+
+
+namespace {
+int p8_cus() {
+  static const int n_cu = [] {
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n < 8)
+      return 256;
+    return n;
+  }();
+  return n_cu;
+}
+int p8_order() {  // work-item order (LLMD_MOE8_ORDER: 0 XCD chunks, 1 round-robin)
+  static const int order = [] {
+    const char* v = getenv("LLMD_MOE8_ORDER");
+    return v ? atoi(v) : 0;
+  }();
+  return order;
+}
 }  // namespace
 
 // Same operands as llmd_moe_gemm4_fp8 (moe4.hip) plus total_p: moe_align's padded slot total on
@@ -426,17 +714,8 @@ extern "C" int llmd_moe_gemm8_fp8(const void* X, int64_t x_stride, const float* 
   if (x_rows * x_stride + K > 0x7fffffffLL || (int64_t)N * K > 0x7fffffffLL || x_rows * xs_stride * 4 > 0x7fffffffLL)
     return -2;
   if (num_tiles == 0) return 0;
-  static const int n_cu = [] {
-    int dev = 0, n = 0;
-    if (hipGetDevice(&dev) != hipSuccess ||
-        hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n < 8)
-      return 256;
-    return n;
-  }();
-  static const int order = [] {  // work-item order (LLMD_MOE8_ORDER: 0 XCD chunks, 1 round-robin)
-    const char* v = getenv("LLMD_MOE8_ORDER");
-    return v ? atoi(v) : 0;
-  }();
+  const int n_cu = p8_cus();
+  const int order = p8_order();
   const int ntn = (N + P8_BN - 1) / P8_BN;
   const int64_t upper = (int64_t)num_tiles * ntn;
   const int grid = (int)std::min<int64_t>(n_cu / 8 * 8, (upper + 7) / 8 * 8);  // a multiple of 8 (XCDs)
@@ -452,5 +731,35 @@ extern "C" int llmd_moe_gemm8_fp8(const void* X, int64_t x_stride, const float* 
     if (mode == 0) P8_LAUNCH(0, 192); else P8_LAUNCH(1, 192);
   }
 #undef P8_LAUNCH
+  return (int)hipGetLastError();
+}
+
+// Same operands as llmd_moe_gemm4_bf16 (moe4.hip) plus total_p (see above). K % 64 == 0, K / 64 >= 4.
+extern "C" int llmd_moe_gemm8_bf16(const void* X, int64_t x_stride, int topk, const int* sorted_ids,
+                                   const int* tile_expert, const int* total_p, int num_tiles, const void* W,
+                                   int64_t w_expert_stride, int N, int K, void* Y, int64_t y_stride, int mode, int act,
+                                   float alpha, float limit, int a_rows_are_slots, const void* bias, int64_t x_rows,
+                                   int tile_m, hipStream_t st) {
+  if (K % 64 || K / 64 < 4 || x_stride % 8 || w_expert_stride % 8 || N % 8 || (mode == 1 && N % 16) ||
+      y_stride % 8 || total_p == nullptr)
+    return -1;
+  if (tile_m != 256 && tile_m != 192) return -1;
+  if ((x_rows * x_stride + K) * 2 > 0x7fffffffLL || ((int64_t)N * K) * 2 > 0x7fffffffLL) return -2;
+  if (num_tiles == 0) return 0;
+  const int ntn = (N + P8_BN - 1) / P8_BN;
+  const int64_t upper = (int64_t)num_tiles * ntn;
+  const int grid = (int)std::min<int64_t>(p8_cus() / 8 * 8, (upper + 7) / 8 * 8);
+  const int order = p8_order();
+#define P8B_LAUNCH(MODE_, TBM_)                                                                                    \
+  hipLaunchKernelGGL((moe_gemm8_bf16_kernel<MODE_, TBM_>), dim3(grid), dim3(P8_NT), 0, st, (const uint16_t*)X,     \
+                     x_stride, topk, sorted_ids, tile_expert, total_p, num_tiles, ntn, order, (const uint16_t*)W, \
+                     w_expert_stride, N, K, (uint16_t*)Y, y_stride, act, alpha, limit, a_rows_are_slots,          \
+                     (const uint16_t*)bias)
+  if (tile_m == 256) {
+    if (mode == 0) P8B_LAUNCH(0, 256); else P8B_LAUNCH(1, 256);
+  } else {
+    if (mode == 0) P8B_LAUNCH(0, 192); else P8B_LAUNCH(1, 192);
+  }
+#undef P8B_LAUNCH
   return (int)hipGetLastError();
 }

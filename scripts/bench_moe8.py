@@ -30,8 +30,10 @@ def run(name, T, E, k, d, F, act, tiles):
     C = ops.native()
     c128 = lambda n: (n + 127) // 128 * 128  # noqa: E731
     x = torch.randn(T, d, device=dev, dtype=torch.bfloat16)
-    w1q, w1s = ops.quant_fp8_block_weight(torch.randn(E, 2 * F, d, device=dev, dtype=torch.bfloat16) * 0.02)
-    w2q, w2s = ops.quant_fp8_block_weight(torch.randn(E, d, F, device=dev, dtype=torch.bfloat16) * 0.02)
+    w1 = torch.randn(E, 2 * F, d, device=dev, dtype=torch.bfloat16) * 0.02
+    w2 = torch.randn(E, d, F, device=dev, dtype=torch.bfloat16) * 0.02
+    w1q, w1s = ops.quant_fp8_block_weight(w1)
+    w2q, w2s = ops.quant_fp8_block_weight(w2)
     w1q, w2q = ops.pad_fp8_k(w1q, c128(d)), ops.pad_fp8_k(w2q, c128(F))
     b1 = torch.randn(E, 2 * F, device=dev, dtype=torch.bfloat16) * 0.1 if act == 2 else None
     b2 = torch.randn(E, d, device=dev, dtype=torch.bfloat16) * 0.1 if act == 2 else None
@@ -58,9 +60,11 @@ def run(name, T, E, k, d, F, act, tiles):
                                               tile, ver, total))
             ops.MOE4_TILE, ops.MOE_FP8_V8 = str(tile), ver == 8
             lay = t_it(lambda: ops.moe_experts_fp8(x, ids, wts, w1q, w1s, w2q, w2s, act, b1=b1, b2=b2))
-            row.append(f"v{ver}: gate/up {g1 * 1e3:.3f} ms {f1 / g1 / 1e12:.0f} TF/s, down {g2 * 1e3:.3f} ms "
+            ops.MOE_BF16_V8 = ver == 8
+            b_lay = t_it(lambda: ops.moe_experts(x, ids, wts, w1, w2, act, b1=b1, b2=b2))
+            row.append(f"v{ver}: bf16 layer {b_lay * 1e3:.3f} ms {(f1 + f2) / b_lay / 1e12:.0f} TF/s, fp8 gate/up {g1 * 1e3:.3f} ms {f1 / g1 / 1e12:.0f} TF/s, down {g2 * 1e3:.3f} ms "
                        f"{f2 / g2 / 1e12:.0f} TF/s, layer {lay * 1e3:.3f} ms {(f1 + f2) / lay / 1e12:.0f} TF/s")
-        ops.MOE4_TILE, ops.MOE_FP8_V8 = "auto", False
+        ops.MOE4_TILE, ops.MOE_FP8_V8, ops.MOE_BF16_V8 = "auto", True, False
         print(f"{name} T={T} tile={tile} rows/expert={n / E:.0f}: " + " | ".join(row), flush=True)
 
 

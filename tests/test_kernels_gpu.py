@@ -423,14 +423,17 @@ def test_moe_experts(T, E, k, d, F, act):
     _close(o2, r2, atol=3e-2, rtol=3e-2)
 
 
+@pytest.mark.parametrize("v8", [False, True])
 @pytest.mark.parametrize("tile", ["256", "192"])
 @pytest.mark.parametrize("T,E,k,d,F,act", [(1024, 8, 2, 1024, 512, 0), (800, 16, 4, 2880, 2880, 2),
                                             (2048, 32, 8, 1024, 768, 0)])
-def test_moe_experts_bf16_v4(T, E, k, d, F, act, tile, monkeypatch):
+def test_moe_experts_bf16_v4(T, E, k, d, F, act, tile, v8, monkeypatch):
     """The v4 bf16 grouped GEMM (csrc/ops/moe4.hip: 4-wave PGR2 tiles of 256 or 192 rows, A rows
-    gathered by the LDS-DMA, gated activation in registers) vs the fp32 reference, with biases,
-    gpt-oss widths (N = 5760 and 2880: partial last column tiles) and EP-style masked experts."""
+    gathered by the LDS-DMA, gated activation in registers) and its persistent form (v8,
+    csrc/ops/moe8.hip) vs the fp32 reference, with biases, gpt-oss widths (N = 5760 and 2880:
+    partial last column tiles) and EP-style masked experts."""
     monkeypatch.setattr(ops, "MOE_BF16_V4", True)
+    monkeypatch.setattr(ops, "MOE_BF16_V8", v8)
     monkeypatch.setattr(ops, "MOE4_TILE", tile)
     torch.manual_seed(13)
     x = torch.randn(T, d, device=DEV, dtype=torch.bfloat16)
