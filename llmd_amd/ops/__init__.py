@@ -629,8 +629,11 @@ MOE_V3_BF16 = os.environ.get("LLMD_MOE_V3_BF16", "1") == "1"  # DeepSeek EP8 T=4
 # bf16 prefill-sized steps on the v4 grouped GEMM (csrc/ops/moe4.hip, the PGR2 structure of the dense
 # prefill GEMM): DeepSeek EP8 T=4096 807 -> 1011 TF/s, gpt-oss T=5120 534 -> 586 (profiles/moe_gemm_v4_r5.txt)
 MOE_BF16_V4 = os.environ.get("LLMD_MOE_BF16_V4", "1") == "1"
-# the persistent form of the v4 bf16 tiles (csrc/ops/moe8.hip moe_gemm8_bf16_kernel)
-MOE_BF16_V8 = os.environ.get("LLMD_MOE_BF16_V8", "0") == "1"
+# the persistent form of the v4 bf16 tiles (csrc/ops/moe8.hip moe_gemm8_bf16_kernel): gpt-oss T=5120 layer
+# 651 -> 680 TF/s, T=8192 728 -> 748; DeepSeek EP8 (K = 7168 gate/up) 1079 -> 1014, so only GEMMs with
+# K <= 4096 take it (profiles/moe_gemm_v8_r6.txt)
+MOE_BF16_V8 = os.environ.get("LLMD_MOE_BF16_V8", "1") == "1"
+MOE_BF16_V8_MAX_K = int(os.environ.get("LLMD_MOE_BF16_V8_MAX_K", "4096"))
 MOE_FUSED_QUANT = os.environ.get("LLMD_MOE_FUSED_QUANT", "0") == "1"
 # v4 expert-tile rows: "auto" picks 192 or 256 by the expected padding at T*k/E rows per expert (gpt-oss
 # at a 5120-token step: 160 rows -> a 256-row tile is 62 % useful rows, a 192-row one 83 %)
@@ -835,9 +838,10 @@ def moe_experts(x, ids, wts, w1, w2, act=0, alpha=1.702, limit=7.0, out=None, b1
     y = torch.empty(max_p, d, dtype=x.dtype, device=dev)
     if v4:
         # v4: the dense prefill GEMM's 4-wave PGR2 structure, rows gathered by the LDS-DMA (csrc/ops/moe4.hip)
-        # (v8: the persistent form, csrc/ops/moe8.hip; >= 4 K-steps of 64)
-        v1 = 8 if MOE_BF16_V8 and w1.shape[2] >= 256 else 4
-        v2 = 8 if MOE_BF16_V8 and w2.shape[2] >= 256 else 4
+        # (v8: the persistent form, csrc/ops/moe8.hip, for K <= MOE_BF16_V8_MAX_K: the bf16 tiles run at
+        # the power cap, so hiding the per-tile cost pays only where K-loops are short)
+        v1 = 8 if MOE_BF16_V8 and 256 <= w1.shape[2] <= MOE_BF16_V8_MAX_K else 4
+        v2 = 8 if MOE_BF16_V8 and 256 <= w2.shape[2] <= MOE_BF16_V8_MAX_K else 4
         C.moe_gemm4(x, k, sorted_ids, tile_e, w1, h, 1, act, alpha, limit, False, b1, bm, v1, total)
         C.moe_gemm4(h, 1, sorted_ids, tile_e, w2, y, 0, 0, 0.0, 0.0, True, b2, bm, v2, total)
     else:
