@@ -327,6 +327,12 @@ __device__ __forceinline__ int p2_pv(int r) {
 
 // V (round-4 A/B switch): bit 0 = K/V fragment reads ring-pipelined with a sched_barrier
 // per step, bit 1 = LDS-DMA from asm (glds16) instead of the builtin
+// (round 6) bit 4 = row sums kept in scalar f32 adds: hipcc SLP-packs the two query blocks' sums
+// into v_pk_add_f32, which beside MFMAs costs ~13 cycles more per instruction than two v_add_f32
+// (MI355X_MICROARCH 'price of one filler beside MFMAs'); bit 5 = whole tiles DMA'd through a
+// per-tile buffer descriptor (scalar base, 32-bit per-lane offsets) instead of 64-bit per-lane
+// addresses (the v_lshl_add_u64 of every piece); bit 6 = the causal / window mask behind a scalar
+// branch (see compute())
 template <int D, int V = 3>
 __global__ __launch_bounds__(NT, 2) void prefill_v2_kernel(
     const uint16_t* __restrict__ q, int64_t q_stride, const uint16_t* __restrict__ kc,
@@ -421,11 +427,23 @@ __global__ __launch_bounds__(NT, 2) void prefill_v2_kernel(
     const char* vb = reinterpret_cast<const char*>(vc) + tb;
     const int rlim = ctx - 1 - ts;
     if (rlim >= 63 && bs >= 64) {
+      if constexpr ((V & 32) != 0) {
+        const __amdgpu_buffer_rsrc_t rk = __builtin_amdgcn_make_buffer_rsrc((void*)kb, 0, 64 * RB, 0x00020000);
+        const __amdgpu_buffer_rsrc_t rv = __builtin_amdgcn_make_buffer_rsrc((void*)vb, 0, 64 * RB, 0x00020000);
 #pragma unroll
-      for (int i = 0; i < NI / 4; ++i) {
-        char* dst = base + 1024 * (ws + 4 * i);
-        dma(kb + koff[i], dst);
-        dma(vb + voff[i], dst + P2_IMG);
+        for (int i = 0; i < NI / 4; ++i) {
+          char* dst = base + 1024 * (ws + 4 * i);
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(rk, (__attribute__((address_space(3))) void*)dst, 16, koff[i], 0, 0, 0);
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(rv, (__attribute__((address_space(3))) void*)(dst + P2_IMG), 16,
+                                                   voff[i], 0, 0, 0);
+        }
+      } else {
+#pragma unroll
+        for (int i = 0; i < NI / 4; ++i) {
+          char* dst = base + 1024 * (ws + 4 * i);
+          dma(kb + koff[i], dst);
+          dma(vb + voff[i], dst + P2_IMG);
+        }
       }
     } else if (rlim >= 63) {
       // blocks of 16 / 32 keys: a wave-instruction's RPI rows sit in one block
@@ -511,8 +529,12 @@ __global__ __launch_bounds__(NT, 2) void prefill_v2_kernel(
 #pragma unroll
       for (int j = 0; j < PF; ++j) vr[j] = vread(j);
     }
-    const bool need_mask = (ts + 63 > p_lo) || (window > 0 && ts <= p_hi - window);
+    bool need_mask = (ts + 63 > p_lo) || (window > 0 && ts <= p_hi - window);
+    if constexpr ((V & 64) != 0) need_mask = __builtin_amdgcn_readfirstlane((int)need_mask) != 0;
     if (need_mask) {
+      // bit 6: a real (scalar) branch - without the asm fence hipcc if-converts the mask into
+      // ~290 selects / compares executed on EVERY tile, not just the diagonal and window-edge ones
+      if constexpr ((V & 64) != 0) asm volatile("" ::: "memory");
 #pragma unroll
       for (int nb = 0; nb < 2; ++nb) {
         const int qp = p_lo + 16 * nb + c16;
@@ -573,6 +595,7 @@ __global__ __launch_bounds__(NT, 2) void prefill_v2_kernel(
           const float p = __builtin_amdgcn_exp2f(fmaf(sc[b4][nb][i], scale_log2, -msub));
           sc[b4][nb][i] = p;
           ps += p;
+          if constexpr ((V & 16) != 0) asm volatile("" : "+v"(ps));  // no SLP packing across nb
         }
       lsum[nb] += ps;  // lane-partial: summed over the row's 4 lanes once, in the epilogue
     }
@@ -1395,12 +1418,15 @@ extern "C" int llmd_paged_prefill(const void* q, int64_t q_stride, const void* k
       // the asm DMA only at full ISL and loses 12 % on one-wave grids (5000 x 512 chunk); reading
       // 6 fragments ahead (bit 2) adds ~1 % -> 5
       const char* e = getenv("LLMD_PREFILL_V2_VARIANT");
-      return e ? (atoi(e) & 15) : 5;
+      return e ? (atoi(e) & 127) : 5;
     }();
-    auto pick = [](int v, bool d128) {  // instantiated: 0-3, 5 (PF 6), 9 (early V), 13 (both)
+    auto pick = [](int v, bool d128) {  // instantiated: 0-3, 5 (PF 6), 9 (early V), 13 (both); D 128: 21, 37, 53, 69, 117
       if (d128) return v == 0 ? prefill_v2_kernel<128, 0> : v == 2 ? prefill_v2_kernel<128, 2>
                      : v == 3 ? prefill_v2_kernel<128, 3> : v == 5 ? prefill_v2_kernel<128, 5>
                      : v == 9 ? prefill_v2_kernel<128, 9> : v == 13 ? prefill_v2_kernel<128, 13>
+                     : v == 21 ? prefill_v2_kernel<128, 21> : v == 37 ? prefill_v2_kernel<128, 37>
+                     : v == 53 ? prefill_v2_kernel<128, 53> : v == 69 ? prefill_v2_kernel<128, 69>
+                     : v == 117 ? prefill_v2_kernel<128, 117>
                      : prefill_v2_kernel<128, 1>;
       return v == 0 ? prefill_v2_kernel<64, 0> : v == 2 ? prefill_v2_kernel<64, 2>
              : v == 3 ? prefill_v2_kernel<64, 3> : v == 5 ? prefill_v2_kernel<64, 5>
