@@ -134,7 +134,9 @@ def _check_launch_stubs(lib: Path) -> None:
         r = subprocess.run(["nm", "-D", "--undefined-only", str(lib)], capture_output=True, text=True, check=True)
     except (OSError, subprocess.CalledProcessError):
         return  # no binutils: the import check of __graft_entry__.build() still catches it
-    missing = [l.split()[-1] for l in r.stdout.splitlines() if "__device_stub__" in l]
+    # the stub is named __device_stub__<kernel> or, for a kernel in an anonymous namespace, after the kernel
+    # itself (_ZN12_GLOBAL__N_...): a library's own anonymous-namespace symbol is never legitimately external
+    missing = [l.split()[-1] for l in r.stdout.splitlines() if "__device_stub__" in l or "_GLOBAL__N_" in l]
     if missing:
         raise RuntimeError(f"{lib.name}: {len(missing)} kernel launch stubs undefined, e.g. {missing[0]}")
 

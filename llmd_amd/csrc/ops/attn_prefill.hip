@@ -406,7 +406,7 @@ __global__ __launch_bounds__(NT, 2) void prefill_v2_kernel(
   // (its V rows past the end must stay finite: P = 0 there, but 0 * NaN would
   // poison O).
   const int ws = __builtin_amdgcn_readfirstlane(w);
-  uint32_t koff[NI / 4], voff[NI / 4];
+  uint32_t koff[4], voff[4];  // NI / 4 used; fixed size: a template-sized array read by the DMA lambda loses the launch stub
 #pragma unroll
   for (int i = 0; i < NI / 4; ++i) {
     const int u = 64 * (w + 4 * i) + lane;
