@@ -1417,8 +1417,10 @@ extern "C" int llmd_paged_prefill(const void* q, int64_t q_stride, const void* k
       // A/B of the round-4 schedule (V above; profiles/attn_prefill_r4_ab.txt): the ring wins everywhere,
       // the asm DMA only at full ISL and loses 12 % on one-wave grids (5000 x 512 chunk); reading
       // 6 fragments ahead (bit 2) adds ~1 % -> 5
+      // round 6 (profiles/attn_prefill_v2_variants_r6.txt): unpacked row sums + buffer-descriptor DMA
+      // (bits 4, 5) +1 to +4 % at ISL 2048-8192 -> 53
       const char* e = getenv("LLMD_PREFILL_V2_VARIANT");
-      return e ? (atoi(e) & 127) : 5;
+      return e ? (atoi(e) & 127) : 53;
     }();
     auto pick = [](int v, bool d128) {  // instantiated: 0-3, 5 (PF 6), 9 (early V), 13 (both); D 128: 21, 37, 53, 69, 117
       if (d128) return v == 0 ? prefill_v2_kernel<128, 0> : v == 2 ? prefill_v2_kernel<128, 2>

@@ -1,6 +1,6 @@
 """Per-kernel time over the last `window` seconds of a rocprofv3 kernel trace (the timed window of
 a bench run ends the trace): total ms, share and count per kernel name, plus the GPU busy share.
-  python scripts/kernel_window.py <kernel_trace.csv> [window_s] [top]"""
+  python scripts/kernel_window.py <kernel_trace.csv | results.db> [window_s] [top]"""
 import csv
 import sys
 from collections import defaultdict
@@ -11,9 +11,15 @@ def main():
     window = float(sys.argv[2]) if len(sys.argv) > 2 else 3.0
     top = int(sys.argv[3]) if len(sys.argv) > 3 else 30
     iv = []
-    with open(path) as f:
-        for row in csv.DictReader(f):
-            iv.append((int(row["Start_Timestamp"]), int(row["End_Timestamp"]), row.get("Kernel_Name", "")))
+    if path.endswith(".db"):  # rocprofv3's default rocpd SQLite output
+        import sqlite3
+
+        con = sqlite3.connect(path)
+        iv = [(int(s), int(e), n) for s, e, n in con.execute("select start, end, name from kernels")]
+    else:
+        with open(path) as f:
+            for row in csv.DictReader(f):
+                iv.append((int(row["Start_Timestamp"]), int(row["End_Timestamp"]), row.get("Kernel_Name", "")))
     end = max(e for _, e, _ in iv)
     lo = end - int(window * 1e9)
     tot, cnt = defaultdict(int), defaultdict(int)
