@@ -76,3 +76,22 @@ def test_bench_pd_routed_through_router_and_sidecar():
     assert d["sidecar_fallbacks"] == 0 and d["kv_transfer_failures"] == 0
     ol = d["open_loop"]
     assert ol["requests"] == 24 and ol["errors"] == 0 and ol["ttft_p50_s"] is not None and ol["rate_req_s"] > 0
+
+
+def test_bench_agg_two_ranks_reports_whole_job():
+    """The driver's N = 2 / 4 scaling points (torchrun, one engine per rank, mode agg): rank 0
+    prints ONE line with the whole-job value (sum over ranks), n_gpus = world, dp<N> and the
+    steady-state window summed over ranks. CPU, 2 ranks, gloo."""
+    env = dict(os.environ, LLMD_BENCH_DEVICE="cpu", OMP_NUM_THREADS="2")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr=127.0.0.1", "--master-port=29719", os.path.join(ROOT, "bench.py"), "--gpus", "2",
+           "--model", "tiny-llama", "--isl", "48", "--osl", "16", "--concurrency", "4", "--steps", "6",
+           "--warmup", "2", "--enforce-eager", "--block-size", "16", "--max-num-batched-tokens", "256"]
+    r = subprocess.run(cmd, env=env, cwd=ROOT, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["config"]["parallelism"] == "dp2" and d["steps"] == 6
+    assert d["value"] > 0 and abs(d["output_tok_s_per_gpu"] - d["value"] / 2) < 0.02
+    assert d["config"]["global_batch"] == 8
