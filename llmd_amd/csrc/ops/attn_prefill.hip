@@ -1364,6 +1364,19 @@ static bool prefill_v4_on() {
   return e && e[0] == '1';
 }
 
+// the software-pipelined v5 (csrc/ops/attn_prefill5.hip): 1 when the shape is not covered
+extern "C" int llmd_paged_prefill_v5(const void* q, int64_t q_stride, const void* kc, const void* vc,
+                                     int64_t block_stride, int bs, const int* block_tables, int bt_stride,
+                                     const int* q_start, const int* q_len, const int* ctx_len, const int* items,
+                                     int n_items, int Hq, int Hkv, int D, float scale_log2, int window,
+                                     const float* sinks, void* out, int64_t out_stride, float v_scale, int xcd,
+                                     hipStream_t st);
+
+static bool prefill_v5_on() {  // LLMD_PREFILL_V5=1 (read per launch: A/B in one process)
+  const char* e = getenv("LLMD_PREFILL_V5");
+  return e && e[0] == '1';
+}
+
 extern "C" int llmd_paged_prefill(const void* q, int64_t q_stride, const void* kc, const void* vc,
                                   int64_t block_stride, int bs, const int* block_tables,
                                   int bt_stride, const int* q_start, const int* q_len,
@@ -1404,6 +1417,12 @@ extern "C" int llmd_paged_prefill(const void* q, int64_t q_stride, const void* k
                        (const uint16_t*)vc, block_stride, bs, block_tables, bt_stride, q_start, q_len, ctx_len,
                        items, Hq, Hkv, G, scale_log2, window, sinks, (uint16_t*)out, out_stride, v_scale,
                        xcd_map && (int64_t)n_items * grid3.y >= 1024 ? 1 : 0);
+  } else if (!fp8 && !v1_only && prefill_v5_on() &&
+             llmd_paged_prefill_v5(q, q_stride, kc, vc, block_stride, bs, block_tables, bt_stride, q_start, q_len,
+                                   ctx_len, items, n_items, Hq, Hkv, D, scale_log2, window, sinks, out, out_stride,
+                                   v_scale, xcd_map && (int64_t)n_items * (Hkv * (G / 4)) >= 1024 ? 1 : 0,
+                                   st) == 0) {
+    // launched by v5
   } else if (D == 128 && !fp8 && bs >= 16 && !v1_only && prefill_v4_on()) {
     const char* e4 = getenv("LLMD_PREFILL_V4_VARIANT");  // 1: builtin DMA, 3: asm DMA, 7: asm DMA + pipelined halves
     auto kern4 = (e4 && e4[0] == '1') ? prefill_v4_kernel<1> : (e4 && e4[0] == '7') ? prefill_v4_kernel<7>

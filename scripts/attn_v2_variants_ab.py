@@ -31,7 +31,8 @@ def main():
     res = {}
     for r in range(a.rounds):
         for v in a.variants.split(","):
-            env = dict(os.environ, LLMD_PREFILL_V2_VARIANT=v)
+            # "v5": the software-pipelined kernel (csrc/ops/attn_prefill5.hip); numbers: v2 variants
+            env = dict(os.environ, LLMD_PREFILL_V5="1") if v == "v5" else dict(os.environ, LLMD_PREFILL_V2_VARIANT=v)
             code = CHILD.format(root=ROOT, cases=CASES, check=(r == 0))
             p = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=300)
             if p.returncode != 0:
@@ -48,7 +49,7 @@ def main():
         parts = []
         for v in a.variants.split(","):
             t = sorted(res[(k, v)])[len(res[(k, v)]) // 2]
-            parts.append(f"V{v} {t * 1e3:.3f} ms {fl / t / 1e12:.0f} TF/s")
+            parts.append(f"{v if v.startswith('v') else 'V' + v} {t * 1e3:.3f} ms {fl / t / 1e12:.0f} TF/s")
         print(f"AB ctx={ctx} q={ql}: " + " | ".join(parts), flush=True)
 
 
