@@ -332,7 +332,12 @@ __device__ __forceinline__ int p2_pv(int r) {
 // (MI355X_MICROARCH 'price of one filler beside MFMAs'); bit 5 = whole tiles DMA'd through a
 // per-tile buffer descriptor (scalar base, 32-bit per-lane offsets) instead of 64-bit per-lane
 // addresses (the v_lshl_add_u64 of every piece); bit 6 = the causal / window mask behind a scalar
-// branch (see compute())
+// branch (see compute()). The loop is issue-bound (profiles/attn_prefill_v2_variants_r6.txt), so
+// bits 7 / 8 take VALU work per score away: bit 7 = Q pre-scaled by scale * log2(e) at load and the
+// S^T accumulators started at -m (the running row max, one broadcast register per query block):
+// the MFMA yields S scale - m, and p = exp2 of it without the per-score v_fma; bit 8 = row sums on
+// the matrix pipe: P . ones (4 extra 16x16x32 MFMAs per tile, accumulators in O's layout) instead of
+// 32 v_add_f32 per lane and tile, and no cross-lane sum in the epilogue
 template <int D, int V = 3>
 __global__ __launch_bounds__(NT, 2) void prefill_v2_kernel(
     const uint16_t* __restrict__ q, int64_t q_stride, const uint16_t* __restrict__ kc,
@@ -389,6 +394,10 @@ __global__ __launch_bounds__(NT, 2) void prefill_v2_kernel(
       u32x4_t v = {0, 0, 0, 0};
       if (tk < ql) v = *reinterpret_cast<const u32x4_t*>(qr + (4 * s + g) * 8);
       qf[nb][s] = __builtin_bit_cast(bf16x8_t, v);
+      if constexpr ((V & 128) != 0) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) qf[nb][s][e] = (__bf16)((float)qf[nb][s][e] * scale_log2);
+      }
     }
   }
   float m[2] = {NEG_INF, NEG_INF}, lsum[2] = {0.f, 0.f};
@@ -397,6 +406,11 @@ __global__ __launch_bounds__(NT, 2) void prefill_v2_kernel(
   for (int nb = 0; nb < 2; ++nb)
 #pragma unroll
     for (int n = 0; n < NB; ++n) o[nb][n] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  // bit 7: -m (0 while no score seen) broadcast, the S^T accumulators' start; bit 8: row sums in O's layout
+  f32x4_t cm[2] = {f32x4_t{0.f, 0.f, 0.f, 0.f}, f32x4_t{0.f, 0.f, 0.f, 0.f}};
+  f32x4_t ls[2] = {f32x4_t{0.f, 0.f, 0.f, 0.f}, f32x4_t{0.f, 0.f, 0.f, 0.f}};
+  constexpr bool RELS = (V & 128) != 0, MSUM = (V & 256) != 0;
+  const float sl2 = RELS ? 1.f : scale_log2;  // scale of the scores the MFMA yields (bit 7: pre-applied)
 
   // DMA: NI K + NI V wave-instructions of 1 KB (1024 / RB rows); wave w issues
   // j = w + 4i. The per-lane source offsets inside a 64-row tile are constant
@@ -512,7 +526,7 @@ __global__ __launch_bounds__(NT, 2) void prefill_v2_kernel(
     if constexpr (V & 1) __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int b4 = 0; b4 < 4; ++b4) {
-      f32x4_t a0 = {0.f, 0.f, 0.f, 0.f}, a1 = {0.f, 0.f, 0.f, 0.f};
+      f32x4_t a0 = cm[0], a1 = cm[1];  // zeros unless bit 7
 #pragma unroll
       for (int s = 0; s < KS; ++s) {
         const int j = KS * b4 + s;
@@ -561,7 +575,12 @@ __global__ __launch_bounds__(NT, 2) void prefill_v2_kernel(
       for (int b4 = 0; b4 < 4; ++b4)
 #pragma unroll
         for (int i = 0; i < 4; ++i) mx = fmaxf(mx, sc[b4][nb][i]);
-      mt[nb] = mx * scale_log2;
+      if constexpr (RELS) {  // scores relative to msub (0 while m = -inf): absolute max = mx + msub
+        const float msub = (m[nb] == NEG_INF) ? 0.f : m[nb];
+        mt[nb] = mx + msub;
+      } else {
+        mt[nb] = mx * scale_log2;
+      }
       grow = grow || (mt[nb] > m[nb] + 8.f);
     }
     if (__ballot(grow) != 0) {  // wave-uniform
@@ -573,6 +592,15 @@ __global__ __launch_bounds__(NT, 2) void prefill_v2_kernel(
         const float mnew = fmaxf(m[nb], mx);
         alpha[nb] = (mnew == NEG_INF) ? 1.f : __builtin_amdgcn_exp2f(m[nb] - mnew);
         lsum[nb] *= alpha[nb];  // per-lane partial sums, same factor on the row's 4 lanes
+        if constexpr (RELS) {   // rebase this tile's relative scores and the next tiles' start
+          const float sold = (m[nb] == NEG_INF) ? 0.f : m[nb], snew = (mnew == NEG_INF) ? 0.f : mnew;
+          const float d = sold - snew;
+#pragma unroll
+          for (int b4 = 0; b4 < 4; ++b4)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) sc[b4][nb][i] += d;
+          cm[nb] = f32x4_t{-snew, -snew, -snew, -snew};
+        }
         m[nb] = mnew;
       }
 #pragma unroll
@@ -582,6 +610,7 @@ __global__ __launch_bounds__(NT, 2) void prefill_v2_kernel(
           const float a = __shfl(alpha[nb], 4 * g + i, 64);
 #pragma unroll
           for (int n = 0; n < NB; ++n) o[nb][n][i] *= a;
+          if constexpr (MSUM) ls[nb][i] *= a;
         }
     }
 #pragma unroll
@@ -592,12 +621,15 @@ __global__ __launch_bounds__(NT, 2) void prefill_v2_kernel(
       for (int b4 = 0; b4 < 4; ++b4)
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-          const float p = __builtin_amdgcn_exp2f(fmaf(sc[b4][nb][i], scale_log2, -msub));
+          const float p = RELS ? __builtin_amdgcn_exp2f(sc[b4][nb][i])
+                               : __builtin_amdgcn_exp2f(fmaf(sc[b4][nb][i], sl2, -msub));
           sc[b4][nb][i] = p;
-          ps += p;
-          if constexpr ((V & 16) != 0) asm volatile("" : "+v"(ps));  // no SLP packing across nb
+          if constexpr (!MSUM) {
+            ps += p;
+            if constexpr ((V & 16) != 0) asm volatile("" : "+v"(ps));  // no SLP packing across nb
+          }
         }
-      lsum[nb] += ps;  // lane-partial: summed over the row's 4 lanes once, in the epilogue
+      if constexpr (!MSUM) lsum[nb] += ps;  // lane-partial: summed over the row's 4 lanes once, in the epilogue
     }
     bf16x8_t pa[2][2];
 #pragma unroll
@@ -609,6 +641,15 @@ __global__ __launch_bounds__(NT, 2) void prefill_v2_kernel(
           pa[t2][nb][j] = (__bf16)sc[2 * t2][nb][j];
           pa[t2][nb][4 + j] = (__bf16)sc[2 * t2 + 1][nb][j];
         }
+    if constexpr (MSUM) {  // row sums of P on the matrix pipe: P . ones, rows in O's layout
+      const bf16x8_t ones = {(__bf16)1.f, (__bf16)1.f, (__bf16)1.f, (__bf16)1.f,
+                             (__bf16)1.f, (__bf16)1.f, (__bf16)1.f, (__bf16)1.f};
+#pragma unroll
+      for (int t2 = 0; t2 < 2; ++t2) {
+        ls[0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pa[t2][0], ones, ls[0], 0, 0, 0);
+        ls[1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pa[t2][1], ones, ls[1], 0, 0, 0);
+      }
+    }
     if constexpr (!(V & 8)) {
 #pragma unroll
       for (int j = 0; j < PF; ++j) vr[j] = vread(j);
@@ -646,9 +687,17 @@ __global__ __launch_bounds__(NT, 2) void prefill_v2_kernel(
     den += __shfl_xor(den, 32, 64);
     if (sinks) den += exp2f(sink - (m[nb] == NEG_INF ? 0.f : m[nb]));
     const float inv = den > 0.f ? vscale / den : 0.f;
+    float mrow[4];  // bit 8: the running max of O's row 4 g + i (m is kept per query column c16)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) mrow[i] = MSUM ? __shfl(m[nb], 4 * g + i, 64) : 0.f;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      const float f = __shfl(inv, 4 * g + i, 64);
+      float f = __shfl(inv, 4 * g + i, 64);
+      if constexpr (MSUM) {
+        float d = ls[nb][i];
+        if (sinks) d += exp2f(sink - (mrow[i] == NEG_INF ? 0.f : mrow[i]));
+        f = d > 0.f ? vscale / d : 0.f;
+      }
       const int tk = tok0 + 16 * nb + 4 * g + i;
       if (tk < ql) {
         uint16_t* orow = out + (int64_t)(qs + tk) * out_stride + (int64_t)head * D;
@@ -1432,29 +1481,33 @@ extern "C" int llmd_paged_prefill(const void* q, int64_t q_stride, const void* k
                        items, Hq, Hkv, G, HPW, scale_log2, window, sinks, (uint16_t*)out, out_stride, v_scale,
                        xcd_map && (int64_t)n_items * grid.y >= 1024 ? 1 : 0);
   } else if ((D == 128 || D == 64) && !fp8 && bs >= 16 && !v1_only) {
-    static const int pv = [] {
+    const int pv = [] {  // read per launch (tests and A/Bs switch it in one process; getenv is ~0.1 us)
       // A/B of the round-4 schedule (V above; profiles/attn_prefill_r4_ab.txt): the ring wins everywhere,
       // the asm DMA only at full ISL and loses 12 % on one-wave grids (5000 x 512 chunk); reading
       // 6 fragments ahead (bit 2) adds ~1 % -> 5
       // round 6 (profiles/attn_prefill_v2_variants_r6.txt): unpacked row sums + buffer-descriptor DMA
       // (bits 4, 5) +1 to +4 % at ISL 2048-8192 -> 53
+      // round 6 (r6w): + Q pre-scaled / accumulators started at -m and row sums on the MFMA (bits 7, 8)
+      // +3 to +6 % more -> 437 for D = 128; D = 64 (gpt-oss) keeps the round-5 default 5 (the new bits
+      // are instantiated and measured for D = 128 only)
       const char* e = getenv("LLMD_PREFILL_V2_VARIANT");
-      return e ? (atoi(e) & 127) : 53;
+      return e ? (atoi(e) & 511) : -1;
     }();
-    auto pick = [](int v, bool d128) {  // instantiated: 0-3, 5 (PF 6), 9 (early V), 13 (both); D 128: 21, 37, 53, 69, 117
+    auto pick = [](int v, bool d128) {  // instantiated: 0-3, 5 (PF 6), 9 (early V), 13 (both); D 128: 21, 37, 53, 69, 117, 181, 309, 437
       if (d128) return v == 0 ? prefill_v2_kernel<128, 0> : v == 2 ? prefill_v2_kernel<128, 2>
                      : v == 3 ? prefill_v2_kernel<128, 3> : v == 5 ? prefill_v2_kernel<128, 5>
                      : v == 9 ? prefill_v2_kernel<128, 9> : v == 13 ? prefill_v2_kernel<128, 13>
                      : v == 21 ? prefill_v2_kernel<128, 21> : v == 37 ? prefill_v2_kernel<128, 37>
                      : v == 53 ? prefill_v2_kernel<128, 53> : v == 69 ? prefill_v2_kernel<128, 69>
-                     : v == 117 ? prefill_v2_kernel<128, 117>
+                     : v == 117 ? prefill_v2_kernel<128, 117> : v == 181 ? prefill_v2_kernel<128, 181>
+                     : v == 309 ? prefill_v2_kernel<128, 309> : v == 437 ? prefill_v2_kernel<128, 437>
                      : prefill_v2_kernel<128, 1>;
       return v == 0 ? prefill_v2_kernel<64, 0> : v == 2 ? prefill_v2_kernel<64, 2>
              : v == 3 ? prefill_v2_kernel<64, 3> : v == 5 ? prefill_v2_kernel<64, 5>
              : v == 9 ? prefill_v2_kernel<64, 9> : v == 13 ? prefill_v2_kernel<64, 13>
              : prefill_v2_kernel<64, 1>;
     };
-    auto kern = pick(pv, D == 128);
+    auto kern = pick(pv >= 0 ? pv : (D == 128 ? 437 : 5), D == 128);
     hipLaunchKernelGGL(kern, grid, blk, 0, st, (const uint16_t*)q, q_stride, (const uint16_t*)kc,
                        (const uint16_t*)vc, block_stride, bs, block_tables, bt_stride, q_start, q_len, ctx_len,
                        items, Hq, Hkv, G, HPW, scale_log2, window, sinks, (uint16_t*)out, out_stride, v_scale,

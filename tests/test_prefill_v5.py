@@ -53,3 +53,22 @@ def test_prefill_v5_long_vs_v2(shapes, monkeypatch):
     o5 = ops.paged_prefill(q, kc, vc, bt, *args, Hq, Hkv, 128, scale)
     assert torch.isfinite(o5.float()).all()
     _close(o5, o2, atol=2e-2, rtol=2e-2)
+
+
+@pytest.mark.parametrize("variant", ["53", "181", "309", "437"])
+@pytest.mark.parametrize("Hq,Hkv,bs", [(64, 8, 64), (32, 8, 16), (8, 8, 64)])
+def test_prefill_v2_variants_match_reference(variant, Hq, Hkv, bs, monkeypatch):
+    """v2 schedule variants (LLMD_PREFILL_V2_VARIANT): 53 = round-6 default; + 128: Q pre-scaled and
+    the S^T accumulators started at -m (no per-score v_fma); + 256: row sums as P . ones MFMAs."""
+    monkeypatch.setenv("LLMD_PREFILL_V5", "0")
+    monkeypatch.setenv("LLMD_PREFILL_V2_VARIANT", variant)
+    shapes = [(1, 1), (37, 37), (200, 200), (130, 1000), (64, 64), (513, 700), (65, 129)]
+    q, kc, vc, bt, args = _run(shapes, Hq, Hkv, bs)
+    r = ref.paged_prefill(q, kc, vc, bt, *args, Hq, Hkv, 128, 1 / math.sqrt(128))
+    o = ops.paged_prefill(q, kc, vc, bt, *args, Hq, Hkv, 128, 1 / math.sqrt(128))
+    _close(o, r)
+    sinks = torch.randn(Hq, device="cuda")
+    q2 = q[:, :Hq * 128].contiguous()
+    for window in (0, 128):
+        _close(ops.paged_prefill(q2, kc, vc, bt, *args, Hq, Hkv, 128, 128 ** -0.5, window, sinks),
+               ref.paged_prefill(q2, kc, vc, bt, *args, Hq, Hkv, 128, 128 ** -0.5, window, sinks))
