@@ -1488,8 +1488,7 @@ extern "C" int llmd_paged_prefill(const void* q, int64_t q_stride, const void* k
       // round 6 (profiles/attn_prefill_v2_variants_r6.txt): unpacked row sums + buffer-descriptor DMA
       // (bits 4, 5) +1 to +4 % at ISL 2048-8192 -> 53
       // round 6 (r6w): + Q pre-scaled / accumulators started at -m and row sums on the MFMA (bits 7, 8)
-      // +3 to +6 % more -> 437 for D = 128; D = 64 (gpt-oss) keeps the round-5 default 5 (the new bits
-      // are instantiated and measured for D = 128 only)
+      // +3 to +6 % more at D = 128, +7 to +9 % over the round-5 V5 at D = 64 (gpt-oss) -> 437 for both
       const char* e = getenv("LLMD_PREFILL_V2_VARIANT");
       return e ? (atoi(e) & 511) : -1;
     }();
@@ -1505,9 +1504,11 @@ extern "C" int llmd_paged_prefill(const void* q, int64_t q_stride, const void* k
       return v == 0 ? prefill_v2_kernel<64, 0> : v == 2 ? prefill_v2_kernel<64, 2>
              : v == 3 ? prefill_v2_kernel<64, 3> : v == 5 ? prefill_v2_kernel<64, 5>
              : v == 9 ? prefill_v2_kernel<64, 9> : v == 13 ? prefill_v2_kernel<64, 13>
+             : v == 53 ? prefill_v2_kernel<64, 53> : v == 181 ? prefill_v2_kernel<64, 181>
+             : v == 437 ? prefill_v2_kernel<64, 437>
              : prefill_v2_kernel<64, 1>;
     };
-    auto kern = pick(pv >= 0 ? pv : (D == 128 ? 437 : 5), D == 128);
+    auto kern = pick(pv >= 0 ? pv : 437, D == 128);
     hipLaunchKernelGGL(kern, grid, blk, 0, st, (const uint16_t*)q, q_stride, (const uint16_t*)kc,
                        (const uint16_t*)vc, block_stride, bs, block_tables, bt_stride, q_start, q_len, ctx_len,
                        items, Hq, Hkv, G, HPW, scale_log2, window, sinks, (uint16_t*)out, out_stride, v_scale,

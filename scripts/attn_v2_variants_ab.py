@@ -11,6 +11,7 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CASES = [(5000, 5000), (8192, 8192), (8192, 4096), (2048, 2048)]
+D64 = os.environ.get("AB_D64") == "1"  # gpt-oss shape: D 64, 64 / 8 heads (full-attention layers)
 
 CHILD = r"""
 import json, sys
@@ -18,7 +19,7 @@ sys.path.insert(0, {root!r})
 from scripts.bench_attn import prefill
 out = {{}}
 for ctx, ql in {cases!r}:
-    out[f"{{ctx}}/{{ql}}"] = prefill(ctx, ql, 64, 8, 128, 64, check={check!r} and ctx == 2048)
+    out[f"{{ctx}}/{{ql}}"] = prefill(ctx, ql, 64, 8, {D}, 64, check={check!r} and ctx == 2048)
 print("RESULT " + json.dumps(out), flush=True)
 """
 
@@ -33,7 +34,7 @@ def main():
         for v in a.variants.split(","):
             # "v5": the software-pipelined kernel (csrc/ops/attn_prefill5.hip); numbers: v2 variants
             env = dict(os.environ, LLMD_PREFILL_V5="1") if v == "v5" else dict(os.environ, LLMD_PREFILL_V2_VARIANT=v)
-            code = CHILD.format(root=ROOT, cases=CASES, check=(r == 0))
+            code = CHILD.format(root=ROOT, cases=CASES, check=(r == 0), D=64 if D64 else 128)
             p = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=300)
             if p.returncode != 0:
                 print(p.stdout[-2000:], p.stderr[-3000:])
@@ -45,7 +46,7 @@ def main():
     for ctx, ql in CASES:
         k = f"{ctx}/{ql}"
         vis = sum(ctx - ql + i + 1 for i in range(ql))
-        fl = 4 * 64 * 128 * vis
+        fl = 4 * 64 * (64 if D64 else 128) * vis
         parts = []
         for v in a.variants.split(","):
             t = sorted(res[(k, v)])[len(res[(k, v)]) // 2]

@@ -72,3 +72,35 @@ def test_prefill_v2_variants_match_reference(variant, Hq, Hkv, bs, monkeypatch):
     for window in (0, 128):
         _close(ops.paged_prefill(q2, kc, vc, bt, *args, Hq, Hkv, 128, 128 ** -0.5, window, sinks),
                ref.paged_prefill(q2, kc, vc, bt, *args, Hq, Hkv, 128, 128 ** -0.5, window, sinks))
+
+
+@pytest.mark.parametrize("variant", ["5", "53", "181", "437"])
+@pytest.mark.parametrize("window", [0, 128])
+def test_prefill_v2_variants_d64_match_reference(variant, window, monkeypatch):
+    """The gpt-oss attention shape (64 / 8 heads, D 64, sliding window 128 on half the layers,
+    sinks) under each v2 variant instantiated for D = 64."""
+    monkeypatch.setenv("LLMD_PREFILL_V2_VARIANT", variant)
+    torch.manual_seed(11)
+    Hq, Hkv, D, bs = 64, 8, 64, 64
+    shapes = [(1, 1), (37, 37), (200, 200), (130, 1000), (513, 700), (65, 129)]
+    ctx = [c for _, c in shapes]
+    ql = [a for a, _ in shapes]
+    nb = [(c + bs - 1) // bs for c in ctx]
+    total = sum(nb) + 3
+    kc = torch.randn(total, Hkv, bs, D, device="cuda", dtype=torch.bfloat16)
+    vc = torch.randn(total, Hkv, bs, D, device="cuda", dtype=torch.bfloat16)
+    perm = torch.randperm(total)
+    bt = torch.zeros(len(ctx), max(nb) + 1, dtype=torch.int32)
+    o = 0
+    for i, n in enumerate(nb):
+        bt[i, :n] = perm[o:o + n].int()
+        o += n
+    bt = bt.cuda()
+    qs = [0]
+    for a in ql[:-1]:
+        qs.append(qs[-1] + a)
+    q = torch.randn(sum(ql), Hq * D, device="cuda", dtype=torch.bfloat16)
+    args = [torch.tensor(x, dtype=torch.int32, device="cuda") for x in (qs, ql, ctx)]
+    sinks = torch.randn(Hq, device="cuda")
+    _close(ops.paged_prefill(q, kc, vc, bt, *args, Hq, Hkv, D, D ** -0.5, window, sinks),
+           ref.paged_prefill(q, kc, vc, bt, *args, Hq, Hkv, D, D ** -0.5, window, sinks))
