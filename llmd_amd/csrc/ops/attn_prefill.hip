@@ -1413,6 +1413,36 @@ static bool prefill_v4_on() {
   return e && e[0] == '1';
 }
 
+namespace {
+// The K / V blocks a prefill step reads from an fp8 (e4m3) paged cache, widened exactly into a dense
+// bf16 copy (block table entry e -> row e of the copy): the fp8-KV prefill then runs on the bf16 v2
+// kernel (k_scale folded into its softmax scale, v_scale into its epilogue, as for the fp8 kernel)
+// instead of the VGPR-staged v1 fp8 kernel (~2x its time at ISL 5000). One workgroup per (entry, K|V);
+// 10 MB of K+V per 5000-token layer: a few microseconds.
+__global__ __launch_bounds__(256) void kv_dequant_gather_kernel(const uint8_t* __restrict__ kc,
+                                                                const uint8_t* __restrict__ vc, int64_t block_stride,
+                                                                const int* __restrict__ bt, int n_blocks,
+                                                                int per_block, uint16_t* __restrict__ kd,
+                                                                uint16_t* __restrict__ vd) {
+  const int e = blockIdx.x;
+  const int b = min(max(bt[e], 0), n_blocks - 1);  // padding entries (never read by the kernel) -> block 0
+  const uint8_t* src = (blockIdx.y ? vc : kc) + (int64_t)b * block_stride;
+  uint16_t* dst = (blockIdx.y ? vd : kd) + (int64_t)e * per_block;
+  for (int i = threadIdx.x * 8; i < per_block; i += 256 * 8)
+    *reinterpret_cast<u32x4_t*>(dst + i) = fp8x8_to_bf16x8(*reinterpret_cast<const u32x2_t*>(src + i));
+}
+}  // namespace
+
+extern "C" int llmd_kv_dequant_gather(const void* kc, const void* vc, int64_t block_stride, const int* bt,
+                                      int n_entries, int n_blocks, int per_block, void* kd, void* vd,
+                                      hipStream_t st) {
+  if (per_block % 8 || block_stride % 8 || n_blocks <= 0) return -1;
+  if (n_entries == 0) return 0;
+  hipLaunchKernelGGL(kv_dequant_gather_kernel, dim3(n_entries, 2), dim3(256), 0, st, (const uint8_t*)kc,
+                     (const uint8_t*)vc, block_stride, bt, n_blocks, per_block, (uint16_t*)kd, (uint16_t*)vd);
+  return (int)hipGetLastError();
+}
+
 // the software-pipelined v5 (csrc/ops/attn_prefill5.hip): 1 when the shape is not covered
 extern "C" int llmd_paged_prefill_v5(const void* q, int64_t q_stride, const void* kc, const void* vc,
                                      int64_t block_stride, int bs, const int* block_tables, int bt_stride,

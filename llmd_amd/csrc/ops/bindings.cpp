@@ -646,6 +646,28 @@ void mgemm_fp8(torch::Tensor y, torch::Tensor xq, torch::Tensor xs, torch::Tenso
   TORCH_CHECK(rc == 0, "mgemm_fp8 failed: ", rc);
 }
 
+extern "C" int llmd_kv_dequant_gather(const void*, const void*, int64_t, const int*, int, int, int, void*, void*,
+                                      hipStream_t);
+
+// fp8 paged K/V blocks of a block table -> dense bf16 copies kd / vd [entries, Hkv, bs, D] (attn_prefill.hip)
+void kv_dequant_gather(torch::Tensor k_cache, torch::Tensor v_cache, torch::Tensor block_tables, torch::Tensor kd,
+                       torch::Tensor vd) {
+  const c10::hip::OptionalHIPGuard device_guard(dev_of(k_cache));
+  CHECK_CUDA(k_cache); CHECK_DT(k_cache, at::kFloat8_e4m3fn); CHECK_DT(v_cache, at::kFloat8_e4m3fn);
+  CHECK_BF16(kd); CHECK_BF16(vd); CHECK_DT(block_tables, at::kInt);
+  TORCH_CHECK(k_cache.dim() == 4 && v_cache.sizes() == k_cache.sizes() && v_cache.stride(0) == k_cache.stride(0),
+              "caches [blocks, Hkv, bs, D], same layout");
+  const int64_t per = k_cache.size(1) * k_cache.size(2) * k_cache.size(3);
+  TORCH_CHECK(k_cache.stride(3) == 1 && k_cache.stride(2) == k_cache.size(3) &&
+              k_cache.stride(1) == k_cache.size(2) * k_cache.size(3), "a block's [Hkv, bs, D] contiguous");
+  TORCH_CHECK(block_tables.is_contiguous() && kd.is_contiguous() && vd.is_contiguous() &&
+              kd.numel() == block_tables.numel() * per && vd.numel() == kd.numel(), "kd / vd [entries, Hkv, bs, D]");
+  const int rc = llmd_kv_dequant_gather(k_cache.data_ptr(), v_cache.data_ptr(), k_cache.stride(0),
+                                        block_tables.data_ptr<int>(), (int)block_tables.numel(),
+                                        (int)k_cache.size(0), (int)per, kd.data_ptr(), vd.data_ptr(), cur_stream());
+  TORCH_CHECK(rc == 0, "kv_dequant_gather failed: ", rc);
+}
+
 void paged_prefill(torch::Tensor out, torch::Tensor q, torch::Tensor k_cache,
                    torch::Tensor v_cache, torch::Tensor block_tables, torch::Tensor q_start,
                    torch::Tensor q_len, torch::Tensor ctx_len, torch::Tensor items, int64_t Hq,
@@ -1212,6 +1234,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {  // _C, or _C_debug (llmd_amd/build.p
   m.def("gated_act", &gated_act);
   m.def("paged_decode", &paged_decode);
   m.def("paged_prefill", &paged_prefill);
+  m.def("kv_dequant_gather", &kv_dequant_gather);
   m.def("prefill_tokens_per_item", [](int64_t Hq, int64_t Hkv, int64_t D, int64_t bs, bool fp8) {
     return llmd_prefill_tokens_per_item((int)Hq, (int)Hkv, (int)D, (int)bs, fp8 ? 1 : 0);
   });

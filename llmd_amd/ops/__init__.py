@@ -386,6 +386,27 @@ def build_prefill_items(q_len: list[int], ctx_len: list[int], tpi: int) -> list[
     return [(s, t0) for _, s, t0 in items]
 
 
+# fp8-KV prefill through a bf16 copy of the step's blocks (kv_dequant_gather) and the bf16 v2 kernel
+# instead of the fp8 v1 kernel (LLMD_PREFILL_FP8_VIA_BF16=0: the v1 fp8 kernel)
+PREFILL_FP8_VIA_BF16 = os.environ.get("LLMD_PREFILL_FP8_VIA_BF16", "1") == "1"
+
+
+def kv_dequant_gather(k_cache, v_cache, block_tables):
+    """(k, v, table): the blocks ``block_tables`` [S, maxb] names in an fp8 paged cache [blocks, Hkv,
+    bs, D], widened exactly to bf16 into dense copies [S * maxb, Hkv, bs, D] and the identity table
+    over them (padding entries copy block 0, never read)."""
+    S, mb = block_tables.shape
+    shape = (S * mb,) + tuple(k_cache.shape[1:])
+    if not _gpu(k_cache):
+        ids = block_tables.reshape(-1).clamp(0, k_cache.shape[0] - 1).long()
+        return (k_cache[ids].to(torch.bfloat16), v_cache[ids].to(torch.bfloat16),
+                torch.arange(S * mb, dtype=torch.int32).view(S, mb))
+    kd = torch.empty(shape, dtype=torch.bfloat16, device=k_cache.device)
+    vd = torch.empty(shape, dtype=torch.bfloat16, device=k_cache.device)
+    native().kv_dequant_gather(k_cache, v_cache, block_tables.contiguous(), kd, vd)
+    return kd, vd, torch.arange(S * mb, dtype=torch.int32, device=k_cache.device).view(S, mb)
+
+
 def paged_prefill(q, k_cache, v_cache, block_tables, q_start, q_len, ctx_len, Hq, Hkv, D, scale,
                   window=0, sinks=None, items=None, out=None, k_scale=1.0, v_scale=1.0):
     if not _gpu(q):
@@ -397,6 +418,9 @@ def paged_prefill(q, k_cache, v_cache, block_tables, q_start, q_len, ctx_len, Hq
         return r
     if out is None:
         out = torch.empty(q.shape[0], Hq * D, dtype=q.dtype, device=q.device)
+    if (PREFILL_FP8_VIA_BF16 and k_cache.dtype == torch.float8_e4m3fn and k_cache.shape[-2] >= 16
+            and D in (64, 128)):
+        k_cache, v_cache, block_tables = kv_dequant_gather(k_cache, v_cache, block_tables)
     if items is None:
         tpi = prefill_tokens_per_item(Hq, Hkv, D, k_cache.shape[-2], k_cache.dtype == torch.float8_e4m3fn)
         it = build_prefill_items(q_len.tolist(), ctx_len.tolist(), tpi)

@@ -119,8 +119,12 @@ def test_paged_decode_fp8_window_sinks():
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("via_bf16", [True, False])
 @pytest.mark.parametrize("Hq,Hkv,D", [(64, 8, 128), (32, 8, 64), (16, 8, 128)])
-def test_paged_prefill_fp8(Hq, Hkv, D):
+def test_paged_prefill_fp8(Hq, Hkv, D, via_bf16, monkeypatch):
+    """fp8 KV prefill: through a bf16 copy of the step's blocks + the bf16 v2 kernel (default) and
+    the fp8 v1 kernel, both against the fp32 reference on the same scaled caches."""
+    monkeypatch.setattr(ops, "PREFILL_FP8_VIA_BF16", via_bf16)
     dev = "cuda"
     shapes = [(1, 1), (37, 37), (200, 200), (130, 1000), (513, 700)]
     ctx = [c for _, c in shapes]
@@ -135,6 +139,20 @@ def test_paged_prefill_fp8(Hq, Hkv, D):
     r = ref.paged_prefill(q, kc, vc, bt, *args, Hq, Hkv, D, 1 / math.sqrt(D), k_scale=ks, v_scale=vs)
     o = ops.paged_prefill(q, kc, vc, bt, *args, Hq, Hkv, D, 1 / math.sqrt(D), k_scale=ks, v_scale=vs)
     _close(o, r)
+
+
+def test_kv_dequant_gather_cpu_widens_exactly():
+    """The CPU form of the gather (the GPU kernel's contract): entry e of the table -> row e, e4m3
+    widened exactly, padding entries (-1) -> block 0, identity table over the copy."""
+    torch.manual_seed(0)
+    kc = (torch.randn(6, 2, 16, 64) * 3).to(ops.FP8)
+    vc = (torch.randn(6, 2, 16, 64) * 3).to(ops.FP8)
+    bt = torch.tensor([[4, 1, -1], [2, 5, 0]], dtype=torch.int32)
+    kd, vd, t2 = ops.kv_dequant_gather(kc, vc, bt)
+    assert kd.dtype == torch.bfloat16 and kd.shape == (6, 2, 16, 64)
+    assert torch.equal(kd[0].float(), kc[4].float()) and torch.equal(vd[4].float(), vc[5].float())
+    assert torch.equal(kd[2].float(), kc[0].float())
+    assert torch.equal(t2, torch.arange(6, dtype=torch.int32).view(2, 3))
 
 
 def test_fp8_linear_cpu_matches_fp32():
