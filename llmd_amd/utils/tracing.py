@@ -120,6 +120,10 @@ class _SpanCtx:
             return None
         parent = _current.get()
         if parent is not None:
+            if not parent.sampled and not _TRACE_ALL and _otel_tracer is None:
+                # a child of an unsampled trace is never recorded or exported: skip the Span (ids,
+                # attrs, context var) - the EPP opens several per decision (~1 us each)
+                return None
             tid, pid, sampled = parent.trace_id, parent.span_id, parent.sampled
         else:
             ext = parse_traceparent(self.tp)
