@@ -681,6 +681,17 @@ MOE_FP8_V4 = os.environ.get("LLMD_MOE_FP8_V4", "1") == "1"
 MOE_FP8_V8 = os.environ.get("LLMD_MOE_FP8_V8", "1") == "1"
 
 
+def moe_tile_version(kind: str, K: int) -> int:
+    """Which expert-tile GEMM runs a prefill-sized grouped GEMM of reduction depth K: 8 = the
+    persistent form (csrc/ops/moe8.hip; needs >= 4 K-steps: 128-deep fp8, 64-deep bf16), else the
+    one-workgroup-per-tile v4 (moe4.hip). bf16 takes v8 only for K <= MOE_BF16_V8_MAX_K: those tiles
+    run at the power cap, so hiding the per-tile cost pays only where K-loops are short
+    (profiles/moe_gemm_v8_r6.txt)."""
+    if kind == "fp8":
+        return 8 if MOE_FP8_V8 and K >= 512 else 4
+    return 8 if MOE_BF16_V8 and 256 <= K <= MOE_BF16_V8_MAX_K else 4
+
+
 class Fp8Rows:
     """Activation rows already quantised to block fp8 (e4m3 ``q`` [T, dp] with
     dp = d padded to 128 and zeros past d, fp32 group scales ``s`` [T, dp/128]):
@@ -761,9 +772,7 @@ def moe_experts_fp8(x, ids, wts, w1q, w1s, w2q, w2s, act=0, alpha=1.702, limit=7
     elif v4:
         # v4: PGR2 4-wave tiles, A rows and their act scales gathered by the LDS-DMA (csrc/ops/moe4.hip)
         h = torch.empty(max_p, F, dtype=torch.bfloat16, device=dev)
-        # v8: the persistent form (K-step stream across tiles, epilogue from registers; >= 4 K-steps)
-        v1 = 8 if MOE_FP8_V8 and Kp1 >= 512 else 4
-        v2 = 8 if MOE_FP8_V8 and Kp2 >= 512 else 4
+        v1, v2 = moe_tile_version("fp8", Kp1), moe_tile_version("fp8", Kp2)
         C.moe_gemm4_fp8(xq, xs, k, sorted_ids, tile_e, w1q, w1s, h, 1, act, alpha, limit, False, b1, bm, v1, total)
         hq, hs = _quant_groups_padded(h, Kp2, total)  # slots past the last real tile are never read
         y = torch.empty(max_p, d, dtype=torch.bfloat16, device=dev)
@@ -862,10 +871,7 @@ def moe_experts(x, ids, wts, w1, w2, act=0, alpha=1.702, limit=7.0, out=None, b1
     y = torch.empty(max_p, d, dtype=x.dtype, device=dev)
     if v4:
         # v4: the dense prefill GEMM's 4-wave PGR2 structure, rows gathered by the LDS-DMA (csrc/ops/moe4.hip)
-        # (v8: the persistent form, csrc/ops/moe8.hip, for K <= MOE_BF16_V8_MAX_K: the bf16 tiles run at
-        # the power cap, so hiding the per-tile cost pays only where K-loops are short)
-        v1 = 8 if MOE_BF16_V8 and 256 <= w1.shape[2] <= MOE_BF16_V8_MAX_K else 4
-        v2 = 8 if MOE_BF16_V8 and 256 <= w2.shape[2] <= MOE_BF16_V8_MAX_K else 4
+        v1, v2 = moe_tile_version("bf16", w1.shape[2]), moe_tile_version("bf16", w2.shape[2])
         C.moe_gemm4(x, k, sorted_ids, tile_e, w1, h, 1, act, alpha, limit, False, b1, bm, v1, total)
         C.moe_gemm4(h, 1, sorted_ids, tile_e, w2, y, 0, 0, 0.0, 0.0, True, b2, bm, v2, total)
     else:

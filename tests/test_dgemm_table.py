@@ -49,3 +49,15 @@ def test_mgemm_table_entries_and_buckets():
     assert ops.mgemm_choice(129, 5120, 8192) == MGEMM_TABLE[(192, 5120, 8192)][0]
     assert ops.mgemm_choice(257, 5120, 8192) is None
     assert ops.mgemm_choice(64, 1234, 4096) is None
+
+
+def test_moe_tile_version_choice(monkeypatch):
+    """Persistent expert-tile GEMM (moe8) choice: fp8 from 4 K-steps of 128, bf16 only for 4 .. 4096-deep
+    K (gpt-oss 2880 yes, DeepSeek gate/up 7168 no), both switchable off."""
+    assert ops.moe_tile_version("fp8", 2944) == 8 and ops.moe_tile_version("fp8", 7168) == 8
+    assert ops.moe_tile_version("fp8", 384) == 4
+    assert ops.moe_tile_version("bf16", 2880) == 8 and ops.moe_tile_version("bf16", 2048) == 8
+    assert ops.moe_tile_version("bf16", 7168) == 4 and ops.moe_tile_version("bf16", 192) == 4
+    monkeypatch.setattr(ops, "MOE_FP8_V8", False)
+    monkeypatch.setattr(ops, "MOE_BF16_V8", False)
+    assert ops.moe_tile_version("fp8", 2944) == 4 and ops.moe_tile_version("bf16", 2880) == 4
