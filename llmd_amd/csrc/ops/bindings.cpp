@@ -992,6 +992,43 @@ void moe_gemm4_fp8(torch::Tensor X, torch::Tensor xs, int64_t topk, torch::Tenso
   TORCH_CHECK(rc == 0, "moe_gemm4_fp8 failed: ", rc);
 }
 
+extern "C" int llmd_moe_gemm8_mxfp4(const void*, int64_t, const float*, int64_t, int, const int*, const int*,
+                                    const int*, int, const void*, int64_t, const void*, int64_t, int, int, void*,
+                                    int64_t, int, int, float, float, int, const void*, int64_t, int, hipStream_t);
+
+// MXFP4 experts on the persistent tile GEMM (csrc/ops/moe8.hip): W [E, N, K/2] packed e2m1, wsc [E, N, K/32]
+// E8M0, X [rows, K] e4m3 with power-of-two (token, 128) scales xs
+void moe_gemm8_mxfp4(torch::Tensor X, torch::Tensor xs, int64_t topk, torch::Tensor sorted_ids,
+                     torch::Tensor tile_expert, torch::Tensor W, torch::Tensor wsc, torch::Tensor Y, int64_t mode,
+                     int64_t act, double alpha, double limit, bool a_rows_are_slots,
+                     c10::optional<torch::Tensor> bias, int64_t tile_m, torch::Tensor total) {
+  const c10::hip::OptionalHIPGuard device_guard(dev_of(X));
+  CHECK_CUDA(X); CHECK_DT(X, at::kFloat8_e4m3fn); CHECK_DT(W, at::kByte); CHECK_DT(wsc, at::kByte); CHECK_BF16(Y);
+  CHECK_INNER(X); CHECK_INNER(Y); CHECK_DT(xs, at::kFloat); CHECK_DT(total, at::kInt);
+  TORCH_CHECK(W.dim() == 3 && W.is_contiguous() && wsc.dim() == 3 && wsc.is_contiguous(), "W / wsc contiguous [E, N, .]");
+  const int E = W.size(0), N = W.size(1), K = 2 * W.size(2);
+  TORCH_CHECK(wsc.size(0) == E && wsc.size(1) == N && wsc.size(2) == K / 32, "wsc [E, N, K/32]");
+  TORCH_CHECK(X.size(1) == K && K % 128 == 0 && K / 128 >= 4 && X.stride(0) % 16 == 0, "moe_gemm8_mxfp4: K");
+  TORCH_CHECK(tile_m == 256 || tile_m == 192, "moe_gemm8_mxfp4: tile_m 256 or 192");
+  TORCH_CHECK(xs.dim() == 2 && xs.size(0) >= X.size(0) && xs.size(1) >= K / 128 && xs.stride(1) == 1, "xs [rows, K/128]");
+  const int bm = (int)tile_m;
+  const int P = sorted_ids.numel();
+  TORCH_CHECK(P % bm == 0 && tile_expert.numel() >= P / bm && Y.size(0) >= P, "moe_gemm8_mxfp4: rows");
+  TORCH_CHECK(Y.size(1) >= (mode == 1 ? N / 2 : N) && Y.stride(0) % 8 == 0, "moe_gemm8_mxfp4: Y width");
+  const void* bp = nullptr;
+  if (bias.has_value()) {
+    CHECK_BF16(bias.value());
+    TORCH_CHECK(bias->is_contiguous() && bias->numel() == (int64_t)E * N, "bias [E, N]");
+    bp = bias->data_ptr();
+  }
+  const int rc = llmd_moe_gemm8_mxfp4(X.data_ptr(), X.stride(0), xs.data_ptr<float>(), xs.stride(0), topk,
+                                      sorted_ids.data_ptr<int>(), tile_expert.data_ptr<int>(), total.data_ptr<int>(),
+                                      P / bm, W.data_ptr(), W.stride(0), wsc.data_ptr(), wsc.stride(0), N, K,
+                                      Y.data_ptr(), Y.stride(0), mode, act, (float)alpha, (float)limit,
+                                      a_rows_are_slots ? 1 : 0, bp, X.size(0), bm, cur_stream());
+  TORCH_CHECK(rc == 0, "moe_gemm8_mxfp4 failed: ", rc);
+}
+
 void moe_combine(torch::Tensor Y, torch::Tensor inv, torch::Tensor w, int64_t topk, torch::Tensor out) {
   const c10::hip::OptionalHIPGuard device_guard(dev_of(Y));
   CHECK_CUDA(Y); CHECK_BF16(Y); CHECK_BF16(out); CHECK_DT(inv, at::kInt); CHECK_DT(w, at::kFloat);
@@ -1235,6 +1272,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {  // _C, or _C_debug (llmd_amd/build.p
   m.def("paged_decode", &paged_decode);
   m.def("paged_prefill", &paged_prefill);
   m.def("kv_dequant_gather", &kv_dequant_gather);
+  m.def("moe_gemm8_mxfp4", &moe_gemm8_mxfp4);
   m.def("prefill_tokens_per_item", [](int64_t Hq, int64_t Hkv, int64_t D, int64_t bs, bool fp8) {
     return llmd_prefill_tokens_per_item((int)Hq, (int)Hkv, (int)D, (int)bs, fp8 ? 1 : 0);
   });

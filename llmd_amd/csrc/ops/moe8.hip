@@ -414,6 +414,382 @@ __global__ __launch_bounds__(P8_NT, 1) void moe_gemm8_fp8_kernel(
 }
 
 
+typedef int i32x4_t __attribute__((ext_vector_type(4)));
+
+// D(32x32) += (W 32x64 e2m1 x 2^(sw-127) per 32-block) . (A 64x32 e4m3 x 2^(sa-127)): MXFP4 weights as the
+// MFMA's A operand (cbsz:4 = e2m1, 4 VGPRs), fp8 activations as B
+__device__ __forceinline__ void p4_mfma(f32x16_t& acc, const i32x4_t& a, const i32x8_t& b, int sa, int sb) {
+  asm volatile("v_mfma_scale_f32_32x32x64_f8f6f4 %0, %1, %2, %0, %3, %4 op_sel_hi:[0,0,0] cbsz:4"
+               : "+a"(acc) : "v"(a), "v"(b), "v"(sa), "v"(sb));
+}
+
+// MXFP4 form (gpt-oss ships its experts as OCP MXFP4): the fp8 kernel above with e2m1 weights - half
+// the weight bytes per K-step (64 B per row: 4 DMA pieces per wave instead of 8) and an E8M0 scale per
+// (row, 32-element block) DMA'd with each K-step (one 4-B piece per wave) and handed to the MFMA per
+// lane and fragment; activations stay block-fp8 (e4m3, power-of-two (token, 128) scales).
+template <int MODE, int TBM>
+__global__ __launch_bounds__(P8_NT, 1) void moe_gemm8_mxfp4_kernel(
+    const uint8_t* __restrict__ X, int64_t x_stride, const float* __restrict__ xs, int64_t xs_stride, int topk,
+    const int* __restrict__ sorted_ids, const int* __restrict__ tile_expert, const int* __restrict__ total_p,
+    int max_mtiles, int ntn, int order, const uint8_t* __restrict__ W, int64_t w_expert_stride,
+    const uint8_t* __restrict__ wsc, int64_t wsc_expert_stride, int N, int K,
+    uint16_t* __restrict__ Y, int64_t y_stride, int act, float alpha, float limit, int a_rows_are_slots,
+    const uint16_t* __restrict__ bias) {
+  static_assert(TBM == 256 || TBM == 192, "tile rows");
+  constexpr int MB = TBM / 64;                 // 32-row A blocks per wave
+  constexpr int NA = 2 * MB;                   // A DMA pieces per wave per K-step
+  constexpr int OPA = TBM * 128;               // A bytes per K-step
+  constexpr int SCB = TBM * 4 + 256;           // act scales of a K-step (+ the 192 form's overhang)
+  constexpr int WB = 256 * 64;                 // e2m1 W bytes per K-step (256 rows x 128 codes)
+  constexpr int WSB = 256 * 4;                 // E8M0 W scales per K-step (4 per row)
+  constexpr int BUF = OPA + WB + WSB + SCB;
+  constexpr int BSO = 2 * BUF;                 // bias [2 tile slots][256 columns] bf16
+  constexpr int LDSB = BSO + 2 * 512;
+  constexpr int NPC = NA + 4 + 1 + 1;          // DMA ops per wave per K-step: A, W, W scales, act scales (14 / 12)
+  constexpr int NMF = 4 * MB;                  // MFMAs per k-substep
+  constexpr int SROWS = TBM / 4;               // act-scale rows per wave
+  constexpr int NQ = TBM / 64;                 // 64-slot groups of a tile (valid-row ballot)
+  __shared__ __attribute__((aligned(1024))) char lds[LDSB];  // the ONLY LDS object
+
+  const int nk = K / 128;
+  // this workgroup's work items: chunk [c0, c1) of XCD x, items c0 + s, c0 + s + S, ...
+  const int n_items = min(__builtin_amdgcn_readfirstlane(total_p[0]) / TBM, max_mtiles) * ntn;
+  // order 1: items b, b + G, b + 2 G, .. (the v4 grid's order: concurrent items spread over the XCDs)
+  const int xcd = blockIdx.x & 7;
+  const int S = order ? (int)gridDim.x : (int)(gridDim.x >> 3);
+  const int c0 = order ? 0 : (int)((int64_t)n_items * xcd / 8);
+  const int c1 = order ? n_items : (int)((int64_t)n_items * (xcd + 1) / 8);
+  int item = c0 + (int)(order ? blockIdx.x : blockIdx.x >> 3);
+  if (item >= c1) return;
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = w >> 1, wc = w & 1;
+  const int l32 = lane & 31, h = lane >> 5;
+
+  const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc((void*)X, 0, 0x7fffffff, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)xs, 0, 0x7fffffff, 0x00020000);
+
+  // ---- per-tile state (current tile; the next tile's is built at the end of step nk - 3)
+  int m0 = 0, n0 = 0, e = 0, nvalid = 0;
+  __amdgpu_buffer_rsrc_t rw;
+  __amdgpu_buffer_rsrc_t rsw;
+  uint32_t va[8], vw[4], vs, vsw;  // fixed-size arrays (a template-sized one can lose the launch stub, build.py)
+  int sid_a[8], sid_s, sid_v[4], e_ld;  // a tile's metadata, loaded ahead of build()
+  auto meta_load = [&](int it) {
+    const int mm = (it / ntn) * TBM;
+    e_ld = tile_expert[it / ntn];
+#pragma unroll
+    for (int j = 0; j < NA; ++j) sid_a[j] = sorted_ids[mm + 8 * (NA * w + j) + (lane >> 3)];
+    sid_s = sorted_ids[mm + min(SROWS * w + lane, TBM - 1)];
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) sid_v[q] = sorted_ids[mm + 64 * q + lane];
+  };
+  auto build = [&](int it) {
+    const int mt = it / ntn;
+    m0 = mt * TBM;
+    n0 = (it - mt * ntn) * P8_BN;
+    e = __builtin_amdgcn_readfirstlane(e_ld);
+    int nv = 0;
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) nv += __popcll(__ballot(sid_v[q] >= 0));
+    nvalid = __builtin_amdgcn_readfirstlane(nv);
+    if (e < 0) {  // not a real tile (the item list is the real count; defensive): read zeros, store nothing
+      e = 0;
+      nvalid = 0;
+    }
+    rw = __builtin_amdgcn_make_buffer_rsrc((void*)(W + (int64_t)e * w_expert_stride), 0, 0x7fffffff, 0x00020000);
+    rsw = __builtin_amdgcn_make_buffer_rsrc((void*)(wsc + (int64_t)e * wsc_expert_stride), 0, 0x7fffffff, 0x00020000);
+#pragma unroll
+    for (int j = 0; j < NA; ++j) {
+      const int row = 8 * (NA * w + j) + (lane >> 3);
+      const int c = (lane & 7) ^ ((row >> 1) & 7);
+      const int sid = sid_a[j];
+      const int tok = a_rows_are_slots ? m0 + row : sid / topk;
+      va[j] = sid < 0 || nvalid == 0 ? P8_OOB : (uint32_t)((int64_t)tok * x_stride + c * 16);
+    }
+    // W piece j of wave w: rows 64 w + 16 j + (lane >> 2), 64-B row = 4 chunks of 16 B, LDS slot
+    // lane & 3 <- chunk (lane & 3) ^ ((row >> 2) & 3) (conflict-free 16-row fragment reads)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int row = 64 * w + 16 * j + (lane >> 2);
+      const int c = (lane & 3) ^ ((row >> 2) & 3);
+      vw[j] = n0 + row < N ? (uint32_t)((int64_t)(n0 + row) * (K / 2) + c * 16) : P8_OOB;
+    }
+    // W scales: this lane's row 64 w + lane, 4 E8M0 bytes (the K-step's four 32-blocks)
+    vsw = n0 + 64 * w + lane < N ? (uint32_t)((int64_t)(n0 + 64 * w + lane) * (K / 32)) : P8_OOB;
+    {
+      const int row = min(SROWS * w + lane, TBM - 1);
+      const int tok = sid_s < 0 ? 0 : (a_rows_are_slots ? m0 + row : sid_s / topk);
+      vs = (uint32_t)((int64_t)tok * xs_stride * 4);
+    }
+  };
+  // the tile's bias (waves 2 / 3: columns n0 + 128 (w - 2) + [0, 128)) into LDS slot `sl`
+  auto side_dma = [&](int sl) {
+    if (w >= 2 && bias != nullptr) {
+      // 128 bf16 columns = 64 lanes x 4 B; columns past N read zeros (never stored)
+      const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc(
+          (void*)(bias + (int64_t)e * N), 0, (uint32_t)N * 2, 0x00020000);
+      const int col = n0 + 128 * (w - 2) + 2 * lane;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(
+          rb, (__attribute__((address_space(3))) void*)(lds + BSO + sl * 512 + (w - 2) * 256), 4,
+          (uint32_t)(col * 2), 0, 0, 0);
+    }
+  };
+  // op 0 = A piece j, 1 = W piece j (< 4), 2 = act scales, 3 = W scales
+  auto dma = [&](int bsel, int kc, int j, int op) {
+    char* buf = lds + bsel * BUF;
+    if (op == 2)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)(buf + OPA + WB + WSB + w * SROWS * 4),
+                                               4, vs, (uint32_t)(kc * 4), 0, 0);
+    else if (op == 3)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsw, (__attribute__((address_space(3))) void*)(buf + OPA + WB + w * 256),
+                                               4, vsw, (uint32_t)(kc * 4), 0, 0);
+    else if (op == 1)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rw, (__attribute__((address_space(3))) void*)(buf + OPA + (4 * w + j) * 1024),
+                                               16, vw[j], (uint32_t)(kc * 64), 0, 0);
+    else
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, (__attribute__((address_space(3))) void*)(buf + (NA * w + j) * 1024),
+                                               16, va[j], (uint32_t)(kc * 128), 0, 0);
+  };
+  // fragment of 32-row block b, k-substep s: lane row 32 b + l32, chunks 4 s + 2 h and 4 s + 2 h + 1
+  auto frag = [&](const char* base, int b, int s) {
+    const int row = 32 * b + l32;
+    const int f = (row >> 1) & 7;
+    const char* rp = base + row * 128;
+    const u32x4_t lo = *reinterpret_cast<const u32x4_t*>(rp + (((4 * s + 2 * h) ^ f) * 16));
+    const u32x4_t hi = *reinterpret_cast<const u32x4_t*>(rp + (((4 * s + 2 * h + 1) ^ f) * 16));
+    return i32x8_t{(int)lo[0], (int)lo[1], (int)lo[2], (int)lo[3], (int)hi[0], (int)hi[1], (int)hi[2], (int)hi[3]};
+  };
+  // W fragment of 32-row block b, k-substep s: row 32 b + l32 of this wave's 128, 16 B = codes
+  // [64 s + 32 h, +32) = chunk 2 s + h; its E8M0 scale: byte 2 s + h of the row's 4
+  auto wfrag = [&](const char* base, int b, int s) {
+    const int row = 32 * b + l32;
+    const u32x4_t v = *reinterpret_cast<const u32x4_t*>(base + row * 64 + (((2 * s + h) ^ ((row >> 2) & 3)) * 16));
+    return i32x4_t{(int)v[0], (int)v[1], (int)v[2], (int)v[3]};
+  };
+  auto wscale = [&](const char* base, int b, int s) {
+    return (int)*reinterpret_cast<const uint8_t*>(base + (32 * b + l32) * 4 + 2 * s + h);
+  };
+  const int a_base = wr * (TBM / 2) * 128, w_base = OPA + wc * 128 * 64, ws_base = OPA + WB + wc * 128 * 4;
+  const int s_base = OPA + WB + WSB + wr * (TBM / 2) * 4;
+
+  f32x16_t acc[4][MB];  // [W n-block j][A m-block i]
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int i = 0; i < MB; ++i) acc[j][i] = f32x16_t{};
+  i32x4_t fw0[4], fw1[4];
+  i32x8_t fa0[MB], fa1[MB];
+  int sa[MB], sw0[4], sw1[4];
+  float nsf[MB];
+
+  // ---- prologue of the first tile: metadata, side DMAs into slot 0, stream steps 0 and 1
+  meta_load(item);
+  build(item);
+  int slot = 0;  // LDS slot of the current tile's bias
+  side_dma(0);
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+#pragma unroll
+    for (int j = 0; j < NA; ++j) dma(s, s, j, 0);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) dma(s, s, j, 1);
+    dma(s, s, 0, 2);
+    dma(s, s, 0, 3);
+  }
+  if constexpr (NPC == 14) asm volatile("s_waitcnt vmcnt(14)" ::: "memory");  // side DMA + step 0 landed
+  else asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+  p8_bar();
+#pragma unroll
+  for (int b = 0; b < 4; ++b) {
+    fw0[b] = wfrag(lds + w_base, b, 0);
+    sw0[b] = wscale(lds + ws_base, b, 0);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+#pragma unroll
+  for (int b = 0; b < MB; ++b) {
+    fa0[b] = frag(lds + a_base, b, 0);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+#pragma unroll
+  for (int b = 0; b < MB; ++b) sa[b] = e8m0_of(*reinterpret_cast<const float*>(lds + s_base + (32 * b + l32) * 4));
+  __builtin_amdgcn_s_waitcnt(0xC07F);
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_nop 4" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+
+  // one K-step. PH 0: a step of this tile's own stream; 1 (step nk - 3): the next tile's metadata
+  // loads first, its descriptors built after this step's (last own) DMAs; 2 (nk - 2): the next
+  // tile's weight-scale / bias DMAs, then its step 0; 3 (nk - 1): its step 1, and the step-0
+  // fragments / scales read for the next K loop. With no next tile the "next" one is the current
+  // one again (harmless reloads into buffers nobody reads): the step has no data-dependent branch.
+  int gs = 0;  // global stream step (LDS buffer parity)
+  auto step = [&](auto PH_, int kt, int nx) {
+    constexpr int PH = decltype(PH_)::value;
+    const int bsel = gs & 1;
+    const char* cur = lds + bsel * BUF;
+    const char* nxt = lds + (bsel ^ 1) * BUF;
+    const int kc = PH <= 1 ? kt + 2 : PH - 2;  // stream step kt + 2 (own, or the next tile's 0 / 1)
+    if constexpr (PH == 1) meta_load(nx);  // complete by this step's counted wait (older than its DMAs)
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int t = 0; t < NMF; ++t) {
+      const int j = t / MB, i = t % MB;
+      p4_mfma(acc[j][i], fw0[j], fa0[i], sw0[j], sa[i]);
+      if (t < 4) {
+        fw1[t] = wfrag(cur + w_base, t, 1);
+        sw1[t] = wscale(cur + ws_base, t, 1);
+      } else if (t < 4 + MB) {
+        fa1[t - 4] = frag(cur + a_base, t - 4, 1);
+      } else if (t == 4 + MB + 1) {
+        __builtin_amdgcn_s_waitcnt(0xC07F);
+        p8_bar();
+        if constexpr (PH == 2) side_dma(slot ^ 1);  // older than this step's DMAs
+      } else if (t > 4 + MB + 1 && t < 4 + MB + 2 + MB) {
+        const int q = t - (4 + MB + 2);
+        dma(bsel, kc, 2 * q, 0);
+        dma(bsel, kc, 2 * q + 1, 0);
+        if (4 + 2 * MB + 2 >= NMF && t == NMF - 1) dma(bsel, kc, 0, 2);  // 192 rows: the act-scale piece
+      } else if (t == 4 + 2 * MB + 2) {
+        dma(bsel, kc, 0, 2);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+#pragma unroll
+    for (int t = 0; t < NMF; ++t) {
+      const int j = t / MB, i = t % MB;
+      p4_mfma(acc[j][i], fw1[j], fa1[i], sw1[j], sa[i]);
+      if (t < 4) {
+        dma(bsel, kc, t, 1);
+      } else if (t == 4) {
+        dma(bsel, kc, 0, 3);
+      } else if (t == 8) {
+        if constexpr (NPC == 14) asm volatile("s_waitcnt vmcnt(14)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+        p8_bar();
+      } else if (t == 9) {
+        // the next stream step's act scales and its substep-0 W fragments with their scales
+#pragma unroll
+        for (int b = 0; b < MB; ++b) nsf[b] = *reinterpret_cast<const float*>(nxt + s_base + (32 * b + l32) * 4);
+        fw0[0] = wfrag(nxt + w_base, 0, 0);
+        sw0[0] = wscale(nxt + ws_base, 0, 0);
+        if constexpr (MB == 3) {
+          fw0[1] = wfrag(nxt + w_base, 1, 0);
+          sw0[1] = wscale(nxt + ws_base, 1, 0);
+        }
+      } else if constexpr (MB == 4) {
+        if (t < 13) {
+          fw0[t - 9] = wfrag(nxt + w_base, t - 9, 0);
+          sw0[t - 9] = wscale(nxt + ws_base, t - 9, 0);
+        } else if (t < 15) {
+          fa0[2 * (t - 13)] = frag(nxt + a_base, 2 * (t - 13), 0);
+          fa0[2 * (t - 13) + 1] = frag(nxt + a_base, 2 * (t - 13) + 1, 0);
+        }
+      } else {
+        if (t == 10) {
+          fw0[2] = wfrag(nxt + w_base, 2, 0);
+          fw0[3] = wfrag(nxt + w_base, 3, 0);
+          sw0[2] = wscale(nxt + ws_base, 2, 0);
+          sw0[3] = wscale(nxt + ws_base, 3, 0);
+        } else if (t == 11) {
+#pragma unroll
+          for (int b = 0; b < MB; ++b) fa0[b] = frag(nxt + a_base, b, 0);
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+#pragma unroll
+    for (int b = 0; b < MB; ++b) sa[b] = e8m0_of(nsf[b]);
+    // the next tile's descriptors: every DMA of this tile's own steps has been issued
+    if constexpr (PH == 1) build(nx);
+    // drain at the end of every step (asm MFMAs: hipcc does not model their latency)
+    asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    ++gs;
+  };
+  while (true) {
+    const int nxt_item = item + S;
+    const bool has_next = nxt_item < c1;
+    const int nx = has_next ? nxt_item : item;
+    // the current tile's epilogue parameters (build() overwrites the state at step nk - 3)
+    const int cm0 = m0, cn0 = n0, cnv = nvalid, cslot = slot;
+    for (int kt = 0; kt < nk - 3; ++kt) step(std::integral_constant<int, 0>{}, kt, nx);
+    step(std::integral_constant<int, 1>{}, nk - 3, nx);
+    step(std::integral_constant<int, 2>{}, nk - 2, nx);
+    step(std::integral_constant<int, 3>{}, nk - 1, nx);
+    __builtin_amdgcn_sched_barrier(0);
+
+    // ---- epilogue of the current tile straight from the accumulators:
+    // acc[j][i][4 g + q] = C[m][n], m = wr*TBM/2 + 32 i + l32, n = wc*128 + 32 j + 8 g + 4 h + q
+    const int ncol0 = cn0 + wc * 128;
+    const char* bl = lds + BSO + cslot * 512 + wc * 256;  // this wave's 128 bias columns (bf16)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      float bv[4][4];
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        u32x2_t raw = u32x2_t{0u, 0u};
+        if (bias != nullptr) raw = *reinterpret_cast<const u32x2_t*>(bl + (32 * j + 8 * g + 4 * h) * 2);
+        bv[g][0] = __uint_as_float(raw[0] << 16);
+        bv[g][1] = __uint_as_float(raw[0] & 0xffff0000u);
+        bv[g][2] = __uint_as_float(raw[1] << 16);
+        bv[g][3] = __uint_as_float(raw[1] & 0xffff0000u);
+      }
+#pragma unroll
+      for (int i = 0; i < MB; ++i) {
+        const int m = wr * (TBM / 2) + 32 * i + l32;
+        const bool live = m < cnv;
+        uint16_t* yrow = Y + (int64_t)(cm0 + m) * y_stride;
+        float v[4][4];
+#pragma unroll
+        for (int g = 0; g < 4; ++g)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) v[g][q] = acc[j][i][4 * g + q] + bv[g][q];
+        if constexpr (MODE == 0) {
+#pragma unroll
+          for (int gp = 0; gp < 2; ++gp) {
+            const uint32_t a0 = p8_pack(v[2 * gp][0], v[2 * gp][1]), a1 = p8_pack(v[2 * gp][2], v[2 * gp][3]);
+            const uint32_t b0 = p8_pack(v[2 * gp + 1][0], v[2 * gp + 1][1]);
+            const uint32_t b1 = p8_pack(v[2 * gp + 1][2], v[2 * gp + 1][3]);
+            // lane h = 0 keeps column group 2 gp (its 4 columns + the partner's 4), h = 1 group 2 gp + 1
+            const uint32_t r0 = (uint32_t)__shfl_xor((int)(h ? a0 : b0), 32, 64);
+            const uint32_t r1 = (uint32_t)__shfl_xor((int)(h ? a1 : b1), 32, 64);
+            const u32x4_t o = h ? u32x4_t{r0, r1, b0, b1} : u32x4_t{a0, a1, r0, r1};
+            const int n = ncol0 + 32 * j + 8 * (2 * gp + h);
+            if (live && n < N) *reinterpret_cast<u32x4_t*>(yrow + n) = o;
+          }
+        } else {
+          uint32_t o[4];  // o[g]: outputs (n / 2) = wc*64 + 16 j + 4 g + 2 h + {0, 1}
+#pragma unroll
+          for (int g = 0; g < 4; ++g)
+            o[g] = p8_pack(p8_act(v[g][0], v[g][1], act, alpha, limit), p8_act(v[g][2], v[g][3], act, alpha, limit));
+          // lane h = 0 keeps outputs 0..7 of the 16 (groups 0, 1), h = 1 outputs 8..15 (groups 2, 3)
+          const uint32_t r0 = (uint32_t)__shfl_xor((int)(h ? o[0] : o[2]), 32, 64);
+          const uint32_t r1 = (uint32_t)__shfl_xor((int)(h ? o[1] : o[3]), 32, 64);
+          const u32x4_t ov = h ? u32x4_t{r0, o[2], r1, o[3]} : u32x4_t{o[0], r0, o[1], r1};
+          const int hc = ncol0 / 2 + 16 * j + 8 * h;
+          if (live && 2 * hc < N) *reinterpret_cast<u32x4_t*>(yrow + hc) = ov;
+        }
+      }
+    }
+    if (!has_next) break;
+    item = nxt_item;
+    slot ^= 1;
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int i = 0; i < MB; ++i) acc[j][i] = f32x16_t{};
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_nop 4" ::: "memory");  // accumulator writes -> MFMA srcC
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  // the last tile's dummy DMAs must land before the workgroup's LDS is released
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+}
+
+
+
 // bf16 form: the v4 bf16 tile loop (moe4.hip moe_gemm4_bf16_kernel: 16x16x32 bf16 MFMA, 64-deep
 // K-steps, MI = TBM / 32 A fragments per wave, NPC = MI + 8 DMA pieces per wave and step) in the
 // same persistent frame. No scales; the side DMA is the bias only (waves 2 / 3). Epilogue layout:
@@ -761,5 +1137,38 @@ extern "C" int llmd_moe_gemm8_bf16(const void* X, int64_t x_stride, int topk, co
     if (mode == 0) P8B_LAUNCH(0, 192); else P8B_LAUNCH(1, 192);
   }
 #undef P8B_LAUNCH
+  return (int)hipGetLastError();
+}
+
+// MXFP4 experts: X [rows, K] e4m3 with xs [rows, K / 128] power-of-two scales, W [E, N, K / 2] packed
+// e2m1 (element 2i in the low nibble), wsc [E, N, K / 32] E8M0. K % 128 == 0, K / 128 >= 4.
+extern "C" int llmd_moe_gemm8_mxfp4(const void* X, int64_t x_stride, const float* xs, int64_t xs_stride, int topk,
+                                    const int* sorted_ids, const int* tile_expert, const int* total_p, int num_tiles,
+                                    const void* W, int64_t w_expert_stride, const void* wsc, int64_t wsc_expert_stride,
+                                    int N, int K, void* Y, int64_t y_stride, int mode, int act, float alpha,
+                                    float limit, int a_rows_are_slots, const void* bias, int64_t x_rows, int tile_m,
+                                    hipStream_t st) {
+  if (K % 128 || K / 128 < 4 || x_stride % 16 || w_expert_stride % 16 || wsc_expert_stride % 4 || N % 8 ||
+      (mode == 1 && N % 16) || y_stride % 8 || total_p == nullptr)
+    return -1;
+  if (tile_m != 256 && tile_m != 192) return -1;
+  if (x_rows * x_stride + K > 0x7fffffffLL || (int64_t)N * K / 2 > 0x7fffffffLL || x_rows * xs_stride * 4 > 0x7fffffffLL)
+    return -2;
+  if (num_tiles == 0) return 0;
+  const int ntn = (N + P8_BN - 1) / P8_BN;
+  const int64_t upper = (int64_t)num_tiles * ntn;
+  const int grid = (int)std::min<int64_t>(p8_cus() / 8 * 8, (upper + 7) / 8 * 8);
+  const int order = p8_order();
+#define P4_LAUNCH(MODE_, TBM_)                                                                                      \
+  hipLaunchKernelGGL((moe_gemm8_mxfp4_kernel<MODE_, TBM_>), dim3(grid), dim3(P8_NT), 0, st, (const uint8_t*)X,      \
+                     x_stride, xs, xs_stride, topk, sorted_ids, tile_expert, total_p, num_tiles, ntn, order,         \
+                     (const uint8_t*)W, w_expert_stride, (const uint8_t*)wsc, wsc_expert_stride, N, K, (uint16_t*)Y, \
+                     y_stride, act, alpha, limit, a_rows_are_slots, (const uint16_t*)bias)
+  if (tile_m == 256) {
+    if (mode == 0) P4_LAUNCH(0, 256); else P4_LAUNCH(1, 256);
+  } else {
+    if (mode == 0) P4_LAUNCH(0, 192); else P4_LAUNCH(1, 192);
+  }
+#undef P4_LAUNCH
   return (int)hipGetLastError();
 }

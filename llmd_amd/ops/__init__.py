@@ -643,6 +643,109 @@ def dequant_fp8_block_weight(q: torch.Tensor, s: torch.Tensor, block: int = 128)
     return q.float() * full
 
 
+# ---------------------------------------------------------------- MXFP4 experts (OCP MX: e2m1 + E8M0 per 32)
+_E2M1 = (0.0, 0.5, 1.0, 1.5, 2.0, 3.0, 4.0, 6.0)
+
+
+def quant_mxfp4_weight(w: torch.Tensor):
+    """Expert weights [E, N, K] (K % 32 == 0) -> (packed e2m1 codes uint8 [E, N, K / 2]: element 2i in
+    the low nibble, 2i + 1 in the high one; E8M0 scales uint8 [E, N, K / 32]) - the OCP MXFP4 format
+    gpt-oss ships in. Per 32-element block the scale is the power of two that maps the block's amax
+    to <= 6 (the largest e2m1 magnitude); values round to the nearest e2m1 (ties away from zero)."""
+    E, N, K = w.shape
+    assert K % 32 == 0, "MXFP4 needs K % 32 == 0"
+    wf = w.float().view(E, N, K // 32, 32)
+    amax = wf.abs().amax(-1).clamp(min=2.0 ** -126)
+    e = torch.ceil(torch.log2(amax / 6.0)).clamp(-127, 127)
+    scale = torch.exp2(e)
+    x = (wf / scale[..., None]).clamp(-6.0, 6.0)
+    mag = x.abs()
+    grid = torch.tensor(_E2M1, device=w.device)
+    mids = (grid[1:] + grid[:-1]) / 2
+    code = torch.bucketize(mag, mids, right=True).to(torch.uint8)  # ties go up (away from zero)
+    code = code | ((x < 0) & (code > 0)).to(torch.uint8) << 3
+    code = code.view(E, N, K)
+    packed = (code[..., 0::2] | (code[..., 1::2] << 4)).contiguous()
+    return packed, (e + 127).to(torch.uint8).contiguous()
+
+
+def mxfp4_mfma_layout(q: torch.Tensor, inverse: bool = False) -> torch.Tensor:
+    """Packed e2m1 codes [.., K / 2] in the order the scaled MFMA reads them: with an e2m1 A operand,
+    lane (row, h) of a 64-deep k-substep holds K 16h .. 16h+15 and 32+16h .. 32+16h+15 (measured,
+    scripts/probes/fp4_layout_probe.hip), so every 32 bytes (64 codes) are stored as the 8-byte groups
+    [K0-15, K32-47, K16-31, K48-63]: one 16-B LDS read per lane then feeds the MFMA. Self-inverse."""
+    shp = q.shape
+    g = q.reshape(*shp[:-1], shp[-1] // 32, 4, 8)
+    return g[..., [0, 2, 1, 3], :].reshape(shp).contiguous()
+
+
+def dequant_mxfp4_weight(q: torch.Tensor, s: torch.Tensor, mfma_layout: bool = False) -> torch.Tensor:
+    """fp32 [E, N, K] of quant_mxfp4_weight's (codes, scales); ``mfma_layout``: codes in
+    mxfp4_mfma_layout order."""
+    if mfma_layout:
+        q = mxfp4_mfma_layout(q)
+    E, N, K2 = q.shape
+    lo, hi = (q & 0xF).long(), (q >> 4).long()
+    codes = torch.stack([lo, hi], -1).view(E, N, 2 * K2)
+    grid = torch.tensor(_E2M1, device=q.device)
+    v = grid[codes & 7] * torch.where(codes >= 8, -1.0, 1.0)
+    scale = torch.exp2(s.float() - 127).repeat_interleave(32, -1)
+    return v * scale
+
+
+def moe_experts_mxfp4(x, ids, wts, w1q, w1s, w2q, w2s, act=0, alpha=1.702, limit=7.0, out=None, b1=None, b2=None):
+    """MXFP4 routed experts (gpt-oss's own weight format): e2m1 weights with E8M0 scales per 32
+    elements (quant_mxfp4_weight, K padded to 128), activations quantised per (token, 128) group to
+    e4m3 with power-of-two scales, both GEMMs on the persistent expert-tile kernel (csrc/ops/moe8.hip
+    moe_gemm8_mxfp4_kernel: half the weight bytes of fp8, the scaled MFMA at the fp4 rate) at every
+    step size - its weight stream is halved, so it also covers decode-sized steps - and the gated
+    activation fused into GEMM 1, bf16 weighted combine. w1q [E, 2F, Kp1/2], w2q [E, d, Kp2/2], codes in
+    mxfp4_mfma_layout order (done once at load)."""
+    E, N1, Kp1 = w1q.shape[0], w1q.shape[1], 2 * w1q.shape[2]
+    d, Kp2 = w2q.shape[1], 2 * w2q.shape[2]
+    F = N1 // 2
+    if not _gpu(x):
+        xq, xs = quant_fp8_groups(x)
+        xd = (xq.float().view(x.shape[0], -1) * xs.repeat_interleave(128, 1)[:, :x.shape[1]]).to(torch.bfloat16)
+        w1 = dequant_mxfp4_weight(w1q, w1s, mfma_layout=True)[..., :x.shape[1]].to(torch.bfloat16)
+        w2 = dequant_mxfp4_weight(w2q, w2s, mfma_layout=True)[..., :F].to(torch.bfloat16)
+        r = ref.moe_forward(xd, ids, wts, w1, w2, act, alpha, limit, b1, b2)
+        if out is not None:
+            out.copy_(r)
+            return out
+        return r
+    C = native()
+    T = x.shape[0]
+    k = ids.shape[1]
+    bm = moe4_tile_rows(T * k, E)
+    n = T * k
+    max_p = ((n + E * (bm - 1)) + bm - 1) // bm * bm
+    dev = x.device
+    sorted_ids = torch.empty(max_p, dtype=torch.int32, device=dev)
+    tile_e = torch.empty(max_p // bm, dtype=torch.int32, device=dev)
+    offs = torch.empty(E + 1, dtype=torch.int32, device=dev)
+    total = torch.empty(1, dtype=torch.int32, device=dev)
+    inv = torch.empty(n, dtype=torch.int32, device=dev)
+    C.moe_align(ids.contiguous().view(-1).to(torch.int32), E, sorted_ids, tile_e, offs, total, inv, bm)
+    xq, xs = _quant_groups_padded(x, Kp1)
+    h = torch.empty(max_p, F, dtype=torch.bfloat16, device=dev)
+    C.moe_gemm8_mxfp4(xq, xs, k, sorted_ids, tile_e, w1q, w1s, h, 1, act, alpha, limit, False, b1, bm, total)
+    hq, hs = _quant_groups_padded(h, Kp2, total)
+    y = torch.empty(max_p, d, dtype=torch.bfloat16, device=dev)
+    C.moe_gemm8_mxfp4(hq, hs, 1, sorted_ids, tile_e, w2q, w2s, y, 0, 0, 0.0, 0.0, True, b2, bm, total)
+    if out is None:
+        out = torch.empty(T, d, dtype=torch.bfloat16, device=dev)
+    C.moe_combine(y, inv, wts.contiguous().view(-1).float(), k, out)
+    return out
+
+
+def pad_mxfp4_k(w: torch.Tensor, kp: int) -> torch.Tensor:
+    """Zero-pad the K (last) dim of bf16/fp32 expert weights [..., K] to ``kp`` before MXFP4
+    quantisation (the tile kernel streams whole 128-deep K-steps)."""
+    k = w.shape[-1]
+    return w if kp == k else torch.nn.functional.pad(w, (0, kp - k))
+
+
 # rows per local expert from which the tile GEMMs (v4 bf16 / v8 fp8) replace the 64-row streaming kernels:
 # they win from 64 rows on (gpt-oss 1.21-1.25x, DeepSeek EP8 1.29-1.35x) and lose at <= 48
 # (profiles/moe_tile_threshold_r6.txt)
