@@ -553,12 +553,16 @@ __global__ __launch_bounds__(P8_NT, 1) void moe_gemm8_mxfp4_kernel(
                                                16, va[j], (uint32_t)(kc * 128), 0, 0);
   };
   // fragment of 32-row block b, k-substep s: lane row 32 b + l32, chunks 4 s + 2 h and 4 s + 2 h + 1
+  // (e2m1 A operand: lane (row, h) of a 64-deep substep holds K 16h .. 16h+15 and 32+16h .. 32+16h+15 at
+  // one scale, measured by scripts/probes/fp4_layout_probe.hip. Feeding a lane the 32 codes of MX block
+  // 2s + h in natural order makes the product run over the K permutation that swaps [16, 32) and [32, 48)
+  // of every 64; the fp8 activation fragment is read in that same order: chunks 4s + h and 4s + 2 + h.)
   auto frag = [&](const char* base, int b, int s) {
     const int row = 32 * b + l32;
     const int f = (row >> 1) & 7;
     const char* rp = base + row * 128;
-    const u32x4_t lo = *reinterpret_cast<const u32x4_t*>(rp + (((4 * s + 2 * h) ^ f) * 16));
-    const u32x4_t hi = *reinterpret_cast<const u32x4_t*>(rp + (((4 * s + 2 * h + 1) ^ f) * 16));
+    const u32x4_t lo = *reinterpret_cast<const u32x4_t*>(rp + (((4 * s + h) ^ f) * 16));
+    const u32x4_t hi = *reinterpret_cast<const u32x4_t*>(rp + (((4 * s + 2 + h) ^ f) * 16));
     return i32x8_t{(int)lo[0], (int)lo[1], (int)lo[2], (int)lo[3], (int)hi[0], (int)hi[1], (int)hi[2], (int)hi[3]};
   };
   // W fragment of 32-row block b, k-substep s: row 32 b + l32 of this wave's 128, 16 B = codes

@@ -654,6 +654,9 @@ def quant_mxfp4_weight(w: torch.Tensor):
     to <= 6 (the largest e2m1 magnitude); values round to the nearest e2m1 (ties away from zero)."""
     E, N, K = w.shape
     assert K % 32 == 0, "MXFP4 needs K % 32 == 0"
+    if E > 1 and w.numel() > (1 << 28):  # keep torch's elementwise grids small: one expert at a time
+        parts = [quant_mxfp4_weight(w[e:e + 1]) for e in range(E)]
+        return torch.cat([p[0] for p in parts]), torch.cat([p[1] for p in parts])
     wf = w.float().view(E, N, K // 32, 32)
     amax = wf.abs().amax(-1).clamp(min=2.0 ** -126)
     e = torch.ceil(torch.log2(amax / 6.0)).clamp(-127, 127)
@@ -669,21 +672,8 @@ def quant_mxfp4_weight(w: torch.Tensor):
     return packed, (e + 127).to(torch.uint8).contiguous()
 
 
-def mxfp4_mfma_layout(q: torch.Tensor, inverse: bool = False) -> torch.Tensor:
-    """Packed e2m1 codes [.., K / 2] in the order the scaled MFMA reads them: with an e2m1 A operand,
-    lane (row, h) of a 64-deep k-substep holds K 16h .. 16h+15 and 32+16h .. 32+16h+15 (measured,
-    scripts/probes/fp4_layout_probe.hip), so every 32 bytes (64 codes) are stored as the 8-byte groups
-    [K0-15, K32-47, K16-31, K48-63]: one 16-B LDS read per lane then feeds the MFMA. Self-inverse."""
-    shp = q.shape
-    g = q.reshape(*shp[:-1], shp[-1] // 32, 4, 8)
-    return g[..., [0, 2, 1, 3], :].reshape(shp).contiguous()
-
-
-def dequant_mxfp4_weight(q: torch.Tensor, s: torch.Tensor, mfma_layout: bool = False) -> torch.Tensor:
-    """fp32 [E, N, K] of quant_mxfp4_weight's (codes, scales); ``mfma_layout``: codes in
-    mxfp4_mfma_layout order."""
-    if mfma_layout:
-        q = mxfp4_mfma_layout(q)
+def dequant_mxfp4_weight(q: torch.Tensor, s: torch.Tensor) -> torch.Tensor:
+    """fp32 [E, N, K] of quant_mxfp4_weight's (codes, scales)."""
     E, N, K2 = q.shape
     lo, hi = (q & 0xF).long(), (q >> 4).long()
     codes = torch.stack([lo, hi], -1).view(E, N, 2 * K2)
@@ -699,16 +689,16 @@ def moe_experts_mxfp4(x, ids, wts, w1q, w1s, w2q, w2s, act=0, alpha=1.702, limit
     e4m3 with power-of-two scales, both GEMMs on the persistent expert-tile kernel (csrc/ops/moe8.hip
     moe_gemm8_mxfp4_kernel: half the weight bytes of fp8, the scaled MFMA at the fp4 rate) at every
     step size - its weight stream is halved, so it also covers decode-sized steps - and the gated
-    activation fused into GEMM 1, bf16 weighted combine. w1q [E, 2F, Kp1/2], w2q [E, d, Kp2/2], codes in
-    mxfp4_mfma_layout order (done once at load)."""
+    activation fused into GEMM 1, bf16 weighted combine. w1q [E, 2F, Kp1/2], w2q [E, d, Kp2/2] in the
+    standard packed order (the kernel reads activations in the K order the e2m1 operand implies)."""
     E, N1, Kp1 = w1q.shape[0], w1q.shape[1], 2 * w1q.shape[2]
     d, Kp2 = w2q.shape[1], 2 * w2q.shape[2]
     F = N1 // 2
     if not _gpu(x):
         xq, xs = quant_fp8_groups(x)
         xd = (xq.float().view(x.shape[0], -1) * xs.repeat_interleave(128, 1)[:, :x.shape[1]]).to(torch.bfloat16)
-        w1 = dequant_mxfp4_weight(w1q, w1s, mfma_layout=True)[..., :x.shape[1]].to(torch.bfloat16)
-        w2 = dequant_mxfp4_weight(w2q, w2s, mfma_layout=True)[..., :F].to(torch.bfloat16)
+        w1 = dequant_mxfp4_weight(w1q, w1s)[..., :x.shape[1]].to(torch.bfloat16)
+        w2 = dequant_mxfp4_weight(w2q, w2s)[..., :F].to(torch.bfloat16)
         r = ref.moe_forward(xd, ids, wts, w1, w2, act, alpha, limit, b1, b2)
         if out is not None:
             out.copy_(r)

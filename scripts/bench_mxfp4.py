@@ -36,7 +36,6 @@ def main():
     f1q, f2q = ops.pad_fp8_k(f1q, c128(d)), ops.pad_fp8_k(f2q, c128(F))
     m1q, m1s = ops.quant_mxfp4_weight(ops.pad_mxfp4_k(w1.float(), c128(d)))
     m2q, m2s = ops.quant_mxfp4_weight(ops.pad_mxfp4_k(w2.float(), c128(F)))
-    m1q, m2q = ops.mxfp4_mfma_layout(m1q), ops.mxfp4_mfma_layout(m2q)
     del w1, w2
     for T in (256, 1024, 2048, 5405, 8192):
         x = torch.randn(T, d, device=dev, dtype=torch.bfloat16)

@@ -9,7 +9,7 @@ typedef int i32x4 __attribute__((ext_vector_type(4)));
 typedef int i32x8 __attribute__((ext_vector_type(8)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
-__global__ void probe(int L, int J, float* out) {
+__global__ void probe(int L, int J, int hs, float* out) {
   const int lane = threadIdx.x;
   i32x4 a = {0, 0, 0, 0};
   if (lane == L) a[J / 8] = 2 << (4 * (J % 8));  // code 2 = 1.0
@@ -27,10 +27,10 @@ __global__ void probe(int L, int J, float* out) {
     b[r] = (int)v;
   }
   f32x16 acc = {};
-  const int s127 = 127;
+  const int s127 = 127, sa = 127 + (hs ? (lane >> 5) : 0);  // hs: A scale x2 on lanes 32-63
   // the instruction exactly as moe8.hip's p4_mfma issues it (A = 4 VGPRs of e2m1, B = 8 of e4m3)
   asm volatile("v_mfma_scale_f32_32x32x64_f8f6f4 %0, %1, %2, %0, %3, %4 op_sel_hi:[0,0,0] cbsz:4\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7"
-               : "+v"(acc) : "v"(a), "v"(b), "v"(s127), "v"(s127));
+               : "+v"(acc) : "v"(a), "v"(b), "v"(sa), "v"(s127));
   for (int r = 0; r < 16; ++r) out[lane * 16 + r] = acc[r];
 }
 
@@ -39,10 +39,11 @@ int main() {
   hipMalloc(&d, 64 * 16 * sizeof(float));
   float h[64 * 16];
   const int cases[][2] = {{0, 0}, {0, 1}, {0, 2}, {0, 7}, {0, 8}, {0, 15}, {0, 16}, {0, 31}, {1, 0}, {5, 3}, {32, 0}, {32, 9}, {33, 31}};
+  for (int hs = 0; hs < 2; ++hs)
   for (auto& c : cases) {
-    hipLaunchKernelGGL(probe, dim3(1), dim3(64), 0, 0, c[0], c[1], d);
+    hipLaunchKernelGGL(probe, dim3(1), dim3(64), 0, 0, c[0], c[1], hs, d);
     hipMemcpy(h, d, sizeof(h), hipMemcpyDeviceToHost);
-    printf("A lane %2d nibble %2d ->", c[0], c[1]);
+    printf("%s A lane %2d nibble %2d ->", hs ? "[A scale x2 on lanes 32-63]" : "", c[0], c[1]);
     for (int l = 0; l < 64; ++l)
       for (int r = 0; r < 16; ++r)
         if (h[l * 16 + r] != 0.f) printf(" D[row %d][col %d]=%g", (r & 3) + 8 * (r >> 2) + 4 * (l >> 5), l & 31, h[l * 16 + r]);

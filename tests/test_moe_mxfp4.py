@@ -29,24 +29,12 @@ def test_mxfp4_codes_scales_and_packing():
     assert (amax > 0).all()
 
 
-def test_mxfp4_mfma_layout_is_a_self_inverse_group_swap():
-    q = torch.arange(64, dtype=torch.uint8).view(1, 1, 64)
-    m = ops.mxfp4_mfma_layout(q)
-    assert m[0, 0, :32].tolist() == list(range(0, 8)) + list(range(16, 24)) + list(range(8, 16)) + list(range(24, 32))
-    assert torch.equal(ops.mxfp4_mfma_layout(m), q)
-    w = torch.randn(2, 3, 128)
-    q, s = ops.quant_mxfp4_weight(w)
-    assert torch.equal(ops.dequant_mxfp4_weight(ops.mxfp4_mfma_layout(q), s, mfma_layout=True),
-                       ops.dequant_mxfp4_weight(q, s))
-
-
 def test_moe_experts_mxfp4_cpu_reference_runs():
     torch.manual_seed(1)
     T, E, k, d, F = 6, 4, 2, 256, 128
     x = torch.randn(T, d, dtype=torch.bfloat16)
     w1q, w1s = ops.quant_mxfp4_weight(torch.randn(E, 2 * F, d) * 0.05)
     w2q, w2s = ops.quant_mxfp4_weight(torch.randn(E, d, F) * 0.05)
-    w1q, w2q = ops.mxfp4_mfma_layout(w1q), ops.mxfp4_mfma_layout(w2q)
     ids, wts = ops.moe_topk(torch.randn(T, E), k, scoring=0)
     y = ops.moe_experts_mxfp4(x, ids, wts, w1q, w1s, w2q, w2s, act=2)
     assert y.shape == (T, d) and torch.isfinite(y.float()).all()
@@ -82,7 +70,6 @@ def test_moe_gemm8_mxfp4_matches_fp32(mode, tile):
     x = torch.randn(T, K, device=dev, dtype=torch.bfloat16)
     xq, xs = ops._quant_groups_padded(x, K)
     wq, ws = ops.quant_mxfp4_weight(torch.randn(E, N, K, device=dev) * 0.03)
-    wk = ops.mxfp4_mfma_layout(wq)
     bias = torch.randn(E, N, device=dev, dtype=torch.bfloat16) * 0.1
     ids, _ = ops.moe_topk(torch.randn(T, E, device=dev), k, scoring=0)
     n = T * k
@@ -94,7 +81,7 @@ def test_moe_gemm8_mxfp4_matches_fp32(mode, tile):
     inv = torch.empty(n, dtype=torch.int32, device=dev)
     C.moe_align(ids.contiguous().view(-1).to(torch.int32), E, sorted_ids, tile_e, offs, total, inv, tile)
     y = torch.full((max_p, N // 2 if mode == 1 else N), 7.0, device=dev, dtype=torch.bfloat16)
-    C.moe_gemm8_mxfp4(xq, xs, k, sorted_ids, tile_e, wk, ws, y, mode, 2, 1.702, 7.0, False, bias, tile, total)
+    C.moe_gemm8_mxfp4(xq, xs, k, sorted_ids, tile_e, wq, ws, y, mode, 2, 1.702, 7.0, False, bias, tile, total)
     torch.cuda.synchronize()
     ref, live = _oracle_rows(xq, xs, wq, ws, bias, sorted_ids, tile_e, tile, k, mode)
     got = y.float()
@@ -115,7 +102,6 @@ def test_moe_experts_mxfp4_gpu_vs_cpu(T):
     w2 = ops.pad_mxfp4_k(torch.randn(E, d, F, device=dev) * 0.03, c128(F))
     w1q, w1s = ops.quant_mxfp4_weight(w1)
     w2q, w2s = ops.quant_mxfp4_weight(w2)
-    w1q, w2q = ops.mxfp4_mfma_layout(w1q), ops.mxfp4_mfma_layout(w2q)
     b1 = torch.randn(E, 2 * F, device=dev, dtype=torch.bfloat16) * 0.1
     b2 = torch.randn(E, d, device=dev, dtype=torch.bfloat16) * 0.1
     ids, wts = ops.moe_topk(torch.randn(T, E, device=dev), k, scoring=0)
