@@ -108,7 +108,7 @@ def parse():
     p.add_argument("--gpu-memory-utilization", type=float, default=0.92)
     p.add_argument("--kv-cache-gb", type=float, default=None)
     p.add_argument("--json-out", default=None)
-    p.add_argument("--quantization", default=None, choices=[None, "fp8"],
+    p.add_argument("--quantization", default=None, choices=[None, "fp8", "mxfp4"],
                    help="fp8 = W8A8 linears (the reference AMD recipe serves Llama-3.3-70B-FP8); default bf16")
     p.add_argument("--kv-cache-dtype", default="auto", choices=["auto", "fp8"])
     p.add_argument("--no-async-scheduling", action="store_true",
@@ -198,7 +198,8 @@ def main():
                 "metric": _metric(a.model), "value": round(value, 2), "unit": "output tok/s (whole job)",
                 "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
                 "ms_per_step": round(1000 * res["elapsed"] / a.steps, 3), "higher_is_better": True,
-                "scaling": "weak", "vs_baseline": None, "dtype": "fp8" if a.quantization == "fp8" else "bf16",
+                "scaling": "weak", "vs_baseline": None,
+                "dtype": {"fp8": "fp8", "mxfp4": "mxfp4 experts + fp8"}.get(a.quantization, "bf16"),
                 "data": "synthetic (random token prompts, random-init weights)",
                 "config": {"model": "Llama-3-70B" if a.model == "llama-3-70b" else a.model,
                            "global_batch": a.concurrency * res["decode_ranks"], "seq_len": a.isl,
@@ -371,7 +372,7 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "fp8" if a.quantization == "fp8" else "bf16",
+        "dtype": {"fp8": "fp8", "mxfp4": "mxfp4 experts + fp8"}.get(a.quantization, "bf16"),
         "data": "synthetic (random token prompts, random-init weights)",
         "config": {"model": "Llama-3-70B" if a.model == "llama-3-70b" else a.model,
                    "global_batch": a.concurrency * world, "seq_len": a.isl, "isl": a.isl, "osl": a.osl,

@@ -355,6 +355,7 @@ class EngineConfig:
     load_format: str = "dummy"  # "dummy" (random init) | "safetensors"
     weights_path: Optional[str] = None
     quantization: Optional[str] = None  # None | "fp8" (W8A8: per-channel fp8 weights, per-token activations)
+    # | "mxfp4" (routed experts in MXFP4, e2m1 + E8M0 per 32; other linears as fp8)
     tokenizer: Optional[str] = None
     served_model_name: Optional[str] = None
     enforce_eager: bool = False
@@ -408,8 +409,9 @@ def add_engine_args(p: argparse.ArgumentParser) -> argparse.ArgumentParser:
     p.add_argument("--device", default="cuda")
     p.add_argument("--seed", type=int, default=0)
     p.add_argument("--block-size", type=int, default=64)
-    p.add_argument("--quantization", "-q", default=None, choices=[None, "fp8"],
-                   help="fp8: online W8A8 quantisation of the dense linears (hipBLASLt fp8 GEMM)")
+    p.add_argument("--quantization", "-q", default=None, choices=[None, "fp8", "mxfp4"],
+                   help="fp8: online W8A8 quantisation of the dense linears (hipBLASLt fp8 GEMM); "
+                   "mxfp4: routed experts in MXFP4 (gpt-oss's format), dense linears as fp8")
     p.add_argument("--kv-cache-dtype", default="auto", choices=["auto", "bfloat16", "fp8", "fp8_e4m3"],
                    help="KV cache storage: bf16 (auto) or OCP fp8 e4m3fn")
     p.add_argument("--gpu-memory-utilization", type=float, default=0.92)

@@ -126,6 +126,11 @@ class ModelRunner:
 
             n = quantize_fp8(self.model)
             log.info("fp8 W8A8: quantised %d linears", n)
+        elif cfg.quantization == "mxfp4":
+            from llmd_amd.models.layers import quantize_mxfp4
+
+            n = quantize_mxfp4(self.model)
+            log.info("mxfp4 experts + fp8 W8A8 linears: quantised %d tensors", n)
         elif cfg.quantization:
             raise ValueError(f"unsupported quantization {cfg.quantization}")
         if self.is_gpu:
@@ -224,7 +229,8 @@ class ModelRunner:
                 rows = max(rows, int(os.environ.get("LLMD_EP_HT_ROWS", "1024")))
             # block-fp8 experts: quantise in the dispatch kernel (DeepEP-LL use_fp8)
             fp8 = (os.environ.get("LLMD_EP_FP8_DISPATCH", "1") == "1"
-                   and any(getattr(m, "w1_scale", None) is not None and m.w1.dtype == torch.float8_e4m3fn
+                   and any(getattr(m, "w1_scale", None) is not None
+                           and m.w1.dtype in (torch.float8_e4m3fn, torch.uint8)
                            for m in self.model.modules()))
             symm.init(st.ep_rank, st.ep_size, group=st.cpu_group, ep_rows=rows, hidden=self.mc.hidden_size,
                       topk=self.mc.num_experts_per_tok, micro_batches=2 if pc.enable_dbo else 1, ep_fp8=fp8)

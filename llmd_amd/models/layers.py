@@ -70,8 +70,33 @@ def quantize_fp8(model: torch.nn.Module) -> int:
     return n
 
 
+def quantize_mxfp4(model: torch.nn.Module) -> int:
+    """``--quantization mxfp4``: routed-expert weights in OCP MXFP4 (e2m1 codes + E8M0 scale per 32
+    elements - the format gpt-oss's checkpoint ships its experts in; vLLM's mxfp4 method), K padded
+    to 128 for the tile kernel; every Column/Row linear takes the fp8 W8A8 path of quantize_fp8
+    (those GEMMs have no MXFP4 kernel here). Returns the number of quantised tensors."""
+    n = 0
+    for m in model.modules():
+        for name in ("w1", "w2"):
+            w = getattr(m, name, None)
+            if isinstance(w, torch.Tensor) and w.dim() == 3 and w.dtype == torch.bfloat16:
+                kp = (w.shape[2] + 127) // 128 * 128
+                q, s = ops.quant_mxfp4_weight(ops.pad_mxfp4_k(w.data, kp))
+                setattr(m, name, torch.nn.Parameter(q, requires_grad=False))
+                setattr(m, name + "_scale", torch.nn.Parameter(s, requires_grad=False))
+                n += 1
+    return n + quantize_fp8(model)
+
+
+def is_mxfp4_experts(mod) -> bool:
+    return mod.w1.dtype == torch.uint8 and getattr(mod, "w1_scale", None) is not None
+
+
 def run_experts(mod, x, ids, w, act, alpha=1.702, limit=7.0, b1=None, b2=None):
-    """Routed-expert FFN of an MoE module: bf16 or block-fp8 grouped GEMMs."""
+    """Routed-expert FFN of an MoE module: bf16, block-fp8 or MXFP4 grouped GEMMs."""
+    if is_mxfp4_experts(mod):
+        return ops.moe_experts_mxfp4(x, ids, w, mod.w1, mod.w1_scale, mod.w2, mod.w2_scale, act, alpha, limit,
+                                     b1=b1, b2=b2)
     if mod.w1.dtype == torch.float8_e4m3fn:
         return ops.moe_experts_fp8(x, ids, w, mod.w1, mod.w1_scale, mod.w2, mod.w2_scale, act, alpha, limit,
                                    b1=b1, b2=b2)

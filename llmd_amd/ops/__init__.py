@@ -690,11 +690,14 @@ def moe_experts_mxfp4(x, ids, wts, w1q, w1s, w2q, w2s, act=0, alpha=1.702, limit
     moe_gemm8_mxfp4_kernel: half the weight bytes of fp8, the scaled MFMA at the fp4 rate) at every
     step size - its weight stream is halved, so it also covers decode-sized steps - and the gated
     activation fused into GEMM 1, bf16 weighted combine. w1q [E, 2F, Kp1/2], w2q [E, d, Kp2/2] in the
-    standard packed order (the kernel reads activations in the K order the e2m1 operand implies)."""
+    standard packed order (the kernel reads activations in the K order the e2m1 operand implies).
+    ``x`` may be ``Fp8Rows`` (the EP dispatch kernel's per-128 e4m3 rows)."""
     E, N1, Kp1 = w1q.shape[0], w1q.shape[1], 2 * w1q.shape[2]
     d, Kp2 = w2q.shape[1], 2 * w2q.shape[2]
     F = N1 // 2
-    if not _gpu(x):
+    if isinstance(x, Fp8Rows) and not (x.is_cuda and x.q.shape[1] == Kp1):
+        x = x.dequant()
+    if not isinstance(x, Fp8Rows) and not _gpu(x):
         xq, xs = quant_fp8_groups(x)
         xd = (xq.float().view(x.shape[0], -1) * xs.repeat_interleave(128, 1)[:, :x.shape[1]]).to(torch.bfloat16)
         w1 = dequant_mxfp4_weight(w1q, w1s)[..., :x.shape[1]].to(torch.bfloat16)
@@ -717,7 +720,7 @@ def moe_experts_mxfp4(x, ids, wts, w1q, w1s, w2q, w2s, act=0, alpha=1.702, limit
     total = torch.empty(1, dtype=torch.int32, device=dev)
     inv = torch.empty(n, dtype=torch.int32, device=dev)
     C.moe_align(ids.contiguous().view(-1).to(torch.int32), E, sorted_ids, tile_e, offs, total, inv, bm)
-    xq, xs = _quant_groups_padded(x, Kp1)
+    xq, xs = (x.q, x.s) if isinstance(x, Fp8Rows) else _quant_groups_padded(x, Kp1)
     h = torch.empty(max_p, F, dtype=torch.bfloat16, device=dev)
     C.moe_gemm8_mxfp4(xq, xs, k, sorted_ids, tile_e, w1q, w1s, h, 1, act, alpha, limit, False, b1, bm, total)
     hq, hs = _quant_groups_padded(h, Kp2, total)

@@ -27,7 +27,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=4)
     ap.add_argument("--max-num-batched-tokens", type=int, default=8192)
     ap.add_argument("--inflight", type=int, default=6)
-    ap.add_argument("--quantization", default=None, choices=[None, "fp8"])
+    ap.add_argument("--quantization", default=None, choices=[None, "fp8", "mxfp4"])
     ap.add_argument("--kv-cache-dtype", default="auto", choices=["auto", "fp8"])
     a = ap.parse_args()
     cfg = EngineConfig.create(a.model, device="cuda", block_size=64, max_num_seqs=64,

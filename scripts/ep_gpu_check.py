@@ -32,7 +32,7 @@ def main():
     ap.add_argument("--eager", action="store_true", help="no decode graphs at all")
     ap.add_argument("--backend", default="symm_ll", choices=["symm_ll", "symm_ht"],
                     help="symm_ht: prefill-sized steps go through the chunked high-throughput exchange")
-    ap.add_argument("--quantization", default=None, choices=[None, "fp8"],
+    ap.add_argument("--quantization", default=None, choices=[None, "fp8", "mxfp4"],
                     help="fp8: block-fp8 experts, rows quantised to e4m3 in the dispatch kernel (the reference "
                          "engine is quantised the same way)")
     ap.add_argument("--seed", type=int, default=0, help="seed of the random checkpoint")

@@ -202,3 +202,18 @@ def test_gpt_oss_engine_gpu_runs():
     model = eng.runner.model
     for p, r in zip(prompts, reqs):
         assert r.output_token_ids[0] == greedy_reference(model, p, 1)[0]
+
+
+@pytest.mark.gpu
+def test_gpt_oss_mxfp4_engine_gpu_runs():
+    """--quantization mxfp4: MXFP4 experts on the e2m1 tile kernel inside the engine (prefill
+    chunks and decode steps, hipGraphs on); first tokens match the model's plain forward."""
+    eng = make_engine(device="cuda", num_gpu_blocks=128, max_num_batched_tokens=256,
+                      model="tiny-gpt-oss", max_num_seqs=8, quantization="mxfp4")
+    model = eng.runner.model
+    assert any(getattr(m, "w1_scale", None) is not None and m.w1.dtype == torch.uint8 for m in model.modules())
+    prompts = _prompts(7, [5, 100, 40])
+    reqs = eng.generate(prompts, SamplingParams(max_tokens=6, temperature=0.0, ignore_eos=True))
+    for p, r in zip(prompts, reqs):
+        assert len(r.output_token_ids) == 6
+        assert r.output_token_ids[0] == greedy_reference(model, p, 1)[0]

@@ -30,9 +30,9 @@ MODEL = "tiny-llama"
 SP = SamplingParams(max_tokens=6, temperature=0.0, ignore_eos=True, logprobs=1)
 
 
-def _cfg(path, device="cpu", **kw):
+def _cfg(path, device="cpu", model=MODEL, **kw):
     kw.setdefault("enforce_eager", device == "cpu")
-    return EngineConfig.create(MODEL, device=device, block_size=16, num_gpu_blocks=64, max_num_batched_tokens=64,
+    return EngineConfig.create(model, device=device, block_size=16, num_gpu_blocks=64, max_num_batched_tokens=64,
                                max_num_seqs=8, max_model_len=512, load_format="safetensors", weights_path=path, **kw)
 
 
@@ -41,11 +41,11 @@ def _prompts():
     return [rng.integers(3, 500, size=n).tolist() for n in (41, 77, 9)]
 
 
-def _ckpts(tmp_path, tags=("a", "b")):
+def _ckpts(tmp_path, tags=("a", "b"), model=MODEL):
     from llmd_amd.models import build_model
     from llmd_amd.models.loader import export_hf, save_safetensors
 
-    mc = _cfg(None).model_config
+    mc = _cfg(None, model=model).model_config
     paths = []
     for seed, tag in enumerate(tags):
         torch.manual_seed(seed)
@@ -65,11 +65,12 @@ def _run(eng):
     return [(r.output_token_ids, r.output_logprobs) for r in eng.generate(_prompts(), SP)]
 
 
-@pytest.mark.parametrize("quant", [None, "fp8"])
-def test_update_from_disk_matches_fresh_engine(tmp_path, quant):
-    a, b = _ckpts(tmp_path)
-    ref = _run(LLMEngine(_cfg(a, quantization=quant)))
-    eng = LLMEngine(_cfg(b, quantization=quant))
+@pytest.mark.parametrize("model,quant", [(MODEL, None), (MODEL, "fp8"), ("tiny-gpt-oss", "mxfp4")])
+def test_update_from_disk_matches_fresh_engine(tmp_path, model, quant):
+    """mxfp4: the MXFP4 experts are re-quantised from the update exactly as at load."""
+    a, b = _ckpts(tmp_path, model=model)
+    ref = _run(LLMEngine(_cfg(a, model=model, quantization=quant)))
+    eng = LLMEngine(_cfg(b, model=model, quantization=quant))
     before = _run(eng)
     assert [t for t, _ in before] != [t for t, _ in ref]  # the two checkpoints really differ
     res = eng.weight_sync_cmd({"op": "update_from_disk", "path": a})
