@@ -73,14 +73,14 @@ def quantize_fp8(model: torch.nn.Module) -> int:
 def quantize_mxfp4(model: torch.nn.Module) -> int:
     """``--quantization mxfp4``: routed-expert weights in OCP MXFP4 (e2m1 codes + E8M0 scale per 32
     elements - the format gpt-oss's checkpoint ships its experts in; vLLM's mxfp4 method), K padded
-    to 128 for the tile kernel; every Column/Row linear takes the fp8 W8A8 path of quantize_fp8
-    (those GEMMs have no MXFP4 kernel here). Returns the number of quantised tensors."""
+    to a multiple of 128 and to >= 512 (the persistent tile kernel peels its last 3 K-steps); every
+    Column/Row linear takes the fp8 W8A8 path of quantize_fp8 (no MXFP4 kernel for those GEMMs). Returns the number of quantised tensors."""
     n = 0
     for m in model.modules():
         for name in ("w1", "w2"):
             w = getattr(m, name, None)
             if isinstance(w, torch.Tensor) and w.dim() == 3 and w.dtype == torch.bfloat16:
-                kp = (w.shape[2] + 127) // 128 * 128
+                kp = max(512, (w.shape[2] + 127) // 128 * 128)
                 q, s = ops.quant_mxfp4_weight(ops.pad_mxfp4_k(w.data, kp))
                 setattr(m, name, torch.nn.Parameter(q, requires_grad=False))
                 setattr(m, name + "_scale", torch.nn.Parameter(s, requires_grad=False))
