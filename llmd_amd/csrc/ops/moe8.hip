@@ -423,11 +423,20 @@ __device__ __forceinline__ void p4_mfma(f32x16_t& acc, const i32x4_t& a, const i
                : "+a"(acc) : "v"(a), "v"(b), "v"(sa), "v"(sb));
 }
 
+template <int N>
+__device__ __forceinline__ void p4_vmwait() {
+  static_assert(N == 12 || N == 14 || N == 24 || N == 28, "counted waits of the MXFP4 stream");
+  if constexpr (N == 12) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+  else if constexpr (N == 14) asm volatile("s_waitcnt vmcnt(14)" ::: "memory");
+  else if constexpr (N == 24) asm volatile("s_waitcnt vmcnt(24)" ::: "memory");
+  else asm volatile("s_waitcnt vmcnt(28)" ::: "memory");
+}
+
 // MXFP4 form (gpt-oss ships its experts as OCP MXFP4): the fp8 kernel above with e2m1 weights - half
 // the weight bytes per K-step (64 B per row: 4 DMA pieces per wave instead of 8) and an E8M0 scale per
 // (row, 32-element block) DMA'd with each K-step (one 4-B piece per wave) and handed to the MFMA per
 // lane and fragment; activations stay block-fp8 (e4m3, power-of-two (token, 128) scales).
-template <int MODE, int TBM>
+template <int MODE, int TBM, int NS>
 __global__ __launch_bounds__(P8_NT, 1) void moe_gemm8_mxfp4_kernel(
     const uint8_t* __restrict__ X, int64_t x_stride, const float* __restrict__ xs, int64_t xs_stride, int topk,
     const int* __restrict__ sorted_ids, const int* __restrict__ tile_expert, const int* __restrict__ total_p,
@@ -436,6 +445,7 @@ __global__ __launch_bounds__(P8_NT, 1) void moe_gemm8_mxfp4_kernel(
     uint16_t* __restrict__ Y, int64_t y_stride, int act, float alpha, float limit, int a_rows_are_slots,
     const uint16_t* __restrict__ bias) {
   static_assert(TBM == 256 || TBM == 192, "tile rows");
+  static_assert(NS == 2 || NS == 3, "stream depth");
   constexpr int MB = TBM / 64;                 // 32-row A blocks per wave
   constexpr int NA = 2 * MB;                   // A DMA pieces per wave per K-step
   constexpr int OPA = TBM * 128;               // A bytes per K-step
@@ -443,7 +453,7 @@ __global__ __launch_bounds__(P8_NT, 1) void moe_gemm8_mxfp4_kernel(
   constexpr int WB = 256 * 64;                 // e2m1 W bytes per K-step (256 rows x 128 codes)
   constexpr int WSB = 256 * 4;                 // E8M0 W scales per K-step (4 per row)
   constexpr int BUF = OPA + WB + WSB + SCB;
-  constexpr int BSO = 2 * BUF;                 // bias [2 tile slots][256 columns] bf16
+  constexpr int BSO = NS * BUF;                // bias [2 tile slots][256 columns] bf16
   constexpr int LDSB = BSO + 2 * 512;
   constexpr int NPC = NA + 4 + 1 + 1;          // DMA ops per wave per K-step: A, W, W scales, act scales (14 / 12)
   constexpr int NMF = 4 * MB;                  // MFMAs per k-substep
@@ -594,7 +604,7 @@ __global__ __launch_bounds__(P8_NT, 1) void moe_gemm8_mxfp4_kernel(
   int slot = 0;  // LDS slot of the current tile's bias
   side_dma(0);
 #pragma unroll
-  for (int s = 0; s < 2; ++s) {
+  for (int s = 0; s < NS; ++s) {
 #pragma unroll
     for (int j = 0; j < NA; ++j) dma(s, s, j, 0);
 #pragma unroll
@@ -602,8 +612,7 @@ __global__ __launch_bounds__(P8_NT, 1) void moe_gemm8_mxfp4_kernel(
     dma(s, s, 0, 2);
     dma(s, s, 0, 3);
   }
-  if constexpr (NPC == 14) asm volatile("s_waitcnt vmcnt(14)" ::: "memory");  // side DMA + step 0 landed
-  else asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+  p4_vmwait<(NS - 1) * NPC>();  // side DMA + step 0 landed
   p8_bar();
 #pragma unroll
   for (int b = 0; b < 4; ++b) {
@@ -628,13 +637,13 @@ __global__ __launch_bounds__(P8_NT, 1) void moe_gemm8_mxfp4_kernel(
   // tile's weight-scale / bias DMAs, then its step 0; 3 (nk - 1): its step 1, and the step-0
   // fragments / scales read for the next K loop. With no next tile the "next" one is the current
   // one again (harmless reloads into buffers nobody reads): the step has no data-dependent branch.
-  int gs = 0;  // global stream step (LDS buffer parity)
+  int bsel = 0;  // LDS buffer of the current stream step (stream step g lives in buffer g % NS)
   auto step = [&](auto PH_, int kt, int nx) {
     constexpr int PH = decltype(PH_)::value;
-    const int bsel = gs & 1;
+    const int bnx = bsel + 1 == NS ? 0 : bsel + 1;
     const char* cur = lds + bsel * BUF;
-    const char* nxt = lds + (bsel ^ 1) * BUF;
-    const int kc = PH <= 1 ? kt + 2 : PH - 2;  // stream step kt + 2 (own, or the next tile's 0 / 1)
+    const char* nxt = lds + bnx * BUF;
+    const int kc = PH <= 1 ? kt + NS : PH - 2;  // stream step kt + NS (own, or the next tile's 0 .. NS - 1)
     if constexpr (PH == 1) meta_load(nx);  // complete by this step's counted wait (older than its DMAs)
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
@@ -669,8 +678,9 @@ __global__ __launch_bounds__(P8_NT, 1) void moe_gemm8_mxfp4_kernel(
       } else if (t == 4) {
         dma(bsel, kc, 0, 3);
       } else if (t == 8) {
-        if constexpr (NPC == 14) asm volatile("s_waitcnt vmcnt(14)" ::: "memory");
-        else asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+        // stream step kt + 1 landed (NS - 1 steps stay in flight); the PH 1 step also waits for
+        // its metadata loads, which are younger than step kt + 2's DMAs when NS = 3
+        p4_vmwait<(PH == 1 ? 1 : NS - 1) * NPC>();
         p8_bar();
       } else if (t == 9) {
         // the next stream step's act scales and its substep-0 W fragments with their scales
@@ -710,18 +720,19 @@ __global__ __launch_bounds__(P8_NT, 1) void moe_gemm8_mxfp4_kernel(
     // drain at the end of every step (asm MFMAs: hipcc does not model their latency)
     asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
-    ++gs;
+    bsel = bnx;
   };
   while (true) {
     const int nxt_item = item + S;
     const bool has_next = nxt_item < c1;
     const int nx = has_next ? nxt_item : item;
-    // the current tile's epilogue parameters (build() overwrites the state at step nk - 3)
+    // the current tile's epilogue parameters (build() overwrites the state at step nk - NS - 1)
     const int cm0 = m0, cn0 = n0, cnv = nvalid, cslot = slot;
-    for (int kt = 0; kt < nk - 3; ++kt) step(std::integral_constant<int, 0>{}, kt, nx);
-    step(std::integral_constant<int, 1>{}, nk - 3, nx);
-    step(std::integral_constant<int, 2>{}, nk - 2, nx);
-    step(std::integral_constant<int, 3>{}, nk - 1, nx);
+    for (int kt = 0; kt < nk - NS - 1; ++kt) step(std::integral_constant<int, 0>{}, kt, nx);
+    step(std::integral_constant<int, 1>{}, nk - NS - 1, nx);
+    step(std::integral_constant<int, 2>{}, nk - NS, nx);
+    step(std::integral_constant<int, 3>{}, nk - NS + 1, nx);
+    if constexpr (NS == 3) step(std::integral_constant<int, 4>{}, nk - 1, nx);
     __builtin_amdgcn_sched_barrier(0);
 
     // ---- epilogue of the current tile straight from the accumulators:
@@ -1163,8 +1174,17 @@ extern "C" int llmd_moe_gemm8_mxfp4(const void* X, int64_t x_stride, const float
   const int64_t upper = (int64_t)num_tiles * ntn;
   const int grid = (int)std::min<int64_t>(p8_cus() / 8 * 8, (upper + 7) / 8 * 8);
   const int order = p8_order();
+  // stream depth: 2 LDS K-step buffers (the fp8 kernel's); LLMD_MXFP4_STAGES=3 takes 3 (e2m1 weights
+  // leave room: 3 x 50 KB at 256 rows) - measured equal at every gpt-oss step size, so the K-step is
+  // not bound by DMA latency (profiles/moe_mxfp4_r6.txt). Read per launch (tests switch it in-process).
+  const char* nsv = getenv("LLMD_MXFP4_STAGES");
+  const int ns = nsv && atoi(nsv) == 3 ? 3 : 2;
 #define P4_LAUNCH(MODE_, TBM_)                                                                                      \
-  hipLaunchKernelGGL((moe_gemm8_mxfp4_kernel<MODE_, TBM_>), dim3(grid), dim3(P8_NT), 0, st, (const uint8_t*)X,      \
+  do {                                                                                                              \
+    if (ns == 3) P4_LAUNCH_NS(MODE_, TBM_, 3); else P4_LAUNCH_NS(MODE_, TBM_, 2);                                   \
+  } while (0)
+#define P4_LAUNCH_NS(MODE_, TBM_, NS_)                                                                              \
+  hipLaunchKernelGGL((moe_gemm8_mxfp4_kernel<MODE_, TBM_, NS_>), dim3(grid), dim3(P8_NT), 0, st, (const uint8_t*)X,      \
                      x_stride, xs, xs_stride, topk, sorted_ids, tile_expert, total_p, num_tiles, ntn, order,         \
                      (const uint8_t*)W, w_expert_stride, (const uint8_t*)wsc, wsc_expert_stride, N, K, (uint16_t*)Y, \
                      y_stride, act, alpha, limit, a_rows_are_slots, (const uint16_t*)bias)
@@ -1174,5 +1194,6 @@ extern "C" int llmd_moe_gemm8_mxfp4(const void* X, int64_t x_stride, const float
     if (mode == 0) P4_LAUNCH(0, 192); else P4_LAUNCH(1, 192);
   }
 #undef P4_LAUNCH
+#undef P4_LAUNCH_NS
   return (int)hipGetLastError();
 }

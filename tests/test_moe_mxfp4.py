@@ -59,13 +59,17 @@ def _oracle_rows(xq, xs, wq, ws, bias, sorted_ids, tile_e, tile, k, mode):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("mode", [0, 1])
-@pytest.mark.parametrize("tile", [256, 192])
-def test_moe_gemm8_mxfp4_matches_fp32(mode, tile):
+@pytest.mark.parametrize("mode,tile,stages,K", [(0, 256, 3, 2944), (1, 256, 3, 2944), (0, 192, 3, 2944),
+                                                (1, 192, 3, 2944), (0, 256, 2, 2944), (1, 192, 2, 2944),
+                                                (1, 256, 3, 512), (0, 192, 3, 512), (1, 192, 2, 512)])
+def test_moe_gemm8_mxfp4_matches_fp32(mode, tile, stages, K, monkeypatch):
+    """stages: LDS K-step buffers of the stream (3 = default, 2 = the fp8 kernel's depth); K = 512 is
+    the shortest K loop (4 steps: every step is a peeled tile-transition phase)."""
+    monkeypatch.setenv("LLMD_MXFP4_STAGES", str(stages))
     torch.manual_seed(5)
     dev = "cuda"
     C = ops.native()
-    T, E, k, K = 400, 8, 4, 2944
+    T, E, k = 400, 8, 4
     N = 5760 if mode == 1 else 2880
     x = torch.randn(T, K, device=dev, dtype=torch.bfloat16)
     xq, xs = ops._quant_groups_padded(x, K)
