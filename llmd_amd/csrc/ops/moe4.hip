@@ -53,9 +53,9 @@ __device__ __forceinline__ float m4_act(float g, float u, int act, float alpha, 
   if (act == 2) {  // gpt-oss: clamp, (u + 1) * g * sigmoid(alpha * g)
     g = fminf(g, limit);
     u = fminf(fmaxf(u, -limit), limit);
-    return (u + 1.f) * g / (1.f + __expf(-alpha * g));
+    return (u + 1.f) * g * __builtin_amdgcn_rcpf(1.f + __expf(-alpha * g));
   }
-  return g / (1.f + __expf(-g)) * u;
+  return g * __builtin_amdgcn_rcpf(1.f + __expf(-g)) * u;
 }
 
 // TBM: expert-tile rows, 256 or 192 (gpt-oss: ~160 rows per expert at a 5120-token step, so a
