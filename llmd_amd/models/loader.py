@@ -18,6 +18,9 @@ checkpoint tensor maps onto this rank's shard:
                        head_rows)`` - heads are split across ranks, KV heads
                        replicated when there are fewer KV heads than ranks.
 
+Expert weights may also come as MXFP4 ``<name>_blocks`` / ``<name>_scales`` pairs (the format the
+gpt-oss checkpoints ship their experts in): they are dequantised per expert on load.
+
 Only safetensors are read (``safe_open``: no pickle, nothing executed).
 """
 from __future__ import annotations
@@ -82,20 +85,55 @@ def place(param: torch.Tensor, full: torch.Tensor, kind: str, extra=None):
             raise ValueError(kind)
 
 
+def _mxfp4_experts(param: torch.Tensor, blocks: torch.Tensor, scales: torch.Tensor, extra) -> None:
+    """MXFP4 expert tensors as gpt-oss checkpoints ship them: ``<name>_blocks`` uint8 [E, out, K/32, 16]
+    (32 e2m1 codes per block, element 2i in the low nibble) and ``<name>_scales`` uint8 [E, out, K/32]
+    (E8M0, bias 127) -> this rank's experts dequantised into ``param`` [E_local, out, K] one expert at a
+    time on the param's device. ``--quantization mxfp4`` re-quantises them afterwards without loss: every
+    element gets its checkpoint value back (a block's scale may come back one step lower with doubled
+    codes; models/layers.py quantize_mxfp4, tests/test_moe_mxfp4.py)."""
+    from llmd_amd import ops
+
+    sel = extra if isinstance(extra, list) else list(range(extra[0], extra[0] + extra[1]))
+    E, N, nb, w = blocks.shape
+    if w != 16 or scales.shape != (E, N, nb) or param.shape[0] != len(sel) or tuple(param.shape[1:]) != (N, nb * 32):
+        raise ValueError(f"MXFP4 tensor shapes {tuple(blocks.shape)} / {tuple(scales.shape)} do not fit "
+                         f"the parameter {tuple(param.shape)}")
+    with torch.no_grad():
+        for i, e in enumerate(sel):
+            q = blocks[e].reshape(1, N, nb * 16).to(param.device)
+            param[i].copy_(ops.dequant_mxfp4_weight(q, scales[e:e + 1].to(param.device))[0])
+
+
 def load_weights(model: torch.nn.Module, path: str, strict: bool = True) -> int:
+    from contextlib import ExitStack
+
     from safetensors import safe_open
 
     specs = {name: (p, kind, extra) for name, p, kind, extra in model.weight_specs()}
     seen = set()
-    for f in _files(path):
-        with safe_open(f, framework="pt", device="cpu") as fh:
+    with ExitStack() as stack:
+        where = {}
+        for f in _files(path):
+            fh = stack.enter_context(safe_open(f, framework="pt", device="cpu"))
             for name in fh.keys():
-                key = name if name in specs else "model." + name  # base-model checkpoints (e.g. facebook/opt-*)
-                if key not in specs:
-                    continue
-                p, kind, extra = specs[key]
-                place(p, fh.get_tensor(name).to(p.device), kind, extra)
-                seen.add(key)
+                where[name] = fh
+        for name, fh in where.items():
+            key = name if name in specs else "model." + name  # base-model checkpoints (e.g. facebook/opt-*)
+            if key not in specs:
+                continue
+            p, kind, extra = specs[key]
+            place(p, fh.get_tensor(name).to(p.device), kind, extra)
+            seen.add(key)
+        for key, (p, kind, extra) in specs.items():  # experts stored as MXFP4 blocks + scales
+            if key in seen or kind not in ("experts", "experts_t"):
+                continue
+            for base in (key, key[6:] if key.startswith("model.") else None):
+                if base and base + "_blocks" in where and base + "_scales" in where:
+                    _mxfp4_experts(p, where[base + "_blocks"].get_tensor(base + "_blocks"),
+                                   where[base + "_scales"].get_tensor(base + "_scales"), extra)
+                    seen.add(key)
+                    break
     missing = set(specs) - seen
     if missing and strict:
         raise KeyError(f"checkpoint is missing {len(missing)} tensors, e.g. {sorted(missing)[:4]}")

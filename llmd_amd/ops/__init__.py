@@ -657,7 +657,7 @@ def quant_mxfp4_weight(w: torch.Tensor):
     if E > 1 and w.numel() > (1 << 28):  # keep torch's elementwise grids small: one expert at a time
         parts = [quant_mxfp4_weight(w[e:e + 1]) for e in range(E)]
         return torch.cat([p[0] for p in parts]), torch.cat([p[1] for p in parts])
-    wf = w.float().view(E, N, K // 32, 32)
+    wf = w.float().contiguous().view(E, N, K // 32, 32)
     amax = wf.abs().amax(-1).clamp(min=2.0 ** -126)
     e = torch.ceil(torch.log2(amax / 6.0)).clamp(-127, 127)
     scale = torch.exp2(e)

@@ -115,3 +115,51 @@ def test_moe_experts_mxfp4_gpu_vs_cpu(T):
     m = r.float().abs().max().item()
     assert torch.isfinite(y.float()).all()
     assert (y.float().cpu() - r.float()).abs().max().item() < 0.06 * m + 1e-3
+
+
+def test_load_mxfp4_checkpoint_experts_lossless(tmp_path):
+    """gpt-oss checkpoints ship experts as MXFP4 ``*_blocks`` [E, out, K/32, 16] + ``*_scales`` [E, out, K/32]:
+    the loader dequantises them, and ``--quantization mxfp4`` re-quantises them to exactly the checkpoint's values."""
+    from llmd_amd.engine.config import EngineConfig
+    from llmd_amd.engine.engine import LLMEngine
+    from llmd_amd.models import build_model
+    from llmd_amd.models.loader import export_hf, load_weights, save_safetensors
+
+    kw = dict(device="cpu", block_size=16, num_gpu_blocks=64, max_num_batched_tokens=64, max_num_seqs=4,
+              max_model_len=256, enforce_eager=True)
+    mc = EngineConfig.create("tiny-gpt-oss", **kw).model_config
+    torch.manual_seed(0)
+    tensors = export_hf(build_model(mc, device="cpu", max_pos=300))
+    packed = {}
+    for name in [n for n in tensors if n.endswith(("mlp.experts.gate_up_proj", "mlp.experts.down_proj"))]:
+        w = tensors.pop(name).transpose(1, 2).float()  # HF [E, in, out] -> [E, out, in]
+        q, s = ops.quant_mxfp4_weight(w)
+        E, N, K2 = q.shape
+        tensors[name + "_blocks"] = q.view(E, N, K2 // 16, 16)
+        tensors[name + "_scales"] = s
+        packed[name] = (q, s)
+    assert packed
+    path = str(tmp_path / "mx.safetensors")
+    save_safetensors(tensors, path)
+
+    m2 = build_model(mc, device="cpu", max_pos=300)
+    load_weights(m2, path)
+    eng = LLMEngine(EngineConfig.create("tiny-gpt-oss", load_format="safetensors", weights_path=path,
+                                        quantization="mxfp4", **kw))
+    by_name2 = {n: p for n, p, _, _ in m2.weight_specs()}
+    by_name_q = {n: (p, own) for n, p, _, own in eng.runner.model.weight_specs()}
+    mods = {id(getattr(m, a)): (m, a) for m in eng.runner.model.modules() for a in ("w1", "w2")
+            if isinstance(getattr(m, a, None), torch.Tensor)}
+    for name, (q, s) in packed.items():
+        key = name if name in by_name2 else "model." + name
+        assert torch.equal(by_name2[key], ops.dequant_mxfp4_weight(q, s).to(torch.bfloat16))
+        pq = by_name_q[key][0]
+        m, a = mods[id(pq)]
+        assert pq.dtype == torch.uint8
+        # the same values (a block whose largest code is 3 may come back as 6 at half the scale)
+        K = 2 * q.shape[2]
+        got = ops.dequant_mxfp4_weight(pq, getattr(m, a + "_scale"))[..., :K]
+        assert torch.equal(got, ops.dequant_mxfp4_weight(q, s))
+    out = eng.generate([[5, 6, 7, 8, 9]], __import__("llmd_amd.engine.request", fromlist=["SamplingParams"])
+                       .SamplingParams(max_tokens=3, temperature=0.0, ignore_eos=True))
+    assert len(out[0].output_token_ids) == 3
