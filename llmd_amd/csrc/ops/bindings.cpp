@@ -1009,7 +1009,7 @@ void moe_gemm8_mxfp4(torch::Tensor X, torch::Tensor xs, int64_t topk, torch::Ten
   const int E = W.size(0), N = W.size(1), K = 2 * W.size(2);
   TORCH_CHECK(wsc.size(0) == E && wsc.size(1) == N && wsc.size(2) == K / 32, "wsc [E, N, K/32]");
   TORCH_CHECK(X.size(1) == K && K % 128 == 0 && K / 128 >= 4 && X.stride(0) % 16 == 0, "moe_gemm8_mxfp4: K");
-  TORCH_CHECK(tile_m == 256 || tile_m == 192, "moe_gemm8_mxfp4: tile_m 256 or 192");
+  TORCH_CHECK(tile_m == 256 || tile_m == 192 || tile_m == 64, "moe_gemm8_mxfp4: tile_m 256, 192 or 64");
   TORCH_CHECK(xs.dim() == 2 && xs.size(0) >= X.size(0) && xs.size(1) >= K / 128 && xs.stride(1) == 1, "xs [rows, K/128]");
   const int bm = (int)tile_m;
   const int P = sorted_ids.numel();

@@ -427,8 +427,10 @@ __device__ __forceinline__ void p4_mfma(f32x16_t& acc, const i32x4_t& a, const i
 
 template <int N>
 __device__ __forceinline__ void p4_vmwait() {
-  static_assert(N == 12 || N == 14 || N == 24 || N == 28, "counted waits of the MXFP4 stream");
-  if constexpr (N == 12) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+  static_assert(N == 8 || N == 12 || N == 14 || N == 16 || N == 24 || N == 28, "counted waits of the MXFP4 stream");
+  if constexpr (N == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  else if constexpr (N == 16) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+  else if constexpr (N == 12) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
   else if constexpr (N == 14) asm volatile("s_waitcnt vmcnt(14)" ::: "memory");
   else if constexpr (N == 24) asm volatile("s_waitcnt vmcnt(24)" ::: "memory");
   else asm volatile("s_waitcnt vmcnt(28)" ::: "memory");
@@ -446,7 +448,7 @@ __global__ __launch_bounds__(P8_NT, 1) void moe_gemm8_mxfp4_kernel(
     const uint8_t* __restrict__ wsc, int64_t wsc_expert_stride, int N, int K,
     uint16_t* __restrict__ Y, int64_t y_stride, int act, float alpha, float limit, int a_rows_are_slots,
     const uint16_t* __restrict__ bias) {
-  static_assert(TBM == 256 || TBM == 192, "tile rows");
+  static_assert(TBM == 256 || TBM == 192 || TBM == 64, "tile rows");
   static_assert(NS == 2 || NS == 3, "stream depth");
   constexpr int MB = TBM / 64;                 // 32-row A blocks per wave
   constexpr int NA = 2 * MB;                   // A DMA pieces per wave per K-step
@@ -459,6 +461,10 @@ __global__ __launch_bounds__(P8_NT, 1) void moe_gemm8_mxfp4_kernel(
   constexpr int LDSB = BSO + 2 * 512;
   constexpr int NPC = NA + 4 + 1 + 1;          // DMA ops per wave per K-step: A, W, W scales, act scales (14 / 12)
   constexpr int NMF = 4 * MB;                  // MFMAs per k-substep
+  // schedule slots per half: 64-row tiles (MB = 1: 4 MFMAs per substep) run the same op sequence with
+  // slots past the last MFMA issuing only their loads / waits / DMAs
+  constexpr int T1 = MB == 1 ? 4 + 2 * MB + 3 : NMF;
+  constexpr int T2 = MB == 1 ? 12 : NMF;
   constexpr int SROWS = TBM / 4;               // act-scale rows per wave
   constexpr int NQ = TBM / 64;                 // 64-slot groups of a tile (valid-row ballot)
   __shared__ __attribute__((aligned(1024))) char lds[LDSB];  // the ONLY LDS object
@@ -649,9 +655,9 @@ __global__ __launch_bounds__(P8_NT, 1) void moe_gemm8_mxfp4_kernel(
     if constexpr (PH == 1) meta_load(nx);  // complete by this step's counted wait (older than its DMAs)
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-    for (int t = 0; t < NMF; ++t) {
+    for (int t = 0; t < T1; ++t) {
       const int j = t / MB, i = t % MB;
-      p4_mfma(acc[j][i], fw0[j], fa0[i], sw0[j], sa[i]);
+      if (t < NMF) p4_mfma(acc[j][i], fw0[j], fa0[i], sw0[j], sa[i]);
       if (t < 4) {
         fw1[t] = wfrag(cur + w_base, t, 1);
         sw1[t] = wscale(cur + ws_base, t, 1);
@@ -665,16 +671,16 @@ __global__ __launch_bounds__(P8_NT, 1) void moe_gemm8_mxfp4_kernel(
         const int q = t - (4 + MB + 2);
         dma(bsel, kc, 2 * q, 0);
         dma(bsel, kc, 2 * q + 1, 0);
-        if (4 + 2 * MB + 2 >= NMF && t == NMF - 1) dma(bsel, kc, 0, 2);  // 192 rows: the act-scale piece
+        if (4 + 2 * MB + 2 >= T1 && t == T1 - 1) dma(bsel, kc, 0, 2);  // 192 rows: the act-scale piece
       } else if (t == 4 + 2 * MB + 2) {
         dma(bsel, kc, 0, 2);
       }
       __builtin_amdgcn_sched_barrier(0);
     }
 #pragma unroll
-    for (int t = 0; t < NMF; ++t) {
+    for (int t = 0; t < T2; ++t) {
       const int j = t / MB, i = t % MB;
-      p4_mfma(acc[j][i], fw1[j], fa1[i], sw1[j], sa[i]);
+      if (t < NMF) p4_mfma(acc[j][i], fw1[j], fa1[i], sw1[j], sa[i]);
       if (t < 4) {
         dma(bsel, kc, t, 1);
       } else if (t == 4) {
@@ -690,7 +696,7 @@ __global__ __launch_bounds__(P8_NT, 1) void moe_gemm8_mxfp4_kernel(
         for (int b = 0; b < MB; ++b) nsf[b] = *reinterpret_cast<const float*>(nxt + s_base + (32 * b + l32) * 4);
         fw0[0] = wfrag(nxt + w_base, 0, 0);
         sw0[0] = wscale(nxt + ws_base, 0, 0);
-        if constexpr (MB == 3) {
+        if constexpr (MB == 3 || MB == 1) {
           fw0[1] = wfrag(nxt + w_base, 1, 0);
           sw0[1] = wscale(nxt + ws_base, 1, 0);
         }
@@ -1168,13 +1174,16 @@ extern "C" int llmd_moe_gemm8_mxfp4(const void* X, int64_t x_stride, const float
   if (K % 128 || K / 128 < 4 || x_stride % 16 || w_expert_stride % 16 || wsc_expert_stride % 4 || N % 8 ||
       (mode == 1 && N % 16) || y_stride % 8 || total_p == nullptr)
     return -1;
-  if (tile_m != 256 && tile_m != 192) return -1;
+  if (tile_m != 256 && tile_m != 192 && tile_m != 64) return -1;
   if (x_rows * x_stride + K > 0x7fffffffLL || (int64_t)N * K / 2 > 0x7fffffffLL || x_rows * xs_stride * 4 > 0x7fffffffLL)
     return -2;
   if (num_tiles == 0) return 0;
   const int ntn = (N + P8_BN - 1) / P8_BN;
   const int64_t upper = (int64_t)num_tiles * ntn;
-  const int grid = (int)std::min<int64_t>(p8_cus() / 8 * 8, (upper + 7) / 8 * 8);
+  // 64-row tiles fit two workgroups per CU (116 VGPRs + 64 AGPRs, 53 KB LDS): LLMD_MXFP4_WG64 per CU
+  const char* wgv = getenv("LLMD_MXFP4_WG64");
+  const int per_cu = tile_m == 64 ? (wgv && atoi(wgv) == 1 ? 1 : 2) : 1;
+  const int grid = (int)std::min<int64_t>(p8_cus() * per_cu / 8 * 8, (upper + 7) / 8 * 8);
   const int order = p8_order();
   // stream depth: 2 LDS K-step buffers (the fp8 kernel's); LLMD_MXFP4_STAGES=3 takes 3 (e2m1 weights
   // leave room: 3 x 50 KB at 256 rows) - measured equal at every gpt-oss step size, so the K-step is
@@ -1192,8 +1201,10 @@ extern "C" int llmd_moe_gemm8_mxfp4(const void* X, int64_t x_stride, const float
                      y_stride, act, alpha, limit, a_rows_are_slots, (const uint16_t*)bias)
   if (tile_m == 256) {
     if (mode == 0) P4_LAUNCH(0, 256); else P4_LAUNCH(1, 256);
-  } else {
+  } else if (tile_m == 192) {
     if (mode == 0) P4_LAUNCH(0, 192); else P4_LAUNCH(1, 192);
+  } else {
+    if (mode == 0) P4_LAUNCH(0, 64); else P4_LAUNCH(1, 64);
   }
 #undef P4_LAUNCH
 #undef P4_LAUNCH_NS

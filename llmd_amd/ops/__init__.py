@@ -710,7 +710,9 @@ def moe_experts_mxfp4(x, ids, wts, w1q, w1s, w2q, w2s, act=0, alpha=1.702, limit
     C = native()
     T = x.shape[0]
     k = ids.shape[1]
-    bm = moe4_tile_rows(T * k, E)
+    # decode-sized steps: 64-row tiles (4 MFMAs per substep instead of 12-16: the weight stream, not the
+    # MFMA work of mostly-empty rows, sets the time)
+    bm = 64 if T * k < MXFP4_SMALL_ROWS * E else moe4_tile_rows(T * k, E)
     n = T * k
     max_p = ((n + E * (bm - 1)) + bm - 1) // bm * bm
     dev = x.device
@@ -730,6 +732,10 @@ def moe_experts_mxfp4(x, ids, wts, w1q, w1s, w2q, w2s, act=0, alpha=1.702, limit
         out = torch.empty(T, d, dtype=torch.bfloat16, device=dev)
     C.moe_combine(y, inv, wts.contiguous().view(-1).float(), k, out)
     return out
+
+
+# rows per local expert below which the MXFP4 experts take 64-row tiles (scripts/bench_mxfp4.py)
+MXFP4_SMALL_ROWS = int(os.environ.get("LLMD_MXFP4_SMALL_ROWS", "48"))
 
 
 def pad_mxfp4_k(w: torch.Tensor, kp: int) -> torch.Tensor:

@@ -1,8 +1,8 @@
 """gpt-oss-120b MoE layer: block-fp8 experts (moe_experts_fp8: v8 tiles for prefill-sized steps, the
 64-row streaming kernels below 64 rows per expert) vs MXFP4 experts (moe_experts_mxfp4: the persistent
-tile kernel with e2m1 weights at every step size; "2st" its default 2-buffer LDS stream (the fp8
-kernel's depth), "3st" 3 buffers, LLMD_MXFP4_STAGES), same routing and activations, random weights.
-  python scripts/bench_mxfp4.py"""
+tile kernel with e2m1 weights: 64-row tiles for decode-sized steps, 192 / 256 rows above), same
+routing and activations, random weights.
+  python scripts/bench_mxfp4.py [T,T,...]"""
 import os
 import sys
 import time
@@ -38,20 +38,30 @@ def main():
     m1q, m1s = ops.quant_mxfp4_weight(ops.pad_mxfp4_k(w1.float(), c128(d)))
     m2q, m2s = ops.quant_mxfp4_weight(ops.pad_mxfp4_k(w2.float(), c128(F)))
     del w1, w2
-    for T in (256, 1024, 2048, 5405, 8192):
+    sizes = [int(v) for v in sys.argv[1].split(",")] if len(sys.argv) > 1 else [64, 256, 1024, 1536, 2048, 5405]
+    for T in sizes:
         x = torch.randn(T, d, device=dev, dtype=torch.bfloat16)
         ids, wts = ops.moe_topk(torch.randn(T, E, device=dev), k, scoring=0)
         tf = t_it(lambda: ops.moe_experts_fp8(x, ids, wts, f1q, f1s, f2q, f2s, 2, b1=b1, b2=b2))
+        # arms: default (64-row tiles below MXFP4_SMALL_ROWS rows per expert, 2 workgroups per CU),
+        # "1wg" = 64-row tiles at one workgroup per CU, "big" = the 192 / 256-row tiles at every size,
+        # "t64" = 64-row tiles at every size
+        arms = {"dflt": ({}, None), "1wg": ({"LLMD_MXFP4_WG64": "1"}, None), "big": ({}, 0), "t64": ({}, 1 << 20)}
         tm = {}
-        for st in ("2", "3", "2", "3"):  # interleaved, best of two
-            os.environ["LLMD_MXFP4_STAGES"] = st
-            t = t_it(lambda: ops.moe_experts_mxfp4(x, ids, wts, m1q, m1s, m2q, m2s, 2, b1=b1, b2=b2))
-            tm[st] = min(tm.get(st, 1e9), t)
+        small = ops.MXFP4_SMALL_ROWS
+        for _ in range(2):  # interleaved, best of two
+            for name, (env, rows) in arms.items():
+                os.environ.update(env)
+                ops.MXFP4_SMALL_ROWS = small if rows is None else rows
+                t = t_it(lambda: ops.moe_experts_mxfp4(x, ids, wts, m1q, m1s, m2q, m2s, 2, b1=b1, b2=b2))
+                tm[name] = min(tm.get(name, 1e9), t)
+                for key in env:
+                    os.environ.pop(key)
+        ops.MXFP4_SMALL_ROWS = small
         fl = 2 * T * k * 3 * F * d
+        arms_s = " | ".join(f"mxfp4 {n} {t * 1e3:.3f} ms ({fl / t / 1e12:.0f} TF/s)" for n, t in tm.items())
         print(f"gpt-oss-120b MoE layer T={T} ({T * k / E:.0f} rows/expert): fp8 {tf * 1e3:.3f} ms "
-              f"({fl / tf / 1e12:.0f} TF/s) | mxfp4 2st {tm['2'] * 1e3:.3f} ms ({fl / tm['2'] / 1e12:.0f} TF/s) | "
-              f"mxfp4 3st {tm['3'] * 1e3:.3f} ms ({fl / tm['3'] / 1e12:.0f} TF/s) | "
-              f"mxfp4 3st speedup {tf / tm['3']:.2f}x", flush=True)
+              f"({fl / tf / 1e12:.0f} TF/s) | {arms_s} | mxfp4 speedup {tf / tm['dflt']:.2f}x", flush=True)
 
 
 if __name__ == "__main__":
