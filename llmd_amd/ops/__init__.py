@@ -734,8 +734,9 @@ def moe_experts_mxfp4(x, ids, wts, w1q, w1s, w2q, w2s, act=0, alpha=1.702, limit
     return out
 
 
-# rows per local expert below which the MXFP4 experts take 64-row tiles (scripts/bench_mxfp4.py)
-MXFP4_SMALL_ROWS = int(os.environ.get("LLMD_MXFP4_SMALL_ROWS", "48"))
+# rows per local expert below which the MXFP4 experts take 64-row tiles: 64-row tiles win at 48 rows
+# (0.604 vs 0.694 ms, gpt-oss layer), lose at 64 (0.787 vs 0.714; profiles/moe_mxfp4_r6.txt)
+MXFP4_SMALL_ROWS = int(os.environ.get("LLMD_MXFP4_SMALL_ROWS", "56"))
 
 
 def pad_mxfp4_k(w: torch.Tensor, kp: int) -> torch.Tensor:
