@@ -960,7 +960,8 @@ void moe_gemm4_fp8(torch::Tensor X, torch::Tensor xs, int64_t topk, torch::Tenso
   TORCH_CHECK(W.dim() == 3 && W.is_contiguous() && ws.is_contiguous(), "W [E, N, K] / ws contiguous");
   const int E = W.size(0), N = W.size(1), K = W.size(2);
   TORCH_CHECK(X.size(1) == K && K % 128 == 0 && K / 128 <= 64 && X.stride(0) % 16 == 0, "moe_gemm4_fp8: K");
-  TORCH_CHECK(tile_m == 256 || tile_m == 192, "moe_gemm4_fp8: tile_m 256 or 192");
+  TORCH_CHECK(tile_m == 256 || tile_m == 192 || (tile_m == 64 && version == 8),
+              "moe_gemm4_fp8: tile_m 256 or 192 (64: version 8 only)");
   TORCH_CHECK(ws.dim() == 3 && ws.size(0) == E && ws.size(1) == (N + 127) / 128 && ws.size(2) == K / 128,
               "ws [E, ceil(N/128), K/128]");
   TORCH_CHECK(xs.dim() == 2 && xs.size(0) >= X.size(0) && xs.size(1) >= K / 128 && xs.stride(1) == 1,

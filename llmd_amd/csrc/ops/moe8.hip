@@ -85,7 +85,7 @@ __global__ __launch_bounds__(P8_NT, 1) void moe_gemm8_fp8_kernel(
     int max_mtiles, int ntn, int order, const uint8_t* __restrict__ W, int64_t w_expert_stride, const float* __restrict__ ws, int N, int K,
     uint16_t* __restrict__ Y, int64_t y_stride, int act, float alpha, float limit, int a_rows_are_slots,
     const uint16_t* __restrict__ bias) {
-  static_assert(TBM == 256 || TBM == 192, "tile rows");
+  static_assert(TBM == 256 || TBM == 192 || TBM == 64, "tile rows");
   constexpr int MB = TBM / 64;                 // 32-row A blocks per wave
   constexpr int NA = 2 * MB;                   // A DMA pieces per wave per K-step
   constexpr int OPA = TBM * 128;               // A bytes per K-step
@@ -96,6 +96,10 @@ __global__ __launch_bounds__(P8_NT, 1) void moe_gemm8_fp8_kernel(
   constexpr int LDSB = BSO + 2 * 512;
   constexpr int NPC = NA + 8 + 1;              // DMA ops per wave per K-step (17 / 15)
   constexpr int NMF = 4 * MB;                  // MFMAs per k-substep
+  // schedule slots per half: 64-row tiles (MB = 1: 4 MFMAs per substep, decode-sized steps) run the same
+  // op sequence with slots past the last MFMA issuing only their loads / waits / DMAs
+  constexpr int T1 = MB == 1 ? 4 + 2 * MB + 3 : NMF;
+  constexpr int T2 = MB == 1 ? 12 : NMF;
   constexpr int SROWS = TBM / 4;               // act-scale rows per wave
   constexpr int NQ = TBM / 64;                 // 64-slot groups of a tile (valid-row ballot)
   __shared__ __attribute__((aligned(1024))) char lds[LDSB];  // the ONLY LDS object
@@ -232,7 +236,8 @@ __global__ __launch_bounds__(P8_NT, 1) void moe_gemm8_fp8_kernel(
     dma(s, s, 0, 2);
   }
   if constexpr (NPC == 17) asm volatile("s_waitcnt vmcnt(17)" ::: "memory");  // side DMA + step 0 landed
-  else asm volatile("s_waitcnt vmcnt(15)" ::: "memory");
+  else if constexpr (NPC == 15) asm volatile("s_waitcnt vmcnt(15)" ::: "memory");
+  else asm volatile("s_waitcnt vmcnt(11)" ::: "memory");
   p8_bar();
 #pragma unroll
   for (int b = 0; b < 4; ++b) {
@@ -267,9 +272,9 @@ __global__ __launch_bounds__(P8_NT, 1) void moe_gemm8_fp8_kernel(
     if constexpr (PH == 1) meta_load(nx);  // complete by this step's counted wait (older than its DMAs)
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-    for (int t = 0; t < NMF; ++t) {
+    for (int t = 0; t < T1; ++t) {
       const int j = t / MB, i = t % MB;
-      p8_mfma(acc[j][i], fw0[j], fa0[i], swt, sa[i]);
+      if (t < NMF) p8_mfma(acc[j][i], fw0[j], fa0[i], swt, sa[i]);
       if (t < 4) {
         fw1[t] = frag(cur + w_base, t, 1);
       } else if (t < 4 + MB) {
@@ -282,21 +287,22 @@ __global__ __launch_bounds__(P8_NT, 1) void moe_gemm8_fp8_kernel(
         const int q = t - (4 + MB + 2);
         dma(bsel, kc, 2 * q, 0);
         dma(bsel, kc, 2 * q + 1, 0);
-        if (4 + 2 * MB + 2 >= NMF && t == NMF - 1) dma(bsel, kc, 0, 2);  // 192 rows: the act-scale piece
+        if (4 + 2 * MB + 2 >= T1 && t == T1 - 1) dma(bsel, kc, 0, 2);  // 192 rows: the act-scale piece
       } else if (t == 4 + 2 * MB + 2) {
         dma(bsel, kc, 0, 2);
       }
       __builtin_amdgcn_sched_barrier(0);
     }
 #pragma unroll
-    for (int t = 0; t < NMF; ++t) {
+    for (int t = 0; t < T2; ++t) {
       const int j = t / MB, i = t % MB;
-      p8_mfma(acc[j][i], fw1[j], fa1[i], swt, sa[i]);
+      if (t < NMF) p8_mfma(acc[j][i], fw1[j], fa1[i], swt, sa[i]);
       if (t < 8) {
         dma(bsel, kc, t, 1);
       } else if (t == 8) {
         if constexpr (NPC == 17) asm volatile("s_waitcnt vmcnt(17)" ::: "memory");
-        else asm volatile("s_waitcnt vmcnt(15)" ::: "memory");
+        else if constexpr (NPC == 15) asm volatile("s_waitcnt vmcnt(15)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(11)" ::: "memory");
         p8_bar();
       } else if (t == 9) {
         // the next stream step's raw scales: act from its buffer, weight from this tile's slot or
@@ -306,7 +312,7 @@ __global__ __launch_bounds__(P8_NT, 1) void moe_gemm8_fp8_kernel(
         if constexpr (PH == 3) nwf = *reinterpret_cast<const float*>(lds + WSO + (slot ^ 1) * 512 + wc * 256);
         else nwf = *reinterpret_cast<const float*>(lds + WSO + slot * 512 + wc * 256 + (kt + 1) * 4);
         fw0[0] = frag(nxt + w_base, 0, 0);
-        if constexpr (MB == 3) fw0[1] = frag(nxt + w_base, 1, 0);
+        if constexpr (MB == 3 || MB == 1) fw0[1] = frag(nxt + w_base, 1, 0);
       } else if constexpr (MB == 4) {
         if (t < 13) {
           fw0[t - 9] = frag(nxt + w_base, t - 9, 0);
@@ -1109,7 +1115,7 @@ extern "C" int llmd_moe_gemm8_fp8(const void* X, int64_t x_stride, const float* 
   if (K % 128 || K / 128 > 64 || K / 128 < 4 || x_stride % 16 || w_expert_stride % 16 || N % 8 ||
       (mode == 1 && N % 16) || y_stride % 8 || total_p == nullptr)
     return -1;
-  if (tile_m != 256 && tile_m != 192) return -1;
+  if (tile_m != 256 && tile_m != 192 && tile_m != 64) return -1;
   if (x_rows * x_stride + K > 0x7fffffffLL || (int64_t)N * K > 0x7fffffffLL || x_rows * xs_stride * 4 > 0x7fffffffLL)
     return -2;
   if (num_tiles == 0) return 0;
@@ -1126,8 +1132,10 @@ extern "C" int llmd_moe_gemm8_fp8(const void* X, int64_t x_stride, const float* 
                      (const uint16_t*)bias)
   if (tile_m == 256) {
     if (mode == 0) P8_LAUNCH(0, 256); else P8_LAUNCH(1, 256);
-  } else {
+  } else if (tile_m == 192) {
     if (mode == 0) P8_LAUNCH(0, 192); else P8_LAUNCH(1, 192);
+  } else {
+    if (mode == 0) P8_LAUNCH(0, 64); else P8_LAUNCH(1, 64);
   }
 #undef P8_LAUNCH
   return (int)hipGetLastError();

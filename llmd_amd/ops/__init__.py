@@ -782,6 +782,9 @@ MOE_FP8_V4 = os.environ.get("LLMD_MOE_FP8_V4", "1") == "1"
 # gpt-oss T=5120 gate/up 1053-1069 -> 1175-1191 TF/s, down 993 -> 1140; DeepSeek EP8 T=4096 down 1535 -> 1868
 # (profiles/moe_gemm_v8_r6.txt)
 MOE_FP8_V8 = os.environ.get("LLMD_MOE_FP8_V8", "1") == "1"
+# decode-sized fp8 steps (< MOE_V3_MIN_ROWS rows per expert) on 64-row v8 tiles instead of the 64-row
+# weight-streaming kernel (moe.hip moe_gemm_fp8_kernel)
+MOE_FP8_T64 = os.environ.get("LLMD_MOE_FP8_T64", "0") == "1"
 
 
 def moe_tile_version(kind: str, K: int) -> int:
@@ -849,8 +852,13 @@ def moe_experts_fp8(x, ids, wts, w1q, w1s, w2q, w2s, act=0, alpha=1.702, limit=7
                                     and MOE_V3) else C.moe_tile_m()
     v4 = (bm == C.moe_tile_m_prefill() and MOE_FP8_V4 and not MOE_FUSED_QUANT and Kp1 <= 8192 and Kp2 <= 8192
           and N1 % 16 == 0 and d % 8 == 0)
+    # decode-sized steps on 64-row persistent tiles (moe8.hip, MB = 1) instead of the streaming kernel
+    t64 = (not v4 and MOE_FP8_T64 and not MOE_FUSED_QUANT and Kp1 % 128 == 0 and Kp2 % 128 == 0
+           and 512 <= min(Kp1, Kp2) and max(Kp1, Kp2) <= 8192 and N1 % 16 == 0 and d % 8 == 0)
     if v4:
         bm = moe4_tile_rows(T * k, E)
+    elif t64:
+        bm, v4 = 64, True
     n = T * k
     max_p = ((n + E * (bm - 1)) + bm - 1) // bm * bm
     dev = x.device
@@ -875,7 +883,7 @@ def moe_experts_fp8(x, ids, wts, w1q, w1s, w2q, w2s, act=0, alpha=1.702, limit=7
     elif v4:
         # v4: PGR2 4-wave tiles, A rows and their act scales gathered by the LDS-DMA (csrc/ops/moe4.hip)
         h = torch.empty(max_p, F, dtype=torch.bfloat16, device=dev)
-        v1, v2 = moe_tile_version("fp8", Kp1), moe_tile_version("fp8", Kp2)
+        v1, v2 = (8, 8) if bm == 64 else (moe_tile_version("fp8", Kp1), moe_tile_version("fp8", Kp2))
         C.moe_gemm4_fp8(xq, xs, k, sorted_ids, tile_e, w1q, w1s, h, 1, act, alpha, limit, False, b1, bm, v1, total)
         hq, hs = _quant_groups_padded(h, Kp2, total)  # slots past the last real tile are never read
         y = torch.empty(max_p, d, dtype=torch.bfloat16, device=dev)

@@ -375,8 +375,42 @@ def test_moe_fp8_v8_gpu(T, E, k, d, F, act, skew, tile, monkeypatch):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("T,E,k,d,F,act,skew", [(64, 16, 4, 1024, 512, 0, False), (100, 32, 8, 2880, 2880, 2, False),
+                                                (7, 8, 2, 7168, 2048, 0, True), (256, 128, 4, 2880, 2880, 2, True)])
+def test_moe_fp8_t64_gpu(T, E, k, d, F, act, skew, monkeypatch):
+    """Decode-sized steps on 64-row persistent tiles (moe8.hip with MB = 1, LLMD_MOE_FP8_T64) vs the
+    64-row weight-streaming kernel and the CPU reference: partial column tiles, K = 7168, empty experts."""
+    torch.manual_seed(4)
+    dev = "cuda"
+    c128 = lambda n: (n + 127) // 128 * 128  # noqa: E731
+    x = torch.randn(T, d, device=dev, dtype=torch.bfloat16)
+    w1q, w1s = ops.quant_fp8_block_weight(torch.randn(E, 2 * F, d, device=dev, dtype=torch.bfloat16) * 0.03)
+    w2q, w2s = ops.quant_fp8_block_weight(torch.randn(E, d, F, device=dev, dtype=torch.bfloat16) * 0.03)
+    b1 = torch.randn(E, 2 * F, device=dev, dtype=torch.bfloat16) * 0.1
+    b2 = torch.randn(E, d, device=dev, dtype=torch.bfloat16) * 0.1
+    w1q, w2q = ops.pad_fp8_k(w1q, c128(d)), ops.pad_fp8_k(w2q, c128(F))
+    logits = torch.randn(T, E, device=dev)
+    if skew:
+        logits[:, : E // 4] += 2.0
+        logits[:, -2:] -= 8.0
+    ids, wts = ops.moe_topk(logits, k, scoring=0)
+    assert T * k < ops.MOE_V3_MIN_ROWS * E  # a decode-sized step
+    monkeypatch.setattr(ops, "MOE_FUSED_QUANT", False)
+    monkeypatch.setattr(ops, "MOE_FP8_T64", False)
+    ys = ops.moe_experts_fp8(x, ids, wts, w1q, w1s, w2q, w2s, act, b1=b1, b2=b2)
+    monkeypatch.setattr(ops, "MOE_FP8_T64", True)
+    yt = ops.moe_experts_fp8(x, ids, wts, w1q, w1s, w2q, w2s, act, b1=b1, b2=b2)
+    r = ops.moe_experts_fp8(x.cpu(), ids.cpu(), wts.cpu(), w1q.cpu()[..., :d], w1s.cpu(), w2q.cpu()[..., :F],
+                            w2s.cpu(), act, b1=b1.cpu(), b2=b2.cpu())
+    m = r.float().abs().max().item()
+    assert torch.isfinite(yt).all()
+    assert (yt.float().cpu() - r.float()).abs().max().item() < 0.06 * m + 1e-3
+    assert (yt.float() - ys.float()).abs().max().item() < 0.02 * m + 1e-3
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("mode", [0, 1])
-@pytest.mark.parametrize("tile", [256, 192])
+@pytest.mark.parametrize("tile", [256, 192, 64])
 def test_moe_gemm8_fp8_kernel_matches_fp32(mode, tile):
     """One v8 grouped GEMM on its own against the fp32 PyTorch oracle of the same op (dequantised
     operands, gathered rows, expert bias, gpt-oss activation in mode 1); padding slots stay unwritten."""
