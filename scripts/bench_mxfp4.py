@@ -45,8 +45,9 @@ def main():
         tf = t_it(lambda: ops.moe_experts_fp8(x, ids, wts, f1q, f1s, f2q, f2s, 2, b1=b1, b2=b2))
         # arms: default (64-row tiles below MXFP4_SMALL_ROWS rows per expert, 2 workgroups per CU),
         # "1wg" = 64-row tiles at one workgroup per CU, "big" = the 192 / 256-row tiles at every size,
-        # "t64" = 64-row tiles at every size
-        arms = {"dflt": ({}, None), "1wg": ({"LLMD_MXFP4_WG64": "1"}, None), "big": ({}, 0), "t64": ({}, 1 << 20)}
+        # "t64" = 64-row tiles at every size, "3st" = 3 LDS K-step buffers
+        arms = {"dflt": ({}, None), "1wg": ({"LLMD_MXFP4_WG64": "1"}, None), "big": ({}, 0), "t64": ({}, 1 << 20),
+                "3st": ({"LLMD_MXFP4_STAGES": "3"}, None)}
         tm = {}
         small = ops.MXFP4_SMALL_ROWS
         for _ in range(2):  # interleaved, best of two
