@@ -59,9 +59,8 @@ def _oracle_rows(xq, xs, wq, ws, bias, sorted_ids, tile_e, tile, k, mode):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("mode,tile,stages,K", [(0, 256, 3, 2944), (1, 256, 3, 2944), (0, 192, 3, 2944),
-                                                (1, 192, 3, 2944), (0, 256, 2, 2944), (1, 192, 2, 2944),
-                                                (1, 256, 3, 512), (0, 192, 3, 512), (1, 192, 2, 512),
+@pytest.mark.parametrize("mode,tile,stages,K", [(0, 256, 2, 2944), (1, 256, 3, 2944), (1, 192, 2, 2944),
+                                                (0, 192, 3, 2944), (1, 256, 2, 512), (0, 192, 3, 512),
                                                 (0, 64, 2, 2944), (1, 64, 2, 2944), (1, 64, 3, 512)])
 def test_moe_gemm8_mxfp4_matches_fp32(mode, tile, stages, K, monkeypatch):
     """stages: LDS K-step buffers of the stream (3 = default, 2 = the fp8 kernel's depth); K = 512 is
@@ -96,7 +95,7 @@ def test_moe_gemm8_mxfp4_matches_fp32(mode, tile, stages, K, monkeypatch):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("T", [5, 64, 300, 2000])
+@pytest.mark.parametrize("T", [5, 64, 700])
 def test_moe_experts_mxfp4_gpu_vs_cpu(T):
     torch.manual_seed(3)
     dev = "cuda"
