@@ -1,7 +1,7 @@
 """Paged decode time vs the number of KV splits (workgroup-round quantisation):
 B sequences x Hkv heads x nsplit workgroups over 256 CUs at 2 per CU.
 Llama-3-70B / Qwen3-32B TP1 heads (64 q / 8 kv, D 128), bf16 KV, block 64.
-  python scripts/bench_decode_nsplit.py"""
+  python scripts/bench_decode_nsplit.py   [NSPLIT_D=64 NSPLIT_CASES=256:5200,128:5200]"""
 import math
 import os
 import sys
@@ -14,8 +14,12 @@ from llmd_amd import ops  # noqa: E402
 
 
 def main():
-    Hq, Hkv, D, bs = 64, 8, 128, 64
-    for B, ctx in ((48, 7416), (110, 7400), (64, 5125), (96, 5125), (32, 7400), (160, 3000), (24, 12000)):
+    D = int(os.environ.get("NSPLIT_D", "128"))  # 64: gpt-oss heads (64 q / 8 kv, D 64)
+    Hq, Hkv, bs = 64, 8, 64
+    cases = ((48, 7416), (110, 7400), (64, 5125), (96, 5125), (32, 7400), (160, 3000), (24, 12000))
+    if os.environ.get("NSPLIT_CASES"):  # "B:ctx,B:ctx"
+        cases = tuple(tuple(int(v) for v in c.split(":")) for c in os.environ["NSPLIT_CASES"].split(","))
+    for B, ctx in cases:
         per = math.ceil(ctx / bs)
         nb = B * per + 1
         kc = torch.randn(nb, Hkv, bs, D, device="cuda", dtype=torch.bfloat16)
