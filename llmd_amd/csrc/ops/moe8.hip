@@ -446,7 +446,7 @@ __device__ __forceinline__ void p4_vmwait() {
 // the weight bytes per K-step (64 B per row: 4 DMA pieces per wave instead of 8) and an E8M0 scale per
 // (row, 32-element block) DMA'd with each K-step (one 4-B piece per wave) and handed to the MFMA per
 // lane and fragment; activations stay block-fp8 (e4m3, power-of-two (token, 128) scales).
-template <int MODE, int TBM, int NS>
+template <int MODE, int TBM, int NS, int DIAG = 0>
 __global__ __launch_bounds__(P8_NT, 1) void moe_gemm8_mxfp4_kernel(
     const uint8_t* __restrict__ X, int64_t x_stride, const float* __restrict__ xs, int64_t xs_stride, int topk,
     const int* __restrict__ sorted_ids, const int* __restrict__ tile_expert, const int* __restrict__ total_p,
@@ -562,6 +562,7 @@ __global__ __launch_bounds__(P8_NT, 1) void moe_gemm8_mxfp4_kernel(
   };
   // op 0 = A piece j, 1 = W piece j (< 4), 2 = act scales, 3 = W scales
   auto dma = [&](int bsel, int kc, int j, int op) {
+    if constexpr ((DIAG & 2) != 0) return;  // diagnostic: no K-step DMA (LLMD_MXFP4_DIAG)
     char* buf = lds + bsel * BUF;
     if (op == 2)
       __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)(buf + OPA + WB + WSB + w * SROWS * 4),
@@ -582,6 +583,7 @@ __global__ __launch_bounds__(P8_NT, 1) void moe_gemm8_mxfp4_kernel(
   // 2s + h in natural order makes the product run over the K permutation that swaps [16, 32) and [32, 48)
   // of every 64; the fp8 activation fragment is read in that same order: chunks 4s + h and 4s + 2 + h.)
   auto frag = [&](const char* base, int b, int s) {
+    if constexpr ((DIAG & 1) != 0) return i32x8_t{b, s, 0, 0, 0, 0, 0, 0};  // diagnostic: no fragment reads
     const int row = 32 * b + l32;
     const int f = (row >> 1) & 7;
     const char* rp = base + row * 128;
@@ -592,11 +594,13 @@ __global__ __launch_bounds__(P8_NT, 1) void moe_gemm8_mxfp4_kernel(
   // W fragment of 32-row block b, k-substep s: row 32 b + l32 of this wave's 128, 16 B = codes
   // [64 s + 32 h, +32) = chunk 2 s + h; its E8M0 scale: byte 2 s + h of the row's 4
   auto wfrag = [&](const char* base, int b, int s) {
+    if constexpr ((DIAG & 1) != 0) return i32x4_t{b, s, 0, 0};
     const int row = 32 * b + l32;
     const u32x4_t v = *reinterpret_cast<const u32x4_t*>(base + row * 64 + (((2 * s + h) ^ ((row >> 2) & 3)) * 16));
     return i32x4_t{(int)v[0], (int)v[1], (int)v[2], (int)v[3]};
   };
   auto wscale = [&](const char* base, int b, int s) {
+    if constexpr ((DIAG & 1) != 0) return 127;
     return (int)*reinterpret_cast<const uint8_t*>(base + (32 * b + l32) * 4 + 2 * s + h);
   };
   const int a_base = wr * (TBM / 2) * 128, w_base = OPA + wc * 128 * 64, ws_base = OPA + WB + wc * 128 * 4;
@@ -1207,13 +1211,29 @@ extern "C" int llmd_moe_gemm8_mxfp4(const void* X, int64_t x_stride, const float
                      x_stride, xs, xs_stride, topk, sorted_ids, tile_expert, total_p, num_tiles, ntn, order,         \
                      (const uint8_t*)W, w_expert_stride, (const uint8_t*)wsc, wsc_expert_stride, N, K, (uint16_t*)Y, \
                      y_stride, act, alpha, limit, a_rows_are_slots, (const uint16_t*)bias)
-  if (tile_m == 256) {
+  // diagnostic variants (192-row tiles, 2 buffers; outputs are garbage): LLMD_MXFP4_DIAG = 1 no fragment
+  // reads, 2 no K-step DMAs, 3 neither - what is left of a step without each resource
+  const char* dgv = getenv("LLMD_MXFP4_DIAG");
+  const int diag = dgv ? atoi(dgv) & 3 : 0;
+#define P4_DIAG(MODE_, D_)                                                                                          \
+  hipLaunchKernelGGL((moe_gemm8_mxfp4_kernel<MODE_, 192, 2, D_>), dim3(grid), dim3(P8_NT), 0, st, (const uint8_t*)X, \
+                     x_stride, xs, xs_stride, topk, sorted_ids, tile_expert, total_p, num_tiles, ntn, order,         \
+                     (const uint8_t*)W, w_expert_stride, (const uint8_t*)wsc, wsc_expert_stride, N, K, (uint16_t*)Y, \
+                     y_stride, act, alpha, limit, a_rows_are_slots, (const uint16_t*)bias)
+  if (diag && tile_m == 192) {
+    if (mode == 0) {
+      if (diag == 1) P4_DIAG(0, 1); else if (diag == 2) P4_DIAG(0, 2); else P4_DIAG(0, 3);
+    } else {
+      if (diag == 1) P4_DIAG(1, 1); else if (diag == 2) P4_DIAG(1, 2); else P4_DIAG(1, 3);
+    }
+  } else if (tile_m == 256) {
     if (mode == 0) P4_LAUNCH(0, 256); else P4_LAUNCH(1, 256);
   } else if (tile_m == 192) {
     if (mode == 0) P4_LAUNCH(0, 192); else P4_LAUNCH(1, 192);
   } else {
     if (mode == 0) P4_LAUNCH(0, 64); else P4_LAUNCH(1, 64);
   }
+#undef P4_DIAG
 #undef P4_LAUNCH
 #undef P4_LAUNCH_NS
   return (int)hipGetLastError();
