@@ -995,7 +995,8 @@ void moe_gemm4_fp8(torch::Tensor X, torch::Tensor xs, int64_t topk, torch::Tenso
 
 extern "C" int llmd_moe_gemm8_mxfp4(const void*, int64_t, const float*, int64_t, int, const int*, const int*,
                                     const int*, int, const void*, int64_t, const void*, int64_t, int, int, void*,
-                                    int64_t, int, int, float, float, int, const void*, int64_t, int, hipStream_t);
+                                    int64_t, int, int, float, float, int, const void*, int64_t, int, int,
+                                    hipStream_t);
 
 // MXFP4 experts on the persistent tile GEMM (csrc/ops/moe8.hip): W [E, N, K/2] packed e2m1, wsc [E, N, K/32]
 // E8M0, X [rows, K] e4m3 with power-of-two (token, 128) scales xs
@@ -1006,8 +1007,11 @@ void moe_gemm8_mxfp4(torch::Tensor X, torch::Tensor xs, int64_t topk, torch::Ten
   const c10::hip::OptionalHIPGuard device_guard(dev_of(X));
   CHECK_CUDA(X); CHECK_DT(X, at::kFloat8_e4m3fn); CHECK_DT(W, at::kByte); CHECK_DT(wsc, at::kByte); CHECK_BF16(Y);
   CHECK_INNER(X); CHECK_INNER(Y); CHECK_DT(xs, at::kFloat); CHECK_DT(total, at::kInt);
-  TORCH_CHECK(W.dim() == 3 && W.is_contiguous() && wsc.dim() == 3 && wsc.is_contiguous(), "W / wsc contiguous [E, N, .]");
-  const int E = W.size(0), N = W.size(1), K = 2 * W.size(2);
+  // W [E, N, K/2] (the packed standard order) or [E, K/128, N, 64] (K-step major, ops.mxfp4_kernel_layout)
+  TORCH_CHECK((W.dim() == 3 || (W.dim() == 4 && W.size(3) == 64)) && W.is_contiguous() && wsc.dim() == 3 &&
+              wsc.is_contiguous(), "W [E, N, K/2] or [E, K/128, N, 64] / wsc [E, N, K/32], contiguous");
+  const bool kmajor = W.dim() == 4;
+  const int E = W.size(0), N = kmajor ? W.size(2) : W.size(1), K = kmajor ? 128 * W.size(1) : 2 * W.size(2);
   TORCH_CHECK(wsc.size(0) == E && wsc.size(1) == N && wsc.size(2) == K / 32, "wsc [E, N, K/32]");
   TORCH_CHECK(X.size(1) == K && K % 128 == 0 && K / 128 >= 4 && X.stride(0) % 16 == 0, "moe_gemm8_mxfp4: K");
   TORCH_CHECK(tile_m == 256 || tile_m == 192 || tile_m == 64, "moe_gemm8_mxfp4: tile_m 256, 192 or 64");
@@ -1026,7 +1030,7 @@ void moe_gemm8_mxfp4(torch::Tensor X, torch::Tensor xs, int64_t topk, torch::Ten
                                       sorted_ids.data_ptr<int>(), tile_expert.data_ptr<int>(), total.data_ptr<int>(),
                                       P / bm, W.data_ptr(), W.stride(0), wsc.data_ptr(), wsc.stride(0), N, K,
                                       Y.data_ptr(), Y.stride(0), mode, act, (float)alpha, (float)limit,
-                                      a_rows_are_slots ? 1 : 0, bp, X.size(0), bm, cur_stream());
+                                      a_rows_are_slots ? 1 : 0, bp, X.size(0), bm, kmajor ? 1 : 0, cur_stream());
   TORCH_CHECK(rc == 0, "moe_gemm8_mxfp4 failed: ", rc);
 }
 

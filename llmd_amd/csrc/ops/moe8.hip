@@ -453,7 +453,7 @@ __global__ __launch_bounds__(P8_NT, 1) void moe_gemm8_mxfp4_kernel(
     int max_mtiles, int ntn, int order, const uint8_t* __restrict__ W, int64_t w_expert_stride,
     const uint8_t* __restrict__ wsc, int64_t wsc_expert_stride, int N, int K,
     uint16_t* __restrict__ Y, int64_t y_stride, int act, float alpha, float limit, int a_rows_are_slots,
-    const uint16_t* __restrict__ bias) {
+    const uint16_t* __restrict__ bias, int w_kmajor) {
   static_assert(TBM == 256 || TBM == 192 || TBM == 64, "tile rows");
   static_assert(NS == 2 || NS == 3, "stream depth");
   constexpr int MB = TBM / 64;                 // 32-row A blocks per wave
@@ -476,6 +476,7 @@ __global__ __launch_bounds__(P8_NT, 1) void moe_gemm8_mxfp4_kernel(
   __shared__ __attribute__((aligned(1024))) char lds[LDSB];  // the ONLY LDS object
 
   const int nk = K / 128;
+  const int wstep = w_kmajor ? N * 64 : 64;  // W bytes between consecutive K-steps of a row
   // this workgroup's work items: chunk [c0, c1) of XCD x, items c0 + s, c0 + s + S, ...
   const int n_items = min(__builtin_amdgcn_readfirstlane(total_p[0]) / TBM, max_mtiles) * ntn;
   // order 1: items b, b + G, b + 2 G, .. (the v4 grid's order: concurrent items spread over the XCDs)
@@ -538,7 +539,9 @@ __global__ __launch_bounds__(P8_NT, 1) void moe_gemm8_mxfp4_kernel(
     for (int j = 0; j < 4; ++j) {
       const int row = 64 * w + 16 * j + (lane >> 2);
       const int c = (lane & 3) ^ ((row >> 2) & 3);
-      vw[j] = n0 + row < N ? (uint32_t)((int64_t)(n0 + row) * (K / 2) + c * 16) : P8_OOB;
+      // w_kmajor: W stored [E, K/128, N, 64] (mxfp4_kernel_layout) - a K-step of a 256-row tile is one
+      // contiguous 16 KB run instead of 256 half cache lines
+      vw[j] = n0 + row < N ? (uint32_t)((int64_t)(n0 + row) * (w_kmajor ? 64 : K / 2) + c * 16) : P8_OOB;
     }
     // W scales: this lane's row 64 w + lane, 4 E8M0 bytes (the K-step's four 32-blocks)
     vsw = n0 + 64 * w + lane < N ? (uint32_t)((int64_t)(n0 + 64 * w + lane) * (K / 32)) : P8_OOB;
@@ -563,6 +566,8 @@ __global__ __launch_bounds__(P8_NT, 1) void moe_gemm8_mxfp4_kernel(
   // op 0 = A piece j, 1 = W piece j (< 4), 2 = act scales, 3 = W scales
   auto dma = [&](int bsel, int kc, int j, int op) {
     if constexpr ((DIAG & 2) != 0) return;  // diagnostic: no K-step DMA (LLMD_MXFP4_DIAG)
+    if constexpr ((DIAG & 4) != 0) if (op == 0) return;  // diagnostic: no activation (A) pieces
+    if constexpr ((DIAG & 8) != 0) if (op == 1) return;  // diagnostic: no weight (W) pieces
     char* buf = lds + bsel * BUF;
     if (op == 2)
       __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)(buf + OPA + WB + WSB + w * SROWS * 4),
@@ -572,7 +577,7 @@ __global__ __launch_bounds__(P8_NT, 1) void moe_gemm8_mxfp4_kernel(
                                                4, vsw, (uint32_t)(kc * 4), 0, 0);
     else if (op == 1)
       __builtin_amdgcn_raw_ptr_buffer_load_lds(rw, (__attribute__((address_space(3))) void*)(buf + OPA + (4 * w + j) * 1024),
-                                               16, vw[j], (uint32_t)(kc * 64), 0, 0);
+                                               16, vw[j], (uint32_t)(kc * wstep), 0, 0);
     else
       __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, (__attribute__((address_space(3))) void*)(buf + (NA * w + j) * 1024),
                                                16, va[j], (uint32_t)(kc * 128), 0, 0);
@@ -1182,7 +1187,7 @@ extern "C" int llmd_moe_gemm8_mxfp4(const void* X, int64_t x_stride, const float
                                     const void* W, int64_t w_expert_stride, const void* wsc, int64_t wsc_expert_stride,
                                     int N, int K, void* Y, int64_t y_stride, int mode, int act, float alpha,
                                     float limit, int a_rows_are_slots, const void* bias, int64_t x_rows, int tile_m,
-                                    hipStream_t st) {
+                                    int w_kmajor, hipStream_t st) {
   if (K % 128 || K / 128 < 4 || x_stride % 16 || w_expert_stride % 16 || wsc_expert_stride % 4 || N % 8 ||
       (mode == 1 && N % 16) || y_stride % 8 || total_p == nullptr)
     return -1;
@@ -1210,21 +1215,24 @@ extern "C" int llmd_moe_gemm8_mxfp4(const void* X, int64_t x_stride, const float
   hipLaunchKernelGGL((moe_gemm8_mxfp4_kernel<MODE_, TBM_, NS_>), dim3(grid), dim3(P8_NT), 0, st, (const uint8_t*)X,      \
                      x_stride, xs, xs_stride, topk, sorted_ids, tile_expert, total_p, num_tiles, ntn, order,         \
                      (const uint8_t*)W, w_expert_stride, (const uint8_t*)wsc, wsc_expert_stride, N, K, (uint16_t*)Y, \
-                     y_stride, act, alpha, limit, a_rows_are_slots, (const uint16_t*)bias)
+                     y_stride, act, alpha, limit, a_rows_are_slots, (const uint16_t*)bias, w_kmajor)
   // diagnostic variants (192-row tiles, 2 buffers; outputs are garbage): LLMD_MXFP4_DIAG = 1 no fragment
-  // reads, 2 no K-step DMAs, 3 neither - what is left of a step without each resource
+  // reads, 2 no K-step DMAs, 3 neither, 4 no activation pieces, 8 no weight pieces - what is left of a
+  // step without each resource
   const char* dgv = getenv("LLMD_MXFP4_DIAG");
-  const int diag = dgv ? atoi(dgv) & 3 : 0;
+  const int diag = dgv ? atoi(dgv) : 0;
 #define P4_DIAG(MODE_, D_)                                                                                          \
   hipLaunchKernelGGL((moe_gemm8_mxfp4_kernel<MODE_, 192, 2, D_>), dim3(grid), dim3(P8_NT), 0, st, (const uint8_t*)X, \
                      x_stride, xs, xs_stride, topk, sorted_ids, tile_expert, total_p, num_tiles, ntn, order,         \
                      (const uint8_t*)W, w_expert_stride, (const uint8_t*)wsc, wsc_expert_stride, N, K, (uint16_t*)Y, \
-                     y_stride, act, alpha, limit, a_rows_are_slots, (const uint16_t*)bias)
-  if (diag && tile_m == 192) {
+                     y_stride, act, alpha, limit, a_rows_are_slots, (const uint16_t*)bias, w_kmajor)
+  if ((diag == 1 || diag == 2 || diag == 3 || diag == 4 || diag == 8) && tile_m == 192) {
     if (mode == 0) {
-      if (diag == 1) P4_DIAG(0, 1); else if (diag == 2) P4_DIAG(0, 2); else P4_DIAG(0, 3);
+      if (diag == 1) P4_DIAG(0, 1); else if (diag == 2) P4_DIAG(0, 2); else if (diag == 3) P4_DIAG(0, 3);
+      else if (diag == 4) P4_DIAG(0, 4); else P4_DIAG(0, 8);
     } else {
-      if (diag == 1) P4_DIAG(1, 1); else if (diag == 2) P4_DIAG(1, 2); else P4_DIAG(1, 3);
+      if (diag == 1) P4_DIAG(1, 1); else if (diag == 2) P4_DIAG(1, 2); else if (diag == 3) P4_DIAG(1, 3);
+      else if (diag == 4) P4_DIAG(1, 4); else P4_DIAG(1, 8);
     }
   } else if (tile_m == 256) {
     if (mode == 0) P4_LAUNCH(0, 256); else P4_LAUNCH(1, 256);

@@ -142,18 +142,21 @@ class WeightSync:
             return False
         p, kind, extra, own = specs[key]
         full = full.to(p.device)
-        mx = p.dtype == torch.uint8 and p.dim() == 3 and own is not None and hasattr(own[0], own[1] + "_scale")
+        mx = p.dtype == torch.uint8 and p.dim() in (3, 4) and own is not None and hasattr(own[0], own[1] + "_scale")
         if p.dtype != torch.float8_e4m3fn and not mx:
             place(p, full, kind, extra)
             return True
         m, attr = own
         s = getattr(m, attr + "_scale" if attr in ("w1", "w2") else "weight_scale")
         with torch.no_grad():
-            if mx:  # MXFP4 experts [E, N, K/2 (K padded to 128)], E8M0 scales [E, N, K/32]
+            if mx:  # MXFP4 experts (K-step major [E, K/128, N, 64] or [E, N, K/2]), E8M0 scales [E, N, K/32]
                 k = full.shape[1] if kind == "experts_t" else full.shape[-1]
-                stage = ops.dequant_mxfp4_weight(p, s)[..., :k].to(torch.bfloat16).contiguous()
+                std = ops.mxfp4_std_layout(p)
+                stage = ops.dequant_mxfp4_weight(std, s)[..., :k].to(torch.bfloat16).contiguous()
                 place(stage, full, kind, extra)
-                q, ns = ops.quant_mxfp4_weight(ops.pad_mxfp4_k(stage, 2 * p.shape[-1]))
+                q, ns = ops.quant_mxfp4_weight(ops.pad_mxfp4_k(stage, 2 * std.shape[-1]))
+                if p.dim() == 4:
+                    q = ops.mxfp4_kernel_layout(q)
             elif p.dim() == 3:  # block-fp8 experts [E, N, K(padded to 128 on GPU)], scales [E, N/128, K/128]
                 k = full.shape[1] if kind == "experts_t" else full.shape[-1]
                 stage = ops.dequant_fp8_block_weight(p, s)[..., :k].to(torch.bfloat16).contiguous()

@@ -692,12 +692,13 @@ def moe_experts_mxfp4(x, ids, wts, w1q, w1s, w2q, w2s, act=0, alpha=1.702, limit
     activation fused into GEMM 1, bf16 weighted combine. w1q [E, 2F, Kp1/2], w2q [E, d, Kp2/2] in the
     standard packed order (the kernel reads activations in the K order the e2m1 operand implies).
     ``x`` may be ``Fp8Rows`` (the EP dispatch kernel's per-128 e4m3 rows)."""
-    E, N1, Kp1 = w1q.shape[0], w1q.shape[1], 2 * w1q.shape[2]
-    d, Kp2 = w2q.shape[1], 2 * w2q.shape[2]
+    E, N1, Kp1 = w1q.shape[0], _mx_n(w1q), _mx_k(w1q)
+    d, Kp2 = _mx_n(w2q), _mx_k(w2q)
     F = N1 // 2
     if isinstance(x, Fp8Rows) and not (x.is_cuda and x.q.shape[1] == Kp1):
         x = x.dequant()
     if not isinstance(x, Fp8Rows) and not _gpu(x):
+        w1q, w2q = mxfp4_std_layout(w1q), mxfp4_std_layout(w2q)
         xq, xs = quant_fp8_groups(x)
         xd = (xq.float().view(x.shape[0], -1) * xs.repeat_interleave(128, 1)[:, :x.shape[1]]).to(torch.bfloat16)
         w1 = dequant_mxfp4_weight(w1q, w1s)[..., :x.shape[1]].to(torch.bfloat16)
@@ -737,6 +738,34 @@ def moe_experts_mxfp4(x, ids, wts, w1q, w1s, w2q, w2s, act=0, alpha=1.702, limit
 # rows per local expert below which the MXFP4 experts take 64-row tiles: 64-row tiles win at 48 rows
 # (0.604 vs 0.694 ms, gpt-oss layer), lose at 64 (0.787 vs 0.714; profiles/moe_mxfp4_r6.txt)
 MXFP4_SMALL_ROWS = int(os.environ.get("LLMD_MXFP4_SMALL_ROWS", "56"))
+
+
+def mxfp4_kernel_layout(q: torch.Tensor) -> torch.Tensor:
+    """Packed MXFP4 codes [E, N, K/2] -> K-step major [E, K/128, N, 64]: the 64 code bytes of one
+    128-deep K-step of every row of an expert are contiguous, so the tile kernel's weight DMA for a
+    K-step of a 256-row tile is one 16 KB run instead of 256 half cache lines (the weight stream is
+    most of the kernel's step: profiles/moe_kstep_diag_r6.txt). K % 128 == 0."""
+    if q.dim() == 4:
+        return q
+    E, N, K2 = q.shape
+    assert K2 % 64 == 0, "K-step major MXFP4 needs K % 128 == 0"
+    return q.view(E, N, K2 // 64, 64).permute(0, 2, 1, 3).contiguous()
+
+
+def mxfp4_std_layout(q: torch.Tensor) -> torch.Tensor:
+    """Inverse of mxfp4_kernel_layout: [E, K/128, N, 64] -> [E, N, K/2] (3-D input unchanged)."""
+    if q.dim() == 3:
+        return q
+    E, nk, N, _ = q.shape
+    return q.permute(0, 2, 1, 3).reshape(E, N, nk * 64)
+
+
+def _mx_n(q):
+    return q.shape[2] if q.dim() == 4 else q.shape[1]
+
+
+def _mx_k(q):
+    return 128 * q.shape[1] if q.dim() == 4 else 2 * q.shape[2]
 
 
 def pad_mxfp4_k(w: torch.Tensor, kp: int) -> torch.Tensor:

@@ -37,6 +37,7 @@ def main():
     f1q, f2q = ops.pad_fp8_k(f1q, c128(d)), ops.pad_fp8_k(f2q, c128(F))
     m1q, m1s = ops.quant_mxfp4_weight(ops.pad_mxfp4_k(w1.float(), c128(d)))
     m2q, m2s = ops.quant_mxfp4_weight(ops.pad_mxfp4_k(w2.float(), c128(F)))
+    m1k, m2k = ops.mxfp4_kernel_layout(m1q), ops.mxfp4_kernel_layout(m2q)  # the layout the model stores
     del w1, w2
     sizes = [int(v) for v in sys.argv[1].split(",")] if len(sys.argv) > 1 else [64, 256, 1024, 1536, 2048, 5405]
     for T in sizes:
@@ -45,16 +46,17 @@ def main():
         tf = t_it(lambda: ops.moe_experts_fp8(x, ids, wts, f1q, f1s, f2q, f2s, 2, b1=b1, b2=b2))
         # arms: default (64-row tiles below MXFP4_SMALL_ROWS rows per expert, 2 workgroups per CU),
         # "1wg" = 64-row tiles at one workgroup per CU, "big" = the 192 / 256-row tiles at every size,
-        # "t64" = 64-row tiles at every size, "3st" = 3 LDS K-step buffers
-        arms = {"dflt": ({}, None), "1wg": ({"LLMD_MXFP4_WG64": "1"}, None), "big": ({}, 0), "t64": ({}, 1 << 20),
-                "3st": ({"LLMD_MXFP4_STAGES": "3"}, None)}
+        # "t64" = 64-row tiles at every size, "std" = weights in the packed standard order instead of
+        # K-step major (ops.mxfp4_kernel_layout)
+        arms = {"dflt": ({}, None), "std": ({}, None), "big": ({}, 0), "t64": ({}, 1 << 20)}
         tm = {}
         small = ops.MXFP4_SMALL_ROWS
         for _ in range(2):  # interleaved, best of two
             for name, (env, rows) in arms.items():
                 os.environ.update(env)
                 ops.MXFP4_SMALL_ROWS = small if rows is None else rows
-                t = t_it(lambda: ops.moe_experts_mxfp4(x, ids, wts, m1q, m1s, m2q, m2s, 2, b1=b1, b2=b2))
+                a1, a2 = (m1q, m2q) if name == "std" else (m1k, m2k)
+                t = t_it(lambda: ops.moe_experts_mxfp4(x, ids, wts, a1, m1s, a2, m2s, 2, b1=b1, b2=b2))
                 tm[name] = min(tm.get(name, 1e9), t)
                 for key in env:
                     os.environ.pop(key)

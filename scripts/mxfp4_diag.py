@@ -1,6 +1,7 @@
 """Diagnostic decomposition of the MXFP4 tile GEMM's K-step (csrc/ops/moe8.hip LLMD_MXFP4_DIAG): the
 gpt-oss gate/up (mode 1) and down (mode 0) GEMMs at T=5405 on 192-row tiles, timed as built (0), without
-fragment reads (1), without K-step DMAs (2) and without both (3: MFMAs, barriers, waits, epilogue).
+fragment reads (1), without K-step DMAs (2), without both (3: MFMAs, barriers, waits, epilogue),
+without the activation (4) or the weight (8) pieces of the stream.
 Outputs of 1-3 are garbage by design.  python scripts/mxfp4_diag.py"""
 import os
 import sys
@@ -19,6 +20,8 @@ def main():
     torch.manual_seed(0)
     w1q, w1s = ops.quant_mxfp4_weight(ops.pad_mxfp4_k(torch.randn(E, 2 * F, d, device=dev) * 0.02, 2944))
     w2q, w2s = ops.quant_mxfp4_weight(ops.pad_mxfp4_k(torch.randn(E, d, F, device=dev) * 0.02, 2944))
+    if os.environ.get("DIAG_LAYOUT", "kstep") == "kstep":
+        w1q, w2q = ops.mxfp4_kernel_layout(w1q), ops.mxfp4_kernel_layout(w2q)
     x = torch.randn(T, d, device=dev, dtype=torch.bfloat16)
     ids, _ = ops.moe_topk(torch.randn(T, E, device=dev), k, scoring=0)
     bm = 192
@@ -42,7 +45,7 @@ def main():
                                                total), 2 * rows * d * F)):
         res = {}
         for _ in range(2):
-            for dg in ("0", "1", "2", "3"):
+            for dg in ("0", "1", "2", "3", "4", "8"):
                 os.environ["LLMD_MXFP4_DIAG"] = dg
                 for _ in range(3):
                     fn()
@@ -55,7 +58,8 @@ def main():
         os.environ.pop("LLMD_MXFP4_DIAG")
         print(f"{name} (padded rows {rows}): " + " | ".join(
             f"{lab} {res[dg] * 1e3:.3f} ms ({fl / res[dg] / 1e12:.0f} TF/s)" for dg, lab in
-            (("0", "full"), ("1", "no-frag-reads"), ("2", "no-DMA"), ("3", "neither"))), flush=True)
+            (("0", "full"), ("1", "no-frag-reads"), ("2", "no-DMA"), ("3", "neither"), ("4", "no-A-DMA"),
+             ("8", "no-W-DMA"))), flush=True)
 
 
 if __name__ == "__main__":

@@ -63,8 +63,8 @@ def _oracle_rows(xq, xs, wq, ws, bias, sorted_ids, tile_e, tile, k, mode):
                                                 (0, 192, 3, 2944), (1, 256, 2, 512), (0, 192, 3, 512),
                                                 (0, 64, 2, 2944), (1, 64, 2, 2944), (1, 64, 3, 512)])
 def test_moe_gemm8_mxfp4_matches_fp32(mode, tile, stages, K, monkeypatch):
-    """stages: LDS K-step buffers of the stream (3 = default, 2 = the fp8 kernel's depth); K = 512 is
-    the shortest K loop (4 steps: every step is a peeled tile-transition phase)."""
+    """stages: LDS K-step buffers of the stream (2 = default, 3 opt-in); K = 512 is the shortest K loop
+    (4 steps: every step is a peeled tile-transition phase); each case runs both weight layouts."""
     monkeypatch.setenv("LLMD_MXFP4_STAGES", str(stages))
     torch.manual_seed(5)
     dev = "cuda"
@@ -84,14 +84,16 @@ def test_moe_gemm8_mxfp4_matches_fp32(mode, tile, stages, K, monkeypatch):
     total = torch.empty(1, dtype=torch.int32, device=dev)
     inv = torch.empty(n, dtype=torch.int32, device=dev)
     C.moe_align(ids.contiguous().view(-1).to(torch.int32), E, sorted_ids, tile_e, offs, total, inv, tile)
-    y = torch.full((max_p, N // 2 if mode == 1 else N), 7.0, device=dev, dtype=torch.bfloat16)
-    C.moe_gemm8_mxfp4(xq, xs, k, sorted_ids, tile_e, wq, ws, y, mode, 2, 1.702, 7.0, False, bias, tile, total)
-    torch.cuda.synchronize()
     ref, live = _oracle_rows(xq, xs, wq, ws, bias, sorted_ids, tile_e, tile, k, mode)
-    got = y.float()
     m = ref[live].abs().max().item()
-    assert (got[live] - ref[live]).abs().max().item() < 0.01 * m + 1e-2
-    assert (got[~live] == 7.0).all()
+    # both weight layouts: the packed standard order and K-step major (ops.mxfp4_kernel_layout)
+    for w in (wq, ops.mxfp4_kernel_layout(wq)):
+        y = torch.full((max_p, N // 2 if mode == 1 else N), 7.0, device=dev, dtype=torch.bfloat16)
+        C.moe_gemm8_mxfp4(xq, xs, k, sorted_ids, tile_e, w, ws, y, mode, 2, 1.702, 7.0, False, bias, tile, total)
+        torch.cuda.synchronize()
+        got = y.float()
+        assert (got[live] - ref[live]).abs().max().item() < 0.01 * m + 1e-2, w.dim()
+        assert (got[~live] == 7.0).all()
 
 
 @pytest.mark.gpu
@@ -106,6 +108,7 @@ def test_moe_experts_mxfp4_gpu_vs_cpu(T):
     w2 = ops.pad_mxfp4_k(torch.randn(E, d, F, device=dev) * 0.03, c128(F))
     w1q, w1s = ops.quant_mxfp4_weight(w1)
     w2q, w2s = ops.quant_mxfp4_weight(w2)
+    w1q, w2q = ops.mxfp4_kernel_layout(w1q), ops.mxfp4_kernel_layout(w2q)  # the layout the model stores
     b1 = torch.randn(E, 2 * F, device=dev, dtype=torch.bfloat16) * 0.1
     b2 = torch.randn(E, d, device=dev, dtype=torch.bfloat16) * 0.1
     ids, wts = ops.moe_topk(torch.randn(T, E, device=dev), k, scoring=0)
@@ -158,7 +161,8 @@ def test_load_mxfp4_checkpoint_experts_lossless(tmp_path):
         assert pq.dtype == torch.uint8
         # the same values (a block whose largest code is 3 may come back as 6 at half the scale)
         K = 2 * q.shape[2]
-        got = ops.dequant_mxfp4_weight(pq, getattr(m, a + "_scale"))[..., :K]
+        assert pq.dim() == 4  # stored K-step major for the tile kernel
+        got = ops.dequant_mxfp4_weight(ops.mxfp4_std_layout(pq), getattr(m, a + "_scale"))[..., :K]
         assert torch.equal(got, ops.dequant_mxfp4_weight(q, s))
     out = eng.generate([[5, 6, 7, 8, 9]], __import__("llmd_amd.engine.request", fromlist=["SamplingParams"])
                        .SamplingParams(max_tokens=3, temperature=0.0, ignore_eos=True))
