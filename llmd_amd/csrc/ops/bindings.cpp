@@ -1008,11 +1008,18 @@ void moe_gemm8_mxfp4(torch::Tensor X, torch::Tensor xs, int64_t topk, torch::Ten
   CHECK_CUDA(X); CHECK_DT(X, at::kFloat8_e4m3fn); CHECK_DT(W, at::kByte); CHECK_DT(wsc, at::kByte); CHECK_BF16(Y);
   CHECK_INNER(X); CHECK_INNER(Y); CHECK_DT(xs, at::kFloat); CHECK_DT(total, at::kInt);
   // W [E, N, K/2] (the packed standard order) or [E, K/128, N, 64] (K-step major, ops.mxfp4_kernel_layout)
-  TORCH_CHECK((W.dim() == 3 || (W.dim() == 4 && W.size(3) == 64)) && W.is_contiguous() && wsc.dim() == 3 &&
-              wsc.is_contiguous(), "W [E, N, K/2] or [E, K/128, N, 64] / wsc [E, N, K/32], contiguous");
+  // K-step major: W [E, K/128, N, 64] with wsc [E, K/128, N, 4] (ops.mxfp4_kernel_layout / _scales_)
+  TORCH_CHECK((W.dim() == 3 || (W.dim() == 4 && W.size(3) == 64)) && W.is_contiguous() &&
+              wsc.dim() == W.dim() && wsc.is_contiguous(),
+              "W [E, N, K/2] + wsc [E, N, K/32], or W [E, K/128, N, 64] + wsc [E, K/128, N, 4], contiguous");
   const bool kmajor = W.dim() == 4;
   const int E = W.size(0), N = kmajor ? W.size(2) : W.size(1), K = kmajor ? 128 * W.size(1) : 2 * W.size(2);
-  TORCH_CHECK(wsc.size(0) == E && wsc.size(1) == N && wsc.size(2) == K / 32, "wsc [E, N, K/32]");
+  if (kmajor) {
+    TORCH_CHECK(wsc.size(0) == E && wsc.size(1) == K / 128 && wsc.size(2) == N && wsc.size(3) == 4,
+                "wsc [E, K/128, N, 4]");
+  } else {
+    TORCH_CHECK(wsc.size(0) == E && wsc.size(1) == N && wsc.size(2) == K / 32, "wsc [E, N, K/32]");
+  }
   TORCH_CHECK(X.size(1) == K && K % 128 == 0 && K / 128 >= 4 && X.stride(0) % 16 == 0, "moe_gemm8_mxfp4: K");
   TORCH_CHECK(tile_m == 256 || tile_m == 192 || tile_m == 64, "moe_gemm8_mxfp4: tile_m 256, 192 or 64");
   TORCH_CHECK(xs.dim() == 2 && xs.size(0) >= X.size(0) && xs.size(1) >= K / 128 && xs.stride(1) == 1, "xs [rows, K/128]");

@@ -477,6 +477,7 @@ __global__ __launch_bounds__(P8_NT, 1) void moe_gemm8_mxfp4_kernel(
 
   const int nk = K / 128;
   const int wstep = w_kmajor ? N * 64 : 64;  // W bytes between consecutive K-steps of a row
+  const int sstep = w_kmajor ? N * 4 : 4;    // and of its E8M0 scales
   // this workgroup's work items: chunk [c0, c1) of XCD x, items c0 + s, c0 + s + S, ...
   const int n_items = min(__builtin_amdgcn_readfirstlane(total_p[0]) / TBM, max_mtiles) * ntn;
   // order 1: items b, b + G, b + 2 G, .. (the v4 grid's order: concurrent items spread over the XCDs)
@@ -544,7 +545,7 @@ __global__ __launch_bounds__(P8_NT, 1) void moe_gemm8_mxfp4_kernel(
       vw[j] = n0 + row < N ? (uint32_t)((int64_t)(n0 + row) * (w_kmajor ? 64 : K / 2) + c * 16) : P8_OOB;
     }
     // W scales: this lane's row 64 w + lane, 4 E8M0 bytes (the K-step's four 32-blocks)
-    vsw = n0 + 64 * w + lane < N ? (uint32_t)((int64_t)(n0 + 64 * w + lane) * (K / 32)) : P8_OOB;
+    vsw = n0 + 64 * w + lane < N ? (uint32_t)((int64_t)(n0 + 64 * w + lane) * (w_kmajor ? 4 : K / 32)) : P8_OOB;
     {
       const int row = min(SROWS * w + lane, TBM - 1);
       const int tok = sid_s < 0 ? 0 : (a_rows_are_slots ? m0 + row : sid_s / topk);
@@ -574,7 +575,7 @@ __global__ __launch_bounds__(P8_NT, 1) void moe_gemm8_mxfp4_kernel(
                                                4, vs, (uint32_t)(kc * 4), 0, 0);
     else if (op == 3)
       __builtin_amdgcn_raw_ptr_buffer_load_lds(rsw, (__attribute__((address_space(3))) void*)(buf + OPA + WB + w * 256),
-                                               4, vsw, (uint32_t)(kc * 4), 0, 0);
+                                               4, vsw, (uint32_t)(kc * sstep), 0, 0);
     else if (op == 1)
       __builtin_amdgcn_raw_ptr_buffer_load_lds(rw, (__attribute__((address_space(3))) void*)(buf + OPA + (4 * w + j) * 1024),
                                                16, vw[j], (uint32_t)(kc * wstep), 0, 0);

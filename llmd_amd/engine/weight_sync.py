@@ -152,11 +152,12 @@ class WeightSync:
             if mx:  # MXFP4 experts (K-step major [E, K/128, N, 64] or [E, N, K/2]), E8M0 scales [E, N, K/32]
                 k = full.shape[1] if kind == "experts_t" else full.shape[-1]
                 std = ops.mxfp4_std_layout(p)
-                stage = ops.dequant_mxfp4_weight(std, s)[..., :k].to(torch.bfloat16).contiguous()
+                stage = ops.dequant_mxfp4_weight(std, ops.mxfp4_scales_std_layout(s))[..., :k]
+                stage = stage.to(torch.bfloat16).contiguous()
                 place(stage, full, kind, extra)
                 q, ns = ops.quant_mxfp4_weight(ops.pad_mxfp4_k(stage, 2 * std.shape[-1]))
                 if p.dim() == 4:
-                    q = ops.mxfp4_kernel_layout(q)
+                    q, ns = ops.mxfp4_kernel_layout(q), ops.mxfp4_scales_kernel_layout(ns)
             elif p.dim() == 3:  # block-fp8 experts [E, N, K(padded to 128 on GPU)], scales [E, N/128, K/128]
                 k = full.shape[1] if kind == "experts_t" else full.shape[-1]
                 stage = ops.dequant_fp8_block_weight(p, s)[..., :k].to(torch.bfloat16).contiguous()

@@ -82,7 +82,8 @@ def quantize_mxfp4(model: torch.nn.Module) -> int:
             if isinstance(w, torch.Tensor) and w.dim() == 3 and w.dtype == torch.bfloat16:
                 kp = max(512, (w.shape[2] + 127) // 128 * 128)
                 q, s = ops.quant_mxfp4_weight(ops.pad_mxfp4_k(w.data, kp))
-                q = ops.mxfp4_kernel_layout(q)  # K-step major: contiguous weight DMA per K-step
+                # K-step major codes and scales: contiguous weight DMA per K-step
+                q, s = ops.mxfp4_kernel_layout(q), ops.mxfp4_scales_kernel_layout(s)
                 setattr(m, name, torch.nn.Parameter(q, requires_grad=False))
                 setattr(m, name + "_scale", torch.nn.Parameter(s, requires_grad=False))
                 n += 1

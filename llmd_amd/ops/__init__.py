@@ -699,6 +699,7 @@ def moe_experts_mxfp4(x, ids, wts, w1q, w1s, w2q, w2s, act=0, alpha=1.702, limit
         x = x.dequant()
     if not isinstance(x, Fp8Rows) and not _gpu(x):
         w1q, w2q = mxfp4_std_layout(w1q), mxfp4_std_layout(w2q)
+        w1s, w2s = mxfp4_scales_std_layout(w1s), mxfp4_scales_std_layout(w2s)
         xq, xs = quant_fp8_groups(x)
         xd = (xq.float().view(x.shape[0], -1) * xs.repeat_interleave(128, 1)[:, :x.shape[1]]).to(torch.bfloat16)
         w1 = dequant_mxfp4_weight(w1q, w1s)[..., :x.shape[1]].to(torch.bfloat16)
@@ -735,9 +736,9 @@ def moe_experts_mxfp4(x, ids, wts, w1q, w1s, w2q, w2s, act=0, alpha=1.702, limit
     return out
 
 
-# rows per local expert below which the MXFP4 experts take 64-row tiles: 64-row tiles win at 48 rows
-# (0.604 vs 0.694 ms, gpt-oss layer), lose at 64 (0.787 vs 0.714; profiles/moe_mxfp4_r6.txt)
-MXFP4_SMALL_ROWS = int(os.environ.get("LLMD_MXFP4_SMALL_ROWS", "56"))
+# rows per local expert below which the MXFP4 experts take 64-row tiles: with K-step-major weights and
+# scales they win at 64 rows (0.548 vs 0.590 ms, gpt-oss layer) and lose at 169 (profiles/moe_mxfp4_r6.txt)
+MXFP4_SMALL_ROWS = int(os.environ.get("LLMD_MXFP4_SMALL_ROWS", "72"))
 
 
 def mxfp4_kernel_layout(q: torch.Tensor) -> torch.Tensor:
@@ -758,6 +759,22 @@ def mxfp4_std_layout(q: torch.Tensor) -> torch.Tensor:
         return q
     E, nk, N, _ = q.shape
     return q.permute(0, 2, 1, 3).reshape(E, N, nk * 64)
+
+
+def mxfp4_scales_kernel_layout(s: torch.Tensor) -> torch.Tensor:
+    """E8M0 scales [E, N, K/32] -> K-step major [E, K/128, N, 4] (the companion of mxfp4_kernel_layout:
+    a K-step's scales of a 256-row tile are one contiguous 1 KB run)."""
+    if s.dim() == 4:
+        return s
+    E, N, nb = s.shape
+    return s.view(E, N, nb // 4, 4).permute(0, 2, 1, 3).contiguous()
+
+
+def mxfp4_scales_std_layout(s: torch.Tensor) -> torch.Tensor:
+    if s.dim() == 3:
+        return s
+    E, nk, N, _ = s.shape
+    return s.permute(0, 2, 1, 3).reshape(E, N, nk * 4)
 
 
 def _mx_n(q):

@@ -38,7 +38,8 @@ def main():
         if name.startswith("gpt-oss"):
             m1 = ops.quant_mxfp4_weight(ops.pad_mxfp4_k(w1, c128(d)))
             m2 = ops.quant_mxfp4_weight(ops.pad_mxfp4_k(w2, c128(F)))
-            mx = (ops.mxfp4_kernel_layout(m1[0]), m1[1], ops.mxfp4_kernel_layout(m2[0]), m2[1])
+            mx = (ops.mxfp4_kernel_layout(m1[0]), ops.mxfp4_scales_kernel_layout(m1[1]),
+                  ops.mxfp4_kernel_layout(m2[0]), ops.mxfp4_scales_kernel_layout(m2[1]))
         wbytes = f1q.numel() + f2q.numel()
         del w1, w2
         for T in sizes:

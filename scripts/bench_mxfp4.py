@@ -38,6 +38,7 @@ def main():
     m1q, m1s = ops.quant_mxfp4_weight(ops.pad_mxfp4_k(w1.float(), c128(d)))
     m2q, m2s = ops.quant_mxfp4_weight(ops.pad_mxfp4_k(w2.float(), c128(F)))
     m1k, m2k = ops.mxfp4_kernel_layout(m1q), ops.mxfp4_kernel_layout(m2q)  # the layout the model stores
+    m1sk, m2sk = ops.mxfp4_scales_kernel_layout(m1s), ops.mxfp4_scales_kernel_layout(m2s)
     del w1, w2
     sizes = [int(v) for v in sys.argv[1].split(",")] if len(sys.argv) > 1 else [64, 256, 1024, 1536, 2048, 5405]
     for T in sizes:
@@ -55,8 +56,8 @@ def main():
             for name, (env, rows) in arms.items():
                 os.environ.update(env)
                 ops.MXFP4_SMALL_ROWS = small if rows is None else rows
-                a1, a2 = (m1q, m2q) if name == "std" else (m1k, m2k)
-                t = t_it(lambda: ops.moe_experts_mxfp4(x, ids, wts, a1, m1s, a2, m2s, 2, b1=b1, b2=b2))
+                a1, s1, a2, s2 = (m1q, m1s, m2q, m2s) if name == "std" else (m1k, m1sk, m2k, m2sk)
+                t = t_it(lambda: ops.moe_experts_mxfp4(x, ids, wts, a1, s1, a2, s2, 2, b1=b1, b2=b2))
                 tm[name] = min(tm.get(name, 1e9), t)
                 for key in env:
                     os.environ.pop(key)

@@ -22,6 +22,7 @@ def main():
     w2q, w2s = ops.quant_mxfp4_weight(ops.pad_mxfp4_k(torch.randn(E, d, F, device=dev) * 0.02, 2944))
     if os.environ.get("DIAG_LAYOUT", "kstep") == "kstep":
         w1q, w2q = ops.mxfp4_kernel_layout(w1q), ops.mxfp4_kernel_layout(w2q)
+        w1s, w2s = ops.mxfp4_scales_kernel_layout(w1s), ops.mxfp4_scales_kernel_layout(w2s)
     x = torch.randn(T, d, device=dev, dtype=torch.bfloat16)
     ids, _ = ops.moe_topk(torch.randn(T, E, device=dev), k, scoring=0)
     bm = 192

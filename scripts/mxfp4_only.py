@@ -21,6 +21,7 @@ def main():
         q1, s1 = ops.quant_mxfp4_weight(ops.pad_mxfp4_k(w1, 2944))
         q2, s2 = ops.quant_mxfp4_weight(ops.pad_mxfp4_k(w2, 2944))
         q1, q2 = ops.mxfp4_kernel_layout(q1), ops.mxfp4_kernel_layout(q2)
+        s1, s2 = ops.mxfp4_scales_kernel_layout(s1), ops.mxfp4_scales_kernel_layout(s2)
         fn = ops.moe_experts_mxfp4
     else:
         q1, s1 = ops.quant_fp8_block_weight(w1)

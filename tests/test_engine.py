@@ -220,7 +220,8 @@ def test_gpt_oss_mxfp4_engine_gpu_runs():
     for a, b in zip(moes, ref_moes):
         for nm in ("w1", "w2"):
             k = getattr(b, nm).shape[2]
-            w = ops.dequant_mxfp4_weight(ops.mxfp4_std_layout(getattr(a, nm)), getattr(a, nm + "_scale"))[..., :k]
+            w = ops.dequant_mxfp4_weight(ops.mxfp4_std_layout(getattr(a, nm)),
+                                         ops.mxfp4_scales_std_layout(getattr(a, nm + "_scale")))[..., :k]
             setattr(b, nm, torch.nn.Parameter(w.to(torch.bfloat16).contiguous(), requires_grad=False))
             delattr(b, nm + "_scale")
     prompts = _prompts(7, [5, 100, 40, 230])

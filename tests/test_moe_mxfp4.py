@@ -87,9 +87,9 @@ def test_moe_gemm8_mxfp4_matches_fp32(mode, tile, stages, K, monkeypatch):
     ref, live = _oracle_rows(xq, xs, wq, ws, bias, sorted_ids, tile_e, tile, k, mode)
     m = ref[live].abs().max().item()
     # both weight layouts: the packed standard order and K-step major (ops.mxfp4_kernel_layout)
-    for w in (wq, ops.mxfp4_kernel_layout(wq)):
+    for w, sc in ((wq, ws), (ops.mxfp4_kernel_layout(wq), ops.mxfp4_scales_kernel_layout(ws))):
         y = torch.full((max_p, N // 2 if mode == 1 else N), 7.0, device=dev, dtype=torch.bfloat16)
-        C.moe_gemm8_mxfp4(xq, xs, k, sorted_ids, tile_e, w, ws, y, mode, 2, 1.702, 7.0, False, bias, tile, total)
+        C.moe_gemm8_mxfp4(xq, xs, k, sorted_ids, tile_e, w, sc, y, mode, 2, 1.702, 7.0, False, bias, tile, total)
         torch.cuda.synchronize()
         got = y.float()
         assert (got[live] - ref[live]).abs().max().item() < 0.01 * m + 1e-2, w.dim()
@@ -109,6 +109,7 @@ def test_moe_experts_mxfp4_gpu_vs_cpu(T):
     w1q, w1s = ops.quant_mxfp4_weight(w1)
     w2q, w2s = ops.quant_mxfp4_weight(w2)
     w1q, w2q = ops.mxfp4_kernel_layout(w1q), ops.mxfp4_kernel_layout(w2q)  # the layout the model stores
+    w1s, w2s = ops.mxfp4_scales_kernel_layout(w1s), ops.mxfp4_scales_kernel_layout(w2s)
     b1 = torch.randn(E, 2 * F, device=dev, dtype=torch.bfloat16) * 0.1
     b2 = torch.randn(E, d, device=dev, dtype=torch.bfloat16) * 0.1
     ids, wts = ops.moe_topk(torch.randn(T, E, device=dev), k, scoring=0)
@@ -162,7 +163,8 @@ def test_load_mxfp4_checkpoint_experts_lossless(tmp_path):
         # the same values (a block whose largest code is 3 may come back as 6 at half the scale)
         K = 2 * q.shape[2]
         assert pq.dim() == 4  # stored K-step major for the tile kernel
-        got = ops.dequant_mxfp4_weight(ops.mxfp4_std_layout(pq), getattr(m, a + "_scale"))[..., :K]
+        got = ops.dequant_mxfp4_weight(ops.mxfp4_std_layout(pq),
+                                       ops.mxfp4_scales_std_layout(getattr(m, a + "_scale")))[..., :K]
         assert torch.equal(got, ops.dequant_mxfp4_weight(q, s))
     out = eng.generate([[5, 6, 7, 8, 9]], __import__("llmd_amd.engine.request", fromlist=["SamplingParams"])
                        .SamplingParams(max_tokens=3, temperature=0.0, ignore_eos=True))
